@@ -1,0 +1,142 @@
+#!/usr/bin/env python3
+"""Headline benchmark: MNIST MLP (784-100-10, example.py) sync-SGD samples/sec.
+
+Metric/config from BASELINE.json: "samples/sec (whole node) MNIST MLP sync-SGD
+at 1/2/4/8 MI355X; step-time p50".  Per-GPU batch 100 (example.py:43),
+lr 0.0005, sigmoid hidden layer, softmax cross-entropy, plain SGD; bf16 MFMA
+compute with fp32 master weights; gradients all-reduced in bf16 over RCCL
+(BASELINE config #2).  Synthetic MNIST-shaped data (uint8 pixels, streamed
+from pinned host memory with one hipMemcpyAsync per step on a side stream),
+random-init weights.  Weak scaling: per-GPU batch fixed as N grows.
+
+    python bench.py --gpus N --steps K --warmup W
+    (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+from distributed_tensorflow_example_amd.data.mnist import PinnedEpoch, synthetic_mnist  # noqa: E402
+from distributed_tensorflow_example_amd.models.mlp import FusedMLPTrainer, MLPStepRunner  # noqa: E402
+from distributed_tensorflow_example_amd.parallel import world as world_mod  # noqa: E402
+
+METRIC = "samples/sec (whole node) MNIST MLP sync-SGD at 1/2/4/8 MI355X; step-time p50"
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5500)
+    ap.add_argument("--warmup", type=int, default=550)
+    ap.add_argument("--batch", type=int, default=100, help="per-GPU batch (reference: 100)")
+    ap.add_argument("--lr", type=float, default=0.0005)
+    ap.add_argument("--steps-per-graph", type=int, default=50)
+    ap.add_argument("--eager", action="store_true", help="no hipGraph capture")
+    ap.add_argument("--grad-dtype", choices=["bf16", "fp32"], default="bf16")
+    ap.add_argument("--act", choices=["sigmoid", "relu"], default="sigmoid")
+    ap.add_argument("--train-examples", type=int, default=55000)
+    a = ap.parse_args(argv)
+
+    world_size_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_size_env != a.gpus:
+        if a.gpus > 1 and world_size_env == 1:
+            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
+    w = world_mod.init(backend="rccl")
+    dev = w.device
+    torch.manual_seed(1234 + w.rank)
+
+    imgs, labels = synthetic_mnist(a.train_examples, seed=1000 + w.rank)
+    epoch = PinnedEpoch(imgs, labels, a.batch)
+    gd = torch.bfloat16 if a.grad_dtype == "bf16" else torch.float32
+    trainer = FusedMLPTrainer(batch_size=a.batch, lr=a.lr, act=a.act, world=w, grad_dtype=gd,
+                              device=dev)
+    runner = MLPStepRunner(trainer, epoch, steps_per_graph=a.steps_per_graph,
+                           use_graph=not a.eager)
+
+    # warmup: eager first (module load), then the graphs the warmup itself needs
+    runner.use_graph = False
+    runner.run(min(2, a.warmup))
+    runner.use_graph = not a.eager
+    if a.warmup > 2:
+        runner.prepare(a.warmup - 2)
+        runner.run(a.warmup - 2)
+    torch.cuda.synchronize()
+    runner.prepare(a.steps)  # capture outside the timed region
+    torch.cuda.synchronize()
+    step0 = trainer.global_step
+
+    events = []
+    w.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    runner.run(a.steps, events=events)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    w.barrier()
+    elapsed = t1 - t0
+    elapsed_max = w.host_all_reduce(elapsed, "max")
+
+    # step-time p50 from per-graph-replay GPU intervals
+    per_step_ms = []
+    prev = ev0
+    for ev, g in events:
+        per_step_ms.append(prev.elapsed_time(ev) / g)
+        prev = ev
+    p50 = statistics.median(per_step_ms) if per_step_ms else float("nan")
+    p50 = w.host_all_reduce(p50, "max")
+
+    steps_done = trainer.global_step - step0
+    m = trainer.read_metrics(trainer.global_step - 1, trainer.global_step)[0]
+    n = w.world_size
+    samples_per_s = n * a.batch * a.steps / elapsed_max
+    if w.rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(samples_per_s, 1),
+            "unit": "samples/s",
+            "n_gpus": n,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed_max * 1000.0 / a.steps, 5),
+            "step_time_p50_ms": round(p50, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (MNIST-shaped uint8, pinned host -> hipMemcpyAsync side stream), random-init",
+            "config": {
+                "model": "mlp-784-100-10 (example.py)",
+                "global_batch": a.batch * n,
+                "per_gpu_batch": a.batch,
+                "seq_len": None,
+                "parallelism": f"dp{n}",
+                "optimizer": f"sgd lr={a.lr}",
+                "grad_allreduce": a.grad_dtype if n > 1 else "none",
+                "hipgraph_steps": 0 if a.eager else a.steps_per_graph,
+                "activation": a.act,
+            },
+            "final_loss": round(float(m[0]), 5),
+            "final_batch_acc": round(float(m[1]), 4),
+            "global_steps_timed": steps_done,
+        }
+        print(json.dumps(out), flush=True)
+    w.shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,87 @@
+// Shared CDNA4 (gfx950) device helpers: bf16 packing, MFMA wrappers, wave64
+// reductions.  Every kernel in csrc/kernels includes this header; nothing here
+// is CUDA-derived -- wave width is hard-coded to 64 and MFMA shapes are the
+// gfx950 16x16x32 / 32x32x16 bf16 forms.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dtfk {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+constexpr int kWave = 64;
+
+// D = A(16x32) * B(32x16) + C, fp32 accumulate.
+// Lane l holds A[l&15][8*(l>>4)+j], B[8*(l>>4)+j][l&15] (j = 0..7) and
+// C/D[4*(l>>4)+i][l&15] (i = 0..3).
+__device__ __forceinline__ f32x4 mfma16x16x32(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// D = A(32x16) * B(16x32) + C. Lane l holds A[l&31][8*(l>>5)+j],
+// B[8*(l>>5)+j][l&31]; C/D[(r&3)+8*(r>>2)+4*(l>>5)][l&31] (r = 0..15).
+__device__ __forceinline__ f32x16 mfma32x32x16(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// fp32 -> bf16 bits, round-to-nearest-even (hardware cvt on gfx950).
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  __bf16 h = static_cast<__bf16>(f);
+  return __builtin_bit_cast(uint16_t, h);
+}
+__device__ __forceinline__ float bf2f(uint16_t b) {
+  return __uint_as_float(static_cast<uint32_t>(b) << 16);
+}
+__device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
+  return static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
+}
+
+__device__ __forceinline__ bf16x8 ld_bf16x8(const uint16_t* p) {
+  return *reinterpret_cast<const bf16x8*>(p);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+  return v;
+}
+// Reductions over aligned groups of 16 lanes (one MFMA 16x16 output row group).
+__device__ __forceinline__ float group16_sum(float v) {
+#pragma unroll
+  for (int off = 8; off > 0; off >>= 1) v += __shfl_xor(v, off, 16);
+  return v;
+}
+__device__ __forceinline__ float group16_max(float v) {
+#pragma unroll
+  for (int off = 8; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 16));
+  return v;
+}
+
+// Block-wide sum for blockDim.x a multiple of 64 (<= 1024). `scratch` needs
+// blockDim.x/64 floats of LDS. Result valid in every thread.
+__device__ __forceinline__ float block_sum(float v, float* scratch) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nw = blockDim.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < nw; ++i) t += scratch[i];
+  return t;
+}
+
+__device__ __forceinline__ float sigmoidf_(float z) { return 1.f / (1.f + __expf(-z)); }
+
+}  // namespace dtfk
+
+#define DTFK_CHECK_LAUNCH() (hipGetLastError())

@@ -1,0 +1,16 @@
+// Single Python extension module `_C` for the framework's native code:
+// HIP kernels (bound per area), the RCCL communicator and the C++ runtime
+// (TCP store, blocking queue, libsvm parser, CRC32C, TF bundle, tfevents).
+#include <torch/extension.h>
+
+namespace dtf {
+void init_mlp(py::module& m);
+void init_comm(py::module& m);
+}  // namespace dtf
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "MI355X-native kernels and runtime for distributed_tensorflow_example_amd";
+  m.attr("ARCH") = "gfx950";
+  dtf::init_mlp(m);
+  dtf::init_comm(m);
+}

@@ -1,0 +1,209 @@
+"""Process-group bootstrap: one process per GPU, RCCL data plane, gloo control plane.
+
+The reference ties every worker to the ps over TF's gRPC runtime
+(`tf.train.Server`, example.py:38-40; lr2.py:331).  Here each rank is one
+process bound to one MI355X:
+
+* control plane -- `torch.distributed` gloo group (host tensors: barriers,
+  object broadcast, timing reductions, RCCL unique-id exchange).  It is also
+  the *data* plane on CPU-only hosts (BASELINE config #1, "runs without a GPU").
+* data plane    -- native `RcclComm` (csrc/comm/rccl_comm.cpp) issuing RCCL
+  collectives on the caller's HIP stream, so they are hipGraph-capturable.
+
+Rendezvous comes from the torchrun env (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*)
+or explicitly (ClusterSpec path in `compat.train.Server`).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass, field
+from typing import Any, Optional
+
+import torch
+import torch.distributed as dist
+
+_WORLD: Optional["World"] = None
+
+
+@dataclass
+class World:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    device: torch.device = field(default_factory=lambda: torch.device("cpu"))
+    backend: str = "none"          # "rccl" | "gloo" | "none"
+    comm: Any = None               # native RcclComm (GPU data plane)
+    pg_initialized: bool = False
+
+    @property
+    def is_chief(self) -> bool:
+        return self.rank == 0
+
+    @property
+    def distributed(self) -> bool:
+        return self.world_size > 1
+
+    # ------------------------------------------------------------ control plane
+    def barrier(self):
+        if self.pg_initialized:
+            dist.barrier()
+
+    def host_all_reduce(self, value: float, op: str = "sum") -> float:
+        if not self.pg_initialized:
+            return float(value)
+        t = torch.tensor([float(value)], dtype=torch.float64)
+        dist.all_reduce(t, op={"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,
+                               "min": dist.ReduceOp.MIN}[op])
+        return float(t.item())
+
+    def broadcast_object(self, obj: Any, src: int = 0) -> Any:
+        if not self.pg_initialized:
+            return obj
+        lst = [obj]
+        dist.broadcast_object_list(lst, src=src)
+        return lst[0]
+
+    def all_gather_object(self, obj: Any) -> list:
+        if not self.pg_initialized:
+            return [obj]
+        out = [None] * self.world_size
+        dist.all_gather_object(out, obj)
+        return out
+
+    # --------------------------------------------------------------- data plane
+    def all_reduce(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        if self.world_size == 1:
+            return t
+        if t.is_cuda and self.comm is not None:
+            self.comm.all_reduce(t, op)
+        else:
+            if op == "avg":
+                dist.all_reduce(t, op=dist.ReduceOp.SUM)
+                t.div_(self.world_size)
+            else:
+                dist.all_reduce(t, op={"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,
+                                       "min": dist.ReduceOp.MIN}[op])
+        return t
+
+    def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        if self.world_size == 1:
+            return t
+        if t.is_cuda and self.comm is not None:
+            self.comm.broadcast(t, src)
+        else:
+            dist.broadcast(t, src=src)
+        return t
+
+    def all_gather(self, src: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:
+        if self.world_size == 1:
+            dst.copy_(src.reshape(dst.shape))
+            return dst
+        if src.is_cuda and self.comm is not None:
+            self.comm.all_gather(src, dst)
+        else:
+            dist.all_gather_into_tensor(dst, src)
+        return dst
+
+    def reduce_scatter(self, src: torch.Tensor, dst: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        if self.world_size == 1:
+            dst.copy_(src.reshape(dst.shape))
+            return dst
+        if src.is_cuda and self.comm is not None:
+            self.comm.reduce_scatter(src, dst, op)
+        else:
+            dist.reduce_scatter_tensor(dst, src, op=dist.ReduceOp.SUM)
+        return dst
+
+    def all_to_all(self, src: torch.Tensor, send_counts, dst: torch.Tensor, recv_counts) -> torch.Tensor:
+        send_counts = [int(c) for c in send_counts]
+        recv_counts = [int(c) for c in recv_counts]
+        if self.world_size == 1:
+            dst[: recv_counts[0]].copy_(src[: send_counts[0]])
+            return dst
+        if src.is_cuda and self.comm is not None:
+            self.comm.all_to_all(src, send_counts, dst, recv_counts)
+        else:
+            inner = src[0].numel() if src.dim() > 1 else 1
+            dist.all_to_all_single(dst, src, output_split_sizes=recv_counts,
+                                   input_split_sizes=send_counts)
+            del inner
+        return dst
+
+    def shutdown(self):
+        global _WORLD
+        self.comm = None
+        if self.pg_initialized and dist.is_initialized():
+            try:
+                dist.destroy_process_group()
+            except Exception:
+                pass
+        self.pg_initialized = False
+        if _WORLD is self:
+            _WORLD = None
+
+
+def _env_int(name: str, default: int) -> int:
+    v = os.environ.get(name)
+    return int(v) if v not in (None, "") else default
+
+
+def init(rank: Optional[int] = None, world_size: Optional[int] = None,
+         local_rank: Optional[int] = None, master_addr: Optional[str] = None,
+         master_port: Optional[int] = None, backend: str = "auto",
+         timeout_s: float = 600.0) -> World:
+    """Initialise (idempotently) the process world.
+
+    backend: "auto" -> "rccl" when a GPU is visible, else "gloo".
+    """
+    global _WORLD
+    if _WORLD is not None:
+        return _WORLD
+    rank = _env_int("RANK", 0) if rank is None else rank
+    world_size = _env_int("WORLD_SIZE", 1) if world_size is None else world_size
+    local_rank = _env_int("LOCAL_RANK", rank) if local_rank is None else local_rank
+    has_gpu = torch.cuda.is_available()
+    if backend == "auto":
+        backend = "rccl" if has_gpu else "gloo"
+    if backend == "rccl" and not has_gpu:
+        raise RuntimeError("backend 'rccl' requested but no GPU is visible")
+
+    if has_gpu and backend == "rccl":
+        ndev = torch.cuda.device_count()
+        torch.cuda.set_device(local_rank % max(ndev, 1))
+        device = torch.device("cuda", torch.cuda.current_device())
+    else:
+        device = torch.device("cpu")
+
+    w = World(rank=rank, world_size=world_size, local_rank=local_rank, device=device,
+              backend=backend if world_size > 1 else ("rccl" if device.type == "cuda" else "none"))
+    if world_size > 1:
+        if master_addr is not None:
+            os.environ["MASTER_ADDR"] = master_addr
+        if master_port is not None:
+            os.environ["MASTER_PORT"] = str(master_port)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if not dist.is_initialized():
+            dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world_size,
+                                    timeout=datetime.timedelta(seconds=timeout_s))
+        w.pg_initialized = True
+        if backend == "rccl":
+            from .. import _native
+
+            C = _native.load()
+            uid = C.rccl_unique_id() if rank == 0 else None
+            uid = w.broadcast_object(uid, 0)
+            w.comm = C.RcclComm(uid, world_size, rank)
+    _WORLD = w
+    return w
+
+
+def get_world() -> World:
+    return _WORLD if _WORLD is not None else init()
+
+
+def reset():
+    global _WORLD
+    if _WORLD is not None:
+        _WORLD.shutdown()
+    _WORLD = None

@@ -5,9 +5,12 @@ Metric/config from BASELINE.json: "samples/sec (whole node) MNIST MLP sync-SGD
 at 1/2/4/8 MI355X; step-time p50".  Per-GPU batch 100 (example.py:43),
 lr 0.0005, sigmoid hidden layer, softmax cross-entropy, plain SGD; bf16 MFMA
 compute with fp32 master weights; gradients all-reduced in bf16 over RCCL
-(BASELINE config #2).  Synthetic MNIST-shaped data (uint8 pixels, streamed
-from pinned host memory with one hipMemcpyAsync per step on a side stream),
-random-init weights.  Weak scaling: per-GPU batch fixed as N grows.
+(BASELINE config #2).  Synthetic MNIST-shaped data (uint8 pixels resident in
+pinned host memory, streamed to a device stage one 50-step chunk at a time by
+hipMemcpyAsync inside the chunk's hipGraph; --prefetch side double-buffers it
+on a side stream instead), random-init weights.  Weak scaling: per-GPU batch
+fixed as N grows.  Every timed step runs the full fwd + bwd + (all-reduce) +
+SGD update; nothing is skipped or cached.
 
     python bench.py --gpus N --steps K --warmup W
     (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
@@ -48,6 +51,7 @@ def main(argv=None):
     ap.add_argument("--grad-dtype", choices=["bf16", "fp32"], default="bf16")
     ap.add_argument("--act", choices=["sigmoid", "relu"], default="sigmoid")
     ap.add_argument("--train-examples", type=int, default=55000)
+    ap.add_argument("--prefetch", choices=["serial", "side"], default="serial")
     a = ap.parse_args(argv)
 
     world_size_env = int(os.environ.get("WORLD_SIZE", "1"))
@@ -64,7 +68,7 @@ def main(argv=None):
     trainer = FusedMLPTrainer(batch_size=a.batch, lr=a.lr, act=a.act, world=w, grad_dtype=gd,
                               device=dev)
     runner = MLPStepRunner(trainer, epoch, steps_per_graph=a.steps_per_graph,
-                           use_graph=not a.eager)
+                           use_graph=not a.eager, prefetch=a.prefetch)
 
     # warmup: eager first (module load), then the graphs the warmup itself needs
     runner.use_graph = False
@@ -118,7 +122,7 @@ def main(argv=None):
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16",
-            "data": "synthetic (MNIST-shaped uint8, pinned host -> hipMemcpyAsync side stream), random-init",
+            "data": "synthetic MNIST-shaped uint8, streamed per 50-step chunk pinned host -> device by hipMemcpyAsync; random-init weights",
             "config": {
                 "model": "mlp-784-100-10 (example.py)",
                 "global_batch": a.batch * n,
@@ -128,6 +132,7 @@ def main(argv=None):
                 "optimizer": f"sgd lr={a.lr}",
                 "grad_allreduce": a.grad_dtype if n > 1 else "none",
                 "hipgraph_steps": 0 if a.eager else a.steps_per_graph,
+                "input_prefetch": a.prefetch,
                 "activation": a.act,
             },
             "final_loss": round(float(m[0]), 5),

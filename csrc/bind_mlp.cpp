@@ -8,16 +8,19 @@
 #include <string>
 
 extern "C" {
-hipError_t dtfk_mlp_fwd_bwd(const void* x, int x_kind, const void* labels, int B, const void* W1T,
-                            const void* W2T, const float* params, void* xT, void* dz2T, int BP,
-                            float* partials, float inv_batch, int act, int naive_loss,
-                            hipStream_t stream);
-hipError_t dtfk_mlp_wgrad(const void* xT, const void* dz2T, int BP, int B, const float* partials,
-                          float* params, void* W1T, void* W2T, void* grads, int grad_kind,
-                          const float* lr, float* metrics, long long* gstep, int ring,
-                          hipStream_t stream);
+int dtfk_mlp_ksplit();
+hipError_t dtfk_mlp_l1_fwd(const void* x, int x_kind, int B, const void* W1T, float* z2p,
+                           long long* ts, hipStream_t stream);
+hipError_t dtfk_mlp_head_bwd(const float* a2, const void* labels, int B, const void* W2T,
+                             const void* W2N, const float* params, void* dz2T, int BP, float* partials,
+                             float inv_batch, int act, int naive_loss, long long* ts,
+                             hipStream_t stream);
+hipError_t dtfk_mlp_wgrad(const void* x, int x_kind, const void* dz2T, int BP, int B,
+                          const float* partials, float* params, void* W1T, void* W2T, void* W2N,
+                          void* grads, int grad_kind, const float* lr, float* metrics,
+                          long long* gstep, int ring, long long* ts, hipStream_t stream);
 hipError_t dtfk_mlp_apply_flat(float* params, const void* grads, int grad_kind, const float* lr,
-                               float scale, void* W1T, void* W2T, hipStream_t stream);
+                               float scale, void* W1T, void* W2T, void* W2N, hipStream_t stream);
 }
 
 namespace dtf {
@@ -39,46 +42,74 @@ static void need(const at::Tensor& t, at::ScalarType dt, int64_t numel, const ch
 
 constexpr int kNParam = 79510;
 
-// x_kind: 0 u8 pixels, 1 fp32, 2 bf16.  labels: uint8 class ids.
-void mlp_fwd_bwd(at::Tensor x, int64_t x_offset, int x_kind, at::Tensor labels,
-                 int64_t labels_offset, int B, at::Tensor W1T, at::Tensor W2T, at::Tensor params,
-                 at::Tensor xT, at::Tensor dz2T, int BP, at::Tensor partials, double inv_batch,
-                 int act, bool naive_loss) {
-  const int nb = (B + 15) / 16;
-  if (BP < nb * 16 || BP % 32) throw std::runtime_error("bad BP");
+static long long* ts_ptr(const c10::optional<at::Tensor>& ts, int64_t need_numel) {
+  if (!ts.has_value()) return nullptr;
+  need(*ts, at::kLong, need_numel, "ts");
+  return reinterpret_cast<long long*>(ts->data_ptr<int64_t>());
+}
+
+static int bp_of(int B) { return ((B + 31) / 32) * 32; }
+
+// x_kind: 0 u8 pixels (/255), 1 fp32, 2 bf16; rows of 784 features.
+static const char* x_ptr(const at::Tensor& x, int64_t off, int x_kind, int B) {
   const int64_t esz = x_kind == 0 ? 1 : (x_kind == 1 ? 4 : 2);
-  if (!x.is_cuda() || !labels.is_cuda()) throw std::runtime_error("x/labels must be on GPU");
-  if ((int64_t)x.numel() * x.element_size() < x_offset + (int64_t)B * 784 * esz)
+  if (x_kind < 0 || x_kind > 2) throw std::runtime_error("bad x_kind");
+  if (!x.is_cuda() || !x.is_contiguous()) throw std::runtime_error("x must be a contiguous GPU tensor");
+  if ((int64_t)x.numel() * x.element_size() < off + (int64_t)B * 784 * esz)
     throw std::runtime_error("x buffer too small");
-  if ((int64_t)labels.numel() * labels.element_size() < labels_offset + B)
-    throw std::runtime_error("labels buffer too small");
-  if ((x_offset % 16) != 0) throw std::runtime_error("x offset must be 16-byte aligned");
+  if (off % 16 != 0 || (reinterpret_cast<uintptr_t>(x.data_ptr()) % 16) != 0)
+    throw std::runtime_error("x must be 16-byte aligned");
+  return reinterpret_cast<const char*>(x.data_ptr()) + off;
+}
+
+// z2p: per-K-half partial pre-activations [ksplit][nb*16][112] fp32
+void mlp_l1_fwd(at::Tensor x, int64_t x_off, int x_kind, int B, at::Tensor W1T, at::Tensor z2p,
+                c10::optional<at::Tensor> ts) {
+  if (B <= 0) throw std::runtime_error("B must be positive");
+  const int nb = (B + 15) / 16;
+  const char* xb = x_ptr(x, x_off, x_kind, B);
   need(W1T, at::kBFloat16, 112 * 800, "W1T");
+  need(z2p, at::kFloat, (int64_t)dtfk_mlp_ksplit() * nb * 16 * 112, "z2p");
+  hip_check(dtfk_mlp_l1_fwd(xb, x_kind, B, W1T.data_ptr(), z2p.data_ptr<float>(),
+                            ts_ptr(ts, (int64_t)nb * 7 * dtfk_mlp_ksplit() * 16), cur_stream()),
+            "mlp_l1_fwd");
+}
+
+void mlp_head_bwd(at::Tensor z2p, at::Tensor labels, int64_t labels_off, int B, at::Tensor W2T,
+                  at::Tensor W2N, at::Tensor params, at::Tensor dz2T, at::Tensor partials, double inv_batch, int act,
+                  bool naive_loss, c10::optional<at::Tensor> ts) {
+  const int nb = (B + 15) / 16, BP = bp_of(B);
+  need(z2p, at::kFloat, (int64_t)dtfk_mlp_ksplit() * nb * 16 * 112, "z2p");
+  if (!labels.is_cuda() || labels.scalar_type() != at::kByte)
+    throw std::runtime_error("labels must be a uint8 GPU tensor");
+  if (labels.numel() < labels_off + B) throw std::runtime_error("labels buffer too small");
   need(W2T, at::kBFloat16, 16 * 128, "W2T");
+  need(W2N, at::kBFloat16, 112 * 32, "W2N");
   need(params, at::kFloat, kNParam, "params");
-  need(xT, at::kBFloat16, (int64_t)800 * BP, "xT");
   need(dz2T, at::kBFloat16, (int64_t)112 * BP, "dz2T");
   need(partials, at::kFloat, (int64_t)nb * 1112, "partials");
-  const char* xb = reinterpret_cast<const char*>(x.data_ptr()) + x_offset;
-  const char* lb = reinterpret_cast<const char*>(labels.data_ptr()) + labels_offset;
-  hip_check(dtfk_mlp_fwd_bwd(xb, x_kind, lb, B, W1T.data_ptr(), W2T.data_ptr(),
-                             params.data_ptr<float>(), xT.data_ptr(), dz2T.data_ptr(), BP,
-                             partials.data_ptr<float>(), (float)inv_batch, act, naive_loss ? 1 : 0,
-                             cur_stream()),
-            "mlp_fwd_bwd");
+  hip_check(dtfk_mlp_head_bwd(z2p.data_ptr<float>(),
+                              reinterpret_cast<const uint8_t*>(labels.data_ptr()) + labels_off, B,
+                              W2T.data_ptr(), W2N.data_ptr(), params.data_ptr<float>(), dz2T.data_ptr(), BP,
+                              partials.data_ptr<float>(), (float)inv_batch, act, naive_loss ? 1 : 0,
+                              ts_ptr(ts, (int64_t)nb * 16), cur_stream()),
+            "mlp_head_bwd");
 }
 
 // grad_kind: 0 fused SGD (grads ignored), 1 fp32 grads, 2 bf16 grads
-void mlp_wgrad(at::Tensor xT, at::Tensor dz2T, int BP, int B, at::Tensor partials,
-               at::Tensor params, at::Tensor W1T, at::Tensor W2T, c10::optional<at::Tensor> grads,
-               int grad_kind, at::Tensor lr, at::Tensor metrics, at::Tensor gstep) {
-  const int nb = (B + 15) / 16;
-  need(xT, at::kBFloat16, (int64_t)800 * BP, "xT");
+void mlp_wgrad(at::Tensor x, int64_t x_off, int x_kind, at::Tensor dz2T, int B,
+               at::Tensor partials, at::Tensor params, at::Tensor W1T, at::Tensor W2T,
+               at::Tensor W2N, c10::optional<at::Tensor> grads, int grad_kind, at::Tensor lr, at::Tensor metrics,
+               at::Tensor gstep, c10::optional<at::Tensor> ts) {
+  const int nb = (B + 15) / 16, BP = bp_of(B);
+  if (BP > 4096) throw std::runtime_error("per-GPU batch > 4096 not supported by mlp_wgrad");
+  const char* xb = x_ptr(x, x_off, x_kind, B);
   need(dz2T, at::kBFloat16, (int64_t)112 * BP, "dz2T");
   need(partials, at::kFloat, (int64_t)nb * 1112, "partials");
   need(params, at::kFloat, kNParam, "params");
   need(W1T, at::kBFloat16, 112 * 800, "W1T");
   need(W2T, at::kBFloat16, 16 * 128, "W2T");
+  need(W2N, at::kBFloat16, 112 * 32, "W2N");
   need(lr, at::kFloat, 1, "lr");
   need(metrics, at::kFloat, 2, "metrics");
   need(gstep, at::kLong, 1, "global_step");
@@ -89,16 +120,18 @@ void mlp_wgrad(at::Tensor xT, at::Tensor dz2T, int BP, int B, at::Tensor partial
     g = grads->data_ptr();
   }
   const int ring = (int)(metrics.numel() / 2);
-  hip_check(dtfk_mlp_wgrad(xT.data_ptr(), dz2T.data_ptr(), BP, B, partials.data_ptr<float>(),
-                           params.data_ptr<float>(), W1T.data_ptr(), W2T.data_ptr(), g, grad_kind,
+  hip_check(dtfk_mlp_wgrad(xb, x_kind, dz2T.data_ptr(), BP, B, partials.data_ptr<float>(),
+                           params.data_ptr<float>(), W1T.data_ptr(), W2T.data_ptr(),
+                           W2N.data_ptr(), g, grad_kind,
                            lr.data_ptr<float>(), metrics.data_ptr<float>(),
                            reinterpret_cast<long long*>(gstep.data_ptr<int64_t>()), ring,
-                           cur_stream()),
+                           ts_ptr(ts, (int64_t)(49 * 7 + 4) * 16), cur_stream()),
             "mlp_wgrad");
 }
 
 void mlp_apply_flat(at::Tensor params, c10::optional<at::Tensor> grads, at::Tensor lr,
-                    double scale, at::Tensor W1T, at::Tensor W2T) {
+                    double scale, at::Tensor W1T, at::Tensor W2T, at::Tensor W2N) {
+  need(W2N, at::kBFloat16, 112 * 32, "W2N");
   need(params, at::kFloat, kNParam, "params");
   need(lr, at::kFloat, 1, "lr");
   need(W1T, at::kBFloat16, 112 * 800, "W1T");
@@ -113,7 +146,8 @@ void mlp_apply_flat(at::Tensor params, c10::optional<at::Tensor> grads, at::Tens
     g = grads->data_ptr();
   }
   hip_check(dtfk_mlp_apply_flat(params.data_ptr<float>(), g, kind, lr.data_ptr<float>(),
-                                (float)scale, W1T.data_ptr(), W2T.data_ptr(), cur_stream()),
+                                (float)scale, W1T.data_ptr(), W2T.data_ptr(), W2N.data_ptr(),
+                                cur_stream()),
             "mlp_apply_flat");
 }
 
@@ -133,8 +167,18 @@ void memcpy_h2d_async(at::Tensor dst, int64_t dst_offset, at::Tensor src, int64_
 }
 
 void init_mlp(py::module& m) {
-  m.def("mlp_fwd_bwd", &mlp_fwd_bwd);
-  m.def("mlp_wgrad", &mlp_wgrad);
+  m.def("mlp_ksplit", &dtfk_mlp_ksplit);
+  m.def("mlp_l1_fwd", &mlp_l1_fwd, py::arg("x"), py::arg("x_offset"), py::arg("x_kind"),
+        py::arg("B"), py::arg("W1T"), py::arg("z2p"), py::arg("ts") = py::none());
+  m.def("mlp_head_bwd", &mlp_head_bwd, py::arg("z2p"), py::arg("labels"), py::arg("labels_offset"),
+        py::arg("B"), py::arg("W2T"), py::arg("W2N"), py::arg("params"), py::arg("dz2T"),
+        py::arg("partials"),
+        py::arg("inv_batch"), py::arg("act"), py::arg("naive_loss"), py::arg("ts") = py::none());
+  m.def("mlp_wgrad", &mlp_wgrad, py::arg("x"), py::arg("x_offset"), py::arg("x_kind"),
+        py::arg("dz2T"), py::arg("B"), py::arg("partials"), py::arg("params"), py::arg("W1T"),
+        py::arg("W2T"), py::arg("W2N"), py::arg("grads"), py::arg("grad_kind"), py::arg("lr"),
+        py::arg("metrics"),
+        py::arg("gstep"), py::arg("ts") = py::none());
   m.def("mlp_apply_flat", &mlp_apply_flat);
   m.def("memcpy_h2d_async", &memcpy_h2d_async);
 }

@@ -80,6 +80,36 @@ __device__ __forceinline__ float block_sum(float v, float* scratch) {
   return t;
 }
 
+// DPP row (16-lane) all-reduce: rotate-right by 8, 4, 2, 1 within each row of 16
+// lanes; every lane of the row ends with the result.  A few VALU cycles per
+// step instead of an LDS-latency ds_bpermute per __shfl.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL,
+                                                              0xF, 0xF, false));
+}
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, dpp_f<0x128>(v));
+  v = fmaxf(v, dpp_f<0x124>(v));
+  v = fmaxf(v, dpp_f<0x122>(v));
+  v = fmaxf(v, dpp_f<0x121>(v));
+  return v;
+}
+__device__ __forceinline__ float row16_min(float v) {
+  v = fminf(v, dpp_f<0x128>(v));
+  v = fminf(v, dpp_f<0x124>(v));
+  v = fminf(v, dpp_f<0x122>(v));
+  v = fminf(v, dpp_f<0x121>(v));
+  return v;
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f<0x128>(v);
+  v += dpp_f<0x124>(v);
+  v += dpp_f<0x122>(v);
+  v += dpp_f<0x121>(v);
+  return v;
+}
+
 __device__ __forceinline__ float sigmoidf_(float z) { return 1.f / (1.f + __expf(-z)); }
 
 }  // namespace dtfk

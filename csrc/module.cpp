@@ -6,6 +6,8 @@
 namespace dtf {
 void init_mlp(py::module& m);
 void init_comm(py::module& m);
+void init_tfrecord(py::module& m);
+void init_bundle(py::module& m);
 }  // namespace dtf
 
 PYBIND11_MODULE(_C, m) {
@@ -13,4 +15,6 @@ PYBIND11_MODULE(_C, m) {
   m.attr("ARCH") = "gfx950";
   dtf::init_mlp(m);
   dtf::init_comm(m);
+  dtf::init_tfrecord(m);
+  dtf::init_bundle(m);
 }

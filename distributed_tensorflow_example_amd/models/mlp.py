@@ -142,7 +142,9 @@ class FusedMLPTrainer:
         self.params = torch.zeros(NPARAM, dtype=torch.float32, device=dev)
         self.W1T = torch.zeros(112 * 800, dtype=bf, device=dev)
         self.W2T = torch.zeros(16 * 128, dtype=bf, device=dev)
-        self.xT = torch.zeros(800 * self.BP, dtype=bf, device=dev)
+        self.W2N = torch.zeros(112 * 32, dtype=bf, device=dev)
+        self.z2p = torch.zeros(self.C.mlp_ksplit() * self.nb * 16 * 112, dtype=torch.float32,
+                               device=dev)
         self.dz2T = torch.zeros(112 * self.BP, dtype=bf, device=dev)
         self.partials = torch.zeros(self.nb * 1112, dtype=torch.float32, device=dev)
         self.grad_dtype = grad_dtype
@@ -152,10 +154,6 @@ class FusedMLPTrainer:
         self.ring = int(metrics_ring)
         self.metrics = torch.zeros(self.ring * 2, dtype=torch.float32, device=dev)
         self.gstep = torch.zeros(1, dtype=torch.int64, device=dev)
-        from ..data.mnist import record_bytes
-
-        self.rec = record_bytes(B)
-        self.slots = [torch.zeros(self.rec, dtype=torch.uint8, device=dev) for _ in range(2)]
         self.set_params(init_params(seed))
 
     # ---------------------------------------------------------------- state
@@ -166,7 +164,7 @@ class FusedMLPTrainer:
         self.refresh_shadows()
 
     def refresh_shadows(self):
-        self.C.mlp_apply_flat(self.params, None, self.lr, 0.0, self.W1T, self.W2T)
+        self.C.mlp_apply_flat(self.params, None, self.lr, 0.0, self.W1T, self.W2T, self.W2N)
 
     def get_params(self) -> torch.Tensor:
         return self.params.detach().cpu()
@@ -188,128 +186,162 @@ class FusedMLPTrainer:
         return m[idx]
 
     # ----------------------------------------------------------------- steps
-    def compute(self, slot: torch.Tensor):
-        """Enqueue one training step reading batch record `slot` (device)."""
-        C = self.C
-        B = self.B
-        C.mlp_fwd_bwd(slot, 0, 0, slot, B * D_IN, B, self.W1T, self.W2T, self.params, self.xT,
-                      self.dz2T, self.BP, self.partials, 1.0 / B, self.act, self.naive)
-        self.after_fwd_bwd()
+    def enqueue_step(self, x: torch.Tensor, x_off: int, x_kind: int, labels: torch.Tensor,
+                     labels_off: int):
+        """Enqueue one full training step on the current stream.
 
-    def after_fwd_bwd(self):
-        C = self.C
+        x: device buffer holding B rows of 784 features at byte offset x_off
+        (kind 0 uint8 pixels, 1 fp32, 2 bf16); labels: uint8 class ids.
+        """
+        C, B = self.C, self.B
+        C.mlp_l1_fwd(x, x_off, x_kind, B, self.W1T, self.z2p)
+        C.mlp_head_bwd(self.z2p, labels, labels_off, B, self.W2T, self.W2N, self.params, self.dz2T,
+                       self.partials, 1.0 / B, self.act, self.naive)
         if self.world_size == 1:
-            C.mlp_wgrad(self.xT, self.dz2T, self.BP, self.B, self.partials, self.params, self.W1T,
-                        self.W2T, None, 0, self.lr, self.metrics, self.gstep)
+            C.mlp_wgrad(x, x_off, x_kind, self.dz2T, B, self.partials, self.params, self.W1T,
+                        self.W2T, self.W2N, None, 0, self.lr, self.metrics, self.gstep)
         else:
             kind = 1 if self.grad_dtype == torch.float32 else 2
-            C.mlp_wgrad(self.xT, self.dz2T, self.BP, self.B, self.partials, self.params, self.W1T,
-                        self.W2T, self.grads, kind, self.lr, self.metrics, self.gstep)
+            C.mlp_wgrad(x, x_off, x_kind, self.dz2T, B, self.partials, self.params, self.W1T,
+                        self.W2T, self.W2N, self.grads, kind, self.lr, self.metrics, self.gstep)
             self.world.comm.all_reduce(self.grads, "sum")
             C.mlp_apply_flat(self.params, self.grads, self.lr, 1.0 / self.world_size, self.W1T,
-                             self.W2T)
+                             self.W2T, self.W2N)
 
     def step_tensors(self, x: torch.Tensor, labels: torch.Tensor):
-        """Eager step on device tensors (x: uint8/fp32/bf16 [B,784], labels uint8 [B])."""
+        """Eager step on device tensors (x: uint8/fp32/bf16 [B,784], labels [B])."""
         kind = {torch.uint8: 0, torch.float32: 1, torch.bfloat16: 2}[x.dtype]
-        x = x.contiguous()
-        lab = labels.to(torch.uint8).contiguous()
-        self.C.mlp_fwd_bwd(x, 0, kind, lab, 0, self.B, self.W1T, self.W2T, self.params, self.xT,
-                           self.dz2T, self.BP, self.partials, 1.0 / self.B, self.act, self.naive)
-        self.after_fwd_bwd()
+        self.enqueue_step(x.contiguous(), 0, kind, labels.to(torch.uint8).contiguous(), 0)
 
 
 class MLPStepRunner:
     """Drives `FusedMLPTrainer` over a pinned-host epoch.
 
-    Per step: side stream -- hipMemcpyAsync of batch i+1 (pinned -> device
-    double buffer) once step i-1 has consumed that slot; main stream -- wait
-    for batch i, fwd/bwd kernel, wgrad(+SGD | all-reduce + apply).  `g` such
-    steps are captured into one hipGraph (keyed by first batch index) and
-    replayed, so the host issues one launch per `g` steps.
+    The epoch lives batch-major in pinned host memory; the device holds only a
+    *chunk* stage of `g` batches (g*78.5 KB at B=100).  Each chunk is one
+    hipGraph: hipMemcpyAsync(chunk, pinned -> stage) followed by the `g` fused
+    steps; the host issues one launch per `g` steps.
+
+    prefetch="serial" (default): the copy is a node at the head of the chunk
+        graph on the compute stream (+1.7 us/step amortised: 85 us per 3.9 MB
+        chunk at PCIe rate).
+    prefetch="side": double-buffered stage, the next chunk is copied on a side
+        stream under the current replay, synchronised by events.  On MI355X /
+        ROCm 7 every cross-queue event dependency costs ~150 us of GPU idle
+        (measured, scripts/diag_mlp3.py: 14.9 us/step vs 13.2 serial; the same
+        fork/join captured inside the graph: 16.4), so it only pays where
+        cross-queue waits are cheap.
     """
 
     def __init__(self, trainer: FusedMLPTrainer, epoch, steps_per_graph: int = 50,
-                 use_graph: bool = True):
+                 use_graph: bool = True, prefetch: str = "serial"):
+        if prefetch not in ("serial", "side"):
+            raise ValueError("prefetch must be 'serial' or 'side'")
         self.t = trainer
         self.epoch = epoch
-        self.g = int(steps_per_graph)
+        self.g = int(min(steps_per_graph, epoch.num_batches))
         self.use_graph = use_graph
+        self.prefetch = prefetch
         self.side = torch.cuda.Stream(device=trainer.device)
-        self.graphs: Dict[Tuple[int, int], torch.cuda.CUDAGraph] = {}
-        self.cursor = 0  # next batch index (global, mod num_batches)
+        self.graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
+        nbuf = 2 if prefetch == "side" else 1
+        self.stage = [torch.zeros(self.g * epoch.rec, dtype=torch.uint8, device=trainer.device)
+                      for _ in range(nbuf)]
+        self.cursor = 0        # next batch index (global)
+        self.parity = 0        # (side) stage buffer holding the chunk at `cursor`
+        self.loaded = None     # (side) (b0, g) resident in stage[parity]
+        self._freed = None     # (side) event: last replay reading stage[parity ^ 1] done
 
-    def _emit(self, b0: int, g: int):
-        t, C, ep = self.t, self.t.C, self.epoch
-        main = torch.cuda.current_stream()
-        side = self.side
-        start = torch.cuda.Event()
-        start.record(main)
-        copied = [torch.cuda.Event() for _ in range(g)]
-        consumed = [torch.cuda.Event() for _ in range(g)]
-        nbytes = ep.rec
+    def _copy_chunk(self, dst: torch.Tensor, b0: int, g: int):
+        ep = self.epoch
+        self.t.C.memcpy_h2d_async(dst, 0, ep.host, b0 * ep.rec, g * ep.rec)
 
-        def copy(i):
-            b = (b0 + i) % ep.num_batches
-            C.memcpy_h2d_async(t.slots[i % 2], 0, ep.host, b * ep.rec, nbytes)
-
-        with torch.cuda.stream(side):
-            side.wait_event(start)
-            copy(0)
-            copied[0].record(side)
+    def _emit_steps(self, g: int, buf: torch.Tensor):
+        t = self.t
+        rec, B = self.epoch.rec, t.B
         for i in range(g):
-            if i + 1 < g:
-                with torch.cuda.stream(side):
-                    if i >= 1:
-                        side.wait_event(consumed[i - 1])
-                    copy(i + 1)
-                    copied[i + 1].record(side)
-            main.wait_event(copied[i])
-            slot = t.slots[i % 2]
-            B = t.B
-            C.mlp_fwd_bwd(slot, 0, 0, slot, B * D_IN, B, t.W1T, t.W2T, t.params, t.xT, t.dz2T,
-                          t.BP, t.partials, 1.0 / B, t.act, t.naive)
-            consumed[i].record(main)
-            t.after_fwd_bwd()
+            off = i * rec
+            t.enqueue_step(buf, off, 0, buf, off + B * D_IN)
 
-    def _graph(self, b0: int, g: int) -> torch.cuda.CUDAGraph:
-        key = (b0, g)
+    def _emit(self, key):
+        if self.prefetch == "serial":
+            b0, g = key
+            self._copy_chunk(self.stage[0], b0, g)
+            self._emit_steps(g, self.stage[0])
+        else:
+            g, par = key
+            self._emit_steps(g, self.stage[par])
+
+    def _graph(self, key) -> torch.cuda.CUDAGraph:
         gr = self.graphs.get(key)
         if gr is None:
             torch.cuda.synchronize()
             gr = torch.cuda.CUDAGraph()
             s = torch.cuda.Stream(device=self.t.device)
             with torch.cuda.graph(gr, stream=s):
-                self._emit(b0, g)
+                self._emit(key)
             torch.cuda.synchronize()
             self.graphs[key] = gr
         return gr
 
-    def plan(self, steps: int) -> List[Tuple[int, int]]:
-        out, cur, left = [], self.cursor, steps
+    def _chunks(self, cursor: int, steps: int) -> List[Tuple[int, int]]:
+        out, left = [], steps
         nb = self.epoch.num_batches
         while left > 0:
-            b0 = cur % nb
+            b0 = cursor % nb
             g = min(self.g, left, nb - b0)
             out.append((b0, g))
-            cur += g
+            cursor += g
             left -= g
         return out
+
+    def plan(self, steps: int):
+        """[(b0, g, parity, next)] for the next `steps` steps from the cursor."""
+        ch = self._chunks(self.cursor, steps)
+        after = self._chunks(self.cursor + steps, self.g)[0]  # speculative prefetch
+        out, par = [], self.parity
+        for j, (b0, g) in enumerate(ch):
+            nxt = ch[j + 1] if j + 1 < len(ch) else after
+            out.append((b0, g, par, nxt))
+            par ^= 1
+        return out
+
+    def _key(self, b0, g, par):
+        return (b0, g) if self.prefetch == "serial" else (g, par)
 
     def prepare(self, steps: int):
         """Capture every graph `run(steps)` will need (keeps capture out of timing)."""
         if self.use_graph:
-            for b0, g in self.plan(steps):
-                self._graph(b0, g)
+            for (b0, g, par, _) in self.plan(steps):
+                self._graph(self._key(b0, g, par))
 
     def run(self, steps: int, events: Optional[list] = None):
-        for b0, g in self.plan(steps):
+        main = torch.cuda.current_stream()
+        for (b0, g, par, nxt) in self.plan(steps):
+            key = self._key(b0, g, par)
+            if self.prefetch == "side" and self.loaded != (b0, g):  # cold start / plan change
+                self._copy_chunk(self.stage[par], b0, g)
+                self._freed = None
             if self.use_graph:
-                self._graph(b0, g).replay()
+                self._graph(key).replay()
             else:
-                self._emit(b0, g)
+                self._emit(key)
             if events is not None:
                 ev = torch.cuda.Event(enable_timing=True)
-                ev.record()
+                ev.record(main)
                 events.append((ev, g))
+            if self.prefetch == "side":
+                # next chunk into the other buffer, behind the end of the replay that
+                # last read it; fresh events (no re-record with pending waits)
+                ev_copy = torch.cuda.Event()
+                if self._freed is not None:
+                    self.side.wait_event(self._freed)
+                with torch.cuda.stream(self.side):
+                    self._copy_chunk(self.stage[par ^ 1], nxt[0], nxt[1])
+                ev_copy.record(self.side)
+                self._freed = torch.cuda.Event()
+                self._freed.record(main)
+                main.wait_event(ev_copy)
+                self.parity = par ^ 1
+                self.loaded = nxt
             self.cursor += g

@@ -29,7 +29,7 @@ rc=$?; tail -1 $OUT/bench_eager.log
 
 if [ "${SKIP_PROF:-0}" != "1" ]; then
   rm -rf $OUT/prof
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python3 bench.py --steps 1000 --warmup 200 > $OUT/prof.log 2>&1
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv rocpd -d $OUT/prof -o run -- python3 bench.py --steps 1000 --warmup 200 > $OUT/prof.log 2>&1
   rc=$?; tail -2 $OUT/prof.log
   [ $rc -ne 0 ] && { echo "prof rc=$rc"; exit $rc; }
   find $OUT/prof -name "*stats*" | head

@@ -21,7 +21,7 @@ def _ref(flat, x_u8, labels, act="sigmoid"):
     return mlp.reference_loss_and_grad(f, x, labels, act)
 
 
-@pytest.mark.parametrize("B", [100, 16, 37, 256])
+@pytest.mark.parametrize("B", [100, 16, 37, 256, 1000])
 @pytest.mark.parametrize("act", ["sigmoid", "relu"])
 def test_fused_step_matches_reference(native, B, act):
     torch.manual_seed(0)
@@ -58,16 +58,16 @@ def test_grad_mode_and_apply(native):
     y = torch.from_numpy(labels).to(dev)
     grads = torch.zeros(mlp.NPARAM, dtype=torch.float32, device=dev)
     C = native
-    C.mlp_fwd_bwd(x, 0, 0, y, 0, B, tr.W1T, tr.W2T, tr.params, tr.xT, tr.dz2T, tr.BP,
-                  tr.partials, 1.0 / B, 0, False)
-    C.mlp_wgrad(tr.xT, tr.dz2T, tr.BP, B, tr.partials, tr.params, tr.W1T, tr.W2T, grads, 1,
+    C.mlp_l1_fwd(x, 0, 0, B, tr.W1T, tr.z2p)
+    C.mlp_head_bwd(tr.z2p, y, 0, B, tr.W2T, tr.W2N, tr.params, tr.dz2T, tr.partials, 1.0 / B, 0, False)
+    C.mlp_wgrad(x, 0, 0, tr.dz2T, B, tr.partials, tr.params, tr.W1T, tr.W2T, tr.W2N, grads, 1,
                 tr.lr, tr.metrics, tr.gstep)
     torch.cuda.synchronize()
     _, _, g = _ref(p0, torch.from_numpy(imgs), torch.from_numpy(labels))
     assert (grads.cpu() - g).abs().max().item() < 2e-2 * g.abs().max().item() + 1e-4
     # params untouched in grad mode
     assert torch.equal(tr.get_params(), p0)
-    C.mlp_apply_flat(tr.params, grads, tr.lr, 0.5, tr.W1T, tr.W2T)
+    C.mlp_apply_flat(tr.params, grads, tr.lr, 0.5, tr.W1T, tr.W2T, tr.W2N)
     torch.cuda.synchronize()
     ref = p0 - 0.05 * 0.5 * grads.cpu()
     assert torch.allclose(tr.get_params(), ref, atol=1e-6)
@@ -104,3 +104,18 @@ def test_training_converges(native):
     m = tr.read_metrics(0, 1000)
     assert m[-50:, 0].mean() < m[:50, 0].mean() * 0.5
     assert m[-50:, 1].mean() > 0.8
+
+
+@pytest.mark.parametrize("kind", [torch.float32, torch.bfloat16])
+def test_float_inputs(native, kind):
+    B = 64
+    imgs, labels = synthetic_mnist(B, seed=9)
+    dev = torch.device("cuda")
+    tr = mlp.FusedMLPTrainer(batch_size=B, lr=0.1, device=dev)
+    p0 = tr.get_params().clone()
+    x = (torch.from_numpy(imgs).float() / 255.0).to(kind).to(dev)
+    tr.step_tensors(x, torch.from_numpy(labels).to(dev))
+    torch.cuda.synchronize()
+    _, _, g = _ref(p0, torch.from_numpy(imgs), torch.from_numpy(labels))
+    g_k = (p0 - tr.get_params()) / 0.1
+    assert ((g_k - g).norm() / g.norm()).item() < 2e-2

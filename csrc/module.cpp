@@ -8,6 +8,9 @@ void init_mlp(py::module& m);
 void init_comm(py::module& m);
 void init_tfrecord(py::module& m);
 void init_bundle(py::module& m);
+void init_store(py::module& m);
+void init_queue(py::module& m);
+void init_libsvm(py::module& m);
 }  // namespace dtf
 
 PYBIND11_MODULE(_C, m) {
@@ -17,4 +20,7 @@ PYBIND11_MODULE(_C, m) {
   dtf::init_comm(m);
   dtf::init_tfrecord(m);
   dtf::init_bundle(m);
+  dtf::init_store(m);
+  dtf::init_queue(m);
+  dtf::init_libsvm(m);
 }

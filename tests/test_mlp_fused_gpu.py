@@ -119,3 +119,37 @@ def test_float_inputs(native, kind):
     _, _, g = _ref(p0, torch.from_numpy(imgs), torch.from_numpy(labels))
     g_k = (p0 - tr.get_params()) / 0.1
     assert ((g_k - g).norm() / g.norm()).item() < 2e-2
+
+
+def test_grad_mode_with_rccl_comm_in_graph(native):
+    """GRAD mode (wgrad -> RCCL all-reduce -> flat SGD) on a 1-rank RCCL
+    communicator, eager and hipGraph-captured: the multi-GPU code path."""
+    from distributed_tensorflow_example_amd.parallel.world import World
+
+    dev = torch.device("cuda")
+    comm = native.RcclComm(native.rccl_unique_id(), 1, 0)
+    w = World(rank=0, world_size=1, device=dev, backend="rccl", comm=comm)
+    B = 100
+    imgs, labels = synthetic_mnist(2000, seed=13)
+    ep = PinnedEpoch(imgs, labels, B)
+    res = []
+    for grad_dtype in (torch.float32, torch.bfloat16):
+        for use_graph in (False, True):
+            tr = mlp.FusedMLPTrainer(batch_size=B, lr=0.01, device=dev, world=w,
+                                     grad_dtype=grad_dtype)
+            tr.world_size = 2  # force GRAD mode: all-reduce(sum) over 1 rank, scale 1/2
+            tr.grads = torch.zeros(mlp.NPARAM, dtype=grad_dtype, device=dev)
+            r = mlp.MLPStepRunner(tr, ep, steps_per_graph=5, use_graph=use_graph)
+            r.run(10)
+            torch.cuda.synchronize()
+            res.append(tr.get_params())
+            assert tr.global_step == 10
+    # eager == graph for each grad dtype
+    assert torch.equal(res[0], res[1])
+    assert torch.equal(res[2], res[3])
+    # fp32-grad DP path with lr scaled by 1/world == fused path at lr/2
+    tr = mlp.FusedMLPTrainer(batch_size=B, lr=0.005, device=dev)
+    r = mlp.MLPStepRunner(tr, ep, steps_per_graph=5, use_graph=False)
+    r.run(10)
+    torch.cuda.synchronize()
+    assert torch.allclose(tr.get_params(), res[0], atol=1e-5)

@@ -1,0 +1,208 @@
+// Python bindings for the generic op / optimizer kernels (csrc/kernels/gemm.hip, ops.hip).
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+#include <stdexcept>
+#include <string>
+
+extern "C" {
+hipError_t dtfk_gemm(const void* A, int a_bf16, int lda, int transA, const void* B, int b_bf16, int ldb,
+                     int transB, void* C, int c_bf16, int ldc, float* Z, const float* bias, int M, int N,
+                     int K, float alpha, float beta, int act, hipStream_t stream);
+hipError_t dtfk_act_backward(const float* dy, const float* y, const float* z, float* dz, int64_t n, int act,
+                             hipStream_t s);
+hipError_t dtfk_col_sum(const float* X, float* out, int M, int N, hipStream_t s);
+hipError_t dtfk_softmax_xent(const float* logits, const int64_t* labels, const float* ydense, float* loss_rows,
+                             float* grad, int64_t* correct, int B, int C, float grad_scale, int naive,
+                             hipStream_t s);
+hipError_t dtfk_sigmoid_xent(const float* x, const float* t, float* loss, float* grad, int64_t n,
+                             float grad_scale, hipStream_t s);
+hipError_t dtfk_embedding_bag_fwd(const float* W, int64_t V, int D, const int64_t* ids, const int64_t* offsets,
+                                  const float* psw, int B, int mode, float* out, int64_t* bad, hipStream_t s);
+hipError_t dtfk_embedding_bag_bwd(float* target, int64_t V, int D, const int64_t* ids, const int64_t* offsets,
+                                  const float* psw, const float* dout, int B, int mode, float lr,
+                                  hipStream_t s);
+hipError_t dtfk_argmax_correct(const float* x, const int64_t* labels, int B, int C, int64_t* count,
+                               hipStream_t s);
+hipError_t dtfk_auc_hist(const float* pred, const float* label, int64_t n, int nbins, unsigned long long* pos,
+                         unsigned long long* neg, hipStream_t s);
+hipError_t dtfk_multi_tensor_apply(const void* tab, const void* chunks, int nchunks, int kind, int gbf,
+                                   const float* lr_ptr, float lr, float gscale, float wd, float b1, float b2,
+                                   float eps, float momentum, int nesterov, const long long* step,
+                                   hipStream_t s);
+hipError_t dtfk_multi_tensor_sumsq(const void* tab, const void* chunks, int nchunks, int gbf, float* out,
+                                   hipStream_t s);
+int dtfk_mt_chunk();
+int dtfk_tensor_rec_bytes();
+}
+
+namespace dtf {
+
+static hipStream_t cs() { return c10::hip::getCurrentHIPStream().stream(); }
+static void ck(hipError_t e, const char* w) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(w) + ": " + hipGetErrorString(e));
+}
+static void gpu(const at::Tensor& t, const char* n) {
+  if (!t.is_cuda()) throw std::runtime_error(std::string(n) + " must be a GPU tensor");
+}
+static void f32c(const at::Tensor& t, const char* n) {
+  gpu(t, n);
+  if (t.scalar_type() != at::kFloat) throw std::runtime_error(std::string(n) + " must be float32");
+  if (!t.is_contiguous()) throw std::runtime_error(std::string(n) + " must be contiguous");
+}
+static void i64c(const at::Tensor& t, const char* n) {
+  gpu(t, n);
+  if (t.scalar_type() != at::kLong) throw std::runtime_error(std::string(n) + " must be int64");
+  if (!t.is_contiguous()) throw std::runtime_error(std::string(n) + " must be contiguous");
+}
+template <typename T>
+static T* opt_ptr(const c10::optional<at::Tensor>& t) {
+  return t.has_value() ? t->data_ptr<T>() : nullptr;
+}
+
+// out = act(alpha * op(A) @ op(B) + bias) (+ beta * out); Z (optional) gets the pre-activation.
+void gemm(at::Tensor A, bool transA, at::Tensor B, bool transB, at::Tensor out,
+          c10::optional<at::Tensor> bias, int act, double alpha, double beta, c10::optional<at::Tensor> Z) {
+  gpu(A, "A"); gpu(B, "B"); gpu(out, "out");
+  if (A.dim() != 2 || B.dim() != 2 || out.dim() != 2) throw std::runtime_error("gemm operands must be 2-D");
+  if (A.stride(1) != 1 || B.stride(1) != 1 || out.stride(1) != 1)
+    throw std::runtime_error("gemm operands must have unit inner stride");
+  auto dt_ok = [](const at::Tensor& t) { return t.scalar_type() == at::kFloat || t.scalar_type() == at::kBFloat16; };
+  if (!dt_ok(A) || !dt_ok(B) || !dt_ok(out)) throw std::runtime_error("gemm supports float32/bfloat16");
+  const int M = (int)(transA ? A.size(1) : A.size(0));
+  const int K = (int)(transA ? A.size(0) : A.size(1));
+  const int KB = (int)(transB ? B.size(1) : B.size(0));
+  const int N = (int)(transB ? B.size(0) : B.size(1));
+  if (K != KB) throw std::runtime_error("gemm inner dimensions differ");
+  if (out.size(0) != M || out.size(1) != N) throw std::runtime_error("gemm out has wrong shape");
+  if (bias.has_value()) { f32c(*bias, "bias"); if (bias->numel() != N) throw std::runtime_error("bias size"); }
+  if (Z.has_value()) { f32c(*Z, "Z"); if (Z->size(0) != M || Z->size(1) != N) throw std::runtime_error("Z shape"); }
+  ck(dtfk_gemm(A.data_ptr(), A.scalar_type() == at::kBFloat16, (int)A.stride(0), transA, B.data_ptr(),
+               B.scalar_type() == at::kBFloat16, (int)B.stride(0), transB, out.data_ptr(),
+               out.scalar_type() == at::kBFloat16, (int)out.stride(0), opt_ptr<float>(Z), opt_ptr<float>(bias),
+               M, N, K, (float)alpha, (float)beta, act, cs()),
+     "gemm");
+}
+
+void act_backward(at::Tensor dy, c10::optional<at::Tensor> y, c10::optional<at::Tensor> z, at::Tensor dz,
+                  int act) {
+  f32c(dy, "dy"); f32c(dz, "dz");
+  if (y.has_value()) f32c(*y, "y");
+  if (z.has_value()) f32c(*z, "z");
+  ck(dtfk_act_backward(dy.data_ptr<float>(), opt_ptr<float>(y), opt_ptr<float>(z), dz.data_ptr<float>(),
+                       dy.numel(), act, cs()),
+     "act_backward");
+}
+
+void col_sum(at::Tensor X, at::Tensor out) {
+  f32c(X, "X"); f32c(out, "out");
+  const int N = (int)X.size(-1);
+  const int M = (int)(X.numel() / std::max<int64_t>(1, N));
+  ck(dtfk_col_sum(X.data_ptr<float>(), out.data_ptr<float>(), M, N, cs()), "col_sum");
+}
+
+void softmax_xent(at::Tensor logits, c10::optional<at::Tensor> labels, c10::optional<at::Tensor> ydense,
+                  at::Tensor loss_rows, c10::optional<at::Tensor> grad, c10::optional<at::Tensor> correct,
+                  double grad_scale, bool naive) {
+  f32c(logits, "logits"); f32c(loss_rows, "loss_rows");
+  const int B = (int)logits.size(0), C = (int)logits.size(1);
+  if (labels.has_value()) i64c(*labels, "labels");
+  if (ydense.has_value()) f32c(*ydense, "ydense");
+  if (!labels.has_value() && !ydense.has_value()) throw std::runtime_error("labels or ydense required");
+  if (grad.has_value()) f32c(*grad, "grad");
+  if (correct.has_value()) i64c(*correct, "correct");
+  ck(dtfk_softmax_xent(logits.data_ptr<float>(), opt_ptr<int64_t>(labels), opt_ptr<float>(ydense),
+                       loss_rows.data_ptr<float>(), opt_ptr<float>(grad), opt_ptr<int64_t>(correct), B, C,
+                       (float)grad_scale, naive ? 1 : 0, cs()),
+     "softmax_xent");
+}
+
+void sigmoid_xent(at::Tensor x, at::Tensor t, at::Tensor loss, c10::optional<at::Tensor> grad, double gs) {
+  f32c(x, "x"); f32c(t, "t"); f32c(loss, "loss");
+  if (grad.has_value()) f32c(*grad, "grad");
+  ck(dtfk_sigmoid_xent(x.data_ptr<float>(), t.data_ptr<float>(), loss.data_ptr<float>(), opt_ptr<float>(grad),
+                       x.numel(), (float)gs, cs()),
+     "sigmoid_xent");
+}
+
+void embedding_bag_fwd(at::Tensor W, at::Tensor ids, at::Tensor offsets, c10::optional<at::Tensor> psw, int mode,
+                       at::Tensor out, c10::optional<at::Tensor> bad) {
+  f32c(W, "weight"); i64c(ids, "ids"); i64c(offsets, "offsets"); f32c(out, "out");
+  if (psw.has_value()) f32c(*psw, "per_sample_weights");
+  if (bad.has_value()) i64c(*bad, "bad");
+  const int B = (int)offsets.numel() - 1;
+  const int D = W.dim() == 1 ? 1 : (int)W.size(1);
+  ck(dtfk_embedding_bag_fwd(W.data_ptr<float>(), W.size(0), D, ids.data_ptr<int64_t>(),
+                            offsets.data_ptr<int64_t>(), opt_ptr<float>(psw), B, mode, out.data_ptr<float>(),
+                            opt_ptr<int64_t>(bad), cs()),
+     "embedding_bag_fwd");
+}
+
+void embedding_bag_bwd(at::Tensor target, at::Tensor ids, at::Tensor offsets, c10::optional<at::Tensor> psw,
+                       at::Tensor dout, int mode, double lr) {
+  f32c(target, "target"); i64c(ids, "ids"); i64c(offsets, "offsets"); f32c(dout, "dout");
+  if (psw.has_value()) f32c(*psw, "per_sample_weights");
+  const int B = (int)offsets.numel() - 1;
+  const int D = target.dim() == 1 ? 1 : (int)target.size(1);
+  ck(dtfk_embedding_bag_bwd(target.data_ptr<float>(), target.size(0), D, ids.data_ptr<int64_t>(),
+                            offsets.data_ptr<int64_t>(), opt_ptr<float>(psw), dout.data_ptr<float>(), B, mode,
+                            (float)lr, cs()),
+     "embedding_bag_bwd");
+}
+
+void argmax_correct(at::Tensor x, at::Tensor labels, at::Tensor count) {
+  f32c(x, "x"); i64c(labels, "labels"); i64c(count, "count");
+  ck(dtfk_argmax_correct(x.data_ptr<float>(), labels.data_ptr<int64_t>(), (int)x.size(0), (int)x.size(1),
+                         count.data_ptr<int64_t>(), cs()),
+     "argmax_correct");
+}
+
+void auc_hist(at::Tensor pred, at::Tensor label, at::Tensor pos, at::Tensor neg) {
+  f32c(pred, "pred"); f32c(label, "label"); i64c(pos, "pos"); i64c(neg, "neg");
+  ck(dtfk_auc_hist(pred.data_ptr<float>(), label.data_ptr<float>(), pred.numel(), (int)pos.numel(),
+                   reinterpret_cast<unsigned long long*>(pos.data_ptr<int64_t>()),
+                   reinterpret_cast<unsigned long long*>(neg.data_ptr<int64_t>()), cs()),
+     "auc_hist");
+}
+
+void multi_tensor_apply(at::Tensor tab, at::Tensor chunks, int kind, bool grad_bf16,
+                        c10::optional<at::Tensor> lr_t, double lr, double gscale, double wd, double b1,
+                        double b2, double eps, double momentum, bool nesterov, c10::optional<at::Tensor> step) {
+  gpu(tab, "table"); gpu(chunks, "chunks");
+  if (lr_t.has_value()) f32c(*lr_t, "lr");
+  if (step.has_value()) i64c(*step, "step");
+  ck(dtfk_multi_tensor_apply(tab.data_ptr(), chunks.data_ptr(), (int)chunks.size(0), kind, grad_bf16 ? 1 : 0,
+                             opt_ptr<float>(lr_t), (float)lr, (float)gscale, (float)wd, (float)b1, (float)b2,
+                             (float)eps, (float)momentum, nesterov ? 1 : 0,
+                             step.has_value() ? reinterpret_cast<const long long*>(step->data_ptr<int64_t>()) : nullptr,
+                             cs()),
+     "multi_tensor_apply");
+}
+
+void multi_tensor_sumsq(at::Tensor tab, at::Tensor chunks, bool grad_bf16, at::Tensor out) {
+  gpu(tab, "table"); gpu(chunks, "chunks"); f32c(out, "out");
+  ck(dtfk_multi_tensor_sumsq(tab.data_ptr(), chunks.data_ptr(), (int)chunks.size(0), grad_bf16 ? 1 : 0,
+                             out.data_ptr<float>(), cs()),
+     "multi_tensor_sumsq");
+}
+
+void init_ops(py::module& m) {
+  m.def("gemm", &gemm, py::arg("A"), py::arg("transA"), py::arg("B"), py::arg("transB"), py::arg("out"),
+        py::arg("bias") = py::none(), py::arg("act") = 0, py::arg("alpha") = 1.0, py::arg("beta") = 0.0,
+        py::arg("Z") = py::none());
+  m.def("act_backward", &act_backward);
+  m.def("col_sum", &col_sum);
+  m.def("softmax_xent", &softmax_xent);
+  m.def("sigmoid_xent", &sigmoid_xent);
+  m.def("embedding_bag_fwd", &embedding_bag_fwd);
+  m.def("embedding_bag_bwd", &embedding_bag_bwd);
+  m.def("argmax_correct", &argmax_correct);
+  m.def("auc_hist", &auc_hist);
+  m.def("multi_tensor_apply", &multi_tensor_apply);
+  m.def("multi_tensor_sumsq", &multi_tensor_sumsq);
+  m.def("mt_chunk", &dtfk_mt_chunk);
+  m.def("tensor_rec_bytes", &dtfk_tensor_rec_bytes);
+}
+
+}  // namespace dtf

@@ -1,0 +1,191 @@
+// Generic bf16-MFMA GEMM with a fused epilogue: C = act(alpha * op(A) op(B) + bias)
+//
+// Backs `ops.linear_act` (forward: bias + {none, relu, sigmoid, tanh, gelu}),
+// its backward GEMMs (dX = dZ W^T with transB, dW = X^T dZ with transA) and the
+// dense layers of the Wide&Deep / BERT / ResNet heads.  The reference graph's
+// matmul + bias + sigmoid (example.py:95-97) is exactly this op.
+//
+// Tiling for CDNA4: 256-thread workgroup = 4 waves (2x2), 64x64 output tile,
+// each wave 32x32 = 2x2 MFMA 16x16x32 bf16 tiles, K-step 32.  Operands are
+// read in any of fp32 / bf16 with any transpose, converted to bf16 and staged
+// in LDS as [row][k] (A) and [col][k] (B) with a +8 element pad so every MFMA
+// fragment is one conflict-free 16-byte ds_read.  Global loads are branch-free
+// (clamped addresses + masks; see mlp_step.hip for why) and the next K-tile is
+// prefetched into registers while the current one is multiplied.  Block ids
+// are remapped so consecutive tiles of one output row band land on one XCD
+// (shared A panel in that XCD's L2).
+#include "common.h"
+
+namespace dtfk {
+namespace gemm {
+
+constexpr int BM = 64, BN = 64, BK = 32, LDK = BK + 8;
+
+enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_SIGMOID = 2, ACT_TANH = 3, ACT_GELU = 4 };
+
+__device__ __forceinline__ float apply_act(float z, int act) {
+  switch (act) {
+    case ACT_RELU: return fmaxf(z, 0.f);
+    case ACT_SIGMOID: return 1.f / (1.f + __expf(-z));
+    case ACT_TANH: return tanhf(z);
+    case ACT_GELU: return 0.5f * z * (1.f + erff(z * 0.70710678118654752f));
+    default: return z;
+  }
+}
+
+template <bool BF16>
+__device__ __forceinline__ float ld_elem(const void* p, size_t i) {
+  if constexpr (BF16) return bf2f(reinterpret_cast<const uint16_t*>(p)[i]);
+  else return reinterpret_cast<const float*>(p)[i];
+}
+
+// Loads this thread's share of a 64 x 32 operand tile into registers.
+// Tile element (r, k) lives at  base[(r0 + r) * ld + k0 + k]  when K is the
+// contiguous dimension (KCONT), else at base[(k0 + k) * ld + r0 + r].
+// 256 threads x 8 elements = 2048 = 64 x 32.
+template <bool BF16, bool KCONT>
+__device__ __forceinline__ void load_tile(const void* base, int ld, int R, int K, int r0, int k0,
+                                          float v[8]) {
+  const int t = threadIdx.x;
+  if constexpr (KCONT) {
+    const int r = t >> 2, kk = (t & 3) * 8;  // 8 consecutive k of row r
+    const int rr = min(r0 + r, R - 1);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = min(k0 + kk + j, K - 1);
+      const float x = ld_elem<BF16>(base, (size_t)rr * ld + k);
+      v[j] = (r0 + r < R && k0 + kk + j < K) ? x : 0.f;
+    }
+  } else {
+    const int k = t >> 3, rr8 = (t & 7) * 8;  // 8 consecutive r of k-row k
+    const int kc = min(k0 + k, K - 1);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int r = min(r0 + rr8 + j, R - 1);
+      const float x = ld_elem<BF16>(base, (size_t)kc * ld + r);
+      v[j] = (r0 + rr8 + j < R && k0 + k < K) ? x : 0.f;
+    }
+  }
+}
+
+template <bool KCONT>
+__device__ __forceinline__ void store_tile(uint16_t* s, const float v[8]) {
+  const int t = threadIdx.x;
+  if constexpr (KCONT) {
+    const int r = t >> 2, kk = (t & 3) * 8;
+    *reinterpret_cast<uint4*>(&s[r * LDK + kk]) =
+        make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7]));
+  } else {
+    const int k = t >> 3, rr8 = (t & 7) * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[(rr8 + j) * LDK + k] = f2bf(v[j]);
+  }
+}
+
+// C[M,N] = act(alpha * A'[M,K] B'[K,N] + bias[N]) (+ beta * C_in when accumulate)
+// A' = A (row-major [M,K], lda) or A^T (A is [K,M]);  B' = B ([K,N]) or B^T ([N,K]).
+template <bool ABF, bool BBF, bool TA, bool TB, bool OBF>
+__global__ __launch_bounds__(256) void gemm_bias_act(
+    const void* __restrict__ A, int lda, const void* __restrict__ Bm, int ldb,
+    void* __restrict__ C, int ldc, float* __restrict__ Zout, const float* __restrict__ bias,
+    int M, int N, int K, float alpha, float beta, int act) {
+  __shared__ __attribute__((aligned(16))) uint16_t As[BM * LDK];
+  __shared__ __attribute__((aligned(16))) uint16_t Bs[BN * LDK];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, lh = lane >> 4;
+  const int wr = wave >> 1, wc = wave & 1;
+
+  // XCD-aware remap: hardware deals block ids round-robin over 8 XCDs; give
+  // each XCD a contiguous run of tiles (bijective for any grid size).
+  const int nt_n = (N + BN - 1) / BN;
+  const int nwg = gridDim.x;
+  const int orig = blockIdx.x;
+  const int xcd = orig % 8, q = nwg / 8, rem = nwg % 8;
+  const int wg = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + orig / 8;
+  const int m0 = (wg / nt_n) * BM, n0 = (wg % nt_n) * BN;
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  float va[8], vb[8];
+  // A' tile rows = m, K contiguous iff !TA;  B' tile rows = n, K contiguous iff TB
+  load_tile<ABF, !TA>(A, lda, M, K, m0, 0, va);
+  load_tile<BBF, TB>(Bm, ldb, N, K, n0, 0, vb);
+  for (int k0 = 0; k0 < K; k0 += BK) {
+    __syncthreads();
+    store_tile<!TA>(As, va);
+    store_tile<TB>(Bs, vb);
+    __syncthreads();
+    if (k0 + BK < K) {  // prefetch next K tile into registers (branch is uniform)
+      load_tile<ABF, !TA>(A, lda, M, K, m0, k0 + BK, va);
+      load_tile<BBF, TB>(Bm, ldb, N, K, n0, k0 + BK, vb);
+    }
+    bf16x8 fa[2], fb[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) fa[i] = ld_bf16x8(&As[(wr * 32 + i * 16 + lr) * LDK + lh * 8]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) fb[j] = ld_bf16x8(&Bs[(wc * 32 + j * 16 + lr) * LDK + lh * 8]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = mfma16x16x32(fa[i], fb[j], acc[i][j]);
+  }
+
+  // epilogue: lane holds rows 4*lh + r, column lr of each 16x16 tile
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = n0 + wc * 32 + j * 16 + lr;
+    const float bv = (bias != nullptr && n < N) ? bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wr * 32 + i * 16 + 4 * lh + r;
+        if (m < M && n < N) {
+          float z = alpha * acc[i][j][r] + bv;
+          const size_t o = (size_t)m * ldc + n;
+          if (beta != 0.f) z += beta * (OBF ? bf2f(reinterpret_cast<uint16_t*>(C)[o]) : reinterpret_cast<float*>(C)[o]);
+          if (Zout != nullptr) Zout[o] = z;
+          const float y = apply_act(z, act);
+          if constexpr (OBF) reinterpret_cast<uint16_t*>(C)[o] = f2bf(y);
+          else reinterpret_cast<float*>(C)[o] = y;
+        }
+      }
+    }
+  }
+}
+
+}  // namespace gemm
+}  // namespace dtfk
+
+extern "C" hipError_t dtfk_gemm(const void* A, int a_bf16, int lda, int transA, const void* B,
+                                int b_bf16, int ldb, int transB, void* C, int c_bf16, int ldc,
+                                float* Z, const float* bias, int M, int N, int K, float alpha,
+                                float beta, int act, hipStream_t stream) {
+  using namespace dtfk::gemm;
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  if (tiles == 0) return hipSuccess;
+  const dim3 grid(tiles), block(256);
+#define DTFK_G(AB, BB, TA, TB, OB)                                                               \
+  hipLaunchKernelGGL((gemm_bias_act<AB, BB, TA, TB, OB>), grid, block, 0, stream, A, lda, B, ldb, \
+                     C, ldc, Z, bias, M, N, K, alpha, beta, act)
+#define DTFK_G_OB(AB, BB, TA, TB) \
+  if (c_bf16) DTFK_G(AB, BB, TA, TB, true); else DTFK_G(AB, BB, TA, TB, false)
+#define DTFK_G_TB(AB, BB, TA) \
+  if (transB) { DTFK_G_OB(AB, BB, TA, true); } else { DTFK_G_OB(AB, BB, TA, false); }
+#define DTFK_G_TA(AB, BB) \
+  if (transA) { DTFK_G_TB(AB, BB, true); } else { DTFK_G_TB(AB, BB, false); }
+  if (a_bf16) {
+    if (b_bf16) { DTFK_G_TA(true, true); } else { DTFK_G_TA(true, false); }
+  } else {
+    if (b_bf16) { DTFK_G_TA(false, true); } else { DTFK_G_TA(false, false); }
+  }
+#undef DTFK_G_TA
+#undef DTFK_G_TB
+#undef DTFK_G_OB
+#undef DTFK_G
+  return hipGetLastError();
+}

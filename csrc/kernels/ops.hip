@@ -1,0 +1,421 @@
+// Fused elementwise / reduction / sparse kernels behind `distributed_tensorflow_example_amd.ops`
+// and `.optim`:
+//   act_backward      dZ = dY * act'(.)                    (SigmoidGrad / ReluGrad ...)
+//   col_sum           db = sum_rows dZ                     (bias gradient, K2/K5)
+//   softmax_xent      fused softmax cross-entropy fwd+bwd  (K6; stable or reference-naive)
+//   sigmoid_xent      fused sigmoid cross-entropy fwd+bwd  (K11, lr2.py:391)
+//   embedding_bag     CSR bag sum/mean with per-id weights (K10, embedding_lookup_sparse)
+//   embedding_bag_bwd scatter-add / fused scatter-SGD      (K10 backward + K8 sparse apply)
+//   argmax_correct    accuracy counter                     (K7)
+//   auc_hist          streaming_auc confusion histograms   (K12)
+//   multi-tensor SGD / momentum / Adam (TF epsilon-hat semantics) / AdamW   (K8, K9)
+// Every kernel is wave64-native: one wave per row/bag where rows are
+// independent, shuffles over 64 lanes, no warp-32 idioms.
+#include "common.h"
+
+namespace dtfk {
+namespace ops {
+
+__device__ __forceinline__ float act_grad(float dy, float y, float z, int act) {
+  switch (act) {
+    case 1: return y > 0.f ? dy : 0.f;                 // relu (from y)
+    case 2: return dy * y * (1.f - y);                 // sigmoid (from y)
+    case 3: return dy * (1.f - y * y);                 // tanh (from y)
+    case 4: {                                          // gelu (from z)
+      const float cdf = 0.5f * (1.f + erff(z * 0.70710678118654752f));
+      const float pdf = 0.3989422804014327f * __expf(-0.5f * z * z);
+      return dy * (cdf + z * pdf);
+    }
+    default: return dy;
+  }
+}
+
+__global__ void act_backward(const float* __restrict__ dy, const float* __restrict__ y,
+                             const float* __restrict__ z, float* __restrict__ dz, int64_t n, int act) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dz[i] = act_grad(dy[i], y ? y[i] : 0.f, z ? z[i] : 0.f, act);
+}
+
+// out[n] = sum_m X[m, n] (X row-major [M, N]); block = 256 threads covers 64
+// columns x 4 row-groups, grid.y splits rows, partials atomically added.
+__global__ void col_sum(const float* __restrict__ X, float* __restrict__ out, int M, int N,
+                        int rows_per_block) {
+  __shared__ float red[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int g = threadIdx.x >> 6;
+  const int r0 = blockIdx.y * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  float s = 0.f;
+  if (c < N)
+    for (int r = r0 + g; r < r1; r += 4) s += X[(size_t)r * N + c];
+  red[g][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (g == 0 && c < N) {
+    const float t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    if (gridDim.y == 1) out[c] = t;
+    else atomicAdd(&out[c], t);
+  }
+}
+
+// One wave per row. labels: int64 class ids (label_kind 0) or dense one-hot /
+// probabilities [B, C] (label_kind 1, the reference's y_ placeholder).
+// loss_rows[b]; grad = (softmax - y) * grad_scale.  naive=1 reproduces
+// -sum(y * log(softmax)) (example.py:103) including its inf/NaN behaviour.
+__global__ void softmax_xent(const float* __restrict__ logits, const int64_t* __restrict__ labels,
+                             const float* __restrict__ ydense, float* __restrict__ loss_rows,
+                             float* __restrict__ grad, int64_t* __restrict__ correct, int Bn, int Cn,
+                             float grad_scale, int naive) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= Bn) return;
+  const float* z = logits + (size_t)row * Cn;
+  float m = -3.0e38f;
+  int am = 0x7fffffff;
+  for (int c = lane; c < Cn; c += 64) {
+    const float v = z[c];
+    if (v > m || (v == m && c < am)) { m = v; am = c; }
+  }
+  // wave argmax with first-index tie break
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const float om = __shfl_xor(m, off, 64);
+    const int oa = __shfl_xor(am, off, 64);
+    if (om > m || (om == m && oa < am)) { m = om; am = oa; }
+  }
+  float s = 0.f;
+  for (int c = lane; c < Cn; c += 64) s += __expf(z[c] - m);
+  s = wave_sum(s);
+  const float lse = m + __logf(s);
+  float loss = 0.f;
+  int y = -1;
+  if (ydense == nullptr) {
+    y = (int)labels[row];
+    y = y < 0 ? 0 : (y >= Cn ? Cn - 1 : y);  // out-of-range ids cannot read past the row
+    if (lane == 0) loss = naive ? -__logf(__expf(z[y] - m) / s) : lse - z[y];
+  } else {
+    float l = 0.f, ymax = -1.f;
+    int ya = 0;
+    for (int c = lane; c < Cn; c += 64) {
+      const float yc = ydense[(size_t)row * Cn + c];
+      if (naive) l += -yc * __logf(__expf(z[c] - m) / s);
+      else l += yc * (lse - z[c]);
+      if (yc > ymax) { ymax = yc; ya = c; }
+    }
+    loss = wave_sum(l);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const float om = __shfl_xor(ymax, off, 64);
+      const int oa = __shfl_xor(ya, off, 64);
+      if (om > ymax || (om == ymax && oa < ya)) { ymax = om; ya = oa; }
+    }
+    y = ya;
+  }
+  if (lane == 0) {
+    loss_rows[row] = loss;
+    if (correct) atomicAdd((unsigned long long*)correct, (unsigned long long)(am == y ? 1 : 0));
+  }
+  if (grad != nullptr) {
+    for (int c = lane; c < Cn; c += 64) {
+      const float p = __expf(z[c] - m) / s;
+      const float t = ydense ? ydense[(size_t)row * Cn + c] : (c == y ? 1.f : 0.f);
+      grad[(size_t)row * Cn + c] = (p - t) * grad_scale;
+    }
+  }
+}
+
+// max(x,0) - x*t + log1p(exp(-|x|)); grad (sigmoid(x) - t) * scale
+__global__ void sigmoid_xent(const float* __restrict__ x, const float* __restrict__ t,
+                             float* __restrict__ loss, float* __restrict__ grad, int64_t n,
+                             float grad_scale) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float v = x[i], z = t[i];
+    loss[i] = fmaxf(v, 0.f) - v * z + log1pf(__expf(-fabsf(v)));
+    if (grad) grad[i] = (1.f / (1.f + __expf(-v)) - z) * grad_scale;
+  }
+}
+
+// out[b, :] = combine_{j in bag b} w_j * W[ids_j, :]   (mode 0 sum, 1 mean, 2 sqrtn)
+// One wave per bag; lanes stride the embedding dim (D >= 64) or, for narrow
+// tables (D < 64, e.g. the LR weight D = 1), lanes stride the bag's ids.
+__global__ void embedding_bag_fwd(const float* __restrict__ W, int64_t V, int D,
+                                  const int64_t* __restrict__ ids, const int64_t* __restrict__ offsets,
+                                  const float* __restrict__ psw, int Bn, int mode,
+                                  float* __restrict__ out, int64_t* __restrict__ bad_ids) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (b >= Bn) return;
+  const int64_t s = offsets[b], e = offsets[b + 1];
+  float wsum = 0.f;
+  if (D < 64) {
+    for (int d = 0; d < D; ++d) {
+      float acc = 0.f, ws = 0.f;
+      for (int64_t j = s + lane; j < e; j += 64) {
+        int64_t id = ids[j];
+        const float w = psw ? psw[j] : 1.f;
+        if (id < 0 || id >= V) { if (bad_ids && d == 0) atomicAdd((unsigned long long*)bad_ids, 1ull); continue; }
+        acc += w * W[id * D + d];
+        ws += mode == 2 ? w * w : w;
+      }
+      acc = wave_sum(acc);
+      wsum = wave_sum(ws);
+      if (lane == 0) {
+        float scale = 1.f;
+        if (mode == 1 && e > s) scale = 1.f / fmaxf(wsum, 1e-30f);
+        if (mode == 2 && e > s) scale = rsqrtf(fmaxf(wsum, 1e-30f));
+        out[(size_t)b * D + d] = acc * scale;
+      }
+    }
+    return;
+  }
+  for (int d0 = 0; d0 < D; d0 += 64) {
+    const int d = d0 + lane;
+    float acc = 0.f, ws = 0.f;
+    for (int64_t j = s; j < e; ++j) {
+      const int64_t id = ids[j];
+      const float w = psw ? psw[j] : 1.f;
+      if (id < 0 || id >= V) continue;
+      if (d < D) acc += w * W[id * D + d];
+      ws += mode == 2 ? w * w : w;
+    }
+    float scale = 1.f;
+    if (mode == 1 && e > s) scale = 1.f / fmaxf(ws, 1e-30f);
+    if (mode == 2 && e > s) scale = rsqrtf(fmaxf(ws, 1e-30f));
+    if (d < D) out[(size_t)b * D + d] = acc * scale;
+  }
+}
+
+// dW[ids_j, :] += w_j * scale_b * dOut[b, :]  (dense fp32 gradient table), or with
+// lr != 0: W[ids_j, :] -= lr * (...) directly (fused sparse SGD apply; the
+// reference applies IndexedSlices with ScatterSub on the ps).  Float atomics
+// (execute at the memory side; duplicates within and across bags combine).
+__global__ void embedding_bag_bwd(float* __restrict__ target, int64_t V, int D,
+                                  const int64_t* __restrict__ ids, const int64_t* __restrict__ offsets,
+                                  const float* __restrict__ psw, const float* __restrict__ dout, int Bn,
+                                  int mode, float lr) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (b >= Bn) return;
+  const int64_t s = offsets[b], e = offsets[b + 1];
+  float ws = 0.f;
+  if (mode != 0) {
+    for (int64_t j = s + lane; j < e; j += 64) {
+      const float w = psw ? psw[j] : 1.f;
+      ws += mode == 2 ? w * w : w;
+    }
+    ws = wave_sum(ws);
+  }
+  float scale = 1.f;
+  if (mode == 1 && e > s) scale = 1.f / fmaxf(ws, 1e-30f);
+  if (mode == 2 && e > s) scale = rsqrtf(fmaxf(ws, 1e-30f));
+  const float mul = lr != 0.f ? -lr * scale : scale;
+  if (D < 64) {
+    for (int64_t j = s + lane; j < e; j += 64) {
+      const int64_t id = ids[j];
+      if (id < 0 || id >= V) continue;
+      const float w = (psw ? psw[j] : 1.f) * mul;
+      for (int d = 0; d < D; ++d) atomicAdd(&target[id * D + d], w * dout[(size_t)b * D + d]);
+    }
+    return;
+  }
+  for (int64_t j = s; j < e; ++j) {
+    const int64_t id = ids[j];
+    if (id < 0 || id >= V) continue;
+    const float w = (psw ? psw[j] : 1.f) * mul;
+    for (int d = lane; d < D; d += 64) atomicAdd(&target[id * D + d], w * dout[(size_t)b * D + d]);
+  }
+}
+
+// rows of [N, C] logits vs int64 labels -> number of argmax hits
+__global__ void argmax_correct(const float* __restrict__ x, const int64_t* __restrict__ labels, int Bn,
+                               int Cn, int64_t* __restrict__ count) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= Bn) return;
+  float m = -3.0e38f;
+  int am = 0x7fffffff;
+  for (int c = lane; c < Cn; c += 64) {
+    const float v = x[(size_t)row * Cn + c];
+    if (v > m || (v == m && c < am)) { m = v; am = c; }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const float om = __shfl_xor(m, off, 64);
+    const int oa = __shfl_xor(am, off, 64);
+    if (om > m || (om == m && oa < am)) { m = om; am = oa; }
+  }
+  if (lane == 0 && am == (int)labels[row]) atomicAdd((unsigned long long*)count, 1ull);
+}
+
+// Per-bin positive / negative counts of predictions in [0, 1]; bin k covers
+// thresholds [k/(nb-1) ...).  Counts accumulate across calls (streaming).
+__global__ void auc_hist(const float* __restrict__ pred, const float* __restrict__ label, int64_t n,
+                         int nbins, unsigned long long* __restrict__ pos, unsigned long long* __restrict__ neg) {
+  extern __shared__ unsigned int h[];  // [2][nbins]
+  for (int i = threadIdx.x; i < 2 * nbins; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float p = fminf(fmaxf(pred[i], 0.f), 1.f);
+    int b = (int)(p * (nbins - 1));
+    b = min(max(b, 0), nbins - 1);
+    atomicAdd(&h[(label[i] > 0.5f ? 0 : nbins) + b], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nbins; i += blockDim.x) {
+    if (h[i]) atomicAdd(&pos[i], (unsigned long long)h[i]);
+    if (h[nbins + i]) atomicAdd(&neg[i], (unsigned long long)h[nbins + i]);
+  }
+}
+
+// ---------------------------------------------------------------- optimizers
+// Multi-tensor: `tab` holds per-tensor {param*, grad*, m*, v*, numel}; the grid
+// walks (tensor, chunk) pairs from `chunks` (tensor index, start element).
+struct TensorRec {
+  float* p;
+  const void* g;
+  float* m;
+  float* v;
+  int64_t n;
+};
+constexpr int CHUNK = 4096;
+
+__device__ __forceinline__ float ld_grad(const void* g, int64_t i, int gbf) {
+  return gbf ? bf2f(reinterpret_cast<const uint16_t*>(g)[i]) : reinterpret_cast<const float*>(g)[i];
+}
+
+// kind 0: sgd, 1: momentum (use_nesterov in flags bit0), 2: adam (TF), 3: adamw
+__global__ void multi_tensor_apply(const TensorRec* __restrict__ tab, const int2* __restrict__ chunks,
+                                   int nchunks, int kind, int gbf, const float* __restrict__ lr_ptr,
+                                   float lr_scalar, float gscale, float wd, float b1, float b2, float eps,
+                                   float momentum, int nesterov, const long long* __restrict__ step_ptr) {
+  const int cidx = blockIdx.x;
+  if (cidx >= nchunks) return;
+  const int2 ch = chunks[cidx];
+  const TensorRec t = tab[ch.x];
+  const float lr = lr_ptr ? *lr_ptr : lr_scalar;
+  float lr_t = lr;
+  if (kind >= 2) {
+    const double st = (double)(step_ptr ? *step_ptr : 1);
+    // TF AdamOptimizer: lr_t = lr * sqrt(1 - b2^t) / (1 - b1^t), eps outside the sqrt
+    lr_t = (float)(lr * sqrt(1.0 - pow((double)b2, st)) / (1.0 - pow((double)b1, st)));
+  }
+  const int64_t s = (int64_t)ch.y, e = min(t.n, s + CHUNK);
+  for (int64_t i = s + threadIdx.x; i < e; i += blockDim.x) {
+    float g = ld_grad(t.g, i, gbf) * gscale;
+    float p = t.p[i];
+    if (kind == 0) {
+      if (wd != 0.f) g += wd * p;
+      p -= lr * g;
+    } else if (kind == 1) {
+      if (wd != 0.f) g += wd * p;
+      const float mv = momentum * t.m[i] + g;
+      t.m[i] = mv;
+      p -= lr * (nesterov ? g + momentum * mv : mv);
+    } else {
+      if (kind == 2 && wd != 0.f) g += wd * p;
+      const float mv = b1 * t.m[i] + (1.f - b1) * g;
+      const float vv = b2 * t.v[i] + (1.f - b2) * g * g;
+      t.m[i] = mv;
+      t.v[i] = vv;
+      p -= lr_t * mv / (sqrtf(vv) + eps);
+      if (kind == 3 && wd != 0.f) p -= lr * wd * t.p[i];
+    }
+    t.p[i] = p;
+  }
+}
+
+// global-norm of a set of tensors (for clipping / NaN checks): sum of squares
+__global__ void multi_tensor_sumsq(const TensorRec* __restrict__ tab, const int2* __restrict__ chunks,
+                                   int nchunks, int gbf, float* __restrict__ out) {
+  __shared__ float scratch[4];
+  const int2 ch = chunks[blockIdx.x];
+  const TensorRec t = tab[ch.x];
+  const int64_t s = (int64_t)ch.y, e = min(t.n, s + CHUNK);
+  float acc = 0.f;
+  for (int64_t i = s + threadIdx.x; i < e; i += blockDim.x) {
+    const float g = ld_grad(t.g, i, gbf);
+    acc += g * g;
+  }
+  acc = block_sum(acc, scratch);
+  if (threadIdx.x == 0) atomicAdd(out, acc);
+}
+
+}  // namespace ops
+}  // namespace dtfk
+
+// ---------------------------------------------------------------- launchers
+using namespace dtfk::ops;
+
+static int nblk(int64_t n, int per = 256, int cap = 4096) {
+  int64_t b = (n + per - 1) / per;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(b, cap));
+}
+
+extern "C" {
+hipError_t dtfk_act_backward(const float* dy, const float* y, const float* z, float* dz, int64_t n,
+                             int act, hipStream_t s) {
+  hipLaunchKernelGGL(act_backward, dim3(nblk(n)), dim3(256), 0, s, dy, y, z, dz, n, act);
+  return hipGetLastError();
+}
+hipError_t dtfk_col_sum(const float* X, float* out, int M, int N, hipStream_t s) {
+  const int rows_per_block = 512;
+  const int gy = std::max(1, (M + rows_per_block - 1) / rows_per_block);
+  if (gy > 1) (void)hipMemsetAsync(out, 0, sizeof(float) * N, s);
+  hipLaunchKernelGGL(col_sum, dim3((N + 63) / 64, gy), dim3(256), 0, s, X, out, M, N, rows_per_block);
+  return hipGetLastError();
+}
+hipError_t dtfk_softmax_xent(const float* logits, const int64_t* labels, const float* ydense, float* loss_rows,
+                             float* grad, int64_t* correct, int B, int C, float grad_scale, int naive,
+                             hipStream_t s) {
+  hipLaunchKernelGGL(softmax_xent, dim3((B + 3) / 4), dim3(256), 0, s, logits, labels, ydense, loss_rows,
+                     grad, correct, B, C, grad_scale, naive);
+  return hipGetLastError();
+}
+hipError_t dtfk_sigmoid_xent(const float* x, const float* t, float* loss, float* grad, int64_t n,
+                             float grad_scale, hipStream_t s) {
+  hipLaunchKernelGGL(sigmoid_xent, dim3(nblk(n)), dim3(256), 0, s, x, t, loss, grad, n, grad_scale);
+  return hipGetLastError();
+}
+hipError_t dtfk_embedding_bag_fwd(const float* W, int64_t V, int D, const int64_t* ids, const int64_t* offsets,
+                                  const float* psw, int B, int mode, float* out, int64_t* bad, hipStream_t s) {
+  hipLaunchKernelGGL(embedding_bag_fwd, dim3((B + 3) / 4), dim3(256), 0, s, W, V, D, ids, offsets, psw, B,
+                     mode, out, bad);
+  return hipGetLastError();
+}
+hipError_t dtfk_embedding_bag_bwd(float* target, int64_t V, int D, const int64_t* ids, const int64_t* offsets,
+                                  const float* psw, const float* dout, int B, int mode, float lr,
+                                  hipStream_t s) {
+  hipLaunchKernelGGL(embedding_bag_bwd, dim3((B + 3) / 4), dim3(256), 0, s, target, V, D, ids, offsets, psw,
+                     dout, B, mode, lr);
+  return hipGetLastError();
+}
+hipError_t dtfk_argmax_correct(const float* x, const int64_t* labels, int B, int C, int64_t* count,
+                               hipStream_t s) {
+  hipLaunchKernelGGL(argmax_correct, dim3((B + 3) / 4), dim3(256), 0, s, x, labels, B, C, count);
+  return hipGetLastError();
+}
+hipError_t dtfk_auc_hist(const float* pred, const float* label, int64_t n, int nbins,
+                         unsigned long long* pos, unsigned long long* neg, hipStream_t s) {
+  hipLaunchKernelGGL(auc_hist, dim3(nblk(n, 256, 1024)), dim3(256), 2 * nbins * sizeof(unsigned int), s, pred,
+                     label, n, nbins, pos, neg);
+  return hipGetLastError();
+}
+hipError_t dtfk_multi_tensor_apply(const void* tab, const void* chunks, int nchunks, int kind, int gbf,
+                                   const float* lr_ptr, float lr, float gscale, float wd, float b1, float b2,
+                                   float eps, float momentum, int nesterov, const long long* step,
+                                   hipStream_t s) {
+  if (nchunks == 0) return hipSuccess;
+  hipLaunchKernelGGL(multi_tensor_apply, dim3(nchunks), dim3(256), 0, s, (const TensorRec*)tab,
+                     (const int2*)chunks, nchunks, kind, gbf, lr_ptr, lr, gscale, wd, b1, b2, eps, momentum,
+                     nesterov, step);
+  return hipGetLastError();
+}
+hipError_t dtfk_multi_tensor_sumsq(const void* tab, const void* chunks, int nchunks, int gbf, float* out,
+                                   hipStream_t s) {
+  (void)hipMemsetAsync(out, 0, sizeof(float), s);
+  if (nchunks == 0) return hipSuccess;
+  hipLaunchKernelGGL(multi_tensor_sumsq, dim3(nchunks), dim3(256), 0, s, (const TensorRec*)tab,
+                     (const int2*)chunks, nchunks, gbf, out);
+  return hipGetLastError();
+}
+int dtfk_mt_chunk() { return CHUNK; }
+int dtfk_tensor_rec_bytes() { return (int)sizeof(TensorRec); }
+}

@@ -11,6 +11,7 @@ void init_bundle(py::module& m);
 void init_store(py::module& m);
 void init_queue(py::module& m);
 void init_libsvm(py::module& m);
+void init_ops(py::module& m);
 }  // namespace dtf
 
 PYBIND11_MODULE(_C, m) {
@@ -23,4 +24,5 @@ PYBIND11_MODULE(_C, m) {
   dtf::init_store(m);
   dtf::init_queue(m);
   dtf::init_libsvm(m);
+  dtf::init_ops(m);
 }

@@ -1,0 +1,679 @@
+"""A small deferred-execution tensor layer with TF-1 graph semantics.
+
+The reference builds TF graphs (placeholders, Variables under name scopes,
+matmul/add/sigmoid/softmax, reduce_mean, ...) and evaluates them with
+`sess.run(fetches, feed_dict)` (example.py:69-170; lr2.py:363-446).  This
+module keeps that programming model -- so the reference scripts port almost
+line by line -- while executing eagerly on PyTorch-ROCm tensors when a fetch
+is run:
+
+* `Tensor` nodes record (fn, inputs); `Session.run` evaluates the requested
+  fetches once per call with memoisation (a run's loss and accuracy share the
+  forward pass), autograd flows through Variables;
+* `Variable`s own a device tensor (GPU when present), carry TF names
+  (`weights/Variable_1:0`) and live in the GLOBAL/TRAINABLE/LOCAL collections,
+  which the Saver uses for TF-format checkpoints;
+* matmul dispatches to the framework's MFMA GEMM (`ops.linear_act`) on GPU.
+"""
+from __future__ import annotations
+
+import contextlib
+import threading
+from collections import defaultdict
+from typing import Any, Callable, Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+# ----------------------------------------------------------------------- dtypes
+float32 = torch.float32
+float64 = torch.float64
+float16 = torch.float16
+bfloat16 = torch.bfloat16
+int32 = torch.int32
+int64 = torch.int64
+uint8 = torch.uint8
+bool_ = torch.bool
+string = "string"
+
+GLOBAL_VARIABLES = "variables"
+TRAINABLE_VARIABLES = "trainable_variables"
+LOCAL_VARIABLES = "local_variables"
+SUMMARIES = "summaries"
+QUEUE_RUNNERS = "queue_runners"
+GLOBAL_STEP = "global_step"
+UPDATE_OPS = "update_ops"
+
+
+def default_device() -> torch.device:
+    return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+
+
+class Graph:
+    """Name scopes, collections, unique names and the device-placement stack."""
+
+    def __init__(self):
+        self._collections: Dict[str, List[Any]] = defaultdict(list)
+        self._names: Dict[str, int] = {}
+        self._scope: List[str] = []
+        self._var_scope: List[str] = []
+        self._var_reuse: List[bool] = []
+        self._devices: List[Any] = []
+        self._vars_by_name: Dict[str, "Variable"] = {}
+        self.seed: Optional[int] = None
+        self._op_seed = 0
+        self.device = default_device()
+        self.finalized = False
+
+    def unique_name(self, name: str) -> str:
+        full = "/".join(self._scope + [name]) if self._scope else name
+        n = self._names.get(full, 0)
+        self._names[full] = n + 1
+        return full if n == 0 else f"{full}_{n}"
+
+    def add_to_collection(self, key, value):
+        self._collections[key].append(value)
+
+    def get_collection(self, key, scope: Optional[str] = None):
+        vals = list(self._collections.get(key, []))
+        if scope:
+            vals = [v for v in vals if getattr(v, "name", "").startswith(scope)]
+        return vals
+
+    def get_collection_ref(self, key):
+        return self._collections[key]
+
+    def finalize(self):
+        self.finalized = True
+
+    def as_graph_def(self) -> bytes:
+        """Opaque stand-in for GraphDef (used by summary writers / exporters)."""
+        names = [v.name for v in self._collections.get(GLOBAL_VARIABLES, [])]
+        return ("\n".join(names)).encode()
+
+    def next_seed(self):
+        self._op_seed += 1
+        if self.seed is None:
+            return None
+        return (self.seed * 1000003 + self._op_seed) % (2 ** 31)
+
+
+_local = threading.local()
+
+
+def get_default_graph() -> Graph:
+    g = getattr(_local, "graph", None)
+    if g is None:
+        g = _local.graph = Graph()
+    return g
+
+
+def reset_default_graph():
+    _local.graph = Graph()
+
+
+def set_random_seed(seed: int):
+    get_default_graph().seed = int(seed)
+
+
+@contextlib.contextmanager
+def name_scope(name: str):
+    g = get_default_graph()
+    scope = g.unique_name(name) if name else None
+    if scope:
+        g._scope.append(scope.split("/")[-1])
+    try:
+        yield scope
+    finally:
+        if scope:
+            g._scope.pop()
+
+
+@contextlib.contextmanager
+def variable_scope(name: str, reuse: Optional[bool] = None):
+    g = get_default_graph()
+    g._var_scope.append(name)
+    g._scope.append(name)
+    g._var_reuse.append(bool(reuse))
+    try:
+        yield name
+    finally:
+        g._var_scope.pop()
+        g._scope.pop()
+        g._var_reuse.pop()
+
+
+@contextlib.contextmanager
+def device(spec):
+    """Device scope.  `spec` may be a device string or a placement function
+    (e.g. `train.replica_device_setter(...)`).  Placement is recorded on
+    Variables (`.placement`); compute runs on this process's accelerator."""
+    g = get_default_graph()
+    g._devices.append(spec)
+    try:
+        yield spec
+    finally:
+        g._devices.pop()
+
+
+def _current_placement(op_type: str, name: str, numel: int) -> Optional[str]:
+    g = get_default_graph()
+    for spec in reversed(g._devices):
+        if callable(spec):
+            return spec(_PlacementQuery(op_type, name, numel))
+        if spec:
+            return str(spec)
+    return None
+
+
+class _PlacementQuery:
+    def __init__(self, op_type, name, numel):
+        self.type = op_type
+        self.name = name
+        self.numel = numel
+        self.device = ""
+
+
+# ----------------------------------------------------------------------- tensors
+class RunContext:
+    def __init__(self, feeds: Dict[Any, Any], device: torch.device):
+        self.feeds = feeds
+        self.device = device
+        self.memo: Dict[int, Any] = {}
+        self.state: Dict[str, Any] = {}
+
+    def eval(self, x):
+        if isinstance(x, Tensor):
+            k = id(x)
+            if k not in self.memo:
+                self.memo[k] = x._eval(self)
+            return self.memo[k]
+        if isinstance(x, (list, tuple)):
+            return type(x)(self.eval(v) for v in x)
+        return _to_tensor(x, self.device)
+
+
+def _to_tensor(x, dev, dtype=None):
+    if isinstance(x, torch.Tensor):
+        t = x.to(dev)
+    elif isinstance(x, np.ndarray):
+        t = torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+    elif isinstance(x, (bytes, str)):
+        return x
+    else:
+        t = torch.tensor(x, device=dev)
+    if t.dtype == torch.float64:
+        t = t.float()
+    if dtype is not None and dtype != string:
+        t = t.to(dtype)
+    return t
+
+
+class Tensor:
+    """Deferred value: fn(*inputs) evaluated inside Session.run."""
+
+    _is_op = False
+
+    def __init__(self, fn: Callable, inputs: Sequence[Any] = (), name: str = "Tensor", dtype=None,
+                 shape=None):
+        self.fn = fn
+        self.inputs = list(inputs)
+        self.name = get_default_graph().unique_name(name) + ":0"
+        self.dtype = dtype
+        self.shape = shape
+        self.op = self
+
+    def _eval(self, ctx: RunContext):
+        vals = [ctx.eval(i) for i in self.inputs]
+        return self.fn(*vals)
+
+    # arithmetic ----------------------------------------------------------
+    def __add__(self, o): return Tensor(lambda a, b: a + b, [self, o], "add")
+    def __radd__(self, o): return Tensor(lambda a, b: b + a, [self, o], "add")
+    def __sub__(self, o): return Tensor(lambda a, b: a - b, [self, o], "sub")
+    def __rsub__(self, o): return Tensor(lambda a, b: b - a, [self, o], "sub")
+    def __mul__(self, o): return Tensor(lambda a, b: a * b, [self, o], "mul")
+    def __rmul__(self, o): return Tensor(lambda a, b: b * a, [self, o], "mul")
+    def __truediv__(self, o): return Tensor(lambda a, b: a / b, [self, o], "truediv")
+    def __rtruediv__(self, o): return Tensor(lambda a, b: b / a, [self, o], "truediv")
+    def __pow__(self, o): return Tensor(lambda a, b: a ** b, [self, o], "pow")
+    def __neg__(self): return Tensor(lambda a: -a, [self], "neg")
+    def __matmul__(self, o): return matmul(self, o)
+    def __getitem__(self, idx): return Tensor(lambda a: a[idx], [self], "strided_slice")
+
+    def eval(self, session=None, feed_dict=None):
+        from .session import get_default_session
+
+        sess = session or get_default_session()
+        return sess.run(self, feed_dict=feed_dict)
+
+    def get_shape(self):
+        return self.shape
+
+    def __repr__(self):
+        return f"<dtf Tensor {self.name}>"
+
+
+class Operation(Tensor):
+    """A node run for its side effect; Session.run returns None for it."""
+
+    _is_op = True
+
+    def __init__(self, fn: Callable, inputs: Sequence[Any] = (), name: str = "Op"):
+        super().__init__(fn, inputs, name)
+
+    def run(self, session=None, feed_dict=None):
+        from .session import get_default_session
+
+        (session or get_default_session()).run(self, feed_dict=feed_dict)
+
+
+def group(*ops, name="group_deps") -> Operation:
+    flat = []
+    for o in ops:
+        flat.extend(o if isinstance(o, (list, tuple)) else [o])
+    return Operation(lambda *a: None, flat, name)
+
+
+def no_op(name="NoOp") -> Operation:
+    return Operation(lambda: None, [], name)
+
+
+def constant(value, dtype=None, shape=None, name="Const") -> Tensor:
+    def f():
+        t = _to_tensor(value, get_default_graph().device, dtype)
+        return t.reshape(shape) if shape is not None and isinstance(t, torch.Tensor) else t
+    return Tensor(f, [], name, dtype=dtype, shape=shape)
+
+
+class Placeholder(Tensor):
+    def __init__(self, dtype=float32, shape=None, name="Placeholder"):
+        super().__init__(None, [], name, dtype=dtype, shape=shape)
+
+    def _eval(self, ctx: RunContext):
+        for key in (self, self.name, self.name[:-2]):
+            try:
+                if key in ctx.feeds:
+                    return _to_tensor(ctx.feeds[key], ctx.device, self.dtype)
+            except TypeError:
+                continue
+        raise KeyError(f"You must feed a value for placeholder {self.name}")
+
+
+def placeholder(dtype=float32, shape=None, name="Placeholder") -> Placeholder:
+    return Placeholder(dtype, shape, name)
+
+
+# ----------------------------------------------------------------------- variables
+class Variable(Tensor):
+    """TF-style variable: named, initialised by an initializer op, placed per
+    the device scope (replica_device_setter records ps/worker placement)."""
+
+    def __init__(self, initial_value=None, trainable: bool = True, name: Optional[str] = None,
+                 dtype=None, collections=None, _full_name: Optional[str] = None):
+        g = get_default_graph()
+        self._init_value = initial_value
+        base = _full_name or g.unique_name(name or "Variable")
+        self.fn = None
+        self.inputs = []
+        self.name = base + ":0"
+        self.op = self
+        self.trainable = trainable
+        init = self._materialize_initial()
+        if dtype is not None:
+            init = init.to(dtype)
+        self.dtype = init.dtype
+        self.shape = tuple(init.shape)
+        self.placement = _current_placement("VariableV2", base, init.numel())
+        self.value = torch.nn.Parameter(init.to(g.device).clone(), requires_grad=trainable and init.is_floating_point())
+        self.initialized = False
+        self.initializer = Operation(lambda: self._initialize(), [], base + "/Assign")
+        cols = collections or ([GLOBAL_VARIABLES] + ([TRAINABLE_VARIABLES] if trainable else []))
+        for c in cols:
+            g.add_to_collection(c, self)
+        g._vars_by_name[base] = self
+
+    def _materialize_initial(self) -> torch.Tensor:
+        iv = self._init_value
+        if callable(iv) and not isinstance(iv, Tensor):
+            iv = iv()
+        if isinstance(iv, Tensor):
+            ctx = RunContext({}, torch.device("cpu"))
+            iv = ctx.eval(iv)
+        if not isinstance(iv, torch.Tensor):
+            iv = torch.as_tensor(np.asarray(iv))
+            if iv.dtype == torch.float64:
+                iv = iv.float()
+        return iv.detach().cpu()
+
+    def _initialize(self):
+        with torch.no_grad():
+            self.value.data.copy_(self._materialize_initial().to(self.value.device, self.value.dtype))
+        self.initialized = True
+
+    def _eval(self, ctx: RunContext):
+        return self.value
+
+    @property
+    def op_name(self) -> str:
+        return self.name[:-2]
+
+    def assign(self, value) -> Operation:
+        def f(v):
+            with torch.no_grad():
+                self.value.data.copy_(torch.as_tensor(v).to(self.value.device, self.value.dtype))
+            return self.value
+        return Operation(f, [value], self.op_name + "/Assign")
+
+    def assign_add(self, delta) -> Operation:
+        def f(d):
+            with torch.no_grad():
+                self.value.data.add_(torch.as_tensor(d).to(self.value.device, self.value.dtype))
+            return self.value
+        return Operation(f, [delta], self.op_name + "/AssignAdd")
+
+    def load(self, value, session=None):
+        with torch.no_grad():
+            self.value.data.copy_(torch.as_tensor(np.asarray(value)).to(self.value.device, self.value.dtype))
+
+    def read_value(self):
+        return self.value.detach()
+
+    def numpy(self):
+        return self.value.detach().cpu().numpy()
+
+    def __repr__(self):
+        return f"<dtf Variable '{self.name}' shape={self.shape} dtype={self.dtype}>"
+
+
+# initializers ---------------------------------------------------------------
+def _gen(seed):
+    g = torch.Generator()
+    if seed is None:
+        seed = get_default_graph().next_seed()
+    if seed is None:
+        g.seed()
+    else:
+        g.manual_seed(int(seed))
+    return g
+
+
+def random_normal(shape, mean=0.0, stddev=1.0, dtype=float32, seed=None, name="random_normal"):
+    gen = _gen(seed)
+    shape = tuple(int(s) for s in shape)
+    return lambda: (torch.randn(shape, generator=gen, dtype=torch.float32) * stddev + mean).to(dtype)
+
+
+def truncated_normal(shape, mean=0.0, stddev=1.0, dtype=float32, seed=None, name="truncated_normal"):
+    gen = _gen(seed)
+    shape = tuple(int(s) for s in shape)
+
+    def f():
+        t = torch.randn(shape, generator=gen)
+        while True:
+            bad = t.abs() > 2
+            if not bad.any():
+                break
+            t[bad] = torch.randn(int(bad.sum()), generator=gen)
+        return (t * stddev + mean).to(dtype)
+    return f
+
+
+def zeros(shape, dtype=float32, name="zeros"):
+    return lambda: torch.zeros(tuple(int(s) for s in shape), dtype=dtype)
+
+
+def ones(shape, dtype=float32, name="ones"):
+    return lambda: torch.ones(tuple(int(s) for s in shape), dtype=dtype)
+
+
+def random_uniform(shape, minval=0.0, maxval=1.0, dtype=float32, seed=None, name="random_uniform"):
+    gen = _gen(seed)
+    return lambda: (torch.rand(tuple(int(s) for s in shape), generator=gen) * (maxval - minval) + minval).to(dtype)
+
+
+class constant_initializer:
+    def __init__(self, value=0.0, dtype=float32):
+        self.value = value
+        self.dtype = dtype
+
+    def __call__(self, shape, dtype=None):
+        return torch.full(tuple(int(s) for s in shape), float(self.value), dtype=dtype or torch.float32)
+
+
+class random_normal_initializer:
+    def __init__(self, mean=0.0, stddev=1.0, seed=None, dtype=float32):
+        self.mean, self.stddev, self.seed = mean, stddev, seed
+
+    def __call__(self, shape, dtype=None):
+        return random_normal(shape, self.mean, self.stddev, dtype or float32, self.seed)()
+
+
+class truncated_normal_initializer(random_normal_initializer):
+    def __call__(self, shape, dtype=None):
+        return truncated_normal(shape, self.mean, self.stddev, dtype or float32, self.seed)()
+
+
+class zeros_initializer:
+    def __init__(self, dtype=float32):
+        self.dtype = dtype
+
+    def __call__(self, shape, dtype=None):
+        return torch.zeros(tuple(int(s) for s in shape), dtype=dtype or torch.float32)
+
+
+class glorot_uniform_initializer:
+    def __init__(self, seed=None, dtype=float32):
+        self.seed = seed
+
+    def __call__(self, shape, dtype=None):
+        fan_in, fan_out = (shape[0], shape[-1]) if len(shape) >= 2 else (shape[0], shape[0])
+        lim = (6.0 / (fan_in + fan_out)) ** 0.5
+        return random_uniform(shape, -lim, lim, seed=self.seed)()
+
+
+def get_variable(name, shape=None, dtype=float32, initializer=None, trainable=True, collections=None,
+                 partitioner=None) -> Variable:
+    """tf.get_variable: honours variable_scope (names) and reuse.  Default
+    initializer is glorot-uniform as in TF; `constant_initializer(0)` with no
+    dtype yields float32 (the reference's float32 global_step, A5)."""
+    g = get_default_graph()
+    full = "/".join(g._var_scope + [name]) if g._var_scope else name
+    if full in g._vars_by_name:
+        if g._var_reuse and g._var_reuse[-1]:
+            return g._vars_by_name[full]
+        raise ValueError(f"Variable {full} already exists, disallowed. Did you mean to set reuse=True?")
+    init = initializer if initializer is not None else glorot_uniform_initializer()
+    shp = tuple(int(s) for s in (shape or ()))
+    iv = (lambda: init(shp, dtype)) if callable(init) else init
+    v = Variable(iv, trainable=trainable, dtype=dtype, collections=collections, _full_name=full)
+    g._names[full] = g._names.get(full, 0) + 1
+    if partitioner is not None:
+        v.partitioner = partitioner
+    return v
+
+
+def global_variables():
+    return get_default_graph().get_collection(GLOBAL_VARIABLES)
+
+
+def all_variables():
+    return global_variables()
+
+
+def trainable_variables():
+    return get_default_graph().get_collection(TRAINABLE_VARIABLES)
+
+
+def local_variables():
+    return get_default_graph().get_collection(LOCAL_VARIABLES)
+
+
+def variables_initializer(var_list, name="init") -> Operation:
+    return Operation(lambda: [v._initialize() for v in var_list], [], name)
+
+
+def global_variables_initializer() -> Operation:
+    return Operation(lambda: [v._initialize() for v in global_variables()], [], "init")
+
+
+initialize_all_variables = global_variables_initializer
+
+
+def local_variables_initializer() -> Operation:
+    return Operation(lambda: [v._initialize() for v in local_variables()], [], "init_local")
+
+
+def report_uninitialized_variables(var_list=None):
+    vs = var_list if var_list is not None else global_variables()
+    return [v.name for v in vs if not v.initialized]
+
+
+# ----------------------------------------------------------------------- math ops
+def _binary(fn, name):
+    def op(a, b, name=None):
+        return Tensor(fn, [a, b], name or op_name)
+    op_name = name
+    return op
+
+
+add = _binary(lambda a, b: a + b, "Add")
+subtract = _binary(lambda a, b: a - b, "Sub")
+sub = subtract
+multiply = _binary(lambda a, b: a * b, "Mul")
+mul = multiply
+divide = _binary(lambda a, b: a / b, "RealDiv")
+div = divide
+truediv = divide
+maximum = _binary(torch.maximum, "Maximum")
+minimum = _binary(torch.minimum, "Minimum")
+pow = _binary(lambda a, b: a ** b, "Pow")  # noqa: A001
+
+
+def matmul(a, b, transpose_a=False, transpose_b=False, name="MatMul") -> Tensor:
+    def f(x, y):
+        x = x.t() if transpose_a else x
+        y = y.t() if transpose_b else y
+        if x.is_cuda and x.dim() == 2 and y.dim() == 2 and x.dtype == torch.float32 and y.dtype == torch.float32:
+            from ..ops import linear_act
+
+            return linear_act(x, y, None, "none")
+        return x @ y
+    return Tensor(f, [a, b], name)
+
+
+def _unary(fn, name):
+    def op(x, name=None):
+        return Tensor(fn, [x], name or op_name)
+    op_name = name
+    return op
+
+
+log = _unary(torch.log, "Log")
+exp = _unary(torch.exp, "Exp")
+sqrt = _unary(torch.sqrt, "Sqrt")
+square = _unary(torch.square, "Square")
+abs = _unary(torch.abs, "Abs")  # noqa: A001
+negative = _unary(torch.neg, "Neg")
+sigmoid = _unary(torch.sigmoid, "Sigmoid")
+tanh = _unary(torch.tanh, "Tanh")
+sin = _unary(torch.sin, "Sin")
+cos = _unary(torch.cos, "Cos")
+identity = _unary(lambda x: x, "Identity")
+stop_gradient = _unary(lambda x: x.detach(), "StopGradient")
+
+
+def _axes(reduction_indices, axis):
+    ax = axis if axis is not None else reduction_indices
+    if ax is None:
+        return None
+    return tuple(ax) if isinstance(ax, (list, tuple)) else (ax,)
+
+
+def reduce_mean(x, axis=None, keep_dims=False, reduction_indices=None, name="Mean", keepdims=None):
+    kd = keep_dims if keepdims is None else keepdims
+    ax = _axes(reduction_indices, axis)
+    return Tensor(lambda t: t.float().mean() if ax is None else t.float().mean(dim=ax, keepdim=kd), [x], name)
+
+
+def reduce_sum(x, axis=None, keep_dims=False, reduction_indices=None, name="Sum", keepdims=None):
+    kd = keep_dims if keepdims is None else keepdims
+    ax = _axes(reduction_indices, axis)
+    return Tensor(lambda t: t.sum() if ax is None else t.sum(dim=ax, keepdim=kd), [x], name)
+
+
+def reduce_max(x, axis=None, keep_dims=False, reduction_indices=None, name="Max"):
+    ax = _axes(reduction_indices, axis)
+    return Tensor(lambda t: t.max() if ax is None else t.amax(dim=ax, keepdim=keep_dims), [x], name)
+
+
+def argmax(x, axis=None, dimension=None, name="ArgMax"):
+    ax = axis if axis is not None else (dimension if dimension is not None else 0)
+    return Tensor(lambda t: t.argmax(dim=ax), [x], name)
+
+
+def argmin(x, axis=None, dimension=None, name="ArgMin"):
+    ax = axis if axis is not None else (dimension if dimension is not None else 0)
+    return Tensor(lambda t: t.argmin(dim=ax), [x], name)
+
+
+def equal(a, b, name="Equal"):
+    return Tensor(lambda x, y: x == y, [a, b], name)
+
+
+def cast(x, dtype, name="Cast"):
+    return Tensor(lambda t: t.to(dtype), [x], name, dtype=dtype)
+
+
+def reshape(x, shape, name="Reshape"):
+    return Tensor(lambda t: t.reshape(tuple(shape)), [x], name)
+
+
+def transpose(x, perm=None, name="transpose"):
+    return Tensor(lambda t: t.permute(*perm) if perm is not None else t.t(), [x], name)
+
+
+def concat(values, axis, name="concat"):
+    return Tensor(lambda *ts: torch.cat(ts, dim=axis), list(values), name)
+
+
+def stack(values, axis=0, name="stack"):
+    return Tensor(lambda *ts: torch.stack(ts, dim=axis), list(values), name)
+
+
+def shape(x, name="Shape"):
+    return Tensor(lambda t: torch.tensor(list(t.shape)), [x], name)
+
+
+def size(x, name="Size"):
+    return Tensor(lambda t: torch.tensor(t.numel()), [x], name)
+
+
+def zeros_like(x, name="zeros_like"):
+    return Tensor(torch.zeros_like, [x], name)
+
+
+def ones_like(x, name="ones_like"):
+    return Tensor(torch.ones_like, [x], name)
+
+
+def clip_by_value(x, lo, hi, name="clip_by_value"):
+    return Tensor(lambda t, a, b: torch.clamp(t, a, b), [x, lo, hi], name)
+
+
+def convert_to_tensor(x, dtype=None, name="Const"):
+    return x if isinstance(x, Tensor) else constant(x, dtype=dtype, name=name)
+
+
+def dynamic_partition(data, partitions, num_partitions, name="DynamicPartition"):
+    """Returns a list of tensors: data[partitions == i] (input_pipeline.py:30)."""
+    outs = []
+    for i in range(num_partitions):
+        def f(d, p, i=i):
+            if isinstance(d, (list, tuple)):
+                return [x for x, q in zip(d, p.tolist()) if q == i]
+            if isinstance(d, np.ndarray):
+                return d[p.cpu().numpy() == i]
+            return d[p == i]
+        outs.append(Tensor(f, [data, partitions], f"{name}_{i}"))
+    return outs

@@ -1,0 +1,266 @@
+"""TF-format checkpoints (V2 tensor bundle) for compat Variables.
+
+Reference: `tf.train.Saver()` (model_export.py:53) and the Supervisor's
+implicit saver (inactive there, no logdir); BASELINE requires the TF
+checkpoint format to stay compatible.  Bytes are produced by the native
+writer (csrc/runtime/tf_bundle.cpp): `prefix.index` (leveldb table of
+BundleEntryProto) + `prefix.data-00000-of-00001` + the text `checkpoint`
+state file (`model_checkpoint_path: "model.ckpt-N"`).  Variable names are the
+TF names (`weights/Variable_1`, `global_step`, Adam slots `w/Adam`, `w/Adam_1`,
+`beta1_power`...).  Only the chief writes; every rank can restore.
+"""
+from __future__ import annotations
+
+import glob
+import json
+import os
+import re
+import time
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from .. import _native
+
+TORCH_TO_TF = {torch.float32: 1, torch.float64: 2, torch.int32: 3, torch.uint8: 4, torch.int16: 5,
+               torch.int8: 6, torch.int64: 9, torch.bool: 10, torch.bfloat16: 14, torch.float16: 19}
+TF_TO_TORCH = {v: k for k, v in TORCH_TO_TF.items()}
+TF_TO_NUMPY = {1: np.float32, 2: np.float64, 3: np.int32, 4: np.uint8, 5: np.int16, 6: np.int8, 9: np.int64,
+               10: np.bool_, 19: np.float16}
+
+
+def write_bundle(prefix: str, tensors: Dict[str, torch.Tensor], shard_id: int = 0, num_shards: int = 1):
+    """Write {name: tensor} as a TF V2 bundle (names sorted inside the index)."""
+    C = _native.load()
+    d = os.path.dirname(prefix)
+    if d:
+        os.makedirs(d, exist_ok=True)
+    w = C.BundleWriter(prefix, shard_id, num_shards)
+    for name in sorted(tensors):
+        t = tensors[name].detach().cpu().contiguous()
+        dt = TORCH_TO_TF.get(t.dtype)
+        if dt is None:
+            raise TypeError(f"unsupported dtype {t.dtype} for {name}")
+        arr = t.view(torch.int16).numpy() if t.dtype == torch.bfloat16 else t.numpy()
+        w.add(name, dt, list(t.shape), np.ascontiguousarray(arr).reshape(-1).view(np.uint8))
+    w.finish()
+
+
+def read_bundle_index(prefix: str) -> dict:
+    return _native.load().bundle_read_index(prefix)
+
+
+def read_tensor(prefix: str, name: str) -> torch.Tensor:
+    C = _native.load()
+    idx = C.bundle_read_index(prefix)
+    if name not in idx:
+        raise KeyError(f"{name} not found in checkpoint {prefix}")
+    e = idx[name]
+    raw = C.bundle_read_tensor(prefix, name, True)
+    dt = e["dtype"]
+    if dt == 14:
+        t = torch.from_numpy(np.frombuffer(raw, dtype=np.int16).copy()).view(torch.bfloat16)
+    else:
+        t = torch.from_numpy(np.frombuffer(raw, dtype=TF_TO_NUMPY[dt]).copy())
+    return t.reshape(e["shape"])
+
+
+def list_variables(ckpt: str):
+    prefix = _resolve(ckpt)
+    return [(k, list(v["shape"])) for k, v in sorted(read_bundle_index(prefix).items()) if k]
+
+
+def load_variable(ckpt: str, name: str) -> np.ndarray:
+    return read_tensor(_resolve(ckpt), name).float().numpy() if read_tensor(_resolve(ckpt), name).dtype == torch.bfloat16 \
+        else read_tensor(_resolve(ckpt), name).numpy()
+
+
+class CheckpointReader:
+    """tf.train.NewCheckpointReader equivalent."""
+
+    def __init__(self, prefix):
+        self.prefix = _resolve(prefix)
+        self._idx = read_bundle_index(self.prefix)
+
+    def get_variable_to_shape_map(self):
+        return {k: list(v["shape"]) for k, v in self._idx.items() if k}
+
+    def get_variable_to_dtype_map(self):
+        return {k: TF_TO_TORCH.get(v["dtype"]) for k, v in self._idx.items() if k}
+
+    def has_tensor(self, name):
+        return name in self._idx and name != ""
+
+    def get_tensor(self, name) -> np.ndarray:
+        t = read_tensor(self.prefix, name)
+        return t.float().numpy() if t.dtype == torch.bfloat16 else t.numpy()
+
+
+def NewCheckpointReader(prefix):  # noqa: N802 (TF name)
+    return CheckpointReader(prefix)
+
+
+# ----------------------------------------------------------------------- state file
+class CheckpointState:
+    def __init__(self, model_checkpoint_path: str, all_model_checkpoint_paths: List[str]):
+        self.model_checkpoint_path = model_checkpoint_path
+        self.all_model_checkpoint_paths = list(all_model_checkpoint_paths)
+
+    def __repr__(self):
+        return f"CheckpointState({self.model_checkpoint_path!r}, {self.all_model_checkpoint_paths!r})"
+
+
+def _state_path(d):
+    return os.path.join(d, "checkpoint")
+
+
+def update_checkpoint_state(save_dir: str, model_checkpoint_path: str, all_model_checkpoint_paths=None,
+                            latest_filename: str = "checkpoint"):
+    allp = list(all_model_checkpoint_paths or [model_checkpoint_path])
+    if model_checkpoint_path not in allp:
+        allp.append(model_checkpoint_path)
+
+    def rel(p):
+        return os.path.relpath(p, save_dir) if os.path.isabs(p) and os.path.dirname(p) == os.path.abspath(save_dir) else p
+    lines = [f'model_checkpoint_path: "{rel(model_checkpoint_path)}"']
+    lines += [f'all_model_checkpoint_paths: "{rel(p)}"' for p in allp]
+    tmp = os.path.join(save_dir, latest_filename + ".tmp")
+    with open(tmp, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    os.replace(tmp, os.path.join(save_dir, latest_filename))
+
+
+def get_checkpoint_state(checkpoint_dir: str, latest_filename: str = "checkpoint") -> Optional[CheckpointState]:
+    p = os.path.join(checkpoint_dir, latest_filename)
+    if not os.path.exists(p):
+        return None
+    model, allp = None, []
+    for line in open(p):
+        m = re.match(r'\s*(model_checkpoint_path|all_model_checkpoint_paths)\s*:\s*"(.*)"', line)
+        if not m:
+            continue
+        path = m.group(2)
+        if not os.path.isabs(path):
+            path = os.path.join(checkpoint_dir, path)
+        if m.group(1) == "model_checkpoint_path":
+            model = path
+        else:
+            allp.append(path)
+    return CheckpointState(model, allp) if model else None
+
+
+def checkpoint_exists(prefix: str) -> bool:
+    return os.path.exists(prefix + ".index")
+
+
+def latest_checkpoint(checkpoint_dir: str, latest_filename: str = "checkpoint") -> Optional[str]:
+    st = get_checkpoint_state(checkpoint_dir, latest_filename)
+    if st and checkpoint_exists(st.model_checkpoint_path):
+        return st.model_checkpoint_path
+    return None
+
+
+def _resolve(ckpt: str) -> str:
+    if os.path.isdir(ckpt):
+        p = latest_checkpoint(ckpt)
+        if p is None:
+            raise FileNotFoundError(f"no checkpoint in {ckpt}")
+        return p
+    return ckpt
+
+
+# ----------------------------------------------------------------------- Saver
+class Saver:
+    def __init__(self, var_list=None, max_to_keep: int = 5, keep_checkpoint_every_n_hours: float = 10000.0,
+                 sharded: bool = False, name: str = None, restore_sequentially: bool = False,
+                 write_version: int = 2, save_relative_paths: bool = False, defer_build=False, **kw):
+        self._var_list = var_list
+        self.max_to_keep = max_to_keep
+        self.keep_every = keep_checkpoint_every_n_hours * 3600.0
+        self._last_kept = time.time()
+        self._kept: List[str] = []
+        self.sharded = sharded
+
+    def _vars(self) -> Dict[str, object]:
+        from .graph import global_variables
+
+        vl = self._var_list
+        if vl is None:
+            vl = global_variables()
+        if isinstance(vl, dict):
+            return dict(vl)
+        out = {}
+        for v in vl:
+            out[v.name[:-2] if v.name.endswith(":0") else v.name] = v
+        return out
+
+    @staticmethod
+    def _value(v) -> torch.Tensor:
+        if hasattr(v, "value") and isinstance(v.value, torch.Tensor):
+            return v.value
+        if isinstance(v, torch.Tensor):
+            return v
+        raise TypeError(f"cannot save {v!r}")
+
+    def save(self, sess=None, save_path: str = "model.ckpt", global_step=None, latest_filename="checkpoint",
+             meta_graph_suffix="meta", write_meta_graph=True, write_state=True) -> Optional[str]:
+        from ..parallel.world import get_world
+
+        step = global_step
+        if step is not None and not isinstance(step, (int, np.integer)):
+            step = int(np.asarray(sess.run(step) if hasattr(step, "_eval") else step))
+        prefix = f"{save_path}-{int(step)}" if step is not None else save_path
+        w = get_world()
+        tensors = {k: self._value(v) for k, v in self._vars().items()}
+        if w.rank == 0:
+            write_bundle(prefix, tensors)
+            if write_meta_graph:
+                meta = {k: {"shape": list(t.shape), "dtype": str(t.dtype)} for k, t in tensors.items()}
+                with open(prefix + ".meta.json", "w") as f:
+                    json.dump({"variables": meta, "format": "dtf-meta-v1"}, f, indent=1)
+            d = os.path.dirname(os.path.abspath(prefix))
+            self._kept.append(prefix)
+            while self.max_to_keep and len(self._kept) > self.max_to_keep:
+                old = self._kept.pop(0)
+                if time.time() - self._last_kept >= self.keep_every:
+                    self._last_kept = time.time()
+                    continue
+                for f in glob.glob(old + ".*"):
+                    try:
+                        os.remove(f)
+                    except OSError:
+                        pass
+            if write_state:
+                update_checkpoint_state(d, os.path.abspath(prefix), [os.path.abspath(p) for p in self._kept],
+                                        latest_filename)
+        return prefix
+
+    def restore(self, sess=None, save_path: str = None):
+        prefix = _resolve(save_path)
+        idx = read_bundle_index(prefix)
+        missing = []
+        for name, v in self._vars().items():
+            if name not in idx:
+                missing.append(name)
+                continue
+            t = read_tensor(prefix, name)
+            dst = self._value(v)
+            if tuple(t.shape) != tuple(dst.shape):
+                raise ValueError(f"shape mismatch for {name}: ckpt {tuple(t.shape)} vs {tuple(dst.shape)}")
+            with torch.no_grad():
+                dst.data.copy_(t.to(dst.device, dst.dtype))
+            if hasattr(v, "initialized"):
+                v.initialized = True
+        if missing:
+            raise KeyError(f"variables not found in checkpoint {prefix}: {missing}")
+
+    def recover_last_checkpoints(self, paths):
+        self._kept = [p for p in paths if checkpoint_exists(p)]
+
+    @property
+    def last_checkpoints(self):
+        return list(self._kept)
+
+    def as_saver_def(self):
+        return {"version": 2, "max_to_keep": self.max_to_keep}

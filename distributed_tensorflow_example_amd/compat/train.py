@@ -1,0 +1,948 @@
+"""tf.train equivalents: Server, replica_device_setter, optimizers,
+SyncReplicasOptimizer, Supervisor, MonitoredTrainingSession + hooks, Saver.
+
+Semantics shift: the reference trains asynchronously
+against one parameter server (between-graph replication, Hogwild updates).
+Here every worker holds a full replica on its own GPU and each `train_op`
+run is one *synchronous* data-parallel step: local gradients are averaged by
+an all-reduce (RCCL over xGMI on GPU, gloo on CPU) and applied by the fused
+optimizer kernel.  `global_step` therefore counts synchronous steps (not
+worker-steps).  Chief-only init + broadcast replaces every worker re-running
+init_op (the lr2.py:419 race, A6); ps tasks are control-plane members that
+exit when all workers have sent their done token (lr2.py:337-346 intent).
+"""
+from __future__ import annotations
+
+import atexit
+import contextlib
+import os
+import threading
+import time
+from typing import Any, Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from .. import optim as _optim
+from ..parallel import world as _world
+from ..parallel.cluster import ClusterSpec, Rendezvous, split_address
+from ..utils import logging as _log
+from . import saver as _saver
+from .graph import (GLOBAL_STEP, GLOBAL_VARIABLES, LOCAL_VARIABLES, TRAINABLE_VARIABLES, Operation,
+                    RunContext, Tensor, Variable, constant_initializer, get_default_graph, get_variable,
+                    global_variables, local_variables, trainable_variables)
+from .queues import (Coordinator, QueueRunner, add_queue_runner, batch, shuffle_batch, slice_input_producer,
+                     start_queue_runners, string_input_producer)
+from .saver import (CheckpointReader, NewCheckpointReader, Saver, checkpoint_exists, get_checkpoint_state,
+                    latest_checkpoint, list_variables, load_variable, update_checkpoint_state)
+from .session import ConfigProto, Session
+from .summary import FileWriter, SummaryWriter
+
+__all__ = [
+    "ClusterSpec", "Server", "replica_device_setter", "GradientDescentOptimizer", "MomentumOptimizer",
+    "AdamOptimizer", "AdagradOptimizer", "RMSPropOptimizer", "SyncReplicasOptimizer", "Supervisor",
+    "MonitoredTrainingSession", "MonitoredSession", "SingularMonitoredSession", "Scaffold", "Saver",
+    "Coordinator", "QueueRunner", "start_queue_runners", "add_queue_runner", "batch", "shuffle_batch",
+    "slice_input_producer", "string_input_producer", "latest_checkpoint", "get_checkpoint_state",
+    "get_global_step", "get_or_create_global_step", "create_global_step", "global_step", "SummaryWriter",
+    "SessionRunHook", "SessionRunArgs", "StopAtStepHook", "CheckpointSaverHook", "SummarySaverHook",
+    "LoggingTensorHook", "NanTensorHook", "StepCounterHook", "FinalOpsHook", "NanLossDuringTrainingError",
+]
+
+_SERVER: Optional["Server"] = None
+
+
+# ======================================================================= Server
+class Server:
+    """tf.train.Server: one per task.  Joins the cluster rendezvous (native TCP
+    store hosted by worker:0) and, for workers, the data-parallel world."""
+
+    def __init__(self, server_or_cluster_def, job_name: str = None, task_index: int = 0, protocol=None,
+                 config=None, start: bool = True, timeout_s: float = None):
+        global _SERVER
+        cluster = server_or_cluster_def
+        if isinstance(cluster, dict):
+            cluster = ClusterSpec(cluster)
+        if not isinstance(cluster, ClusterSpec):
+            raise TypeError("Server needs a ClusterSpec or dict")
+        if not job_name:
+            raise ValueError("job_name is required (e.g. --job_name=worker)")
+        self.cluster = cluster
+        self.job_name = job_name
+        self.task_index = int(task_index)
+        self.server_def = {"cluster": cluster.as_dict(), "job_name": job_name, "task_index": self.task_index}
+        timeout_s = float(timeout_s or os.environ.get("DTF_RENDEZVOUS_TIMEOUT", 300))
+        self.rdv = Rendezvous(cluster, job_name, self.task_index, timeout_s=timeout_s)
+        host, port = split_address(cluster.task_address(job_name, self.task_index))
+        self.target = f"dtf://{host}:{port}"
+        self.world = None
+        if self.rdv.is_worker:
+            backend = os.environ.get("DTF_BACKEND", "auto")
+            self.world = _world.init_from_rendezvous(self.rdv, backend=backend, timeout_s=timeout_s)
+            get_default_graph().device = self.world.device
+        self.rdv.start_heartbeat()
+        self._done = False
+        _SERVER = self
+        atexit.register(self._atexit)
+
+    @property
+    def is_chief(self) -> bool:
+        return self.rdv.is_chief
+
+    def start(self):
+        return self
+
+    def join(self, timeout: float = -1.0):
+        """ps: block until every worker sent its done token (then return).
+        worker: same wait (TF's join never returns; returning lets tasks exit)."""
+        _log.info(f"[{self.job_name}:{self.task_index}] join: waiting for {self.rdv.num_workers} worker(s)")
+
+        def on_dead(dead):
+            _log.warning(f"[{self.job_name}:{self.task_index}] no heartbeat from worker(s) {dead}")
+        ok = self.rdv.wait_all_workers_done(timeout=timeout, on_dead=on_dead)
+        _log.info(f"[{self.job_name}:{self.task_index}] join finished ({'all done' if ok else 'timeout'})")
+        return ok
+
+    def signal_done(self):
+        if not self._done and self.rdv.is_worker:
+            self._done = True
+            try:
+                self.rdv.signal_done()
+            except Exception:
+                pass
+
+    def _atexit(self):
+        self.signal_done()
+
+    @staticmethod
+    def create_local_server(config=None, start=True):
+        from ..parallel.cluster import ClusterSpec as CS
+
+        import socket
+
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        return Server(CS({"worker": [f"127.0.0.1:{port}"]}), "worker", 0)
+
+
+def current_server() -> Optional[Server]:
+    return _SERVER
+
+
+def _world_or_local():
+    w = _world._WORLD
+    return w if w is not None else _world.World(device=get_default_graph().device)
+
+
+# ======================================================================= placement
+def replica_device_setter(ps_tasks: int = 0, ps_device: str = "/job:ps", worker_device: str = "/job:worker",
+                          merge_devices: bool = True, cluster=None, ps_ops=None, ps_strategy=None):
+    """Returns the placement function of tf.train.replica_device_setter:
+    variables round-robin over ps tasks, everything else on worker_device.
+    The placement is recorded on each Variable (`.placement`) -- under sync DP
+    dense variables are replicated on every worker's GPU and all-reduced, and
+    `parallel.sharded_embedding` row-shards the huge ones across workers."""
+    if cluster is not None:
+        cs = cluster if isinstance(cluster, ClusterSpec) else ClusterSpec(cluster)
+        ps_tasks = cs.num_tasks("ps")
+    ps_ops = ps_ops or ["Variable", "VariableV2", "VarHandleOp", "AutoReloadVariable", "MutableHashTable"]
+    state = {"next": 0}
+
+    def place(op):
+        if ps_tasks and getattr(op, "type", "") in ps_ops:
+            if ps_strategy is not None:
+                k = ps_strategy(op)
+            else:
+                k = state["next"] % ps_tasks
+                state["next"] += 1
+            return f"{ps_device}/task:{k}"
+        return worker_device
+    place.ps_tasks = ps_tasks
+    return place
+
+
+# ======================================================================= global step
+def create_global_step(graph=None) -> Variable:
+    g = get_default_graph()
+    if g.get_collection(GLOBAL_STEP):
+        raise ValueError("global_step already exists")
+    v = get_variable("global_step", [], dtype=torch.int64, initializer=constant_initializer(0), trainable=False)
+    g.add_to_collection(GLOBAL_STEP, v)
+    return v
+
+
+def get_global_step(graph=None) -> Optional[Variable]:
+    g = get_default_graph()
+    c = g.get_collection(GLOBAL_STEP)
+    if c:
+        return c[0]
+    v = g._vars_by_name.get("global_step")
+    return v
+
+
+def get_or_create_global_step(graph=None) -> Variable:
+    return get_global_step() or create_global_step()
+
+
+def global_step(sess, global_step_tensor) -> int:
+    return int(np.asarray(sess.run(global_step_tensor)))
+
+
+# ======================================================================= gradient sync
+class _GradSync:
+    """Flat-bucket all-reduce (average) of a var_list's gradients across workers."""
+
+    def __init__(self, params: List[torch.Tensor], comm_dtype=None):
+        self.params = params
+        self.sizes = [p.numel() for p in params]
+        self.flat = torch.zeros(sum(self.sizes), dtype=torch.float32, device=params[0].device)
+        self.views = []
+        off = 0
+        for p, n in zip(params, self.sizes):
+            self.views.append(self.flat[off:off + n].view_as(p))
+            off += n
+        self.comm_dtype = comm_dtype
+
+    def __call__(self, grads: List[Optional[torch.Tensor]]) -> List[torch.Tensor]:
+        with torch.no_grad():
+            for v, g in zip(self.views, grads):
+                if g is None:
+                    v.zero_()
+                else:
+                    v.copy_(g)
+            w = _world_or_local()
+            if w.world_size > 1:
+                if self.comm_dtype is not None and self.flat.is_cuda:
+                    buf = self.flat.to(self.comm_dtype)
+                    w.all_reduce(buf, "sum")
+                    self.flat.copy_(buf)
+                else:
+                    w.all_reduce(self.flat, "sum")
+        return self.views
+
+
+# ======================================================================= optimizers
+class Optimizer:
+    """Base: compute_gradients / apply_gradients / minimize over compat Variables.
+
+    `minimize` returns an Operation; running it performs one synchronous step:
+    forward (memoised with other fetches of the same run), backward,
+    all-reduce of the gradients across workers, fused optimizer update,
+    global_step += 1."""
+
+    _kind = "sgd"
+    _slot_names: Sequence[str] = ()
+
+    def __init__(self, learning_rate, use_locking=False, name=None, **kw):
+        self.learning_rate = learning_rate
+        self.name = name or type(self).__name__.replace("Optimizer", "")
+        self._kw = kw
+        self.sync_replicas = True
+        self.comm_dtype = None
+
+    def _make_fused(self, params):
+        lr = float(self._lr_value())
+        return _optim.FusedSGD(params, lr)
+
+    def _lr_value(self):
+        lr = self.learning_rate
+        if isinstance(lr, Tensor):
+            v = RunContext({}, get_default_graph().device).eval(lr)
+            return float(v.detach().cpu()) if isinstance(v, torch.Tensor) else float(v)
+        return float(lr)
+
+    def compute_gradients(self, loss, var_list=None, **kw):
+        var_list = list(var_list if var_list is not None else trainable_variables())
+        key = id(loss)
+
+        def grads_of(ctx):
+            st = ctx.state.setdefault("grads", {})
+            if key not in st:
+                l = ctx.eval(loss)
+                gs = torch.autograd.grad(l, [v.value for v in var_list], allow_unused=True)
+                st[key] = list(gs)
+            return st[key]
+        pairs = []
+        for i, v in enumerate(var_list):
+            t = Tensor(None, [], "gradients")
+            t._eval = (lambda ctx, i=i: grads_of(ctx)[i])
+            pairs.append((t, v))
+        return pairs
+
+    def apply_gradients(self, grads_and_vars, global_step=None, name=None) -> Operation:
+        pairs = list(grads_and_vars)
+        vars_ = [v for _, v in pairs]
+        gtens = [g for g, _ in pairs]
+        opt = self
+        params = [v.value for v in vars_]
+        # slots exist as soon as the train op does (TF creates them in
+        # minimize), so a Saver built afterwards checkpoints/restores them
+        fused = opt._make_fused(params)
+        opt._register_slots(vars_, fused)
+        sync = _GradSync(params, opt.comm_dtype)
+
+        def run(ctx):
+            gs = [ctx.eval(g) if g is not None else None for g in gtens]
+            if opt.sync_replicas:
+                gs = sync(gs)
+            else:
+                gs = [g if g is not None else torch.zeros_like(p) for g, p in zip(gs, params)]
+            if isinstance(opt.learning_rate, Tensor):
+                fused.set_lr(opt._lr_value())
+            fused.step(grads=[g.contiguous() for g in gs])
+            if global_step is not None:
+                with torch.no_grad():
+                    global_step.value.data += 1
+            return None
+        op = Operation(None, [], name or self.name)
+        op._eval = run
+        return op
+
+    def minimize(self, loss, global_step=None, var_list=None, name=None, **kw) -> Operation:
+        op = self.apply_gradients(self.compute_gradients(loss, var_list), global_step=global_step, name=name)
+        op.loss = loss
+        return op
+
+    # slot variables with TF names (w/Adam, w/Adam_1, beta1_power, ...) for checkpoints
+    def _register_slots(self, vars_, fused):
+        g = get_default_graph()
+        for i, v in enumerate(vars_):
+            base = v.name[:-2]
+            for sname, tens in zip(self._slot_names, (fused.m[i], fused.v[i])):
+                if tens is None:
+                    continue
+                sv = _SlotVariable(f"{base}/{sname}", tens)
+                g.add_to_collection(GLOBAL_VARIABLES, sv)
+
+    def get_slot_names(self):
+        return list(self._slot_names)
+
+
+class _SlotVariable:
+    def __init__(self, name, tensor):
+        self.name = name + ":0"
+        self.value = tensor
+        self.initialized = True
+        self.trainable = False
+
+    def _initialize(self):
+        with torch.no_grad():
+            self.value.zero_()
+
+
+class GradientDescentOptimizer(Optimizer):
+    def _make_fused(self, params):
+        return _optim.FusedSGD(params, self._lr_value())
+
+
+class MomentumOptimizer(Optimizer):
+    _slot_names = ("Momentum",)
+
+    def __init__(self, learning_rate, momentum, use_locking=False, name="Momentum", use_nesterov=False):
+        super().__init__(learning_rate, use_locking, name)
+        self.momentum, self.nesterov = momentum, use_nesterov
+
+    def _make_fused(self, params):
+        return _optim.FusedMomentum(params, self._lr_value(), self.momentum, self.nesterov)
+
+
+class AdamOptimizer(Optimizer):
+    _slot_names = ("Adam", "Adam_1")
+
+    def __init__(self, learning_rate=0.001, beta1=0.9, beta2=0.999, epsilon=1e-8, use_locking=False,
+                 name="Adam"):
+        super().__init__(learning_rate, use_locking, name)
+        self.beta1, self.beta2, self.epsilon = beta1, beta2, epsilon
+
+    def _make_fused(self, params):
+        return _optim.FusedAdam(params, self._lr_value(), self.beta1, self.beta2, self.epsilon)
+
+    def _register_slots(self, vars_, fused):
+        super()._register_slots(vars_, fused)
+        g = get_default_graph()
+        # TF's non-slot accumulators beta1_power / beta2_power (= beta^t)
+        b1p = _PowerVariable("beta1_power", self.beta1, fused)
+        b2p = _PowerVariable("beta2_power", self.beta2, fused)
+        for v in (b1p, b2p):
+            g.add_to_collection(GLOBAL_VARIABLES, v)
+
+
+class _PowerVariable:
+    """beta^t as a saveable variable, tied to the fused optimizer's step."""
+
+    def __init__(self, name, beta, fused):
+        self.name = name + ":0"
+        self.beta = beta
+        self.fused = fused
+        self.initialized = True
+        self._buf = torch.zeros((), dtype=torch.float32)
+
+    @property
+    def value(self):
+        t = int(self.fused.step_t.item())
+        self._buf.fill_(self.beta ** (t + 1))  # TF stores beta^(t+1) after t updates
+        return self._buf
+
+    def _initialize(self):
+        pass
+
+
+class AdagradOptimizer(Optimizer):
+    _slot_names = ("Adagrad",)
+
+    def __init__(self, learning_rate, initial_accumulator_value=0.1, use_locking=False, name="Adagrad"):
+        super().__init__(learning_rate, use_locking, name)
+        self.init_acc = initial_accumulator_value
+
+    def _make_fused(self, params):
+        return _TorchOpt(params, self._lr_value(), "adagrad", init_acc=self.init_acc)
+
+
+class RMSPropOptimizer(Optimizer):
+    _slot_names = ("RMSProp", "Momentum")
+
+    def __init__(self, learning_rate, decay=0.9, momentum=0.0, epsilon=1e-10, use_locking=False,
+                 centered=False, name="RMSProp"):
+        super().__init__(learning_rate, use_locking, name)
+        self.decay, self.mom, self.eps = decay, momentum, epsilon
+
+    def _make_fused(self, params):
+        return _TorchOpt(params, self._lr_value(), "rmsprop", decay=self.decay, mom=self.mom, eps=self.eps)
+
+
+class _TorchOpt:
+    """Less common TF optimizers, expressed with PyTorch ops (any device)."""
+
+    def __init__(self, params, lr, kind, init_acc=0.1, decay=0.9, mom=0.0, eps=1e-10):
+        self.params, self.kind = params, kind
+        self.lr_v = lr
+        self.m = [torch.full_like(p, init_acc) if kind == "adagrad" else torch.ones_like(p) for p in params]
+        self.v = [torch.zeros_like(p) for p in params]
+        self.decay, self.mom, self.eps = decay, mom, eps
+        self.step_t = torch.zeros(1, dtype=torch.int64)
+
+    def set_lr(self, lr):
+        self.lr_v = lr
+
+    @torch.no_grad()
+    def step(self, grads):
+        self.step_t += 1
+        for p, g, m, v in zip(self.params, grads, self.m, self.v):
+            if self.kind == "adagrad":
+                m.add_(g * g)
+                p.sub_(self.lr_v * g / m.sqrt())
+            else:
+                m.mul_(self.decay).add_((1 - self.decay) * g * g)
+                v.mul_(self.mom).add_(self.lr_v * g / (m + self.eps).sqrt())
+                p.sub_(v)
+
+
+class SyncReplicasOptimizer(Optimizer):
+    """tf.train.SyncReplicasOptimizer (the commented path of example.py:109-123).
+
+    Aggregation is an all-reduce over the workers; `replicas_to_aggregate` must
+    equal the number of workers (backup workers / stale-gradient dropping are
+    not modelled: every step is fully synchronous)."""
+
+    def __init__(self, opt: Optimizer, replicas_to_aggregate: int, total_num_replicas: int = None,
+                 replica_id: int = None, variable_averages=None, variables_to_average=None,
+                 use_locking=False, name="sync_replicas"):
+        super().__init__(opt.learning_rate, use_locking, name)
+        self.opt = opt
+        self.replicas_to_aggregate = replicas_to_aggregate
+        self.total_num_replicas = total_num_replicas or replicas_to_aggregate
+        w = _world._WORLD
+        if w is not None and w.world_size > 1 and replicas_to_aggregate != w.world_size:
+            _log.warning(f"SyncReplicasOptimizer: replicas_to_aggregate={replicas_to_aggregate} but "
+                         f"{w.world_size} workers; all workers are aggregated every step")
+
+    def compute_gradients(self, *a, **kw):
+        return self.opt.compute_gradients(*a, **kw)
+
+    def apply_gradients(self, grads_and_vars, global_step=None, name=None):
+        self.opt.sync_replicas = True
+        return self.opt.apply_gradients(grads_and_vars, global_step, name)
+
+    def get_init_tokens_op(self, num_tokens=-1):
+        return Operation(lambda: None, [], "sync_token_init")
+
+    def get_chief_queue_runner(self):
+        return QueueRunner(None, [])
+
+    def make_session_run_hook(self, is_chief, num_tokens=-1):
+        return SessionRunHook()
+
+
+# ======================================================================= init / sync helpers
+def _broadcast_variables(vars_):
+    w = _world_or_local()
+    if w.world_size <= 1:
+        return
+    with torch.no_grad():
+        for v in vars_:
+            val = v.value
+            if isinstance(val, torch.Tensor):
+                w.broadcast(val.data, 0)
+
+
+def _init_or_restore(sess, is_chief, init_op, local_init_op, init_fn, checkpoint_dir, saver, init_feed_dict):
+    restored = None
+    if checkpoint_dir:
+        ck = latest_checkpoint(checkpoint_dir)
+        if ck:
+            (saver or Saver()).restore(sess, ck)
+            restored = ck
+    if restored is None:
+        if is_chief:
+            if init_op is not None:
+                sess.run(init_op, feed_dict=init_feed_dict)
+            else:
+                for v in global_variables():
+                    v._initialize()
+            if init_fn is not None:
+                init_fn(sess)
+    # non-chief workers receive the chief's values (no re-initialisation race)
+    _broadcast_variables([v for v in global_variables() if isinstance(v, Variable)])
+    for v in global_variables():
+        if isinstance(v, Variable):
+            v.initialized = True
+    if local_init_op is not None:
+        sess.run(local_init_op)
+    else:
+        for v in local_variables():
+            v._initialize()
+    return restored
+
+
+# ======================================================================= Supervisor
+class Supervisor:
+    USE_DEFAULT = object()
+
+    def __init__(self, graph=None, ready_op=USE_DEFAULT, is_chief=True, init_op=USE_DEFAULT,
+                 init_feed_dict=None, local_init_op=USE_DEFAULT, logdir=None, summary_op=USE_DEFAULT,
+                 saver=USE_DEFAULT, global_step=USE_DEFAULT, save_summaries_secs=120, save_model_secs=600,
+                 recovery_wait_secs=30, stop_grace_secs=120, checkpoint_basename="model.ckpt",
+                 session_manager=None, summary_writer=USE_DEFAULT, init_fn=None, **kw):
+        self.is_chief = is_chief
+        self.init_op = None if init_op is self.USE_DEFAULT else init_op
+        if isinstance(self.init_op, (list, tuple)):
+            from .graph import group
+
+            self.init_op = group(*self.init_op)
+        self.local_init_op = None if local_init_op is self.USE_DEFAULT else local_init_op
+        self.init_feed_dict = init_feed_dict
+        self.init_fn = init_fn
+        self.logdir = logdir
+        self.global_step = get_global_step() if global_step is self.USE_DEFAULT else global_step
+        self.saver = (Saver() if logdir else None) if saver is self.USE_DEFAULT else saver
+        self.summary_op = None if summary_op is self.USE_DEFAULT else summary_op
+        self.save_model_secs = save_model_secs
+        self.save_summaries_secs = save_summaries_secs
+        self.checkpoint_basename = checkpoint_basename
+        self.coord = Coordinator()
+        self.summary_writer = None
+        if logdir and is_chief and summary_writer is self.USE_DEFAULT:
+            self.summary_writer = FileWriter(logdir, get_default_graph())
+        elif summary_writer not in (self.USE_DEFAULT, None):
+            self.summary_writer = summary_writer
+        self._threads: List[threading.Thread] = []
+        self._sess = None
+        self.save_path = os.path.join(logdir, checkpoint_basename) if logdir else None
+
+    def prepare_or_wait_for_session(self, master="", config=None, wait_for_checkpoint=False,
+                                    max_wait_secs=7200, start_standard_services=True) -> Session:
+        sess = Session(master, config=config)
+        _init_or_restore(sess, self.is_chief, self.init_op, self.local_init_op, self.init_fn,
+                         self.logdir, self.saver, self.init_feed_dict)
+        self._sess = sess
+        if start_standard_services and self.is_chief and self.logdir:
+            self._start_services(sess)
+        return sess
+
+    def _start_services(self, sess):
+        if self.saver is not None and self.save_model_secs:
+            def ckpt_loop():
+                while not self.coord.wait_for_stop(self.save_model_secs):
+                    self.saver.save(sess, self.save_path, global_step=self._gstep(sess))
+            t = threading.Thread(target=ckpt_loop, daemon=True, name="sv-checkpoint")
+            t.start()
+            self._threads.append(t)
+        if self.summary_op is not None and self.summary_writer is not None and self.save_summaries_secs:
+            def sum_loop():
+                while not self.coord.wait_for_stop(self.save_summaries_secs):
+                    try:
+                        self.summary_writer.add_summary(sess.run(self.summary_op), self._gstep(sess))
+                    except Exception:
+                        pass
+            t = threading.Thread(target=sum_loop, daemon=True, name="sv-summary")
+            t.start()
+            self._threads.append(t)
+
+    def _gstep(self, sess):
+        return int(np.asarray(sess.run(self.global_step))) if self.global_step is not None else None
+
+    @contextlib.contextmanager
+    def managed_session(self, master="", config=None, start_standard_services=True, close_summary_writer=True):
+        sess = self.prepare_or_wait_for_session(master, config, start_standard_services=start_standard_services)
+        try:
+            yield sess
+        except Exception as e:
+            self.coord.request_stop(e)
+            raise
+        finally:
+            self.stop(close_summary_writer=close_summary_writer)
+
+    def start_queue_runners(self, sess, queue_runners=None):
+        threads = []
+        for qr in (queue_runners or get_default_graph().get_collection("queue_runners")):
+            threads += qr.create_threads(sess, coord=self.coord, daemon=True, start=True)
+        return threads
+
+    def summary_computed(self, sess, summary, global_step=None):
+        if self.summary_writer is not None:
+            self.summary_writer.add_summary(summary, global_step if global_step is not None else self._gstep(sess))
+
+    def should_stop(self):
+        return self.coord.should_stop()
+
+    def request_stop(self, ex=None):
+        self.coord.request_stop(ex)
+
+    def stop(self, threads=None, close_summary_writer=True, ignore_live_threads=False):
+        self.coord.request_stop()
+        for t in self._threads:
+            t.join(5)
+        if self.is_chief and self.saver is not None and self._sess is not None and self.logdir:
+            self.saver.save(self._sess, self.save_path, global_step=self._gstep(self._sess))
+        if close_summary_writer and self.summary_writer is not None:
+            self.summary_writer.close()
+        srv = current_server()
+        if srv is not None:
+            srv.signal_done()
+
+    def wait_for_stop(self):
+        self.coord.wait_for_stop()
+
+    @property
+    def session_manager(self):
+        return self
+
+
+# ======================================================================= hooks
+class SessionRunArgs:
+    def __init__(self, fetches=None, feed_dict=None, options=None):
+        self.fetches = fetches
+        self.feed_dict = feed_dict
+        self.options = options
+
+
+class SessionRunValues:
+    def __init__(self, results, options=None, run_metadata=None):
+        self.results = results
+        self.options = options
+        self.run_metadata = run_metadata
+
+
+class SessionRunContext:
+    def __init__(self, original_args, session):
+        self.original_args = original_args
+        self.session = session
+        self._stop = False
+
+    def request_stop(self):
+        self._stop = True
+
+    @property
+    def stop_requested(self):
+        return self._stop
+
+
+class SessionRunHook:
+    def begin(self):
+        pass
+
+    def after_create_session(self, session, coord):
+        pass
+
+    def before_run(self, run_context):
+        return None
+
+    def after_run(self, run_context, run_values):
+        pass
+
+    def end(self, session):
+        pass
+
+
+class NanLossDuringTrainingError(RuntimeError):
+    pass
+
+
+class StopAtStepHook(SessionRunHook):
+    def __init__(self, num_steps=None, last_step=None):
+        if (num_steps is None) == (last_step is None):
+            raise ValueError("exactly one of num_steps and last_step")
+        self.num_steps, self.last_step = num_steps, last_step
+
+    def after_create_session(self, session, coord):
+        gs = get_global_step()
+        cur = int(np.asarray(session.run(gs))) if gs is not None else 0
+        if self.last_step is None:
+            self.last_step = cur + self.num_steps
+
+    def before_run(self, ctx):
+        gs = get_global_step()
+        return SessionRunArgs(gs) if gs is not None else None
+
+    def after_run(self, ctx, vals):
+        if vals.results is not None and int(np.asarray(vals.results)) + 1 >= self.last_step:
+            ctx.request_stop()
+
+
+class CheckpointSaverHook(SessionRunHook):
+    def __init__(self, checkpoint_dir, save_secs=None, save_steps=None, saver=None,
+                 checkpoint_basename="model.ckpt", scaffold=None, listeners=None):
+        self.dir = checkpoint_dir
+        self.save_secs, self.save_steps = save_secs, save_steps
+        self.saver = saver
+        self.path = os.path.join(checkpoint_dir, checkpoint_basename)
+        self._last_t = time.time()
+        self._last_step = None
+        self.listeners = listeners or []
+
+    def _gs(self, sess):
+        gs = get_global_step()
+        return int(np.asarray(sess.run(gs))) if gs is not None else 0
+
+    def after_create_session(self, session, coord):
+        self.saver = self.saver or Saver()
+        self._last_step = self._gs(session)
+        if not latest_checkpoint(self.dir):
+            self.saver.save(session, self.path, global_step=self._last_step)
+
+    def after_run(self, ctx, vals):
+        step = self._gs(ctx.session)
+        due = (self.save_steps and step - self._last_step >= self.save_steps) or \
+              (self.save_secs and time.time() - self._last_t >= self.save_secs)
+        if due:
+            self.saver.save(ctx.session, self.path, global_step=step)
+            self._last_step, self._last_t = step, time.time()
+            for l in self.listeners:
+                getattr(l, "after_save", lambda *a: None)(ctx.session, step)
+
+    def end(self, session):
+        step = self._gs(session)
+        if step != self._last_step:
+            self.saver.save(session, self.path, global_step=step)
+
+
+class SummarySaverHook(SessionRunHook):
+    def __init__(self, save_steps=None, save_secs=None, output_dir=None, summary_writer=None, scaffold=None,
+                 summary_op=None):
+        self.save_steps, self.save_secs = save_steps, save_secs
+        self.writer = summary_writer or (FileWriter(output_dir) if output_dir else None)
+        self.op = summary_op
+        self._n = 0
+
+    def before_run(self, ctx):
+        op = self.op
+        if op is None:
+            from .summary import merge_all
+
+            op = self.op = merge_all()
+        due = op is not None and self.save_steps and self._n % self.save_steps == 0
+        gs = get_global_step()
+        return SessionRunArgs({"s": op if due else None, "g": gs})
+
+    def after_run(self, ctx, vals):
+        self._n += 1
+        r = vals.results or {}
+        if r.get("s") is not None and self.writer is not None:
+            self.writer.add_summary(r["s"], int(np.asarray(r["g"])) if r.get("g") is not None else self._n)
+
+    def end(self, session):
+        if self.writer is not None:
+            self.writer.flush()
+
+
+class LoggingTensorHook(SessionRunHook):
+    def __init__(self, tensors, every_n_iter=None, every_n_secs=None, at_end=False, formatter=None):
+        self.tensors = tensors if isinstance(tensors, dict) else {getattr(t, "name", str(t)): t for t in tensors}
+        self.n = every_n_iter or 1
+        self._i = 0
+        self.formatter = formatter
+
+    def before_run(self, ctx):
+        return SessionRunArgs(self.tensors) if self._i % self.n == 0 else None
+
+    def after_run(self, ctx, vals):
+        if vals.results:
+            msg = self.formatter(vals.results) if self.formatter else ", ".join(
+                f"{k} = {v}" for k, v in vals.results.items())
+            _log.info(msg)
+        self._i += 1
+
+
+class NanTensorHook(SessionRunHook):
+    def __init__(self, loss_tensor, fail_on_nan_loss=True):
+        self.loss, self.fail = loss_tensor, fail_on_nan_loss
+
+    def before_run(self, ctx):
+        return SessionRunArgs(self.loss)
+
+    def after_run(self, ctx, vals):
+        if vals.results is not None and not np.all(np.isfinite(vals.results)):
+            if self.fail:
+                raise NanLossDuringTrainingError("NaN loss during training.")
+            ctx.request_stop()
+
+
+class StepCounterHook(SessionRunHook):
+    def __init__(self, every_n_steps=100, every_n_secs=None, output_dir=None, summary_writer=None):
+        self.n = every_n_steps
+        self.writer = summary_writer or (FileWriter(output_dir) if output_dir else None)
+        self._i, self._t = 0, time.time()
+
+    def after_run(self, ctx, vals):
+        self._i += 1
+        if self._i % self.n == 0:
+            dt = time.time() - self._t
+            sps = self.n / max(dt, 1e-9)
+            if self.writer is not None:
+                self.writer.add_scalar("global_step/sec", sps, self._i)
+            _log.info(f"global_step/sec: {sps:.2f}")
+            self._t = time.time()
+
+
+class FinalOpsHook(SessionRunHook):
+    def __init__(self, final_ops, final_ops_feed_dict=None):
+        self.final_ops, self.feed = final_ops, final_ops_feed_dict
+        self.final_ops_values = None
+
+    def end(self, session):
+        self.final_ops_values = session.run(self.final_ops, feed_dict=self.feed)
+
+
+# ======================================================================= MonitoredSession
+class Scaffold:
+    def __init__(self, init_op=None, init_feed_dict=None, init_fn=None, ready_op=None, local_init_op=None,
+                 summary_op=None, saver=None):
+        self.init_op, self.init_feed_dict, self.init_fn = init_op, init_feed_dict, init_fn
+        self.local_init_op, self.summary_op, self.saver = local_init_op, summary_op, saver
+
+    def finalize(self):
+        return self
+
+
+class MonitoredSession:
+    def __init__(self, is_chief=True, checkpoint_dir=None, scaffold=None, hooks=None, master="", config=None):
+        self.scaffold = scaffold or Scaffold()
+        self.hooks = list(hooks or [])
+        self._sess = Session(master, config=config)
+        self.coord = Coordinator()
+        for h in self.hooks:
+            h.begin()
+        _init_or_restore(self._sess, is_chief, self.scaffold.init_op, self.scaffold.local_init_op,
+                         self.scaffold.init_fn, checkpoint_dir, self.scaffold.saver, self.scaffold.init_feed_dict)
+        self._qr_threads = start_queue_runners(self._sess, self.coord)
+        for h in self.hooks:
+            h.after_create_session(self._sess, self.coord)
+        self._stop = False
+        self._closed = False
+
+    @property
+    def graph(self):
+        return get_default_graph()
+
+    def run(self, fetches, feed_dict=None, options=None, run_metadata=None):
+        ctx = SessionRunContext(SessionRunArgs(fetches, feed_dict, options), self._sess)
+        extra = [h.before_run(ctx) for h in self.hooks]
+        merged_feed = dict(feed_dict or {})
+        for e in extra:
+            if e is not None and e.feed_dict:
+                merged_feed.update(e.feed_dict)
+        all_fetches = {"__main": fetches, "__hooks": [e.fetches if e is not None else None for e in extra]}
+        res = self._sess.run(all_fetches, feed_dict=merged_feed, options=options)
+        for h, e, r in zip(self.hooks, extra, res["__hooks"]):
+            h.after_run(ctx, SessionRunValues(r if e is not None else None))
+        if ctx.stop_requested:
+            self._stop = True
+        return res["__main"]
+
+    def run_step_fn(self, step_fn):
+        return step_fn(self)
+
+    def should_stop(self) -> bool:
+        return self._stop or self.coord.should_stop()
+
+    def request_stop(self):
+        self._stop = True
+
+    def close(self):
+        if self._closed:
+            return
+        self._closed = True
+        for h in self.hooks:
+            h.end(self._sess)
+        self.coord.request_stop()
+        self._sess.close()
+        srv = current_server()
+        if srv is not None:
+            srv.signal_done()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, et, ev, tb):
+        if ev is not None and not isinstance(ev, Exception):
+            pass
+        self.close()
+        return False
+
+
+SingularMonitoredSession = MonitoredSession
+
+
+def MonitoredTrainingSession(master="", is_chief=True, checkpoint_dir=None, scaffold=None, hooks=None,  # noqa: N802
+                             chief_only_hooks=None, save_checkpoint_secs=600, save_summaries_steps=100,
+                             save_summaries_secs=None, config=None, stop_grace_period_secs=120,
+                             log_step_count_steps=100, max_wait_secs=7200, save_checkpoint_steps=None,
+                             summary_dir=None):
+    """tf.train.MonitoredTrainingSession: chief restores-or-initialises and
+    broadcasts, runs checkpoint / summary / step-counter hooks."""
+    all_hooks = list(hooks or [])
+    if is_chief:
+        all_hooks += list(chief_only_hooks or [])
+        sdir = summary_dir or checkpoint_dir
+        if checkpoint_dir and (save_checkpoint_secs or save_checkpoint_steps):
+            all_hooks.append(CheckpointSaverHook(checkpoint_dir, save_secs=save_checkpoint_secs,
+                                                 save_steps=save_checkpoint_steps,
+                                                 saver=(scaffold.saver if scaffold else None)))
+        if sdir and save_summaries_steps:
+            all_hooks.append(SummarySaverHook(save_steps=save_summaries_steps, output_dir=sdir,
+                                              summary_op=(scaffold.summary_op if scaffold else None)))
+        if sdir and log_step_count_steps:
+            all_hooks.append(StepCounterHook(log_step_count_steps, output_dir=sdir))
+    return MonitoredSession(is_chief, checkpoint_dir, scaffold, all_hooks, master, config)
+
+
+# ======================================================================= lr schedules
+def exponential_decay(learning_rate, global_step, decay_steps, decay_rate, staircase=False, name=None):
+    def f(gs):
+        p = float(gs) / decay_steps
+        if staircase:
+            p = float(int(p))
+        return torch.tensor(learning_rate * decay_rate ** p)
+    return Tensor(f, [global_step], name or "ExponentialDecay")
+
+
+def piecewise_constant(x, boundaries, values, name=None):
+    def f(v):
+        v = float(v)
+        for b, val in zip(boundaries, values):
+            if v <= b:
+                return torch.tensor(float(val))
+        return torch.tensor(float(values[-1]))
+    return Tensor(f, [x], name or "PiecewiseConstant")

@@ -1,0 +1,291 @@
+"""Framework ops: autograd functions over the hand-written CDNA4 HIP kernels.
+
+GPU tensors always take the native path (csrc/kernels/*.hip); if the
+extension is missing on a GPU box the op raises -- there is no silent eager
+fallback.  CPU tensors use plain PyTorch (the CPU/gloo configuration and the
+numerics oracle in tests).
+
+Reference op map: linear_act = MatMul + Add + Sigmoid/Relu
+(example.py:95-97), softmax_xent (example.py:98-103), sigmoid_xent
+(lr2.py:391), embedding_bag (tf.nn.embedding_lookup_sparse, lr2.py:390),
+accuracy (example.py:125-128), AUC histograms (streaming_auc, lr2.py:400).
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import _native
+
+ACT = {"none": 0, None: 0, "linear": 0, "relu": 1, "sigmoid": 2, "tanh": 3, "gelu": 4}
+EMB_MODE = {"sum": 0, "mean": 1, "sqrtn": 2}
+
+
+def _C():
+    return _native.load()
+
+
+def _act_cpu(z, act):
+    a = ACT[act]
+    if a == 1:
+        return torch.relu(z)
+    if a == 2:
+        return torch.sigmoid(z)
+    if a == 3:
+        return torch.tanh(z)
+    if a == 4:
+        return torch.nn.functional.gelu(z)
+    return z
+
+
+# --------------------------------------------------------------------------- GEMM
+def matmul(a: torch.Tensor, b: torch.Tensor, trans_a: bool = False, trans_b: bool = False,
+           bias=None, act="none", out_dtype=None) -> torch.Tensor:
+    """act(op(a) @ op(b) + bias) on the bf16 MFMA GEMM (no autograd)."""
+    if not a.is_cuda:
+        A = a.t() if trans_a else a
+        Bm = b.t() if trans_b else b
+        z = A.float() @ Bm.float()
+        if bias is not None:
+            z = z + bias
+        return _act_cpu(z, act).to(out_dtype or torch.float32)
+    a = a if a.stride(-1) == 1 else a.contiguous()
+    b = b if b.stride(-1) == 1 else b.contiguous()
+    M = a.shape[1] if trans_a else a.shape[0]
+    N = b.shape[0] if trans_b else b.shape[1]
+    out = torch.empty((M, N), dtype=out_dtype or torch.float32, device=a.device)
+    _C().gemm(a, trans_a, b, trans_b, out, bias, ACT[act], 1.0, 0.0, None)
+    return out
+
+
+class _LinearAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, act):
+        C = _C()
+        x2 = x.reshape(-1, x.shape[-1])
+        x2 = x2 if x2.stride(-1) == 1 else x2.contiguous()
+        M, N = x2.shape[0], w.shape[1]
+        y = torch.empty((M, N), dtype=torch.float32, device=x.device)
+        z = torch.empty_like(y) if ACT[act] == 4 else None
+        C.gemm(x2, False, w.contiguous(), False, y, b.contiguous() if b is not None else None, ACT[act],
+               1.0, 0.0, z)
+        ctx.save_for_backward(x2, w, y if z is None else z)
+        ctx.act = ACT[act]
+        ctx.has_b = b is not None
+        ctx.xshape = x.shape
+        return y.reshape(*x.shape[:-1], N)
+
+    @staticmethod
+    def backward(ctx, gy):
+        C = _C()
+        x2, w, yz = ctx.saved_tensors
+        gy = gy.reshape(-1, w.shape[1]).contiguous().float()
+        if ctx.act != 0:
+            dz = torch.empty_like(gy)
+            if ctx.act == 4:
+                C.act_backward(gy, None, yz, dz, 4)
+            else:
+                C.act_backward(gy, yz, None, dz, ctx.act)
+        else:
+            dz = gy
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.empty((dz.shape[0], w.shape[0]), dtype=torch.float32, device=dz.device)
+            C.gemm(dz, False, w.contiguous(), True, gx, None, 0, 1.0, 0.0, None)   # dZ W^T
+            gx = gx.reshape(ctx.xshape)
+        if ctx.needs_input_grad[1]:
+            gw = torch.empty_like(w, dtype=torch.float32)
+            C.gemm(x2, True, dz, False, gw, None, 0, 1.0, 0.0, None)                # X^T dZ
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            gb = torch.empty(w.shape[1], dtype=torch.float32, device=dz.device)
+            C.col_sum(dz, gb)
+        return gx, gw, gb, None
+
+
+def linear_act(x: torch.Tensor, w: torch.Tensor, b=None, act="none") -> torch.Tensor:
+    """y = act(x @ w + b), w: [in, out] (TF layout), fused bias + activation epilogue."""
+    if not x.is_cuda:
+        z = x.float() @ w
+        if b is not None:
+            z = z + b
+        return _act_cpu(z, act)
+    return _LinearAct.apply(x, w, b, act)
+
+
+class Linear(torch.nn.Module):
+    """Dense layer with TF-layout weight [in, out] on the fused MFMA GEMM."""
+
+    def __init__(self, fan_in, fan_out, act="none", bias=True, init_std=None):
+        super().__init__()
+        std = init_std if init_std is not None else (1.0 / fan_in) ** 0.5
+        self.weight = torch.nn.Parameter(torch.randn(fan_in, fan_out) * std)
+        self.bias = torch.nn.Parameter(torch.zeros(fan_out)) if bias else None
+        self.act = act
+
+    def forward(self, x):
+        return linear_act(x, self.weight, self.bias, self.act)
+
+
+# --------------------------------------------------------------------------- losses
+class _SoftmaxXent(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, dense, naive):
+        C = _C()
+        lg = logits.contiguous().float()
+        Bn = lg.shape[0]
+        loss_rows = torch.empty(Bn, dtype=torch.float32, device=lg.device)
+        grad = torch.empty_like(lg)
+        if dense:
+            C.softmax_xent(lg, None, labels.contiguous().float(), loss_rows, grad, None, 1.0 / Bn, naive)
+        else:
+            C.softmax_xent(lg, labels.contiguous().long(), None, loss_rows, grad, None, 1.0 / Bn, naive)
+        ctx.save_for_backward(grad)
+        return loss_rows.mean()
+
+    @staticmethod
+    def backward(ctx, g):
+        (grad,) = ctx.saved_tensors
+        return grad * g, None, None, None
+
+
+def softmax_xent(logits, labels, naive: bool = False):
+    """mean softmax cross-entropy; labels: int class ids [B] or dense [B, C]."""
+    dense = labels.dim() == 2
+    if not logits.is_cuda:
+        logp = torch.log_softmax(logits.float(), 1)
+        if naive:
+            logp = torch.log(torch.softmax(logits.float(), 1))
+        if dense:
+            return (-(labels.float() * logp).sum(1)).mean()
+        return torch.nn.functional.nll_loss(logp, labels.long())
+    return _SoftmaxXent.apply(logits, labels, dense, naive)
+
+
+class _SigmoidXent(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, t, reduction):
+        C = _C()
+        xf = x.contiguous().float()
+        tf_ = t.contiguous().float().reshape(xf.shape)
+        loss = torch.empty_like(xf)
+        n = xf.numel()
+        grad = torch.empty_like(xf)
+        C.sigmoid_xent(xf, tf_, loss, grad, 1.0 / n if reduction == "mean" else 1.0)
+        ctx.save_for_backward(grad)
+        ctx.reduction = reduction
+        return loss.mean() if reduction == "mean" else (loss.sum() if reduction == "sum" else loss)
+
+    @staticmethod
+    def backward(ctx, g):
+        (grad,) = ctx.saved_tensors
+        return grad * g, None, None
+
+
+def sigmoid_xent(logits, targets, reduction: str = "mean"):
+    """tf.nn.sigmoid_cross_entropy_with_logits (+ reduction), fused fwd/bwd."""
+    if not logits.is_cuda:
+        loss = torch.nn.functional.binary_cross_entropy_with_logits(
+            logits.float(), targets.float().reshape(logits.shape), reduction=reduction)
+        return loss
+    if reduction not in ("mean", "sum"):
+        x = logits.float()
+        t = targets.float().reshape(x.shape)
+        return torch.clamp(x, min=0) - x * t + torch.log1p(torch.exp(-x.abs()))
+    return _SigmoidXent.apply(logits, targets, reduction)
+
+
+# --------------------------------------------------------------------------- embeddings
+class _EmbeddingBag(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, weight, ids, offsets, psw, mode):
+        C = _C()
+        B = offsets.numel() - 1
+        D = 1 if weight.dim() == 1 else weight.shape[1]
+        out = torch.empty((B, D), dtype=torch.float32, device=weight.device)
+        C.embedding_bag_fwd(weight.contiguous(), ids, offsets, psw, EMB_MODE[mode], out, None)
+        ctx.save_for_backward(ids, offsets, psw if psw is not None else torch.empty(0))
+        ctx.has_psw = psw is not None
+        ctx.mode = mode
+        ctx.wshape = weight.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        C = _C()
+        ids, offsets, psw = ctx.saved_tensors
+        gw = torch.zeros(ctx.wshape, dtype=torch.float32, device=gout.device)
+        C.embedding_bag_bwd(gw, ids, offsets, psw if ctx.has_psw else None, gout.contiguous().float(),
+                            EMB_MODE[ctx.mode], 0.0)
+        return gw, None, None, None, None
+
+
+def embedding_bag(weight, ids, offsets, per_sample_weights=None, mode: str = "sum"):
+    """Bag-combine rows of `weight` [V, D] for CSR bags (offsets [B+1]).
+
+    == tf.nn.embedding_lookup_sparse(W, sp_ids, sp_weights, combiner=mode).
+    """
+    ids = ids.long()
+    offsets = offsets.long()
+    if not weight.is_cuda:
+        W = weight if weight.dim() == 2 else weight.reshape(-1, 1)
+        out = torch.nn.functional.embedding_bag(ids, W, offsets[:-1], mode="sum",
+                                                per_sample_weights=per_sample_weights,
+                                                include_last_offset=False)
+        if mode != "sum":
+            w = per_sample_weights if per_sample_weights is not None else torch.ones_like(ids, dtype=W.dtype)
+            seg = torch.repeat_interleave(torch.arange(offsets.numel() - 1), offsets[1:] - offsets[:-1])
+            den = torch.zeros(offsets.numel() - 1, dtype=W.dtype).index_add_(0, seg, w if mode == "mean" else w * w)
+            den = den if mode == "mean" else den.sqrt()
+            out = out / den.clamp_min(1e-30).unsqueeze(1)
+        return out
+    psw = per_sample_weights.contiguous().float() if per_sample_weights is not None else None
+    return _EmbeddingBag.apply(weight, ids.contiguous(), offsets.contiguous(), psw, mode)
+
+
+def embedding_bag_sgd_(weight, ids, offsets, per_sample_weights, grad_out, lr: float, mode: str = "sum"):
+    """Fused sparse SGD: weight[ids] -= lr * w * grad_out[bag]  (ScatterSub apply)."""
+    if not weight.is_cuda:
+        seg = torch.repeat_interleave(torch.arange(offsets.numel() - 1), offsets[1:] - offsets[:-1])
+        w = per_sample_weights if per_sample_weights is not None else torch.ones(ids.numel())
+        W = weight if weight.dim() == 2 else weight.view(-1, 1)
+        W.index_add_(0, ids.long(), -lr * w.unsqueeze(1) * grad_out[seg])
+        return weight
+    _C().embedding_bag_bwd(weight, ids.long().contiguous(), offsets.long().contiguous(),
+                           per_sample_weights.contiguous().float() if per_sample_weights is not None else None,
+                           grad_out.contiguous().float(), EMB_MODE[mode], float(lr))
+    return weight
+
+
+# --------------------------------------------------------------------------- metrics
+def argmax_correct(logits, labels) -> torch.Tensor:
+    """number of rows whose argmax equals the label (int64 tensor, on device)."""
+    if not logits.is_cuda:
+        return (logits.argmax(1) == labels.long()).sum()
+    cnt = torch.zeros(1, dtype=torch.int64, device=logits.device)
+    _C().argmax_correct(logits.contiguous().float(), labels.long().contiguous(), cnt)
+    return cnt[0]
+
+
+def auc_histogram_(pred, labels, pos_counts, neg_counts):
+    """Accumulate positive/negative histograms of predictions over len(pos) bins."""
+    nb = pos_counts.numel()
+    if not pred.is_cuda:
+        p = pred.float().clamp(0, 1).reshape(-1)
+        b = (p * (nb - 1)).long().clamp(0, nb - 1)
+        lab = labels.reshape(-1).float() > 0.5
+        pos_counts += torch.bincount(b[lab], minlength=nb)
+        neg_counts += torch.bincount(b[~lab], minlength=nb)
+        return
+    _C().auc_hist(pred.contiguous().float().reshape(-1), labels.contiguous().float().reshape(-1),
+                  pos_counts, neg_counts)
+
+
+def auc_from_histograms(pos, neg) -> float:
+    """Trapezoidal ROC AUC from per-bin counts (thresholds at bin edges)."""
+    pos = pos.double().cpu().flip(0).cumsum(0)
+    neg = neg.double().cpu().flip(0).cumsum(0)
+    P, N = float(pos[-1]), float(neg[-1])
+    if P == 0 or N == 0:
+        return float("nan")
+    tpr = torch.cat([torch.zeros(1, dtype=torch.float64), pos / P])
+    fpr = torch.cat([torch.zeros(1, dtype=torch.float64), neg / N])
+    return float(torch.trapz(tpr, fpr))

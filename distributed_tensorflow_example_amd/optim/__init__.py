@@ -1,0 +1,202 @@
+"""Fused multi-tensor optimizers (csrc/kernels/ops.hip: multi_tensor_apply).
+
+One launch updates every parameter of a group: the
+reference's per-variable ApplyGradientDescent / ApplyAdam ops become a single
+kernel over a (tensor, 4096-element chunk) work list.  Learning rate and step
+live on the device so a whole training step (including the update) can be
+captured in a hipGraph and the schedule changed without re-capture.
+
+Semantics follow TensorFlow where the reference uses it:
+  GradientDescent  p -= lr * g                         (example.py:108)
+  Momentum         m = mu*m + g; p -= lr*m (or Nesterov)
+  Adam (TF)        lr_t = lr*sqrt(1-b2^t)/(1-b1^t); p -= lr_t*m/(sqrt(v)+eps)
+                   (epsilon outside the sqrt, "epsilon hat"; model_export.py:38)
+  AdamW            decoupled weight decay (BERT recipe)
+`grad_scale` folds the 1/N of a summed all-reduce into the update.
+CPU tensors use the same math in PyTorch (CPU/gloo configuration).
+"""
+from __future__ import annotations
+
+from typing import Iterable, List, Optional
+
+import torch
+
+from .. import _native
+
+KINDS = {"sgd": 0, "momentum": 1, "adam": 2, "adamw": 3}
+
+
+class _FusedBase:
+    kind = "sgd"
+
+    def __init__(self, params: Iterable[torch.nn.Parameter], lr: float, weight_decay: float = 0.0,
+                 beta1: float = 0.9, beta2: float = 0.999, eps: float = 1e-8, momentum: float = 0.0,
+                 nesterov: bool = False):
+        self.params: List[torch.Tensor] = [p for p in params]
+        if not self.params:
+            raise ValueError("optimizer got an empty parameter list")
+        self.device = self.params[0].device
+        self.wd, self.b1, self.b2, self.eps = weight_decay, beta1, beta2, eps
+        self.momentum, self.nesterov = momentum, nesterov
+        self.lr_t = torch.tensor([float(lr)], dtype=torch.float32, device=self.device)
+        self.step_t = torch.zeros(1, dtype=torch.int64, device=self.device)
+        need_m = self.kind in ("momentum", "adam", "adamw")
+        need_v = self.kind in ("adam", "adamw")
+        self.m = [torch.zeros_like(p, dtype=torch.float32) if need_m else None for p in self.params]
+        self.v = [torch.zeros_like(p, dtype=torch.float32) if need_v else None for p in self.params]
+        self._tab_key = None
+        self._tab = None
+        self._chunks = None
+
+    # ------------------------------------------------------------------ state
+    @property
+    def lr(self) -> float:
+        return float(self.lr_t.item())
+
+    def set_lr(self, lr: float):
+        self.lr_t.fill_(float(lr))
+
+    def state_dict(self):
+        return {"lr": self.lr, "step": int(self.step_t.item()),
+                "m": [t.detach().cpu() if t is not None else None for t in self.m],
+                "v": [t.detach().cpu() if t is not None else None for t in self.v]}
+
+    def load_state_dict(self, sd):
+        self.set_lr(sd["lr"])
+        self.step_t.fill_(int(sd["step"]))
+        for dst, src in zip(self.m, sd["m"]):
+            if dst is not None and src is not None:
+                dst.copy_(src)
+        for dst, src in zip(self.v, sd["v"]):
+            if dst is not None and src is not None:
+                dst.copy_(src)
+
+    def zero_grad(self, set_to_none: bool = False):
+        for p in self.params:
+            if p.grad is not None:
+                if set_to_none:
+                    p.grad = None
+                else:
+                    p.grad.zero_()
+
+    # ------------------------------------------------------------------ native table
+    def _table(self, grads):
+        key = tuple((p.data_ptr(), g.data_ptr(), g.dtype) for p, g in zip(self.params, grads))
+        if key != self._tab_key:
+            C = _native.load()
+            chunk = C.mt_chunk()
+            rows, chunks = [], []
+            for i, (p, g) in enumerate(zip(self.params, grads)):
+                if not (p.is_contiguous() and g.is_contiguous()) or p.dtype != torch.float32:
+                    raise ValueError("fused optimizer needs contiguous fp32 params and contiguous grads")
+                m, v = self.m[i], self.v[i]
+                rows.append([p.data_ptr(), g.data_ptr(), m.data_ptr() if m is not None else 0,
+                             v.data_ptr() if v is not None else 0, p.numel()])
+                for s in range(0, p.numel(), chunk):
+                    chunks.append([i, s])
+            self._tab = torch.tensor(rows, dtype=torch.int64).to(self.device)
+            self._chunks = torch.tensor(chunks, dtype=torch.int32).reshape(-1, 2).to(self.device)
+            self._tab_key = key
+        return self._tab, self._chunks
+
+    def _grads(self, grads):
+        if grads is None:
+            grads = [p.grad for p in self.params]
+        out = []
+        for p, g in zip(self.params, grads):
+            out.append(torch.zeros_like(p) if g is None else g)
+        return out
+
+    @torch.no_grad()
+    def step(self, grads: Optional[List[torch.Tensor]] = None, grad_scale: float = 1.0):
+        grads = self._grads(grads)
+        self.step_t += 1
+        if self.device.type != "cuda":
+            return self._step_cpu(grads, grad_scale)
+        gdt = {g.dtype for g in grads}
+        if len(gdt) != 1 or next(iter(gdt)) not in (torch.float32, torch.bfloat16):
+            grads = [g.float() for g in grads]
+        gbf = grads[0].dtype == torch.bfloat16
+        tab, chunks = self._table(grads)
+        _native.load().multi_tensor_apply(tab, chunks, KINDS[self.kind], gbf, self.lr_t, 0.0,
+                                          float(grad_scale), self.wd, self.b1, self.b2, self.eps,
+                                          self.momentum, self.nesterov, self.step_t)
+
+    def _step_cpu(self, grads, gs):
+        lr = float(self.lr_t.item())
+        t = int(self.step_t.item())
+        for i, (p, g) in enumerate(zip(self.params, grads)):
+            g = g.float() * gs
+            if self.kind == "sgd":
+                if self.wd:
+                    g = g + self.wd * p
+                p.sub_(lr * g)
+            elif self.kind == "momentum":
+                if self.wd:
+                    g = g + self.wd * p
+                m = self.m[i]
+                m.mul_(self.momentum).add_(g)
+                p.sub_(lr * (g + self.momentum * m if self.nesterov else m))
+            else:
+                if self.kind == "adam" and self.wd:
+                    g = g + self.wd * p
+                m, v = self.m[i], self.v[i]
+                m.mul_(self.b1).add_((1 - self.b1) * g)
+                v.mul_(self.b2).add_((1 - self.b2) * g * g)
+                lr_t = lr * (1 - self.b2 ** t) ** 0.5 / (1 - self.b1 ** t)
+                p0 = p.clone() if self.kind == "adamw" else None
+                p.sub_(lr_t * m / (v.sqrt() + self.eps))
+                if self.kind == "adamw" and self.wd:
+                    p.sub_(lr * self.wd * p0)
+
+
+class FusedSGD(_FusedBase):
+    kind = "sgd"
+
+    def __init__(self, params, lr, weight_decay=0.0):
+        super().__init__(params, lr, weight_decay=weight_decay)
+
+
+class FusedMomentum(_FusedBase):
+    kind = "momentum"
+
+    def __init__(self, params, lr, momentum=0.9, nesterov=False, weight_decay=0.0):
+        super().__init__(params, lr, weight_decay=weight_decay, momentum=momentum, nesterov=nesterov)
+
+
+class FusedAdam(_FusedBase):
+    """TF AdamOptimizer semantics (defaults lr=0.001, b1=0.9, b2=0.999, eps=1e-8)."""
+
+    kind = "adam"
+
+    def __init__(self, params, lr=0.001, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0):
+        super().__init__(params, lr, weight_decay=weight_decay, beta1=beta1, beta2=beta2, eps=eps)
+
+
+class FusedAdamW(_FusedBase):
+    kind = "adamw"
+
+    def __init__(self, params, lr=1e-4, beta1=0.9, beta2=0.999, eps=1e-6, weight_decay=0.01):
+        super().__init__(params, lr, weight_decay=weight_decay, beta1=beta1, beta2=beta2, eps=eps)
+
+
+def global_grad_norm(grads: List[torch.Tensor]) -> torch.Tensor:
+    """sqrt(sum g^2) over tensors, one fused launch on GPU."""
+    if not grads:
+        return torch.zeros(())
+    if not grads[0].is_cuda:
+        return torch.sqrt(sum((g.float() ** 2).sum() for g in grads))
+    C = _native.load()
+    chunk = C.mt_chunk()
+    rows, chunks = [], []
+    for i, g in enumerate(grads):
+        g = g.contiguous()
+        rows.append([g.data_ptr(), g.data_ptr(), 0, 0, g.numel()])
+        for s in range(0, g.numel(), chunk):
+            chunks.append([i, s])
+    dev = grads[0].device
+    tab = torch.tensor(rows, dtype=torch.int64).to(dev)
+    ch = torch.tensor(chunks, dtype=torch.int32).reshape(-1, 2).to(dev)
+    out = torch.zeros(1, dtype=torch.float32, device=dev)
+    C.multi_tensor_sumsq(tab, ch, grads[0].dtype == torch.bfloat16, out)
+    return out.sqrt()[0]

@@ -124,10 +124,8 @@ class World:
         if src.is_cuda and self.comm is not None:
             self.comm.all_to_all(src, send_counts, dst, recv_counts)
         else:
-            inner = src[0].numel() if src.dim() > 1 else 1
             dist.all_to_all_single(dst, src, output_split_sizes=recv_counts,
                                    input_split_sizes=send_counts)
-            del inner
         return dst
 
     def shutdown(self):
@@ -193,6 +191,48 @@ def init(rank: Optional[int] = None, world_size: Optional[int] = None,
             C = _native.load()
             uid = C.rccl_unique_id() if rank == 0 else None
             uid = w.broadcast_object(uid, 0)
+            w.comm = C.RcclComm(uid, world_size, rank)
+    _WORLD = w
+    return w
+
+
+def init_from_rendezvous(rdv, backend: str = "auto", timeout_s: float = 600.0) -> World:
+    """Data-parallel world of the *workers* of a ClusterSpec (ps tasks excluded).
+
+    gloo bootstraps through the native store (NativeStore); the RCCL unique id
+    is exchanged through it as well.
+    """
+    global _WORLD
+    if _WORLD is not None:
+        return _WORLD
+    if not rdv.is_worker:
+        raise RuntimeError("only worker tasks join the data-parallel world")
+    from .cluster import NativeStore
+
+    rank, world_size = rdv.task_index, rdv.num_workers
+    has_gpu = torch.cuda.is_available()
+    if backend == "auto":
+        backend = "rccl" if has_gpu else "gloo"
+    if backend == "rccl":
+        ndev = torch.cuda.device_count()
+        torch.cuda.set_device(rank % max(ndev, 1))
+        device = torch.device("cuda", torch.cuda.current_device())
+    else:
+        device = torch.device("cpu")
+    w = World(rank=rank, world_size=world_size, local_rank=rank, device=device,
+              backend=backend if world_size > 1 else ("rccl" if device.type == "cuda" else "none"))
+    if world_size > 1:
+        store = dist.PrefixStore("dp", NativeStore(rdv.store))
+        dist.init_process_group("gloo", store=store, rank=rank, world_size=world_size,
+                                timeout=datetime.timedelta(seconds=timeout_s))
+        w.pg_initialized = True
+        if backend == "rccl":
+            from .. import _native
+
+            C = _native.load()
+            if rank == 0:
+                rdv.store.set("rccl_uid", C.rccl_unique_id())
+            uid = rdv.store.get("rccl_uid", timeout_s)
             w.comm = C.RcclComm(uid, world_size, rank)
     _WORLD = w
     return w

@@ -189,6 +189,9 @@ class RunContext:
                 self.memo[k] = x._eval(self)
             return self.memo[k]
         if isinstance(x, (list, tuple)):
+            if x and not any(isinstance(v, (Tensor, list, tuple, str, bytes, torch.Tensor, np.ndarray))
+                             for v in x):
+                return _to_tensor(list(x), self.device)     # python numbers -> constant tensor
             return type(x)(self.eval(v) for v in x)
         return _to_tensor(x, self.device)
 

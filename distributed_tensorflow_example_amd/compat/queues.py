@@ -100,9 +100,13 @@ class FIFOQueue:
                 self.put(tuple(c[i] for c in cols))
         return Operation(f, list(vals), name or "enqueue_many")
 
-    def dequeue(self, name=None) -> Tensor:
-        def f():
-            raise RuntimeError("unreachable")
+    def _components(self, t: Tensor, name: str):
+        # TF returns one tensor per component; they share the (memoised) dequeue
+        if len(self.dtypes) <= 1:
+            return t
+        return [Tensor(lambda v, i=i: v[i], [t], f"{name}_{i}") for i in range(len(self.dtypes))]
+
+    def dequeue(self, name=None):
         t = Tensor(None, [], name or "dequeue")
         q = self
 
@@ -110,9 +114,9 @@ class FIFOQueue:
             item = q.get(_timeout(ctx))
             return item[0] if len(item) == 1 else list(item)
         t._eval = ev
-        return t
+        return self._components(t, name or "dequeue")
 
-    def dequeue_many(self, n, name=None) -> Tensor:
+    def dequeue_many(self, n, name=None):
         t = Tensor(None, [], name or "dequeue_many")
         q = self
 
@@ -120,16 +124,16 @@ class FIFOQueue:
             items = q.get_many(n, _timeout(ctx))
             return _stack_items(items)
         t._eval = ev
-        return t
+        return self._components(t, name or "dequeue_many")
 
-    def dequeue_up_to(self, n, name=None) -> Tensor:
+    def dequeue_up_to(self, n, name=None):
         t = Tensor(None, [], name or "dequeue_up_to")
         q = self
 
         def ev(ctx):
             return _stack_items(q.get_many(n, _timeout(ctx), True))
         t._eval = ev
-        return t
+        return self._components(t, name or "dequeue_up_to")
 
     def close(self, cancel_pending_enqueues: bool = False, name=None) -> Operation:
         return Operation(lambda: self._q.close(cancel_pending_enqueues), [], name or "close")
@@ -314,9 +318,7 @@ def batch(tensors, batch_size, num_threads=1, capacity=32, enqueue_many=False, s
     enq = q.enqueue_many(tlist) if enqueue_many else q.enqueue(tlist)
     add_queue_runner(QueueRunner(q, [enq] * num_threads))
     out = q.dequeue_up_to(batch_size) if allow_smaller_final_batch else q.dequeue_many(batch_size)
-    if single:
-        return out
-    return [Tensor(lambda v, i=i: v[i], [out], f"{name}_{i}") for i in range(len(tlist))]
+    return out if single else list(out) if len(tlist) > 1 else [out]
 
 
 def shuffle_batch(tensors, batch_size, capacity, min_after_dequeue, num_threads=1, seed=None,
@@ -328,7 +330,7 @@ def shuffle_batch(tensors, batch_size, capacity, min_after_dequeue, num_threads=
     out = q.dequeue_many(batch_size)
     if not isinstance(tensors, (list, tuple)):
         return out
-    return [Tensor(lambda v, i=i: v[i], [out], f"{name}_{i}") for i in range(len(tlist))]
+    return list(out) if len(tlist) > 1 else [out]
 
 
 def slice_input_producer(tensor_list, num_epochs=None, shuffle=True, seed=None, capacity=32,
@@ -351,9 +353,7 @@ def slice_input_producer(tensor_list, num_epochs=None, shuffle=True, seed=None, 
             q.put(tuple(c[i] for c in cols))
     add_queue_runner(QueueRunner(q, [Operation(feed, tl, name + "/enqueue")]))
     deq = q.dequeue()
-    if len(tl) == 1:
-        return [deq]
-    return [Tensor(lambda v, i=i: v[i], [deq], f"{name}_{i}") for i in range(len(tl))]
+    return [deq] if len(tl) == 1 else list(deq)
 
 
 def string_input_producer(string_tensor, num_epochs=None, shuffle=True, seed=None, capacity=32,
@@ -362,7 +362,7 @@ def string_input_producer(string_tensor, num_epochs=None, shuffle=True, seed=Non
 
 
 def read_file(filename, name="ReadFile") -> Tensor:
-    from .gfile import GFile
+    from ..utils.gfile import GFile
 
     def f(fn):
         fn = fn.decode() if isinstance(fn, bytes) else str(fn)

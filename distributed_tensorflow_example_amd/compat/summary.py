@@ -120,6 +120,10 @@ class Event:
                     self.summary.append((tag, sv, kind))
 
 
+    def scalars(self):
+        return [(t, v) for t, v, k in self.summary if k == "scalar"]
+
+
 def summary_iterator(path: str) -> Iterator[Event]:
     for rec in _native.load().read_records(path, True):
         yield Event(rec)

@@ -99,17 +99,43 @@ class Server:
 
         def on_dead(dead):
             _log.warning(f"[{self.job_name}:{self.task_index}] no heartbeat from worker(s) {dead}")
-        ok = self.rdv.wait_all_workers_done(timeout=timeout, on_dead=on_dead)
+        try:
+            ok = self.rdv.wait_all_workers_done(timeout=timeout, on_dead=on_dead)
+        except Exception:      # store gone: the chief has already exited
+            ok = True
         _log.info(f"[{self.job_name}:{self.task_index}] join finished ({'all done' if ok else 'timeout'})")
+        self._leave()
         return ok
 
-    def signal_done(self):
-        if not self._done and self.rdv.is_worker:
-            self._done = True
+    def _leave(self):
+        try:
+            self.rdv.store.set(f"left/{self.job_name}/{self.task_index}", b"1")
+        except Exception:
+            pass
+
+    def signal_done(self, linger_s: float = 60.0):
+        """Worker finished: done token for the ps.  The chief hosts the store,
+        so it lingers until every other task has left (bounded by linger_s)."""
+        if self._done or not self.rdv.is_worker:
+            return
+        self._done = True
+        try:
+            self.rdv.signal_done()
+        except Exception:
+            return
+        if not self.is_chief:
+            self._leave()
+            return
+        others = [f"left/{j}/{i}" for j in self.cluster.jobs for i in range(self.cluster.num_tasks(j))
+                  if not (j == self.job_name and i == self.task_index)]
+        t0 = time.time()
+        while time.time() - t0 < linger_s:
             try:
-                self.rdv.signal_done()
+                if not others or self.rdv.store.check(others):
+                    break
             except Exception:
-                pass
+                break
+            time.sleep(0.1)
 
     def _atexit(self):
         self.signal_done()
@@ -692,12 +718,9 @@ class StopAtStepHook(SessionRunHook):
         if self.last_step is None:
             self.last_step = cur + self.num_steps
 
-    def before_run(self, ctx):
-        gs = get_global_step()
-        return SessionRunArgs(gs) if gs is not None else None
-
     def after_run(self, ctx, vals):
-        if vals.results is not None and int(np.asarray(vals.results)) + 1 >= self.last_step:
+        gs = get_global_step()
+        if gs is not None and int(np.asarray(ctx.session.run(gs))) >= self.last_step:
             ctx.request_stop()
 
 

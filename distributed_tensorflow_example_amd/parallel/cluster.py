@@ -113,9 +113,42 @@ def split_address(addr: str):
 class NativeStore(dist.Store):
     """torch.distributed Store backed by the native TCP store (gloo bootstraps through it)."""
 
-    def __init__(self, native):
+    def __init__(self, native, host: Optional[str] = None, port: Optional[int] = None, timeout_s: float = 300.0,
+                 prefix: str = ""):
+        # (torch's PrefixStore cannot wrap a Python store -- its clone() does
+        # not dispatch back to Python -- so key prefixing is done here)
         super().__init__()
         self.s = native
+        self._addr = (host, port, timeout_s)
+        self.prefix = prefix
+
+    def _k(self, key):
+        return self.prefix + key
+
+    def clone(self):
+        # gloo opens extra store connections (one per async work thread)
+        host, port, t = self._addr
+        if host is None:
+            return self
+        return NativeStore(_native.load().TCPStore(host, port, False, t), host, port, t, self.prefix)
+
+    def multi_get(self, keys):
+        return [self.get(k) for k in keys]
+
+    def multi_set(self, keys, values):
+        for k, v in zip(keys, values):
+            self.set(k, v)
+
+    def append(self, key, value):
+        while True:
+            k = self._k(key)
+            cur = self.s.get(k, 0.0) if self.s.check([k]) else b""
+            new = cur + self._b(value)
+            if self.s.compare_set(k, cur, new) == new:
+                return
+
+    def has_extended_api(self):
+        return True
 
     @staticmethod
     def _b(v):
@@ -124,31 +157,31 @@ class NativeStore(dist.Store):
         return bytes(v)
 
     def set(self, key, value):
-        self.s.set(key, self._b(value))
+        self.s.set(self._k(key), self._b(value))
 
     def get(self, key):
-        return self.s.get(key)
+        return self.s.get(self._k(key))
 
     def add(self, key, value):
-        return self.s.add(key, int(value))
+        return self.s.add(self._k(key), int(value))
 
     def wait(self, keys, timeout=None):
         t = -1.0
         if isinstance(timeout, datetime.timedelta):
             t = timeout.total_seconds()
-        self.s.wait(list(keys), t)
+        self.s.wait([self._k(k) for k in keys], t)
 
     def check(self, keys):
-        return self.s.check(list(keys))
+        return self.s.check([self._k(k) for k in keys])
 
     def delete_key(self, key):
-        return self.s.delete_key(key)
+        return self.s.delete_key(self._k(key))
 
     def num_keys(self):
         return self.s.num_keys()
 
     def compare_set(self, key, expected, desired):
-        return self.s.compare_set(key, self._b(expected), self._b(desired))
+        return self.s.compare_set(self._k(key), self._b(expected), self._b(desired))
 
 
 class Rendezvous:

@@ -80,9 +80,9 @@ class DistributedDataParallel(torch.nn.Module):
         self.buckets = [_Bucket(b, torch.float32, self.device) for b in buckets]
         self._param_bucket = {}
         for bi, b in enumerate(self.buckets):
-            for p, v in zip(b.params, b.views):
+            for idx, (p, v) in enumerate(zip(b.params, b.views)):
                 p.grad = v  # gradient-as-bucket-view
-                self._param_bucket[p] = bi
+                self._param_bucket[p] = (bi, idx)
         self._hooks = []
         if overlap:
             for p in params:
@@ -103,16 +103,13 @@ class DistributedDataParallel(torch.nn.Module):
 
     # ------------------------------------------------------------------ hooks
     def _on_grad(self, p):
-        if p.grad is not None and p.grad.data_ptr() != self.buckets[self._param_bucket[p]].views[
-                self.buckets[self._param_bucket[p]].params.index(p)].data_ptr():
-            # autograd replaced .grad (e.g. set_to_none): copy into the bucket view
-            bi = self._param_bucket[p]
-            b = self.buckets[bi]
-            idx = b.params.index(p)
-            b.views[idx].copy_(p.grad)
-            p.grad = b.views[idx]
-        bi = self._param_bucket[p]
+        bi, idx = self._param_bucket[p]
         b = self.buckets[bi]
+        view = b.views[idx]
+        if p.grad is not None and p.grad.data_ptr() != view.data_ptr():
+            # autograd replaced .grad (e.g. after set_to_none): fold it into the bucket view
+            view.copy_(p.grad)
+            p.grad = view
         b.ready += 1
         if b.ready == len(b.params) and bi not in self._launched:
             self._launch(bi)

@@ -222,7 +222,10 @@ def init_from_rendezvous(rdv, backend: str = "auto", timeout_s: float = 600.0) -
     w = World(rank=rank, world_size=world_size, local_rank=rank, device=device,
               backend=backend if world_size > 1 else ("rccl" if device.type == "cuda" else "none"))
     if world_size > 1:
-        store = dist.PrefixStore("dp", NativeStore(rdv.store))
+        from .cluster import split_address
+
+        host, port = split_address(rdv.cluster.chief_address())
+        store = NativeStore(rdv.store, host, port, timeout_s, prefix="dp/")
         dist.init_process_group("gloo", store=store, rank=rank, world_size=world_size,
                                 timeout=datetime.timedelta(seconds=timeout_s))
         w.pg_initialized = True

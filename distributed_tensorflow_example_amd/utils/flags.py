@@ -43,8 +43,7 @@ class _FlagValues:
         for name, d in self._defs.items():
             k = d["kind"]
             if k == "bool":
-                p.add_argument(f"--{name}", nargs="?", const=True, default=d["default"], type=_str2bool,
-                               help=d["help"])
+                p.add_argument(f"--{name}", default=d["default"], type=_str2bool, help=d["help"])
                 p.add_argument(f"--no{name}", dest=name, action="store_false")
             elif k == "list":
                 p.add_argument(f"--{name}", default=d["default"],
@@ -59,6 +58,9 @@ class _FlagValues:
     def __call__(self, argv: Optional[List[str]] = None, known_only: bool = True) -> List[str]:
         argv = list(sys.argv if argv is None else argv)
         prog, args = argv[:1], argv[1:]
+        # gflags booleans: bare `--flag` means true and never consumes the next word
+        bools = {n for n, d in self._defs.items() if d["kind"] == "bool"}
+        args = [f"{a}=true" if a.startswith("--") and a[2:] in bools else a for a in args]
         ns, rest = self._parser().parse_known_args(args)
         for k, v in vars(ns).items():
             self._values[k] = v

@@ -1,0 +1,210 @@
+"""MNIST 784-100-10 sigmoid MLP, ps/worker cluster, written against the TF-1.x
+compat front end -- the counterpart of the reference's headline script
+(example.py:1-192).
+
+    python examples/mnist_example.py --job_name=ps     --task_index=0
+    python examples/mnist_example.py --job_name=worker --task_index=0
+    python examples/mnist_example.py --job_name=worker --task_index=1
+
+Cluster: `--ps_hosts/--worker_hosts` (comma lists) or `--cluster_conf` JSON
+(cluster_conf.json shape); defaults mirror example.py:23-30 on localhost.
+
+What differs from the reference (README "semantics"):
+* workers train *synchronously*: every train_op run averages the gradients of
+  all workers (RCCL all-reduce on MI355X, gloo on CPU) -- the
+  SyncReplicasOptimizer path the reference left commented out
+  (example.py:109-123) is the only path; global_step counts sync steps;
+* chief initialises and broadcasts (no re-init race); ps tasks exit from
+  `server.join()` once every worker has finished;
+* input is the synthetic MNIST-shaped set (no network): same shapes/dtypes;
+* `--fused` runs the whole step (fwd+bwd+all-reduce+SGD) as the MFMA
+  kernel chain of models.mlp.FusedMLPTrainer instead of the op-by-op graph.
+"""
+from __future__ import annotations
+
+import json
+import os
+import shutil
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+
+import distributed_tensorflow_example_amd.compat as tf  # noqa: E402
+from distributed_tensorflow_example_amd.data import mnist as mnist_data  # noqa: E402
+from distributed_tensorflow_example_amd.utils.logging import step_line  # noqa: E402
+
+flags = tf.app.flags
+flags.DEFINE_string("job_name", "", "Either 'ps' or 'worker'")
+flags.DEFINE_integer("task_index", 0, "Index of task within the job")
+flags.DEFINE_string("ps_hosts", "localhost:2222", "comma-separated ps host:port list")
+flags.DEFINE_string("worker_hosts", "localhost:2223,localhost:2224", "comma-separated worker host:port list")
+flags.DEFINE_string("cluster_conf", "", "JSON file {\"ps\": [...], \"worker\": [...]} (overrides *_hosts)")
+flags.DEFINE_integer("batch_size", 100, "per-worker batch")
+flags.DEFINE_float("learning_rate", 0.0005, "SGD learning rate")
+flags.DEFINE_integer("training_epochs", 5, "epochs over the training split")
+flags.DEFINE_integer("max_steps", 0, "stop after this many steps (0 = full epochs)")
+flags.DEFINE_integer("train_size", 55000, "synthetic training examples")
+flags.DEFINE_integer("frequency", 100, "print every N batches")
+flags.DEFINE_string("logs_path", "./logs/mnist", "summary root; task dir {job}_{task} appended")
+flags.DEFINE_string("activation", "sigmoid", "sigmoid | relu")
+flags.DEFINE_boolean("fused", False, "run the fused MFMA train step (GPU only)")
+flags.DEFINE_string("result_json", "", "write final metrics + params checksum here (tests)")
+FLAGS = flags.FLAGS
+
+
+def cluster_spec():
+    if FLAGS.cluster_conf:
+        with open(FLAGS.cluster_conf) as f:
+            return tf.train.ClusterSpec(json.load(f))
+    return tf.train.ClusterSpec({"ps": [h for h in FLAGS.ps_hosts.split(",") if h],
+                                 "worker": [h for h in FLAGS.worker_hosts.split(",") if h]})
+
+
+def build_graph(cluster, task_index):
+    """Graph of example.py:64-135 (placement, model, loss, SGD, accuracy, summaries)."""
+    tf.set_random_seed(1)
+    with tf.device(tf.train.replica_device_setter(worker_device=f"/job:worker/task:{task_index}",
+                                                  cluster=cluster)):
+        global_step = tf.get_variable("global_step", [], initializer=tf.constant_initializer(0),
+                                      trainable=False)
+        with tf.name_scope("input"):
+            x = tf.placeholder(tf.float32, shape=[None, 784], name="x-input")
+            y_ = tf.placeholder(tf.float32, shape=[None, 10], name="y-input")
+        with tf.name_scope("weights"):
+            W1 = tf.Variable(tf.random_normal([784, 100]))
+            W2 = tf.Variable(tf.random_normal([100, 10]))
+        with tf.name_scope("biases"):
+            b1 = tf.Variable(tf.zeros([100]))
+            b2 = tf.Variable(tf.zeros([10]))
+        with tf.name_scope("softmax"):
+            act = tf.nn.sigmoid if FLAGS.activation == "sigmoid" else tf.nn.relu
+            a2 = act(tf.add(tf.matmul(x, W1), b1))
+            y = tf.nn.softmax(tf.add(tf.matmul(a2, W2), b2))
+        with tf.name_scope("cross_entropy"):
+            cross_entropy = tf.reduce_mean(-tf.reduce_sum(y_ * tf.log(y), reduction_indices=[1]))
+        with tf.name_scope("train"):
+            train_op = tf.train.GradientDescentOptimizer(FLAGS.learning_rate).minimize(
+                cross_entropy, global_step=global_step)
+        with tf.name_scope("Accuracy"):
+            correct = tf.equal(tf.argmax(y, 1), tf.argmax(y_, 1))
+            accuracy = tf.reduce_mean(tf.cast(correct, tf.float32))
+        tf.summary.scalar("cost", cross_entropy)
+        tf.summary.scalar("accuracy", accuracy)
+        summary_op = tf.summary.merge_all()
+        init_op = tf.global_variables_initializer()
+    return dict(global_step=global_step, x=x, y_=y_, W=[W1, W2, b1, b2], cross_entropy=cross_entropy,
+                train_op=train_op, accuracy=accuracy, summary_op=summary_op, init_op=init_op)
+
+
+def run_graph_worker(server, mnist, logs_path):
+    g = build_graph(server.cluster, FLAGS.task_index)
+    sv = tf.train.Supervisor(is_chief=server.is_chief, global_step=g["global_step"], init_op=g["init_op"])
+    begin = time.time()
+    cost = float("nan")
+    steps = 0
+    with sv.prepare_or_wait_for_session(server.target) as sess:
+        writer = tf.summary.FileWriter(logs_path, graph=tf.get_default_graph())
+        batch_count = mnist.train.num_examples // FLAGS.batch_size
+        t0 = time.time()
+        done = False
+        for epoch in range(FLAGS.training_epochs):
+            count = 0
+            for i in range(batch_count):
+                bx, by = mnist.train.next_batch(FLAGS.batch_size)
+                _, cost, summary, step = sess.run([g["train_op"], g["cross_entropy"], g["summary_op"],
+                                                   g["global_step"]], feed_dict={g["x"]: bx, g["y_"]: by})
+                writer.add_summary(summary, int(step))
+                steps += 1
+                count += 1
+                if count % FLAGS.frequency == 0 or i + 1 == batch_count:
+                    dt = time.time() - t0
+                    t0 = time.time()
+                    print(step_line(steps, int(sess.run(g["global_step"])), epoch + 1, i + 1, batch_count,
+                                    float(cost), dt * 1000.0 / FLAGS.frequency), flush=True)
+                    count = 0
+                if FLAGS.max_steps and steps >= FLAGS.max_steps:
+                    done = True
+                    break
+            if done:
+                break
+        acc = float(sess.run(g["accuracy"], feed_dict={g["x"]: mnist.test.images, g["y_"]: mnist.test.labels}))
+        params = [np.asarray(sess.run(v)) for v in g["W"]]
+        gstep = int(sess.run(g["global_step"]))
+        writer.close()
+    sv.stop()
+    return acc, float(cost), time.time() - begin, params, gstep
+
+
+def run_fused_worker(server, mnist):
+    """Whole-step MFMA kernel chain (models.mlp) fed from the same dataset."""
+    import torch
+
+    from distributed_tensorflow_example_amd.models import mlp
+
+    world = server.world
+    tr = mlp.FusedMLPTrainer(batch_size=FLAGS.batch_size, lr=FLAGS.learning_rate, act=FLAGS.activation,
+                             world=world)
+    begin = time.time()
+    batch_count = mnist.train.num_examples // FLAGS.batch_size
+    steps = 0
+    loss = float("nan")
+    for epoch in range(FLAGS.training_epochs):
+        for i in range(batch_count):
+            bx, by = mnist.train.next_batch(FLAGS.batch_size)
+            xt = torch.from_numpy(bx).to(tr.device)
+            yt = torch.from_numpy(by.argmax(1).astype(np.int32)).to(tr.device)
+            tr.step_tensors(xt, yt)
+            steps += 1
+            if steps % FLAGS.frequency == 0 or i + 1 == batch_count:
+                m = tr.read_metrics(steps - 1, steps)
+                loss = float(m[-1][0])
+                print(step_line(steps, tr.global_step(), epoch + 1, i + 1, batch_count, loss, 0.0), flush=True)
+            if FLAGS.max_steps and steps >= FLAGS.max_steps:
+                break
+        if FLAGS.max_steps and steps >= FLAGS.max_steps:
+            break
+    p = mlp.unflatten(tr.get_params().cpu())
+    z = mlp.reference_forward(tr.get_params().cpu(), torch.from_numpy(mnist.test.images), FLAGS.activation)
+    acc = float((z.argmax(1).numpy() == mnist.test.labels.argmax(1)).mean())
+    params = [p[k].numpy() for k in ("weights/Variable", "weights/Variable_1", "biases/Variable",
+                                     "biases/Variable_1")]
+    server.signal_done()
+    return acc, loss, time.time() - begin, params, tr.global_step()
+
+
+def main(_argv):
+    cluster = cluster_spec()
+    server = tf.train.Server(cluster, job_name=FLAGS.job_name, task_index=FLAGS.task_index)
+    logs_path = os.path.join(FLAGS.logs_path, f"{FLAGS.job_name}_{FLAGS.task_index}")
+    shutil.rmtree(logs_path, ignore_errors=True)
+    os.makedirs(logs_path, exist_ok=True)
+
+    if FLAGS.job_name == "ps":
+        print(f"ps {FLAGS.task_index} start ...", flush=True)
+        server.join()
+        print(f"ps {FLAGS.task_index} done", flush=True)
+        return 0
+    print(f"worker {FLAGS.task_index} start ...", flush=True)
+    mnist = mnist_data.read_data_sets(f"MNIST_data/{FLAGS.job_name}_{FLAGS.task_index}", one_hot=True,
+                                      seed=FLAGS.task_index, train_size=FLAGS.train_size)
+    if FLAGS.fused:
+        acc, cost, total, params, gstep = run_fused_worker(server, mnist)
+    else:
+        acc, cost, total, params, gstep = run_graph_worker(server, mnist, logs_path)
+    print("Test-Accuracy: %2.2f" % acc)
+    print("Total Time: %3.2fs" % total)
+    print("Final Cost: %.4f" % cost)
+    if FLAGS.result_json:
+        with open(FLAGS.result_json, "w") as f:
+            json.dump({"accuracy": acc, "cost": cost, "global_step": gstep,
+                       "param_sums": [float(np.float64(p).sum()) for p in params],
+                       "param_abs": [float(np.abs(np.float64(p)).sum()) for p in params]}, f)
+    print("done", flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    tf.app.run(main)

@@ -1,0 +1,308 @@
+"""CPU tests of the native runtime (csrc/runtime/*): CRC32C, TFRecord / tfevents
+framing, TF V2 checkpoint bundles (checked with an independent pure-Python
+SSTable parser), TCP rendezvous store, blocking queue, libsvm parser."""
+import os
+import struct
+import threading
+import time
+
+import numpy as np
+import pytest
+
+
+# --------------------------------------------------------------- pure-python oracles
+def _crc32c_py(data: bytes) -> int:
+    poly = 0x82F63B78
+    tab = []
+    for i in range(256):
+        c = i
+        for _ in range(8):
+            c = (c >> 1) ^ poly if c & 1 else c >> 1
+        tab.append(c)
+    crc = 0xFFFFFFFF
+    for b in data:
+        crc = tab[(crc ^ b) & 0xFF] ^ (crc >> 8)
+    return crc ^ 0xFFFFFFFF
+
+
+def _mask(c):
+    return ((((c >> 15) | (c << 17)) & 0xFFFFFFFF) + 0xA282EAD8) & 0xFFFFFFFF
+
+
+def _varint(b, i):
+    r = s = 0
+    while True:
+        x = b[i]
+        i += 1
+        r |= (x & 0x7F) << s
+        s += 7
+        if not x & 0x80:
+            return r, i
+
+
+def _proto_fields(b):
+    i, out = 0, {}
+    while i < len(b):
+        key, i = _varint(b, i)
+        f, wt = key >> 3, key & 7
+        if wt == 0:
+            v, i = _varint(b, i)
+        elif wt == 2:
+            n, i = _varint(b, i)
+            v = b[i:i + n]
+            i += n
+        elif wt == 5:
+            v = struct.unpack("<I", b[i:i + 4])[0]
+            i += 4
+        elif wt == 1:
+            v = struct.unpack("<Q", b[i:i + 8])[0]
+            i += 8
+        else:
+            raise ValueError(wt)
+        out.setdefault(f, []).append(v)
+    return out
+
+
+def _block_entries(block):
+    nrest = struct.unpack("<I", block[-4:])[0]
+    end = len(block) - 4 - 4 * nrest
+    i, key, out = 0, b"", []
+    while i < end:
+        shared, i = _varint(block, i)
+        nonshared, i = _varint(block, i)
+        vlen, i = _varint(block, i)
+        key = key[:shared] + block[i:i + nonshared]
+        i += nonshared
+        out.append((key, block[i:i + vlen]))
+        i += vlen
+    return out
+
+
+def _read_block(data, off, size):
+    blk = data[off:off + size]
+    typ = data[off + size]
+    crc = struct.unpack("<I", data[off + size + 1:off + size + 5])[0]
+    assert typ == 0
+    assert crc == _mask(_crc32c_py(blk + bytes([typ])))
+    return blk
+
+
+def sstable_py(path):
+    data = open(path, "rb").read()
+    foot = data[-48:]
+    assert struct.unpack("<Q", foot[40:])[0] == 0xDB4775248B80FB57
+    _, i = _varint(foot, 0)
+    _, i = _varint(foot, i)            # metaindex handle
+    ioff, i = _varint(foot, i)
+    isz, i = _varint(foot, i)
+    out = {}
+    for _, h in _block_entries(_read_block(data, ioff, isz)):
+        off, j = _varint(h, 0)
+        sz, _ = _varint(h, j)
+        for k, v in _block_entries(_read_block(data, off, sz)):
+            out[k] = v
+    return out
+
+
+# --------------------------------------------------------------- CRC / records
+def test_crc32c_vectors(native):
+    for s in [b"", b"a", b"123456789", bytes(range(256)) * 13, os.urandom(1000)]:
+        assert native.crc32c(s) == _crc32c_py(s)
+    assert native.crc32c(b"123456789") == 0xE3069283
+    assert native.masked_crc32c(b"abc") == _mask(_crc32c_py(b"abc"))
+
+
+def test_tfrecord_roundtrip_and_framing(native, tmp_path):
+    recs = [b"", b"x", os.urandom(5000), b"hello world"]
+    p = str(tmp_path / "r.tfrecord")
+    native.write_records(p, recs)
+    raw = open(p, "rb").read()
+    i, got = 0, []
+    while i < len(raw):
+        n = struct.unpack("<Q", raw[i:i + 8])[0]
+        assert struct.unpack("<I", raw[i + 8:i + 12])[0] == _mask(_crc32c_py(raw[i:i + 8]))
+        body = raw[i + 12:i + 12 + n]
+        assert struct.unpack("<I", raw[i + 12 + n:i + 16 + n])[0] == _mask(_crc32c_py(body))
+        got.append(body)
+        i += 16 + n
+    assert got == recs
+    assert native.read_records(p) == recs
+
+
+def test_event_file_writer_scalars(native, tmp_path):
+    from distributed_tensorflow_example_amd.compat import summary
+
+    w = summary.FileWriter(str(tmp_path))
+    for s in range(5):
+        w.add_summary(summary.summary_proto([summary.scalar_value("cost", 1.0 / (s + 1))]), s)
+    w.add_scalar("acc", 0.5, 7) if hasattr(w, "add_scalar") else None
+    w.close()
+    files = [f for f in os.listdir(tmp_path) if "tfevents" in f]
+    assert len(files) == 1
+    evs = list(summary.summary_iterator(str(tmp_path / files[0])))
+    assert evs[0].file_version.startswith("brain.Event:")
+    costs = [(e.step, v) for e in evs for (t, v) in e.scalars() if t == "cost"]
+    assert [c[0] for c in costs] == list(range(5))
+    assert abs(costs[2][1] - 1 / 3) < 1e-6
+
+
+# --------------------------------------------------------------- bundle
+def test_bundle_roundtrip_and_format(native, tmp_path):
+    import torch
+
+    from distributed_tensorflow_example_amd.compat import saver
+
+    tens = {"weights/Variable": torch.randn(784, 100), "biases/Variable": torch.zeros(100),
+            "global_step": torch.tensor(7, dtype=torch.int64), "h": torch.arange(6, dtype=torch.int32).reshape(2, 3),
+            "d": torch.randn(3, dtype=torch.float64)}
+    prefix = str(tmp_path / "model.ckpt-7")
+    saver.write_bundle(prefix, tens)
+    assert os.path.exists(prefix + ".index")
+    assert os.path.exists(prefix + ".data-00000-of-00001")
+    for k, v in tens.items():
+        assert torch.equal(saver.read_tensor(prefix, k), v)
+    # independent parse of the SSTable index + data file
+    tab = sstable_py(prefix + ".index")
+    hdr = _proto_fields(tab[b""])
+    assert hdr.get(1, [1])[0] == 1                               # num_shards
+    data = open(prefix + ".data-00000-of-00001", "rb").read()
+    keys = sorted(k for k in tab if k)
+    assert keys == sorted(k.encode() for k in tens)
+    dt = {1: np.float32, 2: np.float64, 3: np.int32, 9: np.int64}
+    for k in keys:
+        e = _proto_fields(tab[k])
+        dims = [_proto_fields(d)[1][0] if 1 in _proto_fields(d) else 0 for d in _proto_fields(e[2][0]).get(2, [])] \
+            if 2 in e else []
+        off = e.get(4, [0])[0]
+        size = e[5][0]
+        blob = data[off:off + size]
+        assert e[6][0] == _mask(_crc32c_py(blob))
+        arr = np.frombuffer(blob, dtype=dt[e[1][0]]).reshape(dims)
+        assert np.array_equal(arr, tens[k.decode()].numpy())
+
+
+def test_saver_checkpoint_state_and_max_to_keep(tmp_path):
+    import distributed_tensorflow_example_amd.compat as tf
+
+    tf.reset_default_graph()
+    v = tf.Variable(tf.zeros([3]), name="v")
+    s = tf.train.Saver(max_to_keep=2)
+    with tf.Session() as sess:
+        sess.run(tf.global_variables_initializer())
+        for step in (1, 2, 3):
+            v.load(np.full(3, step, np.float32))
+            s.save(sess, str(tmp_path / "model.ckpt"), global_step=step)
+        assert tf.train.latest_checkpoint(str(tmp_path)).endswith("model.ckpt-3")
+        assert not tf.train.checkpoint_exists(str(tmp_path / "model.ckpt-1"))
+        st = tf.train.get_checkpoint_state(str(tmp_path))
+        assert len(st.all_model_checkpoint_paths) == 2
+        s.restore(sess, str(tmp_path / "model.ckpt-2"))
+        assert np.allclose(sess.run(v), 2)
+    r = tf.train.NewCheckpointReader(str(tmp_path / "model.ckpt-3"))
+    assert r.has_tensor("v") and np.allclose(r.get_tensor("v"), 3)
+    assert dict(tf.train.list_variables(str(tmp_path)))["v"] == [3]
+
+
+# --------------------------------------------------------------- store
+def test_tcp_store_kv_and_barrier(native):
+    srv = native.TCPStore("127.0.0.1", 0, True, 30.0)
+    port = srv.port
+    cl = native.TCPStore("127.0.0.1", port, False, 30.0)
+    cl.set("a", b"1")
+    assert srv.get("a") == b"1"
+    assert cl.add("ctr", 5) == 5 and srv.add("ctr", 2) == 7
+    assert srv.check(["a", "ctr"]) and not srv.check(["zz"])
+    got = {}
+
+    def late():
+        time.sleep(0.2)
+        cl.set("late", b"xyz")
+    t = threading.Thread(target=late)
+    t.start()
+    got["late"] = srv.get("late", 10.0)
+    t.join()
+    assert got["late"] == b"xyz"
+    with pytest.raises(Exception):
+        srv.get("never", 0.2)
+    # 3-party barrier
+    clients = [native.TCPStore("127.0.0.1", port, False, 30.0) for _ in range(3)]
+    done = []
+    ths = [threading.Thread(target=lambda c=c: (c.barrier("b0", 3, 10.0), done.append(1))) for c in clients]
+    [x.start() for x in ths]
+    [x.join() for x in ths]
+    assert len(done) == 3
+    assert cl.compare_set("cs", b"", b"v1") == b"v1"
+    assert cl.delete_key("a")
+    assert srv.num_keys() >= 1
+
+
+# --------------------------------------------------------------- queue
+def test_blocking_queue(native):
+    q = native.BlockingQueue(4)
+    for i in range(4):
+        q.put(i)
+    assert q.size() == 4
+    with pytest.raises(native.QueueTimeoutError):
+        q.put(99, 0.1)
+    assert [q.get() for _ in range(4)] == [0, 1, 2, 3]
+    res = []
+
+    def cons():
+        try:
+            while True:
+                res.append(q.get())
+        except native.QueueClosedError:
+            pass
+    th = [threading.Thread(target=cons) for _ in range(3)]
+    [t.start() for t in th]
+    prods = [threading.Thread(target=lambda k=k: [q.put(k * 1000 + j) for j in range(200)]) for k in range(3)]
+    [p.start() for p in prods]
+    [p.join() for p in prods]
+    while q.size():
+        time.sleep(0.01)
+    q.close(False)
+    [t.join() for t in th]
+    assert sorted(res) == sorted(k * 1000 + j for k in range(3) for j in range(200))
+
+
+# --------------------------------------------------------------- libsvm
+def test_libsvm_parse_matches_python(native, tmp_path):
+    lines = ["1 3:0.5 10:1.25\n", "0 1:2\n", "1\t7:1 8:-3.5 9:4e-2\n", "\n", "0 100:1\n"]
+    y, rp, ids, vals = native.libsvm_parse_bytes("".join(lines).encode())
+    assert list(y) == [1, 0, 1, 0]
+    assert list(rp) == [0, 2, 3, 6, 7]
+    assert list(ids) == [3, 10, 1, 7, 8, 9, 100]
+    assert np.allclose(vals, [0.5, 1.25, 2, 1, -3.5, 0.04, 1])
+    # multi-file, multithreaded, sampled
+    rng = np.random.default_rng(0)
+    files = []
+    for f in range(4):
+        p = tmp_path / f"part-{f}"
+        with open(p, "w") as fh:
+            for r in range(500):
+                nz = rng.integers(1, 6)
+                fh.write(f"{r % 2} " + " ".join(f"{int(i)}:1" for i in rng.integers(0, 1000, nz)) + "\n")
+        files.append(str(p))
+    y, rp, ids, vals = native.libsvm_parse_files(files, 3, 1.0, 0)
+    assert len(y) == 2000 and rp[-1] == len(ids)
+    y2, _, _, _ = native.libsvm_parse_files(files, 3, 0.25, 1)
+    assert 350 < len(y2) < 650
+
+
+def test_libsvm_stream_batches(native, tmp_path):
+    p = tmp_path / "d.svm"
+    with open(p, "w") as fh:
+        for r in range(1000):
+            fh.write(f"{r % 2} {r}:1\n")
+    st = native.LibsvmStream([str(p)], 128, 2, 1.0, False, 8, 0)
+    total = 0
+    seen = set()
+    while True:
+        b = st.next(10.0)
+        if b is None:
+            break
+        y, rp, ids, vals = b
+        total += len(y)
+        seen.update(int(i) for i in ids)
+    st.stop()
+    assert total == 1000 and seen == set(range(1000))

@@ -1,0 +1,263 @@
+"""Numerics of the generic HIP kernels (csrc/kernels/gemm.hip, ops.hip) against
+plain PyTorch fp32 references of the same op."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return float((a - b).norm() / b.norm().clamp_min(1e-12))
+
+
+def _act(z, act):
+    return {"none": z, "relu": torch.relu(z), "sigmoid": torch.sigmoid(z), "tanh": torch.tanh(z),
+            "gelu": torch.nn.functional.gelu(z)}[act]
+
+
+@pytest.mark.parametrize("M,N,K", [(100, 100, 784), (100, 10, 100), (37, 129, 65), (256, 512, 1024),
+                                   (1, 1, 1), (1000, 1, 1), (784, 100, 100)])
+@pytest.mark.parametrize("ta,tb", [(False, False), (True, False), (False, True), (True, True)])
+def test_gemm_shapes_transposes(native, M, N, K, ta, tb):
+    from distributed_tensorflow_example_amd import ops
+    g = torch.Generator().manual_seed(M * 7 + N * 3 + K)
+    A = torch.randn((K, M) if ta else (M, K), generator=g)
+    B = torch.randn((N, K) if tb else (K, N), generator=g)
+    out = ops.matmul(A.cuda(), B.cuda(), ta, tb)
+    ref = (A.t() if ta else A) @ (B.t() if tb else B)
+    assert out.shape == ref.shape
+    assert rel(out, ref) < 1e-2
+
+
+@pytest.mark.parametrize("act", ["none", "relu", "sigmoid", "tanh", "gelu"])
+@pytest.mark.parametrize("bf16_in", [False, True])
+def test_gemm_bias_act_epilogue(native, act, bf16_in):
+    from distributed_tensorflow_example_amd import ops
+    g = torch.Generator().manual_seed(5)
+    A, B, b = torch.randn(200, 300, generator=g), torch.randn(300, 130, generator=g), torch.randn(130, generator=g)
+    dt = torch.bfloat16 if bf16_in else torch.float32
+    out = ops.matmul(A.cuda().to(dt), B.cuda().to(dt), bias=b.cuda(), act=act)
+    ref = _act(A.to(dt).float() @ B.to(dt).float() + b, act)
+    assert rel(out, ref) < 1e-2
+
+
+def test_gemm_alpha_beta_and_bf16_out(native):
+    C = native
+    A, B = torch.randn(64, 96).cuda(), torch.randn(96, 80).cuda()
+    out = torch.randn(64, 80).cuda()
+    o0 = out.clone()
+    C.gemm(A, False, B, False, out, None, 0, 0.5, 2.0, None)
+    assert rel(out, 0.5 * (A @ B) + 2.0 * o0) < 1e-2
+    ob = torch.empty(64, 80, dtype=torch.bfloat16, device="cuda")
+    C.gemm(A, False, B, False, ob, None, 0, 1.0, 0.0, None)
+    assert rel(ob, A @ B) < 1e-2
+
+
+@pytest.mark.parametrize("act", ["none", "relu", "sigmoid", "tanh", "gelu"])
+def test_linear_act_autograd(native, act):
+    from distributed_tensorflow_example_amd import ops
+    torch.manual_seed(0)
+    # operands pre-rounded to bf16 (what the MFMA GEMM consumes) so relu's
+    # mask is the same on both sides; the fp32 reference then isolates the
+    # kernel's own error
+    x = torch.randn(100, 784).bfloat16().float().requires_grad_()
+    w = torch.randn(784, 100).bfloat16().float().requires_grad_()
+    b = torch.randn(100, requires_grad=True)
+    y = _act(x @ w + b, act)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    xg, wg, bg = [t.detach().cuda().requires_grad_() for t in (x, w, b)]
+    yg = ops.linear_act(xg, wg, bg, act)
+    yg.backward(gy.cuda())
+    assert rel(yg, y) < 1e-2
+    assert rel(xg.grad, x.grad) < 2e-2
+    assert rel(wg.grad, w.grad) < 2e-2
+    assert rel(bg.grad, b.grad) < 2e-2
+
+
+def test_col_sum(native):
+    X = torch.randn(1000, 37).cuda()
+    out = torch.empty(37, device="cuda")
+    native.col_sum(X, out)
+    assert torch.allclose(out.cpu(), X.cpu().sum(0), atol=1e-3, rtol=1e-4)
+
+
+@pytest.mark.parametrize("dense", [False, True])
+@pytest.mark.parametrize("naive", [False, True])
+@pytest.mark.parametrize("B,Cn", [(100, 10), (7, 1000), (256, 3)])
+def test_softmax_xent(native, dense, naive, B, Cn):
+    from distributed_tensorflow_example_amd import ops
+    torch.manual_seed(B + Cn)
+    z = torch.randn(B, Cn) * 3
+    lab = torch.randint(0, Cn, (B,))
+    y = torch.nn.functional.one_hot(lab, Cn).float() if dense else lab
+    zr = z.clone().requires_grad_()
+    lr_ = torch.nn.functional.cross_entropy(zr, lab)
+    lr_.backward()
+    zg = z.cuda().requires_grad_()
+    l = ops.softmax_xent(zg, y.cuda(), naive=naive)
+    l.backward()
+    assert abs(float(l) - float(lr_)) < 1e-4 * max(1.0, abs(float(lr_)))
+    assert torch.allclose(zg.grad.cpu(), zr.grad, atol=1e-6)
+
+
+def test_softmax_xent_correct_count(native):
+    z = torch.randn(300, 10).cuda()
+    lab = torch.randint(0, 10, (300,)).cuda()
+    loss_rows = torch.empty(300, device="cuda")
+    grad = torch.empty_like(z)
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    native.softmax_xent(z, lab, None, loss_rows, grad, cnt, 1.0 / 300, False)
+    assert int(cnt.item()) == int((z.argmax(1) == lab).sum())
+
+
+@pytest.mark.parametrize("n", [1, 500, 4097])
+def test_sigmoid_xent(native, n):
+    from distributed_tensorflow_example_amd import ops
+    torch.manual_seed(n)
+    x = torch.randn(n, 1) * 4
+    t = (torch.rand(n, 1) > 0.5).float()
+    xr = x.clone().requires_grad_()
+    ref = torch.nn.functional.binary_cross_entropy_with_logits(xr, t)
+    ref.backward()
+    xg = x.cuda().requires_grad_()
+    l = ops.sigmoid_xent(xg, t.cuda())
+    l.backward()
+    assert abs(float(l) - float(ref)) < 1e-5 * max(1, abs(float(ref)))
+    assert torch.allclose(xg.grad.cpu(), xr.grad, atol=1e-7)
+
+
+def _bags(B, V, maxlen, seed):
+    g = torch.Generator().manual_seed(seed)
+    lens = torch.randint(0, maxlen + 1, (B,), generator=g)
+    offsets = torch.zeros(B + 1, dtype=torch.int64)
+    offsets[1:] = lens.cumsum(0)
+    ids = torch.randint(0, V, (int(offsets[-1]),), generator=g)
+    w = torch.rand(ids.numel(), generator=g)
+    return ids, offsets, w
+
+
+@pytest.mark.parametrize("D", [1, 16, 128, 33])
+@pytest.mark.parametrize("mode", ["sum", "mean", "sqrtn"])
+def test_embedding_bag_fwd_bwd(native, D, mode):
+    from distributed_tensorflow_example_amd import ops
+    V, B = 5000, 64
+    ids, offsets, w = _bags(B, V, 40, D)
+    W = torch.randn(V, D)
+    Wr = W.clone().requires_grad_()
+    ref = ops.embedding_bag(Wr, ids, offsets, w, mode)   # CPU path = torch oracle
+    go = torch.randn_like(ref)
+    ref.backward(go)
+    Wg = W.cuda().requires_grad_()
+    out = ops.embedding_bag(Wg, ids.cuda(), offsets.cuda(), w.cuda(), mode)
+    out.backward(go.cuda())
+    assert torch.allclose(out.cpu(), ref.detach(), atol=1e-4, rtol=1e-4)
+    assert torch.allclose(Wg.grad.cpu(), Wr.grad, atol=1e-4, rtol=1e-4)
+
+
+def test_embedding_bag_sgd_scatter(native):
+    from distributed_tensorflow_example_amd import ops
+    V, D, B = 1000, 1, 200
+    ids, offsets, w = _bags(B, V, 30, 1)
+    W = torch.randn(V)
+    go = torch.randn(B, 1)
+    ref = ops.embedding_bag_sgd_(W.clone(), ids, offsets, w, go, 0.5)
+    got = ops.embedding_bag_sgd_(W.clone().cuda(), ids.cuda(), offsets.cuda(), w.cuda(), go.cuda(), 0.5)
+    assert torch.allclose(got.cpu(), ref, atol=1e-5)
+
+
+def test_argmax_correct(native):
+    from distributed_tensorflow_example_amd import ops
+    z = torch.randn(10000, 10)
+    lab = torch.randint(0, 10, (10000,))
+    assert int(ops.argmax_correct(z.cuda(), lab.cuda())) == int((z.argmax(1) == lab).sum())
+
+
+def test_auc_histogram(native):
+    from distributed_tensorflow_example_amd import ops
+    n, nb = 20000, 200
+    lab = (torch.rand(n) > 0.7).float()
+    pred = torch.sigmoid(torch.randn(n) + 1.5 * lab)
+    pc, nc = torch.zeros(nb, dtype=torch.int64), torch.zeros(nb, dtype=torch.int64)
+    ops.auc_histogram_(pred, lab, pc, nc)
+    pg, ng = torch.zeros(nb, dtype=torch.int64, device="cuda"), torch.zeros(nb, dtype=torch.int64, device="cuda")
+    ops.auc_histogram_(pred.cuda(), lab.cuda(), pg, ng)
+    assert torch.equal(pg.cpu(), pc) and torch.equal(ng.cpu(), nc)
+    # exact rank AUC
+    order = pred.argsort()
+    ranks = torch.empty(n)
+    ranks[order] = torch.arange(1, n + 1).float()
+    P = lab.sum()
+    exact = float((ranks[lab > 0].sum() - P * (P + 1) / 2) / (P * (n - P)))
+    assert abs(ops.auc_from_histograms(pg, ng) - exact) < 5e-3
+
+
+@pytest.mark.parametrize("kind", ["sgd", "momentum", "nesterov", "adam", "adamw"])
+@pytest.mark.parametrize("gdt", [torch.float32, torch.bfloat16])
+def test_fused_optimizers_match_cpu(native, kind, gdt):
+    from distributed_tensorflow_example_amd import optim
+    torch.manual_seed(1)
+    shapes = [(784, 100), (100,), (100, 10), (10,), (5000,)]
+    ps = [torch.randn(s) for s in shapes]
+
+    def mk(params):
+        if kind == "sgd":
+            return optim.FusedSGD(params, 0.1)
+        if kind in ("momentum", "nesterov"):
+            return optim.FusedMomentum(params, 0.1, 0.9, nesterov=kind == "nesterov")
+        if kind == "adam":
+            return optim.FusedAdam(params, 0.01)
+        return optim.FusedAdamW(params, 0.01, weight_decay=0.1)
+    pc = [p.clone() for p in ps]
+    pg = [p.clone().cuda() for p in ps]
+    oc, og = mk(pc), mk(pg)
+    for it in range(5):
+        gs = [torch.randn(s).to(gdt) for s in shapes]
+        oc.step(grads=[g.float() for g in gs], grad_scale=0.5)
+        og.step(grads=[g.cuda() for g in gs], grad_scale=0.5)
+    for a, b in zip(pg, pc):
+        assert torch.allclose(a.cpu(), b, atol=2e-5, rtol=1e-5), (a.cpu() - b).abs().max()
+
+
+def test_global_grad_norm(native):
+    from distributed_tensorflow_example_amd import optim
+    gs = [torch.randn(1000), torch.randn(77, 13), torch.randn(5)]
+    n = optim.global_grad_norm([g.cuda() for g in gs])
+    ref = math.sqrt(sum(float((g ** 2).sum()) for g in gs))
+    assert abs(float(n) - ref) < 1e-4 * ref
+
+
+def test_compat_mnist_graph_trains_on_gpu(native):
+    """example.py-shaped graph through the compat layer on the GPU (MFMA linear)."""
+    import numpy as np
+
+    import distributed_tensorflow_example_amd.compat as tf
+    from distributed_tensorflow_example_amd.data import mnist
+
+    tf.reset_default_graph()
+    ds = mnist.read_data_sets("/tmp/unused", one_hot=True, train_size=5000, test_size=1000)
+    x = tf.placeholder(tf.float32, [None, 784])
+    y_ = tf.placeholder(tf.float32, [None, 10])
+    W1 = tf.Variable(tf.random_normal([784, 100], seed=1))
+    W2 = tf.Variable(tf.random_normal([100, 10], seed=2))
+    b1, b2 = tf.Variable(tf.zeros([100])), tf.Variable(tf.zeros([10]))
+    a2 = tf.nn.sigmoid(tf.add(tf.matmul(x, W1), b1))
+    y = tf.nn.softmax(tf.add(tf.matmul(a2, W2), b2))
+    ce = tf.reduce_mean(-tf.reduce_sum(y_ * tf.log(y), reduction_indices=[1]))
+    gs = tf.get_variable("global_step", [], initializer=tf.constant_initializer(0), trainable=False)
+    train_op = tf.train.GradientDescentOptimizer(0.05).minimize(ce, global_step=gs)
+    acc = tf.reduce_mean(tf.cast(tf.equal(tf.argmax(y, 1), tf.argmax(y_, 1)), tf.float32))
+    with tf.Session() as sess:
+        sess.run(tf.global_variables_initializer())
+        first = None
+        for _ in range(200):
+            bx, by = ds.train.next_batch(100)
+            _, c = sess.run([train_op, ce], {x: bx, y_: by})
+            first = c if first is None else first
+        a = sess.run(acc, {x: ds.test.images, y_: ds.test.labels})
+        assert int(np.asarray(sess.run(gs))) == 200
+    assert W1.value.is_cuda
+    assert c < first and a > 0.5

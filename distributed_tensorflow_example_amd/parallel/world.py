@@ -116,13 +116,15 @@ class World:
         return dst
 
     def all_to_all(self, src: torch.Tensor, send_counts, dst: torch.Tensor, recv_counts) -> torch.Tensor:
+        """Uneven all-to-all; counts are in rows (first dimension) per peer."""
         send_counts = [int(c) for c in send_counts]
         recv_counts = [int(c) for c in recv_counts]
         if self.world_size == 1:
             dst[: recv_counts[0]].copy_(src[: send_counts[0]])
             return dst
         if src.is_cuda and self.comm is not None:
-            self.comm.all_to_all(src, send_counts, dst, recv_counts)
+            inner = src[0].numel() if src.dim() > 1 else 1   # counts are in rows; RCCL wants elements
+            self.comm.all_to_all(src, [c * inner for c in send_counts], dst, [c * inner for c in recv_counts])
         else:
             dist.all_to_all_single(dst, src, output_split_sizes=recv_counts,
                                    input_split_sizes=send_counts)

@@ -1,0 +1,192 @@
+"""Sparse LR path on CPU: libsvm DataProvider (sharding, sampling, batching),
+the row-sharded embedding table over gloo (2 ranks == 1 rank, bit-for-bit
+init independent of world size), sharded TF checkpoints, and the lr2-style
+ps/worker example end to end."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.fixture(scope="module")
+def svm_dir(tmp_path_factory):
+    from distributed_tensorflow_example_amd.data import libsvm
+
+    d = tmp_path_factory.mktemp("svm")
+    tr = libsvm.write_synthetic(str(d / "train" / "part"), 4, 700, 3000, 12, seed=0)
+    te = libsvm.write_synthetic(str(d / "test" / "part"), 2, 400, 3000, 12, seed=1)
+    with open(d / "train_file_list", "w") as f:
+        f.write("\n".join(tr) + "\n")
+    return d, tr, te
+
+
+def test_data_provider_sharding_and_batches(svm_dir):
+    from distributed_tensorflow_example_amd.data import libsvm
+
+    d, tr, te = svm_dir
+    # test_lr2.py: DataProvider(1, 0, 2, mode='all') over the file list -> every training sample
+    dp = libsvm.DataProvider(1, 0, 2, "all", train="@" + str(d / "train_file_list"), test=",".join(te),
+                             batch_size=128).init()
+    dp.LoadData()
+    assert len(dp.GetTrainSamples()) == 4 * 700
+    # worker 1 of 2 gets files[1::2]
+    dp1 = libsvm.DataProvider(2, 1, 2, "all", train=str(d / "train" / "part-*"), test=te[0]).init()
+    assert dp1.train_file_list == [tr[1], tr[3]]
+    dp1.LoadData()
+    assert len(dp1.GetTrainSamples()) == 1400
+    # batches cover the epoch exactly once; CSR invariants; COO view
+    dp.Shuffle()
+    seen = 0
+    for b in dp.NextBatch("train"):
+        assert b.offsets[0] == 0 and b.offsets[-1] == b.nnz and b.labels.shape == (b.size, 1)
+        coo = b.coo_indices()
+        assert coo.shape == (b.nnz, 2) and (np.diff(coo[:, 0]) >= 0).all()
+        seen += b.size
+    assert seen == 2800
+    s = dp.GetTestSamplesSampled(sampling_rate=0.1, sampling_max_num=50)
+    assert s.size == 50
+    # sampling rate in the native parser
+    dps = libsvm.DataProvider(1, 0, 2, "all", train=",".join(tr), test=te[0], train_sampling_rate=0.25).init()
+    dps.LoadData()
+    assert 500 < len(dps.GetTrainSamples()) < 900
+
+
+def test_data_provider_queue_mode(svm_dir):
+    from distributed_tensorflow_example_amd.data import libsvm
+
+    d, tr, te = svm_dir
+    dp = libsvm.DataProvider(1, 0, 2, "queue", train=",".join(tr), test=",".join(te), batch_size=100).init()
+    dp.LoadData()
+    bs = list(dp.NextBatch("train", max_batches=40))      # > one pass: the stream loops
+    assert len(bs) == 40 and all(b.size == 100 for b in bs)
+    t = dp.GetTestSamplesSampled(0.1, 300)
+    assert t.size == 300
+    dp.close()
+
+
+def test_parse_parity_with_python_reference_parser():
+    """Native parser == the reference's per-line split/int/float parse (lr2.py:57-67)."""
+    from distributed_tensorflow_example_amd.data import libsvm
+
+    lines = ["1 5:0.25 17:3\n", "0\t2:1\t9:-0.5\n", "1 100000000:1\n"]
+    d = libsvm.parse_lines(lines)
+    for i, line in enumerate(lines):
+        parts = line.strip().replace("\t", " ").split(" ")
+        lab = int(parts[0])
+        idx = [int(p.split(":")[0]) for p in parts[1:]]
+        val = [float(p.split(":")[1]) for p in parts[1:]]
+        s, e = d.offsets[i], d.offsets[i + 1]
+        assert d.labels[i] == lab and list(d.ids[s:e]) == idx and np.allclose(d.vals[s:e], val)
+
+
+def _sharded_worker(rank, ws, port, q, files, steps, lr):
+    try:
+        sys.path.insert(0, REPO)
+        os.environ.update(RANK=str(rank), WORLD_SIZE=str(ws), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                          MASTER_PORT=str(port))
+        from distributed_tensorflow_example_amd import ckpt
+        from distributed_tensorflow_example_amd.data import libsvm
+        from distributed_tensorflow_example_amd.models import sparse_lr
+        from distributed_tensorflow_example_amd.parallel import world as W
+
+        w = W.init(backend="gloo")
+        data = libsvm.load_files(files, 2)
+        tr = sparse_lr.SparseLRTrainer(3000, lr, w, seed=5)
+        init_tab = tr.W.full_table().numpy().copy()
+        B = 200
+        for s in range(steps):
+            rows = np.arange(s * B, (s + 1) * B)
+            mine = rows[rank * B // ws:(rank + 1) * B // ws]
+            tr.train_step(data.take(mine))
+        final = tr.W.full_table().numpy().copy()
+        local, repl = tr.checkpoint_tensors()
+        prefix = ckpt.save_sharded(os.path.join(os.path.dirname(files[0]), f"ck{ws}", "lr"), local, repl, w,
+                                   global_step=tr.global_step)
+        q.put((rank, init_tab, final, float(tr.b.detach()[0]), prefix))
+    except Exception:
+        import traceback
+
+        q.put((rank, traceback.format_exc(), None, None, None))
+
+
+def _run(ws, *args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_sharded_worker, args=(r, ws, port, q) + args) for r in range(ws)]
+    [p.start() for p in ps]
+    out = sorted([q.get(timeout=240) for _ in range(ws)], key=lambda r: r[0])
+    [p.join(60) for p in ps]
+    for r in out:
+        assert not isinstance(r[1], str), r[1]
+    return out
+
+
+def test_sharded_table_two_ranks_equal_one(svm_dir):
+    from distributed_tensorflow_example_amd.compat import saver
+
+    d, tr, te = svm_dir
+    one = _run(1, tr, 8, 0.5)
+    two = _run(2, tr, 8, 0.5)
+    assert np.array_equal(one[0][1], two[0][1])                 # init independent of sharding
+    assert np.array_equal(two[0][2], two[1][2])
+    assert np.allclose(one[0][2], two[0][2], atol=1e-6)         # sync 2x100 == 1x200
+    assert abs(one[0][3] - two[0][3]) < 1e-6
+    prefix = two[0][4]
+    idx = saver.read_bundle_index(prefix)
+    assert {"weights/Variable/part_0", "weights/Variable/part_1", "bias/Variable", "global_step"} <= set(idx)
+    p0 = saver.read_tensor(prefix, "weights/Variable/part_0").numpy()
+    p1 = saver.read_tensor(prefix, "weights/Variable/part_1").numpy()
+    full = np.empty((3000, 1), np.float32)
+    full[0::2], full[1::2] = p0, p1
+    assert np.array_equal(full, two[0][2])
+
+
+def test_lr2_example_ps_two_workers(svm_dir, tmp_path):
+    d, tr, te = svm_dir
+    p = _free_port()
+    conf = tmp_path / "cluster_conf.json"
+    conf.write_text(json.dumps({"ps": [f"127.0.0.1:{_free_port()}"],
+                                "worker": [f"127.0.0.1:{p}", f"127.0.0.1:{_free_port()}"]}))
+    common = [f"--cluster_conf={conf}", f"--train={','.join(tr)}", f"--test={','.join(te)}", "--features=3000",
+              "--num_epochs=2", "--learning_rate=0.5", "--batch_size=100", "--trace_step_interval=5",
+              f"--checkpoint={tmp_path}/ck/lr"]
+    env = dict(os.environ, PYTHONPATH=REPO, DTF_RENDEZVOUS_TIMEOUT="120")
+    script = os.path.join(REPO, "examples", "sparse_lr.py")
+    procs = [subprocess.Popen([sys.executable, script, "--job_name=ps", "--task_index=0"] + common, env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)]
+    for i in (1, 0):
+        procs.append(subprocess.Popen([sys.executable, script, "--job_name=worker", f"--task_index={i}",
+                                       f"--result_json={tmp_path}/w{i}.json"] + common, env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    outs = []
+    try:
+        for pr in procs:
+            outs.append(pr.communicate(timeout=240)[0])
+    finally:
+        for pr in procs:
+            if pr.poll() is None:
+                pr.kill()
+    for pr, o in zip(procs, outs):
+        assert pr.returncode == 0, o
+    r0, r1 = (json.load(open(tmp_path / f"w{i}.json")) for i in (0, 1))
+    assert r0["global_step"] == r1["global_step"] == 28          # 2 epochs x 14 batches (1400 / 100)
+    assert r0["auc"] == r1["auc"] and r0["b"] == r1["b"]
+    assert "Finish evaluate, auc:" in outs[2]
+    assert os.path.exists(tmp_path / "ck" / "lr-28.index")

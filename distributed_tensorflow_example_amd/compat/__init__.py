@@ -14,6 +14,7 @@ import types as _types
 from ..utils import flags as _flags
 from ..utils import gfile as _gfile
 from ..utils import logging as _logging
+from . import export as _export
 from . import metrics as _metrics
 from . import nn
 from . import queues as _queues
@@ -49,7 +50,8 @@ image = _types.SimpleNamespace(decode_jpeg=decode_jpeg)
 metrics = _types.SimpleNamespace(auc=_metrics.auc, accuracy=_metrics.accuracy)
 contrib = _types.SimpleNamespace(
     metrics=_types.SimpleNamespace(streaming_auc=_metrics.streaming_auc,
-                                   streaming_accuracy=_metrics.streaming_accuracy))
+                                   streaming_accuracy=_metrics.streaming_accuracy),
+    session_bundle=_types.SimpleNamespace(exporter=_export, load_session_bundle=_export.load_session_bundle))
 
 # TF 0.x aliases used by the reference (example.py:130-135, lr2.py:408) --------
 initialize_all_variables = global_variables_initializer

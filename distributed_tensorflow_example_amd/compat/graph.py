@@ -203,6 +203,8 @@ def _to_tensor(x, dev, dtype=None):
         t = torch.from_numpy(np.ascontiguousarray(x)).to(dev)
     elif isinstance(x, (bytes, str)):
         return x
+    elif isinstance(x, (list, tuple)) and x and all(isinstance(v, (bytes, str)) for v in x):
+        return list(x)                      # string tensors stay host-side lists
     else:
         t = torch.tensor(x, device=dev)
     if t.dtype == torch.float64:
@@ -252,6 +254,19 @@ class Tensor:
 
     def get_shape(self):
         return self.shape
+
+    def set_shape(self, shape):
+        """Static shape annotation; checked against the value at run time."""
+        self.shape = list(shape)
+        inner = self._eval
+
+        def checked(ctx, inner=inner, shape=tuple(shape)):
+            v = inner(ctx)
+            vs = tuple(getattr(v, "shape", ()))
+            if len(vs) != len(shape) or any(a is not None and a != b for a, b in zip(shape, vs)):
+                raise ValueError(f"{self.name}: value shape {vs} incompatible with set_shape {list(shape)}")
+            return v
+        self._eval = checked
 
     def __repr__(self):
         return f"<dtf Tensor {self.name}>"

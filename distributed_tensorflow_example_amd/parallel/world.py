@@ -143,6 +143,14 @@ class World:
             _WORLD = None
 
 
+def _cpu_threads(local_world: int):
+    """CPU data plane: split the host's cores between co-located ranks (as
+    torchrun does with OMP_NUM_THREADS) unless the user chose a count."""
+    if "OMP_NUM_THREADS" in os.environ:
+        return
+    torch.set_num_threads(max(1, min(4, (os.cpu_count() or 1) // max(1, local_world))))
+
+
 def _env_int(name: str, default: int) -> int:
     v = os.environ.get(name)
     return int(v) if v not in (None, "") else default
@@ -177,6 +185,8 @@ def init(rank: Optional[int] = None, world_size: Optional[int] = None,
 
     w = World(rank=rank, world_size=world_size, local_rank=local_rank, device=device,
               backend=backend if world_size > 1 else ("rccl" if device.type == "cuda" else "none"))
+    if device.type == "cpu":
+        _cpu_threads(_env_int("LOCAL_WORLD_SIZE", world_size))
     if world_size > 1:
         if master_addr is not None:
             os.environ["MASTER_ADDR"] = master_addr
@@ -223,6 +233,8 @@ def init_from_rendezvous(rdv, backend: str = "auto", timeout_s: float = 600.0) -
         device = torch.device("cpu")
     w = World(rank=rank, world_size=world_size, local_rank=rank, device=device,
               backend=backend if world_size > 1 else ("rccl" if device.type == "cuda" else "none"))
+    if device.type == "cpu":
+        _cpu_threads(rdv.cluster.total_tasks())
     if world_size > 1:
         from .cluster import split_address
 

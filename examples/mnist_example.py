@@ -161,7 +161,7 @@ def run_fused_worker(server, mnist):
             if steps % FLAGS.frequency == 0 or i + 1 == batch_count:
                 m = tr.read_metrics(steps - 1, steps)
                 loss = float(m[-1][0])
-                print(step_line(steps, tr.global_step(), epoch + 1, i + 1, batch_count, loss, 0.0), flush=True)
+                print(step_line(steps, tr.global_step, epoch + 1, i + 1, batch_count, loss, 0.0), flush=True)
             if FLAGS.max_steps and steps >= FLAGS.max_steps:
                 break
         if FLAGS.max_steps and steps >= FLAGS.max_steps:
@@ -172,7 +172,7 @@ def run_fused_worker(server, mnist):
     params = [p[k].numpy() for k in ("weights/Variable", "weights/Variable_1", "biases/Variable",
                                      "biases/Variable_1")]
     server.signal_done()
-    return acc, loss, time.time() - begin, params, tr.global_step()
+    return acc, loss, time.time() - begin, params, tr.global_step
 
 
 def main(_argv):

@@ -27,6 +27,14 @@ timeout -k 10 300 python bench.py --steps $STEPS --warmup 500 --eager > $OUT/ben
 rc=$?; tail -1 $OUT/bench_eager.log
 [ $rc -ne 0 ] && { echo "bench eager rc=$rc"; exit $rc; }
 
+if [ "${MODEL_BENCH:-0}" = "1" ]; then
+  for m in sparse_lr wide_deep; do
+    timeout -k 10 300 python scripts/bench_models.py --model $m --steps 100 --warmup 10 > $OUT/bench_$m.log 2>&1
+    rc=$?; tail -1 $OUT/bench_$m.log
+    [ $rc -ne 0 ] && { echo "bench $m rc=$rc"; exit $rc; }
+  done
+fi
+
 if [ "${SKIP_PROF:-0}" != "1" ]; then
   rm -rf $OUT/prof
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv rocpd -d $OUT/prof -o run -- python3 bench.py --steps 1000 --warmup 200 > $OUT/prof.log 2>&1

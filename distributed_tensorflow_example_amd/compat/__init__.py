@@ -25,6 +25,8 @@ from .graph import *  # noqa: F401,F403
 from .graph import (GLOBAL_VARIABLES, LOCAL_VARIABLES, QUEUE_RUNNERS, SUMMARIES, TRAINABLE_VARIABLES, Graph,
                     Operation, Tensor, Variable, get_default_graph, global_variables_initializer,
                     local_variables_initializer, variables_initializer)
+from .partitioned import (PartitionedVariable, fixed_size_partitioner, min_max_variable_partitioner,
+                          shard_across_workers, variable_axis_size_partitioner)
 from .queues import FIFOQueue, RandomShuffleQueue, decode_jpeg, read_file
 from .session import ConfigProto, InteractiveSession, RunMetadata, RunOptions, Session, get_default_session
 from .sparse import SparseTensor, SparseTensorValue, sparse_tensor_to_dense

@@ -328,10 +328,12 @@ class Variable(Tensor):
     the device scope (replica_device_setter records ps/worker placement)."""
 
     def __init__(self, initial_value=None, trainable: bool = True, name: Optional[str] = None,
-                 dtype=None, collections=None, _full_name: Optional[str] = None):
+                 dtype=None, collections=None, _full_name: Optional[str] = None, partitioner=None):
         g = get_default_graph()
         self._init_value = initial_value
         base = _full_name or g.unique_name(name or "Variable")
+        if self._become_partitioned(base, initial_value, trainable, dtype, collections, partitioner):
+            return
         self.fn = None
         self.inputs = []
         self.name = base + ":0"
@@ -350,6 +352,23 @@ class Variable(Tensor):
         for c in cols:
             g.add_to_collection(c, self)
         g._vars_by_name[base] = self
+
+    def _become_partitioned(self, base, iv, trainable, dtype, collections, partitioner) -> bool:
+        from . import partitioned as P
+
+        shape = getattr(iv, "_shape", None)
+        spec = getattr(iv, "_init_spec", None)
+        if shape is None or spec is None or len(shape) not in (1, 2):
+            return False
+        if dtype is not None and dtype not in (float32, torch.float32):
+            return False
+        placement = _current_placement("VariableV2", base, int(np.prod(shape)))
+        on_ps = bool(placement) and "/job:ps" in str(placement)
+        if partitioner is None and not (on_ps and shape[0] >= P.SHARD_MIN_ROWS):
+            return False
+        self.__class__ = P.PartitionedVariable
+        P.PartitionedVariable.__init__(self, base, shape, spec, trainable, collections, partitioner, placement)
+        return True
 
     def _materialize_initial(self) -> torch.Tensor:
         iv = self._init_value
@@ -416,10 +435,19 @@ def _gen(seed):
     return g
 
 
+def _spec(fn, shape, kind, a, b, seed):
+    fn._init_spec = (kind, a, b, seed)
+    fn._shape = tuple(int(s) for s in shape)
+    return fn
+
+
 def random_normal(shape, mean=0.0, stddev=1.0, dtype=float32, seed=None, name="random_normal"):
+    if seed is None:
+        seed = get_default_graph().next_seed()
     gen = _gen(seed)
     shape = tuple(int(s) for s in shape)
-    return lambda: (torch.randn(shape, generator=gen, dtype=torch.float32) * stddev + mean).to(dtype)
+    return _spec(lambda: (torch.randn(shape, generator=gen, dtype=torch.float32) * stddev + mean).to(dtype),
+                 shape, "normal", mean, stddev, seed)
 
 
 def truncated_normal(shape, mean=0.0, stddev=1.0, dtype=float32, seed=None, name="truncated_normal"):
@@ -438,11 +466,11 @@ def truncated_normal(shape, mean=0.0, stddev=1.0, dtype=float32, seed=None, name
 
 
 def zeros(shape, dtype=float32, name="zeros"):
-    return lambda: torch.zeros(tuple(int(s) for s in shape), dtype=dtype)
+    return _spec(lambda: torch.zeros(tuple(int(s) for s in shape), dtype=dtype), shape, "const", 0.0, 0, 0)
 
 
 def ones(shape, dtype=float32, name="ones"):
-    return lambda: torch.ones(tuple(int(s) for s in shape), dtype=dtype)
+    return _spec(lambda: torch.ones(tuple(int(s) for s in shape), dtype=dtype), shape, "const", 1.0, 0, 0)
 
 
 def random_uniform(shape, minval=0.0, maxval=1.0, dtype=float32, seed=None, name="random_uniform"):
@@ -504,10 +532,15 @@ def get_variable(name, shape=None, dtype=float32, initializer=None, trainable=Tr
     init = initializer if initializer is not None else glorot_uniform_initializer()
     shp = tuple(int(s) for s in (shape or ()))
     iv = (lambda: init(shp, dtype)) if callable(init) else init
-    v = Variable(iv, trainable=trainable, dtype=dtype, collections=collections, _full_name=full)
+    if callable(iv):
+        if isinstance(init, random_normal_initializer) and not isinstance(init, truncated_normal_initializer):
+            seed = init.seed if init.seed is not None else g.next_seed()
+            iv = _spec(iv, shp, "normal", init.mean, init.stddev, seed)
+        elif isinstance(init, (constant_initializer, zeros_initializer)):
+            iv = _spec(iv, shp, "const", float(getattr(init, "value", 0.0)), 0, 0)
+    v = Variable(iv, trainable=trainable, dtype=dtype, collections=collections, _full_name=full,
+                 partitioner=partitioner)
     g._names[full] = g._names.get(full, 0) + 1
-    if partitioner is not None:
-        v.partitioner = partitioner
     return v
 
 

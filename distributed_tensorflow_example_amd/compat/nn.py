@@ -68,7 +68,17 @@ def sigmoid_cross_entropy_with_logits(*args, logits=None, labels=None, targets=N
                   name or "SigmoidCrossEntropyWithLogits")
 
 
+def _partitioned(params):
+    return getattr(params, "is_partitioned", False)
+
+
 def embedding_lookup(params, ids, name="embedding_lookup"):
+    if _partitioned(params):
+        from .partitioned import lookup_dense
+
+        t = Tensor(None, [ids], name)
+        t._eval = lambda ctx: lookup_dense(ctx, params, ctx.eval(ids))
+        return t
     return Tensor(lambda w, i: w[i.long()], [params, ids], name)
 
 
@@ -79,6 +89,14 @@ def embedding_lookup_sparse(params, sp_ids, sp_weights, combiner="mean", name="e
     TF's default combiner is "mean", the reference passes combiner='sum'.
     """
     from .sparse import SparseTensor
+
+    if _partitioned(params):
+        from .partitioned import lookup_sparse
+
+        t = Tensor(None, [sp_ids, sp_weights], name)
+        t._eval = lambda ctx: lookup_sparse(ctx, params, ctx.eval(sp_ids),
+                                            ctx.eval(sp_weights) if sp_weights is not None else None, combiner)
+        return t
 
     def f(w, ids_sp, wts_sp):
         offsets, ids, vals = SparseTensor.to_csr(ids_sp, wts_sp)

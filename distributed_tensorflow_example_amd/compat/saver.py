@@ -192,6 +192,9 @@ class Saver:
             return dict(vl)
         out = {}
         for v in vl:
+            if getattr(v, "is_partitioned", False):
+                out[v.part_name] = v            # TF partitioned naming: W/part_k (this rank's shard)
+                continue
             out[v.name[:-2] if v.name.endswith(":0") else v.name] = v
         return out
 
@@ -212,9 +215,22 @@ class Saver:
             step = int(np.asarray(sess.run(step) if hasattr(step, "_eval") else step))
         prefix = f"{save_path}-{int(step)}" if step is not None else save_path
         w = get_world()
-        tensors = {k: self._value(v) for k, v in self._vars().items()}
-        if w.rank == 0:
+        vars_ = self._vars()
+        tensors = {k: self._value(v) for k, v in vars_.items()}
+        if w.world_size > 1 and any(getattr(v, "is_partitioned", False) for v in vars_.values()):
+            # every rank writes its own shard of the partitioned tables in parallel
+            local = {k: t for k, t in tensors.items() if getattr(vars_[k], "is_partitioned", False)}
+            repl = {k: t for k, t in tensors.items() if k not in local}
+            write_bundle(prefix, dict(local, **(repl if w.rank == 0 else {})), shard_id=w.rank,
+                         num_shards=w.world_size)
+            w.barrier()
+            if w.rank == 0:
+                _native.load().bundle_merge_shard_indexes(prefix, w.world_size, True)
+            tensors = repl
+            write_meta_graph = write_meta_graph and w.rank == 0
+        elif w.rank == 0:
             write_bundle(prefix, tensors)
+        if w.rank == 0:
             if write_meta_graph:
                 meta = {k: {"shape": list(t.shape), "dtype": str(t.dtype)} for k, t in tensors.items()}
                 with open(prefix + ".meta.json", "w") as f:
@@ -241,6 +257,11 @@ class Saver:
         idx = read_bundle_index(prefix)
         missing = []
         for name, v in self._vars().items():
+            if getattr(v, "is_partitioned", False):
+                base = v.name[:-2] + "/part_"
+                nparts = sum(1 for k in idx if k.startswith(base))
+                if (name not in idx or nparts != v.world.world_size) and self._restore_resharded(prefix, idx, v):
+                    continue
             if name not in idx:
                 missing.append(name)
                 continue
@@ -254,6 +275,22 @@ class Saver:
                 v.initialized = True
         if missing:
             raise KeyError(f"variables not found in checkpoint {prefix}: {missing}")
+
+    @staticmethod
+    def _restore_resharded(prefix, idx, v) -> bool:
+        """Checkpoint written with K shards, restored on a different world size:
+        row r lived in part_(r % K) at r // K; rebuild and re-slice."""
+        base = v.name[:-2]
+        parts = sorted((int(k.rsplit("_", 1)[1]), k) for k in idx if k.startswith(base + "/part_"))
+        if not parts:
+            return False
+        K = len(parts)
+        full = torch.empty((v.rows, v.dim), dtype=torch.float32)
+        for k, name in parts:
+            full[k::K] = read_tensor(prefix, name).reshape(-1, v.dim)
+        v.table.load_full(full)
+        v.initialized = True
+        return True
 
     def recover_last_checkpoints(self, paths):
         self._kept = [p for p in paths if checkpoint_exists(p)]

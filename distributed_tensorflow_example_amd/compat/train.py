@@ -217,6 +217,10 @@ def global_step(sess, global_step_tensor) -> int:
 
 
 # ======================================================================= gradient sync
+def _is_pv(v) -> bool:
+    return getattr(v, "is_partitioned", False)
+
+
 class _GradSync:
     """Flat-bucket all-reduce (average) of a var_list's gradients across workers."""
 
@@ -246,6 +250,7 @@ class _GradSync:
                     self.flat.copy_(buf)
                 else:
                     w.all_reduce(self.flat, "sum")
+                self.flat.mul_(1.0 / w.world_size)      # mean over workers == global-batch gradient
         return self.views
 
 
@@ -280,6 +285,8 @@ class Optimizer:
         return float(lr)
 
     def compute_gradients(self, loss, var_list=None, **kw):
+        """Dense variables get dense gradients; a PartitionedVariable gets the
+        list of (lookup state, gradient rows) of the run -- TF's IndexedSlices."""
         var_list = list(var_list if var_list is not None else trainable_variables())
         key = id(loss)
 
@@ -287,8 +294,15 @@ class Optimizer:
             st = ctx.state.setdefault("grads", {})
             if key not in st:
                 l = ctx.eval(loss)
-                gs = torch.autograd.grad(l, [v.value for v in var_list], allow_unused=True)
-                st[key] = list(gs)
+                dense = [v for v in var_list if not _is_pv(v)]
+                looks = [(pv, stt) for pv, stt in ctx.state.get("pv_lookups", []) if any(pv is v for v in var_list)]
+                rows = [stt[0] for _, stt in looks]
+                gs = torch.autograd.grad(l, [v.value for v in dense] + rows, allow_unused=True)
+                dg = dict(zip(map(id, dense), gs[:len(dense)]))
+                sparse = {}
+                for (pv, stt), g in zip(looks, gs[len(dense):]):
+                    sparse.setdefault(id(pv), []).append((stt[1], g))
+                st[key] = [sparse.get(id(v), []) if _is_pv(v) else dg[id(v)] for v in var_list]
             return st[key]
         pairs = []
         for i, v in enumerate(var_list):
@@ -299,25 +313,38 @@ class Optimizer:
 
     def apply_gradients(self, grads_and_vars, global_step=None, name=None) -> Operation:
         pairs = list(grads_and_vars)
-        vars_ = [v for _, v in pairs]
-        gtens = [g for g, _ in pairs]
+        dense_pairs = [(g, v) for g, v in pairs if not _is_pv(v)]
+        sparse_pairs = [(g, v) for g, v in pairs if _is_pv(v)]
+        if sparse_pairs and self._kind != "sgd":
+            raise NotImplementedError(f"{type(self).__name__}: partitioned (sharded) variables support "
+                                      "GradientDescentOptimizer only")
+        vars_ = [v for _, v in dense_pairs]
+        gtens = [g for g, _ in dense_pairs]
         opt = self
         params = [v.value for v in vars_]
         # slots exist as soon as the train op does (TF creates them in
         # minimize), so a Saver built afterwards checkpoints/restores them
-        fused = opt._make_fused(params)
-        opt._register_slots(vars_, fused)
-        sync = _GradSync(params, opt.comm_dtype)
+        fused = opt._make_fused(params) if params else None
+        if fused is not None:
+            opt._register_slots(vars_, fused)
+        sync = _GradSync(params, opt.comm_dtype) if params else None
 
         def run(ctx):
-            gs = [ctx.eval(g) if g is not None else None for g in gtens]
-            if opt.sync_replicas:
-                gs = sync(gs)
-            else:
-                gs = [g if g is not None else torch.zeros_like(p) for g, p in zip(gs, params)]
-            if isinstance(opt.learning_rate, Tensor):
-                fused.set_lr(opt._lr_value())
-            fused.step(grads=[g.contiguous() for g in gs])
+            ws = _world_or_local().world_size
+            if fused is not None:
+                gs = [ctx.eval(g) if g is not None else None for g in gtens]
+                if opt.sync_replicas:
+                    gs = sync(gs)
+                else:
+                    gs = [g if g is not None else torch.zeros_like(p) for g, p in zip(gs, params)]
+                if isinstance(opt.learning_rate, Tensor):
+                    fused.set_lr(opt._lr_value())
+                fused.step(grads=[g.contiguous() for g in gs])
+            lr = opt._lr_value()
+            for g, pv in sparse_pairs:      # owner-side scatter SGD, sync-average folded in
+                for lctx, rows_grad in ctx.eval(g):
+                    pv.table.apply_sgd(lctx, rows_grad if rows_grad is not None else
+                                       torch.zeros((lctx.uniq.numel(), pv.dim), device=pv.table.device), lr / ws)
             if global_step is not None:
                 with torch.no_grad():
                     global_step.value.data += 1
@@ -364,6 +391,7 @@ class GradientDescentOptimizer(Optimizer):
 
 
 class MomentumOptimizer(Optimizer):
+    _kind = "momentum"
     _slot_names = ("Momentum",)
 
     def __init__(self, learning_rate, momentum, use_locking=False, name="Momentum", use_nesterov=False):
@@ -375,6 +403,7 @@ class MomentumOptimizer(Optimizer):
 
 
 class AdamOptimizer(Optimizer):
+    _kind = "adam"
     _slot_names = ("Adam", "Adam_1")
 
     def __init__(self, learning_rate=0.001, beta1=0.9, beta2=0.999, epsilon=1e-8, use_locking=False,
@@ -416,6 +445,7 @@ class _PowerVariable:
 
 
 class AdagradOptimizer(Optimizer):
+    _kind = "adagrad"
     _slot_names = ("Adagrad",)
 
     def __init__(self, learning_rate, initial_accumulator_value=0.1, use_locking=False, name="Adagrad"):
@@ -427,6 +457,7 @@ class AdagradOptimizer(Optimizer):
 
 
 class RMSPropOptimizer(Optimizer):
+    _kind = "rmsprop"
     _slot_names = ("RMSProp", "Momentum")
 
     def __init__(self, learning_rate, decay=0.9, momentum=0.0, epsilon=1e-10, use_locking=False,
@@ -529,8 +560,13 @@ def _init_or_restore(sess, is_chief, init_op, local_init_op, init_fn, checkpoint
                     v._initialize()
             if init_fn is not None:
                 init_fn(sess)
-    # non-chief workers receive the chief's values (no re-initialisation race)
-    _broadcast_variables([v for v in global_variables() if isinstance(v, Variable)])
+    # non-chief workers receive the chief's values (no re-initialisation race);
+    # sharded (partitioned) variables are owned per rank: each initialises its shard
+    if restored is None and not is_chief:
+        for v in global_variables():
+            if _is_pv(v):
+                v._initialize()
+    _broadcast_variables([v for v in global_variables() if isinstance(v, Variable) and not _is_pv(v)])
     for v in global_variables():
         if isinstance(v, Variable):
             v.initialized = True

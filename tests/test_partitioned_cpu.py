@@ -1,0 +1,117 @@
+"""replica_device_setter path for big tables: a ps-placed tf.Variable becomes
+a row-sharded PartitionedVariable; lr2.py's graph trains identically on 1
+and 2 gloo workers; checkpoints carry W/part_k and re-shard on restore."""
+import os
+import socket
+import sys
+
+import numpy as np
+import torch.multiprocessing as mp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+F = 4000
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _graph(tf):
+    with tf.device(tf.train.replica_device_setter(ps_tasks=1)):
+        gs = tf.get_variable("global_step", [], initializer=tf.constant_initializer(0), trainable=False)
+        with tf.name_scope("input"):
+            shp, idx = tf.placeholder(tf.int64), tf.placeholder(tf.int64)
+            fid, fv = tf.placeholder(tf.int64), tf.placeholder(tf.float32)
+            y = tf.placeholder(tf.float32, [None, 1])
+            sp_f = tf.SparseTensor(shape=shp, indices=idx, values=fid)
+            sp_v = tf.SparseTensor(shape=shp, indices=idx, values=fv)
+        with tf.name_scope("weights"):
+            W = tf.Variable(tf.random_normal([F, 1]))
+        with tf.name_scope("bias"):
+            b = tf.Variable(tf.zeros([1]))
+        with tf.name_scope("loss"):
+            py_x = tf.add(tf.nn.embedding_lookup_sparse(W, sp_f, sp_v, combiner="sum"), b)
+            ce = tf.reduce_mean(tf.nn.sigmoid_cross_entropy_with_logits(py_x, y))
+        train = tf.train.GradientDescentOptimizer(0.5).minimize(ce, global_step=gs)
+    return dict(gs=gs, shp=shp, idx=idx, fid=fid, fv=fv, y=y, W=W, b=b, train=train)
+
+
+def _feed(g, batch):
+    labels, fids, fvals, sp_indices, n = batch.as_tf_feed()
+    return {g["y"]: labels, g["shp"]: np.array([F, n]), g["idx"]: sp_indices, g["fid"]: fids, g["fv"]: fvals}
+
+
+def _worker(rank, ws, port, q, files, ckdir):
+    try:
+        sys.path.insert(0, REPO)
+        os.environ.update(RANK=str(rank), WORLD_SIZE=str(ws), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                          MASTER_PORT=str(port), DTF_SHARD_MIN_ROWS="1000")
+        import distributed_tensorflow_example_amd.compat as tf
+        from distributed_tensorflow_example_amd.data import libsvm
+        from distributed_tensorflow_example_amd.parallel import world as Wm
+
+        w = Wm.init(backend="gloo")
+        data = libsvm.load_files(files)
+        tf.set_random_seed(7)
+        g = _graph(tf)
+        assert type(g["W"]).__name__ == "PartitionedVariable"
+        sv = tf.train.Supervisor(is_chief=(rank == 0), global_step=g["gs"], init_op=tf.global_variables_initializer())
+        with sv.prepare_or_wait_for_session() as sess:
+            for s in range(6):
+                rows = np.arange(s * 200, (s + 1) * 200)[rank * 200 // ws:(rank + 1) * 200 // ws]
+                sess.run(g["train"], feed_dict=_feed(g, data.take(rows)))
+            full = g["W"].numpy().copy()
+            bias = sess.run(g["b"]).copy()
+            path = tf.train.Saver().save(sess, os.path.join(ckdir, f"ws{ws}", "m"), global_step=g["gs"])
+            step = float(sess.run(g["gs"]))
+        q.put((rank, full, bias, path, step))
+    except Exception:
+        import traceback
+
+        q.put((rank, traceback.format_exc(), None, None, None))
+
+
+def _run(ws, files, ckdir):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, ws, port, q, files, ckdir)) for r in range(ws)]
+    [p.start() for p in ps]
+    out = sorted([q.get(timeout=240) for _ in range(ws)], key=lambda r: r[0])
+    [p.join(60) for p in ps]
+    for r in out:
+        assert not isinstance(r[1], str), r[1]
+    return out
+
+
+def test_partitioned_variable_sync_workers(tmp_path):
+    sys.path.insert(0, REPO)
+    os.environ["DTF_SHARD_MIN_ROWS"] = "1000"
+    from distributed_tensorflow_example_amd.data import libsvm
+
+    files = libsvm.write_synthetic(str(tmp_path / "p"), 1, 1200, F, 10, seed=4)
+    one = _run(1, files, str(tmp_path))
+    two = _run(2, files, str(tmp_path))
+    assert np.array_equal(two[0][1], two[1][1]) and np.array_equal(two[0][2], two[1][2])
+    assert np.allclose(one[0][1], two[0][1], atol=1e-6)
+    assert np.allclose(one[0][2], two[0][2], atol=1e-6)
+    assert one[0][4] == two[0][4] == 6.0
+    # 2-shard checkpoint restored into a 1-worker graph (re-sharding)
+    import distributed_tensorflow_example_amd.compat as tf
+    from distributed_tensorflow_example_amd.parallel import world as Wm
+
+    Wm.reset()
+    idx = tf.train.list_variables(os.path.dirname(two[0][3]))
+    names = dict(idx)
+    assert names["weights/Variable/part_0"] == [F // 2, 1] and names["weights/Variable/part_1"] == [F // 2, 1]
+    tf.reset_default_graph()
+    g = _graph(tf)
+    with tf.Session() as sess:
+        tf.train.Saver().restore(sess, two[0][3])
+        assert np.allclose(g["W"].numpy(), two[0][1])
+        assert float(sess.run(g["gs"])) == 6.0
+    tf.reset_default_graph()

@@ -344,7 +344,8 @@ class Variable(Tensor):
             init = init.to(dtype)
         self.dtype = init.dtype
         self.shape = tuple(init.shape)
-        self.placement = _current_placement("VariableV2", base, init.numel())
+        cached = self.__dict__.pop("_placement_cache", None)
+        self.placement = cached[0] if cached else _current_placement("VariableV2", base, init.numel())
         self.value = torch.nn.Parameter(init.to(g.device).clone(), requires_grad=trainable and init.is_floating_point())
         self.initialized = False
         self.initializer = Operation(lambda: self._initialize(), [], base + "/Assign")
@@ -363,8 +364,9 @@ class Variable(Tensor):
         if dtype is not None and dtype not in (float32, torch.float32):
             return False
         placement = _current_placement("VariableV2", base, int(np.prod(shape)))
+        self._placement_cache = (placement,)
         on_ps = bool(placement) and "/job:ps" in str(placement)
-        if partitioner is None and not (on_ps and shape[0] >= P.SHARD_MIN_ROWS):
+        if partitioner is None and not (on_ps and shape[0] >= P.shard_min_rows()):
             return False
         self.__class__ = P.PartitionedVariable
         P.PartitionedVariable.__init__(self, base, shape, spec, trainable, collections, partitioner, placement)

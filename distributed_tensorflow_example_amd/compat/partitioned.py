@@ -33,7 +33,8 @@ from ..parallel import world as _worldmod
 from ..parallel.sharded_embedding import ShardedEmbedding
 from .graph import (GLOBAL_VARIABLES, TRAINABLE_VARIABLES, RunContext, Tensor, Variable, get_default_graph)
 
-SHARD_MIN_ROWS = int(os.environ.get("DTF_SHARD_MIN_ROWS", 1 << 20))
+def shard_min_rows() -> int:
+    return int(os.environ.get("DTF_SHARD_MIN_ROWS", 1 << 20))
 
 
 class _Partitioner:

@@ -12,6 +12,7 @@ void init_store(py::module& m);
 void init_queue(py::module& m);
 void init_libsvm(py::module& m);
 void init_ops(py::module& m);
+void init_transformer(py::module& m);
 }  // namespace dtf
 
 PYBIND11_MODULE(_C, m) {
@@ -25,4 +26,5 @@ PYBIND11_MODULE(_C, m) {
   dtf::init_queue(m);
   dtf::init_libsvm(m);
   dtf::init_ops(m);
+  dtf::init_transformer(m);
 }

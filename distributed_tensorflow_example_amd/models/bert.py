@@ -1,0 +1,155 @@
+"""BERT-base masked-LM pretraining model (BASELINE config #4).
+
+Not in the reference (SURVEY s2.7 lists it as a BASELINE extension); built on
+the same runtime: fp32 master weights, bf16 activations, hipBLASLt for the
+plain GEMMs and the framework's fused HIP kernels for everything around them:
+
+  embeddings   word + position + type (fp32 sum) -> LN + dropout      (_EmbLN)
+  attention    QKV one GEMM -> Q.K^T batched GEMM -> scale+mask+softmax
+               +prob-dropout (one kernel) -> P.V -> out GEMM ->
+               bias+dropout+residual+LN (one kernel)
+  FFN          GEMM -> bias+GELU (one kernel) -> GEMM -> bias+dropout+residual+LN
+  MLM head     only the masked positions (~15%): dense -> bias+GELU -> LN ->
+               tied-decoder GEMM -> fused softmax-xent kernel
+
+Data parallelism: parallel.ddp.DistributedDataParallel -- gradient-as-bucket
+views, buckets launched on a comm stream as soon as backward fills them
+(RCCL over xGMI overlapped with the remaining backward).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+from ..ops import transformer as T
+
+
+@dataclass
+class BertConfig:
+    vocab_size: int = 30522
+    hidden: int = 768
+    layers: int = 12
+    heads: int = 12
+    intermediate: int = 3072
+    max_position: int = 512
+    type_vocab: int = 2
+    dropout: float = 0.1
+    attn_dropout: float = 0.1
+    ln_eps: float = 1e-12
+    init_std: float = 0.02
+
+    @staticmethod
+    def base():
+        return BertConfig()
+
+    @staticmethod
+    def tiny():
+        return BertConfig(vocab_size=1024, hidden=256, layers=2, heads=4, intermediate=1024, max_position=128)
+
+
+def _lin(o, i, std):
+    return torch.nn.Parameter(torch.randn(o, i) * std)
+
+
+def _mm(x, w):
+    """x [.., in] @ w[out, in]^T in the activation dtype (bf16 on GPU)."""
+    return F.linear(x, w.to(x.dtype))
+
+
+class BertLayer(torch.nn.Module):
+    def __init__(self, c: BertConfig):
+        super().__init__()
+        h, f, s = c.hidden, c.intermediate, c.init_std
+        self.c = c
+        self.w_qkv = _lin(3 * h, h, s)
+        self.b_qkv = torch.nn.Parameter(torch.zeros(3 * h))
+        self.w_o = _lin(h, h, s)
+        self.b_o = torch.nn.Parameter(torch.zeros(h))
+        self.ln1_g = torch.nn.Parameter(torch.ones(h))
+        self.ln1_b = torch.nn.Parameter(torch.zeros(h))
+        self.w_1 = _lin(f, h, s)
+        self.b_1 = torch.nn.Parameter(torch.zeros(f))
+        self.w_2 = _lin(h, f, s)
+        self.b_2 = torch.nn.Parameter(torch.zeros(h))
+        self.ln2_g = torch.nn.Parameter(torch.ones(h))
+        self.ln2_b = torch.nn.Parameter(torch.zeros(h))
+
+    def forward(self, x, mask):
+        c = self.c
+        B, S, H = x.shape
+        nh, d = c.heads, H // c.heads
+        qkv = (_mm(x, self.w_qkv) + self.b_qkv.to(x.dtype)).view(B, S, 3, nh, d)
+        q = qkv[:, :, 0].permute(0, 2, 1, 3)
+        k = qkv[:, :, 1].permute(0, 2, 3, 1)
+        v = qkv[:, :, 2].permute(0, 2, 1, 3)
+        scores = torch.matmul(q, k)                                   # [B, nh, S, S]
+        probs = T.attention_softmax(scores, mask, 1.0 / math.sqrt(d), c.attn_dropout, self.training)
+        ctx = torch.matmul(probs.to(v.dtype), v).permute(0, 2, 1, 3).reshape(B, S, H)
+        a = T.bias_dropout_residual_layernorm(_mm(ctx, self.w_o), self.b_o, x, self.ln1_g, self.ln1_b,
+                                              c.dropout, c.ln_eps, self.training)
+        hmid = T.bias_gelu(_mm(a, self.w_1), self.b_1)
+        out = T.bias_dropout_residual_layernorm(_mm(hmid, self.w_2), self.b_2, a, self.ln2_g, self.ln2_b,
+                                                c.dropout, c.ln_eps, self.training)
+        return out
+
+
+class BertForMLM(torch.nn.Module):
+    def __init__(self, c: BertConfig = None, seed: int = 0):
+        super().__init__()
+        c = c or BertConfig.base()
+        self.c = c
+        g = torch.random.fork_rng(devices=[])
+        with g:
+            torch.manual_seed(seed)
+            s = c.init_std
+            self.word = torch.nn.Parameter(torch.randn(c.vocab_size, c.hidden) * s)
+            self.pos = torch.nn.Parameter(torch.randn(c.max_position, c.hidden) * s)
+            self.typ = torch.nn.Parameter(torch.randn(c.type_vocab, c.hidden) * s)
+            self.emb_g = torch.nn.Parameter(torch.ones(c.hidden))
+            self.emb_b = torch.nn.Parameter(torch.zeros(c.hidden))
+            self.layers = torch.nn.ModuleList([BertLayer(c) for _ in range(c.layers)])
+            self.head_w = _lin(c.hidden, c.hidden, s)
+            self.head_b = torch.nn.Parameter(torch.zeros(c.hidden))
+            self.head_g = torch.nn.Parameter(torch.ones(c.hidden))
+            self.head_beta = torch.nn.Parameter(torch.zeros(c.hidden))
+            self.dec_b = torch.nn.Parameter(torch.zeros(c.vocab_size))
+
+    def forward(self, input_ids, token_type, attn_mask, mlm_positions, mlm_labels):
+        """Returns the mean MLM loss over the masked positions.
+
+        input_ids/token_type [B, S] int64; attn_mask [B, S] (1 keep, 0 pad);
+        mlm_positions [M] flat indices into B*S; mlm_labels [M] int64."""
+        c = self.c
+        B, S = input_ids.shape
+        emb = self.word[input_ids] + self.pos[:S].unsqueeze(0) + self.typ[token_type]
+        x = T.layernorm_dropout(emb, self.emb_g, self.emb_b, c.dropout, c.ln_eps, self.training)
+        act = torch.bfloat16 if x.is_cuda else torch.float32
+        x = x.to(act)
+        add_mask = (1.0 - attn_mask.float()) * -10000.0
+        for layer in self.layers:
+            x = layer(x, add_mask)
+        h = x.reshape(B * S, c.hidden).index_select(0, mlm_positions)
+        h = T.bias_gelu(_mm(h, self.head_w), self.head_b)
+        zero = torch.zeros(c.hidden, device=h.device)
+        h = T.bias_dropout_residual_layernorm(h, zero, None, self.head_g, self.head_beta, 0.0, c.ln_eps,
+                                              self.training)
+        logits = (_mm(h, self.word) + self.dec_b.to(h.dtype)).float()
+        return ops.softmax_xent(logits, mlm_labels)
+
+
+def synthetic_mlm_batch(batch: int, seq: int, vocab: int, device, mask_prob: float = 0.15, seed: int = 0):
+    """Random token ids with 15% MLM positions (fixed count per batch)."""
+    g = torch.Generator().manual_seed(seed)
+    ids = torch.randint(0, vocab, (batch, seq), generator=g)
+    typ = torch.zeros(batch, seq, dtype=torch.int64)
+    typ[:, seq // 2:] = 1
+    am = torch.ones(batch, seq, dtype=torch.int64)
+    m = max(1, int(round(batch * seq * mask_prob)))
+    pos = torch.randperm(batch * seq, generator=g)[:m].sort().values
+    labels = ids.reshape(-1)[pos].clone()
+    ids.view(-1)[pos] = 103 % vocab                                  # [MASK]
+    return tuple(t.to(device) for t in (ids, typ, am, pos, labels))

@@ -1,0 +1,77 @@
+"""ResNet-50 (v1.5) on synthetic ImageNet-shaped input (BASELINE config #3).
+
+Not in the reference.  MI355X layout: channels_last (NHWC)
+bf16 activations so MIOpen picks its implicit-GEMM MFMA convolutions, fp32
+master weights updated by the fused multi-tensor momentum kernel, the loss
+by the fused softmax-xent kernel, and gradients averaged by the bucketed
+DDP all-reduce overlapped with backward (parallel.ddp).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import ops
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, cin, width, stride=1, down=False):
+        super().__init__()
+        cout = width * 4
+        self.conv1 = nn.Conv2d(cin, width, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(width)
+        self.conv2 = nn.Conv2d(width, width, 3, stride, 1, bias=False)   # v1.5: stride on the 3x3
+        self.bn2 = nn.BatchNorm2d(width)
+        self.conv3 = nn.Conv2d(width, cout, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(cout)
+        nn.init.zeros_(self.bn3.weight)                                  # zero-init last BN gamma
+        self.down = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False), nn.BatchNorm2d(cout)) if down else None
+
+    def forward(self, x):
+        idt = self.down(x) if self.down is not None else x
+        y = F.relu(self.bn1(self.conv1(x)), inplace=True)
+        y = F.relu(self.bn2(self.conv2(y)), inplace=True)
+        y = self.bn3(self.conv3(y))
+        return F.relu(y + idt, inplace=True)
+
+
+class ResNet(nn.Module):
+    def __init__(self, layers=(3, 4, 6, 3), num_classes=1000):
+        super().__init__()
+        self.conv1 = nn.Conv2d(3, 64, 7, 2, 3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        blocks, cin = [], 64
+        for i, (n, w) in enumerate(zip(layers, (64, 128, 256, 512))):
+            for j in range(n):
+                blocks.append(Bottleneck(cin, w, stride=(2 if (i > 0 and j == 0) else 1), down=(j == 0)))
+                cin = w * 4
+        self.blocks = nn.Sequential(*blocks)
+        self.fc = nn.Linear(cin, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+
+    def forward(self, x):
+        with torch.autocast(device_type="cuda", dtype=torch.bfloat16, enabled=x.is_cuda):
+            x = F.relu(self.bn1(self.conv1(x)), inplace=True)
+            x = F.max_pool2d(x, 3, 2, 1)
+            x = self.blocks(x)
+            x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
+            return self.fc(x)
+
+    def loss(self, images, labels):
+        return ops.softmax_xent(self.forward(images).float(), labels)
+
+
+def resnet50(num_classes: int = 1000) -> ResNet:
+    return ResNet((3, 4, 6, 3), num_classes)
+
+
+def synthetic_imagenet_batch(batch: int, device, seed: int = 0, size: int = 224, num_classes: int = 1000):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(batch, 3, size, size, generator=g).to(device).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, num_classes, (batch,), generator=g).to(device)
+    return x, y

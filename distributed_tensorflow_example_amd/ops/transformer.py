@@ -1,0 +1,208 @@
+"""Autograd wrappers for the fused transformer kernels (csrc/kernels/transformer.hip).
+
+GPU tensors run the HIP kernels (bf16 activations, fp32 statistics and
+parameters); CPU tensors run an equivalent PyTorch formulation -- the
+numerics oracle for the GPU tests (dropout p = 0 there; the GPU dropout mask
+is a counter hash of (seed, element index) regenerated in backward).
+"""
+from __future__ import annotations
+
+import itertools
+import math
+from typing import Optional
+
+import torch
+
+from .. import _native
+
+_seed_counter = itertools.count(1)
+_BASE_SEED = 0x5EED
+
+
+def next_seed() -> int:
+    return (_BASE_SEED * 1000003 + next(_seed_counter) * 0x9E3779B1) & ((1 << 62) - 1)
+
+
+def set_dropout_seed(seed: int):
+    global _seed_counter, _BASE_SEED
+    _BASE_SEED = int(seed)
+    _seed_counter = itertools.count(1)
+
+
+def _C():
+    return _native.load()
+
+
+def _ln_part(N: int, H: int, device) -> torch.Tensor:
+    grid = max(1, min(512, (N + 3) // 4))
+    return torch.empty(3 * grid * H, dtype=torch.float32, device=device)
+
+
+# ---------------------------------------------------------------- bias + dropout + residual + LN
+class _BDRLN(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, bias, res, gamma, beta, p, eps):
+        C = _C()
+        H = x.shape[-1]
+        x2 = x.reshape(-1, H).contiguous()
+        N = x2.shape[0]
+        y = torch.empty_like(x2)
+        s = torch.empty_like(x2)
+        mean = torch.empty(N, dtype=torch.float32, device=x.device)
+        rstd = torch.empty_like(mean)
+        seed = next_seed() if p > 0 else 0
+        r2 = res.reshape(-1, H).contiguous() if res is not None else None
+        C.bdrln_fwd(x2, bias, r2, gamma, beta, y, s, mean, rstd, eps, p, seed)
+        ctx.save_for_backward(s, mean, rstd, gamma)
+        ctx.p, ctx.seed, ctx.has_res, ctx.shape = p, seed, res is not None, x.shape
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = _C()
+        s, mean, rstd, gamma = ctx.saved_tensors
+        H = s.shape[-1]
+        dy2 = dy.reshape(-1, H).to(torch.bfloat16).contiguous()
+        N = dy2.shape[0]
+        ds = torch.empty_like(dy2)
+        dxb = torch.empty_like(dy2)
+        dgamma = torch.empty(H, dtype=torch.float32, device=dy.device)
+        dbeta = torch.empty_like(dgamma)
+        dbias = torch.empty_like(dgamma)
+        C.ln_bwd(dy2, s, mean, rstd, gamma, ds, dxb, _ln_part(N, H, dy.device), dgamma, dbeta, dbias, ctx.p, ctx.seed)
+        dres = ds.view(ctx.shape) if ctx.has_res else None
+        return dxb.view(ctx.shape), dbias, dres, dgamma, dbeta, None, None
+
+
+def bias_dropout_residual_layernorm(x, bias, residual, gamma, beta, p: float = 0.0, eps: float = 1e-12,
+                                   training: bool = True):
+    """LayerNorm(dropout(x + bias) + residual) -- the post-sublayer epilogue."""
+    p = p if training else 0.0
+    if not x.is_cuda:
+        t = x.float() + bias
+        if p > 0:
+            t = torch.nn.functional.dropout(t, p, True)
+        if residual is not None:
+            t = t + residual.float()
+        return torch.nn.functional.layer_norm(t, (t.shape[-1],), gamma, beta, eps)
+    return _BDRLN.apply(x.to(torch.bfloat16), bias, None if residual is None else residual.to(torch.bfloat16),
+                        gamma, beta, float(p), float(eps))
+
+
+class _EmbLN(torch.autograd.Function):
+    """y = dropout(LayerNorm(x)); x fp32 (summed embeddings), y bf16."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, p, eps):
+        C = _C()
+        H = x.shape[-1]
+        x2 = x.reshape(-1, H).contiguous().float()
+        N = x2.shape[0]
+        y = torch.empty(x2.shape, dtype=torch.bfloat16, device=x.device)
+        s = torch.empty_like(y)
+        mean = torch.empty(N, dtype=torch.float32, device=x.device)
+        rstd = torch.empty_like(mean)
+        seed = next_seed() if p > 0 else 0
+        C.ln_fwd_f32in(x2, gamma, beta, y, s, mean, rstd, eps, p, seed)
+        ctx.save_for_backward(s, mean, rstd, gamma)
+        ctx.p, ctx.seed, ctx.shape = p, seed, x.shape
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = _C()
+        s, mean, rstd, gamma = ctx.saved_tensors
+        H = s.shape[-1]
+        dy2 = dy.reshape(-1, H).to(torch.bfloat16).contiguous()
+        if ctx.p > 0:
+            dyd = torch.empty_like(dy2)
+            C.dropout_bf16(dy2, dyd, ctx.p, ctx.seed)
+            dy2 = dyd
+        N = dy2.shape[0]
+        ds = torch.empty_like(dy2)
+        dgamma = torch.empty(H, dtype=torch.float32, device=dy.device)
+        dbeta = torch.empty_like(dgamma)
+        C.ln_bwd(dy2, s, mean, rstd, gamma, ds, None, _ln_part(N, H, dy.device), dgamma, dbeta, None, 0.0, 0)
+        return ds.float().view(ctx.shape), dgamma, dbeta, None, None
+
+
+def layernorm_dropout(x, gamma, beta, p: float = 0.0, eps: float = 1e-12, training: bool = True):
+    p = p if training else 0.0
+    if not x.is_cuda:
+        y = torch.nn.functional.layer_norm(x.float(), (x.shape[-1],), gamma, beta, eps)
+        return torch.nn.functional.dropout(y, p, True) if p > 0 else y
+    return _EmbLN.apply(x, gamma, beta, float(p), float(eps))
+
+
+# ---------------------------------------------------------------- bias + GELU
+class _BiasGelu(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, bias):
+        C = _C()
+        x2 = x.contiguous()
+        y = torch.empty_like(x2)
+        C.bias_gelu_fwd(x2, bias, y)
+        ctx.save_for_backward(x2, bias)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = _C()
+        x, bias = ctx.saved_tensors
+        H = x.shape[-1]
+        N = x.numel() // H
+        dx = torch.empty_like(x)
+        slices = max(1, min(256, N // 16))
+        part = torch.empty(slices * H, dtype=torch.float32, device=x.device)
+        dbias = torch.empty(H, dtype=torch.float32, device=x.device)
+        C.bias_gelu_bwd(dy.to(torch.bfloat16).contiguous(), x, bias, dx, part, dbias)
+        return dx, dbias
+
+
+def bias_gelu(x, bias):
+    if not x.is_cuda:
+        return torch.nn.functional.gelu(x.float() + bias)
+    return _BiasGelu.apply(x.to(torch.bfloat16), bias)
+
+
+# ---------------------------------------------------------------- attention softmax
+class _AttnSoftmax(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, scores, mask, scale, p, rows_per_batch):
+        C = _C()
+        S = scores.contiguous()
+        P = torch.empty_like(S)
+        Pd = torch.empty_like(S) if p > 0 else None
+        seed = next_seed() if p > 0 else 0
+        C.softmax_fwd(S, mask, P, Pd, rows_per_batch, scale, p, seed)
+        ctx.save_for_backward(P)
+        ctx.scale, ctx.p, ctx.seed = scale, p, seed
+        return Pd if Pd is not None else P
+
+    @staticmethod
+    def backward(ctx, dPd):
+        C = _C()
+        (P,) = ctx.saved_tensors
+        dS = torch.empty_like(P)
+        C.softmax_bwd(dPd.to(torch.bfloat16).contiguous(), P, dS, ctx.scale, ctx.p, ctx.seed)
+        return dS, None, None, None, None
+
+
+def attention_softmax(scores, mask: Optional[torch.Tensor], scale: float, p: float = 0.0, training: bool = True):
+    """softmax(scale * scores + mask) with fused prob-dropout.
+
+    scores [B, heads, Sq, Sk] (bf16 on GPU); mask [B, Sk] additive fp32 or None."""
+    p = p if training else 0.0
+    B, Hh, Sq, Sk = scores.shape
+    if not scores.is_cuda:
+        z = scores.float() * scale
+        if mask is not None:
+            z = z + mask.float()[:, None, None, :]
+        pr = torch.softmax(z, -1)
+        return torch.nn.functional.dropout(pr, p, True) if p > 0 else pr
+    m = mask.float().contiguous() if mask is not None else None
+    return _AttnSoftmax.apply(scores.to(torch.bfloat16), m, float(scale), float(p), Hh * Sq)
+
+
+def gelu_ref(x):
+    return 0.5 * x * (1.0 + torch.erf(x / math.sqrt(2.0)))

@@ -37,10 +37,12 @@ def synthetic_sparse_batches(n_batches, batch, num_features, nnz, seed, device):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--model", choices=["wide_deep", "sparse_lr"], default="wide_deep")
+    ap.add_argument("--model", choices=["wide_deep", "sparse_lr", "bert_base", "resnet50"], default="wide_deep")
+    ap.add_argument("--seq", type=int, default=128)
+    ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=4096, help="per-GPU batch")
+    ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (0 = model default)")
     ap.add_argument("--features", type=int, default=100_000_000, help="table rows (sharded)")
     ap.add_argument("--emb-dim", type=int, default=64)
     ap.add_argument("--nnz", type=int, default=32, help="features per sample")
@@ -51,6 +53,9 @@ def main():
 
     w = W.init()
     dev = w.device
+    if a.model in ("bert_base", "resnet50"):
+        return dense_bench(a, w)
+    a.batch = a.batch or 4096
     if a.model == "wide_deep":
         from distributed_tensorflow_example_amd.models.wide_deep import WideDeep
 
@@ -85,6 +90,71 @@ def main():
                           "ms_per_step": round(dt / a.steps * 1e3, 4), "higher_is_better": True,
                           "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic zipf ids",
                           "config": cfg, "final_loss": float(loss)}), flush=True)
+    w.shutdown()
+
+
+def dense_bench(a, w):
+    """BERT-base MLM / ResNet-50 with bucketed DDP (comm overlapped with backward)."""
+    from distributed_tensorflow_example_amd import optim
+    from distributed_tensorflow_example_amd.parallel.ddp import DistributedDataParallel
+
+    dev = w.device
+    if a.model == "bert_base":
+        from distributed_tensorflow_example_amd.models.bert import BertConfig, BertForMLM, synthetic_mlm_batch
+
+        a.batch = a.batch or 32
+        model = BertForMLM(BertConfig.base(), seed=0).to(dev)
+        batches = [synthetic_mlm_batch(a.batch, a.seq, 30522, dev, seed=w.rank * 100 + i) for i in range(4)]
+        opt = optim.FusedAdamW(list(model.parameters()), 1e-4, weight_decay=0.01)
+        unit, per = "sequences/s", a.batch
+        cfg = {"model": "bert-base-uncased MLM (110M)", "global_batch": a.batch * w.world_size,
+               "per_gpu_batch": a.batch, "seq_len": a.seq, "parallelism": f"dp{w.world_size}",
+               "optimizer": "adamw", "grad_allreduce": f"bucketed {a.bucket_mb}MB, overlapped"}
+        run = lambda m, b: m(*b)
+    else:
+        from distributed_tensorflow_example_amd.models.resnet import resnet50, synthetic_imagenet_batch
+
+        a.batch = a.batch or 128
+        model = resnet50().to(dev).to(memory_format=torch.channels_last)
+        batches = [synthetic_imagenet_batch(a.batch, dev, seed=w.rank * 100 + i) for i in range(2)]
+        opt = optim.FusedMomentum(list(model.parameters()), 0.1, 0.9, weight_decay=1e-4)
+        unit, per = "images/s", a.batch
+        cfg = {"model": "resnet50 (25.6M)", "global_batch": a.batch * w.world_size, "per_gpu_batch": a.batch,
+               "seq_len": None, "parallelism": f"dp{w.world_size}", "optimizer": "sgd-momentum",
+               "grad_allreduce": f"bucketed {a.bucket_mb}MB, overlapped", "input": "224x224 synthetic, channels_last"}
+        run = lambda m, b: m.loss(*b)
+    ddp = DistributedDataParallel(model, w, bucket_mb=a.bucket_mb)
+
+    def step(b):
+        ddp.zero_grad()
+        ddp._launched.clear()
+        for bk in ddp.buckets:
+            bk.ready = 0
+        loss = run(model, b)
+        loss.backward()
+        ddp.finish_gradient_synchronization()
+        opt.step()
+        return loss
+
+    for i in range(a.warmup):
+        step(batches[i % len(batches)])
+    w.barrier()
+    torch.cuda.synchronize()
+    t0 = time.time()
+    for i in range(a.steps):
+        loss = step(batches[i % len(batches)])
+    torch.cuda.synchronize()
+    w.barrier()
+    dt = w.host_all_reduce(time.time() - t0, "max")
+    v = per * w.world_size * a.steps / dt
+    if w.rank == 0:
+        out = {"metric": f"{a.model} {unit} (whole node)", "value": round(v, 2), "unit": unit,
+               "n_gpus": w.world_size, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 3),
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+               "data": "synthetic", "config": cfg, "final_loss": float(loss)}
+        if a.model == "bert_base":
+            out["tokens_per_s"] = round(v * a.seq, 1)
+        print(json.dumps(out), flush=True)
     w.shutdown()
 
 

@@ -1,0 +1,142 @@
+"""Fused transformer kernels vs PyTorch fp32 references, and a BERT step on GPU."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return float((a - b).norm() / b.norm().clamp_min(1e-12))
+
+
+@pytest.mark.parametrize("H", [256, 768, 1024, 3072])
+@pytest.mark.parametrize("with_res", [True, False])
+def test_bias_dropout_residual_layernorm_p0(native, H, with_res):
+    from distributed_tensorflow_example_amd.ops import transformer as T
+    torch.manual_seed(H)
+    N = 333
+    x = torch.randn(N, H).bfloat16()
+    r = torch.randn(N, H).bfloat16() if with_res else None
+    bias, g, b = torch.randn(H) * 0.1, 1 + 0.1 * torch.randn(H), 0.1 * torch.randn(H)
+    xs = [t.float().clone().requires_grad_() if t is not None else None for t in (x, r)]
+    ps = [t.clone().requires_grad_() for t in (bias, g, b)]
+    ref = T.bias_dropout_residual_layernorm(xs[0], ps[0], xs[1], ps[1], ps[2], 0.0, 1e-12)
+    dy = torch.randn(N, H)
+    ref.backward(dy)
+    xg = x.cuda().requires_grad_()
+    rg = r.cuda().requires_grad_() if r is not None else None
+    pg = [t.cuda().requires_grad_() for t in (bias, g, b)]
+    out = T.bias_dropout_residual_layernorm(xg, pg[0], rg, pg[1], pg[2], 0.0, 1e-12)
+    out.backward(dy.cuda().bfloat16())
+    assert rel(out, ref) < 1e-2
+    assert rel(xg.grad, xs[0].grad) < 2e-2
+    if r is not None:
+        assert rel(rg.grad, xs[1].grad) < 2e-2
+    for a, b_ in zip(pg, ps):
+        assert rel(a.grad, b_.grad) < 2e-2
+
+
+def test_bdrln_dropout_mask_consistency(native):
+    """With p > 0: kept fraction ~ 1-p and backward uses exactly the forward mask."""
+    from distributed_tensorflow_example_amd.ops import transformer as T
+    N, H, p = 512, 768, 0.25
+    x = torch.randn(N, H, device="cuda").bfloat16().requires_grad_()
+    bias = torch.zeros(H, device="cuda", requires_grad=True)
+    g, b = torch.ones(H, device="cuda"), torch.zeros(H, device="cuda")
+    out = T.bias_dropout_residual_layernorm(x, bias, None, g, b, p, 1e-12)
+    out.backward(torch.ones_like(out))
+    # dropped elements receive exactly zero gradient
+    zero_grad = (x.grad == 0).float().mean().item()
+    assert abs(zero_grad - p) < 0.02
+
+
+def test_layernorm_dropout_embeddings(native):
+    from distributed_tensorflow_example_amd.ops import transformer as T
+    N, H = 200, 768
+    x = torch.randn(N, H)
+    g, b = 1 + 0.1 * torch.randn(H), 0.1 * torch.randn(H)
+    xr, gr, br = x.clone().requires_grad_(), g.clone().requires_grad_(), b.clone().requires_grad_()
+    ref = T.layernorm_dropout(xr, gr, br, 0.0)
+    dy = torch.randn(N, H)
+    ref.backward(dy)
+    xg, gg, bg = x.cuda().requires_grad_(), g.cuda().requires_grad_(), b.cuda().requires_grad_()
+    out = T.layernorm_dropout(xg, gg, bg, 0.0)
+    out.backward(dy.cuda().bfloat16())
+    assert rel(out, ref) < 1e-2 and rel(xg.grad, xr.grad) < 2e-2 and rel(gg.grad, gr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("N,H", [(128, 3072), (1000, 768), (7, 1024)])
+def test_bias_gelu(native, N, H):
+    from distributed_tensorflow_example_amd.ops import transformer as T
+    x = torch.randn(N, H).bfloat16()
+    bias = torch.randn(H) * 0.2
+    xr, br = x.float().requires_grad_(), bias.clone().requires_grad_()
+    ref = T.bias_gelu(xr, br)
+    dy = torch.randn(N, H)
+    ref.backward(dy)
+    xg, bg = x.cuda().requires_grad_(), bias.cuda().requires_grad_()
+    out = T.bias_gelu(xg, bg)
+    out.backward(dy.cuda().bfloat16())
+    assert rel(out, ref) < 1e-2 and rel(xg.grad, xr.grad) < 2e-2 and rel(bg.grad, br.grad) < 2e-2
+
+
+@pytest.mark.parametrize("S", [64, 128, 384, 512])
+def test_attention_softmax(native, S):
+    from distributed_tensorflow_example_amd.ops import transformer as T
+    B, Hh = 3, 4
+    sc = (torch.randn(B, Hh, S, S) * 4).bfloat16()
+    mask = torch.zeros(B, S)
+    mask[1, S // 2:] = -10000.0
+    scr = sc.float().requires_grad_()
+    ref = T.attention_softmax(scr, mask, 1 / 8, 0.0)
+    dp = torch.randn_like(ref)
+    ref.backward(dp)
+    sg = sc.cuda().requires_grad_()
+    out = T.attention_softmax(sg, mask.cuda(), 1 / 8, 0.0)
+    out.backward(dp.cuda().bfloat16())
+    assert rel(out, ref) < 1e-2
+    assert rel(sg.grad, scr.grad) < 3e-2
+    assert float(out[1, :, :, S // 2:].float().abs().max()) < 1e-6       # masked keys get ~0 prob
+
+
+def test_attention_softmax_dropout_stats(native):
+    from distributed_tensorflow_example_amd.ops import transformer as T
+    sc = torch.zeros(2, 2, 128, 128, device="cuda", dtype=torch.bfloat16)
+    out = T.attention_softmax(sc, None, 1.0, 0.1)
+    kept = (out > 0).float().mean().item()
+    assert abs(kept - 0.9) < 0.01
+    assert abs(out.float().sum(-1).mean().item() - 1.0) < 0.02      # inverted dropout keeps the expectation
+
+
+def test_bert_tiny_gpu_matches_cpu_and_trains(native):
+    from distributed_tensorflow_example_amd import optim
+    from distributed_tensorflow_example_amd.models.bert import BertConfig, BertForMLM, synthetic_mlm_batch
+
+    c = BertConfig.tiny()
+    c.dropout = c.attn_dropout = 0.0
+    cpu = BertForMLM(c, seed=3)
+    gpu = BertForMLM(c, seed=3).cuda()
+    b = synthetic_mlm_batch(8, 128, c.vocab_size, "cpu", seed=1)
+    lc = cpu(*b)
+    lg = gpu(*[t.cuda() for t in b])
+    assert abs(float(lc) - float(lg)) < 0.05 * abs(float(lc))
+    lc.backward()
+    lg.backward()
+    for (n, pc), pg in zip(cpu.named_parameters(), gpu.parameters()):
+        if pc.grad is not None and pc.grad.norm() > 1e-6:
+            assert rel(pg.grad, pc.grad) < 0.1, n
+    c.dropout = c.attn_dropout = 0.1
+    m = BertForMLM(c, seed=4).cuda()
+    opt = optim.FusedAdamW(list(m.parameters()), 1e-3, weight_decay=0.01)
+    losses = []
+    for i in range(30):
+        for p in m.parameters():
+            p.grad = None
+        l = m(*[t.cuda() for t in b])
+        l.backward()
+        opt.step()
+        losses.append(float(l))
+    assert losses[-1] < losses[0] - 1.0

@@ -4,8 +4,10 @@
 Metric/config from BASELINE.json: "samples/sec (whole node) MNIST MLP sync-SGD
 at 1/2/4/8 MI355X; step-time p50".  Per-GPU batch 100 (example.py:43),
 lr 0.0005, sigmoid hidden layer, softmax cross-entropy, plain SGD; bf16 MFMA
-compute with fp32 master weights; gradients all-reduced in bf16 over RCCL
-(BASELINE config #2).  Synthetic MNIST-shaped data (uint8 pixels resident in
+compute with fp32 master weights; gradients all-reduced in bf16 (BASELINE
+config #2): by default a one-shot all-reduce over IPC-mapped xGMI peer
+buffers fused into the SGD apply kernel (validated against replica drift
+after warmup, falling back to RCCL), or RCCL (--allreduce rccl).  Synthetic MNIST-shaped data (uint8 pixels resident in
 pinned host memory, streamed to a device stage one 50-step chunk at a time by
 hipMemcpyAsync inside the chunk's hipGraph; --prefetch side double-buffers it
 on a side stream instead), random-init weights.  Weak scaling: per-GPU batch
@@ -52,34 +54,71 @@ def main(argv=None):
     ap.add_argument("--act", choices=["sigmoid", "relu"], default="sigmoid")
     ap.add_argument("--train-examples", type=int, default=55000)
     ap.add_argument("--prefetch", choices=["serial", "side"], default="serial")
+    ap.add_argument("--allreduce", choices=["auto", "ipc", "rccl"], default="auto",
+                    help="N>1 gradient all-reduce: one-shot IPC over xGMI fused into the SGD apply, or RCCL")
     a = ap.parse_args(argv)
 
     world_size_env = int(os.environ.get("WORLD_SIZE", "1"))
     if world_size_env != a.gpus:
         if a.gpus > 1 and world_size_env == 1:
             raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
-    w = world_mod.init(backend="rccl")
+    if os.environ.get("DTF_BENCH_SAME_GPU") == "1" and world_size_env > 1:
+        # test mode: all ranks share cuda:0 (gloo control plane, IPC data plane only);
+        # validates the multi-rank IPC path + graphs on a 1-GPU box, timings not meaningful
+        import datetime
+
+        import torch.distributed as dist
+
+        rank = int(os.environ["RANK"])
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world_size_env,
+                                timeout=datetime.timedelta(seconds=300))
+        w = world_mod.World(rank=rank, world_size=world_size_env, local_rank=rank, device=torch.device("cuda", 0),
+                            backend="gloo", pg_initialized=True)
+        world_mod._WORLD = w
+    else:
+        w = world_mod.init(backend="rccl")
     dev = w.device
     torch.manual_seed(1234 + w.rank)
 
     imgs, labels = synthetic_mnist(a.train_examples, seed=1000 + w.rank)
     epoch = PinnedEpoch(imgs, labels, a.batch)
     gd = torch.bfloat16 if a.grad_dtype == "bf16" else torch.float32
-    trainer = FusedMLPTrainer(batch_size=a.batch, lr=a.lr, act=a.act, world=w, grad_dtype=gd,
-                              device=dev)
-    runner = MLPStepRunner(trainer, epoch, steps_per_graph=a.steps_per_graph,
-                           use_graph=not a.eager, prefetch=a.prefetch)
 
-    # warmup: eager first (module load), then the graphs the warmup itself needs
-    runner.use_graph = False
-    runner.run(min(2, a.warmup))
-    runner.use_graph = not a.eager
-    if a.warmup > 2:
-        runner.prepare(a.warmup - 2)
-        runner.run(a.warmup - 2)
-    torch.cuda.synchronize()
-    runner.prepare(a.steps)  # capture outside the timed region
-    torch.cuda.synchronize()
+    def setup(allreduce):
+        trainer = FusedMLPTrainer(batch_size=a.batch, lr=a.lr, act=a.act, world=w, grad_dtype=gd,
+                                  device=dev, allreduce=allreduce)
+        runner = MLPStepRunner(trainer, epoch, steps_per_graph=a.steps_per_graph,
+                               use_graph=not a.eager, prefetch=a.prefetch)
+        # warmup: eager first (module load), then the graphs the warmup itself needs
+        runner.use_graph = False
+        runner.run(min(2, a.warmup))
+        runner.use_graph = not a.eager
+        if a.warmup > 2:
+            runner.prepare(a.warmup - 2)
+            runner.run(a.warmup - 2)
+        torch.cuda.synchronize()
+        runner.prepare(a.steps)  # capture outside the timed region
+        torch.cuda.synchronize()
+        return trainer, runner
+
+    def consistent(trainer) -> bool:
+        """No IPC timeout anywhere and bit-identical replicas on every rank."""
+        if w.world_size == 1:
+            return True
+        bad = w.host_all_reduce(float(trainer.ipc_error()), "max")
+        c = float(trainer.params.double().sum().item())
+        spread = w.host_all_reduce(c, "max") - w.host_all_reduce(c, "min")
+        return bad == 0.0 and spread == 0.0
+
+    trainer, runner = setup(a.allreduce)
+    if not consistent(trainer):
+        if trainer.allreduce != "ipc":
+            raise SystemExit("replicas diverged after warmup")
+        print("bench: IPC all-reduce failed validation; falling back to RCCL", file=sys.stderr, flush=True)
+        trainer, runner = setup("rccl")
+        if not consistent(trainer):
+            raise SystemExit("replicas diverged after warmup (rccl)")
     step0 = trainer.global_step
 
     events = []
@@ -104,6 +143,8 @@ def main(argv=None):
     p50 = statistics.median(per_step_ms) if per_step_ms else float("nan")
     p50 = w.host_all_reduce(p50, "max")
 
+    if w.world_size > 1 and not consistent(trainer):
+        raise SystemExit("replicas diverged / IPC timeout during the timed run; result discarded")
     steps_done = trainer.global_step - step0
     m = trainer.read_metrics(trainer.global_step - 1, trainer.global_step)[0]
     n = w.world_size
@@ -130,7 +171,7 @@ def main(argv=None):
                 "seq_len": None,
                 "parallelism": f"dp{n}",
                 "optimizer": f"sgd lr={a.lr}",
-                "grad_allreduce": a.grad_dtype if n > 1 else "none",
+                "grad_allreduce": f"{a.grad_dtype} {trainer.allreduce}" if n > 1 else "none",
                 "hipgraph_steps": 0 if a.eager else a.steps_per_graph,
                 "input_prefetch": a.prefetch,
                 "activation": a.act,

@@ -21,6 +21,11 @@ hipError_t dtfk_mlp_wgrad(const void* x, int x_kind, const void* dz2T, int BP, i
                           long long* gstep, int ring, long long* ts, hipStream_t stream);
 hipError_t dtfk_mlp_apply_flat(float* params, const void* grads, int grad_kind, const float* lr,
                                float scale, void* W1T, void* W2T, void* W2N, hipStream_t stream);
+int dtfk_mlp_ipc_flag_bytes();
+hipError_t dtfk_mlp_ipc_reduce_apply(float* params, void* const* peer_table, int W, int rank, int parity,
+                                     long long slot_bytes, const long long* gstep, const float* lr, float scale,
+                                     void* W1T, void* W2T, void* W2N, int* err, long long timeout_ticks,
+                                     hipStream_t stream);
 }
 
 namespace dtf {
@@ -129,6 +134,25 @@ void mlp_wgrad(at::Tensor x, int64_t x_off, int x_kind, at::Tensor dz2T, int B,
             "mlp_wgrad");
 }
 
+// one-shot IPC all-reduce fused with SGD apply (see mlp_step.hip); peer_table is the
+// device address of IpcPeerBuffers.table_ptr(); err: int32[1] device flag
+void mlp_ipc_reduce_apply(at::Tensor params, int64_t peer_table, int W, int rank, int parity, int64_t slot_bytes,
+                          at::Tensor gstep, at::Tensor lr, double scale, at::Tensor W1T, at::Tensor W2T,
+                          at::Tensor W2N, at::Tensor err, double timeout_s) {
+  need(params, at::kFloat, kNParam, "params");
+  need(W1T, at::kBFloat16, 112 * 800, "W1T");
+  need(W2T, at::kBFloat16, 16 * 128, "W2T");
+  need(W2N, at::kBFloat16, 112 * 32, "W2N");
+  if (!err.is_cuda() || err.scalar_type() != at::kInt) throw std::runtime_error("err must be a GPU int32 tensor");
+  if (peer_table == 0 || W < 2 || rank < 0 || rank >= W || (parity & ~1) || slot_bytes < kNParam * 2)
+    throw std::runtime_error("mlp_ipc_reduce_apply: bad arguments");
+  const long long ticks = (long long)(timeout_s * 1.0e8);  // s_memrealtime runs at 100 MHz
+  hip_check(dtfk_mlp_ipc_reduce_apply(params.data_ptr<float>(), reinterpret_cast<void* const*>(peer_table), W, rank, parity,
+                               slot_bytes, reinterpret_cast<const long long*>(gstep.data_ptr<int64_t>()), lr.data_ptr<float>(), (float)scale,
+                               W1T.data_ptr(), W2T.data_ptr(), W2N.data_ptr(), err.data_ptr<int>(), ticks, cur_stream()),
+     "mlp_ipc_reduce_apply");
+}
+
 void mlp_apply_flat(at::Tensor params, c10::optional<at::Tensor> grads, at::Tensor lr,
                     double scale, at::Tensor W1T, at::Tensor W2T, at::Tensor W2N) {
   need(W2N, at::kBFloat16, 112 * 32, "W2N");
@@ -180,6 +204,8 @@ void init_mlp(py::module& m) {
         py::arg("metrics"),
         py::arg("gstep"), py::arg("ts") = py::none());
   m.def("mlp_apply_flat", &mlp_apply_flat);
+  m.def("mlp_ipc_reduce_apply", &mlp_ipc_reduce_apply);
+  m.def("mlp_ipc_flag_bytes", &dtfk_mlp_ipc_flag_bytes);
   m.def("memcpy_h2d_async", &memcpy_h2d_async);
 }
 

@@ -473,6 +473,79 @@ __global__ __launch_bounds__(256) void mlp_apply_flat(
     W2N[(j / NCLS) * 32 + j % NCLS] = f2bf(p);
   }
 }
+// ---------------------------------------------------------------------- C'
+// One-shot all-reduce fused into the SGD apply, for N GPUs of one node.
+// Every rank's wgrad (GRAD mode, bf16) wrote its gradient into its own
+// IPC-exported uncached buffer (parity slot); peers' buffers are mapped.
+//   1. each block's thread 0 publishes this rank's epoch (= device global
+//      step, bumped by wgrad) in its flag word -- idempotent, so no block
+//      depends on another being scheduled;
+//   2. it waits (bounded, s_memrealtime) until every peer's flag reached the
+//      epoch: all gradients of this step are complete and visible;
+//   3. the block sums the N gradients in rank order (identical on every rank
+//      -> replicas stay bit-identical), p -= lr*scale*sum, refreshes shadows.
+// Each rank reads (N-1) x 159 KB over its xGMI links in parallel instead of a
+// ring's 2(N-1) latency-bound hops.  Double-buffered by step parity: a rank
+// rewrites slot p only after its next apply saw every peer's flag for the
+// step in between, i.e. after every peer finished reading slot p.
+constexpr int IPC_FLAG_BYTES = 256;
+
+__global__ __launch_bounds__(256) void mlp_ipc_reduce_apply(
+    float* __restrict__ params, void* const* __restrict__ peer_base, int W, int rank, int parity,
+    long long slot_bytes, const long long* __restrict__ gstep, const float* __restrict__ lr_ptr, float scale,
+    uint16_t* __restrict__ W1T, uint16_t* __restrict__ W2T, uint16_t* __restrict__ W2N, int* __restrict__ err,
+    long long timeout_ticks) {
+  __shared__ int ok;
+  const unsigned long long epoch = (unsigned long long)(*gstep);
+  if (threadIdx.x == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+    ok = 0;                                  // a previous step timed out: fail fast, never wait again
+  } else if (threadIdx.x == 0) {
+    __threadfence_system();
+    unsigned long long* mine = reinterpret_cast<unsigned long long*>(peer_base[rank]);
+    __hip_atomic_store(mine, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    int good = 1;
+    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+    for (int r = 0; r < W && good; ++r) {
+      const unsigned long long* f = reinterpret_cast<const unsigned long long*>(peer_base[r]);
+      while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
+        __builtin_amdgcn_s_sleep(1);
+        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
+          good = 0;
+          atomicOr(err, 1);
+          break;
+        }
+      }
+    }
+    ok = good;
+  }
+  __syncthreads();
+  if (!ok) return;
+  const int i0 = (blockIdx.x * blockDim.x + threadIdx.x) * 2;   // 2 params per thread (4-byte loads)
+  if (i0 >= NPARAM) return;
+  const long long off = IPC_FLAG_BYTES + (long long)parity * slot_bytes;
+  float g0 = 0.f, g1 = 0.f;
+  for (int r = 0; r < W; ++r) {
+    const uint32_t u = __builtin_nontemporal_load(
+        reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(peer_base[r]) + off) + (i0 >> 1));
+    g0 += bf2f(u & 0xFFFF);
+    g1 += bf2f(u >> 16);
+  }
+  const float step = (*lr_ptr) * scale;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int i = i0 + j;
+    const float p = params[i] - step * (j == 0 ? g0 : g1);
+    params[i] = p;
+    if (i < OFF_W2) {
+      W1T[(size_t)(i % HID) * DINP + i / HID] = f2bf(p);
+    } else if (i < OFF_B1) {
+      const int q = i - OFF_W2;
+      W2T[(q % NCLS) * HIDK + q / NCLS] = f2bf(p);
+      W2N[(q / NCLS) * 32 + q % NCLS] = f2bf(p);
+    }
+  }
+}
+
 #undef TS
 
 }  // namespace mlp
@@ -549,6 +622,19 @@ hipError_t dtfk_mlp_apply_flat(float* params, const void* grads, int grad_kind, 
   hipLaunchKernelGGL(mlp_apply_flat, dim3((NPARAM + 255) / 256), dim3(256), 0, stream, params,
                      grads, grad_kind == 2 ? 1 : 0, lr, scale, (uint16_t*)W1T, (uint16_t*)W2T,
                      (uint16_t*)W2N);
+  return hipGetLastError();
+}
+
+int dtfk_mlp_ipc_flag_bytes() { return dtfk::mlp::IPC_FLAG_BYTES; }
+
+hipError_t dtfk_mlp_ipc_reduce_apply(float* params, void* const* peer_table, int W, int rank, int parity,
+                                     long long slot_bytes, const long long* gstep, const float* lr, float scale,
+                                     void* W1T, void* W2T, void* W2N, int* err, long long timeout_ticks,
+                                     hipStream_t stream) {
+  using namespace dtfk::mlp;
+  hipLaunchKernelGGL(mlp_ipc_reduce_apply, dim3((NPARAM / 2 + 255) / 256), dim3(256), 0, stream, params, peer_table,
+                     W, rank, parity, slot_bytes, gstep, lr, scale, (uint16_t*)W1T, (uint16_t*)W2T, (uint16_t*)W2N,
+                     err, timeout_ticks);
   return hipGetLastError();
 }
 

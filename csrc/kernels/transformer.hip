@@ -282,14 +282,25 @@ __global__ __launch_bounds__(256) void bias_gelu_bwd(const uint16_t* __restrict_
   p[0] = acc[0]; p[1] = acc[1]; p[2] = acc[2]; p[3] = acc[3];
 }
 
-// column sums of a [P, H] fp32 partial buffer -> out[H] (deterministic)
-__global__ __launch_bounds__(256) void colsum_partials(const float* __restrict__ part, float* __restrict__ out, int P,
-                                                       int H) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= H) return;
+// column sums of a [P, H] fp32 partial buffer -> out[H] (deterministic).
+// 1024 threads = 64 consecutive columns x 16 row groups (coalesced 256 B
+// rows), LDS tree over the groups; grid = ceil(H / 64).
+__global__ __launch_bounds__(1024) void colsum_partials(const float* __restrict__ part, float* __restrict__ out,
+                                                        int P, int H) {
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
   float s = 0.f;
-  for (int p = 0; p < P; ++p) s += part[(size_t)p * H + c];
-  out[c] = s;
+  if (c < H)
+    for (int p = g; p < P; p += 16) s += part[(size_t)p * H + c];
+  red[g][lane] = s;
+  __syncthreads();
+  if (g == 0 && c < H) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[i][lane];
+    out[c] = t;
+  }
 }
 
 // ---------------------------------------------------------------- attention softmax
@@ -468,7 +479,7 @@ hipError_t dtfk_ln_bwd(const void* dy, const void* s, const float* mean, const f
 }
 
 hipError_t dtfk_colsum_partials(const float* part, float* out, int P, int H, hipStream_t st) {
-  hipLaunchKernelGGL(colsum_partials, dim3((H + 255) / 256), dim3(256), 0, st, part, out, P, H);
+  hipLaunchKernelGGL(colsum_partials, dim3((H + 63) / 64), dim3(1024), 0, st, part, out, P, H);
   return hipGetLastError();
 }
 

@@ -13,6 +13,7 @@ void init_queue(py::module& m);
 void init_libsvm(py::module& m);
 void init_ops(py::module& m);
 void init_transformer(py::module& m);
+void init_ipc(py::module& m);
 }  // namespace dtf
 
 PYBIND11_MODULE(_C, m) {
@@ -27,4 +28,5 @@ PYBIND11_MODULE(_C, m) {
   dtf::init_libsvm(m);
   dtf::init_ops(m);
   dtf::init_transformer(m);
+  dtf::init_ipc(m);
 }

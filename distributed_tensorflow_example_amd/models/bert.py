@@ -60,6 +60,16 @@ def _mm(x, w):
     return F.linear(x, w.to(x.dtype))
 
 
+def _lookup(table, ids):
+    """Row gather whose backward is the framework's scatter-add kernel
+    (torch's sort-based index backward is ~14% of a BERT step on MI355X)."""
+    flat = ids.reshape(-1)
+    if not table.is_cuda:
+        return table[flat]
+    offs = torch.arange(flat.numel() + 1, device=flat.device)
+    return ops.embedding_bag(table, flat, offs, None, "sum")
+
+
 class BertLayer(torch.nn.Module):
     def __init__(self, c: BertConfig):
         super().__init__()
@@ -125,7 +135,11 @@ class BertForMLM(torch.nn.Module):
         mlm_positions [M] flat indices into B*S; mlm_labels [M] int64."""
         c = self.c
         B, S = input_ids.shape
-        emb = self.word[input_ids] + self.pos[:S].unsqueeze(0) + self.typ[token_type]
+        if c.type_vocab == 2:       # 2-row table: a lerp (reduction backward) beats contended scatter-adds
+            typ = self.typ[0] + token_type.reshape(-1, 1).to(self.typ.dtype) * (self.typ[1] - self.typ[0])
+        else:
+            typ = _lookup(self.typ, token_type)
+        emb = (_lookup(self.word, input_ids) + typ).view(B, S, c.hidden) + self.pos[:S].unsqueeze(0)
         x = T.layernorm_dropout(emb, self.emb_g, self.emb_b, c.dropout, c.ln_eps, self.training)
         act = torch.bfloat16 if x.is_cuda else torch.float32
         x = x.to(act)

@@ -22,6 +22,7 @@ Parameter layout (flat fp32, TF variable order and names):
 from __future__ import annotations
 
 import math
+import os
 import time
 from collections import OrderedDict
 from typing import Dict, List, Optional, Tuple
@@ -125,7 +126,8 @@ class FusedMLPTrainer:
 
     def __init__(self, batch_size: int = 100, lr: float = 0.0005, act: str = "sigmoid",
                  world=None, grad_dtype: torch.dtype = torch.bfloat16, naive_loss: bool = False,
-                 metrics_ring: int = 8192, seed: int = 1, device=None):
+                 metrics_ring: int = 8192, seed: int = 1, device=None, allreduce: str = "auto",
+                 ipc_timeout_s: float = 5.0):
         self.C = _native.load()
         self.world = world
         self.world_size = 1 if world is None else world.world_size
@@ -154,7 +156,43 @@ class FusedMLPTrainer:
         self.ring = int(metrics_ring)
         self.metrics = torch.zeros(self.ring * 2, dtype=torch.float32, device=dev)
         self.gstep = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.allreduce = "none"
+        self.ipc = None
+        self.ipc_parity = 0
+        self.ipc_timeout_s = float(ipc_timeout_s)
+        if self.world_size > 1:
+            self.allreduce = "rccl"
+            if allreduce in ("ipc", "auto"):
+                try:
+                    self._setup_ipc()
+                    self.allreduce = "ipc"
+                except Exception as e:  # noqa: BLE001
+                    if allreduce == "ipc":
+                        raise
+                    import warnings
+
+                    warnings.warn(f"IPC all-reduce unavailable ({e}); using RCCL")
         self.set_params(init_params(seed))
+
+    # ---------------------------------------------------------------- IPC one-shot all-reduce
+    def _setup_ipc(self):
+        """Map every rank's gradient buffer (xGMI peers of one node); handles go
+        through the gloo control plane.  Layout: [flags][grad slot 0][grad slot 1]."""
+        w = self.world
+        if int(os.environ.get("LOCAL_WORLD_SIZE", w.world_size)) != w.world_size:
+            raise RuntimeError("IPC all-reduce needs all ranks on one node")
+        C = self.C
+        self.ipc_flag_bytes = C.mlp_ipc_flag_bytes()
+        self.ipc_slot = ((NPARAM * 2 + 255) // 256) * 256
+        buf = C.IpcPeerBuffers(self.ipc_flag_bytes + 2 * self.ipc_slot, w.world_size, w.rank)
+        handles = w.all_gather_object(bytes(buf.handle()))
+        buf.open(list(handles))
+        self.ipc = buf
+        self.ipc_grads = [buf.tensor(self.ipc_flag_bytes + p * self.ipc_slot, NPARAM, 1) for p in (0, 1)]
+        self.ipc_err = torch.zeros(1, dtype=torch.int32, device=self.device)
+
+    def ipc_error(self) -> int:
+        return int(self.ipc_err.item()) if self.ipc is not None else 0
 
     # ---------------------------------------------------------------- state
     def set_params(self, flat_cpu: torch.Tensor, broadcast: bool = True):
@@ -187,7 +225,7 @@ class FusedMLPTrainer:
 
     # ----------------------------------------------------------------- steps
     def enqueue_step(self, x: torch.Tensor, x_off: int, x_kind: int, labels: torch.Tensor,
-                     labels_off: int):
+                     labels_off: int, ipc_parity: Optional[int] = None):
         """Enqueue one full training step on the current stream.
 
         x: device buffer holding B rows of 784 features at byte offset x_off
@@ -200,6 +238,17 @@ class FusedMLPTrainer:
         if self.world_size == 1:
             C.mlp_wgrad(x, x_off, x_kind, self.dz2T, B, self.partials, self.params, self.W1T,
                         self.W2T, self.W2N, None, 0, self.lr, self.metrics, self.gstep)
+        elif self.ipc is not None:
+            # one-shot: bf16 grads into this rank's exported slot, then every rank
+            # sums all peers' slots over xGMI inside the SGD apply kernel
+            par = self.ipc_parity if ipc_parity is None else int(ipc_parity) & 1
+            if ipc_parity is None:
+                self.ipc_parity ^= 1
+            C.mlp_wgrad(x, x_off, x_kind, self.dz2T, B, self.partials, self.params, self.W1T,
+                        self.W2T, self.W2N, self.ipc_grads[par], 2, self.lr, self.metrics, self.gstep)
+            C.mlp_ipc_reduce_apply(self.params, self.ipc.table_ptr(), self.world_size, self.world.rank, par,
+                                   self.ipc_slot, self.gstep, self.lr, 1.0 / self.world_size, self.W1T, self.W2T,
+                                   self.W2N, self.ipc_err, self.ipc_timeout_s)
         else:
             kind = 1 if self.grad_dtype == torch.float32 else 2
             C.mlp_wgrad(x, x_off, x_kind, self.dz2T, B, self.partials, self.params, self.W1T,
@@ -256,21 +305,21 @@ class MLPStepRunner:
         ep = self.epoch
         self.t.C.memcpy_h2d_async(dst, 0, ep.host, b0 * ep.rec, g * ep.rec)
 
-    def _emit_steps(self, g: int, buf: torch.Tensor):
+    def _emit_steps(self, g: int, buf: torch.Tensor, ipar: int):
         t = self.t
         rec, B = self.epoch.rec, t.B
         for i in range(g):
             off = i * rec
-            t.enqueue_step(buf, off, 0, buf, off + B * D_IN)
+            t.enqueue_step(buf, off, 0, buf, off + B * D_IN, ipc_parity=(ipar + i) & 1)
 
     def _emit(self, key):
         if self.prefetch == "serial":
-            b0, g = key
+            b0, g, ipar = key
             self._copy_chunk(self.stage[0], b0, g)
-            self._emit_steps(g, self.stage[0])
+            self._emit_steps(g, self.stage[0], ipar)
         else:
-            g, par = key
-            self._emit_steps(g, self.stage[par])
+            g, par, ipar = key
+            self._emit_steps(g, self.stage[par], ipar)
 
     def _graph(self, key) -> torch.cuda.CUDAGraph:
         gr = self.graphs.get(key)
@@ -296,29 +345,31 @@ class MLPStepRunner:
         return out
 
     def plan(self, steps: int):
-        """[(b0, g, parity, next)] for the next `steps` steps from the cursor."""
+        """[(b0, g, parity, next, ipc_parity)] for the next `steps` steps from the cursor."""
         ch = self._chunks(self.cursor, steps)
         after = self._chunks(self.cursor + steps, self.g)[0]  # speculative prefetch
-        out, par = [], self.parity
+        out, par, ipar = [], self.parity, self.t.ipc_parity
         for j, (b0, g) in enumerate(ch):
             nxt = ch[j + 1] if j + 1 < len(ch) else after
-            out.append((b0, g, par, nxt))
+            out.append((b0, g, par, nxt, ipar))
             par ^= 1
+            ipar = (ipar + g) & 1
         return out
 
-    def _key(self, b0, g, par):
-        return (b0, g) if self.prefetch == "serial" else (g, par)
+    def _key(self, b0, g, par, ipar=0):
+        return (b0, g, ipar) if self.prefetch == "serial" else (g, par, ipar)
 
     def prepare(self, steps: int):
         """Capture every graph `run(steps)` will need (keeps capture out of timing)."""
         if self.use_graph:
-            for (b0, g, par, _) in self.plan(steps):
-                self._graph(self._key(b0, g, par))
+            for (b0, g, par, _, ipar) in self.plan(steps):
+                self._graph(self._key(b0, g, par, ipar))
 
     def run(self, steps: int, events: Optional[list] = None):
         main = torch.cuda.current_stream()
-        for (b0, g, par, nxt) in self.plan(steps):
-            key = self._key(b0, g, par)
+        for (b0, g, par, nxt, ipar) in self.plan(steps):
+            key = self._key(b0, g, par, ipar)
+            self.t.ipc_parity = (ipar + g) & 1
             if self.prefetch == "side" and self.loaded != (b0, g):  # cold start / plan change
                 self._copy_chunk(self.stage[par], b0, g)
                 self._freed = None

@@ -34,7 +34,7 @@ def _C():
 
 
 def _ln_part(N: int, H: int, device) -> torch.Tensor:
-    grid = max(1, min(512, (N + 3) // 4))
+    grid = max(1, min(256, (N + 15) // 16))      # >= 4 rows per wave, one partial row per block
     return torch.empty(3 * grid * H, dtype=torch.float32, device=device)
 
 
@@ -152,7 +152,7 @@ class _BiasGelu(torch.autograd.Function):
         H = x.shape[-1]
         N = x.numel() // H
         dx = torch.empty_like(x)
-        slices = max(1, min(256, N // 16))
+        slices = max(1, min(128, N // 32))
         part = torch.empty(slices * H, dtype=torch.float32, device=x.device)
         dbias = torch.empty(H, dtype=torch.float32, device=x.device)
         C.bias_gelu_bwd(dy.to(torch.bfloat16).contiguous(), x, bias, dx, part, dbias)

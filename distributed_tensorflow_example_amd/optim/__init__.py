@@ -26,6 +26,17 @@ from .. import _native
 KINDS = {"sgd": 0, "momentum": 1, "adam": 2, "adamw": 3}
 
 
+def _dense(t: torch.Tensor) -> bool:
+    """Non-overlapping dense storage (row-major or channels_last): the kernels
+    walk params/grads/slots as flat arrays, so only identical layouts matter."""
+    return t.is_contiguous() or (t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last))
+
+
+def _same_layout(a: torch.Tensor, b: torch.Tensor) -> bool:
+    # strides of size-1 dims are irrelevant (a [o, i, 1, 1] weight is both contiguous and channels_last)
+    return a.shape == b.shape and all(x == y for x, y, n in zip(a.stride(), b.stride(), a.shape) if n > 1)
+
+
 class _FusedBase:
     kind = "sgd"
 
@@ -87,8 +98,8 @@ class _FusedBase:
             chunk = C.mt_chunk()
             rows, chunks = [], []
             for i, (p, g) in enumerate(zip(self.params, grads)):
-                if not (p.is_contiguous() and g.is_contiguous()) or p.dtype != torch.float32:
-                    raise ValueError("fused optimizer needs contiguous fp32 params and contiguous grads")
+                if p.dtype != torch.float32 or not _dense(p) or not _same_layout(p, g) or not _dense(g):
+                    raise ValueError("fused optimizer needs dense fp32 params with grads of identical layout")
                 m, v = self.m[i], self.v[i]
                 rows.append([p.data_ptr(), g.data_ptr(), m.data_ptr() if m is not None else 0,
                              v.data_ptr() if v is not None else 0, p.numel()])

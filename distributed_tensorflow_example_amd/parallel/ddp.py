@@ -39,7 +39,10 @@ class _Bucket:
         self.views = []
         off = 0
         for p in params:
-            v = self.buf[off:off + p.numel()].view_as(p)
+            seg = self.buf[off:off + p.numel()]
+            # the grad view mirrors the param's layout (e.g. channels_last conv
+            # weights) so fused optimizers can walk param/grad as flat arrays
+            v = seg.view_as(p) if p.is_contiguous() else seg.as_strided(p.size(), p.stride())
             self.views.append(v)
             off += p.numel()
         self.ready = 0

@@ -28,8 +28,8 @@ rc=$?; tail -1 $OUT/bench_eager.log
 [ $rc -ne 0 ] && { echo "bench eager rc=$rc"; exit $rc; }
 
 if [ "${MODEL_BENCH:-0}" = "1" ]; then
-  for m in sparse_lr wide_deep; do
-    timeout -k 10 300 python scripts/bench_models.py --model $m --steps 100 --warmup 10 > $OUT/bench_$m.log 2>&1
+  for m in ${MODELS:-sparse_lr wide_deep bert_base resnet50}; do
+    timeout -k 10 300 python scripts/bench_models.py --model $m --steps ${MODEL_STEPS:-50} --warmup 10 > $OUT/bench_$m.log 2>&1
     rc=$?; tail -1 $OUT/bench_$m.log
     [ $rc -ne 0 ] && { echo "bench $m rc=$rc"; exit $rc; }
   done

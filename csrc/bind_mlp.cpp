@@ -26,6 +26,10 @@ hipError_t dtfk_mlp_ipc_reduce_apply(float* params, void* const* peer_table, int
                                      long long slot_bytes, const long long* gstep, const float* lr, float scale,
                                      void* W1T, void* W2T, void* W2N, int* err, long long timeout_ticks,
                                      hipStream_t stream);
+hipError_t dtfk_mlp_fwd_head(const void* x, int x_kind, int B, const void* W1T, float* z2p, const void* labels,
+                             const void* W2T, const void* W2N, const float* params, void* dz2T, int BP,
+                             float* partials, float inv_batch, int act, int naive_loss, int* counters,
+                             hipStream_t stream);
 }
 
 namespace dtf {
@@ -78,6 +82,32 @@ void mlp_l1_fwd(at::Tensor x, int64_t x_off, int x_kind, int B, at::Tensor W1T, 
   hip_check(dtfk_mlp_l1_fwd(xb, x_kind, B, W1T.data_ptr(), z2p.data_ptr<float>(),
                             ts_ptr(ts, (int64_t)nb * 7 * dtfk_mlp_ksplit() * 16), cur_stream()),
             "mlp_l1_fwd");
+}
+
+// A1 + A2 in one launch (last-arriver row-block handoff); counters: int32[nb], zero at rest
+void mlp_fwd_head(at::Tensor x, int64_t x_off, int x_kind, int B, at::Tensor W1T, at::Tensor z2p, at::Tensor labels,
+                  int64_t labels_off, at::Tensor W2T, at::Tensor W2N, at::Tensor params, at::Tensor dz2T,
+                  at::Tensor partials, double inv_batch, int act, bool naive_loss, at::Tensor counters) {
+  if (B <= 0) throw std::runtime_error("B must be positive");
+  const int nb = (B + 15) / 16, BP = bp_of(B);
+  const char* xb = x_ptr(x, x_off, x_kind, B);
+  need(W1T, at::kBFloat16, 112 * 800, "W1T");
+  need(z2p, at::kFloat, (int64_t)dtfk_mlp_ksplit() * nb * 16 * 112, "z2p");
+  if (!labels.is_cuda() || labels.scalar_type() != at::kByte)
+    throw std::runtime_error("labels must be a uint8 GPU tensor");
+  if (labels.numel() < labels_off + B) throw std::runtime_error("labels buffer too small");
+  need(W2T, at::kBFloat16, 16 * 128, "W2T");
+  need(W2N, at::kBFloat16, 112 * 32, "W2N");
+  need(params, at::kFloat, kNParam, "params");
+  need(dz2T, at::kBFloat16, (int64_t)112 * BP, "dz2T");
+  need(partials, at::kFloat, (int64_t)nb * 1112, "partials");
+  need(counters, at::kInt, nb, "counters");
+  hip_check(dtfk_mlp_fwd_head(xb, x_kind, B, W1T.data_ptr(), z2p.data_ptr<float>(),
+                              reinterpret_cast<const uint8_t*>(labels.data_ptr()) + labels_off, W2T.data_ptr(),
+                              W2N.data_ptr(), params.data_ptr<float>(), dz2T.data_ptr(), BP,
+                              partials.data_ptr<float>(), (float)inv_batch, act, naive_loss ? 1 : 0,
+                              counters.data_ptr<int>(), cur_stream()),
+            "mlp_fwd_head");
 }
 
 void mlp_head_bwd(at::Tensor z2p, at::Tensor labels, int64_t labels_off, int B, at::Tensor W2T,
@@ -204,6 +234,7 @@ void init_mlp(py::module& m) {
         py::arg("metrics"),
         py::arg("gstep"), py::arg("ts") = py::none());
   m.def("mlp_apply_flat", &mlp_apply_flat);
+  m.def("mlp_fwd_head", &mlp_fwd_head);
   m.def("mlp_ipc_reduce_apply", &mlp_ipc_reduce_apply);
   m.def("mlp_ipc_flag_bytes", &dtfk_mlp_ipc_flag_bytes);
   m.def("memcpy_h2d_async", &memcpy_h2d_async);

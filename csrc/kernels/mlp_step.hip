@@ -156,14 +156,26 @@ __global__ __launch_bounds__(256) void mlp_l1_fwd(
 }
 
 // ---------------------------------------------------------------------- A2
-// one 512-thread workgroup per 16 batch rows
-__global__ __launch_bounds__(512) void mlp_head_bwd(
-    const float* __restrict__ z2p, const uint8_t* __restrict__ labels, int B,
+// agent-coherent (L2-bypassing, sc1) loads of a float4 written by another XCD
+__device__ __forceinline__ float4 ld_coherent4(const float* p) {
+  float4 r;
+  r.x = __hip_atomic_load(p + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  r.y = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  r.z = __hip_atomic_load(p + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  r.w = __hip_atomic_load(p + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return r;
+}
+
+// one 512-thread workgroup per 16 batch rows (row block rb of nblk).
+// COHERENT_Z: z2p was produced by other workgroups of the SAME launch (merged
+// kernel) -> read it with agent-coherent loads instead of plain cached loads.
+template <bool COHERENT_Z>
+__device__ __forceinline__ void head_bwd_block(
+    int rb, int nblk, const float* __restrict__ z2p, const uint8_t* __restrict__ labels, int B,
     const uint16_t* __restrict__ W2T, const uint16_t* __restrict__ W2N,
     const float* __restrict__ params, uint16_t* __restrict__ dz2T, int BP,
     float* __restrict__ partials, float inv_batch, int act, int naive_loss,
     long long* __restrict__ ts) {
-  TS(0);
   __shared__ __attribute__((aligned(16))) float a2f[ROWS * HIDP];      // [r][n] fp32
   __shared__ __attribute__((aligned(16))) uint16_t a2b[ROWS * A2S];    // [r][n] bf16, n<128
   __shared__ __attribute__((aligned(16))) uint16_t a2T[HIDP * D3S];    // [n][r] bf16, r<32
@@ -173,17 +185,19 @@ __global__ __launch_bounds__(512) void mlp_head_bwd(
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, lh = lane >> 4;
-  const int r0 = blockIdx.x * ROWS;
-  const size_t nrows = (size_t)gridDim.x * ROWS;
-  float* part = partials + (size_t)blockIdx.x * PART;
+  const int r0 = rb * ROWS;
+  const size_t nrows = (size_t)nblk * ROWS;
+  float* part = partials + (size_t)rb * PART;
 
   // ---- all global loads up front (branch-free) ----
   const int qi = min(tid, ROWS * HIDP / 4 - 1);  // float4 index in the 16x112 slice
   const int qr = (4 * qi) / HIDP, qc = (4 * qi) % HIDP;
-  float4 zq = reinterpret_cast<const float4*>(z2p + (size_t)r0 * HIDP)[qi];
+  float4 zq = COHERENT_Z ? ld_coherent4(z2p + (size_t)r0 * HIDP + 4 * qi)
+                         : reinterpret_cast<const float4*>(z2p + (size_t)r0 * HIDP)[qi];
 #pragma unroll
   for (int k = 1; k < KSPLIT; ++k) {
-    const float4 z = reinterpret_cast<const float4*>(z2p + ((size_t)k * nrows + r0) * HIDP)[qi];
+    const float4 z = COHERENT_Z ? ld_coherent4(z2p + ((size_t)k * nrows + r0) * HIDP + 4 * qi)
+                                : reinterpret_cast<const float4*>(z2p + ((size_t)k * nrows + r0) * HIDP)[qi];
     zq.x += z.x; zq.y += z.y; zq.z += z.z; zq.w += z.w;
   }
   float b1q[4];
@@ -291,7 +305,89 @@ __global__ __launch_bounds__(512) void mlp_head_bwd(
     if (lane < NCLS) part[1100 + lane] = v;
     else if (lane >= 16) part[1110 + (lane - 16)] = v;
   }
+}
+
+__global__ __launch_bounds__(512) void mlp_head_bwd(
+    const float* __restrict__ z2p, const uint8_t* __restrict__ labels, int B,
+    const uint16_t* __restrict__ W2T, const uint16_t* __restrict__ W2N,
+    const float* __restrict__ params, uint16_t* __restrict__ dz2T, int BP,
+    float* __restrict__ partials, float inv_batch, int act, int naive_loss,
+    long long* __restrict__ ts) {
+  TS(0);
+  head_bwd_block<false>(blockIdx.x, gridDim.x, z2p, labels, B, W2T, W2N, params, dz2T, BP, partials, inv_batch,
+                        act, naive_loss, ts);
   TS(3);
+}
+
+// ---------------------------------------------------------------------- A (A1 + A2 in one launch)
+// Same layer-1 tiling as A1 with 8 waves per workgroup; the LAST of the
+// 7 x KSPLIT workgroups of a row block to finish (device-scope counter,
+// release/acquire fences) runs that row block's head/backward (A2) in place.
+// Removes the A1 -> A2 kernel boundary (~2.6 us of launch gap measured with
+// s_memrealtime stamps) and lets early row blocks start A2 while others still
+// run layer 1.  The counter is reset by its last arriver (graph-replay safe).
+constexpr int KJ8 = (KS_PER + 7) / 8;   // k-steps per wave with 8 waves
+
+template <int XK>
+__global__ __launch_bounds__(512) void mlp_fwd_head(
+    const uint8_t* __restrict__ xin, int B, const uint16_t* __restrict__ W1T, float* __restrict__ z2p,
+    const uint8_t* __restrict__ labels, const uint16_t* __restrict__ W2T, const uint16_t* __restrict__ W2N,
+    const float* __restrict__ params, uint16_t* __restrict__ dz2T, int BP, float* __restrict__ partials,
+    float inv_batch, int act, int naive_loss, int* __restrict__ counters) {
+  __shared__ float red8[8][16][17];
+  __shared__ int last;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, lh = lane >> 4;
+  const int ct = blockIdx.x;
+  const int ks0 = blockIdx.y * KS_PER;
+  const int ks1 = min(25, ks0 + KS_PER);
+  const int rb = blockIdx.z;
+  const int r0 = rb * ROWS;
+  const int row = r0 + lr;
+  const bool rv = row < B;
+  const size_t xrow = (size_t)min(row, B - 1) * DIN;
+
+  bf16x8 bw[KJ8];
+  float xv[KJ8][8];
+  const uint16_t* pw = W1T + (size_t)(ct * 16 + lr) * DINP + lh * 8;
+#pragma unroll
+  for (int j = 0; j < KJ8; ++j) {
+    const int ks = ks0 + wave + 8 * j;
+    bw[j] = ld_bf16x8(pw + min(ks, 24) * 32);
+    load_x8<XK>(xin, xrow + min(ks * 32 + lh * 8, DIN - 8), xv[j]);
+  }
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < KJ8; ++j) {
+    const int ks = ks0 + wave + 8 * j;
+    const bool keep = rv && ks < ks1 && ks * 32 + lh * 8 < DIN;
+    acc = mfma16x16x32(to_bf16x8(xv[j], keep), bw[j], acc);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) red8[wave][4 * lh + i][lr] = acc[i];
+  __syncthreads();
+  if (tid < 256) {
+    const int r = tid >> 4, c = tid & 15;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) v += red8[w][r][c];
+    // agent-coherent write-through store (sc1): visible to the other XCDs
+    // without a full-L2 writeback (a __threadfence() release here costs a
+    // buffer_wbl2 per workgroup: measured 13 -> 31 us per step)
+    __hip_atomic_store(&z2p[((size_t)blockIdx.y * gridDim.z * ROWS + r0 + r) * HIDP + ct * 16 + c], v,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __builtin_amdgcn_s_waitcnt(0);   // this thread's stores acknowledged
+  __syncthreads();                 // ... for every thread of the block
+  if (tid == 0) {
+    const int prev = __hip_atomic_fetch_add(&counters[rb], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = prev == (int)(gridDim.x * gridDim.y) - 1;
+    if (last) __hip_atomic_store(&counters[rb], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!last) return;
+  head_bwd_block<true>(rb, gridDim.z, z2p, labels, B, W2T, W2N, params, dz2T, BP, partials, inv_batch, act,
+                       naive_loss, nullptr);
 }
 
 // ---------------------------------------------------------------------- B
@@ -567,6 +663,26 @@ hipError_t dtfk_mlp_l1_fwd(const void* x, int x_kind, int B, const void* W1T, fl
     case 1: hipLaunchKernelGGL(mlp_l1_fwd<1>, grid, dim3(256), 0, stream, xp, B, w, z2p, ts); break;
     default: hipLaunchKernelGGL(mlp_l1_fwd<2>, grid, dim3(256), 0, stream, xp, B, w, z2p, ts); break;
   }
+  return hipGetLastError();
+}
+
+hipError_t dtfk_mlp_fwd_head(const void* x, int x_kind, int B, const void* W1T, float* z2p, const void* labels,
+                             const void* W2T, const void* W2N, const float* params, void* dz2T, int BP,
+                             float* partials, float inv_batch, int act, int naive_loss, int* counters,
+                             hipStream_t stream) {
+  using namespace dtfk::mlp;
+  const dim3 grid(HIDP / 16, KSPLIT, (B + 15) / 16);
+  const uint8_t* xp = (const uint8_t*)x;
+#define DTFK_FH(XK)                                                                                        \
+  hipLaunchKernelGGL(mlp_fwd_head<XK>, grid, dim3(512), 0, stream, xp, B, (const uint16_t*)W1T, z2p,       \
+                     (const uint8_t*)labels, (const uint16_t*)W2T, (const uint16_t*)W2N, params,            \
+                     (uint16_t*)dz2T, BP, partials, inv_batch, act, naive_loss, counters)
+  switch (x_kind) {
+    case 0: DTFK_FH(0); break;
+    case 1: DTFK_FH(1); break;
+    default: DTFK_FH(2); break;
+  }
+#undef DTFK_FH
   return hipGetLastError();
 }
 

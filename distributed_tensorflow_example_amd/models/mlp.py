@@ -156,6 +156,10 @@ class FusedMLPTrainer:
         self.ring = int(metrics_ring)
         self.metrics = torch.zeros(self.ring * 2, dtype=torch.float32, device=dev)
         self.gstep = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.counters = torch.zeros(max(64, self.nb), dtype=torch.int32, device=dev)
+        # A1+A2 merged by last-arriver handoff: correct, but measured 13.56 vs 13.16 us/step
+        # for the split pair on MI355X (the split boundary is cheaper than the handoff), so opt-in
+        self.merged_head = os.environ.get("DTF_MLP_MERGED_HEAD", "0") == "1"
         self.allreduce = "none"
         self.ipc = None
         self.ipc_parity = 0
@@ -232,9 +236,13 @@ class FusedMLPTrainer:
         (kind 0 uint8 pixels, 1 fp32, 2 bf16); labels: uint8 class ids.
         """
         C, B = self.C, self.B
-        C.mlp_l1_fwd(x, x_off, x_kind, B, self.W1T, self.z2p)
-        C.mlp_head_bwd(self.z2p, labels, labels_off, B, self.W2T, self.W2N, self.params, self.dz2T,
-                       self.partials, 1.0 / B, self.act, self.naive)
+        if self.merged_head:   # A1+A2 in one launch (last-arriver handoff per row block)
+            C.mlp_fwd_head(x, x_off, x_kind, B, self.W1T, self.z2p, labels, labels_off, self.W2T, self.W2N,
+                           self.params, self.dz2T, self.partials, 1.0 / B, self.act, self.naive, self.counters)
+        else:
+            C.mlp_l1_fwd(x, x_off, x_kind, B, self.W1T, self.z2p)
+            C.mlp_head_bwd(self.z2p, labels, labels_off, B, self.W2T, self.W2N, self.params, self.dz2T,
+                           self.partials, 1.0 / B, self.act, self.naive)
         if self.world_size == 1:
             C.mlp_wgrad(x, x_off, x_kind, self.dz2T, B, self.partials, self.params, self.W1T,
                         self.W2T, self.W2N, None, 0, self.lr, self.metrics, self.gstep)

@@ -54,8 +54,9 @@ def main(argv=None):
     ap.add_argument("--act", choices=["sigmoid", "relu"], default="sigmoid")
     ap.add_argument("--train-examples", type=int, default=55000)
     ap.add_argument("--prefetch", choices=["serial", "side"], default="serial")
-    ap.add_argument("--allreduce", choices=["auto", "ipc", "rccl"], default="auto",
-                    help="N>1 gradient all-reduce: one-shot IPC over xGMI fused into the SGD apply, or RCCL")
+    ap.add_argument("--allreduce", choices=["auto", "ipc-fused", "ipc-apply", "rccl"], default="auto",
+                    help="N>1 gradient exchange: IPC over xGMI inside the wgrad kernel (ipc-fused, default), "
+                         "IPC one-shot in a separate reduce+apply kernel (ipc-apply), or RCCL")
     a = ap.parse_args(argv)
 
     world_size_env = int(os.environ.get("WORLD_SIZE", "1"))
@@ -111,14 +112,16 @@ def main(argv=None):
         spread = w.host_all_reduce(c, "max") - w.host_all_reduce(c, "min")
         return bad == 0.0 and spread == 0.0
 
-    trainer, runner = setup(a.allreduce)
-    if not consistent(trainer):
-        if trainer.allreduce != "ipc":
-            raise SystemExit("replicas diverged after warmup")
-        print("bench: IPC all-reduce failed validation; falling back to RCCL", file=sys.stderr, flush=True)
-        trainer, runner = setup("rccl")
-        if not consistent(trainer):
-            raise SystemExit("replicas diverged after warmup (rccl)")
+    # fallback chain: in-kernel IPC exchange -> separate IPC reduce+apply -> RCCL
+    chain = {"auto": ["ipc-fused", "ipc-apply", "rccl"], "ipc-fused": ["ipc-fused"],
+             "ipc-apply": ["ipc-apply"], "rccl": ["rccl"]}[a.allreduce] if w.world_size > 1 else ["rccl"]
+    for i, mode in enumerate(chain):
+        trainer, runner = setup(mode)
+        if consistent(trainer):
+            break
+        if i + 1 == len(chain):
+            raise SystemExit(f"replicas diverged after warmup ({trainer.allreduce})")
+        print(f"bench: {trainer.allreduce} failed validation; trying {chain[i + 1]}", file=sys.stderr, flush=True)
     step0 = trainer.global_step
 
     events = []

@@ -13,12 +13,14 @@ hipError_t dtfk_mlp_l1_fwd(const void* x, int x_kind, int B, const void* W1T, fl
                            long long* ts, hipStream_t stream);
 hipError_t dtfk_mlp_head_bwd(const float* a2, const void* labels, int B, const void* W2T,
                              const void* W2N, const float* params, void* dz2T, int BP, float* partials,
-                             float inv_batch, int act, int naive_loss, long long* ts,
+                             float inv_batch, int act, int naive_loss, long long* gstep, long long* ts,
                              hipStream_t stream);
 hipError_t dtfk_mlp_wgrad(const void* x, int x_kind, const void* dz2T, int BP, int B,
                           const float* partials, float* params, void* W1T, void* W2T, void* W2N,
                           void* grads, int grad_kind, const float* lr, float* metrics,
-                          long long* gstep, int ring, long long* ts, hipStream_t stream);
+                          long long* gstep, int ring, long long* ts, void* const* ipc_table, int ipc_W,
+                          int ipc_rank, int ipc_parity, long long ipc_slot_bytes, int* ipc_err,
+                          long long ipc_timeout, hipStream_t stream);
 hipError_t dtfk_mlp_apply_flat(float* params, const void* grads, int grad_kind, const float* lr,
                                float scale, void* W1T, void* W2T, void* W2N, hipStream_t stream);
 int dtfk_mlp_ipc_flag_bytes();
@@ -29,7 +31,7 @@ hipError_t dtfk_mlp_ipc_reduce_apply(float* params, void* const* peer_table, int
 hipError_t dtfk_mlp_fwd_head(const void* x, int x_kind, int B, const void* W1T, float* z2p, const void* labels,
                              const void* W2T, const void* W2N, const float* params, void* dz2T, int BP,
                              float* partials, float inv_batch, int act, int naive_loss, int* counters,
-                             hipStream_t stream);
+                             long long* gstep, hipStream_t stream);
 }
 
 namespace dtf {
@@ -87,7 +89,8 @@ void mlp_l1_fwd(at::Tensor x, int64_t x_off, int x_kind, int B, at::Tensor W1T, 
 // A1 + A2 in one launch (last-arriver row-block handoff); counters: int32[nb], zero at rest
 void mlp_fwd_head(at::Tensor x, int64_t x_off, int x_kind, int B, at::Tensor W1T, at::Tensor z2p, at::Tensor labels,
                   int64_t labels_off, at::Tensor W2T, at::Tensor W2N, at::Tensor params, at::Tensor dz2T,
-                  at::Tensor partials, double inv_batch, int act, bool naive_loss, at::Tensor counters) {
+                  at::Tensor partials, double inv_batch, int act, bool naive_loss, at::Tensor counters,
+                  at::Tensor gstep) {
   if (B <= 0) throw std::runtime_error("B must be positive");
   const int nb = (B + 15) / 16, BP = bp_of(B);
   const char* xb = x_ptr(x, x_off, x_kind, B);
@@ -106,13 +109,14 @@ void mlp_fwd_head(at::Tensor x, int64_t x_off, int x_kind, int B, at::Tensor W1T
                               reinterpret_cast<const uint8_t*>(labels.data_ptr()) + labels_off, W2T.data_ptr(),
                               W2N.data_ptr(), params.data_ptr<float>(), dz2T.data_ptr(), BP,
                               partials.data_ptr<float>(), (float)inv_batch, act, naive_loss ? 1 : 0,
-                              counters.data_ptr<int>(), cur_stream()),
+                              counters.data_ptr<int>(), reinterpret_cast<long long*>(gstep.data_ptr<int64_t>()),
+                              cur_stream()),
             "mlp_fwd_head");
 }
 
 void mlp_head_bwd(at::Tensor z2p, at::Tensor labels, int64_t labels_off, int B, at::Tensor W2T,
                   at::Tensor W2N, at::Tensor params, at::Tensor dz2T, at::Tensor partials, double inv_batch, int act,
-                  bool naive_loss, c10::optional<at::Tensor> ts) {
+                  bool naive_loss, at::Tensor gstep, c10::optional<at::Tensor> ts) {
   const int nb = (B + 15) / 16, BP = bp_of(B);
   need(z2p, at::kFloat, (int64_t)dtfk_mlp_ksplit() * nb * 16 * 112, "z2p");
   if (!labels.is_cuda() || labels.scalar_type() != at::kByte)
@@ -127,6 +131,7 @@ void mlp_head_bwd(at::Tensor z2p, at::Tensor labels, int64_t labels_off, int B, 
                               reinterpret_cast<const uint8_t*>(labels.data_ptr()) + labels_off, B,
                               W2T.data_ptr(), W2N.data_ptr(), params.data_ptr<float>(), dz2T.data_ptr(), BP,
                               partials.data_ptr<float>(), (float)inv_batch, act, naive_loss ? 1 : 0,
+                              reinterpret_cast<long long*>(gstep.data_ptr<int64_t>()),
                               ts_ptr(ts, (int64_t)nb * 16), cur_stream()),
             "mlp_head_bwd");
 }
@@ -135,7 +140,8 @@ void mlp_head_bwd(at::Tensor z2p, at::Tensor labels, int64_t labels_off, int B, 
 void mlp_wgrad(at::Tensor x, int64_t x_off, int x_kind, at::Tensor dz2T, int B,
                at::Tensor partials, at::Tensor params, at::Tensor W1T, at::Tensor W2T,
                at::Tensor W2N, c10::optional<at::Tensor> grads, int grad_kind, at::Tensor lr, at::Tensor metrics,
-               at::Tensor gstep, c10::optional<at::Tensor> ts) {
+               at::Tensor gstep, c10::optional<at::Tensor> ts, int64_t ipc_table, int ipc_W, int ipc_rank,
+               int ipc_parity, int64_t ipc_slot_bytes, c10::optional<at::Tensor> ipc_err, double ipc_timeout_s) {
   const int nb = (B + 15) / 16, BP = bp_of(B);
   if (BP > 4096) throw std::runtime_error("per-GPU batch > 4096 not supported by mlp_wgrad");
   const char* xb = x_ptr(x, x_off, x_kind, B);
@@ -149,7 +155,14 @@ void mlp_wgrad(at::Tensor x, int64_t x_off, int x_kind, at::Tensor dz2T, int B,
   need(metrics, at::kFloat, 2, "metrics");
   need(gstep, at::kLong, 1, "global_step");
   void* g = nullptr;
-  if (grad_kind != 0) {
+  int* errp = nullptr;
+  if (grad_kind == 3) {
+    if (ipc_table == 0 || ipc_W < 2 || ipc_rank < 0 || ipc_rank >= ipc_W || ipc_W > 64 || (ipc_parity & ~1) ||
+        ipc_slot_bytes < kNParam * 2 || !ipc_err.has_value())
+      throw std::runtime_error("mlp_wgrad: bad IPC arguments");
+    if (!ipc_err->is_cuda() || ipc_err->scalar_type() != at::kInt) throw std::runtime_error("ipc_err: GPU int32");
+    errp = ipc_err->data_ptr<int>();
+  } else if (grad_kind != 0) {
     if (!grads.has_value()) throw std::runtime_error("grads required");
     need(*grads, grad_kind == 1 ? at::kFloat : at::kBFloat16, kNParam, "grads");
     g = grads->data_ptr();
@@ -160,7 +173,9 @@ void mlp_wgrad(at::Tensor x, int64_t x_off, int x_kind, at::Tensor dz2T, int B,
                            W2N.data_ptr(), g, grad_kind,
                            lr.data_ptr<float>(), metrics.data_ptr<float>(),
                            reinterpret_cast<long long*>(gstep.data_ptr<int64_t>()), ring,
-                           ts_ptr(ts, (int64_t)(49 * 7 + 4) * 16), cur_stream()),
+                           ts_ptr(ts, (int64_t)(49 * 7 + 4) * 16), reinterpret_cast<void* const*>(ipc_table),
+                           grad_kind == 3 ? ipc_W : 0, ipc_rank, ipc_parity, ipc_slot_bytes, errp,
+                           (long long)(ipc_timeout_s * 1.0e8), cur_stream()),
             "mlp_wgrad");
 }
 
@@ -227,12 +242,14 @@ void init_mlp(py::module& m) {
   m.def("mlp_head_bwd", &mlp_head_bwd, py::arg("z2p"), py::arg("labels"), py::arg("labels_offset"),
         py::arg("B"), py::arg("W2T"), py::arg("W2N"), py::arg("params"), py::arg("dz2T"),
         py::arg("partials"),
-        py::arg("inv_batch"), py::arg("act"), py::arg("naive_loss"), py::arg("ts") = py::none());
+        py::arg("inv_batch"), py::arg("act"), py::arg("naive_loss"), py::arg("gstep"), py::arg("ts") = py::none());
   m.def("mlp_wgrad", &mlp_wgrad, py::arg("x"), py::arg("x_offset"), py::arg("x_kind"),
         py::arg("dz2T"), py::arg("B"), py::arg("partials"), py::arg("params"), py::arg("W1T"),
         py::arg("W2T"), py::arg("W2N"), py::arg("grads"), py::arg("grad_kind"), py::arg("lr"),
         py::arg("metrics"),
-        py::arg("gstep"), py::arg("ts") = py::none());
+        py::arg("gstep"), py::arg("ts") = py::none(), py::arg("ipc_table") = 0, py::arg("ipc_W") = 0,
+        py::arg("ipc_rank") = 0, py::arg("ipc_parity") = 0, py::arg("ipc_slot_bytes") = 0,
+        py::arg("ipc_err") = py::none(), py::arg("ipc_timeout_s") = 5.0);
   m.def("mlp_apply_flat", &mlp_apply_flat);
   m.def("mlp_fwd_head", &mlp_fwd_head);
   m.def("mlp_ipc_reduce_apply", &mlp_ipc_reduce_apply);

@@ -65,6 +65,10 @@ constexpr int RCH = (PART + NRED - 1) / NRED;  // 278 slab entries per reducer
 constexpr int KSPLIT = 2;              // layer-1 K halves (spreads W1 reads over 2x CUs)
 constexpr int KS_PER = 13;             // k-steps per half: [0,13) and [13,25)
 constexpr int KJ = (KS_PER + 3) / 4;   // k-steps per wave
+// IPC exchange buffer: [flag area][grad slot 0][grad slot 1]; flag area holds
+// the step flag (offset 0) and one flag per wgrad workgroup (offset 64 + 8*wg)
+constexpr int IPC_FLAG_BYTES = 4096;
+constexpr int IPC_WG_FLAG0 = 64;
 
 // debug stamps: slot ph = s_memrealtime (100 MHz), slot 8+ph = s_memtime (core clock)
 #define TS(ph)                                                                       \
@@ -175,7 +179,7 @@ __device__ __forceinline__ void head_bwd_block(
     const uint16_t* __restrict__ W2T, const uint16_t* __restrict__ W2N,
     const float* __restrict__ params, uint16_t* __restrict__ dz2T, int BP,
     float* __restrict__ partials, float inv_batch, int act, int naive_loss,
-    long long* __restrict__ ts) {
+    long long* __restrict__ gstep, long long* __restrict__ ts) {
   __shared__ __attribute__((aligned(16))) float a2f[ROWS * HIDP];      // [r][n] fp32
   __shared__ __attribute__((aligned(16))) uint16_t a2b[ROWS * A2S];    // [r][n] bf16, n<128
   __shared__ __attribute__((aligned(16))) uint16_t a2T[HIDP * D3S];    // [n][r] bf16, r<32
@@ -305,6 +309,9 @@ __device__ __forceinline__ void head_bwd_block(
     if (lane < NCLS) part[1100 + lane] = v;
     else if (lane >= 16) part[1110 + (lane - 16)] = v;
   }
+  // the device global step advances here (not in B), so B -- and the IPC
+  // exchange inside it -- sees one stable epoch value
+  if (rb == 0 && tid == 0) *gstep += 1;
 }
 
 __global__ __launch_bounds__(512) void mlp_head_bwd(
@@ -312,10 +319,10 @@ __global__ __launch_bounds__(512) void mlp_head_bwd(
     const uint16_t* __restrict__ W2T, const uint16_t* __restrict__ W2N,
     const float* __restrict__ params, uint16_t* __restrict__ dz2T, int BP,
     float* __restrict__ partials, float inv_batch, int act, int naive_loss,
-    long long* __restrict__ ts) {
+    long long* __restrict__ gstep, long long* __restrict__ ts) {
   TS(0);
   head_bwd_block<false>(blockIdx.x, gridDim.x, z2p, labels, B, W2T, W2N, params, dz2T, BP, partials, inv_batch,
-                        act, naive_loss, ts);
+                        act, naive_loss, gstep, ts);
   TS(3);
 }
 
@@ -333,7 +340,7 @@ __global__ __launch_bounds__(512) void mlp_fwd_head(
     const uint8_t* __restrict__ xin, int B, const uint16_t* __restrict__ W1T, float* __restrict__ z2p,
     const uint8_t* __restrict__ labels, const uint16_t* __restrict__ W2T, const uint16_t* __restrict__ W2N,
     const float* __restrict__ params, uint16_t* __restrict__ dz2T, int BP, float* __restrict__ partials,
-    float inv_batch, int act, int naive_loss, int* __restrict__ counters) {
+    float inv_batch, int act, int naive_loss, int* __restrict__ counters, long long* __restrict__ gstep) {
   __shared__ float red8[8][16][17];
   __shared__ int last;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -387,19 +394,66 @@ __global__ __launch_bounds__(512) void mlp_fwd_head(
   __syncthreads();
   if (!last) return;
   head_bwd_block<true>(rb, gridDim.z, z2p, labels, B, W2T, W2N, params, dz2T, BP, partials, inv_batch, act,
-                       naive_loss, nullptr);
+                       naive_loss, gstep, nullptr);
+}
+
+// ---------------------------------------------------------------------- IPC (in-B exchange)
+struct IpcArgs {
+  void* const* peer_base;   // W base pointers of the exchange buffers (own + mapped peers)
+  int W, rank, parity;
+  long long slot_bytes;
+  float scale;              // 1 / W
+  int* err;
+  long long timeout;        // s_memrealtime ticks
+};
+
+__device__ __forceinline__ uint16_t* ipc_slot(const IpcArgs& a, int r) {
+  return reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(a.peer_base[r]) + IPC_FLAG_BYTES +
+                                     (long long)a.parity * a.slot_bytes);
+}
+
+// Single-wave workgroup `wg` publishes its epoch flag after its gradient
+// stores (uncached exchange memory: completion == visibility, no L2 writeback
+// needed), then lane r waits for peer r's flag of the same workgroup -- the W
+// remote polls overlap.  Returns false (and raises err) on timeout.
+__device__ __forceinline__ bool ipc_wg_sync(const IpcArgs& a, int wg, unsigned long long epoch, int lane) {
+  __builtin_amdgcn_s_waitcnt(0);
+  const long long off = IPC_WG_FLAG0 + 8LL * wg;
+  if (lane == 0)
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(a.peer_base[a.rank]) + off),
+                       epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  int good = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
+  if (good && lane < a.W && lane != a.rank) {
+    const unsigned long long* f =
+        reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(a.peer_base[lane]) + off);
+    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
+      __builtin_amdgcn_s_sleep(1);
+      if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) {
+        atomicOr(a.err, 1);
+        good = 0;
+        break;
+      }
+    }
+  }
+  return __all(good);
 }
 
 // ---------------------------------------------------------------------- B
 // grid: NSTRIP*7 tile workgroups (16-row strip of dW1 x 16-column tile) + NRED
-template <int KSTEPS, int XK, bool FUSED>  // KSTEPS > 0: K = 32*KSTEPS; 0: runtime BP
+// MODE 0: fused SGD (1 GPU); 1: gradients to a flat bucket (RCCL); 2: IPC --
+// every workgroup exchanges its own gradient block with the same workgroup on
+// all peer GPUs and applies SGD in place (no separate all-reduce/apply launch).
+template <int KSTEPS, int XK, int MODE>  // KSTEPS > 0: K = 32*KSTEPS; 0: runtime BP
 __global__ __launch_bounds__(64) void mlp_wgrad(
     const uint8_t* __restrict__ xin, const uint16_t* __restrict__ dz2T, int BP, int B,
     const float* __restrict__ partials, int nblk_rows, float* __restrict__ params,
     uint16_t* __restrict__ W1T, uint16_t* __restrict__ W2T, uint16_t* __restrict__ W2N,
     void* __restrict__ grads, int grad_bf16, const float* __restrict__ lr_ptr,
     float* __restrict__ metrics, long long* __restrict__ gstep, int ring,
-    long long* __restrict__ ts) {
+    long long* __restrict__ ts, IpcArgs ipc) {
+  constexpr bool FUSED = MODE == 0;
+  constexpr bool NEEDP = MODE != 1;     // master params read for an in-kernel update
   TS(0);
   extern __shared__ __attribute__((aligned(16))) uint16_t xt[];  // [16][BP + 8] bf16
   const int lane = threadIdx.x;
@@ -414,7 +468,7 @@ __global__ __launch_bounds__(64) void mlp_wgrad(
     const int XTS = BP + 8;
     float pm[4];
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    if constexpr (FUSED) {  // master W1 for the SGD epilogue, issued first
+    if constexpr (NEEDP) {  // master W1 for the SGD epilogue, issued first
 #pragma unroll
       for (int i = 0; i < 4; ++i) pm[i] = params[OFF_W1 + (kr + i) * HID + min(n, HID - 1)];
     }
@@ -458,6 +512,37 @@ __global__ __launch_bounds__(64) void mlp_wgrad(
         acc = mfma16x16x32(ld_bf16x8(xt + lr * XTS + kb + lh * 8), ld_bf16x8(pb + kb), acc);
     }
     TS(2);
+    if constexpr (MODE == 2) {
+      const unsigned long long epoch = (unsigned long long)(*gstep);
+      const int nc = min(n, HID - 1);
+      uint16_t gb[4];
+      uint16_t* mine = ipc_slot(ipc, ipc.rank);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        gb[i] = f2bf(acc[i]);
+        if (n < HID) mine[OFF_W1 + (kr + i) * HID + n] = gb[i];
+      }
+      if (!ipc_wg_sync(ipc, blockIdx.x, epoch, lane)) return;
+      float g[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int r = 0; r < ipc.W; ++r) {   // rank order: identical sums on every GPU
+        const uint16_t* src = ipc_slot(ipc, r);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          g[i] += bf2f(r == ipc.rank ? gb[i] : __builtin_nontemporal_load(src + OFF_W1 + (kr + i) * HID + nc));
+      }
+      if (n < HID) {
+        const float step = (*lr_ptr) * ipc.scale;
+        float p[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          p[i] = pm[i] - step * g[i];
+          params[OFF_W1 + (kr + i) * HID + n] = p[i];
+        }
+        *reinterpret_cast<uint2*>(&W1T[(size_t)n * DINP + kr]) = make_uint2(pack2bf(p[0], p[1]), pack2bf(p[2], p[3]));
+      }
+      TS(3);
+      return;
+    }
     if (n < HID) {
       if constexpr (FUSED) {
         const float lrate = *lr_ptr;
@@ -497,7 +582,7 @@ __global__ __launch_bounds__(64) void mlp_wgrad(
       const int i = min(lo + lane + 64 * u, PART - 1);
 #pragma unroll
       for (int b = 0; b < NBM; ++b) v[u][b] = partials[(size_t)min(b, nblk_rows - 1) * PART + i];
-      if constexpr (FUSED) pv[u] = params[OFF_W2 + min(i, 1109)];
+      if constexpr (NEEDP) pv[u] = params[OFF_W2 + min(i, 1109)];
     }
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
@@ -511,11 +596,40 @@ __global__ __launch_bounds__(64) void mlp_wgrad(
       const int i = min(lo + lane + 64 * u, PART - 1);
       s[u] = 0.f;
       for (int b = 0; b < nblk_rows; ++b) s[u] += partials[(size_t)b * PART + i];
-      if constexpr (FUSED) pv[u] = params[OFF_W2 + min(i, 1109)];
+      if constexpr (NEEDP) pv[u] = params[OFF_W2 + min(i, 1109)];
     }
   }
   float* lred = reinterpret_cast<float*>(xt);
   const float lrate = *lr_ptr;
+  if constexpr (MODE == 2) {   // exchange the small-parameter gradients of this reducer's range
+    const unsigned long long epoch = (unsigned long long)(*gstep);
+    uint16_t* mine = ipc_slot(ipc, ipc.rank);
+    uint16_t gb[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int i = lo + lane + 64 * u;
+      gb[u] = f2bf(s[u]);
+      if (i < hi && i < 1110) mine[OFF_W2 + i] = gb[u];
+    }
+    const bool ok = ipc_wg_sync(ipc, blockIdx.x, epoch, lane);
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int i = lo + lane + 64 * u;
+      const int ic = min(i, 1109);
+      float g = 0.f;
+      for (int r = 0; r < ipc.W; ++r)
+        g += bf2f(r == ipc.rank ? gb[u] : __builtin_nontemporal_load(ipc_slot(ipc, r) + OFF_W2 + ic));
+      if (i >= hi) continue;
+      if (i >= 1110) { lred[i - 1110] = s[u]; continue; }
+      if (!ok) continue;
+      const float p = pv[u] - lrate * ipc.scale * g;
+      params[OFF_W2 + i] = p;
+      if (i < 1000) {
+        W2T[(i % NCLS) * HIDK + i / NCLS] = f2bf(p);
+        W2N[(i / NCLS) * 32 + i % NCLS] = f2bf(p);
+      }
+    }
+  } else {
 #pragma unroll
   for (int u = 0; u < NU; ++u) {
     const int i = lo + lane + 64 * u;
@@ -534,14 +648,14 @@ __global__ __launch_bounds__(64) void mlp_wgrad(
       reinterpret_cast<float*>(grads)[OFF_W2 + i] = s[u];
     }
   }
+  }
   if (hi == PART) {
     __syncthreads();
     if (lane == 0) {
-      const long long st = *gstep;
+      const long long st = *gstep - 1;   // the head kernel already advanced the step
       const int slot = (int)(st % ring);
       metrics[2 * slot] = lred[0] / (float)B;
       metrics[2 * slot + 1] = lred[1] / (float)B;
-      *gstep = st + 1;
     }
   }
   TS(3);
@@ -584,8 +698,6 @@ __global__ __launch_bounds__(256) void mlp_apply_flat(
 // ring's 2(N-1) latency-bound hops.  Double-buffered by step parity: a rank
 // rewrites slot p only after its next apply saw every peer's flag for the
 // step in between, i.e. after every peer finished reading slot p.
-constexpr int IPC_FLAG_BYTES = 256;
-
 __global__ __launch_bounds__(256) void mlp_ipc_reduce_apply(
     float* __restrict__ params, void* const* __restrict__ peer_base, int W, int rank, int parity,
     long long slot_bytes, const long long* __restrict__ gstep, const float* __restrict__ lr_ptr, float scale,
@@ -593,26 +705,26 @@ __global__ __launch_bounds__(256) void mlp_ipc_reduce_apply(
     long long timeout_ticks) {
   __shared__ int ok;
   const unsigned long long epoch = (unsigned long long)(*gstep);
-  if (threadIdx.x == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
-    ok = 0;                                  // a previous step timed out: fail fast, never wait again
-  } else if (threadIdx.x == 0) {
+  if (threadIdx.x == 0) {
+    ok = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;  // fail fast after a timeout
     __threadfence_system();
-    unsigned long long* mine = reinterpret_cast<unsigned long long*>(peer_base[rank]);
-    __hip_atomic_store(mine, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    int good = 1;
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(peer_base[rank]), epoch, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __syncthreads();
+  // lane r polls peer r's flag: the W remote round trips overlap instead of
+  // running back to back (~1 us each over xGMI)
+  if (ok && threadIdx.x < W) {
+    const unsigned long long* f = reinterpret_cast<const unsigned long long*>(peer_base[threadIdx.x]);
     const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-    for (int r = 0; r < W && good; ++r) {
-      const unsigned long long* f = reinterpret_cast<const unsigned long long*>(peer_base[r]);
-      while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
-        __builtin_amdgcn_s_sleep(1);
-        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
-          good = 0;
-          atomicOr(err, 1);
-          break;
-        }
+    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
+      __builtin_amdgcn_s_sleep(1);
+      if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
+        atomicOr(err, 1);
+        ok = 0;
+        break;
       }
     }
-    ok = good;
   }
   __syncthreads();
   if (!ok) return;
@@ -669,14 +781,14 @@ hipError_t dtfk_mlp_l1_fwd(const void* x, int x_kind, int B, const void* W1T, fl
 hipError_t dtfk_mlp_fwd_head(const void* x, int x_kind, int B, const void* W1T, float* z2p, const void* labels,
                              const void* W2T, const void* W2N, const float* params, void* dz2T, int BP,
                              float* partials, float inv_batch, int act, int naive_loss, int* counters,
-                             hipStream_t stream) {
+                             long long* gstep, hipStream_t stream) {
   using namespace dtfk::mlp;
   const dim3 grid(HIDP / 16, KSPLIT, (B + 15) / 16);
   const uint8_t* xp = (const uint8_t*)x;
 #define DTFK_FH(XK)                                                                                        \
   hipLaunchKernelGGL(mlp_fwd_head<XK>, grid, dim3(512), 0, stream, xp, B, (const uint16_t*)W1T, z2p,       \
                      (const uint8_t*)labels, (const uint16_t*)W2T, (const uint16_t*)W2N, params,            \
-                     (uint16_t*)dz2T, BP, partials, inv_batch, act, naive_loss, counters)
+                     (uint16_t*)dz2T, BP, partials, inv_batch, act, naive_loss, counters, gstep)
   switch (x_kind) {
     case 0: DTFK_FH(0); break;
     case 1: DTFK_FH(1); break;
@@ -689,30 +801,34 @@ hipError_t dtfk_mlp_fwd_head(const void* x, int x_kind, int B, const void* W1T, 
 hipError_t dtfk_mlp_head_bwd(const float* z2p, const void* labels, int B, const void* W2T,
                              const void* W2N, const float* params, void* dz2T, int BP,
                              float* partials, float inv_batch, int act, int naive_loss,
-                             long long* ts, hipStream_t stream) {
+                             long long* gstep, long long* ts, hipStream_t stream) {
   using namespace dtfk::mlp;
   hipLaunchKernelGGL(mlp_head_bwd, dim3((B + 15) / 16), dim3(512), 0, stream, z2p,
                      (const uint8_t*)labels, B, (const uint16_t*)W2T, (const uint16_t*)W2N, params,
-                     (uint16_t*)dz2T, BP, partials, inv_batch, act, naive_loss, ts);
+                     (uint16_t*)dz2T, BP, partials, inv_batch, act, naive_loss, gstep, ts);
   return hipGetLastError();
 }
 
-// grad_kind: 0 fused SGD, 1 fp32 grads, 2 bf16 grads
+// grad_kind: 0 fused SGD, 1 fp32 grads, 2 bf16 grads, 3 IPC exchange + SGD (ipc_* args)
 hipError_t dtfk_mlp_wgrad(const void* x, int x_kind, const void* dz2T, int BP, int B,
                           const float* partials, float* params, void* W1T, void* W2T, void* W2N,
                           void* grads, int grad_kind, const float* lr, float* metrics,
-                          long long* gstep, int ring, long long* ts, hipStream_t stream) {
+                          long long* gstep, int ring, long long* ts, void* const* ipc_table, int ipc_W,
+                          int ipc_rank, int ipc_parity, long long ipc_slot_bytes, int* ipc_err,
+                          long long ipc_timeout, hipStream_t stream) {
   using namespace dtfk::mlp;
   const dim3 grid(NSTRIP * 7 + NRED), block(64);
   const size_t lds = (size_t)16 * (BP + 8) * sizeof(uint16_t);
   const int gb = grad_kind == 2 ? 1 : 0;
-#define DTFK_WG(KS, XK, F)                                                                        \
-  hipLaunchKernelGGL((mlp_wgrad<KS, XK, F>), grid, block, lds, stream, (const uint8_t*)x,         \
+  IpcArgs ipc{ipc_table, ipc_W, ipc_rank, ipc_parity, ipc_slot_bytes, ipc_W > 0 ? 1.f / ipc_W : 1.f, ipc_err,
+              ipc_timeout};
+#define DTFK_WG(KS, XK, M)                                                                        \
+  hipLaunchKernelGGL((mlp_wgrad<KS, XK, M>), grid, block, lds, stream, (const uint8_t*)x,         \
                      (const uint16_t*)dz2T, BP, B, partials, (B + 15) / 16, params,               \
                      (uint16_t*)W1T, (uint16_t*)W2T, (uint16_t*)W2N, grads, gb, lr, metrics, gstep, \
-                     ring, ts)
+                     ring, ts, ipc)
 #define DTFK_WG_F(KS, XK) \
-  if (grad_kind == 0) DTFK_WG(KS, XK, true); else DTFK_WG(KS, XK, false)
+  if (grad_kind == 0) DTFK_WG(KS, XK, 0); else if (grad_kind == 3) DTFK_WG(KS, XK, 2); else DTFK_WG(KS, XK, 1)
 #define DTFK_WG_X(KS)                         \
   switch (x_kind) {                           \
     case 0: DTFK_WG_F(KS, 0); break;          \

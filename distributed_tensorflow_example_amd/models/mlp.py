@@ -163,15 +163,17 @@ class FusedMLPTrainer:
         self.allreduce = "none"
         self.ipc = None
         self.ipc_parity = 0
+        self.ipc_mode = None
         self.ipc_timeout_s = float(ipc_timeout_s)
         if self.world_size > 1:
             self.allreduce = "rccl"
-            if allreduce in ("ipc", "auto"):
+            if allreduce in ("ipc", "ipc-fused", "ipc-apply", "auto"):
                 try:
                     self._setup_ipc()
-                    self.allreduce = "ipc"
+                    self.ipc_mode = "apply" if allreduce == "ipc-apply" else "fused"
+                    self.allreduce = "ipc-" + self.ipc_mode
                 except Exception as e:  # noqa: BLE001
-                    if allreduce == "ipc":
+                    if allreduce.startswith("ipc"):
                         raise
                     import warnings
 
@@ -238,25 +240,34 @@ class FusedMLPTrainer:
         C, B = self.C, self.B
         if self.merged_head:   # A1+A2 in one launch (last-arriver handoff per row block)
             C.mlp_fwd_head(x, x_off, x_kind, B, self.W1T, self.z2p, labels, labels_off, self.W2T, self.W2N,
-                           self.params, self.dz2T, self.partials, 1.0 / B, self.act, self.naive, self.counters)
+                           self.params, self.dz2T, self.partials, 1.0 / B, self.act, self.naive, self.counters,
+                           self.gstep)
         else:
             C.mlp_l1_fwd(x, x_off, x_kind, B, self.W1T, self.z2p)
             C.mlp_head_bwd(self.z2p, labels, labels_off, B, self.W2T, self.W2N, self.params, self.dz2T,
-                           self.partials, 1.0 / B, self.act, self.naive)
+                           self.partials, 1.0 / B, self.act, self.naive, self.gstep)
         if self.world_size == 1:
             C.mlp_wgrad(x, x_off, x_kind, self.dz2T, B, self.partials, self.params, self.W1T,
                         self.W2T, self.W2N, None, 0, self.lr, self.metrics, self.gstep)
         elif self.ipc is not None:
-            # one-shot: bf16 grads into this rank's exported slot, then every rank
-            # sums all peers' slots over xGMI inside the SGD apply kernel
             par = self.ipc_parity if ipc_parity is None else int(ipc_parity) & 1
             if ipc_parity is None:
                 self.ipc_parity ^= 1
-            C.mlp_wgrad(x, x_off, x_kind, self.dz2T, B, self.partials, self.params, self.W1T,
-                        self.W2T, self.W2N, self.ipc_grads[par], 2, self.lr, self.metrics, self.gstep)
-            C.mlp_ipc_reduce_apply(self.params, self.ipc.table_ptr(), self.world_size, self.world.rank, par,
-                                   self.ipc_slot, self.gstep, self.lr, 1.0 / self.world_size, self.W1T, self.W2T,
-                                   self.W2N, self.ipc_err, self.ipc_timeout_s)
+            if self.ipc_mode == "fused":
+                # every wgrad workgroup swaps its gradient block with the same workgroup
+                # on all peers (IPC over xGMI) and applies SGD in place: 3 launches/step
+                C.mlp_wgrad(x, x_off, x_kind, self.dz2T, B, self.partials, self.params, self.W1T,
+                            self.W2T, self.W2N, None, 3, self.lr, self.metrics, self.gstep, None,
+                            self.ipc.table_ptr(), self.world_size, self.world.rank, par, self.ipc_slot,
+                            self.ipc_err, self.ipc_timeout_s)
+            else:
+                # one-shot: bf16 grads into this rank's exported slot, then every rank
+                # sums all peers' slots over xGMI inside the SGD apply kernel
+                C.mlp_wgrad(x, x_off, x_kind, self.dz2T, B, self.partials, self.params, self.W1T,
+                            self.W2T, self.W2N, self.ipc_grads[par], 2, self.lr, self.metrics, self.gstep)
+                C.mlp_ipc_reduce_apply(self.params, self.ipc.table_ptr(), self.world_size, self.world.rank, par,
+                                       self.ipc_slot, self.gstep, self.lr, 1.0 / self.world_size, self.W1T,
+                                       self.W2T, self.W2N, self.ipc_err, self.ipc_timeout_s)
         else:
             kind = 1 if self.grad_dtype == torch.float32 else 2
             C.mlp_wgrad(x, x_off, x_kind, self.dz2T, B, self.partials, self.params, self.W1T,

@@ -40,7 +40,7 @@ def main():
     dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=ws,
                             timeout=datetime.timedelta(seconds=120))
     w = World(rank=rank, world_size=ws, local_rank=rank, device=dev, backend="gloo", pg_initialized=True)
-    tr = mlp.FusedMLPTrainer(batch_size=100, lr=0.05, world=w, device=dev, allreduce="ipc", ipc_timeout_s=5.0)
+    tr = mlp.FusedMLPTrainer(batch_size=100, lr=0.05, world=w, device=dev, allreduce=os.environ.get("DTF_IPC_MODE", "ipc-fused"), ipc_timeout_s=5.0)
     g = torch.Generator().manual_seed(7)
     xs = torch.randint(0, 256, (a.steps, ws, 100, 784), generator=g, dtype=torch.uint8)
     ys = torch.randint(0, 10, (a.steps, ws, 100), generator=g)

@@ -52,7 +52,7 @@ def main():
 
     def A2(ts=None):
         C.mlp_head_bwd(tr.z2p, y, 0, B, tr.W2T, tr.W2N, tr.params, tr.dz2T, tr.partials, 1.0 / B, 0,
-                       False, ts)
+                       False, tr.gstep, ts)
 
     def A(ts=None):
         A1(None if ts is None else ts[0])

@@ -21,12 +21,13 @@ def _port():
     return p
 
 
+@pytest.mark.parametrize("mode", ["ipc-fused", "ipc-apply"])
 @pytest.mark.parametrize("nproc", [2, 3])
-def test_ipc_allreduce_same_gpu(native, nproc):
+def test_ipc_allreduce_same_gpu(native, nproc, mode):
     cmd = [sys.executable, "-m", "torch.distributed.run", f"--nproc-per-node={nproc}", "--master-addr=127.0.0.1",
            f"--master-port={_port()}", os.path.join(REPO, "scripts", "ipc_selftest.py"), "--same-gpu",
            "--steps=12"]
-    env = dict(os.environ, PYTHONPATH=REPO, OMP_NUM_THREADS="2")
+    env = dict(os.environ, PYTHONPATH=REPO, OMP_NUM_THREADS="2", DTF_IPC_MODE=mode)
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
     out = r.stdout + r.stderr
     line = [l for l in r.stdout.splitlines() if l.startswith("{")]

@@ -59,7 +59,7 @@ def test_grad_mode_and_apply(native):
     grads = torch.zeros(mlp.NPARAM, dtype=torch.float32, device=dev)
     C = native
     C.mlp_l1_fwd(x, 0, 0, B, tr.W1T, tr.z2p)
-    C.mlp_head_bwd(tr.z2p, y, 0, B, tr.W2T, tr.W2N, tr.params, tr.dz2T, tr.partials, 1.0 / B, 0, False)
+    C.mlp_head_bwd(tr.z2p, y, 0, B, tr.W2T, tr.W2N, tr.params, tr.dz2T, tr.partials, 1.0 / B, 0, False, tr.gstep)
     C.mlp_wgrad(x, 0, 0, tr.dz2T, B, tr.partials, tr.params, tr.W1T, tr.W2T, tr.W2N, grads, 1,
                 tr.lr, tr.metrics, tr.gstep)
     torch.cuda.synchronize()

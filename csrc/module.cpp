@@ -14,6 +14,7 @@ void init_libsvm(py::module& m);
 void init_ops(py::module& m);
 void init_transformer(py::module& m);
 void init_ipc(py::module& m);
+void init_roctx(py::module& m);
 }  // namespace dtf
 
 PYBIND11_MODULE(_C, m) {
@@ -29,4 +30,5 @@ PYBIND11_MODULE(_C, m) {
   dtf::init_ops(m);
   dtf::init_transformer(m);
   dtf::init_ipc(m);
+  dtf::init_roctx(m);
 }

@@ -60,7 +60,7 @@ def write_ninja() -> str:
         f"-DTORCH_EXTENSION_NAME={EXT_NAME}", "-Wno-deprecated-declarations", "-Wno-unused-result",
         f"-I{ROCM}/include", f"-I{py_inc}",
     ] + [f"-I{p}" for p in inc] + common_inc
-    ldflags = ["-shared", f"-L{ROCM}/lib", "-lamdhip64", "-lrccl", "-lroctx64"]
+    ldflags = ["-shared", f"-L{ROCM}/lib", "-lamdhip64", "-lrccl", "-lroctx64", "-lrocprofiler-sdk-roctx"]
     for d in libdirs:
         ldflags += [f"-L{d}", f"-Wl,-rpath,{d}"]
     ldflags += ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python", "-lpthread"]

@@ -63,6 +63,8 @@ class Session:
         self.config = config
         self._closed = False
         self._ctx_stack = []
+        self._post_run = []
+        self._in_post = False
 
     # ---------------------------------------------------------------- run
     def run(self, fetches, feed_dict=None, options: RunOptions = None, run_metadata=None):
@@ -72,6 +74,15 @@ class Session:
         ctx.session = self
         ctx.options = options
         out = self._run(fetches, ctx)
+        if self._post_run and not self._in_post:
+            # step-boundary services (Supervisor checkpoints): run in the training
+            # thread between steps, never concurrently with a train op
+            self._in_post = True
+            try:
+                for cb in list(self._post_run):
+                    cb(self)
+            finally:
+                self._in_post = False
         return out
 
     def _run(self, f, ctx):

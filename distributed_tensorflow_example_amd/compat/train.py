@@ -24,6 +24,8 @@ import numpy as np
 import torch
 
 from .. import optim as _optim
+from ..utils import debug as _debug
+from ..utils import profiling as _prof
 from ..parallel import world as _world
 from ..parallel.cluster import ClusterSpec, Rendezvous, split_address
 from ..utils import logging as _log
@@ -82,12 +84,38 @@ class Server:
             get_default_graph().device = self.world.device
         self.rdv.start_heartbeat()
         self._done = False
+        self._start_watchdog()
         _SERVER = self
         atexit.register(self._atexit)
 
     @property
     def is_chief(self) -> bool:
         return self.rdv.is_chief
+
+    def _start_watchdog(self):
+        """Failure detection: a worker whose peer stopped heart-beating aborts its
+        RCCL communicator and exits non-zero instead of blocking forever in a
+        collective (the launcher then tears the job down; restart resumes from
+        the last checkpoint).  DTF_PEER_TIMEOUT seconds (0 disables)."""
+        stale = float(os.environ.get("DTF_PEER_TIMEOUT", "60"))
+        if stale <= 0 or not self.rdv.is_worker or self.rdv.num_workers < 2:
+            return
+
+        def watch():
+            while not self._done:
+                time.sleep(min(2.0, stale / 4))
+                try:
+                    dead = [d for d in self.rdv.dead_workers(stale_s=stale) if d != self.task_index]
+                except Exception:  # noqa: BLE001 - store gone: chief exited
+                    return
+                if dead and not self._done:
+                    _log.error(f"[{self.job_name}:{self.task_index}] workers {dead} stopped responding; aborting")
+                    try:
+                        if self.world is not None and self.world.comm is not None:
+                            self.world.comm.abort()
+                    finally:
+                        os._exit(3)
+        threading.Thread(target=watch, daemon=True, name="dtf-watchdog").start()
 
     def start(self):
         return self
@@ -272,6 +300,7 @@ class Optimizer:
         self._kw = kw
         self.sync_replicas = True
         self.comm_dtype = None
+        self._steps = 0
 
     def _make_fused(self, params):
         lr = float(self._lr_value())
@@ -330,11 +359,16 @@ class Optimizer:
         sync = _GradSync(params, opt.comm_dtype) if params else None
 
         def run(ctx):
-            ws = _world_or_local().world_size
+            w = _world_or_local()
+            ws = w.world_size
+            opt._steps += 1
+            _debug.fault_point(opt._steps, w.rank)
             if fused is not None:
-                gs = [ctx.eval(g) if g is not None else None for g in gtens]
+                with _prof.range("compute_gradients"):
+                    gs = [ctx.eval(g) if g is not None else None for g in gtens]
                 if opt.sync_replicas:
-                    gs = sync(gs)
+                    with _prof.range("allreduce"):
+                        gs = sync(gs)
                 else:
                     gs = [g if g is not None else torch.zeros_like(p) for g, p in zip(gs, params)]
                 if isinstance(opt.learning_rate, Tensor):
@@ -348,6 +382,9 @@ class Optimizer:
             if global_step is not None:
                 with torch.no_grad():
                     global_step.value.data += 1
+            n = _debug.check_every()
+            if n and opt._steps % n == 0:
+                _debug.assert_replicas_consistent(w, params + [p.value for _, p in sparse_pairs], opt.name)
             return None
         op = Operation(None, [], name or self.name)
         op._eval = run
@@ -601,6 +638,8 @@ class Supervisor:
         self.saver = (Saver() if logdir else None) if saver is self.USE_DEFAULT else saver
         self.summary_op = None if summary_op is self.USE_DEFAULT else summary_op
         self.save_model_secs = save_model_secs
+        self.save_model_steps = int(kw.pop("save_model_steps", 0) or 0)
+        self._last_saved = None
         self.save_summaries_secs = save_summaries_secs
         self.checkpoint_basename = checkpoint_basename
         self.coord = Coordinator()
@@ -619,19 +658,51 @@ class Supervisor:
         _init_or_restore(sess, self.is_chief, self.init_op, self.local_init_op, self.init_fn,
                          self.logdir, self.saver, self.init_feed_dict)
         self._sess = sess
-        if start_standard_services and self.is_chief and self.logdir:
+        if start_standard_services and self.logdir:
             self._start_services(sess)
         return sess
 
+    def _collective_save(self) -> bool:
+        """Sharded (partitioned) variables make a save collective: every rank
+        writes its shard.  Otherwise only the chief writes."""
+        w = _world._WORLD
+        return w is not None and w.world_size > 1 and any(_is_pv(v) for v in global_variables())
+
+    def _save(self, sess):
+        self.saver.save(sess, self.save_path, global_step=self._gstep(sess))
+
     def _start_services(self, sess):
-        if self.saver is not None and self.save_model_secs:
-            def ckpt_loop():
-                while not self.coord.wait_for_stop(self.save_model_secs):
-                    self.saver.save(sess, self.save_path, global_step=self._gstep(sess))
-            t = threading.Thread(target=ckpt_loop, daemon=True, name="sv-checkpoint")
-            t.start()
-            self._threads.append(t)
-        if self.summary_op is not None and self.summary_writer is not None and self.save_summaries_secs:
+        """Checkpoints are taken at step boundaries by a post-run callback in the
+        training thread (a timer only raises the flag): a checkpoint never mixes
+        parameters of two steps.  `save_model_steps` (extension) gives a
+        deterministic cadence every rank agrees on -- required for collective
+        saves of sharded tables."""
+        if self.saver is not None and (self.save_model_secs or self.save_model_steps):
+            collective = self._collective_save()
+            if self.save_model_steps:
+                def on_step(s):
+                    g = self._gstep(s)
+                    if g and g % self.save_model_steps == 0 and g != self._last_saved:
+                        self._last_saved = g
+                        self._save(s)
+                sess._post_run.append(on_step)
+            elif self.is_chief and not collective:
+                due = threading.Event()
+
+                def timer():
+                    while not self.coord.wait_for_stop(self.save_model_secs):
+                        due.set()
+                t = threading.Thread(target=timer, daemon=True, name="sv-checkpoint-timer")
+                t.start()
+                self._threads.append(t)
+
+                def on_run(s):
+                    if due.is_set():
+                        due.clear()
+                        self._save(s)
+                sess._post_run.append(on_run)
+        if self.is_chief and self.summary_op is not None and self.summary_writer is not None and \
+                self.save_summaries_secs:
             def sum_loop():
                 while not self.coord.wait_for_stop(self.save_summaries_secs):
                     try:
@@ -643,7 +714,12 @@ class Supervisor:
             self._threads.append(t)
 
     def _gstep(self, sess):
-        return int(np.asarray(sess.run(self.global_step))) if self.global_step is not None else None
+        gs = self.global_step
+        if gs is None:
+            return None
+        if isinstance(gs, Variable):          # readable after the session closed (sv.stop())
+            return int(float(gs.value.detach().reshape(-1)[0]))
+        return int(np.asarray(sess.run(gs)))
 
     @contextlib.contextmanager
     def managed_session(self, master="", config=None, start_standard_services=True, close_summary_writer=True):
@@ -676,8 +752,10 @@ class Supervisor:
         self.coord.request_stop()
         for t in self._threads:
             t.join(5)
-        if self.is_chief and self.saver is not None and self._sess is not None and self.logdir:
-            self.saver.save(self._sess, self.save_path, global_step=self._gstep(self._sess))
+        if self.saver is not None and self._sess is not None and self.logdir and \
+                (self.is_chief or self._collective_save()):
+            self._sess._post_run.clear()
+            self._save(self._sess)
         if close_summary_writer and self.summary_writer is not None:
             self.summary_writer.close()
         srv = current_server()

@@ -35,6 +35,7 @@ import numpy as np  # noqa: E402
 import distributed_tensorflow_example_amd.compat as tf  # noqa: E402
 from distributed_tensorflow_example_amd.data import mnist as mnist_data  # noqa: E402
 from distributed_tensorflow_example_amd.utils.logging import step_line  # noqa: E402
+from distributed_tensorflow_example_amd.utils.metrics import MetricsWriter  # noqa: E402
 
 flags = tf.app.flags
 flags.DEFINE_string("job_name", "", "Either 'ps' or 'worker'")
@@ -52,6 +53,10 @@ flags.DEFINE_string("logs_path", "./logs/mnist", "summary root; task dir {job}_{
 flags.DEFINE_string("activation", "sigmoid", "sigmoid | relu")
 flags.DEFINE_boolean("fused", False, "run the fused MFMA train step (GPU only)")
 flags.DEFINE_string("result_json", "", "write final metrics + params checksum here (tests)")
+flags.DEFINE_string("checkpoint_dir", "", "Supervisor logdir: restore on start, checkpoint while training")
+flags.DEFINE_integer("save_model_secs", 600, "checkpoint period (chief, seconds)")
+flags.DEFINE_integer("save_model_steps", 0, "checkpoint every N global steps (all ranks agree; overrides secs)")
+flags.DEFINE_string("metrics_jsonl", "", "append JSON-lines step metrics here")
 FLAGS = flags.FLAGS
 
 
@@ -101,11 +106,19 @@ def build_graph(cluster, task_index):
 
 def run_graph_worker(server, mnist, logs_path):
     g = build_graph(server.cluster, FLAGS.task_index)
-    sv = tf.train.Supervisor(is_chief=server.is_chief, global_step=g["global_step"], init_op=g["init_op"])
+    sv_kw = {}
+    if FLAGS.checkpoint_dir:   # the reference passes no logdir, so it can never recover
+        sv_kw = dict(logdir=FLAGS.checkpoint_dir, save_model_secs=FLAGS.save_model_secs,
+                     save_model_steps=FLAGS.save_model_steps, summary_op=None)
+    sv = tf.train.Supervisor(is_chief=server.is_chief, global_step=g["global_step"], init_op=g["init_op"], **sv_kw)
     begin = time.time()
     cost = float("nan")
     steps = 0
+    mw = MetricsWriter(FLAGS.metrics_jsonl) if FLAGS.metrics_jsonl else None
     with sv.prepare_or_wait_for_session(server.target) as sess:
+        start_gstep = int(sess.run(g["global_step"]))
+        if start_gstep:
+            print(f"restored from checkpoint at global step {start_gstep}", flush=True)
         writer = tf.summary.FileWriter(logs_path, graph=tf.get_default_graph())
         batch_count = mnist.train.num_examples // FLAGS.batch_size
         t0 = time.time()
@@ -119,18 +132,23 @@ def run_graph_worker(server, mnist, logs_path):
                 writer.add_summary(summary, int(step))
                 steps += 1
                 count += 1
+                if mw is not None:
+                    mw.write("step", int(step), cost=float(cost))
                 if count % FLAGS.frequency == 0 or i + 1 == batch_count:
                     dt = time.time() - t0
                     t0 = time.time()
                     print(step_line(steps, int(sess.run(g["global_step"])), epoch + 1, i + 1, batch_count,
                                     float(cost), dt * 1000.0 / FLAGS.frequency), flush=True)
                     count = 0
-                if FLAGS.max_steps and steps >= FLAGS.max_steps:
+                if FLAGS.max_steps and int(step) >= FLAGS.max_steps:   # global steps (resume-aware)
                     done = True
                     break
             if done:
                 break
         acc = float(sess.run(g["accuracy"], feed_dict={g["x"]: mnist.test.images, g["y_"]: mnist.test.labels}))
+        if mw is not None:
+            mw.write("final", int(sess.run(g["global_step"])), accuracy=acc, cost=float(cost))
+            mw.close()
         params = [np.asarray(sess.run(v)) for v in g["W"]]
         gstep = int(sess.run(g["global_step"]))
         writer.close()

@@ -170,6 +170,8 @@ void multi_tensor_apply(at::Tensor tab, at::Tensor chunks, int kind, bool grad_b
                         c10::optional<at::Tensor> lr_t, double lr, double gscale, double wd, double b1,
                         double b2, double eps, double momentum, bool nesterov, c10::optional<at::Tensor> step) {
   gpu(tab, "table"); gpu(chunks, "chunks");
+  if (tab.dim() != 2 || tab.size(1) * 8 != dtfk_tensor_rec_bytes())
+    throw std::runtime_error("multi_tensor_apply: table rows must be TensorRec {p, g, m, v, n, shadow}");
   if (lr_t.has_value()) f32c(*lr_t, "lr");
   if (step.has_value()) i64c(*step, "step");
   ck(dtfk_multi_tensor_apply(tab.data_ptr(), chunks.data_ptr(), (int)chunks.size(0), kind, grad_bf16 ? 1 : 0,

@@ -274,6 +274,7 @@ struct TensorRec {
   float* m;
   float* v;
   int64_t n;
+  uint16_t* shadow;   // optional bf16 copy of p refreshed in the same pass (compute weights)
 };
 constexpr int CHUNK = 4096;
 
@@ -319,6 +320,7 @@ __global__ void multi_tensor_apply(const TensorRec* __restrict__ tab, const int2
       if (kind == 3 && wd != 0.f) p -= lr * wd * t.p[i];
     }
     t.p[i] = p;
+    if (t.shadow) t.shadow[i] = f2bf(p);
   }
 }
 

@@ -55,8 +55,30 @@ def _lin(o, i, std):
     return torch.nn.Parameter(torch.randn(o, i) * std)
 
 
+class _ShadowLinear(torch.autograd.Function):
+    """y = x @ w16^T with the optimizer-maintained bf16 shadow of the fp32
+    master w (no per-step cast kernels); dW comes out of the bf16 GEMM in fp32
+    directly (hipBLASLt out_dtype), straight into the DDP bucket."""
+
+    @staticmethod
+    def forward(ctx, x, w, w16):
+        ctx.save_for_backward(x, w16)
+        return F.linear(x, w16)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w16 = ctx.saved_tensors
+        gy = gy.to(w16.dtype)
+        gx = gy @ w16
+        gw = torch.mm(gy.reshape(-1, gy.shape[-1]).t(), x.reshape(-1, x.shape[-1]), out_dtype=torch.float32)
+        return gx, gw, None
+
+
 def _mm(x, w):
     """x [.., in] @ w[out, in]^T in the activation dtype (bf16 on GPU)."""
+    w16 = getattr(w, "_shadow", None)
+    if w16 is not None and x.is_cuda and x.dtype == w16.dtype:
+        return _ShadowLinear.apply(x, w, w16)
     return F.linear(x, w.to(x.dtype))
 
 
@@ -127,6 +149,24 @@ class BertForMLM(torch.nn.Module):
             self.head_g = torch.nn.Parameter(torch.ones(c.hidden))
             self.head_beta = torch.nn.Parameter(torch.zeros(c.hidden))
             self.dec_b = torch.nn.Parameter(torch.zeros(c.vocab_size))
+
+    def gemm_weights(self):
+        ws = [self.head_w, self.word]
+        for l in self.layers:
+            ws += [l.w_qkv, l.w_o, l.w_1, l.w_2]
+        return ws
+
+    def attach_shadows(self, optimizer=None):
+        """bf16 compute copies of every GEMM weight, refreshed by the fused
+        optimizer kernel in the same pass that updates the fp32 master."""
+        for w in self.gemm_weights():
+            if not hasattr(w, "_shadow"):
+                w._shadow = torch.empty_like(w, dtype=torch.bfloat16)
+            if optimizer is not None:
+                optimizer.attach_shadow(w, w._shadow)
+            else:
+                with torch.no_grad():
+                    w._shadow.copy_(w)
 
     def forward(self, input_ids, token_type, attn_mask, mlm_positions, mlm_labels):
         """Returns the mean MLM loss over the masked positions.

@@ -58,6 +58,17 @@ class _FusedBase:
         self._tab_key = None
         self._tab = None
         self._chunks = None
+        self.shadows = {}
+
+    def attach_shadow(self, param: torch.Tensor, shadow: torch.Tensor):
+        """Keep `shadow` (bf16, same layout) equal to bf16(param) after every step,
+        written by the optimizer kernel itself -- no separate cast kernels."""
+        if shadow.dtype != torch.bfloat16 or shadow.shape != param.shape or not _same_layout(param, shadow):
+            raise ValueError("shadow must be a bf16 tensor with the param's shape and layout")
+        self.shadows[id(param)] = shadow
+        with torch.no_grad():
+            shadow.copy_(param)
+        self._tab_key = None
 
     # ------------------------------------------------------------------ state
     @property
@@ -101,8 +112,10 @@ class _FusedBase:
                 if p.dtype != torch.float32 or not _dense(p) or not _same_layout(p, g) or not _dense(g):
                     raise ValueError("fused optimizer needs dense fp32 params with grads of identical layout")
                 m, v = self.m[i], self.v[i]
+                sh = self.shadows.get(id(p))
                 rows.append([p.data_ptr(), g.data_ptr(), m.data_ptr() if m is not None else 0,
-                             v.data_ptr() if v is not None else 0, p.numel()])
+                             v.data_ptr() if v is not None else 0, p.numel(),
+                             sh.data_ptr() if sh is not None else 0])
                 for s in range(0, p.numel(), chunk):
                     chunks.append([i, s])
             self._tab = torch.tensor(rows, dtype=torch.int64).to(self.device)
@@ -134,6 +147,13 @@ class _FusedBase:
                                           self.momentum, self.nesterov, self.step_t)
 
     def _step_cpu(self, grads, gs):
+        self._step_cpu_math(grads, gs)
+        for p in self.params:
+            sh = self.shadows.get(id(p))
+            if sh is not None:
+                sh.copy_(p)
+
+    def _step_cpu_math(self, grads, gs):
         lr = float(self.lr_t.item())
         t = int(self.step_t.item())
         for i, (p, g) in enumerate(zip(self.params, grads)):
@@ -202,7 +222,7 @@ def global_grad_norm(grads: List[torch.Tensor]) -> torch.Tensor:
     rows, chunks = [], []
     for i, g in enumerate(grads):
         g = g.contiguous()
-        rows.append([g.data_ptr(), g.data_ptr(), 0, 0, g.numel()])
+        rows.append([g.data_ptr(), g.data_ptr(), 0, 0, g.numel(), 0])
         for s in range(0, g.numel(), chunk):
             chunks.append([i, s])
     dev = grads[0].device

@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--model", choices=["wide_deep", "sparse_lr", "bert_base", "resnet50"], default="wide_deep")
     ap.add_argument("--seq", type=int, default=128)
     ap.add_argument("--bucket-mb", type=float, default=32.0)
+    ap.add_argument("--no-shadow", action="store_true", help="BERT: cast fp32 weights per GEMM instead")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (0 = model default)")
@@ -124,6 +125,8 @@ def dense_bench(a, w):
                "grad_allreduce": f"bucketed {a.bucket_mb}MB, overlapped", "input": "224x224 synthetic, channels_last"}
         run = lambda m, b: m.loss(*b)
     ddp = DistributedDataParallel(model, w, bucket_mb=a.bucket_mb)
+    if a.model == "bert_base" and not a.no_shadow:
+        model.attach_shadows(opt)          # after the DDP broadcast: shadows match rank 0's weights
 
     def step(b):
         ddp.zero_grad()

@@ -1,0 +1,93 @@
+// Python bindings for the fused NHWC BatchNorm(+residual)(+ReLU) kernels (csrc/kernels/bn.hip).
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+#include <stdexcept>
+#include <string>
+
+extern "C" {
+int dtfk_bn_partial_rows(int M, int C);
+hipError_t dtfk_bn_fwd(const void* x, const void* res, const float* gamma, const float* beta, void* y, float* part,
+                       float* mean, float* invstd, float* scale, float* shift, float* run_mean, float* run_var,
+                       int M, int C, float momentum, float eps, int relu, hipStream_t st);
+hipError_t dtfk_bn_apply(const void* x, const void* res, const float* scale, const float* shift, void* y, int M, int C,
+                         int relu, hipStream_t st);
+hipError_t dtfk_bn_bwd(const void* dy, const void* x, const void* res, const float* gamma, const float* mean,
+                       const float* invstd, const float* scale, const float* shift, float* part, float* coef,
+                       void* dx, void* dres, float* dgamma, float* dbeta, int M, int C, int relu, hipStream_t st);
+}
+
+namespace dtf {
+namespace {
+hipStream_t cs() { return c10::hip::getCurrentHIPStream().stream(); }
+void ck(hipError_t e, const char* w) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(w) + ": " + hipGetErrorString(e));
+}
+// NHWC bf16 activation viewed as [M, C]: channels_last 4-D or plain 2-D row-major
+int64_t rows_of(const at::Tensor& t, int64_t C) {
+  if (!t.is_cuda() || t.scalar_type() != at::kBFloat16) throw std::runtime_error("bn: bf16 GPU activations");
+  const bool ok = t.dim() == 4 ? (t.size(1) == C && t.is_contiguous(at::MemoryFormat::ChannelsLast))
+                               : (t.dim() == 2 && t.size(1) == C && t.is_contiguous());
+  if (!ok) throw std::runtime_error("bn: activation must be channels_last NCHW (or [M, C]) with C channels");
+  return t.numel() / C;
+}
+void f32(const at::Tensor& t, int64_t n, const char* w) {
+  if (!t.is_cuda() || t.scalar_type() != at::kFloat || !t.is_contiguous() || t.numel() < n)
+    throw std::runtime_error(std::string("bn: ") + w + " must be a contiguous fp32 GPU tensor");
+}
+float* optf(const c10::optional<at::Tensor>& t) { return t.has_value() ? t->data_ptr<float>() : nullptr; }
+}  // namespace
+
+int64_t bn_partial_rows(int64_t M, int64_t C) { return dtfk_bn_partial_rows((int)M, (int)C); }
+
+void bn_fwd(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor gamma, at::Tensor beta, at::Tensor y,
+            at::Tensor part, at::Tensor stats, c10::optional<at::Tensor> run_mean, c10::optional<at::Tensor> run_var,
+            double momentum, double eps, bool relu) {
+  const int64_t C = gamma.numel();
+  const int64_t M = rows_of(x, C);
+  if (rows_of(y, C) != M) throw std::runtime_error("bn_fwd: y shape");
+  if (res.has_value() && rows_of(*res, C) != M) throw std::runtime_error("bn_fwd: residual shape");
+  f32(gamma, C, "gamma"); f32(beta, C, "beta"); f32(stats, 4 * C, "stats");
+  f32(part, 2 * (int64_t)dtfk_bn_partial_rows((int)M, (int)C) * C, "part");
+  float* s = stats.data_ptr<float>();
+  ck(dtfk_bn_fwd(x.data_ptr(), res.has_value() ? res->data_ptr() : nullptr, gamma.data_ptr<float>(),
+                 beta.data_ptr<float>(), y.data_ptr(), part.data_ptr<float>(), s, s + C, s + 2 * C, s + 3 * C,
+                 optf(run_mean), optf(run_var), (int)M, (int)C, (float)momentum, (float)eps, relu ? 1 : 0, cs()),
+     "bn_fwd");
+}
+
+void bn_apply(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor scale, at::Tensor shift, at::Tensor y,
+              bool relu) {
+  const int64_t C = scale.numel();
+  const int64_t M = rows_of(x, C);
+  ck(dtfk_bn_apply(x.data_ptr(), res.has_value() ? res->data_ptr() : nullptr, scale.data_ptr<float>(),
+                   shift.data_ptr<float>(), y.data_ptr(), (int)M, (int)C, relu ? 1 : 0, cs()),
+     "bn_apply");
+}
+
+void bn_bwd(at::Tensor dy, at::Tensor x, c10::optional<at::Tensor> res, at::Tensor gamma, at::Tensor stats,
+            at::Tensor part, at::Tensor coef, at::Tensor dx, c10::optional<at::Tensor> dres, at::Tensor dgamma,
+            at::Tensor dbeta, bool relu) {
+  const int64_t C = gamma.numel();
+  const int64_t M = rows_of(x, C);
+  if (rows_of(dy, C) != M || rows_of(dx, C) != M) throw std::runtime_error("bn_bwd: shapes");
+  if (res.has_value() != dres.has_value()) throw std::runtime_error("bn_bwd: res and dres go together");
+  f32(stats, 4 * C, "stats"); f32(coef, 3 * C, "coef"); f32(dgamma, C, "dgamma"); f32(dbeta, C, "dbeta");
+  f32(part, 2 * (int64_t)dtfk_bn_partial_rows((int)M, (int)C) * C, "part");
+  const float* s = stats.data_ptr<float>();
+  ck(dtfk_bn_bwd(dy.data_ptr(), x.data_ptr(), res.has_value() ? res->data_ptr() : nullptr, gamma.data_ptr<float>(),
+                 s, s + C, s + 2 * C, s + 3 * C, part.data_ptr<float>(), coef.data_ptr<float>(), dx.data_ptr(),
+                 dres.has_value() ? dres->data_ptr() : nullptr, dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
+                 (int)M, (int)C, relu ? 1 : 0, cs()),
+     "bn_bwd");
+}
+
+void init_bn(pybind11::module& m) {
+  m.def("bn_partial_rows", &bn_partial_rows);
+  m.def("bn_fwd", &bn_fwd);
+  m.def("bn_apply", &bn_apply);
+  m.def("bn_bwd", &bn_bwd);
+}
+
+}  // namespace dtf

@@ -1,0 +1,342 @@
+// Fused BatchNorm(+residual)(+ReLU) for NHWC (channels_last) bf16 activations
+// -- the ResNet-50 path (BASELINE config #3).  MIOpen's BN needs three
+// kernels forward/backward plus separate add / ReLU / ReLU-backward passes;
+// here the normalise, affine, residual add and ReLU are one read+write pass,
+// and the backward recomputes x_hat and the ReLU mask from x instead of
+// storing them.
+//
+//   bn_partials    per-block channel sums of x and x^2        (fwd stats)
+//   bn_finalize    mean / inv-std (+ running-stat update), scale/shift
+//   bn_apply       y = relu(x * scale + shift [+ res])
+//   bn_bwd_partials per-block channel sums of g and g * x_hat, g = dy * relu'
+//   bn_bwd_finalize dgamma, dbeta, coefficients
+//   bn_bwd_apply   dx = a*g + b*x + c  (per channel), d_res = g
+//
+// Layout: x is [M, C] with M = N*H*W rows, 8 channels per thread (16-byte
+// bf16x8 accesses), C % 8 == 0.  Partial buffers are [P, C] fp32 and are
+// reduced in a fixed order (deterministic).
+#include "common.h"
+
+namespace dtfk {
+namespace bn {
+
+__device__ __forceinline__ void ld8(const uint16_t* p, float* f) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { f[2 * j] = bf2f(w[j] & 0xffff); f[2 * j + 1] = bf2f(w[j] >> 16); }
+}
+__device__ __forceinline__ void st8(uint16_t* p, const float* f) {
+  uint4 u;
+  u.x = pack2bf(f[0], f[1]); u.y = pack2bf(f[2], f[3]); u.z = pack2bf(f[4], f[5]); u.w = pack2bf(f[6], f[7]);
+  *reinterpret_cast<uint4*>(p) = u;
+}
+
+// Block = 256 threads = TPR threads per row (C/8) x RPB rows.  Every thread
+// accumulates its 8 channels over rows row0 + tr, row0 + tr + RPB*gridDim,...
+// then the RPB partials of a channel group are combined in LDS.
+__global__ __launch_bounds__(256) void bn_partials(const uint16_t* __restrict__ x, float* __restrict__ part, int M,
+                                                   int C) {
+  __shared__ float red[256 * 8];   // [RPB][C] partials of one pass (sums, then sums of squares)
+  const int TPR = C >> 3;
+  const int tid = threadIdx.x;
+  const int active = (256 / TPR) * TPR;        // threads in whole rows
+  const int RPB = 256 / TPR;
+  const int tc = tid % TPR, tr = tid / TPR;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (tid < active) {
+    for (int r = blockIdx.x * RPB + tr; r < M; r += gridDim.x * RPB) {
+      float v[8];
+      ld8(x + (size_t)r * C + tc * 8, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { s[j] += v[j]; q[j] += v[j] * v[j]; }
+    }
+  }
+  // combine the RPB rows sharing a channel group (TPR * 8 == C floats per pass)
+  float* rs = red;
+  for (int pass = 0; pass < 2; ++pass) {
+    const float* src = pass == 0 ? s : q;
+    __syncthreads();
+    if (tid < active)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) rs[(tr * TPR + tc) * 8 + j] = src[j];
+    __syncthreads();
+    for (int c = tid; c < C; c += 256) {
+      float t = 0.f;
+      for (int r = 0; r < RPB; ++r) t += rs[r * C + c];
+      part[((size_t)pass * gridDim.x + blockIdx.x) * C + c] = t;
+    }
+  }
+}
+
+// Column sums of the [2P, C] partials: 1024 threads = 64 channels x 16 row
+// groups (coalesced), LDS tree.  Returns (sum of pass 0, sum of pass 1) to the
+// g == 0 threads.
+__device__ __forceinline__ void sum_partials(const float* __restrict__ part, int P, int C, int c, int lane, int g,
+                                             double& s0, double& s1) {
+  __shared__ double red[2][16][64];
+  double a = 0.0, b = 0.0;
+  if (c < C)
+    for (int p = g; p < P; p += 16) {
+      a += part[(size_t)p * C + c];
+      b += part[((size_t)P + p) * C + c];
+    }
+  red[0][g][lane] = a;
+  red[1][g][lane] = b;
+  __syncthreads();
+  s0 = s1 = 0.0;
+  if (g == 0)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { s0 += red[0][i][lane]; s1 += red[1][i][lane]; }
+}
+
+// mean/var (double), running stats, scale = gamma*invstd, shift = beta - mean*scale.
+__global__ __launch_bounds__(1024) void bn_finalize(const float* __restrict__ part, int P, int M, int C,
+                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                    float* __restrict__ mean, float* __restrict__ invstd,
+                                                    float* __restrict__ scale, float* __restrict__ shift,
+                                                    float* __restrict__ run_mean, float* __restrict__ run_var,
+                                                    float momentum, float eps) {
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  double s, q;
+  sum_partials(part, P, C, c, lane, g, s, q);
+  if (g != 0 || c >= C) return;
+  const double mu = s / M;
+  double var = q / M - mu * mu;
+  if (var < 0.0) var = 0.0;
+  const float is = (float)(1.0 / sqrt(var + (double)eps));
+  mean[c] = (float)mu;
+  invstd[c] = is;
+  const float sc = gamma[c] * is;
+  scale[c] = sc;
+  shift[c] = beta[c] - (float)mu * sc;
+  if (run_mean) {
+    const double unbiased = M > 1 ? var * M / (M - 1) : var;
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mu;
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)unbiased;
+  }
+}
+
+template <bool RES, bool RELU>
+__global__ __launch_bounds__(256) void bn_apply(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
+                                                const float* __restrict__ scale, const float* __restrict__ shift,
+                                                uint16_t* __restrict__ y, int64_t n8, int C) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c0 = (int)((i * 8) % C);
+    float v[8], sc[8], sh[8];
+    ld8(x + i * 8, v);
+    *reinterpret_cast<float4*>(sc) = *reinterpret_cast<const float4*>(scale + c0);
+    *reinterpret_cast<float4*>(sc + 4) = *reinterpret_cast<const float4*>(scale + c0 + 4);
+    *reinterpret_cast<float4*>(sh) = *reinterpret_cast<const float4*>(shift + c0);
+    *reinterpret_cast<float4*>(sh + 4) = *reinterpret_cast<const float4*>(shift + c0 + 4);
+    float r[8];
+    if constexpr (RES) ld8(res + i * 8, r);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float o = v[j] * sc[j] + sh[j];
+      if constexpr (RES) o += r[j];
+      if constexpr (RELU) o = fmaxf(o, 0.f);
+      v[j] = o;
+    }
+    st8(y + i * 8, v);
+  }
+}
+
+// g = dy * relu'(y) with y recomputed from x (and res); partial sums of g and g*x_hat.
+template <bool RES, bool RELU>
+__global__ __launch_bounds__(256) void bn_bwd_partials(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
+                                                       const uint16_t* __restrict__ res,
+                                                       const float* __restrict__ mean,
+                                                       const float* __restrict__ invstd,
+                                                       const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, float* __restrict__ part,
+                                                       int M, int C) {
+  __shared__ float red[256 * 8];
+  const int TPR = C >> 3;
+  const int tid = threadIdx.x;
+  const int RPB = 256 / TPR;
+  const int active = RPB * TPR;
+  const int tc = tid % TPR, tr = tid / TPR;
+  float sg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sgx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (tid < active) {
+    float mu[8], is[8], sc[8], sh[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      mu[j] = mean[tc * 8 + j]; is[j] = invstd[tc * 8 + j]; sc[j] = scale[tc * 8 + j]; sh[j] = shift[tc * 8 + j];
+    }
+    for (int r = blockIdx.x * RPB + tr; r < M; r += gridDim.x * RPB) {
+      const size_t e = (size_t)r * C + tc * 8;
+      float d[8], v[8], rr[8];
+      ld8(dy + e, d);
+      ld8(x + e, v);
+      if constexpr (RES) ld8(res + e, rr);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float g = d[j];
+        if constexpr (RELU) {
+          float o = v[j] * sc[j] + sh[j];
+          if constexpr (RES) o += rr[j];
+          g = o > 0.f ? g : 0.f;
+        }
+        sg[j] += g;
+        sgx[j] += g * (v[j] - mu[j]) * is[j];
+      }
+    }
+  }
+  for (int pass = 0; pass < 2; ++pass) {
+    const float* src = pass == 0 ? sg : sgx;
+    __syncthreads();
+    if (tid < active)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[(tr * TPR + tc) * 8 + j] = src[j];
+    __syncthreads();
+    for (int c = tid; c < C; c += 256) {
+      float t = 0.f;
+      for (int r = 0; r < RPB; ++r) t += red[r * C + c];
+      part[((size_t)pass * gridDim.x + blockIdx.x) * C + c] = t;
+    }
+  }
+}
+
+// dbeta = sum g, dgamma = sum g*x_hat; dx = gamma*is*(g - dbeta/M - x_hat*dgamma/M)
+//   = A*g + B*x + Cc with A = gamma*is, B = -gamma*is^2*dgamma/M, Cc = -A*dbeta/M - B*mean
+__global__ __launch_bounds__(1024) void bn_bwd_finalize(const float* __restrict__ part, int P, int M, int C,
+                                                        const float* __restrict__ gamma,
+                                                        const float* __restrict__ mean,
+                                                        const float* __restrict__ invstd, float* __restrict__ dgamma,
+                                                        float* __restrict__ dbeta, float* __restrict__ coef) {
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  double sgd, sgxd;
+  sum_partials(part, P, C, c, lane, g, sgd, sgxd);
+  if (g != 0 || c >= C) return;
+  const float sg = (float)sgd, sgx = (float)sgxd;
+  dbeta[c] = sg;
+  dgamma[c] = sgx;
+  const float is = invstd[c];
+  const float A = gamma[c] * is;
+  const float Bc = -A * is * sgx / M;
+  coef[c] = A;
+  coef[C + c] = Bc;
+  coef[2 * C + c] = -A * sg / M - Bc * mean[c];
+}
+
+__device__ __forceinline__ void ld8f(const float* p, float* f) {
+  *reinterpret_cast<float4*>(f) = *reinterpret_cast<const float4*>(p);
+  *reinterpret_cast<float4*>(f + 4) = *reinterpret_cast<const float4*>(p + 4);
+}
+
+template <bool RES, bool RELU>
+__global__ __launch_bounds__(256) void bn_bwd_apply(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
+                                                    const uint16_t* __restrict__ res,
+                                                    const float* __restrict__ scale, const float* __restrict__ shift,
+                                                    const float* __restrict__ coef, uint16_t* __restrict__ dx,
+                                                    uint16_t* __restrict__ dres, int64_t n8, int C) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c0 = (int)((i * 8) % C);
+    float d[8], v[8], rr[8], o[8], g[8], A[8], Bv[8], Cv[8], sc[8], sh[8];
+    ld8(dy + i * 8, d);
+    ld8(x + i * 8, v);
+    if constexpr (RES) ld8(res + i * 8, rr);
+    ld8f(coef + c0, A);
+    ld8f(coef + C + c0, Bv);
+    ld8f(coef + 2 * C + c0, Cv);
+    if constexpr (RELU) {
+      ld8f(scale + c0, sc);
+      ld8f(shift + c0, sh);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float gj = d[j];
+      if constexpr (RELU) {
+        float y = v[j] * sc[j] + sh[j];
+        if constexpr (RES) y += rr[j];
+        gj = y > 0.f ? gj : 0.f;
+      }
+      g[j] = gj;
+      o[j] = A[j] * gj + Bv[j] * v[j] + Cv[j];
+    }
+    st8(dx + i * 8, o);
+    if constexpr (RES) st8(dres + i * 8, g);
+  }
+}
+
+}  // namespace bn
+}  // namespace dtfk
+
+using namespace dtfk::bn;
+
+static int bn_grid(int M, int C) {
+  const int RPB = 256 / (C / 8 > 0 ? C / 8 : 1);
+  int g = (M + RPB * 8 - 1) / (RPB * 8);     // >= 8 rows per thread
+  return g < 1 ? 1 : (g > 1024 ? 1024 : g);
+}
+static unsigned ew_grid(long long n8) {
+  long long g = (n8 + 255) / 256;
+  return (unsigned)(g > 16384 ? 16384 : (g < 1 ? 1 : g));
+}
+
+extern "C" {
+
+int dtfk_bn_partial_rows(int M, int C) { return bn_grid(M, C); }
+
+// forward: stats + finalize + apply.  part: [2 * P, C] fp32, stats: mean, invstd, scale, shift [C]
+hipError_t dtfk_bn_fwd(const void* x, const void* res, const float* gamma, const float* beta, void* y, float* part,
+                       float* mean, float* invstd, float* scale, float* shift, float* run_mean, float* run_var,
+                       int M, int C, float momentum, float eps, int relu, hipStream_t st) {
+  if (C % 8 || C > 2048) return hipErrorInvalidValue;
+  const int P = bn_grid(M, C);
+  hipLaunchKernelGGL(bn_partials, dim3(P), dim3(256), 0, st, (const uint16_t*)x, part, M, C);
+  hipLaunchKernelGGL(bn_finalize, dim3((C + 63) / 64), dim3(1024), 0, st, part, P, M, C, gamma, beta, mean, invstd,
+                     scale, shift, run_mean, run_var, momentum, eps);
+  const long long n8 = (long long)M * C / 8;
+  const uint16_t* xp = (const uint16_t*)x;
+  const uint16_t* rp = (const uint16_t*)res;
+  uint16_t* yp = (uint16_t*)y;
+  if (res && relu) hipLaunchKernelGGL((bn_apply<true, true>), dim3(ew_grid(n8)), dim3(256), 0, st, xp, rp, scale, shift, yp, n8, C);
+  else if (res) hipLaunchKernelGGL((bn_apply<true, false>), dim3(ew_grid(n8)), dim3(256), 0, st, xp, rp, scale, shift, yp, n8, C);
+  else if (relu) hipLaunchKernelGGL((bn_apply<false, true>), dim3(ew_grid(n8)), dim3(256), 0, st, xp, rp, scale, shift, yp, n8, C);
+  else hipLaunchKernelGGL((bn_apply<false, false>), dim3(ew_grid(n8)), dim3(256), 0, st, xp, rp, scale, shift, yp, n8, C);
+  return hipGetLastError();
+}
+
+// eval-mode / inference apply with given scale/shift
+hipError_t dtfk_bn_apply(const void* x, const void* res, const float* scale, const float* shift, void* y, int M, int C,
+                         int relu, hipStream_t st) {
+  if (C % 8) return hipErrorInvalidValue;
+  const long long n8 = (long long)M * C / 8;
+  const uint16_t* xp = (const uint16_t*)x;
+  const uint16_t* rp = (const uint16_t*)res;
+  uint16_t* yp = (uint16_t*)y;
+  if (res && relu) hipLaunchKernelGGL((bn_apply<true, true>), dim3(ew_grid(n8)), dim3(256), 0, st, xp, rp, scale, shift, yp, n8, C);
+  else if (res) hipLaunchKernelGGL((bn_apply<true, false>), dim3(ew_grid(n8)), dim3(256), 0, st, xp, rp, scale, shift, yp, n8, C);
+  else if (relu) hipLaunchKernelGGL((bn_apply<false, true>), dim3(ew_grid(n8)), dim3(256), 0, st, xp, rp, scale, shift, yp, n8, C);
+  else hipLaunchKernelGGL((bn_apply<false, false>), dim3(ew_grid(n8)), dim3(256), 0, st, xp, rp, scale, shift, yp, n8, C);
+  return hipGetLastError();
+}
+
+// backward.  coef: [3, C] scratch; part: [2 * P, C]
+hipError_t dtfk_bn_bwd(const void* dy, const void* x, const void* res, const float* gamma, const float* mean,
+                       const float* invstd, const float* scale, const float* shift, float* part, float* coef,
+                       void* dx, void* dres, float* dgamma, float* dbeta, int M, int C, int relu, hipStream_t st) {
+  if (C % 8 || C > 2048) return hipErrorInvalidValue;
+  const int P = bn_grid(M, C);
+  const uint16_t* dyp = (const uint16_t*)dy;
+  const uint16_t* xp = (const uint16_t*)x;
+  const uint16_t* rp = (const uint16_t*)res;
+#define DTFK_BNP(R, L) hipLaunchKernelGGL((bn_bwd_partials<R, L>), dim3(P), dim3(256), 0, st, dyp, xp, rp, mean, invstd, scale, shift, part, M, C)
+  if (res && relu) DTFK_BNP(true, true); else if (res) DTFK_BNP(true, false);
+  else if (relu) DTFK_BNP(false, true); else DTFK_BNP(false, false);
+#undef DTFK_BNP
+  hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + 63) / 64), dim3(1024), 0, st, part, P, M, C, gamma, mean, invstd,
+                     dgamma, dbeta, coef);
+  const long long n8 = (long long)M * C / 8;
+#define DTFK_BNA(R, L) hipLaunchKernelGGL((bn_bwd_apply<R, L>), dim3(ew_grid(n8)), dim3(256), 0, st, dyp, xp, rp, scale, shift, coef, (uint16_t*)dx, (uint16_t*)dres, n8, C)
+  if (res && relu) DTFK_BNA(true, true); else if (res) DTFK_BNA(true, false);
+  else if (relu) DTFK_BNA(false, true); else DTFK_BNA(false, false);
+#undef DTFK_BNA
+  return hipGetLastError();
+}
+
+}  // extern "C"

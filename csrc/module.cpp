@@ -15,6 +15,7 @@ void init_ops(py::module& m);
 void init_transformer(py::module& m);
 void init_ipc(py::module& m);
 void init_roctx(py::module& m);
+void init_bn(py::module& m);
 }  // namespace dtf
 
 PYBIND11_MODULE(_C, m) {
@@ -31,4 +32,5 @@ PYBIND11_MODULE(_C, m) {
   dtf::init_transformer(m);
   dtf::init_ipc(m);
   dtf::init_roctx(m);
+  dtf::init_bn(m);
 }

@@ -13,6 +13,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
+from ..ops.bn import FusedBatchNorm2d
 
 
 class Bottleneck(nn.Module):
@@ -22,27 +23,27 @@ class Bottleneck(nn.Module):
         super().__init__()
         cout = width * 4
         self.conv1 = nn.Conv2d(cin, width, 1, bias=False)
-        self.bn1 = nn.BatchNorm2d(width)
+        self.bn1 = FusedBatchNorm2d(width)
         self.conv2 = nn.Conv2d(width, width, 3, stride, 1, bias=False)   # v1.5: stride on the 3x3
-        self.bn2 = nn.BatchNorm2d(width)
+        self.bn2 = FusedBatchNorm2d(width)
         self.conv3 = nn.Conv2d(width, cout, 1, bias=False)
-        self.bn3 = nn.BatchNorm2d(cout)
+        self.bn3 = FusedBatchNorm2d(cout)
         nn.init.zeros_(self.bn3.weight)                                  # zero-init last BN gamma
-        self.down = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False), nn.BatchNorm2d(cout)) if down else None
+        self.down_conv = nn.Conv2d(cin, cout, 1, stride, bias=False) if down else None
+        self.down_bn = FusedBatchNorm2d(cout) if down else None
 
     def forward(self, x):
-        idt = self.down(x) if self.down is not None else x
-        y = F.relu(self.bn1(self.conv1(x)), inplace=True)
-        y = F.relu(self.bn2(self.conv2(y)), inplace=True)
-        y = self.bn3(self.conv3(y))
-        return F.relu(y + idt, inplace=True)
+        idt = self.down_bn(self.down_conv(x)) if self.down_conv is not None else x
+        y = self.bn1(self.conv1(x), relu=True)           # BN + ReLU: one fused pass
+        y = self.bn2(self.conv2(y), relu=True)
+        return self.bn3(self.conv3(y), residual=idt, relu=True)   # BN + residual add + ReLU
 
 
 class ResNet(nn.Module):
     def __init__(self, layers=(3, 4, 6, 3), num_classes=1000):
         super().__init__()
         self.conv1 = nn.Conv2d(3, 64, 7, 2, 3, bias=False)
-        self.bn1 = nn.BatchNorm2d(64)
+        self.bn1 = FusedBatchNorm2d(64)
         blocks, cin = [], 64
         for i, (n, w) in enumerate(zip(layers, (64, 128, 256, 512))):
             for j in range(n):
@@ -56,7 +57,7 @@ class ResNet(nn.Module):
 
     def forward(self, x):
         with torch.autocast(device_type="cuda", dtype=torch.bfloat16, enabled=x.is_cuda):
-            x = F.relu(self.bn1(self.conv1(x)), inplace=True)
+            x = self.bn1(self.conv1(x), relu=True)
             x = F.max_pool2d(x, 3, 2, 1)
             x = self.blocks(x)
             x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)

@@ -1,0 +1,78 @@
+"""Fused BatchNorm2d (+residual add)(+ReLU) on NHWC bf16 (csrc/kernels/bn.hip).
+
+`FusedBatchNorm2d` is a drop-in nn.BatchNorm2d whose forward takes an
+optional residual and a relu flag: in training on a channels_last bf16 GPU
+activation it runs the fused kernels (stats, normalise+affine+add+ReLU in one
+pass; backward recomputes x_hat and the ReLU mask from x); otherwise it runs
+the equivalent PyTorch ops (CPU oracle / eval / other layouts).
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from .. import _native
+
+
+def _C():
+    return _native.load()
+
+
+def _nhwc(x: torch.Tensor) -> bool:
+    return x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)
+
+
+# DTF_FUSED_BN=0 routes every layer through MIOpen's BN + separate add/ReLU (A/B runs)
+_ENABLED = os.environ.get("DTF_FUSED_BN", "1") != "0"
+
+
+class _FusedBN(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, res, running_mean, running_var, momentum, eps, relu):
+        C = _C()
+        ch = gamma.numel()
+        M = x.numel() // ch
+        y = torch.empty_like(x)
+        stats = torch.empty(4 * ch, dtype=torch.float32, device=x.device)
+        part = torch.empty(2 * C.bn_partial_rows(M, ch) * ch, dtype=torch.float32, device=x.device)
+        C.bn_fwd(x, res, gamma, beta, y, part, stats, running_mean, running_var, momentum, eps, relu)
+        ctx.save_for_backward(x, res if res is not None else torch.empty(0, device=x.device), gamma, stats)
+        ctx.has_res, ctx.relu = res is not None, relu
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = _C()
+        x, res, gamma, stats = ctx.saved_tensors
+        ch = gamma.numel()
+        M = x.numel() // ch
+        dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        dx = torch.empty_like(x)
+        dres = torch.empty_like(res) if ctx.has_res else None
+        dgamma = torch.empty(ch, dtype=torch.float32, device=x.device)
+        dbeta = torch.empty_like(dgamma)
+        coef = torch.empty(3 * ch, dtype=torch.float32, device=x.device)
+        part = torch.empty(2 * C.bn_partial_rows(M, ch) * ch, dtype=torch.float32, device=x.device)
+        C.bn_bwd(dy, x, res if ctx.has_res else None, gamma, stats, part, coef, dx, dres, dgamma, dbeta, ctx.relu)
+        return dx, dgamma, dbeta, dres, None, None, None, None, None
+
+
+class FusedBatchNorm2d(torch.nn.BatchNorm2d):
+    def forward(self, x, residual: Optional[torch.Tensor] = None, relu: bool = False):  # noqa: D401
+        fused_ok = (_ENABLED and self.training and x.is_cuda and x.dtype == torch.bfloat16 and _nhwc(x)
+                    and self.affine and x.shape[1] % 8 == 0 and x.shape[1] <= 2048
+                    and (residual is None or (residual.dtype == torch.bfloat16 and _nhwc(residual))))
+        if fused_ok:
+            if self.track_running_stats:
+                self.num_batches_tracked += 1
+            mom = self.momentum if self.momentum is not None else 0.1
+            return _FusedBN.apply(x, self.weight, self.bias, residual, self.running_mean if self.track_running_stats
+                                  else None, self.running_var if self.track_running_stats else None, float(mom),
+                                  float(self.eps), bool(relu))
+        y = super().forward(x)
+        if residual is not None:
+            y = y + residual
+        return F.relu(y) if relu else y

@@ -1,0 +1,72 @@
+"""Fused NHWC BatchNorm(+residual)(+ReLU) kernels vs a PyTorch fp32 reference."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return float((a - b).norm() / b.norm().clamp_min(1e-12))
+
+
+@pytest.mark.parametrize("C,HW", [(64, 56), (256, 14), (2048, 7), (24, 9)])
+@pytest.mark.parametrize("res,relu", [(False, True), (True, True), (False, False)])
+def test_fused_bn_matches_reference(native, C, HW, res, relu):
+    from distributed_tensorflow_example_amd.ops.bn import FusedBatchNorm2d
+
+    torch.manual_seed(C + HW)
+    N = 8
+    x = (torch.randn(N, C, HW, HW) * 2 + 0.5).bfloat16().float()
+    r = torch.randn(N, C, HW, HW).bfloat16().float() if res else None
+    bn = FusedBatchNorm2d(C)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    ref_bn = torch.nn.BatchNorm2d(C)
+    ref_bn.load_state_dict(bn.state_dict())
+    xr = x.clone().requires_grad_()
+    rr = r.clone().requires_grad_() if res else None
+    yr = ref_bn(xr)
+    if res:
+        yr = yr + rr
+    if relu:
+        yr = F.relu(yr)
+    dy = torch.randn_like(yr)
+    yr.backward(dy)
+
+    g = bn.cuda()
+    xg = x.cuda().bfloat16().contiguous(memory_format=torch.channels_last).requires_grad_()
+    rg = r.cuda().bfloat16().contiguous(memory_format=torch.channels_last).requires_grad_() if res else None
+    y = g(xg, residual=rg, relu=relu)
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    y.backward(dy.cuda().bfloat16().contiguous(memory_format=torch.channels_last))
+    assert rel(y, yr) < 1e-2
+    assert rel(xg.grad, xr.grad) < 3e-2
+    if res:
+        assert rel(rg.grad, rr.grad) < 2e-2
+    assert rel(g.weight.grad, ref_bn.weight.grad) < 2e-2
+    assert rel(g.bias.grad, ref_bn.bias.grad) < 2e-2
+    assert rel(g.running_mean, ref_bn.running_mean) < 1e-3
+    assert rel(g.running_var, ref_bn.running_var) < 1e-3
+
+
+def test_resnet50_fused_bn_step_trains(native):
+    from distributed_tensorflow_example_amd import optim
+    from distributed_tensorflow_example_amd.models.resnet import resnet50, synthetic_imagenet_batch
+
+    torch.manual_seed(0)
+    m = resnet50(num_classes=10).cuda().to(memory_format=torch.channels_last)
+    x, y = synthetic_imagenet_batch(16, "cuda", seed=1, size=64, num_classes=10)
+    opt = optim.FusedMomentum(list(m.parameters()), 0.05, 0.9)
+    losses = []
+    for _ in range(12):
+        for p in m.parameters():
+            p.grad = None
+        l = m.loss(x, y)
+        l.backward()
+        opt.step()
+        losses.append(float(l))
+    assert all(l == l for l in losses)          # no NaN
+    assert losses[-1] < losses[0]

@@ -32,41 +32,59 @@ __device__ __forceinline__ void st8(uint16_t* p, const float* f) {
   *reinterpret_cast<uint4*>(p) = u;
 }
 
-// Block = 256 threads = TPR threads per row (C/8) x RPB rows.  Every thread
-// accumulates its 8 channels over rows row0 + tr, row0 + tr + RPB*gridDim,...
-// then the RPB partials of a channel group are combined in LDS.
+// Partial-sum blocks: 256 threads = 8 channel threads (a 64-channel tile, 8
+// channels each, 128 contiguous bytes per row) x 32 row lanes.  Grid is
+// (channel tiles, P); block (t, p) covers rows p*32 + lane, stepping 32*P, four
+// rows in flight per thread.  The 32 row lanes are combined in LDS and written
+// as part[pass][p][c] (pass 0 / 1 = the two sums), so P stays small enough for
+// the finalize to read the partials in a few microseconds.
+template <typename F>
+__device__ __forceinline__ void bn_tile_rows(int M, int P, F&& f) {
+  const int tr = threadIdx.x >> 3;
+  const int stride = 32 * P;
+  int r = blockIdx.y * 32 + tr;
+  for (; r + 3 * stride < M; r += 4 * stride) {
+    f(r, r + stride, r + 2 * stride, r + 3 * stride);
+  }
+  for (; r < M; r += stride) f(r, -1, -1, -1);
+}
+
+__device__ __forceinline__ void bn_tile_store(const float* s, const float* q, float* __restrict__ part, int P, int C,
+                                              int c0) {
+  __shared__ float red[2][32][65];
+  const int tc = threadIdx.x & 7, tr = threadIdx.x >> 3;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { red[0][tr][tc * 8 + j] = s[j]; red[1][tr][tc * 8 + j] = q[j]; }
+  __syncthreads();
+  if (threadIdx.x < 128) {
+    const int pass = threadIdx.x >> 6, c = threadIdx.x & 63;
+    float t = 0.f;
+#pragma unroll 8
+    for (int i = 0; i < 32; ++i) t += red[pass][i][c];
+    if (c0 + c < C) part[((size_t)pass * P + blockIdx.y) * C + c0 + c] = t;
+  }
+}
+
 __global__ __launch_bounds__(256) void bn_partials(const uint16_t* __restrict__ x, float* __restrict__ part, int M,
                                                    int C) {
-  __shared__ float red[256 * 8];   // [RPB][C] partials of one pass (sums, then sums of squares)
-  const int TPR = C >> 3;
-  const int tid = threadIdx.x;
-  const int active = (256 / TPR) * TPR;        // threads in whole rows
-  const int RPB = 256 / TPR;
-  const int tc = tid % TPR, tr = tid / TPR;
+  const int P = gridDim.y;
+  const int c0 = blockIdx.x * 64;
+  const int cc = c0 + (threadIdx.x & 7) * 8;
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (tid < active) {
-    for (int r = blockIdx.x * RPB + tr; r < M; r += gridDim.x * RPB) {
-      float v[8];
-      ld8(x + (size_t)r * C + tc * 8, v);
+  if (cc < C)
+    bn_tile_rows(M, P, [&](int r0, int r1, int r2, int r3) {
+      float v[4][8];
+      const int rs[4] = {r0, r1, r2, r3};
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { s[j] += v[j]; q[j] += v[j] * v[j]; }
-    }
-  }
-  // combine the RPB rows sharing a channel group (TPR * 8 == C floats per pass)
-  float* rs = red;
-  for (int pass = 0; pass < 2; ++pass) {
-    const float* src = pass == 0 ? s : q;
-    __syncthreads();
-    if (tid < active)
+      for (int k = 0; k < 4; ++k)
+        if (rs[k] >= 0) ld8(x + (size_t)rs[k] * C + cc, v[k]);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) rs[(tr * TPR + tc) * 8 + j] = src[j];
-    __syncthreads();
-    for (int c = tid; c < C; c += 256) {
-      float t = 0.f;
-      for (int r = 0; r < RPB; ++r) t += rs[r * C + c];
-      part[((size_t)pass * gridDim.x + blockIdx.x) * C + c] = t;
-    }
-  }
+      for (int k = 0; k < 4; ++k)
+        if (rs[k] >= 0)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) { s[j] += v[k][j]; q[j] += v[k][j] * v[k][j]; }
+    });
+  bn_tile_store(s, q, part, P, C, c0);
 }
 
 // Column sums of the [2P, C] partials: 1024 threads = 64 channels x 16 row
@@ -76,11 +94,21 @@ __device__ __forceinline__ void sum_partials(const float* __restrict__ part, int
                                              double& s0, double& s1) {
   __shared__ double red[2][16][64];
   double a = 0.0, b = 0.0;
-  if (c < C)
-    for (int p = g; p < P; p += 16) {
+  if (c < C) {
+    int p = g;
+    for (; p + 48 < P; p += 64) {      // four independent loads per sum in flight
+      float x0 = part[(size_t)p * C + c], x1 = part[(size_t)(p + 16) * C + c];
+      float x2 = part[(size_t)(p + 32) * C + c], x3 = part[(size_t)(p + 48) * C + c];
+      float y0 = part[((size_t)P + p) * C + c], y1 = part[((size_t)P + p + 16) * C + c];
+      float y2 = part[((size_t)P + p + 32) * C + c], y3 = part[((size_t)P + p + 48) * C + c];
+      a += ((double)x0 + x1) + ((double)x2 + x3);
+      b += ((double)y0 + y1) + ((double)y2 + y3);
+    }
+    for (; p < P; p += 16) {
       a += part[(size_t)p * C + c];
       b += part[((size_t)P + p) * C + c];
     }
+  }
   red[0][g][lane] = a;
   red[1][g][lane] = b;
   __syncthreads();
@@ -152,51 +180,48 @@ __global__ __launch_bounds__(256) void bn_bwd_partials(const uint16_t* __restric
                                                        const float* __restrict__ scale,
                                                        const float* __restrict__ shift, float* __restrict__ part,
                                                        int M, int C) {
-  __shared__ float red[256 * 8];
-  const int TPR = C >> 3;
-  const int tid = threadIdx.x;
-  const int RPB = 256 / TPR;
-  const int active = RPB * TPR;
-  const int tc = tid % TPR, tr = tid / TPR;
+  const int P = gridDim.y;
+  const int c0 = blockIdx.x * 64;
+  const int cc = c0 + (threadIdx.x & 7) * 8;
   float sg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sgx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (tid < active) {
+  if (cc < C) {
     float mu[8], is[8], sc[8], sh[8];
+    *reinterpret_cast<float4*>(mu) = *reinterpret_cast<const float4*>(mean + cc);
+    *reinterpret_cast<float4*>(mu + 4) = *reinterpret_cast<const float4*>(mean + cc + 4);
+    *reinterpret_cast<float4*>(is) = *reinterpret_cast<const float4*>(invstd + cc);
+    *reinterpret_cast<float4*>(is + 4) = *reinterpret_cast<const float4*>(invstd + cc + 4);
+    *reinterpret_cast<float4*>(sc) = *reinterpret_cast<const float4*>(scale + cc);
+    *reinterpret_cast<float4*>(sc + 4) = *reinterpret_cast<const float4*>(scale + cc + 4);
+    *reinterpret_cast<float4*>(sh) = *reinterpret_cast<const float4*>(shift + cc);
+    *reinterpret_cast<float4*>(sh + 4) = *reinterpret_cast<const float4*>(shift + cc + 4);
+    bn_tile_rows(M, P, [&](int r0, int r1, int r2, int r3) {
+      const int rs[4] = {r0, r1, r2, r3};
+      float d[4][8], v[4][8], rr[4][8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      mu[j] = mean[tc * 8 + j]; is[j] = invstd[tc * 8 + j]; sc[j] = scale[tc * 8 + j]; sh[j] = shift[tc * 8 + j];
-    }
-    for (int r = blockIdx.x * RPB + tr; r < M; r += gridDim.x * RPB) {
-      const size_t e = (size_t)r * C + tc * 8;
-      float d[8], v[8], rr[8];
-      ld8(dy + e, d);
-      ld8(x + e, v);
-      if constexpr (RES) ld8(res + e, rr);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float g = d[j];
-        if constexpr (RELU) {
-          float o = v[j] * sc[j] + sh[j];
-          if constexpr (RES) o += rr[j];
-          g = o > 0.f ? g : 0.f;
+      for (int k = 0; k < 4; ++k)
+        if (rs[k] >= 0) {
+          const size_t e = (size_t)rs[k] * C + cc;
+          ld8(dy + e, d[k]);
+          ld8(x + e, v[k]);
+          if constexpr (RES) ld8(res + e, rr[k]);
         }
-        sg[j] += g;
-        sgx[j] += g * (v[j] - mu[j]) * is[j];
-      }
-    }
-  }
-  for (int pass = 0; pass < 2; ++pass) {
-    const float* src = pass == 0 ? sg : sgx;
-    __syncthreads();
-    if (tid < active)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) red[(tr * TPR + tc) * 8 + j] = src[j];
-    __syncthreads();
-    for (int c = tid; c < C; c += 256) {
-      float t = 0.f;
-      for (int r = 0; r < RPB; ++r) t += red[r * C + c];
-      part[((size_t)pass * gridDim.x + blockIdx.x) * C + c] = t;
-    }
+      for (int k = 0; k < 4; ++k)
+        if (rs[k] >= 0)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float g = d[k][j];
+            if constexpr (RELU) {
+              float o = v[k][j] * sc[j] + sh[j];
+              if constexpr (RES) o += rr[k][j];
+              g = o > 0.f ? g : 0.f;
+            }
+            sg[j] += g;
+            sgx[j] += g * (v[k][j] - mu[j]) * is[j];
+          }
+    });
   }
+  bn_tile_store(sg, sgx, part, P, C, c0);
 }
 
 // dbeta = sum g, dgamma = sum g*x_hat; dx = gamma*is*(g - dbeta/M - x_hat*dgamma/M)
@@ -267,10 +292,14 @@ __global__ __launch_bounds__(256) void bn_bwd_apply(const uint16_t* __restrict__
 
 using namespace dtfk::bn;
 
+// partial rows P: >= 8 rows per thread, ~2048 blocks in total, at most 512
 static int bn_grid(int M, int C) {
-  const int RPB = 256 / (C / 8 > 0 ? C / 8 : 1);
-  int g = (M + RPB * 8 - 1) / (RPB * 8);     // >= 8 rows per thread
-  return g < 1 ? 1 : (g > 1024 ? 1024 : g);
+  const int ct = (C + 63) / 64;
+  int g = (M + 32 * 8 - 1) / (32 * 8);
+  const int cap = (2048 + ct - 1) / ct;
+  if (g > cap) g = cap;
+  if (g > 512) g = 512;
+  return g < 1 ? 1 : g;
 }
 static unsigned ew_grid(long long n8) {
   long long g = (n8 + 255) / 256;
@@ -285,9 +314,9 @@ int dtfk_bn_partial_rows(int M, int C) { return bn_grid(M, C); }
 hipError_t dtfk_bn_fwd(const void* x, const void* res, const float* gamma, const float* beta, void* y, float* part,
                        float* mean, float* invstd, float* scale, float* shift, float* run_mean, float* run_var,
                        int M, int C, float momentum, float eps, int relu, hipStream_t st) {
-  if (C % 8 || C > 2048) return hipErrorInvalidValue;
+  if (C % 8) return hipErrorInvalidValue;
   const int P = bn_grid(M, C);
-  hipLaunchKernelGGL(bn_partials, dim3(P), dim3(256), 0, st, (const uint16_t*)x, part, M, C);
+  hipLaunchKernelGGL(bn_partials, dim3((C + 63) / 64, P), dim3(256), 0, st, (const uint16_t*)x, part, M, C);
   hipLaunchKernelGGL(bn_finalize, dim3((C + 63) / 64), dim3(1024), 0, st, part, P, M, C, gamma, beta, mean, invstd,
                      scale, shift, run_mean, run_var, momentum, eps);
   const long long n8 = (long long)M * C / 8;
@@ -320,12 +349,12 @@ hipError_t dtfk_bn_apply(const void* x, const void* res, const float* scale, con
 hipError_t dtfk_bn_bwd(const void* dy, const void* x, const void* res, const float* gamma, const float* mean,
                        const float* invstd, const float* scale, const float* shift, float* part, float* coef,
                        void* dx, void* dres, float* dgamma, float* dbeta, int M, int C, int relu, hipStream_t st) {
-  if (C % 8 || C > 2048) return hipErrorInvalidValue;
+  if (C % 8) return hipErrorInvalidValue;
   const int P = bn_grid(M, C);
   const uint16_t* dyp = (const uint16_t*)dy;
   const uint16_t* xp = (const uint16_t*)x;
   const uint16_t* rp = (const uint16_t*)res;
-#define DTFK_BNP(R, L) hipLaunchKernelGGL((bn_bwd_partials<R, L>), dim3(P), dim3(256), 0, st, dyp, xp, rp, mean, invstd, scale, shift, part, M, C)
+#define DTFK_BNP(R, L) hipLaunchKernelGGL((bn_bwd_partials<R, L>), dim3((C + 63) / 64, P), dim3(256), 0, st, dyp, xp, rp, mean, invstd, scale, shift, part, M, C)
   if (res && relu) DTFK_BNP(true, true); else if (res) DTFK_BNP(true, false);
   else if (relu) DTFK_BNP(false, true); else DTFK_BNP(false, false);
 #undef DTFK_BNP

@@ -61,17 +61,38 @@ class _FusedBN(torch.autograd.Function):
 
 
 class FusedBatchNorm2d(torch.nn.BatchNorm2d):
+    """BatchNorm2d whose training forward optionally fuses a residual add and ReLU.
+
+    ``num_batches_tracked`` is only read by PyTorch when ``momentum is None``;
+    on the fused path its increments are counted on the host and folded into
+    the buffer when the state dict is taken, instead of one tiny device add per
+    layer per step.
+    """
+
+    _pending_batches = 0
+
+    def _flush_batches(self):
+        if self._pending_batches and self.num_batches_tracked is not None:
+            with torch.no_grad():
+                self.num_batches_tracked += self._pending_batches
+        self._pending_batches = 0
+
+    def _save_to_state_dict(self, destination, prefix, keep_vars):
+        self._flush_batches()
+        super()._save_to_state_dict(destination, prefix, keep_vars)
+
     def forward(self, x, residual: Optional[torch.Tensor] = None, relu: bool = False):  # noqa: D401
         fused_ok = (_ENABLED and self.training and x.is_cuda and x.dtype == torch.bfloat16 and _nhwc(x)
-                    and self.affine and x.shape[1] % 8 == 0 and x.shape[1] <= 2048
+                    and self.affine and x.shape[1] % 8 == 0 and self.momentum is not None
                     and (residual is None or (residual.dtype == torch.bfloat16 and _nhwc(residual))))
         if fused_ok:
             if self.track_running_stats:
-                self.num_batches_tracked += 1
-            mom = self.momentum if self.momentum is not None else 0.1
+                self._pending_batches += 1
+            mom = self.momentum
             return _FusedBN.apply(x, self.weight, self.bias, residual, self.running_mean if self.track_running_stats
                                   else None, self.running_var if self.track_running_stats else None, float(mom),
                                   float(self.eps), bool(relu))
+        self._flush_batches()
         y = super().forward(x)
         if residual is not None:
             y = y + residual

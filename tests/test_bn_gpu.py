@@ -11,7 +11,7 @@ def rel(a, b):
     return float((a - b).norm() / b.norm().clamp_min(1e-12))
 
 
-@pytest.mark.parametrize("C,HW", [(64, 56), (256, 14), (2048, 7), (24, 9)])
+@pytest.mark.parametrize("C,HW", [(64, 56), (256, 14), (2048, 7), (24, 9), (4096, 3), (136, 5)])
 @pytest.mark.parametrize("res,relu", [(False, True), (True, True), (False, False)])
 def test_fused_bn_matches_reference(native, C, HW, res, relu):
     from distributed_tensorflow_example_amd.ops.bn import FusedBatchNorm2d
@@ -50,6 +50,7 @@ def test_fused_bn_matches_reference(native, C, HW, res, relu):
     assert rel(g.bias.grad, ref_bn.bias.grad) < 2e-2
     assert rel(g.running_mean, ref_bn.running_mean) < 1e-3
     assert rel(g.running_var, ref_bn.running_var) < 1e-3
+    assert int(g.state_dict()["num_batches_tracked"]) == int(ref_bn.num_batches_tracked) == 1
 
 
 def test_resnet50_fused_bn_step_trains(native):

@@ -15,7 +15,8 @@ hipError_t dtfk_bn_apply(const void* x, const void* res, const float* scale, con
                          int relu, hipStream_t st);
 hipError_t dtfk_bn_bwd(const void* dy, const void* x, const void* res, const float* gamma, const float* mean,
                        const float* invstd, const float* scale, const float* shift, float* part, float* coef,
-                       void* dx, void* dres, float* dgamma, float* dbeta, int M, int C, int relu, hipStream_t st);
+                       void* dx, void* dres, float* dgamma, float* dbeta, int M, int C, int relu, int accum,
+                       hipStream_t st);
 }
 
 namespace dtf {
@@ -68,7 +69,7 @@ void bn_apply(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor scale, at:
 
 void bn_bwd(at::Tensor dy, at::Tensor x, c10::optional<at::Tensor> res, at::Tensor gamma, at::Tensor stats,
             at::Tensor part, at::Tensor coef, at::Tensor dx, c10::optional<at::Tensor> dres, at::Tensor dgamma,
-            at::Tensor dbeta, bool relu) {
+            at::Tensor dbeta, bool relu, bool accum) {
   const int64_t C = gamma.numel();
   const int64_t M = rows_of(x, C);
   if (rows_of(dy, C) != M || rows_of(dx, C) != M) throw std::runtime_error("bn_bwd: shapes");
@@ -79,7 +80,7 @@ void bn_bwd(at::Tensor dy, at::Tensor x, c10::optional<at::Tensor> res, at::Tens
   ck(dtfk_bn_bwd(dy.data_ptr(), x.data_ptr(), res.has_value() ? res->data_ptr() : nullptr, gamma.data_ptr<float>(),
                  s, s + C, s + 2 * C, s + 3 * C, part.data_ptr<float>(), coef.data_ptr<float>(), dx.data_ptr(),
                  dres.has_value() ? dres->data_ptr() : nullptr, dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
-                 (int)M, (int)C, relu ? 1 : 0, cs()),
+                 (int)M, (int)C, relu ? 1 : 0, accum ? 1 : 0, cs()),
      "bn_bwd");
 }
 

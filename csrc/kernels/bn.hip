@@ -230,15 +230,18 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize(const float* __restrict_
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ mean,
                                                         const float* __restrict__ invstd, float* __restrict__ dgamma,
-                                                        float* __restrict__ dbeta, float* __restrict__ coef) {
+                                                        float* __restrict__ dbeta, float* __restrict__ coef,
+                                                        int accum) {
   const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
   double sgd, sgxd;
   sum_partials(part, P, C, c, lane, g, sgd, sgxd);
   if (g != 0 || c >= C) return;
   const float sg = (float)sgd, sgx = (float)sgxd;
-  dbeta[c] = sg;
-  dgamma[c] = sgx;
+  // accum: dgamma/dbeta are the parameters' .grad (e.g. DDP bucket views) and
+  // are accumulated into, as autograd would
+  dbeta[c] = accum ? dbeta[c] + sg : sg;
+  dgamma[c] = accum ? dgamma[c] + sgx : sgx;
   const float is = invstd[c];
   const float A = gamma[c] * is;
   const float Bc = -A * is * sgx / M;
@@ -348,7 +351,8 @@ hipError_t dtfk_bn_apply(const void* x, const void* res, const float* scale, con
 // backward.  coef: [3, C] scratch; part: [2 * P, C]
 hipError_t dtfk_bn_bwd(const void* dy, const void* x, const void* res, const float* gamma, const float* mean,
                        const float* invstd, const float* scale, const float* shift, float* part, float* coef,
-                       void* dx, void* dres, float* dgamma, float* dbeta, int M, int C, int relu, hipStream_t st) {
+                       void* dx, void* dres, float* dgamma, float* dbeta, int M, int C, int relu, int accum,
+                       hipStream_t st) {
   if (C % 8) return hipErrorInvalidValue;
   const int P = bn_grid(M, C);
   const uint16_t* dyp = (const uint16_t*)dy;
@@ -359,7 +363,7 @@ hipError_t dtfk_bn_bwd(const void* dy, const void* x, const void* res, const flo
   else if (relu) DTFK_BNP(false, true); else DTFK_BNP(false, false);
 #undef DTFK_BNP
   hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + 63) / 64), dim3(1024), 0, st, part, P, M, C, gamma, mean, invstd,
-                     dgamma, dbeta, coef);
+                     dgamma, dbeta, coef, accum);
   const long long n8 = (long long)M * C / 8;
 #define DTFK_BNA(R, L) hipLaunchKernelGGL((bn_bwd_apply<R, L>), dim3(ew_grid(n8)), dim3(256), 0, st, dyp, xp, rp, scale, shift, coef, (uint16_t*)dx, (uint16_t*)dres, n8, C)
   if (res && relu) DTFK_BNA(true, true); else if (res) DTFK_BNA(true, false);

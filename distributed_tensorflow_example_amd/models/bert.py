@@ -25,6 +25,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import ops
+from ..ops import grad_sink
 from ..ops import transformer as T
 
 
@@ -63,6 +64,7 @@ class _ShadowLinear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, w16):
         ctx.save_for_backward(x, w16)
+        ctx.w = w
         return F.linear(x, w16)
 
     @staticmethod
@@ -70,7 +72,14 @@ class _ShadowLinear(torch.autograd.Function):
         x, w16 = ctx.saved_tensors
         gy = gy.to(w16.dtype)
         gx = gy @ w16
-        gw = torch.mm(gy.reshape(-1, gy.shape[-1]).t(), x.reshape(-1, x.shape[-1]), out_dtype=torch.float32)
+        gy2, x2 = gy.reshape(-1, gy.shape[-1]).t(), x.reshape(-1, x.shape[-1])
+        w = ctx.w
+        if grad_sink.enabled(w) and (w.grad is None or w.grad.is_contiguous()):
+            g = grad_sink.target(w)
+            torch.addmm(g, gy2, x2, out_dtype=torch.float32, out=g)   # beta = 1 onto the bucket view
+            grad_sink.done(w)
+            return gx, None, None
+        gw = torch.mm(gy2, x2, out_dtype=torch.float32)
         return gx, gw, None
 
 

@@ -14,6 +14,7 @@ import torch.nn.functional as F
 
 from .. import ops
 from ..ops.bn import FusedBatchNorm2d
+from ..ops.conv import ShadowConv2d, attach_shadows as _attach_conv_shadows
 
 
 class Bottleneck(nn.Module):
@@ -22,14 +23,14 @@ class Bottleneck(nn.Module):
     def __init__(self, cin, width, stride=1, down=False):
         super().__init__()
         cout = width * 4
-        self.conv1 = nn.Conv2d(cin, width, 1, bias=False)
+        self.conv1 = ShadowConv2d(cin, width, 1, bias=False)
         self.bn1 = FusedBatchNorm2d(width)
-        self.conv2 = nn.Conv2d(width, width, 3, stride, 1, bias=False)   # v1.5: stride on the 3x3
+        self.conv2 = ShadowConv2d(width, width, 3, stride, 1, bias=False)   # v1.5: stride on the 3x3
         self.bn2 = FusedBatchNorm2d(width)
-        self.conv3 = nn.Conv2d(width, cout, 1, bias=False)
+        self.conv3 = ShadowConv2d(width, cout, 1, bias=False)
         self.bn3 = FusedBatchNorm2d(cout)
         nn.init.zeros_(self.bn3.weight)                                  # zero-init last BN gamma
-        self.down_conv = nn.Conv2d(cin, cout, 1, stride, bias=False) if down else None
+        self.down_conv = ShadowConv2d(cin, cout, 1, stride, bias=False) if down else None
         self.down_bn = FusedBatchNorm2d(cout) if down else None
 
     def forward(self, x):
@@ -42,7 +43,7 @@ class Bottleneck(nn.Module):
 class ResNet(nn.Module):
     def __init__(self, layers=(3, 4, 6, 3), num_classes=1000):
         super().__init__()
-        self.conv1 = nn.Conv2d(3, 64, 7, 2, 3, bias=False)
+        self.conv1 = ShadowConv2d(3, 64, 7, 2, 3, bias=False)
         self.bn1 = FusedBatchNorm2d(64)
         blocks, cin = [], 64
         for i, (n, w) in enumerate(zip(layers, (64, 128, 256, 512))):
@@ -62,6 +63,10 @@ class ResNet(nn.Module):
             x = self.blocks(x)
             x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
             return self.fc(x)
+
+    def attach_shadows(self, optimizer=None):
+        """bf16 conv weights maintained by the fused optimizer (ops.conv)."""
+        _attach_conv_shadows(self, optimizer)
 
     def loss(self, images, labels):
         return ops.softmax_xent(self.forward(images).float(), labels)

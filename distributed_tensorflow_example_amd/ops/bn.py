@@ -15,6 +15,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import _native
+from . import grad_sink
 
 
 def _C():
@@ -31,7 +32,7 @@ _ENABLED = os.environ.get("DTF_FUSED_BN", "1") != "0"
 
 class _FusedBN(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, res, running_mean, running_var, momentum, eps, relu):
+    def forward(ctx, x, gamma, beta, res, running_mean, running_var, momentum, eps, relu, sink):
         C = _C()
         ch = gamma.numel()
         M = x.numel() // ch
@@ -41,6 +42,7 @@ class _FusedBN(torch.autograd.Function):
         C.bn_fwd(x, res, gamma, beta, y, part, stats, running_mean, running_var, momentum, eps, relu)
         ctx.save_for_backward(x, res if res is not None else torch.empty(0, device=x.device), gamma, stats)
         ctx.has_res, ctx.relu = res is not None, relu
+        ctx.sink = sink           # (weight, bias) whose .grad the finalize kernel accumulates into, or None
         return y
 
     @staticmethod
@@ -52,12 +54,20 @@ class _FusedBN(torch.autograd.Function):
         dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         dx = torch.empty_like(x)
         dres = torch.empty_like(res) if ctx.has_res else None
-        dgamma = torch.empty(ch, dtype=torch.float32, device=x.device)
-        dbeta = torch.empty_like(dgamma)
+        if ctx.sink is not None:
+            dgamma, dbeta = grad_sink.target(ctx.sink[0]), grad_sink.target(ctx.sink[1])
+        else:
+            dgamma = torch.empty(ch, dtype=torch.float32, device=x.device)
+            dbeta = torch.empty_like(dgamma)
         coef = torch.empty(3 * ch, dtype=torch.float32, device=x.device)
         part = torch.empty(2 * C.bn_partial_rows(M, ch) * ch, dtype=torch.float32, device=x.device)
-        C.bn_bwd(dy, x, res if ctx.has_res else None, gamma, stats, part, coef, dx, dres, dgamma, dbeta, ctx.relu)
-        return dx, dgamma, dbeta, dres, None, None, None, None, None
+        C.bn_bwd(dy, x, res if ctx.has_res else None, gamma, stats, part, coef, dx, dres, dgamma, dbeta, ctx.relu,
+                 ctx.sink is not None)
+        if ctx.sink is not None:
+            grad_sink.done(ctx.sink[0])
+            grad_sink.done(ctx.sink[1])
+            return dx, None, None, dres, None, None, None, None, None, None
+        return dx, dgamma, dbeta, dres, None, None, None, None, None, None
 
 
 class FusedBatchNorm2d(torch.nn.BatchNorm2d):
@@ -77,6 +87,12 @@ class FusedBatchNorm2d(torch.nn.BatchNorm2d):
                 self.num_batches_tracked += self._pending_batches
         self._pending_batches = 0
 
+    def _sink(self):
+        w, b = self.weight, self.bias
+        ok = (grad_sink.enabled(w) and grad_sink.enabled(b)
+              and all(p.grad is None or (p.grad.dtype == torch.float32 and p.grad.is_contiguous()) for p in (w, b)))
+        return (w, b) if ok else None
+
     def _save_to_state_dict(self, destination, prefix, keep_vars):
         self._flush_batches()
         super()._save_to_state_dict(destination, prefix, keep_vars)
@@ -91,7 +107,7 @@ class FusedBatchNorm2d(torch.nn.BatchNorm2d):
             mom = self.momentum
             return _FusedBN.apply(x, self.weight, self.bias, residual, self.running_mean if self.track_running_stats
                                   else None, self.running_var if self.track_running_stats else None, float(mom),
-                                  float(self.eps), bool(relu))
+                                  float(self.eps), bool(relu), self._sink())
         self._flush_batches()
         y = super().forward(x)
         if residual is not None:

@@ -14,6 +14,9 @@ Design for MI355X / RCCL over xGMI:
   event on the compute stream -- later buckets keep computing meanwhile;
 * optional bf16 communication (`comm_dtype=torch.bfloat16`): the bucket is
   cast once, reduced in bf16 (half the xGMI bytes), cast back;
+* fused backward ops (BN, shadow-weight conv / GEMM) "sink" their weight
+  gradients: they accumulate into the bucket view inside their own kernels
+  and call the bucket-ready hook themselves (ops.grad_sink);
 * the 1/world average is folded into the optimizer (`grad_scale`) when the
   caller asks for it, else applied to the bucket.
 Bucket size matters on xGMI: a ring moves 2(n-1)/n of the bytes over one link
@@ -28,7 +31,12 @@ from typing import List, Optional
 import torch
 import torch.distributed as dist
 
+from ..ops import grad_sink
 from .world import World, get_world
+
+
+def _no_hook(p):
+    pass
 
 
 class _Bucket:
@@ -90,6 +98,10 @@ class DistributedDataParallel(torch.nn.Module):
         if overlap:
             for p in params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+        # fused backward kernels may accumulate straight into the bucket views
+        # and report readiness themselves (ops.grad_sink)
+        for p in params:
+            grad_sink.install(p, self._on_grad if overlap else _no_hook)
         self.comm_stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
         if broadcast_params and self.world.world_size > 1:
             with torch.no_grad():

@@ -40,7 +40,9 @@ def main():
     ap.add_argument("--model", choices=["wide_deep", "sparse_lr", "bert_base", "resnet50"], default="wide_deep")
     ap.add_argument("--seq", type=int, default=128)
     ap.add_argument("--bucket-mb", type=float, default=32.0)
-    ap.add_argument("--no-shadow", action="store_true", help="BERT: cast fp32 weights per GEMM instead")
+    ap.add_argument("--no-shadow", action="store_true", help="cast fp32 weights per GEMM/conv (autocast) instead of bf16 shadows")
+    ap.add_argument("--conv-find", type=int, default=1,
+                    help="ResNet: 1 = let MIOpen benchmark conv solvers (torch.backends.cudnn.benchmark)")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (0 = model default)")
@@ -116,16 +118,18 @@ def dense_bench(a, w):
         from distributed_tensorflow_example_amd.models.resnet import resnet50, synthetic_imagenet_batch
 
         a.batch = a.batch or 128
+        torch.backends.cudnn.benchmark = bool(a.conv_find)
         model = resnet50().to(dev).to(memory_format=torch.channels_last)
         batches = [synthetic_imagenet_batch(a.batch, dev, seed=w.rank * 100 + i) for i in range(2)]
         opt = optim.FusedMomentum(list(model.parameters()), 0.1, 0.9, weight_decay=1e-4)
         unit, per = "images/s", a.batch
         cfg = {"model": "resnet50 (25.6M)", "global_batch": a.batch * w.world_size, "per_gpu_batch": a.batch,
                "seq_len": None, "parallelism": f"dp{w.world_size}", "optimizer": "sgd-momentum",
-               "grad_allreduce": f"bucketed {a.bucket_mb}MB, overlapped", "input": "224x224 synthetic, channels_last"}
+               "grad_allreduce": f"bucketed {a.bucket_mb}MB, overlapped", "input": "224x224 synthetic, channels_last",
+               "conv_solver_search": bool(a.conv_find)}
         run = lambda m, b: m.loss(*b)
     ddp = DistributedDataParallel(model, w, bucket_mb=a.bucket_mb)
-    if a.model == "bert_base" and not a.no_shadow:
+    if not a.no_shadow:
         model.attach_shadows(opt)          # after the DDP broadcast: shadows match rank 0's weights
 
     def step(b):

@@ -25,6 +25,12 @@ hipError_t dtfk_softmax_fwd(const void* S, const float* mask, void* P, void* Pd,
 hipError_t dtfk_softmax_bwd(const void* dPd, const void* P, void* dS, int rows, int Sk, float scale, float p,
                             unsigned long long seed, hipStream_t st);
 hipError_t dtfk_dropout_bf16(const void* x, void* y, long long n, float p, unsigned long long seed, hipStream_t st);
+int dtfk_attn_supported(int S, int d);
+hipError_t dtfk_attn_fwd(const void* qkv, const float* bias, const float* mask, void* ctx, float* lse, int B, int S,
+                         int NH, float scale, float p, unsigned long long seed, hipStream_t st);
+hipError_t dtfk_attn_bwd(const void* qkv, const float* bias, const float* mask, const void* ctx, const void* dctx,
+                         const float* lse, float* Dbuf, void* dqkv, int B, int S, int NH, float scale, float p,
+                         unsigned long long seed, hipStream_t st);
 }
 
 namespace dtf {
@@ -143,7 +149,54 @@ void dropout_bf16(at::Tensor x, at::Tensor y, double p, int64_t seed) {
   ck(dtfk_dropout_bf16(x.data_ptr(), y.data_ptr(), x.numel(), (float)p, (unsigned long long)seed, cs()), "dropout");
 }
 
+// qkv [B, S, 3*NH*64] bf16 (pre-bias projection), bias [3*NH*64] fp32 or None,
+// mask [B, S] additive fp32 or None -> ctx [B, S, NH*64] bf16, lse [B, NH, S] fp32
+void attn_check(const at::Tensor& qkv, const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& mask,
+                int64_t NH) {
+  req(qkv, at::kBFloat16, "qkv");
+  if (qkv.dim() != 3 || qkv.size(2) != 3 * NH * 64) throw std::runtime_error("attn: qkv must be [B, S, 3*NH*64]");
+  if (!dtfk_attn_supported((int)qkv.size(1), 64)) throw std::runtime_error("attn: unsupported sequence length");
+  if (bias.has_value()) {
+    req(*bias, at::kFloat, "bias");
+    if (bias->numel() != qkv.size(2)) throw std::runtime_error("attn: bias size");
+  }
+  if (mask.has_value()) {
+    req(*mask, at::kFloat, "mask");
+    if (mask->numel() != qkv.size(0) * qkv.size(1)) throw std::runtime_error("attn: mask must be [B, S]");
+  }
+}
+
+void attn_fwd(at::Tensor qkv, c10::optional<at::Tensor> bias, c10::optional<at::Tensor> mask, at::Tensor ctx,
+              at::Tensor lse, int64_t NH, double scale, double p, int64_t seed) {
+  attn_check(qkv, bias, mask, NH);
+  const int64_t B = qkv.size(0), S = qkv.size(1);
+  req(ctx, at::kBFloat16, "ctx"); req(lse, at::kFloat, "lse");
+  if (ctx.numel() != B * S * NH * 64 || lse.numel() != B * NH * S) throw std::runtime_error("attn_fwd: output sizes");
+  ck(dtfk_attn_fwd(qkv.data_ptr(), optf(bias), optf(mask), ctx.data_ptr(), lse.data_ptr<float>(), (int)B, (int)S,
+                   (int)NH, (float)scale, (float)p, (unsigned long long)seed, cs()),
+     "attn_fwd");
+}
+
+void attn_bwd(at::Tensor qkv, c10::optional<at::Tensor> bias, c10::optional<at::Tensor> mask, at::Tensor ctx,
+              at::Tensor dctx, at::Tensor lse, at::Tensor Dbuf, at::Tensor dqkv, int64_t NH, double scale, double p,
+              int64_t seed) {
+  attn_check(qkv, bias, mask, NH);
+  const int64_t B = qkv.size(0), S = qkv.size(1);
+  req(ctx, at::kBFloat16, "ctx"); req(dctx, at::kBFloat16, "dctx"); req(dqkv, at::kBFloat16, "dqkv");
+  req(lse, at::kFloat, "lse"); req(Dbuf, at::kFloat, "Dbuf");
+  if (ctx.numel() != B * S * NH * 64 || dctx.numel() != ctx.numel() || dqkv.numel() != qkv.numel() ||
+      lse.numel() != B * NH * S || Dbuf.numel() != lse.numel())
+    throw std::runtime_error("attn_bwd: sizes");
+  ck(dtfk_attn_bwd(qkv.data_ptr(), optf(bias), optf(mask), ctx.data_ptr(), dctx.data_ptr(), lse.data_ptr<float>(),
+                   Dbuf.data_ptr<float>(), dqkv.data_ptr(), (int)B, (int)S, (int)NH, (float)scale, (float)p,
+                   (unsigned long long)seed, cs()),
+     "attn_bwd");
+}
+
 void init_transformer(pybind11::module& m) {
+  m.def("attn_supported", [](int64_t S, int64_t d) { return dtfk_attn_supported((int)S, (int)d) != 0; });
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd", &attn_bwd);
   m.def("bdrln_fwd", &bdrln_fwd);
   m.def("ln_fwd_f32in", &ln_fwd_f32in);
   m.def("ln_bwd", &ln_bwd);

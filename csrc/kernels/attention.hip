@@ -1,0 +1,424 @@
+// Fused multi-head self-attention for BERT-shaped layers (head dim 64,
+// S <= 256, S % 32 == 0) on CDNA4 MFMA -- forward and backward.
+//
+// The unfused path is QK^T (batched GEMM) -> masked softmax + dropout ->
+// PV (batched GEMM), plus permute copies of q/k/v/ctx in both directions,
+// slice-backward fills and the qkv bias add: ~0.5 ms per BERT-base layer at
+// B=128, S=128 on MI355X.  Here one workgroup owns (batch, head, 128 rows):
+//
+//   attn_fwd      reads q/k/v straight out of the packed [B, S, 3, NH, 64]
+//                 projection (+ bias, fused), keeps the whole score row in
+//                 registers (S <= 256), writes ctx as [B, S, NH*64] and the
+//                 row log-sum-exp for the backward.
+//   attn_bwd_dq   recomputes P from lse, dP = dO V^T, dS, writes dQ and
+//                 D = rowsum(dO * O).
+//   attn_bwd_dkv  per 16-key slab, loops over all queries: dV += Pd^T dO,
+//                 dK += dS^T Q.
+//
+// MFMA orientation (16x16x32 bf16; lane l, g = l >> 4, c = l & 15):
+// the score tile is computed transposed, S^T = K Q^T, so a lane holds keys
+// 4g+i of a 16-key tile for ONE query c.  The next product (O^T = V^T P^T)
+// sums over keys, i.e. over the accumulator's row index, so P^T feeds the
+// B operand straight from registers: the k-slot (g, j) of a 32-key block is
+// key 4g+j (j < 4) or 16+4g+(j-4) (j >= 4), and the A operand (V^T) is read
+// from an LDS image of V^T with the same key permutation (two 8-byte reads).
+// The backward products follow the same rule (dQ^T = K^T dS^T; dV = Pd^T dO,
+// dK = dS^T Q in the key-major kernel), using transposed LDS images of K, Q
+// and dO written once per workgroup.
+//
+// Dropout keep(i) = hash32(seed, i) >= p * 2^32 with i the element index of
+// the [B, NH, S, S] probability tensor -- the same convention as the unfused
+// softmax kernel (transformer.hip), so both paths drop the same elements.
+#include "common.h"
+
+namespace dtfk {
+namespace attn {
+
+constexpr int D = 64;
+constexpr int KP = 72;     // padded row of a [S][64] LDS image (144 B: rows spread over banks)
+
+__device__ __forceinline__ uint4 add_bias8(uint4 u, const float* __restrict__ bias) {
+  if (!bias) return u;
+  const float4 b0 = *reinterpret_cast<const float4*>(bias);
+  const float4 b1 = *reinterpret_cast<const float4*>(bias + 4);
+  const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+  uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    w[j] = pack2bf(bf2f(w[j] & 0xffff) + bb[2 * j], bf2f(w[j] >> 16) + bb[2 * j + 1]);
+  return uint4{w[0], w[1], w[2], w[3]};
+}
+
+__device__ __forceinline__ uint4 ld16(const uint16_t* p) { return *reinterpret_cast<const uint4*>(p); }
+
+__device__ __forceinline__ bf16x8 as_frag(uint4 u) { return __builtin_bit_cast(bf16x8, u); }
+
+// two 4-element (8-byte) runs -> one 8-element fragment
+__device__ __forceinline__ bf16x8 ld_pair(const uint16_t* p0, const uint16_t* p1) {
+  const uint2 a = *reinterpret_cast<const uint2*>(p0);
+  const uint2 b = *reinterpret_cast<const uint2*>(p1);
+  return as_frag(uint4{a.x, a.y, b.x, b.y});
+}
+
+__device__ __forceinline__ bf16x8 pack8(const float* f) {
+  return as_frag(uint4{pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]), pack2bf(f[6], f[7])});
+}
+
+__device__ __forceinline__ float keepf(uint64_t seed, uint64_t i, uint32_t thresh, float inv_keep) {
+  return (thresh == 0u) ? 1.f : (hash32(seed, i) >= thresh ? inv_keep : 0.f);
+}
+
+// stage a [S][64] tile (rows of the packed projection, or of a [B,S,NH*64]
+// tensor) into a row image rows[S][KP] and, optionally, a transposed image
+// cols[64][S+8]
+template <int S>
+__device__ __forceinline__ void stage(const uint16_t* __restrict__ src, long long row_stride,
+                                      const float* __restrict__ bias, uint16_t* rows, uint16_t* cols) {
+  constexpr int VT = S + 8;
+  for (int ch = threadIdx.x; ch < S * 8; ch += blockDim.x) {
+    const int r = ch >> 3, part = ch & 7;
+    const uint4 v = add_bias8(ld16(src + r * row_stride + part * 8), bias ? bias + part * 8 : nullptr);
+    if (rows) *reinterpret_cast<uint4*>(rows + r * KP + part * 8) = v;
+    if (cols) {
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        cols[(part * 8 + 2 * j) * VT + r] = (uint16_t)(w[j] & 0xffff);
+        cols[(part * 8 + 2 * j + 1) * VT + r] = (uint16_t)(w[j] >> 16);
+      }
+    }
+  }
+}
+
+template <int NKB>
+__global__ __launch_bounds__(512) void attn_fwd(const uint16_t* __restrict__ qkv, const float* __restrict__ bias,
+                                                const float* __restrict__ mask, uint16_t* __restrict__ ctx,
+                                                float* __restrict__ lse, int NH, float scale, uint32_t thresh,
+                                                float inv_keep, uint64_t seed) {
+  constexpr int S = 32 * NKB, VT = S + 8;
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  uint16_t* Ks = lds;                 // [S][KP]
+  uint16_t* Vt = lds + S * KP;        // [64][VT]
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, g = l >> 4, c = l & 15;
+  const long long RS = 3LL * NH * D;
+  const uint16_t* base = qkv + (long long)b * S * RS + h * D;
+  const float* bq = bias ? bias + h * D : nullptr;
+  const float* bk = bias ? bias + (NH + h) * D : nullptr;
+  const float* bv = bias ? bias + (2 * NH + h) * D : nullptr;
+  stage<S>(base + NH * D, RS, bk, Ks, nullptr);
+  stage<S>(base + 2 * NH * D, RS, bv, nullptr, Vt);
+  __syncthreads();
+  const int q = blockIdx.x * 128 + w * 16 + c;
+  if (blockIdx.x * 128 + w * 16 >= S) return;          // wave-uniform; no barrier follows
+
+  bf16x8 bqf[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+    bqf[s] = as_frag(add_bias8(ld16(base + (long long)q * RS + 32 * s + 8 * g), bq ? bq + 32 * s + 8 * g : nullptr));
+  f32x4 sc[2 * NKB];
+#pragma unroll
+  for (int t = 0; t < 2 * NKB; ++t) {
+    sc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 2; ++s) sc[t] = mfma16x16x32(ld_bf16x8(Ks + (16 * t + c) * KP + 32 * s + 8 * g), bqf[s], sc[t]);
+  }
+  float mx = -3.0e38f;
+#pragma unroll
+  for (int t = 0; t < 2 * NKB; ++t) {
+    float4 mk = mask ? *reinterpret_cast<const float4*>(mask + (long long)b * S + 16 * t + 4 * g)
+                     : float4{0.f, 0.f, 0.f, 0.f};
+    const float m4[4] = {mk.x, mk.y, mk.z, mk.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      sc[t][i] = sc[t][i] * scale + m4[i];
+      mx = fmaxf(mx, sc[t][i]);
+    }
+  }
+  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int t = 0; t < 2 * NKB; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      sc[t][i] = __expf(sc[t][i] - mx);
+      sum += sc[t][i];
+    }
+  sum += __shfl_xor(sum, 16, 64);
+  sum += __shfl_xor(sum, 32, 64);
+  const float inv = 1.f / sum;
+  const long long row = ((long long)b * NH + h) * S + q;
+  if (g == 0) lse[row] = mx + __logf(sum);
+  const uint64_t ebase = (uint64_t)row * S;
+  bf16x8 pb[NKB];
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb) {
+    float f[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k0 = 32 * kb + 4 * g + j;
+      f[j] = sc[2 * kb][j] * inv * keepf(seed, ebase + k0, thresh, inv_keep);
+      f[4 + j] = sc[2 * kb + 1][j] * inv * keepf(seed, ebase + k0 + 16, thresh, inv_keep);
+    }
+    pb[kb] = pack8(f);
+  }
+  uint16_t* out = ctx + ((long long)b * S + q) * NH * D + h * D;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    f32x4 o = {0.f, 0.f, 0.f, 0.f};
+    const uint16_t* vr = Vt + (16 * u + c) * VT + 4 * g;
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) o = mfma16x16x32(ld_pair(vr + 32 * kb, vr + 32 * kb + 16), pb[kb], o);
+    *reinterpret_cast<uint2*>(out + 16 * u + 4 * g) = uint2{pack2bf(o[0], o[1]), pack2bf(o[2], o[3])};
+  }
+}
+
+template <int NKB>
+__global__ __launch_bounds__(512) void attn_bwd_dq(const uint16_t* __restrict__ qkv, const float* __restrict__ bias,
+                                                   const float* __restrict__ mask, const uint16_t* __restrict__ ctx,
+                                                   const uint16_t* __restrict__ dctx, const float* __restrict__ lse,
+                                                   float* __restrict__ Dbuf, uint16_t* __restrict__ dqkv, int NH,
+                                                   float scale, uint32_t thresh, float inv_keep, uint64_t seed) {
+  constexpr int S = 32 * NKB, VT = S + 8;
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  uint16_t* Ks = lds;                    // [S][KP]
+  uint16_t* Vs = lds + S * KP;           // [S][KP]
+  uint16_t* Kt = lds + 2 * S * KP;       // [64][VT]
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, g = l >> 4, c = l & 15;
+  const long long RS = 3LL * NH * D, HS = (long long)NH * D;
+  const uint16_t* base = qkv + (long long)b * S * RS + h * D;
+  const float* bq = bias ? bias + h * D : nullptr;
+  stage<S>(base + NH * D, RS, bias ? bias + (NH + h) * D : nullptr, Ks, Kt);
+  stage<S>(base + 2 * NH * D, RS, bias ? bias + (2 * NH + h) * D : nullptr, Vs, nullptr);
+  __syncthreads();
+  const int q = blockIdx.x * 128 + w * 16 + c;
+  if (blockIdx.x * 128 + w * 16 >= S) return;
+
+  bf16x8 bqf[2], bdo[2];
+  const uint16_t* dor = dctx + ((long long)b * S + q) * HS + h * D;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    bqf[s] = as_frag(add_bias8(ld16(base + (long long)q * RS + 32 * s + 8 * g), bq ? bq + 32 * s + 8 * g : nullptr));
+    bdo[s] = as_frag(ld16(dor + 32 * s + 8 * g));
+  }
+  // D = rowsum(dO * O): lane group g covers d = 16g .. 16g+15
+  const uint16_t* orow = ctx + ((long long)b * S + q) * HS + h * D + 16 * g;
+  float dsum = 0.f;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    const uint4 ov = ld16(orow + 8 * half), dv = ld16(dor + 16 * g + 8 * half);
+    const uint32_t a[4] = {ov.x, ov.y, ov.z, ov.w}, d4[4] = {dv.x, dv.y, dv.z, dv.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      dsum += bf2f(a[j] & 0xffff) * bf2f(d4[j] & 0xffff) + bf2f(a[j] >> 16) * bf2f(d4[j] >> 16);
+  }
+  dsum += __shfl_xor(dsum, 16, 64);
+  dsum += __shfl_xor(dsum, 32, 64);
+  const long long row = ((long long)b * NH + h) * S + q;
+  if (g == 0) Dbuf[row] = dsum;
+  const float L = lse[row];
+  const uint64_t ebase = (uint64_t)row * S;
+  bf16x8 dsb[NKB];
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb) {
+    float f[8];
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      const int t = 2 * kb + tt;
+      f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        sv = mfma16x16x32(ld_bf16x8(Ks + (16 * t + c) * KP + 32 * s + 8 * g), bqf[s], sv);
+        dp = mfma16x16x32(ld_bf16x8(Vs + (16 * t + c) * KP + 32 * s + 8 * g), bdo[s], dp);
+      }
+      float4 mk = mask ? *reinterpret_cast<const float4*>(mask + (long long)b * S + 16 * t + 4 * g)
+                       : float4{0.f, 0.f, 0.f, 0.f};
+      const float m4[4] = {mk.x, mk.y, mk.z, mk.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = 16 * t + 4 * g + i;
+        const float P = __expf(sv[i] * scale + m4[i] - L);
+        const float dpd = dp[i] * keepf(seed, ebase + key, thresh, inv_keep);
+        f[4 * tt + i] = P * (dpd - dsum);
+      }
+    }
+    dsb[kb] = pack8(f);
+  }
+  uint16_t* dq = dqkv + ((long long)b * S + q) * RS + h * D;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const uint16_t* kr = Kt + (16 * u + c) * VT + 4 * g;
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) acc = mfma16x16x32(ld_pair(kr + 32 * kb, kr + 32 * kb + 16), dsb[kb], acc);
+    *reinterpret_cast<uint2*>(dq + 16 * u + 4 * g) =
+        uint2{pack2bf(acc[0] * scale, acc[1] * scale), pack2bf(acc[2] * scale, acc[3] * scale)};
+  }
+}
+
+template <int NKB>
+__global__ __launch_bounds__(512) void attn_bwd_dkv(const uint16_t* __restrict__ qkv, const float* __restrict__ bias,
+                                                    const float* __restrict__ mask, const uint16_t* __restrict__ dctx,
+                                                    const float* __restrict__ lse, const float* __restrict__ Dbuf,
+                                                    uint16_t* __restrict__ dqkv, int NH, float scale, uint32_t thresh,
+                                                    float inv_keep, uint64_t seed) {
+  constexpr int S = 32 * NKB, VT = S + 8;
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  uint16_t* Qs = lds;                          // [S][KP]
+  uint16_t* dOs = lds + S * KP;                // [S][KP]
+  uint16_t* Qt = lds + 2 * S * KP;             // [64][VT]
+  uint16_t* dOt = lds + 2 * S * KP + D * VT;   // [64][VT]
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, g = l >> 4, c = l & 15;
+  const long long RS = 3LL * NH * D, HS = (long long)NH * D;
+  const uint16_t* base = qkv + (long long)b * S * RS + h * D;
+  stage<S>(base, RS, bias ? bias + h * D : nullptr, Qs, Qt);
+  stage<S>(dctx + (long long)b * S * HS + h * D, HS, nullptr, dOs, dOt);
+  __syncthreads();
+  const int k0 = blockIdx.x * 128 + w * 16;
+  if (k0 >= S) return;
+  const int key = k0 + c;
+
+  const float* bk = bias ? bias + (NH + h) * D : nullptr;
+  const float* bv = bias ? bias + (2 * NH + h) * D : nullptr;
+  bf16x8 kf[2], vf[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    kf[s] = as_frag(add_bias8(ld16(base + (long long)key * RS + NH * D + 32 * s + 8 * g), bk ? bk + 32 * s + 8 * g : nullptr));
+    vf[s] = as_frag(add_bias8(ld16(base + (long long)key * RS + 2 * NH * D + 32 * s + 8 * g), bv ? bv + 32 * s + 8 * g : nullptr));
+  }
+  const float mk = mask ? mask[(long long)b * S + key] : 0.f;
+  const long long rbase = ((long long)b * NH + h) * S;
+  f32x4 dv[4], dk[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    dv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    dk[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  for (int qb = 0; qb < NKB; ++qb) {
+    float pd[8], ds[8];
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      const int t = 2 * qb + tt;
+      f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        sv = mfma16x16x32(ld_bf16x8(Qs + (16 * t + c) * KP + 32 * s + 8 * g), kf[s], sv);
+        dp = mfma16x16x32(ld_bf16x8(dOs + (16 * t + c) * KP + 32 * s + 8 * g), vf[s], dp);
+      }
+      const float4 L4 = *reinterpret_cast<const float4*>(lse + rbase + 16 * t + 4 * g);
+      const float4 D4 = *reinterpret_cast<const float4*>(Dbuf + rbase + 16 * t + 4 * g);
+      const float Ls[4] = {L4.x, L4.y, L4.z, L4.w}, Ds[4] = {D4.x, D4.y, D4.z, D4.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int q = 16 * t + 4 * g + i;
+        const float P = __expf(sv[i] * scale + mk - Ls[i]);
+        const float kp = keepf(seed, (uint64_t)(rbase + q) * S + key, thresh, inv_keep);
+        pd[4 * tt + i] = P * kp;
+        ds[4 * tt + i] = P * (dp[i] * kp - Ds[i]);
+      }
+    }
+    const bf16x8 ap = pack8(pd), as = pack8(ds);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint16_t* dr = dOt + (16 * u + c) * VT + 32 * qb + 4 * g;
+      const uint16_t* qr = Qt + (16 * u + c) * VT + 32 * qb + 4 * g;
+      dv[u] = mfma16x16x32(ap, ld_pair(dr, dr + 16), dv[u]);
+      dk[u] = mfma16x16x32(as, ld_pair(qr, qr + 16), dk[u]);
+    }
+  }
+  // lane holds dV/dK[key k0 + 4g + i][d 16u + c]
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    uint16_t* rowp = dqkv + ((long long)b * S + k0 + 4 * g + i) * RS + h * D + c;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      rowp[NH * D + 16 * u] = f2bf(dk[u][i] * scale);
+      rowp[2 * NH * D + 16 * u] = f2bf(dv[u][i]);
+    }
+  }
+}
+
+}  // namespace attn
+}  // namespace dtfk
+
+using namespace dtfk::attn;
+
+static inline uint32_t attn_thresh(float p) {
+  if (p <= 0.f) return 0u;
+  double t = (double)p * 4294967296.0;
+  return t >= 4294967295.0 ? 4294967295u : (uint32_t)t;
+}
+
+// >64 KB dynamic LDS must be opted into once per kernel instantiation
+template <typename K>
+static hipError_t allow_lds(K kern, size_t lds) {
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)lds);
+}
+
+extern "C" {
+
+int dtfk_attn_supported(int S, int d) {
+  const int n = S / 32;
+  return d == D && S % 32 == 0 && (n == 1 || n == 2 || n == 4 || n == 6 || n == 8);
+}
+
+#define DTFK_ATTN_DISPATCH(S, MACRO) \
+  switch ((S) / 32) {                \
+    case 1: MACRO(1); break;         \
+    case 2: MACRO(2); break;         \
+    case 4: MACRO(4); break;         \
+    case 6: MACRO(6); break;         \
+    case 8: MACRO(8); break;         \
+    default: return hipErrorInvalidValue; \
+  }
+
+hipError_t dtfk_attn_fwd(const void* qkv, const float* bias, const float* mask, void* ctx, float* lse, int B, int S,
+                         int NH, float scale, float p, unsigned long long seed, hipStream_t st) {
+  if (!dtfk_attn_supported(S, D)) return hipErrorInvalidValue;
+  const dim3 grid((S + 127) / 128, NH, B);
+  const float ik = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const size_t lds = (size_t)(S * KP + D * (S + 8)) * 2;
+#define L_FWD(N)                                                                                                \
+  {                                                                                                             \
+    static hipError_t e = allow_lds(attn_fwd<N>, lds);                                                          \
+    if (e != hipSuccess) return e;                                                                              \
+    hipLaunchKernelGGL(attn_fwd<N>, grid, dim3(512), lds, st, (const uint16_t*)qkv, bias, mask, (uint16_t*)ctx, \
+                       lse, NH, scale, attn_thresh(p), ik, (uint64_t)seed);                                     \
+  }
+  DTFK_ATTN_DISPATCH(S, L_FWD)
+#undef L_FWD
+  return hipGetLastError();
+}
+
+// dqkv [B, S, 3, NH, 64] is fully written; Dbuf [B, NH, S] fp32 scratch
+hipError_t dtfk_attn_bwd(const void* qkv, const float* bias, const float* mask, const void* ctx, const void* dctx,
+                         const float* lse, float* Dbuf, void* dqkv, int B, int S, int NH, float scale, float p,
+                         unsigned long long seed, hipStream_t st) {
+  if (!dtfk_attn_supported(S, D)) return hipErrorInvalidValue;
+  const dim3 grid((S + 127) / 128, NH, B);
+  const float ik = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const uint32_t th = attn_thresh(p);
+  const size_t lds_q = (size_t)(2 * S * KP + D * (S + 8)) * 2;
+  const size_t lds_kv = (size_t)(2 * S * KP + 2 * D * (S + 8)) * 2;
+#define L_BWD(N)                                                                                                   \
+  {                                                                                                                \
+    static hipError_t e1 = allow_lds(attn_bwd_dq<N>, lds_q);                                                       \
+    static hipError_t e2 = allow_lds(attn_bwd_dkv<N>, lds_kv);                                                     \
+    if (e1 != hipSuccess) return e1;                                                                               \
+    if (e2 != hipSuccess) return e2;                                                                               \
+    hipLaunchKernelGGL(attn_bwd_dq<N>, grid, dim3(512), lds_q, st, (const uint16_t*)qkv, bias, mask,               \
+                       (const uint16_t*)ctx, (const uint16_t*)dctx, lse, Dbuf, (uint16_t*)dqkv, NH, scale, th, ik, \
+                       (uint64_t)seed);                                                                            \
+    hipLaunchKernelGGL(attn_bwd_dkv<N>, grid, dim3(512), lds_kv, st, (const uint16_t*)qkv, bias, mask,             \
+                       (const uint16_t*)dctx, lse, Dbuf, (uint16_t*)dqkv, NH, scale, th, ik, (uint64_t)seed);      \
+  }
+  DTFK_ATTN_DISPATCH(S, L_BWD)
+#undef L_BWD
+  return hipGetLastError();
+}
+
+}  // extern "C"

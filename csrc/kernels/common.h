@@ -40,6 +40,16 @@ __device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
   return static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
 }
 
+// Counter-based dropout hash (splitmix64 finaliser): keep(i) = hash32(seed, i)
+// >= p * 2^32.  Shared by every kernel that regenerates a mask in backward.
+__device__ __forceinline__ uint32_t hash32(uint64_t seed, uint64_t i) {
+  uint64_t x = seed ^ (i * 0x9E3779B97F4A7C15ull);
+  x ^= x >> 30; x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 27; x *= 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  return static_cast<uint32_t>(x);
+}
+
 __device__ __forceinline__ bf16x8 ld_bf16x8(const uint16_t* p) {
   return *reinterpret_cast<const bf16x8*>(p);
 }

@@ -19,13 +19,6 @@ namespace dtfk {
 namespace tfm {
 
 
-__device__ __forceinline__ uint32_t hash32(uint64_t seed, uint64_t i) {
-  uint64_t x = seed ^ (i * 0x9E3779B97F4A7C15ull);
-  x ^= x >> 30; x *= 0xBF58476D1CE4E5B9ull;
-  x ^= x >> 27; x *= 0x94D049BB133111EBull;
-  x ^= x >> 31;
-  return static_cast<uint32_t>(x);
-}
 __device__ __forceinline__ bool keep_elem(uint64_t seed, uint64_t i, uint32_t thresh) {
   return thresh == 0u || hash32(seed, i) >= thresh;
 }

@@ -42,6 +42,7 @@ class BertConfig:
     attn_dropout: float = 0.1
     ln_eps: float = 1e-12
     init_std: float = 0.02
+    fused_attention: bool = True    # GPU: attention.hip straight from the packed QKV projection
 
     @staticmethod
     def base():
@@ -123,13 +124,18 @@ class BertLayer(torch.nn.Module):
         c = self.c
         B, S, H = x.shape
         nh, d = c.heads, H // c.heads
-        qkv = (_mm(x, self.w_qkv) + self.b_qkv.to(x.dtype)).view(B, S, 3, nh, d)
-        q = qkv[:, :, 0].permute(0, 2, 1, 3)
-        k = qkv[:, :, 1].permute(0, 2, 3, 1)
-        v = qkv[:, :, 2].permute(0, 2, 1, 3)
-        scores = torch.matmul(q, k)                                   # [B, nh, S, S]
-        probs = T.attention_softmax(scores, mask, 1.0 / math.sqrt(d), c.attn_dropout, self.training)
-        ctx = torch.matmul(probs.to(v.dtype), v).permute(0, 2, 1, 3).reshape(B, S, H)
+        if x.is_cuda and c.fused_attention and T.attention_supported(S, d):
+            # q/k/v read in place from the packed projection, bias fused (attention.hip)
+            ctx = T.fused_attention(_mm(x, self.w_qkv), self.b_qkv, mask, nh, 1.0 / math.sqrt(d),
+                                    c.attn_dropout, self.training)
+        else:
+            qkv = (_mm(x, self.w_qkv) + self.b_qkv.to(x.dtype)).view(B, S, 3, nh, d)
+            q = qkv[:, :, 0].permute(0, 2, 1, 3)
+            k = qkv[:, :, 1].permute(0, 2, 3, 1)
+            v = qkv[:, :, 2].permute(0, 2, 1, 3)
+            scores = torch.matmul(q, k)                                   # [B, nh, S, S]
+            probs = T.attention_softmax(scores, mask, 1.0 / math.sqrt(d), c.attn_dropout, self.training)
+            ctx = torch.matmul(probs.to(v.dtype), v).permute(0, 2, 1, 3).reshape(B, S, H)
         a = T.bias_dropout_residual_layernorm(_mm(ctx, self.w_o), self.b_o, x, self.ln1_g, self.ln1_b,
                                               c.dropout, c.ln_eps, self.training)
         hmid = T.bias_gelu(_mm(a, self.w_1), self.b_1)

@@ -204,5 +204,73 @@ def attention_softmax(scores, mask: Optional[torch.Tensor], scale: float, p: flo
     return _AttnSoftmax.apply(scores.to(torch.bfloat16), m, float(scale), float(p), Hh * Sq)
 
 
+# ---------------------------------------------------------------- fused self-attention
+class _FusedAttention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, bias, mask, nh, scale, p):
+        C = _C()
+        B, S, H3 = qkv.shape
+        out = torch.empty(B, S, H3 // 3, dtype=torch.bfloat16, device=qkv.device)
+        lse = torch.empty(B, nh, S, dtype=torch.float32, device=qkv.device)
+        seed = next_seed() if p > 0 else 0
+        C.attn_fwd(qkv, bias, mask, out, lse, nh, scale, p, seed)
+        ctx.save_for_backward(qkv, bias if bias is not None else torch.empty(0, device=qkv.device),
+                              mask if mask is not None else torch.empty(0, device=qkv.device), out, lse)
+        ctx.has_bias, ctx.has_mask = bias is not None, mask is not None
+        ctx.nh, ctx.scale, ctx.p, ctx.seed = nh, scale, p, seed
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        C = _C()
+        qkv, bias, mask, out, lse = ctx.saved_tensors
+        dqkv = torch.empty_like(qkv)
+        Dbuf = torch.empty_like(lse)
+        C.attn_bwd(qkv, bias if ctx.has_bias else None, mask if ctx.has_mask else None, out,
+                   dout.to(torch.bfloat16).contiguous(), lse, Dbuf, dqkv, ctx.nh, ctx.scale, ctx.p, ctx.seed)
+        dbias = dqkv.view(-1, dqkv.shape[-1]).sum(0, dtype=torch.float32) if ctx.has_bias else None
+        return dqkv, dbias, None, None, None, None
+
+
+def attention_reference(qkv, bias, mask, nh: int, scale: float, p: float = 0.0):
+    """softmax(scale * q k^T + mask) v per head from a packed [B, S, 3*H]
+    projection (+ bias); fp32 PyTorch (CPU oracle / fallback)."""
+    B, S, H3 = qkv.shape
+    d = H3 // (3 * nh)
+    x = qkv.float() + (bias.float() if bias is not None else 0.0)
+    x = x.view(B, S, 3, nh, d)
+    q, k, v = (x[:, :, i].permute(0, 2, 1, 3) for i in range(3))
+    z = torch.matmul(q, k.transpose(-1, -2)) * scale
+    if mask is not None:
+        z = z + mask.float()[:, None, None, :]
+    pr = torch.softmax(z, -1)
+    if p > 0:
+        pr = torch.nn.functional.dropout(pr, p, True)
+    return torch.matmul(pr, v).permute(0, 2, 1, 3).reshape(B, S, nh * d)
+
+
+def attention_supported(S: int, head_dim: int) -> bool:
+    try:
+        return bool(_C().attn_supported(S, head_dim))
+    except Exception:   # extension not built: callers take the unfused path
+        return False
+
+
+def fused_attention(qkv, bias, mask: Optional[torch.Tensor], nh: int, scale: float, p: float = 0.0,
+                    training: bool = True):
+    """Multi-head self-attention straight from the packed QKV projection.
+
+    qkv [B, S, 3*nh*64] (pre-bias GEMM output, bf16 on GPU), bias [3*nh*64]
+    fp32 or None, mask [B, S] additive fp32 or None -> context [B, S, nh*64].
+    GPU: csrc/kernels/attention.hip (one pass forward, two backward; prob
+    dropout regenerated from its hash).  CPU: attention_reference."""
+    p = p if training else 0.0
+    if not qkv.is_cuda:
+        return attention_reference(qkv, bias, mask, nh, scale, p)
+    m = mask.float().contiguous() if mask is not None else None
+    b = bias.float().contiguous() if bias is not None else None
+    return _FusedAttention.apply(qkv.to(torch.bfloat16).contiguous(), b, m, int(nh), float(scale), float(p))
+
+
 def gelu_ref(x):
     return 0.5 * x * (1.0 + torch.erf(x / math.sqrt(2.0)))

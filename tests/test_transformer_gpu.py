@@ -170,3 +170,65 @@ def test_bert_bf16_shadow_weights_match_casts(native):
             assert float((p1 - p2).abs().max()) < 6e-3, n
     for w in shad.gemm_weights():
         assert torch.equal(w._shadow, w.detach().bfloat16())
+
+
+def _unfused_attention(qkv, bias, mask, nh, scale, p):
+    """The model's pre-fusion GPU path: bias add, batched GEMMs, softmax kernel."""
+    from distributed_tensorflow_example_amd.ops import transformer as T
+    B, S, H3 = qkv.shape
+    d = H3 // (3 * nh)
+    x = (qkv + bias.to(qkv.dtype)).view(B, S, 3, nh, d)
+    q, k, v = x[:, :, 0].permute(0, 2, 1, 3), x[:, :, 1].permute(0, 2, 3, 1), x[:, :, 2].permute(0, 2, 1, 3)
+    probs = T.attention_softmax(torch.matmul(q, k), mask, scale, p)
+    return torch.matmul(probs.to(v.dtype), v).permute(0, 2, 1, 3).reshape(B, S, nh * d)
+
+
+@pytest.mark.parametrize("S", [32, 64, 128, 192, 256])
+def test_fused_attention_matches_fp32_reference(native, S):
+    from distributed_tensorflow_example_amd.ops import transformer as T
+    assert T.attention_supported(S, 64)
+    torch.manual_seed(S)
+    B, nh = 3, 4
+    qkv = (torch.randn(B, S, 3 * nh * 64) * 2).bfloat16()
+    bias = torch.randn(3 * nh * 64) * 0.5
+    mask = torch.zeros(B, S)
+    mask[1, S // 2:] = -10000.0
+    mask[2, S - 5:] = -10000.0
+    scale = 1 / 8
+    xr, br = qkv.float().requires_grad_(), bias.clone().requires_grad_()
+    ref = T.attention_reference(xr, br, mask, nh, scale)
+    dy = torch.randn_like(ref)
+    ref.backward(dy)
+    xg, bg = qkv.cuda().requires_grad_(), bias.cuda().requires_grad_()
+    out = T.fused_attention(xg, bg, mask.cuda(), nh, scale)
+    out.backward(dy.cuda().bfloat16())
+    assert out.shape == (B, S, nh * 64) and out.dtype == torch.bfloat16
+    assert rel(out, ref) < 1e-2
+    assert rel(xg.grad, xr.grad) < 3e-2
+    for part in range(3):                          # q, k, v blocks separately
+        sl = slice(part * nh * 64, (part + 1) * nh * 64)
+        assert rel(xg.grad[..., sl], xr.grad[..., sl]) < 3e-2, part
+    assert rel(bg.grad, br.grad) < 3e-2
+
+
+def test_fused_attention_dropout_matches_unfused_kernel_path(native):
+    """Same seed -> the fused kernel drops exactly the elements the softmax kernel drops."""
+    from distributed_tensorflow_example_amd.ops import transformer as T
+    torch.manual_seed(0)
+    B, S, nh, p = 2, 128, 4, 0.2
+    qkv = torch.randn(B, S, 3 * nh * 64, device="cuda").bfloat16()
+    bias = torch.randn(3 * nh * 64, device="cuda") * 0.3
+    mask = torch.zeros(B, S, device="cuda")
+    mask[0, 100:] = -10000.0
+    dy = torch.randn(B, S, nh * 64, device="cuda").bfloat16()
+    outs = []
+    for fused in (True, False):
+        T.set_dropout_seed(1234)
+        x, b = qkv.clone().requires_grad_(), bias.clone().requires_grad_()
+        o = T.fused_attention(x, b, mask, nh, 0.125, p) if fused else _unfused_attention(x, b, mask, nh, 0.125, p)
+        o.backward(dy)
+        outs.append((o, x.grad, b.grad))
+    (o1, g1, b1), (o2, g2, b2) = outs
+    assert rel(o1, o2) < 2e-2
+    assert rel(g1, g2) < 4e-2
+    assert rel(b1, b2) < 4e-2

@@ -73,15 +73,40 @@ class _ShadowLinear(torch.autograd.Function):
         x, w16 = ctx.saved_tensors
         gy = gy.to(w16.dtype)
         gx = gy @ w16
-        gy2, x2 = gy.reshape(-1, gy.shape[-1]).t(), x.reshape(-1, x.shape[-1])
+        gy2, x2 = gy.reshape(-1, gy.shape[-1]), x.reshape(-1, x.shape[-1])
         w = ctx.w
         if grad_sink.enabled(w) and (w.grad is None or w.grad.is_contiguous()):
-            g = grad_sink.target(w)
-            torch.addmm(g, gy2, x2, out_dtype=torch.float32, out=g)   # beta = 1 onto the bucket view
+            _wgrad(gy2, x2, into=grad_sink.target(w))
             grad_sink.done(w)
             return gx, None, None
-        gw = torch.mm(gy2, x2, out_dtype=torch.float32)
-        return gx, gw, None
+        return gx, _wgrad(gy2, x2), None
+
+
+def _wgrad_split(T: int, out: int, inp: int) -> int:
+    """Token-slab count for the weight-gradient GEMM.  dW = gy^T x has a long
+    reduction (T = B*S tokens) and few output tiles (36-144 of 128x128 for
+    BERT-base), so one hipBLASLt GEMM leaves most of the 256 CUs idle
+    (~0.5 PFLOP/s measured, scripts/wgrad_probe.py); slabs run as one batched
+    GEMM with ~4 tile waves and are reduced in fp32 (1.5-2.5x faster)."""
+    tiles = max(1, (out // 128) * (inp // 128))
+    s = 1
+    while s < 16 and tiles * s * 2 <= 1024 and T % (2 * s) == 0 and T // (2 * s) >= 512:
+        s *= 2
+    return s
+
+
+def _wgrad(gy2, x2, into=None):
+    """dW[out, in] = gy2[T, out]^T @ x2[T, in] in fp32 (accumulated into `into`)."""
+    T, out = gy2.shape
+    s = _wgrad_split(T, out, x2.shape[1]) if gy2.is_cuda else 1
+    if s == 1:
+        if into is not None:
+            return torch.addmm(into, gy2.t(), x2, out_dtype=torch.float32, out=into)
+        return torch.mm(gy2.t(), x2, out_dtype=torch.float32)
+    parts = torch.bmm(gy2.view(s, T // s, out).transpose(1, 2), x2.view(s, T // s, -1), out_dtype=torch.float32)
+    if into is not None:
+        return into.add_(parts.sum(0))
+    return parts.sum(0)
 
 
 def _mm(x, w):
@@ -164,6 +189,7 @@ class BertForMLM(torch.nn.Module):
             self.head_g = torch.nn.Parameter(torch.ones(c.hidden))
             self.head_beta = torch.nn.Parameter(torch.zeros(c.hidden))
             self.dec_b = torch.nn.Parameter(torch.zeros(c.vocab_size))
+        grad_sink.mark_tied(self.word)          # embedding lookup + MLM decoder
 
     def gemm_weights(self):
         ws = [self.head_w, self.word]

@@ -24,7 +24,14 @@ _HOOK = "_dtf_sink_hook"
 
 
 def enabled(p: torch.Tensor) -> bool:
-    return getattr(p, _HOOK, None) is not None and p.requires_grad
+    # a tied parameter (used by several ops, e.g. BERT's word embedding and
+    # decoder) must reach .grad through autograd, which sums its uses and fires
+    # the bucket-ready hook once
+    return getattr(p, _HOOK, None) is not None and p.requires_grad and not getattr(p, "_dtf_tied", False)
+
+
+def mark_tied(p: torch.Tensor) -> None:
+    p._dtf_tied = True
 
 
 def target(p: torch.Tensor) -> torch.Tensor:

@@ -108,16 +108,27 @@ class DistributedDataParallel(torch.nn.Module):
                 for p in params:
                     self.world.broadcast(p.data, 0)  # chief init + broadcast
         self._launched = set()
+        self._counted = set()
 
     # ------------------------------------------------------------------ forward
-    def forward(self, *a, **kw):
+    def reset_step(self):
+        """Start a new iteration's readiness bookkeeping (forward() calls it)."""
         self._launched.clear()
+        self._counted.clear()
         for b in self.buckets:
             b.ready = 0
+
+    def forward(self, *a, **kw):
+        self.reset_step()
         return self.module(*a, **kw)
 
     # ------------------------------------------------------------------ hooks
     def _on_grad(self, p):
+        # a sunk gradient reports itself and autograd's post-accumulate hook
+        # still fires (with nothing accumulated) afterwards: count once
+        if id(p) in self._counted:
+            return
+        self._counted.add(id(p))
         bi, idx = self._param_bucket[p]
         b = self.buckets[bi]
         view = b.views[idx]
@@ -168,9 +179,7 @@ class DistributedDataParallel(torch.nn.Module):
                 b.work = None
                 if self.average and w.world_size > 1:
                     b.buf.mul_(1.0 / w.world_size)
-        self._launched.clear()
-        for b in self.buckets:
-            b.ready = 0
+        self.reset_step()
 
     def zero_grad(self):
         for b in self.buckets:

@@ -134,9 +134,7 @@ def dense_bench(a, w):
 
     def step(b):
         ddp.zero_grad()
-        ddp._launched.clear()
-        for bk in ddp.buckets:
-            bk.ready = 0
+        ddp.reset_step()
         loss = run(model, b)
         loss.backward()
         ddp.finish_gradient_synchronization()

@@ -76,7 +76,9 @@ def test_bert_gemm_sink_matches_plain(native):
     ddp = _ddp(sunk)
     for _ in range(2):
         plain(*b).backward()
-        sunk(*b).backward()
+        ddp(*b).backward()                       # DDP.forward resets the per-bucket ready counts
+        # every parameter reported ready exactly once (tied word embedding included)
+        assert [bk.ready for bk in ddp.buckets] == [len(bk.params) for bk in ddp.buckets]
     gw = {id(w) for w in sunk.gemm_weights()}
     for (n, p1), p2 in zip(plain.named_parameters(), sunk.parameters()):
         assert rel(p2.grad, p1.grad) < 1e-3, n

@@ -18,6 +18,10 @@ hipError_t dtfk_softmax_xent(const float* logits, const int64_t* labels, const f
                              hipStream_t s);
 hipError_t dtfk_sigmoid_xent(const float* x, const float* t, float* loss, float* grad, int64_t n,
                              float grad_scale, hipStream_t s);
+hipError_t dtfk_xent_fwd_bf16(const void* logits, const float* bias, const int64_t* labels, float* lse_rows,
+                              float* loss_rows, int B, int C, hipStream_t s);
+hipError_t dtfk_xent_bwd_bf16(const void* logits, const float* bias, const int64_t* labels, const float* lse_rows,
+                              const float* dloss, void* grad, int B, int C, float scale, hipStream_t s);
 hipError_t dtfk_embedding_bag_fwd(const float* W, int64_t V, int D, const int64_t* ids, const int64_t* offsets,
                                   const float* psw, int B, int mode, float* out, int64_t* bad, hipStream_t s);
 hipError_t dtfk_embedding_bag_bwd(float* target, int64_t V, int D, const int64_t* ids, const int64_t* offsets,
@@ -100,6 +104,41 @@ void col_sum(at::Tensor X, at::Tensor out) {
   const int N = (int)X.size(-1);
   const int M = (int)(X.numel() / std::max<int64_t>(1, N));
   ck(dtfk_col_sum(X.data_ptr<float>(), out.data_ptr<float>(), M, N, cs()), "col_sum");
+}
+
+static void bf16xent_check(const at::Tensor& logits, const c10::optional<at::Tensor>& bias, const at::Tensor& labels) {
+  if (!logits.is_cuda() || logits.scalar_type() != at::kBFloat16 || !logits.is_contiguous() || logits.dim() != 2 ||
+      logits.size(1) % 2)
+    throw std::runtime_error("xent_bf16: logits must be contiguous [B, C] bf16 on GPU with C even");
+  i64c(labels, "labels");
+  if (labels.numel() != logits.size(0)) throw std::runtime_error("xent_bf16: labels must be [B]");
+  if (bias.has_value()) {
+    f32c(*bias, "bias");
+    if (bias->numel() != logits.size(1)) throw std::runtime_error("xent_bf16: bias must be [C]");
+  }
+}
+
+void xent_fwd_bf16(at::Tensor logits, c10::optional<at::Tensor> bias, at::Tensor labels, at::Tensor lse_rows,
+                   at::Tensor loss_rows) {
+  bf16xent_check(logits, bias, labels);
+  f32c(lse_rows, "lse_rows"); f32c(loss_rows, "loss_rows");
+  ck(dtfk_xent_fwd_bf16(logits.data_ptr(), opt_ptr<float>(bias), labels.data_ptr<int64_t>(), lse_rows.data_ptr<float>(),
+                        loss_rows.data_ptr<float>(), (int)logits.size(0), (int)logits.size(1), cs()),
+     "xent_fwd_bf16");
+}
+
+void xent_bwd_bf16(at::Tensor logits, c10::optional<at::Tensor> bias, at::Tensor labels, at::Tensor lse_rows,
+                   c10::optional<at::Tensor> dloss, at::Tensor grad, double scale) {
+  bf16xent_check(logits, bias, labels);
+  f32c(lse_rows, "lse_rows");
+  if (dloss.has_value()) f32c(*dloss, "dloss");
+  if (!grad.is_cuda() || grad.scalar_type() != at::kBFloat16 || !grad.is_contiguous() ||
+      grad.numel() != logits.numel())
+    throw std::runtime_error("xent_bwd_bf16: grad must be a contiguous bf16 tensor like logits");
+  ck(dtfk_xent_bwd_bf16(logits.data_ptr(), opt_ptr<float>(bias), labels.data_ptr<int64_t>(), lse_rows.data_ptr<float>(),
+                        opt_ptr<float>(dloss), grad.data_ptr(), (int)logits.size(0), (int)logits.size(1),
+                        (float)scale, cs()),
+     "xent_bwd_bf16");
 }
 
 void softmax_xent(at::Tensor logits, c10::optional<at::Tensor> labels, c10::optional<at::Tensor> ydense,
@@ -196,6 +235,8 @@ void init_ops(py::module& m) {
   m.def("act_backward", &act_backward);
   m.def("col_sum", &col_sum);
   m.def("softmax_xent", &softmax_xent);
+  m.def("xent_fwd_bf16", &xent_fwd_bf16);
+  m.def("xent_bwd_bf16", &xent_bwd_bf16);
   m.def("sigmoid_xent", &sigmoid_xent);
   m.def("embedding_bag_fwd", &embedding_bag_fwd);
   m.def("embedding_bag_bwd", &embedding_bag_bwd);

@@ -122,6 +122,73 @@ __global__ void softmax_xent(const float* __restrict__ logits, const int64_t* __
   }
 }
 
+// bf16 logits (+ fp32 bias), int64 labels, one 256-thread block per row (vocab-
+// sized rows: the MLM decoder's [masked tokens, 30522]).  Forward is one read
+// with an online max/sum (lse and loss per row); backward recomputes
+// softmax from lse and writes dlogits = (softmax - onehot) * scale * dloss in
+// bf16 -- the upstream scalar gradient is read from device memory, so no
+// separate scaling pass.  C must be even (4-byte = 2-logit accesses).
+__device__ __forceinline__ void lse_combine(float& m, float& s, float om, float os) {
+  const float nm = fmaxf(m, om);
+  s = s * __expf(m - nm) + os * __expf(om - nm);
+  m = nm;
+}
+
+__global__ __launch_bounds__(256) void xent_fwd_bf16(const uint16_t* __restrict__ logits, const float* __restrict__ bias,
+                                                     const int64_t* __restrict__ labels, float* __restrict__ lse_rows,
+                                                     float* __restrict__ loss_rows, int Cn) {
+  __shared__ float sm[4], ss[4];
+  const int row = blockIdx.x;
+  const uint32_t* z = reinterpret_cast<const uint32_t*>(logits + (size_t)row * Cn);
+  const int n2 = Cn >> 1;
+  float m = -3.0e38f, s = 0.f;
+  for (int i = threadIdx.x; i < n2; i += 256) {
+    const uint32_t w = z[i];
+    float a = bf2f(w & 0xffff), b = bf2f(w >> 16);
+    if (bias) { a += bias[2 * i]; b += bias[2 * i + 1]; }
+    const float nm = fmaxf(m, fmaxf(a, b));
+    s = s * __expf(m - nm) + __expf(a - nm) + __expf(b - nm);
+    m = nm;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) lse_combine(m, s, __shfl_xor(m, off, 64), __shfl_xor(s, off, 64));
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { sm[w] = m; ss[w] = s; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float M = sm[0], S = ss[0];
+    for (int k = 1; k < 4; ++k) lse_combine(M, S, sm[k], ss[k]);
+    const float lse = M + __logf(S);
+    int y = (int)labels[row];
+    y = y < 0 ? 0 : (y >= Cn ? Cn - 1 : y);
+    const float zy = bf2f(logits[(size_t)row * Cn + y]) + (bias ? bias[y] : 0.f);
+    lse_rows[row] = lse;
+    loss_rows[row] = lse - zy;
+  }
+}
+
+__global__ __launch_bounds__(256) void xent_bwd_bf16(const uint16_t* __restrict__ logits, const float* __restrict__ bias,
+                                                     const int64_t* __restrict__ labels,
+                                                     const float* __restrict__ lse_rows, const float* __restrict__ dloss,
+                                                     uint16_t* __restrict__ grad, int Cn, float scale) {
+  const int row = blockIdx.x;
+  const uint32_t* z = reinterpret_cast<const uint32_t*>(logits + (size_t)row * Cn);
+  uint32_t* gr = reinterpret_cast<uint32_t*>(grad + (size_t)row * Cn);
+  const float lse = lse_rows[row];
+  const float sc = scale * (dloss ? dloss[0] : 1.f);
+  int y = (int)labels[row];
+  y = y < 0 ? 0 : (y >= Cn ? Cn - 1 : y);
+  const int n2 = Cn >> 1;
+  for (int i = threadIdx.x; i < n2; i += 256) {
+    const uint32_t w = z[i];
+    float a = bf2f(w & 0xffff), b = bf2f(w >> 16);
+    if (bias) { a += bias[2 * i]; b += bias[2 * i + 1]; }
+    const float ga = (__expf(a - lse) - (2 * i == y ? 1.f : 0.f)) * sc;
+    const float gb = (__expf(b - lse) - (2 * i + 1 == y ? 1.f : 0.f)) * sc;
+    gr[i] = pack2bf(ga, gb);
+  }
+}
+
 // max(x,0) - x*t + log1p(exp(-|x|)); grad (sigmoid(x) - t) * scale
 __global__ void sigmoid_xent(const float* __restrict__ x, const float* __restrict__ t,
                              float* __restrict__ loss, float* __restrict__ grad, int64_t n,
@@ -369,6 +436,20 @@ hipError_t dtfk_softmax_xent(const float* logits, const int64_t* labels, const f
                              hipStream_t s) {
   hipLaunchKernelGGL(softmax_xent, dim3((B + 3) / 4), dim3(256), 0, s, logits, labels, ydense, loss_rows,
                      grad, correct, B, C, grad_scale, naive);
+  return hipGetLastError();
+}
+hipError_t dtfk_xent_fwd_bf16(const void* logits, const float* bias, const int64_t* labels, float* lse_rows,
+                              float* loss_rows, int B, int C, hipStream_t s) {
+  if (C % 2) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(xent_fwd_bf16, dim3(B), dim3(256), 0, s, (const uint16_t*)logits, bias, labels, lse_rows,
+                     loss_rows, C);
+  return hipGetLastError();
+}
+hipError_t dtfk_xent_bwd_bf16(const void* logits, const float* bias, const int64_t* labels, const float* lse_rows,
+                              const float* dloss, void* grad, int B, int C, float scale, hipStream_t s) {
+  if (C % 2) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(xent_bwd_bf16, dim3(B), dim3(256), 0, s, (const uint16_t*)logits, bias, labels, lse_rows, dloss,
+                     (uint16_t*)grad, C, scale);
   return hipGetLastError();
 }
 hipError_t dtfk_sigmoid_xent(const float* x, const float* t, float* loss, float* grad, int64_t n,

@@ -275,6 +275,76 @@ __global__ __launch_bounds__(256) void bias_gelu_bwd(const uint16_t* __restrict_
   p[0] = acc[0]; p[1] = acc[1]; p[2] = acc[2]; p[3] = acc[3];
 }
 
+// 8-wide forms (H % 8 == 0): 16-byte accesses, four rows in flight per thread.
+__device__ __forceinline__ void ld8v(const uint16_t* p, float* f) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { f[2 * j] = bf2f(w[j] & 0xffff); f[2 * j + 1] = bf2f(w[j] >> 16); }
+}
+__device__ __forceinline__ void st8v(uint16_t* p, const float* f) {
+  *reinterpret_cast<uint4*>(p) = uint4{pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]), pack2bf(f[6], f[7])};
+}
+
+__global__ __launch_bounds__(256) void bias_gelu_fwd8(const uint16_t* __restrict__ x, const float* __restrict__ bias,
+                                                      uint16_t* __restrict__ y, int64_t n8, int H) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)((i * 8) % H);
+    float xv[8], bv[8], o[8];
+    ld8v(x + i * 8, xv);
+    ld4f(bias + c, bv);
+    ld4f(bias + c + 4, bv + 4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = gelu_f(xv[j] + bv[j]);
+    st8v(y + i * 8, o);
+  }
+}
+
+// Block = 128 threads x 8 columns (a 1024-column strip); grid = (strips, row slices)
+__global__ __launch_bounds__(128) void bias_gelu_bwd8(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
+                                                      const float* __restrict__ bias, uint16_t* __restrict__ dx,
+                                                      float* __restrict__ part, int N, int H, int rows_per) {
+  const int c = (blockIdx.x * 128 + threadIdx.x) * 8;
+  if (c >= H) return;
+  const int r0 = blockIdx.y * rows_per, r1 = min(N, r0 + rows_per);
+  float bv[8], acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  ld4f(bias + c, bv);
+  ld4f(bias + c + 4, bv + 4);
+  int r = r0;
+  for (; r + 3 < r1; r += 4) {
+    float dv[4][8], xv[4][8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      ld8v(dy + (size_t)(r + k) * H + c, dv[k]);
+      ld8v(x + (size_t)(r + k) * H + c, xv[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        o[j] = dv[k][j] * gelu_grad(xv[k][j] + bv[j]);
+        acc[j] += o[j];
+      }
+      st8v(dx + (size_t)(r + k) * H + c, o);
+    }
+  }
+  for (; r < r1; ++r) {
+    float dv[8], xv[8], o[8];
+    ld8v(dy + (size_t)r * H + c, dv);
+    ld8v(x + (size_t)r * H + c, xv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      o[j] = dv[j] * gelu_grad(xv[j] + bv[j]);
+      acc[j] += o[j];
+    }
+    st8v(dx + (size_t)r * H + c, o);
+  }
+  float* p = part + (size_t)blockIdx.y * H + c;
+  *reinterpret_cast<float4*>(p) = float4{acc[0], acc[1], acc[2], acc[3]};
+  *reinterpret_cast<float4*>(p + 4) = float4{acc[4], acc[5], acc[6], acc[7]};
+}
+
 // column sums of a [P, H] fp32 partial buffer -> out[H] (deterministic).
 // 1024 threads = 64 consecutive columns x 16 row groups (coalesced 256 B
 // rows), LDS tree over the groups; grid = ceil(H / 64).
@@ -477,6 +547,14 @@ hipError_t dtfk_colsum_partials(const float* part, float* out, int P, int H, hip
 }
 
 hipError_t dtfk_bias_gelu_fwd(const void* x, const float* bias, void* y, long long n, int H, hipStream_t st) {
+  if (H % 8 == 0) {
+    const long long n8 = n / 8;
+    long long g8 = (n8 + 255) / 256;
+    if (g8 > 32768) g8 = 32768;
+    hipLaunchKernelGGL(bias_gelu_fwd8, dim3((unsigned)g8), dim3(256), 0, st, (const uint16_t*)x, bias,
+                       (uint16_t*)y, (int64_t)n8, H);
+    return hipGetLastError();
+  }
   const long long n4 = n / 4;
   long long g = (n4 + 255) / 256;
   if (g > 65536) g = 65536;
@@ -488,8 +566,12 @@ hipError_t dtfk_bias_gelu_fwd(const void* x, const float* bias, void* y, long lo
 hipError_t dtfk_bias_gelu_bwd(const void* dy, const void* x, const float* bias, void* dx, float* part, int N, int H,
                               int row_slices, hipStream_t st) {
   const int rows_per = (N + row_slices - 1) / row_slices;
-  hipLaunchKernelGGL(bias_gelu_bwd, dim3((H / 4 + 255) / 256, row_slices), dim3(256), 0, st, (const uint16_t*)dy,
-                     (const uint16_t*)x, bias, (uint16_t*)dx, part, N, H, rows_per);
+  if (H % 8 == 0)
+    hipLaunchKernelGGL(bias_gelu_bwd8, dim3((H / 8 + 127) / 128, row_slices), dim3(128), 0, st, (const uint16_t*)dy,
+                       (const uint16_t*)x, bias, (uint16_t*)dx, part, N, H, rows_per);
+  else
+    hipLaunchKernelGGL(bias_gelu_bwd, dim3((H / 4 + 255) / 256, row_slices), dim3(256), 0, st, (const uint16_t*)dy,
+                       (const uint16_t*)x, bias, (uint16_t*)dx, part, N, H, rows_per);
   return hipGetLastError();
 }
 

@@ -232,8 +232,7 @@ class BertForMLM(torch.nn.Module):
         zero = torch.zeros(c.hidden, device=h.device)
         h = T.bias_dropout_residual_layernorm(h, zero, None, self.head_g, self.head_beta, 0.0, c.ln_eps,
                                               self.training)
-        logits = (_mm(h, self.word) + self.dec_b.to(h.dtype)).float()
-        return ops.softmax_xent(logits, mlm_labels)
+        return ops.softmax_xent(_mm(h, self.word), mlm_labels, bias=self.dec_b)   # bias fused in the xent kernels
 
 
 def synthetic_mlm_batch(batch: int, seq: int, vocab: int, device, mask_prob: float = 0.15, seed: int = 0):

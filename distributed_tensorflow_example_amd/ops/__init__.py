@@ -147,9 +147,43 @@ class _SoftmaxXent(torch.autograd.Function):
         return grad * g, None, None, None
 
 
-def softmax_xent(logits, labels, naive: bool = False):
-    """mean softmax cross-entropy; labels: int class ids [B] or dense [B, C]."""
+class _XentBF16(torch.autograd.Function):
+    """Vocab-sized rows: bf16 logits (+ fp32 bias) read once forward, once backward."""
+
+    @staticmethod
+    def forward(ctx, logits, bias, labels):
+        C = _C()
+        Bn = logits.shape[0]
+        lse = torch.empty(Bn, dtype=torch.float32, device=logits.device)
+        loss_rows = torch.empty_like(lse)
+        C.xent_fwd_bf16(logits, bias, labels, lse, loss_rows)
+        ctx.save_for_backward(logits, bias if bias is not None else torch.empty(0, device=logits.device), labels, lse)
+        ctx.has_bias = bias is not None
+        return loss_rows.mean()
+
+    @staticmethod
+    def backward(ctx, g):
+        C = _C()
+        logits, bias, labels, lse = ctx.saved_tensors
+        grad = torch.empty_like(logits)
+        C.xent_bwd_bf16(logits, bias if ctx.has_bias else None, labels, lse, g.float().reshape(1).contiguous(), grad,
+                        1.0 / logits.shape[0])
+        dbias = grad.sum(0, dtype=torch.float32) if ctx.has_bias else None
+        return grad, dbias, None
+
+
+def softmax_xent(logits, labels, naive: bool = False, bias=None):
+    """mean softmax cross-entropy; labels: int class ids [B] or dense [B, C].
+
+    `bias` [C] (optional) is added to the logits inside the kernels; bf16 GPU
+    logits with int labels take the vocab-row kernels (no fp32 copy)."""
     dense = labels.dim() == 2
+    if (logits.is_cuda and logits.dtype == torch.bfloat16 and not dense and not naive
+            and logits.dim() == 2 and logits.shape[1] % 2 == 0):
+        b = bias.float().contiguous() if bias is not None else None
+        return _XentBF16.apply(logits.contiguous(), b, labels.contiguous().long())
+    if bias is not None:
+        logits = logits.float() + bias.float()
     if not logits.is_cuda:
         logp = torch.log_softmax(logits.float(), 1)
         if naive:

@@ -152,7 +152,7 @@ class _BiasGelu(torch.autograd.Function):
         H = x.shape[-1]
         N = x.numel() // H
         dx = torch.empty_like(x)
-        slices = max(1, min(128, N // 32))
+        slices = max(1, min(512, N // 32))        # >= 32 rows per thread, ~1.5k blocks at BERT-base
         part = torch.empty(slices * H, dtype=torch.float32, device=x.device)
         dbias = torch.empty(H, dtype=torch.float32, device=x.device)
         C.bias_gelu_bwd(dy.to(torch.bfloat16).contiguous(), x, bias, dx, part, dbias)

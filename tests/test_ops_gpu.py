@@ -261,3 +261,23 @@ def test_compat_mnist_graph_trains_on_gpu(native):
         assert int(np.asarray(sess.run(gs))) == 200
     assert W1.value.is_cuda
     assert c < first and a > 0.4
+
+
+@pytest.mark.parametrize("C", [30522, 10, 1002])
+def test_bf16_vocab_xent_with_bias(native, C):
+    from distributed_tensorflow_example_amd import ops
+    torch.manual_seed(C)
+    B = 37
+    logits = (torch.randn(B, C) * 3).bfloat16()
+    bias = torch.randn(C) * 0.5
+    labels = torch.randint(0, C, (B,))
+    lr_, br = logits.float().requires_grad_(), bias.clone().requires_grad_()
+    ref = torch.nn.functional.cross_entropy(lr_ + br, labels)
+    (ref * 3.0).backward()
+    lg, bg = logits.cuda().requires_grad_(), bias.cuda().requires_grad_()
+    out = ops.softmax_xent(lg, labels.cuda(), bias=bg)
+    (out * 3.0).backward()                       # upstream scale is read on device
+    assert abs(float(out) - float(ref)) < 1e-3 * max(1.0, abs(float(ref)))
+    assert lg.grad.dtype == torch.bfloat16
+    assert float((lg.grad.float().cpu() - lr_.grad).norm() / lr_.grad.norm()) < 1e-2
+    assert float((bg.grad.cpu() - br.grad).norm() / br.grad.norm()) < 1e-2

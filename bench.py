@@ -35,7 +35,8 @@ if REPO not in sys.path:
     sys.path.insert(0, REPO)
 
 from distributed_tensorflow_example_amd.data.mnist import PinnedEpoch, synthetic_mnist  # noqa: E402
-from distributed_tensorflow_example_amd.models.mlp import FusedMLPTrainer, MLPStepRunner  # noqa: E402
+from distributed_tensorflow_example_amd.models.mlp import (  # noqa: E402
+    FusedMLPTrainer, MLPStepRunner, PersistentMLPRunner)
 from distributed_tensorflow_example_amd.parallel import world as world_mod  # noqa: E402
 
 METRIC = "samples/sec (whole node) MNIST MLP sync-SGD at 1/2/4/8 MI355X; step-time p50"
@@ -54,6 +55,9 @@ def main(argv=None):
     ap.add_argument("--act", choices=["sigmoid", "relu"], default="sigmoid")
     ap.add_argument("--train-examples", type=int, default=55000)
     ap.add_argument("--prefetch", choices=["serial", "side"], default="serial")
+    ap.add_argument("--engine", choices=["auto", "persistent", "launches"], default="launches",
+                    help="1 GPU: persistent weight-stationary kernel, one launch per chunk (default), or "
+                         "3 fused launches per step replayed from hipGraphs")
     ap.add_argument("--allreduce", choices=["auto", "ipc-fused", "ipc-apply", "rccl"], default="auto",
                     help="N>1 gradient exchange: IPC over xGMI inside the wgrad kernel (ipc-fused, default), "
                          "IPC one-shot in a separate reduce+apply kernel (ipc-apply), or RCCL")
@@ -86,9 +90,18 @@ def main(argv=None):
     epoch = PinnedEpoch(imgs, labels, a.batch)
     gd = torch.bfloat16 if a.grad_dtype == "bf16" else torch.float32
 
+    persistent = a.engine == "persistent" or (a.engine == "auto" and w.world_size == 1 and a.batch <= 112)
+
     def setup(allreduce):
         trainer = FusedMLPTrainer(batch_size=a.batch, lr=a.lr, act=a.act, world=w, grad_dtype=gd,
                                   device=dev, allreduce=allreduce)
+        if persistent:
+            runner = PersistentMLPRunner(trainer, epoch, steps_per_launch=a.steps_per_graph)
+            runner.run(a.warmup)
+            torch.cuda.synchronize()
+            if runner.error():
+                raise SystemExit("persistent kernel exchange timed out during warmup")
+            return trainer, runner
         runner = MLPStepRunner(trainer, epoch, steps_per_graph=a.steps_per_graph,
                                use_graph=not a.eager, prefetch=a.prefetch)
         # warmup: eager first (module load), then the graphs the warmup itself needs
@@ -146,6 +159,8 @@ def main(argv=None):
     p50 = statistics.median(per_step_ms) if per_step_ms else float("nan")
     p50 = w.host_all_reduce(p50, "max")
 
+    if persistent and runner.error():
+        raise SystemExit("persistent kernel exchange timed out during the timed run; result discarded")
     if w.world_size > 1 and not consistent(trainer):
         raise SystemExit("replicas diverged / IPC timeout during the timed run; result discarded")
     steps_done = trainer.global_step - step0
@@ -166,7 +181,9 @@ def main(argv=None):
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16",
-            "data": "synthetic MNIST-shaped uint8, streamed per 50-step chunk pinned host -> device by hipMemcpyAsync; random-init weights",
+            "data": ("synthetic MNIST-shaped uint8 resident in pinned host memory, streamed per chunk over PCIe "
+                     + ("by copier workgroups inside the persistent launch" if persistent else
+                        "by hipMemcpyAsync inside the chunk's hipGraph") + "; random-init weights"),
             "config": {
                 "model": "mlp-784-100-10 (example.py)",
                 "global_batch": a.batch * n,
@@ -175,8 +192,10 @@ def main(argv=None):
                 "parallelism": f"dp{n}",
                 "optimizer": f"sgd lr={a.lr}",
                 "grad_allreduce": f"{a.grad_dtype} {trainer.allreduce}" if n > 1 else "none",
-                "hipgraph_steps": 0 if a.eager else a.steps_per_graph,
-                "input_prefetch": a.prefetch,
+                "engine": "persistent" if persistent else "launches",
+                "steps_per_launch": a.steps_per_graph if persistent else 1,
+                "hipgraph_steps": 0 if (a.eager or persistent) else a.steps_per_graph,
+                "input_prefetch": "in-kernel copier workgroups" if persistent else a.prefetch,
                 "activation": a.act,
             },
             "final_loss": round(float(m[0]), 5),

@@ -4,6 +4,7 @@
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <stdexcept>
 #include <string>
 
@@ -28,6 +29,15 @@ hipError_t dtfk_mlp_ipc_reduce_apply(float* params, void* const* peer_table, int
                                      long long slot_bytes, const long long* gstep, const float* lr, float scale,
                                      void* W1T, void* W2T, void* W2N, int* err, long long timeout_ticks,
                                      hipStream_t stream);
+int dtfk_mlp_persist_gran_count();
+int dtfk_mlp_persist_xt_bytes();
+int dtfk_mlp_persist_max_batch();
+int dtfk_mlp_persist_stage_rec(int B);
+hipError_t dtfk_mlp_persist(const void* xs, const void* xts, long long rec, long long rec_h, int B, int nsteps, float* params,
+                            const float* lr, float* metrics, int ring, int act, int naive, long long* gstep,
+                            unsigned long long* seq, unsigned long long* gran, int* err, long long timeout,
+                            const void* host_next, int next_steps, void* xs_next, void* xts_next,
+                            long long* ts, hipStream_t stream);
 hipError_t dtfk_mlp_fwd_head(const void* x, int x_kind, int B, const void* W1T, float* z2p, const void* labels,
                              const void* W2T, const void* W2N, const float* params, void* dz2T, int BP,
                              float* partials, float inv_batch, int act, int naive_loss, int* counters,
@@ -235,7 +245,75 @@ void memcpy_h2d_async(at::Tensor dst, int64_t dst_offset, at::Tensor src, int64_
             "hipMemcpyAsync");
 }
 
+// Persistent weight-stationary MLP launch (csrc/kernels/mlp_persist.hip):
+// runs `nsteps` SGD steps of the chunk staged in (xs, xts) and, in the same
+// launch, copies `next_steps` records starting at byte `host_off` of the
+// pinned host epoch into (xs_next, xts_next).  nsteps = 0: copy only.
+void mlp_persist(at::Tensor xs, at::Tensor xts, int64_t rec, int B, int nsteps, at::Tensor params, at::Tensor lr,
+                 at::Tensor metrics, at::Tensor gstep, at::Tensor seq, at::Tensor gran, at::Tensor err,
+                 double timeout_s, int act, int naive, c10::optional<at::Tensor> host, int64_t host_off,
+                 int next_steps, c10::optional<at::Tensor> xs_next, c10::optional<at::Tensor> xts_next,
+                 c10::optional<at::Tensor> ts) {
+  if (B <= 0 || B > dtfk_mlp_persist_max_batch()) throw std::runtime_error("mlp_persist: B out of range");
+  if (rec < (int64_t)B * 785 || rec % 16 != 0) throw std::runtime_error("mlp_persist: bad record size");
+  const int64_t rec_h = rec;                        // host record (pinned epoch)
+  const int64_t rec_s = dtfk_mlp_persist_stage_rec(B);   // device stage record (permuted rows)
+  const int64_t xtb = dtfk_mlp_persist_xt_bytes();
+  need(xs, at::kByte, (int64_t)std::max(nsteps, 1) * rec_s, "xs");
+  need(xts, at::kByte, (int64_t)std::max(nsteps, 1) * xtb, "xts");
+  need(params, at::kFloat, kNParam, "params");
+  need(lr, at::kFloat, 1, "lr");
+  need(metrics, at::kFloat, 2, "metrics");
+  need(gstep, at::kLong, 1, "gstep");
+  need(seq, at::kLong, 1, "seq");
+  need(gran, at::kLong, dtfk_mlp_persist_gran_count(), "gran");
+  need(err, at::kInt, 1, "err");
+  if (((uintptr_t)xs.data_ptr() | (uintptr_t)xts.data_ptr()) % 16 != 0)
+    throw std::runtime_error("mlp_persist: stage buffers must be 16-byte aligned");
+  const void* hn = nullptr;
+  void* xn = nullptr;
+  void* xtn = nullptr;
+  if (next_steps > 0) {
+    if (!host.has_value() || !xs_next.has_value() || !xts_next.has_value())
+      throw std::runtime_error("mlp_persist: next chunk needs host, xs_next, xts_next");
+    const at::Tensor& h = *host;
+    if (h.is_cuda() || !h.is_pinned()) throw std::runtime_error("mlp_persist: host must be pinned host memory");
+    if (host_off < 0 || host_off % 16 != 0 ||
+        host_off + (int64_t)next_steps * rec_h > (int64_t)(h.numel() * h.element_size()))
+      throw std::runtime_error("mlp_persist: host range out of bounds");
+    need(*xs_next, at::kByte, (int64_t)next_steps * rec_s, "xs_next");
+    need(*xts_next, at::kByte, (int64_t)next_steps * xtb, "xts_next");
+    void* dp = nullptr;
+    char* hp = reinterpret_cast<char*>(h.data_ptr()) + host_off;
+    if (hipHostGetDevicePointer(&dp, hp, 0) != hipSuccess || dp == nullptr) {
+      (void)hipGetLastError();
+      dp = hp;   // unified addressing: the host address is device-visible
+    }
+    if (reinterpret_cast<uintptr_t>(dp) % 16 != 0) throw std::runtime_error("mlp_persist: host not aligned");
+    hn = dp;
+    xn = xs_next->data_ptr();
+    xtn = xts_next->data_ptr();
+  }
+  const long long ticks = (long long)(timeout_s * 1e8);   // s_memrealtime: 100 MHz
+  hip_check(dtfk_mlp_persist(xs.data_ptr(), xts.data_ptr(), rec_s, rec_h, B, nsteps, params.data_ptr<float>(),
+                             lr.data_ptr<float>(), metrics.data_ptr<float>(), (int)(metrics.numel() / 2), act, naive,
+                             reinterpret_cast<long long*>(gstep.data_ptr<int64_t>()),
+                             reinterpret_cast<unsigned long long*>(seq.data_ptr<int64_t>()),
+                             reinterpret_cast<unsigned long long*>(gran.data_ptr<int64_t>()), err.data_ptr<int>(),
+                             ticks, hn, next_steps, xn, xtn, ts_ptr(ts, 64 * 8 * 16 + 2 * 64), cur_stream()),
+            "mlp_persist");
+}
+
 void init_mlp(py::module& m) {
+  m.def("mlp_persist", &mlp_persist, py::arg("xs"), py::arg("xts"), py::arg("rec"), py::arg("B"),
+        py::arg("nsteps"), py::arg("params"), py::arg("lr"), py::arg("metrics"), py::arg("gstep"), py::arg("seq"),
+        py::arg("gran"), py::arg("err"), py::arg("timeout_s"), py::arg("act"), py::arg("naive"),
+        py::arg("host") = py::none(), py::arg("host_offset") = 0, py::arg("next_steps") = 0,
+        py::arg("xs_next") = py::none(), py::arg("xts_next") = py::none(), py::arg("ts") = py::none());
+  m.def("mlp_persist_xt_bytes", &dtfk_mlp_persist_xt_bytes);
+  m.def("mlp_persist_gran_count", &dtfk_mlp_persist_gran_count);
+  m.def("mlp_persist_max_batch", &dtfk_mlp_persist_max_batch);
+  m.def("mlp_persist_stage_rec", &dtfk_mlp_persist_stage_rec);
   m.def("mlp_ksplit", &dtfk_mlp_ksplit);
   m.def("mlp_l1_fwd", &mlp_l1_fwd, py::arg("x"), py::arg("x_offset"), py::arg("x_kind"),
         py::arg("B"), py::arg("W1T"), py::arg("z2p"), py::arg("ts") = py::none());

@@ -178,6 +178,7 @@ class FusedMLPTrainer:
                     import warnings
 
                     warnings.warn(f"IPC all-reduce unavailable ({e}); using RCCL")
+        self.shadows_stale = False   # set by PersistentMLPRunner (it updates only the fp32 master)
         self.set_params(init_params(seed))
 
     # ---------------------------------------------------------------- IPC one-shot all-reduce
@@ -209,6 +210,7 @@ class FusedMLPTrainer:
 
     def refresh_shadows(self):
         self.C.mlp_apply_flat(self.params, None, self.lr, 0.0, self.W1T, self.W2T, self.W2N)
+        self.shadows_stale = False
 
     def get_params(self) -> torch.Tensor:
         return self.params.detach().cpu()
@@ -238,6 +240,8 @@ class FusedMLPTrainer:
         (kind 0 uint8 pixels, 1 fp32, 2 bf16); labels: uint8 class ids.
         """
         C, B = self.C, self.B
+        if self.shadows_stale:
+            self.refresh_shadows()
         if self.merged_head:   # A1+A2 in one launch (last-arriver handoff per row block)
             C.mlp_fwd_head(x, x_off, x_kind, B, self.W1T, self.z2p, labels, labels_off, self.W2T, self.W2N,
                            self.params, self.dz2T, self.partials, 1.0 / B, self.act, self.naive, self.counters,
@@ -415,3 +419,88 @@ class MLPStepRunner:
                 self.parity = par ^ 1
                 self.loaded = nxt
             self.cursor += g
+
+
+class PersistentMLPRunner:
+    """Drives the persistent weight-stationary kernel (csrc/kernels/mlp_persist.hip)
+    over a pinned-host epoch: ONE launch per chunk of `g` steps.
+
+    Inside each launch 7 workgroups run the chunk's SGD steps with the weights
+    resident on-chip, while 57 copier workgroups pull the NEXT chunk from
+    pinned host memory over PCIe into the other device stage (row-major
+    records + a feature-major copy for the weight gradient).  No second stream,
+    no cross-queue events, no graph capture (one launch per 50 steps).
+
+    Single GPU (world_size 1), batch <= 112; the multi-rank path stays on
+    `MLPStepRunner` (IPC / RCCL gradient exchange between steps).
+    """
+
+    def __init__(self, trainer: FusedMLPTrainer, epoch, steps_per_launch: int = 50,
+                 timeout_s: float = 5.0):
+        C = trainer.C
+        if trainer.world_size != 1:
+            raise ValueError("PersistentMLPRunner is the single-GPU engine")
+        if trainer.B > C.mlp_persist_max_batch():
+            raise ValueError(f"PersistentMLPRunner needs batch <= {C.mlp_persist_max_batch()}")
+        if epoch.batch_size != trainer.B:
+            raise ValueError("epoch batch size != trainer batch size")
+        self.t = trainer
+        self.epoch = epoch
+        self.g = int(min(steps_per_launch, epoch.num_batches))
+        self.timeout_s = float(timeout_s)
+        dev = trainer.device
+        rec = C.mlp_persist_stage_rec(trainer.B)   # device stage record (k-step-pair interleaved rows)
+        xtb = C.mlp_persist_xt_bytes()
+        self.xs = [torch.zeros(self.g * rec, dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.xts = [torch.zeros(self.g * xtb, dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.gran = torch.zeros(C.mlp_persist_gran_count(), dtype=torch.int64, device=dev)
+        self.seq = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.err = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.cursor = 0
+        self.parity = 0
+        self.loaded = None      # (b0, g) staged in xs[parity]
+        self.use_graph = False  # MLPStepRunner interface
+        self.prefetch = "in-kernel"
+
+    def _chunks(self, cursor: int, steps: int) -> List[Tuple[int, int]]:
+        out, left = [], steps
+        nb = self.epoch.num_batches
+        while left > 0:
+            b0 = cursor % nb
+            g = min(self.g, left, nb - b0)
+            out.append((b0, g))
+            cursor += g
+            left -= g
+        return out
+
+    def _launch(self, par: int, nsteps: int, nxt: Tuple[int, int], dst_par: int):
+        t, ep = self.t, self.epoch
+        t.C.mlp_persist(self.xs[par], self.xts[par], ep.rec, t.B, nsteps, t.params, t.lr, t.metrics, t.gstep,
+                        self.seq, self.gran, self.err, self.timeout_s, t.act, int(t.naive),
+                        host=ep.host, host_offset=nxt[0] * ep.rec, next_steps=nxt[1],
+                        xs_next=self.xs[dst_par], xts_next=self.xts[dst_par])
+
+    def prepare(self, steps: int):
+        """Nothing to capture (kept for the MLPStepRunner interface)."""
+
+    def error(self) -> int:
+        return int(self.err.item())
+
+    def run(self, steps: int, events: Optional[list] = None):
+        main = torch.cuda.current_stream()
+        ch = self._chunks(self.cursor, steps)
+        after = self._chunks(self.cursor + steps, self.g)[0]   # speculative next chunk
+        for k, (b0, g) in enumerate(ch):
+            nxt = ch[k + 1] if k + 1 < len(ch) else after
+            par = self.parity
+            if self.loaded != (b0, g):   # cold start / plan change: copy-only launch
+                self._launch(par, 0, (b0, g), par)
+            self._launch(par, g, nxt, par ^ 1)
+            if events is not None:
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record(main)
+                events.append((ev, g))
+            self.parity = par ^ 1
+            self.loaded = nxt
+            self.cursor += g
+        self.t.shadows_stale = True

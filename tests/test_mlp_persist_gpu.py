@@ -1,0 +1,118 @@
+"""Persistent weight-stationary MLP kernel (csrc/kernels/mlp_persist.hip) vs the
+plain PyTorch fp32 reference of example.py's step (models/mlp.reference_step)."""
+import numpy as np
+import pytest
+import torch
+
+from distributed_tensorflow_example_amd.data.mnist import PinnedEpoch, synthetic_mnist
+from distributed_tensorflow_example_amd.models import mlp
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref_run(p0, imgs, labels, B, batches, lr, act="sigmoid"):
+    """fp32 SGD over the given batch indices; returns params and per-step losses."""
+    p = p0.clone()
+    losses, accs = [], []
+    for b in batches:
+        x = torch.from_numpy(imgs[b * B:(b + 1) * B]).float() / 255.0
+        y = torch.from_numpy(labels[b * B:(b + 1) * B])
+        loss, acc = mlp.reference_step(p, x, y, lr, act)
+        losses.append(loss.item())
+        accs.append(acc.item())
+    return p, np.array(losses), np.array(accs)
+
+
+@pytest.mark.parametrize("B", [100, 37, 112])
+@pytest.mark.parametrize("act", ["sigmoid", "relu"])
+def test_persist_one_step_gradient(native, B, act):
+    imgs, labels = synthetic_mnist(B, seed=11)
+    dev = torch.device("cuda")
+    tr = mlp.FusedMLPTrainer(batch_size=B, lr=1.0, act=act, device=dev)
+    p0 = tr.get_params().clone()
+    ep = PinnedEpoch(imgs, labels, B)
+    run = mlp.PersistentMLPRunner(tr, ep, steps_per_launch=1)
+    run.run(1)
+    torch.cuda.synchronize()
+    assert run.error() == 0
+    assert tr.global_step == 1
+    _, _, g = mlp.reference_loss_and_grad(p0, torch.from_numpy(imgs).float() / 255.0,
+                                          torch.from_numpy(labels), act)
+    loss, acc, _ = mlp.reference_loss_and_grad(p0, torch.from_numpy(imgs).float() / 255.0,
+                                               torch.from_numpy(labels), act)
+    g_k = p0 - tr.get_params()
+    for name, (off, shape) in mlp.PARAM_SPECS.items():
+        n = int(np.prod(shape))
+        a, b = g_k[off:off + n], g[off:off + n]
+        rel = ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+        assert rel < (5e-3 if act == "sigmoid" else 1e-2), (name, rel)
+    m = tr.read_metrics(0, 1)[0]
+    assert abs(m[0] - loss.item()) < 2e-3 * max(1.0, abs(loss.item())), (m, loss)
+    assert abs(m[1] - acc.item()) < 1e-6
+
+
+def test_persist_chunks_wrap_and_match_reference(native):
+    B, nb = 100, 6
+    imgs, labels = synthetic_mnist(B * nb, seed=12)
+    dev = torch.device("cuda")
+    lr = 0.05
+    tr = mlp.FusedMLPTrainer(batch_size=B, lr=lr, device=dev)
+    p0 = tr.get_params().clone()
+    ep = PinnedEpoch(imgs, labels, B)
+    run = mlp.PersistentMLPRunner(tr, ep, steps_per_launch=4)
+    run.run(7)     # chunks (0,4) (4,2) (0,1): copy-only cold start, in-kernel copies, epoch wrap
+    run.run(4)     # (1,3) (4,1): plan change -> copy-only launch again
+    torch.cuda.synchronize()
+    assert run.error() == 0
+    assert tr.global_step == 11
+    batches = [0, 1, 2, 3, 4, 5, 0, 1, 2, 3, 4]
+    p_ref, losses, accs = _ref_run(p0, imgs, labels, B, batches, lr)
+    d_k = tr.get_params() - p0
+    d_r = p_ref - p0
+    rel = ((d_k - d_r).norm() / d_r.norm()).item()
+    assert rel < 5e-3, rel
+    m = tr.read_metrics(0, 11)
+    assert np.allclose(m[:, 0], losses, rtol=2e-3, atol=2e-3), (m[:, 0], losses)
+    assert np.allclose(m[:, 1], accs, atol=1e-6)
+
+
+def test_persist_deterministic_and_hands_over_to_step_path(native):
+    B = 100
+    imgs, labels = synthetic_mnist(B * 4, seed=13)
+    dev = torch.device("cuda")
+    outs = []
+    for _ in range(2):
+        tr = mlp.FusedMLPTrainer(batch_size=B, lr=0.01, device=dev)
+        ep = PinnedEpoch(imgs, labels, B)
+        run = mlp.PersistentMLPRunner(tr, ep, steps_per_launch=3)
+        run.run(5)
+        torch.cuda.synchronize()
+        outs.append(tr.get_params())
+    assert torch.equal(outs[0], outs[1])       # bit-identical replays
+    # the 3-kernel path continues from the persistent state (bf16 shadows refreshed)
+    p5 = tr.get_params().clone()
+    x = torch.from_numpy(imgs[:B]).to(dev)
+    y = torch.from_numpy(labels[:B]).to(dev)
+    tr.step_tensors(x, y)
+    torch.cuda.synchronize()
+    assert tr.global_step == 6
+    _, _, g = mlp.reference_loss_and_grad(p5, torch.from_numpy(imgs[:B]).float() / 255.0,
+                                          torch.from_numpy(labels[:B]))
+    g_k = (p5 - tr.get_params()) / 0.01
+    assert ((g_k - g).norm() / g.norm()).item() < 3e-2
+
+
+def test_persist_long_run_learns(native):
+    """1000 steps at the reference's lr on synthetic MNIST: loss goes down."""
+    B = 100
+    imgs, labels = synthetic_mnist(B * 50, seed=14)
+    dev = torch.device("cuda")
+    tr = mlp.FusedMLPTrainer(batch_size=B, lr=0.05, device=dev)
+    ep = PinnedEpoch(imgs, labels, B)
+    run = mlp.PersistentMLPRunner(tr, ep, steps_per_launch=50)
+    run.run(1000)
+    torch.cuda.synchronize()
+    assert run.error() == 0
+    m = tr.read_metrics(0, 1000)
+    assert np.isfinite(m).all()
+    assert m[-50:, 0].mean() < 0.7 * m[:50, 0].mean(), (m[:50, 0].mean(), m[-50:, 0].mean())

@@ -55,7 +55,7 @@ def main(argv=None):
     ap.add_argument("--act", choices=["sigmoid", "relu"], default="sigmoid")
     ap.add_argument("--train-examples", type=int, default=55000)
     ap.add_argument("--prefetch", choices=["serial", "side"], default="serial")
-    ap.add_argument("--engine", choices=["auto", "persistent", "launches"], default="launches",
+    ap.add_argument("--engine", choices=["auto", "persistent", "launches"], default="auto",
                     help="1 GPU: persistent weight-stationary kernel, one launch per chunk (default), or "
                          "3 fused launches per step replayed from hipGraphs")
     ap.add_argument("--allreduce", choices=["auto", "ipc-fused", "ipc-apply", "rccl"], default="auto",
@@ -180,7 +180,7 @@ def main(argv=None):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "fp16" if persistent else "bf16",
             "data": ("synthetic MNIST-shaped uint8 resident in pinned host memory, streamed per chunk over PCIe "
                      + ("by copier workgroups inside the persistent launch" if persistent else
                         "by hipMemcpyAsync inside the chunk's hipGraph") + "; random-init weights"),
@@ -197,6 +197,9 @@ def main(argv=None):
                 "hipgraph_steps": 0 if (a.eager or persistent) else a.steps_per_graph,
                 "input_prefetch": "in-kernel copier workgroups" if persistent else a.prefetch,
                 "activation": a.act,
+                "precision": ("fp16 MFMA operands (pixels exact as 1024+u, 10-bit mantissa >= bf16's 7), fp32 "
+                              "accumulate, fp32 master weights" if persistent else
+                              "bf16 MFMA operands, fp32 accumulate, fp32 master weights"),
             },
             "final_loss": round(float(m[0]), 5),
             "final_batch_acc": round(float(m[1]), 4),

@@ -51,6 +51,7 @@ typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
 typedef __attribute__((ext_vector_type(2))) _Float16 f16x2;
 typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
 typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned gu32;
 
 constexpr int DIN = 784;
 constexpr int NF = 800;        // features padded to 25 k-steps of 32 (xT rows)
@@ -66,8 +67,10 @@ constexpr int OFF_W2 = 78400, OFF_B1 = 79400, OFF_B2 = 79500;
 constexpr int THREADS = 512;
 constexpr int XCD_STRIDE = 8;  // compute workgroup j runs as blockIdx 8j
 constexpr int GRID = 64;       // 7 compute + 57 copier workgroups
-constexpr int GRAN_PER_SLOT = NWG * NBT * NCLS * 16;   // u64 granules per parity slot
-constexpr int GRAN_TOTAL = 2 * GRAN_PER_SLOT + 16;     // + per-launch placement header
+constexpr int PAYLOAD = 48 * 4;                        // floats per (producer, tile): lanes g<3 x float4
+// exchange buffer (u64 units): [16 header granules][2][64] u32 flags = 64 u64 [2][7][7][PAYLOAD] floats
+constexpr int XCH_HDR = 16, XCH_FLAGS = 64, XCH_DENSE = NWG * NBT * PAYLOAD;   // dense: u64 units per parity
+constexpr int GRAN_TOTAL = XCH_HDR + XCH_FLAGS + 2 * XCH_DENSE;
 
 struct Args {
   const uint8_t* xs;        // this chunk: stage records of `rec` bytes (B x 832 permuted pixels, B labels)
@@ -82,7 +85,9 @@ struct Args {
   int act, naive;
   long long* gstep;
   unsigned long long* seq;  // exchange sequence number (monotonic across launches)
-  unsigned long long* gran; // [2][7][7][10][16] granules
+  unsigned long long* gran; // placement header granules [16]
+  float* dense;             // [2][7 producers][7 tiles][PAYLOAD] partial logits
+  unsigned* flags;          // [2][64] (producer, tile) flags = step tag
   int* err;
   long long timeout;        // s_memrealtime ticks (100 MHz)
   // copier: next chunk
@@ -225,6 +230,7 @@ __device__ void compute(const Args& a, const int j, uint8_t* smem) {
   float* rdb2 = reinterpret_cast<float*>(smem + L_RDB2);
   float* rmet = reinterpret_cast<float*>(smem + L_RMET);
   int* abort_flag = reinterpret_cast<int*>(smem + L_FLAG);
+  int* small_done = abort_flag + 1;   // steps whose small-parameter update is complete
 
   // ---- load state
   for (int k = tid; k < 3 * 16 * BPT; k += THREADS) dz2T[k] = (_Float16)0.f;   // also a2T, dz3T
@@ -240,6 +246,7 @@ __device__ void compute(const Args& a, const int j, uint8_t* smem) {
     b2s[c] = c < NCLS ? a.params[OFF_B2 + c] : 0.f;
   } else if (tid == 288) {
     *abort_flag = 0;
+    *small_done = 0;
   }
   const int hid = 16 * j + r;       // this lane's hidden unit in the W1^T-fragment / dW1 layouts
   const bool hv = hid < HID;
@@ -304,7 +311,7 @@ __device__ void compute(const Args& a, const int j, uint8_t* smem) {
   __shared__ int same_xcd;
   if (tid == 0) {
     const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20) & 15u;
-    gu64* hdr = (gu64*)(a.gran) + 2 * GRAN_PER_SLOT;
+    gu64* hdr = (gu64*)(a.gran);
     const unsigned tag0 = (unsigned)(seq0 + 1ull);
     __hip_atomic_store(hdr + j, ((unsigned long long)tag0 << 32) | xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int same = 1;
@@ -333,7 +340,6 @@ __device__ void compute(const Args& a, const int j, uint8_t* smem) {
   for (int st = 0; st < a.nsteps; ++st) {
     const unsigned long long sq = seq0 + (unsigned long long)st + 1ull;
     const unsigned tag = (unsigned)sq;
-    gu64* slot = (gu64*)(a.gran) + (size_t)(sq & 1ull) * GRAN_PER_SLOT;
     if (w == 0) { TSP(0); }
 
     // ---------------- forward + head (wave w < 7: batch tile w)
@@ -345,6 +351,11 @@ __device__ void compute(const Args& a, const int j, uint8_t* smem) {
       f32x4 z = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < NKS; ++s) z = mfma_h(wfrag[s * 64 + lane], frag_px(xw(s, 0), xw(s, 1)), z);
+      // b1/W2/b2 of step st-1's update (wave 7) before they are read here
+      while (__hip_atomic_load(small_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < st)
+        __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+      if (w == 0) { TSP(13); }
       // lane (batch r, g): z^T[hidden 16j+4g+i][batch b]
       float a2[4];
 #pragma unroll
@@ -362,18 +373,24 @@ __device__ void compute(const Args& a, const int j, uint8_t* smem) {
                               w2s[(4 * g + 3) * 16 + r]);
       const f32x4 pl = mfma_h(Aw2, frag4(a2[0], a2[1], a2[2], a2[3]), f32x4{0.f, 0.f, 0.f, 0.f});
       if (w == 0) { TSP(1); }
-      // publish: granule (class c, batch r) of (slot, j, w)
-      gu64* mine = slot + ((size_t)(j * NBT + w) * NCLS) * 16;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int c = 4 * g + i;
-        const unsigned long long gv = ((unsigned long long)tag << 32) | (unsigned long long)__float_as_uint(pl[i]);
-        if (c < NCLS) {
-          if (l2_local)   // plain 8-byte store: the line stays in the shared L2
-            __hip_atomic_store(mine + c * 16 + r, gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          else            // write-through (sc1): visible to other XCDs' sc1 loads
-            __hip_atomic_store(mine + c * 16 + r, gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+      const int par = (int)(sq & 1ull);
+      // publish this tile's partial logits: dense fp32 (lane g <= 2: classes
+      // 4g..4g+3 of batch row r), drained, then ONE flag word per (workgroup, wave)
+      float* mine = a.dense + ((size_t)(par * NWG + j) * NBT + w) * PAYLOAD;
+      const f32x4 plv = pl;
+      if (g < 3) {
+        if (l2_local)   // plain stores: the lines stay in the shared L2
+          *reinterpret_cast<f32x4*>(mine + 4 * lane) = plv;
+        else            // write-through (sc1): visible to other XCDs' sc1 loads
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, plv),
+                                                 __builtin_amdgcn_make_buffer_rsrc(mine, 0, PAYLOAD * 4, 0x00020000),
+                                                 16 * lane, 0, 16);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // payload acknowledged before the flag
+      gu32* flg = (gu32*)(a.flags) + par * 64;
+      if (lane == 0) {
+        if (l2_local) __hip_atomic_store(flg + j * NBT + w, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        else __hip_atomic_store(flg + j * NBT + w, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       // while the exchange is in flight: x rows -> LDS image (read transposed by the
       // weight-gradient MFMAs), a2 -> LDS (dW2)
@@ -384,31 +401,16 @@ __device__ void compute(const Args& a, const int j, uint8_t* smem) {
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) a2T[(4 * g + i) * BPT + b] = (_Float16)a2[i];
-      // gather the other blocks' partials (sc1 sweep until every tag matches)
-      float part[NWG][4];
       if (w == 0) { TSP(6); }
+      // lanes 0..6 poll the 7 producers' flags of this tile (relaxed sc1 loads)
       {
         const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
         int sweeps = 0;
         for (;;) {
           ++sweeps;
           bool ok = true;
-#pragma unroll
-          for (int jj = 0; jj < NWG; ++jj) {
-            const gu64* src = slot + ((size_t)(jj * NBT + w) * NCLS) * 16;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const int c = 4 * g + i;
-              if (c < NCLS && jj != j) {
-                const unsigned long long v = __hip_atomic_load(src + c * 16 + r, __ATOMIC_RELAXED,
-                                                               __HIP_MEMORY_SCOPE_AGENT);
-                part[jj][i] = __uint_as_float((unsigned)v);
-                ok = ok && (unsigned)(v >> 32) == tag;
-              } else {
-                part[jj][i] = pl[i];
-              }
-            }
-          }
+          if (lane < NWG && lane != j)
+            ok = __hip_atomic_load(flg + lane * NBT + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == tag;
           if (__all(ok)) {
             if (a.ts != nullptr && w == 0 && lane == 0 && st < 64) a.ts[((long long)st * 8 + j) * 16 + 7] = sweeps;
             break;
@@ -421,7 +423,21 @@ __device__ void compute(const Args& a, const int j, uint8_t* smem) {
             }
             break;
           }
-          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      // the other producers' payloads: one sc1 (L1-bypassing) 16-byte load each
+      float part[NWG][4];
+#pragma unroll
+      for (int jj = 0; jj < NWG; ++jj) {
+        if (jj == j || g >= 3) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) part[jj][i] = pl[i];
+        } else {
+          const float* src = a.dense + ((size_t)(par * NWG + jj) * NBT + w) * PAYLOAD;
+          const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(
+              __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, PAYLOAD * 4, 0x00020000), 16 * lane, 0, 16);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) part[jj][i] = __uint_as_float(v[i]);
         }
       }
       if (w == 0) { TSP(2); }
@@ -436,6 +452,7 @@ __device__ void compute(const Args& a, const int j, uint8_t* smem) {
         lg[i] = v;
         if (4 * g + i < NCLS) m = fmaxf(m, v);
       }
+      if (w == 0) { TSP(11); }
       m = fmaxf(m, xor16(m));
       m = fmaxf(m, xor32(m));
       float ssum = 0.f, zy = 0.f, am = 1e9f;
@@ -484,43 +501,10 @@ __device__ void compute(const Args& a, const int j, uint8_t* smem) {
         if (r == 0) rdb1[w * 16 + 4 * g + i] = s;
       }
     }
+    if (w == 0) { TSP(12); }
     lds_barrier();     // S_b: x image, dz2^T, a2^T, dz3^T and the per-tile sums are complete
     if (w == 0) { TSP(3); }
     if (*abort_flag) { aborted = true; break; }
-
-    // ---------------- small parameters (wave 7): dW2 on MFMA, db1, db2, metrics
-    if (w == 7) {
-      TSP(8);
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        acc = mfma_h(*reinterpret_cast<const f16x8*>(dz3T + r * BPT + 32 * q + 8 * g),
-                     *reinterpret_cast<const f16x8*>(a2T + r * BPT + 32 * q + 8 * g), acc);
-      // lane (hidden r, g): dW2[16j + r][class 4g + i]
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (hv && 4 * g + i < NCLS) w2s[r * 16 + 4 * g + i] -= lrB * acc[i];
-      if (lane < 16) {
-        float s = 0.f;
-#pragma unroll
-        for (int w2 = 0; w2 < NBT; ++w2) s += rdb1[w2 * 16 + lane];
-        if (16 * j + lane < HID) b1s[lane] -= lrB * s;
-      } else if (lane < 16 + NCLS) {
-        const int c = lane - 16;
-        float s = 0.f;
-#pragma unroll
-        for (int w2 = 0; w2 < NBT; ++w2) s += rdb2[w2 * 16 + c];
-        b2s[c] -= lrB * s;
-      } else if (lane == 63 && j == 0) {
-        float ls = 0.f, cr = 0.f;
-#pragma unroll
-        for (int w2 = 0; w2 < NBT; ++w2) { ls += rmet[2 * w2]; cr += rmet[2 * w2 + 1]; }
-        const int sl = (int)((gstep0 + st) % a.ring);
-        a.metrics[2 * sl] = ls / (float)B;
-        a.metrics[2 * sl + 1] = cr / (float)B;
-      }
-      TSP(9);
-    }
 
     // ---------------- dW1 block (all waves): x^T . dz2, SGD in the accumulator layout
     {
@@ -571,8 +555,46 @@ __device__ void compute(const Args& a, const int j, uint8_t* smem) {
     publish_w1();
     lds_barrier();     // S_a: next step's W1 fragments + column sums visible
     if (w == 0) { TSP(5); }
+    // ---------------- small parameters (wave 7, overlapping the next step's forward):
+    // dW2 on MFMA, db1, db2, metrics of step st; the next head waits on small_done
+    if (w == 7) {
+      TSP(8);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        acc = mfma_h(*reinterpret_cast<const f16x8*>(dz3T + r * BPT + 32 * q + 8 * g),
+                     *reinterpret_cast<const f16x8*>(a2T + r * BPT + 32 * q + 8 * g), acc);
+      // lane (hidden r, g): dW2[16j + r][class 4g + i]
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (hv && 4 * g + i < NCLS) w2s[r * 16 + 4 * g + i] -= lrB * acc[i];
+      if (lane < 16) {
+        float s = 0.f;
+#pragma unroll
+        for (int w2 = 0; w2 < NBT; ++w2) s += rdb1[w2 * 16 + lane];
+        if (16 * j + lane < HID) b1s[lane] -= lrB * s;
+      } else if (lane < 16 + NCLS) {
+        const int c = lane - 16;
+        float s = 0.f;
+#pragma unroll
+        for (int w2 = 0; w2 < NBT; ++w2) s += rdb2[w2 * 16 + c];
+        b2s[c] -= lrB * s;
+      } else if (lane == 63 && j == 0) {
+        float ls = 0.f, cr = 0.f;
+#pragma unroll
+        for (int w2 = 0; w2 < NBT; ++w2) { ls += rmet[2 * w2]; cr += rmet[2 * w2 + 1]; }
+        const int sl = (int)((gstep0 + st) % a.ring);
+        a.metrics[2 * sl] = ls / (float)B;
+        a.metrics[2 * sl + 1] = cr / (float)B;
+      }
+      TSP(9);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+      if (lane == 0) __hip_atomic_store(small_done, st + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+
   }
   if (aborted) return;
+  __syncthreads();   // wave 7's last small-parameter update
 
   // ---- write back the block (fp32 master), global step and exchange sequence
 #pragma unroll
@@ -648,6 +670,8 @@ hipError_t dtfk_mlp_persist(const void* xs, const void* xts, long long rec, long
   a.gstep = gstep;
   a.seq = seq;
   a.gran = gran;
+  a.flags = reinterpret_cast<unsigned*>(gran + dtfk::mlpp::XCH_HDR);
+  a.dense = reinterpret_cast<float*>(gran + dtfk::mlpp::XCH_HDR + dtfk::mlpp::XCH_FLAGS);
   a.err = err;
   a.timeout = timeout;
   a.host_next = static_cast<const uint8_t*>(host_next);

@@ -78,6 +78,13 @@ def main():
     out["wave7_small_params_us"] = round(float(np.median(w7a)), 3)
     out["wave7_wgrad_us"] = round(float(np.median(w7b)), 3)
     out["wave7_publish_to_S_a_exit_us"] = round(float(np.median(w7c)), 3)
+    def seg(a_, b_):
+        d = (raw[1:, :, b_] - raw[1:, :, a_]).astype(np.float64) * 0.01
+        return round(float(np.median(d)), 3)
+    out["fwd_plus_wait_small_us"] = seg(0, 13)
+    out["payload_return_us"] = seg(2, 11)
+    out["softmax_to_S_b_us"] = seg(11, 12)
+    out["S_b_wait_us"] = seg(12, 3)
     steps = st[2:, 0, 0] - st[1:-1, 0, 0]
     out["step_us_median"] = round(float(np.median(steps)), 3)
     out["phase_us_median_p90"] = ph

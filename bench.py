@@ -90,17 +90,17 @@ def main(argv=None):
     epoch = PinnedEpoch(imgs, labels, a.batch)
     gd = torch.bfloat16 if a.grad_dtype == "bf16" else torch.float32
 
-    persistent = a.engine == "persistent" or (a.engine == "auto" and w.world_size == 1 and a.batch <= 112)
+    can_persist = a.batch <= 112 and a.engine != "launches"
 
-    def setup(allreduce):
+    def setup(mode):
+        """mode: 'persistent' (one launch per chunk, in-kernel N-GPU exchange) or the
+        3-launch path's gradient exchange ('ipc-fused' / 'ipc-apply' / 'rccl')."""
         trainer = FusedMLPTrainer(batch_size=a.batch, lr=a.lr, act=a.act, world=w, grad_dtype=gd,
-                                  device=dev, allreduce=allreduce)
-        if persistent:
+                                  device=dev, allreduce="rccl" if mode == "persistent" else mode)
+        if mode == "persistent":
             runner = PersistentMLPRunner(trainer, epoch, steps_per_launch=a.steps_per_graph)
             runner.run(a.warmup)
             torch.cuda.synchronize()
-            if runner.error():
-                raise SystemExit("persistent kernel exchange timed out during warmup")
             return trainer, runner
         runner = MLPStepRunner(trainer, epoch, steps_per_graph=a.steps_per_graph,
                                use_graph=not a.eager, prefetch=a.prefetch)
@@ -116,25 +116,33 @@ def main(argv=None):
         torch.cuda.synchronize()
         return trainer, runner
 
-    def consistent(trainer) -> bool:
-        """No IPC timeout anywhere and bit-identical replicas on every rank."""
+    def consistent(trainer, runner) -> bool:
+        """No exchange timeout anywhere and bit-identical replicas on every rank."""
+        err = runner.error() if isinstance(runner, PersistentMLPRunner) else trainer.ipc_error()
         if w.world_size == 1:
-            return True
-        bad = w.host_all_reduce(float(trainer.ipc_error()), "max")
+            return err == 0
+        bad = w.host_all_reduce(float(err), "max")
         c = float(trainer.params.double().sum().item())
         spread = w.host_all_reduce(c, "max") - w.host_all_reduce(c, "min")
         return bad == 0.0 and spread == 0.0
 
-    # fallback chain: in-kernel IPC exchange -> separate IPC reduce+apply -> RCCL
-    chain = {"auto": ["ipc-fused", "ipc-apply", "rccl"], "ipc-fused": ["ipc-fused"],
-             "ipc-apply": ["ipc-apply"], "rccl": ["rccl"]}[a.allreduce] if w.world_size > 1 else ["rccl"]
+    # fallback chain: persistent (in-kernel exchange) -> 3 launches with the IPC
+    # exchange inside the wgrad kernel -> separate IPC reduce+apply -> RCCL
+    if w.world_size == 1:
+        chain = ["persistent"] if can_persist else ["rccl"]
+    else:
+        chain = {"auto": ["ipc-fused", "ipc-apply", "rccl"], "ipc-fused": ["ipc-fused"],
+                 "ipc-apply": ["ipc-apply"], "rccl": ["rccl"]}[a.allreduce]
+        if can_persist and a.allreduce == "auto":
+            chain = ["persistent"] + chain
     for i, mode in enumerate(chain):
         trainer, runner = setup(mode)
-        if consistent(trainer):
+        if consistent(trainer, runner):
             break
         if i + 1 == len(chain):
-            raise SystemExit(f"replicas diverged after warmup ({trainer.allreduce})")
-        print(f"bench: {trainer.allreduce} failed validation; trying {chain[i + 1]}", file=sys.stderr, flush=True)
+            raise SystemExit(f"replicas diverged / exchange timed out after warmup ({mode})")
+        print(f"bench: {mode} failed validation; trying {chain[i + 1]}", file=sys.stderr, flush=True)
+    persistent = isinstance(runner, PersistentMLPRunner)
     step0 = trainer.global_step
 
     events = []
@@ -159,9 +167,7 @@ def main(argv=None):
     p50 = statistics.median(per_step_ms) if per_step_ms else float("nan")
     p50 = w.host_all_reduce(p50, "max")
 
-    if persistent and runner.error():
-        raise SystemExit("persistent kernel exchange timed out during the timed run; result discarded")
-    if w.world_size > 1 and not consistent(trainer):
+    if not consistent(trainer, runner):
         raise SystemExit("replicas diverged / IPC timeout during the timed run; result discarded")
     steps_done = trainer.global_step - step0
     m = trainer.read_metrics(trainer.global_step - 1, trainer.global_step)[0]
@@ -191,7 +197,8 @@ def main(argv=None):
                 "seq_len": None,
                 "parallelism": f"dp{n}",
                 "optimizer": f"sgd lr={a.lr}",
-                "grad_allreduce": f"{a.grad_dtype} {trainer.allreduce}" if n > 1 else "none",
+                "grad_allreduce": ("none" if n == 1 else "bf16 in-kernel one-shot over IPC/xGMI" if persistent
+                                   else f"{a.grad_dtype} {trainer.allreduce}"),
                 "engine": "persistent" if persistent else "launches",
                 "steps_per_launch": a.steps_per_graph if persistent else 1,
                 "hipgraph_steps": 0 if (a.eager or persistent) else a.steps_per_graph,

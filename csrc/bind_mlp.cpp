@@ -33,11 +33,12 @@ int dtfk_mlp_persist_gran_count();
 int dtfk_mlp_persist_xt_bytes();
 int dtfk_mlp_persist_max_batch();
 int dtfk_mlp_persist_stage_rec(int B);
+int dtfk_mlp_persist_ipc_bytes();
 hipError_t dtfk_mlp_persist(const void* xs, const void* xts, long long rec, long long rec_h, int B, int nsteps, float* params,
                             const float* lr, float* metrics, int ring, int act, int naive, long long* gstep,
                             unsigned long long* seq, unsigned long long* gran, int* err, long long timeout,
                             const void* host_next, int next_steps, void* xs_next, void* xts_next,
-                            long long* ts, hipStream_t stream);
+                            long long* ts, void* const* peer_base, int W, int rank, hipStream_t stream);
 hipError_t dtfk_mlp_fwd_head(const void* x, int x_kind, int B, const void* W1T, float* z2p, const void* labels,
                              const void* W2T, const void* W2N, const float* params, void* dz2T, int BP,
                              float* partials, float inv_batch, int act, int naive_loss, int* counters,
@@ -253,7 +254,9 @@ void mlp_persist(at::Tensor xs, at::Tensor xts, int64_t rec, int B, int nsteps, 
                  at::Tensor metrics, at::Tensor gstep, at::Tensor seq, at::Tensor gran, at::Tensor err,
                  double timeout_s, int act, int naive, c10::optional<at::Tensor> host, int64_t host_off,
                  int next_steps, c10::optional<at::Tensor> xs_next, c10::optional<at::Tensor> xts_next,
-                 c10::optional<at::Tensor> ts) {
+                 c10::optional<at::Tensor> ts, int64_t ipc_table, int ipc_W, int ipc_rank) {
+  if (ipc_W > 1 && (ipc_table == 0 || ipc_rank < 0 || ipc_rank >= ipc_W))
+    throw std::runtime_error("mlp_persist: N-GPU exchange needs the IPC peer table");
   if (B <= 0 || B > dtfk_mlp_persist_max_batch()) throw std::runtime_error("mlp_persist: B out of range");
   if (rec < (int64_t)B * 785 || rec % 16 != 0) throw std::runtime_error("mlp_persist: bad record size");
   const int64_t rec_h = rec;                        // host record (pinned epoch)
@@ -300,7 +303,9 @@ void mlp_persist(at::Tensor xs, at::Tensor xts, int64_t rec, int B, int nsteps, 
                              reinterpret_cast<long long*>(gstep.data_ptr<int64_t>()),
                              reinterpret_cast<unsigned long long*>(seq.data_ptr<int64_t>()),
                              reinterpret_cast<unsigned long long*>(gran.data_ptr<int64_t>()), err.data_ptr<int>(),
-                             ticks, hn, next_steps, xn, xtn, ts_ptr(ts, 64 * 8 * 16 + 2 * 64), cur_stream()),
+                             ticks, hn, next_steps, xn, xtn, ts_ptr(ts, 64 * 8 * 16 + 2 * 64),
+                             reinterpret_cast<void* const*>(ipc_table), ipc_W > 1 ? ipc_W : 1, ipc_W > 1 ? ipc_rank : 0,
+                             cur_stream()),
             "mlp_persist");
 }
 
@@ -309,7 +314,9 @@ void init_mlp(py::module& m) {
         py::arg("nsteps"), py::arg("params"), py::arg("lr"), py::arg("metrics"), py::arg("gstep"), py::arg("seq"),
         py::arg("gran"), py::arg("err"), py::arg("timeout_s"), py::arg("act"), py::arg("naive"),
         py::arg("host") = py::none(), py::arg("host_offset") = 0, py::arg("next_steps") = 0,
-        py::arg("xs_next") = py::none(), py::arg("xts_next") = py::none(), py::arg("ts") = py::none());
+        py::arg("xs_next") = py::none(), py::arg("xts_next") = py::none(), py::arg("ts") = py::none(),
+        py::arg("ipc_table") = 0, py::arg("ipc_W") = 1, py::arg("ipc_rank") = 0);
+  m.def("mlp_persist_ipc_bytes", &dtfk_mlp_persist_ipc_bytes);
   m.def("mlp_persist_xt_bytes", &dtfk_mlp_persist_xt_bytes);
   m.def("mlp_persist_gran_count", &dtfk_mlp_persist_gran_count);
   m.def("mlp_persist_max_batch", &dtfk_mlp_persist_max_batch);

@@ -96,7 +96,20 @@ struct Args {
   uint8_t* xs_next;
   uint8_t* xts_next;
   long long* ts;            // optional phase stamps (s_memrealtime), see TSP
+  // N GPUs: IPC-mapped uncached exchange buffers of every rank (W = 1: none)
+  void* const* peer_base;
+  int W, rank;
 };
+
+// IPC exchange buffer of one rank: [flags: block j at byte 64j][2 parities][7 blocks][slot]
+// slot: dW1 block as [tile 49][g 4][r 16] x 4 bf16, then small grads
+// (dW2 [g][r] x 4 bf16 = 512 B, db1/db2 bf16 at +512 (lanes 0..25))
+constexpr int IPC_FLAGS = 4096;
+constexpr int IPC_SMALL = 49 * 4 * 16 * 8;
+constexpr int IPC_SLOT = IPC_SMALL + 576;
+constexpr int IPC_BYTES = IPC_FLAGS + 2 * NWG * IPC_SLOT;
+__device__ __forceinline__ int par_of(int st) { return st & 1; }
+__device__ __forceinline__ float bfround(float x) { return bf2f(f2bf(x)); }
 
 // debug stamps: compute workgroup j, wave w, lane 0 -> ts[(step*8 + j)*16 + phase]
 __device__ __forceinline__ void lds_barrier() {   // orders LDS only: no vmcnt(0) on in-flight loads
@@ -212,7 +225,7 @@ constexpr int LDS_BYTES = L_FLAG + 16;
 // work, so it takes the 25th k-step.
 __device__ __forceinline__ int kstep_of(int w, int u) { return u < 3 ? w + 8 * u : (w == 7 ? NKS - 1 : -1); }
 
-template <int ACT>   // 0 sigmoid, 1 relu
+template <int ACT, bool MULTI>   // ACT 0 sigmoid, 1 relu; MULTI: N-GPU gradient exchange
 __device__ void compute(const Args& a, const int j, uint8_t* smem) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
@@ -506,7 +519,63 @@ __device__ void compute(const Args& a, const int j, uint8_t* smem) {
     if (w == 0) { TSP(3); }
     if (*abort_flag) { aborted = true; break; }
 
-    // ---------------- dW1 block (all waves): x^T . dz2, SGD in the accumulator layout
+    // ---------------- small-parameter gradients (wave 7): dW2 on MFMA, db1, db2, metrics.
+    // 1 GPU: applied after S_a, overlapping the next forward (the next head waits on
+    // small_done).  N GPUs: computed here, exchanged with the block's gradient.
+    auto small_grads = [&](float (&gw2)[4], float& gb) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        acc = mfma_h(*reinterpret_cast<const f16x8*>(dz3T + r * BPT + 32 * q + 8 * g),
+                     *reinterpret_cast<const f16x8*>(a2T + r * BPT + 32 * q + 8 * g), acc);
+      // lane (hidden r, g): dW2[16j + r][class 4g + i] (x B: dz3 is unscaled)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) gw2[i] = (hv && 4 * g + i < NCLS) ? acc[i] : 0.f;
+      gb = 0.f;
+      if (lane < 16) {
+#pragma unroll
+        for (int w2 = 0; w2 < NBT; ++w2) gb += rdb1[w2 * 16 + lane];
+        if (16 * j + lane >= HID) gb = 0.f;
+      } else if (lane < 16 + NCLS) {
+#pragma unroll
+        for (int w2 = 0; w2 < NBT; ++w2) gb += rdb2[w2 * 16 + lane - 16];
+      } else if (lane == 63 && j == 0) {
+        float ls = 0.f, cr = 0.f;
+#pragma unroll
+        for (int w2 = 0; w2 < NBT; ++w2) { ls += rmet[2 * w2]; cr += rmet[2 * w2 + 1]; }
+        const int sl = (int)((gstep0 + st) % a.ring);
+        a.metrics[2 * sl] = ls / (float)B;
+        a.metrics[2 * sl + 1] = cr / (float)B;
+      }
+    };
+    auto small_apply = [&](const float (&gw2)[4], float gb, float scale) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (hv && 4 * g + i < NCLS) w2s[r * 16 + 4 * g + i] -= scale * gw2[i];
+      if (lane < 16) b1s[lane] -= scale * gb;
+      else if (lane < 16 + NCLS) b2s[lane - 16] -= scale * gb;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+      if (lane == 0) __hip_atomic_store(small_done, st + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    constexpr bool multi = MULTI;
+    float sgw2[4] = {0.f, 0.f, 0.f, 0.f};
+    float sgb = 0.f;
+    char* own_slot = nullptr;
+    if constexpr (MULTI) {
+      own_slot = static_cast<char*>(a.peer_base[a.rank]) + IPC_FLAGS + (size_t)(par_of(st) * NWG + j) * IPC_SLOT;
+      if (w == 7) {   // small gradients (mean over the local batch) -> own slot, bf16
+        small_grads(sgw2, sgb);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sgw2[i] = bfround(sgw2[i] * (1.f / (float)B));
+        sgb = bfround(sgb * (1.f / (float)B));
+        *reinterpret_cast<uint2*>(own_slot + IPC_SMALL + (g * 16 + r) * 8) =
+            make_uint2(pack2bf(sgw2[0], sgw2[1]), pack2bf(sgw2[2], sgw2[3]));
+        if (lane < 16 + NCLS) *reinterpret_cast<uint16_t*>(own_slot + IPC_SMALL + 512 + 2 * lane) = f2bf(sgb);
+      }
+    }
+
+    // ---------------- dW1 block (all waves): x^T . dz2, in the accumulator layout
+    uint2 gq[NU][2];   // N GPUs: this rank's bf16 gradient of the wave's tiles
     {
       f16x8 bq[4];
       float cs2 = 0.f;
@@ -542,56 +611,122 @@ __device__ void compute(const Args& a, const int j, uint8_t* smem) {
                 acc = mfma_h(frag_px((uint32_t)v.x, (uint32_t)v.y), bq[q], acc);
               }
             }
+            if constexpr (!MULTI) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const int f = 16 * t + 4 * g + i;
-              if (f < DIN && hv) Wm[u][h][i] -= lrX * (acc[i] - corr);
+              for (int i = 0; i < 4; ++i) {
+                const int f = 16 * t + 4 * g + i;
+                if (f < DIN && hv) Wm[u][h][i] -= lrX * (acc[i] - corr);
+              }
+            } else {
+              float gg[4];
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                const int f = 16 * t + 4 * g + i;
+                gg[i] = (f < DIN && hv) ? (acc[i] - corr) * (1.f / (255.f * (float)B)) : 0.f;
+              }
+              gq[u][h] = make_uint2(pack2bf(gg[0], gg[1]), pack2bf(gg[2], gg[3]));
+              if (t < DIN / 16) *reinterpret_cast<uint2*>(own_slot + ((t * 4 + g) * 16 + r) * 8) = gq[u][h];
             }
           }
         }
+      }
+    }
+    if constexpr (MULTI) {
+      // ---- one-shot exchange of block j with the same workgroup on every peer GPU
+      // (IPC-mapped uncached buffers: completion == visibility; rank-order sums keep
+      // the replicas bit-identical)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave: its slot stores landed
+      lds_barrier();
+      if (tid == 0)
+        __hip_atomic_store(reinterpret_cast<unsigned*>(static_cast<char*>(a.peer_base[a.rank]) + 64 * j), tag,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (w == 0) {
+        const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+        for (;;) {
+          bool ok = true;
+          if (lane < a.W && lane != a.rank) {
+            const unsigned v = __hip_atomic_load(
+                reinterpret_cast<const unsigned*>(static_cast<const char*>(a.peer_base[lane]) + 64 * j),
+                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            ok = (int)(v - tag) >= 0;
+          }
+          if (__all(ok)) break;
+          if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > a.timeout ||
+              __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+            if (lane == 0) {
+              atomicOr(a.err, 2);
+              *abort_flag = 1;
+            }
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      lds_barrier();
+      if (*abort_flag) { aborted = true; break; }
+      const float lrW = lr / (float)a.W;
+      const size_t soff = IPC_FLAGS + (size_t)(par_of(st) * NWG + j) * IPC_SLOT;
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const int s = kstep_of(w, u);
+        if (s >= 0) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int t = 2 * s + h;
+            if (t < DIN / 16) {
+              float sum[4] = {0.f, 0.f, 0.f, 0.f};
+              for (int rr = 0; rr < a.W; ++rr) {
+                uint2 v = gq[u][h];
+                if (rr != a.rank) {
+                  const unsigned long long x = __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(
+                      static_cast<const char*>(a.peer_base[rr]) + soff + ((t * 4 + g) * 16 + r) * 8));
+                  v = make_uint2((unsigned)x, (unsigned)(x >> 32));
+                }
+                sum[0] += bf2f(v.x & 0xffff); sum[1] += bf2f(v.x >> 16);
+                sum[2] += bf2f(v.y & 0xffff); sum[3] += bf2f(v.y >> 16);
+              }
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                const int f = 16 * t + 4 * g + i;
+                if (f < DIN && hv) Wm[u][h][i] -= lrW * sum[i];
+              }
+            }
+          }
+        }
+      }
+      if (w == 7) {
+        float sw2[4] = {0.f, 0.f, 0.f, 0.f};
+        float sb = 0.f;
+        for (int rr = 0; rr < a.W; ++rr) {
+          float v2[4] = {sgw2[0], sgw2[1], sgw2[2], sgw2[3]};
+          float vb = sgb;
+          if (rr != a.rank) {
+            const char* ps = static_cast<const char*>(a.peer_base[rr]) + soff + IPC_SMALL;
+            const unsigned long long x =
+                __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(ps + (g * 16 + r) * 8));
+            v2[0] = bf2f((unsigned)x & 0xffff); v2[1] = bf2f(((unsigned)x) >> 16);
+            v2[2] = bf2f((unsigned)(x >> 32) & 0xffff); v2[3] = bf2f((unsigned)(x >> 48));
+            vb = lane < 16 + NCLS ? bf2f(__builtin_nontemporal_load(reinterpret_cast<const uint16_t*>(ps + 512) + lane))
+                                  : 0.f;
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) sw2[i] += v2[i];
+          sb += vb;
+        }
+        small_apply(sw2, sb, lrW);
       }
     }
     if (w == 0 || w == 7) { TSP(w == 0 ? 4 : 10); }
     publish_w1();
     lds_barrier();     // S_a: next step's W1 fragments + column sums visible
     if (w == 0) { TSP(5); }
-    // ---------------- small parameters (wave 7, overlapping the next step's forward):
-    // dW2 on MFMA, db1, db2, metrics of step st; the next head waits on small_done
-    if (w == 7) {
+    if (!MULTI && w == 7) {   // 1 GPU: small parameters while the next forward runs
       TSP(8);
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        acc = mfma_h(*reinterpret_cast<const f16x8*>(dz3T + r * BPT + 32 * q + 8 * g),
-                     *reinterpret_cast<const f16x8*>(a2T + r * BPT + 32 * q + 8 * g), acc);
-      // lane (hidden r, g): dW2[16j + r][class 4g + i]
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (hv && 4 * g + i < NCLS) w2s[r * 16 + 4 * g + i] -= lrB * acc[i];
-      if (lane < 16) {
-        float s = 0.f;
-#pragma unroll
-        for (int w2 = 0; w2 < NBT; ++w2) s += rdb1[w2 * 16 + lane];
-        if (16 * j + lane < HID) b1s[lane] -= lrB * s;
-      } else if (lane < 16 + NCLS) {
-        const int c = lane - 16;
-        float s = 0.f;
-#pragma unroll
-        for (int w2 = 0; w2 < NBT; ++w2) s += rdb2[w2 * 16 + c];
-        b2s[c] -= lrB * s;
-      } else if (lane == 63 && j == 0) {
-        float ls = 0.f, cr = 0.f;
-#pragma unroll
-        for (int w2 = 0; w2 < NBT; ++w2) { ls += rmet[2 * w2]; cr += rmet[2 * w2 + 1]; }
-        const int sl = (int)((gstep0 + st) % a.ring);
-        a.metrics[2 * sl] = ls / (float)B;
-        a.metrics[2 * sl + 1] = cr / (float)B;
-      }
+      float gw2[4], gb;
+      small_grads(gw2, gb);
+      small_apply(gw2, gb, lrB);
       TSP(9);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-      if (lane == 0) __hip_atomic_store(small_done, st + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-
   }
   if (aborted) return;
   __syncthreads();   // wave 7's last small-parameter update
@@ -622,12 +757,12 @@ __device__ void compute(const Args& a, const int j, uint8_t* smem) {
   }
 }
 
-template <int ACT>
+template <int ACT, bool MULTI>
 __global__ __launch_bounds__(THREADS, 1) void mlp_persist(Args a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int b = blockIdx.x;
   if (b % XCD_STRIDE == 0 && b / XCD_STRIDE < NWG) {
-    if (a.nsteps > 0) compute<ACT>(a, b / XCD_STRIDE, smem);
+    if (a.nsteps > 0) compute<ACT, MULTI>(a, b / XCD_STRIDE, smem);
     return;
   }
   // copier id among the non-compute blocks
@@ -646,15 +781,20 @@ int dtfk_mlp_persist_gran_count() { return dtfk::mlpp::GRAN_TOTAL; }
 int dtfk_mlp_persist_xt_bytes() { return dtfk::mlpp::NF * dtfk::mlpp::BPT; }
 int dtfk_mlp_persist_max_batch() { return 16 * dtfk::mlpp::NBT; }
 
+int dtfk_mlp_persist_ipc_bytes() { return dtfk::mlpp::IPC_BYTES; }
+
 int dtfk_mlp_persist_stage_rec(int B) { return ((B * (dtfk::mlpp::XR + 1) + 15) / 16) * 16; }
 
 hipError_t dtfk_mlp_persist(const void* xs, const void* xts, long long rec, long long rec_h, int B, int nsteps, float* params,
                             const float* lr, float* metrics, int ring, int act, int naive, long long* gstep,
                             unsigned long long* seq, unsigned long long* gran, int* err, long long timeout,
                             const void* host_next, int next_steps, void* xs_next, void* xts_next,
-                            long long* ts, hipStream_t stream) {
+                            long long* ts, void* const* peer_base, int W, int rank, hipStream_t stream) {
   Args a;
   a.ts = ts;
+  a.peer_base = peer_base;
+  a.W = W;
+  a.rank = rank;
   a.xs = static_cast<const uint8_t*>(xs);
   a.xts = static_cast<const uint8_t*>(xts);
   a.rec = rec;
@@ -680,21 +820,25 @@ hipError_t dtfk_mlp_persist(const void* xs, const void* xts, long long rec, long
   a.xts_next = static_cast<uint8_t*>(xts_next);
   constexpr size_t lds = dtfk::mlpp::LDS_BYTES;
   static bool attr_set = false;
+  using namespace dtfk::mlpp;
+  const void* kerns[4] = {reinterpret_cast<const void*>(mlp_persist<0, false>),
+                          reinterpret_cast<const void*>(mlp_persist<1, false>),
+                          reinterpret_cast<const void*>(mlp_persist<0, true>),
+                          reinterpret_cast<const void*>(mlp_persist<1, true>)};
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(dtfk::mlpp::mlp_persist<0>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e == hipSuccess)
-      e = hipFuncSetAttribute(reinterpret_cast<const void*>(dtfk::mlpp::mlp_persist<1>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
+    for (const void* k : kerns) {
+      const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+    }
     attr_set = true;
   }
-  if (act == 0)
-    hipLaunchKernelGGL(dtfk::mlpp::mlp_persist<0>, dim3(dtfk::mlpp::GRID), dim3(dtfk::mlpp::THREADS), lds,
-                       stream, a);
-  else
-    hipLaunchKernelGGL(dtfk::mlpp::mlp_persist<1>, dim3(dtfk::mlpp::GRID), dim3(dtfk::mlpp::THREADS), lds,
-                       stream, a);
+  const int which = (act == 0 ? 0 : 1) + (W > 1 ? 2 : 0);
+  switch (which) {
+    case 0: hipLaunchKernelGGL((mlp_persist<0, false>), dim3(GRID), dim3(THREADS), lds, stream, a); break;
+    case 1: hipLaunchKernelGGL((mlp_persist<1, false>), dim3(GRID), dim3(THREADS), lds, stream, a); break;
+    case 2: hipLaunchKernelGGL((mlp_persist<0, true>), dim3(GRID), dim3(THREADS), lds, stream, a); break;
+    default: hipLaunchKernelGGL((mlp_persist<1, true>), dim3(GRID), dim3(THREADS), lds, stream, a); break;
+  }
   return hipGetLastError();
 }
 

@@ -431,15 +431,15 @@ class PersistentMLPRunner:
     records + a feature-major copy for the weight gradient).  No second stream,
     no cross-queue events, no graph capture (one launch per 50 steps).
 
-    Single GPU (world_size 1), batch <= 112; the multi-rank path stays on
-    `MLPStepRunner` (IPC / RCCL gradient exchange between steps).
+    N GPUs of one node (world_size > 1): every compute workgroup exchanges its
+    block's bf16 gradient with the same workgroup on every peer through
+    IPC-mapped uncached buffers inside the same launch (flag per block and step,
+    rank-order sums -> bit-identical replicas).  Batch <= 112 per GPU.
     """
 
     def __init__(self, trainer: FusedMLPTrainer, epoch, steps_per_launch: int = 50,
                  timeout_s: float = 5.0):
         C = trainer.C
-        if trainer.world_size != 1:
-            raise ValueError("PersistentMLPRunner is the single-GPU engine")
         if trainer.B > C.mlp_persist_max_batch():
             raise ValueError(f"PersistentMLPRunner needs batch <= {C.mlp_persist_max_batch()}")
         if epoch.batch_size != trainer.B:
@@ -461,6 +461,17 @@ class PersistentMLPRunner:
         self.loaded = None      # (b0, g) staged in xs[parity]
         self.use_graph = False  # MLPStepRunner interface
         self.prefetch = "in-kernel"
+        self.ipc = None
+        self.W, self.rank = 1, 0
+        w = trainer.world
+        if w is not None and w.world_size > 1:
+            if int(os.environ.get("LOCAL_WORLD_SIZE", w.world_size)) != w.world_size:
+                raise RuntimeError("the persistent N-GPU exchange needs all ranks on one node")
+            buf = C.IpcPeerBuffers(C.mlp_persist_ipc_bytes(), w.world_size, w.rank)
+            handles = w.all_gather_object(bytes(buf.handle()))
+            buf.open(list(handles))
+            self.ipc = buf
+            self.W, self.rank = w.world_size, w.rank
 
     def _chunks(self, cursor: int, steps: int) -> List[Tuple[int, int]]:
         out, left = [], steps
@@ -478,7 +489,9 @@ class PersistentMLPRunner:
         t.C.mlp_persist(self.xs[par], self.xts[par], ep.rec, t.B, nsteps, t.params, t.lr, t.metrics, t.gstep,
                         self.seq, self.gran, self.err, self.timeout_s, t.act, int(t.naive),
                         host=ep.host, host_offset=nxt[0] * ep.rec, next_steps=nxt[1],
-                        xs_next=self.xs[dst_par], xts_next=self.xts[dst_par])
+                        xs_next=self.xs[dst_par], xts_next=self.xts[dst_par],
+                        ipc_table=self.ipc.table_ptr() if self.ipc is not None else 0, ipc_W=self.W,
+                        ipc_rank=self.rank)
 
     def prepare(self, steps: int):
         """Nothing to capture (kept for the MLPStepRunner interface)."""

@@ -116,3 +116,29 @@ def test_persist_long_run_learns(native):
     m = tr.read_metrics(0, 1000)
     assert np.isfinite(m).all()
     assert m[-50:, 0].mean() < 0.7 * m[:50, 0].mean(), (m[:50, 0].mean(), m[-50:, 0].mean())
+
+
+@pytest.mark.parametrize("nproc", [2, 3])
+def test_persist_multi_rank_same_gpu(native, nproc):
+    """N ranks sharing cuda:0: in-kernel IPC exchange, bit-identical replicas, sync-SGD math."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", f"--nproc-per-node={nproc}", "--master-addr=127.0.0.1",
+           f"--master-port={port}", os.path.join(repo, "scripts", "persist_selftest.py"), "--same-gpu",
+           "--steps=10", "--per-launch=4"]
+    env = dict(os.environ, PYTHONPATH=repo, OMP_NUM_THREADS="2")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=100, env=env)
+    out = r.stdout + r.stderr
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert r.returncode == 0 and line, out[-3000:]
+    res = json.loads(line[-1])
+    assert res["persist_selftest"] == "pass", res

@@ -49,7 +49,10 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=550)
     ap.add_argument("--batch", type=int, default=100, help="per-GPU batch (reference: 100)")
     ap.add_argument("--lr", type=float, default=0.0005)
-    ap.add_argument("--steps-per-graph", type=int, default=50)
+    ap.add_argument("--steps-per-graph", type=int, default=50, help="3-launch path: steps per captured hipGraph")
+    ap.add_argument("--steps-per-launch", type=int, default=550,
+                    help="persistent engine: steps per launch (<= one epoch of batches; the next chunk is copied "
+                         "from pinned host memory inside the launch)")
     ap.add_argument("--eager", action="store_true", help="no hipGraph capture")
     ap.add_argument("--grad-dtype", choices=["bf16", "fp32"], default="bf16")
     ap.add_argument("--act", choices=["sigmoid", "relu"], default="sigmoid")
@@ -100,7 +103,7 @@ def main(argv=None):
         trainer = FusedMLPTrainer(batch_size=a.batch, lr=a.lr, act=a.act, world=w, grad_dtype=gd,
                                   device=dev, allreduce="rccl" if mode == "persistent" else mode)
         if mode == "persistent":
-            runner = PersistentMLPRunner(trainer, epoch, steps_per_launch=a.steps_per_graph)
+            runner = PersistentMLPRunner(trainer, epoch, steps_per_launch=a.steps_per_launch)
             runner.run(a.warmup)
             torch.cuda.synchronize()
             return trainer, runner
@@ -157,7 +160,7 @@ def main(argv=None):
     if len(picked) > 1:
         for mode, tr_, rn_ in picked:
             rn_.prepare(a.tune_steps)
-            rn_.run(a.steps_per_graph)   # settle
+            rn_.run(min(50, a.tune_steps))   # settle
             w.barrier()
             torch.cuda.synchronize()
             t_ = time.perf_counter()
@@ -232,7 +235,7 @@ def main(argv=None):
                 "grad_allreduce": ("none" if n == 1 else "bf16 in-kernel one-shot over IPC/xGMI" if persistent
                                    else f"{a.grad_dtype} {trainer.allreduce}"),
                 "engine": "persistent" if persistent else "launches",
-                "steps_per_launch": a.steps_per_graph if persistent else 1,
+                "steps_per_launch": runner.g if persistent else 1,
                 "hipgraph_steps": 0 if (a.eager or persistent) else a.steps_per_graph,
                 "input_prefetch": "in-kernel copier workgroups" if persistent else a.prefetch,
                 "activation": a.act,

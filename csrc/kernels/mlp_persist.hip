@@ -219,7 +219,7 @@ constexpr int L_RDB1 = L_B2 + 64;                // [8][16] fp32
 constexpr int L_RDB2 = L_RDB1 + 512;             // [8][16] fp32
 constexpr int L_RMET = L_RDB2 + 512;             // [8][2] fp32
 constexpr int L_FLAG = L_RMET + 64;              // abort flag
-constexpr int LDS_BYTES = L_FLAG + 16;
+constexpr int LDS_BYTES = L_FLAG + 48;
 
 // k-step owned by wave w in slot u (-1: none).  Wave 7 does no forward/head
 // work, so it takes the 25th k-step.
@@ -244,6 +244,7 @@ __device__ void compute(const Args& a, const int j, uint8_t* smem) {
   float* rmet = reinterpret_cast<float*>(smem + L_RMET);
   int* abort_flag = reinterpret_cast<int*>(smem + L_FLAG);
   int* small_done = abort_flag + 1;   // steps whose small-parameter update is complete
+  int* wready = abort_flag + 4;       // [8]: steps whose W1 fragments wave v has published
 
   // ---- load state
   for (int k = tid; k < 3 * 16 * BPT; k += THREADS) dz2T[k] = (_Float16)0.f;   // also a2T, dz3T
@@ -260,6 +261,7 @@ __device__ void compute(const Args& a, const int j, uint8_t* smem) {
   } else if (tid == 288) {
     *abort_flag = 0;
     *small_done = 0;
+    for (int v = 0; v < 8; ++v) wready[v] = 0;
   }
   const int hid = 16 * j + r;       // this lane's hidden unit in the W1^T-fragment / dW1 layouts
   const bool hv = hid < HID;
@@ -362,8 +364,18 @@ __device__ void compute(const Args& a, const int j, uint8_t* smem) {
       const int y0 = a.xs[(long long)st * a.rec + (long long)B * XR + xrow];
       const int y = y0 < NCLS ? y0 : 0;
       f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      // owner v's fragments as soon as v has published step st's W1 (no block barrier)
 #pragma unroll
-      for (int s = 0; s < NKS; ++s) z = mfma_h(wfrag[s * 64 + lane], frag_px(xw(s, 0), xw(s, 1)), z);
+      for (int v = 0; v < 8; ++v) {
+        while (__hip_atomic_load(wready + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < st)
+          __builtin_amdgcn_s_sleep(0);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+          const int s = (u < 3) ? v + 8 * u : (v == 7 ? NKS - 1 : -1);
+          if (s >= 0) z = mfma_h(wfrag[s * 64 + lane], frag_px(xw(s, 0), xw(s, 1)), z);
+        }
+      }
       // b1/W2/b2 of step st-1's update (wave 7) before they are read here
       while (__hip_atomic_load(small_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < st)
         __builtin_amdgcn_s_sleep(1);
@@ -718,7 +730,8 @@ __device__ void compute(const Args& a, const int j, uint8_t* smem) {
     }
     if (w == 0 || w == 7) { TSP(w == 0 ? 4 : 10); }
     publish_w1();
-    lds_barrier();     // S_a: next step's W1 fragments + column sums visible
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    if (lane == 0) __hip_atomic_store(wready + w, st + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (w == 0) { TSP(5); }
     if (!MULTI && w == 7) {   // 1 GPU: small parameters while the next forward runs
       TSP(8);

@@ -20,7 +20,7 @@ from distributed_tensorflow_example_amd.models import mlp  # noqa: E402
 
 
 def main():
-    B, G = 100, 50
+    B, G = 100, 50  # per-launch stamps cover 50 steps
     dev = torch.device("cuda", 0)
     imgs, labels = synthetic_mnist(55000, seed=1)
     ep = PinnedEpoch(imgs, labels, B)

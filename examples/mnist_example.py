@@ -52,6 +52,8 @@ flags.DEFINE_integer("frequency", 100, "print every N batches")
 flags.DEFINE_string("logs_path", "./logs/mnist", "summary root; task dir {job}_{task} appended")
 flags.DEFINE_string("activation", "sigmoid", "sigmoid | relu")
 flags.DEFINE_boolean("fused", False, "run the fused MFMA train step (GPU only)")
+flags.DEFINE_boolean("persistent", False, "with --fused: the persistent weight-stationary engine (one kernel "
+                     "launch per epoch, batch <= 112, input streamed from pinned host memory in-kernel)")
 flags.DEFINE_string("result_json", "", "write final metrics + params checksum here (tests)")
 flags.DEFINE_string("checkpoint_dir", "", "Supervisor logdir: restore on start, checkpoint while training")
 flags.DEFINE_integer("save_model_secs", 600, "checkpoint period (chief, seconds)")
@@ -165,6 +167,8 @@ def run_fused_worker(server, mnist):
     world = server.world
     tr = mlp.FusedMLPTrainer(batch_size=FLAGS.batch_size, lr=FLAGS.learning_rate, act=FLAGS.activation,
                              world=world)
+    if FLAGS.persistent:
+        return run_persistent_worker(server, mnist, tr)
     begin = time.time()
     batch_count = mnist.train.num_examples // FLAGS.batch_size
     steps = 0
@@ -187,6 +191,49 @@ def run_fused_worker(server, mnist):
     p = mlp.unflatten(tr.get_params().cpu())
     z = mlp.reference_forward(tr.get_params().cpu(), torch.from_numpy(mnist.test.images), FLAGS.activation)
     acc = float((z.argmax(1).numpy() == mnist.test.labels.argmax(1)).mean())
+    params = [p[k].numpy() for k in ("weights/Variable", "weights/Variable_1", "biases/Variable",
+                                     "biases/Variable_1")]
+    server.signal_done()
+    return acc, loss, time.time() - begin, params, tr.global_step
+
+
+def run_persistent_worker(server, mnist, tr):
+    """One persistent launch per epoch (csrc/kernels/mlp_persist.hip); the
+    per-epoch shuffle of next_batch is re-packed into the pinned epoch and the
+    step lines come from the device metrics ring."""
+    import torch
+
+    from distributed_tensorflow_example_amd.data.mnist import PinnedEpoch
+    from distributed_tensorflow_example_amd.models import mlp
+
+    train = mnist.train
+    epoch = PinnedEpoch(train.images_u8, train.labels_u8, FLAGS.batch_size)
+    run = mlp.PersistentMLPRunner(tr, epoch, steps_per_launch=epoch.num_batches)
+    batch_count = epoch.num_batches
+    begin = time.time()
+    steps, loss = 0, float("nan")
+    for ep in range(FLAGS.training_epochs):
+        if ep:
+            epoch.shuffle(seed=1000 * FLAGS.task_index + ep)
+            run.loaded = None            # the staged chunk came from the previous packing
+        n = batch_count if not FLAGS.max_steps else min(batch_count, FLAGS.max_steps - steps)
+        if n <= 0:
+            break
+        g0 = tr.global_step
+        run.run(n)
+        torch.cuda.synchronize()
+        if run.error():
+            raise RuntimeError("persistent kernel exchange timed out")
+        m = tr.read_metrics(g0, g0 + n)
+        for i in range(n):
+            if (steps + i + 1) % FLAGS.frequency == 0 or i + 1 == batch_count:
+                print(step_line(steps + i + 1, g0 + i + 1, ep + 1, i + 1, batch_count, float(m[i][0]), 0.0),
+                      flush=True)
+        loss = float(m[-1][0])
+        steps += n
+    z = mlp.reference_forward(tr.get_params().cpu(), torch.from_numpy(mnist.test.images), FLAGS.activation)
+    acc = float((z.argmax(1).numpy() == mnist.test.labels.argmax(1)).mean())
+    p = mlp.unflatten(tr.get_params().cpu())
     params = [p[k].numpy() for k in ("weights/Variable", "weights/Variable_1", "biases/Variable",
                                      "biases/Variable_1")]
     server.signal_done()

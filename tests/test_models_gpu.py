@@ -68,13 +68,13 @@ def test_sharded_embedding_bag_dim128_on_gpu(native):
 
 
 def test_mnist_example_single_worker_gpu(tmp_path):
-    for fused in ("--nofused", "--fused"):
+    for fused in ("--nofused", "--fused", "--fused --persistent"):
         p = _free_port()
         env = dict(os.environ, PYTHONPATH=REPO)
         cmd = [sys.executable, os.path.join(REPO, "examples", "mnist_example.py"), "--job_name=worker",
                "--task_index=0", "--ps_hosts=", f"--worker_hosts=127.0.0.1:{p}", "--max_steps=300",
                "--train_size=10000", "--learning_rate=0.1", f"--logs_path={tmp_path}/logs",
-               f"--result_json={tmp_path}/r.json", fused]
+               f"--result_json={tmp_path}/r.json"] + fused.split()
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
         assert r.returncode == 0, r.stdout + r.stderr
         res = json.load(open(tmp_path / "r.json"))

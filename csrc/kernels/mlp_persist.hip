@@ -364,11 +364,13 @@ __device__ void compute(const Args& a, const int j, uint8_t* smem) {
       const int y0 = a.xs[(long long)st * a.rec + (long long)B * XR + xrow];
       const int y = y0 < NCLS ? y0 : 0;
       f32x4 z = {0.f, 0.f, 0.f, 0.f};
-      // owner v's fragments as soon as v has published step st's W1 (no block barrier)
+      // owner v's fragments as soon as v has published step st's W1 (no block barrier);
+      // waves 3 and 7 share SIMD 3 (13 of the 49 weight-gradient tiles) and finish last
 #pragma unroll
-      for (int v = 0; v < 8; ++v) {
+      for (int vi = 0; vi < 8; ++vi) {
+        const int v = vi < 3 ? vi : (vi < 6 ? vi + 1 : (vi == 6 ? 3 : 7));
         while (__hip_atomic_load(wready + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < st)
-          __builtin_amdgcn_s_sleep(0);
+          __builtin_amdgcn_s_sleep(1);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 #pragma unroll
         for (int u = 0; u < NU; ++u) {

@@ -17,6 +17,11 @@ hipError_t dtfk_ln_bwd(const void* dy, const void* s, const float* mean, const f
                        void* ds, void* dxb, float* part_g, float* part_b, float* part_bias, int grid, int N, int H,
                        float p, unsigned long long seed, hipStream_t st);
 hipError_t dtfk_colsum_partials(const float* part, float* out, int P, int H, hipStream_t st);
+hipError_t dtfk_colsum_partials_multi(const float* const* parts, float* const* outs, int nbuf, int P, int H,
+                                      int accumulate, hipStream_t st);
+hipError_t dtfk_colsum_bf16(const void* x, float* part, float* out, int N, int H, int P, int accumulate,
+                            hipStream_t st);
+hipError_t dtfk_slab_sum(const float* slabs, float* out, int S, long long n, int accumulate, hipStream_t st);
 hipError_t dtfk_bias_gelu_fwd(const void* x, const float* bias, void* y, long long n, int H, hipStream_t st);
 hipError_t dtfk_bias_gelu_bwd(const void* dy, const void* x, const float* bias, void* dx, float* part, int N, int H,
                               int row_slices, hipStream_t st);
@@ -82,7 +87,8 @@ void ln_fwd_f32in(at::Tensor x, at::Tensor gamma, at::Tensor beta, at::Tensor y,
 // returns nothing; dgamma/dbeta/dbias (fp32 [H]) written if given
 void ln_bwd(at::Tensor dy, at::Tensor s, at::Tensor mean, at::Tensor rstd, at::Tensor gamma, at::Tensor ds,
             c10::optional<at::Tensor> dxb, at::Tensor part, c10::optional<at::Tensor> dgamma,
-            c10::optional<at::Tensor> dbeta, c10::optional<at::Tensor> dbias, double p, int64_t seed) {
+            c10::optional<at::Tensor> dbeta, c10::optional<at::Tensor> dbias, double p, int64_t seed,
+            bool accumulate) {
   const int H = (int)dy.size(-1);
   req(dy, at::kBFloat16, "dy"); req(s, at::kBFloat16, "s"); req(ds, at::kBFloat16, "ds");
   req(part, at::kFloat, "part");
@@ -97,9 +103,42 @@ void ln_bwd(at::Tensor dy, at::Tensor s, at::Tensor mean, at::Tensor rstd, at::T
                  ds.data_ptr(), optp(dxb), dgamma.has_value() ? pg : nullptr, dbeta.has_value() ? pb : nullptr,
                  dbias.has_value() ? px : nullptr, grid, N, H, (float)p, (unsigned long long)seed, cs()),
      "ln_bwd");
-  if (dgamma.has_value()) ck(dtfk_colsum_partials(pg, dgamma->data_ptr<float>(), grid, H, cs()), "colsum");
-  if (dbeta.has_value()) ck(dtfk_colsum_partials(pb, dbeta->data_ptr<float>(), grid, H, cs()), "colsum");
-  if (dbias.has_value()) ck(dtfk_colsum_partials(px, dbias->data_ptr<float>(), grid, H, cs()), "colsum");
+  // dgamma / dbeta / dbias: one finishing launch (accumulate: += into sunk .grad)
+  const float* parts[3];
+  float* outs[3];
+  int nb = 0;
+  auto add = [&](const c10::optional<at::Tensor>& t, const float* pp) {
+    if (!t.has_value()) return;
+    req(*t, at::kFloat, "param grad");
+    if (t->numel() < H) throw std::runtime_error("ln_bwd: gradient output too small");
+    parts[nb] = pp;
+    outs[nb++] = t->data_ptr<float>();
+  };
+  add(dgamma, pg);
+  add(dbeta, pb);
+  add(dbias, px);
+  if (nb) ck(dtfk_colsum_partials_multi(parts, outs, nb, grid, H, accumulate ? 1 : 0, cs()), "colsum");
+}
+
+// bias gradient of a bf16 [N, H] matrix: out (+)= column sums (part: P*H floats)
+void colsum_bf16(at::Tensor x, at::Tensor part, at::Tensor out, bool accumulate) {
+  req(x, at::kBFloat16, "x"); req(part, at::kFloat, "part"); req(out, at::kFloat, "out");
+  const int H = (int)x.size(-1);
+  const int N = rows_of(x, H);
+  const int P = (int)(part.numel() / H);
+  if (P < 1 || out.numel() < H) throw std::runtime_error("colsum_bf16 shapes");
+  ck(dtfk_colsum_bf16(x.data_ptr(), part.data_ptr<float>(), out.data_ptr<float>(), N, H, P, accumulate ? 1 : 0, cs()),
+     "colsum_bf16");
+}
+
+// out (+)= sum over the leading dim of slabs [S, n] (fp32; 16-byte vector path when aligned)
+void slab_sum(at::Tensor slabs, at::Tensor out, bool accumulate) {
+  req(slabs, at::kFloat, "slabs"); req(out, at::kFloat, "out");
+  const int64_t n = out.numel();
+  if (n == 0 || slabs.numel() % n) throw std::runtime_error("slab_sum shapes");
+  if (!slabs.is_contiguous() || !out.is_contiguous()) throw std::runtime_error("slab_sum: contiguous tensors only");
+  const int S = (int)(slabs.numel() / n);
+  ck(dtfk_slab_sum(slabs.data_ptr<float>(), out.data_ptr<float>(), S, n, accumulate ? 1 : 0, cs()), "slab_sum");
 }
 
 void bias_gelu_fwd(at::Tensor x, at::Tensor bias, at::Tensor y) {
@@ -109,7 +148,8 @@ void bias_gelu_fwd(at::Tensor x, at::Tensor bias, at::Tensor y) {
   ck(dtfk_bias_gelu_fwd(x.data_ptr(), bias.data_ptr<float>(), y.data_ptr(), x.numel(), H, cs()), "bias_gelu_fwd");
 }
 
-void bias_gelu_bwd(at::Tensor dy, at::Tensor x, at::Tensor bias, at::Tensor dx, at::Tensor part, at::Tensor dbias) {
+void bias_gelu_bwd(at::Tensor dy, at::Tensor x, at::Tensor bias, at::Tensor dx, at::Tensor part, at::Tensor dbias,
+                   bool accumulate) {
   req(dy, at::kBFloat16, "dy"); req(x, at::kBFloat16, "x"); req(dx, at::kBFloat16, "dx");
   req(part, at::kFloat, "part"); req(dbias, at::kFloat, "dbias");
   const int H = (int)x.size(-1);
@@ -119,7 +159,9 @@ void bias_gelu_bwd(at::Tensor dy, at::Tensor x, at::Tensor bias, at::Tensor dx, 
   ck(dtfk_bias_gelu_bwd(dy.data_ptr(), x.data_ptr(), bias.data_ptr<float>(), dx.data_ptr(), part.data_ptr<float>(), N,
                         H, slices, cs()),
      "bias_gelu_bwd");
-  ck(dtfk_colsum_partials(part.data_ptr<float>(), dbias.data_ptr<float>(), slices, H, cs()), "colsum");
+  const float* pp[1] = {part.data_ptr<float>()};
+  float* po[1] = {dbias.data_ptr<float>()};
+  ck(dtfk_colsum_partials_multi(pp, po, 1, slices, H, accumulate ? 1 : 0, cs()), "colsum");
 }
 
 void softmax_fwd(at::Tensor S, c10::optional<at::Tensor> mask, at::Tensor P, c10::optional<at::Tensor> Pd,
@@ -199,9 +241,14 @@ void init_transformer(pybind11::module& m) {
   m.def("attn_bwd", &attn_bwd);
   m.def("bdrln_fwd", &bdrln_fwd);
   m.def("ln_fwd_f32in", &ln_fwd_f32in);
-  m.def("ln_bwd", &ln_bwd);
+  m.def("ln_bwd", &ln_bwd, py::arg("dy"), py::arg("s"), py::arg("mean"), py::arg("rstd"), py::arg("gamma"),
+        py::arg("ds"), py::arg("dxb"), py::arg("part"), py::arg("dgamma"), py::arg("dbeta"), py::arg("dbias"),
+        py::arg("p"), py::arg("seed"), py::arg("accumulate") = false);
+  m.def("colsum_bf16", &colsum_bf16, py::arg("x"), py::arg("part"), py::arg("out"), py::arg("accumulate") = false);
+  m.def("slab_sum", &slab_sum, py::arg("slabs"), py::arg("out"), py::arg("accumulate") = false);
   m.def("bias_gelu_fwd", &bias_gelu_fwd);
-  m.def("bias_gelu_bwd", &bias_gelu_bwd);
+  m.def("bias_gelu_bwd", &bias_gelu_bwd, py::arg("dy"), py::arg("x"), py::arg("bias"), py::arg("dx"), py::arg("part"),
+        py::arg("dbias"), py::arg("accumulate") = false);
   m.def("softmax_fwd", &softmax_fwd);
   m.def("softmax_bwd", &softmax_bwd);
   m.def("dropout_bf16", &dropout_bf16);

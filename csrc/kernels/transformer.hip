@@ -345,12 +345,19 @@ __global__ __launch_bounds__(128) void bias_gelu_bwd8(const uint16_t* __restrict
   *reinterpret_cast<float4*>(p + 4) = float4{acc[4], acc[5], acc[6], acc[7]};
 }
 
-// column sums of a [P, H] fp32 partial buffer -> out[H] (deterministic).
-// 1024 threads = 64 consecutive columns x 16 row groups (coalesced 256 B
-// rows), LDS tree over the groups; grid = ceil(H / 64).
-__global__ __launch_bounds__(1024) void colsum_partials(const float* __restrict__ part, float* __restrict__ out,
-                                                        int P, int H) {
+// column sums of up to 3 [P, H] fp32 partial buffers -> out_k[H] (deterministic;
+// blockIdx.y picks the buffer).  accumulate: out_k += sum (a gradient sunk into
+// the parameter's .grad) instead of out_k = sum.  1024 threads = 64 consecutive
+// columns x 16 row groups (coalesced 256 B rows), LDS tree over the groups;
+// grid = (ceil(H / 64), nbuf).
+struct ColsumArgs {
+  const float* part[3];
+  float* out[3];
+};
+__global__ __launch_bounds__(1024) void colsum_partials(ColsumArgs a, int P, int H, int accumulate) {
   __shared__ float red[16][64];
+  const float* __restrict__ part = a.part[blockIdx.y];
+  float* __restrict__ out = a.out[blockIdx.y];
   const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
   float s = 0.f;
@@ -362,8 +369,55 @@ __global__ __launch_bounds__(1024) void colsum_partials(const float* __restrict_
     float t = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) t += red[i][lane];
-    out[c] = t;
+    out[c] = accumulate ? out[c] + t : t;
   }
+}
+
+// per-slice column sums of a bf16 [N, H] matrix -> part[P][H] fp32 (first stage of
+// a bias gradient; colsum_partials finishes it).  grid = (ceil(H / 512), P), block
+// 256 = 64 lanes x 8 columns each (16-byte loads) x 4 row groups; slice p covers
+// rows [p*N/P, (p+1)*N/P).  H % 8 == 0.
+__global__ __launch_bounds__(256) void colsum_bf16_partials(const uint16_t* __restrict__ x, float* __restrict__ part,
+                                                            int N, int H) {
+  __shared__ float red[4][512];
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c0 = blockIdx.x * 512 + 8 * lane;
+  const int P = gridDim.y;
+  const int r0 = (int)((long long)N * blockIdx.y / P), r1 = (int)((long long)N * (blockIdx.y + 1) / P);
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c0 < H)
+    for (int r = r0 + g; r < r1; r += 4) {
+      const uint4 v = *reinterpret_cast<const uint4*>(x + (size_t)r * H + c0);
+      const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { s[2 * k] += bf2f(wv[k] & 0xffff); s[2 * k + 1] += bf2f(wv[k] >> 16); }
+    }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[g][8 * lane + k] = s[k];
+  __syncthreads();
+  for (int c = threadIdx.x; c < 512; c += 256)
+    if (blockIdx.x * 512 + c < H)
+      part[(size_t)blockIdx.y * H + blockIdx.x * 512 + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+}
+
+// out[i] (+)= sum_s slabs[s][i]: the split-K weight-gradient slabs folded into
+// the gradient (sink) in one pass; fp32, n % 4 == 0.
+__global__ __launch_bounds__(256) void slab_sum(const float* __restrict__ slabs, float* __restrict__ out, int S,
+                                                long long n4, int accumulate) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  const float4* sl = reinterpret_cast<const float4*>(slabs);
+  float4 t = sl[i];
+  for (int k = 1; k < S; ++k) {
+    const float4 v = sl[(long long)k * n4 + i];
+    t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+  }
+  float4* o = reinterpret_cast<float4*>(out);
+  if (accumulate) {
+    const float4 v = o[i];
+    t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+  }
+  o[i] = t;
 }
 
 // ---------------------------------------------------------------- attention softmax
@@ -542,7 +596,47 @@ hipError_t dtfk_ln_bwd(const void* dy, const void* s, const float* mean, const f
 }
 
 hipError_t dtfk_colsum_partials(const float* part, float* out, int P, int H, hipStream_t st) {
-  hipLaunchKernelGGL(colsum_partials, dim3((H + 63) / 64), dim3(1024), 0, st, part, out, P, H);
+  dtfk::tfm::ColsumArgs a = {{part, nullptr, nullptr}, {out, nullptr, nullptr}};
+  hipLaunchKernelGGL(colsum_partials, dim3((H + 63) / 64, 1), dim3(1024), 0, st, a, P, H, 0);
+  return hipGetLastError();
+}
+
+// nbuf (<= 3) partial buffers -> outputs in ONE launch; accumulate: out += sum
+hipError_t dtfk_colsum_partials_multi(const float* const* parts, float* const* outs, int nbuf, int P, int H,
+                                      int accumulate, hipStream_t st) {
+  dtfk::tfm::ColsumArgs a = {{nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr}};
+  for (int k = 0; k < nbuf; ++k) { a.part[k] = parts[k]; a.out[k] = outs[k]; }
+  hipLaunchKernelGGL(colsum_partials, dim3((H + 63) / 64, nbuf), dim3(1024), 0, st, a, P, H, accumulate);
+  return hipGetLastError();
+}
+
+hipError_t dtfk_colsum_bf16(const void* x, float* part, float* out, int N, int H, int P, int accumulate,
+                            hipStream_t st) {
+  if (H % 8 || ((uintptr_t)x % 16)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(colsum_bf16_partials, dim3((H + 511) / 512, P), dim3(256), 0, st,
+                     static_cast<const uint16_t*>(x), part, N, H);
+  dtfk::tfm::ColsumArgs a = {{part, nullptr, nullptr}, {out, nullptr, nullptr}};
+  hipLaunchKernelGGL(colsum_partials, dim3((H + 63) / 64, 1), dim3(1024), 0, st, a, P, H, accumulate);
+  return hipGetLastError();
+}
+
+// scalar form for views that are not 16-byte aligned (DDP bucket offsets)
+__global__ __launch_bounds__(256) void slab_sum1(const float* __restrict__ slabs, float* __restrict__ out, int S,
+                                                 long long n, int accumulate) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float t = slabs[i];
+  for (int k = 1; k < S; ++k) t += slabs[(long long)k * n + i];
+  out[i] = accumulate ? out[i] + t : t;
+}
+
+hipError_t dtfk_slab_sum(const float* slabs, float* out, int S, long long n, int accumulate, hipStream_t st) {
+  if ((n % 4) || (((uintptr_t)slabs | (uintptr_t)out) % 16)) {
+    hipLaunchKernelGGL(slab_sum1, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, slabs, out, S, n, accumulate);
+    return hipGetLastError();
+  }
+  const long long n4 = n / 4;
+  hipLaunchKernelGGL(slab_sum, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, slabs, out, S, n4, accumulate);
   return hipGetLastError();
 }
 

@@ -104,9 +104,15 @@ def _wgrad(gy2, x2, into=None):
             return torch.addmm(into, gy2.t(), x2, out_dtype=torch.float32, out=into)
         return torch.mm(gy2.t(), x2, out_dtype=torch.float32)
     parts = torch.bmm(gy2.view(s, T // s, out).transpose(1, 2), x2.view(s, T // s, -1), out_dtype=torch.float32)
+    from .. import _native
+    if into is not None and into.is_contiguous():   # one pass: into += sum of the slabs
+        _native.load().slab_sum(parts, into, accumulate=True)
+        return into
+    res = torch.empty(parts.shape[1:], dtype=torch.float32, device=parts.device)
+    _native.load().slab_sum(parts, res, accumulate=False)
     if into is not None:
-        return into.add_(parts.sum(0))
-    return parts.sum(0)
+        return into.add_(res)
+    return res
 
 
 def _mm(x, w):

@@ -30,6 +30,17 @@ def enabled(p: torch.Tensor) -> bool:
     return getattr(p, _HOOK, None) is not None and p.requires_grad and not getattr(p, "_dtf_tied", False)
 
 
+def all_enabled(*params) -> bool:
+    """Every given parameter sinks (and any existing .grad is a plain contiguous
+    fp32 buffer the kernels can accumulate into)."""
+    for p in params:
+        if p is None or not enabled(p) or p.dtype != torch.float32:
+            return False
+        if p.grad is not None and not p.grad.is_contiguous():
+            return False
+    return True
+
+
 def mark_tied(p: torch.Tensor) -> None:
     p._dtf_tied = True
 

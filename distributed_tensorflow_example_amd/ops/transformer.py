@@ -29,6 +29,9 @@ def set_dropout_seed(seed: int):
     _seed_counter = itertools.count(1)
 
 
+from . import grad_sink  # noqa: E402
+
+
 def _C():
     return _native.load()
 
@@ -54,6 +57,7 @@ class _BDRLN(torch.autograd.Function):
         r2 = res.reshape(-1, H).contiguous() if res is not None else None
         C.bdrln_fwd(x2, bias, r2, gamma, beta, y, s, mean, rstd, eps, p, seed)
         ctx.save_for_backward(s, mean, rstd, gamma)
+        ctx.params = (gamma, beta, bias)   # for sinking dgamma/dbeta/dbias into .grad
         ctx.p, ctx.seed, ctx.has_res, ctx.shape = p, seed, res is not None, x.shape
         return y.view(x.shape)
 
@@ -66,11 +70,21 @@ class _BDRLN(torch.autograd.Function):
         N = dy2.shape[0]
         ds = torch.empty_like(dy2)
         dxb = torch.empty_like(dy2)
-        dgamma = torch.empty(H, dtype=torch.float32, device=dy.device)
-        dbeta = torch.empty_like(dgamma)
-        dbias = torch.empty_like(dgamma)
-        C.ln_bwd(dy2, s, mean, rstd, gamma, ds, dxb, _ln_part(N, H, dy.device), dgamma, dbeta, dbias, ctx.p, ctx.seed)
+        pg, pb, px = ctx.params
+        sink = grad_sink.all_enabled(pg, pb, px)
+        if sink:   # accumulate straight into the DDP bucket views (no AccumulateGrad adds)
+            dgamma, dbeta, dbias = grad_sink.target(pg), grad_sink.target(pb), grad_sink.target(px)
+        else:
+            dgamma = torch.empty(H, dtype=torch.float32, device=dy.device)
+            dbeta = torch.empty_like(dgamma)
+            dbias = torch.empty_like(dgamma)
+        C.ln_bwd(dy2, s, mean, rstd, gamma, ds, dxb, _ln_part(N, H, dy.device), dgamma, dbeta, dbias, ctx.p, ctx.seed,
+                 accumulate=sink)
         dres = ds.view(ctx.shape) if ctx.has_res else None
+        if sink:
+            for q in (pg, pb, px):
+                grad_sink.done(q)
+            return dxb.view(ctx.shape), None, dres, None, None, None, None
         return dxb.view(ctx.shape), dbias, dres, dgamma, dbeta, None, None
 
 
@@ -105,6 +119,7 @@ class _EmbLN(torch.autograd.Function):
         seed = next_seed() if p > 0 else 0
         C.ln_fwd_f32in(x2, gamma, beta, y, s, mean, rstd, eps, p, seed)
         ctx.save_for_backward(s, mean, rstd, gamma)
+        ctx.params = (gamma, beta)
         ctx.p, ctx.seed, ctx.shape = p, seed, x.shape
         return y.view(x.shape)
 
@@ -120,9 +135,19 @@ class _EmbLN(torch.autograd.Function):
             dy2 = dyd
         N = dy2.shape[0]
         ds = torch.empty_like(dy2)
-        dgamma = torch.empty(H, dtype=torch.float32, device=dy.device)
-        dbeta = torch.empty_like(dgamma)
-        C.ln_bwd(dy2, s, mean, rstd, gamma, ds, None, _ln_part(N, H, dy.device), dgamma, dbeta, None, 0.0, 0)
+        pg, pb = ctx.params
+        sink = grad_sink.all_enabled(pg, pb)
+        if sink:
+            dgamma, dbeta = grad_sink.target(pg), grad_sink.target(pb)
+        else:
+            dgamma = torch.empty(H, dtype=torch.float32, device=dy.device)
+            dbeta = torch.empty_like(dgamma)
+        C.ln_bwd(dy2, s, mean, rstd, gamma, ds, None, _ln_part(N, H, dy.device), dgamma, dbeta, None, 0.0, 0,
+                 accumulate=sink)
+        if sink:
+            grad_sink.done(pg)
+            grad_sink.done(pb)
+            return ds.float().view(ctx.shape), None, None, None, None
         return ds.float().view(ctx.shape), dgamma, dbeta, None, None
 
 
@@ -143,6 +168,7 @@ class _BiasGelu(torch.autograd.Function):
         y = torch.empty_like(x2)
         C.bias_gelu_fwd(x2, bias, y)
         ctx.save_for_backward(x2, bias)
+        ctx.bias_param = bias
         return y
 
     @staticmethod
@@ -154,8 +180,13 @@ class _BiasGelu(torch.autograd.Function):
         dx = torch.empty_like(x)
         slices = max(1, min(512, N // 32))        # >= 32 rows per thread, ~1.5k blocks at BERT-base
         part = torch.empty(slices * H, dtype=torch.float32, device=x.device)
-        dbias = torch.empty(H, dtype=torch.float32, device=x.device)
-        C.bias_gelu_bwd(dy.to(torch.bfloat16).contiguous(), x, bias, dx, part, dbias)
+        pb = ctx.bias_param
+        sink = grad_sink.all_enabled(pb)
+        dbias = grad_sink.target(pb) if sink else torch.empty(H, dtype=torch.float32, device=x.device)
+        C.bias_gelu_bwd(dy.to(torch.bfloat16).contiguous(), x, bias, dx, part, dbias, accumulate=sink)
+        if sink:
+            grad_sink.done(pb)
+            return dx, None
         return dx, dbias
 
 
@@ -218,6 +249,7 @@ class _FusedAttention(torch.autograd.Function):
                               mask if mask is not None else torch.empty(0, device=qkv.device), out, lse)
         ctx.has_bias, ctx.has_mask = bias is not None, mask is not None
         ctx.nh, ctx.scale, ctx.p, ctx.seed = nh, scale, p, seed
+        ctx.bias_param = bias
         return out
 
     @staticmethod
@@ -228,7 +260,18 @@ class _FusedAttention(torch.autograd.Function):
         Dbuf = torch.empty_like(lse)
         C.attn_bwd(qkv, bias if ctx.has_bias else None, mask if ctx.has_mask else None, out,
                    dout.to(torch.bfloat16).contiguous(), lse, Dbuf, dqkv, ctx.nh, ctx.scale, ctx.p, ctx.seed)
-        dbias = dqkv.view(-1, dqkv.shape[-1]).sum(0, dtype=torch.float32) if ctx.has_bias else None
+        dbias = None
+        if ctx.has_bias:
+            H3 = dqkv.shape[-1]
+            N = dqkv.numel() // H3
+            part = torch.empty(max(1, min(256, N // 64)) * H3, dtype=torch.float32, device=dqkv.device)
+            pb = ctx.bias_param
+            sink = grad_sink.all_enabled(pb)
+            dbias = grad_sink.target(pb) if sink else torch.empty(H3, dtype=torch.float32, device=dqkv.device)
+            C.colsum_bf16(dqkv.view(-1, H3), part, dbias, accumulate=sink)   # bias grad = column sums of dqkv
+            if sink:
+                grad_sink.done(pb)
+                dbias = None
         return dqkv, dbias, None, None, None, None
 
 

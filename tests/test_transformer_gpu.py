@@ -232,3 +232,26 @@ def test_fused_attention_dropout_matches_unfused_kernel_path(native):
     assert rel(o1, o2) < 2e-2
     assert rel(g1, g2) < 4e-2
     assert rel(b1, b2) < 4e-2
+
+
+@pytest.mark.parametrize("N,H", [(16384, 2304), (1000, 768), (37, 64), (300, 520)])
+def test_colsum_bf16_matches_torch(native, N, H):
+    x = torch.randn(N, H, device="cuda").bfloat16()
+    part = torch.empty(max(1, min(256, N // 64)) * H, device="cuda")
+    out = torch.full((H,), 0.5, device="cuda")
+    native.colsum_bf16(x, part, out, accumulate=True)
+    ref = x.float().sum(0) + 0.5
+    assert torch.allclose(out, ref, rtol=1e-4, atol=1e-3 * (N ** 0.5))
+    native.colsum_bf16(x, part, out, accumulate=False)
+    assert torch.allclose(out, ref - 0.5, rtol=1e-4, atol=1e-3 * (N ** 0.5))
+
+
+@pytest.mark.parametrize("S,n", [(1, 4), (3, 1001), (4, 768 * 3072), (16, 2304 * 768)])
+def test_slab_sum_matches_torch(native, S, n):
+    slabs = torch.randn(S, n, device="cuda")
+    out = torch.randn(n, device="cuda")
+    ref = out + slabs.sum(0)
+    native.slab_sum(slabs, out, accumulate=True)
+    assert torch.allclose(out, ref, rtol=1e-5, atol=1e-5)
+    native.slab_sum(slabs, out, accumulate=False)
+    assert torch.allclose(out, slabs.sum(0), rtol=1e-5, atol=1e-5)

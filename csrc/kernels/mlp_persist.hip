@@ -219,7 +219,7 @@ constexpr int L_RDB1 = L_B2 + 64;                // [8][16] fp32
 constexpr int L_RDB2 = L_RDB1 + 512;             // [8][16] fp32
 constexpr int L_RMET = L_RDB2 + 512;             // [8][2] fp32
 constexpr int L_FLAG = L_RMET + 64;              // abort flag
-constexpr int LDS_BYTES = L_FLAG + 48;
+constexpr int LDS_BYTES = L_FLAG + 80;
 
 // k-step owned by wave w in slot u (-1: none).  Wave 7 does no forward/head
 // work, so it takes the 25th k-step.
@@ -245,6 +245,7 @@ __device__ void compute(const Args& a, const int j, uint8_t* smem) {
   int* abort_flag = reinterpret_cast<int*>(smem + L_FLAG);
   int* small_done = abort_flag + 1;   // steps whose small-parameter update is complete
   int* wready = abort_flag + 4;       // [8]: steps whose W1 fragments wave v has published
+  int* tready = abort_flag + 12;      // [8]: steps whose head outputs batch tile v has published
 
   // ---- load state
   for (int k = tid; k < 3 * 16 * BPT; k += THREADS) dz2T[k] = (_Float16)0.f;   // also a2T, dz3T
@@ -261,7 +262,7 @@ __device__ void compute(const Args& a, const int j, uint8_t* smem) {
   } else if (tid == 288) {
     *abort_flag = 0;
     *small_done = 0;
-    for (int v = 0; v < 8; ++v) wready[v] = 0;
+    for (int v = 0; v < 8; ++v) wready[v] = tready[v] = 0;
   }
   const int hid = 16 * j + r;       // this lane's hidden unit in the W1^T-fragment / dW1 layouts
   const bool hv = hid < HID;
@@ -527,11 +528,18 @@ __device__ void compute(const Args& a, const int j, uint8_t* smem) {
         const float s = row16_sum(d);
         if (r == 0) rdb1[w * 16 + 4 * g + i] = s;
       }
+      // batch tile w's x-image rows, dz2^T / a2^T / dz3^T columns and sums are in LDS
+      // (an abort flag set above is ordered before this release)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+      if (lane == 0) __hip_atomic_store(tready + w, st + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     if (w == 0) { TSP(12); }
-    lds_barrier();     // S_b: x image, dz2^T, a2^T, dz3^T and the per-tile sums are complete
+    auto wait_tile = [&](int v) {
+      while (__hip_atomic_load(tready + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < st + 1)
+        __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    };
     if (w == 0) { TSP(3); }
-    if (*abort_flag) { aborted = true; break; }
 
     // ---------------- small-parameter gradients (wave 7): dW2 on MFMA, db1, db2, metrics.
     // 1 GPU: applied after S_a, overlapping the next forward (the next head waits on
@@ -578,6 +586,7 @@ __device__ void compute(const Args& a, const int j, uint8_t* smem) {
     if constexpr (MULTI) {
       own_slot = static_cast<char*>(a.peer_base[a.rank]) + IPC_FLAGS + (size_t)(par_of(st) * NWG + j) * IPC_SLOT;
       if (w == 7) {   // small gradients (mean over the local batch) -> own slot, bf16
+        for (int v = 0; v < NBT; ++v) wait_tile(v);
         small_grads(sgw2, sgb);
 #pragma unroll
         for (int i = 0; i < 4; ++i) sgw2[i] = bfround(sgw2[i] * (1.f / (float)B));
@@ -588,25 +597,47 @@ __device__ void compute(const Args& a, const int j, uint8_t* smem) {
       }
     }
 
-    // ---------------- dW1 block (all waves): x^T . dz2, in the accumulator layout
+    // ---------------- dW1 block (all waves): x^T . dz2, in the accumulator layout.
+    // The batch contraction runs in 4 steps of 32 rows (batch tiles 2q, 2q+1), each
+    // as soon as those tiles' head outputs are published -- no block barrier.
     uint2 gq[NU][2];   // N GPUs: this rank's bf16 gradient of the wave's tiles
     {
-      f16x8 bq[4];
+      f32x4 acc[NU][2];
+#pragma unroll
+      for (int u = 0; u < NU; ++u) acc[u][0] = acc[u][1] = f32x4{0.f, 0.f, 0.f, 0.f};
       float cs2 = 0.f;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        bq[q] = *reinterpret_cast<const f16x8*>(dz2T + r * BPT + 32 * q + 8 * g);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) cs2 += (float)bq[q][e];
-      }
-      cs2 += xor16(cs2);
-      cs2 += xor32(cs2);
-      const float corr = 1024.f * cs2;
       // transposed x fragment: lane 2p'+hh of each 16-lane group addresses batch row
       // 32q + 8g + p' and columns 8hh..8hh+7 of the tile; lane r receives feature
       // column r of those 8 rows (rows >= 112 read row - 16: multiplied by dz2 = 0)
       const int prow = 8 * g + (r >> 1);
       const int pcol = 8 * (r & 1);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        wait_tile(2 * q);
+        if (2 * q + 1 < NBT) wait_tile(2 * q + 1);
+        const f16x8 bq = *reinterpret_cast<const f16x8*>(dz2T + r * BPT + 32 * q + 8 * g);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) cs2 += (float)bq[e];
+        int row = 32 * q + prow;
+        row = row < 112 ? row : row - 16;
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+          const int s = kstep_of(w, u);
+          if (s >= 0) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int t = 2 * s + h;
+              if (t < DIN / 16) {
+                const v2i v = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(xim + row * XS + 16 * t + pcol));
+                acc[u][h] = mfma_h(frag_px((uint32_t)v.x, (uint32_t)v.y), bq, acc[u][h]);
+              }
+            }
+          }
+        }
+      }
+      cs2 += xor16(cs2);
+      cs2 += xor32(cs2);
+      const float corr = 1024.f * cs2;
 #pragma unroll
       for (int u = 0; u < NU; ++u) {
         const int s = kstep_of(w, u);
@@ -614,29 +645,18 @@ __device__ void compute(const Args& a, const int j, uint8_t* smem) {
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             const int t = 2 * s + h;
-            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-            if (t < DIN / 16) {
-#pragma unroll
-              for (int q = 0; q < 4; ++q) {
-                int row = 32 * q + prow;
-                row = row < 112 ? row : row - 16;
-                const v2i v = __builtin_amdgcn_ds_read_tr8_b64_v2i32(
-                    (lds_v2i*)(xim + row * XS + 16 * t + pcol));
-                acc = mfma_h(frag_px((uint32_t)v.x, (uint32_t)v.y), bq[q], acc);
-              }
-            }
             if constexpr (!MULTI) {
 #pragma unroll
               for (int i = 0; i < 4; ++i) {
                 const int f = 16 * t + 4 * g + i;
-                if (f < DIN && hv) Wm[u][h][i] -= lrX * (acc[i] - corr);
+                if (f < DIN && hv) Wm[u][h][i] -= lrX * (acc[u][h][i] - corr);
               }
             } else {
               float gg[4];
 #pragma unroll
               for (int i = 0; i < 4; ++i) {
                 const int f = 16 * t + 4 * g + i;
-                gg[i] = (f < DIN && hv) ? (acc[i] - corr) * (1.f / (255.f * (float)B)) : 0.f;
+                gg[i] = (f < DIN && hv) ? (acc[u][h][i] - corr) * (1.f / (255.f * (float)B)) : 0.f;
               }
               gq[u][h] = make_uint2(pack2bf(gg[0], gg[1]), pack2bf(gg[2], gg[3]));
               if (t < DIN / 16) *reinterpret_cast<uint2*>(own_slot + ((t * 4 + g) * 16 + r) * 8) = gq[u][h];
@@ -645,6 +665,8 @@ __device__ void compute(const Args& a, const int j, uint8_t* smem) {
         }
       }
     }
+    // every wave has now seen every tile's readiness (and so any abort set before it)
+    if (*abort_flag) { aborted = true; break; }
     if constexpr (MULTI) {
       // ---- one-shot exchange of block j with the same workgroup on every peer GPU
       // (IPC-mapped uncached buffers: completion == visibility; rank-order sums keep

@@ -146,7 +146,11 @@ def main(argv=None):
     # the xGMI fabric, so it is measured, not assumed.
     picked = []
     for i, mode in enumerate(chain):
-        trainer, runner = setup(mode)
+        try:   # setup failures (IPC mapping, ...) are agreed on collectively, so every rank skips together
+            trainer, runner = setup(mode)
+        except RuntimeError as e:
+            print(f"bench: {mode} unavailable ({e})", file=sys.stderr, flush=True)
+            continue
         if consistent(trainer, runner):
             picked.append((mode, trainer, runner))
             if w.world_size == 1 or len(picked) == 2 or a.tune_steps <= 0:

@@ -191,9 +191,8 @@ class FusedMLPTrainer:
         C = self.C
         self.ipc_flag_bytes = C.mlp_ipc_flag_bytes()
         self.ipc_slot = ((NPARAM * 2 + 255) // 256) * 256
-        buf = C.IpcPeerBuffers(self.ipc_flag_bytes + 2 * self.ipc_slot, w.world_size, w.rank)
-        handles = w.all_gather_object(bytes(buf.handle()))
-        buf.open(list(handles))
+        from ..parallel.world import open_peer_buffers
+        buf = open_peer_buffers(C, self.ipc_flag_bytes + 2 * self.ipc_slot, w)
         self.ipc = buf
         self.ipc_grads = [buf.tensor(self.ipc_flag_bytes + p * self.ipc_slot, NPARAM, 1) for p in (0, 1)]
         self.ipc_err = torch.zeros(1, dtype=torch.int32, device=self.device)
@@ -467,10 +466,8 @@ class PersistentMLPRunner:
         if w is not None and w.world_size > 1:
             if int(os.environ.get("LOCAL_WORLD_SIZE", w.world_size)) != w.world_size:
                 raise RuntimeError("the persistent N-GPU exchange needs all ranks on one node")
-            buf = C.IpcPeerBuffers(C.mlp_persist_ipc_bytes(), w.world_size, w.rank)
-            handles = w.all_gather_object(bytes(buf.handle()))
-            buf.open(list(handles))
-            self.ipc = buf
+            from ..parallel.world import open_peer_buffers
+            self.ipc = open_peer_buffers(C, C.mlp_persist_ipc_bytes(), w)
             self.W, self.rank = w.world_size, w.rank
 
     def _chunks(self, cursor: int, steps: int) -> List[Tuple[int, int]]:

@@ -264,3 +264,36 @@ def reset():
     if _WORLD is not None:
         _WORLD.shutdown()
     _WORLD = None
+
+
+def open_peer_buffers(C, nbytes: int, world) -> "object":
+    """Collective, failure-tolerant setup of `IpcPeerBuffers` (csrc/comm/ipc_peer.cpp)
+    on every rank of `world`: every rank joins the handle exchange even if its own
+    allocation failed, and all ranks agree on the outcome -- either every rank gets
+    its mapped buffers or every rank raises RuntimeError (so a fallback path taken
+    afterwards issues the same collectives everywhere)."""
+    err, buf, h = None, None, b""
+    try:
+        buf = C.IpcPeerBuffers(int(nbytes), world.world_size, world.rank)
+        h = bytes(buf.handle())
+    except Exception as e:  # noqa: BLE001
+        err = e
+    handles = world.all_gather_object(h)
+    if err is None:
+        if not all(handles):
+            err = RuntimeError("a peer failed to allocate its IPC buffer")
+        else:
+            try:
+                buf.open(list(handles))
+            except Exception as e:  # noqa: BLE001
+                err = e
+    ok = world.host_all_reduce(0.0 if err is not None else 1.0, "min")
+    if ok < 1.0:
+        if buf is not None:
+            try:
+                buf.close()
+            except Exception:  # noqa: BLE001
+                pass
+        raise RuntimeError(f"IPC peer buffers unavailable on some rank ({err})")
+    return buf
+

@@ -167,3 +167,62 @@ def test_cluster_ps_worker_example(tmp_path):
     assert "Step: 20,  Global Step: 20" in outs["w0"]
     assert "Test-Accuracy:" in outs["w0"] and "ps 0 done" in outs["ps"]
     assert os.listdir(tmp_path / "logs" / "worker_0")
+
+
+class _FakeBuf:
+    def __init__(self, nbytes, ws, rank, fail_alloc, fail_open):
+        if fail_alloc:
+            raise RuntimeError("hipExtMallocWithFlags failed (simulated)")
+        self.fail_open, self.closed = fail_open, False
+
+    def handle(self):
+        return b"h" * 8
+
+    def open(self, handles):
+        if self.fail_open:
+            raise RuntimeError("hipIpcOpenMemHandle failed (simulated)")
+
+    def close(self):
+        self.closed = True
+
+
+def _ipc_setup_worker(rank, ws, port, q, bad_rank, how):
+    try:
+        sys.path.insert(0, REPO)
+        _env(rank, ws, port)
+        from distributed_tensorflow_example_amd.parallel import world as W
+
+        w = W.init(backend="gloo")
+
+        class C:
+            @staticmethod
+            def IpcPeerBuffers(nbytes, ws_, r_):
+                return _FakeBuf(nbytes, ws_, r_, how == "alloc" and r_ == bad_rank, how == "open" and r_ == bad_rank)
+
+        try:
+            W.open_peer_buffers(C, 1024, w)
+            res = "ok"
+        except RuntimeError:
+            res = "raised"
+        # the fallback path after it must still line up collectively on every rank
+        assert w.host_all_reduce(1.0, "sum") == ws
+        q.put((rank, res))
+    except Exception as e:  # pragma: no cover
+        q.put((rank, repr(e)))
+
+
+@pytest.mark.parametrize("how", ["none", "alloc", "open"])
+def test_open_peer_buffers_fails_collectively(how):
+    """IPC setup failing on ONE rank (allocation or mapping) makes EVERY rank raise,
+    with no rank stuck in the handle exchange (the bench's fallback chain relies on it)."""
+    ws, port = 3, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_ipc_setup_worker, args=(r, ws, port, q, 1, how)) for r in range(ws)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(ws))
+    for p in ps:
+        p.join(timeout=60)
+    want = "ok" if how == "none" else "raised"
+    assert all(v == want for v in res.values()), res

@@ -27,6 +27,9 @@ hipError_t dtfk_embedding_bag_fwd(const float* W, int64_t V, int D, const int64_
 hipError_t dtfk_embedding_bag_bwd(float* target, int64_t V, int D, const int64_t* ids, const int64_t* offsets,
                                   const float* psw, const float* dout, int B, int mode, float lr,
                                   hipStream_t s);
+hipError_t dtfk_embedding_bag_bwd_sorted(float* target, int64_t V, int D, const int* rows, const int64_t* occ,
+                                         const int* bag_of, const float* psw, const float* dout, int64_t N,
+                                         hipStream_t s);
 hipError_t dtfk_argmax_correct(const float* x, const int64_t* labels, int B, int C, int64_t* count,
                                hipStream_t s);
 hipError_t dtfk_auc_hist(const float* pred, const float* label, int64_t n, int nbins, unsigned long long* pos,
@@ -190,6 +193,25 @@ void embedding_bag_bwd(at::Tensor target, at::Tensor ids, at::Tensor offsets, c1
      "embedding_bag_bwd");
 }
 
+void embedding_bag_bwd_sorted(at::Tensor target, at::Tensor rows, at::Tensor occ, at::Tensor bag_of,
+                              c10::optional<at::Tensor> psw, at::Tensor dout) {
+  f32c(target, "target"); i64c(occ, "occ"); f32c(dout, "dout");
+  gpu(rows, "rows"); gpu(bag_of, "bag_of");
+  if (rows.scalar_type() != at::kInt || bag_of.scalar_type() != at::kInt || !rows.is_contiguous() ||
+      !bag_of.is_contiguous())
+    throw std::runtime_error("embedding_bag_bwd_sorted: rows / bag_of must be contiguous int32");
+  if (psw.has_value()) f32c(*psw, "per_sample_weights");
+  const int64_t N = rows.numel();
+  const int D = target.dim() == 1 ? 1 : (int)target.size(1);
+  if (occ.numel() != N || bag_of.numel() != N) throw std::runtime_error("embedding_bag_bwd_sorted: length mismatch");
+  if (psw.has_value() && psw->numel() != N) throw std::runtime_error("embedding_bag_bwd_sorted: psw length");
+  if (dout.dim() != 2 || dout.size(1) != D) throw std::runtime_error("embedding_bag_bwd_sorted: dout must be [B, D]");
+  ck(dtfk_embedding_bag_bwd_sorted(target.data_ptr<float>(), target.size(0), D, rows.data_ptr<int>(),
+                                   occ.data_ptr<int64_t>(), bag_of.data_ptr<int>(), opt_ptr<float>(psw),
+                                   dout.data_ptr<float>(), N, cs()),
+     "embedding_bag_bwd_sorted");
+}
+
 void argmax_correct(at::Tensor x, at::Tensor labels, at::Tensor count) {
   f32c(x, "x"); i64c(labels, "labels"); i64c(count, "count");
   ck(dtfk_argmax_correct(x.data_ptr<float>(), labels.data_ptr<int64_t>(), (int)x.size(0), (int)x.size(1),
@@ -240,6 +262,7 @@ void init_ops(py::module& m) {
   m.def("sigmoid_xent", &sigmoid_xent);
   m.def("embedding_bag_fwd", &embedding_bag_fwd);
   m.def("embedding_bag_bwd", &embedding_bag_bwd);
+  m.def("embedding_bag_bwd_sorted", &embedding_bag_bwd_sorted);
   m.def("argmax_correct", &argmax_correct);
   m.def("auc_hist", &auc_hist);
   m.def("multi_tensor_apply", &multi_tensor_apply);

@@ -88,7 +88,7 @@ template <bool ABF, bool BBF, bool TA, bool TB, bool OBF>
 __global__ __launch_bounds__(256) void gemm_bias_act(
     const void* __restrict__ A, int lda, const void* __restrict__ Bm, int ldb,
     void* __restrict__ C, int ldc, float* __restrict__ Zout, const float* __restrict__ bias,
-    int M, int N, int K, float alpha, float beta, int act) {
+    int M, int N, int K, float alpha, float beta, int act, int kchunk) {
   __shared__ __attribute__((aligned(16))) uint16_t As[BM * LDK];
   __shared__ __attribute__((aligned(16))) uint16_t Bs[BN * LDK];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -110,18 +110,20 @@ __global__ __launch_bounds__(256) void gemm_bias_act(
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // split-K (gridDim.y > 1): this block contracts k in [kb, ke) only
+  const int kb = blockIdx.y * kchunk, ke = min(K, kb + kchunk);
   float va[8], vb[8];
   // A' tile rows = m, K contiguous iff !TA;  B' tile rows = n, K contiguous iff TB
-  load_tile<ABF, !TA>(A, lda, M, K, m0, 0, va);
-  load_tile<BBF, TB>(Bm, ldb, N, K, n0, 0, vb);
-  for (int k0 = 0; k0 < K; k0 += BK) {
+  load_tile<ABF, !TA>(A, lda, M, ke, m0, kb, va);
+  load_tile<BBF, TB>(Bm, ldb, N, ke, n0, kb, vb);
+  for (int k0 = kb; k0 < ke; k0 += BK) {
     __syncthreads();
     store_tile<!TA>(As, va);
     store_tile<TB>(Bs, vb);
     __syncthreads();
-    if (k0 + BK < K) {  // prefetch next K tile into registers (branch is uniform)
-      load_tile<ABF, !TA>(A, lda, M, K, m0, k0 + BK, va);
-      load_tile<BBF, TB>(Bm, ldb, N, K, n0, k0 + BK, vb);
+    if (k0 + BK < ke) {  // prefetch next K tile into registers (branch is uniform)
+      load_tile<ABF, !TA>(A, lda, M, ke, m0, k0 + BK, va);
+      load_tile<BBF, TB>(Bm, ldb, N, ke, n0, k0 + BK, vb);
     }
     bf16x8 fa[2], fb[2];
 #pragma unroll
@@ -145,6 +147,11 @@ __global__ __launch_bounds__(256) void gemm_bias_act(
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + wr * 32 + i * 16 + 4 * lh + r;
         if (m < M && n < N) {
+          if (gridDim.y > 1) {  // split-K: linear epilogue (host-checked), partial sums meet in fp32 C
+            atomicAdd(reinterpret_cast<float*>(C) + (size_t)m * ldc + n,
+                      alpha * acc[i][j][r] + (blockIdx.y == 0 ? bv : 0.f));
+            continue;
+          }
           float z = alpha * acc[i][j][r] + bv;
           const size_t o = (size_t)m * ldc + n;
           if (beta != 0.f) z += beta * (OBF ? bf2f(reinterpret_cast<uint16_t*>(C)[o]) : reinterpret_cast<float*>(C)[o]);
@@ -168,10 +175,27 @@ extern "C" hipError_t dtfk_gemm(const void* A, int a_bf16, int lda, int transA, 
   using namespace dtfk::gemm;
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   if (tiles == 0) return hipSuccess;
-  const dim3 grid(tiles), block(256);
+  // Split-K when the output has too few 64x64 tiles to fill 256 CUs and K is
+  // long -- the weight gradients X^T dZ (M x N = fan_in x fan_out, K = batch).
+  // Only for a linear fp32 epilogue: the partial products meet by atomics.
+  int split = 1, kchunk = K;
+  if (act == ACT_NONE && Z == nullptr && !c_bf16 && (beta == 0.f || beta == 1.f) && tiles < 256 && K >= 512) {
+    split = (512 + tiles - 1) / tiles;
+    if (split > K / 256) split = K / 256;
+    if (split > 1) {
+      kchunk = ((K + split - 1) / split + BK - 1) / BK * BK;
+      split = (K + kchunk - 1) / kchunk;
+    }
+    if (split <= 1) { split = 1; kchunk = K; }
+  }
+  if (split > 1 && beta == 0.f) {
+    const hipError_t e = hipMemset2DAsync(C, (size_t)ldc * sizeof(float), 0, (size_t)N * sizeof(float), M, stream);
+    if (e != hipSuccess) return e;
+  }
+  const dim3 grid(tiles, split), block(256);
 #define DTFK_G(AB, BB, TA, TB, OB)                                                               \
   hipLaunchKernelGGL((gemm_bias_act<AB, BB, TA, TB, OB>), grid, block, 0, stream, A, lda, B, ldb, \
-                     C, ldc, Z, bias, M, N, K, alpha, beta, act)
+                     C, ldc, Z, bias, M, N, K, alpha, beta, act, kchunk)
 #define DTFK_G_OB(AB, BB, TA, TB) \
   if (c_bf16) DTFK_G(AB, BB, TA, TB, true); else DTFK_G(AB, BB, TA, TB, false)
 #define DTFK_G_TB(AB, BB, TA) \

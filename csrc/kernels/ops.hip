@@ -291,6 +291,74 @@ __global__ void embedding_bag_bwd(float* __restrict__ target, int64_t V, int D,
   }
 }
 
+// Sum-bag gradient without atomic pile-ups on hot ids.  Occurrences arrive
+// sorted by target row (one radix sort per step, shared by every table that
+// reads the same ids), each wave reduces 64 consecutive occurrences in
+// registers and issues one atomic per (row run, column): a Zipf-hot row seen
+// 10^4 times in a batch costs ~10^4/64 atomics instead of 10^4 serialised ones.
+//   rows[p]  target row of sorted occurrence p (int32), occ[p] its CSR position,
+//   bag_of[j] the bag of CSR position j.
+__global__ void embedding_bag_bwd_sorted(float* __restrict__ target, int64_t V, int D,
+                                         const int* __restrict__ rows, const int64_t* __restrict__ occ,
+                                         const int* __restrict__ bag_of, const float* __restrict__ psw,
+                                         const float* __restrict__ dout, int64_t N) {
+  const int lane = threadIdx.x & 63;
+  const int64_t p0 = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64;
+  if (p0 >= N) return;
+  const int cnt = (int)min((int64_t)64, N - p0);
+  const int64_t p = p0 + lane;
+  int row = -1, b = 0;
+  float w = 0.f;
+  if (lane < cnt) {
+    const int r = rows[p];
+    const int64_t j = occ[p];
+    b = bag_of[j];
+    if (r >= 0 && r < V) { row = r; w = psw ? psw[j] : 1.f; }
+  }
+  if (D < 64) {
+    // lanes own occurrences: segmented inclusive scan over equal (sorted) rows
+    const int nxt = __shfl_down(row, 1, 64);
+    const bool tail = row >= 0 && (lane == cnt - 1 || nxt != row);
+    for (int d = 0; d < D; ++d) {
+      float v = w * dout[(size_t)b * D + d];
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const float vu = __shfl_up(v, off, 64);
+        const int ru = __shfl_up(row, off, 64);
+        if (lane >= off && ru == row) v += vu;
+      }
+      if (tail) atomicAdd(&target[(int64_t)row * D + d], v);
+    }
+    return;
+  }
+  // lanes own columns: walk the 64 occurrences, 8 loads in flight at a time
+  for (int d0 = 0; d0 < D; d0 += 64) {
+    const int d = d0 + lane;
+    const int dc = min(d, D - 1);
+    float acc = 0.f;
+    for (int q0 = 0; q0 < cnt; q0 += 8) {
+      float v[8];
+      int r[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int q = min(q0 + u, 63);
+        r[u] = q0 + u < cnt ? __shfl(row, q, 64) : -1;
+        v[u] = __shfl(w, q, 64) * dout[(size_t)__shfl(b, q, 64) * D + dc];
+      }
+      const int r_next = q0 + 8 < cnt ? __shfl(row, min(q0 + 8, 63), 64) : -2;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        acc += v[u];
+        const int rn = u < 7 ? r[u + 1] : r_next;
+        if (rn != r[u]) {
+          if (r[u] >= 0 && d < D) atomicAdd(&target[(int64_t)r[u] * D + d], acc);
+          acc = 0.f;
+        }
+      }
+    }
+  }
+}
+
 // rows of [N, C] logits vs int64 labels -> number of argmax hits
 __global__ void argmax_correct(const float* __restrict__ x, const int64_t* __restrict__ labels, int Bn,
                                int Cn, int64_t* __restrict__ count) {
@@ -468,6 +536,15 @@ hipError_t dtfk_embedding_bag_bwd(float* target, int64_t V, int D, const int64_t
                                   hipStream_t s) {
   hipLaunchKernelGGL(embedding_bag_bwd, dim3((B + 3) / 4), dim3(256), 0, s, target, V, D, ids, offsets, psw,
                      dout, B, mode, lr);
+  return hipGetLastError();
+}
+hipError_t dtfk_embedding_bag_bwd_sorted(float* target, int64_t V, int D, const int* rows, const int64_t* occ,
+                                         const int* bag_of, const float* psw, const float* dout, int64_t N,
+                                         hipStream_t s) {
+  if (N <= 0) return hipSuccess;
+  const int64_t waves = (N + 63) / 64;
+  hipLaunchKernelGGL(embedding_bag_bwd_sorted, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, target, V, D,
+                     rows, occ, bag_of, psw, dout, N);
   return hipGetLastError();
 }
 hipError_t dtfk_argmax_correct(const float* x, const int64_t* labels, int B, int C, int64_t* count,

@@ -24,7 +24,7 @@ from typing import List, Optional, Sequence
 import torch
 
 from .. import ops, optim
-from ..parallel.sharded_embedding import ShardedEmbedding
+from ..parallel.sharded_embedding import ShardedEmbedding, apply_sgd_shared, lookup_shared
 from ..parallel.world import World, get_world
 
 
@@ -66,19 +66,27 @@ class WideDeep:
         self.global_step = 0
 
     def forward(self, labels, offsets, ids, vals):
-        wide, wst = self.wide.bag_forward(ids, offsets, vals, "sum")
-        emb, est = self.emb.bag_forward(ids, offsets, vals, self.combiner)
+        # both tables read the same ids over the same row partition: one
+        # dedup + id exchange, one row exchange carrying [U, 1 + D]
+        ctx = self.wide.route(ids)
+        wrows, erows = lookup_shared([self.wide, self.emb], ctx)
+        wrows = wrows.detach().requires_grad_(True)
+        erows = erows.detach().requires_grad_(True)
+        offsets = offsets.to(self.device).long()
+        vals = None if vals is None else vals.to(self.device).float()
+        wide = ops.embedding_bag(wrows, ctx.inverse, offsets, vals, "sum")
+        emb = ops.embedding_bag(erows, ctx.inverse, offsets, vals, self.combiner)
         h = emb
         nl = len(self.layers) // 2
         for i in range(nl):
             h = ops.linear_act(h, self.layers[2 * i], self.layers[2 * i + 1], "relu" if i < nl - 1 else "none")
         logit = wide + h + self.bias
-        return logit, (wst, est)
+        return logit, (wrows, erows, ctx)
 
     def train_step(self, batch) -> torch.Tensor:
         labels, offsets, ids, vals = batch.to(self.device) if hasattr(batch, "to") else batch
         self.flat_grad.zero_()
-        logit, (wst, est) = self.forward(labels, offsets, ids, vals)
+        logit, (wrows, erows, lctx) = self.forward(labels, offsets, ids, vals)
         loss = ops.sigmoid_xent(logit, labels)
         loss.backward()
         ws = self.world.world_size
@@ -93,8 +101,8 @@ class WideDeep:
                 ev.record(self.comm_stream)
             else:
                 self.world.all_reduce(self.flat_grad)
-        self.wide.bag_backward_sgd(wst, self.lr / ws)
-        self.emb.bag_backward_sgd(est, self.lr / ws)
+        grads = [r.grad if r.grad is not None else torch.zeros_like(r) for r in (wrows, erows)]
+        apply_sgd_shared([self.wide, self.emb], lctx, grads, [self.lr / ws] * 2)
         if ev is not None:
             torch.cuda.current_stream().wait_event(ev)
         self.opt.step(grad_scale=1.0 / ws)

@@ -247,9 +247,35 @@ class _EmbeddingBag(torch.autograd.Function):
         C = _C()
         ids, offsets, psw = ctx.saved_tensors
         gw = torch.zeros(ctx.wshape, dtype=torch.float32, device=gout.device)
-        C.embedding_bag_bwd(gw, ids, offsets, psw if ctx.has_psw else None, gout.contiguous().float(),
-                            EMB_MODE[ctx.mode], 0.0)
+        psw = psw if ctx.has_psw else None
+        if ctx.mode == "sum" and 0 < ids.numel() < 2 ** 31 and ctx.wshape[0] < 2 ** 31:
+            rows, occ, bag_of = _bag_plan(ids, offsets)
+            C.embedding_bag_bwd_sorted(gw, rows, occ, bag_of, psw, gout.reshape(offsets.numel() - 1, -1)
+                                       .contiguous().float())
+        else:
+            C.embedding_bag_bwd(gw, ids, offsets, psw, gout.contiguous().float(), EMB_MODE[ctx.mode], 0.0)
         return gw, None, None, None, None
+
+
+_BAG_PLAN = [None]
+
+
+def _bag_plan(ids: torch.Tensor, offsets: torch.Tensor):
+    """(rows int32 sorted, CSR position of each sorted occurrence, bag of each
+    CSR position) for the sorted-segment bag backward.  The last plan is kept
+    (with strong refs, so its data pointers cannot be recycled): the wide and
+    deep tables of one Wide&Deep step read the same ids and share one sort."""
+    key = (ids.data_ptr(), ids.numel(), ids._version, offsets.data_ptr(), offsets.numel(), offsets._version)
+    c = _BAG_PLAN[0]
+    if c is not None and c[0] == key:
+        return c[3]
+    n, B = ids.numel(), offsets.numel() - 1
+    rows, occ = torch.sort(ids.to(torch.int32))
+    bag_of = torch.repeat_interleave(torch.arange(B, dtype=torch.int32, device=ids.device),
+                                     offsets[1:] - offsets[:-1], output_size=n)
+    plan = (rows.contiguous(), occ.contiguous(), bag_of.contiguous())
+    _BAG_PLAN[0] = (key, ids, offsets, plan)
+    return plan
 
 
 def embedding_bag(weight, ids, offsets, per_sample_weights=None, mode: str = "sum"):

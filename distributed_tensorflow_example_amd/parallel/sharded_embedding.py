@@ -86,12 +86,15 @@ class ShardedEmbedding:
                     self.local[s:e] = counter_normal(grow, self.dim, seed, init_std)
 
     # ------------------------------------------------------------------ exchange
-    def lookup(self, ids: torch.Tensor):
-        """rows [U, D] for the unique ids of `ids`, plus the routing context."""
+    def route(self, ids: torch.Tensor) -> LookupCtx:
+        """Dedup `ids` and send each owner the unique ids it serves (no rows yet).
+
+        The context depends only on the ids and the row partition, so tables
+        with the same row count and world share it (`lookup_shared`)."""
         ids = ids.to(self.device).long()
         uniq, inverse = torch.unique(ids, return_inverse=True)
         if self.W == 1:
-            return self.local.index_select(0, uniq), LookupCtx(uniq, inverse, None, None, None, uniq)
+            return LookupCtx(uniq, inverse, None, None, None, uniq)
         owner = uniq % self.W
         order = torch.argsort(owner, stable=True)
         uniq_sorted = uniq[order]
@@ -101,22 +104,18 @@ class ShardedEmbedding:
         send_l, recv_l = send.tolist(), recv.tolist()
         recv_ids = torch.empty(sum(recv_l), dtype=torch.int64, device=self.device)
         self.world.all_to_all(uniq_sorted, send_l, recv_ids, recv_l)
-        recv_local = recv_ids // self.W
-        served = self.local.index_select(0, recv_local)
-        got = torch.empty((uniq.numel(), self.dim), dtype=torch.float32, device=self.device)
-        self.world.all_to_all(served, recv_l, got, send_l)
-        rows = torch.empty_like(got)
-        rows[order] = got
-        return rows, LookupCtx(uniq, inverse, order, send_l, recv_l, recv_local)
+        return LookupCtx(uniq, inverse, order, send_l, recv_l, recv_ids // self.W)
+
+    def lookup(self, ids: torch.Tensor):
+        """rows [U, D] for the unique ids of `ids`, plus the routing context."""
+        ctx = self.route(ids)
+        return lookup_shared([self], ctx)[0], ctx
 
     def apply_sgd(self, ctx: LookupCtx, grad_rows: torch.Tensor, lr: float):
         """local[owner rows] -= lr * grad (grad_rows aligned with ctx.uniq)."""
-        g = grad_rows.float().reshape(-1, self.dim)
-        if self.W > 1:
-            g_sorted = g[ctx.order].contiguous()
-            recv_g = torch.empty((sum(ctx.recv), self.dim), dtype=torch.float32, device=self.device)
-            self.world.all_to_all(g_sorted, ctx.send, recv_g, ctx.recv)
-            g = recv_g
+        apply_sgd_shared([self], ctx, [grad_rows], [lr])
+
+    def _sgd_local(self, ctx: LookupCtx, g: torch.Tensor, lr: float):
         n = g.shape[0]
         if n == 0:
             return
@@ -161,3 +160,45 @@ class ShardedEmbedding:
     def load_full(self, table: torch.Tensor):
         with torch.no_grad():
             self.local.copy_(table.to(self.device)[self.rank::self.W])
+
+
+def _check_shared(tables):
+    t0 = tables[0]
+    for t in tables[1:]:
+        if t.num_rows != t0.num_rows or t.world is not t0.world:
+            raise ValueError("tables sharing one routing context need the same row count and world")
+
+
+def lookup_shared(tables, ctx: LookupCtx):
+    """Rows of every table for ctx.uniq with ONE row all-to-all: owners gather
+    each table's rows side by side ([n, sum D]) so W&D's wide and deep tables
+    (same ids, same partition) pay one dedup, one id exchange and one row
+    exchange per step instead of two of each."""
+    _check_shared(tables)
+    t0 = tables[0]
+    if t0.W == 1:
+        return [t.local.index_select(0, ctx.uniq) for t in tables]
+    dims = [t.dim for t in tables]
+    served = torch.cat([t.local.index_select(0, ctx.recv_local) for t in tables], 1) if len(tables) > 1 else \
+        t0.local.index_select(0, ctx.recv_local)
+    got = torch.empty((ctx.uniq.numel(), sum(dims)), dtype=torch.float32, device=t0.device)
+    t0.world.all_to_all(served.contiguous(), ctx.recv, got, ctx.send)
+    rows = torch.empty_like(got)
+    rows[ctx.order] = got
+    return list(rows.split(dims, 1)) if len(tables) > 1 else [rows]
+
+
+def apply_sgd_shared(tables, ctx: LookupCtx, grads, lrs):
+    """Sparse SGD on every table; the gradients travel to the owners in ONE
+    all-to-all (columns side by side, same routing as `lookup_shared`)."""
+    _check_shared(tables)
+    t0 = tables[0]
+    gs = [g.float().reshape(-1, t.dim) for t, g in zip(tables, grads)]
+    if t0.W > 1:
+        g = torch.cat(gs, 1) if len(gs) > 1 else gs[0]
+        g_sorted = g[ctx.order].contiguous()
+        recv_g = torch.empty((sum(ctx.recv), g.shape[1]), dtype=torch.float32, device=t0.device)
+        t0.world.all_to_all(g_sorted, ctx.send, recv_g, ctx.recv)
+        gs = list(recv_g.split([t.dim for t in tables], 1))
+    for t, g, lr in zip(tables, gs, lrs):
+        t._sgd_local(ctx, g.contiguous(), lr)

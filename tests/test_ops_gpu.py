@@ -158,6 +158,44 @@ def test_embedding_bag_fwd_bwd(native, D, mode):
     assert torch.allclose(Wg.grad.cpu(), Wr.grad, atol=1e-4, rtol=1e-4)
 
 
+@pytest.mark.parametrize("D", [1, 7, 64, 130])
+def test_embedding_bag_bwd_sorted_hot_ids(native, D):
+    """Zipf ids (one row hit thousands of times, runs crossing wave chunks) through
+    the sorted-segment backward; a second table over the same ids reuses the plan."""
+    from distributed_tensorflow_example_amd import ops
+    import numpy as np
+    rng = np.random.default_rng(D)
+    B, nnz, V = 512, 24, 3000
+    ids = torch.from_numpy((rng.zipf(1.1, B * nnz) - 1) % V).long()
+    offsets = torch.arange(0, B * nnz + 1, nnz, dtype=torch.int64)
+    w = torch.rand(ids.numel())
+    W1, W2 = torch.randn(V, D), torch.randn(V, 3)
+    go1, go2 = torch.randn(B, D), torch.randn(B, 3)
+    refs = []
+    for W, go in ((W1, go1), (W2, go2)):
+        Wr = W.clone().requires_grad_()
+        ops.embedding_bag(Wr, ids, offsets, w, "sum").backward(go)
+        refs.append(Wr.grad)
+    idc, offc, wc = ids.cuda(), offsets.cuda(), w.cuda()
+    for (W, go), ref in zip(((W1, go1), (W2, go2)), refs):
+        Wg = W.cuda().requires_grad_()
+        ops.embedding_bag(Wg, idc, offc, wc, "sum").backward(go.cuda())
+        assert rel(Wg.grad, ref) < 1e-5
+
+
+@pytest.mark.parametrize("beta", [0.0, 1.0])
+def test_gemm_split_k_weight_grad(native, beta):
+    """X^T dZ with K = batch 4096 and a 64 x 512 output: split over K, atomics into C."""
+    C = native
+    torch.manual_seed(3)
+    X, dZ = torch.randn(4096, 64).cuda(), torch.randn(4096, 512).cuda()
+    out = torch.randn(64, 512).cuda()
+    o0 = out.clone()
+    C.gemm(X, True, dZ, False, out, None, 0, 0.5, beta, None)
+    ref = 0.5 * (X.bfloat16().float().t() @ dZ.bfloat16().float()) + beta * o0
+    assert rel(out, ref) < 1e-4
+
+
 def test_embedding_bag_sgd_scatter(native):
     from distributed_tensorflow_example_amd import ops
     V, D, B = 1000, 1, 200

@@ -189,6 +189,7 @@ class Stream {
   }
   ~Stream() { stop(); }
   void stop() {
+    std::lock_guard<std::mutex> g(stop_mu_);   // one joiner at a time
     {
       std::lock_guard<std::mutex> lk(mu_);
       stop_ = true;
@@ -286,6 +287,7 @@ class Stream {
   bool stop_ = false;
   std::string err_;
   std::atomic<int64_t> emitted_{0};
+  std::mutex stop_mu_;
   std::vector<std::thread> th_;
 };
 

@@ -125,6 +125,10 @@ class Server {
   ~Server() { stop(); }
   int port() const { return port_; }
   void stop() {
+    // serialised: a second caller (e.g. the destructor racing an explicit
+    // stop() from another thread) waits until the threads are joined instead
+    // of returning early and destroying joinable std::threads (-> terminate)
+    std::lock_guard<std::mutex> g(stop_mu_);
     if (stopping_.exchange(true)) return;
     ::shutdown(fd_, SHUT_RDWR);
     ::close(fd_);
@@ -231,6 +235,7 @@ class Server {
 
   int fd_ = -1, port_ = 0;
   std::atomic<bool> stopping_{false};
+  std::mutex stop_mu_;
   std::mutex mu_;
   std::condition_variable cv_;
   std::map<std::string, std::string> kv_;

@@ -172,6 +172,9 @@ class EventFileWriter {
     if (f_) fflush(f_);
   }
   void close() {
+    // serialised so a racing second close (destructor vs. explicit close on
+    // another thread) waits for the join instead of leaving th_ joinable
+    std::lock_guard<std::mutex> g(close_mu_);
     {
       std::lock_guard<std::mutex> lk(mu_);
       if (closed_) return;
@@ -234,6 +237,7 @@ class EventFileWriter {
   std::deque<std::string> q_;
   bool closed_ = false, flush_req_ = false, writing_ = false;
   std::atomic<int64_t> written_{0};
+  std::mutex close_mu_;
   std::thread th_;
 };
 

@@ -257,25 +257,40 @@ class _EmbeddingBag(torch.autograd.Function):
         return gw, None, None, None, None
 
 
-_BAG_PLAN = [None]
+_SORT_PLAN = [None]   # (key, ids ref, (rows int32 sorted, occ))
+_BAG_OF = [None]      # (key, offsets ref, bag_of int32)
+
+
+def _tkey(t: torch.Tensor):
+    return (t.data_ptr(), t.numel(), t._version)
+
+
+def register_sorted_ids(ids: torch.Tensor, rows_sorted: torch.Tensor, occ: torch.Tensor) -> None:
+    """Hand the bag backward a sort of `ids` that the caller already has (the
+    sharded-table router sorts ids to dedup them; the dedup inverse it produces
+    is monotone in the ids, so the same permutation sorts the inverse)."""
+    _SORT_PLAN[0] = (_tkey(ids), ids, (rows_sorted.to(torch.int32).contiguous(), occ.contiguous()))
 
 
 def _bag_plan(ids: torch.Tensor, offsets: torch.Tensor):
     """(rows int32 sorted, CSR position of each sorted occurrence, bag of each
-    CSR position) for the sorted-segment bag backward.  The last plan is kept
-    (with strong refs, so its data pointers cannot be recycled): the wide and
-    deep tables of one Wide&Deep step read the same ids and share one sort."""
-    key = (ids.data_ptr(), ids.numel(), ids._version, offsets.data_ptr(), offsets.numel(), offsets._version)
-    c = _BAG_PLAN[0]
-    if c is not None and c[0] == key:
-        return c[3]
-    n, B = ids.numel(), offsets.numel() - 1
-    rows, occ = torch.sort(ids.to(torch.int32))
-    bag_of = torch.repeat_interleave(torch.arange(B, dtype=torch.int32, device=ids.device),
-                                     offsets[1:] - offsets[:-1], output_size=n)
-    plan = (rows.contiguous(), occ.contiguous(), bag_of.contiguous())
-    _BAG_PLAN[0] = (key, ids, offsets, plan)
-    return plan
+    CSR position) for the sorted-segment bag backward.  The last sort and bag
+    map are kept (with strong refs, so their data pointers cannot be recycled):
+    the wide and deep tables of one Wide&Deep step read the same ids and share
+    one sort, which the router usually supplied already."""
+    c = _SORT_PLAN[0]
+    if c is None or c[0] != _tkey(ids):
+        rows, occ = torch.sort(ids.to(torch.int32))
+        c = (_tkey(ids), ids, (rows.contiguous(), occ.contiguous()))
+        _SORT_PLAN[0] = c
+    b = _BAG_OF[0]
+    if b is None or b[0] != _tkey(offsets):
+        B = offsets.numel() - 1
+        bag_of = torch.repeat_interleave(torch.arange(B, dtype=torch.int32, device=ids.device),
+                                         offsets[1:] - offsets[:-1], output_size=ids.numel())
+        b = (_tkey(offsets), offsets, bag_of.contiguous())
+        _BAG_OF[0] = b
+    return c[2][0], c[2][1], b[2]
 
 
 def embedding_bag(weight, ids, offsets, per_sample_weights=None, mode: str = "sum"):

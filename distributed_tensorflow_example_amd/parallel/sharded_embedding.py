@@ -92,7 +92,17 @@ class ShardedEmbedding:
         The context depends only on the ids and the row partition, so tables
         with the same row count and world share it (`lookup_shared`)."""
         ids = ids.to(self.device).long()
-        uniq, inverse = torch.unique(ids, return_inverse=True)
+        if ids.is_cuda and 0 < ids.numel() and self.num_rows < 2 ** 31:
+            # one int32 radix sort serves both the dedup and (handed over to
+            # ops) the sorted-segment backward of every bag over these ids
+            sids, perm = torch.sort(ids.to(torch.int32))
+            uniq32, inv_sorted = torch.unique_consecutive(sids, return_inverse=True)
+            uniq = uniq32.long()
+            inverse = torch.empty_like(ids)
+            inverse[perm] = inv_sorted
+            ops.register_sorted_ids(inverse, inv_sorted, perm)
+        else:
+            uniq, inverse = torch.unique(ids, return_inverse=True)
         if self.W == 1:
             return LookupCtx(uniq, inverse, None, None, None, uniq)
         owner = uniq % self.W

@@ -37,7 +37,9 @@ def _C():
 
 
 def _ln_part(N: int, H: int, device) -> torch.Tensor:
-    grid = max(1, min(256, (N + 15) // 16))      # >= 4 rows per wave, one partial row per block
+    # 4 blocks per CU (16 waves) with ~4 rows per wave: at 1 block per CU the
+    # per-row load -> reduce -> store latency chain ran 3x off HBM bandwidth
+    grid = max(1, min(1024, (N + 15) // 16))     # one partial row per block
     return torch.empty(3 * grid * H, dtype=torch.float32, device=device)
 
 

@@ -331,9 +331,11 @@ __global__ void embedding_bag_bwd_sorted(float* __restrict__ target, int64_t V, 
     }
     return;
   }
-  // lanes own columns: walk the 64 occurrences, 8 loads in flight at a time
-  for (int d0 = 0; d0 < D; d0 += 64) {
-    const int d = d0 + lane;
+  // lanes own columns (one 64-column slice per blockIdx.y, so wide rows such
+  // as BERT's 768-wide token table still spread over many waves): walk the 64
+  // occurrences, 8 loads in flight at a time
+  {
+    const int d = blockIdx.y * 64 + lane;
     const int dc = min(d, D - 1);
     float acc = 0.f;
     for (int q0 = 0; q0 < cnt; q0 += 8) {
@@ -543,7 +545,8 @@ hipError_t dtfk_embedding_bag_bwd_sorted(float* target, int64_t V, int D, const 
                                          hipStream_t s) {
   if (N <= 0) return hipSuccess;
   const int64_t waves = (N + 63) / 64;
-  hipLaunchKernelGGL(embedding_bag_bwd_sorted, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, target, V, D,
+  const unsigned col_blocks = D < 64 ? 1u : (unsigned)((D + 63) / 64);
+  hipLaunchKernelGGL(embedding_bag_bwd_sorted, dim3((unsigned)((waves + 3) / 4), col_blocks), dim3(256), 0, s, target, V, D,
                      rows, occ, bag_of, psw, dout, N);
   return hipGetLastError();
 }

@@ -233,7 +233,7 @@ __global__ void embedding_bag_fwd(const float* __restrict__ W, int64_t V, int D,
     }
     return;
   }
-  for (int d0 = 0; d0 < D; d0 += 64) {
+  for (int d0 = blockIdx.y * 64; d0 < D; d0 += 64 * gridDim.y) {   // wide rows: one 64-column slice per blockIdx.y
     const int d = d0 + lane;
     float acc = 0.f, ws = 0.f;
     for (int64_t j = s; j < e; ++j) {
@@ -529,7 +529,8 @@ hipError_t dtfk_sigmoid_xent(const float* x, const float* t, float* loss, float*
 }
 hipError_t dtfk_embedding_bag_fwd(const float* W, int64_t V, int D, const int64_t* ids, const int64_t* offsets,
                                   const float* psw, int B, int mode, float* out, int64_t* bad, hipStream_t s) {
-  hipLaunchKernelGGL(embedding_bag_fwd, dim3((B + 3) / 4), dim3(256), 0, s, W, V, D, ids, offsets, psw, B,
+  hipLaunchKernelGGL(embedding_bag_fwd, dim3((B + 3) / 4, D < 64 ? 1 : (D + 63) / 64), dim3(256), 0, s, W, V, D,
+                     ids, offsets, psw, B,
                      mode, out, bad);
   return hipGetLastError();
 }

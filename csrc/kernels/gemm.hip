@@ -9,9 +9,11 @@
 // each wave 32x32 = 2x2 MFMA 16x16x32 bf16 tiles, K-step 32.  Operands are
 // read in any of fp32 / bf16 with any transpose, converted to bf16 and staged
 // in LDS as [row][k] (A) and [col][k] (B) with a +8 element pad so every MFMA
-// fragment is one conflict-free 16-byte ds_read.  Global loads are branch-free
-// (clamped addresses + masks; see mlp_step.hip for why) and the next K-tile is
-// prefetched into registers while the current one is multiplied.  Block ids
+// fragment is one conflict-free 16-byte ds_read.  Interior runs of 8 elements
+// are one (bf16) or two (fp32) 16-byte loads; edge runs fall back to clamped,
+// masked scalar loads with no per-element branch (see mlp_step.hip for why),
+// and the next K-tile is prefetched into registers while the current one is
+// multiplied.  Block ids
 // are remapped so consecutive tiles of one output row band land on one XCD
 // (shared A panel in that XCD's L2).
 #include "common.h"
@@ -47,6 +49,34 @@ template <bool BF16, bool KCONT>
 __device__ __forceinline__ void load_tile(const void* base, int ld, int R, int K, int r0, int k0,
                                           float v[8]) {
   const int t = threadIdx.x;
+  {
+    // interior fast path: the thread's 8 elements are contiguous in memory
+    // (along k when KCONT, along r otherwise) -> one 16-byte (bf16) or two
+    // 16-byte (fp32) loads instead of 8 clamped scalar loads
+    int outer, inner;
+    bool full;
+    if constexpr (KCONT) {
+      outer = r0 + (t >> 2); inner = k0 + (t & 3) * 8;
+      full = outer < R && inner + 8 <= K;
+    } else {
+      outer = k0 + (t >> 3); inner = r0 + (t & 7) * 8;
+      full = outer < K && inner + 8 <= R;
+    }
+    const size_t off = (size_t)outer * ld + inner;
+    if (full && ((reinterpret_cast<uintptr_t>(base) + off * (BF16 ? 2 : 4)) & 15) == 0) {
+      if constexpr (BF16) {
+        const uint4 u = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(base) + off);
+        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { v[2 * j] = bf2f(w[j] & 0xFFFF); v[2 * j + 1] = bf2f(w[j] >> 16); }
+      } else {
+        const float4 a = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(base) + off);
+        const float4 b = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(base) + off + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+      }
+      return;
+    }
+  }
   if constexpr (KCONT) {
     const int r = t >> 2, kk = (t & 3) * 8;  // 8 consecutive k of row r
     const int rr = min(r0 + r, R - 1);

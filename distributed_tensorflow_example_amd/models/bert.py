@@ -63,23 +63,30 @@ class _ShadowLinear(torch.autograd.Function):
     directly (hipBLASLt out_dtype), straight into the DDP bucket."""
 
     @staticmethod
-    def forward(ctx, x, w, w16):
+    def forward(ctx, x, w, w16, slot=None):
         ctx.save_for_backward(x, w16)
         ctx.w = w
+        ctx.slot = slot
         return F.linear(x, w16)
 
     @staticmethod
     def backward(ctx, gy):
         x, w16 = ctx.saved_tensors
         gy = gy.to(w16.dtype)
-        gx = gy @ w16
         gy2, x2 = gy.reshape(-1, gy.shape[-1]), x.reshape(-1, x.shape[-1])
+        extra = ctx.slot.take() if ctx.slot is not None else None
+        if extra is not None:   # residual-branch gradient of x folded in as the GEMM's beta = 1 term
+            # in place: ds is a fresh buffer nobody else reads, and addmm_ on it
+            # is one GEMM with beta = 1 (an out-of-place addmm would copy it first)
+            gx = extra.reshape(-1, x.shape[-1]).addmm_(gy2, w16).view(x.shape)
+        else:
+            gx = gy @ w16
         w = ctx.w
         if grad_sink.enabled(w) and (w.grad is None or w.grad.is_contiguous()):
             _wgrad(gy2, x2, into=grad_sink.target(w))
             grad_sink.done(w)
-            return gx, None, None
-        return gx, _wgrad(gy2, x2), None
+            return gx, None, None, None
+        return gx, _wgrad(gy2, x2), None, None
 
 
 def _wgrad_split(T: int, out: int, inp: int) -> int:
@@ -115,12 +122,19 @@ def _wgrad(gy2, x2, into=None):
     return res
 
 
-def _mm(x, w):
-    """x [.., in] @ w[out, in]^T in the activation dtype (bf16 on GPU)."""
+def _mm(x, w, slot=None):
+    """x [.., in] @ w[out, in]^T in the activation dtype (bf16 on GPU).  `slot`
+    (a GradSlot shared with the LN epilogue that also reads x) is only handed
+    out when this GEMM takes the shadow path, whose backward consumes it."""
     w16 = getattr(w, "_shadow", None)
     if w16 is not None and x.is_cuda and x.dtype == w16.dtype:
-        return _ShadowLinear.apply(x, w, w16)
+        return _ShadowLinear.apply(x, w, w16, slot)
     return F.linear(x, w.to(x.dtype))
+
+
+def _slot_for(x, w):
+    w16 = getattr(w, "_shadow", None)
+    return T.GradSlot() if (w16 is not None and x.is_cuda and x.dtype == w16.dtype) else None
 
 
 def _lookup(table, ids):
@@ -155,12 +169,13 @@ class BertLayer(torch.nn.Module):
         c = self.c
         B, S, H = x.shape
         nh, d = c.heads, H // c.heads
+        slot_x = _slot_for(x, self.w_qkv)      # LN1's residual grad of x -> QKV GEMM's dX
         if x.is_cuda and c.fused_attention and T.attention_supported(S, d):
             # q/k/v read in place from the packed projection, bias fused (attention.hip)
-            ctx = T.fused_attention(_mm(x, self.w_qkv), self.b_qkv, mask, nh, 1.0 / math.sqrt(d),
+            ctx = T.fused_attention(_mm(x, self.w_qkv, slot_x), self.b_qkv, mask, nh, 1.0 / math.sqrt(d),
                                     c.attn_dropout, self.training)
         else:
-            qkv = (_mm(x, self.w_qkv) + self.b_qkv.to(x.dtype)).view(B, S, 3, nh, d)
+            qkv = (_mm(x, self.w_qkv, slot_x) + self.b_qkv.to(x.dtype)).view(B, S, 3, nh, d)
             q = qkv[:, :, 0].permute(0, 2, 1, 3)
             k = qkv[:, :, 1].permute(0, 2, 3, 1)
             v = qkv[:, :, 2].permute(0, 2, 1, 3)
@@ -168,10 +183,11 @@ class BertLayer(torch.nn.Module):
             probs = T.attention_softmax(scores, mask, 1.0 / math.sqrt(d), c.attn_dropout, self.training)
             ctx = torch.matmul(probs.to(v.dtype), v).permute(0, 2, 1, 3).reshape(B, S, H)
         a = T.bias_dropout_residual_layernorm(_mm(ctx, self.w_o), self.b_o, x, self.ln1_g, self.ln1_b,
-                                              c.dropout, c.ln_eps, self.training)
-        hmid = T.bias_gelu(_mm(a, self.w_1), self.b_1)
+                                              c.dropout, c.ln_eps, self.training, residual_slot=slot_x)
+        slot_a = _slot_for(a, self.w_1)        # LN2's residual grad of a -> W1 GEMM's dX
+        hmid = T.bias_gelu(_mm(a, self.w_1, slot_a), self.b_1)
         out = T.bias_dropout_residual_layernorm(_mm(hmid, self.w_2), self.b_2, a, self.ln2_g, self.ln2_b,
-                                                c.dropout, c.ln_eps, self.training)
+                                                c.dropout, c.ln_eps, self.training, residual_slot=slot_a)
         return out
 
 

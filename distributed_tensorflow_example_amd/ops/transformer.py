@@ -44,9 +44,30 @@ def _ln_part(N: int, H: int, device) -> torch.Tensor:
 
 
 # ---------------------------------------------------------------- bias + dropout + residual + LN
+class GradSlot:
+    """Hands the residual-branch gradient of a post-LN epilogue to the GEMM
+    whose input is the same activation (BERT: a layer's input feeds both the
+    QKV projection and LN1's residual; LN1's output feeds both W1 and LN2's
+    residual).  The LN backward parks ds here instead of returning it, and the
+    GEMM backward folds it in as the beta = 1 term of its dX GEMM -- one fewer
+    full-activation bf16 add per residual per step.  The LN backward always
+    runs first (the GEMM's upstream gradient depends on it); if the GEMM's
+    backward somehow ran first (`consumed`), the LN returns ds normally."""
+
+    __slots__ = ("g", "consumed")
+
+    def __init__(self):
+        self.g = None
+        self.consumed = False
+
+    def take(self):
+        g, self.g, self.consumed = self.g, None, True
+        return g
+
+
 class _BDRLN(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, bias, res, gamma, beta, p, eps):
+    def forward(ctx, x, bias, res, gamma, beta, p, eps, slot=None):
         C = _C()
         H = x.shape[-1]
         x2 = x.reshape(-1, H).contiguous()
@@ -61,6 +82,7 @@ class _BDRLN(torch.autograd.Function):
         ctx.save_for_backward(s, mean, rstd, gamma)
         ctx.params = (gamma, beta, bias)   # for sinking dgamma/dbeta/dbias into .grad
         ctx.p, ctx.seed, ctx.has_res, ctx.shape = p, seed, res is not None, x.shape
+        ctx.slot = slot if res is not None else None
         return y.view(x.shape)
 
     @staticmethod
@@ -83,16 +105,20 @@ class _BDRLN(torch.autograd.Function):
         C.ln_bwd(dy2, s, mean, rstd, gamma, ds, dxb, _ln_part(N, H, dy.device), dgamma, dbeta, dbias, ctx.p, ctx.seed,
                  accumulate=sink)
         dres = ds.view(ctx.shape) if ctx.has_res else None
+        if dres is not None and ctx.slot is not None and not ctx.slot.consumed:
+            ctx.slot.g, dres = dres, None   # folded into the consuming GEMM's dX
         if sink:
             for q in (pg, pb, px):
                 grad_sink.done(q)
-            return dxb.view(ctx.shape), None, dres, None, None, None, None
-        return dxb.view(ctx.shape), dbias, dres, dgamma, dbeta, None, None
+            return dxb.view(ctx.shape), None, dres, None, None, None, None, None
+        return dxb.view(ctx.shape), dbias, dres, dgamma, dbeta, None, None, None
 
 
 def bias_dropout_residual_layernorm(x, bias, residual, gamma, beta, p: float = 0.0, eps: float = 1e-12,
-                                   training: bool = True):
-    """LayerNorm(dropout(x + bias) + residual) -- the post-sublayer epilogue."""
+                                   training: bool = True, residual_slot: "GradSlot" = None):
+    """LayerNorm(dropout(x + bias) + residual) -- the post-sublayer epilogue.
+
+    `residual_slot`: see GradSlot (GPU path, bf16 residual only)."""
     p = p if training else 0.0
     if not x.is_cuda:
         t = x.float() + bias
@@ -101,8 +127,10 @@ def bias_dropout_residual_layernorm(x, bias, residual, gamma, beta, p: float = 0
         if residual is not None:
             t = t + residual.float()
         return torch.nn.functional.layer_norm(t, (t.shape[-1],), gamma, beta, eps)
+    if residual is not None and residual.dtype != torch.bfloat16:
+        residual_slot = None      # the cast node, not the GEMM input, would receive the gradient
     return _BDRLN.apply(x.to(torch.bfloat16), bias, None if residual is None else residual.to(torch.bfloat16),
-                        gamma, beta, float(p), float(eps))
+                        gamma, beta, float(p), float(eps), residual_slot)
 
 
 class _EmbLN(torch.autograd.Function):

@@ -172,6 +172,32 @@ def test_bert_bf16_shadow_weights_match_casts(native):
         assert torch.equal(w._shadow, w.detach().bfloat16())
 
 
+def test_bert_residual_grad_slot_matches_autograd_add(native):
+    """Shadow-weight BERT folds LN residual gradients into the dX GEMMs
+    (GradSlot); one backward must give the same gradients as the plain model,
+    whose residual gradients meet in autograd's add."""
+    from distributed_tensorflow_example_amd.models.bert import BertConfig, BertForMLM, synthetic_mlm_batch
+    from distributed_tensorflow_example_amd.ops import transformer as T
+
+    c = BertConfig.tiny()
+    c.dropout = c.attn_dropout = 0.0
+    b = [t.cuda() for t in synthetic_mlm_batch(8, 128, c.vocab_size, "cpu", seed=4)]
+    plain, shad = BertForMLM(c, seed=6).cuda(), BertForMLM(c, seed=6).cuda()
+    shad.attach_shadows()
+    taken = []
+    orig = T.GradSlot.take
+    T.GradSlot.take = lambda self: taken.append(self.g is not None) or orig(self)
+    try:
+        plain(*b).backward()
+        shad(*b).backward()
+    finally:
+        T.GradSlot.take = orig
+    assert taken and all(taken), taken          # every slot was filled by its LN before the GEMM ran
+    for (n, p1), p2 in zip(plain.named_parameters(), shad.parameters()):
+        if p1.grad is not None and p1.grad.norm() > 1e-6:
+            assert rel(p2.grad, p1.grad) < 2e-2, n
+
+
 def _unfused_attention(qkv, bias, mask, nh, scale, p):
     """The model's pre-fusion GPU path: bias add, batched GEMMs, softmax kernel."""
     from distributed_tensorflow_example_amd.ops import transformer as T

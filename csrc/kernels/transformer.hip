@@ -379,10 +379,19 @@ __global__ __launch_bounds__(1024) void colsum_partials(ColsumArgs a, int P, int
   float* __restrict__ out = a.out[blockIdx.y];
   const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
-  float s = 0.f;
-  if (c < H)
-    for (int p = g; p < P; p += 16) s += part[(size_t)p * H + c];
-  red[g][lane] = s;
+  // 4 independent accumulators: 4 loads in flight per thread (the partial
+  // buffers have up to 1024 rows, and this grid is only H/64 blocks wide);
+  // the summation order is still fixed, so the result stays deterministic
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  if (c < H) {
+    int p = g;
+    for (; p + 48 < P; p += 64) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s[u] += part[(size_t)(p + 16 * u) * H + c];
+    }
+    for (; p < P; p += 16) s[0] += part[(size_t)p * H + c];
+  }
+  red[g][lane] = (s[0] + s[1]) + (s[2] + s[3]);
   __syncthreads();
   if (g == 0 && c < H) {
     float t = 0.f;

@@ -29,6 +29,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--same-gpu", action="store_true")
+    ap.add_argument("--ipc-timeout", type=float, default=30.0,
+                    help="in-kernel wait bound per exchange (s); ranks sharing one GPU are time-sliced")
     ap.add_argument("--graph", action="store_true", help="also replay the steps from a captured hipGraph")
     a = ap.parse_args()
     rank, ws = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
@@ -40,11 +42,15 @@ def main():
     dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=ws,
                             timeout=datetime.timedelta(seconds=120))
     w = World(rank=rank, world_size=ws, local_rank=rank, device=dev, backend="gloo", pg_initialized=True)
-    tr = mlp.FusedMLPTrainer(batch_size=100, lr=0.05, world=w, device=dev, allreduce=os.environ.get("DTF_IPC_MODE", "ipc-fused"), ipc_timeout_s=5.0)
+    tr = mlp.FusedMLPTrainer(batch_size=100, lr=0.05, world=w, device=dev, allreduce=os.environ.get("DTF_IPC_MODE", "ipc-fused"), ipc_timeout_s=a.ipc_timeout)
     g = torch.Generator().manual_seed(7)
     xs = torch.randint(0, 256, (a.steps, ws, 100, 784), generator=g, dtype=torch.uint8)
     ys = torch.randint(0, 10, (a.steps, ws, 100), generator=g)
     ref = mlp.init_params(1).clone()
+    # start the first exchange together: a rank still paging in torch/HIP on a
+    # cold box must not eat the peers' in-kernel wait budget
+    torch.cuda.synchronize()
+    dist.barrier()
     for s in range(a.steps):
         tr.step_tensors(xs[s, rank].to(dev), ys[s, rank].to(dev))
         # reference: mean over ranks of per-rank mean gradients == one 200-row batch

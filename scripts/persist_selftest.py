@@ -47,8 +47,11 @@ def main():
     xs = torch.randint(0, 256, (a.steps, ws, B, 784), generator=g, dtype=torch.uint8)
     ys = torch.randint(0, 10, (a.steps, ws, B), generator=g).to(torch.uint8)
     ep = PinnedEpoch(xs[:, rank].reshape(-1, 784).numpy(), ys[:, rank].reshape(-1).numpy(), B)
-    run = mlp.PersistentMLPRunner(tr, ep, steps_per_launch=a.per_launch, timeout_s=5.0)
+    run = mlp.PersistentMLPRunner(tr, ep, steps_per_launch=a.per_launch, timeout_s=30.0)
     p0 = mlp.init_params(1).double()
+    # all ranks enter the persistent launch together (cold-box import skew)
+    torch.cuda.synchronize()
+    dist.barrier()
     run.run(a.steps)
     torch.cuda.synchronize()
     ref = mlp.init_params(1).clone()

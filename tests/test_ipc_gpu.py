@@ -31,6 +31,6 @@ def test_ipc_allreduce_same_gpu(native, nproc, mode):
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
     out = r.stdout + r.stderr
     line = [l for l in r.stdout.splitlines() if l.startswith("{")]
-    assert r.returncode == 0 and line, out[-3000:]
+    assert r.returncode == 0 and line, "\n".join(line) + "\n" + out[:1500] + "\n...\n" + out[-1500:]
     res = json.loads(line[-1])
     assert res["ipc_selftest"] == "pass", res

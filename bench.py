@@ -3,16 +3,25 @@
 
 Metric/config from BASELINE.json: "samples/sec (whole node) MNIST MLP sync-SGD
 at 1/2/4/8 MI355X; step-time p50".  Per-GPU batch 100 (example.py:43),
-lr 0.0005, sigmoid hidden layer, softmax cross-entropy, plain SGD; bf16 MFMA
-compute with fp32 master weights; gradients all-reduced in bf16 (BASELINE
-config #2): by default a one-shot all-reduce over IPC-mapped xGMI peer
-buffers fused into the SGD apply kernel (validated against replica drift
-after warmup, falling back to RCCL), or RCCL (--allreduce rccl).  Synthetic MNIST-shaped data (uint8 pixels resident in
-pinned host memory, streamed to a device stage one 50-step chunk at a time by
-hipMemcpyAsync inside the chunk's hipGraph; --prefetch side double-buffers it
-on a side stream instead), random-init weights.  Weak scaling: per-GPU batch
-fixed as N grows.  Every timed step runs the full fwd + bwd + (all-reduce) +
-SGD update; nothing is skipped or cached.
+lr 0.0005, sigmoid hidden layer, softmax cross-entropy, plain SGD.
+
+Default engine: the persistent fp32 kernel (csrc/kernels/mlp_persist_f32.hip)
+-- the reference's precision (example.py:77-118 is fp32 end to end): exact
+f32-input MFMA, fp32 accumulate, fp32 master weights.  `--precision fp16`
+selects the f16-MFMA persistent kernel (labelled as such in the output line).
+N GPUs: gradients exchanged inside the persistent launch over IPC-mapped xGMI
+peer buffers (bf16 payload per BASELINE config #2, `--grad-dtype fp32` for
+fp32), falling back to 3 fused launches per step with an IPC or RCCL
+all-reduce if the in-kernel exchange fails validation.
+
+Synthetic MNIST-shaped data: uint8 pixels resident in pinned host memory,
+streamed to the device by copier workgroups inside each launch (the chunk the
+timed run starts with is staged by the warmup's last launch, and the timed run
+streams the chunk after it); random-init weights.  Weak scaling: per-GPU batch
+fixed as N grows.  Every timed step runs the full fwd + bwd + (exchange) + SGD
+update; nothing is skipped or cached.  step_time_p50/p90 come from per-step
+device timestamps (s_memrealtime at every step start) on the persistent
+engines.
 
     python bench.py --gpus N --steps K --warmup W
     (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
@@ -50,6 +59,10 @@ def main(argv=None):
     ap.add_argument("--batch", type=int, default=100, help="per-GPU batch (reference: 100)")
     ap.add_argument("--lr", type=float, default=0.0005)
     ap.add_argument("--steps-per-graph", type=int, default=50, help="3-launch path: steps per captured hipGraph")
+    ap.add_argument("--precision", choices=["fp32", "fp16"], default="fp32",
+                    help="persistent engine operand precision (reference: fp32)")
+    ap.add_argument("--exchange-timeout", type=float, default=30.0,
+                    help="in-kernel exchange wait bound (s); a cold multi-GPU start can skew ranks by seconds")
     ap.add_argument("--steps-per-launch", type=int, default=550,
                     help="persistent engine: steps per launch (<= one epoch of batches; the next chunk is copied "
                          "from pinned host memory inside the launch)")
@@ -101,10 +114,17 @@ def main(argv=None):
         """mode: 'persistent' (one launch per chunk, in-kernel N-GPU exchange) or the
         3-launch path's gradient exchange ('ipc-fused' / 'ipc-apply' / 'rccl')."""
         trainer = FusedMLPTrainer(batch_size=a.batch, lr=a.lr, act=a.act, world=w, grad_dtype=gd,
-                                  device=dev, allreduce="rccl" if mode == "persistent" else mode)
+                                  device=dev, allreduce="rccl" if mode == "persistent" else mode,
+                                  ipc_timeout_s=a.exchange_timeout)
         if mode == "persistent":
-            runner = PersistentMLPRunner(trainer, epoch, steps_per_launch=a.steps_per_launch)
-            runner.run(a.warmup)
+            runner = PersistentMLPRunner(trainer, epoch, steps_per_launch=a.steps_per_launch,
+                                         timeout_s=a.exchange_timeout, precision=a.precision,
+                                         grad_bf16=a.grad_dtype == "bf16")
+            runner.prepare(max(a.warmup, 1))
+            torch.cuda.synchronize()
+            w.barrier()   # every rank's buffers mapped and first chunk staged before any exchange
+            # the warmup's last launch stages exactly the chunk the timed run starts with
+            runner.run(a.warmup, lookahead=a.steps)
             torch.cuda.synchronize()
             return trainer, runner
         runner = MLPStepRunner(trainer, epoch, steps_per_graph=a.steps_per_graph,
@@ -145,17 +165,20 @@ def main(argv=None):
     # reads vs the 3-launch path's exchange spread over 347 workgroups depends on
     # the xGMI fabric, so it is measured, not assumed.
     picked = []
+    fallbacks = {}
     for i, mode in enumerate(chain):
         try:   # setup failures (IPC mapping, ...) are agreed on collectively, so every rank skips together
             trainer, runner = setup(mode)
         except RuntimeError as e:
             print(f"bench: {mode} unavailable ({e})", file=sys.stderr, flush=True)
+            fallbacks[mode] = f"unavailable: {str(e)[:160]}"
             continue
         if consistent(trainer, runner):
             picked.append((mode, trainer, runner))
             if w.world_size == 1 or len(picked) == 2 or a.tune_steps <= 0:
                 break
             continue
+        fallbacks[mode] = "failed validation (exchange timeout or replica drift after warmup)"
         print(f"bench: {mode} failed validation" + (f"; trying {chain[i + 1]}" if i + 1 < len(chain) else ""),
               file=sys.stderr, flush=True)
     if not picked:
@@ -179,10 +202,11 @@ def main(argv=None):
         if tuned[picked[0][0]] is None:
             raise SystemExit("every exchange strategy failed validation during tuning")
     mode, trainer, runner = picked[0]
-    runner.prepare(a.steps)   # graphs for the timed plan (the tuning moved the cursor)
+    runner.prepare(a.steps)   # graphs / first staged chunk for the timed plan (the tuning moved the cursor)
     torch.cuda.synchronize()
     persistent = isinstance(runner, PersistentMLPRunner)
     step0 = trainer.global_step
+    cold0 = runner.copy_only_launches if persistent else 0
 
     events = []
     w.barrier()
@@ -197,14 +221,24 @@ def main(argv=None):
     elapsed = t1 - t0
     elapsed_max = w.host_all_reduce(elapsed, "max")
 
-    # step-time p50 from per-graph-replay GPU intervals
-    per_step_ms = []
-    prev = ev0
-    for ev, g in events:
-        per_step_ms.append(prev.elapsed_time(ev) / g)
-        prev = ev
-    p50 = statistics.median(per_step_ms) if per_step_ms else float("nan")
+    if persistent:
+        # true per-step times: device stamps at every step start (100 MHz s_memrealtime)
+        per_step_ms = list(runner.step_times_ms(step0, step0 + a.steps))
+        p50_source = "per-step device timestamps (s_memrealtime at every step start)"
+    else:
+        # 3-launch path: average per step of each graph replay
+        per_step_ms = []
+        prev = ev0
+        for ev, g in events:
+            per_step_ms.append(prev.elapsed_time(ev) / g)
+            prev = ev
+        p50_source = "per-graph-replay average"
+    srt = sorted(per_step_ms)
+    p50 = statistics.median(srt) if srt else float("nan")
+    p90 = srt[min(len(srt) - 1, int(0.9 * len(srt)))] if srt else float("nan")
     p50 = w.host_all_reduce(p50, "max")
+    p90 = w.host_all_reduce(p90, "max")
+    cold_timed = (runner.copy_only_launches - cold0) if persistent else 0
 
     if not consistent(trainer, runner):
         raise SystemExit("replicas diverged / IPC timeout during the timed run; result discarded")
@@ -222,10 +256,12 @@ def main(argv=None):
             "warmup": a.warmup,
             "ms_per_step": round(elapsed_max * 1000.0 / a.steps, 5),
             "step_time_p50_ms": round(p50, 5),
+            "step_time_p90_ms": round(p90, 5),
+            "p50_source": p50_source,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp16" if persistent else "bf16",
+            "dtype": (a.precision if persistent else "bf16"),
             "data": ("synthetic MNIST-shaped uint8 resident in pinned host memory, streamed per chunk over PCIe "
                      + ("by copier workgroups inside the persistent launch" if persistent else
                         "by hipMemcpyAsync inside the chunk's hipGraph") + "; random-init weights"),
@@ -236,17 +272,21 @@ def main(argv=None):
                 "seq_len": None,
                 "parallelism": f"dp{n}",
                 "optimizer": f"sgd lr={a.lr}",
-                "grad_allreduce": ("none" if n == 1 else "bf16 in-kernel one-shot over IPC/xGMI" if persistent
-                                   else f"{a.grad_dtype} {trainer.allreduce}"),
-                "engine": "persistent" if persistent else "launches",
+                "grad_allreduce": ("none" if n == 1 else f"{a.grad_dtype} in-kernel one-shot over IPC/xGMI"
+                                   if persistent else f"{a.grad_dtype} {trainer.allreduce}"),
+                "engine": f"persistent-{a.precision}" if persistent else "launches",
+                "exchange_mode": mode,
+                "fallbacks": fallbacks or None,
+                "copy_only_launches_in_timed_run": cold_timed,
                 "steps_per_launch": runner.g if persistent else 1,
                 "hipgraph_steps": 0 if (a.eager or persistent) else a.steps_per_graph,
                 "input_prefetch": "in-kernel copier workgroups" if persistent else a.prefetch,
                 "activation": a.act,
                 "exchange_tuning_us_per_step": tuned or None,
-                "precision": ("fp16 MFMA operands (pixels exact as 1024+u, 10-bit mantissa >= bf16's 7), fp32 "
-                              "accumulate, fp32 master weights" if persistent else
-                              "bf16 MFMA operands, fp32 accumulate, fp32 master weights"),
+                "precision": (("fp32 MFMA operands (v_mfma_f32_16x16x4_f32, exact f32 products), fp32 accumulate, "
+                               "fp32 master weights" if a.precision == "fp32" else
+                               "fp16 MFMA operands (pixels exact as 1024+u), fp32 accumulate, fp32 master weights")
+                              if persistent else "bf16 MFMA operands, fp32 accumulate, fp32 master weights"),
             },
             "final_loss": round(float(m[0]), 5),
             "final_batch_acc": round(float(m[1]), 4),

@@ -38,7 +38,17 @@ hipError_t dtfk_mlp_persist(const void* xs, const void* xts, long long rec, long
                             const float* lr, float* metrics, int ring, int act, int naive, long long* gstep,
                             unsigned long long* seq, unsigned long long* gran, int* err, long long timeout,
                             const void* host_next, int next_steps, void* xs_next, void* xts_next,
-                            long long* ts, void* const* peer_base, int W, int rank, hipStream_t stream);
+                            long long* ts, void* const* peer_base, int W, int rank, long long* step_ts,
+                            int ts_ring, hipStream_t stream);
+long long dtfk_mlpf_stage_rec();
+long long dtfk_mlpf_xbuf_bytes();
+long long dtfk_mlpf_ipc_bytes();
+int dtfk_mlpf_max_batch();
+hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int nsteps, float* params, const float* lr,
+                                float* metrics, int ring, int act, int naive, long long* gstep, unsigned long long* seq,
+                                void* xbuf, int* err, long long timeout, long long* step_ts, int ts_ring,
+                                const void* host_next, int next_steps, void* stage_next, void* const* peer_base, int W,
+                                int rank, int gbf16, hipStream_t stream);
 hipError_t dtfk_mlp_fwd_head(const void* x, int x_kind, int B, const void* W1T, float* z2p, const void* labels,
                              const void* W2T, const void* W2N, const float* params, void* dz2T, int BP,
                              float* partials, float inv_batch, int act, int naive_loss, int* counters,
@@ -68,6 +78,32 @@ static long long* ts_ptr(const c10::optional<at::Tensor>& ts, int64_t need_numel
   if (!ts.has_value()) return nullptr;
   need(*ts, at::kLong, need_numel, "ts");
   return reinterpret_cast<long long*>(ts->data_ptr<int64_t>());
+}
+
+// optional per-step s_memrealtime ring (int64)
+static long long* step_ts_ptr(const c10::optional<at::Tensor>& t, int* ring) {
+  *ring = 1;
+  if (!t.has_value()) return nullptr;
+  need(*t, at::kLong, 2, "step_ts");
+  *ring = (int)t->numel();
+  return reinterpret_cast<long long*>(t->data_ptr<int64_t>());
+}
+
+// device-visible address of `nbytes` of pinned host memory at `off`
+static const void* pinned_device_ptr(const c10::optional<at::Tensor>& host, int64_t off, int64_t nbytes) {
+  if (!host.has_value()) throw std::runtime_error("next chunk needs the pinned host epoch");
+  const at::Tensor& h = *host;
+  if (h.is_cuda() || !h.is_pinned()) throw std::runtime_error("host must be pinned host memory");
+  if (off < 0 || off % 16 != 0 || off + nbytes > (int64_t)(h.numel() * h.element_size()))
+    throw std::runtime_error("host range out of bounds");
+  void* dp = nullptr;
+  char* hp = reinterpret_cast<char*>(h.data_ptr()) + off;
+  if (hipHostGetDevicePointer(&dp, hp, 0) != hipSuccess || dp == nullptr) {
+    (void)hipGetLastError();
+    dp = hp;   // unified addressing: the host address is device-visible
+  }
+  if (reinterpret_cast<uintptr_t>(dp) % 16 != 0) throw std::runtime_error("pinned host pointer not aligned");
+  return dp;
 }
 
 static int bp_of(int B) { return ((B + 31) / 32) * 32; }
@@ -254,7 +290,8 @@ void mlp_persist(at::Tensor xs, at::Tensor xts, int64_t rec, int B, int nsteps, 
                  at::Tensor metrics, at::Tensor gstep, at::Tensor seq, at::Tensor gran, at::Tensor err,
                  double timeout_s, int act, int naive, c10::optional<at::Tensor> host, int64_t host_off,
                  int next_steps, c10::optional<at::Tensor> xs_next, c10::optional<at::Tensor> xts_next,
-                 c10::optional<at::Tensor> ts, int64_t ipc_table, int ipc_W, int ipc_rank) {
+                 c10::optional<at::Tensor> ts, int64_t ipc_table, int ipc_W, int ipc_rank,
+                 c10::optional<at::Tensor> step_ts) {
   if (ipc_W > 1 && (ipc_table == 0 || ipc_rank < 0 || ipc_rank >= ipc_W))
     throw std::runtime_error("mlp_persist: N-GPU exchange needs the IPC peer table");
   if (B <= 0 || B > dtfk_mlp_persist_max_batch()) throw std::runtime_error("mlp_persist: B out of range");
@@ -298,6 +335,8 @@ void mlp_persist(at::Tensor xs, at::Tensor xts, int64_t rec, int B, int nsteps, 
     xtn = xts_next->data_ptr();
   }
   const long long ticks = (long long)(timeout_s * 1e8);   // s_memrealtime: 100 MHz
+  int ts_ring = 1;
+  long long* sts = step_ts_ptr(step_ts, &ts_ring);
   hip_check(dtfk_mlp_persist(xs.data_ptr(), xts.data_ptr(), rec_s, rec_h, B, nsteps, params.data_ptr<float>(),
                              lr.data_ptr<float>(), metrics.data_ptr<float>(), (int)(metrics.numel() / 2), act, naive,
                              reinterpret_cast<long long*>(gstep.data_ptr<int64_t>()),
@@ -305,8 +344,57 @@ void mlp_persist(at::Tensor xs, at::Tensor xts, int64_t rec, int B, int nsteps, 
                              reinterpret_cast<unsigned long long*>(gran.data_ptr<int64_t>()), err.data_ptr<int>(),
                              ticks, hn, next_steps, xn, xtn, ts_ptr(ts, 64 * 8 * 16 + 2 * 64),
                              reinterpret_cast<void* const*>(ipc_table), ipc_W > 1 ? ipc_W : 1, ipc_W > 1 ? ipc_rank : 0,
-                             cur_stream()),
+                             sts, ts_ring, cur_stream()),
             "mlp_persist");
+}
+
+// fp32 persistent engine (csrc/kernels/mlp_persist_f32.hip): `nsteps` SGD steps of
+// the chunk staged in `stage` (records of mlpf_stage_rec() bytes) and, in the same
+// launch, `next_steps` host records from byte `host_off` of the pinned epoch into
+// `stage_next`.  nsteps = 0: copy only.  xbuf: exchange buffer (zeroed once).
+void mlp_persist_f32(at::Tensor stage, int64_t rec_h, int B, int nsteps, at::Tensor params, at::Tensor lr,
+                     at::Tensor metrics, at::Tensor gstep, at::Tensor seq, at::Tensor xbuf, at::Tensor err,
+                     double timeout_s, int act, int naive, c10::optional<at::Tensor> host, int64_t host_off,
+                     int next_steps, c10::optional<at::Tensor> stage_next, c10::optional<at::Tensor> step_ts,
+                     int64_t ipc_table, int ipc_W, int ipc_rank, bool grad_bf16) {
+  if (ipc_W > 1 && (ipc_table == 0 || ipc_rank < 0 || ipc_rank >= ipc_W || ipc_W > 64))
+    throw std::runtime_error("mlp_persist_f32: N-GPU exchange needs the IPC peer table");
+  if (B <= 0 || B > dtfk_mlpf_max_batch()) throw std::runtime_error("mlp_persist_f32: B out of range");
+  if (rec_h < (int64_t)B * 785 || rec_h % 16 != 0) throw std::runtime_error("mlp_persist_f32: bad host record size");
+  if (nsteps < 0 || next_steps < 0) throw std::runtime_error("mlp_persist_f32: negative step count");
+  const int64_t rec_s = dtfk_mlpf_stage_rec();
+  need(stage, at::kByte, (int64_t)std::max(nsteps, 1) * rec_s, "stage");
+  need(params, at::kFloat, kNParam, "params");
+  need(lr, at::kFloat, 1, "lr");
+  need(metrics, at::kFloat, 2, "metrics");
+  need(gstep, at::kLong, 1, "gstep");
+  need(seq, at::kLong, 1, "seq");
+  need(xbuf, at::kByte, dtfk_mlpf_xbuf_bytes(), "xbuf");
+  need(err, at::kInt, 1, "err");
+  if (((uintptr_t)stage.data_ptr() | (uintptr_t)xbuf.data_ptr()) % 16 != 0)
+    throw std::runtime_error("mlp_persist_f32: stage / xbuf must be 16-byte aligned");
+  const void* hn = nullptr;
+  void* sn = nullptr;
+  if (next_steps > 0) {
+    if (!stage_next.has_value()) throw std::runtime_error("mlp_persist_f32: next chunk needs stage_next");
+    need(*stage_next, at::kByte, (int64_t)next_steps * rec_s, "stage_next");
+    if ((uintptr_t)stage_next->data_ptr() % 16 != 0) throw std::runtime_error("stage_next must be 16-byte aligned");
+    if (stage_next->data_ptr() == stage.data_ptr() && nsteps > 0)
+      throw std::runtime_error("mlp_persist_f32: stage_next must not alias the running stage");
+    hn = pinned_device_ptr(host, host_off, (int64_t)next_steps * rec_h);
+    sn = stage_next->data_ptr();
+  }
+  int ts_ring = 1;
+  long long* sts = step_ts_ptr(step_ts, &ts_ring);
+  const long long ticks = (long long)(timeout_s * 1e8);   // s_memrealtime: 100 MHz
+  hip_check(dtfk_mlp_persist_f32(stage.data_ptr(), rec_h, B, nsteps, params.data_ptr<float>(), lr.data_ptr<float>(),
+                                 metrics.data_ptr<float>(), (int)(metrics.numel() / 2), act, naive,
+                                 reinterpret_cast<long long*>(gstep.data_ptr<int64_t>()),
+                                 reinterpret_cast<unsigned long long*>(seq.data_ptr<int64_t>()), xbuf.data_ptr(),
+                                 err.data_ptr<int>(), ticks, sts, ts_ring, hn, next_steps, sn,
+                                 reinterpret_cast<void* const*>(ipc_table), ipc_W > 1 ? ipc_W : 1,
+                                 ipc_W > 1 ? ipc_rank : 0, grad_bf16 ? 1 : 0, cur_stream()),
+            "mlp_persist_f32");
 }
 
 void init_mlp(py::module& m) {
@@ -315,7 +403,17 @@ void init_mlp(py::module& m) {
         py::arg("gran"), py::arg("err"), py::arg("timeout_s"), py::arg("act"), py::arg("naive"),
         py::arg("host") = py::none(), py::arg("host_offset") = 0, py::arg("next_steps") = 0,
         py::arg("xs_next") = py::none(), py::arg("xts_next") = py::none(), py::arg("ts") = py::none(),
-        py::arg("ipc_table") = 0, py::arg("ipc_W") = 1, py::arg("ipc_rank") = 0);
+        py::arg("ipc_table") = 0, py::arg("ipc_W") = 1, py::arg("ipc_rank") = 0, py::arg("step_ts") = py::none());
+  m.def("mlp_persist_f32", &mlp_persist_f32, py::arg("stage"), py::arg("rec_h"), py::arg("B"), py::arg("nsteps"),
+        py::arg("params"), py::arg("lr"), py::arg("metrics"), py::arg("gstep"), py::arg("seq"), py::arg("xbuf"),
+        py::arg("err"), py::arg("timeout_s"), py::arg("act"), py::arg("naive"), py::arg("host") = py::none(),
+        py::arg("host_offset") = 0, py::arg("next_steps") = 0, py::arg("stage_next") = py::none(),
+        py::arg("step_ts") = py::none(), py::arg("ipc_table") = 0, py::arg("ipc_W") = 1, py::arg("ipc_rank") = 0,
+        py::arg("grad_bf16") = true);
+  m.def("mlpf_stage_rec", &dtfk_mlpf_stage_rec);
+  m.def("mlpf_xbuf_bytes", &dtfk_mlpf_xbuf_bytes);
+  m.def("mlpf_ipc_bytes", &dtfk_mlpf_ipc_bytes);
+  m.def("mlpf_max_batch", &dtfk_mlpf_max_batch);
   m.def("mlp_persist_ipc_bytes", &dtfk_mlp_persist_ipc_bytes);
   m.def("mlp_persist_xt_bytes", &dtfk_mlp_persist_xt_bytes);
   m.def("mlp_persist_gran_count", &dtfk_mlp_persist_gran_count);

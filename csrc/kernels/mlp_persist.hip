@@ -99,6 +99,8 @@ struct Args {
   // N GPUs: IPC-mapped uncached exchange buffers of every rank (W = 1: none)
   void* const* peer_base;
   int W, rank;
+  long long* step_ts;       // optional: s_memrealtime at the start of every global step (ring)
+  int ts_ring;
 };
 
 // IPC exchange buffer of one rank: [flags: block j at byte 64j][2 parities][7 blocks][slot]
@@ -356,6 +358,8 @@ __device__ void compute(const Args& a, const int j, uint8_t* smem) {
   for (int st = 0; st < a.nsteps; ++st) {
     const unsigned long long sq = seq0 + (unsigned long long)st + 1ull;
     const unsigned tag = (unsigned)sq;
+    if (j == 0 && tid == 0 && a.step_ts != nullptr)
+      a.step_ts[(gstep0 + st) % a.ts_ring] = (long long)__builtin_amdgcn_s_memrealtime();
     if (w == 0) { TSP(0); }
 
     // ---------------- forward + head (wave w < 7: batch tile w)
@@ -699,6 +703,7 @@ __device__ void compute(const Args& a, const int j, uint8_t* smem) {
         }
       }
       lds_barrier();
+      asm volatile("" ::: "memory");   // no peer-slot load hoisted above the flag match
       if (*abort_flag) { aborted = true; break; }
       const float lrW = lr / (float)a.W;
       const size_t soff = IPC_FLAGS + (size_t)(par_of(st) * NWG + j) * IPC_SLOT;
@@ -791,6 +796,8 @@ __device__ void compute(const Args& a, const int j, uint8_t* smem) {
   } else if (tid == 300 && j == 0) {
     *a.gstep = gstep0 + a.nsteps;
     *a.seq = seq0 + (unsigned long long)a.nsteps;
+    if (a.step_ts != nullptr)
+      a.step_ts[(gstep0 + a.nsteps) % a.ts_ring] = (long long)__builtin_amdgcn_s_memrealtime();
   }
 }
 
@@ -826,8 +833,11 @@ hipError_t dtfk_mlp_persist(const void* xs, const void* xts, long long rec, long
                             const float* lr, float* metrics, int ring, int act, int naive, long long* gstep,
                             unsigned long long* seq, unsigned long long* gran, int* err, long long timeout,
                             const void* host_next, int next_steps, void* xs_next, void* xts_next,
-                            long long* ts, void* const* peer_base, int W, int rank, hipStream_t stream) {
+                            long long* ts, void* const* peer_base, int W, int rank, long long* step_ts,
+                            int ts_ring, hipStream_t stream) {
   Args a;
+  a.step_ts = step_ts;
+  a.ts_ring = ts_ring > 0 ? ts_ring : 1;
   a.ts = ts;
   a.peer_base = peer_base;
   a.W = W;

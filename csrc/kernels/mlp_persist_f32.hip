@@ -1,0 +1,684 @@
+// Persistent, weight-stationary training kernel for the reference's 784-100-10
+// MLP at the reference's precision: every product is an fp32 x fp32 MFMA
+// (v_mfma_f32_16x16x4_f32, bitwise an fmaf chain), fp32 accumulate, fp32
+// master weights held in VGPRs for the whole launch (example.py:77-118 is fp32
+// end to end: x*W1+b1 -> sigmoid -> *W2+b2 -> softmax cross-entropy -> SGD).
+//
+// The f32-input MFMA runs at 1/16 of the f16 rate, so where the f16 engine
+// (mlp_persist.hip) keeps a hidden block per CU, this one spreads each block's
+// weights over 7 CUs:
+//
+//  * 49 compute workgroups (512 threads) c = (j, q): hidden block j (units
+//    16j..16j+15, 7 blocks) x feature slice q (7 tiles of 16 features, 49 tiles
+//    = 784 exactly).  Wave t < 7 OWNS feature tile 7q+t of block j: 4 fp32 VGPRs
+//    per lane hold W1[16(7q+t)+4g+e][16j+r] (r = lane&15, g = lane>>4), which is
+//    at once its forward A operand (k-step e) and the C layout of its weight
+//    gradient, so the SGD update is in-register.
+//  * per step:
+//      P0  forward partial z^T[hidden][batch] of tile t for all 7 batch tiles
+//          (28 MFMAs, 7 independent chains) -> LDS; the 7 tiles are summed in a
+//          fixed order (wave w: batch tile w).
+//      E1  the slice partial of (j, batch tile w) goes to the 6 other slices of
+//          block j (16-byte write-through stores + per-wave tag flag, 1 KB);
+//          everyone sums the 7 slices in slice order -> identical z in all 7.
+//      P1  a2 = act(z/255 + b1), partial logits^T of block j (4 MFMAs; a2 is
+//          the B operand straight from the accumulator layout).
+//      E2  partial logits go to the workgroup of the same slice in every other
+//          block; logits = b2 + sum_j (block order) -> identical in all 49.
+//          softmax / cross-entropy / argmax, dz3, da2 = W2 dz3 (4 MFMAs),
+//          dz2 = da2 * act' -> LDS.
+//      P2  wave t: dW1 tile = x^T dz2 over the batch (28 MFMAs, x^T bytes from
+//          the feature-major stage copy), W1 -= lr/(255 B) dW1 in registers;
+//          wave 7: dW2 (28 MFMAs), db1, db2, metrics, update of the LDS copies
+//          of W2[block j], b1[block j], b2 -- identical in every workgroup that
+//          holds them (same inputs, same order), so no exchange is needed.
+//    Two LDS barriers and two inter-workgroup edges per step; the data of
+//    every edge is double-buffered by step parity and tagged with the global
+//    exchange sequence number, so buffers are never reset between launches.
+//  * x enters the MFMAs as exact integers 0..255 (v_cvt_f32_ubyte); the 1/255
+//    pixel scale and the 1/B loss mean are applied to the fp32 sums.
+//  * the remaining 15 workgroups are COPIERS: while the compute workgroups run
+//    chunk c they pull chunk c+1 from pinned host memory over PCIe into the
+//    other device stage (row-major x, feature-major x^T, labels).
+//  * N GPUs (MULTI): after P2 every compute workgroup exchanges its gradient
+//    (7 dW1 tiles + the block's small gradients) with the same workgroup on
+//    every peer through IPC-mapped uncached buffers -- 49 CUs per GPU carry the
+//    peer traffic -- and sums the ranks in rank order (bit-identical replicas).
+//
+// Placement: workgroup (j, q) runs as blockIdx j + 8q, so under the observed
+// round-robin dispatch the 7 slices of block j share an XCD (E1 stays in one
+// L2).  Speed only: every hand-off uses write-through stores and L1-bypassing
+// loads, correct under any placement.
+#include "common.h"
+
+namespace dtfk {
+namespace mlpf {
+
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+typedef __attribute__((address_space(1))) unsigned gu32;
+
+constexpr int DIN = 784, HID = 100, NCLS = 10;
+constexpr int NJ = 7;              // hidden blocks of 16
+constexpr int NQ = 7;              // feature slices
+constexpr int NT = 7;              // feature tiles (of 16) per slice = MFMA waves
+constexpr int NBT = 7;             // batch tiles of 16 (B <= 112)
+constexpr int BROWS = 16 * NBT;    // 112
+constexpr int XTS = 128;           // x^T row stride (batch padded)
+constexpr int NCOMP = NJ * NQ;     // 49
+constexpr int THREADS = 512;
+constexpr int GRID = 64;           // 49 compute + 15 copier workgroups
+constexpr int NCOP = GRID - NCOMP;
+constexpr int OFF_W2 = 78400, OFF_B1 = 79400, OFF_B2 = 79500;
+
+// device stage record of one step
+constexpr long long XROW_BYTES = (long long)BROWS * DIN;   // [112][784] u8, rows >= B zero
+constexpr long long XT_BYTES = (long long)DIN * XTS;       // [784][128] u8, batch >= B zero
+constexpr long long REC = XROW_BYTES + XT_BYTES + 128;     // + labels [128]
+
+// exchange buffer (bytes): flags F1 [2][NJ][NBT][8] u32, F2 [2][NQ][NBT][8] u32,
+// payloads E1 [2][NJ][NQ][NBT] x 1 KB, E2 [2][NQ][NBT][NJ] x 1 KB
+constexpr int SLOT = 1024;
+constexpr long long F1_OFF = 0;
+constexpr long long F2_OFF = F1_OFF + 2 * NJ * NBT * 8 * 4;
+constexpr long long E1_OFF = 8192;
+constexpr long long E2_OFF = E1_OFF + 2LL * NJ * NQ * NBT * SLOT;
+constexpr long long XBUF_BYTES = E2_OFF + 2LL * NQ * NBT * NJ * SLOT;
+
+// IPC buffer of one rank (N GPUs): [flags: workgroup c at byte 64c][2 parities][49 slots]
+// slot: 7 dW1 tiles x 64 lanes x 16 B (fp32; bf16 payload uses the first 8 B of
+// each 16) | dW2 64 lanes x 16 B | db1 (16) db2 (16) fp32
+constexpr int IPC_FLAGS = 4096;
+constexpr int IPC_SMALL = NT * 64 * 16;
+constexpr int IPC_SLOT = IPC_SMALL + 1024 + 128;
+constexpr long long IPC_BYTES = IPC_FLAGS + 2LL * NCOMP * IPC_SLOT;
+
+// LDS carve (compute); the copier reuses the same dynamic allocation
+constexpr int LS = BROWS + 4;                          // [16][LS] fp32 images (float4-aligned rows)
+constexpr int L_ZBUF = 0;                              // [NT][NBT][64] f32x4 forward partials  50176
+constexpr int L_A2T = L_ZBUF + NT * NBT * 64 * 16;     // [16 hidden][LS] a2
+constexpr int L_DZ2T = L_A2T + 16 * LS * 4;            // [16 hidden][LS] dz2
+constexpr int L_DZ3T = L_DZ2T + 16 * LS * 4;           // [16 class][LS] dz3
+constexpr int L_W2 = L_DZ3T + 16 * LS * 4;             // [16 hidden][16 class] W2 of block j
+constexpr int L_B1 = L_W2 + 1024;                      // [16]
+constexpr int L_B2 = L_B1 + 64;                        // [16]
+constexpr int L_RDB1 = L_B2 + 64;                      // [8][16]
+constexpr int L_RDB2 = L_RDB1 + 512;                   // [8][16]
+constexpr int L_RMET = L_RDB2 + 512;                   // [8][2]
+constexpr int L_FLAG = L_RMET + 64;
+constexpr int LDS_COMPUTE = L_FLAG + 64;
+constexpr int CROW = DIN + 16;                         // copier LDS row stride (800)
+constexpr int LDS_COPIER = BROWS * CROW;               // 89600
+constexpr int LDS_BYTES = LDS_COMPUTE > LDS_COPIER ? LDS_COMPUTE : LDS_COPIER;
+
+struct Args {
+  const uint8_t* stage;     // this chunk: nsteps records of REC bytes
+  long long rec_h;          // host record bytes (B*785 rounded up to 16)
+  int B, nsteps;
+  float* params;            // flat fp32 master, TF variable order (read at start, written at end)
+  const float* lr;
+  float* metrics;
+  int ring;
+  int act, naive;
+  long long* gstep;
+  unsigned long long* seq;  // exchange sequence number (monotonic across launches)
+  uint8_t* xbuf;            // exchange buffer (XBUF_BYTES, zeroed once)
+  int* err;
+  long long timeout;        // s_memrealtime ticks (100 MHz)
+  long long* step_ts;       // optional: s_memrealtime at the start of every global step (ring)
+  int ts_ring;
+  const uint8_t* host_next; // device-visible pointer into pinned host memory
+  int next_steps;
+  uint8_t* stage_next;
+  void* const* peer_base;   // N GPUs: IPC-mapped exchange buffers of every rank
+  int W, rank;
+  int gbf16;                // N GPUs: dW1 payload in bf16 (BASELINE config #2) instead of fp32
+};
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ float ub(uint32_t w, int e) { return (float)((w >> (8 * e)) & 0xffu); }
+
+__device__ __forceinline__ void lds_barrier() {   // orders LDS only: no vmcnt(0) on in-flight prefetches
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// 16-byte write-through (sc1) store / L1-bypassing (sc1) load through a buffer
+// resource over a wave-uniform region of `bytes` (one descriptor per edge and
+// step: slot and lane go into the VGPR offset)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t region_rsrc(const void* base, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, 0x00020000);
+}
+__device__ __forceinline__ void st16_sc1(__amdgpu_buffer_rsrc_t rs, int voff, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, voff, 0, 16);
+}
+__device__ __forceinline__ f32x4 ld16_sc1(__amdgpu_buffer_rsrc_t rs, int voff) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, 16));
+}
+
+// lane l <- lane l^16 / l^32 with gfx950's VALU row swaps
+__device__ __forceinline__ float xor16(float v) {
+  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(((threadIdx.x >> 4) & 1) ? p[0] : p[1]);
+}
+__device__ __forceinline__ float xor32(float v) {
+  const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float((threadIdx.x & 32) ? p[0] : p[1]);
+}
+
+// Poll `n` u32 tag flags at f[0..n) (lanes < n, except `skip`) until every one
+// equals `tag`; false on timeout or a raised error word.
+__device__ __forceinline__ bool poll_flags(const unsigned* f, int n, int skip, unsigned tag, int lane, const Args& a) {
+  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    bool ok = true;
+    if (lane < n && lane != skip)
+      ok = __hip_atomic_load(f + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == tag;
+    if (__all(ok)) break;
+    if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > a.timeout ||
+        __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+      if (lane == 0) atomicOr(a.err, 1);
+      return false;
+    }
+  }
+  asm volatile("" ::: "memory");   // no payload load above the flag match
+  return true;
+}
+
+// ------------------------------------------------------------------ copier
+// task = one step of the next chunk: 112 rows of 784 pixels from the pinned host
+// record into LDS (rows >= B zero), then the row-major image, the feature-major
+// copy (4x4 byte transposes with v_perm) and the labels into the device stage.
+__device__ void copier(const Args& a, int cid, uint8_t* smem) {
+  const int tid = threadIdx.x;
+  const int B = a.B;
+  for (int st = cid; st < a.next_steps; st += NCOP) {
+    const uint8_t* src = a.host_next + (long long)st * a.rec_h;
+    uint8_t* dst = a.stage_next + (long long)st * REC;
+    constexpr int C16 = DIN / 16;   // 49
+    for (int k = tid; k < BROWS * C16; k += THREADS) {
+      const int row = k / C16, c = k % C16;
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (row < B) v = reinterpret_cast<const uint4*>(src)[row * C16 + c];
+      *reinterpret_cast<uint4*>(smem + row * CROW + 16 * c) = v;
+    }
+    if (tid < 128) dst[XROW_BYTES + XT_BYTES + tid] = tid < B ? src[(long long)B * DIN + tid] : (uint8_t)0;
+    __syncthreads();
+    for (int k = tid; k < BROWS * C16; k += THREADS) {
+      const int row = k / C16, c = k % C16;
+      reinterpret_cast<uint4*>(dst)[row * C16 + c] = *reinterpret_cast<const uint4*>(smem + row * CROW + 16 * c);
+    }
+    uint8_t* xt = dst + XROW_BYTES;
+    for (int k = tid; k < (DIN / 4) * (BROWS / 4); k += THREADS) {
+      const int fq = k / (BROWS / 4), rq = k % (BROWS / 4);
+      const uint8_t* p = smem + 4 * rq * CROW + 4 * fq;
+      const uint32_t r0 = *reinterpret_cast<const uint32_t*>(p);
+      const uint32_t r1 = *reinterpret_cast<const uint32_t*>(p + CROW);
+      const uint32_t r2 = *reinterpret_cast<const uint32_t*>(p + 2 * CROW);
+      const uint32_t r3 = *reinterpret_cast<const uint32_t*>(p + 3 * CROW);
+      // t01 = [r0.b0 r1.b0 r0.b1 r1.b1], u01 = [r0.b2 r1.b2 r0.b3 r1.b3] (likewise r2/r3)
+      const uint32_t t01 = __builtin_amdgcn_perm(r1, r0, 0x05010400u);
+      const uint32_t t23 = __builtin_amdgcn_perm(r3, r2, 0x05010400u);
+      const uint32_t u01 = __builtin_amdgcn_perm(r1, r0, 0x07030602u);
+      const uint32_t u23 = __builtin_amdgcn_perm(r3, r2, 0x07030602u);
+      uint32_t* o = reinterpret_cast<uint32_t*>(xt + (long long)(4 * fq) * XTS + 4 * rq);
+      o[0] = __builtin_amdgcn_perm(t23, t01, 0x05040100u);             // feature 4fq+0, batch 4rq..4rq+3
+      o[XTS / 4] = __builtin_amdgcn_perm(t23, t01, 0x07060302u);       // 4fq+1
+      o[2 * XTS / 4] = __builtin_amdgcn_perm(u23, u01, 0x05040100u);   // 4fq+2
+      o[3 * XTS / 4] = __builtin_amdgcn_perm(u23, u01, 0x07060302u);   // 4fq+3
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------ compute
+template <int ACT, bool MULTI>   // ACT 0 sigmoid, 1 relu; MULTI: N-GPU gradient exchange
+__device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int c = j * NQ + q;
+  const int B = a.B;
+  f32x4* zbuf = reinterpret_cast<f32x4*>(smem + L_ZBUF);
+  float* a2T = reinterpret_cast<float*>(smem + L_A2T);
+  float* dz2T = reinterpret_cast<float*>(smem + L_DZ2T);
+  float* dz3T = reinterpret_cast<float*>(smem + L_DZ3T);
+  float* w2s = reinterpret_cast<float*>(smem + L_W2);
+  float* b1s = reinterpret_cast<float*>(smem + L_B1);
+  float* b2s = reinterpret_cast<float*>(smem + L_B2);
+  float* rdb1 = reinterpret_cast<float*>(smem + L_RDB1);
+  float* rdb2 = reinterpret_cast<float*>(smem + L_RDB2);
+  float* rmet = reinterpret_cast<float*>(smem + L_RMET);
+  int* abort_flag = reinterpret_cast<int*>(smem + L_FLAG);
+
+  // ---- load state
+  for (int k = tid; k < 3 * 16 * LS; k += THREADS) a2T[k] = 0.f;   // a2T, dz2T, dz3T (batch pad stays 0)
+  if (tid < 256) {
+    const int n = tid >> 4, cl = tid & 15;
+    const int hn = 16 * j + n;
+    w2s[tid] = (hn < HID && cl < NCLS) ? a.params[OFF_W2 + hn * NCLS + cl] : 0.f;
+  } else if (tid < 272) {
+    const int hn = 16 * j + (tid - 256);
+    b1s[tid - 256] = hn < HID ? a.params[OFF_B1 + hn] : 0.f;
+  } else if (tid < 288) {
+    const int cl = tid - 272;
+    b2s[cl] = cl < NCLS ? a.params[OFF_B2 + cl] : 0.f;
+  } else if (tid == 288) {
+    *abort_flag = 0;
+  }
+  const int hid = 16 * j + r;       // this lane's hidden unit in the W1 / dW1 layouts
+  const bool hv = hid < HID;
+  const int ft = NT * q + w;        // wave w < 7: feature tile (16 features)
+  float Wt[4] = {0.f, 0.f, 0.f, 0.f};
+  if (w < NT && hv) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) Wt[e] = a.params[(16 * ft + 4 * g + e) * HID + hid];
+  }
+  const unsigned long long seq0 = *a.seq;
+  const long long gstep0 = *a.gstep;
+  const float lr = *a.lr;
+  const float lrB = lr / (float)(B * (MULTI ? a.W : 1));
+  const float lrX = lrB * (1.f / 255.f);
+  const bool failed_in = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+
+  // x operands of the wave's feature tile (waves < 7), current and next step:
+  //  xf[bt]: row 16bt+r, features 16ft+4g..+3 (forward B operand)
+  //  xt[s] : feature 16ft+r, batch 16s+4g..+3 (weight-gradient A operand)
+  //  lab   : label of batch row 16w+r (head)
+  uint32_t xf[NBT], xt[NBT];
+  int lab = 0;
+  auto load_x = [&](int st, uint32_t (&f)[NBT], uint32_t (&t)[NBT], int& y) {
+    const uint8_t* rec = a.stage + (long long)st * REC;
+#pragma unroll
+    for (int b = 0; b < NBT; ++b) {
+      f[b] = *reinterpret_cast<const uint32_t*>(rec + (16 * b + r) * DIN + 16 * ft + 4 * g);
+      t[b] = *reinterpret_cast<const uint32_t*>(rec + XROW_BYTES + (16 * ft + r) * XTS + 16 * b + 4 * g);
+    }
+    y = rec[XROW_BYTES + XT_BYTES + 16 * w + r];
+  };
+  __syncthreads();
+  if (failed_in) return;
+  if (w < NT && a.nsteps > 0) load_x(0, xf, xt, lab);
+
+  bool aborted = false;
+  for (int st = 0; st < a.nsteps; ++st) {
+    const unsigned long long sq = seq0 + (unsigned long long)st + 1ull;
+    const unsigned tag = (unsigned)sq;
+    const int par = (int)(sq & 1ull);
+    if (c == 0 && tid == 0 && a.step_ts != nullptr)
+      a.step_ts[(gstep0 + st) % a.ts_ring] = (long long)__builtin_amdgcn_s_memrealtime();
+
+    // ---------------- P0: forward partial of feature tile ft, all batch tiles
+    if (w < NT) {
+      f32x4 acc[NBT];
+#pragma unroll
+      for (int b = 0; b < NBT; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int b = 0; b < NBT; ++b) acc[b] = mfma4(Wt[e], ub(xf[b], e), acc[b]);
+#pragma unroll
+      for (int b = 0; b < NBT; ++b) zbuf[(w * NBT + b) * 64 + lane] = acc[b];
+    }
+    lds_barrier();
+
+    // ---------------- E1 + P1 + E2 + head (wave w < 7: batch tile w)
+    uint32_t xfn[NBT], xtn[NBT];
+    int labn = 0;
+    if (w < NT) {
+      const int bw = 16 * w + r;          // this lane's batch row
+      const bool bv = bw < B;
+      f32x4 zs = zbuf[w * 64 + lane];
+#pragma unroll
+      for (int t = 1; t < NT; ++t) zs += zbuf[(t * NBT + w) * 64 + lane];
+      // publish the slice partial of (j, batch tile w); flag after the drain
+      // E1 region of (parity, block j): [slice][batch tile] slots
+      const auto r1 = region_rsrc(a.xbuf + E1_OFF + (long long)(par * NJ + j) * NQ * NBT * SLOT, NQ * NBT * SLOT);
+      unsigned* f1 = reinterpret_cast<unsigned*>(a.xbuf + F1_OFF) + ((par * NJ + j) * NBT + w) * 8;
+      st16_sc1(r1, (q * NBT + w) * SLOT + 16 * lane, zs);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_store(f1 + q, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      bool ok = poll_flags(f1, NQ, q, tag, lane, a);
+      f32x4 part[NQ];
+#pragma unroll
+      for (int qq = 0; qq < NQ; ++qq)
+        part[qq] = (qq == q) ? zs : ld16_sc1(r1, (qq * NBT + w) * SLOT + 16 * lane);
+      f32x4 z = part[0];
+#pragma unroll
+      for (int qq = 1; qq < NQ; ++qq) z += part[qq];
+      // lane (batch r, g): hidden 16j+4g+i
+      float a2[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int hl = 4 * g + i;
+        const float zt = z[i] * (1.f / 255.f) + b1s[hl];
+        const float av = ACT == 0 ? 1.f / (1.f + expf(-zt)) : fmaxf(zt, 0.f);
+        a2[i] = (16 * j + hl < HID) ? av : 0.f;
+      }
+      // partial logits^T[class][batch] of block j: A = W2^T (lane: class r), B = a2^T
+      f32x4 pl = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) pl = mfma4(w2s[(4 * g + e) * 16 + r], a2[e], pl);
+      // E2 region of (parity, slice q, batch tile w): [block] slots
+      const auto r2 = region_rsrc(a.xbuf + E2_OFF + (long long)((par * NQ + q) * NBT + w) * NJ * SLOT, NJ * SLOT);
+      unsigned* f2 = reinterpret_cast<unsigned*>(a.xbuf + F2_OFF) + ((par * NQ + q) * NBT + w) * 8;
+      if (g < 3) st16_sc1(r2, j * SLOT + 16 * lane, pl);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_store(f2 + j, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // while the logits are in flight: a2 -> LDS (dW2)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a2T[(4 * g + i) * LS + bw] = a2[i];
+      ok = poll_flags(f2, NJ, j, tag, lane, a) && ok;
+      f32x4 lp[NJ];
+#pragma unroll
+      for (int jj = 0; jj < NJ; ++jj)
+        lp[jj] = (jj == j) ? pl : ld16_sc1(r2, jj * SLOT + 16 * lane);
+      // next step's x operands: in flight across the head and the weight gradient
+      if (st + 1 < a.nsteps) load_x(st + 1, xfn, xtn, labn);
+      if (!ok && lane == 0) *abort_flag = 1;
+      // logits, softmax cross-entropy, accuracy -- identical in every workgroup
+      float lg[4], ex[4];
+      float m = -3.0e38f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float v = b2s[4 * g + i];
+#pragma unroll
+        for (int jj = 0; jj < NJ; ++jj) v += (g < 3) ? lp[jj][i] : 0.f;
+        lg[i] = v;
+        if (4 * g + i < NCLS) m = fmaxf(m, v);
+      }
+      m = fmaxf(m, xor16(m));
+      m = fmaxf(m, xor32(m));
+      const int y = lab < NCLS ? lab : 0;
+      float ssum = 0.f, zy = 0.f, am = 1e9f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int cl = 4 * g + i;
+        ex[i] = cl < NCLS ? expf(lg[i] - m) : 0.f;
+        ssum += ex[i];
+        zy += (cl == y) ? lg[i] : 0.f;
+        if (cl < NCLS && lg[i] == m) am = fminf(am, (float)cl);
+      }
+      ssum += xor16(ssum); ssum += xor32(ssum);
+      zy += xor16(zy); zy += xor32(zy);
+      am = fminf(am, xor16(am)); am = fminf(am, xor32(am));
+      const float inv = 1.f / ssum;
+      float dz3[4], py = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int cl = 4 * g + i;
+        const float p = ex[i] * inv;
+        py += (cl == y) ? p : 0.f;
+        dz3[i] = (bv && cl < NCLS) ? p - (cl == y ? 1.f : 0.f) : 0.f;   // unscaled: 1/B at the update
+      }
+      py += xor16(py); py += xor32(py);
+      const float loss = a.naive ? -logf(py) : (m + logf(ssum) - zy);
+      // da2^T = W2 . dz3^T (A = W2, lane: hidden r), dz2 = da2 * act'(a2)
+      f32x4 da = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) da = mfma4(w2s[r * 16 + 4 * g + e], dz3[e], da);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float d = ACT == 0 ? da[i] * a2[i] * (1.f - a2[i]) : (a2[i] > 0.f ? da[i] : 0.f);
+        dz2T[(4 * g + i) * LS + bw] = d;
+        dz3T[(4 * g + i) * LS + bw] = dz3[i];
+        const float s1 = row16_sum(d);
+        const float s2 = row16_sum(dz3[i]);
+        if (r == 0) {
+          rdb1[w * 16 + 4 * g + i] = s1;
+          rdb2[w * 16 + 4 * g + i] = s2;
+        }
+      }
+      const float ls = row16_sum((g == 0 && bv) ? loss : 0.f);
+      const float cr = row16_sum((g == 0 && bv && (int)am == y) ? 1.f : 0.f);
+      if (lane == 0) { rmet[2 * w] = ls; rmet[2 * w + 1] = cr; }
+    }
+    lds_barrier();
+    if (*abort_flag) { aborted = true; break; }
+
+    // ---------------- P2: weight gradients
+    f32x4 G = {0.f, 0.f, 0.f, 0.f};      // waves < 7: dW1[16ft+4g+i][16j+r] (x 255 B)
+    f32x4 D = {0.f, 0.f, 0.f, 0.f};      // wave 7: dW2[16j+4g+i][class r] (x B)
+    float gb = 0.f;                      // wave 7: db1 (lanes < 16) / db2 (lanes 16..25) (x B)
+    if (w < NT) {
+      f32x4 g0 = {0.f, 0.f, 0.f, 0.f}, g1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < NBT; ++s) {
+        const f32x4 bz = *reinterpret_cast<const f32x4*>(dz2T + r * LS + 16 * s + 4 * g);
+        g0 = mfma4(ub(xt[s], 0), bz[0], g0);
+        g1 = mfma4(ub(xt[s], 1), bz[1], g1);
+        g0 = mfma4(ub(xt[s], 2), bz[2], g0);
+        g1 = mfma4(ub(xt[s], 3), bz[3], g1);
+      }
+      G = g0 + g1;
+    } else {
+      f32x4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < NBT; ++s) {
+        const f32x4 av = *reinterpret_cast<const f32x4*>(a2T + r * LS + 16 * s + 4 * g);
+        const f32x4 dv = *reinterpret_cast<const f32x4*>(dz3T + r * LS + 16 * s + 4 * g);
+        d0 = mfma4(av[0], dv[0], d0);
+        d1 = mfma4(av[1], dv[1], d1);
+        d0 = mfma4(av[2], dv[2], d0);
+        d1 = mfma4(av[3], dv[3], d1);
+      }
+      D = d0 + d1;
+      if (lane < 16) {
+#pragma unroll
+        for (int v = 0; v < NBT; ++v) gb += rdb1[v * 16 + lane];
+      } else if (lane < 16 + NCLS) {
+#pragma unroll
+        for (int v = 0; v < NBT; ++v) gb += rdb2[v * 16 + lane - 16];
+      } else if (lane == 63 && c == 0) {
+        float ls = 0.f, cr = 0.f;
+#pragma unroll
+        for (int v = 0; v < NBT; ++v) { ls += rmet[2 * v]; cr += rmet[2 * v + 1]; }
+        const int sl = (int)((gstep0 + st) % a.ring);
+        a.metrics[2 * sl] = ls / (float)B;
+        a.metrics[2 * sl + 1] = cr / (float)B;
+      }
+    }
+    if constexpr (MULTI) {
+      // ---- one-shot exchange of this workgroup's gradient with the same
+      // workgroup on every peer GPU (uncached IPC buffers: completion ==
+      // visibility); rank-order sums keep the replicas bit-identical
+      const size_t soff = IPC_FLAGS + (size_t)(par * NCOMP + c) * IPC_SLOT;
+      char* own = static_cast<char*>(a.peer_base[a.rank]) + soff;
+      if (w < NT) {
+        if (a.gbf16) {
+          const uint2 v = make_uint2(pack2bf(G[0], G[1]), pack2bf(G[2], G[3]));
+          G = f32x4{bf2f(v.x & 0xffff), bf2f(v.x >> 16), bf2f(v.y & 0xffff), bf2f(v.y >> 16)};
+          *reinterpret_cast<uint2*>(own + (w * 64 + lane) * 16) = v;
+        } else {
+          *reinterpret_cast<f32x4*>(own + (w * 64 + lane) * 16) = G;
+        }
+      } else {
+        *reinterpret_cast<f32x4*>(own + IPC_SMALL + lane * 16) = D;
+        if (lane < 16 + NCLS) *reinterpret_cast<float*>(own + IPC_SMALL + 1024 + lane * 4) = gb;
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave: its slot stores landed
+      lds_barrier();
+      if (tid == 0)
+        __hip_atomic_store(reinterpret_cast<unsigned*>(static_cast<char*>(a.peer_base[a.rank]) + 64 * c), tag,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (w == 0) {
+        const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+        for (;;) {
+          bool ok = true;
+          if (lane < a.W && lane != a.rank) {
+            const unsigned v = __hip_atomic_load(
+                reinterpret_cast<const unsigned*>(static_cast<const char*>(a.peer_base[lane]) + 64 * c),
+                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            ok = (int)(v - tag) >= 0;
+          }
+          if (__all(ok)) break;
+          if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > a.timeout ||
+              __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+            if (lane == 0) {
+              atomicOr(a.err, 2);
+              *abort_flag = 1;
+            }
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      lds_barrier();
+      asm volatile("" ::: "memory");   // no peer-slot load hoisted above the flag match
+      if (*abort_flag) { aborted = true; break; }
+      f32x4 sum = {0.f, 0.f, 0.f, 0.f};
+      float sb = 0.f;
+      for (int rr = 0; rr < a.W; ++rr) {
+        f32x4 v = w < NT ? G : D;
+        float vb = gb;
+        if (rr != a.rank) {
+          const char* ps = static_cast<const char*>(a.peer_base[rr]) + soff;
+          if (w < NT) {
+            if (a.gbf16) {
+              const unsigned long long x =
+                  __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(ps + (w * 64 + lane) * 16));
+              v = f32x4{bf2f((unsigned)x & 0xffff), bf2f(((unsigned)x) >> 16), bf2f((unsigned)(x >> 32) & 0xffff),
+                        bf2f((unsigned)(x >> 48))};
+            } else {
+              v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(ps + (w * 64 + lane) * 16));
+            }
+          } else {
+            v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(ps + IPC_SMALL + lane * 16));
+            vb = lane < 16 + NCLS ? __builtin_nontemporal_load(reinterpret_cast<const float*>(ps + IPC_SMALL + 1024) + lane)
+                                  : 0.f;
+          }
+        }
+        sum += v;
+        sb += vb;
+      }
+      if (w < NT) G = sum; else { D = sum; gb = sb; }
+    }
+    // ---------------- updates (lr / (W B), 1/255 for the pixel scale)
+    if (w < NT) {
+      if (hv) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) Wt[i] -= lrX * G[i];
+      }
+#pragma unroll   // rotate the prefetched operands in
+      for (int b = 0; b < NBT; ++b) { xf[b] = xfn[b]; xt[b] = xtn[b]; }
+      lab = labn;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (16 * j + 4 * g + i < HID && r < NCLS) w2s[(4 * g + i) * 16 + r] -= lrB * D[i];
+      if (lane < 16) {
+        if (16 * j + lane < HID) b1s[lane] -= lrB * gb;
+      } else if (lane < 16 + NCLS) {
+        b2s[lane - 16] -= lrB * gb;
+      }
+    }
+  }
+  if (aborted) return;
+  __syncthreads();   // wave 7's last small-parameter update
+
+  // ---- write back (fp32 master), global step, exchange sequence, end stamp
+  if (w < NT && hv) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) a.params[(16 * ft + 4 * g + e) * HID + hid] = Wt[e];
+  }
+  if (q == 0) {
+    if (tid < 256) {
+      const int n = tid >> 4, cl = tid & 15;
+      const int hn = 16 * j + n;
+      if (hn < HID && cl < NCLS) a.params[OFF_W2 + hn * NCLS + cl] = w2s[tid];
+    } else if (tid < 272) {
+      const int hn = 16 * j + (tid - 256);
+      if (hn < HID) a.params[OFF_B1 + hn] = b1s[tid - 256];
+    }
+  }
+  if (c == 0) {
+    if (tid >= 272 && tid < 272 + NCLS) a.params[OFF_B2 + (tid - 272)] = b2s[tid - 272];
+    if (tid == 300) {
+      *a.gstep = gstep0 + a.nsteps;
+      *a.seq = seq0 + (unsigned long long)a.nsteps;
+      if (a.step_ts != nullptr)
+        a.step_ts[(gstep0 + a.nsteps) % a.ts_ring] = (long long)__builtin_amdgcn_s_memrealtime();
+    }
+  }
+}
+
+template <int ACT, bool MULTI>
+__global__ __launch_bounds__(THREADS, 1) void mlp_persist_f32(Args a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int b = blockIdx.x;
+  const int j = b & 7, q = b >> 3;
+  if (j < NJ && q < NQ) {
+    if (a.nsteps > 0) compute<ACT, MULTI>(a, j, q, smem);
+    return;
+  }
+  // copier id among the non-compute blocks: b%8 == 7 (b < 56) -> 0..6, b >= 56 -> 7..14
+  const int cid = q < NQ ? q : NQ + (b - 8 * NQ);
+  copier(a, cid, smem);
+}
+
+}  // namespace mlpf
+}  // namespace dtfk
+
+extern "C" {
+
+long long dtfk_mlpf_stage_rec() { return dtfk::mlpf::REC; }
+long long dtfk_mlpf_xbuf_bytes() { return dtfk::mlpf::XBUF_BYTES; }
+long long dtfk_mlpf_ipc_bytes() { return dtfk::mlpf::IPC_BYTES; }
+int dtfk_mlpf_max_batch() { return dtfk::mlpf::BROWS; }
+
+hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int nsteps, float* params, const float* lr,
+                                float* metrics, int ring, int act, int naive, long long* gstep, unsigned long long* seq,
+                                void* xbuf, int* err, long long timeout, long long* step_ts, int ts_ring,
+                                const void* host_next, int next_steps, void* stage_next, void* const* peer_base, int W,
+                                int rank, int gbf16, hipStream_t stream) {
+  using namespace dtfk::mlpf;
+  Args a;
+  a.stage = static_cast<const uint8_t*>(stage);
+  a.rec_h = rec_h;
+  a.B = B;
+  a.nsteps = nsteps;
+  a.params = params;
+  a.lr = lr;
+  a.metrics = metrics;
+  a.ring = ring;
+  a.act = act;
+  a.naive = naive;
+  a.gstep = gstep;
+  a.seq = seq;
+  a.xbuf = static_cast<uint8_t*>(xbuf);
+  a.err = err;
+  a.timeout = timeout;
+  a.step_ts = step_ts;
+  a.ts_ring = ts_ring > 0 ? ts_ring : 1;
+  a.host_next = static_cast<const uint8_t*>(host_next);
+  a.next_steps = next_steps;
+  a.stage_next = static_cast<uint8_t*>(stage_next);
+  a.peer_base = peer_base;
+  a.W = W;
+  a.rank = rank;
+  a.gbf16 = gbf16;
+  constexpr size_t lds = LDS_BYTES;
+  static bool attr_set = false;
+  const void* kerns[4] = {reinterpret_cast<const void*>(mlp_persist_f32<0, false>),
+                          reinterpret_cast<const void*>(mlp_persist_f32<1, false>),
+                          reinterpret_cast<const void*>(mlp_persist_f32<0, true>),
+                          reinterpret_cast<const void*>(mlp_persist_f32<1, true>)};
+  if (!attr_set) {
+    for (const void* k : kerns) {
+      const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+    }
+    attr_set = true;
+  }
+  const int which = (act == 0 ? 0 : 1) + (W > 1 ? 2 : 0);
+  switch (which) {
+    case 0: hipLaunchKernelGGL((mlp_persist_f32<0, false>), dim3(GRID), dim3(THREADS), lds, stream, a); break;
+    case 1: hipLaunchKernelGGL((mlp_persist_f32<1, false>), dim3(GRID), dim3(THREADS), lds, stream, a); break;
+    case 2: hipLaunchKernelGGL((mlp_persist_f32<0, true>), dim3(GRID), dim3(THREADS), lds, stream, a); break;
+    default: hipLaunchKernelGGL((mlp_persist_f32<1, true>), dim3(GRID), dim3(THREADS), lds, stream, a); break;
+  }
+  return hipGetLastError();
+}
+
+}  // extern "C"

@@ -416,8 +416,15 @@ __device__ __forceinline__ uint16_t* ipc_slot(const IpcArgs& a, int r) {
 // stores (uncached exchange memory: completion == visibility, no L2 writeback
 // needed), then lane r waits for peer r's flag of the same workgroup -- the W
 // remote polls overlap.  Returns false (and raises err) on timeout.
+// Ordering: the asm wait is both the hardware drain (every slot store of this
+// wave acknowledged by the fabric) and a compiler memory barrier (the
+// `__builtin_amdgcn_s_waitcnt` builtin is IntrNoMem and let the flag store be
+// scheduled above the payload stores).  The consumer side ends its poll with a
+// second asm barrier so no slot load is hoisted above the flag match; its slot
+// loads are non-temporal loads of uncached memory (the guide's sc1-load form
+// of the acquire, MI355X_MICROARCH.md "Valid forms").
 __device__ __forceinline__ bool ipc_wg_sync(const IpcArgs& a, int wg, unsigned long long epoch, int lane) {
-  __builtin_amdgcn_s_waitcnt(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const long long off = IPC_WG_FLAG0 + 8LL * wg;
   if (lane == 0)
     __hip_atomic_store(reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(a.peer_base[a.rank]) + off),
@@ -436,7 +443,9 @@ __device__ __forceinline__ bool ipc_wg_sync(const IpcArgs& a, int wg, unsigned l
       }
     }
   }
-  return __all(good);
+  const bool all_good = __all(good);
+  asm volatile("" ::: "memory");   // no peer-slot load above the flag match
+  return all_good;
 }
 
 // ---------------------------------------------------------------------- B

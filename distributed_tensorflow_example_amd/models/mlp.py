@@ -421,43 +421,74 @@ class MLPStepRunner:
 
 
 class PersistentMLPRunner:
-    """Drives the persistent weight-stationary kernel (csrc/kernels/mlp_persist.hip)
-    over a pinned-host epoch: ONE launch per chunk of `g` steps.
+    """Drives a persistent weight-stationary training kernel over a pinned-host
+    epoch: ONE launch per chunk of up to `g` steps.
 
-    Inside each launch 7 workgroups run the chunk's SGD steps with the weights
-    resident on-chip, while 57 copier workgroups pull the NEXT chunk from
-    pinned host memory over PCIe into the other device stage (row-major
-    records + a feature-major copy for the weight gradient).  No second stream,
-    no cross-queue events, no graph capture (one launch per 50 steps).
+    precision="fp32" (default, the reference's precision: example.py:77-118 is
+        fp32 end to end) -- csrc/kernels/mlp_persist_f32.hip: 49 compute
+        workgroups (7 hidden blocks x 7 feature slices) on exact f32-input MFMA,
+        fp32 master weights in VGPRs, 15 copier workgroups.
+    precision="fp16" -- csrc/kernels/mlp_persist.hip: 7 compute workgroups on
+        f16 MFMA (pixels exact as 1024+u, weights/activations rounded to fp16),
+        57 copier workgroups.
+
+    Inside each launch the copier workgroups pull the NEXT chunk from pinned host
+    memory over PCIe into the other device stage while the compute workgroups
+    run this one.  No second stream, no cross-queue events, no graph capture.
+
+    Staging is range-based: a request whose steps lie inside a staged chunk
+    runs from it at an offset (no copy).  The chunk prefetched inside a launch
+    is the next planned chunk, or -- for the last launch of a `run()` -- a
+    speculative chunk of the same length as that `run()` (`lookahead` overrides
+    it, e.g. a warmup priming exactly the timed run), so a short timed run never
+    streams more than it computes.  `copy_only_launches` counts cold starts.
 
     N GPUs of one node (world_size > 1): every compute workgroup exchanges its
-    block's bf16 gradient with the same workgroup on every peer through
-    IPC-mapped uncached buffers inside the same launch (flag per block and step,
-    rank-order sums -> bit-identical replicas).  Batch <= 112 per GPU.
+    gradient with the same workgroup on every peer through IPC-mapped uncached
+    buffers inside the same launch (flag per workgroup and step, rank-order sums
+    -> bit-identical replicas).  Batch <= 112 per GPU.
+
+    `step_ts` (int64 ring on the device) receives the s_memrealtime (100 MHz)
+    stamp of every global step's start, plus the end of each launch:
+    `step_times_ms(first, last)` gives true per-step durations.
     """
 
-    def __init__(self, trainer: FusedMLPTrainer, epoch, steps_per_launch: int = 50,
-                 timeout_s: float = 5.0):
+    TS_RING = 16384
+
+    def __init__(self, trainer: FusedMLPTrainer, epoch, steps_per_launch: int = 550,
+                 timeout_s: float = 30.0, precision: str = "fp32", grad_bf16: bool = True):
         C = trainer.C
-        if trainer.B > C.mlp_persist_max_batch():
-            raise ValueError(f"PersistentMLPRunner needs batch <= {C.mlp_persist_max_batch()}")
+        if precision not in ("fp32", "fp16"):
+            raise ValueError("precision must be 'fp32' or 'fp16'")
+        self.precision = precision
+        maxb = C.mlpf_max_batch() if precision == "fp32" else C.mlp_persist_max_batch()
+        if trainer.B > maxb:
+            raise ValueError(f"PersistentMLPRunner needs batch <= {maxb}")
         if epoch.batch_size != trainer.B:
             raise ValueError("epoch batch size != trainer batch size")
         self.t = trainer
         self.epoch = epoch
         self.g = int(min(steps_per_launch, epoch.num_batches))
         self.timeout_s = float(timeout_s)
+        self.grad_bf16 = bool(grad_bf16)
         dev = trainer.device
-        rec = C.mlp_persist_stage_rec(trainer.B)   # device stage record (k-step-pair interleaved rows)
-        xtb = C.mlp_persist_xt_bytes()
-        self.xs = [torch.zeros(self.g * rec, dtype=torch.uint8, device=dev) for _ in range(2)]
-        self.xts = [torch.zeros(self.g * xtb, dtype=torch.uint8, device=dev) for _ in range(2)]
-        self.gran = torch.zeros(C.mlp_persist_gran_count(), dtype=torch.int64, device=dev)
+        if precision == "fp32":
+            self.rec_s = int(C.mlpf_stage_rec())
+            self.stages = [torch.zeros(self.g * self.rec_s, dtype=torch.uint8, device=dev) for _ in range(2)]
+            self.xbuf = torch.zeros(int(C.mlpf_xbuf_bytes()), dtype=torch.uint8, device=dev)
+        else:
+            self.rec_s = int(C.mlp_persist_stage_rec(trainer.B))   # k-step-pair interleaved rows
+            self.xtb = int(C.mlp_persist_xt_bytes())
+            self.xs = [torch.zeros(self.g * self.rec_s, dtype=torch.uint8, device=dev) for _ in range(2)]
+            self.xts = [torch.zeros(self.g * self.xtb, dtype=torch.uint8, device=dev) for _ in range(2)]
+            self.gran = torch.zeros(C.mlp_persist_gran_count(), dtype=torch.int64, device=dev)
         self.seq = torch.zeros(1, dtype=torch.int64, device=dev)
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.step_ts = torch.zeros(self.TS_RING, dtype=torch.int64, device=dev)
         self.cursor = 0
-        self.parity = 0
-        self.loaded = None      # (b0, g) staged in xs[parity]
+        self.staged: List[Optional[Tuple[int, int]]] = [None, None]   # (b0, g) resident per stage buffer
+        self.copy_only_launches = 0
+        self.last_prefetch_steps = 0
         self.use_graph = False  # MLPStepRunner interface
         self.prefetch = "in-kernel"
         self.ipc = None
@@ -467,7 +498,8 @@ class PersistentMLPRunner:
             if int(os.environ.get("LOCAL_WORLD_SIZE", w.world_size)) != w.world_size:
                 raise RuntimeError("the persistent N-GPU exchange needs all ranks on one node")
             from ..parallel.world import open_peer_buffers
-            self.ipc = open_peer_buffers(C, C.mlp_persist_ipc_bytes(), w)
+            nbytes = C.mlpf_ipc_bytes() if precision == "fp32" else C.mlp_persist_ipc_bytes()
+            self.ipc = open_peer_buffers(C, int(nbytes), w)
             self.W, self.rank = w.world_size, w.rank
 
     def _chunks(self, cursor: int, steps: int) -> List[Tuple[int, int]]:
@@ -481,36 +513,90 @@ class PersistentMLPRunner:
             left -= g
         return out
 
-    def _launch(self, par: int, nsteps: int, nxt: Tuple[int, int], dst_par: int):
+    def _launch(self, par: int, off: int, nsteps: int, nxt: Tuple[int, int]):
+        """Run `nsteps` from stage `par` at step offset `off`; copy `nxt` into stage par^1."""
         t, ep = self.t, self.epoch
-        t.C.mlp_persist(self.xs[par], self.xts[par], ep.rec, t.B, nsteps, t.params, t.lr, t.metrics, t.gstep,
-                        self.seq, self.gran, self.err, self.timeout_s, t.act, int(t.naive),
-                        host=ep.host, host_offset=nxt[0] * ep.rec, next_steps=nxt[1],
-                        xs_next=self.xs[dst_par], xts_next=self.xts[dst_par],
-                        ipc_table=self.ipc.table_ptr() if self.ipc is not None else 0, ipc_W=self.W,
-                        ipc_rank=self.rank)
+        dst = par ^ 1
+        ipc = dict(ipc_table=self.ipc.table_ptr() if self.ipc is not None else 0, ipc_W=self.W, ipc_rank=self.rank)
+        if self.precision == "fp32":
+            st = self.stages[par][off * self.rec_s:] if nsteps > 0 else self.stages[par]
+            t.C.mlp_persist_f32(st, ep.rec, t.B, nsteps, t.params, t.lr, t.metrics, t.gstep, self.seq, self.xbuf,
+                                self.err, self.timeout_s, t.act, int(t.naive), host=ep.host,
+                                host_offset=nxt[0] * ep.rec, next_steps=nxt[1], stage_next=self.stages[dst],
+                                step_ts=self.step_ts, grad_bf16=self.grad_bf16, **ipc)
+        else:
+            xs = self.xs[par][off * self.rec_s:] if nsteps > 0 else self.xs[par]
+            xts = self.xts[par][off * self.xtb:] if nsteps > 0 else self.xts[par]
+            t.C.mlp_persist(xs, xts, ep.rec, t.B, nsteps, t.params, t.lr, t.metrics, t.gstep,
+                            self.seq, self.gran, self.err, self.timeout_s, t.act, int(t.naive),
+                            host=ep.host, host_offset=nxt[0] * ep.rec, next_steps=nxt[1],
+                            xs_next=self.xs[dst], xts_next=self.xts[dst], step_ts=self.step_ts, **ipc)
+        if nxt[1] > 0:
+            self.staged[dst] = nxt
+        self.last_prefetch_steps = nxt[1]
+
+    def _locate(self, b0: int, g: int) -> Optional[Tuple[int, int]]:
+        for par in (0, 1):
+            s = self.staged[par]
+            if s is not None and s[0] <= b0 and b0 + g <= s[0] + s[1]:
+                return par, b0 - s[0]
+        return None
+
+    def _ensure(self, b0: int, g: int) -> Tuple[int, int]:
+        """(stage, offset) holding steps [b0, b0+g); copy-only launch on a miss."""
+        loc = self._locate(b0, g)
+        if loc is None:
+            # cold start / plan change: copy (b0, g) into a stage buffer with a
+            # copy-only launch (the stage it "runs" from is untouched)
+            dst = 0 if self.staged[0] is None else (1 if self.staged[1] is None else 0)
+            par = dst ^ 1
+            self._launch(par, 0, 0, (b0, g))
+            self.copy_only_launches += 1
+            loc = (par ^ 1, 0)
+        return loc
 
     def prepare(self, steps: int):
-        """Nothing to capture (kept for the MLPStepRunner interface)."""
+        """Stage the first chunk of the next `run(steps)` (outside any timed region)."""
+        b0, g = self._chunks(self.cursor, steps)[0]
+        self._ensure(b0, g)
+
+    def invalidate(self):
+        """Forget staged chunks (call after re-packing the pinned epoch, e.g. a shuffle)."""
+        self.staged = [None, None]
 
     def error(self) -> int:
         return int(self.err.item())
 
-    def run(self, steps: int, events: Optional[list] = None):
+    def run(self, steps: int, events: Optional[list] = None, lookahead: Optional[int] = None):
         main = torch.cuda.current_stream()
         ch = self._chunks(self.cursor, steps)
-        after = self._chunks(self.cursor + steps, self.g)[0]   # speculative next chunk
+        la = min(self.g, steps if lookahead is None else int(lookahead))
         for k, (b0, g) in enumerate(ch):
-            nxt = ch[k + 1] if k + 1 < len(ch) else after
-            par = self.parity
-            if self.loaded != (b0, g):   # cold start / plan change: copy-only launch
-                self._launch(par, 0, (b0, g), par)
-            self._launch(par, g, nxt, par ^ 1)
+            if k + 1 < len(ch):
+                nxt = ch[k + 1]
+            else:
+                nxt = self._chunks(self.cursor + g, la)[0] if la > 0 else (0, 0)
+            par, off = self._ensure(b0, g)
+            if nxt[1] > 0 and self.staged[par ^ 1] is not None and self._covers(self.staged[par ^ 1], nxt):
+                nxt_copy = (nxt[0], 0)      # already resident in the other stage: nothing to stream
+            else:
+                nxt_copy = nxt
+            self._launch(par, off, g, nxt_copy)
             if events is not None:
                 ev = torch.cuda.Event(enable_timing=True)
                 ev.record(main)
                 events.append((ev, g))
-            self.parity = par ^ 1
-            self.loaded = nxt
             self.cursor += g
         self.t.shadows_stale = True
+
+    @staticmethod
+    def _covers(s: Tuple[int, int], r: Tuple[int, int]) -> bool:
+        return s[0] <= r[0] and r[0] + r[1] <= s[0] + s[1]
+
+    def step_times_ms(self, first: int, last: int) -> np.ndarray:
+        """Per-step durations (ms) of global steps [first, last) from the device stamps."""
+        if last - first >= self.TS_RING:
+            first = last - self.TS_RING + 1
+        ts = self.step_ts.cpu().numpy()
+        idx = np.arange(first, last + 1) % self.TS_RING
+        return np.diff(ts[idx]).astype(np.float64) * 1e-5     # 100 MHz ticks -> ms

@@ -215,7 +215,7 @@ def run_persistent_worker(server, mnist, tr):
     for ep in range(FLAGS.training_epochs):
         if ep:
             epoch.shuffle(seed=1000 * FLAGS.task_index + ep)
-            run.loaded = None            # the staged chunk came from the previous packing
+            run.invalidate()             # the staged chunks came from the previous packing
         n = batch_count if not FLAGS.max_steps else min(batch_count, FLAGS.max_steps - steps)
         if n <= 0:
             break
@@ -225,9 +225,11 @@ def run_persistent_worker(server, mnist, tr):
         if run.error():
             raise RuntimeError("persistent kernel exchange timed out")
         m = tr.read_metrics(g0, g0 + n)
+        dt = run.step_times_ms(g0, g0 + n)   # device per-step stamps (example.py:174-183 AvgTime)
         for i in range(n):
             if (steps + i + 1) % FLAGS.frequency == 0 or i + 1 == batch_count:
-                print(step_line(steps + i + 1, g0 + i + 1, ep + 1, i + 1, batch_count, float(m[i][0]), 0.0),
+                avg = float(dt[max(0, i + 1 - FLAGS.frequency):i + 1].mean())
+                print(step_line(steps + i + 1, g0 + i + 1, ep + 1, i + 1, batch_count, float(m[i][0]), avg),
                       flush=True)
         loss = float(m[-1][0])
         steps += n

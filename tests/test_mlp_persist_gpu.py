@@ -1,5 +1,6 @@
-"""Persistent weight-stationary MLP kernel (csrc/kernels/mlp_persist.hip) vs the
-plain PyTorch fp32 reference of example.py's step (models/mlp.reference_step)."""
+"""Persistent weight-stationary MLP kernels (csrc/kernels/mlp_persist_f32.hip,
+the fp32 default, and csrc/kernels/mlp_persist.hip, fp16 operands) vs the plain
+PyTorch fp32 reference of example.py's step (models/mlp.reference_step)."""
 import numpy as np
 import pytest
 import torch
@@ -25,13 +26,97 @@ def _ref_run(p0, imgs, labels, B, batches, lr, act="sigmoid"):
 
 @pytest.mark.parametrize("B", [100, 37, 112])
 @pytest.mark.parametrize("act", ["sigmoid", "relu"])
+def test_persist_f32_one_step_gradient_fp32_exact(native, B, act):
+    """fp32 engine: every parameter's gradient within 1e-5 (relative, per tensor)
+    of the fp32 autograd reference.  lr = 1000 makes lr*g >> ulp(W), so the
+    gradient recovered from the update is accurate to ~1e-8."""
+    imgs, labels = synthetic_mnist(B, seed=11)
+    dev = torch.device("cuda")
+    lr = 1000.0
+    tr = mlp.FusedMLPTrainer(batch_size=B, lr=lr, act=act, device=dev)
+    p0 = tr.get_params().clone()
+    ep = PinnedEpoch(imgs, labels, B)
+    run = mlp.PersistentMLPRunner(tr, ep, steps_per_launch=1, precision="fp32")
+    run.run(1)
+    torch.cuda.synchronize()
+    assert run.error() == 0
+    assert tr.global_step == 1
+    x = torch.from_numpy(imgs).float() / 255.0
+    loss, acc, g = mlp.reference_loss_and_grad(p0, x, torch.from_numpy(labels), act)
+    g_k = (p0.double() - tr.get_params().double()) / lr
+    for name, (off, shape) in mlp.PARAM_SPECS.items():
+        n = int(np.prod(shape))
+        a, b = g_k[off:off + n], g[off:off + n].double()
+        rel = ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+        assert rel < 1e-5, (name, rel)
+    m = tr.read_metrics(0, 1)[0]
+    assert abs(m[0] - loss.item()) < 1e-5 * max(1.0, abs(loss.item())), (m, loss)
+    assert abs(m[1] - acc.item()) < 1e-6
+
+
+def test_persist_f32_multi_step_matches_reference(native):
+    """11 steps over wrapping chunks (cold start, in-kernel prefetch, offsets into
+    a staged chunk, epoch wrap): fp32 engine tracks fp32 SGD to ~1e-6."""
+    B, nb = 100, 6
+    imgs, labels = synthetic_mnist(B * nb, seed=12)
+    dev = torch.device("cuda")
+    lr = 0.05
+    tr = mlp.FusedMLPTrainer(batch_size=B, lr=lr, device=dev)
+    p0 = tr.get_params().clone()
+    ep = PinnedEpoch(imgs, labels, B)
+    run = mlp.PersistentMLPRunner(tr, ep, steps_per_launch=4, precision="fp32")
+    run.run(7)     # (0,4) cold copy, (4,2), (0,1) epoch wrap; speculative (1,4) staged
+    run.run(2)     # (1,2): inside the staged (1,4); streams (3,2) into the other stage
+    run.run(2)     # (3,2): staged by the previous launch
+    torch.cuda.synchronize()
+    assert run.error() == 0
+    assert tr.global_step == 11
+    assert run.copy_only_launches == 1
+    batches = [0, 1, 2, 3, 4, 5, 0, 1, 2, 3, 4]
+    p_ref, losses, accs = _ref_run(p0, imgs, labels, B, batches, lr)
+    d_k = tr.get_params().double() - p0.double()
+    d_r = p_ref.double() - p0.double()
+    rel = ((d_k - d_r).norm() / d_r.norm()).item()
+    assert rel < 2e-5, rel
+    m = tr.read_metrics(0, 11)
+    assert np.allclose(m[:, 0], losses, rtol=1e-5, atol=1e-5), (m[:, 0], losses)
+    assert np.allclose(m[:, 1], accs, atol=1e-6)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "fp16"])
+def test_persist_short_timed_run_streams_only_what_it_computes(native, precision):
+    """The bench's pattern: warmup(5) primes exactly the timed run's chunk; the
+    timed run(20) needs no copy-only launch and prefetches <= 20 steps; the
+    per-step device stamps give 20 positive durations."""
+    B = 100
+    imgs, labels = synthetic_mnist(B * 550, seed=15)
+    dev = torch.device("cuda")
+    tr = mlp.FusedMLPTrainer(batch_size=B, lr=0.0005, device=dev)
+    ep = PinnedEpoch(imgs, labels, B)
+    run = mlp.PersistentMLPRunner(tr, ep, steps_per_launch=550, precision=precision)
+    run.prepare(5)
+    run.run(5, lookahead=20)
+    torch.cuda.synchronize()
+    cold = run.copy_only_launches
+    s0 = tr.global_step
+    run.run(20)
+    torch.cuda.synchronize()
+    assert run.error() == 0
+    assert run.copy_only_launches == cold
+    assert 0 < run.last_prefetch_steps <= 20
+    dt = run.step_times_ms(s0, s0 + 20)
+    assert dt.shape == (20,) and (dt > 0).all() and (dt < 1.0).all(), dt
+
+
+@pytest.mark.parametrize("B", [100, 37, 112])
+@pytest.mark.parametrize("act", ["sigmoid", "relu"])
 def test_persist_one_step_gradient(native, B, act):
     imgs, labels = synthetic_mnist(B, seed=11)
     dev = torch.device("cuda")
     tr = mlp.FusedMLPTrainer(batch_size=B, lr=1.0, act=act, device=dev)
     p0 = tr.get_params().clone()
     ep = PinnedEpoch(imgs, labels, B)
-    run = mlp.PersistentMLPRunner(tr, ep, steps_per_launch=1)
+    run = mlp.PersistentMLPRunner(tr, ep, steps_per_launch=1, precision="fp16")
     run.run(1)
     torch.cuda.synchronize()
     assert run.error() == 0
@@ -59,9 +144,9 @@ def test_persist_chunks_wrap_and_match_reference(native):
     tr = mlp.FusedMLPTrainer(batch_size=B, lr=lr, device=dev)
     p0 = tr.get_params().clone()
     ep = PinnedEpoch(imgs, labels, B)
-    run = mlp.PersistentMLPRunner(tr, ep, steps_per_launch=4)
+    run = mlp.PersistentMLPRunner(tr, ep, steps_per_launch=4, precision="fp16")
     run.run(7)     # chunks (0,4) (4,2) (0,1): copy-only cold start, in-kernel copies, epoch wrap
-    run.run(4)     # (1,3) (4,1): plan change -> copy-only launch again
+    run.run(4)     # (1,3) (4,1): inside / outside the staged speculative chunk
     torch.cuda.synchronize()
     assert run.error() == 0
     assert tr.global_step == 11
@@ -76,7 +161,8 @@ def test_persist_chunks_wrap_and_match_reference(native):
     assert np.allclose(m[:, 1], accs, atol=1e-6)
 
 
-def test_persist_deterministic_and_hands_over_to_step_path(native):
+@pytest.mark.parametrize("precision", ["fp32", "fp16"])
+def test_persist_deterministic_and_hands_over_to_step_path(native, precision):
     B = 100
     imgs, labels = synthetic_mnist(B * 4, seed=13)
     dev = torch.device("cuda")
@@ -84,7 +170,7 @@ def test_persist_deterministic_and_hands_over_to_step_path(native):
     for _ in range(2):
         tr = mlp.FusedMLPTrainer(batch_size=B, lr=0.01, device=dev)
         ep = PinnedEpoch(imgs, labels, B)
-        run = mlp.PersistentMLPRunner(tr, ep, steps_per_launch=3)
+        run = mlp.PersistentMLPRunner(tr, ep, steps_per_launch=3, precision=precision)
         run.run(5)
         torch.cuda.synchronize()
         outs.append(tr.get_params())
@@ -102,14 +188,15 @@ def test_persist_deterministic_and_hands_over_to_step_path(native):
     assert ((g_k - g).norm() / g.norm()).item() < 3e-2
 
 
-def test_persist_long_run_learns(native):
-    """1000 steps at the reference's lr on synthetic MNIST: loss goes down."""
+@pytest.mark.parametrize("precision", ["fp32", "fp16"])
+def test_persist_long_run_learns(native, precision):
+    """1000 steps on synthetic MNIST: loss goes down."""
     B = 100
     imgs, labels = synthetic_mnist(B * 50, seed=14)
     dev = torch.device("cuda")
     tr = mlp.FusedMLPTrainer(batch_size=B, lr=0.05, device=dev)
     ep = PinnedEpoch(imgs, labels, B)
-    run = mlp.PersistentMLPRunner(tr, ep, steps_per_launch=50)
+    run = mlp.PersistentMLPRunner(tr, ep, steps_per_launch=50, precision=precision)
     run.run(1000)
     torch.cuda.synchronize()
     assert run.error() == 0
@@ -118,8 +205,9 @@ def test_persist_long_run_learns(native):
     assert m[-50:, 0].mean() < 0.7 * m[:50, 0].mean(), (m[:50, 0].mean(), m[-50:, 0].mean())
 
 
+@pytest.mark.parametrize("precision,grad", [("fp32", "bf16"), ("fp32", "fp32"), ("fp16", "bf16")])
 @pytest.mark.parametrize("nproc", [2, 3])
-def test_persist_multi_rank_same_gpu(native, nproc):
+def test_persist_multi_rank_same_gpu(native, nproc, precision, grad):
     """N ranks sharing cuda:0: in-kernel IPC exchange, bit-identical replicas, sync-SGD math."""
     import json
     import os
@@ -134,7 +222,7 @@ def test_persist_multi_rank_same_gpu(native, nproc):
     s.close()
     cmd = [sys.executable, "-m", "torch.distributed.run", f"--nproc-per-node={nproc}", "--master-addr=127.0.0.1",
            f"--master-port={port}", os.path.join(repo, "scripts", "persist_selftest.py"), "--same-gpu",
-           "--steps=10", "--per-launch=4"]
+           "--steps=10", "--per-launch=4", f"--precision={precision}", f"--grad-dtype={grad}"]
     env = dict(os.environ, PYTHONPATH=repo, OMP_NUM_THREADS="2")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=100, env=env)
     out = r.stdout + r.stderr

@@ -59,8 +59,10 @@ def main(argv=None):
     ap.add_argument("--batch", type=int, default=100, help="per-GPU batch (reference: 100)")
     ap.add_argument("--lr", type=float, default=0.0005)
     ap.add_argument("--steps-per-graph", type=int, default=50, help="3-launch path: steps per captured hipGraph")
-    ap.add_argument("--precision", choices=["fp32", "fp16"], default="fp32",
-                    help="persistent engine operand precision (reference: fp32)")
+    ap.add_argument("--precision", choices=["fp32", "fp32-split", "fp16"], default="fp32",
+                    help="persistent engine (reference precision: fp32): fp32 = f32-input MFMA for every product; "
+                         "fp32-split = exact 3-way bf16 split of every fp32 GEMM operand (exact products, fp32 "
+                         "accumulate); fp16 = f16 MFMA operands")
     ap.add_argument("--exchange-timeout", type=float, default=30.0,
                     help="in-kernel exchange wait bound (s); a cold multi-GPU start can skew ranks by seconds")
     ap.add_argument("--steps-per-launch", type=int, default=550,
@@ -261,7 +263,7 @@ def main(argv=None):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": (a.precision if persistent else "bf16"),
+            "dtype": (("fp32" if a.precision.startswith("fp32") else a.precision) if persistent else "bf16"),
             "data": ("synthetic MNIST-shaped uint8 resident in pinned host memory, streamed per chunk over PCIe "
                      + ("by copier workgroups inside the persistent launch" if persistent else
                         "by hipMemcpyAsync inside the chunk's hipGraph") + "; random-init weights"),
@@ -283,9 +285,13 @@ def main(argv=None):
                 "input_prefetch": "in-kernel copier workgroups" if persistent else a.prefetch,
                 "activation": a.act,
                 "exchange_tuning_us_per_step": tuned or None,
-                "precision": (("fp32 MFMA operands (v_mfma_f32_16x16x4_f32, exact f32 products), fp32 accumulate, "
-                               "fp32 master weights" if a.precision == "fp32" else
-                               "fp16 MFMA operands (pixels exact as 1024+u), fp32 accumulate, fp32 master weights")
+                "precision": ({"fp32-split": "fp32 GEMMs as exact 3-way bf16 splits (hi+mid+lo == each fp32 "
+                                             "weight / gradient, uint8 pixels exact): exact products, fp32 "
+                                             "accumulate; head on v_mfma_f32_16x16x4_f32; fp32 master weights",
+                               "fp32": "fp32 MFMA operands (v_mfma_f32_16x16x4_f32, exact f32 products), "
+                                       "fp32 accumulate, fp32 master weights",
+                               "fp16": "fp16 MFMA operands (pixels exact as 1024+u), fp32 accumulate, fp32 master "
+                                       "weights"}[a.precision]
                               if persistent else "bf16 MFMA operands, fp32 accumulate, fp32 master weights"),
             },
             "final_loss": round(float(m[0]), 5),

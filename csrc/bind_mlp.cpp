@@ -48,7 +48,15 @@ hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int n
                                 float* metrics, int ring, int act, int naive, long long* gstep, unsigned long long* seq,
                                 void* xbuf, int* err, long long timeout, long long* step_ts, int ts_ring,
                                 const void* host_next, int next_steps, void* stage_next, void* const* peer_base, int W,
-                                int rank, int gbf16, hipStream_t stream);
+                                int rank, int gbf16, long long* phase_ts, int spread, hipStream_t stream);
+long long dtfk_mlpx_stage_rec();
+long long dtfk_mlpx_xbuf_bytes();
+long long dtfk_mlpx_ipc_bytes();
+hipError_t dtfk_mlp_persist_x3(const void* stage, long long rec_h, int B, int nsteps, float* params, const float* lr,
+                               float* metrics, int ring, int act, int naive, long long* gstep, unsigned long long* seq,
+                               void* xbuf, int* err, long long timeout, long long* step_ts, int ts_ring,
+                               const void* host_next, int next_steps, void* stage_next, void* const* peer_base, int W,
+                               int rank, int gbf16, long long* phase_ts, int spread, hipStream_t stream);
 hipError_t dtfk_mlp_fwd_head(const void* x, int x_kind, int B, const void* W1T, float* z2p, const void* labels,
                              const void* W2T, const void* W2N, const float* params, void* dz2T, int BP,
                              float* partials, float inv_batch, int act, int naive_loss, int* counters,
@@ -348,7 +356,8 @@ void mlp_persist(at::Tensor xs, at::Tensor xts, int64_t rec, int B, int nsteps, 
             "mlp_persist");
 }
 
-// fp32 persistent engine (csrc/kernels/mlp_persist_f32.hip): `nsteps` SGD steps of
+// fp32 persistent engines: csrc/kernels/mlp_persist_f32.hip (f32-input MFMA) or, with
+// exact_split, csrc/kernels/mlp_persist_x3.hip (exact 3-way bf16 split): `nsteps` SGD steps of
 // the chunk staged in `stage` (records of mlpf_stage_rec() bytes) and, in the same
 // launch, `next_steps` host records from byte `host_off` of the pinned epoch into
 // `stage_next`.  nsteps = 0: copy only.  xbuf: exchange buffer (zeroed once).
@@ -356,20 +365,21 @@ void mlp_persist_f32(at::Tensor stage, int64_t rec_h, int B, int nsteps, at::Ten
                      at::Tensor metrics, at::Tensor gstep, at::Tensor seq, at::Tensor xbuf, at::Tensor err,
                      double timeout_s, int act, int naive, c10::optional<at::Tensor> host, int64_t host_off,
                      int next_steps, c10::optional<at::Tensor> stage_next, c10::optional<at::Tensor> step_ts,
-                     int64_t ipc_table, int ipc_W, int ipc_rank, bool grad_bf16) {
+                     int64_t ipc_table, int ipc_W, int ipc_rank, bool grad_bf16,
+                     c10::optional<at::Tensor> phase_ts, bool spread, bool exact_split) {
   if (ipc_W > 1 && (ipc_table == 0 || ipc_rank < 0 || ipc_rank >= ipc_W || ipc_W > 64))
     throw std::runtime_error("mlp_persist_f32: N-GPU exchange needs the IPC peer table");
   if (B <= 0 || B > dtfk_mlpf_max_batch()) throw std::runtime_error("mlp_persist_f32: B out of range");
   if (rec_h < (int64_t)B * 785 || rec_h % 16 != 0) throw std::runtime_error("mlp_persist_f32: bad host record size");
   if (nsteps < 0 || next_steps < 0) throw std::runtime_error("mlp_persist_f32: negative step count");
-  const int64_t rec_s = dtfk_mlpf_stage_rec();
+  const int64_t rec_s = exact_split ? dtfk_mlpx_stage_rec() : dtfk_mlpf_stage_rec();
   need(stage, at::kByte, (int64_t)std::max(nsteps, 1) * rec_s, "stage");
   need(params, at::kFloat, kNParam, "params");
   need(lr, at::kFloat, 1, "lr");
   need(metrics, at::kFloat, 2, "metrics");
   need(gstep, at::kLong, 1, "gstep");
   need(seq, at::kLong, 1, "seq");
-  need(xbuf, at::kByte, dtfk_mlpf_xbuf_bytes(), "xbuf");
+  need(xbuf, at::kByte, exact_split ? dtfk_mlpx_xbuf_bytes() : dtfk_mlpf_xbuf_bytes(), "xbuf");
   need(err, at::kInt, 1, "err");
   if (((uintptr_t)stage.data_ptr() | (uintptr_t)xbuf.data_ptr()) % 16 != 0)
     throw std::runtime_error("mlp_persist_f32: stage / xbuf must be 16-byte aligned");
@@ -387,13 +397,15 @@ void mlp_persist_f32(at::Tensor stage, int64_t rec_h, int B, int nsteps, at::Ten
   int ts_ring = 1;
   long long* sts = step_ts_ptr(step_ts, &ts_ring);
   const long long ticks = (long long)(timeout_s * 1e8);   // s_memrealtime: 100 MHz
-  hip_check(dtfk_mlp_persist_f32(stage.data_ptr(), rec_h, B, nsteps, params.data_ptr<float>(), lr.data_ptr<float>(),
-                                 metrics.data_ptr<float>(), (int)(metrics.numel() / 2), act, naive,
-                                 reinterpret_cast<long long*>(gstep.data_ptr<int64_t>()),
-                                 reinterpret_cast<unsigned long long*>(seq.data_ptr<int64_t>()), xbuf.data_ptr(),
-                                 err.data_ptr<int>(), ticks, sts, ts_ring, hn, next_steps, sn,
-                                 reinterpret_cast<void* const*>(ipc_table), ipc_W > 1 ? ipc_W : 1,
-                                 ipc_W > 1 ? ipc_rank : 0, grad_bf16 ? 1 : 0, cur_stream()),
+  auto launch = exact_split ? dtfk_mlp_persist_x3 : dtfk_mlp_persist_f32;
+  hip_check(launch(stage.data_ptr(), rec_h, B, nsteps, params.data_ptr<float>(), lr.data_ptr<float>(),
+                   metrics.data_ptr<float>(), (int)(metrics.numel() / 2), act, naive,
+                   reinterpret_cast<long long*>(gstep.data_ptr<int64_t>()),
+                   reinterpret_cast<unsigned long long*>(seq.data_ptr<int64_t>()), xbuf.data_ptr(),
+                   err.data_ptr<int>(), ticks, sts, ts_ring, hn, next_steps, sn,
+                   reinterpret_cast<void* const*>(ipc_table), ipc_W > 1 ? ipc_W : 1,
+                   ipc_W > 1 ? ipc_rank : 0, grad_bf16 ? 1 : 0, ts_ptr(phase_ts, 64 * 64 * 16),
+                   spread ? 1 : 0, cur_stream()),
             "mlp_persist_f32");
 }
 
@@ -409,7 +421,11 @@ void init_mlp(py::module& m) {
         py::arg("err"), py::arg("timeout_s"), py::arg("act"), py::arg("naive"), py::arg("host") = py::none(),
         py::arg("host_offset") = 0, py::arg("next_steps") = 0, py::arg("stage_next") = py::none(),
         py::arg("step_ts") = py::none(), py::arg("ipc_table") = 0, py::arg("ipc_W") = 1, py::arg("ipc_rank") = 0,
-        py::arg("grad_bf16") = true);
+        py::arg("grad_bf16") = true, py::arg("phase_ts") = py::none(), py::arg("spread") = false,
+        py::arg("exact_split") = false);
+  m.def("mlpx_stage_rec", &dtfk_mlpx_stage_rec);
+  m.def("mlpx_xbuf_bytes", &dtfk_mlpx_xbuf_bytes);
+  m.def("mlpx_ipc_bytes", &dtfk_mlpx_ipc_bytes);
   m.def("mlpf_stage_rec", &dtfk_mlpf_stage_rec);
   m.def("mlpf_xbuf_bytes", &dtfk_mlpf_xbuf_bytes);
   m.def("mlpf_ipc_bytes", &dtfk_mlpf_ipc_bytes);

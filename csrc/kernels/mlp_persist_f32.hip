@@ -6,50 +6,57 @@
 //
 // The f32-input MFMA runs at 1/16 of the f16 rate, so where the f16 engine
 // (mlp_persist.hip) keeps a hidden block per CU, this one spreads each block's
-// weights over 7 CUs:
+// weights over 4 CUs:
 //
-//  * 49 compute workgroups (512 threads) c = (j, q): hidden block j (units
-//    16j..16j+15, 7 blocks) x feature slice q (7 tiles of 16 features, 49 tiles
-//    = 784 exactly).  Wave t < 7 OWNS feature tile 7q+t of block j: 4 fp32 VGPRs
-//    per lane hold W1[16(7q+t)+4g+e][16j+r] (r = lane&15, g = lane>>4), which is
-//    at once its forward A operand (k-step e) and the C layout of its weight
-//    gradient, so the SGD update is in-register.
+//  * 28 compute workgroups (512 threads) c = (j, q): hidden block j (units
+//    16j..16j+15, 7 blocks) x feature slice q (13, 12, 12, 12 tiles of 16
+//    features; 49 tiles = 784 exactly).  Wave w owns local tiles w and w + 8 of
+//    the slice: 4 fp32 VGPRs per lane and tile hold W1[16t+4g+e][16j+r]
+//    (r = lane&15, g = lane>>4), which is at once its forward A operand
+//    (k-step e) and the C layout of its weight gradient, so the SGD update is
+//    in-register.
 //  * per step:
-//      P0  forward partial z^T[hidden][batch] of tile t for all 7 batch tiles
-//          (28 MFMAs, 7 independent chains) -> LDS; the 7 tiles are summed in a
-//          fixed order (wave w: batch tile w).
-//      E1  the slice partial of (j, batch tile w) goes to the 6 other slices of
-//          block j (16-byte write-through stores + per-wave tag flag, 1 KB);
-//          everyone sums the 7 slices in slice order -> identical z in all 7.
+//      P0  forward partial z^T[hidden][batch] of the wave's tiles for all 7
+//          batch tiles (7 independent MFMA chains) -> LDS; wave w (batch tile
+//          w) sums the 8 waves' partials in a fixed order.
+//      E1  the slice partial of (j, batch tile w) goes to the 3 other slices of
+//          block j as tagged 8-byte granules (the data is the flag); everyone
+//          sums the 4 slices in slice order -> identical z in all 4.
 //      P1  a2 = act(z/255 + b1), partial logits^T of block j (4 MFMAs; a2 is
 //          the B operand straight from the accumulator layout).
 //      E2  partial logits go to the workgroup of the same slice in every other
-//          block; logits = b2 + sum_j (block order) -> identical in all 49.
+//          block; logits = b2 + sum_j (block order) -> identical in all 28.
 //          softmax / cross-entropy / argmax, dz3, da2 = W2 dz3 (4 MFMAs),
 //          dz2 = da2 * act' -> LDS.
-//      P2  wave t: dW1 tile = x^T dz2 over the batch (28 MFMAs, x^T bytes from
+//      P2  dW1 tiles = x^T dz2 over the batch (28 MFMAs per tile, x^T bytes from
 //          the feature-major stage copy), W1 -= lr/(255 B) dW1 in registers;
-//          wave 7: dW2 (28 MFMAs), db1, db2, metrics, update of the LDS copies
-//          of W2[block j], b1[block j], b2 -- identical in every workgroup that
-//          holds them (same inputs, same order), so no exchange is needed.
+//          wave 7 also: dW2 (28 MFMAs), db1, db2, metrics, update of the LDS
+//          copies of W2[block j], b1[block j], b2 -- identical in every
+//          workgroup that holds them (same inputs, same order).
 //    Two LDS barriers and two inter-workgroup edges per step; the data of
 //    every edge is double-buffered by step parity and tagged with the global
 //    exchange sequence number, so buffers are never reset between launches.
 //  * x enters the MFMAs as exact integers 0..255 (v_cvt_f32_ubyte); the 1/255
 //    pixel scale and the 1/B loss mean are applied to the fp32 sums.
-//  * the remaining 15 workgroups are COPIERS: while the compute workgroups run
-//    chunk c they pull chunk c+1 from pinned host memory over PCIe into the
-//    other device stage (row-major x, feature-major x^T, labels).
+//  * 16 COPIER workgroups pull chunk c+1 from pinned host memory over PCIe into
+//    the other device stage (row-major x, feature-major x^T, labels) while the
+//    compute workgroups run chunk c.
 //  * N GPUs (MULTI): after P2 every compute workgroup exchanges its gradient
-//    (7 dW1 tiles + the block's small gradients) with the same workgroup on
-//    every peer through IPC-mapped uncached buffers -- 49 CUs per GPU carry the
+//    (its dW1 tiles + the block's small gradients) with the same workgroup on
+//    every peer through IPC-mapped uncached buffers -- 28 CUs per GPU carry the
 //    peer traffic -- and sums the ranks in rank order (bit-identical replicas).
 //
-// Placement: workgroup (j, q) runs as blockIdx j + 8q, so under the observed
-// round-robin dispatch the 7 slices of block j share an XCD (E1 stays in one
-// L2).  Speed only: every hand-off uses write-through stores and L1-bypassing
-// loads, correct under any placement.
+// Placement: packed (default) runs workgroup c as blockIdx 8c, so under the
+// observed round-robin dispatch all 28 share one XCD and both edges stay in one
+// L2 (plain stores); spread (several ranks on one GPU: tests) runs them as
+// blocks 0..27.  A per-launch census of HW_REG_XCC_ID picks each edge's store
+// flavour (plain if L2-local, write-through otherwise): speed only, never
+// correctness.  Measured on MI355X (profiles/): ~13 us/step; the per-step
+// critical path is the two hops (~1.3 and ~1.9 us after the last producer)
+// plus producer skew, not the MFMA phases (~1.6 + 1.8 us).
 #include "common.h"
+
+#include <cstdlib>
 
 namespace dtfk {
 namespace mlpf {
@@ -59,15 +66,18 @@ typedef __attribute__((address_space(1))) unsigned gu32;
 
 constexpr int DIN = 784, HID = 100, NCLS = 10;
 constexpr int NJ = 7;              // hidden blocks of 16
-constexpr int NQ = 7;              // feature slices
-constexpr int NT = 7;              // feature tiles (of 16) per slice = MFMA waves
+constexpr int NQ = 4;              // feature slices: 13, 12, 12, 12 tiles of 16 features (49 = 784 / 16)
+constexpr int NTW = 2;             // feature tiles per wave (local tiles w and w + 8)
 constexpr int NBT = 7;             // batch tiles of 16 (B <= 112)
 constexpr int BROWS = 16 * NBT;    // 112
 constexpr int XTS = 128;           // x^T row stride (batch padded)
-constexpr int NCOMP = NJ * NQ;     // 49
+constexpr int NCOMP = NJ * NQ;     // 28 compute workgroups: one XCD
 constexpr int THREADS = 512;
-constexpr int GRID = 64;           // 49 compute + 15 copier workgroups
-constexpr int NCOP = GRID - NCOMP;
+constexpr int NCOP = 16;           // copier workgroups
+constexpr int GRID_PACKED = 8 * NCOMP;
+constexpr int GRID_SPREAD = NCOMP + NCOP;
+__host__ __device__ constexpr int tile0(int q) { return q == 0 ? 0 : 13 + 12 * (q - 1); }
+__host__ __device__ constexpr int ntile(int q) { return q == 0 ? 13 : 12; }
 constexpr int OFF_W2 = 78400, OFF_B1 = 79400, OFF_B2 = 79500;
 
 // device stage record of one step
@@ -75,27 +85,28 @@ constexpr long long XROW_BYTES = (long long)BROWS * DIN;   // [112][784] u8, row
 constexpr long long XT_BYTES = (long long)DIN * XTS;       // [784][128] u8, batch >= B zero
 constexpr long long REC = XROW_BYTES + XT_BYTES + 128;     // + labels [128]
 
-// exchange buffer (bytes): flags F1 [2][NJ][NBT][8] u32, F2 [2][NQ][NBT][8] u32,
-// payloads E1 [2][NJ][NQ][NBT] x 1 KB, E2 [2][NQ][NBT][NJ] x 1 KB
-constexpr int SLOT = 1024;
-constexpr long long F1_OFF = 0;
-constexpr long long F2_OFF = F1_OFF + 2 * NJ * NBT * 8 * 4;
-constexpr long long E1_OFF = 8192;
-constexpr long long E2_OFF = E1_OFF + 2LL * NJ * NQ * NBT * SLOT;
-constexpr long long XBUF_BYTES = E2_OFF + 2LL * NQ * NBT * NJ * SLOT;
+// exchange buffer (bytes): every payload float travels as an 8-byte granule
+// {value, tag} (the data is the flag: no separate flag word, no drain before a
+// flag, one hop); a slot = 64 lanes x 4 granules = 2 KB.
+// E1 [2][NJ][NQ][NBT] slots, E2 [2][NQ][NBT][NJ] slots
+constexpr int GSLOT = 2048;
+constexpr long long E1_OFF = 0;
+constexpr long long E2_OFF = E1_OFF + 2LL * NJ * NQ * NBT * GSLOT;
+constexpr long long HDR_OFF = E2_OFF + 2LL * NQ * NBT * NJ * GSLOT;   // [64] u64 placement census
+constexpr long long XBUF_BYTES = HDR_OFF + 64 * 8;
 
 // IPC buffer of one rank (N GPUs): [flags: workgroup c at byte 64c][2 parities][49 slots]
 // slot: 7 dW1 tiles x 64 lanes x 16 B (fp32; bf16 payload uses the first 8 B of
 // each 16) | dW2 64 lanes x 16 B | db1 (16) db2 (16) fp32
 constexpr int IPC_FLAGS = 4096;
-constexpr int IPC_SMALL = NT * 64 * 16;
+constexpr int IPC_SMALL = 8 * NTW * 64 * 16;
 constexpr int IPC_SLOT = IPC_SMALL + 1024 + 128;
 constexpr long long IPC_BYTES = IPC_FLAGS + 2LL * NCOMP * IPC_SLOT;
 
 // LDS carve (compute); the copier reuses the same dynamic allocation
 constexpr int LS = BROWS + 4;                          // [16][LS] fp32 images (float4-aligned rows)
-constexpr int L_ZBUF = 0;                              // [NT][NBT][64] f32x4 forward partials  50176
-constexpr int L_A2T = L_ZBUF + NT * NBT * 64 * 16;     // [16 hidden][LS] a2
+constexpr int L_ZBUF = 0;                              // [8 waves][NBT][64] f32x4 forward partials  57344
+constexpr int L_A2T = L_ZBUF + 8 * NBT * 64 * 16;      // [16 hidden][LS] a2
 constexpr int L_DZ2T = L_A2T + 16 * LS * 4;            // [16 hidden][LS] dz2
 constexpr int L_DZ3T = L_DZ2T + 16 * LS * 4;           // [16 class][LS] dz3
 constexpr int L_W2 = L_DZ3T + 16 * LS * 4;             // [16 hidden][16 class] W2 of block j
@@ -121,7 +132,7 @@ struct Args {
   int act, naive;
   long long* gstep;
   unsigned long long* seq;  // exchange sequence number (monotonic across launches)
-  uint8_t* xbuf;            // exchange buffer (XBUF_BYTES, zeroed once)
+  uint8_t* xbuf;            // granule exchange buffer (XBUF_BYTES, zeroed once)
   int* err;
   long long timeout;        // s_memrealtime ticks (100 MHz)
   long long* step_ts;       // optional: s_memrealtime at the start of every global step (ring)
@@ -132,7 +143,14 @@ struct Args {
   void* const* peer_base;   // N GPUs: IPC-mapped exchange buffers of every rank
   int W, rank;
   int gbf16;                // N GPUs: dW1 payload in bf16 (BASELINE config #2) instead of fp32
+  int spread;               // placement: 0 packed on one XCD (default), 1 spread (several ranks per GPU)
+  long long* phase_ts;      // optional phase stamps: [step < 64][workgroup 64][16] (wave 0 / wave 7, lane 0)
 };
+
+// phase stamp ph of step st (s_memrealtime, 100 MHz) -- profiling only
+#define PH(ph)                                                                                 \
+  if (a.phase_ts != nullptr && lane == 0 && st < 64)                                         \
+    a.phase_ts[((long long)st * 64 + c) * 16 + (ph)] = (long long)__builtin_amdgcn_s_memrealtime();
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -145,17 +163,34 @@ __device__ __forceinline__ void lds_barrier() {   // orders LDS only: no vmcnt(0
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-// 16-byte write-through (sc1) store / L1-bypassing (sc1) load through a buffer
-// resource over a wave-uniform region of `bytes` (one descriptor per edge and
-// step: slot and lane go into the VGPR offset)
+// Granule hand-off through a buffer resource over a wave-uniform region (one
+// descriptor per edge and step; slot and lane go into the VGPR offset).
+// Producer: 4 floats -> 4 granules {value, tag} in two 16-byte write-through
+// (sc1) stores; consumer: two L1-bypassing (sc1) 16-byte loads, valid when all
+// four tags match (8-byte halves of a 16-byte sc1 store are observed untorn on
+// gfx950: MI355X_MICROARCH.md "Valid forms", R2).
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t region_rsrc(const void* base, int bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, 0x00020000);
 }
-__device__ __forceinline__ void st16_sc1(__amdgpu_buffer_rsrc_t rs, int voff, f32x4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, voff, 0, 16);
+// l2_local: every consumer shares the producer's XCD (verified at launch) ->
+// plain stores, the lines stay in that L2 where the consumers' sc1 loads hit;
+// otherwise write-through (sc1) stores, visible to other XCDs' sc1 loads.
+__device__ __forceinline__ void put_gran(__amdgpu_buffer_rsrc_t rs, int voff, f32x4 v, unsigned tag, bool l2_local) {
+  const u32x4 lo = {__float_as_uint(v[0]), tag, __float_as_uint(v[1]), tag};
+  const u32x4 hi = {__float_as_uint(v[2]), tag, __float_as_uint(v[3]), tag};
+  if (l2_local) {
+    __builtin_amdgcn_raw_buffer_store_b128(lo, rs, voff, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(hi, rs, voff + 16, 0, 0);
+  } else {
+    __builtin_amdgcn_raw_buffer_store_b128(lo, rs, voff, 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(hi, rs, voff + 16, 0, 16);
+  }
 }
-__device__ __forceinline__ f32x4 ld16_sc1(__amdgpu_buffer_rsrc_t rs, int voff) {
-  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, 16));
+__device__ __forceinline__ bool get_gran(__amdgpu_buffer_rsrc_t rs, int voff, unsigned tag, f32x4& out) {
+  const u32x4 lo = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, 16);
+  const u32x4 hi = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 16, 0, 16);
+  out = f32x4{__uint_as_float(lo[0]), __uint_as_float(lo[2]), __uint_as_float(hi[0]), __uint_as_float(hi[2])};
+  return lo[1] == tag && lo[3] == tag && hi[1] == tag && hi[3] == tag;
 }
 
 // lane l <- lane l^16 / l^32 with gfx950's VALU row swaps
@@ -168,23 +203,56 @@ __device__ __forceinline__ float xor32(float v) {
   return __uint_as_float((threadIdx.x & 32) ? p[0] : p[1]);
 }
 
-// Poll `n` u32 tag flags at f[0..n) (lanes < n, except `skip`) until every one
-// equals `tag`; false on timeout or a raised error word.
-__device__ __forceinline__ bool poll_flags(const unsigned* f, int n, int skip, unsigned tag, int lane, const Args& a) {
+// Gather the N granule slots slot(k) (k != skip) of this lane until every tag
+// matches; part[skip] = own (constant-index selects only: a runtime index would
+// demote the array to scratch).  `need` false: this lane takes no data (zeros;
+// it still joins the wave-wide exit test).  Polling is cheap: lane k < N watches
+// ONE granule of producer k (the last one lane `probe` writes) until it carries
+// the tag; only then does every lane load its own granules -- and re-loads the
+// few that were not there yet (no order between a producer's lanes).  A sweep
+// of every lane over every slot per poll was ~5 MB of L2 traffic per round.
+// false on timeout / error.
+template <int N, typename SlotOff>
+__device__ __forceinline__ bool gather_gran(__amdgpu_buffer_rsrc_t rs, SlotOff slot, int skip, bool need, int probe,
+                                            unsigned tag, f32x4 own, f32x4 (&part)[N], int lane, const Args& a) {
+  bool have[N];
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    have[k] = (k == skip) || !need;
+    part[k] = (k == skip) ? own : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+  bool seen = lane >= N || lane == skip || a.gmode != 0;
   for (;;) {
-    bool ok = true;
-    if (lane < n && lane != skip)
-      ok = __hip_atomic_load(f + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == tag;
-    if (__all(ok)) break;
+    asm volatile("" ::: "memory");   // re-load every pass (no loop-invariant hoisting)
+    if (!seen) {
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, slot(lane) + 32 * probe + 16, 0, 16);
+      seen = v[1] == tag && v[3] == tag;
+    }
+    if (__all(seen)) break;
     if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > a.timeout ||
         __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
       if (lane == 0) atomicOr(a.err, 1);
       return false;
     }
   }
-  asm volatile("" ::: "memory");   // no payload load above the flag match
-  return true;
+  for (;;) {
+    asm volatile("" ::: "memory");
+    bool all = true;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      if (!have[k]) have[k] = get_gran(rs, slot(k) + 32 * lane, tag, part[k]);
+      all = all && have[k];
+    }
+    if (__all(all)) return true;
+    if (a.gmode == 2) __builtin_amdgcn_s_sleep(2);
+    else if (a.gmode == 3) __builtin_amdgcn_s_sleep(8);
+    if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > a.timeout ||
+        __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+      if (lane == 0) atomicOr(a.err, 1);
+      return false;
+    }
+  }
 }
 
 // ------------------------------------------------------------------ copier
@@ -251,6 +319,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
   float* rdb2 = reinterpret_cast<float*>(smem + L_RDB2);
   float* rmet = reinterpret_cast<float*>(smem + L_RMET);
   int* abort_flag = reinterpret_cast<int*>(smem + L_FLAG);
+  int* census = abort_flag + 1;
 
   // ---- load state
   for (int k = tid; k < 3 * 16 * LS; k += THREADS) a2T[k] = 0.f;   // a2T, dz2T, dz3T (batch pad stays 0)
@@ -269,12 +338,19 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
   }
   const int hid = 16 * j + r;       // this lane's hidden unit in the W1 / dW1 layouts
   const bool hv = hid < HID;
-  const int ft = NT * q + w;        // wave w < 7: feature tile (16 features)
-  float Wt[4] = {0.f, 0.f, 0.f, 0.f};
-  if (w < NT && hv) {
+  // wave w owns local feature tiles w and w + 8 of the slice (global tile ft[k])
+  const int nt = ntile(q);
+  // (constant-index scalars, not arrays a lambda captures: those would live in scratch)
+  const bool tv0 = w < nt, tv1 = w + 8 < nt;
+  const int ft0 = tile0(q) + w, ft1 = tile0(q) + (tv1 ? w + 8 : 0);
+  auto tvk = [=](int k) { return k ? tv1 : tv0; };
+  auto ftk = [=](int k) { return k ? ft1 : ft0; };
+  float Wt[NTW][4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) Wt[e] = a.params[(16 * ft + 4 * g + e) * HID + hid];
-  }
+  for (int k = 0; k < NTW; ++k)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      Wt[k][e] = (tvk(k) && hv) ? a.params[(16 * ftk(k) + 4 * g + e) * HID + hid] : 0.f;
   const unsigned long long seq0 = *a.seq;
   const long long gstep0 = *a.gstep;
   const float lr = *a.lr;
@@ -282,24 +358,60 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
   const float lrX = lrB * (1.f / 255.f);
   const bool failed_in = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
 
-  // x operands of the wave's feature tile (waves < 7), current and next step:
-  //  xf[bt]: row 16bt+r, features 16ft+4g..+3 (forward B operand)
-  //  xt[s] : feature 16ft+r, batch 16s+4g..+3 (weight-gradient A operand)
-  //  lab   : label of batch row 16w+r (head)
-  uint32_t xf[NBT], xt[NBT];
+  // x operands of the wave's feature tiles, current and next step:
+  //  xf[k][bt]: row 16bt+r, features 16ft+4g..+3 (forward B operand)
+  //  xt[k][s] : feature 16ft+r, batch 16s+4g..+3 (weight-gradient A operand)
+  //  lab      : label of batch row 16w+r (head, waves < 7)
+  uint32_t xf[NTW][NBT], xt[NTW][NBT];
   int lab = 0;
-  auto load_x = [&](int st, uint32_t (&f)[NBT], uint32_t (&t)[NBT], int& y) {
+  auto load_x = [&](int st, uint32_t (&f)[NTW][NBT], uint32_t (&t)[NTW][NBT]) -> int {
+    // unconditional (an absent second tile reads tile ft1 = the slice's first: valid
+    // memory, never used) -- a conditional store into the array would demote it to scratch
     const uint8_t* rec = a.stage + (long long)st * REC;
 #pragma unroll
-    for (int b = 0; b < NBT; ++b) {
-      f[b] = *reinterpret_cast<const uint32_t*>(rec + (16 * b + r) * DIN + 16 * ft + 4 * g);
-      t[b] = *reinterpret_cast<const uint32_t*>(rec + XROW_BYTES + (16 * ft + r) * XTS + 16 * b + 4 * g);
+    for (int k = 0; k < NTW; ++k) {
+#pragma unroll
+      for (int b = 0; b < NBT; ++b) {
+        f[k][b] = *reinterpret_cast<const uint32_t*>(rec + (16 * b + r) * DIN + 16 * ftk(k) + 4 * g);
+        t[k][b] = *reinterpret_cast<const uint32_t*>(rec + XROW_BYTES + (16 * ftk(k) + r) * XTS + 16 * b + 4 * g);
+      }
     }
-    y = rec[XROW_BYTES + XT_BYTES + 16 * w + r];
+    return w < NBT ? rec[XROW_BYTES + XT_BYTES + 16 * w + r] : 0;   // label of batch row 16w+r
   };
   __syncthreads();
   if (failed_in) return;
-  if (w < NT && a.nsteps > 0) load_x(0, xf, xt, lab);
+  // ---- placement census: E1 group (the NQ slices of block j) and E2 group (the
+  // NJ blocks of slice q) each on this workgroup's XCD -> that edge stays in one
+  // L2 (plain stores).  Decided per launch from HW_REG_XCC_ID, never assumed.
+  if (tid == 0) {
+    const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20) & 15u;
+    unsigned long long* hdr = reinterpret_cast<unsigned long long*>(a.xbuf + HDR_OFF);
+    const unsigned tag0 = (unsigned)(seq0 + 1ull);
+    __hip_atomic_store(hdr + c, ((unsigned long long)tag0 << 32) | xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int e1 = 1, e2 = 1, bad = 0;
+    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+    for (int cc = 0; cc < NCOMP && !bad; ++cc) {
+      unsigned long long v;
+      while (((v = __hip_atomic_load(hdr + cc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) != tag0) {
+        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) {
+          atomicOr(a.err, 1);
+          bad = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      if ((unsigned)v != xcc) {
+        if (cc / NQ == j) e1 = 0;
+        if (cc % NQ == q) e2 = 0;
+      }
+    }
+    *census = bad ? -1 : (e1 | (e2 << 1));
+  }
+  __syncthreads();
+  if (*census < 0) return;
+  const bool l2_e1 = (*census & 1) != 0;
+  const bool l2_e2 = (*census & 2) != 0;
+  if (a.nsteps > 0) lab = load_x(0, xf, xt);
 
   bool aborted = false;
   for (int st = 0; st < a.nsteps; ++st) {
@@ -308,45 +420,50 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
     const int par = (int)(sq & 1ull);
     if (c == 0 && tid == 0 && a.step_ts != nullptr)
       a.step_ts[(gstep0 + st) % a.ts_ring] = (long long)__builtin_amdgcn_s_memrealtime();
+    if (w == 0) { PH(0); }
 
-    // ---------------- P0: forward partial of feature tile ft, all batch tiles
-    if (w < NT) {
+    // ---------------- P0: forward partial of the wave's tiles, all batch tiles
+    {
       f32x4 acc[NBT];
 #pragma unroll
       for (int b = 0; b < NBT; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
+      for (int k = 0; k < NTW; ++k) {
+        if (tvk(k)) {
 #pragma unroll
-        for (int b = 0; b < NBT; ++b) acc[b] = mfma4(Wt[e], ub(xf[b], e), acc[b]);
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int b = 0; b < NBT; ++b) acc[b] = mfma4(Wt[k][e], ub(xf[k][b], e), acc[b]);
+        }
+      }
 #pragma unroll
       for (int b = 0; b < NBT; ++b) zbuf[(w * NBT + b) * 64 + lane] = acc[b];
     }
+    if (w == 0) { PH(1); }
     lds_barrier();
+    if (w == 0) { PH(2); }
 
     // ---------------- E1 + P1 + E2 + head (wave w < 7: batch tile w)
-    uint32_t xfn[NBT], xtn[NBT];
+    uint32_t xfn[NTW][NBT], xtn[NTW][NBT];
     int labn = 0;
-    if (w < NT) {
+    if (w < NBT) {
       const int bw = 16 * w + r;          // this lane's batch row
       const bool bv = bw < B;
       f32x4 zs = zbuf[w * 64 + lane];
 #pragma unroll
-      for (int t = 1; t < NT; ++t) zs += zbuf[(t * NBT + w) * 64 + lane];
-      // publish the slice partial of (j, batch tile w); flag after the drain
+      for (int v = 1; v < 8; ++v) zs += zbuf[(v * NBT + w) * 64 + lane];
+      // publish the slice partial of (j, batch tile w) as granules; gather the others
       // E1 region of (parity, block j): [slice][batch tile] slots
-      const auto r1 = region_rsrc(a.xbuf + E1_OFF + (long long)(par * NJ + j) * NQ * NBT * SLOT, NQ * NBT * SLOT);
-      unsigned* f1 = reinterpret_cast<unsigned*>(a.xbuf + F1_OFF) + ((par * NJ + j) * NBT + w) * 8;
-      st16_sc1(r1, (q * NBT + w) * SLOT + 16 * lane, zs);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) __hip_atomic_store(f1 + q, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      bool ok = poll_flags(f1, NQ, q, tag, lane, a);
+      const auto r1 = region_rsrc(a.xbuf + E1_OFF + (long long)(par * NJ + j) * NQ * NBT * GSLOT, NQ * NBT * GSLOT);
+      put_gran(r1, (q * NBT + w) * GSLOT + 32 * lane, zs, tag, l2_e1);
+      if (w == 0) { PH(3); }
       f32x4 part[NQ];
-#pragma unroll
-      for (int qq = 0; qq < NQ; ++qq)
-        part[qq] = (qq == q) ? zs : ld16_sc1(r1, (qq * NBT + w) * SLOT + 16 * lane);
+      bool ok = gather_gran<NQ>(r1, [&](int k) { return (k * NBT + w) * GSLOT; }, q, true, 63, tag, zs, part, lane, a);
+      if (w == 0) { PH(4); }
       f32x4 z = part[0];
 #pragma unroll
       for (int qq = 1; qq < NQ; ++qq) z += part[qq];
+      if (w == 0) { PH(5); }
       // lane (batch r, g): hidden 16j+4g+i
       float a2[4];
 #pragma unroll
@@ -361,21 +478,15 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
 #pragma unroll
       for (int e = 0; e < 4; ++e) pl = mfma4(w2s[(4 * g + e) * 16 + r], a2[e], pl);
       // E2 region of (parity, slice q, batch tile w): [block] slots
-      const auto r2 = region_rsrc(a.xbuf + E2_OFF + (long long)((par * NQ + q) * NBT + w) * NJ * SLOT, NJ * SLOT);
-      unsigned* f2 = reinterpret_cast<unsigned*>(a.xbuf + F2_OFF) + ((par * NQ + q) * NBT + w) * 8;
-      if (g < 3) st16_sc1(r2, j * SLOT + 16 * lane, pl);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) __hip_atomic_store(f2 + j, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const auto r2 = region_rsrc(a.xbuf + E2_OFF + (long long)((par * NQ + q) * NBT + w) * NJ * GSLOT, NJ * GSLOT);
+      if (g < 3) put_gran(r2, j * GSLOT + 32 * lane, pl, tag, l2_e2);
+      if (w == 0) { PH(6); }
       // while the logits are in flight: a2 -> LDS (dW2)
 #pragma unroll
       for (int i = 0; i < 4; ++i) a2T[(4 * g + i) * LS + bw] = a2[i];
-      ok = poll_flags(f2, NJ, j, tag, lane, a) && ok;
       f32x4 lp[NJ];
-#pragma unroll
-      for (int jj = 0; jj < NJ; ++jj)
-        lp[jj] = (jj == j) ? pl : ld16_sc1(r2, jj * SLOT + 16 * lane);
-      // next step's x operands: in flight across the head and the weight gradient
-      if (st + 1 < a.nsteps) load_x(st + 1, xfn, xtn, labn);
+      ok = gather_gran<NJ>(r2, [&](int k) { return k * GSLOT; }, j, g < 3, 47, tag, pl, lp, lane, a) && ok;
+      if (w == 0) { PH(7); }
       if (!ok && lane == 0) *abort_flag = 1;
       // logits, softmax cross-entropy, accuracy -- identical in every workgroup
       float lg[4], ex[4];
@@ -384,10 +495,11 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
       for (int i = 0; i < 4; ++i) {
         float v = b2s[4 * g + i];
 #pragma unroll
-        for (int jj = 0; jj < NJ; ++jj) v += (g < 3) ? lp[jj][i] : 0.f;
+        for (int jj = 0; jj < NJ; ++jj) v += lp[jj][i];
         lg[i] = v;
         if (4 * g + i < NCLS) m = fmaxf(m, v);
       }
+      if (w == 0) { PH(8); }
       m = fmaxf(m, xor16(m));
       m = fmaxf(m, xor32(m));
       const int y = lab < NCLS ? lab : 0;
@@ -433,26 +545,36 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
       const float ls = row16_sum((g == 0 && bv) ? loss : 0.f);
       const float cr = row16_sum((g == 0 && bv && (int)am == y) ? 1.f : 0.f);
       if (lane == 0) { rmet[2 * w] = ls; rmet[2 * w + 1] = cr; }
+      if (w == 0) { PH(9); }
     }
+    // next step's x operands: in flight across the rest of the step
+    if (st + 1 < a.nsteps) labn = load_x(st + 1, xfn, xtn);
     lds_barrier();
+    if (w == 0) { PH(10); }
     if (*abort_flag) { aborted = true; break; }
 
-    // ---------------- P2: weight gradients
-    f32x4 G = {0.f, 0.f, 0.f, 0.f};      // waves < 7: dW1[16ft+4g+i][16j+r] (x 255 B)
+    // ---------------- P2: weight gradients of the wave's tiles
+    f32x4 G[NTW];                        // dW1[16ft+4g+i][16j+r] (x 255 B)
+#pragma unroll
+    for (int k = 0; k < NTW; ++k) {
+      G[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (tvk(k)) {
+        f32x4 g0 = {0.f, 0.f, 0.f, 0.f}, g1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < NBT; ++s) {
+          const f32x4 bz = *reinterpret_cast<const f32x4*>(dz2T + r * LS + 16 * s + 4 * g);
+          g0 = mfma4(ub(xt[k][s], 0), bz[0], g0);
+          g1 = mfma4(ub(xt[k][s], 1), bz[1], g1);
+          g0 = mfma4(ub(xt[k][s], 2), bz[2], g0);
+          g1 = mfma4(ub(xt[k][s], 3), bz[3], g1);
+        }
+        G[k] = g0 + g1;
+      }
+    }
+    if (w == 0) { PH(11); }
     f32x4 D = {0.f, 0.f, 0.f, 0.f};      // wave 7: dW2[16j+4g+i][class r] (x B)
     float gb = 0.f;                      // wave 7: db1 (lanes < 16) / db2 (lanes 16..25) (x B)
-    if (w < NT) {
-      f32x4 g0 = {0.f, 0.f, 0.f, 0.f}, g1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < NBT; ++s) {
-        const f32x4 bz = *reinterpret_cast<const f32x4*>(dz2T + r * LS + 16 * s + 4 * g);
-        g0 = mfma4(ub(xt[s], 0), bz[0], g0);
-        g1 = mfma4(ub(xt[s], 1), bz[1], g1);
-        g0 = mfma4(ub(xt[s], 2), bz[2], g0);
-        g1 = mfma4(ub(xt[s], 3), bz[3], g1);
-      }
-      G = g0 + g1;
-    } else {
+    if (w == 7) {
       f32x4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < NBT; ++s) {
@@ -485,15 +607,18 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
       // visibility); rank-order sums keep the replicas bit-identical
       const size_t soff = IPC_FLAGS + (size_t)(par * NCOMP + c) * IPC_SLOT;
       char* own = static_cast<char*>(a.peer_base[a.rank]) + soff;
-      if (w < NT) {
+#pragma unroll
+      for (int k = 0; k < NTW; ++k) {
+        char* p = own + ((w * NTW + k) * 64 + lane) * 16;
         if (a.gbf16) {
-          const uint2 v = make_uint2(pack2bf(G[0], G[1]), pack2bf(G[2], G[3]));
-          G = f32x4{bf2f(v.x & 0xffff), bf2f(v.x >> 16), bf2f(v.y & 0xffff), bf2f(v.y >> 16)};
-          *reinterpret_cast<uint2*>(own + (w * 64 + lane) * 16) = v;
-        } else {
-          *reinterpret_cast<f32x4*>(own + (w * 64 + lane) * 16) = G;
+          const uint2 v = make_uint2(pack2bf(G[k][0], G[k][1]), pack2bf(G[k][2], G[k][3]));
+          G[k] = f32x4{bf2f(v.x & 0xffff), bf2f(v.x >> 16), bf2f(v.y & 0xffff), bf2f(v.y >> 16)};
+          if (tvk(k)) *reinterpret_cast<uint2*>(p) = v;
+        } else if (tvk(k)) {
+          *reinterpret_cast<f32x4*>(p) = G[k];
         }
-      } else {
+      }
+      if (w == 7) {
         *reinterpret_cast<f32x4*>(own + IPC_SMALL + lane * 16) = D;
         if (lane < 16 + NCLS) *reinterpret_cast<float*>(own + IPC_SMALL + 1024 + lane * 4) = gb;
       }
@@ -527,43 +652,58 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
       lds_barrier();
       asm volatile("" ::: "memory");   // no peer-slot load hoisted above the flag match
       if (*abort_flag) { aborted = true; break; }
-      f32x4 sum = {0.f, 0.f, 0.f, 0.f};
+      f32x4 sum[NTW];
+      f32x4 sD = {0.f, 0.f, 0.f, 0.f};
       float sb = 0.f;
+#pragma unroll
+      for (int k = 0; k < NTW; ++k) sum[k] = f32x4{0.f, 0.f, 0.f, 0.f};
       for (int rr = 0; rr < a.W; ++rr) {
-        f32x4 v = w < NT ? G : D;
-        float vb = gb;
-        if (rr != a.rank) {
-          const char* ps = static_cast<const char*>(a.peer_base[rr]) + soff;
-          if (w < NT) {
+        const char* ps = static_cast<const char*>(a.peer_base[rr]) + soff;
+#pragma unroll
+        for (int k = 0; k < NTW; ++k) {
+          f32x4 v = G[k];
+          if (rr != a.rank && tvk(k)) {
+            const char* pk = ps + ((w * NTW + k) * 64 + lane) * 16;
             if (a.gbf16) {
-              const unsigned long long x =
-                  __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(ps + (w * 64 + lane) * 16));
+              const unsigned long long x = __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(pk));
               v = f32x4{bf2f((unsigned)x & 0xffff), bf2f(((unsigned)x) >> 16), bf2f((unsigned)(x >> 32) & 0xffff),
                         bf2f((unsigned)(x >> 48))};
             } else {
-              v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(ps + (w * 64 + lane) * 16));
+              v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(pk));
             }
-          } else {
+          }
+          sum[k] += v;
+        }
+        if (w == 7) {
+          f32x4 v = D;
+          float vb = gb;
+          if (rr != a.rank) {
             v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(ps + IPC_SMALL + lane * 16));
             vb = lane < 16 + NCLS ? __builtin_nontemporal_load(reinterpret_cast<const float*>(ps + IPC_SMALL + 1024) + lane)
                                   : 0.f;
           }
+          sD += v;
+          sb += vb;
         }
-        sum += v;
-        sb += vb;
       }
-      if (w < NT) G = sum; else { D = sum; gb = sb; }
+#pragma unroll
+      for (int k = 0; k < NTW; ++k) G[k] = sum[k];
+      if (w == 7) { D = sD; gb = sb; }
     }
     // ---------------- updates (lr / (W B), 1/255 for the pixel scale)
-    if (w < NT) {
-      if (hv) {
+    if (hv) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) Wt[i] -= lrX * G[i];
-      }
+      for (int k = 0; k < NTW; ++k)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) Wt[k][i] -= lrX * G[k][i];
+    }
 #pragma unroll   // rotate the prefetched operands in
-      for (int b = 0; b < NBT; ++b) { xf[b] = xfn[b]; xt[b] = xtn[b]; }
-      lab = labn;
-    } else {
+    for (int k = 0; k < NTW; ++k)
+#pragma unroll
+      for (int b = 0; b < NBT; ++b) { xf[k][b] = xfn[k][b]; xt[k][b] = xtn[k][b]; }
+    lab = labn;
+    if (w == 0) { PH(12); }
+    if (w == 7) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         if (16 * j + 4 * g + i < HID && r < NCLS) w2s[(4 * g + i) * 16 + r] -= lrB * D[i];
@@ -578,9 +718,13 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
   __syncthreads();   // wave 7's last small-parameter update
 
   // ---- write back (fp32 master), global step, exchange sequence, end stamp
-  if (w < NT && hv) {
+  if (hv) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) a.params[(16 * ft + 4 * g + e) * HID + hid] = Wt[e];
+    for (int k = 0; k < NTW; ++k)
+      if (tvk(k)) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) a.params[(16 * ftk(k) + 4 * g + e) * HID + hid] = Wt[k][e];
+      }
   }
   if (q == 0) {
     if (tid < 256) {
@@ -603,18 +747,26 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
   }
 }
 
+// packed placement (a.spread == 0): compute workgroup c runs as blockIdx 8c, so
+// under the observed round-robin dispatch all 28 share ONE XCD (both edges in one
+// L2); the first NCOP other blocks copy, the rest exit.  spread (several ranks on
+// one GPU, tests): compute = blocks 0..27, copiers = 28..43.  Placement is speed
+// only: the census above decides each edge's store flavour.
 template <int ACT, bool MULTI>
 __global__ __launch_bounds__(THREADS, 1) void mlp_persist_f32(Args a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int b = blockIdx.x;
-  const int j = b & 7, q = b >> 3;
-  if (j < NJ && q < NQ) {
-    if (a.nsteps > 0) compute<ACT, MULTI>(a, j, q, smem);
+  int c = -1, cid = -1;
+  if (a.spread) {
+    if (b < NCOMP) c = b; else cid = b - NCOMP;
+  } else {
+    if ((b & 7) == 0) c = b >> 3; else cid = b - (b >> 3) - 1;
+  }
+  if (c >= 0) {
+    if (a.nsteps > 0) compute<ACT, MULTI>(a, c / NQ, c % NQ, smem);
     return;
   }
-  // copier id among the non-compute blocks: b%8 == 7 (b < 56) -> 0..6, b >= 56 -> 7..14
-  const int cid = q < NQ ? q : NQ + (b - 8 * NQ);
-  copier(a, cid, smem);
+  if (cid < NCOP) copier(a, cid, smem);
 }
 
 }  // namespace mlpf
@@ -631,9 +783,10 @@ hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int n
                                 float* metrics, int ring, int act, int naive, long long* gstep, unsigned long long* seq,
                                 void* xbuf, int* err, long long timeout, long long* step_ts, int ts_ring,
                                 const void* host_next, int next_steps, void* stage_next, void* const* peer_base, int W,
-                                int rank, int gbf16, hipStream_t stream) {
+                                int rank, int gbf16, long long* phase_ts, int spread, hipStream_t stream) {
   using namespace dtfk::mlpf;
   Args a;
+  a.phase_ts = phase_ts;
   a.stage = static_cast<const uint8_t*>(stage);
   a.rec_h = rec_h;
   a.B = B;
@@ -658,6 +811,11 @@ hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int n
   a.W = W;
   a.rank = rank;
   a.gbf16 = gbf16;
+  a.spread = spread;
+  {
+    const char* gm = getenv("DTF_GATHER_MODE");
+    a.gmode = gm ? atoi(gm) : 0;
+  }
   constexpr size_t lds = LDS_BYTES;
   static bool attr_set = false;
   const void* kerns[4] = {reinterpret_cast<const void*>(mlp_persist_f32<0, false>),
@@ -672,11 +830,12 @@ hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int n
     attr_set = true;
   }
   const int which = (act == 0 ? 0 : 1) + (W > 1 ? 2 : 0);
+  const int grid = spread ? GRID_SPREAD : GRID_PACKED;
   switch (which) {
-    case 0: hipLaunchKernelGGL((mlp_persist_f32<0, false>), dim3(GRID), dim3(THREADS), lds, stream, a); break;
-    case 1: hipLaunchKernelGGL((mlp_persist_f32<1, false>), dim3(GRID), dim3(THREADS), lds, stream, a); break;
-    case 2: hipLaunchKernelGGL((mlp_persist_f32<0, true>), dim3(GRID), dim3(THREADS), lds, stream, a); break;
-    default: hipLaunchKernelGGL((mlp_persist_f32<1, true>), dim3(GRID), dim3(THREADS), lds, stream, a); break;
+    case 0: hipLaunchKernelGGL((mlp_persist_f32<0, false>), dim3(grid), dim3(THREADS), lds, stream, a); break;
+    case 1: hipLaunchKernelGGL((mlp_persist_f32<1, false>), dim3(grid), dim3(THREADS), lds, stream, a); break;
+    case 2: hipLaunchKernelGGL((mlp_persist_f32<0, true>), dim3(grid), dim3(THREADS), lds, stream, a); break;
+    default: hipLaunchKernelGGL((mlp_persist_f32<1, true>), dim3(grid), dim3(THREADS), lds, stream, a); break;
   }
   return hipGetLastError();
 }

@@ -425,9 +425,17 @@ class PersistentMLPRunner:
     epoch: ONE launch per chunk of up to `g` steps.
 
     precision="fp32" (default, the reference's precision: example.py:77-118 is
-        fp32 end to end) -- csrc/kernels/mlp_persist_f32.hip: 49 compute
-        workgroups (7 hidden blocks x 7 feature slices) on exact f32-input MFMA,
-        fp32 master weights in VGPRs, 15 copier workgroups.
+        fp32 end to end) -- csrc/kernels/mlp_persist_f32.hip: 28 compute
+        workgroups (7 hidden blocks x 4 feature slices, packed on one XCD) on
+        f32-input MFMA (v_mfma_f32_16x16x4_f32, bitwise an fmaf chain) for every
+        product; fp32 master weights in VGPRs.
+    precision="fp32-split" -- csrc/kernels/mlp_persist_x3.hip: 7 compute
+        workgroups (one per hidden block); the two large GEMMs on bf16 MFMA
+        through an EXACT 3-way split of every fp32 operand (hi + mid + lo == the
+        fp32 value; pixels exact), so every product is exact and accumulates in
+        fp32; small head products on f32-input MFMA.  One inter-workgroup edge
+        per step instead of two, but 7 CUs carry all the MFMA work (measured
+        14.7 vs 13.0 us/step).
     precision="fp16" -- csrc/kernels/mlp_persist.hip: 7 compute workgroups on
         f16 MFMA (pixels exact as 1024+u, weights/activations rounded to fp16),
         57 copier workgroups.
@@ -456,12 +464,15 @@ class PersistentMLPRunner:
     TS_RING = 16384
 
     def __init__(self, trainer: FusedMLPTrainer, epoch, steps_per_launch: int = 550,
-                 timeout_s: float = 30.0, precision: str = "fp32", grad_bf16: bool = True):
+                 timeout_s: float = 30.0, precision: str = "fp32", grad_bf16: bool = True,
+                 placement: str = "auto"):
         C = trainer.C
-        if precision not in ("fp32", "fp16"):
-            raise ValueError("precision must be 'fp32' or 'fp16'")
+        if precision not in ("fp32", "fp32-split", "fp16"):
+            raise ValueError("precision must be 'fp32', 'fp32-split' or 'fp16'")
         self.precision = precision
-        maxb = C.mlpf_max_batch() if precision == "fp32" else C.mlp_persist_max_batch()
+        self.f32 = precision in ("fp32", "fp32-split")
+        self.exact_split = precision == "fp32-split"
+        maxb = C.mlpf_max_batch() if self.f32 else C.mlp_persist_max_batch()
         if trainer.B > maxb:
             raise ValueError(f"PersistentMLPRunner needs batch <= {maxb}")
         if epoch.batch_size != trainer.B:
@@ -471,11 +482,19 @@ class PersistentMLPRunner:
         self.g = int(min(steps_per_launch, epoch.num_batches))
         self.timeout_s = float(timeout_s)
         self.grad_bf16 = bool(grad_bf16)
+        if placement == "auto":
+            # several ranks sharing one GPU (tests): their compute workgroups cannot all sit on one XCD
+            nloc = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
+            placement = "spread" if nloc > max(1, torch.cuda.device_count()) else "packed"
+        if placement not in ("packed", "spread"):
+            raise ValueError("placement must be 'auto', 'packed' or 'spread'")
+        self.placement = placement
         dev = trainer.device
-        if precision == "fp32":
-            self.rec_s = int(C.mlpf_stage_rec())
+        if self.f32:
+            self.rec_s = int(C.mlpx_stage_rec() if self.exact_split else C.mlpf_stage_rec())
             self.stages = [torch.zeros(self.g * self.rec_s, dtype=torch.uint8, device=dev) for _ in range(2)]
-            self.xbuf = torch.zeros(int(C.mlpf_xbuf_bytes()), dtype=torch.uint8, device=dev)
+            nx = C.mlpx_xbuf_bytes() if self.exact_split else C.mlpf_xbuf_bytes()
+            self.xbuf = torch.zeros(int(nx), dtype=torch.uint8, device=dev)
         else:
             self.rec_s = int(C.mlp_persist_stage_rec(trainer.B))   # k-step-pair interleaved rows
             self.xtb = int(C.mlp_persist_xt_bytes())
@@ -485,6 +504,7 @@ class PersistentMLPRunner:
         self.seq = torch.zeros(1, dtype=torch.int64, device=dev)
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
         self.step_ts = torch.zeros(self.TS_RING, dtype=torch.int64, device=dev)
+        self.phase_ts = None    # fp32 engine: optional [64 steps][64 wg][16] phase stamps (profiling)
         self.cursor = 0
         self.staged: List[Optional[Tuple[int, int]]] = [None, None]   # (b0, g) resident per stage buffer
         self.copy_only_launches = 0
@@ -498,7 +518,8 @@ class PersistentMLPRunner:
             if int(os.environ.get("LOCAL_WORLD_SIZE", w.world_size)) != w.world_size:
                 raise RuntimeError("the persistent N-GPU exchange needs all ranks on one node")
             from ..parallel.world import open_peer_buffers
-            nbytes = C.mlpf_ipc_bytes() if precision == "fp32" else C.mlp_persist_ipc_bytes()
+            nbytes = ((C.mlpx_ipc_bytes() if self.exact_split else C.mlpf_ipc_bytes()) if self.f32
+                      else C.mlp_persist_ipc_bytes())
             self.ipc = open_peer_buffers(C, int(nbytes), w)
             self.W, self.rank = w.world_size, w.rank
 
@@ -518,12 +539,13 @@ class PersistentMLPRunner:
         t, ep = self.t, self.epoch
         dst = par ^ 1
         ipc = dict(ipc_table=self.ipc.table_ptr() if self.ipc is not None else 0, ipc_W=self.W, ipc_rank=self.rank)
-        if self.precision == "fp32":
+        if self.f32:
             st = self.stages[par][off * self.rec_s:] if nsteps > 0 else self.stages[par]
             t.C.mlp_persist_f32(st, ep.rec, t.B, nsteps, t.params, t.lr, t.metrics, t.gstep, self.seq, self.xbuf,
                                 self.err, self.timeout_s, t.act, int(t.naive), host=ep.host,
                                 host_offset=nxt[0] * ep.rec, next_steps=nxt[1], stage_next=self.stages[dst],
-                                step_ts=self.step_ts, grad_bf16=self.grad_bf16, **ipc)
+                                step_ts=self.step_ts, grad_bf16=self.grad_bf16, phase_ts=self.phase_ts,
+                                spread=self.placement == "spread", exact_split=self.exact_split, **ipc)
         else:
             xs = self.xs[par][off * self.rec_s:] if nsteps > 0 else self.xs[par]
             xts = self.xts[par][off * self.xtb:] if nsteps > 0 else self.xts[par]

@@ -30,7 +30,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--per-launch", type=int, default=4)
     ap.add_argument("--same-gpu", action="store_true")
-    ap.add_argument("--precision", choices=["fp32", "fp16"], default="fp32")
+    ap.add_argument("--precision", choices=["fp32", "fp32-split", "fp16"], default="fp32")
     ap.add_argument("--grad-dtype", choices=["bf16", "fp32"], default="bf16")
     a = ap.parse_args()
     rank, ws = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
@@ -72,7 +72,7 @@ def main():
     d_k, d_r = p - p0, ref.double() - p0
     rel = float((d_k - d_r).norm() / d_r.norm())
     # bf16 gradient payload (or fp16 operands): bf16-level tolerance; fp32 end to end: fp32 level
-    tol = 1e-5 if (a.precision == "fp32" and a.grad_dtype == "fp32") else 2e-2
+    tol = 1e-5 if (a.precision.startswith("fp32") and a.grad_dtype == "fp32") else 2e-2
     ok = identical and all(e == 0 for _, _, e in sums) and rel < tol and tr.global_step == a.steps
     if rank == 0:
         print(json.dumps({"persist_selftest": "pass" if ok else "FAIL", "world": ws, "same_gpu": a.same_gpu,

@@ -1,0 +1,100 @@
+"""Phase timing of the fp32 persistent MLP kernel (csrc/kernels/mlp_persist_f32.hip)
+from in-kernel s_memrealtime stamps (100 MHz).
+
+Stamps per step (workgroup c, wave 0, lane 0): 0 step start, 1 forward MFMAs
+done, 2 after LDS barrier A, 3 E1 published, 4 E1 flags matched, 5 z summed,
+6 E2 published, 7 E2 flags matched, 8 logits summed, 9 head done, 10 after LDS
+barrier B, 11 weight-gradient MFMAs done, 12 update done.
+Prints the median / p90 of every segment over steps 1..63 and all compute
+workgroups, plus per-step time and launch-level timing.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+from distributed_tensorflow_example_amd.data.mnist import PinnedEpoch, synthetic_mnist  # noqa: E402
+from distributed_tensorflow_example_amd.models import mlp  # noqa: E402
+
+NAMES = {"fp32": ["fwd_mfma", "barrier_A", "E1_publish", "E1_wait", "E1_load_sum", "P1_logit_publish",
+                       "E2_wait", "E2_load_sum", "head", "barrier_B", "wgrad_mfma", "update"],
+         # exact-split engine (mlp_persist_x3.hip): 0 start 1 fwd 2 barA 3 E2 pub 4 E2 gathered 5 head 6 barB
+         # 7 wgrad 8 update
+         "fp32-split": ["fwd_mfma_and_prefetch_issue", "barrier_A", "zsum_act_logits_publish", "E2_wait", "head",
+                  "barrier_B", "wgrad_mfma", "update"]}
+
+
+def main():
+    prec = sys.argv[1] if len(sys.argv) > 1 else "fp32"
+    names = NAMES[prec]
+    B, G = 100, 64
+    dev = torch.device("cuda", 0)
+    imgs, labels = synthetic_mnist(55000, seed=1)
+    ep = PinnedEpoch(imgs, labels, B)
+    tr = mlp.FusedMLPTrainer(batch_size=B, lr=0.0005, device=dev)
+    run = mlp.PersistentMLPRunner(tr, ep, steps_per_launch=550, precision=prec)
+    run.prepare(550)
+    run.run(550 * 4)
+    torch.cuda.synchronize()
+    out = {}
+    # launch-level: G-step launches back to back, host wall and device per-step stamps
+    for g in (20, 64, 550):
+        run.prepare(g)
+        run.run(g, lookahead=g)
+        torch.cuda.synchronize()
+        s0 = tr.global_step
+        t0 = torch.cuda.Event(enable_timing=True)
+        t1 = torch.cuda.Event(enable_timing=True)
+        t0.record()
+        run.run(g)
+        t1.record()
+        torch.cuda.synchronize()
+        dt = run.step_times_ms(s0, s0 + g) * 1000.0
+        out[f"launch_{g}"] = {"event_us": round(t0.elapsed_time(t1) * 1000.0, 2),
+                              "sum_step_us": round(float(dt.sum()), 2),
+                              "p50_step_us": round(float(np.median(dt)), 3)}
+    ts = torch.zeros(64 * 64 * 16, dtype=torch.int64, device=dev)
+    run.phase_ts = ts
+    run.prepare(G)
+    run.run(G, lookahead=G)
+    torch.cuda.synchronize()
+    run.phase_ts = None
+    raw = ts.cpu().numpy().reshape(64, 64, 16)
+    nj, nq = (7, 4) if prec == "fp32" else (7, 1)
+    ns = len(names) + 1
+    r = raw[1:G, : nj * nq, :ns].astype(np.float64) * 0.01   # us
+    seg = {}
+    for k, name in enumerate(names):
+        d = r[:, :, k + 1] - r[:, :, k]
+        seg[name] = [round(float(np.median(d)), 3), round(float(np.percentile(d, 90)), 3)]
+    out["segments_us_median_p90"] = seg
+    step = r[1:, :, 0] - r[:-1, :, 0]
+    out["step_us_median"] = round(float(np.median(step)), 3)
+    pub = 6 if prec == "fp32" else 3
+    got = pub + 1
+    last = r[:, :, pub].max(axis=1, keepdims=True)
+    hop = r[:, :, got] - last
+    out["logit_edge_hop_after_last_publish_us_median_p90"] = [round(float(np.median(hop)), 3),
+                                                               round(float(np.percentile(hop, 90)), 3)]
+    out["logit_publish_skew_us_median"] = round(float(np.median(r[:, :, pub].max(1) - r[:, :, pub].min(1))), 3)
+    late = (r[:, :, 0] - r[:, :, 0].min(axis=1, keepdims=True)).mean(axis=0)
+    out["step_start_lateness_us_by_wg"] = np.round(late, 2).tolist()
+    if prec == "fp32-split":
+        rr = raw[1:G, :7, :].astype(np.float64) * 0.01
+        med = lambda x: round(float(np.median(x)), 3)
+        out["x3_fwd_detail_us"] = {"w0_start_to_mfma_done": med(rr[:, :, 9] - rr[:, :, 0]),
+                                   "w4_start_to_mfma_done": med(rr[:, :, 10] - rr[:, :, 12]),
+                                   "w0_mfma_done_to_pair_barrier": med(rr[:, :, 11] - rr[:, :, 9]),
+                                   "w0_pair_barrier_to_stamp1": med(rr[:, :, 1] - rr[:, :, 11]),
+                                   "w4_start_minus_w0_start": med(rr[:, :, 12] - rr[:, :, 0])}
+    np.save(os.path.join(REPO, "gpurun_out", f"phase_raw_{prec}.npy"), raw[:G])
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

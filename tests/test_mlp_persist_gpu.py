@@ -24,9 +24,10 @@ def _ref_run(p0, imgs, labels, B, batches, lr, act="sigmoid"):
     return p, np.array(losses), np.array(accs)
 
 
+@pytest.mark.parametrize("engine", ["fp32", "fp32-split"])
 @pytest.mark.parametrize("B", [100, 37, 112])
 @pytest.mark.parametrize("act", ["sigmoid", "relu"])
-def test_persist_f32_one_step_gradient_fp32_exact(native, B, act):
+def test_persist_f32_one_step_gradient_fp32_exact(native, B, act, engine):
     """fp32 engine: every parameter's gradient within 1e-5 (relative, per tensor)
     of the fp32 autograd reference.  lr = 1000 makes lr*g >> ulp(W), so the
     gradient recovered from the update is accurate to ~1e-8."""
@@ -36,7 +37,7 @@ def test_persist_f32_one_step_gradient_fp32_exact(native, B, act):
     tr = mlp.FusedMLPTrainer(batch_size=B, lr=lr, act=act, device=dev)
     p0 = tr.get_params().clone()
     ep = PinnedEpoch(imgs, labels, B)
-    run = mlp.PersistentMLPRunner(tr, ep, steps_per_launch=1, precision="fp32")
+    run = mlp.PersistentMLPRunner(tr, ep, steps_per_launch=1, precision=engine)
     run.run(1)
     torch.cuda.synchronize()
     assert run.error() == 0
@@ -54,7 +55,8 @@ def test_persist_f32_one_step_gradient_fp32_exact(native, B, act):
     assert abs(m[1] - acc.item()) < 1e-6
 
 
-def test_persist_f32_multi_step_matches_reference(native):
+@pytest.mark.parametrize("engine", ["fp32", "fp32-split"])
+def test_persist_f32_multi_step_matches_reference(native, engine):
     """11 steps over wrapping chunks (cold start, in-kernel prefetch, offsets into
     a staged chunk, epoch wrap): fp32 engine tracks fp32 SGD to ~1e-6."""
     B, nb = 100, 6
@@ -64,7 +66,7 @@ def test_persist_f32_multi_step_matches_reference(native):
     tr = mlp.FusedMLPTrainer(batch_size=B, lr=lr, device=dev)
     p0 = tr.get_params().clone()
     ep = PinnedEpoch(imgs, labels, B)
-    run = mlp.PersistentMLPRunner(tr, ep, steps_per_launch=4, precision="fp32")
+    run = mlp.PersistentMLPRunner(tr, ep, steps_per_launch=4, precision=engine)
     run.run(7)     # (0,4) cold copy, (4,2), (0,1) epoch wrap; speculative (1,4) staged
     run.run(2)     # (1,2): inside the staged (1,4); streams (3,2) into the other stage
     run.run(2)     # (3,2): staged by the previous launch
@@ -83,7 +85,7 @@ def test_persist_f32_multi_step_matches_reference(native):
     assert np.allclose(m[:, 1], accs, atol=1e-6)
 
 
-@pytest.mark.parametrize("precision", ["fp32", "fp16"])
+@pytest.mark.parametrize("precision", ["fp32", "fp32-split", "fp16"])
 def test_persist_short_timed_run_streams_only_what_it_computes(native, precision):
     """The bench's pattern: warmup(5) primes exactly the timed run's chunk; the
     timed run(20) needs no copy-only launch and prefetches <= 20 steps; the
@@ -161,7 +163,7 @@ def test_persist_chunks_wrap_and_match_reference(native):
     assert np.allclose(m[:, 1], accs, atol=1e-6)
 
 
-@pytest.mark.parametrize("precision", ["fp32", "fp16"])
+@pytest.mark.parametrize("precision", ["fp32", "fp32-split", "fp16"])
 def test_persist_deterministic_and_hands_over_to_step_path(native, precision):
     B = 100
     imgs, labels = synthetic_mnist(B * 4, seed=13)
@@ -188,7 +190,7 @@ def test_persist_deterministic_and_hands_over_to_step_path(native, precision):
     assert ((g_k - g).norm() / g.norm()).item() < 3e-2
 
 
-@pytest.mark.parametrize("precision", ["fp32", "fp16"])
+@pytest.mark.parametrize("precision", ["fp32", "fp32-split", "fp16"])
 def test_persist_long_run_learns(native, precision):
     """1000 steps on synthetic MNIST: loss goes down."""
     B = 100
@@ -205,7 +207,8 @@ def test_persist_long_run_learns(native, precision):
     assert m[-50:, 0].mean() < 0.7 * m[:50, 0].mean(), (m[:50, 0].mean(), m[-50:, 0].mean())
 
 
-@pytest.mark.parametrize("precision,grad", [("fp32", "bf16"), ("fp32", "fp32"), ("fp16", "bf16")])
+@pytest.mark.parametrize("precision,grad", [("fp32", "bf16"), ("fp32", "fp32"), ("fp32-split", "fp32"),
+                                            ("fp16", "bf16")])
 @pytest.mark.parametrize("nproc", [2, 3])
 def test_persist_multi_rank_same_gpu(native, nproc, precision, grad):
     """N ranks sharing cuda:0: in-kernel IPC exchange, bit-identical replicas, sync-SGD math."""

@@ -122,6 +122,27 @@ __device__ __forceinline__ float row16_sum(float v) {
 
 __device__ __forceinline__ float sigmoidf_(float z) { return 1.f / (1.f + __expf(-z)); }
 
+// Peer (IPC-mapped) exchange data is read with system-scope loads (sc0 sc1):
+// never served from a cache line of this XCD or device, whatever memory type
+// the importing process's mapping of the peer buffer got.  (Non-temporal loads
+// are L2-served: a stale line there breaks bit-identical replicas.)
+__device__ __forceinline__ unsigned long long ld_sys_u64(const void* p) {
+  return __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint32_t ld_sys_u32(const void* p) {
+  return __hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint16_t ld_sys_u16(const void* p) {
+  return __hip_atomic_load(reinterpret_cast<const uint16_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ float ld_sys_f32(const void* p) { return __uint_as_float(ld_sys_u32(p)); }
+__device__ __forceinline__ f32x4 ld_sys_f32x4(const void* p) {
+  const unsigned long long a = ld_sys_u64(p), b = ld_sys_u64(static_cast<const char*>(p) + 8);
+  return f32x4{__uint_as_float((uint32_t)a), __uint_as_float((uint32_t)(a >> 32)), __uint_as_float((uint32_t)b),
+               __uint_as_float((uint32_t)(b >> 32))};
+}
+
 }  // namespace dtfk
 
 #define DTFK_CHECK_LAUNCH() (hipGetLastError())

@@ -719,7 +719,7 @@ __device__ void compute(const Args& a, const int j, uint8_t* smem) {
               for (int rr = 0; rr < a.W; ++rr) {
                 uint2 v = gq[u][h];
                 if (rr != a.rank) {
-                  const unsigned long long x = __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(
+                  const unsigned long long x = ld_sys_u64((
                       static_cast<const char*>(a.peer_base[rr]) + soff + ((t * 4 + g) * 16 + r) * 8));
                   v = make_uint2((unsigned)x, (unsigned)(x >> 32));
                 }
@@ -744,10 +744,10 @@ __device__ void compute(const Args& a, const int j, uint8_t* smem) {
           if (rr != a.rank) {
             const char* ps = static_cast<const char*>(a.peer_base[rr]) + soff + IPC_SMALL;
             const unsigned long long x =
-                __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(ps + (g * 16 + r) * 8));
+                ld_sys_u64((ps + (g * 16 + r) * 8));
             v2[0] = bf2f((unsigned)x & 0xffff); v2[1] = bf2f(((unsigned)x) >> 16);
             v2[2] = bf2f((unsigned)(x >> 32) & 0xffff); v2[3] = bf2f((unsigned)(x >> 48));
-            vb = lane < 16 + NCLS ? bf2f(__builtin_nontemporal_load(reinterpret_cast<const uint16_t*>(ps + 512) + lane))
+            vb = lane < 16 + NCLS ? bf2f(ld_sys_u16(ps + 512 + 2 * lane))
                                   : 0.f;
           }
 #pragma unroll

@@ -747,11 +747,11 @@ __device__ void compute(const Args& a, const int j, uint8_t* smem) {
             if (rr != a.rank) {
               const char* pk = ps + (((w * NU + u) * 2 + h) * 64 + lane) * 16;
               if (a.gbf16) {
-                const unsigned long long x = __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(pk));
+                const unsigned long long x = ld_sys_u64((pk));
                 v = f32x4{bf2f((unsigned)x & 0xffff), bf2f(((unsigned)x) >> 16), bf2f((unsigned)(x >> 32) & 0xffff),
                           bf2f((unsigned)(x >> 48))};
               } else {
-                v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(pk));
+                v = ld_sys_f32x4((pk));
               }
             }
             sum[u][h] += v;
@@ -761,11 +761,11 @@ __device__ void compute(const Args& a, const int j, uint8_t* smem) {
           if (rr != a.rank) {
             const char* pk = ps + IPC_T48 + lane * 16;
             if (a.gbf16) {
-              const unsigned long long x = __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(pk));
+              const unsigned long long x = ld_sys_u64((pk));
               v = f32x4{bf2f((unsigned)x & 0xffff), bf2f(((unsigned)x) >> 16), bf2f((unsigned)(x >> 32) & 0xffff),
                         bf2f((unsigned)(x >> 48))};
             } else {
-              v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(pk));
+              v = ld_sys_f32x4((pk));
             }
           }
           s48 += v;
@@ -774,8 +774,8 @@ __device__ void compute(const Args& a, const int j, uint8_t* smem) {
           f32x4 v = D;
           float vb = gb;
           if (rr != a.rank) {
-            v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(ps + IPC_SMALL + lane * 16));
-            vb = lane < 16 + NCLS ? __builtin_nontemporal_load(reinterpret_cast<const float*>(ps + IPC_SMALL + 1024) + lane)
+            v = ld_sys_f32x4((ps + IPC_SMALL + lane * 16));
+            vb = lane < 16 + NCLS ? ld_sys_f32(ps + IPC_SMALL + 1024 + 4 * lane)
                                   : 0.f;
           }
           sD += v;

@@ -537,7 +537,7 @@ __global__ __launch_bounds__(64) void mlp_wgrad(
         const uint16_t* src = ipc_slot(ipc, r);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          g[i] += bf2f(r == ipc.rank ? gb[i] : __builtin_nontemporal_load(src + OFF_W1 + (kr + i) * HID + nc));
+          g[i] += bf2f(r == ipc.rank ? gb[i] : ld_sys_u16(src + OFF_W1 + (kr + i) * HID + nc));
       }
       if (n < HID) {
         const float step = (*lr_ptr) * ipc.scale;
@@ -627,7 +627,7 @@ __global__ __launch_bounds__(64) void mlp_wgrad(
       const int ic = min(i, 1109);
       float g = 0.f;
       for (int r = 0; r < ipc.W; ++r)
-        g += bf2f(r == ipc.rank ? gb[u] : __builtin_nontemporal_load(ipc_slot(ipc, r) + OFF_W2 + ic));
+        g += bf2f(r == ipc.rank ? gb[u] : ld_sys_u16(ipc_slot(ipc, r) + OFF_W2 + ic));
       if (i >= hi) continue;
       if (i >= 1110) { lred[i - 1110] = s[u]; continue; }
       if (!ok) continue;
@@ -742,7 +742,7 @@ __global__ __launch_bounds__(256) void mlp_ipc_reduce_apply(
   const long long off = IPC_FLAG_BYTES + (long long)parity * slot_bytes;
   float g0 = 0.f, g1 = 0.f;
   for (int r = 0; r < W; ++r) {
-    const uint32_t u = __builtin_nontemporal_load(
+    const uint32_t u = ld_sys_u32(
         reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(peer_base[r]) + off) + (i0 >> 1));
     g0 += bf2f(u & 0xFFFF);
     g1 += bf2f(u >> 16);

@@ -384,21 +384,35 @@ __global__ void argmax_correct(const float* __restrict__ x, const int64_t* __res
 
 // Per-bin positive / negative counts of predictions in [0, 1]; bin k covers
 // thresholds [k/(nb-1) ...).  Counts accumulate across calls (streaming).
-__global__ void auc_hist(const float* __restrict__ pred, const float* __restrict__ label, int64_t n,
-                         int nbins, unsigned long long* __restrict__ pos, unsigned long long* __restrict__ neg) {
-  extern __shared__ unsigned int h[];  // [2][nbins]
-  for (int i = threadIdx.x; i < 2 * nbins; i += blockDim.x) h[i] = 0;
-  __syncthreads();
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    float p = fminf(fmaxf(pred[i], 0.f), 1.f);
-    int b = (int)(p * (nbins - 1));
-    b = min(max(b, 0), nbins - 1);
-    atomicAdd(&h[(label[i] > 0.5f ? 0 : nbins) + b], 1u);
+// streaming_auc's thresholds (TF contrib.metrics): t_0 = -1e-7, t_j = j/(T-1) for
+// 0 < j < T-1 (a Python double rounded to fp32), t_{T-1} = 1 + 1e-7.  Bin k of a
+// prediction p = #{i : t_i < p} in [0, T]; the confusion counts at threshold i
+// (predicted positive <=> p > t_i) are then suffix sums over bins > i.
+__device__ __forceinline__ int tf_threshold_bin(float p, int T) {
+  if (!(p > -1e-7f)) return 0;          // (also NaN)
+  if (p > 1.f + 1e-7f) return T;
+  int lo = 1, hi = T - 1;               // first interior j with t_j >= p
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    const float t = (float)((double)mid / (double)(T - 1));
+    if (t < p) lo = mid + 1; else hi = mid;
   }
+  return lo;                            // 1 (t_0) + (lo - 1) interior thresholds below p
+}
+
+// labels: nonzero = positive (TF casts to bool); pos/neg: [T + 1] bins
+__global__ void auc_hist(const float* __restrict__ pred, const float* __restrict__ label, int64_t n,
+                         int T, unsigned long long* __restrict__ pos, unsigned long long* __restrict__ neg) {
+  extern __shared__ unsigned int h[];  // [2][T + 1]
+  const int nb = T + 1;
+  for (int i = threadIdx.x; i < 2 * nb; i += blockDim.x) h[i] = 0;
   __syncthreads();
-  for (int i = threadIdx.x; i < nbins; i += blockDim.x) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    atomicAdd(&h[(label[i] != 0.f ? 0 : nb) + tf_threshold_bin(pred[i], T)], 1u);
+  __syncthreads();
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) {
     if (h[i]) atomicAdd(&pos[i], (unsigned long long)h[i]);
-    if (h[nbins + i]) atomicAdd(&neg[i], (unsigned long long)h[nbins + i]);
+    if (h[nb + i]) atomicAdd(&neg[i], (unsigned long long)h[nb + i]);
   }
 }
 
@@ -558,8 +572,10 @@ hipError_t dtfk_argmax_correct(const float* x, const int64_t* labels, int B, int
 }
 hipError_t dtfk_auc_hist(const float* pred, const float* label, int64_t n, int nbins,
                          unsigned long long* pos, unsigned long long* neg, hipStream_t s) {
+  // nbins = T + 1 histogram bins for T thresholds
+  if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(auc_hist, dim3(nblk(n, 256, 1024)), dim3(256), 2 * nbins * sizeof(unsigned int), s, pred,
-                     label, n, nbins, pos, neg);
+                     label, n, nbins - 1, pos, neg);
   return hipGetLastError();
 }
 hipError_t dtfk_multi_tensor_apply(const void* tab, const void* chunks, int nchunks, int kind, int gbf,

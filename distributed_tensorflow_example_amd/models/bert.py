@@ -93,7 +93,7 @@ def _wgrad_split(T: int, out: int, inp: int) -> int:
     """Token-slab count for the weight-gradient GEMM.  dW = gy^T x has a long
     reduction (T = B*S tokens) and few output tiles (36-144 of 128x128 for
     BERT-base), so one hipBLASLt GEMM leaves most of the 256 CUs idle
-    (~0.5 PFLOP/s measured, scripts/wgrad_probe.py); slabs run as one batched
+    (~0.5 PFLOP/s measured, scripts/probes/wgrad_probe.py); slabs run as one batched
     GEMM with ~4 tile waves and are reduced in fp32 (1.5-2.5x faster)."""
     tiles = max(1, (out // 128) * (inp // 128))
     s = 1

@@ -299,7 +299,7 @@ class MLPStepRunner:
     prefetch="side": double-buffered stage, the next chunk is copied on a side
         stream under the current replay, synchronised by events.  On MI355X /
         ROCm 7 every cross-queue event dependency costs ~150 us of GPU idle
-        (measured, scripts/diag_mlp3.py: 14.9 us/step vs 13.2 serial; the same
+        (measured, scripts/probes/diag_mlp3.py: 14.9 us/step vs 13.2 serial; the same
         fork/join captured inside the graph: 16.4), so it only pays where
         cross-queue waits are cheap.
     """

@@ -38,8 +38,9 @@ class SparseLRTrainer:
                                   name="weights/Variable")
         self.b = torch.zeros(1, dtype=torch.float32, device=self.device, requires_grad=True)
         self.global_step = 0
-        self.auc_pos = torch.zeros(auc_bins, dtype=torch.int64, device=self.device)
-        self.auc_neg = torch.zeros(auc_bins, dtype=torch.int64, device=self.device)
+        # streaming_auc's num_thresholds = auc_bins -> auc_bins + 1 histogram bins
+        self.auc_pos = torch.zeros(auc_bins + 1, dtype=torch.int64, device=self.device)
+        self.auc_neg = torch.zeros(auc_bins + 1, dtype=torch.int64, device=self.device)
 
     # ----------------------------------------------------------------- steps
     def _forward(self, batch):

@@ -340,27 +340,56 @@ def argmax_correct(logits, labels) -> torch.Tensor:
     return cnt[0]
 
 
-def auc_histogram_(pred, labels, pos_counts, neg_counts):
-    """Accumulate positive/negative histograms of predictions over len(pos) bins."""
+def auc_thresholds(num_thresholds: int) -> torch.Tensor:
+    """streaming_auc's fp32 thresholds: -1e-7, j/(T-1) for 0 < j < T-1, 1 + 1e-7 (TF contrib.metrics)."""
+    t = [0.0 - 1e-7] + [(i + 1) * 1.0 / (num_thresholds - 1) for i in range(num_thresholds - 2)] + [1.0 + 1e-7]
+    return torch.tensor(t, dtype=torch.float32)
+
+
+def auc_histogram_(pred, labels, pos_counts, neg_counts, weights=None):
+    """Accumulate positive / negative histograms of predictions over the T + 1
+    bins between streaming_auc's T thresholds (len(pos_counts) = T + 1): bin k
+    holds predictions p with #{i : t_i < p} = k.  Labels: nonzero = positive."""
     nb = pos_counts.numel()
-    if not pred.is_cuda:
-        p = pred.float().clamp(0, 1).reshape(-1)
-        b = (p * (nb - 1)).long().clamp(0, nb - 1)
-        lab = labels.reshape(-1).float() > 0.5
-        pos_counts += torch.bincount(b[lab], minlength=nb)
-        neg_counts += torch.bincount(b[~lab], minlength=nb)
+    if nb < 3:
+        raise ValueError("need num_thresholds >= 2 (T + 1 >= 3 bins)")
+    if not pred.is_cuda or weights is not None:
+        p = pred.detach().float().reshape(-1).cpu()
+        b = torch.searchsorted(auc_thresholds(nb - 1), p.contiguous())
+        lab = labels.detach().reshape(-1).cpu() != 0
+        wt = None if weights is None else torch.broadcast_to(torch.as_tensor(weights).float().cpu(), p.shape).reshape(-1)
+        pos_counts += torch.bincount(b[lab], weights=None if wt is None else wt[lab], minlength=nb).to(
+            pos_counts.device, pos_counts.dtype)
+        neg_counts += torch.bincount(b[~lab], weights=None if wt is None else wt[~lab], minlength=nb).to(
+            neg_counts.device, neg_counts.dtype)
         return
     _C().auc_hist(pred.contiguous().float().reshape(-1), labels.contiguous().float().reshape(-1),
                   pos_counts, neg_counts)
 
 
-def auc_from_histograms(pos, neg) -> float:
-    """Trapezoidal ROC AUC from per-bin counts (thresholds at bin edges)."""
-    pos = pos.double().cpu().flip(0).cumsum(0)
-    neg = neg.double().cpu().flip(0).cumsum(0)
-    P, N = float(pos[-1]), float(neg[-1])
-    if P == 0 or N == 0:
-        return float("nan")
-    tpr = torch.cat([torch.zeros(1, dtype=torch.float64), pos / P])
-    fpr = torch.cat([torch.zeros(1, dtype=torch.float64), neg / N])
-    return float(torch.trapz(tpr, fpr))
+def auc_confusion(pos, neg):
+    """(tp, fn, tn, fp) per threshold, fp32 like TF's local variables, from T+1-bin histograms."""
+    pos = pos.detach().double().cpu()
+    neg = neg.detach().double().cpu()
+    tp = pos.flip(0).cumsum(0).flip(0)[1:]          # sum over bins k > i
+    fp = neg.flip(0).cumsum(0).flip(0)[1:]
+    return (tp.float(), (pos.sum() - tp).float(), (neg.sum() - fp).float(), fp.float())
+
+
+def auc_from_confusion(tp, fn, tn, fp, curve: str = "ROC") -> float:
+    """TF contrib.metrics compute_auc: trapezoid over thresholds, epsilon 1e-6, fp32."""
+    eps = 1e-6
+    tp, fn, tn, fp = (torch.as_tensor(v).float().cpu() for v in (tp, fn, tn, fp))
+    rec = (tp + eps) / (tp + fn + eps)
+    if curve == "ROC":
+        x = fp / (fp + tn + eps)
+        y = rec
+    else:
+        x = rec
+        y = (tp + eps) / (tp + fp + eps)
+    return float(torch.sum((x[:-1] - x[1:]) * (y[:-1] + y[1:]) / 2.0))
+
+
+def auc_from_histograms(pos, neg, curve: str = "ROC") -> float:
+    """streaming_auc's value from T+1-bin positive / negative histograms."""
+    return auc_from_confusion(*auc_confusion(pos, neg), curve=curve)

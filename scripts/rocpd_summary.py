@@ -1,0 +1,29 @@
+"""Per-kernel summary (CSV) of a rocprofv3 --kernel-trace database (rocpd SQLite).
+
+    python scripts/rocpd_summary.py gpurun_out/<dir>/<name>_results.db [out.csv]
+
+Columns: kernel name, calls, total_us, avg_us, pct, vgpr, sgpr, lds, scratch, grid.
+"""
+import csv
+import sqlite3
+import sys
+
+
+def main():
+    db = sys.argv[1]
+    out = sys.argv[2] if len(sys.argv) > 2 else None
+    c = sqlite3.connect(db)
+    rows = c.execute(
+        "select name, count(*), sum(duration), avg(duration), max(vgpr_count), max(sgpr_count), max(lds_size), "
+        "max(scratch_size), max(grid_x * grid_y * grid_z) from kernels group by name order by sum(duration) desc"
+    ).fetchall()
+    tot = sum(r[2] for r in rows) or 1
+    table = [["kernel", "calls", "total_us", "avg_us", "pct", "vgpr", "sgpr", "lds_bytes", "scratch", "grid_threads"]]
+    for name, n, s, a, v, sg, l, sc, gr in rows:
+        table.append([name[:160], n, round(s / 1e3, 2), round(a / 1e3, 3), round(100.0 * s / tot, 2), v, sg, l, sc, gr])
+    f = open(out, "w", newline="") if out else sys.stdout
+    csv.writer(f).writerows(table)
+
+
+if __name__ == "__main__":
+    main()

@@ -15,15 +15,34 @@
 #
 # Accepted forms: --name=value, --name value, -s value, -svalue (short name),
 # --bool / --nobool / --bool=true|false|1|0 for booleans, '--' ends the flags.
-# Types are validated (integer, float, boolean).  --help / -h prints the flag
-# table and makes FLAGS return 2 (FLAGS_HELP holds the text).  Multi-value
-# flags (DEFINE_multi_*) accumulate every occurrence into a bash array
-# FLAGS_<name>.  flags_reset forgets every definition.
+# Types are validated (integer, float, boolean).  Multi-value flags
+# (DEFINE_multi_*) accumulate every occurrence into a bash array FLAGS_<name>.
+# flags_reset forgets every definition.
+#
+# Help surface (reference shflags:1842-2097): --help / -h (usage, description,
+# flag table), --helpshort (usage + flag names only), --helpxml (XML flag
+# dump), --helpman (roff man page on stdout), --version (HELP_VERSION).  Each
+# makes FLAGS print and return 2 (FLAGS_HELP holds the text).  Optional
+# HELP_COMMAND / HELP_VERSION / HELP_DESCRIPTION / HELP_CONTACT /
+# HELP_COPYRIGHT variables fill the texts.  Flags defined with a trailing
+# 'required' category (DEFINE_string name default help short required) must be
+# given on the command line.
+#
+# Parsing is pure bash, so long flags work whatever getopt(1) the system has;
+# flags_getoptIsEnh / flags_getoptIsStd / flags_getoptInfo still report the
+# system getopt flavour (enhanced = util-linux `getopt -T` exits 4) for scripts
+# that branch on it.
 
+[ -n "${FLAGS_VERSION:-}" ] && [ -n "${__dtf_flags_loaded:-}" ] && return 0
+__dtf_flags_loaded=1
+FLAGS_VERSION='1.0.5'       # API level of the shflags surface reproduced here
+FLAGS_TRUE=0
+FLAGS_FALSE=1
+FLAGS_ERROR=2
 __dtf_flag_names=()
 
-_dtf_flags_define() {   # type name default help [short]
-  local type=$1 name=$2 default=$3 help=$4 short=${5:-}
+_dtf_flags_define() {   # type name default help [short] [required]
+  local type=$1 name=$2 default=$3 help=$4 short=${5:-} cat=${6:-}
   if [ $# -lt 4 ]; then
     echo "flags: DEFINE_${type} needs: name default help [short]" >&2
     return 1
@@ -45,6 +64,7 @@ _dtf_flags_define() {   # type name default help [short]
   eval "__dtf_default_${name}=\"\${default}\""
   eval "__dtf_help_${name}=\"\${help}\""
   eval "__dtf_short_${name}=\"\${short}\""
+  eval "__dtf_required_${name}=$([ "${cat}" = required ] && echo 1 || echo 0)"
   if [[ ${type} == multi_* ]]; then
     eval "FLAGS_${name}=()"
     [ -n "${default}" ] && eval "FLAGS_${name}=(\"\${default}\")"
@@ -98,11 +118,41 @@ _dtf_flags_set() {      # name value
   fi
 }
 
-flags_help() {          # the flag table (what --help prints)
-  local n t d h s
+_dtf_flags_command() { echo "${HELP_COMMAND:-${FLAGS_PARENT:-${0##*/}}}"; }
+
+flags_usage() {         # synopsis: required flags bare, optional ones in brackets
+  local n s u line
+  line="USAGE: $(_dtf_flags_command)"
+  for n in "${__dtf_flag_names[@]}"; do
+    eval "s=\${__dtf_short_${n}} u=\${__dtf_required_${n}}"
+    local f="--${n}"
+    [ -n "${s}" ] && f="-${s}|--${n}"
+    if [ "${u}" = 1 ]; then line+=" ${f}"; else line+=" [${f}]"; fi
+  done
+  echo "${line} [args]"
+}
+
+flags_helpshort() {     # usage + flag names and types, no descriptions
+  local n t s
+  flags_usage
+  echo "flags:"
+  for n in "${__dtf_flag_names[@]}"; do
+    eval "t=\${__dtf_type_${n}} s=\${__dtf_short_${n}}"
+    if [ -n "${s}" ]; then printf '  -%s,--%s (%s)\n' "${s}" "${n}" "${t}"
+    else printf '  --%s (%s)\n' "${n}" "${t}"
+    fi
+  done
+}
+
+flags_help() {          # usage, description and the flag table (what --help prints)
+  local n t d h s u
+  flags_usage
+  [ -n "${HELP_DESCRIPTION:-}" ] && printf '%s\n' "${HELP_DESCRIPTION}"
   echo "flags:"
   for n in "${__dtf_flag_names[@]}"; do
     eval "t=\${__dtf_type_${n}} d=\${__dtf_default_${n}} h=\${__dtf_help_${n}} s=\${__dtf_short_${n}}"
+    eval "u=\${__dtf_required_${n}}"
+    [ "${u}" = 1 ] && h="${h} [required]"
     if [ -n "${s}" ]; then
       printf '  -%s,--%s:  %s (default: %s, type: %s)\n' "${s}" "${n}" "${h}" "'${d}'" "${t}"
     else
@@ -111,17 +161,84 @@ flags_help() {          # the flag table (what --help prints)
   done
 }
 
+_dtf_xml() {            # XML-escape $1
+  local v=${1//&/&amp;}
+  v=${v//</&lt;}; v=${v//>/&gt;}; v=${v//\"/&quot;}
+  printf '%s' "${v}"
+}
+
+flags_helpxml() {       # machine-readable flag dump
+  local n t d h s u
+  echo '<?xml version="1.0"?>'
+  echo '<AllFlags>'
+  echo "  <name>$(_dtf_xml "$(_dtf_flags_command)")</name>"
+  echo "  <version>$(_dtf_xml "${HELP_VERSION:-unknown}")</version>"
+  echo "  <description>$(_dtf_xml "${HELP_DESCRIPTION:-}")</description>"
+  for n in "${__dtf_flag_names[@]}"; do
+    eval "t=\${__dtf_type_${n}} d=\${__dtf_default_${n}} h=\${__dtf_help_${n}} s=\${__dtf_short_${n}}"
+    eval "u=\${__dtf_required_${n}}"
+    echo '  <flag>'
+    echo "    <category>$([ "${u}" = 1 ] && echo required || echo optional)</category>"
+    echo "    <name>$(_dtf_xml "${n}")</name>"
+    echo "    <short_name>$(_dtf_xml "${s}")</short_name>"
+    echo "    <meaning>$(_dtf_xml "${h}")</meaning>"
+    echo "    <default>$(_dtf_xml "${d}")</default>"
+    echo "    <current>$(_dtf_xml "$(eval "echo \"\${FLAGS_${n}[*]}\"")")</current>"
+    echo "    <type>${t}</type>"
+    echo '  </flag>'
+  done
+  echo '</AllFlags>'
+}
+
+flags_helpman() {       # man(7) page on stdout (pipe to `man -l -`)
+  local n t d h s cmd
+  cmd=$(_dtf_flags_command)
+  echo ".TH \"$(echo "${cmd}" | tr '[:lower:]' '[:upper:]')\" 1 \"\" \"${HELP_VERSION:-}\""
+  echo '.SH NAME'
+  echo "${cmd}"
+  echo '.SH SYNOPSIS'
+  flags_usage | sed 's/^USAGE: //'
+  if [ -n "${HELP_DESCRIPTION:-}" ]; then echo '.SH DESCRIPTION'; printf '%s\n' "${HELP_DESCRIPTION}"; fi
+  echo '.SH OPTIONS'
+  for n in "${__dtf_flag_names[@]}"; do
+    eval "t=\${__dtf_type_${n}} d=\${__dtf_default_${n}} h=\${__dtf_help_${n}} s=\${__dtf_short_${n}}"
+    echo '.TP'
+    if [ -n "${s}" ]; then echo "\\fB\\-${s}\\fR, \\fB\\-\\-${n}\\fR"; else echo "\\fB\\-\\-${n}\\fR"; fi
+    echo "${h} (default: ${d}; type: ${t})"
+  done
+  [ -n "${HELP_CONTACT:-}" ] && { echo '.SH CONTACT'; printf '%s\n' "${HELP_CONTACT}"; }
+  [ -n "${HELP_COPYRIGHT:-}" ] && { echo '.SH COPYRIGHT'; printf '%s\n' "${HELP_COPYRIGHT}"; }
+  return 0
+}
+
+flags_version() { echo "$(_dtf_flags_command) ${HELP_VERSION:-unknown}"; }
+
+# system getopt flavour: util-linux (enhanced, long options) returns 4 for -T
+__dtf_getopt_enh() { ${FLAGS_GETOPT_CMD:-getopt} -T >/dev/null 2>&1; [ $? -eq 4 ]; }
+flags_getoptIsEnh() { __dtf_getopt_enh; }
+flags_getoptIsStd() { ! __dtf_getopt_enh; }
+flags_getoptInfo() {
+  echo "flags:DEBUG shell: bash ${BASH_VERSION}" >&2
+  echo "flags:DEBUG getopt: $(${FLAGS_GETOPT_CMD:-getopt} --version 2>&1 | head -1)" >&2
+  echo "flags:DEBUG getopt flavour: $(__dtf_getopt_enh && echo enhanced || echo standard)" >&2
+  echo "flags:DEBUG parser: built-in (long flags on any getopt)" >&2
+}
+
 FLAGS() {               # parse "$@"; sets FLAGS_<name> and FLAGS_ARGV; 2 after --help
   FLAGS_ARGV=''
   FLAGS_HELP=''
   local arg name value type rest=()
-  local saw_multi=' '
+  local saw_multi=' ' given=' '
   while [ $# -gt 0 ]; do
     arg=$1
     shift
     case "${arg}" in
       --) rest+=("$@"); break ;;
       -h|--help) FLAGS_HELP=$(flags_help); echo "${FLAGS_HELP}"; return 2 ;;
+      --helpshort) FLAGS_HELP=$(flags_helpshort); echo "${FLAGS_HELP}"; return 2 ;;
+      --helpxml) FLAGS_HELP=$(flags_helpxml); echo "${FLAGS_HELP}"; return 2 ;;
+      --helpman) FLAGS_HELP=$(flags_helpman); echo "${FLAGS_HELP}"; return 2 ;;
+      --version) FLAGS_HELP=$(flags_version); echo "${FLAGS_HELP}"; return 2 ;;
       --*=*) name=${arg%%=*}; name=${name#--}; value=${arg#*=} ;;
       --*)
         name=${arg#--}
@@ -154,18 +271,29 @@ FLAGS() {               # parse "$@"; sets FLAGS_<name> and FLAGS_ARGV; 2 after 
       saw_multi+="${name} "
     fi
     _dtf_flags_set "${name}" "${value}" || return 1
+    given+="${name} "
   done
   local a
   for a in "${rest[@]}"; do
     FLAGS_ARGV="${FLAGS_ARGV:+${FLAGS_ARGV} }'${a//\'/\'\\\'\'}'"
   done
+  local u missing=''
+  for name in "${__dtf_flag_names[@]}"; do
+    eval "u=\${__dtf_required_${name}}"
+    [ "${u}" = 1 ] && [[ ${given} != *" ${name} "* ]] && missing+=" --${name}"
+  done
+  if [ -n "${missing}" ]; then
+    echo "flags: missing required flag(s):${missing}" >&2
+    return 1
+  fi
   return 0
 }
 
 flags_reset() {         # forget every definition (tests, re-sourcing)
   local n
   for n in "${__dtf_flag_names[@]}"; do
-    unset "FLAGS_${n}" "__dtf_type_${n}" "__dtf_default_${n}" "__dtf_help_${n}" "__dtf_short_${n}"
+    unset "FLAGS_${n}" "__dtf_type_${n}" "__dtf_default_${n}" "__dtf_help_${n}" "__dtf_short_${n}" \
+      "__dtf_required_${n}"
   done
   __dtf_flag_names=()
   FLAGS_ARGV=''

@@ -267,6 +267,63 @@ def test_streaming_auc_and_local_init():
     assert abs(a - exact) < 5e-3
 
 
+def _tf_streaming_auc_numpy(p, l, T=200):
+    """TF contrib.metrics.streaming_auc from its definition (thresholds, confusion
+    counts at p > t, compute_auc with epsilon 1e-6), in numpy fp32."""
+    t = np.array([0.0 - 1e-7] + [(i + 1) * 1.0 / (T - 1) for i in range(T - 2)] + [1.0 + 1e-7], np.float32)
+    above = p.astype(np.float32)[None, :] > t[:, None]
+    pos = l.astype(bool)[None, :]
+    tp = (above & pos).sum(1).astype(np.float32)
+    fn = (~above & pos).sum(1).astype(np.float32)
+    tn = (~above & ~pos).sum(1).astype(np.float32)
+    fp = (above & ~pos).sum(1).astype(np.float32)
+    e = np.float32(1e-6)
+    rec = (tp + e) / (tp + fn + e)
+    fpr = fp / (fp + tn + e)
+    return float(np.sum((fpr[:-1] - fpr[1:]) * (rec[:-1] + rec[1:]) / np.float32(2.0))), (tp, fn, tn, fp)
+
+
+def test_streaming_auc_tf_semantics():
+    """TF variable names, exact TF thresholds / compute_auc, update_op = post-update
+    value, value fetched with the update = pre-update value."""
+    pred = tf.placeholder(tf.float32, [None])
+    lab = tf.placeholder(tf.float32, [None])
+    auc, upd = tf.contrib.metrics.streaming_auc(pred, lab)
+    names = sorted(v.name for v in tf.local_variables() if v.name.startswith("auc"))
+    assert names == ["auc/false_negatives:0", "auc/false_positives:0", "auc/true_negatives:0",
+                     "auc/true_positives:0"]
+    rng = np.random.default_rng(1)
+    batches = []
+    for _ in range(3):
+        l = (rng.random(700) > 0.5).astype(np.float32)
+        p = rng.random(700).astype(np.float32)
+        p[:5] = [0.0, 1.0, 0.5, 1.0 / 199, 198.0 / 199]      # on / next to thresholds
+        batches.append((p, l))
+    with tf.Session() as sess:
+        sess.run(tf.local_variables_initializer())
+        seen_p, seen_l = [], []
+        for p, l in batches:
+            before = _tf_streaming_auc_numpy(np.concatenate(seen_p), np.concatenate(seen_l))[0] if seen_p else None
+            v_pre, v_post = sess.run([auc, upd], {pred: p, lab: l})
+            seen_p.append(p)
+            seen_l.append(l)
+            ref, (tp, fn, tn, fp) = _tf_streaming_auc_numpy(np.concatenate(seen_p), np.concatenate(seen_l))
+            assert abs(float(v_post) - ref) < 1e-6, (float(v_post), ref)
+            if before is not None:
+                assert abs(float(v_pre) - before) < 1e-6
+            # fetch order does not change what the value tensor reports in that run
+        v_post2, v_pre2 = sess.run([upd, auc], {pred: batches[0][0], lab: batches[0][1]})
+        assert abs(float(v_pre2) - ref) < 1e-6
+        got = {v.name: v.value.numpy() for v in tf.local_variables() if v.name.startswith("auc")}
+    seen_p.append(batches[0][0])
+    seen_l.append(batches[0][1])
+    _, (tp, fn, tn, fp) = _tf_streaming_auc_numpy(np.concatenate(seen_p), np.concatenate(seen_l))
+    np.testing.assert_array_equal(got["auc/true_positives:0"], tp)
+    np.testing.assert_array_equal(got["auc/false_negatives:0"], fn)
+    np.testing.assert_array_equal(got["auc/true_negatives:0"], tn)
+    np.testing.assert_array_equal(got["auc/false_positives:0"], fp)
+
+
 def test_embedding_lookup_sparse_lr_graph():
     """lr2.py model: W[F,1], sum combiner over (fid, fval), sigmoid xent, SGD."""
     F = 50

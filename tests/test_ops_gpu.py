@@ -219,6 +219,11 @@ def test_auc_histogram(native):
     n, nb = 20000, 200
     lab = (torch.rand(n) > 0.7).float()
     pred = torch.sigmoid(torch.randn(n) + 1.5 * lab)
+    # predictions exactly on TF's fp32 thresholds and one ulp either side: the GPU
+    # binary search must bin them like the CPU searchsorted (p > t is strict)
+    t = ops.auc_thresholds(nb - 1)
+    edge = torch.cat([t, torch.nextafter(t, torch.full_like(t, 2.0)), torch.nextafter(t, torch.full_like(t, -2.0))])
+    pred[: edge.numel()] = edge
     pc, nc = torch.zeros(nb, dtype=torch.int64), torch.zeros(nb, dtype=torch.int64)
     ops.auc_histogram_(pred, lab, pc, nc)
     pg, ng = torch.zeros(nb, dtype=torch.int64, device="cuda"), torch.zeros(nb, dtype=torch.int64, device="cuda")

@@ -79,3 +79,36 @@ def test_run_sh_writes_file_lists(tmp_path):
     assert r.returncode == 0, r.stdout + r.stderr
     lines = (tmp_path / "tl").read_text().split()
     assert len(lines) == 3 and all("part-" in l for l in lines)
+
+
+def test_help_variants_version_and_required():
+    defs = DEFS + "DEFINE_string 'train' '' 'training files' 't' required\n"
+    env_txt = "HELP_VERSION=2.1\nHELP_DESCRIPTION='Sparse LR launcher'\nHELP_COMMAND=run_lr2\n"
+    r = _bash(env_txt + defs + 'FLAGS "$@"; echo "rc=$?"', "--helpshort")
+    assert "USAGE: run_lr2 [-j|--job_name]" in r.stdout and "-t|--train" in r.stdout
+    assert "  -j,--job_name (string)" in r.stdout and "job name" not in r.stdout and "rc=2" in r.stdout
+    r = _bash(env_txt + defs + 'FLAGS "$@"; echo "rc=$?"', "--version")
+    assert r.stdout.splitlines()[0] == "run_lr2 2.1" and "rc=2" in r.stdout
+    r = _bash(env_txt + defs + 'FLAGS "$@"', "--helpxml")
+    import xml.etree.ElementTree as ET
+    root = ET.fromstring(r.stdout)
+    assert root.find("name").text == "run_lr2" and root.find("version").text == "2.1"
+    flags = {f.find("name").text: f for f in root.findall("flag")}
+    assert flags["train"].find("category").text == "required"
+    assert flags["task_index"].find("default").text == "0" and flags["task_index"].find("type").text == "integer"
+    r = _bash(env_txt + defs + 'FLAGS "$@"', "--helpman")
+    assert r.stdout.startswith('.TH "RUN_LR2" 1') and ".SH OPTIONS" in r.stdout and "Sparse LR launcher" in r.stdout
+    r = _bash(env_txt + defs + 'FLAGS "$@"; echo "rc=$?"', "--job_name=worker")
+    assert "rc=1" in r.stdout and "missing required flag(s): --train" in r.stderr
+    r = _bash(env_txt + defs + 'FLAGS "$@" && echo "ok $FLAGS_train"', "-t", "/data/a")
+    assert r.stdout.strip() == "ok /data/a", r.stderr
+    r = _bash(env_txt + defs + 'FLAGS "$@"; echo "rc=$?"', "--help")
+    assert "Sparse LR launcher" in r.stdout and "training files [required]" in r.stdout
+
+
+def test_getopt_introspection():
+    r = _bash('if flags_getoptIsEnh; then echo enh; fi; if flags_getoptIsStd; then echo std; fi; '
+              'flags_getoptInfo; echo "v=$FLAGS_VERSION"')
+    out = r.stdout.split()
+    assert (("enh" in out) != ("std" in out)) and "v=1.0.5" in out
+    assert "flags:DEBUG parser: built-in" in r.stderr

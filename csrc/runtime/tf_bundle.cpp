@@ -15,6 +15,15 @@
 //   BundleHeaderProto{num_shards=1, endianness=2, version=3{producer=1,min_consumer=2}}
 //   BundleEntryProto {dtype=1, shape=2{dim=2{size=1,name=2}}, shard_id=3, offset=4,
 //                     size=5, crc32c=6 (fixed32, masked crc of the bytes), slices=7}
+//   TensorSliceProto {extent=1{start=1, length=2 (oneof: absent = full extent)}}
+// Partitioned variables (TF Saver + SaveSliceInfo, [TF-semantics]): the full
+// tensor's key carries dtype, full shape and one TensorSliceProto per saved
+// slice, and no data; each slice's bytes live under the key
+// EncodeTensorNameSlice(name, slice) = OrderedCode NumIncreasing(0), String(name),
+// NumIncreasing(dims), then per dim SignedNumIncreasing(start),
+// SignedNumIncreasing(length) (length -1 = full).  Like SaveV2, every slice of
+// a partitioned variable goes through this path (even a single partition).
+// Shard indexes merge the slice lists of a full key written by several shards.
 #include <torch/extension.h>
 
 #include <algorithm>
@@ -231,6 +240,93 @@ static std::vector<std::pair<std::string, std::string>> read_table(const std::st
   return out;
 }
 
+// ---- OrderedCode (tensorflow/core/lib/strings/ordered_code) subset used by slice keys
+static void oc_num_increasing(std::string& d, uint64_t v) {
+  unsigned char buf[9];
+  int len = 0;
+  while (v > 0) {
+    ++len;
+    buf[9 - len] = (unsigned char)(v & 0xff);
+    v >>= 8;
+  }
+  buf[9 - len - 1] = (unsigned char)len;
+  d.append(reinterpret_cast<const char*>(buf + 9 - len - 1), len + 1);
+}
+static void oc_string(std::string& d, const std::string& s) {
+  for (char c : s) {
+    if (c == '\x00') d.append("\x00\xff", 2);
+    else if (c == '\xff') d.append("\xff\x00", 2);
+    else d.push_back(c);
+  }
+  d.append("\x00\x01", 2);
+}
+static void oc_signed_num_increasing(std::string& d, int64_t val) {
+  static const unsigned char kHeader[11][2] = {{0, 0},       {0x80, 0}, {0xc0, 0}, {0xe0, 0},
+                                               {0xf0, 0},    {0xf8, 0}, {0xfc, 0}, {0xfe, 0},
+                                               {0xff, 0},    {0xff, 0x80}, {0xff, 0xc0}};
+  const uint64_t x = val < 0 ? ~(uint64_t)val : (uint64_t)val;
+  if (x < 64) {
+    d.push_back((char)(kHeader[1][0] ^ (unsigned char)val));
+    return;
+  }
+  // significant bits after the sign -> encoded length (7 payload bits per byte)
+  int bits = 64 - __builtin_clzll(x);
+  int len = (bits + 1 + 6) / 7;   // bits 7..13 -> 2, 14..20 -> 3, ...
+  if (len > 10) len = 10;
+  unsigned char buf[10];
+  const unsigned char sign = val < 0 ? 0xff : 0x00;
+  buf[0] = buf[1] = sign;
+  for (int i = 0; i < 8; ++i) buf[2 + i] = (unsigned char)((uint64_t)val >> (56 - 8 * i));
+  unsigned char* b = buf + 10 - len;
+  b[0] ^= kHeader[len][0];
+  b[1] ^= kHeader[len][1];
+  d.append(reinterpret_cast<const char*>(b), len);
+}
+using Extents = std::vector<std::pair<int64_t, int64_t>>;   // (start, length); length -1 = full
+static std::string encode_slice_key(const std::string& name, const Extents& ext) {
+  std::string k;
+  oc_num_increasing(k, 0);
+  oc_string(k, name);
+  oc_num_increasing(k, ext.size());
+  for (auto& e : ext) {
+    oc_signed_num_increasing(k, e.second < 0 ? 0 : e.first);
+    oc_signed_num_increasing(k, e.second);
+  }
+  return k;
+}
+static std::string encode_slice_proto(const Extents& ext) {
+  std::string sp;
+  for (auto& e : ext) {
+    std::string x;
+    if (e.second >= 0) {
+      if (e.first) wire::put_int(x, 1, e.first);
+      wire::put_int(x, 2, e.second);   // oneof member: serialized even when 0
+    }
+    wire::put_bytes(sp, 1, x);
+  }
+  return sp;
+}
+static Extents decode_slice_proto(const std::string& sp) {
+  Extents out;
+  wire::Reader r(sp.data(), sp.size());
+  int f, wt;
+  while (r.next(f, wt)) {
+    if (f == 1 && wt == wire::LEN) {
+      std::string x = r.bytes();
+      wire::Reader xr(x.data(), x.size());
+      int64_t start = 0, len = -1;
+      int f2, w2;
+      while (xr.next(f2, w2)) {
+        if (f2 == 1 && w2 == wire::VARINT) start = (int64_t)xr.varint();
+        else if (f2 == 2 && w2 == wire::VARINT) len = (int64_t)xr.varint();
+        else xr.skip(w2);
+      }
+      out.emplace_back(start, len);
+    } else r.skip(wt);
+  }
+  return out;
+}
+
 struct Entry {
   int dtype = 0;
   std::vector<int64_t> shape;
@@ -363,6 +459,28 @@ class Writer {
     off_ += nbytes;
     entries_[name] = e;
   }
+  // One slice of a partitioned variable: data under the slice key, the slice
+  // recorded in the full tensor's entry (dtype, full shape, slices; no data).
+  void add_slice(const std::string& full_name, int dtype, std::vector<int64_t> full_shape, Extents ext,
+                 py::buffer buf) {
+    if (full_name.empty()) throw std::runtime_error("empty tensor name");
+    if (ext.size() != full_shape.size()) throw std::runtime_error("slice rank != tensor rank for " + full_name);
+    std::vector<int64_t> sshape;
+    for (size_t d = 0; d < ext.size(); ++d) {
+      const int64_t len = ext[d].second < 0 ? full_shape[d] : ext[d].second;
+      const int64_t st = ext[d].second < 0 ? 0 : ext[d].first;
+      if (st < 0 || len < 0 || st + len > full_shape[d]) throw std::runtime_error("slice out of range: " + full_name);
+      sshape.push_back(len);
+    }
+    Entry& fe = entries_[full_name];
+    if (fe.size != 0 || (fe.dtype && fe.dtype != dtype) || (!fe.shape.empty() && fe.shape != full_shape))
+      throw std::runtime_error("conflicting entries for sliced tensor " + full_name);
+    fe.dtype = dtype;
+    fe.shape = full_shape;
+    fe.shard_id = 0;
+    wire::put_bytes(fe.slices_raw, 7, encode_slice_proto(ext));
+    add(encode_slice_key(full_name, ext), dtype, sshape, buf);
+  }
   void finish() {
     if (f_) {
       fflush(f_);
@@ -390,8 +508,17 @@ void merge_shard_indexes(const std::string& prefix, int num_shards, bool remove_
     std::string p = prefix + ".index.shard-" + std::to_string(k);
     for (auto& kv : read_table(p, true)) {
       if (kv.first.empty()) continue;
-      if (all.count(kv.first)) throw std::runtime_error("tensor in two shards: " + kv.first);
-      all[kv.first] = kv.second;
+      auto it = all.find(kv.first);
+      if (it == all.end()) {
+        all[kv.first] = kv.second;
+        continue;
+      }
+      // the same sliced tensor from several shards: concatenate the slice lists
+      Entry a = decode_entry(it->second), b = decode_entry(kv.second);
+      if (a.slices_raw.empty() || b.slices_raw.empty() || a.size || b.size || a.dtype != b.dtype || a.shape != b.shape)
+        throw std::runtime_error("tensor in two shards: " + kv.first);
+      a.slices_raw += b.slices_raw;
+      it->second = encode_entry(a);
     }
     if (remove_parts) remove(p.c_str());
   }
@@ -414,11 +541,24 @@ py::dict read_index(const std::string& prefix) {
       d[py::str("")] = py::dict(py::arg("num_shards") = ns);
       continue;
     }
+    if (kv.first[0] == '\x00') continue;   // a slice's data entry (EncodeTensorNameSlice key)
     Entry e = decode_entry(kv.second);
+    py::list slices;
+    if (!e.slices_raw.empty()) {
+      wire::Reader r(e.slices_raw.data(), e.slices_raw.size());
+      int f, wt;
+      while (r.next(f, wt)) {
+        if (f == 7 && wt == wire::LEN) {
+          py::list ext;
+          for (auto& x : decode_slice_proto(r.bytes())) ext.append(py::make_tuple(x.first, x.second));
+          slices.append(ext);
+        } else r.skip(wt);
+      }
+    }
     d[py::str(kv.first)] = py::dict(py::arg("dtype") = e.dtype, py::arg("shape") = e.shape,
                                     py::arg("shard_id") = e.shard_id, py::arg("offset") = e.offset,
                                     py::arg("size") = e.size, py::arg("crc32c") = e.crc,
-                                    py::arg("has_slices") = !e.slices_raw.empty());
+                                    py::arg("has_slices") = !e.slices_raw.empty(), py::arg("slices") = slices);
   }
   return d;
 }
@@ -462,10 +602,15 @@ void init_bundle(py::module& m) {
       .def(py::init<const std::string&, int, int>(), py::arg("prefix"), py::arg("shard_id") = 0,
            py::arg("num_shards") = 1)
       .def("add", &Writer::add)
+      .def("add_slice", &Writer::add_slice)
       .def("finish", &Writer::finish);
   m.def("bundle_merge_shard_indexes", &merge_shard_indexes, py::arg("prefix"), py::arg("num_shards"),
         py::arg("remove_parts") = true);
   m.def("bundle_read_index", &read_index);
+  m.def("bundle_slice_key", [](const std::string& name, Extents ext) { return py::bytes(encode_slice_key(name, ext)); });
+  m.def("bundle_read_slice", [](const std::string& prefix, const std::string& name, Extents ext, bool verify) {
+    return read_tensor(prefix, encode_slice_key(name, ext), verify);
+  }, py::arg("prefix"), py::arg("name"), py::arg("extents"), py::arg("verify") = true);
   m.def("bundle_read_tensor", &read_tensor, py::arg("prefix"), py::arg("name"), py::arg("verify") = true);
   m.def("sstable_read", [](const std::string& path) {
     py::list out;

@@ -15,8 +15,10 @@ the compat layer turns it into a `PartitionedVariable`:
 * `embedding_lookup(_sparse)` on it runs the all-to-all lookup + CSR bag
   kernel; the optimizer applies the IndexedSlices-style gradient at the
   owners (sparse SGD / ScatterSub), with the 1/W sync-average folded in;
-* checkpoints hold TF partitioned names `W/part_k`, one per rank, written
-  in parallel into one multi-shard bundle;
+* checkpoints hold the TF PartitionedVariable layout (full-name entry with
+  TensorSliceProto slices + one EncodeTensorNameSlice entry per contiguous
+  partition; the partitioner's shard count, else one per worker), written in
+  parallel into one multi-shard bundle;
 * dense use (e.g. matmul on the whole table) gathers the full table with a
   warning -- supported for small tables / tests only.
 """

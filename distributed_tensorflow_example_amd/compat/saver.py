@@ -8,6 +8,15 @@ BundleEntryProto) + `prefix.data-00000-of-00001` + the text `checkpoint`
 state file (`model_checkpoint_path: "model.ckpt-N"`).  Variable names are the
 TF names (`weights/Variable_1`, `global_step`, Adam slots `w/Adam`, `w/Adam_1`,
 `beta1_power`...).  Only the chief writes; every rank can restore.
+
+Partitioned variables are laid out as TF's Saver writes a PartitionedVariable
+(SaveSliceInfo + SaveV2 -> BundleWriter::AddSlice): the full name (`W`)
+carries dtype, full shape and a TensorSliceProto per partition, each
+partition's bytes sit under `EncodeTensorNameSlice(W, slice)`, and the
+partitions are contiguous row ranges as tf.fixed_size_partitioner makes them.
+Every rank assembles and writes the partitions it is assigned into its own
+data shard; restore accepts any partition count and any writer world size,
+or a plain full entry (an unpartitioned TF variable).
 """
 from __future__ import annotations
 
@@ -30,21 +39,82 @@ TF_TO_NUMPY = {1: np.float32, 2: np.float64, 3: np.int32, 4: np.uint8, 5: np.int
                10: np.bool_, 19: np.float16}
 
 
-def write_bundle(prefix: str, tensors: Dict[str, torch.Tensor], shard_id: int = 0, num_shards: int = 1):
-    """Write {name: tensor} as a TF V2 bundle (names sorted inside the index)."""
+def _np_bytes(t: torch.Tensor):
+    t = t.detach().cpu().contiguous()
+    dt = TORCH_TO_TF.get(t.dtype)
+    if dt is None:
+        raise TypeError(f"unsupported dtype {t.dtype}")
+    arr = t.view(torch.int16).numpy() if t.dtype == torch.bfloat16 else t.numpy()
+    return dt, np.ascontiguousarray(arr).reshape(-1).view(np.uint8)
+
+
+def write_bundle(prefix: str, tensors: Dict[str, torch.Tensor], shard_id: int = 0, num_shards: int = 1,
+                 slices=None):
+    """Write {name: tensor} as a TF V2 bundle (names sorted inside the index).
+
+    `slices`: [(full_name, full_shape, extents, tensor)] -- partitions of a
+    variable as TF's SaveV2 writes them for SaveSliceInfo specs: the data under
+    the EncodeTensorNameSlice key, the slice recorded in the full-name entry.
+    `extents` = [(start, length)] per dim (length -1 = the whole dim)."""
     C = _native.load()
     d = os.path.dirname(prefix)
     if d:
         os.makedirs(d, exist_ok=True)
     w = C.BundleWriter(prefix, shard_id, num_shards)
     for name in sorted(tensors):
-        t = tensors[name].detach().cpu().contiguous()
-        dt = TORCH_TO_TF.get(t.dtype)
-        if dt is None:
-            raise TypeError(f"unsupported dtype {t.dtype} for {name}")
-        arr = t.view(torch.int16).numpy() if t.dtype == torch.bfloat16 else t.numpy()
-        w.add(name, dt, list(t.shape), np.ascontiguousarray(arr).reshape(-1).view(np.uint8))
+        dt, buf = _np_bytes(tensors[name])
+        w.add(name, dt, list(tensors[name].shape), buf)
+    for full_name, full_shape, ext, t in slices or ():
+        dt, buf = _np_bytes(t)
+        w.add_slice(full_name, dt, [int(x) for x in full_shape], [(int(a), int(b)) for a, b in ext], buf)
     w.finish()
+
+
+def slice_key(name: str, extents) -> bytes:
+    """checkpoint::EncodeTensorNameSlice(name, slice) (OrderedCode bytes)."""
+    return _native.load().bundle_slice_key(name, [(int(a), int(b)) for a, b in extents])
+
+
+def partition_extents(rows: int, num_partitions: int):
+    """Row ranges of tf.fixed_size_partitioner(P) on axis 0: the first
+    rows % P partitions hold one extra row (variable_scope's
+    _get_partitioned_variable slicing)."""
+    P = max(1, min(int(num_partitions), int(rows))) if rows else 1
+    base, extra = divmod(int(rows), P)
+    out, s = [], 0
+    for k in range(P):
+        n = base + (1 if k < extra else 0)
+        out.append((s, n))
+        s += n
+    return out
+
+
+def _to_torch(raw, dt, shape) -> torch.Tensor:
+    if dt == 14:
+        t = torch.from_numpy(np.frombuffer(raw, dtype=np.int16).copy()).view(torch.bfloat16)
+    else:
+        t = torch.from_numpy(np.frombuffer(raw, dtype=TF_TO_NUMPY[dt]).copy())
+    return t.reshape(shape)
+
+
+def _slice_shape(full_shape, ext):
+    return [fs if n < 0 else n for fs, (_, n) in zip(full_shape, ext)]
+
+
+def read_slice(prefix: str, name: str, extents, entry=None) -> torch.Tensor:
+    """One saved slice of a partitioned tensor."""
+    C = _native.load()
+    e = entry or C.bundle_read_index(prefix)[name]
+    raw = C.bundle_read_slice(prefix, name, [(int(a), int(b)) for a, b in extents], True)
+    return _to_torch(raw, e["dtype"], _slice_shape(e["shape"], extents))
+
+
+def iter_slices(prefix: str, name: str, entry=None):
+    """(extents, tensor) for every saved slice of `name` -- one slice resident
+    at a time, so a partitioned 1e9-row table is restored in pieces."""
+    e = entry or read_bundle_index(prefix)[name]
+    for ext in e["slices"]:
+        yield [tuple(x) for x in ext], read_slice(prefix, name, ext, e)
 
 
 def read_bundle_index(prefix: str) -> dict:
@@ -52,18 +122,27 @@ def read_bundle_index(prefix: str) -> dict:
 
 
 def read_tensor(prefix: str, name: str) -> torch.Tensor:
+    """The full tensor `name`; a partitioned (sliced) entry is assembled from
+    its slices, as tf.train.NewCheckpointReader does."""
     C = _native.load()
     idx = C.bundle_read_index(prefix)
     if name not in idx:
         raise KeyError(f"{name} not found in checkpoint {prefix}")
     e = idx[name]
-    raw = C.bundle_read_tensor(prefix, name, True)
-    dt = e["dtype"]
-    if dt == 14:
-        t = torch.from_numpy(np.frombuffer(raw, dtype=np.int16).copy()).view(torch.bfloat16)
-    else:
-        t = torch.from_numpy(np.frombuffer(raw, dtype=TF_TO_NUMPY[dt]).copy())
-    return t.reshape(e["shape"])
+    if not e["has_slices"]:
+        return _to_torch(C.bundle_read_tensor(prefix, name, True), e["dtype"], e["shape"])
+    out = None
+    covered = 0
+    for ext, t in iter_slices(prefix, name, e):
+        if out is None:
+            out = torch.empty(list(e["shape"]), dtype=t.dtype)
+        sl = tuple(slice(None) if n < 0 else slice(a, a + n) for a, n in ext)
+        out[sl] = t
+        covered += t.numel()
+    if out is None or covered != out.numel():
+        raise ValueError(f"slices of {name} in {prefix} do not cover the tensor ({covered} of "
+                         f"{0 if out is None else out.numel()} elements)")
+    return out
 
 
 def list_variables(ckpt: str):
@@ -171,6 +250,14 @@ def _resolve(ckpt: str) -> str:
 
 
 # ----------------------------------------------------------------------- Saver
+def _num_partitions(v) -> int:
+    """Partitions TF would create: the partitioner's shard count, else (PS
+    placement / shard_across_workers) one per worker."""
+    p = getattr(v, "partitioner", None)
+    n = getattr(p, "num_shards", None) if p is not None else None
+    return int(n) if n else v.world.world_size
+
+
 class Saver:
     def __init__(self, var_list=None, max_to_keep: int = 5, keep_checkpoint_every_n_hours: float = 10000.0,
                  sharded: bool = False, name: str = None, restore_sequentially: bool = False,
@@ -192,9 +279,6 @@ class Saver:
             return dict(vl)
         out = {}
         for v in vl:
-            if getattr(v, "is_partitioned", False):
-                out[v.part_name] = v            # TF partitioned naming: W/part_k (this rank's shard)
-                continue
             out[v.name[:-2] if v.name.endswith(":0") else v.name] = v
         return out
 
@@ -216,23 +300,33 @@ class Saver:
         prefix = f"{save_path}-{int(step)}" if step is not None else save_path
         w = get_world()
         vars_ = self._vars()
-        tensors = {k: self._value(v) for k, v in vars_.items()}
-        if w.world_size > 1 and any(getattr(v, "is_partitioned", False) for v in vars_.values()):
-            # every rank writes its own shard of the partitioned tables in parallel
-            local = {k: t for k, t in tensors.items() if getattr(vars_[k], "is_partitioned", False)}
-            repl = {k: t for k, t in tensors.items() if k not in local}
-            write_bundle(prefix, dict(local, **(repl if w.rank == 0 else {})), shard_id=w.rank,
-                         num_shards=w.world_size)
-            w.barrier()
-            if w.rank == 0:
-                _native.load().bundle_merge_shard_indexes(prefix, w.world_size, True)
-            tensors = repl
-            write_meta_graph = write_meta_graph and w.rank == 0
+        parts = {k: v for k, v in vars_.items() if getattr(v, "is_partitioned", False)}
+        tensors = {k: self._value(v) for k, v in vars_.items() if k not in parts}
+        if parts:
+            # TF layout: full-name entry + one slice entry per fixed_size partition;
+            # partition k is assembled (rows gathered from the modulo-sharded
+            # storage) on rank k % W, which writes it into its own data shard
+            from ..ckpt import gather_partitions
+
+            mine = []
+            for name in sorted(parts):
+                v = parts[name]
+                mine += gather_partitions(v.table, name, list(v.shape), _num_partitions(v), w)
+            if w.world_size > 1:
+                write_bundle(prefix, tensors if w.rank == 0 else {}, shard_id=w.rank, num_shards=w.world_size,
+                             slices=mine)
+                w.barrier()
+                if w.rank == 0:
+                    _native.load().bundle_merge_shard_indexes(prefix, w.world_size, True)
+                write_meta_graph = write_meta_graph and w.rank == 0
+            else:
+                write_bundle(prefix, tensors, slices=mine)
         elif w.rank == 0:
             write_bundle(prefix, tensors)
         if w.rank == 0:
             if write_meta_graph:
-                meta = {k: {"shape": list(t.shape), "dtype": str(t.dtype)} for k, t in tensors.items()}
+                meta = {k: {"shape": list(parts[k].shape) if k in parts else list(tensors[k].shape),
+                            "dtype": str(torch.float32 if k in parts else tensors[k].dtype)} for k in vars_}
                 with open(prefix + ".meta.json", "w") as f:
                     json.dump({"variables": meta, "format": "dtf-meta-v1"}, f, indent=1)
             d = os.path.dirname(os.path.abspath(prefix))
@@ -257,13 +351,16 @@ class Saver:
         idx = read_bundle_index(prefix)
         missing = []
         for name, v in self._vars().items():
-            if getattr(v, "is_partitioned", False):
-                base = v.name[:-2] + "/part_"
-                nparts = sum(1 for k in idx if k.startswith(base))
-                if (name not in idx or nparts != v.world.world_size) and self._restore_resharded(prefix, idx, v):
-                    continue
             if name not in idx:
                 missing.append(name)
+                continue
+            if getattr(v, "is_partitioned", False):
+                # sliced (any partition count, any writer world size) or a plain
+                # full entry: each rank keeps the rows it owns
+                from ..ckpt import restore_table
+
+                restore_table(prefix, name, v.table, idx[name])
+                v.initialized = True
                 continue
             t = read_tensor(prefix, name)
             dst = self._value(v)
@@ -275,22 +372,6 @@ class Saver:
                 v.initialized = True
         if missing:
             raise KeyError(f"variables not found in checkpoint {prefix}: {missing}")
-
-    @staticmethod
-    def _restore_resharded(prefix, idx, v) -> bool:
-        """Checkpoint written with K shards, restored on a different world size:
-        row r lived in part_(r % K) at r // K; rebuild and re-slice."""
-        base = v.name[:-2]
-        parts = sorted((int(k.rsplit("_", 1)[1]), k) for k in idx if k.startswith(base + "/part_"))
-        if not parts:
-            return False
-        K = len(parts)
-        full = torch.empty((v.rows, v.dim), dtype=torch.float32)
-        for k, name in parts:
-            full[k::K] = read_tensor(prefix, name).reshape(-1, v.dim)
-        v.table.load_full(full)
-        v.initialized = True
-        return True
 
     def recover_last_checkpoints(self, paths):
         self._kept = [p for p in paths if checkpoint_exists(p)]

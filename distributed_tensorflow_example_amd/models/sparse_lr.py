@@ -88,7 +88,7 @@ class SparseLRTrainer:
 
     # ----------------------------------------------------------------- state
     def checkpoint_tensors(self):
-        local = {self.W.shard_name(): self.W.local}
+        local = {"weights/Variable": self.W}      # saved as a TF partitioned variable
         repl = {"bias/Variable": self.b.detach(), "global_step": torch.tensor(float(self.global_step))}
         return local, repl
 

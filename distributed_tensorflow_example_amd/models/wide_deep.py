@@ -116,7 +116,7 @@ class WideDeep:
         return torch.sigmoid(logit).reshape(-1)
 
     def checkpoint_tensors(self):
-        local = {self.wide.shard_name(): self.wide.local, self.emb.shard_name(): self.emb.local}
+        local = {self.wide.name: self.wide, self.emb.name: self.emb}   # TF partitioned variables
         names = []
         for i in range(len(self.layers) // 2):
             names += [f"deep/dense_{i}/kernel", f"deep/dense_{i}/bias"]

@@ -20,7 +20,8 @@ HBM per GPU holds a 1e9 x 1 fp32 shard 8x over).  Per step:
 Each row has exactly one owner, so there is no replica drift and no
 all-reduce of a dense F x D gradient.  Initial values are a counter-based
 normal of the *global* row id, so a table is bit-identical for any world size.
-Checkpoints use TF's partitioned-variable naming (`name/part_k`).
+Checkpoints store the table as a TF partitioned variable (contiguous
+fixed_size_partitioner slices, see ckpt/__init__.py).
 """
 from __future__ import annotations
 

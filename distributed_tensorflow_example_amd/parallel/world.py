@@ -16,6 +16,7 @@ or explicitly (ClusterSpec path in `compat.train.Server`).
 from __future__ import annotations
 
 import datetime
+import math
 import os
 from dataclasses import dataclass, field
 from typing import Any, Optional
@@ -123,7 +124,7 @@ class World:
             dst[: recv_counts[0]].copy_(src[: send_counts[0]])
             return dst
         if src.is_cuda and self.comm is not None:
-            inner = src[0].numel() if src.dim() > 1 else 1   # counts are in rows; RCCL wants elements
+            inner = math.prod(src.shape[1:])   # counts are in rows; RCCL wants elements
             self.comm.all_to_all(src, [c * inner for c in send_counts], dst, [c * inner for c in recv_counts])
         else:
             dist.all_to_all_single(dst, src, output_split_sizes=recv_counts,

@@ -181,6 +181,110 @@ def test_bundle_roundtrip_and_format(native, tmp_path):
         assert np.array_equal(arr, tens[k.decode()].numpy())
 
 
+# OrderedCode, written from tensorflow/core/lib/strings/ordered_code.cc's
+# definitions (independent of the C++ writer)
+def _oc_num_inc(v):
+    b = v.to_bytes(8, "big").lstrip(b"\x00") if v else b""
+    return bytes([len(b)]) + b
+
+
+def _oc_string(s):
+    esc = {0: b"\x00\xff", 0xFF: b"\xff\x00"}
+    return b"".join(esc.get(c, bytes([c])) for c in s.encode("latin-1")) + b"\x00\x01"
+
+
+def _oc_signed(v):
+    x = ~v if v < 0 else v
+    if x < 64:
+        return bytes([(0x80 ^ v) & 0xFF])
+    n = min(10, x.bit_length() // 7 + 1)
+    body = bytearray((v & ((1 << 80) - 1)).to_bytes(10, "big")[10 - n:])   # sign-extended
+    hdr = [(0, 0), (0x80, 0), (0xc0, 0), (0xe0, 0), (0xf0, 0), (0xf8, 0), (0xfc, 0), (0xfe, 0), (0xff, 0),
+           (0xff, 0x80), (0xff, 0xc0)][n]
+    body[0] ^= hdr[0]
+    body[1] ^= hdr[1]
+    return bytes(body)
+
+
+def _slice_key_py(name, ext):
+    k = _oc_num_inc(0) + _oc_string(name) + _oc_num_inc(len(ext))
+    for a, n in ext:
+        k += _oc_signed(0 if n < 0 else a) + _oc_signed(n)
+    return k
+
+
+def test_tensor_name_slice_key_golden(native):
+    from distributed_tensorflow_example_amd.compat import saver
+
+    # hand-derived bytes: NumIncreasing(0)=00, "W" 00 01, dims=01 02, then
+    # SignedNumIncreasing start/length per dim (one byte 0x80^v for |v| < 64)
+    assert saver.slice_key("W", [(0, 2), (0, 1)]) == b"\x00W\x00\x01\x01\x02\x80\x82\x80\x81"
+    assert saver.slice_key("W", [(0, -1)]) == b"\x00W\x00\x01\x01\x01\x80\x7f"   # full extent
+    assert _oc_signed(100) == b"\xc0\x64" and _oc_signed(10000) == b"\xe0\x27\x10" and _oc_signed(-100) == b"\x3f\x9c"
+    rng = np.random.default_rng(0)
+    vals = [0, 1, 63, 64, -64, -65, 127, 8191, 8192, -8193, 2 ** 31, 10 ** 9, 2 ** 62, 2 ** 63 - 1, -(2 ** 63)]
+    vals += [int(v) for v in rng.integers(-(2 ** 40), 2 ** 40, 50)]
+    for v in vals:
+        assert saver.slice_key("emb/x", [(abs(v) % (2 ** 62), v)]) == _slice_key_py("emb/x", [(abs(v) % (2 ** 62), v)])
+    # order-preserving: the encoding sorts like the integers
+    enc = sorted(vals, key=lambda v: _oc_signed(v))
+    assert enc == sorted(vals)
+    assert saver.slice_key("a\x00b", [(5, 7)]) == b"\x00a\x00\xffb\x00\x01\x01\x01\x85\x87"
+
+
+def test_bundle_partitioned_variable_layout(native, tmp_path):
+    """A 3-way fixed_size partition of a [10, 4] variable: the bytes TF's
+    BundleWriter::AddSlice produces (full entry = dtype, shape, slices; no data)."""
+    import torch
+
+    from distributed_tensorflow_example_amd.compat import saver
+
+    full = torch.arange(40, dtype=torch.float32).reshape(10, 4)
+    ext = saver.partition_extents(10, 3)
+    assert ext == [(0, 4), (4, 3), (7, 3)]                       # first 10 % 3 partitions get +1
+    prefix = str(tmp_path / "p.ckpt")
+    slices = [("emb/W", [10, 4], [(a, n), (0, 4)], full[a:a + n]) for a, n in ext]
+    saver.write_bundle(prefix, {"b": torch.ones(2)}, slices=slices)
+    tab = sstable_py(prefix + ".index")
+    # full entry: dtype=1, shape [10, 4], three TensorSliceProtos
+    shape = b"\x12\x02\x08\x0a\x12\x02\x08\x04"
+    sl = [b"\x0a\x02\x10\x04\x0a\x02\x10\x04",                          # {length:4} {length:4}
+          b"\x0a\x04\x08\x04\x10\x03\x0a\x02\x10\x04",                  # {start:4 length:3} {length:4}
+          b"\x0a\x04\x08\x07\x10\x03\x0a\x02\x10\x04"]
+    want = b"\x08\x01\x12" + bytes([len(shape)]) + shape + b"".join(b"\x3a" + bytes([len(x)]) + x for x in sl)
+    assert tab[b"emb/W"] == want
+    data = open(prefix + ".data-00000-of-00001", "rb").read()
+    for (a, n) in ext:
+        k = _slice_key_py("emb/W", [(a, n), (0, 4)])
+        e = _proto_fields(tab[k])
+        off, size = e.get(4, [0])[0], e[5][0]
+        assert np.array_equal(np.frombuffer(data[off:off + size], np.float32).reshape(n, 4), full[a:a + n].numpy())
+        assert e[6][0] == _mask(_crc32c_py(data[off:off + size]))
+    idx = saver.read_bundle_index(prefix)
+    assert set(idx) - {""} == {"emb/W", "b"}                     # slice keys hidden from the name map
+    assert idx["emb/W"]["slices"] == [[(0, 4), (0, 4)], [(4, 3), (0, 4)], [(7, 3), (0, 4)]]
+    assert torch.equal(saver.read_tensor(prefix, "emb/W"), full)
+    assert dict(saver.list_variables(prefix))["emb/W"] == [10, 4]
+
+
+def test_bundle_sliced_shards_merge(native, tmp_path):
+    """Slices of one variable written by two shards merge into one full entry."""
+    import torch
+
+    from distributed_tensorflow_example_amd.compat import saver
+
+    full = torch.randn(7, 3)
+    prefix = str(tmp_path / "m.ckpt")
+    for r, (a, n) in enumerate(saver.partition_extents(7, 2)):
+        saver.write_bundle(prefix, {"g": torch.tensor(3)} if r == 0 else {}, shard_id=r, num_shards=2,
+                           slices=[("W", [7, 3], [(a, n), (0, 3)], full[a:a + n])])
+    native.bundle_merge_shard_indexes(prefix, 2, True)
+    idx = saver.read_bundle_index(prefix)
+    assert idx["W"]["slices"] == [[(0, 4), (0, 3)], [(4, 3), (0, 3)]]
+    assert torch.equal(saver.read_tensor(prefix, "W"), full)
+    assert int(saver.read_tensor(prefix, "g")) == 3
+
+
 def test_saver_checkpoint_state_and_max_to_keep(tmp_path):
     import distributed_tensorflow_example_amd.compat as tf
 

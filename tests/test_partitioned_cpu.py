@@ -1,6 +1,7 @@
 """replica_device_setter path for big tables: a ps-placed tf.Variable becomes
 a row-sharded PartitionedVariable; lr2.py's graph trains identically on 1
-and 2 gloo workers; checkpoints carry W/part_k and re-shard on restore."""
+and 2 gloo workers; checkpoints hold TF's PartitionedVariable layout
+(full-name entry + contiguous slices) and re-shard on restore."""
 import os
 import socket
 import sys
@@ -107,7 +108,12 @@ def test_partitioned_variable_sync_workers(tmp_path):
     Wm.reset()
     idx = tf.train.list_variables(os.path.dirname(two[0][3]))
     names = dict(idx)
-    assert names["weights/Variable/part_0"] == [F // 2, 1] and names["weights/Variable/part_1"] == [F // 2, 1]
+    assert names["weights/Variable"] == [F, 1] and not any("part_" in k for k in names)
+    from distributed_tensorflow_example_amd.compat import saver as S
+
+    e = S.read_bundle_index(two[0][3])["weights/Variable"]
+    assert e["slices"] == [[(0, F // 2), (0, 1)], [(F // 2, F // 2), (0, 1)]]   # one partition per worker
+    assert np.array_equal(S.read_tensor(two[0][3], "weights/Variable").numpy(), two[0][1])
     tf.reset_default_graph()
     g = _graph(tf)
     with tf.Session() as sess:

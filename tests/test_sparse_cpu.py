@@ -161,12 +161,9 @@ def test_sharded_table_two_ranks_equal_one(svm_dir):
     assert abs(one[0][3] - two[0][3]) < 1e-6
     prefix = two[0][4]
     idx = saver.read_bundle_index(prefix)
-    assert {"weights/Variable/part_0", "weights/Variable/part_1", "bias/Variable", "global_step"} <= set(idx)
-    p0 = saver.read_tensor(prefix, "weights/Variable/part_0").numpy()
-    p1 = saver.read_tensor(prefix, "weights/Variable/part_1").numpy()
-    full = np.empty((3000, 1), np.float32)
-    full[0::2], full[1::2] = p0, p1
-    assert np.array_equal(full, two[0][2])
+    assert {"weights/Variable", "bias/Variable", "global_step"} <= set(idx)
+    assert idx["weights/Variable"]["slices"] == [[(0, 1500), (0, 1)], [(1500, 1500), (0, 1)]]
+    assert np.array_equal(saver.read_tensor(prefix, "weights/Variable").numpy(), two[0][2])
 
 
 def test_lr2_example_ps_two_workers(svm_dir, tmp_path):

@@ -64,6 +64,16 @@ class Graph:
         self._op_seed = 0
         self.device = default_device()
         self.finalized = False
+        self._nodes: List["Tensor"] = []          # creation order (GraphDef node order)
+
+    @contextlib.contextmanager
+    def as_default(self):
+        prev = getattr(_local, "graph", None)
+        _local.graph = self
+        try:
+            yield self
+        finally:
+            _local.graph = prev
 
     def unique_name(self, name: str) -> str:
         full = "/".join(self._scope + [name]) if self._scope else name
@@ -87,9 +97,27 @@ class Graph:
         self.finalized = True
 
     def as_graph_def(self) -> bytes:
-        """Opaque stand-in for GraphDef (used by summary writers / exporters)."""
-        names = [v.name for v in self._collections.get(GLOBAL_VARIABLES, [])]
-        return ("\n".join(names)).encode()
+        """Serialized tensorflow.GraphDef of the nodes built so far
+        (compat/meta_graph.py)."""
+        from .meta_graph import graph_def_bytes
+
+        return graph_def_bytes(self)
+
+    def get_operations(self):
+        return list(self._nodes)
+
+    def get_tensor_by_name(self, name: str):
+        idx = self.__dict__.get("_name_index")
+        if idx is None or idx[0] != len(self._nodes):
+            m = {}
+            for t in self._nodes:
+                m[t.name] = t
+                m.setdefault(t.name[:-2], t)
+            idx = self._name_index = (len(self._nodes), m)
+        t = idx[1].get(name)
+        if t is None:
+            raise KeyError(f"The name '{name}' refers to a Tensor which does not exist")
+        return t
 
     def next_seed(self):
         self._op_seed += 1
@@ -175,6 +203,21 @@ class _PlacementQuery:
 
 
 # ----------------------------------------------------------------------- tensors
+_LOWER_OPS = {"add": "Add", "sub": "Sub", "mul": "Mul", "truediv": "RealDiv", "pow": "Pow", "neg": "Neg",
+              "strided_slice": "StridedSlice", "transpose": "Transpose", "concat": "ConcatV2", "stack": "Pack",
+              "zeros_like": "ZerosLike", "ones_like": "OnesLike", "clip_by_value": "ClipByValue",
+              "gradients": "Gradients", "init": "NoOp", "init_local": "NoOp", "group_deps": "NoOp"}
+
+
+def _op_type_from_name(name: str) -> str:
+    """TF op type for a node built without an explicit one: the
+    constructor's default name ("MatMul", "Sigmoid", ...) is the type."""
+    base = name.rsplit("/", 1)[-1]
+    if base in _LOWER_OPS:
+        return _LOWER_OPS[base]
+    return base[:1].upper() + base[1:] if base else "Identity"
+
+
 class RunContext:
     def __init__(self, feeds: Dict[Any, Any], device: torch.device):
         self.feeds = feeds
@@ -220,31 +263,36 @@ class Tensor:
     _is_op = False
 
     def __init__(self, fn: Callable, inputs: Sequence[Any] = (), name: str = "Tensor", dtype=None,
-                 shape=None):
+                 shape=None, op_type: Optional[str] = None, attrs: Optional[Dict[str, Any]] = None):
+        g = get_default_graph()
         self.fn = fn
         self.inputs = list(inputs)
-        self.name = get_default_graph().unique_name(name) + ":0"
+        self.name = g.unique_name(name) + ":0"
         self.dtype = dtype
         self.shape = shape
         self.op = self
+        self.op_type = op_type or _op_type_from_name(name)   # TF op type for GraphDef / graph rewrites
+        self.attrs = attrs or {}
+        g._nodes.append(self)
 
     def _eval(self, ctx: RunContext):
         vals = [ctx.eval(i) for i in self.inputs]
         return self.fn(*vals)
 
     # arithmetic ----------------------------------------------------------
-    def __add__(self, o): return Tensor(lambda a, b: a + b, [self, o], "add")
-    def __radd__(self, o): return Tensor(lambda a, b: b + a, [self, o], "add")
-    def __sub__(self, o): return Tensor(lambda a, b: a - b, [self, o], "sub")
-    def __rsub__(self, o): return Tensor(lambda a, b: b - a, [self, o], "sub")
-    def __mul__(self, o): return Tensor(lambda a, b: a * b, [self, o], "mul")
-    def __rmul__(self, o): return Tensor(lambda a, b: b * a, [self, o], "mul")
-    def __truediv__(self, o): return Tensor(lambda a, b: a / b, [self, o], "truediv")
-    def __rtruediv__(self, o): return Tensor(lambda a, b: b / a, [self, o], "truediv")
-    def __pow__(self, o): return Tensor(lambda a, b: a ** b, [self, o], "pow")
-    def __neg__(self): return Tensor(lambda a: -a, [self], "neg")
+    # reflected forms keep TF's operand order (x - y with x a constant)
+    def __add__(self, o): return Tensor(lambda a, b: a + b, [self, o], "add", op_type="Add")
+    def __radd__(self, o): return Tensor(lambda a, b: a + b, [o, self], "add", op_type="Add")
+    def __sub__(self, o): return Tensor(lambda a, b: a - b, [self, o], "sub", op_type="Sub")
+    def __rsub__(self, o): return Tensor(lambda a, b: a - b, [o, self], "sub", op_type="Sub")
+    def __mul__(self, o): return Tensor(lambda a, b: a * b, [self, o], "mul", op_type="Mul")
+    def __rmul__(self, o): return Tensor(lambda a, b: a * b, [o, self], "mul", op_type="Mul")
+    def __truediv__(self, o): return Tensor(lambda a, b: a / b, [self, o], "truediv", op_type="RealDiv")
+    def __rtruediv__(self, o): return Tensor(lambda a, b: a / b, [o, self], "truediv", op_type="RealDiv")
+    def __pow__(self, o): return Tensor(lambda a, b: a ** b, [self, o], "pow", op_type="Pow")
+    def __neg__(self): return Tensor(lambda a: -a, [self], "Neg", op_type="Neg")
     def __matmul__(self, o): return matmul(self, o)
-    def __getitem__(self, idx): return Tensor(lambda a: a[idx], [self], "strided_slice")
+    def __getitem__(self, idx): return Tensor(lambda a: a[idx], [self], "strided_slice", op_type="StridedSlice")
 
     def eval(self, session=None, feed_dict=None):
         from .session import get_default_session
@@ -277,8 +325,8 @@ class Operation(Tensor):
 
     _is_op = True
 
-    def __init__(self, fn: Callable, inputs: Sequence[Any] = (), name: str = "Op"):
-        super().__init__(fn, inputs, name)
+    def __init__(self, fn: Callable, inputs: Sequence[Any] = (), name: str = "Op", op_type: Optional[str] = None):
+        super().__init__(fn, inputs, name, op_type=op_type or ("NoOp" if not inputs else None))
 
     def run(self, session=None, feed_dict=None):
         from .session import get_default_session
@@ -290,23 +338,23 @@ def group(*ops, name="group_deps") -> Operation:
     flat = []
     for o in ops:
         flat.extend(o if isinstance(o, (list, tuple)) else [o])
-    return Operation(lambda *a: None, flat, name)
+    return Operation(lambda *a: None, flat, name, op_type="NoOp")
 
 
 def no_op(name="NoOp") -> Operation:
-    return Operation(lambda: None, [], name)
+    return Operation(lambda: None, [], name, op_type="NoOp")
 
 
 def constant(value, dtype=None, shape=None, name="Const") -> Tensor:
     def f():
         t = _to_tensor(value, get_default_graph().device, dtype)
         return t.reshape(shape) if shape is not None and isinstance(t, torch.Tensor) else t
-    return Tensor(f, [], name, dtype=dtype, shape=shape)
+    return Tensor(f, [], name, dtype=dtype, shape=shape, op_type="Const", attrs={"value": value})
 
 
 class Placeholder(Tensor):
     def __init__(self, dtype=float32, shape=None, name="Placeholder"):
-        super().__init__(None, [], name, dtype=dtype, shape=shape)
+        super().__init__(None, [], name, dtype=dtype, shape=shape, op_type="Placeholder")
 
     def _eval(self, ctx: RunContext):
         for key in (self, self.name, self.name[:-2]):
@@ -338,6 +386,8 @@ class Variable(Tensor):
         self.inputs = []
         self.name = base + ":0"
         self.op = self
+        self.op_type, self.attrs = "VariableV2", {}
+        g._nodes.append(self)
         self.trainable = trainable
         init = self._materialize_initial()
         if dtype is not None:
@@ -348,7 +398,8 @@ class Variable(Tensor):
         self.placement = cached[0] if cached else _current_placement("VariableV2", base, init.numel())
         self.value = torch.nn.Parameter(init.to(g.device).clone(), requires_grad=trainable and init.is_floating_point())
         self.initialized = False
-        self.initializer = Operation(lambda: self._initialize(), [], base + "/Assign")
+        self.initializer = Operation(lambda: self._initialize(), [], base + "/Assign", op_type="Assign")
+        self.initializer.name = base + "/Assign:0"          # absolute, like the variable's own name
         cols = collections or ([GLOBAL_VARIABLES] + ([TRAINABLE_VARIABLES] if trainable else []))
         for c in cols:
             g.add_to_collection(c, self)
@@ -398,18 +449,18 @@ class Variable(Tensor):
         return self.name[:-2]
 
     def assign(self, value) -> Operation:
-        def f(v):
+        def f(_ref, v):
             with torch.no_grad():
                 self.value.data.copy_(torch.as_tensor(v).to(self.value.device, self.value.dtype))
             return self.value
-        return Operation(f, [value], self.op_name + "/Assign")
+        return Operation(f, [self, value], self.op_name + "/Assign", op_type="Assign")
 
     def assign_add(self, delta) -> Operation:
-        def f(d):
+        def f(_ref, d):
             with torch.no_grad():
                 self.value.data.add_(torch.as_tensor(d).to(self.value.device, self.value.dtype))
             return self.value
-        return Operation(f, [delta], self.op_name + "/AssignAdd")
+        return Operation(f, [self, delta], self.op_name + "/AssignAdd", op_type="AssignAdd")
 
     def load(self, value, session=None):
         with torch.no_grad():
@@ -585,7 +636,7 @@ def report_uninitialized_variables(var_list=None):
 # ----------------------------------------------------------------------- math ops
 def _binary(fn, name):
     def op(a, b, name=None):
-        return Tensor(fn, [a, b], name or op_name)
+        return Tensor(fn, [a, b], name or op_name, op_type=op_name)
     op_name = name
     return op
 
@@ -612,12 +663,13 @@ def matmul(a, b, transpose_a=False, transpose_b=False, name="MatMul") -> Tensor:
 
             return linear_act(x, y, None, "none")
         return x @ y
-    return Tensor(f, [a, b], name)
+    return Tensor(f, [a, b], name, op_type="MatMul",
+                  attrs={"transpose_a": bool(transpose_a), "transpose_b": bool(transpose_b)})
 
 
 def _unary(fn, name):
     def op(x, name=None):
-        return Tensor(fn, [x], name or op_name)
+        return Tensor(fn, [x], name or op_name, op_type=op_name)
     op_name = name
     return op
 
@@ -646,44 +698,48 @@ def _axes(reduction_indices, axis):
 def reduce_mean(x, axis=None, keep_dims=False, reduction_indices=None, name="Mean", keepdims=None):
     kd = keep_dims if keepdims is None else keepdims
     ax = _axes(reduction_indices, axis)
-    return Tensor(lambda t: t.float().mean() if ax is None else t.float().mean(dim=ax, keepdim=kd), [x], name)
+    return Tensor(lambda t: t.float().mean() if ax is None else t.float().mean(dim=ax, keepdim=kd), [x], name,
+                  op_type="Mean", attrs={"axis": ax, "keep_dims": bool(kd)})
 
 
 def reduce_sum(x, axis=None, keep_dims=False, reduction_indices=None, name="Sum", keepdims=None):
     kd = keep_dims if keepdims is None else keepdims
     ax = _axes(reduction_indices, axis)
-    return Tensor(lambda t: t.sum() if ax is None else t.sum(dim=ax, keepdim=kd), [x], name)
+    return Tensor(lambda t: t.sum() if ax is None else t.sum(dim=ax, keepdim=kd), [x], name,
+                  op_type="Sum", attrs={"axis": ax, "keep_dims": bool(kd)})
 
 
 def reduce_max(x, axis=None, keep_dims=False, reduction_indices=None, name="Max"):
     ax = _axes(reduction_indices, axis)
-    return Tensor(lambda t: t.max() if ax is None else t.amax(dim=ax, keepdim=keep_dims), [x], name)
+    return Tensor(lambda t: t.max() if ax is None else t.amax(dim=ax, keepdim=keep_dims), [x], name,
+                  op_type="Max", attrs={"axis": ax, "keep_dims": bool(keep_dims)})
 
 
 def argmax(x, axis=None, dimension=None, name="ArgMax"):
     ax = axis if axis is not None else (dimension if dimension is not None else 0)
-    return Tensor(lambda t: t.argmax(dim=ax), [x], name)
+    return Tensor(lambda t: t.argmax(dim=ax), [x], name, op_type="ArgMax", attrs={"axis": ax})
 
 
 def argmin(x, axis=None, dimension=None, name="ArgMin"):
     ax = axis if axis is not None else (dimension if dimension is not None else 0)
-    return Tensor(lambda t: t.argmin(dim=ax), [x], name)
+    return Tensor(lambda t: t.argmin(dim=ax), [x], name, op_type="ArgMin", attrs={"axis": ax})
 
 
 def equal(a, b, name="Equal"):
-    return Tensor(lambda x, y: x == y, [a, b], name)
+    return Tensor(lambda x, y: x == y, [a, b], name, op_type="Equal")
 
 
 def cast(x, dtype, name="Cast"):
-    return Tensor(lambda t: t.to(dtype), [x], name, dtype=dtype)
+    return Tensor(lambda t: t.to(dtype), [x], name, dtype=dtype, op_type="Cast", attrs={"DstT": dtype})
 
 
 def reshape(x, shape, name="Reshape"):
-    return Tensor(lambda t: t.reshape(tuple(shape)), [x], name)
+    return Tensor(lambda t: t.reshape(tuple(shape)), [x], name, op_type="Reshape", attrs={"shape": list(shape)})
 
 
 def transpose(x, perm=None, name="transpose"):
-    return Tensor(lambda t: t.permute(*perm) if perm is not None else t.t(), [x], name)
+    return Tensor(lambda t: t.permute(*perm) if perm is not None else t.t(), [x], name, op_type="Transpose",
+                  attrs={"perm": None if perm is None else list(perm)})
 
 
 def concat(values, axis, name="concat"):

@@ -8,15 +8,15 @@ from .graph import Tensor
 
 
 def sigmoid(x, name="Sigmoid"):
-    return Tensor(torch.sigmoid, [x], name)
+    return Tensor(torch.sigmoid, [x], name, op_type="Sigmoid")
 
 
 def relu(x, name="Relu"):
-    return Tensor(torch.relu, [x], name)
+    return Tensor(torch.relu, [x], name, op_type="Relu")
 
 
 def tanh(x, name="Tanh"):
-    return Tensor(torch.tanh, [x], name)
+    return Tensor(torch.tanh, [x], name, op_type="Tanh")
 
 
 def gelu(x, name="Gelu"):
@@ -24,15 +24,15 @@ def gelu(x, name="Gelu"):
 
 
 def softmax(logits, dim=-1, name="Softmax"):
-    return Tensor(lambda t: torch.softmax(t, dim), [logits], name)
+    return Tensor(lambda t: torch.softmax(t, dim), [logits], name, op_type="Softmax", attrs={"dim": dim})
 
 
 def log_softmax(logits, dim=-1, name="LogSoftmax"):
-    return Tensor(lambda t: torch.log_softmax(t, dim), [logits], name)
+    return Tensor(lambda t: torch.log_softmax(t, dim), [logits], name, op_type="LogSoftmax", attrs={"dim": dim})
 
 
 def bias_add(value, bias, name="BiasAdd"):
-    return Tensor(lambda v, b: v + b, [value, bias], name)
+    return Tensor(lambda v, b: v + b, [value, bias], name, op_type="BiasAdd")
 
 
 def xw_plus_b(x, w, b, name="xw_plus_b"):

@@ -80,6 +80,8 @@ class PartitionedVariable(Variable):
         self.inputs = []
         self.name = full_name + ":0"
         self.op = self
+        self.op_type, self.attrs = "VariableV2", {}
+        g._nodes.append(self)
         self.trainable = trainable
         self.dtype = torch.float32
         self.shape = tuple(int(s) for s in shape)
@@ -99,7 +101,8 @@ class PartitionedVariable(Variable):
         self.initialized = False
         from .graph import Operation
 
-        self.initializer = Operation(lambda: self._initialize(), [], full_name + "/Assign")
+        self.initializer = Operation(lambda: self._initialize(), [], full_name + "/Assign", op_type="Assign")
+        self.initializer.name = full_name + "/Assign:0"
         cols = collections or ([GLOBAL_VARIABLES] + ([TRAINABLE_VARIABLES] if trainable else []))
         for c in cols:
             g.add_to_collection(c, self)

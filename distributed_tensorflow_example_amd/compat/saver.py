@@ -21,7 +21,6 @@ or a plain full entry (an unpartitioned TF variable).
 from __future__ import annotations
 
 import glob
-import json
 import os
 import re
 import time
@@ -249,6 +248,26 @@ def _resolve(ckpt: str) -> str:
     return ckpt
 
 
+# ----------------------------------------------------------------------- meta graphs
+def export_meta_graph(filename: Optional[str] = None, **kw) -> bytes:
+    """tf.train.export_meta_graph: MetaGraphDef bytes of the default graph."""
+    from .meta_graph import export_meta_graph_bytes
+
+    b = export_meta_graph_bytes()
+    if filename:
+        with open(filename, "wb") as f:
+            f.write(b)
+    return b
+
+
+def read_meta_graph(filename: str) -> dict:
+    """Decoded MetaGraphDef (plain dicts; compat/meta_graph.parse_meta_graph)."""
+    from .meta_graph import parse_meta_graph
+
+    with open(filename, "rb") as f:
+        return parse_meta_graph(f.read())
+
+
 # ----------------------------------------------------------------------- Saver
 def _num_partitions(v) -> int:
     """Partitions TF would create: the partitioner's shard count, else (PS
@@ -325,10 +344,7 @@ class Saver:
             write_bundle(prefix, tensors)
         if w.rank == 0:
             if write_meta_graph:
-                meta = {k: {"shape": list(parts[k].shape) if k in parts else list(tensors[k].shape),
-                            "dtype": str(torch.float32 if k in parts else tensors[k].dtype)} for k in vars_}
-                with open(prefix + ".meta.json", "w") as f:
-                    json.dump({"variables": meta, "format": "dtf-meta-v1"}, f, indent=1)
+                self.export_meta_graph(f"{prefix}.{meta_graph_suffix}")
             d = os.path.dirname(os.path.abspath(prefix))
             self._kept.append(prefix)
             while self.max_to_keep and len(self._kept) > self.max_to_keep:
@@ -372,6 +388,20 @@ class Saver:
                 v.initialized = True
         if missing:
             raise KeyError(f"variables not found in checkpoint {prefix}: {missing}")
+
+    def export_meta_graph(self, filename: Optional[str] = None, collection_list=None, as_text=False, **kw) -> bytes:
+        """Serialized MetaGraphDef of the default graph (graph_def, this
+        saver's SaverDef, the collections) -- what Saver.save writes to
+        `prefix.meta`."""
+        from .meta_graph import export_meta_graph_bytes
+
+        b = export_meta_graph_bytes(saver=self)
+        if filename:
+            tmp = filename + ".tmp"
+            with open(tmp, "wb") as f:
+                f.write(b)
+            os.replace(tmp, filename)
+        return b
 
     def recover_last_checkpoints(self, paths):
         self._kept = [p for p in paths if checkpoint_exists(p)]

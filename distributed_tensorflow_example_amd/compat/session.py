@@ -93,6 +93,8 @@ class Session:
             return vals if isinstance(f, list) else tuple(vals)
         if isinstance(f, dict):
             return {k: self._run(v, ctx) for k, v in f.items()}
+        if isinstance(f, str):                 # "y:0" / "train_op" fetch by name
+            f = self.graph.get_tensor_by_name(f)
         if isinstance(f, Tensor):
             v = ctx.eval(f)
             return None if f._is_op else _to_numpy(v)

@@ -35,8 +35,9 @@ from .graph import (GLOBAL_STEP, GLOBAL_VARIABLES, LOCAL_VARIABLES, TRAINABLE_VA
                     global_variables, local_variables, trainable_variables)
 from .queues import (Coordinator, QueueRunner, add_queue_runner, batch, shuffle_batch, slice_input_producer,
                      start_queue_runners, string_input_producer)
-from .saver import (CheckpointReader, NewCheckpointReader, Saver, checkpoint_exists, get_checkpoint_state,
-                    latest_checkpoint, list_variables, load_variable, update_checkpoint_state)
+from .saver import (CheckpointReader, NewCheckpointReader, Saver, checkpoint_exists, export_meta_graph,
+                    get_checkpoint_state, latest_checkpoint, list_variables, load_variable, read_meta_graph,
+                    update_checkpoint_state)
 from .session import ConfigProto, Session
 from .summary import FileWriter, SummaryWriter
 
@@ -44,6 +45,7 @@ __all__ = [
     "ClusterSpec", "Server", "replica_device_setter", "GradientDescentOptimizer", "MomentumOptimizer",
     "AdamOptimizer", "AdagradOptimizer", "RMSPropOptimizer", "SyncReplicasOptimizer", "Supervisor",
     "MonitoredTrainingSession", "MonitoredSession", "SingularMonitoredSession", "Scaffold", "Saver",
+    "export_meta_graph", "read_meta_graph",
     "Coordinator", "QueueRunner", "start_queue_runners", "add_queue_runner", "batch", "shuffle_batch",
     "slice_input_producer", "string_input_producer", "latest_checkpoint", "get_checkpoint_state",
     "get_global_step", "get_or_create_global_step", "create_global_step", "global_step", "SummaryWriter",
@@ -411,6 +413,8 @@ class Optimizer:
 
 
 class _SlotVariable:
+    op_type, attrs = "VariableV2", {}       # a VariableV2 node in the exported GraphDef
+
     def __init__(self, name, tensor):
         self.name = name + ":0"
         self.value = tensor
@@ -463,6 +467,8 @@ class AdamOptimizer(Optimizer):
 
 class _PowerVariable:
     """beta^t as a saveable variable, tied to the fused optimizer's step."""
+
+    op_type, attrs, shape, dtype = "VariableV2", {}, (), torch.float32
 
     def __init__(self, name, beta, fused):
         self.name = name + ":0"

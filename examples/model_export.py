@@ -4,8 +4,10 @@ Data x = 0, 0.1, ..., 99.9 and y = x + 20 sin(x / 10) (model_export.py:18-24);
 `test/weights` [1,1] ~ N(0,1), `test/bias` [1] = 0; loss = sum((y - xw - b)^2 /
 1000) over random batches of 100 drawn with replacement; Adam(0.01) for 500
 steps (TF Adam semantics, fused optimizer kernel on GPU); then a Saver-backed
-Exporter writes `<work_dir>/<%08d version>/` (session-bundle layout with a
-TF V2 bundle) and the export is reloaded and served as a check.
+Exporter writes `<work_dir>/<%08d version>/` (session-bundle layout: the
+`export.meta` MetaGraphDef carrying the serving signatures + a TF V2 bundle),
+and the export is reloaded -- graph rebuilt from the GraphDef, variables
+restored -- and served through its signatures as a check.
 """
 from __future__ import annotations
 
@@ -53,8 +55,7 @@ def main(_argv):
             model_exporter = exporter.Exporter(tf.train.Saver())
             model_exporter.init(sess.graph.as_graph_def(),
                                 named_graph_signatures={"inputs": exporter.generic_signature({"x": x}),
-                                                        "outputs": exporter.generic_signature({"y": y_pred})},
-                                serving_recipe={"type": "linear", "w": "test/weights", "b": "test/bias"})
+                                                        "outputs": exporter.generic_signature({"y": y_pred})})
             path = model_exporter.export(FLAGS.work_dir, tf.constant(FLAGS.export_version), sess)
             wv, bv = sess.run(w), sess.run(b)
     bundle = exporter.load_session_bundle(path)

@@ -21,14 +21,19 @@ def test_model_export(tmp_path):
     assert rc == 0, out
     d = tmp_path / "model" / "00000003"
     assert (d / "export.index").exists() and (d / "export.data-00000-of-00001").exists()
-    meta = json.load(open(d / "export.meta.json"))
-    assert set(meta["signatures"]) == {"inputs", "outputs"}
-    assert meta["signatures"]["inputs"]["map"]["x"]["name"] == "x:0"
-    assert {"test/weights", "test/bias", "test/weights/Adam", "beta1_power"} <= set(meta["variables"])
-    # y = x + 20 sin(x/10) on [0, 100): least squares slope ~ 0.97 -- 500 Adam steps get close
+    assert (d / "export.meta").exists() and (d / "checkpoint").exists()
     sys.path.insert(0, REPO)
     from distributed_tensorflow_example_amd.compat import export
+    from distributed_tensorflow_example_amd.compat import meta_graph as M
 
+    meta = M.parse_meta_graph((d / "export.meta").read_bytes())
+    sigs = M.parse_signatures(meta["collection_def"]["serving_signatures"]["value"][0]["value"])["named_signatures"]
+    assert set(sigs) == {"inputs", "outputs"}
+    assert sigs["inputs"] == {"kind": "generic", "map": {"x": "x:0"}}
+    assert sigs["outputs"]["map"]["y"] == "test/add:0"
+    names = [M.parse_variable_def(v)["variable_name"] for v in meta["collection_def"]["variables"]["value"]]
+    assert {"test/weights:0", "test/bias:0", "test/weights/Adam:0", "beta1_power:0"} <= set(names)
+    # y = x + 20 sin(x/10) on [0, 100): least squares slope ~ 0.97 -- 500 Adam steps get close
     b = export.load_session_bundle(str(d))
     w = float(b.tensors["test/weights"].reshape(-1)[0])
     assert 0.5 < w < 1.5

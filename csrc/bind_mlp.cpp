@@ -49,6 +49,11 @@ hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int n
                                 void* xbuf, int* err, long long timeout, long long* step_ts, int ts_ring,
                                 const void* host_next, int next_steps, void* stage_next, void* const* peer_base, int W,
                                 int rank, int gbf16, long long* phase_ts, int spread, hipStream_t stream);
+long long dtfk_graph_mlp_lds(int B, int HP);
+hipError_t dtfk_graph_mlp_step(const float* x, const float* ylab, float* W1, float* b1, float* W2, float* b2,
+                               float* a2buf, float* dz2buf, float* gW1, float* gb1, float* gW2, float* gb2,
+                               float* metrics, void* gstep, int gstep_kind, float lr, int B, int K, int H, int C,
+                               int act, int naive, int sgd, hipStream_t stream);
 long long dtfk_mlpx_stage_rec();
 long long dtfk_mlpx_xbuf_bytes();
 long long dtfk_mlpx_ipc_bytes();
@@ -409,7 +414,61 @@ void mlp_persist_f32(at::Tensor stage, int64_t rec_h, int B, int nsteps, at::Ten
             "mlp_persist_f32");
 }
 
+// The compat graph's matched MLP training step (csrc/kernels/graph_mlp.hip).
+// sgd: W/b updated in place with lr; else gradients into g* (same shapes).
+void graph_mlp_step(at::Tensor x, at::Tensor ylab, at::Tensor W1, at::Tensor b1, at::Tensor W2, at::Tensor b2,
+                    at::Tensor a2buf, at::Tensor dz2buf, c10::optional<std::vector<at::Tensor>> grads,
+                    at::Tensor metrics,
+                    c10::optional<at::Tensor> gstep, double lr, int act, bool naive, bool sgd) {
+  for (const at::Tensor* t : {&x, &ylab, &W1, &b1, &W2, &b2, &a2buf, &dz2buf, &metrics}) {
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous(),
+                "graph_mlp_step: fp32 contiguous device tensors expected");
+  }
+  TORCH_CHECK(x.dim() == 2 && W1.dim() == 2 && W2.dim() == 2, "graph_mlp_step: 2-D x, W1, W2");
+  const int B = (int)x.size(0), K = (int)x.size(1), H = (int)W1.size(1), C = (int)W2.size(1);
+  TORCH_CHECK(W1.size(0) == K && W2.size(0) == H && b1.numel() == H && b2.numel() == C &&
+                  ylab.numel() == (int64_t)B * C,
+              "graph_mlp_step: shape mismatch");
+  const int HP = (H + 15) & ~15, BP = (B + 15) & ~15;
+  TORCH_CHECK(a2buf.numel() >= (int64_t)BP * HP && dz2buf.numel() >= (int64_t)BP * HP && metrics.numel() >= 2,
+              "graph_mlp_step: scratch too small");
+  float *gW1 = nullptr, *gb1 = nullptr, *gW2 = nullptr, *gb2 = nullptr;
+  if (!sgd) {
+    TORCH_CHECK(grads.has_value() && grads->size() == 4, "graph_mlp_step: gradients [dW1, db1, dW2, db2] expected");
+    const int64_t n[4] = {(int64_t)K * H, H, (int64_t)H * C, C};
+    float** dst[4] = {&gW1, &gb1, &gW2, &gb2};
+    for (int i = 0; i < 4; ++i) {
+      const at::Tensor& g = (*grads)[i];
+      TORCH_CHECK(g.is_cuda() && g.scalar_type() == at::kFloat && g.is_contiguous() && g.numel() == n[i],
+                  "graph_mlp_step: bad gradient tensor ", i);
+      *dst[i] = g.data_ptr<float>();
+    }
+  }
+  void* gp = nullptr;
+  int kind = 0;
+  if (gstep.has_value()) {
+    TORCH_CHECK(gstep->is_cuda() && gstep->numel() == 1, "graph_mlp_step: device scalar global_step");
+    gp = gstep->data_ptr();
+    switch (gstep->scalar_type()) {
+      case at::kFloat: kind = 0; break;
+      case at::kLong: kind = 1; break;
+      case at::kInt: kind = 2; break;
+      case at::kDouble: kind = 3; break;
+      default: TORCH_CHECK(false, "graph_mlp_step: unsupported global_step dtype");
+    }
+  }
+  hip_check(dtfk_graph_mlp_step(x.data_ptr<float>(), ylab.data_ptr<float>(), W1.data_ptr<float>(),
+                                b1.data_ptr<float>(), W2.data_ptr<float>(), b2.data_ptr<float>(),
+                                a2buf.data_ptr<float>(), dz2buf.data_ptr<float>(), gW1, gb1, gW2, gb2,
+                                metrics.data_ptr<float>(), gp, kind, (float)lr, B, K, H, C, act, naive ? 1 : 0,
+                                sgd ? 1 : 0, cur_stream()),
+            "graph_mlp_step");
+}
+
 void init_mlp(py::module& m) {
+  m.def("graph_mlp_step", &graph_mlp_step, py::arg("x"), py::arg("ylab"), py::arg("W1"), py::arg("b1"),
+        py::arg("W2"), py::arg("b2"), py::arg("a2buf"), py::arg("dz2buf"), py::arg("grads"), py::arg("metrics"),
+        py::arg("gstep"), py::arg("lr"), py::arg("act"), py::arg("naive"), py::arg("sgd"));
   m.def("mlp_persist", &mlp_persist, py::arg("xs"), py::arg("xts"), py::arg("rec"), py::arg("B"),
         py::arg("nsteps"), py::arg("params"), py::arg("lr"), py::arg("metrics"), py::arg("gstep"), py::arg("seq"),
         py::arg("gran"), py::arg("err"), py::arg("timeout_s"), py::arg("act"), py::arg("naive"),

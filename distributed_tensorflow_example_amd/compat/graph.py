@@ -656,12 +656,11 @@ pow = _binary(lambda a, b: a ** b, "Pow")  # noqa: A001
 
 def matmul(a, b, transpose_a=False, transpose_b=False, name="MatMul") -> Tensor:
     def f(x, y):
+        # fp32 stays fp32 (the reference graph's precision): the eager path is
+        # a plain library GEMM; the matched training graph runs on the
+        # exact-fp32 MFMA kernels of compat/lowering.py instead
         x = x.t() if transpose_a else x
         y = y.t() if transpose_b else y
-        if x.is_cuda and x.dim() == 2 and y.dim() == 2 and x.dtype == torch.float32 and y.dtype == torch.float32:
-            from ..ops import linear_act
-
-            return linear_act(x, y, None, "none")
         return x @ y
     return Tensor(f, [a, b], name, op_type="MatMul",
                   attrs={"transpose_a": bool(transpose_a), "transpose_b": bool(transpose_b)})

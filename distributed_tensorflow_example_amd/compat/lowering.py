@@ -1,0 +1,298 @@
+"""Graph lowering for Session.run: replace matched subgraphs by fused kernels.
+
+The compat graph records TF op types and attrs on every node
+(compat/graph.py), so a Session can recognise the reference's training
+graph instead of running it op by op (Session.run -> fused step).
+Matched today -- the headline graph (example.py:93-118):
+
+    a2   = Sigmoid|Relu(Add|BiasAdd(MatMul(x, W1), b1))
+    z3   = Add|BiasAdd(MatMul(a2, W2), b2)
+    loss = Mean(Neg(Sum(Mul(y_, Log(Softmax(z3))), axis 1)))      naive form
+         | Mean(SoftmaxCrossEntropyWithLogits(y_, z3))             stable form
+    train_op = <Optimizer>.minimize(loss, global_step)
+    accuracy = Mean(Cast(Equal(ArgMax(Softmax(z3), 1), ArgMax(y_, 1))))   (optional)
+
+A run that fetches train_op executes three exact-fp32 MFMA kernels
+(csrc/kernels/graph_mlp.hip): forward, head + backward of layer 2, and the
+layer-1 weight gradient.  With GradientDescentOptimizer on one worker the
+SGD update and global_step += 1 happen inside those kernels; otherwise the
+kernels write the four gradients straight into the optimizer's all-reduce
+bucket and the usual sync + fused optimizer step follows.  The loss and
+accuracy of the run (pre-update, as TF evaluates them in the same run) are
+seeded into the run's memo, so summaries / cost fetches of the same run cost
+no extra kernels.
+
+A run is lowered only if nothing else it fetches reads the matched
+variables or interior nodes (those would see post-update weights); anything
+unmatched -- other shapes, CPU tensors, other fetch sets -- runs eagerly as
+before.  DTF_GRAPH_LOWERING=0 disables lowering.
+"""
+from __future__ import annotations
+
+import os
+import weakref
+from typing import Any, Dict, List, Optional
+
+import torch
+
+from .graph import Operation, Tensor
+
+_CACHE: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()   # train_op -> plan | False
+
+
+def enabled() -> bool:
+    return os.environ.get("DTF_GRAPH_LOWERING", "1") != "0"
+
+
+def _is(t, *types) -> bool:
+    return isinstance(t, Tensor) and getattr(t, "op_type", None) in types
+
+
+def _is_plain_var(t) -> bool:
+    return getattr(t, "op_type", None) == "VariableV2" and not getattr(t, "is_partitioned", False) and \
+        isinstance(getattr(t, "value", None), torch.Tensor)
+
+
+def _dense(t):
+    """(lhs, W, b) of Add|BiasAdd(MatMul(lhs, W), b) with plain variables, else None."""
+    if not _is(t, "Add", "AddV2", "BiasAdd") or len(t.inputs) != 2:
+        return None
+    mm, b = t.inputs
+    if not _is(mm, "MatMul"):
+        mm, b = b, mm
+    if not _is(mm, "MatMul") or mm.attrs.get("transpose_a") or mm.attrs.get("transpose_b"):
+        return None
+    lhs, W = mm.inputs
+    if not (_is_plain_var(W) and _is_plain_var(b)):
+        return None
+    if W.value.dim() != 2 or b.value.dim() != 1 or b.value.numel() != W.value.shape[1]:
+        return None
+    return lhs, W, b, [t, mm]
+
+
+class MLPPattern:
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+def match_mlp(loss) -> Optional[MLPPattern]:
+    """Match the reference loss graph; returns the pattern or None."""
+    if not _is(loss, "Mean") or loss.attrs.get("axis") is not None:
+        return None
+    inner = loss.inputs[0]
+    interior = [loss]
+    naive = True
+    if _is(inner, "SoftmaxCrossEntropyWithLogits"):
+        if inner.attrs.get("dim", -1) not in (-1, 1):
+            return None
+        ylab, z3 = inner.inputs
+        naive = False
+        sm = None
+        interior.append(inner)
+    else:
+        if not _is(inner, "Neg"):
+            return None
+        s = inner.inputs[0]
+        if not _is(s, "Sum") or tuple(s.attrs.get("axis") or ()) not in ((1,), (-1,)) or s.attrs.get("keep_dims"):
+            return None
+        mul = s.inputs[0]
+        if not _is(mul, "Mul") or len(mul.inputs) != 2:
+            return None
+        a, b = mul.inputs
+        if not _is(b, "Log"):
+            a, b = b, a
+        if not _is(b, "Log"):
+            return None
+        sm = b.inputs[0]
+        if not _is(sm, "Softmax") or sm.attrs.get("dim", -1) not in (-1, 1):
+            return None
+        ylab, z3 = a, sm.inputs[0]
+        interior += [inner, s, mul, b, sm]
+    d2 = _dense(z3)
+    if d2 is None:
+        return None
+    a2, W2, b2, int2 = d2
+    if not _is(a2, "Sigmoid", "Relu"):
+        return None
+    d1 = _dense(a2.inputs[0])
+    if d1 is None:
+        return None
+    x, W1, b1, int1 = d1
+    if W1.value.shape[1] != W2.value.shape[0]:
+        return None
+    if isinstance(ylab, Tensor) and (ylab is x):
+        return None
+    return MLPPattern(loss=loss, x=x, ylab=ylab, W1=W1, b1=b1, W2=W2, b2=b2, softmax=sm, z3=z3, a2=a2,
+                      act=0 if a2.op_type == "Sigmoid" else 1, naive=naive,
+                      interior=interior + int2 + [a2] + int1)
+
+
+def _match_accuracy(g, pat) -> Optional[Tensor]:
+    """Mean(Cast(Equal(ArgMax(y, 1), ArgMax(y_, 1)), float)) over the pattern's
+    softmax (or logits) and labels, anywhere in the graph."""
+    preds = {id(pat.z3)} | ({id(pat.softmax)} if pat.softmax is not None else set())
+    for t in g._nodes:
+        if not _is(t, "Mean") or t.attrs.get("axis") is not None:
+            continue
+        c = t.inputs[0]
+        if not _is(c, "Cast") or c.attrs.get("DstT") not in (torch.float32,):
+            continue
+        e = c.inputs[0]
+        if not _is(e, "Equal") or len(e.inputs) != 2:
+            continue
+        am = e.inputs
+        if not all(_is(a, "ArgMax") and a.attrs.get("axis") in (1, -1) for a in am):
+            continue
+        srcs = [a.inputs[0] for a in am]
+        for p, l in (srcs, srcs[::-1]):
+            if (id(p) in preds or (_is(p, "Softmax") and p.inputs[0] is pat.z3)) and l is pat.ylab:
+                return t
+    return None
+
+
+class MLPStepPlan:
+    """Fused execution of one matched train op."""
+
+    def __init__(self, op: Operation, pat: MLPPattern, graph):
+        info = op._lowering
+        self.op, self.pat, self.info = op, pat, info
+        self.accuracy = _match_accuracy(graph, pat)
+        order = {id(v): i for i, v in enumerate(info["vars"])}
+        self.var_index = [order[id(v)] for v in (pat.W1, pat.b1, pat.W2, pat.b2)]
+        self.seeded = {id(pat.loss), id(op)} | ({id(self.accuracy)} if self.accuracy is not None else set())
+        self.blocked = {id(t) for t in pat.interior} | {id(v) for v in (pat.W1, pat.b1, pat.W2, pat.b2)}
+        self._fetch_ok: Dict[tuple, bool] = {}
+        self.a2buf = self.dz2buf = self.metrics = None
+        self.steps = 0
+
+    # -------------------------------------------------------------- checks
+    def fetches_ok(self, fetch_list) -> bool:
+        key = tuple(id(f) for f in fetch_list)
+        ok = self._fetch_ok.get(key)
+        if ok is None:
+            ok = True
+            seen = set()
+            stack = [f for f in fetch_list if isinstance(f, Tensor)]
+            while stack and ok:
+                t = stack.pop()
+                if id(t) in seen or id(t) in self.seeded:
+                    continue
+                seen.add(id(t))
+                if id(t) in self.blocked:
+                    ok = False
+                    break
+                stack.extend(i for i in getattr(t, "inputs", ()) if isinstance(i, Tensor))
+            self._fetch_ok[key] = ok
+        return ok
+
+    # -------------------------------------------------------------- run
+    def run(self, ctx) -> bool:
+        from .. import _native
+
+        pat, info = self.pat, self.info
+        x = ctx.eval(pat.x)
+        y = ctx.eval(pat.ylab)
+        W1, b1, W2, b2 = (v.value for v in (pat.W1, pat.b1, pat.W2, pat.b2))
+        if not (isinstance(x, torch.Tensor) and isinstance(y, torch.Tensor) and x.is_cuda and W1.is_cuda):
+            return False
+        if x.dtype != torch.float32 or y.dtype != torch.float32 or x.dim() != 2:
+            return False
+        B, K = x.shape
+        H, C = W1.shape[1], W2.shape[1]
+        HP, BP = (H + 15) // 16 * 16, (B + 15) // 16 * 16
+        if not (1 <= B <= 256 and BP * HP <= 16384 and H <= 128 and C <= 16 and W1.shape[0] == K
+                and y.numel() == B * C and all(p.dtype == torch.float32 for p in (W1, b1, W2, b2))):
+            return False
+        x = x.contiguous()
+        y = y.reshape(B, C).contiguous()
+        if self.a2buf is None or self.a2buf.numel() < BP * HP:
+            self.a2buf = torch.empty(BP * HP, dtype=torch.float32, device=x.device)
+            self.dz2buf = torch.empty(BP * HP, dtype=torch.float32, device=x.device)
+        if self.metrics is None:
+            self.metrics = torch.zeros(2, dtype=torch.float32, device=x.device)
+        opt, fused, sync, gs_var = info["opt"], info["fused"], info["sync"], info["global_step"]
+        from .train import GradientDescentOptimizer, _world_or_local
+        from ..utils import debug as _debug
+
+        w = _world_or_local()
+        opt._steps += 1
+        _debug.fault_point(opt._steps, w.rank)
+        lr = opt._lr_value()
+        in_kernel = type(opt) is GradientDescentOptimizer and (w.world_size == 1 or not opt.sync_replicas) \
+            and not info["sparse"]
+        gstep = None
+        if in_kernel and gs_var is not None and isinstance(getattr(gs_var, "value", None), torch.Tensor) \
+                and gs_var.value.is_cuda and gs_var.value.numel() == 1 and \
+                gs_var.value.dtype in (torch.float32, torch.int64, torch.int32, torch.float64):
+            gstep = gs_var.value.data
+        C_ = _native.load()
+        if in_kernel:
+            C_.graph_mlp_step(x, y, W1.data, b1.data, W2.data, b2.data, self.a2buf, self.dz2buf, None,
+                              self.metrics, gstep, float(lr), pat.act, pat.naive, True)
+            if gs_var is not None and gstep is None:
+                with torch.no_grad():
+                    gs_var.value.data += 1
+        else:
+            views = sync.views
+            grads = [views[i] for i in self.var_index]
+            C_.graph_mlp_step(x, y, W1.data, b1.data, W2.data, b2.data, self.a2buf, self.dz2buf, grads,
+                              self.metrics, None, float(lr), pat.act, pat.naive, False)
+            gl = [None] * len(info["vars"])
+            for i, g in zip(self.var_index, grads):
+                gl[i] = g
+            if opt.sync_replicas:
+                gl = sync(gl)
+            if fused is not None:
+                from ..compat.graph import Tensor as _T
+
+                if isinstance(opt.learning_rate, _T):
+                    fused.set_lr(lr)
+                fused.step(grads=[g.contiguous() for g in gl])
+            if gs_var is not None:
+                with torch.no_grad():
+                    gs_var.value.data += 1
+        ctx.memo[id(pat.loss)] = self.metrics[0]
+        if self.accuracy is not None:
+            ctx.memo[id(self.accuracy)] = self.metrics[1]
+        ctx.memo[id(self.op)] = None
+        self.steps += 1
+        return True
+
+
+def _flatten(f, out: List[Any]):
+    if isinstance(f, (list, tuple)):
+        for x in f:
+            _flatten(x, out)
+    elif isinstance(f, dict):
+        for x in f.values():
+            _flatten(x, out)
+    elif f is not None:
+        out.append(f)
+    return out
+
+
+def try_lower(session, fetches, ctx) -> None:
+    """Run lowered plans for train ops in `fetches`, seeding ctx.memo."""
+    if not enabled():
+        return
+    flat = _flatten(fetches, [])
+    for f in flat:
+        if not (isinstance(f, Operation) and getattr(f, "_lowering", None) is not None):
+            continue
+        plan = _CACHE.get(f)
+        if plan is None:
+            pat = match_mlp(getattr(f, "loss", None)) if getattr(f, "loss", None) is not None else None
+            plan = False
+            if pat is not None and {id(v) for v in f._lowering["vars"]} == \
+                    {id(v) for v in (pat.W1, pat.b1, pat.W2, pat.b2)}:
+                plan = MLPStepPlan(f, pat, session.graph)
+            _CACHE[f] = plan
+        if plan is False or id(f) in ctx.memo:
+            continue
+        if plan.fetches_ok(flat):
+            plan.run(ctx)
+
+
+def plan_for(train_op) -> Optional[MLPStepPlan]:
+    p = _CACHE.get(train_op)
+    return p if p else None

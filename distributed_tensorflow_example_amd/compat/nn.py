@@ -47,13 +47,15 @@ def softmax_cross_entropy_with_logits(_sentinel=None, labels=None, logits=None, 
     """per-row loss (TF returns a vector); reduce with reduce_mean."""
     def f(y, z):
         return -(y.float() * torch.log_softmax(z.float(), dim)).sum(dim)
-    return Tensor(f, [labels, logits], name or "SoftmaxCrossEntropyWithLogits")
+    return Tensor(f, [labels, logits], name or "SoftmaxCrossEntropyWithLogits", op_type="SoftmaxCrossEntropyWithLogits",
+                  attrs={"dim": dim})
 
 
 def sparse_softmax_cross_entropy_with_logits(_sentinel=None, labels=None, logits=None, name=None):
     def f(y, z):
         return torch.nn.functional.cross_entropy(z.float(), y.long(), reduction="none")
-    return Tensor(f, [labels, logits], name or "SparseSoftmaxCrossEntropyWithLogits")
+    return Tensor(f, [labels, logits], name or "SparseSoftmaxCrossEntropyWithLogits",
+                  op_type="SparseSoftmaxCrossEntropyWithLogits")
 
 
 def sigmoid_cross_entropy_with_logits(*args, logits=None, labels=None, targets=None, name=None):

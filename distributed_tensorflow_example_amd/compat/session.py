@@ -16,6 +16,7 @@ from typing import Any
 import numpy as np
 import torch
 
+from . import lowering as _lowering
 from .graph import Operation, RunContext, Tensor, get_default_graph
 
 _tls = threading.local()
@@ -73,6 +74,8 @@ class Session:
         ctx = RunContext(feed_dict or {}, self.graph.device)
         ctx.session = self
         ctx.options = options
+        if ctx.device.type == "cuda":
+            _lowering.try_lower(self, fetches, ctx)     # fused kernels for matched train ops
         out = self._run(fetches, ctx)
         if self._post_run and not self._in_post:
             # step-boundary services (Supervisor checkpoints): run in the training

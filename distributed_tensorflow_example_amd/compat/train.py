@@ -390,6 +390,10 @@ class Optimizer:
             return None
         op = Operation(None, [], name or self.name)
         op._eval = run
+        # what compat/lowering.py needs to replace forward+backward (+ SGD) of
+        # this op by fused kernels
+        op._lowering = {"opt": opt, "vars": vars_, "fused": fused, "sync": sync, "global_step": global_step,
+                        "sparse": sparse_pairs}
         return op
 
     def minimize(self, loss, global_step=None, var_list=None, name=None, **kw) -> Operation:

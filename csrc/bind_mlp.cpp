@@ -429,8 +429,8 @@ void graph_mlp_step(at::Tensor x, at::Tensor ylab, at::Tensor W1, at::Tensor b1,
   TORCH_CHECK(W1.size(0) == K && W2.size(0) == H && b1.numel() == H && b2.numel() == C &&
                   ylab.numel() == (int64_t)B * C,
               "graph_mlp_step: shape mismatch");
-  const int HP = (H + 15) & ~15, BP = (B + 15) & ~15;
-  TORCH_CHECK(a2buf.numel() >= (int64_t)BP * HP && dz2buf.numel() >= (int64_t)BP * HP && metrics.numel() >= 2,
+  const int HP = (H + 16) & ~15, BP = (B + 15) & ~15;
+  TORCH_CHECK(a2buf.numel() >= (int64_t)BP * HP && dz2buf.numel() >= (int64_t)BP * HP && metrics.numel() >= 3,
               "graph_mlp_step: scratch too small");
   float *gW1 = nullptr, *gb1 = nullptr, *gW2 = nullptr, *gb2 = nullptr;
   if (!sgd) {

@@ -33,6 +33,7 @@ import os
 import weakref
 from typing import Any, Dict, List, Optional
 
+import numpy as np
 import torch
 
 from .graph import Operation, Tensor
@@ -185,21 +186,67 @@ class MLPStepPlan:
             self._fetch_ok[key] = ok
         return ok
 
+    # -------------------------------------------------------------- feeds
+    @staticmethod
+    def _feed_of(ctx, ph):
+        if getattr(ph, "op_type", None) != "Placeholder" or id(ph) in ctx.memo:
+            return None
+        for key in (ph, ph.name, ph.name[:-2]):
+            try:
+                if key in ctx.feeds:
+                    v = ctx.feeds[key]
+                    return v if isinstance(v, np.ndarray) and v.dtype == np.float32 else None
+            except TypeError:
+                continue
+        return None
+
+    def _packed_feeds(self, ctx, dev):
+        """x and y_ fed as float32 numpy arrays -> one pinned staging buffer ->
+        ONE host-to-device copy (instead of one per placeholder)."""
+        fx, fy = self._feed_of(ctx, self.pat.x), self._feed_of(ctx, self.pat.ylab)
+        if fx is None or fy is None or fx.ndim != 2:
+            return None
+        nx, ny = fx.size, fy.size
+        n = nx + ny
+        slot = self._slot = (getattr(self, "_slot", 0) + 1) % 2
+        if getattr(self, "_pinned", None) is None or self._pinned[0].numel() < n:
+            cap = max(n, 1 << 16)
+            self._pinned = [torch.empty(cap, dtype=torch.float32, pin_memory=True) for _ in range(2)]
+            self._events = [None, None]
+            self._dev = torch.empty(cap, dtype=torch.float32, device=dev)
+        ev = self._events[slot]
+        if ev is not None:
+            ev.synchronize()                  # the copy that last read this staging slot is done
+        hb = self._pinned[slot].numpy()
+        hb[:nx] = fx.reshape(-1)
+        hb[nx:n] = fy.reshape(-1)
+        self._dev[:n].copy_(self._pinned[slot][:n], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._events[slot] = ev
+        x = self._dev[:nx].view(fx.shape)
+        y = self._dev[nx:n].view(fy.shape)
+        ctx.memo[id(self.pat.x)] = x
+        ctx.memo[id(self.pat.ylab)] = y
+        return x, y
+
     # -------------------------------------------------------------- run
-    def run(self, ctx) -> bool:
+    def run(self, ctx, flat) -> bool:
         from .. import _native
 
         pat, info = self.pat, self.info
-        x = ctx.eval(pat.x)
-        y = ctx.eval(pat.ylab)
         W1, b1, W2, b2 = (v.value for v in (pat.W1, pat.b1, pat.W2, pat.b2))
-        if not (isinstance(x, torch.Tensor) and isinstance(y, torch.Tensor) and x.is_cuda and W1.is_cuda):
+        if not W1.is_cuda:
+            return False
+        xy = self._packed_feeds(ctx, W1.device)
+        x, y = xy if xy is not None else (ctx.eval(pat.x), ctx.eval(pat.ylab))
+        if not (isinstance(x, torch.Tensor) and isinstance(y, torch.Tensor) and x.is_cuda):
             return False
         if x.dtype != torch.float32 or y.dtype != torch.float32 or x.dim() != 2:
             return False
         B, K = x.shape
         H, C = W1.shape[1], W2.shape[1]
-        HP, BP = (H + 15) // 16 * 16, (B + 15) // 16 * 16
+        HP, BP = (H + 16) // 16 * 16, (B + 15) // 16 * 16       # HP >= H + 1: the kernels' ones column
         if not (1 <= B <= 256 and BP * HP <= 16384 and H <= 128 and C <= 16 and W1.shape[0] == K
                 and y.numel() == B * C and all(p.dtype == torch.float32 for p in (W1, b1, W2, b2))):
             return False
@@ -209,7 +256,8 @@ class MLPStepPlan:
             self.a2buf = torch.empty(BP * HP, dtype=torch.float32, device=x.device)
             self.dz2buf = torch.empty(BP * HP, dtype=torch.float32, device=x.device)
         if self.metrics is None:
-            self.metrics = torch.zeros(2, dtype=torch.float32, device=x.device)
+            self.metrics = torch.zeros(3, dtype=torch.float32, device=x.device)
+            self.host_metrics = torch.zeros(3, dtype=torch.float32, pin_memory=True)
         opt, fused, sync, gs_var = info["opt"], info["fused"], info["sync"], info["global_step"]
         from .train import GradientDescentOptimizer, _world_or_local
         from ..utils import debug as _debug
@@ -243,21 +291,56 @@ class MLPStepPlan:
             if opt.sync_replicas:
                 gl = sync(gl)
             if fused is not None:
-                from ..compat.graph import Tensor as _T
-
-                if isinstance(opt.learning_rate, _T):
+                if isinstance(opt.learning_rate, Tensor):
                     fused.set_lr(lr)
                 fused.step(grads=[g.contiguous() for g in gl])
             if gs_var is not None:
                 with torch.no_grad():
                     gs_var.value.data += 1
-        ctx.memo[id(pat.loss)] = self.metrics[0]
-        if self.accuracy is not None:
-            ctx.memo[id(self.accuracy)] = self.metrics[1]
+        # loss / accuracy (/ global_step) of this run: one device-to-host copy
+        # when the fetches need them, seeded as host scalars
+        needs, gs_seed = self._needs(flat, gs_var, gstep)
+        if needs:
+            self.host_metrics.copy_(self.metrics)
+            m = self.host_metrics
+            ctx.memo[id(pat.loss)] = m[0]
+            if self.accuracy is not None:
+                ctx.memo[id(self.accuracy)] = m[1]
+            if gs_seed:
+                ctx.memo[id(gs_var)] = m[2].to(gs_var.value.dtype)
+        else:
+            ctx.memo[id(pat.loss)] = self.metrics[0]
+            if self.accuracy is not None:
+                ctx.memo[id(self.accuracy)] = self.metrics[1]
         ctx.memo[id(self.op)] = None
         self.steps += 1
         return True
 
+    def _needs(self, flat, gs_var, gstep):
+        """(fetches read the loss/accuracy, global_step may be seeded)."""
+        key = ("needs",) + tuple(id(f) for f in flat)
+        r = self._fetch_ok.get(key)
+        if r is None:
+            targets = {id(self.pat.loss)} | ({id(self.accuracy)} if self.accuracy is not None else set())
+            hit, seen = False, {}
+            stack = [f for f in flat if isinstance(f, Tensor) and f is not self.op]
+            while stack:
+                t = stack.pop()
+                if id(t) in seen:
+                    continue
+                seen[id(t)] = t
+                if id(t) in targets:
+                    hit = True
+                    continue
+                stack.extend(i for i in getattr(t, "inputs", ()) if isinstance(i, Tensor))
+            # global_step is seeded (post-increment, exact in fp32) only when it is
+            # fetched directly and no other node of the run reads it
+            read_by_others = any(i is gs_var for t in seen.values() for i in getattr(t, "inputs", ()))
+            gs_ok = (gstep is not None and gstep.dtype == torch.float32 and any(f is gs_var for f in flat)
+                     and not read_by_others)
+            r = (hit or gs_ok, gs_ok)
+            self._fetch_ok[key] = r
+        return r
 
 def _flatten(f, out: List[Any]):
     if isinstance(f, (list, tuple)):
@@ -290,7 +373,7 @@ def try_lower(session, fetches, ctx) -> None:
         if plan is False or id(f) in ctx.memo:
             continue
         if plan.fetches_ok(flat):
-            plan.run(ctx)
+            plan.run(ctx, flat)
 
 
 def plan_for(train_op) -> Optional[MLPStepPlan]:

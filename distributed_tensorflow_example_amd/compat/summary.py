@@ -132,7 +132,8 @@ def summary_iterator(path: str) -> Iterator[Event]:
 # ----------------------------------------------------------------------- ops
 def _to_float(x):
     if isinstance(x, torch.Tensor):
-        return float(x.detach().float().mean().item())
+        # a scalar is read as is (no reduction kernel on the device)
+        return float(x.item()) if x.numel() == 1 else float(x.detach().float().mean().item())
     return float(np.asarray(x, dtype=np.float64).mean())
 
 

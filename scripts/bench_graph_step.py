@@ -1,0 +1,73 @@
+"""Per-step cost of the compat graph path (examples/mnist_example.py's graph,
+no --fused): Session.run wall time per step with the lowered kernels vs the
+eager op-by-op path (DTF_GRAPH_LOWERING=0), plus device time of the three
+lowered kernels alone (CUDA events around graph_mlp_step).
+
+    python scripts/bench_graph_step.py [steps]
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
+
+
+def main():
+    import distributed_tensorflow_example_amd.compat as tf
+    from distributed_tensorflow_example_amd import _native
+    from distributed_tensorflow_example_amd.compat import lowering as L
+    from test_lowering_cpu import _graph
+
+    steps = int(sys.argv[1]) if len(sys.argv) > 1 else 2000
+    rng = np.random.default_rng(0)
+    B = 100
+    xs = (rng.integers(0, 256, (64, B, 784)) / 255.0).astype(np.float32)
+    ys = np.eye(10, dtype=np.float32)[rng.integers(0, 10, (64, B))]
+    out = {}
+    for mode in ("1", "0"):
+        os.environ["DTF_GRAPH_LOWERING"] = mode
+        g = _graph(tf)
+        with tf.Session() as sess:
+            sess.run(tf.global_variables_initializer())
+            fetch = [g["train"], g["ce"], g["gs"]]
+            for i in range(20):
+                sess.run(fetch, feed_dict={g["x"]: xs[i % 64], g["y_"]: ys[i % 64]})
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(steps):
+                sess.run(fetch, feed_dict={g["x"]: xs[i % 64], g["y_"]: ys[i % 64]})
+            torch.cuda.synchronize()
+            out["lowered" if mode == "1" else "eager"] = (time.perf_counter() - t0) / steps * 1e3
+            if mode == "1":
+                plan = L.plan_for(g["train"])
+                assert plan is not None and plan.steps >= steps
+                # device time of the three kernels alone
+                C = _native.load()
+                W1, b1, W2, b2 = (v.value.data for v in (plan.pat.W1, plan.pat.b1, plan.pat.W2, plan.pat.b2))
+                x = torch.from_numpy(xs[0]).cuda()
+                y = torch.from_numpy(ys[0]).cuda()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                for _ in range(10):
+                    C.graph_mlp_step(x, y, W1, b1, W2, b2, plan.a2buf, plan.dz2buf, None, plan.metrics, None,
+                                     0.0, 0, True, True)
+                e0.record()
+                for _ in range(1000):
+                    C.graph_mlp_step(x, y, W1, b1, W2, b2, plan.a2buf, plan.dz2buf, None, plan.metrics, None,
+                                     0.0, 0, True, True)
+                e1.record()
+                torch.cuda.synchronize()
+                out["kernels_us"] = e0.elapsed_time(e1)
+        tf.reset_default_graph()
+    os.environ.pop("DTF_GRAPH_LOWERING", None)
+    print(json.dumps({"session_run_ms_per_step_lowered": round(out["lowered"], 4),
+                      "session_run_ms_per_step_eager": round(out["eager"], 4),
+                      "lowered_kernels_us_per_step": round(out["kernels_us"], 3), "batch": B, "steps": steps}))
+
+
+if __name__ == "__main__":
+    main()

@@ -233,3 +233,33 @@ def test_persist_multi_rank_same_gpu(native, nproc, precision, grad):
     assert r.returncode == 0 and line, out[-3000:]
     res = json.loads(line[-1])
     assert res["persist_selftest"] == "pass", res
+
+
+def test_bench_two_ranks_same_gpu_short_run(native):
+    """bench.py as the driver launches it for N=2 (torch.distributed.run, one
+    rank per 'GPU'), at the driver's short step count, with both ranks sharing
+    cuda:0 (DTF_BENCH_SAME_GPU=1: gloo control plane, IPC data plane): the
+    exchange strategy is chosen and validated, the timed run completes, and
+    rank 0 prints one contract JSON line.  Timings are not multi-GPU numbers."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(repo, "bench.py"), "--gpus", "2",
+           "--steps", "20", "--warmup", "5", "--tune-steps", "40"]
+    env = dict(os.environ, PYTHONPATH=repo, OMP_NUM_THREADS="2", DTF_BENCH_SAME_GPU="1")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=env, cwd=repo)
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert r.returncode == 0 and len(lines) == 1, (r.stdout + r.stderr)[-3000:]
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["steps"] == 20 and res["warmup"] == 5
+    assert res["value"] > 0 and res["ms_per_step"] > 0 and res["dtype"] == "fp32"
+    assert res["config"]["parallelism"] == "dp2"

@@ -4,9 +4,16 @@
 #include <hip/hip_runtime.h>
 
 #include <stdexcept>
+#include <vector>
 #include <string>
 
 extern "C" {
+int dtfk_route_max_world();
+hipError_t dtfk_sparse_route(const void* sids, int ids32, const int64_t* perm, int N, int W, int cap, int* inv_sorted,
+                             int64_t* inverse, int64_t* uniq, int* dest, int64_t* send, int* count,
+                             hipStream_t stream);
+hipError_t dtfk_philox_normal(float* out, long long rows, int dim, long long row_mul, long long row_add,
+                              unsigned long long seed, float mean, float stddev, hipStream_t stream);
 hipError_t dtfk_gemm(const void* A, int a_bf16, int lda, int transA, const void* B, int b_bf16, int ldb,
                      int transB, void* C, int c_bf16, int ldc, float* Z, const float* bias, int M, int N,
                      int K, float alpha, float beta, int act, hipStream_t stream);
@@ -250,7 +257,41 @@ void multi_tensor_sumsq(at::Tensor tab, at::Tensor chunks, bool grad_bf16, at::T
      "multi_tensor_sumsq");
 }
 
+void philox_normal(at::Tensor out, int64_t row_mul, int64_t row_add, uint64_t seed, double mean, double stddev) {
+  f32c(out, "out");
+  if (out.dim() != 2) throw std::runtime_error("philox_normal: out must be [rows, dim]");
+  ck(dtfk_philox_normal(out.data_ptr<float>(), out.size(0), (int)out.size(1), row_mul, row_add, seed, (float)mean,
+                        (float)stddev, cs()),
+     "philox_normal");
+}
+
+// Dedup + owner bucketing of sorted ids in one kernel (csrc/kernels/sparse_route.hip).
+std::vector<at::Tensor> sparse_route(at::Tensor sids, at::Tensor perm, int W, int64_t cap) {
+  gpu(sids, "sids"); i64c(perm, "perm");
+  if (!sids.is_contiguous() || (sids.scalar_type() != at::kInt && sids.scalar_type() != at::kLong))
+    throw std::runtime_error("sparse_route: sorted ids must be contiguous int32/int64");
+  if (W < 1 || W > dtfk_route_max_world()) throw std::runtime_error("sparse_route: world size out of range");
+  const int64_t N = sids.numel();
+  if (W > 1 && cap < N) throw std::runtime_error("sparse_route: capacity below the batch's id count");
+  if (std::max(N, cap) * std::max(W, 1) >= (1LL << 31)) throw std::runtime_error("sparse_route: batch too large");
+  auto o32 = sids.options().dtype(at::kInt), o64 = sids.options().dtype(at::kLong);
+  at::Tensor inv = at::empty({N}, o32), inverse = at::empty({N}, o64), uniq = at::empty({N}, o64);
+  at::Tensor dest = at::empty({W > 1 ? N : 0}, o32), send = at::empty({W > 1 ? (int64_t)W * cap : 0}, o64);
+  at::Tensor count = at::empty({1}, o32);
+  ck(dtfk_sparse_route(sids.data_ptr(), sids.scalar_type() == at::kInt ? 1 : 0, perm.data_ptr<int64_t>(), (int)N, W,
+                       (int)cap,
+                       inv.data_ptr<int>(), inverse.data_ptr<int64_t>(), uniq.data_ptr<int64_t>(),
+                       W > 1 ? dest.data_ptr<int>() : nullptr, W > 1 ? send.data_ptr<int64_t>() : nullptr,
+                       count.data_ptr<int>(), cs()),
+     "sparse_route");
+  return {inv, inverse, uniq, dest, send, count};
+}
+
 void init_ops(py::module& m) {
+  m.def("sparse_route", &sparse_route, py::arg("sids"), py::arg("perm"), py::arg("W"), py::arg("cap"));
+  m.def("route_max_world", &dtfk_route_max_world);
+  m.def("philox_normal", &philox_normal, py::arg("out"), py::arg("row_mul"), py::arg("row_add"), py::arg("seed"),
+        py::arg("mean"), py::arg("stddev"));
   m.def("gemm", &gemm, py::arg("A"), py::arg("transA"), py::arg("B"), py::arg("transB"), py::arg("out"),
         py::arg("bias") = py::none(), py::arg("act") = 0, py::arg("alpha") = 1.0, py::arg("beta") = 0.0,
         py::arg("Z") = py::none());

@@ -30,12 +30,12 @@ from ..parallel.world import World, get_world
 
 class SparseLRTrainer:
     def __init__(self, num_features: int, lr: float, world: Optional[World] = None, seed: int = 1,
-                 init_std: float = 1.0, device=None, auc_bins: int = 200):
+                 init_std: float = 1.0, device=None, auc_bins: int = 200, ids_capacity: Optional[int] = None):
         self.world = world or get_world()
         self.device = torch.device(device) if device is not None else self.world.device
         self.lr = float(lr)
         self.W = ShardedEmbedding(num_features, 1, self.world, init_std=init_std, seed=seed, device=self.device,
-                                  name="weights/Variable")
+                                  name="weights/Variable", capacity=ids_capacity)
         self.b = torch.zeros(1, dtype=torch.float32, device=self.device, requires_grad=True)
         self.global_step = 0
         # streaming_auc's num_thresholds = auc_bins -> auc_bins + 1 histogram bins

@@ -31,11 +31,13 @@ from ..parallel.world import World, get_world
 class WideDeep:
     def __init__(self, num_features: int, emb_dim: int = 64, hidden: Sequence[int] = (256, 128),
                  lr: float = 0.05, dense_lr: Optional[float] = None, dense_opt: str = "sgd", combiner: str = "sum",
-                 world: Optional[World] = None, seed: int = 1, device=None, emb_std: float = 0.05):
+                 world: Optional[World] = None, seed: int = 1, device=None, emb_std: float = 0.05,
+                 ids_capacity: Optional[int] = None):
         self.world = world or get_world()
         self.device = torch.device(device) if device is not None else self.world.device
         self.lr = float(lr)
         self.combiner = combiner
+        self.ids_capacity = ids_capacity   # per-batch id bound -> device-resident static routing
         self.wide = ShardedEmbedding(num_features, 1, self.world, init_std=0.01, seed=seed, device=self.device,
                                      name="wide/weights")
         self.emb = ShardedEmbedding(num_features, emb_dim, self.world, init_std=emb_std, seed=seed + 1,
@@ -68,7 +70,7 @@ class WideDeep:
     def forward(self, labels, offsets, ids, vals):
         # both tables read the same ids over the same row partition: one
         # dedup + id exchange, one row exchange carrying [U, 1 + D]
-        ctx = self.wide.route(ids)
+        ctx = self.wide.route(ids, capacity=self.ids_capacity)
         wrows, erows = lookup_shared([self.wide, self.emb], ctx)
         wrows = wrows.detach().requires_grad_(True)
         erows = erows.detach().requires_grad_(True)

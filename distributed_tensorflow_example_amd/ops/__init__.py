@@ -12,6 +12,7 @@ accuracy (example.py:125-128), AUC histograms (streaming_auc, lr2.py:400).
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 
 from .. import _native
@@ -322,7 +323,9 @@ def embedding_bag_sgd_(weight, ids, offsets, per_sample_weights, grad_out, lr: f
         seg = torch.repeat_interleave(torch.arange(offsets.numel() - 1), offsets[1:] - offsets[:-1])
         w = per_sample_weights if per_sample_weights is not None else torch.ones(ids.numel())
         W = weight if weight.dim() == 2 else weight.view(-1, 1)
-        W.index_add_(0, ids.long(), -lr * w.unsqueeze(1) * grad_out[seg])
+        ok = (ids >= 0) & (ids < W.shape[0])               # -1 = routing padding (skipped, as on the GPU)
+        W.index_add_(0, ids.long().clamp(0, max(W.shape[0] - 1, 0)),
+                     -lr * (w * ok).unsqueeze(1) * grad_out[seg])
         return weight
     _C().embedding_bag_bwd(weight, ids.long().contiguous(), offsets.long().contiguous(),
                            per_sample_weights.contiguous().float() if per_sample_weights is not None else None,
@@ -393,3 +396,62 @@ def auc_from_confusion(tp, fn, tn, fp, curve: str = "ROC") -> float:
 def auc_from_histograms(pos, neg, curve: str = "ROC") -> float:
     """streaming_auc's value from T+1-bin positive / negative histograms."""
     return auc_from_confusion(*auc_confusion(pos, neg), curve=curve)
+
+
+# --------------------------------------------------------------------------- random init
+_PHILOX_M0, _PHILOX_M1 = 0xD2511F53, 0xCD9E8D57
+_PHILOX_W0, _PHILOX_W1 = 0x9E3779B9, 0xBB67AE85
+_U32 = 0xFFFFFFFF
+
+
+def philox4x32_10(c0, c1, c2, c3, k0: int, k1: int):
+    """Philox4x32-10 (Salmon et al., SC'11) on uint64 arrays holding 32-bit words."""
+    c0, c1, c2, c3 = (np.asarray(c, dtype=np.uint64) for c in (c0, c1, c2, c3))
+    m0, m1, sh, mask = np.uint64(_PHILOX_M0), np.uint64(_PHILOX_M1), np.uint64(32), np.uint64(_U32)
+    for _ in range(10):
+        p0 = m0 * c0
+        p1 = m1 * c2
+        c0, c1, c2, c3 = (p1 >> sh) ^ c1 ^ np.uint64(k0), p1 & mask, (p0 >> sh) ^ c3 ^ np.uint64(k1), p0 & mask
+        k0 = (k0 + _PHILOX_W0) & _U32
+        k1 = (k1 + _PHILOX_W1) & _U32
+    return c0, c1, c2, c3
+
+
+def _philox10_np(q: np.ndarray, seed: int):
+    """Counters (q_lo, q_hi, 0, 0) under key (seed_lo, seed_hi)."""
+    z = np.zeros_like(q)
+    return philox4x32_10(q & np.uint64(_U32), q >> np.uint64(32), z, z, seed & _U32, (seed >> 32) & _U32)
+
+
+def _unit_np(x: np.ndarray) -> np.ndarray:
+    return (((x & np.uint64(0x7FFFFF)) | np.uint64(0x3F800000)).astype(np.uint32).view(np.float32)
+            - np.float32(1.0))
+
+
+def philox_normal_(out: torch.Tensor, row_mul: int, row_add: int, seed: int, mean: float = 0.0,
+                   stddev: float = 1.0, chunk_rows: int = 1 << 20) -> torch.Tensor:
+    """out[r, c] = N(mean, stddev) of global element (r * row_mul + row_add) * dim + c.
+
+    Counter-based (Philox4x32-10 + TF's Box-Muller), so a table row gets the
+    same value on whichever rank holds it.  GPU: csrc/kernels/random.hip;
+    CPU: the same algorithm in numpy (fp32 transcendentals; equal to a few ulp)."""
+    assert out.dim() == 2 and out.dtype == torch.float32 and out.is_contiguous()
+    seed = int(seed) & ((1 << 64) - 1)
+    if out.is_cuda:
+        _C().philox_normal(out, int(row_mul), int(row_add), seed, float(mean), float(stddev))
+        return out
+    rows, dim = out.shape
+    for s in range(0, rows, chunk_rows):
+        e = min(rows, s + chunk_rows)
+        r = np.arange(s, e, dtype=np.uint64) * np.uint64(row_mul) + np.uint64(row_add)
+        g = (r[:, None] * np.uint64(dim) + np.arange(dim, dtype=np.uint64)[None, :]).reshape(-1)
+        c0, c1, c2, c3 = _philox10_np(g >> np.uint64(2), seed)
+        w = (g & np.uint64(3)).astype(np.int64)
+        x0 = np.where(w < 2, c0, c2)
+        x1 = np.where(w < 2, c1, c3)
+        u1 = np.maximum(_unit_np(x0), np.float32(1e-7))
+        v1 = np.float32(6.2831853071795864769) * _unit_np(x1)
+        rr = np.sqrt(np.float32(-2.0) * np.log(u1))
+        z = np.where(w & 1, np.cos(v1) * rr, np.sin(v1) * rr).astype(np.float32)
+        out[s:e] = torch.from_numpy((np.float32(mean) + np.float32(stddev) * z).reshape(e - s, dim))
+    return out

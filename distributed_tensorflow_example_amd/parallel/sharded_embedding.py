@@ -19,13 +19,13 @@ HBM per GPU holds a 1e9 x 1 fp32 shard 8x over).  Per step:
 
 Each row has exactly one owner, so there is no replica drift and no
 all-reduce of a dense F x D gradient.  Initial values are a counter-based
-normal of the *global* row id, so a table is bit-identical for any world size.
+(Philox4x32-10) normal of the *global* element index, generated on the device
+by one kernel, so a table is bit-identical for any world size.
 Checkpoints store the table as a TF partitioned variable (contiguous
 fixed_size_partitioner slices, see ckpt/__init__.py).
 """
 from __future__ import annotations
 
-import math
 from typing import Optional
 
 import torch
@@ -33,47 +33,30 @@ import torch
 from .. import ops
 from .world import World, get_world
 
-_M1 = 0x9E3779B97F4A7C15 - (1 << 64)   # as signed int64
-_M2 = 0xBF58476D1CE4E5B9 - (1 << 64)
-_M3 = 0x94D049BB133111EB - (1 << 64)
-
-
-def _mix(x: torch.Tensor) -> torch.Tensor:
-    """splitmix64 finaliser on int64 tensors (wrap-around arithmetic)."""
-    x = x + _M1
-    x = (x ^ ((x >> 30) & 0x3FFFFFFFF)) * _M2
-    x = (x ^ ((x >> 27) & 0x1FFFFFFFFF)) * _M3
-    return x ^ ((x >> 31) & 0x1FFFFFFFF)
-
-
-def counter_normal(rows: torch.Tensor, dim: int, seed: int, std: float = 1.0) -> torch.Tensor:
-    """N(0, std^2) values for (global row, col), independent of sharding."""
-    col = torch.arange(dim, device=rows.device, dtype=torch.int64)
-    key = rows.long().unsqueeze(1) * dim + col + (int(seed) << 40)
-    a = _mix(key)
-    b = _mix(a ^ 0x5851F42D4C957F2D)
-    u1 = ((a >> 11) & ((1 << 53) - 1)).double().add_(0.5).mul_(1.0 / (1 << 53))
-    u2 = ((b >> 11) & ((1 << 53) - 1)).double().mul_(1.0 / (1 << 53))
-    z = torch.sqrt(-2.0 * torch.log(u1)) * torch.cos(2 * math.pi * u2)
-    return (z * std).float()
-
-
 class LookupCtx:
-    __slots__ = ("uniq", "inverse", "order", "send", "recv", "recv_local")
+    """Routing of one batch.  Dynamic: exact per-peer counts (host lists in
+    send/recv), `order` sorts uniq by owner.  Static: every peer gets `cap`
+    slots (a capacity configured identically on all ranks, >= the ids of any
+    batch, so no bucket can overflow), `order` holds each unique id's slot
+    (dest, -1 for padding) and uniq / recv_local carry -1 padding -- no host
+    read-back, every shape fixed by the batch shape and the capacity."""
+    __slots__ = ("uniq", "inverse", "order", "send", "recv", "recv_local", "static", "n")
 
-    def __init__(self, uniq, inverse, order, send, recv, recv_local):
+    def __init__(self, uniq, inverse, order, send, recv, recv_local, static=False, n=0):
         self.uniq, self.inverse, self.order = uniq, inverse, order
         self.send, self.recv, self.recv_local = send, recv, recv_local
+        self.static, self.n = static, n
 
 
 class ShardedEmbedding:
     def __init__(self, num_rows: int, dim: int = 1, world: Optional[World] = None, init_std: float = 1.0,
                  seed: int = 0, device=None, name: str = "embedding", zero_init: bool = False,
-                 init_chunk_rows: int = 1 << 24):
+                 capacity: Optional[int] = None):
         self.world = world or get_world()
         self.W = self.world.world_size
         self.rank = self.world.rank
         self.num_rows, self.dim, self.name = int(num_rows), int(dim), name
+        self.capacity = capacity          # ids per batch bound (same on every rank) -> static routing
         self.device = torch.device(device) if device is not None else self.world.device
         n_local = (self.num_rows - self.rank + self.W - 1) // self.W if self.rank < self.num_rows else 0
         self.local = torch.empty((n_local, self.dim), dtype=torch.float32, device=self.device)
@@ -81,19 +64,27 @@ class ShardedEmbedding:
             if zero_init:
                 self.local.zero_()
             else:
-                for s in range(0, n_local, init_chunk_rows):
-                    e = min(n_local, s + init_chunk_rows)
-                    grow = torch.arange(s, e, device=self.device, dtype=torch.int64) * self.W + self.rank
-                    self.local[s:e] = counter_normal(grow, self.dim, seed, init_std)
+                # local row i is global row i*W + rank: one counter-based
+                # Philox kernel over the shard (csrc/kernels/random.hip)
+                ops.philox_normal_(self.local, self.W, self.rank, seed, 0.0, init_std)
 
     # ------------------------------------------------------------------ exchange
-    def route(self, ids: torch.Tensor) -> LookupCtx:
+    def route(self, ids: torch.Tensor, capacity: Optional[int] = None) -> LookupCtx:
         """Dedup `ids` and send each owner the unique ids it serves (no rows yet).
 
         The context depends only on the ids and the row partition, so tables
-        with the same row count and world share it (`lookup_shared`)."""
+        with the same row count and world share it (`lookup_shared`).
+        `capacity`: ids-per-batch bound configured identically on every rank ->
+        the device-resident static exchange (no host read-back); without it
+        (W > 1) the exact per-peer counts are exchanged and read on the host."""
         ids = ids.to(self.device).long()
-        if ids.is_cuda and 0 < ids.numel() and self.num_rows < 2 ** 31:
+        N = ids.numel()
+        capacity = self.capacity if capacity is None else capacity
+        if N > 0 and (self.W == 1 or (capacity is not None and self.W <= _max_route_world())):
+            if self.W > 1 and N > capacity:
+                raise ValueError(f"{self.name}: batch has {N} ids, above the routing capacity {capacity}")
+            return self._route_static(ids, int(capacity) if capacity is not None else N)
+        if ids.is_cuda and 0 < N and self.num_rows < 2 ** 31:
             # one int32 radix sort serves both the dedup and (handed over to
             # ops) the sorted-segment backward of every bag over these ids
             sids, perm = torch.sort(ids.to(torch.int32))
@@ -116,6 +107,25 @@ class ShardedEmbedding:
         recv_ids = torch.empty(sum(recv_l), dtype=torch.int64, device=self.device)
         self.world.all_to_all(uniq_sorted, send_l, recv_ids, recv_l)
         return LookupCtx(uniq, inverse, order, send_l, recv_l, recv_ids // self.W)
+
+    def _route_static(self, ids: torch.Tensor, cap: int) -> LookupCtx:
+        """Device-resident routing: radix sort + one dedup/bucketing kernel
+        (csrc/kernels/sparse_route.hip) + an equal-split all-to-all of `cap` id
+        slots per peer.  Nothing is read back to the host."""
+        N, W = ids.numel(), self.W
+        small = self.num_rows < 2 ** 31
+        sids, perm = torch.sort(ids.to(torch.int32) if small else ids)
+        if ids.is_cuda:
+            inv_sorted, inverse, uniq, dest, send, _count = ops._C().sparse_route(sids.contiguous(), perm, W, cap)
+            ops.register_sorted_ids(inverse, inv_sorted, perm)
+        else:
+            inv_sorted, inverse, uniq, dest, send = _route_static_torch(sids, perm, W, cap)
+        if W == 1:
+            return LookupCtx(uniq, inverse, None, None, None, uniq, static=True, n=N)
+        recv = torch.empty(W * cap, dtype=torch.int64, device=self.device)
+        self.world.all_to_all(send, [cap] * W, recv, [cap] * W)
+        recv_local = torch.where(recv >= 0, recv // W, torch.full_like(recv, -1))
+        return LookupCtx(uniq, inverse, dest.long(), [cap] * W, [cap] * W, recv_local, static=True, n=cap)
 
     def lookup(self, ids: torch.Tensor):
         """rows [U, D] for the unique ids of `ids`, plus the routing context."""
@@ -188,14 +198,20 @@ def lookup_shared(tables, ctx: LookupCtx):
     _check_shared(tables)
     t0 = tables[0]
     if t0.W == 1:
-        return [t.local.index_select(0, ctx.uniq) for t in tables]
+        idx = ctx.uniq.clamp_min(0) if ctx.static else ctx.uniq     # padding slots read row 0, never used
+        return [t.local.index_select(0, idx) for t in tables]
     dims = [t.dim for t in tables]
-    served = torch.cat([t.local.index_select(0, ctx.recv_local) for t in tables], 1) if len(tables) > 1 else \
-        t0.local.index_select(0, ctx.recv_local)
-    got = torch.empty((ctx.uniq.numel(), sum(dims)), dtype=torch.float32, device=t0.device)
+    src = ctx.recv_local.clamp_min(0) if ctx.static else ctx.recv_local
+    served = torch.cat([t.local.index_select(0, src) for t in tables], 1) if len(tables) > 1 else \
+        t0.local.index_select(0, src)
+    got = torch.empty((sum(ctx.send), sum(dims)) if ctx.static else (ctx.uniq.numel(), sum(dims)),
+                      dtype=torch.float32, device=t0.device)
     t0.world.all_to_all(served.contiguous(), ctx.recv, got, ctx.send)
-    rows = torch.empty_like(got)
-    rows[ctx.order] = got
+    if ctx.static:
+        rows = got.index_select(0, ctx.order.clamp_min(0))          # slot of each unique id
+    else:
+        rows = torch.empty_like(got)
+        rows[ctx.order] = got
     return list(rows.split(dims, 1)) if len(tables) > 1 else [rows]
 
 
@@ -207,9 +223,49 @@ def apply_sgd_shared(tables, ctx: LookupCtx, grads, lrs):
     gs = [g.float().reshape(-1, t.dim) for t, g in zip(tables, grads)]
     if t0.W > 1:
         g = torch.cat(gs, 1) if len(gs) > 1 else gs[0]
-        g_sorted = g[ctx.order].contiguous()
+        if ctx.static:
+            valid = (ctx.order >= 0).unsqueeze(1).to(g.dtype)
+            g_sorted = torch.zeros((sum(ctx.send), g.shape[1]), dtype=torch.float32, device=t0.device)
+            g_sorted.index_add_(0, ctx.order.clamp_min(0), g * valid)   # padding adds 0
+        else:
+            g_sorted = g[ctx.order].contiguous()
         recv_g = torch.empty((sum(ctx.recv), g.shape[1]), dtype=torch.float32, device=t0.device)
         t0.world.all_to_all(g_sorted, ctx.send, recv_g, ctx.recv)
         gs = list(recv_g.split([t.dim for t in tables], 1))
     for t, g, lr in zip(tables, gs, lrs):
         t._sgd_local(ctx, g.contiguous(), lr)
+
+
+def _max_route_world() -> int:
+    try:
+        return ops._C().route_max_world()
+    except Exception:       # CPU-only build without the extension: the torch emulation has no limit
+        return 1 << 30
+
+
+def _route_static_torch(sids: torch.Tensor, perm: torch.Tensor, W: int, cap: int):
+    """CPU emulation of csrc/kernels/sparse_route.hip (same outputs)."""
+    N = sids.numel()
+    dev = sids.device
+    flag = torch.ones(N, dtype=torch.bool, device=dev)
+    flag[1:] = sids[1:] != sids[:-1]
+    inv_sorted = (torch.cumsum(flag.to(torch.int64), 0) - 1).to(torch.int32)
+    inverse = torch.empty(N, dtype=torch.int64, device=dev)
+    inverse[perm] = inv_sorted.long()
+    u = sids[flag].long()
+    U = u.numel()
+    uniq = torch.full((N,), -1, dtype=torch.int64, device=dev)
+    uniq[:U] = u
+    dest = torch.full((N,), -1, dtype=torch.int32, device=dev)
+    send = torch.full((W * cap,), -1, dtype=torch.int64, device=dev)
+    if W > 1 and U:
+        owner = u % W
+        counts = torch.bincount(owner, minlength=W)
+        start = torch.cumsum(counts, 0) - counts
+        order = torch.argsort(owner, stable=True)          # id order within each owner
+        pos = torch.empty(U, dtype=torch.int64, device=dev)
+        pos[order] = torch.arange(U, device=dev) - start[owner[order]]
+        d = owner * cap + pos
+        dest[:U] = d.to(torch.int32)
+        send[d] = u
+    return inv_sorted, inverse, uniq, dest, send

@@ -37,7 +37,9 @@ def synthetic_sparse_batches(n_batches, batch, num_features, nnz, seed, device):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--model", choices=["wide_deep", "sparse_lr", "bert_base", "resnet50"], default="wide_deep")
+    ap.add_argument("--model", choices=["wide_deep", "sparse_lr", "lr2", "bert_base", "resnet50"], default="wide_deep",
+                    help="lr2 = sparse_lr at the reference's product configuration (run_lr2.sh:55-61: "
+                         "F=1e9 features, batch 500, learning rate 1.0)")
     ap.add_argument("--seq", type=int, default=128)
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--no-shadow", action="store_true", help="cast fp32 weights per GEMM/conv (autocast) instead of bf16 shadows")
@@ -50,7 +52,16 @@ def main():
     ap.add_argument("--emb-dim", type=int, default=64)
     ap.add_argument("--nnz", type=int, default=32, help="features per sample")
     ap.add_argument("--gpus", type=int, default=None)
+    ap.add_argument("--lr", type=float, default=None, help="sparse models: SGD learning rate")
+    ap.add_argument("--trace-marker", action="store_true",
+                    help="launch a spin kernel right before the timed loop, so a kernel trace can be cut to the "
+                         "steady state (scripts/rocpd_summary.py --after spin)")
     a = ap.parse_args()
+    if a.model == "lr2":
+        a.features = a.features if a.features != 100_000_000 else 1_000_000_000
+        a.batch = a.batch or 500
+        a.lr = 1.0 if a.lr is None else a.lr
+        a.nnz = a.nnz if a.nnz != 32 else 40
 
     from distributed_tensorflow_example_amd.parallel import world as W
 
@@ -59,6 +70,10 @@ def main():
     if a.model in ("bert_base", "resnet50"):
         return dense_bench(a, w)
     a.batch = a.batch or 4096
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+        torch.cuda.reset_peak_memory_stats()
+    t_init = time.time()
     if a.model == "wide_deep":
         from distributed_tensorflow_example_amd.models.wide_deep import WideDeep
 
@@ -70,15 +85,23 @@ def main():
     else:
         from distributed_tensorflow_example_amd.models.sparse_lr import SparseLRTrainer
 
-        m = SparseLRTrainer(a.features, 0.1, w)
-        cfg = {"model": f"sparse_lr F={a.features}", "global_batch": a.batch * w.world_size, "per_gpu_batch": a.batch,
+        m = SparseLRTrainer(a.features, 0.1 if a.lr is None else a.lr, w)
+        cfg = {"model": f"{'lr2 ' if a.model == 'lr2' else ''}sparse_lr F={a.features}",
+               "global_batch": a.batch * w.world_size, "per_gpu_batch": a.batch, "lr": 0.1 if a.lr is None else a.lr,
                "seq_len": None, "parallelism": f"emb-shard{w.world_size}", "nnz_per_sample": a.nnz}
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    init_s = time.time() - t_init
+    init_mem = torch.cuda.max_memory_allocated() / 2 ** 30 if dev.type == "cuda" else None
     batches = synthetic_sparse_batches(16, a.batch, a.features, a.nnz, 1234 + w.rank, dev)
     for i in range(a.warmup):
         m.train_step(batches[i % len(batches)])
     w.barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize()
+        if a.trace_marker:
+            torch.cuda._sleep(1000)
+            torch.cuda.synchronize()
     t0 = time.time()
     for i in range(a.steps):
         loss = m.train_step(batches[i % len(batches)])
@@ -92,7 +115,10 @@ def main():
                           "unit": "samples/s", "n_gpus": w.world_size, "steps": a.steps, "warmup": a.warmup,
                           "ms_per_step": round(dt / a.steps * 1e3, 4), "higher_is_better": True,
                           "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic zipf ids",
-                          "config": cfg, "final_loss": float(loss)}), flush=True)
+                          "config": cfg, "final_loss": float(loss), "init_s": round(init_s, 3),
+                          "init_peak_mem_gib": None if init_mem is None else round(init_mem, 3),
+                          "peak_mem_gib": round(torch.cuda.max_memory_allocated() / 2 ** 30, 3)
+                          if dev.type == "cuda" else None}), flush=True)
     w.shutdown()
 
 

@@ -1,6 +1,10 @@
 """Per-kernel summary (CSV) of a rocprofv3 --kernel-trace database (rocpd SQLite).
 
-    python scripts/rocpd_summary.py gpurun_out/<dir>/<name>_results.db [out.csv]
+    python scripts/rocpd_summary.py gpurun_out/<dir>/<name>_results.db [out.csv] [--after NAME]
+
+--after NAME keeps only kernels that start after the last dispatch whose name
+contains NAME ends (e.g. the spin marker bench_models.py --trace-marker puts
+right before its timed loop: the steady state without initialisation).
 
 Columns: kernel name, calls, total_us, avg_us, pct, vgpr, sgpr, lds, scratch, grid.
 """
@@ -10,12 +14,24 @@ import sys
 
 
 def main():
-    db = sys.argv[1]
-    out = sys.argv[2] if len(sys.argv) > 2 else None
+    args = sys.argv[1:]
+    after = None
+    if "--after" in args:
+        i = args.index("--after")
+        after = args[i + 1]
+        args = args[:i] + args[i + 2:]
+    db = args[0]
+    out = args[1] if len(args) > 1 else None
     c = sqlite3.connect(db)
+    where = ""
+    if after:
+        t = c.execute("select max(end) from kernels where name like ?", (f"%{after}%",)).fetchone()[0]
+        if t is None:
+            raise SystemExit(f"no kernel matching {after!r}")
+        where = f"where start > {int(t)}"
     rows = c.execute(
         "select name, count(*), sum(duration), avg(duration), max(vgpr_count), max(sgpr_count), max(lds_size), "
-        "max(scratch_size), max(grid_x * grid_y * grid_z) from kernels group by name order by sum(duration) desc"
+        f"max(scratch_size), max(grid_x * grid_y * grid_z) from kernels {where} group by name order by sum(duration) desc"
     ).fetchall()
     tot = sum(r[2] for r in rows) or 1
     table = [["kernel", "calls", "total_us", "avg_us", "pct", "vgpr", "sgpr", "lds_bytes", "scratch", "grid_threads"]]

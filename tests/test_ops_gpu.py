@@ -324,3 +324,41 @@ def test_bf16_vocab_xent_with_bias(native, C):
     assert lg.grad.dtype == torch.bfloat16
     assert float((lg.grad.float().cpu() - lr_.grad).norm() / lr_.grad.norm()) < 1e-2
     assert float((bg.grad.cpu() - br.grad).norm() / br.grad.norm()) < 1e-2
+
+
+@pytest.mark.gpu
+def test_philox_normal_kernel_matches_cpu():
+    """csrc/kernels/random.hip against the numpy Philox4x32-10 + Box-Muller of
+    the same elements (fp32 transcendentals: a few ulp), incl. a strided shard."""
+    from distributed_tensorflow_example_amd import ops
+
+    for rows, dim, mul, add, seed in [(4097, 1, 1, 0, 123), (1000, 3, 4, 3, (1 << 40) + 5), (257, 64, 8, 1, 9)]:
+        g = ops.philox_normal_(torch.empty(rows, dim, device="cuda"), mul, add, seed, 0.25, 1.5).cpu()
+        c = ops.philox_normal_(torch.empty(rows, dim), mul, add, seed, 0.25, 1.5)
+        assert torch.allclose(g, c, rtol=2e-6, atol=2e-6), (g - c).abs().max()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("W", [1, 3, 8])
+def test_sparse_route_kernel_matches_torch(W):
+    """csrc/kernels/sparse_route.hip (one-workgroup dedup + owner bucketing)
+    against the torch emulation of the same outputs, Zipf ids incl. N < 1024
+    and N spanning many per-thread chunks."""
+    import numpy as np
+
+    from distributed_tensorflow_example_amd import ops
+    from distributed_tensorflow_example_amd.parallel.sharded_embedding import _route_static_torch
+
+    rng = np.random.default_rng(W)
+    for N in (1, 700, 20_000, 131_072):
+        ids = torch.from_numpy(((rng.zipf(1.1, N) - 1) % 1_000_000).astype(np.int64)).cuda()
+        sids, perm = torch.sort(ids.to(torch.int32))
+        cap = N + 17
+        got = ops._C().sparse_route(sids.contiguous(), perm, W, cap)
+        want = _route_static_torch(sids.cpu(), perm.cpu(), W, cap)
+        names = ["inv_sorted", "inverse", "uniq", "dest", "send"]
+        for name, g, w_ in zip(names, got[:5], want):
+            if W == 1 and name in ("dest", "send"):
+                continue
+            assert torch.equal(g.cpu(), w_.to(g.dtype)), (N, name)
+        assert int(got[5].item()) == int(torch.unique(ids).numel())

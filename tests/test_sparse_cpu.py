@@ -107,14 +107,16 @@ def _sharded_worker(rank, ws, port, q, files, steps, lr, kind="lr"):
 
         w = W.init(backend="gloo")
         data = libsvm.load_files(files, 2)
-        if kind == "wd":
+        cap = 200 * 64 if kind.endswith("-static") else None     # ids-per-batch bound: static routing
+        if kind.startswith("wd"):
             from distributed_tensorflow_example_amd.models.wide_deep import WideDeep
 
-            tr = WideDeep(3000, emb_dim=8, hidden=(16,), lr=lr, dense_opt="adam", dense_lr=0.01, world=w, seed=5)
+            tr = WideDeep(3000, emb_dim=8, hidden=(16,), lr=lr, dense_opt="adam", dense_lr=0.01, world=w, seed=5,
+                          ids_capacity=cap)
             tr.W = tr.emb
             tr.b = tr.layers[0]
         else:
-            tr = sparse_lr.SparseLRTrainer(3000, lr, w, seed=5)
+            tr = sparse_lr.SparseLRTrainer(3000, lr, w, seed=5, ids_capacity=cap)
         init_tab = tr.W.full_table().numpy().copy()
         B = 200
         for s in range(steps):
@@ -122,7 +124,7 @@ def _sharded_worker(rank, ws, port, q, files, steps, lr, kind="lr"):
             mine = rows[rank * B // ws:(rank + 1) * B // ws]
             tr.train_step(data.take(mine))
         final = tr.W.full_table().numpy().copy()
-        if kind == "wd":
+        if kind.startswith("wd"):
             q.put((rank, init_tab, final, tr.b.detach().numpy().copy(), tr.wide.full_table().numpy().copy()))
             return
         local, repl = tr.checkpoint_tensors()
@@ -225,3 +227,16 @@ def test_wide_deep_learns(svm_dir):
         for s in range(0, 2800, 200):
             losses.append(float(m.train_step(data.slice(s, s + 200))))
     assert np.mean(losses[-10:]) < np.mean(losses[:10]) - 0.02
+
+
+def test_static_routing_matches_dynamic(svm_dir):
+    """Device-resident routing (configured ids capacity: equal-split exchange,
+    -1 padding, no host read-back) trains exactly like the exact-count path,
+    for sparse LR and for Wide&Deep's shared wide+deep routing."""
+    d, tr, te = svm_dir
+    for kind in ("lr", "wd"):
+        dyn = _run(2, tr, 6, 0.5, kind)
+        sta = _run(2, tr, 6, 0.5, kind + "-static")
+        for a, b in zip(dyn, sta):
+            assert np.array_equal(a[1], b[1])                    # same init
+            assert np.allclose(a[2], b[2], atol=1e-6)            # same trained table

@@ -9,9 +9,10 @@
 
 extern "C" {
 int dtfk_route_max_world();
-hipError_t dtfk_sparse_route(const void* sids, int ids32, const int64_t* perm, int N, int W, int cap, int* inv_sorted,
-                             int64_t* inverse, int64_t* uniq, int* dest, int64_t* send, int* count,
-                             hipStream_t stream);
+hipError_t dtfk_route_flags(const void* sids, int ids32, int N, int W, int* flag, int* onehot, hipStream_t stream);
+hipError_t dtfk_route_scatter(const void* sids, int ids32, const int64_t* perm, const int* incl, const int* owncum,
+                              int N, int W, int cap, int* inv_sorted, int64_t* inverse, int64_t* uniq, int* dest,
+                              int64_t* send, int* count, hipStream_t stream);
 hipError_t dtfk_philox_normal(float* out, long long rows, int dim, long long row_mul, long long row_add,
                               unsigned long long seed, float mean, float stddev, hipStream_t stream);
 hipError_t dtfk_gemm(const void* A, int a_bf16, int lda, int transA, const void* B, int b_bf16, int ldb,
@@ -265,7 +266,8 @@ void philox_normal(at::Tensor out, int64_t row_mul, int64_t row_add, uint64_t se
      "philox_normal");
 }
 
-// Dedup + owner bucketing of sorted ids in one kernel (csrc/kernels/sparse_route.hip).
+// Dedup + owner bucketing of sorted ids (csrc/kernels/sparse_route.hip: flags,
+// rocPRIM scans, one scatter pass).
 std::vector<at::Tensor> sparse_route(at::Tensor sids, at::Tensor perm, int W, int64_t cap) {
   gpu(sids, "sids"); i64c(perm, "perm");
   if (!sids.is_contiguous() || (sids.scalar_type() != at::kInt && sids.scalar_type() != at::kLong))
@@ -278,12 +280,19 @@ std::vector<at::Tensor> sparse_route(at::Tensor sids, at::Tensor perm, int W, in
   at::Tensor inv = at::empty({N}, o32), inverse = at::empty({N}, o64), uniq = at::empty({N}, o64);
   at::Tensor dest = at::empty({W > 1 ? N : 0}, o32), send = at::empty({W > 1 ? (int64_t)W * cap : 0}, o64);
   at::Tensor count = at::empty({1}, o32);
-  ck(dtfk_sparse_route(sids.data_ptr(), sids.scalar_type() == at::kInt ? 1 : 0, perm.data_ptr<int64_t>(), (int)N, W,
-                       (int)cap,
-                       inv.data_ptr<int>(), inverse.data_ptr<int64_t>(), uniq.data_ptr<int64_t>(),
-                       W > 1 ? dest.data_ptr<int>() : nullptr, W > 1 ? send.data_ptr<int64_t>() : nullptr,
-                       count.data_ptr<int>(), cs()),
-     "sparse_route");
+  const int ids32 = sids.scalar_type() == at::kInt ? 1 : 0;
+  at::Tensor flag = at::empty({N}, o32);
+  at::Tensor onehot = at::empty({W > 1 ? N : 0, W}, o32);
+  ck(dtfk_route_flags(sids.data_ptr(), ids32, (int)N, W, flag.data_ptr<int>(), W > 1 ? onehot.data_ptr<int>() : nullptr,
+                      cs()),
+     "route_flags");
+  at::Tensor incl = at::cumsum(flag, 0, at::kInt);                 // dedup index + 1
+  at::Tensor owncum = W > 1 ? at::cumsum(onehot, 0, at::kInt) : onehot;   // position among the owner's ids + 1
+  ck(dtfk_route_scatter(sids.data_ptr(), ids32, perm.data_ptr<int64_t>(), incl.data_ptr<int>(),
+                        W > 1 ? owncum.data_ptr<int>() : nullptr, (int)N, W, (int)cap, inv.data_ptr<int>(),
+                        inverse.data_ptr<int64_t>(), uniq.data_ptr<int64_t>(), W > 1 ? dest.data_ptr<int>() : nullptr,
+                        W > 1 ? send.data_ptr<int64_t>() : nullptr, count.data_ptr<int>(), cs()),
+     "route_scatter");
   return {inv, inverse, uniq, dest, send, count};
 }
 

@@ -38,6 +38,7 @@ class SparseLRTrainer:
                                   name="weights/Variable", capacity=ids_capacity)
         self.b = torch.zeros(1, dtype=torch.float32, device=self.device, requires_grad=True)
         self.global_step = 0
+        self._graphed = None
         # streaming_auc's num_thresholds = auc_bins -> auc_bins + 1 histogram bins
         self.auc_pos = torch.zeros(auc_bins + 1, dtype=torch.int64, device=self.device)
         self.auc_neg = torch.zeros(auc_bins + 1, dtype=torch.int64, device=self.device)
@@ -49,6 +50,32 @@ class SparseLRTrainer:
         return out + self.b, labels, st
 
     def train_step(self, batch) -> torch.Tensor:
+        if self._graphed is not None:
+            labels, offsets, ids, vals = batch.to(self.device) if hasattr(batch, "to") else batch
+            loss = self._graphed(labels, offsets, ids, vals)
+            self.global_step += 1
+            return loss.detach()
+        return self._train_step(batch)
+
+    def enable_graph(self, on: bool = True):
+        """Replay each step as one captured hipGraph (GPU; needs the static
+        device-resident routing: one worker, or an ids capacity for W > 1)."""
+        from ..utils.graphs import GraphedStep
+
+        if not on:
+            self._graphed = None
+            return
+        if self.device.type != "cuda" or (self.world.world_size > 1 and self.W.capacity is None):
+            raise RuntimeError("graph capture needs a GPU and static routing (ids_capacity for W > 1)")
+
+        def step(labels, offsets, ids, vals):
+            gs = self.global_step
+            loss = self._train_step((labels, offsets, ids, vals))
+            self.global_step = gs          # counted by train_step, not by warmup/capture
+            return loss
+        self._graphed = GraphedStep(step, lambda: [self.W.local, self.b.data])
+
+    def _train_step(self, batch) -> torch.Tensor:
         logits, labels, st = self._forward(batch)
         loss = ops.sigmoid_xent(logits, labels)
         if self.b.grad is not None:

@@ -53,6 +53,7 @@ def main():
     ap.add_argument("--nnz", type=int, default=32, help="features per sample")
     ap.add_argument("--gpus", type=int, default=None)
     ap.add_argument("--lr", type=float, default=None, help="sparse models: SGD learning rate")
+    ap.add_argument("--graph", action="store_true", help="sparse_lr / lr2: replay each step as one captured hipGraph")
     ap.add_argument("--trace-marker", action="store_true",
                     help="launch a spin kernel right before the timed loop, so a kernel trace can be cut to the "
                          "steady state (scripts/rocpd_summary.py --after spin)")
@@ -85,10 +86,13 @@ def main():
     else:
         from distributed_tensorflow_example_amd.models.sparse_lr import SparseLRTrainer
 
-        m = SparseLRTrainer(a.features, 0.1 if a.lr is None else a.lr, w)
+        m = SparseLRTrainer(a.features, 0.1 if a.lr is None else a.lr, w, ids_capacity=a.batch * a.nnz)
+        if a.graph:
+            m.enable_graph()
         cfg = {"model": f"{'lr2 ' if a.model == 'lr2' else ''}sparse_lr F={a.features}",
                "global_batch": a.batch * w.world_size, "per_gpu_batch": a.batch, "lr": 0.1 if a.lr is None else a.lr,
-               "seq_len": None, "parallelism": f"emb-shard{w.world_size}", "nnz_per_sample": a.nnz}
+               "seq_len": None, "parallelism": f"emb-shard{w.world_size}", "nnz_per_sample": a.nnz,
+               "graph": bool(a.graph)}
     if dev.type == "cuda":
         torch.cuda.synchronize()
     init_s = time.time() - t_init

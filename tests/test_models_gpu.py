@@ -80,3 +80,35 @@ def test_mnist_example_single_worker_gpu(tmp_path):
         res = json.load(open(tmp_path / "r.json"))
         assert res["global_step"] == 300
         assert res["accuracy"] > 0.5, res
+
+
+def test_sparse_lr_graphed_step_matches_eager():
+    """The device-resident sparse LR step captured in one hipGraph
+    (utils/graphs.GraphedStep) trains like the launch-by-launch step:
+    capture warmups leave no trace, replays see the new batches."""
+    import numpy as np
+
+    from distributed_tensorflow_example_amd.models.sparse_lr import SparseLRTrainer
+    from distributed_tensorflow_example_amd.parallel import world as W
+
+    w = W.get_world() if W._WORLD is not None else W.init()
+    rng = np.random.default_rng(0)
+    B, nnz, F = 500, 40, 1_000_000
+    batches = []
+    for _ in range(6):
+        ids = torch.from_numpy(((rng.zipf(1.1, B * nnz) - 1) % F).astype(np.int64)).cuda()
+        offs = torch.arange(0, B * nnz + 1, nnz, dtype=torch.int64, device="cuda")
+        vals = torch.rand(B * nnz, device="cuda")
+        lab = (torch.rand(B, 1, device="cuda") < 0.3).float()
+        batches.append((lab, offs, ids, vals))
+    eager = SparseLRTrainer(F, 1.0, w, seed=3)
+    graphed = SparseLRTrainer(F, 1.0, w, seed=3)
+    graphed.enable_graph()
+    for i in range(12):
+        le = eager.train_step(batches[i % 6])
+        lg = graphed.train_step(batches[i % 6])
+        assert abs(float(le) - float(lg)) < 1e-5, i
+    assert graphed._graphed.captures == 1 and graphed._graphed.replays == 12
+    assert graphed.global_step == eager.global_step == 12
+    assert torch.allclose(eager.W.local, graphed.W.local, atol=1e-5)
+    assert torch.allclose(eager.b, graphed.b, atol=1e-6)

@@ -8,6 +8,8 @@
 #include <string>
 
 extern "C" {
+hipError_t dtfk_bucket_pack_bf16(const float* g, uint16_t* c, int64_t n, float scale, hipStream_t s);
+hipError_t dtfk_bucket_unpack_bf16(const uint16_t* c, float* g, int64_t n, float scale, hipStream_t s);
 int dtfk_route_max_world();
 hipError_t dtfk_route_flags(const void* sids, int ids32, int N, int W, int* flag, int* onehot, hipStream_t stream);
 hipError_t dtfk_route_scatter(const void* sids, int ids32, const int64_t* perm, const int* incl, const int* owncum,
@@ -296,7 +298,31 @@ std::vector<at::Tensor> sparse_route(at::Tensor sids, at::Tensor perm, int W, in
   return {inv, inverse, uniq, dest, send, count};
 }
 
+// DDP bucket <-> bf16 comm buffer with the 1/N scale folded in (csrc/kernels/ops.hip K16).
+void bucket_pack_bf16(at::Tensor g, at::Tensor c, double scale) {
+  f32c(g, "grad bucket"); gpu(c, "comm buffer");
+  if (c.scalar_type() != at::kBFloat16 || !c.is_contiguous() || c.numel() != g.numel())
+    throw std::runtime_error("bucket_pack_bf16: contiguous bf16 comm buffer of the bucket's size expected");
+  if ((reinterpret_cast<uintptr_t>(g.data_ptr()) & 15) || (reinterpret_cast<uintptr_t>(c.data_ptr()) & 15))
+    throw std::runtime_error("bucket_pack_bf16: 16-byte aligned buffers expected");
+  ck(dtfk_bucket_pack_bf16(g.data_ptr<float>(), reinterpret_cast<uint16_t*>(c.data_ptr()), g.numel(), (float)scale,
+                           cs()),
+     "bucket_pack_bf16");
+}
+void bucket_unpack_bf16(at::Tensor c, at::Tensor g, double scale) {
+  f32c(g, "grad bucket"); gpu(c, "comm buffer");
+  if (c.scalar_type() != at::kBFloat16 || !c.is_contiguous() || c.numel() != g.numel())
+    throw std::runtime_error("bucket_unpack_bf16: contiguous bf16 comm buffer of the bucket's size expected");
+  if ((reinterpret_cast<uintptr_t>(g.data_ptr()) & 15) || (reinterpret_cast<uintptr_t>(c.data_ptr()) & 15))
+    throw std::runtime_error("bucket_unpack_bf16: 16-byte aligned buffers expected");
+  ck(dtfk_bucket_unpack_bf16(reinterpret_cast<const uint16_t*>(c.data_ptr()), g.data_ptr<float>(), g.numel(),
+                             (float)scale, cs()),
+     "bucket_unpack_bf16");
+}
+
 void init_ops(py::module& m) {
+  m.def("bucket_pack_bf16", &bucket_pack_bf16);
+  m.def("bucket_unpack_bf16", &bucket_unpack_bf16);
   m.def("sparse_route", &sparse_route, py::arg("sids"), py::arg("perm"), py::arg("W"), py::arg("cap"));
   m.def("route_max_world", &dtfk_route_max_world);
   m.def("philox_normal", &philox_normal, py::arg("out"), py::arg("row_mul"), py::arg("row_add"), py::arg("seed"),

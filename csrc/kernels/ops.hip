@@ -2,6 +2,7 @@
 // and `.optim`:
 //   act_backward      dZ = dY * act'(.)                    (SigmoidGrad / ReluGrad ...)
 //   col_sum           db = sum_rows dZ                     (bias gradient, K2/K5)
+//   bucket_{pack,unpack}_bf16  DDP bucket <-> bf16 comm buffer, 1/N folded in (K16)
 //   softmax_xent      fused softmax cross-entropy fwd+bwd  (K6; stable or reference-naive)
 //   sigmoid_xent      fused sigmoid cross-entropy fwd+bwd  (K11, lr2.py:391)
 //   embedding_bag     CSR bag sum/mean with per-id weights (K10, embedding_lookup_sparse)
@@ -497,12 +498,63 @@ __global__ void multi_tensor_sumsq(const TensorRec* __restrict__ tab, const int2
 // ---------------------------------------------------------------- launchers
 using namespace dtfk::ops;
 
+namespace dtfk {
+namespace ops {
+// ---------------------------------------------------------------------------
+// DDP bucket <-> communication buffer (K16): one pass each way.
+//   pack:   comm_bf16[i] = bf16(scale * grad_f32[i])   (the 1/N average folded in)
+//   unpack: grad_f32[i]  = scale * f32(comm_bf16[i])
+// 8 elements per thread (two 16-byte fp32 loads -> one 16-byte bf16 store);
+// replaces cast + copy-back + mul_ (three full-bucket passes) around a bf16
+// all-reduce.  Round-to-nearest-even like the cast it replaces.
+__global__ void bucket_pack_bf16(const float* __restrict__ g, uint16_t* __restrict__ c, int64_t n, float scale) {
+  const int64_t n8 = n >> 3;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    const float4 a = reinterpret_cast<const float4*>(g)[2 * i];
+    const float4 b = reinterpret_cast<const float4*>(g)[2 * i + 1];
+    uint4 o;
+    o.x = pack2bf(a.x * scale, a.y * scale);
+    o.y = pack2bf(a.z * scale, a.w * scale);
+    o.z = pack2bf(b.x * scale, b.y * scale);
+    o.w = pack2bf(b.z * scale, b.w * scale);
+    reinterpret_cast<uint4*>(c)[i] = o;
+  }
+  for (int64_t i = (n8 << 3) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    c[i] = f2bf(g[i] * scale);
+}
+
+__global__ void bucket_unpack_bf16(const uint16_t* __restrict__ c, float* __restrict__ g, int64_t n, float scale) {
+  const int64_t n8 = n >> 3;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint4 u = reinterpret_cast<const uint4*>(c)[i];
+    float4 a, b;
+    a.x = bf2f(u.x & 0xFFFF) * scale; a.y = bf2f(u.x >> 16) * scale;
+    a.z = bf2f(u.y & 0xFFFF) * scale; a.w = bf2f(u.y >> 16) * scale;
+    b.x = bf2f(u.z & 0xFFFF) * scale; b.y = bf2f(u.z >> 16) * scale;
+    b.z = bf2f(u.w & 0xFFFF) * scale; b.w = bf2f(u.w >> 16) * scale;
+    reinterpret_cast<float4*>(g)[2 * i] = a;
+    reinterpret_cast<float4*>(g)[2 * i + 1] = b;
+  }
+  for (int64_t i = (n8 << 3) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    g[i] = bf2f(c[i]) * scale;
+}
+}  // namespace ops
+}  // namespace dtfk
+
 static int nblk(int64_t n, int per = 256, int cap = 4096) {
   int64_t b = (n + per - 1) / per;
   return (int)std::max<int64_t>(1, std::min<int64_t>(b, cap));
 }
 
 extern "C" {
+hipError_t dtfk_bucket_pack_bf16(const float* g, uint16_t* c, int64_t n, float scale, hipStream_t s) {
+  hipLaunchKernelGGL(bucket_pack_bf16, dim3(nblk((n + 7) / 8)), dim3(256), 0, s, g, c, n, scale);
+  return hipGetLastError();
+}
+hipError_t dtfk_bucket_unpack_bf16(const uint16_t* c, float* g, int64_t n, float scale, hipStream_t s) {
+  hipLaunchKernelGGL(bucket_unpack_bf16, dim3(nblk((n + 7) / 8)), dim3(256), 0, s, c, g, n, scale);
+  return hipGetLastError();
+}
 hipError_t dtfk_act_backward(const float* dy, const float* y, const float* z, float* dz, int64_t n,
                              int act, hipStream_t s) {
   hipLaunchKernelGGL(act_backward, dim3(nblk(n)), dim3(256), 0, s, dy, y, z, dz, n, act);

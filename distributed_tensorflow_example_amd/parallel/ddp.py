@@ -12,8 +12,9 @@ Design for MI355X / RCCL over xGMI:
 * a post-accumulate-grad hook counts ready parameters; the moment a bucket is
   complete its all-reduce is issued on a dedicated comm stream (RCCL) behind an
   event on the compute stream -- later buckets keep computing meanwhile;
-* optional bf16 communication (`comm_dtype=torch.bfloat16`): the bucket is
-  cast once, reduced in bf16 (half the xGMI bytes), cast back;
+* optional bf16 communication (`comm_dtype=torch.bfloat16`): one kernel packs
+  the bucket into a bf16 buffer with the 1/N average folded in, the all-reduce
+  runs in bf16 (half the xGMI bytes), one kernel unpacks (K16);
 * fused backward ops (BN, shadow-weight conv / GEMM) "sink" their weight
   gradients: they accumulate into the bucket view inside their own kernels
   and call the bucket-ready hook themselves (ops.grad_sink);
@@ -31,6 +32,7 @@ from typing import List, Optional
 import torch
 import torch.distributed as dist
 
+from .. import _native
 from ..ops import grad_sink
 from .world import World, get_world
 
@@ -110,6 +112,16 @@ class DistributedDataParallel(torch.nn.Module):
         self._launched = set()
         self._counted = set()
 
+    def close(self):
+        """Detach from the module: remove the gradient hooks (e.g. before
+        re-wrapping it with another bucket size)."""
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+        for p in self._param_bucket:
+            grad_sink.uninstall(p)
+            p.grad = None
+
     # ------------------------------------------------------------------ forward
     def reset_step(self):
         """Start a new iteration's readiness bookkeeping (forward() calls it)."""
@@ -151,14 +163,27 @@ class DistributedDataParallel(torch.nn.Module):
             ev.record(torch.cuda.current_stream())
             self.comm_stream.wait_event(ev)
             with torch.cuda.stream(self.comm_stream):
-                if self.comm_dtype is not None and self.comm_dtype != torch.float32:
+                scale = 1.0 / w.world_size if self.average else 1.0
+                if self.comm_dtype == torch.bfloat16:
+                    # K16: pack + cast + 1/N in one kernel, reduce in bf16 (half the
+                    # xGMI bytes), unpack in one kernel -- two passes instead of
+                    # cast, copy-back and mul_
+                    if b.comm_buf is None:
+                        b.comm_buf = torch.empty(b.buf.numel(), dtype=torch.bfloat16, device=b.buf.device)
+                    C = _native.load()
+                    C.bucket_pack_bf16(b.buf, b.comm_buf, scale)
+                    w.comm.all_reduce(b.comm_buf, "sum")
+                    C.bucket_unpack_bf16(b.comm_buf, b.buf, 1.0)
+                elif self.comm_dtype is not None and self.comm_dtype != torch.float32:
                     b.comm_buf = b.buf.to(self.comm_dtype)
                     w.comm.all_reduce(b.comm_buf, "sum")
                     b.buf.copy_(b.comm_buf)
+                    if self.average:
+                        b.buf.mul_(scale)
                 else:
                     w.comm.all_reduce(b.buf, "sum")
-                if self.average:
-                    b.buf.mul_(1.0 / w.world_size)
+                    if self.average:
+                        b.buf.mul_(scale)
             b.event = torch.cuda.Event()
             b.event.record(self.comm_stream)
         else:

@@ -42,6 +42,10 @@ def main():
                          "F=1e9 features, batch 500, learning rate 1.0)")
     ap.add_argument("--seq", type=int, default=128)
     ap.add_argument("--bucket-mb", type=float, default=32.0)
+    ap.add_argument("--bucket-sweep", default="",
+                    help="dense models: comma-separated bucket sizes in MB (e.g. 1,4,16,64) re-timed after the main "
+                         "run; ms/step per size lands in the JSON line (xGMI bucket sizing, SURVEY s5.8)")
+    ap.add_argument("--comm-bf16", action="store_true", help="dense models: bf16 gradient all-reduce (BASELINE #2)")
     ap.add_argument("--no-shadow", action="store_true", help="cast fp32 weights per GEMM/conv (autocast) instead of bf16 shadows")
     ap.add_argument("--conv-find", type=int, default=1,
                     help="ResNet: 1 = let MIOpen benchmark conv solvers (torch.backends.cudnn.benchmark)")
@@ -158,7 +162,8 @@ def dense_bench(a, w):
                "grad_allreduce": f"bucketed {a.bucket_mb}MB, overlapped", "input": "224x224 synthetic, channels_last",
                "conv_solver_search": bool(a.conv_find)}
         run = lambda m, b: m.loss(*b)
-    ddp = DistributedDataParallel(model, w, bucket_mb=a.bucket_mb)
+    comm_dtype = torch.bfloat16 if a.comm_bf16 else None
+    ddp = DistributedDataParallel(model, w, bucket_mb=a.bucket_mb, comm_dtype=comm_dtype)
     if not a.no_shadow:
         model.attach_shadows(opt)          # after the DDP broadcast: shadows match rank 0's weights
 
@@ -182,6 +187,22 @@ def dense_bench(a, w):
     w.barrier()
     dt = w.host_all_reduce(time.time() - t0, "max")
     v = per * w.world_size * a.steps / dt
+    sweep = {}
+    for mb in [float(x) for x in a.bucket_sweep.split(",") if x.strip()]:
+        ddp.close()
+        ddp = DistributedDataParallel(model, w, bucket_mb=mb, comm_dtype=comm_dtype, broadcast_params=False)
+        for i in range(3):
+            step(batches[i % len(batches)])
+        w.barrier()
+        torch.cuda.synchronize()
+        t1 = time.time()
+        n = max(1, a.steps // 2)
+        for i in range(n):
+            step(batches[i % len(batches)])
+        torch.cuda.synchronize()
+        w.barrier()
+        sweep[str(mb)] = {"ms_per_step": round(w.host_all_reduce(time.time() - t1, "max") / n * 1e3, 3),
+                          "buckets": len(ddp.buckets)}
     if w.rank == 0:
         out = {"metric": f"{a.model} {unit} (whole node)", "value": round(v, 2), "unit": unit,
                "n_gpus": w.world_size, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 3),
@@ -189,6 +210,9 @@ def dense_bench(a, w):
                "data": "synthetic", "config": cfg, "final_loss": float(loss)}
         if a.model == "bert_base":
             out["tokens_per_s"] = round(v * a.seq, 1)
+        if sweep:
+            out["bucket_sweep"] = sweep
+        out["config"]["grad_comm_dtype"] = "bf16" if a.comm_bf16 else "fp32"
         print(json.dumps(out), flush=True)
     w.shutdown()
 

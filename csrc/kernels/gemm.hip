@@ -1,4 +1,6 @@
-// Generic bf16-MFMA GEMM with a fused epilogue: C = act(alpha * op(A) op(B) + bias)
+// Generic MFMA GEMM with a fused epilogue: C = act(alpha * op(A) op(B) + bias).
+// bf16 (or mixed) operands: 16x16x32 bf16 MFMA below; fp32 x fp32 with an fp32
+// output: the exact-f32 MFMA kernel at the end (no silent bf16 rounding).
 //
 // Backs `ops.linear_act` (forward: bias + {none, relu, sigmoid, tanh, gelu}),
 // its backward GEMMs (dX = dZ W^T with transB, dW = X^T dZ with transA) and the
@@ -9,7 +11,7 @@
 // each wave 32x32 = 2x2 MFMA 16x16x32 bf16 tiles, K-step 32.  Operands are
 // read in any of fp32 / bf16 with any transpose, converted to bf16 and staged
 // in LDS as [row][k] (A) and [col][k] (B) with a +8 element pad so every MFMA
-// fragment is one conflict-free 16-byte ds_read.  Interior runs of 8 elements
+// fragment is one conflict-free 16-byte ds_read (bf16 path).  Interior runs of 8 elements
 // are one (bf16) or two (fp32) 16-byte loads; edge runs fall back to clamped,
 // masked scalar loads with no per-element branch (see mlp_step.hip for why),
 // and the next K-tile is prefetched into registers while the current one is
@@ -195,6 +197,130 @@ __global__ __launch_bounds__(256) void gemm_bias_act(
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// fp32 x fp32: exact-f32 MFMA path (v_mfma_f32_16x16x4_f32, one rounding per
+// product, fp32 accumulate) -- fp32 operands are never rounded to bf16.  Same
+// 64x64 tile / 2x2 waves / epilogue / split-K / XCD remap as the bf16 kernel;
+// BK = 16, operands staged in LDS as fp32 [row][k] with a stride of 20 floats
+// (16-byte rows for ds_write_b128; the 16 rows x 4 k of one fragment read land
+// on 64 distinct banks).  A fragment (lane l): A'[row l&15][k = 4s + (l>>4)].
+constexpr int FBK = 16, FLD = 20;
+
+template <bool KCONT>
+__device__ __forceinline__ void load_tile_f32(const float* base, int ld, int R, int K, int r0, int k0, float v[4]) {
+  // 64 x 16 tile, 256 threads x 4 elements; KCONT: 4 consecutive k of one row,
+  // else 4 consecutive rows of one k
+  const int t = threadIdx.x;
+  int outer, inner;
+  bool full;
+  if constexpr (KCONT) {
+    outer = r0 + (t >> 2); inner = k0 + (t & 3) * 4;
+    full = outer < R && inner + 4 <= K;
+  } else {
+    outer = k0 + (t >> 4); inner = r0 + (t & 15) * 4;
+    full = outer < K && inner + 4 <= R;
+  }
+  const size_t off = (size_t)outer * ld + inner;
+  if (full && ((reinterpret_cast<uintptr_t>(base + off) & 15) == 0)) {
+    const float4 a = *reinterpret_cast<const float4*>(base + off);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    return;
+  }
+  const int oc = min(outer, (KCONT ? R : K) - 1);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int ic = min(inner + j, (KCONT ? K : R) - 1);
+    const float x = base[(size_t)oc * ld + ic];
+    v[j] = (outer < (KCONT ? R : K) && inner + j < (KCONT ? K : R)) ? x : 0.f;
+  }
+}
+
+template <bool KCONT>
+__device__ __forceinline__ void store_tile_f32(float* s, const float v[4]) {
+  const int t = threadIdx.x;
+  if constexpr (KCONT) {
+    *reinterpret_cast<float4*>(&s[(t >> 2) * FLD + (t & 3) * 4]) = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+    const int k = t >> 4, r4 = (t & 15) * 4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s[(r4 + j) * FLD + k] = v[j];
+  }
+}
+
+template <bool TA, bool TB>
+__global__ __launch_bounds__(256) void gemm_f32_bias_act(
+    const float* __restrict__ A, int lda, const float* __restrict__ Bm, int ldb, float* __restrict__ C, int ldc,
+    float* __restrict__ Zout, const float* __restrict__ bias, int M, int N, int K, float alpha, float beta, int act,
+    int kchunk) {
+  __shared__ __attribute__((aligned(16))) float As[BM * FLD];
+  __shared__ __attribute__((aligned(16))) float Bs[BN * FLD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, lh = lane >> 4;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int nt_n = (N + BN - 1) / BN;
+  const int nwg = gridDim.x;
+  const int orig = blockIdx.x;
+  const int xcd = orig % 8, q = nwg / 8, rem = nwg % 8;
+  const int wg = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + orig / 8;
+  const int m0 = (wg / nt_n) * BM, n0 = (wg % nt_n) * BN;
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int kb = blockIdx.y * kchunk, ke = min(K, kb + kchunk);
+  float va[4], vb[4];
+  load_tile_f32<!TA>(A, lda, M, ke, m0, kb, va);
+  load_tile_f32<TB>(Bm, ldb, N, ke, n0, kb, vb);
+  for (int k0 = kb; k0 < ke; k0 += FBK) {
+    __syncthreads();
+    store_tile_f32<!TA>(As, va);
+    store_tile_f32<TB>(Bs, vb);
+    __syncthreads();
+    if (k0 + FBK < ke) {
+      load_tile_f32<!TA>(A, lda, M, ke, m0, k0 + FBK, va);
+      load_tile_f32<TB>(Bm, ldb, N, ke, n0, k0 + FBK, vb);
+    }
+#pragma unroll
+    for (int s = 0; s < FBK / 4; ++s) {
+      float fa[2], fb[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fa[i] = As[(wr * 32 + i * 16 + lr) * FLD + 4 * s + lh];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fb[j] = Bs[(wc * 32 + j * 16 + lr) * FLD + 4 * s + lh];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = n0 + wc * 32 + j * 16 + lr;
+    const float bv = (bias != nullptr && n < N) ? bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wr * 32 + i * 16 + 4 * lh + r;
+        if (m < M && n < N) {
+          if (gridDim.y > 1) {
+            atomicAdd(C + (size_t)m * ldc + n, alpha * acc[i][j][r] + (blockIdx.y == 0 ? bv : 0.f));
+            continue;
+          }
+          float z = alpha * acc[i][j][r] + bv;
+          const size_t o = (size_t)m * ldc + n;
+          if (beta != 0.f) z += beta * C[o];
+          if (Zout != nullptr) Zout[o] = z;
+          C[o] = apply_act(z, act);
+        }
+      }
+    }
+  }
+}
 }  // namespace gemm
 }  // namespace dtfk
 
@@ -223,6 +349,23 @@ extern "C" hipError_t dtfk_gemm(const void* A, int a_bf16, int lda, int transA, 
     if (e != hipSuccess) return e;
   }
   const dim3 grid(tiles, split), block(256);
+  if (!a_bf16 && !b_bf16 && !c_bf16) {
+    // fp32 operands stay fp32 (exact-f32 MFMA); split-K chunks on the fp32 K-step
+    if (split > 1) kchunk = (kchunk + FBK - 1) / FBK * FBK;
+    const float* Af = static_cast<const float*>(A);
+    const float* Bf = static_cast<const float*>(B);
+    float* Cf = static_cast<float*>(C);
+#define DTFK_F(TA, TB) \
+  hipLaunchKernelGGL((gemm_f32_bias_act<TA, TB>), grid, block, 0, stream, Af, lda, Bf, ldb, Cf, ldc, Z, bias, M, N, \
+                     K, alpha, beta, act, kchunk)
+    if (transA) {
+      if (transB) DTFK_F(true, true); else DTFK_F(true, false);
+    } else {
+      if (transB) DTFK_F(false, true); else DTFK_F(false, false);
+    }
+#undef DTFK_F
+    return hipGetLastError();
+  }
 #define DTFK_G(AB, BB, TA, TB, OB)                                                               \
   hipLaunchKernelGGL((gemm_bias_act<AB, BB, TA, TB, OB>), grid, block, 0, stream, A, lda, B, ldb, \
                      C, ldc, Z, bias, M, N, K, alpha, beta, act, kchunk)

@@ -423,6 +423,12 @@ __device__ __forceinline__ uint16_t* ipc_slot(const IpcArgs& a, int r) {
 // second asm barrier so no slot load is hoisted above the flag match; its slot
 // loads are non-temporal loads of uncached memory (the guide's sc1-load form
 // of the acquire, MI355X_MICROARCH.md "Valid forms").
+// Publication order: the slot buffers are hipDeviceMallocUncached (ipc_peer.cpp),
+// so a gradient store's vmcnt completes only once the write has reached memory;
+// the waitcnt below (an asm with a "memory" clobber, so also a compiler barrier)
+// retires every slot store before the flag store issues, and peers read the
+// slots with system-scope loads after seeing the flag.  A release store would
+// add an L2 writeback (buffer_wbl2) that uncached data does not need.
 __device__ __forceinline__ bool ipc_wg_sync(const IpcArgs& a, int wg, unsigned long long epoch, int lane) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const long long off = IPC_WG_FLAG0 + 8LL * wg;

@@ -41,7 +41,8 @@ def _act_cpu(z, act):
 # --------------------------------------------------------------------------- GEMM
 def matmul(a: torch.Tensor, b: torch.Tensor, trans_a: bool = False, trans_b: bool = False,
            bias=None, act="none", out_dtype=None) -> torch.Tensor:
-    """act(op(a) @ op(b) + bias) on the bf16 MFMA GEMM (no autograd)."""
+    """act(op(a) @ op(b) + bias) on the MFMA GEMM (no autograd): fp32 operands on
+    the exact-f32 MFMA kernel, bf16 / mixed operands on the bf16 one."""
     if not a.is_cuda:
         A = a.t() if trans_a else a
         Bm = b.t() if trans_b else b

@@ -379,3 +379,26 @@ def test_bucket_pack_unpack_bf16():
         out = torch.empty(n, device="cuda")
         C.bucket_unpack_bf16(c, out, 2.0)
         assert torch.equal(out, c.float() * 2.0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ta,tb", [(False, False), (True, False), (False, True), (True, True)])
+def test_gemm_fp32_operands_are_exact_f32(ta, tb):
+    """fp32 x fp32 goes through the exact-f32 MFMA path (no bf16 rounding):
+    relative error at fp32 summation level vs fp64, incl. ragged edges, bias +
+    activation epilogue and the split-K (atomic) path."""
+    from distributed_tensorflow_example_amd import ops
+
+    g = torch.Generator(device="cpu").manual_seed(3)
+    for M, N, K, act in [(37, 53, 29, "sigmoid"), (128, 64, 784, "none"), (100, 10, 100, "relu"), (64, 32, 4096, "none")]:
+        a = torch.randn((K, M) if ta else (M, K), generator=g)
+        b = torch.randn((N, K) if tb else (K, N), generator=g)
+        bias = torch.randn(N, generator=g)
+        got = ops.matmul(a.cuda(), b.cuda(), ta, tb, bias.cuda(), act).cpu().double()
+        A = (a.t() if ta else a).double()
+        Bm = (b.t() if tb else b).double()
+        z = A @ Bm + bias.double()
+        want = {"none": z, "relu": torch.relu(z), "sigmoid": torch.sigmoid(z)}[act]
+        scale = (A.abs() @ Bm.abs()).max() + bias.abs().max()
+        err = (got - want).abs().max() / scale
+        assert err < 2e-6, (M, N, K, act, float(err))        # bf16 rounding would be ~4e-3

@@ -434,7 +434,8 @@ __device__ __forceinline__ float ld_grad(const void* g, int64_t i, int gbf) {
   return gbf ? bf2f(reinterpret_cast<const uint16_t*>(g)[i]) : reinterpret_cast<const float*>(g)[i];
 }
 
-// kind 0: sgd, 1: momentum (use_nesterov in flags bit0), 2: adam (TF), 3: adamw
+// kind 0: sgd, 1: momentum (use_nesterov in flags bit0), 2: adam (TF), 3: adamw,
+// 4: adagrad (TF; m = accumulator), 5: rmsprop (TF; m = mean square, v = momentum, b1 = decay)
 __global__ void multi_tensor_apply(const TensorRec* __restrict__ tab, const int2* __restrict__ chunks,
                                    int nchunks, int kind, int gbf, const float* __restrict__ lr_ptr,
                                    float lr_scalar, float gscale, float wd, float b1, float b2, float eps,
@@ -445,7 +446,7 @@ __global__ void multi_tensor_apply(const TensorRec* __restrict__ tab, const int2
   const TensorRec t = tab[ch.x];
   const float lr = lr_ptr ? *lr_ptr : lr_scalar;
   float lr_t = lr;
-  if (kind >= 2) {
+  if (kind == 2 || kind == 3) {
     const double st = (double)(step_ptr ? *step_ptr : 1);
     // TF AdamOptimizer: lr_t = lr * sqrt(1 - b2^t) / (1 - b1^t), eps outside the sqrt
     lr_t = (float)(lr * sqrt(1.0 - pow((double)b2, st)) / (1.0 - pow((double)b1, st)));
@@ -462,6 +463,18 @@ __global__ void multi_tensor_apply(const TensorRec* __restrict__ tab, const int2
       const float mv = momentum * t.m[i] + g;
       t.m[i] = mv;
       p -= lr * (nesterov ? g + momentum * mv : mv);
+    } else if (kind == 4) {
+      // TF ApplyAdagrad: accum += g^2; var -= lr * g / sqrt(accum)
+      const float acc = t.m[i] + g * g;
+      t.m[i] = acc;
+      p -= lr * g / sqrtf(acc);
+    } else if (kind == 5) {
+      // TF ApplyRMSProp: ms = rho ms + (1 - rho) g^2; mom = mu mom + lr g / sqrt(ms + eps); var -= mom
+      const float ms = b1 * t.m[i] + (1.f - b1) * g * g;
+      const float mo = momentum * t.v[i] + lr * g / sqrtf(ms + eps);
+      t.m[i] = ms;
+      t.v[i] = mo;
+      p -= mo;
     } else {
       if (kind == 2 && wd != 0.f) g += wd * p;
       const float mv = b1 * t.m[i] + (1.f - b1) * g;

@@ -327,6 +327,8 @@ def _lower(g, with_saver: bool = True):
         """`name/Initializer/...` subgraph feeding `name/Assign`, as
         get_variable builds it (random_normal / zeros-or-constant Fill)."""
         spec = getattr(getattr(v, "_init_value", None), "_init_spec", None) or getattr(v, "_spec", None)
+        if spec is None and isinstance(getattr(v, "init", None), float):      # optimizer slots
+            spec = ("const", v.init, 0, 0)
         pre = name + "/Initializer"
         if spec and spec[0] == "normal":
             kind, mean, std, seed = spec

@@ -409,25 +409,30 @@ class Optimizer:
             for sname, tens in zip(self._slot_names, (fused.m[i], fused.v[i])):
                 if tens is None:
                     continue
-                sv = _SlotVariable(f"{base}/{sname}", tens)
+                sv = _SlotVariable(f"{base}/{sname}", tens, self._slot_init(sname))
                 g.add_to_collection(GLOBAL_VARIABLES, sv)
 
     def get_slot_names(self):
         return list(self._slot_names)
 
+    def _slot_init(self, sname: str) -> float:
+        """Initial value TF gives the slot (zeros unless the optimizer says otherwise)."""
+        return 0.0
+
 
 class _SlotVariable:
     op_type, attrs = "VariableV2", {}       # a VariableV2 node in the exported GraphDef
 
-    def __init__(self, name, tensor):
+    def __init__(self, name, tensor, init: float = 0.0):
         self.name = name + ":0"
         self.value = tensor
+        self.init = float(init)
         self.initialized = True
         self.trainable = False
 
     def _initialize(self):
         with torch.no_grad():
-            self.value.zero_()
+            self.value.fill_(self.init)
 
 
 class GradientDescentOptimizer(Optimizer):
@@ -500,7 +505,10 @@ class AdagradOptimizer(Optimizer):
         self.init_acc = initial_accumulator_value
 
     def _make_fused(self, params):
-        return _TorchOpt(params, self._lr_value(), "adagrad", init_acc=self.init_acc)
+        return _optim.FusedAdagrad(params, self._lr_value(), self.init_acc)
+
+    def _slot_init(self, sname: str) -> float:
+        return float(self.init_acc)
 
 
 class RMSPropOptimizer(Optimizer):
@@ -510,37 +518,15 @@ class RMSPropOptimizer(Optimizer):
     def __init__(self, learning_rate, decay=0.9, momentum=0.0, epsilon=1e-10, use_locking=False,
                  centered=False, name="RMSProp"):
         super().__init__(learning_rate, use_locking, name)
+        if centered:
+            raise NotImplementedError("RMSPropOptimizer(centered=True) is not supported")
         self.decay, self.mom, self.eps = decay, momentum, epsilon
 
     def _make_fused(self, params):
-        return _TorchOpt(params, self._lr_value(), "rmsprop", decay=self.decay, mom=self.mom, eps=self.eps)
+        return _optim.FusedRMSProp(params, self._lr_value(), self.decay, self.mom, self.eps)
 
-
-class _TorchOpt:
-    """Less common TF optimizers, expressed with PyTorch ops (any device)."""
-
-    def __init__(self, params, lr, kind, init_acc=0.1, decay=0.9, mom=0.0, eps=1e-10):
-        self.params, self.kind = params, kind
-        self.lr_v = lr
-        self.m = [torch.full_like(p, init_acc) if kind == "adagrad" else torch.ones_like(p) for p in params]
-        self.v = [torch.zeros_like(p) for p in params]
-        self.decay, self.mom, self.eps = decay, mom, eps
-        self.step_t = torch.zeros(1, dtype=torch.int64)
-
-    def set_lr(self, lr):
-        self.lr_v = lr
-
-    @torch.no_grad()
-    def step(self, grads):
-        self.step_t += 1
-        for p, g, m, v in zip(self.params, grads, self.m, self.v):
-            if self.kind == "adagrad":
-                m.add_(g * g)
-                p.sub_(self.lr_v * g / m.sqrt())
-            else:
-                m.mul_(self.decay).add_((1 - self.decay) * g * g)
-                v.mul_(self.mom).add_(self.lr_v * g / (m + self.eps).sqrt())
-                p.sub_(v)
+    def _slot_init(self, sname: str) -> float:
+        return 1.0 if sname == "RMSProp" else 0.0      # TF initialises the mean square to ones
 
 
 class SyncReplicasOptimizer(Optimizer):

@@ -12,6 +12,9 @@ Semantics follow TensorFlow where the reference uses it:
   Adam (TF)        lr_t = lr*sqrt(1-b2^t)/(1-b1^t); p -= lr_t*m/(sqrt(v)+eps)
                    (epsilon outside the sqrt, "epsilon hat"; model_export.py:38)
   AdamW            decoupled weight decay (BERT recipe)
+  Adagrad (TF)     acc += g^2; p -= lr*g/sqrt(acc)      (acc starts at 0.1)
+  RMSProp (TF)     ms = rho*ms + (1-rho)*g^2; mom = mu*mom + lr*g/sqrt(ms+eps); p -= mom
+                   (ms starts at 1, as TF's RMSPropOptimizer initialises it)
 `grad_scale` folds the 1/N of a summed all-reduce into the update.
 CPU tensors use the same math in PyTorch (CPU/gloo configuration).
 """
@@ -23,7 +26,7 @@ import torch
 
 from .. import _native
 
-KINDS = {"sgd": 0, "momentum": 1, "adam": 2, "adamw": 3}
+KINDS = {"sgd": 0, "momentum": 1, "adam": 2, "adamw": 3, "adagrad": 4, "rmsprop": 5}
 
 
 def _dense(t: torch.Tensor) -> bool:
@@ -51,9 +54,10 @@ class _FusedBase:
         self.momentum, self.nesterov = momentum, nesterov
         self.lr_t = torch.tensor([float(lr)], dtype=torch.float32, device=self.device)
         self.step_t = torch.zeros(1, dtype=torch.int64, device=self.device)
-        need_m = self.kind in ("momentum", "adam", "adamw")
-        need_v = self.kind in ("adam", "adamw")
-        self.m = [torch.zeros_like(p, dtype=torch.float32) if need_m else None for p in self.params]
+        need_m = self.kind in ("momentum", "adam", "adamw", "adagrad", "rmsprop")
+        need_v = self.kind in ("adam", "adamw", "rmsprop")
+        m0 = {"adagrad": self._init_acc(), "rmsprop": 1.0}.get(self.kind, 0.0)
+        self.m = [torch.full_like(p, m0, dtype=torch.float32) if need_m else None for p in self.params]
         self.v = [torch.zeros_like(p, dtype=torch.float32) if need_v else None for p in self.params]
         self._tab_key = None
         self._tab = None
@@ -69,6 +73,9 @@ class _FusedBase:
         with torch.no_grad():
             shadow.copy_(param)
         self._tab_key = None
+
+    def _init_acc(self) -> float:
+        return 0.0
 
     # ------------------------------------------------------------------ state
     @property
@@ -168,6 +175,15 @@ class _FusedBase:
                 m = self.m[i]
                 m.mul_(self.momentum).add_(g)
                 p.sub_(lr * (g + self.momentum * m if self.nesterov else m))
+            elif self.kind == "adagrad":
+                m = self.m[i]
+                m.add_(g * g)
+                p.sub_(lr * g / m.sqrt())
+            elif self.kind == "rmsprop":
+                m, v = self.m[i], self.v[i]
+                m.mul_(self.b1).add_((1 - self.b1) * g * g)
+                v.mul_(self.momentum).add_(lr * g / (m + self.eps).sqrt())
+                p.sub_(v)
             else:
                 if self.kind == "adam" and self.wd:
                     g = g + self.wd * p
@@ -209,6 +225,28 @@ class FusedAdamW(_FusedBase):
 
     def __init__(self, params, lr=1e-4, beta1=0.9, beta2=0.999, eps=1e-6, weight_decay=0.01):
         super().__init__(params, lr, weight_decay=weight_decay, beta1=beta1, beta2=beta2, eps=eps)
+
+
+class FusedAdagrad(_FusedBase):
+    """TF AdagradOptimizer (initial_accumulator_value 0.1)."""
+
+    kind = "adagrad"
+
+    def __init__(self, params, lr, initial_accumulator_value=0.1):
+        self._acc0 = float(initial_accumulator_value)
+        super().__init__(params, lr)
+
+    def _init_acc(self) -> float:
+        return self._acc0
+
+
+class FusedRMSProp(_FusedBase):
+    """TF RMSPropOptimizer (decay 0.9, momentum 0, epsilon 1e-10; ms slot starts at 1)."""
+
+    kind = "rmsprop"
+
+    def __init__(self, params, lr, decay=0.9, momentum=0.0, epsilon=1e-10):
+        super().__init__(params, lr, beta1=decay, eps=epsilon, momentum=momentum)
 
 
 def global_grad_norm(grads: List[torch.Tensor]) -> torch.Tensor:

@@ -388,3 +388,36 @@ def test_gfile_fake_hdfs(tmp_path, monkeypatch):
         assert [l for l in f] == ["1 3:1\n", "0 4:1\n"]
     assert gfile.Glob("hdfs://nn:9000/data/train/part-*") == ["hdfs://nn:9000/data/train/part-0"]
     assert tf.gfile.ListDirectory("hdfs://nn:9000/data/train") == ["part-0"]
+
+
+def test_adagrad_rmsprop_tf_semantics():
+    """Fused Adagrad / RMSProp follow TF's ApplyAdagrad / ApplyRMSProp (accumulator
+    0.1, mean-square slot initialised to 1), slots named like TF's."""
+    import distributed_tensorflow_example_amd.compat as tf
+
+    for kind in ("adagrad", "rmsprop"):
+        tf.reset_default_graph()
+        w = tf.Variable(tf.constant([1.0, -2.0, 3.0]), name="w")
+        x = tf.placeholder(tf.float32, [3])
+        loss = tf.reduce_sum(w * w * x)
+        opt = tf.train.AdagradOptimizer(0.1) if kind == "adagrad" else tf.train.RMSPropOptimizer(0.01, 0.9, 0.5)
+        train = opt.minimize(loss)
+        names = [v.name for v in tf.global_variables()]
+        assert ("w/Adagrad:0" in names) if kind == "adagrad" else ({"w/RMSProp:0", "w/Momentum:0"} <= set(names))
+        wv = np.array([1.0, -2.0, 3.0])
+        acc, ms, mom = np.full(3, 0.1), np.ones(3), np.zeros(3)
+        xs = np.array([0.5, 1.0, 2.0], np.float32)
+        with tf.Session() as sess:
+            sess.run(tf.global_variables_initializer())
+            for _ in range(3):
+                sess.run(train, feed_dict={x: xs})
+                g = 2 * wv * xs
+                if kind == "adagrad":
+                    acc = acc + g * g
+                    wv = wv - 0.1 * g / np.sqrt(acc)
+                else:
+                    ms = 0.9 * ms + 0.1 * g * g
+                    mom = 0.5 * mom + 0.01 * g / np.sqrt(ms + 1e-10)
+                    wv = wv - mom
+            assert np.allclose(sess.run(w), wv, rtol=1e-5, atol=1e-6)
+    tf.reset_default_graph()

@@ -403,3 +403,24 @@ def test_gemm_fp32_operands_are_exact_f32(ta, tb):
         scale = (A.abs() @ Bm.abs()).max() + bias.abs().max()
         err = (got - want).abs().max() / scale
         assert err < 2e-6, (M, N, K, act, float(err))        # bf16 rounding would be ~4e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["adagrad", "rmsprop"])
+def test_fused_adagrad_rmsprop_match_cpu(kind):
+    """multi_tensor_apply kinds 4/5 against the CPU math of the same optimizer."""
+    from distributed_tensorflow_example_amd import optim
+
+    torch.manual_seed(0)
+    ps = [torch.randn(1000), torch.randn(37, 5)]
+    gs = [[torch.randn_like(p) for p in ps] for _ in range(3)]
+    mk = (lambda q: optim.FusedAdagrad(q, 0.05)) if kind == "adagrad" else \
+        (lambda q: optim.FusedRMSProp(q, 0.01, 0.9, 0.5, 1e-10))
+    pc = [p.clone() for p in ps]
+    pg = [p.clone().cuda() for p in ps]
+    oc, og = mk(pc), mk(pg)
+    for step in gs:
+        oc.step([g.clone() for g in step])
+        og.step([g.clone().cuda() for g in step])
+    for a, b in zip(pc, pg):
+        assert torch.allclose(a, b.cpu(), rtol=1e-5, atol=1e-6)

@@ -113,15 +113,17 @@ def main(argv=None):
     can_persist = a.batch <= 112 and a.engine != "launches"
 
     def setup(mode):
-        """mode: 'persistent' (one launch per chunk, in-kernel N-GPU exchange) or the
-        3-launch path's gradient exchange ('ipc-fused' / 'ipc-apply' / 'rccl')."""
+        """mode: 'persistent' / 'persistent-2shot' (one launch per chunk, in-kernel
+        N-GPU exchange: one-shot or reduce-scatter + all-gather) or the 3-launch
+        path's gradient exchange ('ipc-fused' / 'ipc-apply' / 'rccl')."""
         trainer = FusedMLPTrainer(batch_size=a.batch, lr=a.lr, act=a.act, world=w, grad_dtype=gd,
-                                  device=dev, allreduce="rccl" if mode == "persistent" else mode,
+                                  device=dev, allreduce="rccl" if mode.startswith("persistent") else mode,
                                   ipc_timeout_s=a.exchange_timeout)
-        if mode == "persistent":
+        if mode.startswith("persistent"):
             runner = PersistentMLPRunner(trainer, epoch, steps_per_launch=a.steps_per_launch,
                                          timeout_s=a.exchange_timeout, precision=a.precision,
-                                         grad_bf16=a.grad_dtype == "bf16")
+                                         grad_bf16=a.grad_dtype == "bf16",
+                                         exchange="two-shot" if mode == "persistent-2shot" else "one-shot")
             runner.prepare(max(a.warmup, 1))
             torch.cuda.synchronize()
             w.barrier()   # every rank's buffers mapped and first chunk staged before any exchange
@@ -161,7 +163,8 @@ def main(argv=None):
         chain = {"auto": ["ipc-fused", "ipc-apply", "rccl"], "ipc-fused": ["ipc-fused"],
                  "ipc-apply": ["ipc-apply"], "rccl": ["rccl"]}[a.allreduce]
         if can_persist and a.allreduce == "auto":
-            chain = ["persistent"] + chain
+            # both in-kernel exchanges are timed (the fabric decides which wins)
+            chain = ["persistent"] + (["persistent-2shot"] if a.precision == "fp32" else []) + chain
     # N > 1: the first two valid candidates are timed briefly (outside the timed
     # region) and the faster one is kept -- the in-kernel exchange's per-CU peer
     # reads vs the 3-launch path's exchange spread over 347 workgroups depends on
@@ -177,7 +180,7 @@ def main(argv=None):
             continue
         if consistent(trainer, runner):
             picked.append((mode, trainer, runner))
-            if w.world_size == 1 or len(picked) == 2 or a.tune_steps <= 0:
+            if w.world_size == 1 or len(picked) == 3 or a.tune_steps <= 0:
                 break
             continue
         fallbacks[mode] = "failed validation (exchange timeout or replica drift after warmup)"

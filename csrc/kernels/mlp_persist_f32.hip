@@ -98,10 +98,13 @@ constexpr long long XBUF_BYTES = HDR_OFF + 64 * 8;
 // IPC buffer of one rank (N GPUs): [flags: workgroup c at byte 64c][2 parities][49 slots]
 // slot: 7 dW1 tiles x 64 lanes x 16 B (fp32; bf16 payload uses the first 8 B of
 // each 16) | dW2 64 lanes x 16 B | db1 (16) db2 (16) fp32
+// Two-shot mode adds a reduced area of the same slot layout (fp32 sums) behind
+// the slots, and a second flag per workgroup at byte 64c + 8.
 constexpr int IPC_FLAGS = 4096;
 constexpr int IPC_SMALL = 8 * NTW * 64 * 16;
 constexpr int IPC_SLOT = IPC_SMALL + 1024 + 128;
-constexpr long long IPC_BYTES = IPC_FLAGS + 2LL * NCOMP * IPC_SLOT;
+constexpr long long IPC_RED = IPC_FLAGS + 2LL * NCOMP * IPC_SLOT;
+constexpr long long IPC_BYTES = IPC_RED + 2LL * NCOMP * IPC_SLOT;
 
 // LDS carve (compute); the copier reuses the same dynamic allocation
 constexpr int LS = BROWS + 4;                          // [16][LS] fp32 images (float4-aligned rows)
@@ -147,6 +150,8 @@ struct Args {
   long long* phase_ts;      // optional phase stamps: [step < 64][workgroup 64][16] (wave 0 / wave 7, lane 0)
   int gmode;                // gather: 0 probe one granule per producer, then load; 1-3 direct loads with
                             // no / short / long s_sleep between passes (DTF_GATHER_MODE, tuning)
+  int xmode;                // N GPUs: 0 one-shot (every workgroup reads its slot from every peer),
+                            // 1 two-shot (reduce-scatter by wave chunk, then all-gather of the sums)
 };
 
 // phase stamp ph of step st (s_memrealtime, 100 MHz) -- profiling only
@@ -626,71 +631,132 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave: its slot stores landed
       lds_barrier();
+      char* flags = static_cast<char*>(a.peer_base[a.rank]);
+      // wave 0 waits until every peer's flag word `fo` of this workgroup reached `tag`
+      auto wait_peers = [&](int fo) {
+        if (w == 0) {
+          const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+          for (;;) {
+            bool ok = true;
+            if (lane < a.W && lane != a.rank) {
+              const unsigned v = __hip_atomic_load(
+                  reinterpret_cast<const unsigned*>(static_cast<const char*>(a.peer_base[lane]) + 64 * c + fo),
+                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              ok = (int)(v - tag) >= 0;
+            }
+            if (__all(ok)) break;
+            if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > a.timeout ||
+                __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+              if (lane == 0) {
+                atomicOr(a.err, 2);
+                *abort_flag = 1;
+              }
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+        }
+        lds_barrier();
+        asm volatile("" ::: "memory");   // no peer-slot load hoisted above the flag match
+      };
       if (tid == 0)
-        __hip_atomic_store(reinterpret_cast<unsigned*>(static_cast<char*>(a.peer_base[a.rank]) + 64 * c), tag,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      if (w == 0) {
-        const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-        for (;;) {
-          bool ok = true;
-          if (lane < a.W && lane != a.rank) {
-            const unsigned v = __hip_atomic_load(
-                reinterpret_cast<const unsigned*>(static_cast<const char*>(a.peer_base[lane]) + 64 * c),
-                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            ok = (int)(v - tag) >= 0;
-          }
-          if (__all(ok)) break;
-          if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > a.timeout ||
-              __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
-            if (lane == 0) {
-              atomicOr(a.err, 2);
-              *abort_flag = 1;
-            }
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-      }
-      lds_barrier();
-      asm volatile("" ::: "memory");   // no peer-slot load hoisted above the flag match
+        __hip_atomic_store(reinterpret_cast<unsigned*>(flags + 64 * c), tag, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      wait_peers(0);
       if (*abort_flag) { aborted = true; break; }
-      f32x4 sum[NTW];
-      f32x4 sD = {0.f, 0.f, 0.f, 0.f};
-      float sb = 0.f;
+      // this lane's entry of wave w's chunk in a slot (dW1 tiles) / the small part (wave 7)
+      auto ld_slot = [&](const char* ps, int k) -> f32x4 {
+        const char* pk = ps + ((w * NTW + k) * 64 + lane) * 16;
+        if (a.gbf16) {
+          const unsigned long long x = ld_sys_u64(pk);
+          return f32x4{bf2f((unsigned)x & 0xffff), bf2f(((unsigned)x) >> 16), bf2f((unsigned)(x >> 32) & 0xffff),
+                       bf2f((unsigned)(x >> 48))};
+        }
+        return ld_sys_f32x4(pk);
+      };
+      if (a.xmode == 0) {
+        // one-shot: every wave sums its entries over all ranks (rank order)
+        f32x4 sum[NTW];
+        f32x4 sD = {0.f, 0.f, 0.f, 0.f};
+        float sb = 0.f;
 #pragma unroll
-      for (int k = 0; k < NTW; ++k) sum[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-      for (int rr = 0; rr < a.W; ++rr) {
-        const char* ps = static_cast<const char*>(a.peer_base[rr]) + soff;
+        for (int k = 0; k < NTW; ++k) sum[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int rr = 0; rr < a.W; ++rr) {
+          const char* ps = static_cast<const char*>(a.peer_base[rr]) + soff;
 #pragma unroll
-        for (int k = 0; k < NTW; ++k) {
-          f32x4 v = G[k];
-          if (rr != a.rank && tvk(k)) {
-            const char* pk = ps + ((w * NTW + k) * 64 + lane) * 16;
-            if (a.gbf16) {
-              const unsigned long long x = ld_sys_u64((pk));
-              v = f32x4{bf2f((unsigned)x & 0xffff), bf2f(((unsigned)x) >> 16), bf2f((unsigned)(x >> 32) & 0xffff),
-                        bf2f((unsigned)(x >> 48))};
-            } else {
-              v = ld_sys_f32x4((pk));
+          for (int k = 0; k < NTW; ++k) sum[k] += (rr != a.rank && tvk(k)) ? ld_slot(ps, k) : G[k];
+          if (w == 7) {
+            f32x4 v = D;
+            float vb = gb;
+            if (rr != a.rank) {
+              v = ld_sys_f32x4((ps + IPC_SMALL + lane * 16));
+              vb = lane < 16 + NCLS ? ld_sys_f32(ps + IPC_SMALL + 1024 + 4 * lane) : 0.f;
+            }
+            sD += v;
+            sb += vb;
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < NTW; ++k) G[k] = sum[k];
+        if (w == 7) { D = sD; gb = sb; }
+      } else {
+        // two-shot: wave w's entries form chunk w % W, reduced (rank order) by
+        // that rank only, then every rank reads each chunk's sums from its owner:
+        // 2 (W-1)/W of a slot crosses the fabric per GPU instead of (W-1) slots
+        const int own_chunk = w % a.W;
+        const size_t roff = IPC_RED + (size_t)(par * NCOMP + c) * IPC_SLOT;
+        char* ored = static_cast<char*>(a.peer_base[a.rank]) + roff;
+        if (own_chunk == a.rank) {
+          f32x4 sum[NTW];
+          f32x4 sD = {0.f, 0.f, 0.f, 0.f};
+          float sb = 0.f;
+#pragma unroll
+          for (int k = 0; k < NTW; ++k) sum[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+          for (int rr = 0; rr < a.W; ++rr) {
+            const char* ps = static_cast<const char*>(a.peer_base[rr]) + soff;
+#pragma unroll
+            for (int k = 0; k < NTW; ++k) sum[k] += (rr != a.rank && tvk(k)) ? ld_slot(ps, k) : G[k];
+            if (w == 7) {
+              f32x4 v = D;
+              float vb = gb;
+              if (rr != a.rank) {
+                v = ld_sys_f32x4((ps + IPC_SMALL + lane * 16));
+                vb = lane < 16 + NCLS ? ld_sys_f32(ps + IPC_SMALL + 1024 + 4 * lane) : 0.f;
+              }
+              sD += v;
+              sb += vb;
             }
           }
-          sum[k] += v;
-        }
-        if (w == 7) {
-          f32x4 v = D;
-          float vb = gb;
-          if (rr != a.rank) {
-            v = ld_sys_f32x4((ps + IPC_SMALL + lane * 16));
-            vb = lane < 16 + NCLS ? ld_sys_f32(ps + IPC_SMALL + 1024 + 4 * lane)
-                                  : 0.f;
+#pragma unroll
+          for (int k = 0; k < NTW; ++k) {
+            G[k] = sum[k];
+            if (tvk(k)) *reinterpret_cast<f32x4*>(ored + ((w * NTW + k) * 64 + lane) * 16) = sum[k];
           }
-          sD += v;
-          sb += vb;
+          if (w == 7) {
+            D = sD;
+            gb = sb;
+            *reinterpret_cast<f32x4*>(ored + IPC_SMALL + lane * 16) = D;
+            if (lane < 16 + NCLS) *reinterpret_cast<float*>(ored + IPC_SMALL + 1024 + lane * 4) = gb;
+          }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the reduced chunk landed
+        lds_barrier();
+        if (tid == 0)
+          __hip_atomic_store(reinterpret_cast<unsigned*>(flags + 64 * c + 8), tag, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+        wait_peers(8);
+        if (*abort_flag) { aborted = true; break; }
+        if (own_chunk != a.rank) {
+          const char* pr = static_cast<const char*>(a.peer_base[own_chunk]) + roff;
+#pragma unroll
+          for (int k = 0; k < NTW; ++k)
+            if (tvk(k)) G[k] = ld_sys_f32x4(pr + ((w * NTW + k) * 64 + lane) * 16);
+          if (w == 7) {
+            D = ld_sys_f32x4(pr + IPC_SMALL + lane * 16);
+            gb = lane < 16 + NCLS ? ld_sys_f32(pr + IPC_SMALL + 1024 + 4 * lane) : 0.f;
+          }
         }
       }
-#pragma unroll
-      for (int k = 0; k < NTW; ++k) G[k] = sum[k];
-      if (w == 7) { D = sD; gb = sb; }
     }
     // ---------------- updates (lr / (W B), 1/255 for the pixel scale)
     if (hv) {
@@ -785,7 +851,8 @@ hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int n
                                 float* metrics, int ring, int act, int naive, long long* gstep, unsigned long long* seq,
                                 void* xbuf, int* err, long long timeout, long long* step_ts, int ts_ring,
                                 const void* host_next, int next_steps, void* stage_next, void* const* peer_base, int W,
-                                int rank, int gbf16, long long* phase_ts, int spread, hipStream_t stream) {
+                                int rank, int gbf16, long long* phase_ts, int spread, int xmode,
+                               hipStream_t stream) {
   using namespace dtfk::mlpf;
   Args a;
   a.phase_ts = phase_ts;
@@ -814,6 +881,7 @@ hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int n
   a.rank = rank;
   a.gbf16 = gbf16;
   a.spread = spread;
+  a.xmode = xmode;
   {
     const char* gm = getenv("DTF_GATHER_MODE");   // measured: direct + long sleep 13.04 vs probe 13.32 us/step
     a.gmode = gm ? atoi(gm) : 3;

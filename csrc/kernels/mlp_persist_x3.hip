@@ -876,7 +876,8 @@ hipError_t dtfk_mlp_persist_x3(const void* stage, long long rec_h, int B, int ns
                                float* metrics, int ring, int act, int naive, long long* gstep, unsigned long long* seq,
                                void* xbuf, int* err, long long timeout, long long* step_ts, int ts_ring,
                                const void* host_next, int next_steps, void* stage_next, void* const* peer_base, int W,
-                               int rank, int gbf16, long long* phase_ts, int spread, hipStream_t stream) {
+                               int rank, int gbf16, long long* phase_ts, int spread, int /*xmode: one-shot only*/,
+                               hipStream_t stream) {
   using namespace dtfk::mlpx;
   Args a;
   a.stage = static_cast<const uint8_t*>(stage);

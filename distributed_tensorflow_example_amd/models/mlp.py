@@ -465,13 +465,21 @@ class PersistentMLPRunner:
 
     def __init__(self, trainer: FusedMLPTrainer, epoch, steps_per_launch: int = 550,
                  timeout_s: float = 30.0, precision: str = "fp32", grad_bf16: bool = True,
-                 placement: str = "auto"):
+                 placement: str = "auto", exchange: str = "one-shot"):
         C = trainer.C
         if precision not in ("fp32", "fp32-split", "fp16"):
             raise ValueError("precision must be 'fp32', 'fp32-split' or 'fp16'")
         self.precision = precision
         self.f32 = precision in ("fp32", "fp32-split")
         self.exact_split = precision == "fp32-split"
+        if exchange not in ("one-shot", "two-shot"):
+            raise ValueError("exchange must be 'one-shot' or 'two-shot'")
+        if exchange == "two-shot" and precision != "fp32":
+            raise ValueError("the two-shot exchange exists in the fp32 engine only")
+        # N GPUs: one-shot = each workgroup reads its gradient slot from every
+        # peer ((W-1) slots per GPU per step); two-shot = reduce-scatter by wave
+        # chunk + all-gather of the sums (2 (W-1)/W of a slot, one more hop)
+        self.exchange = exchange
         maxb = C.mlpf_max_batch() if self.f32 else C.mlp_persist_max_batch()
         if trainer.B > maxb:
             raise ValueError(f"PersistentMLPRunner needs batch <= {maxb}")
@@ -545,7 +553,8 @@ class PersistentMLPRunner:
                                 self.err, self.timeout_s, t.act, int(t.naive), host=ep.host,
                                 host_offset=nxt[0] * ep.rec, next_steps=nxt[1], stage_next=self.stages[dst],
                                 step_ts=self.step_ts, grad_bf16=self.grad_bf16, phase_ts=self.phase_ts,
-                                spread=self.placement == "spread", exact_split=self.exact_split, **ipc)
+                                spread=self.placement == "spread", exact_split=self.exact_split,
+                                two_shot=self.exchange == "two-shot", **ipc)
         else:
             xs = self.xs[par][off * self.rec_s:] if nsteps > 0 else self.xs[par]
             xts = self.xts[par][off * self.xtb:] if nsteps > 0 else self.xts[par]

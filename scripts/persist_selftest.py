@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--same-gpu", action="store_true")
     ap.add_argument("--precision", choices=["fp32", "fp32-split", "fp16"], default="fp32")
     ap.add_argument("--grad-dtype", choices=["bf16", "fp32"], default="bf16")
+    ap.add_argument("--exchange", choices=["one-shot", "two-shot"], default="one-shot")
     a = ap.parse_args()
     rank, ws = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     from distributed_tensorflow_example_amd.data.mnist import PinnedEpoch
@@ -50,6 +51,7 @@ def main():
     ys = torch.randint(0, 10, (a.steps, ws, B), generator=g).to(torch.uint8)
     ep = PinnedEpoch(xs[:, rank].reshape(-1, 784).numpy(), ys[:, rank].reshape(-1).numpy(), B)
     run = mlp.PersistentMLPRunner(tr, ep, steps_per_launch=a.per_launch, timeout_s=30.0, precision=a.precision,
+                                  exchange=a.exchange,
                                   grad_bf16=a.grad_dtype == "bf16")
     p0 = mlp.init_params(1).double()
     # all ranks enter the persistent launch together (cold-box import skew)
@@ -76,7 +78,7 @@ def main():
     ok = identical and all(e == 0 for _, _, e in sums) and rel < tol and tr.global_step == a.steps
     if rank == 0:
         print(json.dumps({"persist_selftest": "pass" if ok else "FAIL", "world": ws, "same_gpu": a.same_gpu,
-                          "steps": a.steps, "precision": a.precision,
+                          "steps": a.steps, "precision": a.precision, "exchange": a.exchange,
                           "grad_dtype": a.grad_dtype, "identical_replicas": identical, "rel_err_update_vs_fp32_ref": rel,
                           "errors": [e for _, _, e in sums], "global_step": tr.global_step}), flush=True)
     dist.barrier()

@@ -207,10 +207,11 @@ def test_persist_long_run_learns(native, precision):
     assert m[-50:, 0].mean() < 0.7 * m[:50, 0].mean(), (m[:50, 0].mean(), m[-50:, 0].mean())
 
 
-@pytest.mark.parametrize("precision,grad", [("fp32", "bf16"), ("fp32", "fp32"), ("fp32-split", "fp32"),
-                                            ("fp16", "bf16")])
+@pytest.mark.parametrize("precision,grad,exchange", [("fp32", "bf16", "one-shot"), ("fp32", "fp32", "one-shot"),
+                                                     ("fp32", "bf16", "two-shot"), ("fp32", "fp32", "two-shot"),
+                                                     ("fp32-split", "fp32", "one-shot"), ("fp16", "bf16", "one-shot")])
 @pytest.mark.parametrize("nproc", [2, 3])
-def test_persist_multi_rank_same_gpu(native, nproc, precision, grad):
+def test_persist_multi_rank_same_gpu(native, nproc, precision, grad, exchange):
     """N ranks sharing cuda:0: in-kernel IPC exchange, bit-identical replicas, sync-SGD math."""
     import json
     import os
@@ -225,7 +226,8 @@ def test_persist_multi_rank_same_gpu(native, nproc, precision, grad):
     s.close()
     cmd = [sys.executable, "-m", "torch.distributed.run", f"--nproc-per-node={nproc}", "--master-addr=127.0.0.1",
            f"--master-port={port}", os.path.join(repo, "scripts", "persist_selftest.py"), "--same-gpu",
-           "--steps=10", "--per-launch=4", f"--precision={precision}", f"--grad-dtype={grad}"]
+           "--steps=10", "--per-launch=4", f"--precision={precision}", f"--grad-dtype={grad}",
+           f"--exchange={exchange}"]
     env = dict(os.environ, PYTHONPATH=repo, OMP_NUM_THREADS="2")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=100, env=env)
     out = r.stdout + r.stderr

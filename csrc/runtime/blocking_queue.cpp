@@ -10,6 +10,8 @@
 
 #include <chrono>
 #include <condition_variable>
+
+#include "cv_wait.h"
 #include <deque>
 #include <mutex>
 #include <stdexcept>
@@ -52,7 +54,7 @@ class BlockingQueue {
       std::unique_lock<std::mutex> lk(mu_);
       auto pred = [&] { return closed_ || (int64_t)q_.size() < cap_; };
       if (timeout < 0) not_full_.wait(lk, pred);
-      else ok = not_full_.wait_for(lk, std::chrono::duration<double>(timeout), pred);
+      else ok = cv_wait_for(not_full_, lk, std::chrono::duration<double>(timeout), pred);
       if (timeout < 0) ok = true;
       if (ok && !closed_) {
         q_.push_back(o);
@@ -80,7 +82,7 @@ class BlockingQueue {
       auto pred = [&] { return !q_.empty() || closed_; };
       bool ok = true;
       if (timeout < 0) not_empty_.wait(lk, pred);
-      else ok = not_empty_.wait_for(lk, std::chrono::duration<double>(timeout), pred);
+      else ok = cv_wait_for(not_empty_, lk, std::chrono::duration<double>(timeout), pred);
       if (!q_.empty()) {
         o = q_.front();
         q_.pop_front();

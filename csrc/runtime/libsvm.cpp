@@ -14,6 +14,8 @@
 
 #include <atomic>
 #include <condition_variable>
+
+#include "cv_wait.h"
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -207,7 +209,7 @@ class Stream {
       std::unique_lock<std::mutex> lk(mu_);
       auto pred = [&] { return !q_.empty() || live_ == 0 || !err_.empty(); };
       if (timeout < 0) cv_.wait(lk, pred);
-      else if (!cv_.wait_for(lk, std::chrono::duration<double>(timeout), pred))
+      else if (!cv_wait_for(cv_, lk, std::chrono::duration<double>(timeout), pred))
         throw std::runtime_error("libsvm stream timed out");
       if (!err_.empty()) throw std::runtime_error(err_);
       if (q_.empty()) {

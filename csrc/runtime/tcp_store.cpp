@@ -24,6 +24,8 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+
+#include "cv_wait.h"
 #include <cstring>
 #include <map>
 #include <memory>
@@ -172,7 +174,7 @@ class Server {
         case GET: {  // args: key, timeout_ms
           auto deadline = std::chrono::steady_clock::now() +
                           std::chrono::milliseconds(args.size() > 1 ? to_i64(args[1]) : 0);
-          bool ok = cv_.wait_until(lk, deadline, [&] { return stopping_ || kv_.count(args[0]); });
+          bool ok = cv_wait_until(cv_, lk, deadline, [&] { return stopping_ || kv_.count(args[0]); });
           if (!ok || !kv_.count(args[0])) st = TIMEOUT;
           else out.push_back(kv_[args[0]]);
           break;
@@ -196,7 +198,7 @@ class Server {
             for (size_t i = 1; i < args.size(); ++i) if (!kv_.count(args[i])) return false;
             return true;
           };
-          if (!cv_.wait_until(lk, deadline, [&] { return stopping_ || have(); }) || !have()) st = TIMEOUT;
+          if (!cv_wait_until(cv_, lk, deadline, [&] { return stopping_ || have(); }) || !have()) st = TIMEOUT;
           break;
         }
         case DEL:

@@ -15,6 +15,8 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+
+#include "cv_wait.h"
 #include <cstdio>
 #include <deque>
 #include <mutex>
@@ -204,8 +206,8 @@ class EventFileWriter {
     auto last_flush = std::chrono::steady_clock::now();
     std::unique_lock<std::mutex> lk(mu_);
     while (true) {
-      cv_.wait_for(lk, std::chrono::milliseconds(200),
-                   [this] { return !q_.empty() || closed_ || flush_req_; });
+      cv_wait_for(cv_, lk, std::chrono::milliseconds(200),
+                  [this] { return !q_.empty() || closed_ || flush_req_; });
       std::deque<std::string> batch;
       batch.swap(q_);
       writing_ = true;

@@ -32,7 +32,8 @@ def ext_path() -> str:
 
 def sources():
     hip = sorted(glob.glob(os.path.join(CSRC, "**", "*.hip"), recursive=True))
-    cpp = sorted(glob.glob(os.path.join(CSRC, "**", "*.cpp"), recursive=True))
+    cpp = sorted(p for p in glob.glob(os.path.join(CSRC, "**", "*.cpp"), recursive=True)
+                 if os.sep + "asan" + os.sep not in p)     # csrc/asan: the sanitizer build's own module
     return hip, cpp
 
 

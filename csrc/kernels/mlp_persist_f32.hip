@@ -119,7 +119,18 @@ constexpr int L_RDB1 = L_B2 + 64;                      // [8][16]
 constexpr int L_RDB2 = L_RDB1 + 512;                   // [8][16]
 constexpr int L_RMET = L_RDB2 + 512;                   // [8][2]
 constexpr int L_FLAG = L_RMET + 64;
-constexpr int LDS_COMPUTE = L_FLAG + 64;
+// x operands of one step for this workgroup's feature slice, staged by wave 7
+// with LDS-DMA (global_load_lds_dwordx4, lane-linear 1 KiB pieces) instead of
+// fragment-shaped global loads in every wave (16 cache lines per instruction:
+// those loads were TA-bound, ~2.5 us of every step)
+constexpr int XF_ROW = 13 * 16;                        // [112 rows][13 tiles x 16 features] u8
+constexpr int L_XF = L_FLAG + 64;
+constexpr int XF_CHUNKS = BROWS * 13;                  // 1456 x 16 B
+constexpr int L_XT = L_XF + BROWS * XF_ROW;            // [208 features][128 batch] u8, 16-B chunks XOR-swizzled
+constexpr int XT_CHUNKS = 13 * 16 * 8;                 // 1664 x 16 B
+constexpr int L_LAB = L_XT + 13 * 16 * XTS;            // [128] labels
+constexpr int LDS_COMPUTE = L_LAB + 128;
+static_assert(L_XF % 1024 == 0 && L_XT % 16 == 0 && L_LAB % 16 == 0, "LDS-DMA bases");
 constexpr int CROW = DIN + 16;                         // copier LDS row stride (800)
 constexpr int LDS_COPIER = BROWS * CROW;               // 89600
 constexpr int LDS_BYTES = LDS_COMPUTE > LDS_COPIER ? LDS_COMPUTE : LDS_COPIER;
@@ -168,6 +179,13 @@ __device__ __forceinline__ void lds_barrier() {   // orders LDS only: no vmcnt(0
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// one lane-linear LDS-DMA piece: lane l's 16 bytes at gsrc land at lds + 16 l
+__device__ __forceinline__ void glds16(const void* gsrc, uint8_t* lds) {
+  typedef __attribute__((address_space(1))) void gvoid;
+  typedef __attribute__((address_space(3))) void lvoid;
+  __builtin_amdgcn_global_load_lds((gvoid*)(gsrc), (lvoid*)(lds), 16, 0, 0);
 }
 
 // Granule hand-off through a buffer resource over a wave-uniform region (one
@@ -365,25 +383,52 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
   const float lrX = lrB * (1.f / 255.f);
   const bool failed_in = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
 
-  // x operands of the wave's feature tiles, current and next step:
+  // x operands of the wave's feature tiles (registers, read from the LDS stage):
   //  xf[k][bt]: row 16bt+r, features 16ft+4g..+3 (forward B operand)
   //  xt[k][s] : feature 16ft+r, batch 16s+4g..+3 (weight-gradient A operand)
   //  lab      : label of batch row 16w+r (head, waves < 7)
   uint32_t xf[NTW][NBT], xt[NTW][NBT];
   int lab = 0;
-  auto load_x = [&](int st, uint32_t (&f)[NTW][NBT], uint32_t (&t)[NTW][NBT]) -> int {
-    // unconditional (an absent second tile reads tile ft1 = the slice's first: valid
-    // memory, never used) -- a conditional store into the array would demote it to scratch
+  // local tile of k (an absent second tile reads local tile 0: staged, never used)
+  auto tlk = [=](int k) { return k ? (tv1 ? w + 8 : 0) : w; };
+  // wave 7: step st's slice -> LDS.  x rows: lane-linear [row][13 tiles] (rows of
+  // 208 B, conflict-free reads); x^T rows of the slice's features are contiguous
+  // in the stage, their 16-B batch chunks XOR-swizzled by (feature >> 1) & 7 on the
+  // source address so the fragment reads below are conflict-free
+  auto stage_x = [&](int st) {
     const uint8_t* rec = a.stage + (long long)st * REC;
+    const uint8_t* xr = rec + 16 * tile0(q);
+#pragma unroll 1   // a rolled loop: unrolled, the 49 pieces' addresses get hoisted out of the step loop
+    for (int n = 0; n < (XF_CHUNKS + 63) / 64; ++n) {
+      const int k = 64 * n + lane;
+      // q = 3's 13th tile reads the next row's first 16 B (inside the record): unused
+      if (k < XF_CHUNKS) glds16(xr + (k / 13) * DIN + 16 * (k % 13), smem + L_XF + 1024 * n);
+    }
+    const uint8_t* xtb = rec + XROW_BYTES + (long long)(16 * tile0(q)) * XTS;
+#pragma unroll 1
+    for (int n = 0; n < XT_CHUNKS / 64; ++n) {
+      const int f = 8 * n + (lane >> 3);
+      const int s = (lane & 7) ^ ((f >> 1) & 7);
+      if (f < 16 * nt) glds16(xtb + f * XTS + 16 * s, smem + L_XT + 1024 * n);
+    }
+    if (lane < 8) glds16(rec + XROW_BYTES + XT_BYTES + 16 * lane, smem + L_LAB);
+  };
+  auto read_xf = [&]() {
+#pragma unroll
+    for (int k = 0; k < NTW; ++k)
+#pragma unroll
+      for (int b = 0; b < NBT; ++b)
+        xf[k][b] = *reinterpret_cast<const uint32_t*>(smem + L_XF + (16 * b + r) * XF_ROW + 16 * tlk(k) + 4 * g);
+    lab = smem[L_LAB + 16 * (w < NBT ? w : NBT - 1) + r];
+  };
+  auto read_xt = [&]() {
 #pragma unroll
     for (int k = 0; k < NTW; ++k) {
+      const int f = 16 * tlk(k) + r;
 #pragma unroll
-      for (int b = 0; b < NBT; ++b) {
-        f[k][b] = *reinterpret_cast<const uint32_t*>(rec + (16 * b + r) * DIN + 16 * ftk(k) + 4 * g);
-        t[k][b] = *reinterpret_cast<const uint32_t*>(rec + XROW_BYTES + (16 * ftk(k) + r) * XTS + 16 * b + 4 * g);
-      }
+      for (int s = 0; s < NBT; ++s)
+        xt[k][s] = *reinterpret_cast<const uint32_t*>(smem + L_XT + f * XTS + 16 * (s ^ ((f >> 1) & 7)) + 4 * g);
     }
-    return w < NBT ? rec[XROW_BYTES + XT_BYTES + 16 * w + r] : 0;   // label of batch row 16w+r
   };
   __syncthreads();
   if (failed_in) return;
@@ -418,7 +463,13 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
   if (*census < 0) return;
   const bool l2_e1 = (*census & 1) != 0;
   const bool l2_e2 = (*census & 2) != 0;
-  if (a.nsteps > 0) lab = load_x(0, xf, xt);
+  if (w == 7) {
+    stage_x(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  read_xf();
+  read_xt();
 
   bool aborted = false;
   for (int st = 0; st < a.nsteps; ++st) {
@@ -449,10 +500,13 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
     if (w == 0) { PH(1); }
     lds_barrier();
     if (w == 0) { PH(2); }
+    const bool more = st + 1 < a.nsteps;
+    // everyone's reads of this step's stage retired at barrier A: wave 7 (idle
+    // until P2) stages the next step while the others run the edges and the head
+    if (w == 7 && more) stage_x(st + 1);
+    if (w == 7) { PH(14); }
 
     // ---------------- E1 + P1 + E2 + head (wave w < 7: batch tile w)
-    uint32_t xfn[NTW][NBT], xtn[NTW][NBT];
-    int labn = 0;
     if (w < NBT) {
       const int bw = 16 * w + r;          // this lane's batch row
       const bool bv = bw < B;
@@ -553,12 +607,14 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
       const float cr = row16_sum((g == 0 && bv && (int)am == y) ? 1.f : 0.f);
       if (lane == 0) { rmet[2 * w] = ls; rmet[2 * w + 1] = cr; }
       if (w == 0) { PH(9); }
+      if (w == 6) { PH(13); }
+      if (w == 3) { PH(15); }
     }
-    // next step's x operands: in flight across the rest of the step
-    if (st + 1 < a.nsteps) labn = load_x(st + 1, xfn, xtn);
+    if (w == 7) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next step's stage landed
     lds_barrier();
     if (w == 0) { PH(10); }
     if (*abort_flag) { aborted = true; break; }
+    if (more) read_xf();   // next step's forward operands and label (dead since P0 / the head)
 
     // ---------------- P2: weight gradients of the wave's tiles
     f32x4 G[NTW];                        // dW1[16ft+4g+i][16j+r] (x 255 B)
@@ -578,6 +634,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
         G[k] = g0 + g1;
       }
     }
+    if (more) read_xt();   // next step's weight-gradient operands (this step's are consumed)
     if (w == 0) { PH(11); }
     f32x4 D = {0.f, 0.f, 0.f, 0.f};      // wave 7: dW2[16j+4g+i][class r] (x B)
     float gb = 0.f;                      // wave 7: db1 (lanes < 16) / db2 (lanes 16..25) (x B)
@@ -765,11 +822,6 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
 #pragma unroll
         for (int i = 0; i < 4; ++i) Wt[k][i] -= lrX * G[k][i];
     }
-#pragma unroll   // rotate the prefetched operands in
-    for (int k = 0; k < NTW; ++k)
-#pragma unroll
-      for (int b = 0; b < NBT; ++b) { xf[k][b] = xfn[k][b]; xt[k][b] = xtn[k][b]; }
-    lab = labn;
     if (w == 0) { PH(12); }
     if (w == 7) {
 #pragma unroll

@@ -82,6 +82,14 @@ def main():
     out["logit_edge_hop_after_last_publish_us_median_p90"] = [round(float(np.median(hop)), 3),
                                                                round(float(np.percentile(hop, 90)), 3)]
     out["logit_publish_skew_us_median"] = round(float(np.median(r[:, :, pub].max(1) - r[:, :, pub].min(1))), 3)
+    if prec == "fp32":
+        # extra stamps: 13 wave 6 head done, 14 wave 7 next-step loads issued, 15 wave 3 head done
+        med = lambda x: round(float(np.median(x)), 3)
+        rs = raw[1:G, : nj * nq, :].astype(np.float64) * 0.01
+        out["barrier_B_detail_us_from_step_start"] = {
+            "w0_head_done": med(rs[:, :, 9] - rs[:, :, 0]), "w3_head_done": med(rs[:, :, 15] - rs[:, :, 0]),
+            "w6_head_done": med(rs[:, :, 13] - rs[:, :, 0]), "w7_loads_issued": med(rs[:, :, 14] - rs[:, :, 0]),
+            "barrier_B_exit": med(rs[:, :, 10] - rs[:, :, 0])}
     late = (r[:, :, 0] - r[:, :, 0].min(axis=1, keepdims=True)).mean(axis=0)
     out["step_start_lateness_us_by_wg"] = np.round(late, 2).tolist()
     if prec == "fp32-split":

@@ -48,7 +48,8 @@ hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int n
                                 float* metrics, int ring, int act, int naive, long long* gstep, unsigned long long* seq,
                                 void* xbuf, int* err, long long timeout, long long* step_ts, int ts_ring,
                                 const void* host_next, int next_steps, void* stage_next, void* const* peer_base, int W,
-                                int rank, int gbf16, long long* phase_ts, int spread, int xmode, hipStream_t stream);
+                                int rank, int gbf16, long long* phase_ts, int spread, int xmode, int split,
+                                hipStream_t stream);
 long long dtfk_graph_mlp_lds(int B, int HP);
 hipError_t dtfk_graph_mlp_step(const float* x, const float* ylab, float* W1, float* b1, float* W2, float* b2,
                                float* a2buf, float* dz2buf, float* gW1, float* gb1, float* gW2, float* gb2,
@@ -371,7 +372,8 @@ void mlp_persist_f32(at::Tensor stage, int64_t rec_h, int B, int nsteps, at::Ten
                      double timeout_s, int act, int naive, c10::optional<at::Tensor> host, int64_t host_off,
                      int next_steps, c10::optional<at::Tensor> stage_next, c10::optional<at::Tensor> step_ts,
                      int64_t ipc_table, int ipc_W, int ipc_rank, bool grad_bf16,
-                     c10::optional<at::Tensor> phase_ts, bool spread, bool exact_split, bool two_shot) {
+                     c10::optional<at::Tensor> phase_ts, bool spread, bool exact_split, bool two_shot,
+                     bool mfma_split) {
   if (ipc_W > 1 && (ipc_table == 0 || ipc_rank < 0 || ipc_rank >= ipc_W || ipc_W > 64))
     throw std::runtime_error("mlp_persist_f32: N-GPU exchange needs the IPC peer table");
   if (B <= 0 || B > dtfk_mlpf_max_batch()) throw std::runtime_error("mlp_persist_f32: B out of range");
@@ -402,15 +404,26 @@ void mlp_persist_f32(at::Tensor stage, int64_t rec_h, int B, int nsteps, at::Ten
   int ts_ring = 1;
   long long* sts = step_ts_ptr(step_ts, &ts_ring);
   const long long ticks = (long long)(timeout_s * 1e8);   // s_memrealtime: 100 MHz
-  auto launch = exact_split ? dtfk_mlp_persist_x3 : dtfk_mlp_persist_f32;
-  hip_check(launch(stage.data_ptr(), rec_h, B, nsteps, params.data_ptr<float>(), lr.data_ptr<float>(),
-                   metrics.data_ptr<float>(), (int)(metrics.numel() / 2), act, naive,
-                   reinterpret_cast<long long*>(gstep.data_ptr<int64_t>()),
-                   reinterpret_cast<unsigned long long*>(seq.data_ptr<int64_t>()), xbuf.data_ptr(),
-                   err.data_ptr<int>(), ticks, sts, ts_ring, hn, next_steps, sn,
-                   reinterpret_cast<void* const*>(ipc_table), ipc_W > 1 ? ipc_W : 1,
-                   ipc_W > 1 ? ipc_rank : 0, grad_bf16 ? 1 : 0, ts_ptr(phase_ts, 64 * 64 * 16),
-                   spread ? 1 : 0, two_shot ? 1 : 0, cur_stream()),
+  hipError_t e;
+  if (exact_split)
+    e = dtfk_mlp_persist_x3(stage.data_ptr(), rec_h, B, nsteps, params.data_ptr<float>(), lr.data_ptr<float>(),
+                            metrics.data_ptr<float>(), (int)(metrics.numel() / 2), act, naive,
+                            reinterpret_cast<long long*>(gstep.data_ptr<int64_t>()),
+                            reinterpret_cast<unsigned long long*>(seq.data_ptr<int64_t>()), xbuf.data_ptr(),
+                            err.data_ptr<int>(), ticks, sts, ts_ring, hn, next_steps, sn,
+                            reinterpret_cast<void* const*>(ipc_table), ipc_W > 1 ? ipc_W : 1,
+                            ipc_W > 1 ? ipc_rank : 0, grad_bf16 ? 1 : 0, ts_ptr(phase_ts, 64 * 64 * 16),
+                            spread ? 1 : 0, two_shot ? 1 : 0, cur_stream());
+  else
+    e = dtfk_mlp_persist_f32(stage.data_ptr(), rec_h, B, nsteps, params.data_ptr<float>(), lr.data_ptr<float>(),
+                             metrics.data_ptr<float>(), (int)(metrics.numel() / 2), act, naive,
+                             reinterpret_cast<long long*>(gstep.data_ptr<int64_t>()),
+                             reinterpret_cast<unsigned long long*>(seq.data_ptr<int64_t>()), xbuf.data_ptr(),
+                             err.data_ptr<int>(), ticks, sts, ts_ring, hn, next_steps, sn,
+                             reinterpret_cast<void* const*>(ipc_table), ipc_W > 1 ? ipc_W : 1,
+                             ipc_W > 1 ? ipc_rank : 0, grad_bf16 ? 1 : 0, ts_ptr(phase_ts, 65 * 64 * 16),
+                             spread ? 1 : 0, two_shot ? 1 : 0, mfma_split ? 1 : 0, cur_stream());
+  hip_check(e,
             "mlp_persist_f32");
 }
 
@@ -481,7 +494,7 @@ void init_mlp(py::module& m) {
         py::arg("host_offset") = 0, py::arg("next_steps") = 0, py::arg("stage_next") = py::none(),
         py::arg("step_ts") = py::none(), py::arg("ipc_table") = 0, py::arg("ipc_W") = 1, py::arg("ipc_rank") = 0,
         py::arg("grad_bf16") = true, py::arg("phase_ts") = py::none(), py::arg("spread") = false,
-        py::arg("exact_split") = false, py::arg("two_shot") = false);
+        py::arg("exact_split") = false, py::arg("two_shot") = false, py::arg("mfma_split") = false);
   m.def("mlpx_stage_rec", &dtfk_mlpx_stage_rec);
   m.def("mlpx_xbuf_bytes", &dtfk_mlpx_xbuf_bytes);
   m.def("mlpx_ipc_bytes", &dtfk_mlpx_ipc_bytes);

@@ -129,7 +129,10 @@ constexpr int XF_CHUNKS = BROWS * 13;                  // 1456 x 16 B
 constexpr int L_XT = L_XF + BROWS * XF_ROW;            // [208 features][128 batch] u8, 16-B chunks XOR-swizzled
 constexpr int XT_CHUNKS = 13 * 16 * 8;                 // 1664 x 16 B
 constexpr int L_LAB = L_XT + 13 * 16 * XTS;            // [128] labels
-constexpr int LDS_COMPUTE = L_LAB + 128;
+constexpr int PS = XTS + 8;                            // split mode: bf16 plane row stride (elements)
+constexpr int L_DZP = L_LAB + 128;                     // split mode: [3 pieces][16 hidden][PS] dz2 bf16
+constexpr int L_HFLAG = L_DZP + 3 * 16 * PS * 2;       // [8] head-done flags (step + 1) of waves 0..6
+constexpr int LDS_COMPUTE = L_HFLAG + 64;
 static_assert(L_XF % 1024 == 0 && L_XT % 16 == 0 && L_LAB % 16 == 0, "LDS-DMA bases");
 constexpr int CROW = DIN + 16;                         // copier LDS row stride (800)
 constexpr int LDS_COPIER = BROWS * CROW;               // 89600
@@ -158,7 +161,8 @@ struct Args {
   int W, rank;
   int gbf16;                // N GPUs: dW1 payload in bf16 (BASELINE config #2) instead of fp32
   int spread;               // placement: 0 packed on one XCD (default), 1 spread (several ranks per GPU)
-  long long* phase_ts;      // optional phase stamps: [step < 64][workgroup 64][16] (wave 0 / wave 7, lane 0)
+  long long* phase_ts;      // optional phase stamps: [step < 64][workgroup 64][16] (wave 0 / wave 7, lane 0),
+                            // then [64][workgroup 64][16] launch stamps (prologue / epilogue / copier)
   int gmode;                // gather: 0 probe one granule per producer, then load; 1-3 direct loads with
                             // no / short / long s_sleep between passes (DTF_GATHER_MODE, tuning)
   int xmode;                // N GPUs: 0 one-shot (every workgroup reads its slot from every peer),
@@ -169,6 +173,52 @@ struct Args {
 #define PH(ph)                                                                                 \
   if (a.phase_ts != nullptr && lane == 0 && st < 64)                                         \
     a.phase_ts[((long long)st * 64 + c) * 16 + (ph)] = (long long)__builtin_amdgcn_s_memrealtime();
+
+// The exact three-way split v = hi + mid + lo by truncation, as fp32 bit
+// patterns whose low 16 bits are zero: hi keeps v's top 8 significant bits, the
+// remainder r = v - hi is exact (<= 16 bits), mid keeps its top 8, and r - mid
+// has <= 8 significant bits, so lo is exact too (normal range).  4 VALU ops.
+__device__ __forceinline__ void split3(float v, uint32_t& h, uint32_t& m, uint32_t& l) {
+  h = __float_as_uint(v) & 0xffff0000u;
+  const float r1 = v - __uint_as_float(h);
+  m = __float_as_uint(r1) & 0xffff0000u;
+  l = __float_as_uint(r1 - __uint_as_float(m));
+}
+// two split fp32 patterns -> one packed bf16 pair (upper halves)
+__device__ __forceinline__ uint32_t hi2(uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x07060302u); }
+// 8 fp32 -> the three bf16x8 pieces
+__device__ __forceinline__ void split8(const float (&v)[8], bf16x8& H, bf16x8& M, bf16x8& L) {
+  u32x4 ph, pm, pl;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint32_t h0, m0, l0, h1, m1, l1;
+    split3(v[2 * k], h0, m0, l0);
+    split3(v[2 * k + 1], h1, m1, l1);
+    ph[k] = hi2(h0, h1);
+    pm[k] = hi2(m0, m1);
+    pl[k] = hi2(l0, l1);
+  }
+  H = __builtin_bit_cast(bf16x8, ph);
+  M = __builtin_bit_cast(bf16x8, pm);
+  L = __builtin_bit_cast(bf16x8, pl);
+}
+// 8 pixel bytes (two dwords) -> 8 bf16, exact (<= 8 significant bits): upper half of the f32
+__device__ __forceinline__ bf16x8 px8(uint32_t w0, uint32_t w1) {
+  u32x4 o;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t wd = k < 2 ? w0 : w1;
+    const int sh = (k & 1) * 16;
+    const float f0 = (float)((wd >> sh) & 0xffu), f1 = (float)((wd >> (sh + 8)) & 0xffu);
+    o[k] = hi2(__float_as_uint(f0), __float_as_uint(f1));
+  }
+  return __builtin_bit_cast(bf16x8, o);
+}
+
+// launch-level stamp k of workgroup slot wg (compute c, copier NCOMP + cid), one lane
+#define PRO(wg, k)                                                                             \
+  if (a.phase_ts != nullptr)                                                                   \
+    a.phase_ts[((long long)64 * 64 + (wg)) * 16 + (k)] = (long long)__builtin_amdgcn_s_memrealtime();
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -287,6 +337,7 @@ __device__ __forceinline__ bool gather_gran(__amdgpu_buffer_rsrc_t rs, SlotOff s
 __device__ void copier(const Args& a, int cid, uint8_t* smem) {
   const int tid = threadIdx.x;
   const int B = a.B;
+  if (tid == 0) { PRO(NCOMP + cid, 0); }
   for (int st = cid; st < a.next_steps; st += NCOP) {
     const uint8_t* src = a.host_next + (long long)st * a.rec_h;
     uint8_t* dst = a.stage_next + (long long)st * REC;
@@ -324,10 +375,16 @@ __device__ void copier(const Args& a, int cid, uint8_t* smem) {
     }
     __syncthreads();
   }
+  if (tid == 0) { PRO(NCOMP + cid, 1); }
 }
 
 // ------------------------------------------------------------------ compute
-template <int ACT, bool MULTI>   // ACT 0 sigmoid, 1 relu; MULTI: N-GPU gradient exchange
+// ACT 0 sigmoid, 1 relu; MULTI: N-GPU gradient exchange; SPLIT: the two big
+// GEMMs (forward x W1, weight gradient x^T dz2) on bf16 MFMA through the exact
+// three-way split of their fp32 operand (pixels are exact in bf16), so every
+// product is exact and accumulates in fp32 -- 16x16x32 bf16 MFMAs at 8x the
+// f32-MFMA rate; the head stays on f32-input MFMA
+template <int ACT, bool MULTI, bool SPLIT>
 __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
@@ -345,9 +402,13 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
   float* rmet = reinterpret_cast<float*>(smem + L_RMET);
   int* abort_flag = reinterpret_cast<int*>(smem + L_FLAG);
   int* census = abort_flag + 1;
+  uint16_t* dzp = reinterpret_cast<uint16_t*>(smem + L_DZP);
+  if (tid == 0) { PRO(c, 0); }
 
   // ---- load state
   for (int k = tid; k < 3 * 16 * LS; k += THREADS) a2T[k] = 0.f;   // a2T, dz2T, dz3T (batch pad stays 0)
+  if constexpr (SPLIT)
+    for (int k = tid; k < 3 * 16 * PS; k += THREADS) dzp[k] = (uint16_t)0;   // dz2 planes (batch pad 0)
   if (tid < 256) {
     const int n = tid >> 4, cl = tid & 15;
     const int hn = 16 * j + n;
@@ -360,6 +421,8 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
     b2s[cl] = cl < NCLS ? a.params[OFF_B2 + cl] : 0.f;
   } else if (tid == 288) {
     *abort_flag = 0;
+  } else if (tid >= 296 && tid < 304) {
+    reinterpret_cast<int*>(smem + L_HFLAG)[tid - 296] = 0;
   }
   const int hid = 16 * j + r;       // this lane's hidden unit in the W1 / dW1 layouts
   const bool hv = hid < HID;
@@ -385,9 +448,11 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
 
   // x operands of the wave's feature tiles (registers, read from the LDS stage):
   //  xf[k][bt]: row 16bt+r, features 16ft+4g..+3 (forward B operand)
-  //  xt[k][s] : feature 16ft+r, batch 16s+4g..+3 (weight-gradient A operand)
+  //  xt[k][s] : feature 16ft+r, batch 16s+4g..+3 (weight-gradient A operand);
+  //             SPLIT: dwords 2c, 2c+1 = batch 32c+8g..+7 (c < 4, batch >= 112 zero)
   //  lab      : label of batch row 16w+r (head, waves < 7)
-  uint32_t xf[NTW][NBT], xt[NTW][NBT];
+  constexpr int XTN = SPLIT ? 8 : NBT;
+  uint32_t xf[NTW][NBT], xt[NTW][XTN];
   int lab = 0;
   // local tile of k (an absent second tile reads local tile 0: staged, never used)
   auto tlk = [=](int k) { return k ? (tv1 ? w + 8 : 0) : w; };
@@ -395,23 +460,23 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
   // 208 B, conflict-free reads); x^T rows of the slice's features are contiguous
   // in the stage, their 16-B batch chunks XOR-swizzled by (feature >> 1) & 7 on the
   // source address so the fragment reads below are conflict-free
-  auto stage_x = [&](int st) {
+  auto stage_x = [&](int st, int n0, int dn) {   // pieces n0, n0 + dn, ... of each part
     const uint8_t* rec = a.stage + (long long)st * REC;
     const uint8_t* xr = rec + 16 * tile0(q);
 #pragma unroll 1   // a rolled loop: unrolled, the 49 pieces' addresses get hoisted out of the step loop
-    for (int n = 0; n < (XF_CHUNKS + 63) / 64; ++n) {
+    for (int n = n0; n < (XF_CHUNKS + 63) / 64; n += dn) {
       const int k = 64 * n + lane;
       // q = 3's 13th tile reads the next row's first 16 B (inside the record): unused
       if (k < XF_CHUNKS) glds16(xr + (k / 13) * DIN + 16 * (k % 13), smem + L_XF + 1024 * n);
     }
     const uint8_t* xtb = rec + XROW_BYTES + (long long)(16 * tile0(q)) * XTS;
 #pragma unroll 1
-    for (int n = 0; n < XT_CHUNKS / 64; ++n) {
+    for (int n = n0; n < XT_CHUNKS / 64; n += dn) {
       const int f = 8 * n + (lane >> 3);
       const int s = (lane & 7) ^ ((f >> 1) & 7);
       if (f < 16 * nt) glds16(xtb + f * XTS + 16 * s, smem + L_XT + 1024 * n);
     }
-    if (lane < 8) glds16(rec + XROW_BYTES + XT_BYTES + 16 * lane, smem + L_LAB);
+    if (n0 == 0 && lane < 8) glds16(rec + XROW_BYTES + XT_BYTES + 16 * lane, smem + L_LAB);
   };
   auto read_xf = [&]() {
 #pragma unroll
@@ -425,51 +490,65 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
 #pragma unroll
     for (int k = 0; k < NTW; ++k) {
       const int f = 16 * tlk(k) + r;
+      if constexpr (SPLIT) {
 #pragma unroll
-      for (int s = 0; s < NBT; ++s)
-        xt[k][s] = *reinterpret_cast<const uint32_t*>(smem + L_XT + f * XTS + 16 * (s ^ ((f >> 1) & 7)) + 4 * g);
+        for (int cc = 0; cc < 4; ++cc) {
+          const uint2 v = *reinterpret_cast<const uint2*>(
+              smem + L_XT + f * XTS + 16 * ((2 * cc + (g >> 1)) ^ ((f >> 1) & 7)) + 8 * (g & 1));
+          xt[k][2 * cc] = v.x;
+          xt[k][2 * cc + 1] = v.y;
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < NBT; ++s)
+          xt[k][s] = *reinterpret_cast<const uint32_t*>(smem + L_XT + f * XTS + 16 * (s ^ ((f >> 1) & 7)) + 4 * g);
+      }
     }
   };
   __syncthreads();
+  if (tid == 0) { PRO(c, 4); }
   if (failed_in) return;
   // ---- placement census: E1 group (the NQ slices of block j) and E2 group (the
   // NJ blocks of slice q) each on this workgroup's XCD -> that edge stays in one
   // L2 (plain stores).  Decided per launch from HW_REG_XCC_ID, never assumed.
-  if (tid == 0) {
+  if (w == 0) {   // lane cc watches workgroup cc's entry: all 28 polls in flight at once
     const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20) & 15u;
     unsigned long long* hdr = reinterpret_cast<unsigned long long*>(a.xbuf + HDR_OFF);
     const unsigned tag0 = (unsigned)(seq0 + 1ull);
-    __hip_atomic_store(hdr + c, ((unsigned long long)tag0 << 32) | xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int e1 = 1, e2 = 1, bad = 0;
+    if (lane == 0)
+      __hip_atomic_store(hdr + c, ((unsigned long long)tag0 << 32) | xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-    for (int cc = 0; cc < NCOMP && !bad; ++cc) {
-      unsigned long long v;
-      while (((v = __hip_atomic_load(hdr + cc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) != tag0) {
-        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) {
-          atomicOr(a.err, 1);
-          bad = 1;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(2);
+    unsigned long long v = 0;
+    bool seen = lane >= NCOMP, bad = false;
+    for (;;) {
+      if (!seen) {
+        v = __hip_atomic_load(hdr + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        seen = (unsigned)(v >> 32) == tag0;
       }
-      if ((unsigned)v != xcc) {
-        if (cc / NQ == j) e1 = 0;
-        if (cc % NQ == q) e2 = 0;
+      if (__all(seen)) break;
+      if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) {
+        if (lane == 0) atomicOr(a.err, 1);
+        bad = true;
+        break;
       }
+      __builtin_amdgcn_s_sleep(1);
     }
-    *census = bad ? -1 : (e1 | (e2 << 1));
+    const bool off = lane < NCOMP && (unsigned)v != xcc;   // workgroup `lane` on another XCD
+    const bool e1 = !__any(off && lane / NQ == j);
+    const bool e2 = !__any(off && lane % NQ == q);
+    if (lane == 0) *census = bad ? -1 : ((e1 ? 1 : 0) | (e2 ? 2 : 0));
   }
   __syncthreads();
   if (*census < 0) return;
   const bool l2_e1 = (*census & 1) != 0;
   const bool l2_e2 = (*census & 2) != 0;
-  if (w == 7) {
-    stage_x(0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
+  if (tid == 0) { PRO(c, 1); }
+  stage_x(0, w, 8);   // the first step's stage: every wave a share
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   read_xf();
   read_xt();
+  if (tid == 0) { PRO(c, 2); }
 
   bool aborted = false;
   for (int st = 0; st < a.nsteps; ++st) {
@@ -479,32 +558,54 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
     if (c == 0 && tid == 0 && a.step_ts != nullptr)
       a.step_ts[(gstep0 + st) % a.ts_ring] = (long long)__builtin_amdgcn_s_memrealtime();
     if (w == 0) { PH(0); }
+    if (w == 7) { PH(14); }
 
     // ---------------- P0: forward partial of the wave's tiles, all batch tiles
     {
       f32x4 acc[NBT];
 #pragma unroll
       for (int b = 0; b < NBT; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (SPLIT) {
+        // K = 32: k = 8g + i -> tile i >> 2, feature 4g + (i & 3) -- the A piece is this
+        // lane's 8 master weights, the B operand its two x dwords (an absent second
+        // tile has zero weights); pieces lo, mid, hi (small terms first)
+        float wv[8];
 #pragma unroll
-      for (int k = 0; k < NTW; ++k) {
-        if (tvk(k)) {
+        for (int i = 0; i < 8; ++i) wv[i] = Wt[i >> 2][i & 3];
+        bf16x8 Ah, Am, Al;
+        split8(wv, Ah, Am, Al);
+        bf16x8 X[NBT];
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
+        for (int b = 0; b < NBT; ++b) X[b] = px8(xf[0][b], xf[1][b]);
 #pragma unroll
-            for (int b = 0; b < NBT; ++b) acc[b] = mfma4(Wt[k][e], ub(xf[k][b], e), acc[b]);
+        for (int b = 0; b < NBT; ++b) acc[b] = mfma16x16x32(Al, X[b], acc[b]);
+#pragma unroll
+        for (int b = 0; b < NBT; ++b) acc[b] = mfma16x16x32(Am, X[b], acc[b]);
+#pragma unroll
+        for (int b = 0; b < NBT; ++b) acc[b] = mfma16x16x32(Ah, X[b], acc[b]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < NTW; ++k) {
+          if (tvk(k)) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+              for (int b = 0; b < NBT; ++b) acc[b] = mfma4(Wt[k][e], ub(xf[k][b], e), acc[b]);
+          }
         }
       }
 #pragma unroll
       for (int b = 0; b < NBT; ++b) zbuf[(w * NBT + b) * 64 + lane] = acc[b];
     }
     if (w == 0) { PH(1); }
+    if (w == 7) { PH(13); }
+    if (w == 3) { PH(15); }
     lds_barrier();
     if (w == 0) { PH(2); }
     const bool more = st + 1 < a.nsteps;
     // everyone's reads of this step's stage retired at barrier A: wave 7 (idle
     // until P2) stages the next step while the others run the edges and the head
-    if (w == 7 && more) stage_x(st + 1);
-    if (w == 7) { PH(14); }
+    if (w == 7 && more) stage_x(st + 1, 0, 1);
 
     // ---------------- E1 + P1 + E2 + head (wave w < 7: batch tile w)
     if (w < NBT) {
@@ -594,7 +695,16 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float d = ACT == 0 ? da[i] * a2[i] * (1.f - a2[i]) : (a2[i] > 0.f ? da[i] : 0.f);
-        dz2T[(4 * g + i) * LS + bw] = d;
+        if constexpr (SPLIT) {
+          uint32_t ph, pm, pl;
+          split3(d, ph, pm, pl);
+          const int o = (4 * g + i) * PS + bw;
+          dzp[o] = (uint16_t)(ph >> 16);
+          dzp[16 * PS + o] = (uint16_t)(pm >> 16);
+          dzp[32 * PS + o] = (uint16_t)(pl >> 16);
+        } else {
+          dz2T[(4 * g + i) * LS + bw] = d;
+        }
         dz3T[(4 * g + i) * LS + bw] = dz3[i];
         const float s1 = row16_sum(d);
         const float s2 = row16_sum(dz3[i]);
@@ -606,21 +716,93 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
       const float ls = row16_sum((g == 0 && bv) ? loss : 0.f);
       const float cr = row16_sum((g == 0 && bv && (int)am == y) ? 1.f : 0.f);
       if (lane == 0) { rmet[2 * w] = ls; rmet[2 * w + 1] = cr; }
+      // head of batch tile w done (its a2 / dz3 rows and db partials are in LDS, its
+      // reads of W2 / b1 / b2 are over): wave 7 takes it from here
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+      if (lane == 0)
+        __hip_atomic_store(reinterpret_cast<int*>(smem + L_HFLAG) + w, st + 1, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
       if (w == 0) { PH(9); }
-      if (w == 6) { PH(13); }
-      if (w == 3) { PH(15); }
     }
-    if (w == 7) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next step's stage landed
+    // wave 7 (idle since staging the next step): dW2, db1, db2 and the metrics,
+    // batch tile by batch tile as the heads finish (fixed tile order), so none of
+    // it is left for after barrier B; one GPU: the W2 / b1 / b2 updates too
+    f32x4 D = {0.f, 0.f, 0.f, 0.f};      // wave 7: dW2[16j+4g+i][class r] (x B)
+    float gb = 0.f;                      // wave 7: db1 (lanes < 16) / db2 (lanes 16..25) (x B)
+    float ls = 0.f, cr = 0.f;            // wave 7: loss / correct sums of the batch
+    if (w == 7) {
+      const int* hflag = reinterpret_cast<const int*>(smem + L_HFLAG);
+      // lane < 16: db1 column `lane`; 16..25: db2 column lane - 16 (rdb2 follows rdb1 by 128 floats)
+      const float* gsrc = rdb1 + (lane < 16 ? lane : (lane < 16 + NCLS ? lane + 112 : 0));
+#pragma unroll
+      for (int v = 0; v < NBT; ++v) {
+        while (__hip_atomic_load(hflag + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < st + 1)
+          __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+        const f32x4 av = *reinterpret_cast<const f32x4*>(a2T + r * LS + 16 * v + 4 * g);
+        const f32x4 dv = *reinterpret_cast<const f32x4*>(dz3T + r * LS + 16 * v + 4 * g);
+        f32x4 dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dp = mfma4(av[e], dv[e], dp);
+        D += dp;
+        gb += gsrc[v * 16];
+        ls += rmet[2 * v];
+        cr += rmet[2 * v + 1];
+      }
+      if (lane >= 16 + NCLS) gb = 0.f;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next step's stage landed (long since)
+      if constexpr (!MULTI) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (16 * j + 4 * g + i < HID && r < NCLS) w2s[(4 * g + i) * 16 + r] -= lrB * D[i];
+        if (lane < 16) {
+          if (16 * j + lane < HID) b1s[lane] -= lrB * gb;
+        } else if (lane < 16 + NCLS) {
+          b2s[lane - 16] -= lrB * gb;
+        }
+      }
+    }
     lds_barrier();
     if (w == 0) { PH(10); }
+    if (w == 7 && c == 0 && lane == 63) {   // after the barrier: its store is never waited for there
+      const int sl = (int)((gstep0 + st) % a.ring);
+      a.metrics[2 * sl] = ls / (float)B;
+      a.metrics[2 * sl + 1] = cr / (float)B;
+    }
     if (*abort_flag) { aborted = true; break; }
     if (more) read_xf();   // next step's forward operands and label (dead since P0 / the head)
 
     // ---------------- P2: weight gradients of the wave's tiles
     f32x4 G[NTW];                        // dW1[16ft+4g+i][16j+r] (x 255 B)
 #pragma unroll
+    for (int k = 0; k < NTW; ++k) G[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (SPLIT) {
+      // dW1 tile = x^T dz2 over K = 128 batch rows in 4 chunks: A = x^T bytes (exact),
+      // B = the dz2 pieces; an absent second tile computes a zero-weight copy (unused)
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) {
+        const uint16_t* bp = dzp + r * PS + 32 * cc + 8 * g;
+        const bf16x8 Bh = *reinterpret_cast<const bf16x8*>(bp);
+        const bf16x8 Bm = *reinterpret_cast<const bf16x8*>(bp + 16 * PS);
+        const bf16x8 Bl = *reinterpret_cast<const bf16x8*>(bp + 32 * PS);
+        const bf16x8 X0 = px8(xt[0][2 * cc], xt[0][2 * cc + 1]);
+        if (tv1) {   // wave-uniform: waves without a second tile skip its MFMAs
+          const bf16x8 X1 = px8(xt[1][2 * cc], xt[1][2 * cc + 1]);
+          G[0] = mfma16x16x32(X0, Bl, G[0]);
+          G[1] = mfma16x16x32(X1, Bl, G[1]);
+          G[0] = mfma16x16x32(X0, Bm, G[0]);
+          G[1] = mfma16x16x32(X1, Bm, G[1]);
+          G[0] = mfma16x16x32(X0, Bh, G[0]);
+          G[1] = mfma16x16x32(X1, Bh, G[1]);
+        } else {
+          G[0] = mfma16x16x32(X0, Bl, G[0]);
+          G[0] = mfma16x16x32(X0, Bm, G[0]);
+          G[0] = mfma16x16x32(X0, Bh, G[0]);
+        }
+      }
+    } else {
+#pragma unroll
     for (int k = 0; k < NTW; ++k) {
-      G[k] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (tvk(k)) {
         f32x4 g0 = {0.f, 0.f, 0.f, 0.f}, g1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -634,37 +816,9 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
         G[k] = g0 + g1;
       }
     }
+    }
     if (more) read_xt();   // next step's weight-gradient operands (this step's are consumed)
     if (w == 0) { PH(11); }
-    f32x4 D = {0.f, 0.f, 0.f, 0.f};      // wave 7: dW2[16j+4g+i][class r] (x B)
-    float gb = 0.f;                      // wave 7: db1 (lanes < 16) / db2 (lanes 16..25) (x B)
-    if (w == 7) {
-      f32x4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < NBT; ++s) {
-        const f32x4 av = *reinterpret_cast<const f32x4*>(a2T + r * LS + 16 * s + 4 * g);
-        const f32x4 dv = *reinterpret_cast<const f32x4*>(dz3T + r * LS + 16 * s + 4 * g);
-        d0 = mfma4(av[0], dv[0], d0);
-        d1 = mfma4(av[1], dv[1], d1);
-        d0 = mfma4(av[2], dv[2], d0);
-        d1 = mfma4(av[3], dv[3], d1);
-      }
-      D = d0 + d1;
-      if (lane < 16) {
-#pragma unroll
-        for (int v = 0; v < NBT; ++v) gb += rdb1[v * 16 + lane];
-      } else if (lane < 16 + NCLS) {
-#pragma unroll
-        for (int v = 0; v < NBT; ++v) gb += rdb2[v * 16 + lane - 16];
-      } else if (lane == 63 && c == 0) {
-        float ls = 0.f, cr = 0.f;
-#pragma unroll
-        for (int v = 0; v < NBT; ++v) { ls += rmet[2 * v]; cr += rmet[2 * v + 1]; }
-        const int sl = (int)((gstep0 + st) % a.ring);
-        a.metrics[2 * sl] = ls / (float)B;
-        a.metrics[2 * sl + 1] = cr / (float)B;
-      }
-    }
     if constexpr (MULTI) {
       // ---- one-shot exchange of this workgroup's gradient with the same
       // workgroup on every peer GPU (uncached IPC buffers: completion ==
@@ -823,7 +977,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
         for (int i = 0; i < 4; ++i) Wt[k][i] -= lrX * G[k][i];
     }
     if (w == 0) { PH(12); }
-    if (w == 7) {
+    if (MULTI && w == 7) {   // N GPUs: with the rank sums of dW2 / db1 / db2
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         if (16 * j + 4 * g + i < HID && r < NCLS) w2s[(4 * g + i) * 16 + r] -= lrB * D[i];
@@ -836,6 +990,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
   }
   if (aborted) return;
   __syncthreads();   // wave 7's last small-parameter update
+  if (tid == 0) { PRO(c, 3); }
 
   // ---- write back (fp32 master), global step, exchange sequence, end stamp
   if (hv) {
@@ -865,6 +1020,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
         a.step_ts[(gstep0 + a.nsteps) % a.ts_ring] = (long long)__builtin_amdgcn_s_memrealtime();
     }
   }
+  if (tid == 0) { PRO(c, 5); }
 }
 
 // packed placement (a.spread == 0): compute workgroup c runs as blockIdx 8c, so
@@ -872,7 +1028,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
 // L2); the first NCOP other blocks copy, the rest exit.  spread (several ranks on
 // one GPU, tests): compute = blocks 0..27, copiers = 28..43.  Placement is speed
 // only: the census above decides each edge's store flavour.
-template <int ACT, bool MULTI>
+template <int ACT, bool MULTI, bool SPLIT>
 __global__ __launch_bounds__(THREADS, 1) void mlp_persist_f32(Args a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int b = blockIdx.x;
@@ -883,7 +1039,7 @@ __global__ __launch_bounds__(THREADS, 1) void mlp_persist_f32(Args a) {
     if ((b & 7) == 0) c = b >> 3; else cid = b - (b >> 3) - 1;
   }
   if (c >= 0) {
-    if (a.nsteps > 0) compute<ACT, MULTI>(a, c / NQ, c % NQ, smem);
+    if (a.nsteps > 0) compute<ACT, MULTI, SPLIT>(a, c / NQ, c % NQ, smem);
     return;
   }
   if (cid < NCOP) copier(a, cid, smem);
@@ -903,8 +1059,8 @@ hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int n
                                 float* metrics, int ring, int act, int naive, long long* gstep, unsigned long long* seq,
                                 void* xbuf, int* err, long long timeout, long long* step_ts, int ts_ring,
                                 const void* host_next, int next_steps, void* stage_next, void* const* peer_base, int W,
-                                int rank, int gbf16, long long* phase_ts, int spread, int xmode,
-                               hipStream_t stream) {
+                                int rank, int gbf16, long long* phase_ts, int spread, int xmode, int split,
+                                hipStream_t stream) {
   using namespace dtfk::mlpf;
   Args a;
   a.phase_ts = phase_ts;
@@ -939,26 +1095,23 @@ hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int n
     a.gmode = gm ? atoi(gm) : 3;
   }
   constexpr size_t lds = LDS_BYTES;
+  typedef void (*Kern)(Args);
+  static const Kern kerns[8] = {mlp_persist_f32<0, false, false>, mlp_persist_f32<1, false, false>,
+                                mlp_persist_f32<0, true, false>,  mlp_persist_f32<1, true, false>,
+                                mlp_persist_f32<0, false, true>,  mlp_persist_f32<1, false, true>,
+                                mlp_persist_f32<0, true, true>,   mlp_persist_f32<1, true, true>};
   static bool attr_set = false;
-  const void* kerns[4] = {reinterpret_cast<const void*>(mlp_persist_f32<0, false>),
-                          reinterpret_cast<const void*>(mlp_persist_f32<1, false>),
-                          reinterpret_cast<const void*>(mlp_persist_f32<0, true>),
-                          reinterpret_cast<const void*>(mlp_persist_f32<1, true>)};
   if (!attr_set) {
-    for (const void* k : kerns) {
-      const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    for (Kern k : kerns) {
+      const hipError_t e =
+          hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (e != hipSuccess) return e;
     }
     attr_set = true;
   }
-  const int which = (act == 0 ? 0 : 1) + (W > 1 ? 2 : 0);
+  const int which = (act == 0 ? 0 : 1) + (W > 1 ? 2 : 0) + (split ? 4 : 0);
   const int grid = spread ? GRID_SPREAD : GRID_PACKED;
-  switch (which) {
-    case 0: hipLaunchKernelGGL((mlp_persist_f32<0, false>), dim3(grid), dim3(THREADS), lds, stream, a); break;
-    case 1: hipLaunchKernelGGL((mlp_persist_f32<1, false>), dim3(grid), dim3(THREADS), lds, stream, a); break;
-    case 2: hipLaunchKernelGGL((mlp_persist_f32<0, true>), dim3(grid), dim3(THREADS), lds, stream, a); break;
-    default: hipLaunchKernelGGL((mlp_persist_f32<1, true>), dim3(grid), dim3(THREADS), lds, stream, a); break;
-  }
+  hipLaunchKernelGGL(kerns[which], dim3(grid), dim3(THREADS), lds, stream, a);
   return hipGetLastError();
 }
 

@@ -467,14 +467,15 @@ class PersistentMLPRunner:
                  timeout_s: float = 30.0, precision: str = "fp32", grad_bf16: bool = True,
                  placement: str = "auto", exchange: str = "one-shot"):
         C = trainer.C
-        if precision not in ("fp32", "fp32-split", "fp16"):
-            raise ValueError("precision must be 'fp32', 'fp32-split' or 'fp16'")
+        if precision not in ("fp32", "fp32-split", "fp32-s28", "fp16"):
+            raise ValueError("precision must be 'fp32', 'fp32-split', 'fp32-s28' or 'fp16'")
         self.precision = precision
-        self.f32 = precision in ("fp32", "fp32-split")
+        self.f32 = precision in ("fp32", "fp32-split", "fp32-s28")
         self.exact_split = precision == "fp32-split"
+        self.mfma_split = precision == "fp32-s28"
         if exchange not in ("one-shot", "two-shot"):
             raise ValueError("exchange must be 'one-shot' or 'two-shot'")
-        if exchange == "two-shot" and precision != "fp32":
+        if exchange == "two-shot" and precision not in ("fp32", "fp32-s28"):
             raise ValueError("the two-shot exchange exists in the fp32 engine only")
         # N GPUs: one-shot = each workgroup reads its gradient slot from every
         # peer ((W-1) slots per GPU per step); two-shot = reduce-scatter by wave
@@ -554,7 +555,7 @@ class PersistentMLPRunner:
                                 host_offset=nxt[0] * ep.rec, next_steps=nxt[1], stage_next=self.stages[dst],
                                 step_ts=self.step_ts, grad_bf16=self.grad_bf16, phase_ts=self.phase_ts,
                                 spread=self.placement == "spread", exact_split=self.exact_split,
-                                two_shot=self.exchange == "two-shot", **ipc)
+                                two_shot=self.exchange == "two-shot", mfma_split=self.mfma_split, **ipc)
         else:
             xs = self.xs[par][off * self.rec_s:] if nsteps > 0 else self.xs[par]
             xts = self.xts[par][off * self.xtb:] if nsteps > 0 else self.xts[par]

@@ -31,7 +31,7 @@ NAMES = {"fp32": ["fwd_mfma", "barrier_A", "E1_publish", "E1_wait", "E1_load_sum
 
 def main():
     prec = sys.argv[1] if len(sys.argv) > 1 else "fp32"
-    names = NAMES[prec]
+    names = NAMES["fp32" if prec == "fp32-s28" else prec]
     B, G = 100, 64
     dev = torch.device("cuda", 0)
     imgs, labels = synthetic_mnist(55000, seed=1)
@@ -58,14 +58,28 @@ def main():
         out[f"launch_{g}"] = {"event_us": round(t0.elapsed_time(t1) * 1000.0, 2),
                               "sum_step_us": round(float(dt.sum()), 2),
                               "p50_step_us": round(float(np.median(dt)), 3)}
-    ts = torch.zeros(64 * 64 * 16, dtype=torch.int64, device=dev)
+    ts = torch.zeros(65 * 64 * 16, dtype=torch.int64, device=dev)
     run.phase_ts = ts
     run.prepare(G)
     run.run(G, lookahead=G)
     torch.cuda.synchronize()
     run.phase_ts = None
-    raw = ts.cpu().numpy().reshape(64, 64, 16)
-    nj, nq = (7, 4) if prec == "fp32" else (7, 1)
+    raw = ts.cpu().numpy().reshape(65, 64, 16)
+    if prec in ("fp32", "fp32-s28"):
+        # launch stamps (row 64): compute wg 0 entry, 4 params loaded, 1 census done, 2 first stage read,
+        # 3 loop done, 5 written back; copier 28+cid: 0 entry, 1 done. Relative to the earliest entry, us
+        L = raw[64].astype(np.float64) * 0.01
+        t0 = min(L[:28, 0].min(), L[28:44, 0].min())
+        rel = lambda x: round(float(x - t0), 2)
+        first_step = raw[0, :28, 0].astype(np.float64) * 0.01
+        out["launch_stamps_us"] = {
+            "compute_entry_max": rel(L[:28, 0].max()), "params_loaded_max": rel(L[:28, 4].max()),
+            "census_done_max": rel(L[:28, 1].max()), "first_stage_ready_max": rel(L[:28, 2].max()),
+            "step0_start_max": rel(first_step.max()), "loop_done_max": rel(L[:28, 3].max()),
+            "written_back_max": rel(L[:28, 5].max()), "copier_entry_max": rel(L[28:44, 0].max()),
+            "copier_done_max": rel(L[28:44, 1].max())}
+        raw = raw[:64]
+    nj, nq = (7, 4) if prec in ("fp32", "fp32-s28") else (7, 1)
     ns = len(names) + 1
     r = raw[1:G, : nj * nq, :ns].astype(np.float64) * 0.01   # us
     seg = {}
@@ -75,21 +89,21 @@ def main():
     out["segments_us_median_p90"] = seg
     step = r[1:, :, 0] - r[:-1, :, 0]
     out["step_us_median"] = round(float(np.median(step)), 3)
-    pub = 6 if prec == "fp32" else 3
+    pub = 6 if prec in ("fp32", "fp32-s28") else 3
     got = pub + 1
     last = r[:, :, pub].max(axis=1, keepdims=True)
     hop = r[:, :, got] - last
     out["logit_edge_hop_after_last_publish_us_median_p90"] = [round(float(np.median(hop)), 3),
                                                                round(float(np.percentile(hop, 90)), 3)]
     out["logit_publish_skew_us_median"] = round(float(np.median(r[:, :, pub].max(1) - r[:, :, pub].min(1))), 3)
-    if prec == "fp32":
-        # extra stamps: 13 wave 6 head done, 14 wave 7 next-step loads issued, 15 wave 3 head done
+    if prec in ("fp32", "fp32-s28"):
+        # extra stamps: 13 wave 7 forward done, 14 wave 7 step start, 15 wave 3 forward done
         med = lambda x: round(float(np.median(x)), 3)
         rs = raw[1:G, : nj * nq, :].astype(np.float64) * 0.01
-        out["barrier_B_detail_us_from_step_start"] = {
-            "w0_head_done": med(rs[:, :, 9] - rs[:, :, 0]), "w3_head_done": med(rs[:, :, 15] - rs[:, :, 0]),
-            "w6_head_done": med(rs[:, :, 13] - rs[:, :, 0]), "w7_loads_issued": med(rs[:, :, 14] - rs[:, :, 0]),
-            "barrier_B_exit": med(rs[:, :, 10] - rs[:, :, 0])}
+        out["barrier_A_detail_us_from_w0_step_start"] = {
+            "w0_fwd_done": med(rs[:, :, 1] - rs[:, :, 0]), "w3_fwd_done": med(rs[:, :, 15] - rs[:, :, 0]),
+            "w7_step_start": med(rs[:, :, 14] - rs[:, :, 0]), "w7_fwd_done": med(rs[:, :, 13] - rs[:, :, 0]),
+            "barrier_A_exit": med(rs[:, :, 2] - rs[:, :, 0])}
     late = (r[:, :, 0] - r[:, :, 0].min(axis=1, keepdims=True)).mean(axis=0)
     out["step_start_lateness_us_by_wg"] = np.round(late, 2).tolist()
     if prec == "fp32-split":

@@ -59,7 +59,7 @@ def main(argv=None):
     ap.add_argument("--batch", type=int, default=100, help="per-GPU batch (reference: 100)")
     ap.add_argument("--lr", type=float, default=0.0005)
     ap.add_argument("--steps-per-graph", type=int, default=50, help="3-launch path: steps per captured hipGraph")
-    ap.add_argument("--precision", choices=["fp32", "fp32-split", "fp32-s28", "fp16"], default="fp32",
+    ap.add_argument("--precision", choices=["fp32", "fp32-mfma", "fp32-split7", "fp16"], default="fp32",
                     help="persistent engine (reference precision: fp32): fp32 = f32-input MFMA for every product; "
                          "fp32-split = exact 3-way bf16 split of every fp32 GEMM operand (exact products, fp32 "
                          "accumulate); fp16 = f16 MFMA operands")
@@ -164,7 +164,7 @@ def main(argv=None):
                  "ipc-apply": ["ipc-apply"], "rccl": ["rccl"]}[a.allreduce]
         if can_persist and a.allreduce == "auto":
             # both in-kernel exchanges are timed (the fabric decides which wins)
-            chain = ["persistent"] + (["persistent-2shot"] if a.precision in ("fp32", "fp32-s28") else []) + chain
+            chain = ["persistent"] + (["persistent-2shot"] if a.precision in ("fp32", "fp32-mfma") else []) + chain
     # N > 1: the first two valid candidates are timed briefly (outside the timed
     # region) and the faster one is kept -- the in-kernel exchange's per-CU peer
     # reads vs the 3-launch path's exchange spread over 347 workgroups depends on
@@ -288,14 +288,14 @@ def main(argv=None):
                 "input_prefetch": "in-kernel copier workgroups" if persistent else a.prefetch,
                 "activation": a.act,
                 "exchange_tuning_us_per_step": tuned or None,
-                "precision": ({"fp32-split": "fp32 GEMMs as exact 3-way bf16 splits (hi+mid+lo == each fp32 "
+                "precision": ({"fp32-split7": "7-workgroup engine: fp32 GEMMs as exact 3-way bf16 splits (hi+mid+lo == each fp32 "
                                              "weight / gradient, uint8 pixels exact): exact products, fp32 "
                                              "accumulate; head on v_mfma_f32_16x16x4_f32; fp32 master weights",
-                               "fp32-s28": "fp32 GEMMs as exact 3-way bf16 splits on the 28-workgroup engine "
+                               "fp32": "fp32 GEMMs as exact 3-way bf16 splits on the 28-workgroup engine "
                                            "(hi+mid+lo == each fp32 weight / gradient, uint8 pixels exact): exact "
                                            "products, fp32 accumulate; head on v_mfma_f32_16x16x4_f32; fp32 master "
                                            "weights",
-                               "fp32": "fp32 MFMA operands (v_mfma_f32_16x16x4_f32, exact f32 products), "
+                               "fp32-mfma": "fp32 MFMA operands (v_mfma_f32_16x16x4_f32, exact f32 products), "
                                        "fp32 accumulate, fp32 master weights",
                                "fp16": "fp16 MFMA operands (pixels exact as 1024+u), fp32 accumulate, fp32 master "
                                        "weights"}[a.precision]

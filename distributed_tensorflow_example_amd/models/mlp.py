@@ -425,17 +425,20 @@ class PersistentMLPRunner:
     epoch: ONE launch per chunk of up to `g` steps.
 
     precision="fp32" (default, the reference's precision: example.py:77-118 is
-        fp32 end to end) -- csrc/kernels/mlp_persist_f32.hip: 28 compute
-        workgroups (7 hidden blocks x 4 feature slices, packed on one XCD) on
-        f32-input MFMA (v_mfma_f32_16x16x4_f32, bitwise an fmaf chain) for every
-        product; fp32 master weights in VGPRs.
-    precision="fp32-split" -- csrc/kernels/mlp_persist_x3.hip: 7 compute
-        workgroups (one per hidden block); the two large GEMMs on bf16 MFMA
-        through an EXACT 3-way split of every fp32 operand (hi + mid + lo == the
-        fp32 value; pixels exact), so every product is exact and accumulates in
-        fp32; small head products on f32-input MFMA.  One inter-workgroup edge
-        per step instead of two, but 7 CUs carry all the MFMA work (measured
-        14.7 vs 13.0 us/step).
+        fp32 end to end) -- csrc/kernels/mlp_persist_f32.hip, SPLIT: 28 compute
+        workgroups (7 hidden blocks x 4 feature slices, packed on one XCD); the
+        two big GEMMs (x W1 and x^T dz2) on 16x16x32 bf16 MFMA through the EXACT
+        3-way split of their fp32 operand (hi + mid + lo == the fp32 value;
+        pixels exact in bf16), so every product is exact and accumulates in
+        fp32; the head on f32-input MFMA; fp32 master weights in VGPRs.  Each
+        step's x slice is staged into LDS by one wave with LDS-DMA.
+    precision="fp32-mfma" -- the same engine with every product on f32-input
+        MFMA (v_mfma_f32_16x16x4_f32, bitwise an fmaf chain): 1/8 of the bf16
+        MFMA rate, ~2 us/step slower.
+    precision="fp32-split7" -- csrc/kernels/mlp_persist_x3.hip: 7 compute
+        workgroups (one per hidden block, the exact split on the big GEMMs):
+        one inter-workgroup edge per step instead of two, but 7 CUs carry all
+        the MFMA work.
     precision="fp16" -- csrc/kernels/mlp_persist.hip: 7 compute workgroups on
         f16 MFMA (pixels exact as 1024+u, weights/activations rounded to fp16),
         57 copier workgroups.
@@ -467,15 +470,15 @@ class PersistentMLPRunner:
                  timeout_s: float = 30.0, precision: str = "fp32", grad_bf16: bool = True,
                  placement: str = "auto", exchange: str = "one-shot"):
         C = trainer.C
-        if precision not in ("fp32", "fp32-split", "fp32-s28", "fp16"):
-            raise ValueError("precision must be 'fp32', 'fp32-split', 'fp32-s28' or 'fp16'")
+        if precision not in ("fp32", "fp32-mfma", "fp32-split7", "fp16"):
+            raise ValueError("precision must be 'fp32', 'fp32-mfma', 'fp32-split7' or 'fp16'")
         self.precision = precision
-        self.f32 = precision in ("fp32", "fp32-split", "fp32-s28")
-        self.exact_split = precision == "fp32-split"
-        self.mfma_split = precision == "fp32-s28"
+        self.f32 = precision in ("fp32", "fp32-mfma", "fp32-split7")
+        self.exact_split = precision == "fp32-split7"
+        self.mfma_split = precision == "fp32"
         if exchange not in ("one-shot", "two-shot"):
             raise ValueError("exchange must be 'one-shot' or 'two-shot'")
-        if exchange == "two-shot" and precision not in ("fp32", "fp32-s28"):
+        if exchange == "two-shot" and precision not in ("fp32", "fp32-mfma"):
             raise ValueError("the two-shot exchange exists in the fp32 engine only")
         # N GPUs: one-shot = each workgroup reads its gradient slot from every
         # peer ((W-1) slots per GPU per step); two-shot = reduce-scatter by wave

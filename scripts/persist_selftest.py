@@ -30,7 +30,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--per-launch", type=int, default=4)
     ap.add_argument("--same-gpu", action="store_true")
-    ap.add_argument("--precision", choices=["fp32", "fp32-split", "fp32-s28", "fp16"], default="fp32")
+    ap.add_argument("--precision", choices=["fp32", "fp32-mfma", "fp32-split7", "fp16"], default="fp32")
     ap.add_argument("--grad-dtype", choices=["bf16", "fp32"], default="bf16")
     ap.add_argument("--exchange", choices=["one-shot", "two-shot"], default="one-shot")
     a = ap.parse_args()

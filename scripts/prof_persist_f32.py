@@ -25,13 +25,13 @@ NAMES = {"fp32": ["fwd_mfma", "barrier_A", "E1_publish", "E1_wait", "E1_load_sum
                        "E2_wait", "E2_load_sum", "head", "barrier_B", "wgrad_mfma", "update"],
          # exact-split engine (mlp_persist_x3.hip): 0 start 1 fwd 2 barA 3 E2 pub 4 E2 gathered 5 head 6 barB
          # 7 wgrad 8 update
-         "fp32-split": ["fwd_mfma_and_prefetch_issue", "barrier_A", "zsum_act_logits_publish", "E2_wait", "head",
+         "fp32-split7": ["fwd_mfma_and_prefetch_issue", "barrier_A", "zsum_act_logits_publish", "E2_wait", "head",
                   "barrier_B", "wgrad_mfma", "update"]}
 
 
 def main():
     prec = sys.argv[1] if len(sys.argv) > 1 else "fp32"
-    names = NAMES["fp32" if prec == "fp32-s28" else prec]
+    names = NAMES["fp32" if prec == "fp32-mfma" else prec]
     B, G = 100, 64
     dev = torch.device("cuda", 0)
     imgs, labels = synthetic_mnist(55000, seed=1)
@@ -65,7 +65,7 @@ def main():
     torch.cuda.synchronize()
     run.phase_ts = None
     raw = ts.cpu().numpy().reshape(65, 64, 16)
-    if prec in ("fp32", "fp32-s28"):
+    if prec in ("fp32", "fp32-mfma"):
         # launch stamps (row 64): compute wg 0 entry, 4 params loaded, 1 census done, 2 first stage read,
         # 3 loop done, 5 written back; copier 28+cid: 0 entry, 1 done. Relative to the earliest entry, us
         L = raw[64].astype(np.float64) * 0.01
@@ -79,7 +79,7 @@ def main():
             "written_back_max": rel(L[:28, 5].max()), "copier_entry_max": rel(L[28:44, 0].max()),
             "copier_done_max": rel(L[28:44, 1].max())}
         raw = raw[:64]
-    nj, nq = (7, 4) if prec in ("fp32", "fp32-s28") else (7, 1)
+    nj, nq = (7, 4) if prec in ("fp32", "fp32-mfma") else (7, 1)
     ns = len(names) + 1
     r = raw[1:G, : nj * nq, :ns].astype(np.float64) * 0.01   # us
     seg = {}
@@ -89,14 +89,14 @@ def main():
     out["segments_us_median_p90"] = seg
     step = r[1:, :, 0] - r[:-1, :, 0]
     out["step_us_median"] = round(float(np.median(step)), 3)
-    pub = 6 if prec in ("fp32", "fp32-s28") else 3
+    pub = 6 if prec in ("fp32", "fp32-mfma") else 3
     got = pub + 1
     last = r[:, :, pub].max(axis=1, keepdims=True)
     hop = r[:, :, got] - last
     out["logit_edge_hop_after_last_publish_us_median_p90"] = [round(float(np.median(hop)), 3),
                                                                round(float(np.percentile(hop, 90)), 3)]
     out["logit_publish_skew_us_median"] = round(float(np.median(r[:, :, pub].max(1) - r[:, :, pub].min(1))), 3)
-    if prec in ("fp32", "fp32-s28"):
+    if prec in ("fp32", "fp32-mfma"):
         # extra stamps: 13 wave 7 forward done, 14 wave 7 step start, 15 wave 3 forward done
         med = lambda x: round(float(np.median(x)), 3)
         rs = raw[1:G, : nj * nq, :].astype(np.float64) * 0.01
@@ -106,7 +106,7 @@ def main():
             "barrier_A_exit": med(rs[:, :, 2] - rs[:, :, 0])}
     late = (r[:, :, 0] - r[:, :, 0].min(axis=1, keepdims=True)).mean(axis=0)
     out["step_start_lateness_us_by_wg"] = np.round(late, 2).tolist()
-    if prec == "fp32-split":
+    if prec == "fp32-split7":
         rr = raw[1:G, :7, :].astype(np.float64) * 0.01
         med = lambda x: round(float(np.median(x)), 3)
         out["x3_fwd_detail_us"] = {"w0_start_to_mfma_done": med(rr[:, :, 9] - rr[:, :, 0]),

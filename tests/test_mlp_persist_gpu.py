@@ -24,7 +24,7 @@ def _ref_run(p0, imgs, labels, B, batches, lr, act="sigmoid"):
     return p, np.array(losses), np.array(accs)
 
 
-@pytest.mark.parametrize("engine", ["fp32", "fp32-split", "fp32-s28"])
+@pytest.mark.parametrize("engine", ["fp32", "fp32-mfma", "fp32-split7"])
 @pytest.mark.parametrize("B", [100, 37, 112])
 @pytest.mark.parametrize("act", ["sigmoid", "relu"])
 def test_persist_f32_one_step_gradient_fp32_exact(native, B, act, engine):
@@ -55,7 +55,7 @@ def test_persist_f32_one_step_gradient_fp32_exact(native, B, act, engine):
     assert abs(m[1] - acc.item()) < 1e-6
 
 
-@pytest.mark.parametrize("engine", ["fp32", "fp32-split", "fp32-s28"])
+@pytest.mark.parametrize("engine", ["fp32", "fp32-mfma", "fp32-split7"])
 def test_persist_f32_multi_step_matches_reference(native, engine):
     """11 steps over wrapping chunks (cold start, in-kernel prefetch, offsets into
     a staged chunk, epoch wrap): fp32 engine tracks fp32 SGD to ~1e-6."""
@@ -85,7 +85,7 @@ def test_persist_f32_multi_step_matches_reference(native, engine):
     assert np.allclose(m[:, 1], accs, atol=1e-6)
 
 
-@pytest.mark.parametrize("precision", ["fp32", "fp32-split", "fp32-s28", "fp16"])
+@pytest.mark.parametrize("precision", ["fp32", "fp32-mfma", "fp32-split7", "fp16"])
 def test_persist_short_timed_run_streams_only_what_it_computes(native, precision):
     """The bench's pattern: warmup(5) primes exactly the timed run's chunk; the
     timed run(20) needs no copy-only launch and prefetches <= 20 steps; the
@@ -163,7 +163,7 @@ def test_persist_chunks_wrap_and_match_reference(native):
     assert np.allclose(m[:, 1], accs, atol=1e-6)
 
 
-@pytest.mark.parametrize("precision", ["fp32", "fp32-split", "fp32-s28", "fp16"])
+@pytest.mark.parametrize("precision", ["fp32", "fp32-mfma", "fp32-split7", "fp16"])
 def test_persist_deterministic_and_hands_over_to_step_path(native, precision):
     B = 100
     imgs, labels = synthetic_mnist(B * 4, seed=13)
@@ -190,7 +190,7 @@ def test_persist_deterministic_and_hands_over_to_step_path(native, precision):
     assert ((g_k - g).norm() / g.norm()).item() < 3e-2
 
 
-@pytest.mark.parametrize("precision", ["fp32", "fp32-split", "fp32-s28", "fp16"])
+@pytest.mark.parametrize("precision", ["fp32", "fp32-mfma", "fp32-split7", "fp16"])
 def test_persist_long_run_learns(native, precision):
     """1000 steps on synthetic MNIST: loss goes down."""
     B = 100
@@ -209,8 +209,8 @@ def test_persist_long_run_learns(native, precision):
 
 @pytest.mark.parametrize("precision,grad,exchange", [("fp32", "bf16", "one-shot"), ("fp32", "fp32", "one-shot"),
                                                      ("fp32", "bf16", "two-shot"), ("fp32", "fp32", "two-shot"),
-                                                     ("fp32-split", "fp32", "one-shot"), ("fp16", "bf16", "one-shot"),
-                                                     ("fp32-s28", "bf16", "one-shot"), ("fp32-s28", "fp32", "two-shot")])
+                                                     ("fp32-mfma", "bf16", "one-shot"), ("fp32-mfma", "fp32", "two-shot"),
+                                                     ("fp32-split7", "fp32", "one-shot"), ("fp16", "bf16", "one-shot")])
 @pytest.mark.parametrize("nproc", [2, 3])
 def test_persist_multi_rank_same_gpu(native, nproc, precision, grad, exchange):
     """N ranks sharing cuda:0: in-kernel IPC exchange, bit-identical replicas, sync-SGD math."""

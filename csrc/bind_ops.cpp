@@ -8,6 +8,10 @@
 #include <string>
 
 extern "C" {
+hipError_t dtfk_hogwild_pull(const float* shared, float* local, long long n, hipStream_t s);
+hipError_t dtfk_hogwild_sgd(float* shared, const float* g, float* local, float lr, long long n, int locking,
+                            unsigned long long* counter, long long* gstep_out, hipStream_t s);
+hipError_t dtfk_hogwild_counter(unsigned long long* counter, long long* out, long long set, int do_set, hipStream_t s);
 hipError_t dtfk_bucket_pack_bf16(const float* g, uint16_t* c, int64_t n, float scale, hipStream_t s);
 hipError_t dtfk_bucket_unpack_bf16(const uint16_t* c, float* g, int64_t n, float scale, hipStream_t s);
 int dtfk_route_max_world();
@@ -320,7 +324,38 @@ void bucket_unpack_bf16(at::Tensor c, at::Tensor g, double scale) {
      "bucket_unpack_bf16");
 }
 
+// Hogwild parameter store (csrc/kernels/hogwild.hip): `shared` / `counter` are
+// raw device addresses (an IPC-mapped peer buffer); local / grads / gstep_out GPU tensors.
+static void hogwild_pull(int64_t shared, at::Tensor local) {
+  gpu(local, "local");
+  if (local.scalar_type() != at::kFloat || !local.is_contiguous()) throw std::runtime_error("hogwild: fp32 contiguous");
+  ck(dtfk_hogwild_pull(reinterpret_cast<const float*>(shared), local.data_ptr<float>(), local.numel(), cs()),
+     "hogwild_pull");
+}
+static void hogwild_sgd(int64_t shared, at::Tensor grads, at::Tensor local, double lr, bool locking, int64_t counter,
+                        at::Tensor gstep_out) {
+  gpu(grads, "grads"); gpu(local, "local"); gpu(gstep_out, "gstep_out");
+  if (grads.scalar_type() != at::kFloat || local.scalar_type() != at::kFloat || !grads.is_contiguous() ||
+      !local.is_contiguous() || grads.numel() != local.numel() || gstep_out.scalar_type() != at::kLong)
+    throw std::runtime_error("hogwild_sgd: fp32 contiguous grads/local of one size, int64 gstep_out");
+  ck(dtfk_hogwild_sgd(reinterpret_cast<float*>(shared), grads.data_ptr<float>(), local.data_ptr<float>(), (float)lr,
+                      local.numel(), locking ? 1 : 0, reinterpret_cast<unsigned long long*>(counter),
+                      reinterpret_cast<long long*>(gstep_out.data_ptr<int64_t>()), cs()),
+     "hogwild_sgd");
+}
+static void hogwild_counter(int64_t counter, at::Tensor out, int64_t set, bool do_set) {
+  gpu(out, "out");
+  ck(dtfk_hogwild_counter(reinterpret_cast<unsigned long long*>(counter), reinterpret_cast<long long*>(out.data_ptr<int64_t>()), set, do_set ? 1 : 0,
+                          cs()),
+     "hogwild_counter");
+}
+
 void init_ops(py::module& m) {
+  m.def("hogwild_pull", &hogwild_pull, py::arg("shared"), py::arg("local"));
+  m.def("hogwild_sgd", &hogwild_sgd, py::arg("shared"), py::arg("grads"), py::arg("local"), py::arg("lr"),
+        py::arg("locking"), py::arg("counter"), py::arg("gstep_out"));
+  m.def("hogwild_counter", &hogwild_counter, py::arg("counter"), py::arg("out"), py::arg("set") = 0,
+        py::arg("do_set") = false);
   m.def("bucket_pack_bf16", &bucket_pack_bf16);
   m.def("bucket_unpack_bf16", &bucket_unpack_bf16);
   m.def("sparse_route", &sparse_route, py::arg("sids"), py::arg("perm"), py::arg("W"), py::arg("cap"));

@@ -57,6 +57,19 @@ def _to_numpy(v):
     return v
 
 
+def _pre_run_hooks(fetches) -> list:
+    out, stack = [], [fetches]
+    while stack:
+        f = stack.pop()
+        if isinstance(f, (list, tuple)):
+            stack.extend(f)
+        elif isinstance(f, dict):
+            stack.extend(f.values())
+        elif getattr(f, "_pre_run", None) is not None:
+            out.append(f._pre_run)
+    return out
+
+
 class Session:
     def __init__(self, target: str = "", graph=None, config: ConfigProto = None):
         self.target = target
@@ -76,6 +89,8 @@ class Session:
         ctx.options = options
         if ctx.device.type == "cuda":
             _lowering.try_lower(self, fetches, ctx)     # fused kernels for matched train ops
+        for hook in _pre_run_hooks(fetches):           # async train ops: pull the ps variables first
+            hook()
         out = self._run(fetches, ctx)
         if self._post_run and not self._in_post:
             # step-boundary services (Supervisor checkpoints): run in the training

@@ -26,6 +26,7 @@ import torch
 from .. import optim as _optim
 from ..utils import debug as _debug
 from ..utils import profiling as _prof
+from ..parallel import async_ps as _async_ps
 from ..parallel import world as _world
 from ..parallel.cluster import ClusterSpec, Rendezvous, split_address
 from ..utils import logging as _log
@@ -296,10 +297,14 @@ class Optimizer:
     _kind = "sgd"
     _slot_names: Sequence[str] = ()
 
-    def __init__(self, learning_rate, use_locking=False, name=None, **kw):
+    def __init__(self, learning_rate, use_locking=False, name=None, update_mode=None, **kw):
         self.learning_rate = learning_rate
         self.name = name or type(self).__name__.replace("Optimizer", "")
         self._kw = kw
+        self.use_locking = bool(use_locking)
+        # 'sync' (default: all-reduce data parallelism, the north star) or 'async'
+        # (the reference's Hogwild ps updates, parallel/async_ps.py); None: $DTF_UPDATE_MODE
+        self.update_mode = update_mode
         self.sync_replicas = True
         self.comm_dtype = None
         self._steps = 0
@@ -359,6 +364,8 @@ class Optimizer:
         if fused is not None:
             opt._register_slots(vars_, fused)
         sync = _GradSync(params, opt.comm_dtype) if params else None
+        if _async_ps.update_mode(opt.update_mode) == "async":
+            return self._apply_async(vars_, gtens, params, sparse_pairs, global_step, name)
 
         def run(ctx):
             w = _world_or_local()
@@ -394,6 +401,40 @@ class Optimizer:
         # this op by fused kernels
         op._lowering = {"opt": opt, "vars": vars_, "fused": fused, "sync": sync, "global_step": global_step,
                         "sparse": sparse_pairs}
+        return op
+
+    def _apply_async(self, vars_, gtens, params, sparse_pairs, global_step, name) -> Operation:
+        """The reference's asynchronous update (example.py:106-118 without
+        SyncReplicasOptimizer): pull the ps variables, gradient of this worker's
+        batch, `var -= lr * grad` on the ps variables with no waiting, global_step
+        = every worker's updates so far (parallel/async_ps.py)."""
+        if self._kind != "sgd" or sparse_pairs:
+            raise NotImplementedError("asynchronous (Hogwild) updates: GradientDescentOptimizer on dense "
+                                      "variables only (update_mode='sync' handles the rest)")
+        opt = self
+        state = {}
+
+        def run(ctx):
+            w = _world_or_local()
+            opt._steps += 1
+            _debug.fault_point(opt._steps, w.rank)
+            if "store" not in state:      # collective: every worker's first train step
+                state["store"] = _async_ps.HogwildStore(params, w, use_locking=opt.use_locking)
+            store = state["store"]
+            with _prof.range("compute_gradients"):
+                gs = [ctx.eval(g) if g is not None else None for g in gtens]
+            with _prof.range("hogwild_update"):
+                gstep = store.sgd_step(gs, opt._lr_value())
+            if global_step is not None:
+                with torch.no_grad():
+                    global_step.value.data.fill_(float(gstep))
+            return None
+        op = Operation(None, [], name or self.name)
+        op._eval = run
+        op._async_state = state
+        # Session.run calls this before evaluating anything: the forward of this
+        # run reads the ps variables as they are now (other workers' updates included)
+        op._pre_run = lambda: state["store"].pull() if "store" in state else None
         return op
 
     def minimize(self, loss, global_step=None, var_list=None, name=None, **kw) -> Operation:
@@ -553,6 +594,7 @@ class SyncReplicasOptimizer(Optimizer):
 
     def apply_gradients(self, grads_and_vars, global_step=None, name=None):
         self.opt.sync_replicas = True
+        self.opt.update_mode = "sync"     # aggregation is the point of this wrapper
         return self.opt.apply_gradients(grads_and_vars, global_step, name)
 
     def get_init_tokens_op(self, num_tokens=-1):

@@ -10,10 +10,12 @@ Cluster: `--ps_hosts/--worker_hosts` (comma lists) or `--cluster_conf` JSON
 (cluster_conf.json shape); defaults mirror example.py:23-30 on localhost.
 
 What differs from the reference (README "semantics"):
-* workers train *synchronously*: every train_op run averages the gradients of
-  all workers (RCCL all-reduce on MI355X, gloo on CPU) -- the
+* workers train *synchronously* by default: every train_op run averages the
+  gradients of all workers (RCCL all-reduce on MI355X, gloo on CPU) -- the
   SyncReplicasOptimizer path the reference left commented out
-  (example.py:109-123) is the only path; global_step counts sync steps;
+  (example.py:109-123); global_step counts sync steps.  `--update_mode=async`
+  runs the reference's own asynchronous rule instead (Hogwild updates of shared
+  variables, global_step counts every worker's step);
 * chief initialises and broadcasts (no re-init race); ps tasks exit from
   `server.join()` once every worker has finished;
 * input is the synthetic MNIST-shaped set (no network): same shapes/dtypes;
@@ -59,6 +61,9 @@ flags.DEFINE_string("checkpoint_dir", "", "Supervisor logdir: restore on start, 
 flags.DEFINE_integer("save_model_secs", 600, "checkpoint period (chief, seconds)")
 flags.DEFINE_integer("save_model_steps", 0, "checkpoint every N global steps (all ranks agree; overrides secs)")
 flags.DEFINE_string("metrics_jsonl", "", "append JSON-lines step metrics here")
+flags.DEFINE_string("update_mode", "sync", "sync: every train_op run all-reduces the workers' gradients (default); "
+                    "async: the reference's Hogwild ps updates -- each worker applies its own gradient to the "
+                    "shared variables without waiting (parallel/async_ps.py), global_step counts every worker's step")
 FLAGS = flags.FLAGS
 
 
@@ -93,7 +98,7 @@ def build_graph(cluster, task_index):
         with tf.name_scope("cross_entropy"):
             cross_entropy = tf.reduce_mean(-tf.reduce_sum(y_ * tf.log(y), reduction_indices=[1]))
         with tf.name_scope("train"):
-            train_op = tf.train.GradientDescentOptimizer(FLAGS.learning_rate).minimize(
+            train_op = tf.train.GradientDescentOptimizer(FLAGS.learning_rate, update_mode=FLAGS.update_mode).minimize(
                 cross_entropy, global_step=global_step)
         with tf.name_scope("Accuracy"):
             correct = tf.equal(tf.argmax(y, 1), tf.argmax(y_, 1))

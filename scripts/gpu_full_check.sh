@@ -6,4 +6,5 @@ run() { name=$1; shift; t=$1; shift; timeout -k 10 $t "$@" > gpurun_out/$name.lo
 run smoke 180 python -c "import __graft_entry__ as g; g.smoke()" &&
 run pytest_gpu 1000 python -u -m pytest -v --timeout 300 --timeout-method thread tests -m gpu &&
 run b20 120 python bench.py --gpus 1 --steps 20 --warmup 5 &&
-run b5500 240 python bench.py --gpus 1
+run b5500 240 python bench.py --gpus 1 &&
+run rp_b5500 300 rocprofv3 --kernel-trace --stats -d gpurun_out/rp_b5500 -o rp -- python bench.py --gpus 1

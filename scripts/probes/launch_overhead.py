@@ -99,7 +99,25 @@ def bench_like():
             torch.cuda.synchronize()
             walls.append((time.perf_counter() - t0) * 1e6)
         res[f"gap_{gap_ms}ms"] = [round(w, 1) for w in walls]
-    print(json.dumps({"bench_like_wall_us": res}))
+    # one stamped timed run: when do the copiers (next chunk over PCIe) finish vs the compute loop
+    stamps = []
+    for rep in range(4):
+        run.prepare(5)
+        run.run(5, lookahead=20)
+        run.prepare(20)
+        torch.cuda.synchronize()
+        ts = torch.zeros(65 * 64 * 16, dtype=torch.int64, device=dev)
+        run.phase_ts = ts
+        run.run(20)
+        torch.cuda.synchronize()
+        run.phase_ts = None
+        L = ts.cpu().numpy().reshape(65, 64, 16)[64].astype(np.float64) * 0.01
+        t0 = min(L[:28, 0].min(), L[28:44, 0].min())
+        stamps.append({"step0_start": round(float(ts.cpu().numpy().reshape(65, 64, 16)[0, :28, 0].max() * 0.01 - t0), 2),
+                       "loop_done": round(float(L[:28, 3].max() - t0), 2),
+                       "copier_done": round(float(L[28:44, 1].max() - t0), 2),
+                       "copier_entry": round(float(L[28:44, 0].max() - t0), 2)})
+    print(json.dumps({"bench_like_wall_us": res, "timed_run_launch_stamps_us": stamps}))
 
 
 if __name__ == "__main__" and os.environ.get("BENCH_LIKE"):

@@ -427,6 +427,90 @@ void mlp_persist_f32(at::Tensor stage, int64_t rec_h, int B, int nsteps, at::Ten
             "mlp_persist_f32");
 }
 
+// A prepared launcher for the fp32 persistent engine: every tensor checked and
+// every pointer resolved once, so a launch from Python is a call with 6 ints
+// (the generic binding's ~27 keyword arguments and per-call checks cost ~10 us
+// of host time on a 20-step run: scripts/probes/launch_overhead.py).
+struct PersistF32Plan {
+  at::Tensor stage0, stage1, params, lr, metrics, gstep, seq, xbuf, err, step_ts, host;
+  void* st[2];
+  const char* host_dev = nullptr;
+  int64_t host_bytes = 0, rec_h = 0, rec_s = 0;
+  int B, act, naive, ring, ts_ring = 1, W, rank, gbf16, spread, two_shot, split;
+  long long ticks;
+  int64_t ipc_table;
+
+  PersistF32Plan(at::Tensor s0, at::Tensor s1, int64_t rec_h_, int B_, at::Tensor params_, at::Tensor lr_,
+                 at::Tensor metrics_, at::Tensor gstep_, at::Tensor seq_, at::Tensor xbuf_, at::Tensor err_,
+                 double timeout_s, int act_, int naive_, at::Tensor host_, at::Tensor step_ts_, int64_t ipc_table_,
+                 int ipc_W, int ipc_rank, bool grad_bf16, bool spread_, bool two_shot_, bool mfma_split)
+      : stage0(s0), stage1(s1), params(params_), lr(lr_), metrics(metrics_), gstep(gstep_), seq(seq_), xbuf(xbuf_),
+        err(err_), step_ts(step_ts_), host(host_) {
+    if (ipc_W > 1 && (ipc_table_ == 0 || ipc_rank < 0 || ipc_rank >= ipc_W || ipc_W > 64))
+      throw std::runtime_error("PersistF32Plan: N-GPU exchange needs the IPC peer table");
+    if (B_ <= 0 || B_ > dtfk_mlpf_max_batch()) throw std::runtime_error("PersistF32Plan: B out of range");
+    if (rec_h_ < (int64_t)B_ * 785 || rec_h_ % 16 != 0) throw std::runtime_error("PersistF32Plan: bad record size");
+    rec_s = dtfk_mlpf_stage_rec();
+    need(stage0, at::kByte, rec_s, "stage0");
+    need(stage1, at::kByte, rec_s, "stage1");
+    need(params, at::kFloat, kNParam, "params");
+    need(lr, at::kFloat, 1, "lr");
+    need(metrics, at::kFloat, 2, "metrics");
+    need(gstep, at::kLong, 1, "gstep");
+    need(seq, at::kLong, 1, "seq");
+    need(xbuf, at::kByte, dtfk_mlpf_xbuf_bytes(), "xbuf");
+    need(err, at::kInt, 1, "err");
+    need(step_ts, at::kLong, 2, "step_ts");
+    st[0] = stage0.data_ptr();
+    st[1] = stage1.data_ptr();
+    if ((((uintptr_t)st[0]) | ((uintptr_t)st[1]) | (uintptr_t)xbuf.data_ptr()) % 16 != 0)
+      throw std::runtime_error("PersistF32Plan: stage / xbuf must be 16-byte aligned");
+    host_bytes = host.numel() * host.element_size();
+    host_dev = static_cast<const char*>(pinned_device_ptr(host, 0, host_bytes));
+    rec_h = rec_h_;
+    B = B_;
+    act = act_;
+    naive = naive_;
+    ring = (int)(metrics.numel() / 2);
+    ts_ring = (int)step_ts.numel();
+    ticks = (long long)(timeout_s * 1e8);
+    ipc_table = ipc_table_;
+    W = ipc_W > 1 ? ipc_W : 1;
+    rank = ipc_W > 1 ? ipc_rank : 0;
+    gbf16 = grad_bf16 ? 1 : 0;
+    spread = spread_ ? 1 : 0;
+    two_shot = two_shot_ ? 1 : 0;
+    split = mfma_split ? 1 : 0;
+  }
+
+  // nsteps steps from stage `par` at step offset `off`; next_steps host records from
+  // byte host_off into stage par ^ 1 (same contract as mlp_persist_f32 above)
+  void launch(int par, int64_t off, int nsteps, int64_t host_off, int next_steps) {
+    if ((par & ~1) != 0 || nsteps < 0 || next_steps < 0 || off < 0) throw std::runtime_error("PersistF32Plan: args");
+    const at::Tensor& cur = par ? stage1 : stage0;
+    const at::Tensor& nxt = par ? stage0 : stage1;
+    if ((off + std::max(nsteps, 1)) * rec_s > cur.numel()) throw std::runtime_error("PersistF32Plan: stage overrun");
+    const void* hn = nullptr;
+    void* sn = nullptr;
+    if (next_steps > 0) {
+      if ((int64_t)next_steps * rec_s > nxt.numel()) throw std::runtime_error("PersistF32Plan: next stage too small");
+      if (host_off < 0 || host_off % 16 != 0 || host_off + (int64_t)next_steps * rec_h > host_bytes)
+        throw std::runtime_error("PersistF32Plan: host range out of bounds");
+      hn = host_dev + host_off;
+      sn = st[par ^ 1];
+    }
+    hip_check(dtfk_mlp_persist_f32(static_cast<const char*>(st[par]) + off * rec_s, rec_h, B, nsteps,
+                                   params.data_ptr<float>(), lr.data_ptr<float>(), metrics.data_ptr<float>(), ring,
+                                   act, naive, reinterpret_cast<long long*>(gstep.data_ptr<int64_t>()),
+                                   reinterpret_cast<unsigned long long*>(seq.data_ptr<int64_t>()), xbuf.data_ptr(),
+                                   err.data_ptr<int>(), ticks,
+                                   reinterpret_cast<long long*>(step_ts.data_ptr<int64_t>()), ts_ring, hn,
+                                   next_steps, sn, reinterpret_cast<void* const*>(ipc_table), W, rank, gbf16,
+                                   nullptr, spread, two_shot, split, cur_stream()),
+              "PersistF32Plan.launch");
+  }
+};
+
 // The compat graph's matched MLP training step (csrc/kernels/graph_mlp.hip).
 // sgd: W/b updated in place with lr; else gradients into g* (same shapes).
 void graph_mlp_step(at::Tensor x, at::Tensor ylab, at::Tensor W1, at::Tensor b1, at::Tensor W2, at::Tensor b2,
@@ -495,6 +579,11 @@ void init_mlp(py::module& m) {
         py::arg("step_ts") = py::none(), py::arg("ipc_table") = 0, py::arg("ipc_W") = 1, py::arg("ipc_rank") = 0,
         py::arg("grad_bf16") = true, py::arg("phase_ts") = py::none(), py::arg("spread") = false,
         py::arg("exact_split") = false, py::arg("two_shot") = false, py::arg("mfma_split") = false);
+  py::class_<PersistF32Plan>(m, "PersistF32Plan")
+      .def(py::init<at::Tensor, at::Tensor, int64_t, int, at::Tensor, at::Tensor, at::Tensor, at::Tensor,
+                    at::Tensor, at::Tensor, at::Tensor, double, int, int, at::Tensor, at::Tensor, int64_t, int, int,
+                    bool, bool, bool, bool>())
+      .def("launch", &PersistF32Plan::launch);
   m.def("mlpx_stage_rec", &dtfk_mlpx_stage_rec);
   m.def("mlpx_xbuf_bytes", &dtfk_mlpx_xbuf_bytes);
   m.def("mlpx_ipc_bytes", &dtfk_mlpx_ipc_bytes);

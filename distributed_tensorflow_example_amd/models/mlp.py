@@ -517,6 +517,7 @@ class PersistentMLPRunner:
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
         self.step_ts = torch.zeros(self.TS_RING, dtype=torch.int64, device=dev)
         self.phase_ts = None    # fp32 engine: optional [64 steps][64 wg][16] phase stamps (profiling)
+        self._plan = None       # fp32 engine: prepared C++ launcher (PersistF32Plan)
         self.cursor = 0
         self.staged: List[Optional[Tuple[int, int]]] = [None, None]   # (b0, g) resident per stage buffer
         self.copy_only_launches = 0
@@ -551,7 +552,15 @@ class PersistentMLPRunner:
         t, ep = self.t, self.epoch
         dst = par ^ 1
         ipc = dict(ipc_table=self.ipc.table_ptr() if self.ipc is not None else 0, ipc_W=self.W, ipc_rank=self.rank)
-        if self.f32:
+        if self.f32 and not self.exact_split and self.phase_ts is None:
+            if self._plan is None:   # every pointer resolved once (host-side launch cost)
+                self._plan = t.C.PersistF32Plan(
+                    self.stages[0], self.stages[1], ep.rec, t.B, t.params, t.lr, t.metrics, t.gstep, self.seq,
+                    self.xbuf, self.err, self.timeout_s, t.act, int(t.naive), ep.host, self.step_ts,
+                    ipc["ipc_table"], self.W, self.rank, self.grad_bf16, self.placement == "spread",
+                    self.exchange == "two-shot", self.mfma_split)
+            self._plan.launch(par, off if nsteps > 0 else 0, nsteps, nxt[0] * ep.rec, nxt[1])
+        elif self.f32:
             st = self.stages[par][off * self.rec_s:] if nsteps > 0 else self.stages[par]
             t.C.mlp_persist_f32(st, ep.rec, t.B, nsteps, t.params, t.lr, t.metrics, t.gstep, self.seq, self.xbuf,
                                 self.err, self.timeout_s, t.act, int(t.naive), host=ep.host,

@@ -24,6 +24,9 @@ hipError_t dtfk_philox_normal(float* out, long long rows, int dim, long long row
 hipError_t dtfk_gemm(const void* A, int a_bf16, int lda, int transA, const void* B, int b_bf16, int ldb,
                      int transB, void* C, int c_bf16, int ldc, float* Z, const float* bias, int M, int N,
                      int K, float alpha, float beta, int act, hipStream_t stream);
+hipError_t dtfk_gemm_big(const void* A, int lda, int transA, const void* B, int ldb, int transB, void* C,
+                         int c_bf16, int ldc, const float* bias, int M, int N, int K, float alpha, float beta,
+                         int act, int split_k, hipStream_t stream);
 hipError_t dtfk_act_backward(const float* dy, const float* y, const float* z, float* dz, int64_t n, int act,
                              hipStream_t s);
 hipError_t dtfk_col_sum(const float* X, float* out, int M, int N, hipStream_t s);
@@ -104,6 +107,35 @@ void gemm(at::Tensor A, bool transA, at::Tensor B, bool transB, at::Tensor out,
                out.scalar_type() == at::kBFloat16, (int)out.stride(0), opt_ptr<float>(Z), opt_ptr<float>(bias),
                M, N, K, (float)alpha, (float)beta, act, cs()),
      "gemm");
+}
+
+// Large-tile bf16 GEMM (gemm_big.hip): out = act(alpha * op(A) @ op(B) + bias) (+ beta * out).
+// bf16 operands, bf16 or fp32 out.  Returns false (nothing launched) when the
+// shape is outside the kernel's contract (K % 64, alignment), so callers can
+// pick another GEMM; dtype / rank errors throw.
+bool gemm_big(at::Tensor A, bool transA, at::Tensor B, bool transB, at::Tensor out, c10::optional<at::Tensor> bias,
+              int act, double alpha, double beta, int split_k) {
+  gpu(A, "A"); gpu(B, "B"); gpu(out, "out");
+  if (A.dim() != 2 || B.dim() != 2 || out.dim() != 2) throw std::runtime_error("gemm_big operands must be 2-D");
+  if (A.scalar_type() != at::kBFloat16 || B.scalar_type() != at::kBFloat16)
+    throw std::runtime_error("gemm_big: bf16 operands");
+  if (out.scalar_type() != at::kBFloat16 && out.scalar_type() != at::kFloat)
+    throw std::runtime_error("gemm_big: bf16 or float32 output");
+  if (A.stride(1) != 1 || B.stride(1) != 1 || out.stride(1) != 1)
+    throw std::runtime_error("gemm_big operands must have unit inner stride");
+  const int M = (int)(transA ? A.size(1) : A.size(0));
+  const int K = (int)(transA ? A.size(0) : A.size(1));
+  const int KB = (int)(transB ? B.size(1) : B.size(0));
+  const int N = (int)(transB ? B.size(0) : B.size(1));
+  if (K != KB) throw std::runtime_error("gemm_big inner dimensions differ");
+  if (out.size(0) != M || out.size(1) != N) throw std::runtime_error("gemm_big out has wrong shape");
+  if (bias.has_value()) { f32c(*bias, "bias"); if (bias->numel() != N) throw std::runtime_error("bias size"); }
+  const hipError_t e = dtfk_gemm_big(A.data_ptr(), (int)A.stride(0), transA, B.data_ptr(), (int)B.stride(0), transB,
+                                     out.data_ptr(), out.scalar_type() == at::kBFloat16, (int)out.stride(0),
+                                     opt_ptr<float>(bias), M, N, K, (float)alpha, (float)beta, act, split_k, cs());
+  if (e == hipErrorInvalidValue) { (void)hipGetLastError(); return false; }
+  ck(e, "gemm_big");
+  return true;
 }
 
 void act_backward(at::Tensor dy, c10::optional<at::Tensor> y, c10::optional<at::Tensor> z, at::Tensor dz,
@@ -365,6 +397,9 @@ void init_ops(py::module& m) {
   m.def("gemm", &gemm, py::arg("A"), py::arg("transA"), py::arg("B"), py::arg("transB"), py::arg("out"),
         py::arg("bias") = py::none(), py::arg("act") = 0, py::arg("alpha") = 1.0, py::arg("beta") = 0.0,
         py::arg("Z") = py::none());
+  m.def("gemm_big", &gemm_big, py::arg("A"), py::arg("transA"), py::arg("B"), py::arg("transB"), py::arg("out"),
+        py::arg("bias") = py::none(), py::arg("act") = 0, py::arg("alpha") = 1.0, py::arg("beta") = 0.0,
+        py::arg("split_k") = 0);
   m.def("act_backward", &act_backward);
   m.def("col_sum", &col_sum);
   m.def("softmax_xent", &softmax_xent);

@@ -1,0 +1,300 @@
+// Large-tile bf16 MFMA GEMM for the transformer-size products (BERT-base:
+// T = B*S = 16384 token rows, 768 / 2304 / 3072 wide):
+//
+//   C[M,N] = act(alpha * A'[M,K] B'[K,N] + bias[N]) (+ beta * C)      fp32 accumulate
+//
+// A' = A (row-major [M,K], K contiguous) or A^T (A stored [K,M], M contiguous);
+// B' = B^T (B stored [N,K], K contiguous) or B (stored [K,N], N contiguous).
+// That covers all three products of a linear layer without a transpose copy:
+// forward y = x W^T (K-contig x K-contig), input gradient dX = dY W (K-contig x
+// N-contig) and weight gradient dW = dY^T X (M-contig x N-contig).
+//
+// CDNA4 design (cdna_hip_programming.md s5):
+//  * 512-thread workgroup = 8 waves (2 along M x 4 along N), output tile BM x 256
+//    (BM = 256: each wave owns 128x64 = 8x4 MFMA 16x16x32 accumulators, 128
+//    VGPRs of fp32), K-step 64.
+//  * Operands go HBM -> LDS with LDS-DMA (`global_load_lds_dwordx4`), never
+//    through VGPRs: each wave instruction fills 1 KiB of lane-linear LDS, so the
+//    bank-conflict swizzle is applied to the per-lane GLOBAL source address and
+//    undone on the read (rule 21: linear destination, swizzled source + read).
+//  * An S-stage ring of BK-deep K tiles in ONE __shared__ array (forward: BK 32,
+//    S 5 = 160 KiB at BM = 256; transposed-read layouts: BK 64, S 2): while
+//    tile t is multiplied, tiles t+1 .. t+S-1 are in flight; the wait is a
+//    counted `s_waitcnt vmcnt(N)` and a raw s_barrier, so the prefetch
+//    survives the barrier (a workgroup LDS fence would drain it: the DMA is a
+//    pending LDS write on the vector-memory counter).
+//  * Measured (rocprofv3 PMC, 16384x3072x768): ~8 B/clk/CU of LDS-DMA fill
+//    with a 77 % L2 hit rate bounds the loop at ~25 % MFMA utilisation -- the
+//    operand delivery, not the MFMA issue, is this kernel's limit; hipBLASLt
+//    stays ~2x faster on the large forward/backward shapes, so models pick
+//    per shape (ops/big_gemm.py: use_native) and this kernel runs where it wins.
+//  * K-contiguous images are [rows][BK] with a 16-byte chunk XOR that puts the
+//    16 lanes of a ds_read_b128 group on 16 distinct slots of a bank row.
+//  * M/N-contiguous images are [BK k][rows] and are read with the hardware
+//    transpose `ds_read_b64_tr_b16` (two per fragment); 32-byte groups XOR
+//    (k&3 | (k>>3&1)<<2) keep the 8 k-rows of a 32-lane half on distinct banks.
+//  * XCD-aware tile order (bijective remap): a row band's tiles share one L2.
+//  * Split-K over gridDim.y for the few-tile, long-K weight gradients: fp32
+//    partial tiles meet by atomics in C (which may already hold the gradient
+//    to accumulate into -- beta = 1 is free).
+// Shape contract (checked on the host): K % 64 == 0; 16-byte aligned bases and
+// leading dimensions; an M/N-contiguous operand's M (or N) is a multiple of 8.
+// Row/column tails are clamped (their products only reach unstored outputs).
+#include "common.h"
+
+namespace dtfk {
+namespace gemm2 {
+
+constexpr int BN = 256, NTHR = 512;
+constexpr int KQ = 64;   // K granule of the shape contract / split-K chunks
+
+typedef __attribute__((address_space(3))) void lvoid;
+typedef __attribute__((address_space(1))) void gvoid;
+typedef __attribute__((ext_vector_type(4))) short v4s;
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+
+enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_SIGMOID = 2, ACT_TANH = 3, ACT_GELU = 4 };
+
+// out of line: one call per output element keeps 128 inlined erff/tanhf
+// copies out of every instantiation's epilogue
+__device__ __attribute__((noinline)) float apply_act_slow(float z, int act) {
+  switch (act) {
+    case ACT_RELU: return fmaxf(z, 0.f);
+    case ACT_SIGMOID: return 1.f / (1.f + __expf(-z));
+    case ACT_TANH: return tanhf(z);
+    case ACT_GELU: return 0.5f * z * (1.f + erff(z * 0.70710678118654752f));
+    default: return z;
+  }
+}
+__device__ __forceinline__ float apply_act(float z, int act) { return act == ACT_NONE ? z : apply_act_slow(z, act); }
+
+// ---- LDS images ----------------------------------------------------------
+// K-contiguous [R][BK] bf16 (BK*2-byte rows, CPR 16-byte chunks per row): the
+// chunk XOR (r / (16/CPR)) & (CPR-1) puts the 16 rows of a ds_read_b128 lane
+// group on 16 distinct 16-byte slots of a 256-byte bank row.
+template <int BK>
+__device__ __forceinline__ int kc_off(int r, int c) {
+  constexpr int CPR = BK / 8;
+  return r * (BK * 2) + ((c ^ ((r / (16 / CPR)) & (CPR - 1))) << 4);
+}
+// M/N-contiguous [BK][R] bf16: byte offset of (k, 16-byte chunk ch = mn/8)
+__device__ __forceinline__ int mn_swz(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
+template <int R>
+__device__ __forceinline__ int mn_off(int k, int ch) { return k * (2 * R) + ((ch ^ (mn_swz(k) << 1)) << 4); }
+
+// Stage one operand tile (R rows of the output dimension x BK k) into `img`.
+// KC: src element (row, k) at base[row * ld + k]; else at base[k * ld + row].
+template <int R, int BK, bool KC>
+__device__ __forceinline__ void stage(const uint16_t* __restrict__ base, int ld, int rows, int r0, int k0,
+                                      uint8_t* img, int wave, int lane) {
+  constexpr int CPR = BK / 8;
+#pragma unroll
+  for (int j = 0; j < R * BK / 4096; ++j) {
+    const int wbase = (j * 8 + wave) << 10;    // this wave instruction's 1 KiB
+    const int o = wbase + (lane << 4);
+    const uint16_t* src;
+    if constexpr (KC) {
+      const int r = o / (BK * 2), c = ((o >> 4) % CPR) ^ ((r / (16 / CPR)) & (CPR - 1));
+      src = base + (size_t)min(r0 + r, rows - 1) * ld + k0 + c * 8;
+    } else {
+      const int k = o / (2 * R), ch = ((o % (2 * R)) >> 4) ^ (mn_swz(k) << 1);
+      src = base + (size_t)(k0 + k) * ld + min(r0 + ch * 8, rows - 8);
+    }
+    __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(img + wbase), 16, 0, 0);
+  }
+}
+
+// MFMA 16x16x32 operand fragment of rows [rb, rb+16), k-sub s (k = 32 s ...):
+// lane l gets (row rb + (l&15), k = 32 s + 8 (l>>4) + j), j = 0..7.
+template <int R, int BK, bool KC>
+__device__ __forceinline__ bf16x8 frag(const uint8_t* img, int rb, int s, int lane) {
+  if constexpr (KC) {
+    return *reinterpret_cast<const bf16x8*>(img + kc_off<BK>(rb + (lane & 15), s * 4 + (lane >> 4)));
+  } else {
+    // ds_read_b64_tr_b16: lane 4q+p of a 16-lane group addresses row k0+q,
+    // columns 4p..4p+3 of the 4x16 block; lane i receives column i, row q in q
+    const int k = s * 32 + 8 * (lane >> 4) + ((lane & 15) >> 2);
+    const int mn = rb + 4 * (lane & 3);
+    const int off = mn_off<R>(k, mn >> 3) + ((mn & 7) << 1);
+    const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(img + off));
+    const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(img + off + 4 * 2 * R));
+    typedef __attribute__((ext_vector_type(8))) short v8s;
+    const v8s v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+__device__ __forceinline__ void lds_sync() {
+  // raw barrier: this wave's ds_reads retired, an in-flight DMA (vmcnt) is NOT
+  // drained (a workgroup-scope LDS fence would wait vmcnt(0): the DMA counts
+  // as a pending LDS write).  The asm statements pin LDS accesses on their side.
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// wait until at most `ahead` stages (ND DMA instructions each) are in flight
+template <int ND>
+__device__ __forceinline__ void wait_stages(int ahead) {
+  switch (ahead) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ND) : "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * ND) : "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * ND) : "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * ND) : "memory"); break;
+  }
+}
+
+// S-stage ring of BK-deep K tiles: while tile t is multiplied, tiles t+1 ..
+// t+S-1 are in flight (S-1 stages of DMA bytes hide the HBM/L2 latency).
+template <int BM, int BK, int S, bool AKC, bool BKC, bool OBF>
+__global__ __launch_bounds__(NTHR) void gemm_big(const uint16_t* __restrict__ A, int lda,
+                                                 const uint16_t* __restrict__ B, int ldb, void* __restrict__ C,
+                                                 int ldc, const float* __restrict__ bias, int M, int N, int K,
+                                                 float alpha, float beta, int act, int kchunk) {
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int MT = BM / 32, NT = 4;                    // 16x16 tiles per wave (2 x 4 waves)
+  constexpr int NDMA = (BM + BN) * BK / 4096;            // DMA instructions per stage per thread
+  static_assert(S >= 2 && S <= 5 && S * STAGE <= 160 * 1024, "LDS ring");
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[S * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+
+  const int nt_n = (N + BN - 1) / BN;
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig % 8, q = nwg / 8, rem = nwg % 8;
+  const int wg = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + orig / 8;
+  const int m0 = (wg / nt_n) * BM, n0 = (wg % nt_n) * BN;
+  const int kb = blockIdx.y * kchunk, ke = min(K, kb + kchunk);
+  const int nk = (ke - kb) / BK;
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int p = 0; p < S - 1; ++p) {
+    if (p < nk) {
+      stage<BM, BK, AKC>(A, lda, M, m0, kb + p * BK, smem + p * STAGE, wave, lane);
+      stage<BN, BK, BKC>(B, ldb, N, n0, kb + p * BK, smem + p * STAGE + A_BYTES, wave, lane);
+    }
+  }
+  for (int t = 0; t < nk; ++t) {
+    const uint8_t* cur = smem + (t % S) * STAGE;
+    const int tn = t + S - 1;      // its buffer was last read in iteration t-1 (closing barrier)
+    if (tn < nk) {
+      uint8_t* nxt = smem + (tn % S) * STAGE;
+      stage<BM, BK, AKC>(A, lda, M, m0, kb + tn * BK, nxt, wave, lane);
+      stage<BN, BK, BKC>(B, ldb, N, n0, kb + tn * BK, nxt + A_BYTES, wave, lane);
+    }
+    wait_stages<NDMA>(min(S - 1, nk - 1 - t));   // tile t landed; later tiles stay in flight
+    lds_sync();
+    const uint8_t* ia = cur;
+    const uint8_t* ib = cur + A_BYTES;
+#pragma unroll
+    for (int s = 0; s < BK / 32; ++s) {
+      bf16x8 fb[NT];
+#pragma unroll
+      for (int j = 0; j < NT; ++j) fb[j] = frag<BN, BK, BKC>(ib, wc * 64 + j * 16, s, lane);
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const bf16x8 fa = frag<BM, BK, AKC>(ia, wr * (BM / 2) + i * 16, s, lane);
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = mfma16x16x32(fa, fb[j], acc[i][j]);
+      }
+    }
+    lds_sync();   // every wave done reading `cur` before a later iteration restages it
+  }
+
+  // epilogue: lane holds rows 4*(lane>>4) + r, column lane&15 of each 16x16 tile
+  const bool split = gridDim.y > 1;
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int n = n0 + wc * 64 + j * 16 + (lane & 15);
+    if (n >= N) continue;
+    const float bv = (bias != nullptr) ? bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wr * (BM / 2) + i * 16 + 4 * (lane >> 4) + r;
+        if (m >= M) continue;
+        const size_t o = (size_t)m * ldc + n;
+        if (split) {   // linear fp32 epilogue (host-checked): partial sums meet in C
+          atomicAdd(reinterpret_cast<float*>(C) + o, alpha * acc[i][j][r] + (blockIdx.y == 0 ? bv : 0.f));
+          continue;
+        }
+        float z = alpha * acc[i][j][r] + bv;
+        if (beta != 0.f)
+          z += beta * (OBF ? bf2f(reinterpret_cast<const uint16_t*>(C)[o]) : reinterpret_cast<const float*>(C)[o]);
+        const float y = apply_act(z, act);
+        if constexpr (OBF) reinterpret_cast<uint16_t*>(C)[o] = f2bf(y);
+        else reinterpret_cast<float*>(C)[o] = y;
+      }
+    }
+  }
+}
+
+}  // namespace gemm2
+}  // namespace dtfk
+
+// Returns hipErrorInvalidValue (launching nothing) when the shape contract
+// does not hold; the caller then uses another GEMM.  split_k <= 0: automatic.
+extern "C" hipError_t dtfk_gemm_big(const void* A, int lda, int transA, const void* B, int ldb, int transB,
+                                    void* C, int c_bf16, int ldc, const float* bias, int M, int N, int K,
+                                    float alpha, float beta, int act, int split_k, hipStream_t stream) {
+  using namespace dtfk::gemm2;
+  const bool akc = !transA, bkc = transB != 0;
+  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (M <= 0 || N <= 0 || K <= 0 || K % KQ != 0 || !al16(A) || !al16(B) || lda % 8 || ldb % 8) return hipErrorInvalidValue;
+  if ((!akc && M % 8) || (!bkc && N % 8) || (akc && lda < K) || (bkc && ldb < K) || (!akc && lda < M) ||
+      (!bkc && ldb < N))
+    return hipErrorInvalidValue;
+  const int tn = (N + BN - 1) / BN;
+  // BM = 128 when 256-row tiles would leave CUs idle (e.g. N = 768: 3 column tiles)
+  const long long t256 = (long long)((M + 255) / 256) * tn;
+  const int BMsel = (t256 >= 512 || M <= 128) ? 256 : 128;
+  const long long tiles = (long long)((M + BMsel - 1) / BMsel) * tn;
+  if (tiles > 0x7fffffff) return hipErrorInvalidValue;
+  int split = 1, kchunk = K;
+  const bool linear = act == ACT_NONE && !c_bf16 && (beta == 0.f || beta == 1.f);
+  if (split_k > 1 || (split_k <= 0 && linear && tiles < 256 && K >= 2048)) {
+    if (!linear) return hipErrorInvalidValue;
+    split = split_k > 1 ? split_k : (int)((512 + tiles - 1) / tiles);
+    split = min(split, K / 512 > 0 ? K / 512 : 1);
+    kchunk = ((K + split - 1) / split + KQ - 1) / KQ * KQ;
+    split = (K + kchunk - 1) / kchunk;
+  }
+  if (split > 1 && beta == 0.f) {
+    const hipError_t e = hipMemset2DAsync(C, (size_t)ldc * sizeof(float), 0, (size_t)N * sizeof(float), M, stream);
+    if (e != hipSuccess) return e;
+  }
+  const dim3 grid((unsigned)tiles, split), block(NTHR);
+  const uint16_t* a = static_cast<const uint16_t*>(A);
+  const uint16_t* b = static_cast<const uint16_t*>(B);
+// K-contiguous x K-contiguous (forward): 32-deep tiles in a 5-stage ring (4
+// tiles of DMA in flight); with a transposed-read operand 64-deep tiles, 2
+// stages measured faster (scripts/bench_gemm.py, profiles/gemm_big_*).
+#define DTFK_GB(BMV, AK, BKk, OB)                                                                               \
+  if (AK && BKk)                                                                                                \
+    hipLaunchKernelGGL((gemm_big<BMV, 32, 5, AK, BKk, OB>), grid, block, 0, stream, a, lda, b, ldb, C, ldc, bias, \
+                       M, N, K, alpha, split > 1 ? 1.f : beta, act, kchunk);                                    \
+  else                                                                                                          \
+    hipLaunchKernelGGL((gemm_big<BMV, 64, 2, AK, BKk, OB>), grid, block, 0, stream, a, lda, b, ldb, C, ldc, bias, \
+                       M, N, K, alpha, split > 1 ? 1.f : beta, act, kchunk)
+#define DTFK_GB_O(BMV, AK, BKk) \
+  if (c_bf16) { DTFK_GB(BMV, AK, BKk, true); } else { DTFK_GB(BMV, AK, BKk, false); }
+#define DTFK_GB_B(BMV, AK) \
+  if (bkc) { DTFK_GB_O(BMV, AK, true); } else { DTFK_GB_O(BMV, AK, false); }
+#define DTFK_GB_A(BMV) \
+  if (akc) { DTFK_GB_B(BMV, true); } else { DTFK_GB_B(BMV, false); }
+  if (BMsel == 256) { DTFK_GB_A(256); } else { DTFK_GB_A(128); }
+#undef DTFK_GB_A
+#undef DTFK_GB_B
+#undef DTFK_GB_O
+#undef DTFK_GB
+  return hipGetLastError();
+}

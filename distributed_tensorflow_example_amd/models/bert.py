@@ -25,6 +25,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import ops
+from ..ops import big_gemm
 from ..ops import grad_sink
 from ..ops import transformer as T
 
@@ -67,6 +68,9 @@ class _ShadowLinear(torch.autograd.Function):
         ctx.save_for_backward(x, w16)
         ctx.w = w
         ctx.slot = slot
+        x2 = x.reshape(-1, x.shape[-1])
+        if big_gemm.use_native("fwd", x2.shape[0], w16.shape[0], x2.shape[1], x.device):
+            return big_gemm.linear_fwd(x2, w16).view(*x.shape[:-1], w16.shape[0])
         return F.linear(x, w16)
 
     @staticmethod
@@ -75,12 +79,14 @@ class _ShadowLinear(torch.autograd.Function):
         gy = gy.to(w16.dtype)
         gy2, x2 = gy.reshape(-1, gy.shape[-1]), x.reshape(-1, x.shape[-1])
         extra = ctx.slot.take() if ctx.slot is not None else None
+        native_dx = big_gemm.use_native("dx", gy2.shape[0], w16.shape[1], gy2.shape[1], gy.device)
         if extra is not None:   # residual-branch gradient of x folded in as the GEMM's beta = 1 term
             # in place: ds is a fresh buffer nobody else reads, and addmm_ on it
             # is one GEMM with beta = 1 (an out-of-place addmm would copy it first)
-            gx = extra.reshape(-1, x.shape[-1]).addmm_(gy2, w16).view(x.shape)
+            e2 = extra.reshape(-1, x.shape[-1])
+            gx = (big_gemm.linear_dx(gy2, w16, extra=e2) if native_dx else e2.addmm_(gy2, w16)).view(x.shape)
         else:
-            gx = gy @ w16
+            gx = big_gemm.linear_dx(gy2, w16).view(x.shape) if native_dx else gy @ w16
         w = ctx.w
         if grad_sink.enabled(w) and (w.grad is None or w.grad.is_contiguous()):
             _wgrad(gy2, x2, into=grad_sink.target(w))
@@ -105,6 +111,8 @@ def _wgrad_split(T: int, out: int, inp: int) -> int:
 def _wgrad(gy2, x2, into=None):
     """dW[out, in] = gy2[T, out]^T @ x2[T, in] in fp32 (accumulated into `into`)."""
     T, out = gy2.shape
+    if gy2.is_cuda and big_gemm.use_native("dw", out, x2.shape[1], T, gy2.device):
+        return big_gemm.linear_dw(gy2, x2, into=into)   # split-K over tokens, fp32 atomics into `into`
     s = _wgrad_split(T, out, x2.shape[1]) if gy2.is_cuda else 1
     if s == 1:
         if into is not None:

@@ -1,0 +1,123 @@
+"""The three products of a bf16 linear layer on the large-tile LDS-DMA MFMA
+GEMM (csrc/kernels/gemm_big.hip), with no transpose copies:
+
+    forward        y  = x W^T          (x [T,in], W [out,in])
+    input grad     dx = dy W  (+ r)    (beta = 1 folds a residual-branch gradient in)
+    weight grad    dW = dy^T x (+= dW) fp32 out, split-K over the T tokens
+
+Shapes outside the kernel's contract (K % 64, 16-byte alignment) go to
+torch's GEMM (hipBLASLt).  `use_native(role, M, N, K)` decides per product
+which engine a model runs: DTF_BIG_GEMM=never (default) / always, or auto --
+both engines timed once per shape on scratch operands, the faster one kept
+(`scripts/bench_gemm.py` prints the same comparison for the BERT shapes).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from .. import _native
+
+# never (default): hipBLASLt runs the model GEMMs -- on the BERT-base shapes it
+# is ~2x this kernel (profiles/gemm_big_vs_hipblaslt_r2.jsonl) and a per-shape
+# auto pick measured 3.5 % slower end to end (profiles/bert_base_b128_gemm_policy_r2.txt);
+# auto: time both once per shape, keep the faster; always: this kernel
+_POLICY = os.environ.get("DTF_BIG_GEMM", "never")
+_choice: dict = {}
+_timings: dict = {}
+
+
+def _C():
+    return _native.load()
+
+
+def _time(fn, reps=5):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def _candidates(role, M, N, K, dev):
+    """(ours, torch) closures for one product on scratch operands of its shape."""
+    C = _C()
+    bf = torch.bfloat16
+    if role == "fwd":      # y[M,N] = x[M,K] W[N,K]^T
+        a, b = torch.randn(M, K, device=dev, dtype=bf), torch.randn(N, K, device=dev, dtype=bf)
+        o = torch.empty(M, N, device=dev, dtype=bf)
+        return (lambda: C.gemm_big(a, False, b, True, o)), (lambda: torch.mm(a, b.t(), out=o))
+    if role == "dx":       # dx[M,N] = dy[M,K] W[K,N]
+        a, b = torch.randn(M, K, device=dev, dtype=bf), torch.randn(K, N, device=dev, dtype=bf)
+        o = torch.empty(M, N, device=dev, dtype=bf)
+        return (lambda: C.gemm_big(a, False, b, False, o)), (lambda: torch.mm(a, b, out=o))
+    # dw[M,N] += dy[K,M]^T x[K,N]
+    a, b = torch.randn(K, M, device=dev, dtype=bf), torch.randn(K, N, device=dev, dtype=bf)
+    o = torch.zeros(M, N, device=dev)
+    return ((lambda: C.gemm_big(a, True, b, False, o, beta=1.0, split_k=0)),
+            (lambda: torch.addmm(o, a.t(), b, out_dtype=torch.float32, out=o)))
+
+
+def use_native(role: str, M: int, N: int, K: int, dev) -> bool:
+    """True when gemm_big should run this product: the policy, the kernel's
+    shape contract (K % 64), and -- under 'auto' -- a one-time timing of both
+    engines on scratch operands of the shape (cached per process)."""
+    if _POLICY == "never" or K % 64:
+        return False
+    if _POLICY == "always":
+        return True
+    key = (role, M, N, K)
+    hit = _choice.get(key)
+    if hit is None:
+        if torch.cuda.is_current_stream_capturing():
+            return False
+        ours, theirs = _candidates(role, M, N, K, dev)
+        t_ours, t_theirs = _time(ours), _time(theirs)
+        hit = _choice[key] = t_ours <= t_theirs
+        _timings[key] = (round(t_ours, 4), round(t_theirs, 4))
+    return hit
+
+
+def choices() -> dict:
+    """{(role, M, N, K): (native chosen, (native ms, torch ms))}"""
+    return {k: (v, _timings.get(k)) for k, v in _choice.items()}
+
+
+def linear_fwd(x2, w16, bias=None, act: int = 0, out=None):
+    out = torch.empty(x2.shape[0], w16.shape[0], device=x2.device, dtype=x2.dtype) if out is None else out
+    if not _C().gemm_big(x2, False, w16, True, out, bias=bias, act=act):
+        if bias is not None or act:
+            raise ValueError("linear_fwd: epilogue needs the native kernel's shape contract")
+        torch.mm(x2, w16.t(), out=out)
+    return out
+
+
+def linear_dx(gy2, w16, extra=None):
+    """dx = gy2 @ w16 (+ extra, in place into `extra` when given)."""
+    if extra is not None:
+        if not _C().gemm_big(gy2, False, w16, False, extra, beta=1.0):
+            extra.addmm_(gy2, w16)
+        return extra
+    out = torch.empty(gy2.shape[0], w16.shape[1], device=gy2.device, dtype=gy2.dtype)
+    if not _C().gemm_big(gy2, False, w16, False, out):
+        torch.mm(gy2, w16, out=out)
+    return out
+
+
+def linear_dw(gy2, x2, into=None):
+    """dW[out, in] = gy2^T x2 in fp32 (accumulated into `into` when given)."""
+    if into is None:
+        into = torch.empty(gy2.shape[1], x2.shape[1], device=gy2.device, dtype=torch.float32)
+        beta = 0.0
+    else:
+        beta = 1.0
+    if not _C().gemm_big(gy2, True, x2, False, into, beta=beta, split_k=0):
+        if beta:
+            torch.addmm(into, gy2.t(), x2, out_dtype=torch.float32, out=into)
+        else:
+            torch.mm(gy2.t(), x2, out_dtype=torch.float32, out=into)
+    return into

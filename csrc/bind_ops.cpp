@@ -27,6 +27,8 @@ hipError_t dtfk_gemm(const void* A, int a_bf16, int lda, int transA, const void*
 hipError_t dtfk_gemm_big(const void* A, int lda, int transA, const void* B, int ldb, int transB, void* C,
                          int c_bf16, int ldc, const float* bias, int M, int N, int K, float alpha, float beta,
                          int act, int split_k, hipStream_t stream);
+hipError_t dtfk_gemm_big_cfg(int cfg, const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N,
+                             int K, hipStream_t stream);
 hipError_t dtfk_act_backward(const float* dy, const float* y, const float* z, float* dz, int64_t n, int act,
                              hipStream_t s);
 hipError_t dtfk_col_sum(const float* X, float* out, int M, int N, hipStream_t s);
@@ -136,6 +138,18 @@ bool gemm_big(at::Tensor A, bool transA, at::Tensor B, bool transB, at::Tensor o
   if (e == hipErrorInvalidValue) { (void)hipGetLastError(); return false; }
   ck(e, "gemm_big");
   return true;
+}
+
+// tiling experiments of gemm_big (forward layout only): out[M,N] = A[M,K] B[N,K]^T, bf16
+void gemm_big_cfg(int cfg, at::Tensor A, at::Tensor B, at::Tensor out) {
+  gpu(A, "A"); gpu(B, "B"); gpu(out, "out");
+  if (A.scalar_type() != at::kBFloat16 || B.scalar_type() != at::kBFloat16 || out.scalar_type() != at::kBFloat16 ||
+      !A.is_contiguous() || !B.is_contiguous() || !out.is_contiguous() || A.size(1) != B.size(1) ||
+      out.size(0) != A.size(0) || out.size(1) != B.size(0))
+    throw std::runtime_error("gemm_big_cfg: contiguous bf16 A[M,K], B[N,K], out[M,N]");
+  ck(dtfk_gemm_big_cfg(cfg, A.data_ptr(), (int)A.size(1), B.data_ptr(), (int)B.size(1), out.data_ptr(),
+                       (int)out.size(1), (int)A.size(0), (int)B.size(0), (int)A.size(1), cs()),
+     "gemm_big_cfg");
 }
 
 void act_backward(at::Tensor dy, c10::optional<at::Tensor> y, c10::optional<at::Tensor> z, at::Tensor dz,
@@ -400,6 +414,7 @@ void init_ops(py::module& m) {
   m.def("gemm_big", &gemm_big, py::arg("A"), py::arg("transA"), py::arg("B"), py::arg("transB"), py::arg("out"),
         py::arg("bias") = py::none(), py::arg("act") = 0, py::arg("alpha") = 1.0, py::arg("beta") = 0.0,
         py::arg("split_k") = 0);
+  m.def("gemm_big_cfg", &gemm_big_cfg);
   m.def("act_backward", &act_backward);
   m.def("col_sum", &col_sum);
   m.def("softmax_xent", &softmax_xent);

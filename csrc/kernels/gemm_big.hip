@@ -148,7 +148,7 @@ __device__ __forceinline__ void wait_stages(int ahead) {
 
 // S-stage ring of BK-deep K tiles: while tile t is multiplied, tiles t+1 ..
 // t+S-1 are in flight (S-1 stages of DMA bytes hide the HBM/L2 latency).
-template <int BM, int BK, int S, bool AKC, bool BKC, bool OBF>
+template <int BM, int BK, int S, bool AKC, bool BKC, bool OBF, int VAR = 0>
 __global__ __launch_bounds__(NTHR) void gemm_big(const uint16_t* __restrict__ A, int lda,
                                                  const uint16_t* __restrict__ B, int ldb, void* __restrict__ C,
                                                  int ldc, const float* __restrict__ bias, int M, int N, int K,
@@ -194,16 +194,41 @@ __global__ __launch_bounds__(NTHR) void gemm_big(const uint16_t* __restrict__ A,
     lds_sync();
     const uint8_t* ia = cur;
     const uint8_t* ib = cur + A_BYTES;
+    if constexpr (VAR == 1) {
+      // all fragments of the tile first (ds_reads back to back), then the MFMA
+      // cluster at raised priority: the partner wave's reads overlap our MFMAs
+      bf16x8 fa[BK / 32][MT], fb[BK / 32][NT];
 #pragma unroll
-    for (int s = 0; s < BK / 32; ++s) {
-      bf16x8 fb[NT];
+      for (int s = 0; s < BK / 32; ++s) {
 #pragma unroll
-      for (int j = 0; j < NT; ++j) fb[j] = frag<BN, BK, BKC>(ib, wc * 64 + j * 16, s, lane);
+        for (int j = 0; j < NT; ++j) fb[s][j] = frag<BN, BK, BKC>(ib, wc * 64 + j * 16, s, lane);
 #pragma unroll
-      for (int i = 0; i < MT; ++i) {
-        const bf16x8 fa = frag<BM, BK, AKC>(ia, wr * (BM / 2) + i * 16, s, lane);
+        for (int i = 0; i < MT; ++i) fa[s][i] = frag<BM, BK, AKC>(ia, wr * (BM / 2) + i * 16, s, lane);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int j = 0; j < NT; ++j) acc[i][j] = mfma16x16x32(fa, fb[j], acc[i][j]);
+      for (int s = 0; s < BK / 32; ++s)
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+          for (int j = 0; j < NT; ++j) acc[i][j] = mfma16x16x32(fa[s][i], fb[s][j], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+    } else {
+#pragma unroll
+      for (int s = 0; s < BK / 32; ++s) {
+        bf16x8 fb[NT];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) fb[j] = frag<BN, BK, BKC>(ib, wc * 64 + j * 16, s, lane);
+        if constexpr (VAR == 2) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+          const bf16x8 fa = frag<BM, BK, AKC>(ia, wr * (BM / 2) + i * 16, s, lane);
+#pragma unroll
+          for (int j = 0; j < NT; ++j) acc[i][j] = mfma16x16x32(fa, fb[j], acc[i][j]);
+        }
+        if constexpr (VAR == 2) __builtin_amdgcn_s_setprio(0);
       }
     }
     lds_sync();   // every wave done reading `cur` before a later iteration restages it
@@ -254,9 +279,9 @@ extern "C" hipError_t dtfk_gemm_big(const void* A, int lda, int transA, const vo
       (!bkc && ldb < N))
     return hipErrorInvalidValue;
   const int tn = (N + BN - 1) / BN;
-  // BM = 128 when 256-row tiles would leave CUs idle (e.g. N = 768: 3 column tiles)
-  const long long t256 = (long long)((M + 255) / 256) * tn;
-  const int BMsel = (t256 >= 512 || M <= 128) ? 256 : 128;
+  // 256 x 256 tiles even when they leave CUs idle (N = 768: 192 tiles): measured
+  // faster than 128 x 256 at every BERT shape (scripts/probes/gemm_big_cfg.py)
+  const int BMsel = 256;
   const long long tiles = (long long)((M + BMsel - 1) / BMsel) * tn;
   if (tiles > 0x7fffffff) return hipErrorInvalidValue;
   int split = 1, kchunk = K;
@@ -275,26 +300,46 @@ extern "C" hipError_t dtfk_gemm_big(const void* A, int lda, int transA, const vo
   const dim3 grid((unsigned)tiles, split), block(NTHR);
   const uint16_t* a = static_cast<const uint16_t*>(A);
   const uint16_t* b = static_cast<const uint16_t*>(B);
-// K-contiguous x K-contiguous (forward): 32-deep tiles in a 5-stage ring (4
-// tiles of DMA in flight); with a transposed-read operand 64-deep tiles, 2
-// stages measured faster (scripts/bench_gemm.py, profiles/gemm_big_*).
-#define DTFK_GB(BMV, AK, BKk, OB)                                                                               \
-  if (AK && BKk)                                                                                                \
-    hipLaunchKernelGGL((gemm_big<BMV, 32, 5, AK, BKk, OB>), grid, block, 0, stream, a, lda, b, ldb, C, ldc, bias, \
-                       M, N, K, alpha, split > 1 ? 1.f : beta, act, kchunk);                                    \
-  else                                                                                                          \
-    hipLaunchKernelGGL((gemm_big<BMV, 64, 2, AK, BKk, OB>), grid, block, 0, stream, a, lda, b, ldb, C, ldc, bias, \
-                       M, N, K, alpha, split > 1 ? 1.f : beta, act, kchunk)
-#define DTFK_GB_O(BMV, AK, BKk) \
-  if (c_bf16) { DTFK_GB(BMV, AK, BKk, true); } else { DTFK_GB(BMV, AK, BKk, false); }
-#define DTFK_GB_B(BMV, AK) \
-  if (bkc) { DTFK_GB_O(BMV, AK, true); } else { DTFK_GB_O(BMV, AK, false); }
-#define DTFK_GB_A(BMV) \
-  if (akc) { DTFK_GB_B(BMV, true); } else { DTFK_GB_B(BMV, false); }
-  if (BMsel == 256) { DTFK_GB_A(256); } else { DTFK_GB_A(128); }
-#undef DTFK_GB_A
+// 64-deep tiles, 2 stages for every layout: the 32-deep 5-stage ring and the
+// 128-row tiles measured slower (profiles/gemm_big_cfg_r2.jsonl)
+#define DTFK_GB(AK, BKk, OB)                                                                                  \
+  hipLaunchKernelGGL((gemm_big<256, 64, 2, AK, BKk, OB>), grid, block, 0, stream, a, lda, b, ldb, C, ldc, bias, \
+                     M, N, K, alpha, split > 1 ? 1.f : beta, act, kchunk)
+#define DTFK_GB_O(AK, BKk) \
+  if (c_bf16) { DTFK_GB(AK, BKk, true); } else { DTFK_GB(AK, BKk, false); }
+#define DTFK_GB_B(AK) \
+  if (bkc) { DTFK_GB_O(AK, true); } else { DTFK_GB_O(AK, false); }
+  if (akc) { DTFK_GB_B(true); } else { DTFK_GB_B(false); }
 #undef DTFK_GB_B
 #undef DTFK_GB_O
 #undef DTFK_GB
+  return hipGetLastError();
+}
+
+// Tiling experiments (scripts/probes/gemm_big_cfg.py): the forward layout
+// (K-contiguous x K-contiguous, bf16 out, no epilogue) at a chosen
+// (BM, BK, stages).  Not used by the framework's dispatch above.
+extern "C" hipError_t dtfk_gemm_big_cfg(int cfg, const void* A, int lda, const void* B, int ldb, void* C, int ldc,
+                                        int M, int N, int K, hipStream_t stream) {
+  using namespace dtfk::gemm2;
+  if (K % KQ || M % 256 || N % 256 || lda % 8 || ldb % 8) return hipErrorInvalidValue;
+  const uint16_t* a = static_cast<const uint16_t*>(A);
+  const uint16_t* b = static_cast<const uint16_t*>(B);
+  const int tn = N / BN;
+#define DTFK_CFG(BMV, BKV, SV, ...)                                                                               \
+  hipLaunchKernelGGL((gemm_big<BMV, BKV, SV, true, true, true, ##__VA_ARGS__>), dim3((M / BMV) * tn, 1), dim3(NTHR), 0, stream, \
+                     a, lda, b, ldb, C, ldc, nullptr, M, N, K, 1.f, 0.f, 0, K)
+  switch (cfg) {
+    case 0: DTFK_CFG(256, 32, 5); break;
+    case 1: DTFK_CFG(256, 64, 2); break;
+    case 2: DTFK_CFG(128, 64, 3); break;
+    case 3: DTFK_CFG(128, 32, 5); break;
+    case 4: DTFK_CFG(256, 32, 3); break;
+    case 5: DTFK_CFG(128, 64, 2); break;
+    case 6: DTFK_CFG(256, 64, 2, 1); break;
+    case 7: DTFK_CFG(256, 64, 2, 2); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef DTFK_CFG
   return hipGetLastError();
 }

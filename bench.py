@@ -187,7 +187,13 @@ def main(argv=None):
             continue
         if consistent(trainer, runner):
             picked.append((mode, trainer, runner))
-            if w.world_size == 1 or len(picked) == 3 or a.tune_steps <= 0:
+            nxt_mode = chain[i + 1] if i + 1 < len(chain) else None
+            # the 3-launch candidates are only tuned when no in-kernel exchange
+            # validated: they never win against it (2 ranks: 14 vs 77 us/step)
+            # and leave streams / graphs behind that several ranks sharing one
+            # GPU (tests) then time-slice against
+            if (w.world_size == 1 or len(picked) == 3 or a.tune_steps <= 0 or nxt_mode is None
+                    or (mode.startswith("persistent") and not nxt_mode.startswith("persistent"))):
                 break
             continue
         fallbacks[mode] = "failed validation (exchange timeout or replica drift after warmup)"

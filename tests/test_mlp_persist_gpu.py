@@ -213,6 +213,17 @@ def test_persist_long_run_learns(native, precision):
                                                      ("fp32-split7", "fp32", "one-shot"), ("fp16", "bf16", "one-shot")])
 @pytest.mark.parametrize("nproc", [2, 3])
 def test_persist_multi_rank_same_gpu(native, nproc, precision, grad, exchange):
+    _persist_selftest(nproc, precision, grad, exchange)
+
+
+@pytest.mark.parametrize("exchange", ["one-shot", "two-shot"])
+def test_persist_four_ranks_same_gpu(native, exchange):
+    """4 ranks (the W = 4 chunking of the two-shot exchange: 8 waves over 4
+    owners) sharing cuda:0 with the default fp32 engine and bf16 payload."""
+    _persist_selftest(4, "fp32", "bf16", exchange)
+
+
+def _persist_selftest(nproc, precision, grad, exchange):
     """N ranks sharing cuda:0: in-kernel IPC exchange, bit-identical replicas, sync-SGD math."""
     import json
     import os

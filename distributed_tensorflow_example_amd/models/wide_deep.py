@@ -66,6 +66,7 @@ class WideDeep:
                     self.world.broadcast(p.data, 0)
         self.comm_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
         self.global_step = 0
+        self._graphed = None
 
     def forward(self, labels, offsets, ids, vals):
         # both tables read the same ids over the same row partition: one
@@ -86,6 +87,39 @@ class WideDeep:
         return logit, (wrows, erows, ctx)
 
     def train_step(self, batch) -> torch.Tensor:
+        if self._graphed is not None:
+            labels, offsets, ids, vals = batch.to(self.device) if hasattr(batch, "to") else batch
+            loss = self._graphed(labels, offsets, ids, vals)
+            self.global_step += 1
+            return loss.detach()
+        return self._train_step(batch)
+
+    def enable_graph(self, on: bool = True):
+        """Replay each training step as ONE captured hipGraph: routing, the two
+        table lookups, bags, the MFMA tower, loss, backward, the sparse SGD of
+        both tables and the fused Adam of the tower (~40 kernels) in one launch.
+        Needs a GPU and the static device-resident routing (ids_capacity)."""
+        from ..utils.graphs import GraphedStep
+
+        if not on:
+            self._graphed = None
+            return
+        if self.device.type != "cuda" or self.ids_capacity is None:
+            raise RuntimeError("graph capture needs a GPU and static routing (ids_capacity)")
+
+        def step(labels, offsets, ids, vals):
+            gs = self.global_step
+            loss = self._train_step((labels, offsets, ids, vals))
+            self.global_step = gs          # counted by train_step, not by warmup/capture
+            return loss
+
+        def state():   # everything a step mutates, restored after the capture's warmup
+            st = [self.wide.local, self.emb.local] + [p.data for p in self.dense_params] + [self.opt.step_t]
+            st += [t for t in list(self.opt.m) + list(self.opt.v) if t is not None]
+            return st
+        self._graphed = GraphedStep(step, state)
+
+    def _train_step(self, batch) -> torch.Tensor:
         labels, offsets, ids, vals = batch.to(self.device) if hasattr(batch, "to") else batch
         self.flat_grad.zero_()
         logit, (wrows, erows, lctx) = self.forward(labels, offsets, ids, vals)

@@ -57,7 +57,7 @@ def main():
     ap.add_argument("--nnz", type=int, default=32, help="features per sample")
     ap.add_argument("--gpus", type=int, default=None)
     ap.add_argument("--lr", type=float, default=None, help="sparse models: SGD learning rate")
-    ap.add_argument("--graph", action="store_true", help="sparse_lr / lr2: replay each step as one captured hipGraph")
+    ap.add_argument("--graph", action="store_true", help="sparse_lr / lr2 / wide_deep: replay each step as one captured hipGraph")
     ap.add_argument("--trace-marker", action="store_true",
                     help="launch a spin kernel right before the timed loop, so a kernel trace can be cut to the "
                          "steady state (scripts/rocpd_summary.py --after spin)")
@@ -83,10 +83,12 @@ def main():
         from distributed_tensorflow_example_amd.models.wide_deep import WideDeep
 
         m = WideDeep(a.features, emb_dim=a.emb_dim, hidden=(512, 256), lr=0.05, dense_opt="adam",
-                     dense_lr=1e-3, world=w)
+                     dense_lr=1e-3, world=w, ids_capacity=a.batch * a.nnz if a.graph else None)
+        if a.graph:
+            m.enable_graph()
         cfg = {"model": f"wide_deep F={a.features} D={a.emb_dim} tower=512-256-1", "global_batch": a.batch * w.world_size,
                "per_gpu_batch": a.batch, "seq_len": None, "parallelism": f"dp{w.world_size}+emb-shard{w.world_size}",
-               "nnz_per_sample": a.nnz}
+               "nnz_per_sample": a.nnz, "graph": bool(a.graph)}
     else:
         from distributed_tensorflow_example_amd.models.sparse_lr import SparseLRTrainer
 

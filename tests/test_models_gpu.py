@@ -112,3 +112,36 @@ def test_sparse_lr_graphed_step_matches_eager():
     assert graphed.global_step == eager.global_step == 12
     assert torch.allclose(eager.W.local, graphed.W.local, atol=1e-5)
     assert torch.allclose(eager.b, graphed.b, atol=1e-6)
+
+
+def test_wide_deep_graphed_step_matches_eager(native):
+    """The whole W&D step (routing, lookups, bags, MFMA tower, loss, backward,
+    sparse SGD of both tables, fused Adam) replayed as one hipGraph follows the
+    eager step."""
+    from distributed_tensorflow_example_amd.models.wide_deep import WideDeep
+    from distributed_tensorflow_example_amd.parallel import world as W
+
+    w = W.get_world() if W._WORLD is not None else W.init()
+    F, B, nnz = 50_000, 256, 8
+    g = torch.Generator(device="cuda").manual_seed(0)
+    batches = []
+    for _ in range(5):
+        ids = torch.randint(0, F, (B * nnz,), device="cuda", generator=g)
+        offs = torch.arange(0, B * nnz + 1, nnz, device="cuda")
+        vals = torch.rand(B * nnz, device="cuda", generator=g)
+        lab = (torch.rand(B, 1, device="cuda", generator=g) < 0.3).float()
+        batches.append((lab, offs, ids, vals))
+    mk = lambda: WideDeep(F, emb_dim=16, hidden=(64, 32), lr=0.5, dense_opt="adam", dense_lr=0.01, world=w,
+                          seed=4, ids_capacity=B * nnz)
+    eager, graphed = mk(), mk()
+    graphed.enable_graph()
+    for i in range(10):
+        le = eager.train_step(batches[i % 5])
+        lg = graphed.train_step(batches[i % 5])
+        assert abs(float(le) - float(lg)) < 1e-4, (i, float(le), float(lg))
+    assert graphed._graphed.captures == 1 and graphed._graphed.replays == 10
+    assert graphed.global_step == eager.global_step == 10
+    assert torch.allclose(eager.emb.local, graphed.emb.local, atol=1e-5)
+    assert torch.allclose(eager.wide.local, graphed.wide.local, atol=1e-5)
+    for a, b in zip(eager.dense_params, graphed.dense_params):
+        assert torch.allclose(a, b, atol=1e-5)

@@ -78,11 +78,13 @@ def test_linear_act_autograd(native, act):
     assert rel(bg.grad, b.grad) < 2e-2
 
 
-def test_col_sum(native):
-    X = torch.randn(1000, 37).cuda()
-    out = torch.empty(37, device="cuda")
+@pytest.mark.parametrize("M,N", [(1000, 37), (4096, 512), (4096, 1), (4096, 256), (7, 12), (100000, 64), (33, 1028)])
+def test_col_sum(native, M, N):
+    X = torch.randn(M, N).cuda()
+    out = torch.full((N,), float("nan"), device="cuda")
     native.col_sum(X, out)
-    assert torch.allclose(out.cpu(), X.cpu().sum(0), atol=1e-3, rtol=1e-4)
+    ref = X.cpu().double().sum(0).float()
+    assert torch.allclose(out.cpu(), ref, atol=1e-4 * max(1.0, M ** 0.5), rtol=1e-4)
 
 
 @pytest.mark.parametrize("dense", [False, True])

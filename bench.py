@@ -6,8 +6,9 @@ at 1/2/4/8 MI355X; step-time p50".  Per-GPU batch 100 (example.py:43),
 lr 0.0005, sigmoid hidden layer, softmax cross-entropy, plain SGD.
 
 Default engine: the persistent fp32 kernel (csrc/kernels/mlp_persist_f32.hip)
--- the reference's precision (example.py:77-118 is fp32 end to end): exact
-f32-input MFMA, fp32 accumulate, fp32 master weights.  `--precision fp16`
+-- the reference's precision (example.py:77-118 is fp32 end to end): the two
+big GEMMs as exact 3-way bf16 splits of their fp32 operands (every product
+exact, fp32 accumulate), the head on f32-input MFMA, fp32 master weights.  `--precision fp16`
 selects the f16-MFMA persistent kernel (labelled as such in the output line).
 N GPUs: gradients exchanged inside the persistent launch over IPC-mapped xGMI
 peer buffers (bf16 payload per BASELINE config #2, `--grad-dtype fp32` for
@@ -60,9 +61,10 @@ def main(argv=None):
     ap.add_argument("--lr", type=float, default=0.0005)
     ap.add_argument("--steps-per-graph", type=int, default=50, help="3-launch path: steps per captured hipGraph")
     ap.add_argument("--precision", choices=["fp32", "fp32-mfma", "fp32-split7", "fp16"], default="fp32",
-                    help="persistent engine (reference precision: fp32): fp32 = f32-input MFMA for every product; "
-                         "fp32-split = exact 3-way bf16 split of every fp32 GEMM operand (exact products, fp32 "
-                         "accumulate); fp16 = f16 MFMA operands")
+                    help="persistent engine (reference precision: fp32): fp32 = the 28-workgroup engine with the "
+                         "big GEMMs as exact 3-way bf16 splits of their fp32 operands (exact products, fp32 "
+                         "accumulate); fp32-mfma = every product on f32-input MFMA; fp32-split7 = the 7-workgroup "
+                         "split engine; fp16 = f16 MFMA operands (not the reference's precision)")
     ap.add_argument("--exchange-timeout", type=float, default=30.0,
                     help="in-kernel exchange wait bound (s); a cold multi-GPU start can skew ranks by seconds")
     ap.add_argument("--steps-per-launch", type=int, default=550,

@@ -303,7 +303,9 @@ def main(argv=None):
                 "seq_len": None,
                 "parallelism": f"dp{n}",
                 "optimizer": f"sgd lr={a.lr}",
-                "grad_allreduce": ("none" if n == 1 else f"{a.grad_dtype} in-kernel one-shot over IPC/xGMI"
+                "grad_allreduce": ("none" if n == 1 else
+                                   f"{a.grad_dtype} in-kernel {'two-shot' if mode == 'persistent-2shot' else 'one-shot'}"
+                                   " over IPC/xGMI"
                                    if persistent else f"{a.grad_dtype} {trainer.allreduce}"),
                 "engine": f"persistent-{a.precision}" if persistent else "launches",
                 "exchange_mode": mode,

@@ -104,6 +104,33 @@ __device__ __forceinline__ void stage(const uint16_t* __restrict__ base, int ld,
   }
 }
 
+// Register-staged alternative to stage(): the same lane-linear image, loaded
+// into VGPRs first (global_load_dwordx4) and written with ds_write_b128.
+template <int R, int BK, bool KC>
+__device__ __forceinline__ void gload(const uint16_t* __restrict__ base, int ld, int rows, int r0, int k0, int wave,
+                                      int lane, uint4* v) {
+  constexpr int CPR = BK / 8;
+#pragma unroll
+  for (int j = 0; j < R * BK / 4096; ++j) {
+    const int o = ((j * 8 + wave) << 10) + (lane << 4);
+    const uint16_t* src;
+    if constexpr (KC) {
+      const int r = o / (BK * 2), c = ((o >> 4) % CPR) ^ ((r / (16 / CPR)) & (CPR - 1));
+      src = base + (size_t)min(r0 + r, rows - 1) * ld + k0 + c * 8;
+    } else {
+      const int k = o / (2 * R), ch = ((o % (2 * R)) >> 4) ^ (mn_swz(k) << 1);
+      src = base + (size_t)(k0 + k) * ld + min(r0 + ch * 8, rows - 8);
+    }
+    v[j] = *reinterpret_cast<const uint4*>(src);
+  }
+}
+template <int R, int BK>
+__device__ __forceinline__ void lstore(uint8_t* img, int wave, int lane, const uint4* v) {
+#pragma unroll
+  for (int j = 0; j < R * BK / 4096; ++j)
+    *reinterpret_cast<uint4*>(img + ((j * 8 + wave) << 10) + (lane << 4)) = v[j];
+}
+
 // MFMA 16x16x32 operand fragment of rows [rb, rb+16), k-sub s (k = 32 s ...):
 // lane l gets (row rb + (l&15), k = 32 s + 8 (l>>4) + j), j = 0..7.
 template <int R, int BK, bool KC>
@@ -175,6 +202,45 @@ __global__ __launch_bounds__(NTHR) void gemm_big(const uint16_t* __restrict__ A,
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  if constexpr (VAR == 3) {
+    // register-staged double buffer: tile t+1's global loads are in flight
+    // while tile t is multiplied, then written to the other LDS buffer
+    static_assert(S == 2, "register staging uses two LDS buffers");
+    uint4 va[BM * BK / 4096], vb[BN * BK / 4096];
+    if (nk > 0) {
+      gload<BM, BK, AKC>(A, lda, M, m0, kb, wave, lane, va);
+      gload<BN, BK, BKC>(B, ldb, N, n0, kb, wave, lane, vb);
+      lstore<BM, BK>(smem, wave, lane, va);
+      lstore<BN, BK>(smem + A_BYTES, wave, lane, vb);
+    }
+    __syncthreads();
+    for (int t = 0; t < nk; ++t) {
+      const uint8_t* ia = smem + (t & 1) * STAGE;
+      const uint8_t* ib = ia + A_BYTES;
+      if (t + 1 < nk) {
+        gload<BM, BK, AKC>(A, lda, M, m0, kb + (t + 1) * BK, wave, lane, va);
+        gload<BN, BK, BKC>(B, ldb, N, n0, kb + (t + 1) * BK, wave, lane, vb);
+      }
+#pragma unroll
+      for (int s = 0; s < BK / 32; ++s) {
+        bf16x8 fb[NT];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) fb[j] = frag<BN, BK, BKC>(ib, wc * 64 + j * 16, s, lane);
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+          const bf16x8 fa = frag<BM, BK, AKC>(ia, wr * (BM / 2) + i * 16, s, lane);
+#pragma unroll
+          for (int j = 0; j < NT; ++j) acc[i][j] = mfma16x16x32(fa, fb[j], acc[i][j]);
+        }
+      }
+      if (t + 1 < nk) {
+        uint8_t* nx = smem + ((t + 1) & 1) * STAGE;
+        lstore<BM, BK>(nx, wave, lane, va);
+        lstore<BN, BK>(nx + A_BYTES, wave, lane, vb);
+      }
+      __syncthreads();
+    }
+  } else {
 #pragma unroll
   for (int p = 0; p < S - 1; ++p) {
     if (p < nk) {
@@ -232,6 +298,7 @@ __global__ __launch_bounds__(NTHR) void gemm_big(const uint16_t* __restrict__ A,
       }
     }
     lds_sync();   // every wave done reading `cur` before a later iteration restages it
+  }
   }
 
   // epilogue: lane holds rows 4*(lane>>4) + r, column lane&15 of each 16x16 tile
@@ -338,6 +405,7 @@ extern "C" hipError_t dtfk_gemm_big_cfg(int cfg, const void* A, int lda, const v
     case 5: DTFK_CFG(128, 64, 2); break;
     case 6: DTFK_CFG(256, 64, 2, 1); break;
     case 7: DTFK_CFG(256, 64, 2, 2); break;
+    case 8: DTFK_CFG(256, 64, 2, 3); break;
     default: return hipErrorInvalidValue;
   }
 #undef DTFK_CFG

@@ -11,9 +11,10 @@ from distributed_tensorflow_example_amd import _native  # noqa: E402
 
 CFG = {0: "256x256 BK32 S5", 1: "256x256 BK64 S2", 2: "128x256 BK64 S3", 3: "128x256 BK32 S5",
        4: "256x256 BK32 S3", 5: "128x256 BK64 S2", 6: "256x256 BK64 S2 reads-first+setprio",
-       7: "256x256 BK64 S2 setprio"}
+       7: "256x256 BK64 S2 setprio", 8: "256x256 BK64 register-staged"}
 C = _native.load()
 for (M, N, K) in [(16384, 3072, 768), (16384, 768, 3072), (8192, 8192, 8192)]:
+    torch.cuda.empty_cache()
     a = torch.randn(M, K, device="cuda").bfloat16()
     b = torch.randn(N, K, device="cuda").bfloat16()
     o = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)

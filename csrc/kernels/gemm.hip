@@ -20,6 +20,8 @@
 // (shared A panel in that XCD's L2).
 #include "common.h"
 
+#include <algorithm>
+
 namespace dtfk {
 namespace gemm {
 
@@ -321,6 +323,57 @@ __global__ __launch_bounds__(256) void gemm_f32_bias_act(
     }
   }
 }
+
+// ---------------------------------------------------------------------------
+// N == 1 (matrix-vector) fp32 products -- the W&D tower's 256 -> 1 head and its
+// weight gradient went through 64x64 MFMA tiles with one useful column (16-19
+// us for 4 MB of reads).  b(k) = B[k * ldbk].
+// Row form (A' rows contiguous): one wave per output row, lanes over k.
+__global__ __launch_bounds__(256) void gemv_rows_f32(const float* __restrict__ A, int lda,
+                                                     const float* __restrict__ Bv, int ldbk, float* __restrict__ C,
+                                                     int ldc, float* __restrict__ Zout, const float* __restrict__ bias,
+                                                     int M, int K, float alpha, float beta, int act) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= M) return;   // wave-uniform
+  const float* a = A + (size_t)i * lda;
+  float s0 = 0.f, s1 = 0.f;
+  int k = lane;
+  for (; k + 64 < K; k += 128) {
+    s0 += a[k] * Bv[(size_t)k * ldbk];
+    s1 += a[k + 64] * Bv[(size_t)(k + 64) * ldbk];
+  }
+  if (k < K) s0 += a[k] * Bv[(size_t)k * ldbk];
+  const float t = wave_sum(s0 + s1);
+  if (lane == 0) {
+    float z = alpha * t + (bias != nullptr ? bias[0] : 0.f);
+    const size_t o = (size_t)i * ldc;
+    if (beta != 0.f) z += beta * C[o];
+    if (Zout != nullptr) Zout[o] = z;
+    C[o] = apply_act(z, act);
+  }
+}
+
+// Column form (A' = A^T, A stored [K, M]): out[i] = sum_k A[k, i] b(k), a
+// b-weighted column sum -- 64 columns x 4 k-groups per block, grid.y k-chunks
+// meeting by atomics (linear epilogue only; C pre-zeroed or accumulated into).
+__global__ __launch_bounds__(256) void gemv_cols_f32(const float* __restrict__ A, int lda,
+                                                     const float* __restrict__ Bv, int ldbk, float* __restrict__ C,
+                                                     int ldc, const float* __restrict__ bias, int M, int K,
+                                                     float alpha, int kchunk) {
+  __shared__ float red[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
+  const int k0 = blockIdx.y * kchunk, k1 = min(K, k0 + kchunk);
+  float s = 0.f;
+  if (c < M)
+    for (int k = k0 + g; k < k1; k += 4) s += A[(size_t)k * lda + c] * Bv[(size_t)k * ldbk];
+  red[g][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (g == 0 && c < M) {
+    const float t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    atomicAdd(C + (size_t)c * ldc, alpha * t + (blockIdx.y == 0 && bias != nullptr ? bias[0] : 0.f));
+  }
+}
 }  // namespace gemm
 }  // namespace dtfk
 
@@ -331,6 +384,31 @@ extern "C" hipError_t dtfk_gemm(const void* A, int a_bf16, int lda, int transA, 
   using namespace dtfk::gemm;
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   if (tiles == 0) return hipSuccess;
+  if (!a_bf16 && !b_bf16 && !c_bf16 && N == 1) {
+    // matrix-vector forms (b(k) = B[k * ldbk]: B is [K, 1] or [1, K])
+    const float* Af = static_cast<const float*>(A);
+    const float* Bf = static_cast<const float*>(B);
+    float* Cf = static_cast<float*>(C);
+    const int ldbk = transB ? 1 : ldb;
+    if (!transA) {
+      hipLaunchKernelGGL(gemv_rows_f32, dim3((M + 3) / 4), dim3(256), 0, stream, Af, lda, Bf, ldbk, Cf, ldc, Z, bias,
+                         M, K, alpha, beta, act);
+      return hipGetLastError();
+    }
+    if (act == ACT_NONE && Z == nullptr && (beta == 0.f || beta == 1.f)) {
+      const int bx = (M + 63) / 64;
+      int gy = std::max(1, std::min((K + 63) / 64, 512 / bx));
+      const int kc = (K + gy - 1) / gy;
+      gy = (K + kc - 1) / kc;
+      if (beta == 0.f) {
+        const hipError_t e = hipMemset2DAsync(C, (size_t)ldc * sizeof(float), 0, sizeof(float), M, stream);
+        if (e != hipSuccess) return e;
+      }
+      hipLaunchKernelGGL(gemv_cols_f32, dim3(bx, gy), dim3(256), 0, stream, Af, lda, Bf, ldbk, Cf, ldc, bias, M, K,
+                         alpha, kc);
+      return hipGetLastError();
+    }
+  }
   // Split-K when the output has too few 64x64 tiles to fill 256 CUs and K is
   // long -- the weight gradients X^T dZ (M x N = fan_in x fan_out, K = batch).
   // Only for a linear fp32 epilogue: the partial products meet by atomics.

@@ -426,3 +426,29 @@ def test_fused_adagrad_rmsprop_match_cpu(kind):
         og.step([g.clone().cuda() for g in step])
     for a, b in zip(pc, pg):
         assert torch.allclose(a, b.cpu(), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("ta", [False, True])
+@pytest.mark.parametrize("tb", [False, True])
+@pytest.mark.parametrize("M,K", [(4096, 256), (256, 4096), (37, 5), (1000, 1)])
+def test_gemm_fp32_matrix_vector(native, M, K, ta, tb):
+    """N == 1 fp32 products (W&D head / its weight gradient) on the GEMV kernels."""
+    torch.manual_seed(M + K)
+    A = torch.randn(*((K, M) if ta else (M, K)), device="cuda")
+    B = torch.randn(*((1, K) if tb else (K, 1)), device="cuda")
+    a = (A.t() if ta else A).double()
+    b = (B.t() if tb else B).double()
+    for beta in (0.0, 1.0):
+        C0 = torch.randn(M, 1, device="cuda")
+        C = C0.clone()
+        bias = torch.randn(1, device="cuda")
+        native.gemm(A, ta, B, tb, C, bias=bias, act=0, alpha=0.5, beta=beta)
+        ref = 0.5 * (a @ b) + bias.double() + beta * C0.double()
+        assert torch.allclose(C.double(), ref, rtol=1e-5, atol=1e-4), (beta, float((C.double() - ref).abs().max()))
+    if not ta:   # row form: any epilogue (activation + pre-activation output)
+        C = torch.empty(M, 1, device="cuda")
+        Z = torch.empty(M, 1, device="cuda")
+        native.gemm(A, ta, B, tb, C, act=2, Z=Z)
+        z = a @ b
+        assert torch.allclose(Z.double(), z, rtol=1e-5, atol=1e-4)
+        assert torch.allclose(C.double(), torch.sigmoid(z), rtol=1e-5, atol=1e-5)

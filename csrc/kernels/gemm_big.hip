@@ -202,7 +202,41 @@ __global__ __launch_bounds__(NTHR) void gemm_big(const uint16_t* __restrict__ A,
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if constexpr (VAR == 3) {
+  if constexpr (VAR == 4) {
+    // one barrier per K tile (T3 minimum 2-phase): issue tile t+1's DMA, multiply
+    // tile t, then wait for t+1 and barrier -- that barrier both publishes t+1
+    // and retires every wave's reads of t before t+2 is staged into its buffer
+    static_assert(S == 2, "two LDS buffers");
+    if (nk > 0) {
+      stage<BM, BK, AKC>(A, lda, M, m0, kb, smem, wave, lane);
+      stage<BN, BK, BKC>(B, ldb, N, n0, kb, smem + A_BYTES, wave, lane);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_sync();
+    for (int t = 0; t < nk; ++t) {
+      const uint8_t* ia = smem + (t & 1) * STAGE;
+      const uint8_t* ib = ia + A_BYTES;
+      if (t + 1 < nk) {
+        uint8_t* nx = smem + ((t + 1) & 1) * STAGE;
+        stage<BM, BK, AKC>(A, lda, M, m0, kb + (t + 1) * BK, nx, wave, lane);
+        stage<BN, BK, BKC>(B, ldb, N, n0, kb + (t + 1) * BK, nx + A_BYTES, wave, lane);
+      }
+#pragma unroll
+      for (int s = 0; s < BK / 32; ++s) {
+        bf16x8 fb[NT];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) fb[j] = frag<BN, BK, BKC>(ib, wc * 64 + j * 16, s, lane);
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+          const bf16x8 fa = frag<BM, BK, AKC>(ia, wr * (BM / 2) + i * 16, s, lane);
+#pragma unroll
+          for (int j = 0; j < NT; ++j) acc[i][j] = mfma16x16x32(fa, fb[j], acc[i][j]);
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lds_sync();
+    }
+  } else if constexpr (VAR == 3) {
     // register-staged double buffer: tile t+1's global loads are in flight
     // while tile t is multiplied, then written to the other LDS buffer
     static_assert(S == 2, "register staging uses two LDS buffers");
@@ -367,10 +401,11 @@ extern "C" hipError_t dtfk_gemm_big(const void* A, int lda, int transA, const vo
   const dim3 grid((unsigned)tiles, split), block(NTHR);
   const uint16_t* a = static_cast<const uint16_t*>(A);
   const uint16_t* b = static_cast<const uint16_t*>(B);
-// 64-deep tiles, 2 stages for every layout: the 32-deep 5-stage ring and the
-// 128-row tiles measured slower (profiles/gemm_big_cfg_r2.jsonl)
+// 64-deep tiles, 2 stages, one barrier per tile (VAR 4) for every layout: the
+// 32-deep 5-stage ring, 128-row tiles, register staging and the two-barrier
+// loop measured slower (profiles/gemm_big_cfg_r2.jsonl)
 #define DTFK_GB(AK, BKk, OB)                                                                                  \
-  hipLaunchKernelGGL((gemm_big<256, 64, 2, AK, BKk, OB>), grid, block, 0, stream, a, lda, b, ldb, C, ldc, bias, \
+  hipLaunchKernelGGL((gemm_big<256, 64, 2, AK, BKk, OB, 4>), grid, block, 0, stream, a, lda, b, ldb, C, ldc, bias, \
                      M, N, K, alpha, split > 1 ? 1.f : beta, act, kchunk)
 #define DTFK_GB_O(AK, BKk) \
   if (c_bf16) { DTFK_GB(AK, BKk, true); } else { DTFK_GB(AK, BKk, false); }
@@ -406,6 +441,7 @@ extern "C" hipError_t dtfk_gemm_big_cfg(int cfg, const void* A, int lda, const v
     case 6: DTFK_CFG(256, 64, 2, 1); break;
     case 7: DTFK_CFG(256, 64, 2, 2); break;
     case 8: DTFK_CFG(256, 64, 2, 3); break;
+    case 9: DTFK_CFG(256, 64, 2, 4); break;
     default: return hipErrorInvalidValue;
   }
 #undef DTFK_CFG

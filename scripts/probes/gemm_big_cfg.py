@@ -11,7 +11,8 @@ from distributed_tensorflow_example_amd import _native  # noqa: E402
 
 CFG = {0: "256x256 BK32 S5", 1: "256x256 BK64 S2", 2: "128x256 BK64 S3", 3: "128x256 BK32 S5",
        4: "256x256 BK32 S3", 5: "128x256 BK64 S2", 6: "256x256 BK64 S2 reads-first+setprio",
-       7: "256x256 BK64 S2 setprio", 8: "256x256 BK64 register-staged"}
+       7: "256x256 BK64 S2 setprio", 8: "256x256 BK64 register-staged",
+       9: "256x256 BK64 S2 one barrier per tile"}
 C = _native.load()
 for (M, N, K) in [(16384, 3072, 768), (16384, 768, 3072), (8192, 8192, 8192)]:
     torch.cuda.empty_cache()

@@ -104,16 +104,16 @@ def _spawn(fn, ws, *args):
     return sorted(res, key=lambda r: r[0])
 
 
-@pytest.mark.parametrize("ws", [2, 3])
+@pytest.mark.parametrize("ws", [2, 3, 4])
 def test_world_collectives_gloo(ws):
     res = _spawn(_collectives_worker, ws)
     for r in res:
         assert r[1] == "ok", r[1]
 
 
-@pytest.mark.parametrize("bucket_mb", [25.0, 0.001])
-def test_ddp_matches_full_batch_sgd(bucket_mb):
-    res = _spawn(_ddp_worker, 2, bucket_mb)
+@pytest.mark.parametrize("bucket_mb,ws", [(25.0, 2), (0.001, 2), (0.001, 4)])
+def test_ddp_matches_full_batch_sgd(bucket_mb, ws):
+    res = _spawn(_ddp_worker, ws, bucket_mb)
     for r in res:
         assert isinstance(r[1], list), r[1]
     if bucket_mb < 1:
@@ -129,9 +129,10 @@ def test_ddp_matches_full_batch_sgd(bucket_mb):
         opt.zero_grad()
         torch.nn.functional.cross_entropy(ref(X), Y).backward()
         opt.step()
-    for a, b, p in zip(res[0][1], res[1][1], ref.parameters()):
-        a, b = torch.from_numpy(a), torch.from_numpy(b)
-        assert torch.equal(a, b)
+    for i, p in enumerate(ref.parameters()):
+        a = torch.from_numpy(res[0][1][i])
+        for r in range(1, ws):
+            assert torch.equal(a, torch.from_numpy(res[r][1][i]))
         assert torch.allclose(a, p.detach(), atol=1e-5)
 
 

@@ -168,6 +168,25 @@ def test_sharded_table_two_ranks_equal_one(svm_dir):
     assert np.array_equal(saver.read_tensor(prefix, "weights/Variable").numpy(), two[0][2])
 
 
+def test_sharded_table_four_ranks_equal_one(svm_dir):
+    """W = 4 (an 8-GPU node's partition math at half size): 750-row contiguous
+    partitions, the id exchange with 3 peers, sync SGD == one rank on 4x the batch,
+    and TF's partitioned-variable checkpoint with four slices."""
+    from distributed_tensorflow_example_amd.compat import saver
+
+    d, tr, te = svm_dir
+    one = _run(1, tr, 6, 0.5)
+    four = _run(4, tr, 6, 0.5)
+    assert np.array_equal(one[0][1], four[0][1])
+    for r in range(1, 4):
+        assert np.array_equal(four[0][2], four[r][2])
+    assert np.allclose(one[0][2], four[0][2], atol=1e-6)
+    assert abs(one[0][3] - four[0][3]) < 1e-6
+    idx = saver.read_bundle_index(four[0][4])
+    assert idx["weights/Variable"]["slices"] == [[(750 * k, 750), (0, 1)] for k in range(4)]
+    assert np.array_equal(saver.read_tensor(four[0][4], "weights/Variable").numpy(), four[0][2])
+
+
 def test_lr2_example_ps_two_workers(svm_dir, tmp_path):
     d, tr, te = svm_dir
     p = _free_port()

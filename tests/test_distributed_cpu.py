@@ -104,14 +104,14 @@ def _spawn(fn, ws, *args):
     return sorted(res, key=lambda r: r[0])
 
 
-@pytest.mark.parametrize("ws", [2, 3, 4])
+@pytest.mark.parametrize("ws", [2, 3, 4, 8])
 def test_world_collectives_gloo(ws):
     res = _spawn(_collectives_worker, ws)
     for r in res:
         assert r[1] == "ok", r[1]
 
 
-@pytest.mark.parametrize("bucket_mb,ws", [(25.0, 2), (0.001, 2), (0.001, 4)])
+@pytest.mark.parametrize("bucket_mb,ws", [(25.0, 2), (0.001, 2), (0.001, 4), (25.0, 8)])
 def test_ddp_matches_full_batch_sgd(bucket_mb, ws):
     res = _spawn(_ddp_worker, ws, bucket_mb)
     for r in res:

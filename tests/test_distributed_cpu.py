@@ -111,12 +111,12 @@ def test_world_collectives_gloo(ws):
         assert r[1] == "ok", r[1]
 
 
-@pytest.mark.parametrize("bucket_mb,ws", [(25.0, 2), (0.001, 2), (0.001, 4), (25.0, 8)])
+@pytest.mark.parametrize("bucket_mb,ws", [(25.0, 2), (0.001, 2), (0.001, 4), (25.0, 8), ("auto", 2)])
 def test_ddp_matches_full_batch_sgd(bucket_mb, ws):
     res = _spawn(_ddp_worker, ws, bucket_mb)
     for r in res:
         assert isinstance(r[1], list), r[1]
-    if bucket_mb < 1:
+    if bucket_mb != "auto" and bucket_mb < 1:
         assert res[0][2] > 1                            # really bucketed
     from distributed_tensorflow_example_amd.models.mlp import MLP
 
@@ -227,3 +227,19 @@ def test_open_peer_buffers_fails_collectively(how):
         p.join(timeout=60)
     want = "ok" if how == "none" else "raised"
     assert all(v == want for v in res.values()), res
+
+
+def test_auto_bucket_mb_cost_model():
+    """xGMI bucket sizing (ddp.auto_bucket_mb): k = sqrt(S / (alpha * bw)) buckets."""
+    from distributed_tensorflow_example_amd.parallel.ddp import auto_bucket_mb
+
+    bert_bf16 = 110_000_000 * 2
+    assert auto_bucket_mb(bert_bf16, 1) == 256.0                 # no comm: one big bucket
+    sizes = [auto_bucket_mb(bert_bf16, n) for n in (2, 4, 8)]
+    assert all(4.0 <= s <= 256.0 for s in sizes)
+    assert sizes == sorted(sizes)                              # more hops -> fewer, larger buckets
+    n_buckets = bert_bf16 / 2**20 / sizes[-1]
+    assert 3 <= round(n_buckets) <= 8
+    assert auto_bucket_mb(1000, 8) == 4.0                      # tiny models clamp at the floor
+    # slower hops favour fewer buckets
+    assert auto_bucket_mb(bert_bf16, 8, hop_us=30.0) > sizes[-1]

@@ -222,9 +222,8 @@ class DistributedDataParallel(torch.nn.Module):
                     if self.average:
                         b.buf.mul_(scale)
                 else:
-                    w.comm.all_reduce(b.buf, "sum")
-                    if self.average:
-                        b.buf.mul_(scale)
+                    # RCCL's ncclAvg divides inside the reduction: no extra pass over the bucket
+                    w.comm.all_reduce(b.buf, "avg" if self.average else "sum")
             b.event = torch.cuda.Event()
             b.event.record(self.comm_stream)
         else:

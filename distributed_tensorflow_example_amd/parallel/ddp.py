@@ -31,11 +31,15 @@ count from that cost model: k buckets cost k * alpha of fixed ring latency
 so the exposed time k * alpha + S / (k * bw) is smallest at k = sqrt(S / (alpha
 * bw)).  For BERT-base at n = 8 with bf16 gradients that is 5 buckets of
 ~42 MB on the wire (84 MB of fp32 gradient each); ResNet-50 gets ~16 MB.
+`bucket_mb="measure"` replaces the link model by this machine's numbers: a
+tiny and a 32 MB all-reduce are timed at construction (max over ranks, so all
+ranks agree on the layout).
 """
 from __future__ import annotations
 
 import math
 import os
+import time
 from typing import List, Optional, Union
 
 import torch
@@ -59,19 +63,46 @@ XGMI_HOP_US = 6.0
 
 
 def auto_bucket_mb(comm_bytes: int, world_size: int, link_gbps: float = XGMI_LINK_GBPS,
-                   hop_us: float = XGMI_HOP_US, min_mb: float = 4.0, max_mb: float = 256.0) -> float:
+                   hop_us: float = XGMI_HOP_US, min_mb: float = 4.0, max_mb: float = 256.0,
+                   alpha_s: Optional[float] = None, bw_bps: Optional[float] = None) -> float:
     """Bucket size minimising exposed all-reduce time, in MiB of wire bytes.
 
     comm_bytes: bytes that go over the wire per step (all gradients, in the
-    communication dtype).
+    communication dtype).  alpha_s / bw_bps, when given (measure_allreduce_cost),
+    replace the link model: fixed seconds per all-reduce and bucket bytes per second.
     """
     if world_size <= 1 or comm_bytes <= 0:
         return max_mb
     n = world_size
-    alpha = 2 * (n - 1) * hop_us * 1e-6                      # s of fixed latency per all-reduce
-    bw = link_gbps * 1e9 * n / (2 * (n - 1))                  # bucket bytes reduced per second
+    alpha = alpha_s if alpha_s else 2 * (n - 1) * hop_us * 1e-6      # s of fixed latency per all-reduce
+    bw = bw_bps if bw_bps else link_gbps * 1e9 * n / (2 * (n - 1))   # bucket bytes reduced per second
     k = max(1, round(math.sqrt(comm_bytes / bw / alpha)))
     return float(min(max_mb, max(min_mb, comm_bytes / k / 2**20)))
+
+
+def measure_allreduce_cost(world: World, device: torch.device, dtype=torch.float32, big_mb: float = 32.0,
+                           iters: int = 5):
+    """Time a tiny and a `big_mb` all-reduce on this world's data plane (RCCL on
+    GPU, gloo on CPU): returns (alpha seconds, bytes per second), max over ranks
+    so every rank derives the same bucket layout."""
+    def timed(numel):
+        t = torch.zeros(numel, dtype=dtype, device=device)
+        world.all_reduce(t)                                   # warm the path / connections
+        ts = []
+        for _ in range(iters):
+            if device.type == "cuda":
+                torch.cuda.synchronize(device)
+            t0 = time.perf_counter()
+            world.all_reduce(t)
+            if device.type == "cuda":
+                torch.cuda.synchronize(device)
+            ts.append(time.perf_counter() - t0)
+        return sorted(ts)[len(ts) // 2]
+    esz = torch.empty((), dtype=dtype).element_size()
+    n_big = int(big_mb * 2**20) // esz
+    t_small = world.host_all_reduce(timed(256), "max")
+    t_big = world.host_all_reduce(timed(n_big), "max")
+    return t_small, n_big * esz / max(t_big - t_small, 1e-9)
 
 
 class _Bucket:
@@ -114,11 +145,16 @@ class DistributedDataParallel(torch.nn.Module):
         self.device = params[0].device
         self.comm_dtype = comm_dtype
         bucket_mb = os.environ.get("DTF_BUCKET_MB", bucket_mb)
-        if bucket_mb == "auto":
+        self.comm_cost = None
+        if bucket_mb in ("auto", "measure"):
             wire = 2 if comm_dtype in (torch.bfloat16, torch.float16) else 4
             n_el = sum(p.numel() for p in params)
+            if bucket_mb == "measure" and self.world.world_size > 1:
+                # this machine's alpha / bandwidth instead of the xGMI link model
+                self.comm_cost = measure_allreduce_cost(self.world, self.device, comm_dtype or torch.float32)
+            a_s, bw = self.comm_cost or (None, None)
             # buckets are packed in fp32: scale the wire-byte size back up
-            bucket_mb = auto_bucket_mb(n_el * wire, self.world.world_size) * 4 / wire
+            bucket_mb = auto_bucket_mb(n_el * wire, self.world.world_size, alpha_s=a_s, bw_bps=bw) * 4 / wire
         self.bucket_mb = float(bucket_mb)
         # reverse registration order ~ gradient production order
         buckets, cur, cur_bytes = [], [], 0

@@ -42,7 +42,7 @@ def main():
                          "F=1e9 features, batch 500, learning rate 1.0)")
     ap.add_argument("--seq", type=int, default=128)
     ap.add_argument("--bucket-mb", default="auto",
-                    help="DDP bucket size in MB of fp32 gradient, or auto (xGMI cost model, parallel/ddp.py)")
+                    help="DDP bucket size in MB of fp32 gradient, auto (xGMI cost model) or measure (timed all-reduces; parallel/ddp.py)")
     ap.add_argument("--bucket-sweep", default="",
                     help="dense models: comma-separated bucket sizes in MB (e.g. 1,4,16,64) re-timed after the main "
                          "run; ms/step per size lands in the JSON line (xGMI bucket sizing, SURVEY s5.8)")
@@ -166,9 +166,12 @@ def dense_bench(a, w):
                "conv_solver_search": bool(a.conv_find)}
         run = lambda m, b: m.loss(*b)
     comm_dtype = torch.bfloat16 if a.comm_bf16 else None
-    ddp = DistributedDataParallel(model, w, bucket_mb=a.bucket_mb if a.bucket_mb == "auto" else float(a.bucket_mb),
+    ddp = DistributedDataParallel(model, w, bucket_mb=a.bucket_mb if a.bucket_mb in ("auto", "measure") else float(a.bucket_mb),
                                   comm_dtype=comm_dtype)
     cfg["grad_allreduce"] = f"bucketed {ddp.bucket_mb:.1f}MB x {len(ddp.buckets)} ({a.bucket_mb}), overlapped"
+    if ddp.comm_cost:
+        cfg["allreduce_alpha_us"] = round(ddp.comm_cost[0] * 1e6, 2)
+        cfg["allreduce_GBps"] = round(ddp.comm_cost[1] / 1e9, 2)
     if not a.no_shadow:
         model.attach_shadows(opt)          # after the DDP broadcast: shadows match rank 0's weights
 

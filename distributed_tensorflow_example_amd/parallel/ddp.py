@@ -253,10 +253,8 @@ class DistributedDataParallel(torch.nn.Module):
                     C.bucket_unpack_bf16(b.comm_buf, b.buf, 1.0)
                 elif self.comm_dtype is not None and self.comm_dtype != torch.float32:
                     b.comm_buf = b.buf.to(self.comm_dtype)
-                    w.comm.all_reduce(b.comm_buf, "sum")
+                    w.comm.all_reduce(b.comm_buf, "avg" if self.average else "sum")
                     b.buf.copy_(b.comm_buf)
-                    if self.average:
-                        b.buf.mul_(scale)
                 else:
                     # RCCL's ncclAvg divides inside the reduction: no extra pass over the bucket
                     w.comm.all_reduce(b.buf, "avg" if self.average else "sum")

@@ -9,7 +9,7 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("op", ["sum", "avg", "max", "min"])
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 def test_rccl_world1_ops_identity(native, op, dtype):
     comm = native.RcclComm(native.rccl_unique_id(), 1, 0)
     t = torch.randn(4099, device="cuda").to(dtype)

@@ -15,6 +15,8 @@ import sys
 
 def main():
     args = sys.argv[1:]
+    if not args or args[0] in ("-h", "--help"):
+        raise SystemExit(__doc__)
     after = None
     if "--after" in args:
         i = args.index("--after")
@@ -22,7 +24,8 @@ def main():
         args = args[:i] + args[i + 2:]
     db = args[0]
     out = args[1] if len(args) > 1 else None
-    c = sqlite3.connect(db)
+    # read-only: a mistyped path must not create an empty database
+    c = sqlite3.connect(f"file:{db}?mode=ro", uri=True)
     where = ""
     if after:
         t = c.execute("select max(end) from kernels where name like ?", (f"%{after}%",)).fetchone()[0]

@@ -44,6 +44,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 if REPO not in sys.path:
     sys.path.insert(0, REPO)
 
+from distributed_tensorflow_example_amd import _native  # noqa: E402
 from distributed_tensorflow_example_amd.data.mnist import PinnedEpoch, synthetic_mnist  # noqa: E402
 from distributed_tensorflow_example_amd.models.mlp import (  # noqa: E402
     FusedMLPTrainer, MLPStepRunner, PersistentMLPRunner)
@@ -329,6 +330,7 @@ def main(argv=None):
                                        "weights"}[a.precision]
                               if persistent else "bf16 MFMA operands, fp32 accumulate, fp32 master weights"),
             },
+            "native_src_hash": _native.src_hash(),
             "final_loss": round(float(m[0]), 5),
             "final_batch_acc": round(float(m[1]), 4),
             "global_steps_timed": steps_done,

@@ -27,6 +27,8 @@ hipError_t dtfk_gemm(const void* A, int a_bf16, int lda, int transA, const void*
 hipError_t dtfk_gemm_big(const void* A, int lda, int transA, const void* B, int ldb, int transB, void* C,
                          int c_bf16, int ldc, const float* bias, int M, int N, int K, float alpha, float beta,
                          int act, int split_k, hipStream_t stream);
+int dtfk_gemm_big_supported(const void* A, int lda, int transA, const void* B, int ldb, int transB, int c_bf16, int M,
+                            int N, int K, float beta, int act, int split_k);
 hipError_t dtfk_gemm_big_cfg(int cfg, const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N,
                              int K, hipStream_t stream);
 hipError_t dtfk_act_backward(const float* dy, const float* y, const float* z, float* dz, int64_t n, int act,
@@ -132,11 +134,13 @@ bool gemm_big(at::Tensor A, bool transA, at::Tensor B, bool transB, at::Tensor o
   if (K != KB) throw std::runtime_error("gemm_big inner dimensions differ");
   if (out.size(0) != M || out.size(1) != N) throw std::runtime_error("gemm_big out has wrong shape");
   if (bias.has_value()) { f32c(*bias, "bias"); if (bias->numel() != N) throw std::runtime_error("bias size"); }
-  const hipError_t e = dtfk_gemm_big(A.data_ptr(), (int)A.stride(0), transA, B.data_ptr(), (int)B.stride(0), transB,
-                                     out.data_ptr(), out.scalar_type() == at::kBFloat16, (int)out.stride(0),
-                                     opt_ptr<float>(bias), M, N, K, (float)alpha, (float)beta, act, split_k, cs());
-  if (e == hipErrorInvalidValue) { (void)hipGetLastError(); return false; }
-  ck(e, "gemm_big");
+  const int obf = out.scalar_type() == at::kBFloat16;
+  if (!dtfk_gemm_big_supported(A.data_ptr(), (int)A.stride(0), transA, B.data_ptr(), (int)B.stride(0), transB, obf, M,
+                               N, K, (float)beta, act, split_k))
+    return false;   // outside the kernel's contract: the caller picks another GEMM
+  ck(dtfk_gemm_big(A.data_ptr(), (int)A.stride(0), transA, B.data_ptr(), (int)B.stride(0), transB, out.data_ptr(), obf,
+                   (int)out.stride(0), opt_ptr<float>(bias), M, N, K, (float)alpha, (float)beta, act, split_k, cs()),
+     "gemm_big");   // any launch error is a real error
   return true;
 }
 

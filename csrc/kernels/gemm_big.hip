@@ -367,28 +367,42 @@ __global__ __launch_bounds__(NTHR) void gemm_big(const uint16_t* __restrict__ A,
 }  // namespace gemm2
 }  // namespace dtfk
 
+// The shape / alignment contract of dtfk_gemm_big, checked on the host before
+// any launch: callers pick another GEMM when it fails, and every error the
+// launch itself returns is a real error (never mistaken for "unsupported").
+extern "C" int dtfk_gemm_big_supported(const void* A, int lda, int transA, const void* B, int ldb, int transB,
+                                       int c_bf16, int M, int N, int K, float beta, int act, int split_k) {
+  using namespace dtfk::gemm2;
+  const bool akc = !transA, bkc = transB != 0;
+  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (M <= 0 || N <= 0 || K <= 0 || K % KQ != 0 || !al16(A) || !al16(B) || lda % 8 || ldb % 8) return 0;
+  if ((!akc && M % 8) || (!bkc && N % 8) || (akc && lda < K) || (bkc && ldb < K) || (!akc && lda < M) ||
+      (!bkc && ldb < N))
+    return 0;
+  const long long tiles = (long long)((M + 255) / 256) * ((N + BN - 1) / BN);
+  if (tiles > 0x7fffffff) return 0;
+  const bool linear = act == ACT_NONE && !c_bf16 && (beta == 0.f || beta == 1.f);
+  if (split_k > 1 && !linear) return 0;
+  return 1;
+}
+
 // Returns hipErrorInvalidValue (launching nothing) when the shape contract
-// does not hold; the caller then uses another GEMM.  split_k <= 0: automatic.
+// (dtfk_gemm_big_supported) does not hold.  split_k <= 0: automatic.
 extern "C" hipError_t dtfk_gemm_big(const void* A, int lda, int transA, const void* B, int ldb, int transB,
                                     void* C, int c_bf16, int ldc, const float* bias, int M, int N, int K,
                                     float alpha, float beta, int act, int split_k, hipStream_t stream) {
   using namespace dtfk::gemm2;
   const bool akc = !transA, bkc = transB != 0;
-  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-  if (M <= 0 || N <= 0 || K <= 0 || K % KQ != 0 || !al16(A) || !al16(B) || lda % 8 || ldb % 8) return hipErrorInvalidValue;
-  if ((!akc && M % 8) || (!bkc && N % 8) || (akc && lda < K) || (bkc && ldb < K) || (!akc && lda < M) ||
-      (!bkc && ldb < N))
+  if (!dtfk_gemm_big_supported(A, lda, transA, B, ldb, transB, c_bf16, M, N, K, beta, act, split_k))
     return hipErrorInvalidValue;
   const int tn = (N + BN - 1) / BN;
   // 256 x 256 tiles even when they leave CUs idle (N = 768: 192 tiles): measured
   // faster than 128 x 256 at every BERT shape (scripts/probes/gemm_big_cfg.py)
   const int BMsel = 256;
   const long long tiles = (long long)((M + BMsel - 1) / BMsel) * tn;
-  if (tiles > 0x7fffffff) return hipErrorInvalidValue;
   int split = 1, kchunk = K;
   const bool linear = act == ACT_NONE && !c_bf16 && (beta == 0.f || beta == 1.f);
   if (split_k > 1 || (split_k <= 0 && linear && tiles < 256 && K >= 2048)) {
-    if (!linear) return hipErrorInvalidValue;
     split = split_k > 1 ? split_k : (int)((512 + tiles - 1) / tiles);
     split = min(split, K / 512 > 0 ? K / 512 : 1);
     kchunk = ((K + split - 1) / split + KQ - 1) / KQ * KQ;

@@ -41,10 +41,17 @@
 //  * 16 COPIER workgroups pull chunk c+1 from pinned host memory over PCIe into
 //    the other device stage (row-major x, feature-major x^T, labels) while the
 //    compute workgroups run chunk c.
-//  * N GPUs (MULTI): after P2 every compute workgroup exchanges its gradient
-//    (its dW1 tiles + the block's small gradients) with the same workgroup on
-//    every peer through IPC-mapped uncached buffers -- 28 CUs per GPU carry the
-//    peer traffic -- and sums the ranks in rank order (bit-identical replicas).
+//  * N GPUs (MULTI, NW = the peer-table width W is unrolled for: 2, 4, 8):
+//    after P2 every compute workgroup exchanges its gradient (its dW1 tiles +
+//    the block's small gradients) with the same workgroup on every peer through
+//    IPC-mapped uncached buffers -- 28 CUs per GPU carry the peer traffic, every
+//    peer read a 16-B system-scope buffer load, all NW in flight at once -- and
+//    sums the ranks in rank order (bit-identical replicas).  Publication order:
+//    the slot bytes go to uncached (MTYPE UC) memory with plain stores, every
+//    storing wave waits for them (vmcnt(0)), then a workgroup barrier, then ONE
+//    relaxed system-scope flag store; consumers poll the flag with system-scope
+//    loads and read the bytes with system-scope (sc0 sc1) loads, never served
+//    from a cache of the reading device.
 //
 // Placement: packed (default) runs workgroup c as blockIdx 8c, so under the
 // observed round-robin dispatch all 28 share one XCD and both edges stay in one
@@ -95,11 +102,16 @@ constexpr long long E2_OFF = E1_OFF + 2LL * NJ * NQ * NBT * GSLOT;
 constexpr long long HDR_OFF = E2_OFF + 2LL * NQ * NBT * NJ * GSLOT;   // [64] u64 placement census
 constexpr long long XBUF_BYTES = HDR_OFF + 64 * 8;
 
-// IPC buffer of one rank (N GPUs): [flags: workgroup c at byte 64c][2 parities][49 slots]
-// slot: 7 dW1 tiles x 64 lanes x 16 B (fp32; bf16 payload uses the first 8 B of
-// each 16) | dW2 64 lanes x 16 B | db1 (16) db2 (16) fp32
-// Two-shot mode adds a reduced area of the same slot layout (fp32 sums) behind
-// the slots, and a second flag per workgroup at byte 64c + 8.
+// IPC buffer of one rank (N GPUs): [flags: workgroup c at byte 64c][2 parities][28 slots]
+// slot: dW1 entries of wave w, lane l at 16 (w 64 + l) (bf16: both tiles' 4 bf16 in
+// one 16-B entry, 8 B when the wave has one tile) or 16 ((2 w + k) 64 + l) (fp32:
+// one entry per tile k) | dW2 64 lanes x 16 B at IPC_SMALL | db1 / db2 (16 + 10)
+// fp32 behind it.  Lanes of padding units and the zero dW2 columns are never
+// stored or loaded: the bytes read from a peer are the payload
+// (scripts/exchange_cost_model.py, tests/test_exchange_model_cpu.py).
+// Two-shot mode adds a reduced area of the same slot layout (the owner's sums:
+// bf16 for a bf16 payload, rounded once by the owner) behind the slots, and a
+// second flag per workgroup at byte 64c + 8.
 constexpr int IPC_FLAGS = 4096;
 constexpr int IPC_SMALL = 8 * NTW * 64 * 16;
 constexpr int IPC_SLOT = IPC_SMALL + 1024 + 128;
@@ -330,6 +342,121 @@ __device__ __forceinline__ bool gather_gran(__amdgpu_buffer_rsrc_t rs, SlotOff s
   }
 }
 
+// ------------------------------------------------------------------ N-GPU exchange loads
+// Peer IPC buffers are read with 16-B (8-B / 4-B) system-scope loads (sc0 sc1:
+// never served from a cache of this device) through a wave-uniform buffer
+// resource per rank.  Loads of ranks outside `sel`, of ranks >= W and of
+// masked lanes use an offset past the buffer's range: the buffer unit returns
+// zero without touching memory, so the NW loads of a lane stay unconditional
+// (no branch, no wait between them: all in flight at once) and only payload
+// crosses the fabric.
+typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
+constexpr int SYS = 1 | 16;            // sc0 | sc1
+constexpr int OOB_OFF = 0x7ffffff0;
+// one resource per rank, built once per launch in SGPRs (the table entry is read
+// by one lane and broadcast: a per-use vector load of the pointer would turn
+// every peer load into a waterfall loop behind a vmcnt(0))
+template <int NW>
+struct PeerRs {
+  __amdgpu_buffer_rsrc_t r[NW];
+};
+template <int NW>
+__device__ __forceinline__ PeerRs<NW> peer_rsrcs(void* const* peers, int W) {
+  PeerRs<NW> o;
+#pragma unroll
+  for (int r = 0; r < NW; ++r) {
+    const unsigned long long u = reinterpret_cast<unsigned long long>(peers[r < W ? r : 0]);
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)u);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
+    void* pp = reinterpret_cast<void*>(((unsigned long long)hi << 32) | lo);
+    o.r[r] = __builtin_amdgcn_make_buffer_rsrc(pp, 0, (int)IPC_BYTES, 0x00020000);
+  }
+  return o;
+}
+__device__ __forceinline__ f32x4 unbf4(uint32_t lo, uint32_t hi) {
+  return f32x4{__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u), __uint_as_float(hi << 16),
+               __uint_as_float(hi & 0xffff0000u)};
+}
+__device__ __forceinline__ f32x4 round_bf16x4(f32x4 v) {
+  const uint32_t lo = pack2bf(v[0], v[1]), hi = pack2bf(v[2], v[3]);
+  return unbf4(lo, hi);
+}
+// Rank-order sum of this lane's dW1 entries over the W ranks (this rank's own
+// term G0 / G1 from registers), GRP peer loads in flight per group.  BF: both
+// tiles' bf16 in ONE 16-B entry at e0 (TWO false: the wave has one tile, 8 B);
+// fp32: one 16-B entry per tile at e0 / e1.
+template <int NW, int GRP, bool BF, bool TWO>
+__device__ __forceinline__ void sum_entries(const PeerRs<NW>& prs, int W, int rank, int so, bool hv, int e0, int e1,
+                                            f32x4& G0, f32x4& G1) {
+  f32x4 S0 = {0.f, 0.f, 0.f, 0.f}, S1 = S0;
+#pragma unroll
+  for (int r0 = 0; r0 < NW; r0 += GRP) {
+    if (r0 >= W) break;   // wave-uniform
+    u32x4 v0[GRP], v1[GRP];
+#pragma unroll
+    for (int i = 0; i < GRP; ++i) {
+      const int r = r0 + i;
+      const bool on = r < W && r != rank && hv;
+      const auto rs = prs.r[r];
+      if constexpr (BF) {
+        if constexpr (TWO) {
+          v0[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, on ? so + e0 : OOB_OFF, 0, SYS);
+        } else {
+          const u32x2 h = __builtin_amdgcn_raw_buffer_load_b64(rs, on ? so + e0 : OOB_OFF, 0, SYS);
+          v0[i] = u32x4{h[0], h[1], 0u, 0u};
+        }
+      } else {
+        v0[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, on ? so + e0 : OOB_OFF, 0, SYS);
+        if constexpr (TWO) v1[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, on ? so + e1 : OOB_OFF, 0, SYS);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < GRP; ++i) {
+      const int r = r0 + i;
+      if (r >= W) break;
+      const bool me = r == rank;
+      f32x4 P0, P1 = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (BF) {
+        P0 = unbf4(v0[i][0], v0[i][1]);
+        if constexpr (TWO) P1 = unbf4(v0[i][2], v0[i][3]);
+      } else {
+        P0 = __builtin_bit_cast(f32x4, v0[i]);
+        if constexpr (TWO) P1 = __builtin_bit_cast(f32x4, v1[i]);
+      }
+      S0 += me ? G0 : P0;
+      S1 += me ? G1 : P1;
+    }
+  }
+  G0 = S0;
+  G1 = S1;
+}
+// wave 7's small part: rank-order sums of the dW2 entry (16 B, lanes with data)
+// and db1 / db2 (4 B)
+template <int NW>
+__device__ __forceinline__ void sum_small(const PeerRs<NW>& prs, int W, int rank, int so, bool dlane, bool blane,
+                                          int lane, f32x4& D, float& gb) {
+  u32x4 d[NW];
+  uint32_t b[NW];
+#pragma unroll
+  for (int r = 0; r < NW; ++r) {
+    const bool on = r < W && r != rank;
+    const auto rs = prs.r[r];
+    d[r] = __builtin_amdgcn_raw_buffer_load_b128(rs, (on && dlane) ? so + lane * 16 : OOB_OFF, 0, SYS);
+    b[r] = __builtin_amdgcn_raw_buffer_load_b32(rs, (on && blane) ? so + 1024 + lane * 4 : OOB_OFF, 0, SYS);
+  }
+  f32x4 SD = {0.f, 0.f, 0.f, 0.f};
+  float SB = 0.f;
+#pragma unroll
+  for (int r = 0; r < NW; ++r) {
+    if (r >= W) break;
+    const bool me = r == rank;
+    SD += me ? D : __builtin_bit_cast(f32x4, d[r]);
+    SB += me ? gb : __uint_as_float(b[r]);
+  }
+  D = SD;
+  gb = SB;
+}
+
 // ------------------------------------------------------------------ copier
 // task = one step of the next chunk: 112 rows of 784 pixels from the pinned host
 // record into LDS (rows >= B zero), then the row-major image, the feature-major
@@ -384,8 +511,9 @@ __device__ void copier(const Args& a, int cid, uint8_t* smem) {
 // three-way split of their fp32 operand (pixels are exact in bf16), so every
 // product is exact and accumulates in fp32 -- 16x16x32 bf16 MFMAs at 8x the
 // f32-MFMA rate; the head stays on f32-input MFMA
-template <int ACT, bool MULTI, bool SPLIT>
+template <int ACT, int NW, bool SPLIT>
 __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) {
+  constexpr bool MULTI = NW > 1;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int c = j * NQ + q;
@@ -550,6 +678,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
   read_xt();
   if (tid == 0) { PRO(c, 2); }
 
+  const PeerRs<NW> prs = peer_rsrcs<NW>(a.peer_base, MULTI ? a.W : 1);
   bool aborted = false;
   for (int st = 0; st < a.nsteps; ++st) {
     const unsigned long long sq = seq0 + (unsigned long long)st + 1ull;
@@ -820,25 +949,41 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
     if (more) read_xt();   // next step's weight-gradient operands (this step's are consumed)
     if (w == 0) { PH(11); }
     if constexpr (MULTI) {
-      // ---- one-shot exchange of this workgroup's gradient with the same
-      // workgroup on every peer GPU (uncached IPC buffers: completion ==
-      // visibility); rank-order sums keep the replicas bit-identical
+      // ---- exchange of this workgroup's gradient with the same workgroup on
+      // every peer GPU (uncached IPC buffers: completion == visibility); sums in
+      // rank order keep the replicas bit-identical.  Only payload crosses the
+      // fabric: bf16 packs a lane's two tiles into ONE 16-B entry (8 B when the
+      // wave has one tile), hidden-padding lanes (unit >= 100) and the zero
+      // columns of dW2 (class >= 10) neither store nor load, and every peer is
+      // read with single 16-B system-scope loads, all NW of them in flight
+      // (absent peers / masked lanes read out of the buffer's range: zero, no
+      // memory traffic).
+      const bool pk = a.gbf16 != 0;
       const size_t soff = IPC_FLAGS + (size_t)(par * NCOMP + c) * IPC_SLOT;
       char* own = static_cast<char*>(a.peer_base[a.rank]) + soff;
-#pragma unroll
-      for (int k = 0; k < NTW; ++k) {
-        char* p = own + ((w * NTW + k) * 64 + lane) * 16;
-        if (a.gbf16) {
-          const uint2 v = make_uint2(pack2bf(G[k][0], G[k][1]), pack2bf(G[k][2], G[k][3]));
-          G[k] = f32x4{bf2f(v.x & 0xffff), bf2f(v.x >> 16), bf2f(v.y & 0xffff), bf2f(v.y >> 16)};
-          if (tvk(k)) *reinterpret_cast<uint2*>(p) = v;
-        } else if (tvk(k)) {
-          *reinterpret_cast<f32x4*>(p) = G[k];
+      const int eb = (w * 64 + lane) * 16;                       // bf16: both tiles
+      const int ef0 = ((w * NTW + 0) * 64 + lane) * 16;          // fp32: tile 0
+      const int ef1 = ((w * NTW + 1) * 64 + lane) * 16;          // fp32: tile 1
+      const bool dlane = r < NCLS && 16 * j + 4 * g < HID;       // wave 7: dW2 entry carries data
+      const bool blane = lane < 16 ? 16 * j + lane < HID : lane < 16 + NCLS;   // wave 7: db1 / db2
+      if (hv) {
+        if (pk) {
+          const uint32_t p0 = pack2bf(G[0][0], G[0][1]), p1 = pack2bf(G[0][2], G[0][3]);
+          const uint32_t p2 = pack2bf(G[1][0], G[1][1]), p3 = pack2bf(G[1][2], G[1][3]);
+          if (tv1) *reinterpret_cast<uint4*>(own + eb) = make_uint4(p0, p1, p2, p3);
+          else if (tv0) *reinterpret_cast<uint2*>(own + eb) = make_uint2(p0, p1);
+        } else {
+          if (tv0) *reinterpret_cast<f32x4*>(own + ef0) = G[0];
+          if (tv1) *reinterpret_cast<f32x4*>(own + ef1) = G[1];
         }
       }
+      if (pk) {   // this rank's own term, as every peer sees it
+        G[0] = round_bf16x4(G[0]);
+        G[1] = round_bf16x4(G[1]);
+      }
       if (w == 7) {
-        *reinterpret_cast<f32x4*>(own + IPC_SMALL + lane * 16) = D;
-        if (lane < 16 + NCLS) *reinterpret_cast<float*>(own + IPC_SMALL + 1024 + lane * 4) = gb;
+        if (dlane) *reinterpret_cast<f32x4*>(own + IPC_SMALL + lane * 16) = D;
+        if (blane) *reinterpret_cast<float*>(own + IPC_SMALL + 1024 + lane * 4) = gb;
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave: its slot stores landed
       lds_barrier();
@@ -875,79 +1020,48 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
                            __HIP_MEMORY_SCOPE_SYSTEM);
       wait_peers(0);
       if (*abort_flag) { aborted = true; break; }
-      // this lane's entry of wave w's chunk in a slot (dW1 tiles) / the small part (wave 7)
-      auto ld_slot = [&](const char* ps, int k) -> f32x4 {
-        const char* pk = ps + ((w * NTW + k) * 64 + lane) * 16;
-        if (a.gbf16) {
-          const unsigned long long x = ld_sys_u64(pk);
-          return f32x4{bf2f((unsigned)x & 0xffff), bf2f(((unsigned)x) >> 16), bf2f((unsigned)(x >> 32) & 0xffff),
-                       bf2f((unsigned)(x >> 48))};
+      // rank-order sums of this lane's entries at slot offset `so` over all ranks
+      auto sum_ranks = [&](size_t so) {
+        constexpr int GF = NW < 4 ? NW : 4;   // fp32 payload: 4 peers in flight per group (registers)
+        if (pk) {
+          if (tv1) sum_entries<NW, NW, true, true>(prs, a.W, a.rank, (int)so, hv, eb, eb, G[0], G[1]);
+          else sum_entries<NW, NW, true, false>(prs, a.W, a.rank, (int)so, hv, eb, eb, G[0], G[1]);
+        } else {
+          if (tv1) sum_entries<NW, GF, false, true>(prs, a.W, a.rank, (int)so, hv, ef0, ef1, G[0], G[1]);
+          else sum_entries<NW, GF, false, false>(prs, a.W, a.rank, (int)so, hv, ef0, ef1, G[0], G[1]);
         }
-        return ld_sys_f32x4(pk);
+        if (w == 7) sum_small<NW>(prs, a.W, a.rank, (int)so + IPC_SMALL, dlane, blane, lane, D, gb);
       };
       if (a.xmode == 0) {
-        // one-shot: every wave sums its entries over all ranks (rank order)
-        f32x4 sum[NTW];
-        f32x4 sD = {0.f, 0.f, 0.f, 0.f};
-        float sb = 0.f;
-#pragma unroll
-        for (int k = 0; k < NTW; ++k) sum[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-        for (int rr = 0; rr < a.W; ++rr) {
-          const char* ps = static_cast<const char*>(a.peer_base[rr]) + soff;
-#pragma unroll
-          for (int k = 0; k < NTW; ++k) sum[k] += (rr != a.rank && tvk(k)) ? ld_slot(ps, k) : G[k];
-          if (w == 7) {
-            f32x4 v = D;
-            float vb = gb;
-            if (rr != a.rank) {
-              v = ld_sys_f32x4((ps + IPC_SMALL + lane * 16));
-              vb = lane < 16 + NCLS ? ld_sys_f32(ps + IPC_SMALL + 1024 + 4 * lane) : 0.f;
-            }
-            sD += v;
-            sb += vb;
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < NTW; ++k) G[k] = sum[k];
-        if (w == 7) { D = sD; gb = sb; }
+        // one-shot: every wave sums its entries over all ranks
+        sum_ranks(soff);
       } else {
         // two-shot: wave w's entries form chunk w % W, reduced (rank order) by
         // that rank only, then every rank reads each chunk's sums from its owner:
-        // 2 (W-1)/W of a slot crosses the fabric per GPU instead of (W-1) slots
+        // 2 (W-1)/W of a slot crosses the fabric per GPU instead of (W-1) slots.
+        // bf16 payload: the owner rounds the sum to bf16 once and uses the rounded
+        // value itself, so the all-gather moves bf16 too and replicas stay identical
         const int own_chunk = w % a.W;
         const size_t roff = IPC_RED + (size_t)(par * NCOMP + c) * IPC_SLOT;
         char* ored = static_cast<char*>(a.peer_base[a.rank]) + roff;
         if (own_chunk == a.rank) {
-          f32x4 sum[NTW];
-          f32x4 sD = {0.f, 0.f, 0.f, 0.f};
-          float sb = 0.f;
-#pragma unroll
-          for (int k = 0; k < NTW; ++k) sum[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-          for (int rr = 0; rr < a.W; ++rr) {
-            const char* ps = static_cast<const char*>(a.peer_base[rr]) + soff;
-#pragma unroll
-            for (int k = 0; k < NTW; ++k) sum[k] += (rr != a.rank && tvk(k)) ? ld_slot(ps, k) : G[k];
-            if (w == 7) {
-              f32x4 v = D;
-              float vb = gb;
-              if (rr != a.rank) {
-                v = ld_sys_f32x4((ps + IPC_SMALL + lane * 16));
-                vb = lane < 16 + NCLS ? ld_sys_f32(ps + IPC_SMALL + 1024 + 4 * lane) : 0.f;
-              }
-              sD += v;
-              sb += vb;
+          sum_ranks(soff);
+          if (hv) {
+            if (pk) {
+              const uint32_t p0 = pack2bf(G[0][0], G[0][1]), p1 = pack2bf(G[0][2], G[0][3]);
+              const uint32_t p2 = pack2bf(G[1][0], G[1][1]), p3 = pack2bf(G[1][2], G[1][3]);
+              if (tv1) *reinterpret_cast<uint4*>(ored + eb) = make_uint4(p0, p1, p2, p3);
+              else if (tv0) *reinterpret_cast<uint2*>(ored + eb) = make_uint2(p0, p1);
+              G[0] = round_bf16x4(G[0]);
+              G[1] = round_bf16x4(G[1]);
+            } else {
+              if (tv0) *reinterpret_cast<f32x4*>(ored + ef0) = G[0];
+              if (tv1) *reinterpret_cast<f32x4*>(ored + ef1) = G[1];
             }
           }
-#pragma unroll
-          for (int k = 0; k < NTW; ++k) {
-            G[k] = sum[k];
-            if (tvk(k)) *reinterpret_cast<f32x4*>(ored + ((w * NTW + k) * 64 + lane) * 16) = sum[k];
-          }
           if (w == 7) {
-            D = sD;
-            gb = sb;
-            *reinterpret_cast<f32x4*>(ored + IPC_SMALL + lane * 16) = D;
-            if (lane < 16 + NCLS) *reinterpret_cast<float*>(ored + IPC_SMALL + 1024 + lane * 4) = gb;
+            if (dlane) *reinterpret_cast<f32x4*>(ored + IPC_SMALL + lane * 16) = D;
+            if (blane) *reinterpret_cast<float*>(ored + IPC_SMALL + 1024 + lane * 4) = gb;
           }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the reduced chunk landed
@@ -958,13 +1072,31 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
         wait_peers(8);
         if (*abort_flag) { aborted = true; break; }
         if (own_chunk != a.rank) {
-          const char* pr = static_cast<const char*>(a.peer_base[own_chunk]) + roff;
+          // all-gather: this wave's chunk sums from their owner
+          __amdgpu_buffer_rsrc_t rs = prs.r[0];
 #pragma unroll
-          for (int k = 0; k < NTW; ++k)
-            if (tvk(k)) G[k] = ld_sys_f32x4(pr + ((w * NTW + k) * 64 + lane) * 16);
+          for (int rr = 1; rr < NW; ++rr)
+            if (rr == own_chunk) rs = prs.r[rr];   // wave-uniform
+          const int ro = (int)roff;
+          if (pk) {
+            if (tv1) {
+              const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, hv ? ro + eb : OOB_OFF, 0, SYS);
+              G[0] = unbf4(v[0], v[1]);
+              G[1] = unbf4(v[2], v[3]);
+            } else {
+              const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, hv ? ro + eb : OOB_OFF, 0, SYS);
+              G[0] = unbf4(v[0], v[1]);
+            }
+          } else {
+            G[0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, hv ? ro + ef0 : OOB_OFF, 0, SYS));
+            if (tv1)
+              G[1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, hv ? ro + ef1 : OOB_OFF, 0, SYS));
+          }
           if (w == 7) {
-            D = ld_sys_f32x4(pr + IPC_SMALL + lane * 16);
-            gb = lane < 16 + NCLS ? ld_sys_f32(pr + IPC_SMALL + 1024 + 4 * lane) : 0.f;
+            D = __builtin_bit_cast(
+                f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, dlane ? ro + IPC_SMALL + lane * 16 : OOB_OFF, 0, SYS));
+            gb = __uint_as_float(
+                __builtin_amdgcn_raw_buffer_load_b32(rs, blane ? ro + IPC_SMALL + 1024 + lane * 4 : OOB_OFF, 0, SYS));
           }
         }
       }
@@ -1028,7 +1160,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
 // L2); the first NCOP other blocks copy, the rest exit.  spread (several ranks on
 // one GPU, tests): compute = blocks 0..27, copiers = 28..43.  Placement is speed
 // only: the census above decides each edge's store flavour.
-template <int ACT, bool MULTI, bool SPLIT>
+template <int ACT, int NW, bool SPLIT>
 __global__ __launch_bounds__(THREADS, 1) void mlp_persist_f32(Args a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int b = blockIdx.x;
@@ -1039,7 +1171,7 @@ __global__ __launch_bounds__(THREADS, 1) void mlp_persist_f32(Args a) {
     if ((b & 7) == 0) c = b >> 3; else cid = b - (b >> 3) - 1;
   }
   if (c >= 0) {
-    if (a.nsteps > 0) compute<ACT, MULTI, SPLIT>(a, c / NQ, c % NQ, smem);
+    if (a.nsteps > 0) compute<ACT, NW, SPLIT>(a, c / NQ, c % NQ, smem);
     return;
   }
   if (cid < NCOP) copier(a, cid, smem);
@@ -1096,10 +1228,14 @@ hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int n
   }
   constexpr size_t lds = LDS_BYTES;
   typedef void (*Kern)(Args);
-  static const Kern kerns[8] = {mlp_persist_f32<0, false, false>, mlp_persist_f32<1, false, false>,
-                                mlp_persist_f32<0, true, false>,  mlp_persist_f32<1, true, false>,
-                                mlp_persist_f32<0, false, true>,  mlp_persist_f32<1, false, true>,
-                                mlp_persist_f32<0, true, true>,   mlp_persist_f32<1, true, true>};
+  // NW: peer-table width the exchange is unrolled for (W rounded up to 2 / 4 / 8)
+  static const Kern kerns[16] = {
+      mlp_persist_f32<0, 1, false>, mlp_persist_f32<1, 1, false>, mlp_persist_f32<0, 2, false>,
+      mlp_persist_f32<1, 2, false>, mlp_persist_f32<0, 4, false>, mlp_persist_f32<1, 4, false>,
+      mlp_persist_f32<0, 8, false>, mlp_persist_f32<1, 8, false>, mlp_persist_f32<0, 1, true>,
+      mlp_persist_f32<1, 1, true>,  mlp_persist_f32<0, 2, true>,  mlp_persist_f32<1, 2, true>,
+      mlp_persist_f32<0, 4, true>,  mlp_persist_f32<1, 4, true>,  mlp_persist_f32<0, 8, true>,
+      mlp_persist_f32<1, 8, true>};
   static bool attr_set = false;
   if (!attr_set) {
     for (Kern k : kerns) {
@@ -1109,7 +1245,9 @@ hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int n
     }
     attr_set = true;
   }
-  const int which = (act == 0 ? 0 : 1) + (W > 1 ? 2 : 0) + (split ? 4 : 0);
+  if (W < 1 || W > 8 || rank < 0 || rank >= W) return hipErrorInvalidValue;
+  const int nwi = W <= 1 ? 0 : (W <= 2 ? 1 : (W <= 4 ? 2 : 3));
+  const int which = (act == 0 ? 0 : 1) + 2 * nwi + (split ? 8 : 0);
   const int grid = spread ? GRID_SPREAD : GRID_PACKED;
   hipLaunchKernelGGL(kerns[which], dim3(grid), dim3(THREADS), lds, stream, a);
   return hipGetLastError();

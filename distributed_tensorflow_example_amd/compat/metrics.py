@@ -69,8 +69,13 @@ def streaming_auc(predictions, labels, weights=None, num_thresholds=200, metrics
                     var.value.data += add.to(var.value.device)
             return current()
 
-    val = _Value(None, [], name + "/value")
-    upd = _Update(None, [], name + "/update_op")
+    # the graph edges stay explicit (the GraphDef export and the fused-step
+    # lowering see that the AUC reads the predictions -- hence the weights a
+    # train_op updates -- and the confusion variables); the custom _eval above
+    # decides the values
+    deps = [predictions, labels] + ([] if weights is None else [weights]) + list(cvars)
+    val = _Value(None, list(cvars), name + "/value")
+    upd = _Update(None, deps, name + "/update_op")
     from .graph import get_default_graph
 
     g = get_default_graph()

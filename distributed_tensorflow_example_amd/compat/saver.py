@@ -368,6 +368,22 @@ class Saver:
         missing = []
         for name, v in self._vars().items():
             if name not in idx:
+                old = _old_modulo_parts(idx, name)
+                if old:
+                    # this repo's earlier layout: `name/part_k` = the rows r % P == k
+                    full = _rebuild_modulo(prefix, name, old)
+                    if getattr(v, "is_partitioned", False):
+                        v.table.load_full(full.reshape(v.table.num_rows, v.table.dim))
+                    else:
+                        dst = self._value(v)
+                        if full.numel() != dst.numel():
+                            raise ValueError(f"shape mismatch for {name}: old-layout parts hold {full.numel()} "
+                                             f"values vs {tuple(dst.shape)}")
+                        with torch.no_grad():
+                            dst.data.copy_(full.reshape(dst.shape).to(dst.device, dst.dtype))
+                    if hasattr(v, "initialized"):
+                        v.initialized = True
+                    continue
                 missing.append(name)
                 continue
             if getattr(v, "is_partitioned", False):
@@ -412,3 +428,32 @@ class Saver:
 
     def as_saver_def(self):
         return {"version": 2, "max_to_keep": self.max_to_keep}
+
+
+def _old_modulo_parts(idx, name: str):
+    """Keys `name/part_0 .. name/part_{P-1}` of the pre-TF-slice layout (rows
+    r % P == k in part k, in row order), or [] if absent / incomplete."""
+    keys = [k for k in idx if k.startswith(name + "/part_") and k[len(name) + 6:].isdigit()]
+    if not keys:
+        return []
+    P = len(keys)
+    want = [f"{name}/part_{k}" for k in range(P)]
+    if sorted(keys) != sorted(want):
+        raise KeyError(f"checkpoint has an incomplete old-layout partition set for {name}: {sorted(keys)}")
+    return want
+
+
+def _rebuild_modulo(prefix: str, name: str, keys) -> torch.Tensor:
+    """Full [rows, dim] table from the old modulo parts (row r = part r % P, row r // P)."""
+    parts = [read_tensor(prefix, k).float() for k in keys]
+    P = len(parts)
+    dim = 1 if parts[0].dim() == 1 else int(parts[0].shape[1])
+    parts = [p.reshape(-1, dim) for p in parts]
+    rows = sum(p.shape[0] for p in parts)
+    for k, p in enumerate(parts):
+        if p.shape[0] != (rows - k + P - 1) // P:
+            raise ValueError(f"{name}: old-layout part {k} has {p.shape[0]} rows, expected {(rows - k + P - 1) // P}")
+    full = torch.empty((rows, dim), dtype=torch.float32)
+    for k, p in enumerate(parts):
+        full[k::P] = p
+    return full

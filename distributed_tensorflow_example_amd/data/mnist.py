@@ -1,6 +1,14 @@
-"""Synthetic MNIST-shaped data (no network: the reference downloads MNIST via
-`input_data.read_data_sets`, example.py:59-62; we generate data of the same
-shape/dtype instead).
+"""MNIST input: the real IDX files when they are present, synthetic MNIST-shaped
+data otherwise.
+
+The reference calls `input_data.read_data_sets(path, one_hot=True)`
+(example.py:59-62), which downloads the four IDX files into `path` and splits
+the 60,000 training images into `train` (55,000) and `validation` (the first
+5,000), with `test` = the 10,000 t10k images (example.py:161,165,187 use
+`mnist.train.num_examples`, `mnist.train.next_batch`, `mnist.test.images`).
+There is no network here: `read_data_sets` parses the IDX files if they exist
+in `train_dir` (plain or `.gz`, TF's file names) and falls back to synthetic
+data of the same shape/dtype otherwise, with the same split.
 
 Images are uint8 [N, 784] (the IDX file's native pixel format), labels uint8
 class ids [N].  Each class has a random low-frequency prototype; samples are
@@ -12,6 +20,11 @@ pipeline streams to the GPU with one hipMemcpyAsync per step on a side stream.
 """
 from __future__ import annotations
 
+import gzip
+import os
+import struct
+import sys
+
 import numpy as np
 import torch
 
@@ -19,6 +32,75 @@ IMAGE_PIXELS = 784
 NUM_CLASSES = 10
 TRAIN_EXAMPLES = 55000  # mnist.train.num_examples used by example.py:161
 TEST_EXAMPLES = 10000
+VALIDATION_SIZE = 5000  # TF's read_data_sets default split of the 60k training images
+
+TRAIN_IMAGES = "train-images-idx3-ubyte"
+TRAIN_LABELS = "train-labels-idx1-ubyte"
+TEST_IMAGES = "t10k-images-idx3-ubyte"
+TEST_LABELS = "t10k-labels-idx1-ubyte"
+IDX_IMAGES_MAGIC = 2051   # 0x00000803: ubyte, 3 dims
+IDX_LABELS_MAGIC = 2049   # 0x00000801: ubyte, 1 dim
+
+
+def _open_idx(path: str):
+    return gzip.open(path, "rb") if path.endswith(".gz") else open(path, "rb")
+
+
+def _find_idx(train_dir: str, name: str):
+    """`name` or `name.gz` in train_dir (the plain file wins), else None."""
+    for cand in (name, name + ".gz"):
+        p = os.path.join(train_dir, cand)
+        if os.path.isfile(p):
+            return p
+    return None
+
+
+def read_idx_images(path: str) -> np.ndarray:
+    """IDX3 ubyte images -> uint8 [N, rows*cols] (big-endian header: magic 2051,
+    count, rows, cols; then row-major pixels)."""
+    with _open_idx(path) as f:
+        head = f.read(16)
+        if len(head) != 16:
+            raise ValueError(f"{path}: truncated IDX header")
+        magic, n, rows, cols = struct.unpack(">IIII", head)
+        if magic != IDX_IMAGES_MAGIC:
+            raise ValueError(f"{path}: invalid magic number {magic} in MNIST image file")
+        data = f.read(n * rows * cols)
+    if len(data) != n * rows * cols:
+        raise ValueError(f"{path}: expected {n * rows * cols} pixel bytes, got {len(data)}")
+    return np.frombuffer(data, dtype=np.uint8).reshape(n, rows * cols).copy()
+
+
+def read_idx_labels(path: str) -> np.ndarray:
+    """IDX1 ubyte labels -> uint8 [N] (magic 2049, count, then one byte per label)."""
+    with _open_idx(path) as f:
+        head = f.read(8)
+        if len(head) != 8:
+            raise ValueError(f"{path}: truncated IDX header")
+        magic, n = struct.unpack(">II", head)
+        if magic != IDX_LABELS_MAGIC:
+            raise ValueError(f"{path}: invalid magic number {magic} in MNIST label file")
+        data = f.read(n)
+    if len(data) != n:
+        raise ValueError(f"{path}: expected {n} labels, got {len(data)}")
+    return np.frombuffer(data, dtype=np.uint8).copy()
+
+
+def write_idx_images(path: str, images_u8: np.ndarray, rows: int = 28, cols: int = 28):
+    """Write uint8 [N, rows*cols] as an IDX3 file (gzip if path ends in .gz)."""
+    images_u8 = np.ascontiguousarray(images_u8, dtype=np.uint8)
+    payload = struct.pack(">IIII", IDX_IMAGES_MAGIC, images_u8.shape[0], rows, cols) + images_u8.tobytes()
+    opener = gzip.open if path.endswith(".gz") else open
+    with opener(path, "wb") as f:
+        f.write(payload)
+
+
+def write_idx_labels(path: str, labels_u8: np.ndarray):
+    labels_u8 = np.ascontiguousarray(labels_u8, dtype=np.uint8)
+    payload = struct.pack(">II", IDX_LABELS_MAGIC, labels_u8.shape[0]) + labels_u8.tobytes()
+    opener = gzip.open if path.endswith(".gz") else open
+    with opener(path, "wb") as f:
+        f.write(payload)
 
 
 def _prototypes(seed: int) -> np.ndarray:
@@ -87,18 +169,55 @@ class DataSet:
 
 
 class Datasets:
-    def __init__(self, train: DataSet, test: DataSet):
+    def __init__(self, train: DataSet, test: DataSet, validation: DataSet = None, source: str = "synthetic"):
         self.train = train
+        self.validation = validation
         self.test = test
+        self.source = source   # "idx:<dir>" or "synthetic"
+
+
+def idx_files(train_dir: str):
+    """The four IDX paths in train_dir (plain or .gz), or None if any is missing."""
+    if not train_dir or not os.path.isdir(train_dir):
+        return None
+    paths = [_find_idx(train_dir, n) for n in (TRAIN_IMAGES, TRAIN_LABELS, TEST_IMAGES, TEST_LABELS)]
+    return None if any(p is None for p in paths) else paths
 
 
 def read_data_sets(train_dir: str = "", one_hot: bool = True, seed: int = 0,
-                   train_size: int = TRAIN_EXAMPLES, test_size: int = TEST_EXAMPLES) -> Datasets:
-    """Synthetic drop-in for tensorflow.examples.tutorials.mnist.input_data.read_data_sets."""
-    del train_dir, one_hot
+                   train_size: int = TRAIN_EXAMPLES, test_size: int = TEST_EXAMPLES,
+                   validation_size: int = VALIDATION_SIZE, synthetic_fallback: bool = True) -> Datasets:
+    """Drop-in for tensorflow.examples.tutorials.mnist.input_data.read_data_sets.
+
+    Real data: the IDX files in `train_dir`; the first `validation_size` training
+    images become `validation`, the rest `train` (TF's split), `test` = t10k.
+    `train_size` / `test_size` only size the synthetic fallback, which has the
+    same three splits.  `one_hot` is accepted for signature parity: `labels`
+    are always one-hot float32 (what example.py feeds), `labels_u8` the ids.
+    """
+    del one_hot
+    paths = idx_files(train_dir)
+    if paths is not None:
+        xi, yi = read_idx_images(paths[0]), read_idx_labels(paths[1])
+        xt, yt = read_idx_images(paths[2]), read_idx_labels(paths[3])
+        if len(xi) != len(yi) or len(xt) != len(yt):
+            raise ValueError(f"{train_dir}: image / label counts differ ({len(xi)}/{len(yi)}, {len(xt)}/{len(yt)})")
+        if not 0 <= validation_size <= len(xi):
+            raise ValueError(f"validation size should be between 0 and {len(xi)}; received {validation_size}")
+        return Datasets(DataSet(xi[validation_size:], yi[validation_size:], seed=seed),
+                        DataSet(xt, yt, seed=seed, shuffle=False),
+                        DataSet(xi[:validation_size], yi[:validation_size], seed=seed, shuffle=False),
+                        source=f"idx:{os.path.abspath(train_dir)}")
+    if not synthetic_fallback:
+        raise FileNotFoundError(f"MNIST IDX files not found in {train_dir!r} (no network to download them)")
+    if train_dir:
+        print(f"read_data_sets: no MNIST IDX files in {train_dir!r}; using synthetic MNIST-shaped data",
+              file=sys.stderr, flush=True)
     xi, yi = synthetic_mnist(train_size, seed=seed)
+    xv, yv = synthetic_mnist(validation_size, seed=seed + 104729) if validation_size > 0 else (xi[:0], yi[:0])
     xt, yt = synthetic_mnist(test_size, seed=seed + 7919)
-    return Datasets(DataSet(xi, yi, seed=seed), DataSet(xt, yt, seed=seed, shuffle=False))
+    return Datasets(DataSet(xi, yi, seed=seed), DataSet(xt, yt, seed=seed, shuffle=False),
+                    DataSet(xv, yv, seed=seed, shuffle=False), source="synthetic")
 
 
 def record_bytes(batch_size: int) -> int:

@@ -25,7 +25,8 @@ per step, so buckets must be large enough to stream (>= 16-64 MB) yet small
 enough that the last bucket's all-reduce does not trail the backward pass.
 On CPU (gloo) the same buckets are reduced with async gloo work handles.
 
-`bucket_mb="auto"` (the default; `DTF_BUCKET_MB` overrides) picks the bucket
+`bucket_mb="auto"` (the default; `DTF_BUCKET_MB` replaces "auto" only, never an
+explicit size) picks the bucket
 count from that cost model: k buckets cost k * alpha of fixed ring latency
 (alpha = 2(n-1) hops) and the last bucket, S/k bytes, trails the backward pass,
 so the exposed time k * alpha + S / (k * bw) is smallest at k = sqrt(S / (alpha
@@ -144,7 +145,8 @@ class DistributedDataParallel(torch.nn.Module):
             raise ValueError("module has no trainable parameters")
         self.device = params[0].device
         self.comm_dtype = comm_dtype
-        bucket_mb = os.environ.get("DTF_BUCKET_MB", bucket_mb)
+        if bucket_mb == "auto" and os.environ.get("DTF_BUCKET_MB"):
+            bucket_mb = os.environ["DTF_BUCKET_MB"]   # only the default is overridable: explicit sizes win
         self.comm_cost = None
         if bucket_mb in ("auto", "measure"):
             wire = 2 if comm_dtype in (torch.bfloat16, torch.float16) else 4

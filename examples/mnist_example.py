@@ -49,7 +49,9 @@ flags.DEFINE_integer("batch_size", 100, "per-worker batch")
 flags.DEFINE_float("learning_rate", 0.0005, "SGD learning rate")
 flags.DEFINE_integer("training_epochs", 5, "epochs over the training split")
 flags.DEFINE_integer("max_steps", 0, "stop after this many steps (0 = full epochs)")
-flags.DEFINE_integer("train_size", 55000, "synthetic training examples")
+flags.DEFINE_integer("train_size", 55000, "synthetic training examples (when no IDX files are found)")
+flags.DEFINE_string("data_dir", "", "MNIST IDX directory (train-images-idx3-ubyte[.gz], ...); default "
+                    "MNIST_data/{job}_{task} as example.py:60-62; synthetic data if the files are absent")
 flags.DEFINE_integer("frequency", 100, "print every N batches")
 flags.DEFINE_string("logs_path", "./logs/mnist", "summary root; task dir {job}_{task} appended")
 flags.DEFINE_string("activation", "sigmoid", "sigmoid | relu")
@@ -260,8 +262,10 @@ def main(_argv):
         print(f"ps {FLAGS.task_index} done", flush=True)
         return 0
     print(f"worker {FLAGS.task_index} start ...", flush=True)
-    mnist = mnist_data.read_data_sets(f"MNIST_data/{FLAGS.job_name}_{FLAGS.task_index}", one_hot=True,
-                                      seed=FLAGS.task_index, train_size=FLAGS.train_size)
+    data_dir = FLAGS.data_dir or f"MNIST_data/{FLAGS.job_name}_{FLAGS.task_index}"
+    mnist = mnist_data.read_data_sets(data_dir, one_hot=True, seed=FLAGS.task_index, train_size=FLAGS.train_size)
+    print(f"MNIST source: {mnist.source} (train {mnist.train.num_examples}, validation "
+          f"{mnist.validation.num_examples}, test {mnist.test.num_examples})", flush=True)
     if FLAGS.fused:
         acc, cost, total, params, gstep = run_fused_worker(server, mnist)
     else:

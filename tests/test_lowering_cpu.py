@@ -85,3 +85,21 @@ def test_cpu_session_runs_eagerly():
     if not torch.cuda.is_available():
         assert L.plan_for(g["train"]) is None               # CPU sessions never lower
     tf.reset_default_graph()
+
+
+def test_auc_update_on_the_model_blocks_lowering():
+    """streaming_auc keeps its graph edges (predictions, labels, confusion
+    variables): a run fetching [train_op, auc_update] on the MLP pattern reads
+    the weights the fused step updates, so it must not be lowered (the AUC would
+    see post-update weights)."""
+    import distributed_tensorflow_example_amd.compat as tf
+    from distributed_tensorflow_example_amd.compat import lowering as L
+
+    g = _graph(tf)
+    p = L.match_mlp(g["ce"])
+    plan = L.MLPStepPlan(g["train"], p, tf.get_default_graph())
+    auc_val, auc_upd = tf.contrib.metrics.streaming_auc(g["y"][:, 1], g["y_"][:, 1])
+    assert len(auc_upd.inputs) == 6 and len(auc_val.inputs) == 4      # preds, labels + tp, fn, tn, fp
+    assert not plan.fetches_ok([g["train"], auc_upd])
+    assert plan.fetches_ok([g["train"], g["ce"]])
+    tf.reset_default_graph()

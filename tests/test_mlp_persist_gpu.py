@@ -223,7 +223,24 @@ def test_persist_four_ranks_same_gpu(native, exchange):
     _persist_selftest(4, "fp32", "bf16", exchange)
 
 
-def _persist_selftest(nproc, precision, grad, exchange):
+@pytest.mark.parametrize("grad,exchange", [("bf16", "one-shot"), ("bf16", "two-shot"), ("fp32", "one-shot"),
+                                           ("fp32", "two-shot")])
+def test_persist_eight_ranks_same_gpu(native, grad, exchange):
+    """W = 8 (the driver's whole-node N): the 8-wide peer table, 7 peers per
+    workgroup and the two-shot chunking with one wave chunk per owner, with 8
+    ranks sharing cuda:0.  Pre-staged input (no in-launch copiers), so the 8 x 28
+    compute workgroups (224 of 256 CUs) can be co-resident."""
+    _persist_selftest(8, "fp32", grad, exchange, prestaged=True, timeout=200)
+
+
+@pytest.mark.parametrize("nproc", [5, 6])
+def test_persist_five_six_ranks_same_gpu(native, nproc):
+    """W between the unrolled peer-table widths (5, 6 -> the 8-wide table with
+    absent entries) and two-shot chunks owned unevenly (w % W)."""
+    _persist_selftest(nproc, "fp32", "bf16", "two-shot", prestaged=True, timeout=200)
+
+
+def _persist_selftest(nproc, precision, grad, exchange, prestaged=False, timeout=100):
     """N ranks sharing cuda:0: in-kernel IPC exchange, bit-identical replicas, sync-SGD math."""
     import json
     import os
@@ -239,9 +256,9 @@ def _persist_selftest(nproc, precision, grad, exchange):
     cmd = [sys.executable, "-m", "torch.distributed.run", f"--nproc-per-node={nproc}", "--master-addr=127.0.0.1",
            f"--master-port={port}", os.path.join(repo, "scripts", "persist_selftest.py"), "--same-gpu",
            "--steps=10", "--per-launch=4", f"--precision={precision}", f"--grad-dtype={grad}",
-           f"--exchange={exchange}"]
-    env = dict(os.environ, PYTHONPATH=repo, OMP_NUM_THREADS="2")
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=100, env=env)
+           f"--exchange={exchange}"] + (["--prestaged"] if prestaged else [])
+    env = dict(os.environ, PYTHONPATH=repo, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env)
     out = r.stdout + r.stderr
     line = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert r.returncode == 0 and line, out[-3000:]

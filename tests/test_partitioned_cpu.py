@@ -121,3 +121,39 @@ def test_partitioned_variable_sync_workers(tmp_path):
         assert np.allclose(g["W"].numpy(), two[0][1])
         assert float(sess.run(g["gs"])) == 6.0
     tf.reset_default_graph()
+
+
+def test_restore_reads_the_old_modulo_part_layout(tmp_path):
+    """Checkpoints of this repo's earlier layout (`W/part_k` = rows r % P == k)
+    still restore: the table is rebuilt the modulo way."""
+    import torch
+
+    sys.path.insert(0, REPO)
+    import distributed_tensorflow_example_amd.compat as tf
+    from distributed_tensorflow_example_amd.compat.saver import write_bundle
+
+    tf.reset_default_graph()
+    g = _graph(tf)
+    full = torch.arange(F, dtype=torch.float32).reshape(F, 1) * 0.5
+    prefix = str(tmp_path / "old.ckpt")
+    P = 3
+    write_bundle(prefix, {**{f"weights/Variable/part_{k}": full[k::P].clone() for k in range(P)},
+                          "bias/Variable": torch.tensor([2.5]), "global_step": torch.tensor(7.0)})
+    saver = tf.train.Saver()
+    with tf.Session() as sess:
+        sess.run(tf.global_variables_initializer())
+        saver.restore(sess, prefix)
+        w = sess.run(g["W"])
+        assert np.array_equal(np.asarray(w).reshape(-1), full.numpy().reshape(-1))
+        assert float(np.asarray(sess.run(g["b"])).reshape(-1)[0]) == 2.5
+    # an incomplete old set is a clear error, not "variables not found"
+    write_bundle(prefix, {"weights/Variable/part_0": full[0::3].clone(), "weights/Variable/part_2": full[2::3].clone(),
+                          "bias/Variable": torch.tensor([2.5]), "global_step": torch.tensor(7.0)})
+    with tf.Session() as sess:
+        sess.run(tf.global_variables_initializer())
+        try:
+            saver.restore(sess, prefix)
+            raise AssertionError("restore of an incomplete part set must fail")
+        except KeyError as e:
+            assert "incomplete old-layout" in str(e)
+    tf.reset_default_graph()

@@ -2,9 +2,11 @@
 // and the pinned-host -> device batch copy used by the input pipeline.
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
+#include <pybind11/numpy.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstring>
 #include <stdexcept>
 #include <string>
 
@@ -50,11 +52,11 @@ hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int n
                                 const void* host_next, int next_steps, void* stage_next, void* const* peer_base, int W,
                                 int rank, int gbf16, long long* phase_ts, int spread, int xmode, int split,
                                 hipStream_t stream);
-long long dtfk_graph_mlp_lds(int B, int HP);
+long long dtfk_graph_mlp_part_floats(int B, int H);
 hipError_t dtfk_graph_mlp_step(const float* x, const float* ylab, float* W1, float* b1, float* W2, float* b2,
-                               float* a2buf, float* dz2buf, float* gW1, float* gb1, float* gW2, float* gb2,
-                               float* metrics, void* gstep, int gstep_kind, float lr, int B, int K, int H, int C,
-                               int act, int naive, int sgd, hipStream_t stream);
+                               float* a2buf, float* dz2buf, float* part, float* gW1, float* gb1, float* gW2,
+                               float* gb2, float* metrics, void* gstep, int gstep_kind, const float* lr_ptr, int B,
+                               int K, int H, int C, int act, int naive, int sgd, hipStream_t stream);
 long long dtfk_mlpx_stage_rec();
 long long dtfk_mlpx_xbuf_bytes();
 long long dtfk_mlpx_ipc_bytes();
@@ -511,6 +513,18 @@ struct PersistF32Plan {
   }
 };
 
+static int gstep_kind_of(const at::Tensor& g) {
+  TORCH_CHECK(g.is_cuda() && g.numel() == 1, "graph_mlp_step: device scalar global_step");
+  switch (g.scalar_type()) {
+    case at::kFloat: return 0;
+    case at::kLong: return 1;
+    case at::kInt: return 2;
+    case at::kDouble: return 3;
+    default: TORCH_CHECK(false, "graph_mlp_step: unsupported global_step dtype");
+  }
+  return 0;
+}
+
 // The compat graph's matched MLP training step (csrc/kernels/graph_mlp.hip).
 // sgd: W/b updated in place with lr; else gradients into g* (same shapes).
 void graph_mlp_step(at::Tensor x, at::Tensor ylab, at::Tensor W1, at::Tensor b1, at::Tensor W2, at::Tensor b2,
@@ -544,25 +558,155 @@ void graph_mlp_step(at::Tensor x, at::Tensor ylab, at::Tensor W1, at::Tensor b1,
   void* gp = nullptr;
   int kind = 0;
   if (gstep.has_value()) {
-    TORCH_CHECK(gstep->is_cuda() && gstep->numel() == 1, "graph_mlp_step: device scalar global_step");
+    kind = gstep_kind_of(*gstep);
     gp = gstep->data_ptr();
-    switch (gstep->scalar_type()) {
-      case at::kFloat: kind = 0; break;
-      case at::kLong: kind = 1; break;
-      case at::kInt: kind = 2; break;
-      case at::kDouble: kind = 3; break;
-      default: TORCH_CHECK(false, "graph_mlp_step: unsupported global_step dtype");
-    }
   }
+  // L2's partials + the learning rate on the device (scratch from the caching allocator)
+  at::Tensor part = at::empty({dtfk_graph_mlp_part_floats(B, H) + 1}, x.options());
+  part.narrow(0, 0, 1).fill_(lr);
   hip_check(dtfk_graph_mlp_step(x.data_ptr<float>(), ylab.data_ptr<float>(), W1.data_ptr<float>(),
                                 b1.data_ptr<float>(), W2.data_ptr<float>(), b2.data_ptr<float>(),
-                                a2buf.data_ptr<float>(), dz2buf.data_ptr<float>(), gW1, gb1, gW2, gb2,
-                                metrics.data_ptr<float>(), gp, kind, (float)lr, B, K, H, C, act, naive ? 1 : 0,
-                                sgd ? 1 : 0, cur_stream()),
+                                a2buf.data_ptr<float>(), dz2buf.data_ptr<float>(), part.data_ptr<float>() + 1, gW1,
+                                gb1, gW2, gb2, metrics.data_ptr<float>(), gp, kind, part.data_ptr<float>(), B, K, H, C,
+                                act, naive ? 1 : 0, sgd ? 1 : 0, cur_stream()),
             "graph_mlp_step");
 }
 
+// The lowered Session.run of the reference's training graph as ONE host call
+// (compat/lowering.py, in-kernel SGD): the numpy feeds x [B,K] / y_ [B,C] and the
+// learning rate go into a pinned staging slot (one memcpy, GIL released), ONE
+// host-to-device copy, then L1 / L2 / L3 and the loss / accuracy / global_step
+// device-to-host copy replayed from a captured hipGraph; with `sync` the call
+// returns after the step (the reference fetches the loss every step).
+class GraphStepPlan {
+ public:
+  GraphStepPlan(at::Tensor W1, at::Tensor b1, at::Tensor W2, at::Tensor b2, c10::optional<at::Tensor> gstep, int B,
+                int act, bool naive)
+      : W1_(W1), b1_(b1), W2_(W2), b2_(b2), B_(B), act_(act), naive_(naive) {
+    for (const at::Tensor* t : {&W1, &b1, &W2, &b2})
+      TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous(),
+                  "GraphStepPlan: fp32 contiguous device parameters expected");
+    K_ = (int)W1.size(0);
+    H_ = (int)W1.size(1);
+    C_ = (int)W2.size(1);
+    TORCH_CHECK(W2.size(0) == H_ && b1.numel() == H_ && b2.numel() == C_, "GraphStepPlan: shape mismatch");
+    HP_ = (H_ + 16) & ~15;
+    const int BP = (B_ + 15) & ~15;
+    if (gstep.has_value()) {
+      gkind_ = gstep_kind_of(*gstep);
+      gstep_ = *gstep;
+    }
+    nfeed_ = (int64_t)B_ * K_ + (int64_t)B_ * C_ + 4;   // x | y | lr (+ pad)
+    auto fo = W1.options();
+    dev_ = at::empty({nfeed_}, fo);
+    a2_ = at::empty({(int64_t)BP * HP_}, fo);
+    dz2_ = at::empty({(int64_t)BP * HP_}, fo);
+    part_ = at::empty({dtfk_graph_mlp_part_floats(B_, H_)}, fo);
+    metrics_ = at::zeros({4}, fo);
+    auto ho = at::TensorOptions().dtype(at::kFloat).pinned_memory(true);
+    for (int i = 0; i < 2; ++i) stage_[i] = at::empty({nfeed_}, ho);
+    host_metrics_ = at::zeros({4}, ho);
+    for (int i = 0; i < 2; ++i) hip_check(hipEventCreateWithFlags(&ev_[i], hipEventDisableTiming), "hipEventCreate");
+    hip_check(hipEventCreateWithFlags(&in_ev_, hipEventDisableTiming), "hipEventCreate");
+    hip_check(hipEventCreateWithFlags(&out_ev_, hipEventDisableTiming), "hipEventCreate");
+    // its own stream: graph capture needs one that is not the legacy default stream
+    hip_check(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking), "hipStreamCreate");
+  }
+  ~GraphStepPlan() {
+    if (exec_) (void)hipGraphExecDestroy(exec_);
+    if (graph_) (void)hipGraphDestroy(graph_);
+    for (auto& e : ev_)
+      if (e) (void)hipEventDestroy(e);
+    if (in_ev_) (void)hipEventDestroy(in_ev_);
+    if (out_ev_) (void)hipEventDestroy(out_ev_);
+    if (st_) (void)hipStreamDestroy(st_);
+  }
+
+  at::Tensor host_metrics() const { return host_metrics_; }
+
+  // One training step.  x, y: C-contiguous float32 numpy arrays of the plan's
+  // shapes.  Returns after the step when `sync` (host_metrics() then holds
+  // loss, accuracy, global_step after the step).
+  void run(py::array x, py::array y, double lr, bool sync) {
+    const int64_t nx = (int64_t)B_ * K_, ny = (int64_t)B_ * C_;
+    TORCH_CHECK(x.dtype().is(py::dtype::of<float>()) && y.dtype().is(py::dtype::of<float>()),
+                "GraphStepPlan.run: float32 feeds expected");
+    TORCH_CHECK((x.flags() & py::array::c_style) && (y.flags() & py::array::c_style),
+                "GraphStepPlan.run: C-contiguous feeds expected");
+    TORCH_CHECK(x.size() == nx && y.size() == ny, "GraphStepPlan.run: feed shapes differ from the plan's");
+    const float* xp = static_cast<const float*>(x.data());
+    const float* yp = static_cast<const float*>(y.data());
+    hipStream_t cur = cur_stream(), st = st_;
+    const int slot = slot_ ^= 1;
+    {
+      py::gil_scoped_release nogil;
+      hip_check(hipEventSynchronize(ev_[slot]), "GraphStepPlan: staging slot");   // its last copy is done
+      float* h = stage_[slot].data_ptr<float>();
+      std::memcpy(h, xp, sizeof(float) * nx);
+      std::memcpy(h + nx, yp, sizeof(float) * ny);
+      h[nx + ny] = (float)lr;
+      // after whatever the caller's stream queued (variable init, eager updates)
+      hip_check(hipEventRecord(in_ev_, cur), "GraphStepPlan: event");
+      hip_check(hipStreamWaitEvent(st, in_ev_, 0), "GraphStepPlan: wait");
+      hip_check(hipMemcpyAsync(dev_.data_ptr<float>(), h, sizeof(float) * (nx + ny + 1), hipMemcpyHostToDevice, st),
+                "GraphStepPlan: feed copy");
+      hip_check(hipEventRecord(ev_[slot], st), "GraphStepPlan: event");
+      if (exec_ == nullptr) capture(st);
+      hip_check(hipGraphLaunch(exec_, st), "GraphStepPlan: graph launch");
+      if (sync) {
+        hip_check(hipStreamSynchronize(st), "GraphStepPlan: sync");
+      } else {   // later work on the caller's stream sees the updated variables
+        hip_check(hipEventRecord(out_ev_, st), "GraphStepPlan: event");
+        hip_check(hipStreamWaitEvent(cur, out_ev_, 0), "GraphStepPlan: wait");
+      }
+    }
+    ++steps_;
+  }
+  int64_t steps() const { return steps_; }
+
+ private:
+  void capture(hipStream_t st) {
+    if (exec_) { (void)hipGraphExecDestroy(exec_); exec_ = nullptr; }
+    if (graph_) { (void)hipGraphDestroy(graph_); graph_ = nullptr; }
+    const int64_t nx = (int64_t)B_ * K_, ny = (int64_t)B_ * C_;
+    float* d = dev_.data_ptr<float>();
+    hip_check(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal), "GraphStepPlan: begin capture");
+    hipError_t e = dtfk_graph_mlp_step(d, d + nx, W1_.data_ptr<float>(), b1_.data_ptr<float>(), W2_.data_ptr<float>(),
+                                       b2_.data_ptr<float>(), a2_.data_ptr<float>(), dz2_.data_ptr<float>(),
+                                       part_.data_ptr<float>(), nullptr, nullptr, nullptr, nullptr,
+                                       metrics_.data_ptr<float>(), gstep_.defined() ? gstep_.data_ptr() : nullptr,
+                                       gkind_, d + nx + ny, B_, K_, H_, C_, act_, naive_ ? 1 : 0, 1, st);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(host_metrics_.data_ptr<float>(), metrics_.data_ptr<float>(), 3 * sizeof(float),
+                         hipMemcpyDeviceToHost, st);
+    hipGraph_t g = nullptr;
+    const hipError_t e2 = hipStreamEndCapture(st, &g);
+    hip_check(e, "GraphStepPlan: captured launches");
+    hip_check(e2, "GraphStepPlan: end capture");
+    graph_ = g;
+    hip_check(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0), "GraphStepPlan: instantiate");
+  }
+
+  at::Tensor W1_, b1_, W2_, b2_, gstep_, dev_, a2_, dz2_, part_, metrics_, host_metrics_;
+  at::Tensor stage_[2];
+  hipEvent_t ev_[2] = {nullptr, nullptr};
+  hipEvent_t in_ev_ = nullptr, out_ev_ = nullptr;
+  hipGraph_t graph_ = nullptr;
+  hipGraphExec_t exec_ = nullptr;
+  hipStream_t st_ = nullptr;
+  int B_, K_ = 0, H_ = 0, C_ = 0, HP_ = 0, act_, gkind_ = 0, slot_ = 0;
+  bool naive_;
+  int64_t nfeed_ = 0, steps_ = 0;
+};
+
 void init_mlp(py::module& m) {
+  py::class_<GraphStepPlan>(m, "GraphStepPlan")
+      .def(py::init<at::Tensor, at::Tensor, at::Tensor, at::Tensor, c10::optional<at::Tensor>, int, int, bool>(),
+           py::arg("W1"), py::arg("b1"), py::arg("W2"), py::arg("b2"), py::arg("gstep"), py::arg("B"), py::arg("act"),
+           py::arg("naive"))
+      .def("run", &GraphStepPlan::run, py::arg("x"), py::arg("y"), py::arg("lr"), py::arg("sync"))
+      .def("host_metrics", &GraphStepPlan::host_metrics)
+      .def("steps", &GraphStepPlan::steps);
   m.def("graph_mlp_step", &graph_mlp_step, py::arg("x"), py::arg("ylab"), py::arg("W1"), py::arg("b1"),
         py::arg("W2"), py::arg("b2"), py::arg("a2buf"), py::arg("dz2buf"), py::arg("grads"), py::arg("metrics"),
         py::arg("gstep"), py::arg("lr"), py::arg("act"), py::arg("naive"), py::arg("sgd"));

@@ -58,7 +58,7 @@ hipError_t dtfk_auc_hist(const float* pred, const float* label, int64_t n, int n
 hipError_t dtfk_multi_tensor_apply(const void* tab, const void* chunks, int nchunks, int kind, int gbf,
                                    const float* lr_ptr, float lr, float gscale, float wd, float b1, float b2,
                                    float eps, float momentum, int nesterov, const long long* step,
-                                   hipStream_t s);
+                                   const int* skip, hipStream_t s);
 hipError_t dtfk_multi_tensor_sumsq(const void* tab, const void* chunks, int nchunks, int gbf, float* out,
                                    hipStream_t s);
 int dtfk_mt_chunk();
@@ -293,17 +293,20 @@ void auc_hist(at::Tensor pred, at::Tensor label, at::Tensor pos, at::Tensor neg)
 
 void multi_tensor_apply(at::Tensor tab, at::Tensor chunks, int kind, bool grad_bf16,
                         c10::optional<at::Tensor> lr_t, double lr, double gscale, double wd, double b1,
-                        double b2, double eps, double momentum, bool nesterov, c10::optional<at::Tensor> step) {
+                        double b2, double eps, double momentum, bool nesterov, c10::optional<at::Tensor> step,
+                        c10::optional<at::Tensor> skip) {
   gpu(tab, "table"); gpu(chunks, "chunks");
   if (tab.dim() != 2 || tab.size(1) * 8 != dtfk_tensor_rec_bytes())
     throw std::runtime_error("multi_tensor_apply: table rows must be TensorRec {p, g, m, v, n, shadow}");
   if (lr_t.has_value()) f32c(*lr_t, "lr");
   if (step.has_value()) i64c(*step, "step");
+  if (skip.has_value() && (!skip->is_cuda() || skip->scalar_type() != at::kInt))
+    throw std::runtime_error("multi_tensor_apply: skip must be a device int32 flag");
   ck(dtfk_multi_tensor_apply(tab.data_ptr(), chunks.data_ptr(), (int)chunks.size(0), kind, grad_bf16 ? 1 : 0,
                              opt_ptr<float>(lr_t), (float)lr, (float)gscale, (float)wd, (float)b1, (float)b2,
                              (float)eps, (float)momentum, nesterov ? 1 : 0,
                              step.has_value() ? reinterpret_cast<const long long*>(step->data_ptr<int64_t>()) : nullptr,
-                             cs()),
+                             skip.has_value() ? skip->data_ptr<int>() : nullptr, cs()),
      "multi_tensor_apply");
 }
 
@@ -330,7 +333,7 @@ std::vector<at::Tensor> sparse_route(at::Tensor sids, at::Tensor perm, int W, in
     throw std::runtime_error("sparse_route: sorted ids must be contiguous int32/int64");
   if (W < 1 || W > dtfk_route_max_world()) throw std::runtime_error("sparse_route: world size out of range");
   const int64_t N = sids.numel();
-  if (W > 1 && cap < N) throw std::runtime_error("sparse_route: capacity below the batch's id count");
+  if (W > 1 && cap < 1) throw std::runtime_error("sparse_route: per-peer capacity must be >= 1");
   if (std::max(N, cap) * std::max(W, 1) >= (1LL << 31)) throw std::runtime_error("sparse_route: batch too large");
   auto o32 = sids.options().dtype(at::kInt), o64 = sids.options().dtype(at::kLong);
   at::Tensor inv = at::empty({N}, o32), inverse = at::empty({N}, o64), uniq = at::empty({N}, o64);
@@ -349,7 +352,10 @@ std::vector<at::Tensor> sparse_route(at::Tensor sids, at::Tensor perm, int W, in
                         inverse.data_ptr<int64_t>(), uniq.data_ptr<int64_t>(), W > 1 ? dest.data_ptr<int>() : nullptr,
                         W > 1 ? send.data_ptr<int64_t>() : nullptr, count.data_ptr<int>(), cs()),
      "route_scatter");
-  return {inv, inverse, uniq, dest, send, count};
+  // unique ids per owner (the last row of the per-owner inclusive scan): the
+  // caller's overflow test (> cap) and capacity adaptation, no host read-back
+  at::Tensor ocnt = W > 1 ? owncum.select(0, N - 1).contiguous() : count;
+  return {inv, inverse, uniq, dest, send, count, ocnt};
 }
 
 // DDP bucket <-> bf16 comm buffer with the 1/N scale folded in (csrc/kernels/ops.hip K16).
@@ -430,7 +436,10 @@ void init_ops(py::module& m) {
   m.def("embedding_bag_bwd_sorted", &embedding_bag_bwd_sorted);
   m.def("argmax_correct", &argmax_correct);
   m.def("auc_hist", &auc_hist);
-  m.def("multi_tensor_apply", &multi_tensor_apply);
+  m.def("multi_tensor_apply", &multi_tensor_apply, py::arg("tab"), py::arg("chunks"), py::arg("kind"),
+        py::arg("grad_bf16"), py::arg("lr_t"), py::arg("lr"), py::arg("gscale"), py::arg("wd"), py::arg("b1"),
+        py::arg("b2"), py::arg("eps"), py::arg("momentum"), py::arg("nesterov"), py::arg("step"),
+        py::arg("skip") = py::none());
   m.def("multi_tensor_sumsq", &multi_tensor_sumsq);
   m.def("mt_chunk", &dtfk_mt_chunk);
   m.def("tensor_rec_bytes", &dtfk_tensor_rec_bytes);

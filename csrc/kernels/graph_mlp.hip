@@ -128,101 +128,70 @@ __global__ __launch_bounds__(512) void graph_mlp_l1(const float* __restrict__ x,
 }
 
 // ---------------------------------------------------------------- L2
+// One workgroup (4 waves) per 16-row tile of the batch: z3 = a2 W2 + b2 (split-K
+// over the 4 waves), softmax / loss / accuracy / dz3 (wave 0, 16-lane
+// reductions), then per hidden tile (spread over the waves) da2 = dz3 W2^T ->
+// dz2 = da2 act'(a2) and this row tile's dW2 partial a2^T dz3 (row H of it is
+// db2: a2's ones column).  The partials and the loss / accuracy sums go to a
+// global scratch; L3's finalize workgroups reduce them in fixed row-tile order
+// (deterministic) and update W2 / b2.  It replaces ONE 512-thread workgroup that
+// walked the whole batch serially (~18 us; profiles/mnist_graph_lowered_*).
 struct HeadArgs {
   const float* a2;      // [BP][HP] from L1
   const float* ylab;    // [B][C]
-  float* W2;            // [H][C]
-  float* b1;            // [H]
-  float* b2;            // [C]
+  const float* W2;      // [H][C] (read only here: L3 updates it)
+  const float* b2;      // [C]
   float* dz2;           // [BP][HP] out
-  float* gW2;           // gradient outputs (mode GRAD) or nullptr
-  float* gb1;
-  float* gb2;
-  float* metrics;       // [0] loss, [1] accuracy, [2] global_step after the step
-  void* gstep;          // global_step storage or nullptr
-  int gstep_kind;       // 0 f32, 1 i64, 2 i32, 3 f64
-  float lr;
-  int B, H, HP, C, act, naive, sgd;
+  float* part;          // [NRT][HP][CP] dW2 partials (row H = db2), then [NRT][2] loss / correct
+  int B, H, HP, C, act, naive;
 };
 
-__global__ __launch_bounds__(512) void graph_mlp_head(HeadArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
+constexpr int HW = 4;   // waves per head workgroup
+
+__global__ __launch_bounds__(HW * 64) void graph_mlp_head(HeadArgs a) {
+  __shared__ float a2s[16 * MAXH + 16];       // this tile's a2 rows [16][HP]
+  __shared__ float w2s[(MAXH + 16) * CP];     // W2 [HP][CP], zero padded
+  __shared__ float dz3s[16 * CP];             // dz3 / B of the tile [16][CP]
+  __shared__ f32x4 zp[HW][64];                // split-K partials of z3
   const int B = a.B, H = a.H, HP = a.HP, C = a.C;
-  const int BP = (B + 15) & ~15;
-  float* a2s = sm;                       // [BP][HP] -> later dz2
-  float* w2s = a2s + BP * HP;            // [HP][CP]
-  float* dz3s = w2s + HP * CP;           // [BP][CP]
-  float* labs = dz3s + BP * CP;          // [BP][CP] labels
-  float* red = labs + BP * CP;           // [64] reductions
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
+  const int NRT = (B + 15) / 16;
+  const int rt = blockIdx.x, rb = rt * 16;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
-
-  {
-    // every global operand in one round trip: a2 (<= 16384 floats, as
-    // float4s), W2 (<= 2048), labels (<= 4096), b2 -- clamped, masked, no branches
-    const int n4 = BP * HP / 4, nw2 = HP * CP, nl = BP * CP;
-    const float4* src = reinterpret_cast<const float4*>(a.a2);
-    float4 v[8];
-    float wv[4], lv[8];
-    // indices are clamped and stores unconditional (a clamped lane rewrites
-    // the last element with the same value): no branch the compiler could
-    // sink a load into
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = src[min(tid + j * 512, n4 - 1)];
-    float wt[4], lt[8];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int i = min(tid + j * 512, nw2 - 1), h = i / CP, c = i % CP;
-      wt[j] = a.W2[min(h, H - 1) * C + min(c, C - 1)];
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int i = min(tid + j * 512, nl - 1), m = i / CP, c = i % CP;
-      lt[j] = a.ylab[(size_t)min(m, B - 1) * C + min(c, C - 1)];
-    }
-    // all loads are in flight; only now mask (pin keeps each load unconditional)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int i = min(tid + j * 512, nw2 - 1), h = i / CP, c = i % CP;
-      const float t = pin(wt[j]);
-      wv[j] = (h < H && c < C) ? t : 0.f;
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int i = min(tid + j * 512, nl - 1), m = i / CP, c = i % CP;
-      const float t = pin(lt[j]);
-      lv[j] = (m < B && c < C) ? t : 0.f;
-    }
-    float4* dst = reinterpret_cast<float4*>(a2s);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) dst[min(tid + j * 512, n4 - 1)] = v[j];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) w2s[min(tid + j * 512, nw2 - 1)] = wv[j];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) labs[min(tid + j * 512, nl - 1)] = lv[j];
+  // operands, branch-free (clamped + masked): a2 tile, W2, this lane's label / b2
+  for (int i = tid; i < 16 * HP / 4; i += HW * 64)
+    reinterpret_cast<float4*>(a2s)[i] = reinterpret_cast<const float4*>(a.a2 + (size_t)rb * HP)[i];
+  for (int i = tid; i < HP * CP; i += HW * 64) {
+    const int h = i / CP, c = i % CP;
+    const float v = a.W2[min(h, H - 1) * C + min(c, C - 1)];
+    w2s[i] = (h < H && c < C) ? v : 0.f;
   }
-  if (tid < 2) red[tid] = 0.f;
   __syncthreads();
-
-  // z3 = a2 W2 + b2 -> softmax, loss, accuracy, dz3 (one 16-row tile per wave pass)
-  float loss_part = 0.f, corr_part = 0.f;
-  const float b2v = r < C ? a.b2[r] : 0.f;
-  for (int rt = w; rt < BP / 16; rt += nw) {
-    const int rb = rt * 16;
+  // z3 tile, K = HP split over the waves
+  {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int k = 0; k < HP; k += 4)
-      acc = mfma4(a2s[(rb + r) * HP + k + g], w2s[(k + g) * CP + r], acc);
+    for (int k = 4 * w; k < HP; k += 4 * HW) acc = mfma4(a2s[r * HP + k + g], w2s[(k + g) * CP + r], acc);
+    zp[w][lane] = acc;
+  }
+  __syncthreads();
+  if (w == 0) {
+    f32x4 acc = zp[0][lane];
+#pragma unroll
+    for (int q = 1; q < HW; ++q) acc += zp[q][lane];
+    const float b2v = r < C ? a.b2[min(r, C - 1)] : 0.f;
+    float loss_part = 0.f, corr_part = 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = rb + 4 * g + i;               // row; column = r (class)
       const bool valid = m < B;
       const bool cl = r < C;
+      const float labv = a.ylab[(size_t)min(m, B - 1) * C + min(r, C - 1)];
+      const float lab = (valid && cl) ? labv : 0.f;
       const float z = cl ? acc[i] + b2v : -INFINITY;
       const float mx = row16_max(z);
       const float e = cl ? expf(z - mx) : 0.f;
       const float s = row16_sum(e);
       const float y = e / s;
-      const float lab = labs[m * CP + r];
       const float lsum = row16_sum(lab);
       // loss term: naive -y_ log(softmax) exactly as the graph computes it
       // (0 * log(0) = NaN like TF); stable -y_ (z - max - log sum exp)
@@ -238,57 +207,91 @@ __global__ __launch_bounds__(512) void graph_mlp_head(HeadArgs a) {
         corr_part += pi == li ? 1.f : 0.f;
       }
       const float d = a.naive ? (y * lsum - lab) : (y - lab);
-      dz3s[m * CP + r] = (valid && cl) ? d / (float)B : 0.f;
+      dz3s[(4 * g + i) * CP + r] = (valid && cl) ? d / (float)B : 0.f;
+    }
+    // (lanes with r == 0 hold the partial sums of their 4 rows)
+    loss_part += __shfl_xor(loss_part, 16, 64);
+    loss_part += __shfl_xor(loss_part, 32, 64);
+    corr_part += __shfl_xor(corr_part, 16, 64);
+    corr_part += __shfl_xor(corr_part, 32, 64);
+    if (lane == 0) {
+      float* lc = a.part + (size_t)NRT * HP * CP;
+      lc[2 * rt] = loss_part;
+      lc[2 * rt + 1] = corr_part;
     }
   }
-  loss_part = wave_sum(loss_part);
-  corr_part = wave_sum(corr_part);
-  if (lane == 0) {
-    atomicAdd(&red[0], loss_part);      // LDS atomics: 8 waves
-    atomicAdd(&red[1], corr_part);
-  }
   __syncthreads();
-
-  // dW2 = a2^T dz3 ([HP x CP] over BP); row H of the product is db2 (a2's ones column)
-  for (int ht = w; ht < HP / 16; ht += nw) {
+  // per hidden tile: da2 = dz3 W2^T -> dz2 rows; dW2 partial = a2^T dz3
+  const int nht = HP / 16;
+  for (int ht = w; ht < nht; ht += HW) {
     const int hb = ht * 16;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int k = 0; k < BP; k += 4) acc = mfma4(a2s[(k + g) * HP + hb + r], dz3s[(k + g) * CP + r], acc);
+    f32x4 da = {0.f, 0.f, 0.f, 0.f}, dw = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < CP; k += 4) da = mfma4(dz3s[r * CP + k + g], w2s[(hb + r) * CP + k + g], da);
+#pragma unroll
+    for (int k = 0; k < 16; k += 4) dw = mfma4(a2s[(k + g) * HP + hb + r], dz3s[(k + g) * CP + r], dw);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int h = hb + 4 * g + i;
-      if (r < C) {
-        if (h < H) {
-          if (a.sgd) a.W2[h * C + r] = w2s[h * CP + r] - a.lr * acc[i];
-          else a.gW2[h * C + r] = acc[i];
-        } else if (h == H) {
-          if (a.sgd) a.b2[r] = a.b2[r] - a.lr * acc[i];
-          else a.gb2[r] = acc[i];
-        }
+      const int m = 4 * g + i, h = hb + r;         // da: row m, column h
+      const float av = a2s[m * HP + h];
+      a.dz2[(size_t)(rb + m) * HP + h] = (rb + m < B && h < H) ? da[i] * act_bwd(av, a.act) : 0.f;
+      // dw: row hb + 4g + i (hidden), column r (class)
+      a.part[((size_t)rt * HP + hb + 4 * g + i) * CP + r] = dw[i];
+    }
+  }
+}
+
+// ---------------------------------------------------------------- L3
+// One workgroup per 16x16 tile of [dW1; db1] ((K+1) x H: row K is db1, from a
+// virtual x column of ones); its 4 waves split the batch and prefetch all of
+// their operands (<= 16 batch blocks each) before the MFMAs.
+constexpr int L3PF = 16;
+struct WgradArgs {
+  const float* x;
+  const float* dz2;
+  float* W1;
+  float* b1;
+  float* W2;
+  float* b2;
+  float* gW1;           // gradient outputs (sgd == 0)
+  float* gb1;
+  float* gW2;
+  float* gb2;
+  const float* hpart;   // L2's dW2 partials + loss / correct sums
+  float* metrics;       // [0] loss, [1] accuracy, [2] global_step after the step
+  void* gstep;          // global_step storage or nullptr
+  int gstep_kind;       // 0 f32, 1 i64, 2 i32, 3 f64
+  const float* lr_ptr;  // device learning rate (a captured step reads the current one)
+  int B, K, H, HP, C, sgd, tiles;
+};
+
+// Workgroups >= tiles: one per hidden tile of W2 / b2 -- the sum of L2's row-tile
+// partials in fixed order, the update (or gradients out); the first of them also
+// finalizes loss / accuracy and bumps global_step.
+__device__ void graph_mlp_w2_final(const WgradArgs& a, int ht) {
+  const int tid = threadIdx.x;
+  const int HP = a.HP, H = a.H, C = a.C, NRT = (a.B + 15) / 16;
+  const float lr = *a.lr_ptr;
+  for (int e = tid; e < 16 * CP; e += blockDim.x) {
+    const int h = ht * 16 + e / CP, c = e % CP;
+    float s = 0.f;
+    for (int rt = 0; rt < NRT; ++rt) s += a.hpart[((size_t)rt * HP + h) * CP + c];
+    if (c < C) {
+      if (h < H) {
+        if (a.sgd) a.W2[h * C + c] -= lr * s;
+        else a.gW2[h * C + c] = s;
+      } else if (h == H) {
+        if (a.sgd) a.b2[c] -= lr * s;
+        else a.gb2[c] = s;
       }
     }
   }
-  __syncthreads();   // every wave is done reading a2s as a2 before it becomes dz2
-
-  // da2 = dz3 W2^T ([BP x HP] over CP), dz2 = da2 * act'(a2) (in place)
-  const int nht = HP / 16;
-  for (int t = w; t < (BP / 16) * nht; t += nw) {
-    const int rb = (t / nht) * 16, hb = (t % nht) * 16;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int k = 0; k < CP; k += 4) acc = mfma4(dz3s[(rb + r) * CP + k + g], w2s[(hb + r) * CP + k + g], acc);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = rb + 4 * g + i, h = hb + r;
-      const float av = a2s[m * HP + h];
-      const float d = (m < B && h < H) ? acc[i] * act_bwd(av, a.act) : 0.f;
-      a2s[m * HP + h] = d;
-      a.dz2[(size_t)m * HP + h] = d;
-    }
-  }
-  if (tid == 0) {
-    a.metrics[0] = red[0] / (float)B;
-    a.metrics[1] = red[1] / (float)B;
+  if (ht == 0 && tid == 0) {
+    const float* lc = a.hpart + (size_t)NRT * HP * CP;
+    float ls = 0.f, cr = 0.f;
+    for (int rt = 0; rt < NRT; ++rt) { ls += lc[2 * rt]; cr += lc[2 * rt + 1]; }
+    a.metrics[0] = ls / (float)a.B;
+    a.metrics[1] = cr / (float)a.B;
     if (a.gstep != nullptr) {
       float now;
       switch (a.gstep_kind) {
@@ -302,16 +305,20 @@ __global__ __launch_bounds__(512) void graph_mlp_head(HeadArgs a) {
   }
 }
 
-// ---------------------------------------------------------------- L3
-// One workgroup per 16x16 tile of [dW1; db1] ((K+1) x H: row K is db1, from a
-// virtual x column of ones); its 4 waves split the batch and prefetch all of
-// their operands (<= 16 batch blocks each) before the MFMAs.
-constexpr int L3PF = 16;
-__global__ __launch_bounds__(256) void graph_mlp_wgrad(const float* __restrict__ x, const float* __restrict__ dz2,
-                                                       float* __restrict__ W1, float* __restrict__ b1,
-                                                       float* __restrict__ gW1, float* __restrict__ gb1, float lr,
-                                                       int B, int K, int H, int HP, int sgd) {
+__global__ __launch_bounds__(256) void graph_mlp_wgrad(WgradArgs a) {
   __shared__ f32x4 part[4][64];
+  if ((int)blockIdx.x >= a.tiles) {
+    graph_mlp_w2_final(a, (int)blockIdx.x - a.tiles);
+    return;
+  }
+  const float* __restrict__ x = a.x;
+  const float* __restrict__ dz2 = a.dz2;
+  const int B = a.B, K = a.K, H = a.H, HP = a.HP, sgd = a.sgd;
+  const float lr = *a.lr_ptr;
+  float* W1 = a.W1;
+  float* b1 = a.b1;
+  float* gW1 = a.gW1;
+  float* gb1 = a.gb1;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int nht = HP / 16;
@@ -362,18 +369,20 @@ __global__ __launch_bounds__(256) void graph_mlp_wgrad(const float* __restrict__
 }  // namespace gmlp
 }  // namespace dtfk
 
-// Shared-memory bytes L2 needs (host check before launch).
-extern "C" long long dtfk_graph_mlp_lds(int B, int HP) {
-  const int BP = (B + 15) & ~15;
-  return 4LL * ((long long)BP * HP + HP * dtfk::gmlp::CP + 2LL * BP * dtfk::gmlp::CP + 64);
+// Device scratch (floats) the step needs besides a2 / dz2: L2's partials + loss sums.
+extern "C" long long dtfk_graph_mlp_part_floats(int B, int H) {
+  const int HP = (H + 16) & ~15, NRT = (B + 15) / 16;
+  return (long long)NRT * HP * dtfk::gmlp::CP + 2LL * NRT;
 }
 
 extern "C" hipError_t dtfk_graph_mlp_step(const float* x, const float* ylab, float* W1, float* b1, float* W2,
-                                          float* b2, float* a2buf, float* dz2buf, float* gW1, float* gb1, float* gW2,
-                                          float* gb2, float* metrics, void* gstep, int gstep_kind, float lr, int B,
-                                          int K, int H, int C, int act, int naive, int sgd, hipStream_t stream) {
+                                          float* b2, float* a2buf, float* dz2buf, float* part, float* gW1, float* gb1,
+                                          float* gW2, float* gb2, float* metrics, void* gstep, int gstep_kind,
+                                          const float* lr_ptr, int B, int K, int H, int C, int act, int naive, int sgd,
+                                          hipStream_t stream) {
   using namespace dtfk::gmlp;
-  if (B < 1 || B > MAXB || H < 1 || H > MAXH || C < 1 || C > CP || K < 1) return hipErrorInvalidValue;
+  if (B < 1 || B > MAXB || H < 1 || H > MAXH || C < 1 || C > CP || K < 1 || lr_ptr == nullptr)
+    return hipErrorInvalidValue;
   const int HP = (H + 16) & ~15, BP = (B + 15) & ~15;   // >= H + 1 (ones column)
   if (BP * HP > A2_LDS) return hipErrorInvalidValue;
   const bool vec = (K & 3) == 0 && K >= 4 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
@@ -383,19 +392,11 @@ extern "C" hipError_t dtfk_graph_mlp_step(const float* x, const float* ylab, flo
   else
     hipLaunchKernelGGL(graph_mlp_l1<false>, dim3((BP / 16) * (HP / 16)), dim3(512), 0, stream, x, W1, b1, a2buf, B,
                        K, H, HP, act);
-  HeadArgs h{a2buf, ylab, W2, b1, b2, dz2buf, gW2, gb1, gb2, metrics, gstep, gstep_kind, lr, B, H, HP, C, act,
-             naive, sgd};
-  const size_t lds = (size_t)dtfk_graph_mlp_lds(B, HP);
-  static bool lds_set = false;
-  if (!lds_set) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&graph_mlp_head),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return e;
-    lds_set = true;
-  }
-  hipLaunchKernelGGL(graph_mlp_head, dim3(1), dim3(512), lds, stream, h);
+  HeadArgs h{a2buf, ylab, W2, b2, dz2buf, part, B, H, HP, C, act, naive};
+  hipLaunchKernelGGL(graph_mlp_head, dim3(BP / 16), dim3(HW * 64), 0, stream, h);
   const int tiles = ((K + 1 + 15) / 16) * (HP / 16);
-  hipLaunchKernelGGL(graph_mlp_wgrad, dim3(tiles), dim3(256), 0, stream, x, dz2buf, W1, b1, gW1, gb1, lr, B, K, H,
-                     HP, sgd);
+  WgradArgs wa{x, dz2buf, W1, b1, W2, b2, gW1, gb1, gW2, gb2, part, metrics, gstep, gstep_kind, lr_ptr,
+               B, K, H, HP, C, sgd, tiles};
+  hipLaunchKernelGGL(graph_mlp_wgrad, dim3(tiles + HP / 16), dim3(256), 0, stream, wa);
   return hipGetLastError();
 }

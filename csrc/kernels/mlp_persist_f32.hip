@@ -144,8 +144,10 @@ constexpr int L_LAB = L_XT + 13 * 16 * XTS;            // [128] labels
 constexpr int PS = XTS + 8;                            // split mode: bf16 plane row stride (elements)
 constexpr int L_DZP = L_LAB + 128;                     // split mode: [3 pieces][16 hidden][PS] dz2 bf16
 constexpr int L_HFLAG = L_DZP + 3 * 16 * PS * 2;       // [8] head-done flags (step + 1) of waves 0..6
-constexpr int LDS_COMPUTE = L_HFLAG + 64;
+constexpr int L_DW2P = L_HFLAG + 64;                   // [7 batch tiles][64 lanes] f32x4 dW2 partials
+constexpr int LDS_COMPUTE = L_DW2P + NBT * 64 * 16;
 static_assert(L_XF % 1024 == 0 && L_XT % 16 == 0 && L_LAB % 16 == 0, "LDS-DMA bases");
+static_assert(L_DW2P % 16 == 0, "dW2 partials: 16-B lanes");
 constexpr int CROW = DIN + 16;                         // copier LDS row stride (800)
 constexpr int LDS_COPIER = BROWS * CROW;               // 89600
 constexpr int LDS_BYTES = LDS_COMPUTE > LDS_COPIER ? LDS_COMPUTE : LDS_COPIER;
@@ -179,12 +181,20 @@ struct Args {
                             // no / short / long s_sleep between passes (DTF_GATHER_MODE, tuning)
   int xmode;                // N GPUs: 0 one-shot (every workgroup reads its slot from every peer),
                             // 1 two-shot (reduce-scatter by wave chunk, then all-gather of the sums)
+  int dbg;                  // profiling only (DTF_PERSIST_DBG): bit 0 = never stage the next step's x (wrong
+                            // numerics; what the per-step LDS-DMA stage costs the hand-offs), bit 1 = head
+                            // sub-phase stamps (slots 13-15, wave 0)
 };
 
 // phase stamp ph of step st (s_memrealtime, 100 MHz) -- profiling only
 #define PH(ph)                                                                                 \
   if (a.phase_ts != nullptr && lane == 0 && st < 64)                                         \
     a.phase_ts[((long long)st * 64 + c) * 16 + (ph)] = (long long)__builtin_amdgcn_s_memrealtime();
+// DTF_PERSIST_DBG bit 1: wave 0 stamps the head's sub-phases into slots 13-15 (wave 7's stamps off)
+#define PHX(ph) \
+  if ((a.dbg & 2) != 0) { PH(ph); }
+#define PH7(ph) \
+  if ((a.dbg & 2) == 0) { PH(ph); }
 
 // The exact three-way split v = hi + mid + lo by truncation, as fp32 bit
 // patterns whose low 16 bits are zero: hi keeps v's top 8 significant bits, the
@@ -633,18 +643,21 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
       }
     }
   };
-  __syncthreads();
+  // Prologue, all latency overlapped (it was three serial phases, ~6 us per
+  // launch): the census entry goes out first, the first step's x stage is
+  // issued (LDS-DMA) while the parameter loads above are still in flight, and
+  // wave 0 polls the census meanwhile; one drain + barrier then covers all three.
   if (tid == 0) { PRO(c, 4); }
-  if (failed_in) return;
   // ---- placement census: E1 group (the NQ slices of block j) and E2 group (the
   // NJ blocks of slice q) each on this workgroup's XCD -> that edge stays in one
   // L2 (plain stores).  Decided per launch from HW_REG_XCC_ID, never assumed.
+  const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20) & 15u;
+  unsigned long long* hdr = reinterpret_cast<unsigned long long*>(a.xbuf + HDR_OFF);
+  const unsigned tag0 = (unsigned)(seq0 + 1ull);
+  if (tid == 0)
+    __hip_atomic_store(hdr + c, ((unsigned long long)tag0 << 32) | xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  stage_x(0, w, 8);   // the first step's stage: every wave a share
   if (w == 0) {   // lane cc watches workgroup cc's entry: all 28 polls in flight at once
-    const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20) & 15u;
-    unsigned long long* hdr = reinterpret_cast<unsigned long long*>(a.xbuf + HDR_OFF);
-    const unsigned tag0 = (unsigned)(seq0 + 1ull);
-    if (lane == 0)
-      __hip_atomic_store(hdr + c, ((unsigned long long)tag0 << 32) | xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
     unsigned long long v = 0;
     bool seen = lane >= NCOMP, bad = false;
@@ -666,14 +679,14 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
     const bool e2 = !__any(off && lane % NQ == q);
     if (lane == 0) *census = bad ? -1 : ((e1 ? 1 : 0) | (e2 ? 2 : 0));
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // parameter loads + the first stage landed
   __syncthreads();
-  if (*census < 0) return;
+  // an earlier launch failed (err set): nothing runs.  Checked only here, so the
+  // wait for that load does not serialize the parameter loads behind it
+  if (failed_in || *census < 0) return;
   const bool l2_e1 = (*census & 1) != 0;
   const bool l2_e2 = (*census & 2) != 0;
   if (tid == 0) { PRO(c, 1); }
-  stage_x(0, w, 8);   // the first step's stage: every wave a share
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
   read_xf();
   read_xt();
   if (tid == 0) { PRO(c, 2); }
@@ -687,7 +700,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
     if (c == 0 && tid == 0 && a.step_ts != nullptr)
       a.step_ts[(gstep0 + st) % a.ts_ring] = (long long)__builtin_amdgcn_s_memrealtime();
     if (w == 0) { PH(0); }
-    if (w == 7) { PH(14); }
+    if (w == 7) { PH7(14); }
 
     // ---------------- P0: forward partial of the wave's tiles, all batch tiles
     {
@@ -727,14 +740,12 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
       for (int b = 0; b < NBT; ++b) zbuf[(w * NBT + b) * 64 + lane] = acc[b];
     }
     if (w == 0) { PH(1); }
-    if (w == 7) { PH(13); }
-    if (w == 3) { PH(15); }
     lds_barrier();
     if (w == 0) { PH(2); }
     const bool more = st + 1 < a.nsteps;
     // everyone's reads of this step's stage retired at barrier A: wave 7 (idle
     // until P2) stages the next step while the others run the edges and the head
-    if (w == 7 && more) stage_x(st + 1, 0, 1);
+    if (w == 7 && more && !(a.dbg & 1)) stage_x(st + 1, 0, 1);
 
     // ---------------- E1 + P1 + E2 + head (wave w < 7: batch tile w)
     if (w < NBT) {
@@ -761,7 +772,9 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
       for (int i = 0; i < 4; ++i) {
         const int hl = 4 * g + i;
         const float zt = z[i] * (1.f / 255.f) + b1s[hl];
-        const float av = ACT == 0 ? 1.f / (1.f + expf(-zt)) : fmaxf(zt, 0.f);
+        // v_exp_f32 / v_rcp_f32 (<= 2 ulp each, 1e-7 relative): ~20 instructions per
+        // element less than IEEE expf + division on this single-wave critical path
+        const float av = ACT == 0 ? __builtin_amdgcn_rcpf(1.f + __expf(-zt)) : fmaxf(zt, 0.f);
         a2[i] = (16 * j + hl < HID) ? av : 0.f;
       }
       // partial logits^T[class][batch] of block j: A = W2^T (lane: class r), B = a2^T
@@ -798,7 +811,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int cl = 4 * g + i;
-        ex[i] = cl < NCLS ? expf(lg[i] - m) : 0.f;
+        ex[i] = cl < NCLS ? __expf(lg[i] - m) : 0.f;
         ssum += ex[i];
         zy += (cl == y) ? lg[i] : 0.f;
         if (cl < NCLS && lg[i] == m) am = fminf(am, (float)cl);
@@ -806,7 +819,8 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
       ssum += xor16(ssum); ssum += xor32(ssum);
       zy += xor16(zy); zy += xor32(zy);
       am = fminf(am, xor16(am)); am = fminf(am, xor32(am));
-      const float inv = 1.f / ssum;
+      const float inv = __builtin_amdgcn_rcpf(ssum);
+      if (w == 0) { PHX(13); }
       float dz3[4], py = 0.f;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -816,11 +830,12 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
         dz3[i] = (bv && cl < NCLS) ? p - (cl == y ? 1.f : 0.f) : 0.f;   // unscaled: 1/B at the update
       }
       py += xor16(py); py += xor32(py);
-      const float loss = a.naive ? -logf(py) : (m + logf(ssum) - zy);
+      const float loss = a.naive ? -__logf(py) : (m + __logf(ssum) - zy);
       // da2^T = W2 . dz3^T (A = W2, lane: hidden r), dz2 = da2 * act'(a2)
       f32x4 da = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int e = 0; e < 4; ++e) da = mfma4(w2s[r * 16 + 4 * g + e], dz3[e], da);
+      if (w == 0) { PHX(14); }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float d = ACT == 0 ? da[i] * a2[i] * (1.f - a2[i]) : (a2[i] > 0.f ? da[i] : 0.f);
@@ -842,10 +857,24 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
           rdb2[w * 16 + 4 * g + i] = s2;
         }
       }
+      if (w == 0) { PHX(15); }
       const float ls = row16_sum((g == 0 && bv) ? loss : 0.f);
       const float cr = row16_sum((g == 0 && bv && (int)am == y) ? 1.f : 0.f);
       if (lane == 0) { rmet[2 * w] = ls; rmet[2 * w + 1] = cr; }
-      // head of batch tile w done (its a2 / dz3 rows and db partials are in LDS, its
+      // this tile's dW2 partial (a2^T dz3 over its 16 rows, from the rows this wave
+      // just wrote: LDS ops of one wave complete in order) -- folded here, in
+      // parallel over the 7 head waves, instead of by wave 7 tile after tile
+      // (7 serial folds behind the last head: ~0.7 us of every step)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      {
+        const f32x4 av = *reinterpret_cast<const f32x4*>(a2T + r * LS + 16 * w + 4 * g);
+        const f32x4 dv = *reinterpret_cast<const f32x4*>(dz3T + r * LS + 16 * w + 4 * g);
+        f32x4 dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dp = mfma4(av[e], dv[e], dp);
+        reinterpret_cast<f32x4*>(smem + L_DW2P)[w * 64 + lane] = dp;
+      }
+      // head of batch tile w done (its dW2 / db partials and metrics are in LDS, its
       // reads of W2 / b1 / b2 are over): wave 7 takes it from here
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
       if (lane == 0)
@@ -853,9 +882,9 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
                            __HIP_MEMORY_SCOPE_WORKGROUP);
       if (w == 0) { PH(9); }
     }
-    // wave 7 (idle since staging the next step): dW2, db1, db2 and the metrics,
-    // batch tile by batch tile as the heads finish (fixed tile order), so none of
-    // it is left for after barrier B; one GPU: the W2 / b1 / b2 updates too
+    // wave 7 (idle since staging the next step): sums the 7 head waves' dW2 / db1 /
+    // db2 partials and metrics in fixed tile order (bit-identical to folding them
+    // one by one); one GPU: the W2 / b1 / b2 updates too
     f32x4 D = {0.f, 0.f, 0.f, 0.f};      // wave 7: dW2[16j+4g+i][class r] (x B)
     float gb = 0.f;                      // wave 7: db1 (lanes < 16) / db2 (lanes 16..25) (x B)
     float ls = 0.f, cr = 0.f;            // wave 7: loss / correct sums of the batch
@@ -863,23 +892,26 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
       const int* hflag = reinterpret_cast<const int*>(smem + L_HFLAG);
       // lane < 16: db1 column `lane`; 16..25: db2 column lane - 16 (rdb2 follows rdb1 by 128 floats)
       const float* gsrc = rdb1 + (lane < 16 ? lane : (lane < 16 + NCLS ? lane + 112 : 0));
+      for (;;) {   // lane v < 7 watches head v: all flags in one poll
+        const bool ok = lane >= NBT ||
+                        __hip_atomic_load(hflag + (lane < NBT ? lane : 0), __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_WORKGROUP) >= st + 1;
+        if (__all(ok)) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+      const f32x4* dw2p = reinterpret_cast<const f32x4*>(smem + L_DW2P);
 #pragma unroll
       for (int v = 0; v < NBT; ++v) {
-        while (__hip_atomic_load(hflag + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < st + 1)
-          __builtin_amdgcn_s_sleep(1);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-        const f32x4 av = *reinterpret_cast<const f32x4*>(a2T + r * LS + 16 * v + 4 * g);
-        const f32x4 dv = *reinterpret_cast<const f32x4*>(dz3T + r * LS + 16 * v + 4 * g);
-        f32x4 dp = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) dp = mfma4(av[e], dv[e], dp);
-        D += dp;
+        D += dw2p[v * 64 + lane];
         gb += gsrc[v * 16];
         ls += rmet[2 * v];
         cr += rmet[2 * v + 1];
       }
       if (lane >= 16 + NCLS) gb = 0.f;
+      PH7(13);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next step's stage landed (long since)
+      PH7(15);
       if constexpr (!MULTI) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -1223,8 +1255,10 @@ hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int n
   a.spread = spread;
   a.xmode = xmode;
   {
-    const char* gm = getenv("DTF_GATHER_MODE");   // measured: direct + long sleep 13.04 vs probe 13.32 us/step
-    a.gmode = gm ? atoi(gm) : 3;
+    const char* gm = getenv("DTF_GATHER_MODE");   // r3: direct loads, no sleep 8.68 / long sleep 8.72 / probe 9.56 us
+    a.gmode = gm ? atoi(gm) : 1;
+    const char* db = getenv("DTF_PERSIST_DBG");
+    a.dbg = db ? atoi(db) : 0;
   }
   constexpr size_t lds = LDS_BYTES;
   typedef void (*Kern)(Args);

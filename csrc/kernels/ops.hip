@@ -483,9 +483,11 @@ __device__ __forceinline__ float ld_grad(const void* g, int64_t i, int gbf) {
 __global__ void multi_tensor_apply(const TensorRec* __restrict__ tab, const int2* __restrict__ chunks,
                                    int nchunks, int kind, int gbf, const float* __restrict__ lr_ptr,
                                    float lr_scalar, float gscale, float wd, float b1, float b2, float eps,
-                                   float momentum, int nesterov, const long long* __restrict__ step_ptr) {
+                                   float momentum, int nesterov, const long long* __restrict__ step_ptr,
+                                   const int* __restrict__ skip) {
   const int cidx = blockIdx.x;
   if (cidx >= nchunks) return;
+  if (skip != nullptr && *skip != 0) return;   // a voided step (sharded-table overflow): no update at all
   const int2 ch = chunks[cidx];
   const TensorRec t = tab[ch.x];
   const float lr = lr_ptr ? *lr_ptr : lr_scalar;
@@ -702,11 +704,11 @@ hipError_t dtfk_auc_hist(const float* pred, const float* label, int64_t n, int n
 hipError_t dtfk_multi_tensor_apply(const void* tab, const void* chunks, int nchunks, int kind, int gbf,
                                    const float* lr_ptr, float lr, float gscale, float wd, float b1, float b2,
                                    float eps, float momentum, int nesterov, const long long* step,
-                                   hipStream_t s) {
+                                   const int* skip, hipStream_t s) {
   if (nchunks == 0) return hipSuccess;
   hipLaunchKernelGGL(multi_tensor_apply, dim3(nchunks), dim3(256), 0, s, (const TensorRec*)tab,
                      (const int2*)chunks, nchunks, kind, gbf, lr_ptr, lr, gscale, wd, b1, b2, eps, momentum,
-                     nesterov, step);
+                     nesterov, step, skip);
   return hipGetLastError();
 }
 hipError_t dtfk_multi_tensor_sumsq(const void* tab, const void* chunks, int nchunks, int gbf, float* out,

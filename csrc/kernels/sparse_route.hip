@@ -11,9 +11,12 @@
 //                  (owner = id % W; positions within an owner in id order),
 //   send[W*cap]    W > 1: ids bucketed by owner, -1 padded,
 // with every shape static and nothing read back by the host: the exchange is an
-// equal-split all-to-all of `cap` slots per peer, cap >= N (the ids of this
-// rank's batch bound every bucket, so nothing can overflow) and the same on
-// every rank (a configured capacity), so the sparse step can be captured.
+// equal-split all-to-all of `cap` slots per peer, the same on every rank, so the
+// sparse step can be captured.  `cap` is right-sized to the owners' unique-id
+// load (parallel/sharded_embedding.py adapts it), not to the batch: an owner's
+// ids beyond `cap` are not sent (dest -1) -- the per-owner unique counts come
+// back to the caller, which voids such a step on every rank and replays it
+// through the exact exchange.
 //
 // Fully parallel over the batch: route_flags marks the first occurrence of
 // each id (and, W > 1, its owner as a one-hot row), the host-side binding runs
@@ -61,9 +64,14 @@ __global__ __launch_bounds__(256) void route_scatter(const ID* __restrict__ sids
     uniq[k] = (int64_t)v;
     if (W > 1) {
       const int o = (int)((int64_t)v % W);
-      const int d = o * cap + owncum[(size_t)i * W + o] - 1;
-      dest[k] = d;
-      send[d] = (int64_t)v;
+      const int pos = owncum[(size_t)i * W + o] - 1;     // rank among owner o's unique ids
+      if (pos < cap) {
+        const int d = o * cap + pos;
+        dest[k] = d;
+        send[d] = (int64_t)v;
+      } else {
+        dest[k] = -1;                                    // overflow: not exchanged (the step is voided)
+      }
     }
   }
   if (i >= U) {            // padding slots of the static-length outputs
@@ -103,7 +111,7 @@ extern "C" hipError_t dtfk_route_scatter(const void* sids, int ids32, const int6
                                          int64_t* uniq, int* dest, int64_t* send, int* count, hipStream_t stream) {
   using namespace dtfk::route;
   if (N <= 0) return hipSuccess;
-  if (W > MAXW || (W > 1 && cap < N)) return hipErrorInvalidValue;
+  if (W > MAXW || (W > 1 && cap < 1)) return hipErrorInvalidValue;
   if (W > 1) {
     const long long n = (long long)W * cap;
     hipLaunchKernelGGL(fill_i64, dim3((unsigned)std::min<long long>((n + 255) / 256, 4096)), dim3(256), 0, stream, send,

@@ -238,6 +238,8 @@ class MLPStepPlan:
         W1, b1, W2, b2 = (v.value for v in (pat.W1, pat.b1, pat.W2, pat.b2))
         if not W1.is_cuda:
             return False
+        if self._run_native_plan(ctx, flat, W1, b1, W2, b2):
+            return True
         xy = self._packed_feeds(ctx, W1.device)
         x, y = xy if xy is not None else (ctx.eval(pat.x), ctx.eval(pat.ylab))
         if not (isinstance(x, torch.Tensor) and isinstance(y, torch.Tensor) and x.is_cuda):
@@ -312,6 +314,58 @@ class MLPStepPlan:
             ctx.memo[id(pat.loss)] = self.metrics[0]
             if self.accuracy is not None:
                 ctx.memo[id(self.accuracy)] = self.metrics[1]
+        ctx.memo[id(self.op)] = None
+        self.steps += 1
+        return True
+
+    def _run_native_plan(self, ctx, flat, W1, b1, W2, b2) -> bool:
+        """The reference's case -- plain SGD (one worker, or async), numpy feeds --
+        as ONE native call: C++ packs the feeds (GIL released), one host-to-device
+        copy, the three kernels + the metrics copy replayed from a captured
+        hipGraph (csrc/bind_mlp.cpp GraphStepPlan).  False: not applicable."""
+        from .. import _native
+        from .train import GradientDescentOptimizer, _world_or_local
+        from ..utils import debug as _debug
+
+        pat, info = self.pat, self.info
+        opt, gs_var = info["opt"], info["global_step"]
+        w = _world_or_local()
+        if type(opt) is not GradientDescentOptimizer or info["sparse"] or (w.world_size > 1 and opt.sync_replicas):
+            return False
+        fx, fy = self._feed_of(ctx, pat.x), self._feed_of(ctx, pat.ylab)
+        if fx is None or fy is None or fx.ndim != 2:
+            return False
+        B, K = fx.shape
+        H, C = W1.shape[1], W2.shape[1]
+        HP, BP = (H + 16) // 16 * 16, (B + 15) // 16 * 16
+        if not (1 <= B <= 256 and BP * HP <= 16384 and H <= 128 and C <= 16 and W1.shape[0] == K
+                and fy.size == B * C and all(p.dtype == torch.float32 and p.is_contiguous()
+                                             for p in (W1, b1, W2, b2))):
+            return False
+        gstep = None
+        if gs_var is not None:
+            gv = getattr(gs_var, "value", None)
+            if not (isinstance(gv, torch.Tensor) and gv.is_cuda and gv.numel() == 1
+                    and gv.dtype in (torch.float32, torch.int64, torch.int32, torch.float64)):
+                return False
+            gstep = gv.data
+        key = (B, K, W1.data_ptr(), b1.data_ptr(), W2.data_ptr(), b2.data_ptr(),
+               None if gstep is None else gstep.data_ptr(), pat.act, pat.naive)
+        if getattr(self, "_cplan_key", None) != key:
+            self._cplan = _native.load().GraphStepPlan(W1.data, b1.data, W2.data, b2.data, gstep, B, pat.act,
+                                                       bool(pat.naive))
+            self._cplan_key = key
+        opt._steps += 1
+        _debug.fault_point(opt._steps, w.rank)
+        needs, gs_seed = self._needs(flat, gs_var, gstep)
+        self._cplan.run(np.ascontiguousarray(fx), np.ascontiguousarray(fy).reshape(B, C), float(opt._lr_value()),
+                        bool(needs))
+        m = self._cplan.host_metrics()
+        ctx.memo[id(pat.loss)] = m[0]
+        if self.accuracy is not None:
+            ctx.memo[id(self.accuracy)] = m[1]
+        if gs_seed:
+            ctx.memo[id(gs_var)] = m[2].to(gs_var.value.dtype)
         ctx.memo[id(self.op)] = None
         self.steps += 1
         return True

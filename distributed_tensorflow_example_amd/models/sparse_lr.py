@@ -24,18 +24,22 @@ import numpy as np
 import torch
 
 from .. import ops
-from ..parallel.sharded_embedding import ShardedEmbedding
+from ..parallel.sharded_embedding import ShardedEmbedding, StaticStepMixin, lookup_shared, pad_to_capacity
 from ..parallel.world import World, get_world
 
 
-class SparseLRTrainer:
+class SparseLRTrainer(StaticStepMixin):
     def __init__(self, num_features: int, lr: float, world: Optional[World] = None, seed: int = 1,
-                 init_std: float = 1.0, device=None, auc_bins: int = 200, ids_capacity: Optional[int] = None):
+                 init_std: float = 1.0, device=None, auc_bins: int = 200, ids_capacity: Optional[int] = None,
+                 rows: int = 500, peer_capacity: Optional[int] = None):
         self.world = world or get_world()
         self.device = torch.device(device) if device is not None else self.world.device
         self.lr = float(lr)
         self.W = ShardedEmbedding(num_features, 1, self.world, init_std=init_std, seed=seed, device=self.device,
-                                  name="weights/Variable", capacity=ids_capacity)
+                                  name="weights/Variable", capacity=ids_capacity, peer_capacity=peer_capacity)
+        self.rows = int(rows)              # batch rows of the captured step (lr2: batch_size)
+        self._window = []                  # static steps since the router's last check (replay source)
+        self._example = None
         self.b = torch.zeros(1, dtype=torch.float32, device=self.device, requires_grad=True)
         self.global_step = 0
         self._graphed = None
@@ -44,22 +48,32 @@ class SparseLRTrainer:
         self.auc_neg = torch.zeros(auc_bins + 1, dtype=torch.int64, device=self.device)
 
     # ----------------------------------------------------------------- steps
-    def _forward(self, batch):
+    def _forward(self, batch, exact: bool = False):
         labels, offsets, ids, vals = batch.to(self.device) if hasattr(batch, "to") else batch
-        out, st = self.W.bag_forward(ids, offsets, vals, "sum")
-        return out + self.b, labels, st
+        ctx = self.W.route(ids, exact=exact)
+        rows = lookup_shared([self.W], ctx)[0].detach().requires_grad_(True)
+        out = ops.embedding_bag(rows, ctx.inverse, offsets.to(self.device).long(),
+                                None if vals is None else vals.to(self.device).float(), "sum")
+        return out + self.b, labels, (rows, ctx)
 
-    def train_step(self, batch) -> torch.Tensor:
-        if self._graphed is not None:
-            labels, offsets, ids, vals = batch.to(self.device) if hasattr(batch, "to") else batch
-            loss = self._graphed(labels, offsets, ids, vals)
-            self.global_step += 1
-            return loss.detach()
-        return self._train_step(batch)
+    def _static_batch(self, batch):
+        labels, offsets, ids, vals = batch.to(self.device) if hasattr(batch, "to") else batch
+        offsets = offsets.to(self.device).long()
+        ids = ids.to(self.device)
+        vals = None if vals is None else vals.to(self.device).float()
+        if self.W.capacity is not None:      # fixed shapes for the captured / static step
+            offsets, ids, vals = pad_to_capacity(offsets, ids, vals, self.W.capacity)
+        return labels.to(self.device), offsets, ids, vals
 
-    def enable_graph(self, on: bool = True):
+    def _router(self):
+        return self.W.router
+
+    def enable_graph(self, on: bool = True, example=None):
         """Replay each step as one captured hipGraph (GPU; needs the static
-        device-resident routing: one worker, or an ids capacity for W > 1)."""
+        device-resident routing: one worker, or an ids capacity for W > 1).
+        With W > 1 every rank must call this at the same point: the capture
+        runs the step's collectives (`example`: a batch of the training row
+        count; default: an all-zero batch of `rows` rows)."""
         from ..utils.graphs import GraphedStep
 
         if not on:
@@ -67,39 +81,55 @@ class SparseLRTrainer:
             return
         if self.device.type != "cuda" or (self.world.world_size > 1 and self.W.capacity is None):
             raise RuntimeError("graph capture needs a GPU and static routing (ids_capacity for W > 1)")
+        strict = self.world.world_size > 1
 
         def step(labels, offsets, ids, vals):
-            gs = self.global_step
-            loss = self._train_step((labels, offsets, ids, vals))
-            self.global_step = gs          # counted by train_step, not by warmup/capture
-            return loss
-        self._graphed = GraphedStep(step, lambda: [self.W.local, self.b.data])
+            return self._train_step((labels, offsets, ids, vals))
 
-    def _train_step(self, batch) -> torch.Tensor:
-        logits, labels, st = self._forward(batch)
+        def state():
+            st = [self.W.local, self.b.data]
+            return st + (self.W.router.state() if self.W.router is not None else [])
+        self._graphed = GraphedStep(step, state, strict=strict)
+        self._example = self._static_batch(example if example is not None else self._zero_batch())
+        if strict:
+            self._graphed.capture(*self._example)
+
+    def _zero_batch(self, rows: Optional[int] = None):
+        rows = rows or self.rows
+        n = self.W.capacity or rows
+        per = max(1, n // rows)
+        offsets = torch.clamp(torch.arange(rows + 1, dtype=torch.int64) * per, max=n)
+        offsets[-1] = n
+        return (torch.zeros(rows, 1), offsets, torch.zeros(n, dtype=torch.int64), torch.zeros(n))
+
+    def _train_step(self, batch, exact: bool = False) -> torch.Tensor:
+        logits, labels, (rows, ctx) = self._forward(batch, exact)
         loss = ops.sigmoid_xent(logits, labels)
         if self.b.grad is not None:
             self.b.grad = None
         loss.backward()
         ws = self.world.world_size
-        self.W.bag_backward_sgd(st, self.lr / ws)
+        g = rows.grad if rows.grad is not None else torch.zeros_like(rows)
+        self.W.apply_sgd(ctx, g, self.lr / ws)
         with torch.no_grad():
             gb = self.b.grad.clone()
             if ws > 1:
                 self.world.all_reduce(gb)
+            if ctx.void is not None:          # a voided step changes nothing (replayed exactly later)
+                gb *= (1 - ctx.void).to(gb.dtype)
             self.b -= (self.lr / ws) * gb
-        self.global_step += 1
         return loss.detach()
 
     @torch.no_grad()
     def evaluate(self, batch):
-        """(mean loss, probabilities) without updating (lr2.py Test(), :307-315)."""
-        logits, labels, _ = self._forward(batch)
+        """(mean loss, probabilities) without updating (lr2.py Test(), :307-315).
+        Lookups use the exact exchange: evaluation batches need no fixed shapes."""
+        logits, labels, _ = self._forward(batch, exact=True)
         return ops.sigmoid_xent(logits, labels).detach(), torch.sigmoid(logits).reshape(-1)
 
     @torch.no_grad()
     def auc_update(self, batch):
-        logits, labels, _ = self._forward(batch)
+        logits, labels, _ = self._forward(batch, exact=True)
         ops.auc_histogram_(torch.sigmoid(logits).reshape(-1), labels.reshape(-1), self.auc_pos, self.auc_neg)
 
     def auc(self, all_workers: bool = True) -> float:

@@ -24,24 +24,32 @@ from typing import List, Optional, Sequence
 import torch
 
 from .. import ops, optim
-from ..parallel.sharded_embedding import ShardedEmbedding, apply_sgd_shared, lookup_shared
+from ..parallel.sharded_embedding import (ShardedEmbedding, StaticStepMixin, apply_sgd_shared, lookup_shared,
+                                          pad_to_capacity)
 from ..parallel.world import World, get_world
 
 
-class WideDeep:
+class WideDeep(StaticStepMixin):
     def __init__(self, num_features: int, emb_dim: int = 64, hidden: Sequence[int] = (256, 128),
                  lr: float = 0.05, dense_lr: Optional[float] = None, dense_opt: str = "sgd", combiner: str = "sum",
                  world: Optional[World] = None, seed: int = 1, device=None, emb_std: float = 0.05,
-                 ids_capacity: Optional[int] = None):
+                 ids_capacity: Optional[int] = None, rows: int = 4096, peer_capacity: Optional[int] = None):
         self.world = world or get_world()
         self.device = torch.device(device) if device is not None else self.world.device
         self.lr = float(lr)
         self.combiner = combiner
         self.ids_capacity = ids_capacity   # per-batch id bound -> device-resident static routing
+        if ids_capacity is not None and combiner != "sum":
+            raise ValueError("static routing (ids_capacity) pads batches inside the last bag: 'sum' combiner only")
+        # both tables route the same ids over the same partition: one router
         self.wide = ShardedEmbedding(num_features, 1, self.world, init_std=0.01, seed=seed, device=self.device,
-                                     name="wide/weights")
+                                     name="wide/weights", capacity=ids_capacity, peer_capacity=peer_capacity)
         self.emb = ShardedEmbedding(num_features, emb_dim, self.world, init_std=emb_std, seed=seed + 1,
-                                    device=self.device, name="deep/embedding")
+                                    device=self.device, name="deep/embedding", capacity=ids_capacity,
+                                    router=self.wide.router)
+        self.rows = int(rows)              # batch rows of the captured step
+        self._window = []                  # static steps since the router's last check (replay source)
+        self._example = None
         g = torch.Generator().manual_seed(seed + 2)
         dims = [emb_dim] + list(hidden) + [1]
         self.layers: List[torch.nn.Parameter] = []
@@ -68,10 +76,10 @@ class WideDeep:
         self.global_step = 0
         self._graphed = None
 
-    def forward(self, labels, offsets, ids, vals):
+    def forward(self, labels, offsets, ids, vals, exact: bool = False):
         # both tables read the same ids over the same row partition: one
         # dedup + id exchange, one row exchange carrying [U, 1 + D]
-        ctx = self.wide.route(ids, capacity=self.ids_capacity)
+        ctx = self.wide.route(ids, capacity=self.ids_capacity, exact=exact)
         wrows, erows = lookup_shared([self.wide, self.emb], ctx)
         wrows = wrows.detach().requires_grad_(True)
         erows = erows.detach().requires_grad_(True)
@@ -86,19 +94,26 @@ class WideDeep:
         logit = wide + h + self.bias
         return logit, (wrows, erows, ctx)
 
-    def train_step(self, batch) -> torch.Tensor:
-        if self._graphed is not None:
-            labels, offsets, ids, vals = batch.to(self.device) if hasattr(batch, "to") else batch
-            loss = self._graphed(labels, offsets, ids, vals)
-            self.global_step += 1
-            return loss.detach()
-        return self._train_step(batch)
+    def _static_batch(self, batch):
+        labels, offsets, ids, vals = batch.to(self.device) if hasattr(batch, "to") else batch
+        offsets = offsets.to(self.device).long()
+        ids = ids.to(self.device)
+        vals = None if vals is None else vals.to(self.device).float()
+        if self.ids_capacity is not None:    # fixed shapes for the captured / static step
+            offsets, ids, vals = pad_to_capacity(offsets, ids, vals, self.ids_capacity)
+        return labels.to(self.device), offsets, ids, vals
 
-    def enable_graph(self, on: bool = True):
+    def _router(self):
+        return self.wide.router
+
+    def enable_graph(self, on: bool = True, example=None):
         """Replay each training step as ONE captured hipGraph: routing, the two
         table lookups, bags, the MFMA tower, loss, backward, the sparse SGD of
         both tables and the fused Adam of the tower (~40 kernels) in one launch.
-        Needs a GPU and the static device-resident routing (ids_capacity)."""
+        Needs a GPU and the static device-resident routing (ids_capacity).  With
+        W > 1 every rank calls this at the same point: the capture runs the
+        step's collectives (`example`: a batch of the training row count;
+        default an all-zero batch of `rows` rows)."""
         from ..utils.graphs import GraphedStep
 
         if not on:
@@ -106,23 +121,31 @@ class WideDeep:
             return
         if self.device.type != "cuda" or self.ids_capacity is None:
             raise RuntimeError("graph capture needs a GPU and static routing (ids_capacity)")
+        strict = self.world.world_size > 1
 
         def step(labels, offsets, ids, vals):
-            gs = self.global_step
-            loss = self._train_step((labels, offsets, ids, vals))
-            self.global_step = gs          # counted by train_step, not by warmup/capture
-            return loss
+            return self._train_step((labels, offsets, ids, vals))
 
         def state():   # everything a step mutates, restored after the capture's warmup
             st = [self.wide.local, self.emb.local] + [p.data for p in self.dense_params] + [self.opt.step_t]
             st += [t for t in list(self.opt.m) + list(self.opt.v) if t is not None]
-            return st
-        self._graphed = GraphedStep(step, state)
+            return st + (self.wide.router.state() if self.wide.router is not None else [])
+        self._graphed = GraphedStep(step, state, strict=strict)
+        self._example = self._static_batch(example if example is not None else self._zero_batch())
+        if strict:
+            self._graphed.capture(*self._example)
 
-    def _train_step(self, batch) -> torch.Tensor:
+    def _zero_batch(self):
+        rows, n = self.rows, self.ids_capacity
+        per = max(1, n // rows)
+        offsets = torch.clamp(torch.arange(rows + 1, dtype=torch.int64) * per, max=n)
+        offsets[-1] = n
+        return (torch.zeros(rows, 1), offsets, torch.zeros(n, dtype=torch.int64), torch.zeros(n))
+
+    def _train_step(self, batch, exact: bool = False) -> torch.Tensor:
         labels, offsets, ids, vals = batch.to(self.device) if hasattr(batch, "to") else batch
         self.flat_grad.zero_()
-        logit, (wrows, erows, lctx) = self.forward(labels, offsets, ids, vals)
+        logit, (wrows, erows, lctx) = self.forward(labels, offsets, ids, vals, exact)
         loss = ops.sigmoid_xent(logit, labels)
         loss.backward()
         ws = self.world.world_size
@@ -141,14 +164,15 @@ class WideDeep:
         apply_sgd_shared([self.wide, self.emb], lctx, grads, [self.lr / ws] * 2)
         if ev is not None:
             torch.cuda.current_stream().wait_event(ev)
-        self.opt.step(grad_scale=1.0 / ws)
-        self.global_step += 1
+        # a voided step (sharded exchange overflow on some rank) leaves the tower,
+        # its Adam slots and step count untouched: decided on the device
+        self.opt.step(grad_scale=1.0 / ws, skip=lctx.void)
         return loss.detach()
 
     @torch.no_grad()
     def predict(self, batch) -> torch.Tensor:
         labels, offsets, ids, vals = batch.to(self.device) if hasattr(batch, "to") else batch
-        logit, _ = self.forward(labels, offsets, ids, vals)
+        logit, _ = self.forward(labels, offsets, ids, vals, exact=True)
         return torch.sigmoid(logit).reshape(-1)
 
     def checkpoint_tensors(self):

@@ -139,10 +139,19 @@ class _FusedBase:
         return out
 
     @torch.no_grad()
-    def step(self, grads: Optional[List[torch.Tensor]] = None, grad_scale: float = 1.0):
+    def step(self, grads: Optional[List[torch.Tensor]] = None, grad_scale: float = 1.0,
+             skip: Optional[torch.Tensor] = None):
+        """One fused update.  `skip`: optional device int32 [1] flag; when it is set
+        (a voided step, e.g. a sharded-table exchange overflow) nothing changes --
+        no parameter, slot or step count -- decided on the device, no host sync."""
         grads = self._grads(grads)
-        self.step_t += 1
+        if skip is None:
+            self.step_t += 1
+        else:
+            self.step_t += (1 - skip.reshape(-1)[:1]).to(self.step_t.dtype)
         if self.device.type != "cuda":
+            if skip is not None and int(skip.reshape(-1)[0]) != 0:
+                return None
             return self._step_cpu(grads, grad_scale)
         gdt = {g.dtype for g in grads}
         if len(gdt) != 1 or next(iter(gdt)) not in (torch.float32, torch.bfloat16):
@@ -151,7 +160,8 @@ class _FusedBase:
         tab, chunks = self._table(grads)
         _native.load().multi_tensor_apply(tab, chunks, KINDS[self.kind], gbf, self.lr_t, 0.0,
                                           float(grad_scale), self.wd, self.b1, self.b2, self.eps,
-                                          self.momentum, self.nesterov, self.step_t)
+                                          self.momentum, self.nesterov, self.step_t,
+                                          None if skip is None else skip.reshape(-1)[:1].to(torch.int32))
 
     def _step_cpu(self, grads, gs):
         self._step_cpu_math(grads, gs)

@@ -18,8 +18,22 @@ HBM per GPU holds a 1e9 x 1 fp32 shard 8x over).  Per step:
            -> owners apply SGD with the fused scatter kernel
 
 Each row has exactly one owner, so there is no replica drift and no
-all-reduce of a dense F x D gradient.  Initial values are a counter-based
-(Philox4x32-10) normal of the *global* element index, generated on the device
+all-reduce of a dense F x D gradient.
+
+Static (capturable) routing: with an ids-per-batch bound the exchange is an
+equal-split all-to-all of `peer_cap` id slots per peer, decided on the device
+(no host read-back).  `peer_cap` is right-sized to the owners' measured
+unique-id load (a `StaticRouter` tracks the all-reduced peak per owner and
+resizes every `check_every` steps, identically on every rank), so the padded
+exchange moves ~slack x the exact bytes instead of the whole batch per peer.
+A batch whose ids overflow an owner's slots on ANY rank is VOIDED on every
+rank (the all-reduced flag zeroes the sparse gradients and skips the dense
+updates on the device), and so is every later batch of the check window; the
+check replays them in their original order through the exact exchange --
+deterministic, identical on all ranks, the same updates as a synchronous run,
+never a silent drop.
+
+Initial values are a counter-based (Philox4x32-10) normal of the *global* element index, generated on the device
 by one kernel, so a table is bit-identical for any world size.
 Checkpoints store the table as a TF partitioned variable (contiguous
 fixed_size_partitioner slices, see ckpt/__init__.py).
@@ -33,31 +47,132 @@ import torch
 from .. import ops
 from .world import World, get_world
 
+
 class LookupCtx:
     """Routing of one batch.  Dynamic: exact per-peer counts (host lists in
     send/recv), `order` sorts uniq by owner.  Static: every peer gets `cap`
-    slots (a capacity configured identically on all ranks, >= the ids of any
-    batch, so no bucket can overflow), `order` holds each unique id's slot
-    (dest, -1 for padding) and uniq / recv_local carry -1 padding -- no host
-    read-back, every shape fixed by the batch shape and the capacity."""
-    __slots__ = ("uniq", "inverse", "order", "send", "recv", "recv_local", "static", "n")
+    slots (the router's per-peer capacity, identical on all ranks), `order`
+    holds each unique id's slot (dest, -1 for padding / overflow) and uniq /
+    recv_local carry -1 padding -- no host read-back, every shape fixed by the
+    batch shape and the capacity.  `void`: device int32 [1], 1 when this step
+    overflowed on some rank (static W > 1 only)."""
+    __slots__ = ("uniq", "inverse", "order", "send", "recv", "recv_local", "static", "n", "void")
 
-    def __init__(self, uniq, inverse, order, send, recv, recv_local, static=False, n=0):
+    def __init__(self, uniq, inverse, order, send, recv, recv_local, static=False, n=0, void=None):
         self.uniq, self.inverse, self.order = uniq, inverse, order
         self.send, self.recv, self.recv_local = send, recv, recv_local
-        self.static, self.n = static, n
+        self.static, self.n, self.void = static, n, void
+
+
+class StaticRouter:
+    """Per-peer capacity and overflow bookkeeping of the static exchange, shared
+    by the tables that route the same ids (W&D's wide and deep tables).
+
+    Device state (all mutated inside captured steps, so they are part of a
+    GraphedStep's snapshot): `void` [1] int32 (this step's all-reduced
+    overflow flag), `peak` [1] int64 (all-reduced max unique ids of one owner
+    since the last check), `exact` [1] int64 (ids this rank would have sent in
+    an exact exchange since the last check), `log` [K] int32 (the void flag of
+    each step of the window), `pos` [1] int64 (step index in the window)."""
+
+    def __init__(self, world: World, device, n_cap: int, peer_cap: Optional[int] = None, slack: float = 1.1,
+                 check_every: int = 32, first_check: int = 4, align: int = 32):
+        self.world, self.W = world, world.world_size
+        self.device = torch.device(device)
+        self.n_cap = int(n_cap)
+        self.slack, self.align = float(slack), int(align)
+        self.check_every, self.first_check = int(check_every), int(first_check)
+        # start from a safe share of the batch (right-sized at the first check)
+        self.peer_cap = int(peer_cap) if peer_cap is not None else self._round(-(-self.n_cap // max(1, self.W)))
+        self.fixed = peer_cap is not None
+        self.void = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.peak = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self.exact = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self.log = torch.zeros(max(self.check_every, self.first_check), dtype=torch.int32, device=self.device)
+        self.pos = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self.steps = 0                 # host: steps since the last check
+        self.checks = self.resizes = self.voided = 0
+        self.last_ratio = None         # host: static id slots / exact ids of the last checked window
+
+    def _round(self, n: int) -> int:
+        a = self.align
+        return max(a, -(-int(n) // a) * a)
+
+    def state(self):
+        return [self.void, self.peak, self.exact, self.log, self.pos]
+
+    def record(self, ocnt: torch.Tensor, rank: int):
+        """Device-side bookkeeping of one static step (capturable): all-reduce
+        [overflow, peak] (max) so every rank voids the same steps and resizes to
+        the same capacity; log the void flag at the window position."""
+        mx = ocnt.max().to(torch.int64)
+        stat = torch.stack([(mx > self.peer_cap).to(torch.int64), mx])
+        self.world.all_reduce(stat, "max")
+        # sticky until the check: once a step is voided every later step of the
+        # window is too, so the replay applies them all in their original order
+        # (exact synchronous-SGD semantics, not a reordering)
+        torch.maximum(self.void, stat[:1].to(torch.int32), out=self.void)
+        torch.maximum(self.peak, stat[1:2], out=self.peak)
+        self.exact += ocnt.sum().to(torch.int64) - ocnt[rank].to(torch.int64)
+        self.log.index_copy_(0, self.pos % self.log.numel(), self.void)
+        self.pos += 1
+
+    def due(self) -> bool:
+        lim = self.first_check if self.checks == 0 else self.check_every
+        return self.steps >= min(lim, self.log.numel())
+
+    def check(self):
+        """Host side, every `check_every` steps (ONE sync): the window's void
+        flags (positions to replay exactly) and the all-reduced peak; resize the
+        per-peer capacity to slack x peak (identical on all ranks).  Returns
+        (voided window positions, capacity changed)."""
+        n = self.steps
+        flags = self.log[:n].cpu().tolist() if n else []
+        peak = int(self.peak.item())
+        exact = int(self.exact.item())
+        if n and exact:
+            self.last_ratio = n * (self.W - 1) * self.peer_cap / exact
+        self.log.zero_()
+        self.pos.zero_()
+        self.void.zero_()
+        self.peak.zero_()
+        self.exact.zero_()
+        self.steps = 0
+        self.checks += 1
+        voided = [i for i, f in enumerate(flags) if f]
+        self.voided += len(voided)
+        changed = False
+        if not self.fixed and peak > 0:
+            want = self._round(self.slack * peak)
+            # grow at once; shrink only when oversized by > 10 % (no resize churn)
+            if want > self.peer_cap or want < 0.9 * self.peer_cap:
+                self.peer_cap = want
+                self.resizes += 1
+                changed = True
+        return voided, changed
+
+    def wire_ratio(self) -> Optional[float]:
+        """Id slots the static exchange sent to peers per id an exact exchange
+        would have sent, over the last checked window (rows and gradients travel
+        in the same slots, so this is the byte ratio of all three all-to-alls)."""
+        return self.last_ratio
 
 
 class ShardedEmbedding:
     def __init__(self, num_rows: int, dim: int = 1, world: Optional[World] = None, init_std: float = 1.0,
                  seed: int = 0, device=None, name: str = "embedding", zero_init: bool = False,
-                 capacity: Optional[int] = None):
+                 capacity: Optional[int] = None, peer_capacity: Optional[int] = None,
+                 router: Optional[StaticRouter] = None):
         self.world = world or get_world()
         self.W = self.world.world_size
         self.rank = self.world.rank
         self.num_rows, self.dim, self.name = int(num_rows), int(dim), name
         self.capacity = capacity          # ids per batch bound (same on every rank) -> static routing
         self.device = torch.device(device) if device is not None else self.world.device
+        # the static exchange's per-peer capacity + overflow bookkeeping (shared by
+        # tables that route the same ids: pass the first table's router)
+        self.router = router if router is not None else (
+            StaticRouter(self.world, self.device, capacity, peer_capacity) if capacity is not None else None)
         n_local = (self.num_rows - self.rank + self.W - 1) // self.W if self.rank < self.num_rows else 0
         self.local = torch.empty((n_local, self.dim), dtype=torch.float32, device=self.device)
         with torch.no_grad():
@@ -69,7 +184,7 @@ class ShardedEmbedding:
                 ops.philox_normal_(self.local, self.W, self.rank, seed, 0.0, init_std)
 
     # ------------------------------------------------------------------ exchange
-    def route(self, ids: torch.Tensor, capacity: Optional[int] = None) -> LookupCtx:
+    def route(self, ids: torch.Tensor, capacity: Optional[int] = None, exact: bool = False) -> LookupCtx:
         """Dedup `ids` and send each owner the unique ids it serves (no rows yet).
 
         The context depends only on the ids and the row partition, so tables
@@ -80,9 +195,13 @@ class ShardedEmbedding:
         ids = ids.to(self.device).long()
         N = ids.numel()
         capacity = self.capacity if capacity is None else capacity
+        if exact and self.W > 1:
+            capacity = None          # the exact exchange (replays of voided steps)
         if N > 0 and (self.W == 1 or (capacity is not None and self.W <= _max_route_world())):
             if self.W > 1 and N > capacity:
                 raise ValueError(f"{self.name}: batch has {N} ids, above the routing capacity {capacity}")
+            if capacity is not None and self.W > 1 and self.router is not None and self.router.n_cap != capacity:
+                raise ValueError(f"{self.name}: routing capacity {capacity} != the router's {self.router.n_cap}")
             return self._route_static(ids, int(capacity) if capacity is not None else N)
         if ids.is_cuda and 0 < N and self.num_rows < 2 ** 31:
             # one int32 radix sort serves both the dedup and (handed over to
@@ -110,22 +229,29 @@ class ShardedEmbedding:
 
     def _route_static(self, ids: torch.Tensor, cap: int) -> LookupCtx:
         """Device-resident routing: radix sort + one dedup/bucketing kernel
-        (csrc/kernels/sparse_route.hip) + an equal-split all-to-all of `cap` id
-        slots per peer.  Nothing is read back to the host."""
+        (csrc/kernels/sparse_route.hip) + an equal-split all-to-all of the
+        router's per-peer capacity.  Nothing is read back to the host; an owner
+        overflow voids the step on every rank (StaticRouter)."""
         N, W = ids.numel(), self.W
         small = self.num_rows < 2 ** 31
         sids, perm = torch.sort(ids.to(torch.int32) if small else ids)
+        router = self.router
+        if W > 1 and router is None:
+            router = self.router = StaticRouter(self.world, self.device, cap)
+        pc = router.peer_cap if W > 1 else N
         if ids.is_cuda:
-            inv_sorted, inverse, uniq, dest, send, _count = ops._C().sparse_route(sids.contiguous(), perm, W, cap)
+            inv_sorted, inverse, uniq, dest, send, _count, ocnt = ops._C().sparse_route(sids.contiguous(), perm, W, pc)
             ops.register_sorted_ids(inverse, inv_sorted, perm)
         else:
-            inv_sorted, inverse, uniq, dest, send = _route_static_torch(sids, perm, W, cap)
+            inv_sorted, inverse, uniq, dest, send, ocnt = _route_static_torch(sids, perm, W, pc)
         if W == 1:
             return LookupCtx(uniq, inverse, None, None, None, uniq, static=True, n=N)
-        recv = torch.empty(W * cap, dtype=torch.int64, device=self.device)
-        self.world.all_to_all(send, [cap] * W, recv, [cap] * W)
+        router.record(ocnt, self.rank)
+        recv = torch.empty(W * pc, dtype=torch.int64, device=self.device)
+        self.world.all_to_all(send, [pc] * W, recv, [pc] * W)
         recv_local = torch.where(recv >= 0, recv // W, torch.full_like(recv, -1))
-        return LookupCtx(uniq, inverse, dest.long(), [cap] * W, [cap] * W, recv_local, static=True, n=cap)
+        return LookupCtx(uniq, inverse, dest.long(), [pc] * W, [pc] * W, recv_local, static=True, n=pc,
+                         void=router.void)
 
     def lookup(self, ids: torch.Tensor):
         """rows [U, D] for the unique ids of `ids`, plus the routing context."""
@@ -221,6 +347,9 @@ def apply_sgd_shared(tables, ctx: LookupCtx, grads, lrs):
     _check_shared(tables)
     t0 = tables[0]
     gs = [g.float().reshape(-1, t.dim) for t, g in zip(tables, grads)]
+    if ctx.void is not None:       # a voided step: zero gradients make the scatter-SGD a no-op on every rank
+        live = (1 - ctx.void).to(torch.float32)
+        gs = [g * live for g in gs]
     if t0.W > 1:
         g = torch.cat(gs, 1) if len(gs) > 1 else gs[0]
         if ctx.static:
@@ -258,14 +387,81 @@ def _route_static_torch(sids: torch.Tensor, perm: torch.Tensor, W: int, cap: int
     uniq[:U] = u
     dest = torch.full((N,), -1, dtype=torch.int32, device=dev)
     send = torch.full((W * cap,), -1, dtype=torch.int64, device=dev)
+    ocnt = torch.zeros(W, dtype=torch.int32, device=dev)
     if W > 1 and U:
         owner = u % W
         counts = torch.bincount(owner, minlength=W)
+        ocnt = counts.to(torch.int32)
         start = torch.cumsum(counts, 0) - counts
         order = torch.argsort(owner, stable=True)          # id order within each owner
         pos = torch.empty(U, dtype=torch.int64, device=dev)
         pos[order] = torch.arange(U, device=dev) - start[owner[order]]
+        fits = pos < cap                                    # an owner's ids beyond cap: not exchanged
         d = owner * cap + pos
-        dest[:U] = d.to(torch.int32)
-        send[d] = u
-    return inv_sorted, inverse, uniq, dest, send
+        dest[:U] = torch.where(fits, d, torch.full_like(d, -1)).to(torch.int32)
+        send[d[fits]] = u[fits]
+    return inv_sorted, inverse, uniq, dest, send, ocnt
+
+
+def pad_to_capacity(offsets: torch.Tensor, ids: torch.Tensor, vals: Optional[torch.Tensor], n_cap: int):
+    """Pad a CSR batch's ids to the static capacity so captured steps see fixed
+    shapes: the padding repeats the first id with weight 0 inside the LAST bag
+    (a 'sum' combiner is unchanged, the dedup / owner counts too, and the
+    gradient of a 0-weighted entry is 0).  Returns (offsets, ids, vals)."""
+    n = ids.numel()
+    if n > n_cap:
+        raise ValueError(f"batch has {n} ids, above the static capacity {n_cap}")
+    if vals is None:
+        vals = torch.ones(n, dtype=torch.float32, device=ids.device)
+    if n == n_cap:
+        return offsets, ids, vals
+    fill = ids[:1] if n > 0 else torch.zeros(1, dtype=ids.dtype, device=ids.device)
+    ids = torch.cat([ids, fill.expand(n_cap - n)])
+    vals = torch.cat([vals.float(), torch.zeros(n_cap - n, dtype=torch.float32, device=vals.device)])
+    offsets = offsets.clone()
+    offsets[-1] = n_cap
+    return offsets, ids, vals
+
+
+class StaticStepMixin:
+    """The training-step driver shared by the sparse models (SparseLR, W&D):
+    pads each batch to the static capacity, replays the captured graph when the
+    shapes match (otherwise runs the same collectives eagerly: partial batches,
+    CPU), and every `check_every` steps lets the router replay voided batches
+    through the exact exchange and re-capture after a resize -- on every rank
+    at the same step, so collective sequences always match.
+
+    Needs: `_router()`, `_static_batch(batch)`, `_train_step(batch, exact)`,
+    `_graphed`, `_example`, `_window`, `global_step`, `world`."""
+
+    def train_step(self, batch) -> torch.Tensor:
+        b = self._static_batch(batch)
+        g = self._graphed
+        if g is not None and (g.matches(*b) or not g.strict):   # one rank: (re)capture lazily
+            loss = g(*b)
+        else:   # eager: the same collectives as the graph (partial batches, CPU, no graph)
+            loss = self._train_step(b)
+        self.global_step += 1
+        r = self._router()
+        if r is not None and self.world.world_size > 1:
+            r.steps += 1
+            self._window.append(b)
+            if r.due():
+                self._check_exchange()
+        return loss.detach()
+
+    def sync_exchange(self):
+        """Replay the voided steps of the current window now (call before
+        evaluation / checkpointing: then every batch seen so far is applied)."""
+        r = self._router()
+        if r is not None and self.world.world_size > 1 and r.steps:
+            self._check_exchange()
+
+    def _check_exchange(self):
+        r = self._router()
+        voided, changed = r.check()
+        window, self._window = self._window, []
+        for i in voided:
+            self._train_step(window[i], exact=True)
+        if changed and self._graphed is not None and self._graphed.strict:
+            self._graphed.capture(*self._example)

@@ -19,10 +19,18 @@ import torch
 
 
 class GraphedStep:
-    def __init__(self, step_fn: Callable, state: Callable[[], Sequence[torch.Tensor]], warmup: int = 2):
+    """`strict` (multi-rank steps with collectives): the graph is captured only
+    by an explicit `capture(example)` that every rank makes at the same point
+    (the capture's warmup iterations run the step's collectives), and a call
+    whose input shapes differ from the captured ones raises instead of
+    capturing again on one rank alone."""
+
+    def __init__(self, step_fn: Callable, state: Callable[[], Sequence[torch.Tensor]], warmup: int = 2,
+                 strict: bool = False):
         self.step_fn = step_fn
         self.state = state            # -> the tensors the step mutates (snapshotted around warmup)
         self.warmup = warmup
+        self.strict = strict
         self.key = None
         self.graph = None
         self.static_in: List[torch.Tensor] = []
@@ -55,8 +63,19 @@ class GraphedStep:
         self.key = self._sig(inputs)
         self.captures += 1
 
+    def capture(self, *inputs):
+        """(Re)capture now with `inputs` as the example (state is restored after)."""
+        self._capture(inputs)
+
+    def matches(self, *inputs) -> bool:
+        return self.graph is not None and self._sig(inputs) == self.key
+
     def __call__(self, *inputs):
         if self.graph is None or self._sig(inputs) != self.key:
+            if self.strict:
+                raise RuntimeError("captured multi-rank step called with other input shapes "
+                                   f"({self._sig(inputs)} vs {self.key}): pad inputs to the static capacity; a "
+                                   "re-capture must be collective (capture() on every rank)")
             self._capture(inputs)
         with torch.no_grad():
             for s, t in zip(self.static_in, inputs):

@@ -17,6 +17,8 @@
 #   bench5500     bench.py defaults (10 epochs of 550 steps)
 #   bench2        bench.py --gpus 2 as the driver launches it, both ranks on cuda:0
 #   phases        per-phase device stamps of the fp32 engine (scripts/prof_persist_f32.py)
+#   phase_sweep   the same under each "DBG:GATHER" pair of $PHASE_SWEEP (DTF_PERSIST_DBG /
+#                 DTF_GATHER_MODE kernel knobs; default "0:3 1:3 0:0 0:1")
 #   prof_bench    rocprofv3 kernel trace + stats of bench.py --steps 5500
 #   lowering      compat-graph lowering tests + bench_graph_step
 #   models        BERT-base / ResNet-50 / sparse benches (scripts/bench_models.py)
@@ -60,6 +62,11 @@ for step in "$@"; do
       DTF_BENCH_SAME_GPU=1 run bench2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node=2 \
         --master-addr=127.0.0.1 --master-port=$PORT bench.py --gpus 2 --steps 20 --warmup 5 $extra ;;
     phases) run phases 300 python scripts/prof_persist_f32.py fp32 $extra ;;
+    phase_sweep)
+      for pair in ${PHASE_SWEEP:-0:3 1:3 0:0 0:1}; do
+        DTF_PERSIST_DBG=${pair%%:*} DTF_GATHER_MODE=${pair##*:} run phases_${pair%%:*}_${pair##*:} 300 \
+          python scripts/prof_persist_f32.py fp32 $extra
+      done ;;
     prof_bench)
       rm -rf $OUT/prof_bench
       run prof_bench 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_bench -o run -- \

@@ -73,8 +73,8 @@ def main():
         rel = lambda x: round(float(x - t0), 2)
         first_step = raw[0, :28, 0].astype(np.float64) * 0.01
         out["launch_stamps_us"] = {
-            "compute_entry_max": rel(L[:28, 0].max()), "params_loaded_max": rel(L[:28, 4].max()),
-            "census_done_max": rel(L[:28, 1].max()), "first_stage_ready_max": rel(L[:28, 2].max()),
+            "compute_entry_max": rel(L[:28, 0].max()), "param_loads_issued_max": rel(L[:28, 4].max()),
+            "census_params_stage_done_max": rel(L[:28, 1].max()), "first_x_read_max": rel(L[:28, 2].max()),
             "step0_start_max": rel(first_step.max()), "loop_done_max": rel(L[:28, 3].max()),
             "written_back_max": rel(L[:28, 5].max()), "copier_entry_max": rel(L[28:44, 0].max()),
             "copier_done_max": rel(L[28:44, 1].max())}
@@ -97,13 +97,19 @@ def main():
                                                                round(float(np.percentile(hop, 90)), 3)]
     out["logit_publish_skew_us_median"] = round(float(np.median(r[:, :, pub].max(1) - r[:, :, pub].min(1))), 3)
     if prec in ("fp32", "fp32-mfma"):
-        # extra stamps: 13 wave 7 forward done, 14 wave 7 step start, 15 wave 3 forward done
+        # extra stamps: 13 wave 7 folded the last head tile (dW2 / db / metrics), 14 wave 7 step
+        # start, 15 wave 7 saw its next-step stage land (vmcnt(0)) -- then barrier B
         med = lambda x: round(float(np.median(x)), 3)
         rs = raw[1:G, : nj * nq, :].astype(np.float64) * 0.01
-        out["barrier_A_detail_us_from_w0_step_start"] = {
-            "w0_fwd_done": med(rs[:, :, 1] - rs[:, :, 0]), "w3_fwd_done": med(rs[:, :, 15] - rs[:, :, 0]),
-            "w7_step_start": med(rs[:, :, 14] - rs[:, :, 0]), "w7_fwd_done": med(rs[:, :, 13] - rs[:, :, 0]),
-            "barrier_A_exit": med(rs[:, :, 2] - rs[:, :, 0])}
+        if int(os.environ.get("DTF_PERSIST_DBG", "0")) & 2:
+            out["head_detail_us_from_logits_summed"] = {
+                "softmax_done": med(rs[:, :, 13] - rs[:, :, 8]), "da_mfma_done": med(rs[:, :, 14] - rs[:, :, 8]),
+                "dz2_planes_rowsums_done": med(rs[:, :, 15] - rs[:, :, 8]), "head_done": med(rs[:, :, 9] - rs[:, :, 8])}
+        out["barrier_B_detail_us_from_w0_step_start"] = {
+            "w7_step_start": med(rs[:, :, 14] - rs[:, :, 0]), "w0_head_done": med(rs[:, :, 9] - rs[:, :, 0]),
+            "w7_last_head_folded": med(rs[:, :, 13] - rs[:, :, 0]),
+            "w7_stage_landed": med(rs[:, :, 15] - rs[:, :, 0]),
+            "barrier_B_exit": med(rs[:, :, 10] - rs[:, :, 0])}
     late = (r[:, :, 0] - r[:, :, 0].min(axis=1, keepdims=True)).mean(axis=0)
     out["step_start_lateness_us_by_wg"] = np.round(late, 2).tolist()
     if prec == "fp32-split7":

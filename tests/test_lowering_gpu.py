@@ -67,6 +67,7 @@ def test_lowered_sgd_steps_match_fp64(stable, act, B):
                 assert _rel(got.numpy(), want) < 1e-5
         plan = L.plan_for(g["train"])
         assert plan is not None and plan.steps == 4          # every run went through the kernels
+        assert plan._cplan.steps() == 4                      # ... as one native call + graph replay each
     tf.reset_default_graph()
 
 

@@ -95,7 +95,7 @@ def test_parse_parity_with_python_reference_parser():
         assert d.labels[i] == lab and list(d.ids[s:e]) == idx and np.allclose(d.vals[s:e], val)
 
 
-def _sharded_worker(rank, ws, port, q, files, steps, lr, kind="lr"):
+def _sharded_worker(rank, ws, port, q, files, steps, lr, kind="lr", peer_cap=None):
     try:
         sys.path.insert(0, REPO)
         os.environ.update(RANK=str(rank), WORLD_SIZE=str(ws), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
@@ -112,25 +112,33 @@ def _sharded_worker(rank, ws, port, q, files, steps, lr, kind="lr"):
             from distributed_tensorflow_example_amd.models.wide_deep import WideDeep
 
             tr = WideDeep(3000, emb_dim=8, hidden=(16,), lr=lr, dense_opt="adam", dense_lr=0.01, world=w, seed=5,
-                          ids_capacity=cap)
+                          ids_capacity=cap, rows=200 // ws, peer_capacity=peer_cap)
+            router = tr.wide.router
             tr.W = tr.emb
             tr.b = tr.layers[0]
         else:
-            tr = sparse_lr.SparseLRTrainer(3000, lr, w, seed=5, ids_capacity=cap)
+            tr = sparse_lr.SparseLRTrainer(3000, lr, w, seed=5, ids_capacity=cap, rows=200 // ws,
+                                           peer_capacity=peer_cap)
+            router = tr.W.router
         init_tab = tr.W.full_table().numpy().copy()
         B = 200
         for s in range(steps):
             rows = np.arange(s * B, (s + 1) * B)
             mine = rows[rank * B // ws:(rank + 1) * B // ws]
             tr.train_step(data.take(mine))
+        stats = None
+        if router is not None and ws > 1:
+            tr.sync_exchange()                     # flush the last window (replays voided steps)
+            stats = dict(peer_cap=router.peer_cap, checks=router.checks, resizes=router.resizes,
+                         voided=router.voided, gstep=tr.global_step)
         final = tr.W.full_table().numpy().copy()
         if kind.startswith("wd"):
-            q.put((rank, init_tab, final, tr.b.detach().numpy().copy(), tr.wide.full_table().numpy().copy()))
+            q.put((rank, init_tab, final, tr.b.detach().numpy().copy(), tr.wide.full_table().numpy().copy(), stats))
             return
         local, repl = tr.checkpoint_tensors()
         prefix = ckpt.save_sharded(os.path.join(os.path.dirname(files[0]), f"ck{ws}", "lr"), local, repl, w,
                                    global_step=tr.global_step)
-        q.put((rank, init_tab, final, float(tr.b.detach()[0]), prefix))
+        q.put((rank, init_tab, final, float(tr.b.detach()[0]), prefix, stats))
     except Exception:
         import traceback
 
@@ -259,3 +267,90 @@ def test_static_routing_matches_dynamic(svm_dir):
         for a, b in zip(dyn, sta):
             assert np.array_equal(a[1], b[1])                    # same init
             assert np.allclose(a[2], b[2], atol=1e-6)            # same trained table
+
+
+@pytest.mark.parametrize("ws", [4, 8])
+@pytest.mark.parametrize("kind", ["lr", "wd"])
+def test_static_routing_four_eight_ranks_equal_one(svm_dir, ws, kind):
+    """Right-sized static exchange at W = 4 and 8 (the per-peer capacity starts
+    at N / W and is resized to slack x the all-reduced peak after the first
+    check): sync SGD over the sharded tables equals one rank on the whole batch."""
+    d, tr, te = svm_dir
+    one = _run(1, tr, 8, 0.5, kind)
+    many = _run(ws, tr, 8, 0.5, kind + "-static")
+    for r in range(1, ws):
+        assert np.array_equal(many[0][2], many[r][2])
+    assert np.allclose(one[0][2], many[0][2], atol=1e-5)
+    st = many[0][5]
+    # (a right-sized capacity may be outgrown later: such steps and the rest of
+    # their window are voided and replayed in order -- still equal to one rank)
+    assert st["resizes"] >= 1 and st["peer_cap"] < 200 * 64 // ws, st
+
+
+@pytest.mark.parametrize("kind", ["lr", "wd"])
+def test_overflowing_steps_are_voided_and_replayed_exactly(svm_dir, kind):
+    """A per-peer capacity far below the owners' load (fixed at 1 slot): every
+    step overflows on some rank, is voided on ALL ranks (no table, bias, tower
+    or Adam-slot change) and replayed through the exact exchange at the next
+    check in order -- the result equals one rank on the whole batch."""
+    d, tr, te = svm_dir
+    one = _run(1, tr, 6, 0.5, kind)
+    four = _run(4, tr, 6, 0.5, kind + "-static", 1)
+    for r in range(1, 4):
+        assert np.array_equal(four[0][2], four[r][2])
+    st = four[0][5]
+    assert st["voided"] == 6 and st["gstep"] == 6, st
+    assert np.allclose(one[0][2], four[0][2], atol=1e-5)
+    if kind == "wd":   # the Adam tower replayed too
+        assert np.allclose(one[0][3], four[0][3], atol=1e-5)
+    else:
+        assert abs(one[0][3] - four[0][3]) < 1e-6
+
+
+def _zipf_worker(rank, ws, port, q, steps):
+    try:
+        sys.path.insert(0, REPO)
+        os.environ.update(RANK=str(rank), WORLD_SIZE=str(ws), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                          MASTER_PORT=str(port))
+        import torch
+
+        from distributed_tensorflow_example_amd.models import sparse_lr
+        from distributed_tensorflow_example_amd.parallel import world as W
+
+        w = W.init(backend="gloo")
+        B, nnz, F = 512, 32, 100_000_000          # scripts/bench_models.py's id law (Zipf 1.1), smaller batch
+        tr = sparse_lr.SparseLRTrainer(F // 1000, 0.1, w, seed=5, ids_capacity=B * nnz, rows=B)
+        rng = np.random.default_rng(1234 + rank)
+        for _ in range(steps):
+            ids = torch.from_numpy(((rng.zipf(1.1, B * nnz) - 1) % (F // 1000)).astype(np.int64))
+            offs = torch.arange(0, B * nnz + 1, nnz, dtype=torch.int64)
+            lab = torch.from_numpy((rng.random((B, 1)) < 0.3).astype(np.float32))
+            tr.train_step((lab, offs, ids, torch.ones(B * nnz)))
+        r = tr.W.router
+        q.put((rank, r.wire_ratio(), r.peer_cap, r.voided, r.resizes))
+    except Exception:
+        import traceback
+
+        q.put((rank, traceback.format_exc(), None, None, None))
+
+
+def test_static_exchange_wire_bytes_near_exact_at_w8():
+    """W = 8 with the bench's Zipf ids: after the first resize the padded
+    all-to-all sends <= 1.5x the ids (and so rows / gradients) of an exact
+    exchange (the round-2 layout padded every peer to the whole
+    batch: ~W x)."""
+    ws, steps = 8, 4 + 32 + 32
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_zipf_worker, args=(r, ws, port, q, steps)) for r in range(ws)]
+    [p.start() for p in ps]
+    out = sorted([q.get(timeout=300) for _ in range(ws)], key=lambda r: r[0])
+    [p.join(60) for p in ps]
+    for r in out:
+        assert not isinstance(r[1], str), r[1]
+    for rank, ratio, pc, voided, resizes in out:
+        # an early capacity (4 batches' peak) may be outgrown once or twice:
+        # those steps are voided and replayed exactly, then the capacity grows
+        assert resizes >= 1 and voided <= 3, (rank, voided, resizes)
+        assert ratio is not None and ratio <= 1.5, (rank, ratio, pc)

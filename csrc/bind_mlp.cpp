@@ -581,8 +581,10 @@ void graph_mlp_step(at::Tensor x, at::Tensor ylab, at::Tensor W1, at::Tensor b1,
 class GraphStepPlan {
  public:
   GraphStepPlan(at::Tensor W1, at::Tensor b1, at::Tensor W2, at::Tensor b2, c10::optional<at::Tensor> gstep, int B,
-                int act, bool naive)
-      : W1_(W1), b1_(b1), W2_(W2), b2_(b2), B_(B), act_(act), naive_(naive) {
+                int act, bool naive, bool use_graph)
+      : W1_(W1), b1_(b1), W2_(W2), b2_(b2), B_(B), act_(act), naive_(naive), use_graph_(use_graph) {
+    const char* df = getenv("DTF_GRAPH_STEP_DIRECT_FEED");
+    direct_feed_ = df != nullptr && df[0] == '1';
     for (const at::Tensor* t : {&W1, &b1, &W2, &b2})
       TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous(),
                   "GraphStepPlan: fp32 contiguous device parameters expected");
@@ -636,10 +638,35 @@ class GraphStepPlan {
     TORCH_CHECK(x.size() == nx && y.size() == ny, "GraphStepPlan.run: feed shapes differ from the plan's");
     const float* xp = static_cast<const float*>(x.data());
     const float* yp = static_cast<const float*>(y.data());
-    hipStream_t cur = cur_stream(), st = st_;
+    hipStream_t cur = cur_stream(), st = use_graph_ ? st_ : cur;
     const int slot = slot_ ^= 1;
     {
       py::gil_scoped_release nogil;
+      if (!use_graph_) {   // direct launches on the caller's stream: no cross-stream events, no replay floor
+        hip_check(hipEventSynchronize(ev_[slot]), "GraphStepPlan: staging slot");
+        float* h = stage_[slot].data_ptr<float>();
+        float* d = dev_.data_ptr<float>();
+        if (direct_feed_) {
+          // x / y_ straight from the caller's memory (zero-copy DMA when it is
+          // pinned; HIP's own pipelined staging when pageable); lr via the slot
+          h[nx + ny] = (float)lr;
+          hip_check(hipMemcpyAsync(d, xp, sizeof(float) * nx, hipMemcpyHostToDevice, st), "GraphStepPlan: x copy");
+          hip_check(hipMemcpyAsync(d + nx, yp, sizeof(float) * ny, hipMemcpyHostToDevice, st), "GraphStepPlan: y copy");
+          hip_check(hipMemcpyAsync(d + nx + ny, h + nx + ny, sizeof(float), hipMemcpyHostToDevice, st),
+                    "GraphStepPlan: lr copy");
+        } else {
+          std::memcpy(h, xp, sizeof(float) * nx);
+          std::memcpy(h + nx, yp, sizeof(float) * ny);
+          h[nx + ny] = (float)lr;
+          hip_check(hipMemcpyAsync(d, h, sizeof(float) * (nx + ny + 1), hipMemcpyHostToDevice, st),
+                    "GraphStepPlan: feed copy");
+        }
+        hip_check(hipEventRecord(ev_[slot], st), "GraphStepPlan: event");
+        launch_step(st);
+        if (sync) hip_check(hipStreamSynchronize(st), "GraphStepPlan: sync");
+        ++steps_;
+        return;
+      }
       hip_check(hipEventSynchronize(ev_[slot]), "GraphStepPlan: staging slot");   // its last copy is done
       float* h = stage_[slot].data_ptr<float>();
       std::memcpy(h, xp, sizeof(float) * nx);
@@ -663,14 +690,13 @@ class GraphStepPlan {
     ++steps_;
   }
   int64_t steps() const { return steps_; }
+  bool use_graph() const { return use_graph_; }
 
  private:
-  void capture(hipStream_t st) {
-    if (exec_) { (void)hipGraphExecDestroy(exec_); exec_ = nullptr; }
-    if (graph_) { (void)hipGraphDestroy(graph_); graph_ = nullptr; }
+  // the step's three kernels + the metrics copy back, on stream st
+  hipError_t launch_step(hipStream_t st) {
     const int64_t nx = (int64_t)B_ * K_, ny = (int64_t)B_ * C_;
     float* d = dev_.data_ptr<float>();
-    hip_check(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal), "GraphStepPlan: begin capture");
     hipError_t e = dtfk_graph_mlp_step(d, d + nx, W1_.data_ptr<float>(), b1_.data_ptr<float>(), W2_.data_ptr<float>(),
                                        b2_.data_ptr<float>(), a2_.data_ptr<float>(), dz2_.data_ptr<float>(),
                                        part_.data_ptr<float>(), nullptr, nullptr, nullptr, nullptr,
@@ -679,6 +705,14 @@ class GraphStepPlan {
     if (e == hipSuccess)
       e = hipMemcpyAsync(host_metrics_.data_ptr<float>(), metrics_.data_ptr<float>(), 3 * sizeof(float),
                          hipMemcpyDeviceToHost, st);
+    return e;
+  }
+
+  void capture(hipStream_t st) {
+    if (exec_) { (void)hipGraphExecDestroy(exec_); exec_ = nullptr; }
+    if (graph_) { (void)hipGraphDestroy(graph_); graph_ = nullptr; }
+    hip_check(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal), "GraphStepPlan: begin capture");
+    const hipError_t e = launch_step(st);
     hipGraph_t g = nullptr;
     const hipError_t e2 = hipStreamEndCapture(st, &g);
     hip_check(e, "GraphStepPlan: captured launches");
@@ -695,15 +729,16 @@ class GraphStepPlan {
   hipGraphExec_t exec_ = nullptr;
   hipStream_t st_ = nullptr;
   int B_, K_ = 0, H_ = 0, C_ = 0, HP_ = 0, act_, gkind_ = 0, slot_ = 0;
-  bool naive_;
+  bool naive_, use_graph_, direct_feed_ = false;
   int64_t nfeed_ = 0, steps_ = 0;
 };
 
 void init_mlp(py::module& m) {
   py::class_<GraphStepPlan>(m, "GraphStepPlan")
-      .def(py::init<at::Tensor, at::Tensor, at::Tensor, at::Tensor, c10::optional<at::Tensor>, int, int, bool>(),
+      .def(py::init<at::Tensor, at::Tensor, at::Tensor, at::Tensor, c10::optional<at::Tensor>, int, int, bool, bool>(),
            py::arg("W1"), py::arg("b1"), py::arg("W2"), py::arg("b2"), py::arg("gstep"), py::arg("B"), py::arg("act"),
-           py::arg("naive"))
+           py::arg("naive"), py::arg("use_graph") = false)
+      .def("use_graph", &GraphStepPlan::use_graph)
       .def("run", &GraphStepPlan::run, py::arg("x"), py::arg("y"), py::arg("lr"), py::arg("sync"))
       .def("host_metrics", &GraphStepPlan::host_metrics)
       .def("steps", &GraphStepPlan::steps);

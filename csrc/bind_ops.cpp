@@ -12,6 +12,10 @@ hipError_t dtfk_hogwild_pull(const float* shared, float* local, long long n, hip
 hipError_t dtfk_hogwild_sgd(float* shared, const float* g, float* local, float lr, long long n, int locking,
                             unsigned long long* counter, long long* gstep_out, hipStream_t s);
 hipError_t dtfk_hogwild_counter(unsigned long long* counter, long long* out, long long set, int do_set, hipStream_t s);
+hipError_t dtfk_hogwild_gather_rows(const long long* ids, int n, int D, const float* const* shards, int W, float* out,
+                                   hipStream_t s);
+hipError_t dtfk_hogwild_scatter_sgd(const long long* ids, const float* g, int n, int D, float* const* shards, int W,
+                                    float lr, int locking, hipStream_t s);
 hipError_t dtfk_bucket_pack_bf16(const float* g, uint16_t* c, int64_t n, float scale, hipStream_t s);
 hipError_t dtfk_bucket_unpack_bf16(const uint16_t* c, float* g, int64_t n, float scale, hipStream_t s);
 int dtfk_route_max_world();
@@ -406,7 +410,28 @@ static void hogwild_counter(int64_t counter, at::Tensor out, int64_t set, bool d
      "hogwild_counter");
 }
 
+// rows of IPC-mapped table shards (`shards`: device table of W shard addresses)
+static void hogwild_gather_rows(at::Tensor ids, int64_t shards, int W, at::Tensor out) {
+  i64c(ids, "ids"); f32c(out, "out");
+  if (out.dim() != 2 || out.size(0) != ids.numel()) throw std::runtime_error("hogwild_gather_rows: out [n, D]");
+  ck(dtfk_hogwild_gather_rows(reinterpret_cast<const long long*>(ids.data_ptr<int64_t>()), (int)ids.numel(),
+                              (int)out.size(1), reinterpret_cast<const float* const*>(shards), W,
+                              out.data_ptr<float>(), cs()),
+     "hogwild_gather_rows");
+}
+static void hogwild_scatter_sgd(at::Tensor ids, at::Tensor grads, int64_t shards, int W, double lr, bool locking) {
+  i64c(ids, "ids"); f32c(grads, "grads");
+  if (grads.dim() != 2 || grads.size(0) != ids.numel()) throw std::runtime_error("hogwild_scatter_sgd: grads [n, D]");
+  ck(dtfk_hogwild_scatter_sgd(reinterpret_cast<const long long*>(ids.data_ptr<int64_t>()),
+                              grads.data_ptr<float>(), (int)ids.numel(), (int)grads.size(1),
+                              reinterpret_cast<float* const*>(shards), W, (float)lr, locking ? 1 : 0, cs()),
+     "hogwild_scatter_sgd");
+}
+
 void init_ops(py::module& m) {
+  m.def("hogwild_gather_rows", &hogwild_gather_rows, py::arg("ids"), py::arg("shards"), py::arg("W"), py::arg("out"));
+  m.def("hogwild_scatter_sgd", &hogwild_scatter_sgd, py::arg("ids"), py::arg("grads"), py::arg("shards"), py::arg("W"),
+        py::arg("lr"), py::arg("locking"));
   m.def("hogwild_pull", &hogwild_pull, py::arg("shared"), py::arg("local"));
   m.def("hogwild_sgd", &hogwild_sgd, py::arg("shared"), py::arg("grads"), py::arg("local"), py::arg("lr"),
         py::arg("locking"), py::arg("counter"), py::arg("gstep_out"));

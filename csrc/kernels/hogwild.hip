@@ -66,6 +66,50 @@ __global__ void write_counter(unsigned long long* counter, long long v) {
   __hip_atomic_store(counter, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Row-sharded tables (partitioned variables, lr2.py's ps-held W[F, 1]) under the
+// asynchronous rule: every rank's shard is IPC-mapped into every rank (row r on
+// rank r % W at local row r / W, parallel/sharded_embedding.py); a worker reads
+// its batch's unique rows straight from their owners and applies its scatter
+// SGD into them, without waiting for anyone (TF's ScatterSub on the ps).
+__global__ __launch_bounds__(256) void gather_rows(const long long* __restrict__ ids, int n, int D,
+                                                   const float* const* __restrict__ shards, int W,
+                                                   float* __restrict__ out) {
+  const long long total = (long long)n * D;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const long long u = i / D;
+    const int d = (int)(i - u * D);
+    const long long id = ids[u];
+    const float* sh = shards[(int)(id % W)];
+    out[i] = ld_sys_f32(sh + (id / W) * D + d);
+  }
+}
+
+__global__ __launch_bounds__(256) void scatter_sgd(const long long* __restrict__ ids, const float* __restrict__ g,
+                                                   int n, int D, float* const* __restrict__ shards, int W, float lr,
+                                                   int locking) {
+  const long long total = (long long)n * D;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const long long u = i / D;
+    const int d = (int)(i - u * D);
+    const long long id = ids[u];
+    float* p = shards[(int)(id % W)] + (id / W) * D + d;
+    const float dv = lr * g[i];
+    if (locking) {
+      uint32_t* q = reinterpret_cast<uint32_t*>(p);
+      uint32_t old = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      for (;;) {
+        uint32_t want = old;
+        if (__hip_atomic_compare_exchange_strong(q, &want, __float_as_uint(__uint_as_float(old) - dv),
+                                                 __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))
+          break;
+        old = want;
+      }
+    } else {
+      st_sys_f32(p, ld_sys_f32(p) - dv);    // Hogwild: a concurrent update of the same row may be lost
+    }
+  }
+}
+
 inline int grid_for(long long n) {
   const long long b = (n + 255) / 256;
   return (int)(b < 1024 ? (b < 1 ? 1 : b) : 1024);
@@ -86,6 +130,23 @@ hipError_t dtfk_hogwild_sgd(float* shared, const float* g, float* local, float l
                             unsigned long long* counter, long long* gstep_out, hipStream_t s) {
   using namespace dtfk::hogwild;
   hipLaunchKernelGGL(sgd, dim3(grid_for(n)), dim3(256), 0, s, shared, g, local, lr, n, locking, counter, gstep_out);
+  return hipGetLastError();
+}
+
+hipError_t dtfk_hogwild_gather_rows(const long long* ids, int n, int D, const float* const* shards, int W, float* out,
+                                   hipStream_t s) {
+  using namespace dtfk::hogwild;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(gather_rows, dim3(grid_for((long long)n * D)), dim3(256), 0, s, ids, n, D, shards, W, out);
+  return hipGetLastError();
+}
+
+hipError_t dtfk_hogwild_scatter_sgd(const long long* ids, const float* g, int n, int D, float* const* shards, int W,
+                                    float lr, int locking, hipStream_t s) {
+  using namespace dtfk::hogwild;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(scatter_sgd, dim3(grid_for((long long)n * D)), dim3(256), 0, s, ids, g, n, D, shards, W, lr,
+                     locking);
   return hipGetLastError();
 }
 

@@ -352,8 +352,11 @@ class MLPStepPlan:
         key = (B, K, W1.data_ptr(), b1.data_ptr(), W2.data_ptr(), b2.data_ptr(),
                None if gstep is None else gstep.data_ptr(), pat.act, pat.naive)
         if getattr(self, "_cplan_key", None) != key:
+            # direct launches by default (measured: a hipGraph replay's fixed host cost
+            # exceeds three direct launches here); DTF_GRAPH_STEP_HIPGRAPH=1 replays one
             self._cplan = _native.load().GraphStepPlan(W1.data, b1.data, W2.data, b2.data, gstep, B, pat.act,
-                                                       bool(pat.naive))
+                                                       bool(pat.naive),
+                                                       os.environ.get("DTF_GRAPH_STEP_HIPGRAPH", "0") == "1")
             self._cplan_key = key
         opt._steps += 1
         _debug.fault_point(opt._steps, w.rank)

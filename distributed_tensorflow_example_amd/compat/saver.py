@@ -316,10 +316,15 @@ class Saver:
         step = global_step
         if step is not None and not isinstance(step, (int, np.integer)):
             step = int(np.asarray(sess.run(step) if hasattr(step, "_eval") else step))
-        prefix = f"{save_path}-{int(step)}" if step is not None else save_path
         w = get_world()
         vars_ = self._vars()
         parts = {k: v for k, v in vars_.items() if getattr(v, "is_partitioned", False)}
+        if parts and w.world_size > 1 and step is not None:
+            # a sharded save is collective: every rank must write the same prefix.
+            # Asynchronous workers' global_step copies differ (each saw the shared
+            # counter at its own last update): use the latest of them
+            step = int(w.host_all_reduce(float(step), "max"))
+        prefix = f"{save_path}-{int(step)}" if step is not None else save_path
         tensors = {k: self._value(v) for k, v in vars_.items() if k not in parts}
         if parts:
             # TF layout: full-name entry + one slice entry per fixed_size partition;

@@ -405,26 +405,50 @@ class Optimizer:
 
     def _apply_async(self, vars_, gtens, params, sparse_pairs, global_step, name) -> Operation:
         """The reference's asynchronous update (example.py:106-118 without
-        SyncReplicasOptimizer): pull the ps variables, gradient of this worker's
-        batch, `var -= lr * grad` on the ps variables with no waiting, global_step
-        = every worker's updates so far (parallel/async_ps.py)."""
-        if self._kind != "sgd" or sparse_pairs:
-            raise NotImplementedError("asynchronous (Hogwild) updates: GradientDescentOptimizer on dense "
-                                      "variables only (update_mode='sync' handles the rest)")
+        SyncReplicasOptimizer; lr2.py:359-396's ps-held W trained by ScatterSub):
+        pull the dense ps variables, gradient of this worker's batch, `var -= lr
+        * grad` on the ps variables with no waiting; partitioned variables read
+        their rows from -- and scatter their sparse updates into -- the owners'
+        shared shards (HogwildTable); global_step = every worker's updates so
+        far (parallel/async_ps.py)."""
+        if self._kind != "sgd":
+            raise NotImplementedError("asynchronous (Hogwild) updates: GradientDescentOptimizer only "
+                                      "(update_mode='sync' handles the other optimizers)")
         opt = self
         state = {}
+
+        def ensure():
+            # collective: every worker's first train run, before its first forward
+            # (the partitioned variables' lookups must already read the shared shards)
+            if "store" in state:
+                return
+            w = _world_or_local()
+            dense = params if params else [torch.zeros(1, device=sparse_pairs[0][1].table.device)]
+            state["store"] = _async_ps.HogwildStore(dense, w, use_locking=opt.use_locking)
+            for _, pv in sparse_pairs:
+                if pv.table.hogwild is None:
+                    pv.table.hogwild = _async_ps.HogwildTable(pv.table, w, use_locking=opt.use_locking)
+
+        def pre_run():
+            ensure()
+            state["store"].pull()
 
         def run(ctx):
             w = _world_or_local()
             opt._steps += 1
             _debug.fault_point(opt._steps, w.rank)
-            if "store" not in state:      # collective: every worker's first train step
-                state["store"] = _async_ps.HogwildStore(params, w, use_locking=opt.use_locking)
+            ensure()
             store = state["store"]
+            lr = opt._lr_value()
             with _prof.range("compute_gradients"):
                 gs = [ctx.eval(g) if g is not None else None for g in gtens]
+                sgs = [(pv, ctx.eval(g)) for g, pv in sparse_pairs]
             with _prof.range("hogwild_update"):
-                gstep = store.sgd_step(gs, opt._lr_value())
+                for pv, looks in sgs:       # owner-side scatter SGD into the shared shards, no waiting
+                    for lctx, rows_grad in looks:
+                        if rows_grad is not None:
+                            pv.table.apply_sgd(lctx, rows_grad, lr)
+                gstep = store.sgd_step(gs if params else [None], lr)
             if global_step is not None:
                 with torch.no_grad():
                     global_step.value.data.fill_(float(gstep))
@@ -434,7 +458,7 @@ class Optimizer:
         op._async_state = state
         # Session.run calls this before evaluating anything: the forward of this
         # run reads the ps variables as they are now (other workers' updates included)
-        op._pre_run = lambda: state["store"].pull() if "store" in state else None
+        op._pre_run = pre_run
         return op
 
     def minimize(self, loss, global_step=None, var_list=None, name=None, **kw) -> Operation:

@@ -31,7 +31,8 @@ from ..parallel.world import World, get_world
 class SparseLRTrainer(StaticStepMixin):
     def __init__(self, num_features: int, lr: float, world: Optional[World] = None, seed: int = 1,
                  init_std: float = 1.0, device=None, auc_bins: int = 200, ids_capacity: Optional[int] = None,
-                 rows: int = 500, peer_capacity: Optional[int] = None):
+                 rows: int = 500, peer_capacity: Optional[int] = None, update_mode: Optional[str] = None,
+                 use_locking: bool = False):
         self.world = world or get_world()
         self.device = torch.device(device) if device is not None else self.world.device
         self.lr = float(lr)
@@ -46,12 +47,26 @@ class SparseLRTrainer(StaticStepMixin):
         # streaming_auc's num_thresholds = auc_bins -> auc_bins + 1 histogram bins
         self.auc_pos = torch.zeros(auc_bins + 1, dtype=torch.int64, device=self.device)
         self.auc_neg = torch.zeros(auc_bins + 1, dtype=torch.int64, device=self.device)
+        # 'async': the reference's rule (lr2.py:359-396, plain GradientDescentOptimizer
+        # under replica_device_setter): every worker reads W's rows from -- and
+        # scatters its update into -- the owners' shared shards, b lives in a shared
+        # Hogwild store, global_step counts every worker's update; no collective
+        from ..parallel import async_ps
+        self.update_mode = async_ps.update_mode(update_mode)
+        self._bstore = None
+        if self.update_mode == "async" and self.world.world_size > 1:
+            self.W.hogwild = async_ps.HogwildTable(self.W, self.world, use_locking=use_locking)
+            self._bstore = async_ps.HogwildStore([self.b.data], self.world, use_locking=use_locking)
 
     # ----------------------------------------------------------------- steps
     def _forward(self, batch, exact: bool = False):
         labels, offsets, ids, vals = batch.to(self.device) if hasattr(batch, "to") else batch
-        ctx = self.W.route(ids, exact=exact)
-        rows = lookup_shared([self.W], ctx)[0].detach().requires_grad_(True)
+        if self.W.hogwild is not None:      # asynchronous: the owners' shared shards, no collective
+            rows, ctx = self.W.lookup(ids)
+        else:
+            ctx = self.W.route(ids, exact=exact)
+            rows = lookup_shared([self.W], ctx)[0]
+        rows = rows.detach().requires_grad_(True)
         out = ops.embedding_bag(rows, ctx.inverse, offsets.to(self.device).long(),
                                 None if vals is None else vals.to(self.device).float(), "sum")
         return out + self.b, labels, (rows, ctx)
@@ -67,6 +82,31 @@ class SparseLRTrainer(StaticStepMixin):
 
     def _router(self):
         return self.W.router
+
+    def train_step(self, batch) -> torch.Tensor:
+        if self._bstore is not None:
+            return self._train_step_async(batch)
+        return StaticStepMixin.train_step(self, batch)
+
+    def _train_step_async(self, batch) -> torch.Tensor:
+        """One Hogwild step: pull b, rows straight from their owners, scatter-SGD
+        into the owners' shards and `b -= lr g` in the shared store, no waiting."""
+        self._bstore.pull()
+        logits, labels, (rows, ctx) = self._forward(batch)
+        loss = ops.sigmoid_xent(logits, labels)
+        if self.b.grad is not None:
+            self.b.grad = None
+        loss.backward()
+        g = rows.grad if rows.grad is not None else torch.zeros_like(rows)
+        self.W.apply_sgd(ctx, g, self.lr)
+        self.global_step = self._bstore.sgd_step([self.b.grad], self.lr)
+        return loss.detach()
+
+    def refresh_global_step(self) -> int:
+        """Asynchronous mode: the shared step counter now (every worker's updates)."""
+        if self._bstore is not None:
+            self.global_step = self._bstore.global_step()
+        return self.global_step
 
     def enable_graph(self, on: bool = True, example=None):
         """Replay each step as one captured hipGraph (GPU; needs the static

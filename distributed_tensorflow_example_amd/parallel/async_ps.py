@@ -25,6 +25,14 @@ MI355X-first layout -- no parameter-server process on the data path:
   advisory file lock when `use_locking=True`, racy otherwise.
 * world_size 1: the local parameters are the store.
 
+Partitioned (row-sharded) variables -- lr2.py's ps-held `W[F, 1]` trained by
+`embedding_lookup_sparse` + ScatterSub on the ps -- use `HogwildTable`: every
+rank's shard (row r on rank r % W at local row r // W) is mapped into every
+rank (GPU: IPC peer buffers, csrc/kernels/hogwild.hip row gather / scatter-SGD
+over xGMI; CPU: one /dev/shm file per shard), so a worker reads its batch's
+unique rows straight from their owners and applies its sparse update into
+them without waiting for any other worker -- no collective on the step.
+
 The ps tasks stay control-plane members (done tokens, `server.join()`), as in
 the synchronous mode.
 """
@@ -215,3 +223,136 @@ class HogwildStore:
             self._mm = None
             self._lockf.close()
             self._shm = None
+
+
+class HogwildTable:
+    """A row-sharded table (parallel/sharded_embedding.ShardedEmbedding) shared
+    for asynchronous sparse SGD.  Collective to construct; `lookup` /
+    `scatter_sgd` are rank-local and never wait for another rank.  The table's
+    own shard (`table.local`) is re-homed into the shared mapping, so
+    checkpoints, `full_table()` and evaluation keep seeing the live values."""
+
+    def __init__(self, table, world, use_locking: bool = False):
+        self.table = table
+        self.world = world
+        self.W = world.world_size if world is not None else 1
+        self.rank = world.rank if world is not None else 0
+        self.locking = bool(use_locking)
+        self.D = table.dim
+        self.device = table.device
+        self.kind = "local"
+        self._ipc = None
+        self._maps = []
+        if self.W > 1 and self.device.type == "cuda":
+            self._open_ipc()
+        elif self.W > 1:
+            self._open_shm()
+        if self.W > 1:
+            world.barrier()
+
+    def _rows_of(self, r: int) -> int:
+        F = self.table.num_rows
+        return (F - r + self.W - 1) // self.W if r < F else 0
+
+    def _open_ipc(self):
+        from .. import _native
+        from .world import open_peer_buffers
+
+        C = _native.load()
+        n_max = (self.table.num_rows + self.W - 1) // self.W
+        self._ipc = open_peer_buffers(C, 4 * max(1, n_max * self.D), self.world)
+        own = self._ipc.tensor(0, self._rows_of(self.rank) * self.D, 0).view(-1, self.D)
+        with torch.no_grad():
+            own.copy_(self.table.local)
+        self.table.local = own
+        self._C = C
+        self._shards = int(self._ipc.table_ptr())
+        torch.cuda.synchronize(self.device)
+        self.kind = "ipc"
+
+    def _open_shm(self):
+        n = self._rows_of(self.rank) * self.D
+        fd, path = tempfile.mkstemp(prefix=f"dtf_hogtab_{self.rank}_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
+        os.ftruncate(fd, 4 * max(1, n))
+        os.close(fd)
+        paths = self.world.all_gather_object(path)
+        self._files, self._shards_t = [], []
+        for r, pth in enumerate(paths):
+            f = open(pth, "r+b")
+            nr = self._rows_of(r) * self.D
+            mm = mmap.mmap(f.fileno(), 4 * max(1, nr))
+            self._files.append(f)
+            self._maps.append(mm)
+            self._shards_t.append(torch.from_numpy(np.frombuffer(mm, dtype=np.float32, count=nr)).view(-1, self.D))
+        with torch.no_grad():
+            self._shards_t[self.rank].copy_(self.table.local)
+        self.table.local = self._shards_t[self.rank]
+        self.world.barrier()           # every rank mapped every shard: the names can go
+        os.unlink(path)
+        self.kind = "shm"
+
+    def lookup(self, ids: torch.Tensor):
+        """(rows [U, D] as the owners hold them now, inverse, unique ids)."""
+        ids = ids.to(self.device).long()
+        uniq, inverse = torch.unique(ids, return_inverse=True)
+        if self.kind == "ipc":
+            rows = torch.empty((uniq.numel(), self.D), dtype=torch.float32, device=self.device)
+            self._C.hogwild_gather_rows(uniq.contiguous(), self._shards, self.W, rows)
+        elif self.kind == "shm":
+            rows = torch.empty((uniq.numel(), self.D), dtype=torch.float32)
+            owner, local = uniq % self.W, uniq // self.W
+            for r in range(self.W):
+                m = owner == r
+                if bool(m.any()):
+                    rows[m] = self._shards_t[r].index_select(0, local[m])
+        else:
+            rows = self.table.local.index_select(0, uniq)
+        return rows, inverse, uniq
+
+    def scatter_sgd(self, uniq: torch.Tensor, grads: torch.Tensor, lr: float):
+        """rows[uniq] -= lr * grads on their owners' shards, no waiting (use_locking:
+        per-element CAS on GPU, an advisory lock per shard file on CPU)."""
+        g = grads.float().reshape(-1, self.D).contiguous()
+        if uniq.numel() == 0:
+            return
+        with torch.no_grad():
+            if self.kind == "ipc":
+                self._C.hogwild_scatter_sgd(uniq.contiguous(), g, self._shards, self.W, float(lr), self.locking)
+            elif self.kind == "shm":
+                owner, local = uniq % self.W, uniq // self.W
+                for r in range(self.W):
+                    m = owner == r
+                    if not bool(m.any()):
+                        continue
+                    if self.locking:
+                        fcntl.lockf(self._files[r], fcntl.LOCK_EX)
+                    try:
+                        self._shards_t[r].index_add_(0, local[m], g[m], alpha=-float(lr))
+                    finally:
+                        if self.locking:
+                            fcntl.lockf(self._files[r], fcntl.LOCK_UN)
+            else:
+                self.table.local.index_add_(0, uniq, g, alpha=-float(lr))
+
+    def close(self):
+        """Give the table a private copy of its shard again and unmap the others."""
+        if self.kind == "local":
+            return
+        with torch.no_grad():
+            own = self.table.local.clone()
+        if self.kind == "ipc":
+            torch.cuda.synchronize(self.device)
+            self.world.barrier()        # nobody still reads / writes a peer shard
+            self.table.local = own
+            self._ipc.close()
+            self._ipc = None
+        else:
+            self.world.barrier()
+            self.table.local = own
+            self._shards_t = []
+            for mm in self._maps:
+                mm.close()
+            for f in self._files:
+                f.close()
+            self._maps, self._files = [], []
+        self.kind = "local"

@@ -56,12 +56,13 @@ class LookupCtx:
     recv_local carry -1 padding -- no host read-back, every shape fixed by the
     batch shape and the capacity.  `void`: device int32 [1], 1 when this step
     overflowed on some rank (static W > 1 only)."""
-    __slots__ = ("uniq", "inverse", "order", "send", "recv", "recv_local", "static", "n", "void")
+    __slots__ = ("uniq", "inverse", "order", "send", "recv", "recv_local", "static", "n", "void", "hogwild")
 
-    def __init__(self, uniq, inverse, order, send, recv, recv_local, static=False, n=0, void=None):
+    def __init__(self, uniq, inverse, order, send, recv, recv_local, static=False, n=0, void=None, hogwild=False):
         self.uniq, self.inverse, self.order = uniq, inverse, order
         self.send, self.recv, self.recv_local = send, recv, recv_local
         self.static, self.n, self.void = static, n, void
+        self.hogwild = hogwild      # rows read from the owners' shared shards (asynchronous mode)
 
 
 class StaticRouter:
@@ -173,6 +174,9 @@ class ShardedEmbedding:
         # tables that route the same ids: pass the first table's router)
         self.router = router if router is not None else (
             StaticRouter(self.world, self.device, capacity, peer_capacity) if capacity is not None else None)
+        # asynchronous (Hogwild) mode: every shard mapped into every rank
+        # (parallel/async_ps.HogwildTable); lookups / updates bypass the exchange
+        self.hogwild = None
         n_local = (self.num_rows - self.rank + self.W - 1) // self.W if self.rank < self.num_rows else 0
         self.local = torch.empty((n_local, self.dim), dtype=torch.float32, device=self.device)
         with torch.no_grad():
@@ -255,11 +259,17 @@ class ShardedEmbedding:
 
     def lookup(self, ids: torch.Tensor):
         """rows [U, D] for the unique ids of `ids`, plus the routing context."""
+        if self.hogwild is not None:      # asynchronous: straight from the owners' shards, no collective
+            rows, inverse, uniq = self.hogwild.lookup(ids)
+            return rows, LookupCtx(uniq, inverse, None, None, None, None, hogwild=True)
         ctx = self.route(ids)
         return lookup_shared([self], ctx)[0], ctx
 
     def apply_sgd(self, ctx: LookupCtx, grad_rows: torch.Tensor, lr: float):
         """local[owner rows] -= lr * grad (grad_rows aligned with ctx.uniq)."""
+        if ctx.hogwild:
+            self.hogwild.scatter_sgd(ctx.uniq, grad_rows, lr)
+            return
         apply_sgd_shared([self], ctx, [grad_rows], [lr])
 
     def _sgd_local(self, ctx: LookupCtx, g: torch.Tensor, lr: float):

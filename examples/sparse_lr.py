@@ -55,6 +55,10 @@ flags.DEFINE_integer("steps_per_epoch", 100, "queue mode: batches per epoch")
 flags.DEFINE_string("cluster_conf", "cluster_conf.json", "cluster JSON (lr2.py:325)")
 flags.DEFINE_integer("seed", 1, "init seed")
 flags.DEFINE_string("result_json", "", "write final metrics here (tests)")
+flags.DEFINE_string("update_mode", "", "sync (default: all-reduce / sharded exchange per step) or async (the "
+                    "reference's Hogwild ps updates: rows read from and scattered into the owners' shared shards); "
+                    "'' = $DTF_UPDATE_MODE or sync")
+flags.DEFINE_boolean("use_locking", False, "async: no lost updates (CAS / file locks), TF's use_locking")
 FLAGS = flags.FLAGS
 
 
@@ -81,7 +85,8 @@ def main(_argv):
     log.info("load data")
     dp.LoadData()
     log.info("build model")
-    model = sparse_lr.SparseLRTrainer(FLAGS.features, FLAGS.learning_rate, world, seed=FLAGS.seed)
+    model = sparse_lr.SparseLRTrainer(FLAGS.features, FLAGS.learning_rate, world, seed=FLAGS.seed,
+                                      update_mode=FLAGS.update_mode or None, use_locking=FLAGS.use_locking)
     log.info("sampling test data ...")
     test_data = dp.GetTestSamplesSampled(sampling_rate=0.1, sampling_max_num=1000)
 
@@ -116,7 +121,8 @@ def main(_argv):
     nt = sparse_lr.steps_per_epoch(world, nt)
     for batch in dp.NextBatch("test", max_batches=nt):
         model.auc_update(batch)
-    auc = model.auc(all_workers=True)
+    auc = model.auc(all_workers=True)       # (a collective: every worker finished training)
+    model.refresh_global_step()
     log.info(f"Finish evaluate, auc: {auc}")
     if FLAGS.checkpoint:
         local, repl = model.checkpoint_tensors()

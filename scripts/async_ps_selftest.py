@@ -25,6 +25,9 @@ def main():
     ap.add_argument("--same-gpu", action="store_true")
     ap.add_argument("--no-locking", action="store_true")
     ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--table", action="store_true",
+                    help="a row-sharded table (HogwildTable): rows read from / scatter-updated into the owners' "
+                         "IPC-mapped shards")
     a = ap.parse_args()
     from distributed_tensorflow_example_amd.parallel import async_ps
     from distributed_tensorflow_example_amd.parallel.world import World
@@ -35,6 +38,8 @@ def main():
     dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=ws,
                             timeout=datetime.timedelta(seconds=120))
     w = World(rank=rank, world_size=ws, local_rank=rank, device=dev, backend="gloo", pg_initialized=True)
+    if a.table:
+        return table_test(a, w, dev, rank, ws)
     n = 79510                                  # the MLP's parameter count
     p1 = torch.full((n - 10,), 1000.0, device=dev) if rank == 0 else torch.zeros(n - 10, device=dev)
     p2 = torch.full((10,), 1000.0, device=dev) if rank == 0 else torch.zeros(10, device=dev)
@@ -64,6 +69,49 @@ def main():
         print(json.dumps({"async_ps_selftest": "pass" if (init_ok and steps_ok and vals_ok) else "fail",
                           "kind": st.kind, "final": final, "expect": expect, "global_step": total,
                           "init_ok": init_ok, "steps_ok": steps_ok}), flush=True)
+    dist.destroy_process_group()
+
+
+def table_test(a, w, dev, rank, ws):
+    """Every rank scatter-SGDs its own gradient (rank + 1) into the same 64 rows
+    of a 1003 x 4 table spread over all shards (every owner, odd local rows),
+    `steps` times, without waiting; with locking every update lands."""
+    from distributed_tensorflow_example_amd.parallel import async_ps
+    from distributed_tensorflow_example_amd.parallel.sharded_embedding import ShardedEmbedding
+
+    F, D = 1003, 4
+    t = ShardedEmbedding(F, D, w, device=dev, zero_init=True, name="tab")
+    with torch.no_grad():
+        t.local.fill_(1000.0)
+    hog = async_ps.HogwildTable(t, w, use_locking=not a.no_locking)
+    t.hogwild = hog
+    ids = torch.arange(5, 5 + 64 * 7, 7, device=dev)
+    rows, ctx = t.lookup(ids)
+    init_ok = bool((rows == 1000.0).all().item()) and ctx.hogwild
+    w.barrier()
+    for _ in range(a.steps):
+        rows, ctx = t.lookup(ids)
+        t.apply_sgd(ctx, torch.full((ctx.uniq.numel(), D), float(rank + 1), device=dev), 1.0)
+    torch.cuda.synchronize()
+    w.barrier()
+    rows, _ = t.lookup(ids)
+    others, _ = t.lookup(torch.arange(6, 6 + 64 * 7, 7, device=dev))     # never updated
+    torch.cuda.synchronize()
+    expect = 1000.0 - a.steps * ws * (ws + 1) / 2
+    if a.no_locking:
+        vals_ok = bool(((rows >= expect) & (rows <= 1000.0 - a.steps)).all().item())
+    else:
+        vals_ok = bool((rows == expect).all().item())
+    untouched = bool((others == 1000.0).all().item())
+    full = t.full_table()
+    shard_ok = bool((full[ids] == rows).all().item())
+    kind = hog.kind
+    hog.close()
+    if rank == 0:
+        ok = init_ok and vals_ok and untouched and shard_ok
+        print(json.dumps({"async_ps_selftest": "pass" if ok else "fail", "kind": kind, "table": True, "final": float(rows[0, 0].item()), "expect": expect,
+                          "init_ok": init_ok, "vals_ok": vals_ok, "untouched": untouched, "shard_ok": shard_ok}),
+              flush=True)
     dist.destroy_process_group()
 
 

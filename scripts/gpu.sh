@@ -73,7 +73,10 @@ for step in "$@"; do
         python3 bench.py --gpus 1 --steps 5500 --warmup 550 $extra ;;
     lowering)
       run lowering_tests 500 $PYT -x tests/test_lowering_gpu.py tests/test_lowering_cpu.py $extra
-      run bench_graph 300 python scripts/bench_graph_step.py 2000 ;;
+      run bench_graph 300 python scripts/bench_graph_step.py 2000
+      rm -rf $OUT/prof_graph
+      run prof_graph 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_graph -o run -- \
+        python3 scripts/bench_graph_step.py 500 ;;
     models)
       run bench_resnet50 400 python scripts/bench_models.py --model resnet50 --steps 30 --warmup 5
       run bench_bert_b128 400 python scripts/bench_models.py --model bert_base --batch 128 --steps 20 --warmup 5 $extra ;;

@@ -13,8 +13,11 @@ pytestmark = pytest.mark.gpu
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("nproc,locking", [(2, True), (3, True), (2, False)])
-def test_hogwild_store_ipc_same_gpu(native, nproc, locking):
+@pytest.mark.parametrize("nproc,locking,table", [(2, True, False), (3, True, False), (2, False, False),
+                                                 (2, True, True), (3, True, True), (2, False, True)])
+def test_hogwild_store_ipc_same_gpu(native, nproc, locking, table):
+    """table: a row-sharded table (lr2.py's ps-held W) -- rows gathered from and
+    scatter-SGD'd into the owners' IPC-mapped shards (csrc/kernels/hogwild.hip)."""
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -23,6 +26,8 @@ def test_hogwild_store_ipc_same_gpu(native, nproc, locking):
            f"--master-port={port}", os.path.join(REPO, "scripts", "async_ps_selftest.py"), "--same-gpu"]
     if not locking:
         cmd.append("--no-locking")
+    if table:
+        cmd.append("--table")
     env = dict(os.environ, PYTHONPATH=REPO, OMP_NUM_THREADS="2")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=100, env=env)
     line = [l for l in r.stdout.splitlines() if l.startswith("{")]

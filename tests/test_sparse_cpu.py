@@ -195,7 +195,12 @@ def test_sharded_table_four_ranks_equal_one(svm_dir):
     assert np.array_equal(saver.read_tensor(four[0][4], "weights/Variable").numpy(), four[0][2])
 
 
-def test_lr2_example_ps_two_workers(svm_dir, tmp_path):
+@pytest.mark.parametrize("mode", ["sync", "async"])
+def test_lr2_example_ps_two_workers(svm_dir, tmp_path, mode):
+    """lr2.py's launch shape (1 ps + 2 workers, run_lr2.sh test mode).  sync:
+    lock-step replicas; async (the reference's rule, lr2.py:359-396): W's rows
+    read from / scattered into the owners' shared shards, b in a shared Hogwild
+    store, and global_step counts EVERY worker's update."""
     d, tr, te = svm_dir
     p = _free_port()
     conf = tmp_path / "cluster_conf.json"
@@ -203,7 +208,7 @@ def test_lr2_example_ps_two_workers(svm_dir, tmp_path):
                                 "worker": [f"127.0.0.1:{p}", f"127.0.0.1:{_free_port()}"]}))
     common = [f"--cluster_conf={conf}", f"--train={','.join(tr)}", f"--test={','.join(te)}", "--features=3000",
               "--num_epochs=2", "--learning_rate=0.5", "--batch_size=100", "--trace_step_interval=5",
-              f"--checkpoint={tmp_path}/ck/lr"]
+              f"--checkpoint={tmp_path}/ck/lr", f"--update_mode={mode}"]
     env = dict(os.environ, PYTHONPATH=REPO, DTF_RENDEZVOUS_TIMEOUT="120")
     script = os.path.join(REPO, "examples", "sparse_lr.py")
     procs = [subprocess.Popen([sys.executable, script, "--job_name=ps", "--task_index=0"] + common, env=env,
@@ -223,10 +228,17 @@ def test_lr2_example_ps_two_workers(svm_dir, tmp_path):
     for pr, o in zip(procs, outs):
         assert pr.returncode == 0, o
     r0, r1 = (json.load(open(tmp_path / f"w{i}.json")) for i in (0, 1))
-    assert r0["global_step"] == r1["global_step"] == 28          # 2 epochs x 14 batches (1400 / 100)
-    assert r0["auc"] == r1["auc"] and r0["b"] == r1["b"]
     assert "Finish evaluate, auc:" in outs[2]
-    assert os.path.exists(tmp_path / "ck" / "lr-28.index")
+    assert r0["auc"] == r1["auc"] and 0.0 < r0["auc"] <= 1.0
+    if mode == "sync":
+        assert r0["global_step"] == r1["global_step"] == 28      # 2 epochs x 14 batches (1400 / 100)
+        assert r0["b"] == r1["b"]
+        assert os.path.exists(tmp_path / "ck" / "lr-28.index")
+    else:
+        # each worker ran 28 steps; the shared counter saw both: 56
+        assert r0["steps"] == r1["steps"] == 28
+        assert r0["global_step"] == r1["global_step"] == 56
+        assert os.path.exists(tmp_path / "ck" / "lr-56.index")
 
 
 def test_wide_deep_two_ranks_equal_one(svm_dir):

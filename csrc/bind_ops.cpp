@@ -14,6 +14,9 @@ hipError_t dtfk_hogwild_sgd(float* shared, const float* g, float* local, float l
 hipError_t dtfk_hogwild_counter(unsigned long long* counter, long long* out, long long set, int do_set, hipStream_t s);
 hipError_t dtfk_hogwild_gather_rows(const long long* ids, int n, int D, const float* const* shards, int W, float* out,
                                    hipStream_t s);
+hipError_t dtfk_sparse_rows_apply(float* table, float* slot_a, float* slot_b, const long long* rows, const float* g,
+                                  long long n, int D, int kind, float lr, float mu, int nesterov, float rho, float eps,
+                                  const int* skip, hipStream_t s);
 hipError_t dtfk_hogwild_scatter_sgd(const long long* ids, const float* g, int n, int D, float* const* shards, int W,
                                     float lr, int locking, hipStream_t s);
 hipError_t dtfk_bucket_pack_bf16(const float* g, uint16_t* c, int64_t n, float scale, hipStream_t s);
@@ -30,7 +33,7 @@ hipError_t dtfk_gemm(const void* A, int a_bf16, int lda, int transA, const void*
                      int K, float alpha, float beta, int act, hipStream_t stream);
 hipError_t dtfk_gemm_big(const void* A, int lda, int transA, const void* B, int ldb, int transB, void* C,
                          int c_bf16, int ldc, const float* bias, int M, int N, int K, float alpha, float beta,
-                         int act, int split_k, hipStream_t stream);
+                         int act, int split_k, int variant, hipStream_t stream);
 int dtfk_gemm_big_supported(const void* A, int lda, int transA, const void* B, int ldb, int transB, int c_bf16, int M,
                             int N, int K, float beta, int act, int split_k);
 hipError_t dtfk_gemm_big_cfg(int cfg, const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N,
@@ -122,9 +125,10 @@ void gemm(at::Tensor A, bool transA, at::Tensor B, bool transB, at::Tensor out,
 // shape is outside the kernel's contract (K % 64, alignment), so callers can
 // pick another GEMM; dtype / rank errors throw.
 bool gemm_big(at::Tensor A, bool transA, at::Tensor B, bool transB, at::Tensor out, c10::optional<at::Tensor> bias,
-              int act, double alpha, double beta, int split_k) {
+              int act, double alpha, double beta, int split_k, int variant) {
   gpu(A, "A"); gpu(B, "B"); gpu(out, "out");
   if (A.dim() != 2 || B.dim() != 2 || out.dim() != 2) throw std::runtime_error("gemm_big operands must be 2-D");
+  if (variant != 0 && variant != 4 && variant != 8) throw std::runtime_error("gemm_big: variant 0 (auto), 4 or 8");
   if (A.scalar_type() != at::kBFloat16 || B.scalar_type() != at::kBFloat16)
     throw std::runtime_error("gemm_big: bf16 operands");
   if (out.scalar_type() != at::kBFloat16 && out.scalar_type() != at::kFloat)
@@ -143,7 +147,7 @@ bool gemm_big(at::Tensor A, bool transA, at::Tensor B, bool transB, at::Tensor o
                                N, K, (float)beta, act, split_k))
     return false;   // outside the kernel's contract: the caller picks another GEMM
   ck(dtfk_gemm_big(A.data_ptr(), (int)A.stride(0), transA, B.data_ptr(), (int)B.stride(0), transB, out.data_ptr(), obf,
-                   (int)out.stride(0), opt_ptr<float>(bias), M, N, K, (float)alpha, (float)beta, act, split_k, cs()),
+                   (int)out.stride(0), opt_ptr<float>(bias), M, N, K, (float)alpha, (float)beta, act, split_k, variant, cs()),
      "gemm_big");   // any launch error is a real error
   return true;
 }
@@ -428,7 +432,32 @@ static void hogwild_scatter_sgd(at::Tensor ids, at::Tensor grads, int64_t shards
      "hogwild_scatter_sgd");
 }
 
+// Row-sparse optimizer update of a table shard (sparse_optim.hip): rows[i] >= 0
+// distinct (the owner summed the duplicates), -1 = no update.
+static void sparse_rows_apply(at::Tensor table, c10::optional<at::Tensor> slot_a, c10::optional<at::Tensor> slot_b,
+                              at::Tensor rows, at::Tensor g, int kind, double lr, double mu, bool nesterov,
+                              double rho, double eps, c10::optional<at::Tensor> skip) {
+  f32c(table, "table"); i64c(rows, "rows"); f32c(g, "g");
+  if (table.dim() != 2 || g.dim() != 2 || g.size(0) != rows.numel() || g.size(1) != table.size(1))
+    throw std::runtime_error("sparse_rows_apply: table [R, D], g [n, D], rows [n]");
+  for (auto* t : {&slot_a, &slot_b})
+    if (t->has_value()) {
+      f32c(**t, "slot");
+      if ((*t)->sizes() != table.sizes()) throw std::runtime_error("sparse_rows_apply: slot shape != table shape");
+    }
+  if (skip.has_value() && (skip->scalar_type() != at::kInt || !skip->is_cuda()))
+    throw std::runtime_error("sparse_rows_apply: skip must be a device int32 tensor");
+  ck(dtfk_sparse_rows_apply(table.data_ptr<float>(), opt_ptr<float>(slot_a), opt_ptr<float>(slot_b),
+                            reinterpret_cast<const long long*>(rows.data_ptr<int64_t>()), g.data_ptr<float>(),
+                            rows.numel(), (int)table.size(1), kind, (float)lr, (float)mu, nesterov ? 1 : 0,
+                            (float)rho, (float)eps, opt_ptr<int>(skip), cs()),
+     "sparse_rows_apply");
+}
+
 void init_ops(py::module& m) {
+  m.def("sparse_rows_apply", &sparse_rows_apply, py::arg("table"), py::arg("slot_a"), py::arg("slot_b"),
+        py::arg("rows"), py::arg("g"), py::arg("kind"), py::arg("lr"), py::arg("mu") = 0.0,
+        py::arg("nesterov") = false, py::arg("rho") = 0.9, py::arg("eps") = 1e-10, py::arg("skip") = py::none());
   m.def("hogwild_gather_rows", &hogwild_gather_rows, py::arg("ids"), py::arg("shards"), py::arg("W"), py::arg("out"));
   m.def("hogwild_scatter_sgd", &hogwild_scatter_sgd, py::arg("ids"), py::arg("grads"), py::arg("shards"), py::arg("W"),
         py::arg("lr"), py::arg("locking"));
@@ -448,7 +477,7 @@ void init_ops(py::module& m) {
         py::arg("Z") = py::none());
   m.def("gemm_big", &gemm_big, py::arg("A"), py::arg("transA"), py::arg("B"), py::arg("transB"), py::arg("out"),
         py::arg("bias") = py::none(), py::arg("act") = 0, py::arg("alpha") = 1.0, py::arg("beta") = 0.0,
-        py::arg("split_k") = 0);
+        py::arg("split_k") = 0, py::arg("variant") = 0);
   m.def("gemm_big_cfg", &gemm_big_cfg);
   m.def("act_backward", &act_backward);
   m.def("col_sum", &col_sum);

@@ -364,6 +364,209 @@ __global__ __launch_bounds__(NTHR) void gemm_big(const uint16_t* __restrict__ A,
   }
 }
 
+// ---- 8-phase schedule (cdna_hip_programming.md s5 "The 256^2 8-phase template") ----
+// Same 256 x 256 tile, 8 waves (2 along M x 4 along N, 128 x 64 outputs each),
+// BK 64 and LDS images as gemm_big, but every K tile is split into FOUR
+// half-tiles, one per output quadrant half:
+//   A_q = tile rows [64q, 64q+64) and [128+64q, 128+64q+64)   (quadrant row qm = q of both wave rows)
+//   B_q = tile cols [64c+32q, 64c+32q+32) for c = 0..3          (quadrant col qn = q of all wave columns)
+// each a 128-row x 64-k image of 16 KiB (2 LDS-DMA instructions per thread).
+// Two K tiles (even / odd LDS buffer, 64 KiB each) per loop iteration, 8
+// phases; phase p multiplies one 64 x 32 quadrant of the wave's outputs over
+// the whole K tile (16 MFMA 16x16x32):
+//   phase   quadrant  ds_reads (this K tile)   DMA issued (half-tile, K tile)
+//     1      (0,0)    B_q0 then A_q0            A_q1  of t+1   (odd buffer)
+//     2      (0,1)    B_q1                      B_q0  of t+2   (even buffer)
+//     3      (1,1)    A_q1                      A_q0  of t+2
+//     4      (1,0)    --  (registers)           B_q1  of t+2,  vmcnt(6): t+1 landed
+//   phases 5..8: the same on the odd buffer (DMA: A_q1 of t+2, then B_q0 /
+//   A_q0 / B_q1 of t+3, vmcnt(6) at phase 8: t+2 landed).
+// Three half-tiles (6 DMA instructions) stay in flight across every barrier;
+// vmcnt is counted, never 0 inside the loop.  A buffer region is restaged two
+// phases after its last ds_read, or one phase after when those reads were
+// retired before the reading phase's first barrier (B_q0: its reads are
+// issued first and retired by lgkmcnt(#A reads) before that barrier).
+// The two wave rows run one barrier apart (`if (wr) s_barrier` before the
+// loop): while one group multiplies, the other issues its reads and DMA.
+// A buffer retired by the vmcnt at phase p is read from phase p+1 on (the
+// staggered group passes one more barrier after the other group's wait).
+// Shape contract on top of gemm_big's: the K range of a workgroup is a
+// multiple of 128 (an even number of K tiles).
+template <bool IS_A>
+__device__ __forceinline__ int half_row(int l, int q) {   // half-tile local index -> tile row / col
+  if constexpr (IS_A) return ((l >> 6) << 7) + (q << 6) + (l & 63);
+  else return ((l >> 5) << 6) + (q << 5) + (l & 31);
+}
+
+template <bool IS_A, bool KC>
+__device__ __forceinline__ void stage_half(const uint16_t* __restrict__ base, int ld, int rows, int r0, int k0, int q,
+                                           uint8_t* img, int wave, int lane) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int wbase = (j * 8 + wave) << 10;
+    const int o = wbase + (lane << 4);
+    const uint16_t* src;
+    if constexpr (KC) {   // [128][64] image, kc_off<64> chunk XOR
+      const int rl = o >> 7, c = ((o >> 4) & 7) ^ ((rl >> 1) & 7);
+      src = base + (size_t)min(r0 + half_row<IS_A>(rl, q), rows - 1) * ld + k0 + c * 8;
+    } else {              // [64][128] image, mn_off<128>
+      const int k = o >> 8, ch = ((o & 255) >> 4) ^ (mn_swz(k) << 1);
+      src = base + (size_t)(k0 + k) * ld + min(r0 + half_row<IS_A>(ch * 8, q), rows - 8);
+    }
+    __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(img + wbase), 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ void raw_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <bool AKC, bool BKC, bool OBF>
+__global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A, int lda,
+                                                 const uint16_t* __restrict__ B, int ldb, void* __restrict__ C,
+                                                 int ldc, const float* __restrict__ bias, int M, int N, int K,
+                                                 float alpha, float beta, int act, int kchunk) {
+  constexpr int BM = 256, BK = 64, HALF = 128 * BK * 2, BUF = 4 * HALF;   // A_q0 A_q1 B_q0 B_q1
+  constexpr int NA = AKC ? 8 : 16;                                       // LDS instructions of one A-fragment set
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[2 * BUF];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+
+  const int nt_n = (N + BN - 1) / BN;
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig % 8, q8 = nwg / 8, rem = nwg % 8;
+  const int wg = (xcd < rem ? xcd * (q8 + 1) : rem * (q8 + 1) + (xcd - rem) * q8) + orig / 8;
+  const int m0 = (wg / nt_n) * BM, n0 = (wg % nt_n) * BN;
+  const int kb = blockIdx.y * kchunk, ke = min(K, kb + kchunk);
+  const int nk = (ke - kb) / BK;   // even (host contract)
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // half-tile h of K tile t: 0 B_q0, 1 A_q0, 2 B_q1, 3 A_q1 (staging order)
+  auto stage = [&](int t, int h) {
+    if (t >= nk) return;
+    uint8_t* buf = smem + (t & 1) * BUF;
+    const int k0 = kb + t * BK;
+    if (h == 0) stage_half<false, BKC>(B, ldb, N, n0, k0, 0, buf + 2 * HALF, wave, lane);
+    else if (h == 1) stage_half<true, AKC>(A, lda, M, m0, k0, 0, buf, wave, lane);
+    else if (h == 2) stage_half<false, BKC>(B, ldb, N, n0, k0, 1, buf + 3 * HALF, wave, lane);
+    else stage_half<true, AKC>(A, lda, M, m0, k0, 1, buf + HALF, wave, lane);
+  };
+  bf16x8 fa[2][4], fb[2][2][2];   // A: [k-sub][m-tile] of one quadrant row; B: [qn][k-sub][n-tile]
+  auto read_a = [&](const uint8_t* buf, int qm) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[s][i] = frag<128, BK, AKC>(buf + qm * HALF, wr * 64 + i * 16, s, lane);
+  };
+  auto read_b = [&](const uint8_t* buf, int qn) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fb[qn][s][j] = frag<128, BK, BKC>(buf + (2 + qn) * HALF, wc * 32 + j * 16, s, lane);
+  };
+  auto mma = [&](int qm, int qn) {
+    raw_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[qm * 4 + i][qn * 2 + j] = mfma16x16x32(fa[s][i], fb[qn][s][j], acc[qm * 4 + i][qn * 2 + j]);
+    __builtin_amdgcn_s_setprio(0);
+    raw_barrier();
+  };
+  // phase 1 / 5 reads: B_q0 first, then A_q0; the B reads retire before the barrier
+  auto read_first = [&](const uint8_t* buf) {
+    read_b(buf, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    read_a(buf, 0);
+    if constexpr (NA <= 15) asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NA) : "memory");
+    else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+
+  // prologue: K tile 0 whole, K tile 1 but its A_q1 (issued in phase 1)
+#pragma unroll
+  for (int h = 0; h < 4; ++h) stage(0, h);
+#pragma unroll
+  for (int h = 0; h < 3; ++h) stage(1, h);
+  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  raw_barrier();
+  if (wr) raw_barrier();   // the second wave row runs one barrier behind
+
+  for (int t = 0; t < nk; t += 2) {
+    const uint8_t* ev = smem;
+    const uint8_t* od = smem + BUF;
+    const bool last = t + 2 >= nk;
+    // phases 1-4: even buffer (K tile t)
+    read_first(ev);
+    stage(t + 1, 3);
+    mma(0, 0);
+    read_b(ev, 1);
+    stage(t + 2, 0);
+    mma(0, 1);
+    read_a(ev, 1);
+    stage(t + 2, 1);
+    mma(1, 1);
+    stage(t + 2, 2);
+    if (last) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    mma(1, 0);
+    // phases 5-8: odd buffer (K tile t+1)
+    read_first(od);
+    stage(t + 2, 3);
+    mma(0, 0);
+    read_b(od, 1);
+    stage(t + 3, 0);
+    mma(0, 1);
+    read_a(od, 1);
+    stage(t + 3, 1);
+    mma(1, 1);
+    stage(t + 3, 2);
+    if (!last) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    mma(1, 0);
+  }
+  if (!wr) raw_barrier();   // equal barrier counts for both wave rows
+
+  const bool split = gridDim.y > 1;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + wc * 64 + j * 16 + (lane & 15);
+    if (n >= N) continue;
+    const float bv = (bias != nullptr) ? bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wr * 128 + i * 16 + 4 * (lane >> 4) + r;
+        if (m >= M) continue;
+        const size_t o = (size_t)m * ldc + n;
+        if (split) {
+          atomicAdd(reinterpret_cast<float*>(C) + o, alpha * acc[i][j][r] + (blockIdx.y == 0 ? bv : 0.f));
+          continue;
+        }
+        float z = alpha * acc[i][j][r] + bv;
+        if (beta != 0.f)
+          z += beta * (OBF ? bf2f(reinterpret_cast<const uint16_t*>(C)[o]) : reinterpret_cast<const float*>(C)[o]);
+        const float y = apply_act(z, act);
+        if constexpr (OBF) reinterpret_cast<uint16_t*>(C)[o] = f2bf(y);
+        else reinterpret_cast<float*>(C)[o] = y;
+      }
+    }
+  }
+}
+
 }  // namespace gemm2
 }  // namespace dtfk
 
@@ -388,13 +591,20 @@ extern "C" int dtfk_gemm_big_supported(const void* A, int lda, int transA, const
 
 // Returns hipErrorInvalidValue (launching nothing) when the shape contract
 // (dtfk_gemm_big_supported) does not hold.  split_k <= 0: automatic.
+// variant: 0 = automatic (the 8-phase schedule whenever every workgroup's K
+// range is a multiple of 128, else the one-barrier loop), 4 = one-barrier loop
+// (gemm_big VAR 4), 8 = 8-phase (hipErrorInvalidValue if K % 128).
 extern "C" hipError_t dtfk_gemm_big(const void* A, int lda, int transA, const void* B, int ldb, int transB,
                                     void* C, int c_bf16, int ldc, const float* bias, int M, int N, int K,
-                                    float alpha, float beta, int act, int split_k, hipStream_t stream) {
+                                    float alpha, float beta, int act, int split_k, int variant, hipStream_t stream) {
   using namespace dtfk::gemm2;
   const bool akc = !transA, bkc = transB != 0;
   if (!dtfk_gemm_big_supported(A, lda, transA, B, ldb, transB, c_bf16, M, N, K, beta, act, split_k))
     return hipErrorInvalidValue;
+  if (variant != 0 && variant != 4 && variant != 8) return hipErrorInvalidValue;
+  const bool ph8 = variant == 8 || (variant == 0 && K % 128 == 0);
+  if (ph8 && K % 128) return hipErrorInvalidValue;
+  const int kq = ph8 ? 2 * KQ : KQ;
   const int tn = (N + BN - 1) / BN;
   // 256 x 256 tiles even when they leave CUs idle (N = 768: 192 tiles): measured
   // faster than 128 x 256 at every BERT shape (scripts/probes/gemm_big_cfg.py)
@@ -405,7 +615,7 @@ extern "C" hipError_t dtfk_gemm_big(const void* A, int lda, int transA, const vo
   if (split_k > 1 || (split_k <= 0 && linear && tiles < 256 && K >= 2048)) {
     split = split_k > 1 ? split_k : (int)((512 + tiles - 1) / tiles);
     split = min(split, K / 512 > 0 ? K / 512 : 1);
-    kchunk = ((K + split - 1) / split + KQ - 1) / KQ * KQ;
+    kchunk = ((K + split - 1) / split + kq - 1) / kq * kq;
     split = (K + kchunk - 1) / kchunk;
   }
   if (split > 1 && beta == 0.f) {
@@ -418,9 +628,13 @@ extern "C" hipError_t dtfk_gemm_big(const void* A, int lda, int transA, const vo
 // 64-deep tiles, 2 stages, one barrier per tile (VAR 4) for every layout: the
 // 32-deep 5-stage ring, 128-row tiles, register staging and the two-barrier
 // loop measured slower (profiles/gemm_big_cfg_r2.jsonl)
-#define DTFK_GB(AK, BKk, OB)                                                                                  \
-  hipLaunchKernelGGL((gemm_big<256, 64, 2, AK, BKk, OB, 4>), grid, block, 0, stream, a, lda, b, ldb, C, ldc, bias, \
-                     M, N, K, alpha, split > 1 ? 1.f : beta, act, kchunk)
+#define DTFK_GB(AK, BKk, OB)                                                                                      \
+  if (ph8)                                                                                                       \
+    hipLaunchKernelGGL((gemm_8ph<AK, BKk, OB>), grid, block, 0, stream, a, lda, b, ldb, C, ldc, bias, M, N, K,    \
+                       alpha, split > 1 ? 1.f : beta, act, kchunk);                                              \
+  else                                                                                                           \
+    hipLaunchKernelGGL((gemm_big<256, 64, 2, AK, BKk, OB, 4>), grid, block, 0, stream, a, lda, b, ldb, C, ldc, bias, \
+                       M, N, K, alpha, split > 1 ? 1.f : beta, act, kchunk)
 #define DTFK_GB_O(AK, BKk) \
   if (c_bf16) { DTFK_GB(AK, BKk, true); } else { DTFK_GB(AK, BKk, false); }
 #define DTFK_GB_B(AK) \
@@ -456,6 +670,11 @@ extern "C" hipError_t dtfk_gemm_big_cfg(int cfg, const void* A, int lda, const v
     case 7: DTFK_CFG(256, 64, 2, 2); break;
     case 8: DTFK_CFG(256, 64, 2, 3); break;
     case 9: DTFK_CFG(256, 64, 2, 4); break;
+    case 10:
+      if (K % 128) return hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_8ph<true, true, true>), dim3((M / 256) * tn, 1), dim3(NTHR), 0, stream, a, lda, b, ldb,
+                         C, ldc, nullptr, M, N, K, 1.f, 0.f, 0, K);
+      break;
     default: return hipErrorInvalidValue;
   }
 #undef DTFK_CFG

@@ -153,6 +153,42 @@ class PartitionedVariable(Variable):
         return f"<dtf PartitionedVariable '{self.name}' shape={self.shape} shards={self.world.world_size}>"
 
 
+class PartitionedSlot:
+    """An optimizer slot of a partitioned variable (`<var>/Adagrad`,
+    `<var>/Adam_1`, ...): sharded exactly like the table, checkpointed in the
+    same TF slice layout, not trainable."""
+
+    is_partitioned = True
+    op_type, attrs = "VariableV2", {}
+
+    def __init__(self, pv: PartitionedVariable, slot: str):
+        self.pv, self.slot = pv, slot
+        self.name = f"{pv.name[:-2]}/{slot}:0"
+        self.shape, self.rows, self.dim, self.dtype = pv.shape, pv.rows, pv.dim, torch.float32
+        self.partitioner, self.world = pv.partitioner, pv.world
+        self.trainable = False
+        self.initialized = True
+        self.placement = pv.placement
+        # the value the optimizer gives the slot (Adagrad: initial_accumulator_value, RMSProp ms: 1)
+        self.init = {"Adagrad": float(pv.table.opt_hp.get("initial_accumulator_value", 0.1)),
+                     "RMSProp": 1.0}.get(slot, 0.0)
+
+    @property
+    def table(self):
+        return self.pv.table.slot_view(self.slot)
+
+    @property
+    def value(self):
+        return self.pv.table.slots[self.slot]
+
+    def _initialize(self):
+        with torch.no_grad():
+            self.value.fill_(self.init)
+
+    def __repr__(self):
+        return f"<dtf PartitionedSlot '{self.name}' shape={self.shape}>"
+
+
 def init_spec_of(initial_value, graph_seed_fn) -> Optional[tuple]:
     """('normal', mean, std, seed) | ('const', v, 0, 0) | None for an initial value."""
     spec = getattr(initial_value, "_init_spec", None)

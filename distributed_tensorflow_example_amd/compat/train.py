@@ -351,9 +351,11 @@ class Optimizer:
         pairs = list(grads_and_vars)
         dense_pairs = [(g, v) for g, v in pairs if not _is_pv(v)]
         sparse_pairs = [(g, v) for g, v in pairs if _is_pv(v)]
-        if sparse_pairs and self._kind != "sgd":
-            raise NotImplementedError(f"{type(self).__name__}: partitioned (sharded) variables support "
-                                      "GradientDescentOptimizer only")
+        if sparse_pairs and self._kind not in ("sgd", "momentum", "adagrad", "rmsprop", "adam"):
+            raise NotImplementedError(f"{type(self).__name__}: no sparse (partitioned-variable) update rule")
+        for _, pv in sparse_pairs:      # owner-side sparse rule + sharded slots (TF names var/<slot>)
+            pv.table.set_optimizer(self._kind, **self._sparse_hp())
+            self._register_pv_slots(pv)
         vars_ = [v for _, v in dense_pairs]
         gtens = [g for g, _ in dense_pairs]
         opt = self
@@ -384,10 +386,11 @@ class Optimizer:
                     fused.set_lr(opt._lr_value())
                 fused.step(grads=[g.contiguous() for g in gs])
             lr = opt._lr_value()
-            for g, pv in sparse_pairs:      # owner-side scatter SGD, sync-average folded in
+            for g, pv in sparse_pairs:      # owner-side sparse update, sync average as grad_scale
                 for lctx, rows_grad in ctx.eval(g):
                     pv.table.apply_sgd(lctx, rows_grad if rows_grad is not None else
-                                       torch.zeros((lctx.uniq.numel(), pv.dim), device=pv.table.device), lr / ws)
+                                       torch.zeros((lctx.uniq.numel(), pv.dim), device=pv.table.device), lr,
+                                       grad_scale=1.0 / ws)
             if global_step is not None:
                 with torch.no_grad():
                     global_step.value.data += 1
@@ -466,6 +469,22 @@ class Optimizer:
         op.loss = loss
         return op
 
+    def _sparse_hp(self) -> dict:
+        """Hyper-parameters of this optimizer's sparse (sharded-table) rule."""
+        return {}
+
+    def _register_pv_slots(self, pv):
+        """A partitioned variable's slots: partitioned variables themselves
+        (saved / restored in the TF slice layout like the table)."""
+        from .partitioned import PartitionedSlot
+
+        g = get_default_graph()
+        names = {v.name for v in g.get_collection(GLOBAL_VARIABLES)}
+        for sname in pv.table.slots:
+            sv = PartitionedSlot(pv, sname)
+            if sv.name not in names:
+                g.add_to_collection(GLOBAL_VARIABLES, sv)
+
     # slot variables with TF names (w/Adam, w/Adam_1, beta1_power, ...) for checkpoints
     def _register_slots(self, vars_, fused):
         g = get_default_graph()
@@ -516,6 +535,9 @@ class MomentumOptimizer(Optimizer):
     def _make_fused(self, params):
         return _optim.FusedMomentum(params, self._lr_value(), self.momentum, self.nesterov)
 
+    def _sparse_hp(self):
+        return {"momentum": float(self.momentum), "use_nesterov": bool(self.nesterov)}
+
 
 class AdamOptimizer(Optimizer):
     _kind = "adam"
@@ -528,6 +550,9 @@ class AdamOptimizer(Optimizer):
 
     def _make_fused(self, params):
         return _optim.FusedAdam(params, self._lr_value(), self.beta1, self.beta2, self.epsilon)
+
+    def _sparse_hp(self):
+        return {"beta1": float(self.beta1), "beta2": float(self.beta2), "epsilon": float(self.epsilon)}
 
     def _register_slots(self, vars_, fused):
         super()._register_slots(vars_, fused)
@@ -572,6 +597,9 @@ class AdagradOptimizer(Optimizer):
     def _make_fused(self, params):
         return _optim.FusedAdagrad(params, self._lr_value(), self.init_acc)
 
+    def _sparse_hp(self):
+        return {"initial_accumulator_value": float(self.init_acc)}
+
     def _slot_init(self, sname: str) -> float:
         return float(self.init_acc)
 
@@ -589,6 +617,9 @@ class RMSPropOptimizer(Optimizer):
 
     def _make_fused(self, params):
         return _optim.FusedRMSProp(params, self._lr_value(), self.decay, self.mom, self.eps)
+
+    def _sparse_hp(self):
+        return {"decay": float(self.decay), "momentum": float(self.mom), "epsilon": float(self.eps)}
 
     def _slot_init(self, sname: str) -> float:
         return 1.0 if sname == "RMSProp" else 0.0      # TF initialises the mean square to ones

@@ -14,8 +14,10 @@ replica_device_setter, one shard per rank, all-to-all lookups/updates
 sized for 288 GB HBM per shard); the dense tower is replicated and its
 gradients travel in one flat bucket all-reduce (RCCL over xGMI) that is
 launched on a side stream while the sparse all-to-all updates run.
-Embedding rows use sparse SGD (the ps-side ScatterSub of TF), the tower
-uses SGD or TF-Adam through the fused multi-tensor kernel.
+Embedding rows use sparse SGD (the ps-side ScatterSub of TF) or TF's sparse
+Adagrad / Momentum / RMSProp / Adam rules (`sparse_opt`, applied by the row
+owner: ShardedEmbedding.set_optimizer), the tower uses SGD or TF-Adam
+through the fused multi-tensor kernel.
 """
 from __future__ import annotations
 
@@ -33,7 +35,8 @@ class WideDeep(StaticStepMixin):
     def __init__(self, num_features: int, emb_dim: int = 64, hidden: Sequence[int] = (256, 128),
                  lr: float = 0.05, dense_lr: Optional[float] = None, dense_opt: str = "sgd", combiner: str = "sum",
                  world: Optional[World] = None, seed: int = 1, device=None, emb_std: float = 0.05,
-                 ids_capacity: Optional[int] = None, rows: int = 4096, peer_capacity: Optional[int] = None):
+                 ids_capacity: Optional[int] = None, rows: int = 4096, peer_capacity: Optional[int] = None,
+                 sparse_opt: str = "sgd", sparse_hp: Optional[dict] = None):
         self.world = world or get_world()
         self.device = torch.device(device) if device is not None else self.world.device
         self.lr = float(lr)
@@ -47,6 +50,9 @@ class WideDeep(StaticStepMixin):
         self.emb = ShardedEmbedding(num_features, emb_dim, self.world, init_std=emb_std, seed=seed + 1,
                                     device=self.device, name="deep/embedding", capacity=ids_capacity,
                                     router=self.wide.router)
+        # the tables' owner-side rule: sgd (TF ScatterSub) | adagrad | momentum | rmsprop | adam
+        for t in (self.wide, self.emb):
+            t.set_optimizer(sparse_opt, **(sparse_hp or {}))
         self.rows = int(rows)              # batch rows of the captured step
         self._window = []                  # static steps since the router's last check (replay source)
         self._example = None
@@ -127,7 +133,8 @@ class WideDeep(StaticStepMixin):
             return self._train_step((labels, offsets, ids, vals))
 
         def state():   # everything a step mutates, restored after the capture's warmup
-            st = [self.wide.local, self.emb.local] + [p.data for p in self.dense_params] + [self.opt.step_t]
+            st = self.wide.state_tensors() + self.emb.state_tensors() + [p.data for p in self.dense_params]
+            st += [self.opt.step_t]
             st += [t for t in list(self.opt.m) + list(self.opt.v) if t is not None]
             return st + (self.wide.router.state() if self.wide.router is not None else [])
         self._graphed = GraphedStep(step, state, strict=strict)
@@ -161,7 +168,7 @@ class WideDeep(StaticStepMixin):
             else:
                 self.world.all_reduce(self.flat_grad)
         grads = [r.grad if r.grad is not None else torch.zeros_like(r) for r in (wrows, erows)]
-        apply_sgd_shared([self.wide, self.emb], lctx, grads, [self.lr / ws] * 2)
+        apply_sgd_shared([self.wide, self.emb], lctx, grads, [self.lr] * 2, grad_scale=1.0 / ws)
         if ev is not None:
             torch.cuda.current_stream().wait_event(ev)
         # a voided step (sharded exchange overflow on some rank) leaves the tower,
@@ -177,6 +184,9 @@ class WideDeep(StaticStepMixin):
 
     def checkpoint_tensors(self):
         local = {self.wide.name: self.wide, self.emb.name: self.emb}   # TF partitioned variables
+        for t in (self.wide, self.emb):                                 # their optimizer slots, sharded alike
+            for sname in t.slots:
+                local[f"{t.name}/{sname}"] = t.slot_view(sname)
         names = []
         for i in range(len(self.layers) // 2):
             names += [f"deep/dense_{i}/kernel", f"deep/dense_{i}/bias"]

@@ -40,6 +40,7 @@ fixed_size_partitioner slices, see ckpt/__init__.py).
 """
 from __future__ import annotations
 
+import copy
 from typing import Optional
 
 import torch
@@ -177,6 +178,10 @@ class ShardedEmbedding:
         # asynchronous (Hogwild) mode: every shard mapped into every rank
         # (parallel/async_ps.HogwildTable); lookups / updates bypass the exchange
         self.hogwild = None
+        # owner-side update rule of the sparse gradients (set_optimizer)
+        self.opt_kind, self.opt_hp, self.slots = "sgd", {}, {}
+        self._gacc = None
+        self._adam = None
         n_local = (self.num_rows - self.rank + self.W - 1) // self.W if self.rank < self.num_rows else 0
         self.local = torch.empty((n_local, self.dim), dtype=torch.float32, device=self.device)
         with torch.no_grad():
@@ -265,20 +270,110 @@ class ShardedEmbedding:
         ctx = self.route(ids)
         return lookup_shared([self], ctx)[0], ctx
 
-    def apply_sgd(self, ctx: LookupCtx, grad_rows: torch.Tensor, lr: float):
-        """local[owner rows] -= lr * grad (grad_rows aligned with ctx.uniq)."""
+    def apply_sgd(self, ctx: LookupCtx, grad_rows: torch.Tensor, lr: float, grad_scale: float = 1.0):
+        """The owner-side update of the rows of ctx.uniq (grad_rows aligned with
+        it): `local[rows] -= lr * grad_scale * grad` with the default SGD rule,
+        else the rule of `set_optimizer`."""
         if ctx.hogwild:
-            self.hogwild.scatter_sgd(ctx.uniq, grad_rows, lr)
+            if self.opt_kind != "sgd":
+                raise NotImplementedError("asynchronous (Hogwild) table updates: SGD only")
+            self.hogwild.scatter_sgd(ctx.uniq, grad_rows, lr * grad_scale)
             return
-        apply_sgd_shared([self], ctx, [grad_rows], [lr])
+        apply_sgd_shared([self], ctx, [grad_rows], [lr], grad_scale)
 
-    def _sgd_local(self, ctx: LookupCtx, g: torch.Tensor, lr: float):
+    # ------------------------------------------------------------------ optimizer
+    def set_optimizer(self, kind: str = "sgd", **hp):
+        """The owner-side update of this table's sparse gradients, TensorFlow's
+        sparse-apply semantics (duplicates summed, then each touched row):
+
+          sgd       var -= lr g                                  (ScatterSub / SparseApplyGradientDescent)
+          momentum  acc = mu acc + g; var -= lr acc (nesterov)   slot Momentum   (hp: momentum, use_nesterov)
+          adagrad   acc += g^2; var -= lr g / sqrt(acc)          slot Adagrad    (hp: initial_accumulator_value)
+          rmsprop   ms / mom as tf.train.RMSPropOptimizer        slots RMSProp, Momentum (hp: decay, momentum, epsilon)
+          adam      tf.train.AdamOptimizer's _apply_sparse: m, v decay on EVERY row of the shard,
+                    the step moves every row (dense over the shard)  slots Adam, Adam_1 (hp: beta1, beta2, epsilon)
+
+        Row-local rules run one kernel over the step's touched rows
+        (csrc/kernels/sparse_optim.hip); Adam runs the fused multi-tensor Adam
+        over the shard.  Slots are sharded like the table (`slot_view`)."""
+        if kind not in ("sgd", "momentum", "adagrad", "rmsprop", "adam"):
+            raise ValueError(f"{self.name}: no sparse update rule '{kind}'")
+        if kind == self.opt_kind and hp == self.opt_hp:
+            return
+        self.opt_kind, self.opt_hp = kind, dict(hp)
+        self.slots, self._adam = {}, None
+        z = torch.zeros_like(self.local)
+        if kind == "momentum":
+            self.slots["Momentum"] = z
+        elif kind == "adagrad":
+            self.slots["Adagrad"] = z.fill_(float(hp.get("initial_accumulator_value", 0.1)))
+        elif kind == "rmsprop":
+            self.slots["RMSProp"] = torch.ones_like(self.local)
+            self.slots["Momentum"] = z
+        elif kind == "adam":
+            from .. import optim
+            self._adam = optim.FusedAdam([self.local], 0.001, float(hp.get("beta1", 0.9)),
+                                         float(hp.get("beta2", 0.999)), float(hp.get("epsilon", 1e-8)))
+            self.slots["Adam"], self.slots["Adam_1"] = self._adam.m[0], self._adam.v[0]
+        # [local rows + 1 dump row] accumulator of a step's summed gradients, zero between steps
+        self._gacc = None if kind == "sgd" else torch.zeros((self.local.shape[0] + 1, self.dim),
+                                                            dtype=torch.float32, device=self.device)
+
+    def slot_view(self, slot: str) -> "ShardedEmbedding":
+        """The slot as a table of the same geometry (checkpoint save / restore)."""
+        v = copy.copy(self)
+        v.local, v.name = self.slots[slot], f"{self.name}/{slot}"
+        v.router, v.hogwild, v.slots, v.opt_kind, v._gacc, v._adam = None, None, {}, "sgd", None, None
+        return v
+
+    def state_tensors(self):
+        """Everything an update mutates (graph-capture warmup save / restore)."""
+        st = [self.local] + list(self.slots.values())
+        return st + ([self._adam.step_t] if self._adam is not None else [])
+
+    def _sgd_local(self, ctx: LookupCtx, g: torch.Tensor, lr: float, grad_scale: float = 1.0,
+                   void: Optional[torch.Tensor] = None):
         n = g.shape[0]
         if n == 0:
             return
+        if self.opt_kind != "sgd":
+            self._apply_local(ctx.recv_local, g, lr, grad_scale, void)
+            return
         offs = torch.arange(n + 1, dtype=torch.int64, device=self.device)
         with torch.no_grad():
-            ops.embedding_bag_sgd_(self.local, ctx.recv_local, offs, None, g, float(lr))
+            ops.embedding_bag_sgd_(self.local, ctx.recv_local, offs, None, g, float(lr) * grad_scale)
+
+    @torch.no_grad()
+    def _apply_local(self, idx: torch.Tensor, g: torch.Tensor, lr: float, grad_scale: float,
+                     void: Optional[torch.Tensor]):
+        """idx[i]: local row of gradient row i (-1: padding); rows may repeat
+        (several ranks looked the same row up).  Fixed shapes throughout -- no
+        host read-back, so the update is capturable."""
+        nl = self.local.shape[0]
+        i = torch.where(idx >= 0, idx, torch.full_like(idx, nl))
+        self._gacc.index_add_(0, i, g if grad_scale == 1.0 else g * grad_scale)
+        s, _ = torch.sort(i)
+        hp = self.opt_hp
+        if self.opt_kind == "adam":
+            self._adam.set_lr(lr)
+            self._adam.step([self._gacc[:nl]], skip=void)
+        else:
+            head = torch.ones_like(s, dtype=torch.bool)
+            head[1:] = s[1:] != s[:-1]
+            rows = torch.where(head & (s < nl), s, torch.full_like(s, -1))    # each touched row once
+            gsum = self._gacc.index_select(0, s)
+            kind = {"momentum": 1, "adagrad": 4, "rmsprop": 5}[self.opt_kind]
+            sa = self.slots.get("Adagrad", self.slots.get("RMSProp", self.slots.get("Momentum")))
+            sb = self.slots.get("Momentum") if self.opt_kind == "rmsprop" else None
+            mu = float(hp.get("momentum", 0.0))
+            args = (kind, float(lr), mu, bool(hp.get("use_nesterov", False)), float(hp.get("decay", 0.9)),
+                    float(hp.get("epsilon", 1e-10)))
+            if self.local.is_cuda:
+                ops._C().sparse_rows_apply(self.local, sa, sb, rows, gsum, *args,
+                                           skip=None if void is None else void.reshape(-1)[:1].to(torch.int32))
+            else:
+                _rows_apply_torch(self.local, sa, sb, rows, gsum, *args, skip=void)
+        self._gacc.index_fill_(0, s, 0.0)
 
     # ------------------------------------------------------------------ bags
     def bag_forward(self, ids, offsets, weights=None, mode: str = "sum"):
@@ -351,9 +446,36 @@ def lookup_shared(tables, ctx: LookupCtx):
     return list(rows.split(dims, 1)) if len(tables) > 1 else [rows]
 
 
-def apply_sgd_shared(tables, ctx: LookupCtx, grads, lrs):
-    """Sparse SGD on every table; the gradients travel to the owners in ONE
-    all-to-all (columns side by side, same routing as `lookup_shared`)."""
+def _rows_apply_torch(table, sa, sb, rows, g, kind, lr, mu, nesterov, rho, eps, skip=None):
+    """CPU twin of csrc/kernels/sparse_optim.hip (same per-row math)."""
+    if skip is not None and int(skip.reshape(-1)[0]) != 0:
+        return
+    keep = rows >= 0
+    r, gg = rows[keep], g[keep]
+    var = table[r]
+    if kind == 1:
+        acc = mu * sa[r] + gg
+        sa[r] = acc
+        table[r] = var - lr * (gg + mu * acc if nesterov else acc)
+    elif kind == 4:
+        acc = sa[r] + gg * gg
+        sa[r] = acc
+        table[r] = var - lr * gg * torch.rsqrt(acc)
+    elif kind == 5:
+        ms = rho * sa[r] + (1 - rho) * gg * gg
+        mom = mu * sb[r] + lr * gg * torch.rsqrt(ms + eps)
+        sa[r], sb[r] = ms, mom
+        table[r] = var - mom
+    else:
+        table[r] = var - lr * gg
+
+
+def apply_sgd_shared(tables, ctx: LookupCtx, grads, lrs, grad_scale: float = 1.0):
+    """The sparse update of every table (each table's `set_optimizer` rule,
+    SGD by default); the gradients travel to the owners in ONE all-to-all
+    (columns side by side, same routing as `lookup_shared`).  `grad_scale`
+    multiplies the gradients (e.g. 1/W: the sync average) -- for SGD it is
+    folded into the learning rate."""
     _check_shared(tables)
     t0 = tables[0]
     gs = [g.float().reshape(-1, t.dim) for t, g in zip(tables, grads)]
@@ -372,7 +494,7 @@ def apply_sgd_shared(tables, ctx: LookupCtx, grads, lrs):
         t0.world.all_to_all(g_sorted, ctx.send, recv_g, ctx.recv)
         gs = list(recv_g.split([t.dim for t in tables], 1))
     for t, g, lr in zip(tables, gs, lrs):
-        t._sgd_local(ctx, g.contiguous(), lr)
+        t._sgd_local(ctx, g.contiguous(), lr, grad_scale, ctx.void)
 
 
 def _max_route_world() -> int:

@@ -69,6 +69,8 @@ def main():
     ap.add_argument("--nnz", type=int, default=32, help="features per sample")
     ap.add_argument("--gpus", type=int, default=None)
     ap.add_argument("--lr", type=float, default=None, help="sparse models: SGD learning rate")
+    ap.add_argument("--sparse-opt", default="sgd", choices=["sgd", "adagrad", "momentum", "rmsprop", "adam"],
+                    help="wide_deep: the tables' owner-side update rule")
     ap.add_argument("--graph", action="store_true", help="sparse_lr / lr2 / wide_deep: replay each step as one captured hipGraph")
     ap.add_argument("--trace-marker", action="store_true",
                     help="launch a spin kernel right before the timed loop, so a kernel trace can be cut to the "
@@ -96,12 +98,12 @@ def main():
 
         m = WideDeep(a.features, emb_dim=a.emb_dim, hidden=(512, 256), lr=0.05, dense_opt="adam",
                      dense_lr=1e-3, world=w, ids_capacity=a.batch * a.nnz if (a.graph or w.world_size > 1) else None,
-                     rows=a.batch)
+                     rows=a.batch, sparse_opt=a.sparse_opt)
         if a.graph:
             m.enable_graph()
         cfg = {"model": f"wide_deep F={a.features} D={a.emb_dim} tower=512-256-1", "global_batch": a.batch * w.world_size,
                "per_gpu_batch": a.batch, "seq_len": None, "parallelism": f"dp{w.world_size}+emb-shard{w.world_size}",
-               "nnz_per_sample": a.nnz, "graph": bool(a.graph)}
+               "nnz_per_sample": a.nnz, "graph": bool(a.graph), "sparse_opt": a.sparse_opt}
     else:
         from distributed_tensorflow_example_amd.models.sparse_lr import SparseLRTrainer
 

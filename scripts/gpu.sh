@@ -23,8 +23,10 @@
 #   lowering      compat-graph lowering tests + bench_graph_step
 #   models        BERT-base / ResNet-50 / sparse benches (scripts/bench_models.py)
 #   bert_prof     rocprofv3 kernel stats of BERT-base B=128
-#   gemm          in-tree GEMM vs hipBLASLt (scripts/bench_gemm.py)
-#   sparse        sparse LR / Wide&Deep GPU tests + benches
+#   gemm          gemm_big numerics / race-screen tests, then in-tree GEMM vs
+#                 hipBLASLt (scripts/bench_gemm.py)
+#   gemm_sweep    gemm_big schedules vs hipBLASLt over K (fixed vs per-K-tile cost)
+#   sparse        sparse LR / Wide&Deep / sparse-optimizer GPU tests + benches
 # Env: STEP_ARGS_<step> adds arguments to that step's main command.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -85,9 +87,12 @@ for step in "$@"; do
       run bert_prof 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_bert -o run -- \
         python3 scripts/bench_models.py --model bert_base --batch 128 --steps 10 --warmup 3 $extra
       python3 scripts/prof_summary.py $OUT/prof_bert/run_kernel_trace.csv --steps 13 --top 40 > $OUT/prof_bert_summary.txt ;;
-    gemm) run gemm 400 python scripts/bench_gemm.py $extra ;;
+    gemm_sweep) run gemm_sweep 300 python scripts/probes/gemm_k_sweep.py $extra ;;
+    gemm)
+      run gemm_tests 500 $PYT -x tests/test_gemm_big_gpu.py
+      run gemm 400 python scripts/bench_gemm.py $extra ;;
     sparse)
-      run sparse_tests 500 $PYT -x tests/test_models_gpu.py tests/test_async_ps_gpu.py $extra
+      run sparse_tests 500 $PYT -x tests/test_models_gpu.py tests/test_async_ps_gpu.py tests/test_sparse_optim_gpu.py $extra
       run bench_lr2 300 python scripts/bench_models.py --model sparse_lr --graph
       run bench_wd 300 python scripts/bench_models.py --model wide_deep --graph ;;
     *) echo "unknown step: $step"; exit 2 ;;

@@ -19,8 +19,8 @@ hipError_t dtfk_sparse_rows_apply(float* table, float* slot_a, float* slot_b, co
                                   const int* skip, hipStream_t s);
 hipError_t dtfk_hogwild_scatter_sgd(const long long* ids, const float* g, int n, int D, float* const* shards, int W,
                                     float lr, int locking, hipStream_t s);
-hipError_t dtfk_bucket_pack_bf16(const float* g, uint16_t* c, int64_t n, float scale, hipStream_t s);
-hipError_t dtfk_bucket_unpack_bf16(const uint16_t* c, float* g, int64_t n, float scale, hipStream_t s);
+hipError_t dtfk_bucket_pack(const float* g, uint16_t* c, int64_t n, float scale, int fp16, hipStream_t s);
+hipError_t dtfk_bucket_unpack(const uint16_t* c, float* g, int64_t n, float scale, int fp16, hipStream_t s);
 int dtfk_route_max_world();
 hipError_t dtfk_route_flags(const void* sids, int ids32, int N, int W, int* flag, int* onehot, hipStream_t stream);
 hipError_t dtfk_route_scatter(const void* sids, int ids32, const int64_t* perm, const int* incl, const int* owncum,
@@ -33,7 +33,8 @@ hipError_t dtfk_gemm(const void* A, int a_bf16, int lda, int transA, const void*
                      int K, float alpha, float beta, int act, hipStream_t stream);
 hipError_t dtfk_gemm_big(const void* A, int lda, int transA, const void* B, int ldb, int transB, void* C,
                          int c_bf16, int ldc, const float* bias, int M, int N, int K, float alpha, float beta,
-                         int act, int split_k, int variant, hipStream_t stream);
+                         int act, int split_k, int variant, void* ws, hipStream_t stream);
+long long dtfk_gemm_big_workspace(int M, int N, int K, int c_bf16, float beta, int act, int split_k, int variant);
 int dtfk_gemm_big_supported(const void* A, int lda, int transA, const void* B, int ldb, int transB, int c_bf16, int M,
                             int N, int K, float beta, int act, int split_k);
 hipError_t dtfk_gemm_big_cfg(int cfg, const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N,
@@ -146,8 +147,14 @@ bool gemm_big(at::Tensor A, bool transA, at::Tensor B, bool transB, at::Tensor o
   if (!dtfk_gemm_big_supported(A.data_ptr(), (int)A.stride(0), transA, B.data_ptr(), (int)B.stride(0), transB, obf, M,
                                N, K, (float)beta, act, split_k))
     return false;   // outside the kernel's contract: the caller picks another GEMM
+  // split-K slabs: an fp32 workspace from the caching allocator (freed -- and
+  // reusable -- once the stream has passed the reduction)
+  const long long wsb = dtfk_gemm_big_workspace(M, N, K, obf, (float)beta, act, split_k, variant);
+  at::Tensor ws;
+  if (wsb > 0) ws = at::empty({wsb / 4}, A.options().dtype(at::kFloat));
   ck(dtfk_gemm_big(A.data_ptr(), (int)A.stride(0), transA, B.data_ptr(), (int)B.stride(0), transB, out.data_ptr(), obf,
-                   (int)out.stride(0), opt_ptr<float>(bias), M, N, K, (float)alpha, (float)beta, act, split_k, variant, cs()),
+                   (int)out.stride(0), opt_ptr<float>(bias), M, N, K, (float)alpha, (float)beta, act, split_k, variant,
+                   wsb > 0 ? ws.data_ptr() : nullptr, cs()),
      "gemm_big");   // any launch error is a real error
   return true;
 }
@@ -366,26 +373,28 @@ std::vector<at::Tensor> sparse_route(at::Tensor sids, at::Tensor perm, int W, in
   return {inv, inverse, uniq, dest, send, count, ocnt};
 }
 
-// DDP bucket <-> bf16 comm buffer with the 1/N scale folded in (csrc/kernels/ops.hip K16).
-void bucket_pack_bf16(at::Tensor g, at::Tensor c, double scale) {
+// DDP bucket <-> 16-bit (bf16 / fp16) comm buffer with the 1/N scale folded in
+// (csrc/kernels/ops.hip K16); the comm buffer's dtype picks the format.
+static int comm16(const at::Tensor& g, const at::Tensor& c, const char* who) {
   f32c(g, "grad bucket"); gpu(c, "comm buffer");
-  if (c.scalar_type() != at::kBFloat16 || !c.is_contiguous() || c.numel() != g.numel())
-    throw std::runtime_error("bucket_pack_bf16: contiguous bf16 comm buffer of the bucket's size expected");
+  if ((c.scalar_type() != at::kBFloat16 && c.scalar_type() != at::kHalf) || !c.is_contiguous() ||
+      c.numel() != g.numel())
+    throw std::runtime_error(std::string(who) + ": contiguous bf16 / fp16 comm buffer of the bucket's size expected");
   if ((reinterpret_cast<uintptr_t>(g.data_ptr()) & 15) || (reinterpret_cast<uintptr_t>(c.data_ptr()) & 15))
-    throw std::runtime_error("bucket_pack_bf16: 16-byte aligned buffers expected");
-  ck(dtfk_bucket_pack_bf16(g.data_ptr<float>(), reinterpret_cast<uint16_t*>(c.data_ptr()), g.numel(), (float)scale,
-                           cs()),
-     "bucket_pack_bf16");
+    throw std::runtime_error(std::string(who) + ": 16-byte aligned buffers expected");
+  return c.scalar_type() == at::kHalf;
 }
-void bucket_unpack_bf16(at::Tensor c, at::Tensor g, double scale) {
-  f32c(g, "grad bucket"); gpu(c, "comm buffer");
-  if (c.scalar_type() != at::kBFloat16 || !c.is_contiguous() || c.numel() != g.numel())
-    throw std::runtime_error("bucket_unpack_bf16: contiguous bf16 comm buffer of the bucket's size expected");
-  if ((reinterpret_cast<uintptr_t>(g.data_ptr()) & 15) || (reinterpret_cast<uintptr_t>(c.data_ptr()) & 15))
-    throw std::runtime_error("bucket_unpack_bf16: 16-byte aligned buffers expected");
-  ck(dtfk_bucket_unpack_bf16(reinterpret_cast<const uint16_t*>(c.data_ptr()), g.data_ptr<float>(), g.numel(),
-                             (float)scale, cs()),
-     "bucket_unpack_bf16");
+void bucket_pack(at::Tensor g, at::Tensor c, double scale) {
+  const int f16 = comm16(g, c, "bucket_pack");
+  ck(dtfk_bucket_pack(g.data_ptr<float>(), reinterpret_cast<uint16_t*>(c.data_ptr()), g.numel(), (float)scale, f16,
+                      cs()),
+     "bucket_pack");
+}
+void bucket_unpack(at::Tensor c, at::Tensor g, double scale) {
+  const int f16 = comm16(g, c, "bucket_unpack");
+  ck(dtfk_bucket_unpack(reinterpret_cast<const uint16_t*>(c.data_ptr()), g.data_ptr<float>(), g.numel(),
+                        (float)scale, f16, cs()),
+     "bucket_unpack");
 }
 
 // Hogwild parameter store (csrc/kernels/hogwild.hip): `shared` / `counter` are
@@ -466,8 +475,10 @@ void init_ops(py::module& m) {
         py::arg("locking"), py::arg("counter"), py::arg("gstep_out"));
   m.def("hogwild_counter", &hogwild_counter, py::arg("counter"), py::arg("out"), py::arg("set") = 0,
         py::arg("do_set") = false);
-  m.def("bucket_pack_bf16", &bucket_pack_bf16);
-  m.def("bucket_unpack_bf16", &bucket_unpack_bf16);
+  m.def("bucket_pack", &bucket_pack, py::arg("g"), py::arg("c"), py::arg("scale"));
+  m.def("bucket_unpack", &bucket_unpack, py::arg("c"), py::arg("g"), py::arg("scale"));
+  m.def("bucket_pack_bf16", &bucket_pack);     // round-2 names
+  m.def("bucket_unpack_bf16", &bucket_unpack);
   m.def("sparse_route", &sparse_route, py::arg("sids"), py::arg("perm"), py::arg("W"), py::arg("cap"));
   m.def("route_max_world", &dtfk_route_max_world);
   m.def("philox_normal", &philox_normal, py::arg("out"), py::arg("row_mul"), py::arg("row_add"), py::arg("seed"),

@@ -425,11 +425,11 @@ __device__ __forceinline__ void raw_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <bool AKC, bool BKC, bool OBF>
+template <bool AKC, bool BKC, bool OBF, bool SW>
 __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A, int lda,
                                                  const uint16_t* __restrict__ B, int ldb, void* __restrict__ C,
                                                  int ldc, const float* __restrict__ bias, int M, int N, int K,
-                                                 float alpha, float beta, int act, int kchunk) {
+                                                 float alpha, float beta, int act, int kchunk, long long slab = 0) {
   constexpr int BM = 256, BK = 64, HALF = 128 * BK * 2, BUF = 4 * HALF;   // A_q0 A_q1 B_q0 B_q1
   constexpr int NA = AKC ? 8 : 16;                                       // LDS instructions of one A-fragment set
   __shared__ __attribute__((aligned(1024))) uint8_t smem[2 * BUF];
@@ -483,7 +483,8 @@ __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A,
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[qm * 4 + i][qn * 2 + j] = mfma16x16x32(fa[s][i], fb[qn][s][j], acc[qm * 4 + i][qn * 2 + j]);
+          acc[qm * 4 + i][qn * 2 + j] = SW ? mfma16x16x32(fb[qn][s][j], fa[s][i], acc[qm * 4 + i][qn * 2 + j])
+                                           : mfma16x16x32(fa[s][i], fb[qn][s][j], acc[qm * 4 + i][qn * 2 + j]);
     __builtin_amdgcn_s_setprio(0);
     raw_barrier();
   };
@@ -538,37 +539,203 @@ __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A,
     mma(1, 0);
   }
   if (!wr) raw_barrier();   // equal barrier counts for both wave rows
+  if (act < 0) return;      // probe only (dtfk_gemm_big_cfg 11): the loop without the epilogue
 
-  const bool split = gridDim.y > 1;
+  if constexpr (!SW) {
+    // split-K (fp32, linear): accumulators in MFMA layout -- lane l holds rows
+    // 4 (l >> 4) .. +3 of column (l & 15), so each atomic instruction covers
+    // 16 consecutive columns of 4 rows (4 cache lines, not 16)
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int n = n0 + wc * 64 + j * 16 + (lane & 15);
-    if (n >= N) continue;
-    const float bv = (bias != nullptr) ? bias[n] : 0.f;
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wc * 64 + j * 16 + (lane & 15);
+      if (n >= N) continue;
+      const float bv = (bias != nullptr && blockIdx.y == 0) ? bias[n] : 0.f;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wr * 128 + i * 16 + 4 * (lane >> 4) + r;
+          if (m < M) atomicAdd(reinterpret_cast<float*>(C) + (size_t)m * ldc + n, alpha * acc[i][j][r] + bv);
+        }
+    }
+    return;
+  }
+  // split-K into slabs (fp32 partial products, summed by slab_reduce): this
+  // K range's partial tile is a plain tile of slab blockIdx.y
+  if (slab > 0) C = reinterpret_cast<float*>(C) + blockIdx.y * slab;
+  // The MFMAs ran with swapped operands (B fragment first): each accumulator
+  // is the 16x16 tile TRANSPOSED, so lane l holds output row (l & 15) and the
+  // 4 consecutive columns 4 (l >> 4) .. +3 -- one 8-byte (bf16) / 16-byte
+  // (fp32) store per tile instead of four 2- / 4-byte ones.
+  const bool vec = (ldc & 7) == 0 && (reinterpret_cast<uintptr_t>(C) & 15) == 0;
+  const int mrow = m0 + wr * 128 + (lane & 15), ncol = n0 + wc * 64 + 4 * (lane >> 4);
+  if (vec && m0 + BM <= M && n0 + BN <= N) {
+    // interior tile: no per-lane bounds, only wave-uniform branches (an
+    // exec-masked branch per element costs more than the stores themselves)
+    float bv[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bv[j][r] = bias != nullptr ? bias[ncol + j * 16 + r] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const size_t o = (size_t)(mrow + i * 16) * ldc + ncol + j * 16;
+        float z[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) z[r] = alpha * acc[i][j][r] + bv[j][r];
+        if (beta != 0.f) {
+          if constexpr (OBF) {
+            const uint2 c = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(C) + o);
+            z[0] += beta * bf2f((uint16_t)(c.x & 0xffff));
+            z[1] += beta * bf2f((uint16_t)(c.x >> 16));
+            z[2] += beta * bf2f((uint16_t)(c.y & 0xffff));
+            z[3] += beta * bf2f((uint16_t)(c.y >> 16));
+          } else {
+            const float4 c = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(C) + o);
+            z[0] += beta * c.x; z[1] += beta * c.y; z[2] += beta * c.z; z[3] += beta * c.w;
+          }
+        }
+        if (act != ACT_NONE) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) z[r] = apply_act_slow(z[r], act);
+        }
+        // (non-temporal stores measured 1.2-1.4x slower here: profiles/gemm_8ph_r3.txt)
+        if constexpr (OBF)
+          *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(C) + o) = make_uint2(pack2bf(z[0], z[1]), pack2bf(z[2], z[3]));
+        else
+          *reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + o) = make_float4(z[0], z[1], z[2], z[3]);
+      }
+    return;
+  }
+  const bool split = false;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wr * 128 + i * 16 + (lane & 15);
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wc * 64 + j * 16 + 4 * (lane >> 4);
+      if (n >= N) continue;
+      const size_t o = (size_t)m * ldc + n;
+      const bool full = vec && n + 3 < N;
+      float z[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wr * 128 + i * 16 + 4 * (lane >> 4) + r;
-        if (m >= M) continue;
-        const size_t o = (size_t)m * ldc + n;
-        if (split) {
-          atomicAdd(reinterpret_cast<float*>(C) + o, alpha * acc[i][j][r] + (blockIdx.y == 0 ? bv : 0.f));
-          continue;
+        const float bv = (bias != nullptr && n + r < N && (!split || blockIdx.y == 0)) ? bias[n + r] : 0.f;
+        z[r] = alpha * acc[i][j][r] + bv;
+      }
+      if (split) {   // linear fp32 epilogue (host-checked): partial sums meet in C
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (n + r < N) atomicAdd(reinterpret_cast<float*>(C) + o + r, z[r]);
+        continue;
+      }
+      if (beta != 0.f) {
+        if constexpr (OBF) {
+          if (full) {
+            const uint2 c = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(C) + o);
+            z[0] += beta * bf2f((uint16_t)(c.x & 0xffff));
+            z[1] += beta * bf2f((uint16_t)(c.x >> 16));
+            z[2] += beta * bf2f((uint16_t)(c.y & 0xffff));
+            z[3] += beta * bf2f((uint16_t)(c.y >> 16));
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (n + r < N) z[r] += beta * bf2f(reinterpret_cast<const uint16_t*>(C)[o + r]);
+          }
+        } else {
+          if (full) {
+            const float4 c = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(C) + o);
+            z[0] += beta * c.x; z[1] += beta * c.y; z[2] += beta * c.z; z[3] += beta * c.w;
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (n + r < N) z[r] += beta * reinterpret_cast<const float*>(C)[o + r];
+          }
         }
-        float z = alpha * acc[i][j][r] + bv;
-        if (beta != 0.f)
-          z += beta * (OBF ? bf2f(reinterpret_cast<const uint16_t*>(C)[o]) : reinterpret_cast<const float*>(C)[o]);
-        const float y = apply_act(z, act);
-        if constexpr (OBF) reinterpret_cast<uint16_t*>(C)[o] = f2bf(y);
-        else reinterpret_cast<float*>(C)[o] = y;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) z[r] = apply_act(z[r], act);
+      if constexpr (OBF) {
+        if (full) {
+          uint2 c;
+          c.x = (uint32_t)f2bf(z[0]) | ((uint32_t)f2bf(z[1]) << 16);
+          c.y = (uint32_t)f2bf(z[2]) | ((uint32_t)f2bf(z[3]) << 16);
+          *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(C) + o) = c;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (n + r < N) reinterpret_cast<uint16_t*>(C)[o + r] = f2bf(z[r]);
+        }
+      } else {
+        if (full) {
+          *reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + o) = make_float4(z[0], z[1], z[2], z[3]);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (n + r < N) reinterpret_cast<float*>(C)[o + r] = z[r];
+        }
       }
     }
   }
 }
 
+// C[m, n] = sum_s ws[s][m, n] + bias[n] + beta * C[m, n]: the split-K slabs of
+// gemm_8ph summed in slab order (deterministic), 4 columns per thread.
+__global__ __launch_bounds__(256) void slab_reduce(const float* __restrict__ ws, int S, long long slab,
+                                                   float* __restrict__ C, int ldc, int M, int N,
+                                                   const float* __restrict__ bias, float beta) {
+  const int nq = N / 4;
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long long)M * nq) return;
+  const int m = (int)(e / nq), n = (int)(e - (long long)m * nq) * 4;
+  const float* src = ws + (size_t)m * N + n;
+  f32x4 z = *reinterpret_cast<const f32x4*>(src);
+  for (int s = 1; s < S; ++s) z += *reinterpret_cast<const f32x4*>(src + s * slab);
+  if (bias != nullptr) z += f32x4{bias[n], bias[n + 1], bias[n + 2], bias[n + 3]};
+  float* dst = C + (size_t)m * ldc + n;
+  if (beta != 0.f) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) z[r] += beta * dst[r];
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) dst[r] = z[r];
+}
+
+// Split-K plan of one product: {split, kchunk, slab mode}.  Slab mode (the
+// 8-phase kernel, fp32 linear output, N % 4 == 0): ~one workgroup per CU,
+// partial tiles to a [split, M, N] fp32 workspace + slab_reduce -- plain
+// vector stores instead of per-element atomics.  Otherwise the atomic split
+// of gemm_big (partial tiles meet in C).
+struct SplitPlan { int split, kchunk, slabs; };
+static SplitPlan plan_split(int M, int N, int K, int c_bf16, float beta, int act, int split_k, bool ph8) {
+  using namespace dtfk::gemm2;
+  const int kq = ph8 ? 2 * KQ : KQ;
+  const long long tiles = (long long)((M + 255) / 256) * ((N + BN - 1) / BN);
+  const bool linear = act == ACT_NONE && !c_bf16 && (beta == 0.f || beta == 1.f);
+  SplitPlan p{1, K, 0};
+  if (!(split_k > 1 || (split_k <= 0 && linear && tiles < 256 && K >= 2048))) return p;
+  const bool slabs = ph8 && linear && N % 4 == 0;
+  int split = split_k > 1 ? split_k : (slabs ? (int)max(2LL, 256 / tiles) : (int)((512 + tiles - 1) / tiles));
+  split = min(split, K / (slabs ? 256 : 512) > 0 ? K / (slabs ? 256 : 512) : 1);
+  p.kchunk = ((K + split - 1) / split + kq - 1) / kq * kq;
+  p.split = (K + p.kchunk - 1) / p.kchunk;
+  p.slabs = slabs && p.split > 1;
+  return p;
+}
+
 }  // namespace gemm2
 }  // namespace dtfk
+
+// Bytes of fp32 workspace dtfk_gemm_big needs for this product (0: none).
+extern "C" long long dtfk_gemm_big_workspace(int M, int N, int K, int c_bf16, float beta, int act, int split_k,
+                                             int variant) {
+  const bool ph8 = variant == 8 || (variant == 0 && K % 128 == 0);
+  const dtfk::gemm2::SplitPlan p = dtfk::gemm2::plan_split(M, N, K, c_bf16, beta, act, split_k, ph8);
+  return p.slabs ? (long long)p.split * M * N * 4 : 0;
+}
 
 // The shape / alignment contract of dtfk_gemm_big, checked on the host before
 // any launch: callers pick another GEMM when it fails, and every error the
@@ -596,7 +763,8 @@ extern "C" int dtfk_gemm_big_supported(const void* A, int lda, int transA, const
 // (gemm_big VAR 4), 8 = 8-phase (hipErrorInvalidValue if K % 128).
 extern "C" hipError_t dtfk_gemm_big(const void* A, int lda, int transA, const void* B, int ldb, int transB,
                                     void* C, int c_bf16, int ldc, const float* bias, int M, int N, int K,
-                                    float alpha, float beta, int act, int split_k, int variant, hipStream_t stream) {
+                                    float alpha, float beta, int act, int split_k, int variant, void* ws,
+                                    hipStream_t stream) {
   using namespace dtfk::gemm2;
   const bool akc = !transA, bkc = transB != 0;
   if (!dtfk_gemm_big_supported(A, lda, transA, B, ldb, transB, c_bf16, M, N, K, beta, act, split_k))
@@ -604,19 +772,31 @@ extern "C" hipError_t dtfk_gemm_big(const void* A, int lda, int transA, const vo
   if (variant != 0 && variant != 4 && variant != 8) return hipErrorInvalidValue;
   const bool ph8 = variant == 8 || (variant == 0 && K % 128 == 0);
   if (ph8 && K % 128) return hipErrorInvalidValue;
-  const int kq = ph8 ? 2 * KQ : KQ;
   const int tn = (N + BN - 1) / BN;
   // 256 x 256 tiles even when they leave CUs idle (N = 768: 192 tiles): measured
   // faster than 128 x 256 at every BERT shape (scripts/probes/gemm_big_cfg.py)
-  const int BMsel = 256;
-  const long long tiles = (long long)((M + BMsel - 1) / BMsel) * tn;
-  int split = 1, kchunk = K;
-  const bool linear = act == ACT_NONE && !c_bf16 && (beta == 0.f || beta == 1.f);
-  if (split_k > 1 || (split_k <= 0 && linear && tiles < 256 && K >= 2048)) {
-    split = split_k > 1 ? split_k : (int)((512 + tiles - 1) / tiles);
-    split = min(split, K / 512 > 0 ? K / 512 : 1);
-    kchunk = ((K + split - 1) / split + kq - 1) / kq * kq;
-    split = (K + kchunk - 1) / kchunk;
+  const long long tiles = (long long)((M + 255) / 256) * tn;
+  const SplitPlan plan = plan_split(M, N, K, c_bf16, beta, act, split_k, ph8);
+  const int split = plan.split, kchunk = plan.kchunk;
+  if (plan.slabs && ws == nullptr) return hipErrorInvalidValue;   // dtfk_gemm_big_workspace bytes needed
+  if (plan.slabs) {
+    const long long slab = (long long)M * N;
+    const dim3 grid((unsigned)tiles, split), block(NTHR);
+    const uint16_t* a = static_cast<const uint16_t*>(A);
+    const uint16_t* b = static_cast<const uint16_t*>(B);
+#define DTFK_GS(AK, BKk)                                                                                       \
+  hipLaunchKernelGGL((gemm_8ph<AK, BKk, false, true>), grid, block, 0, stream, a, lda, b, ldb, ws, N, nullptr, M, \
+                     N, K, alpha, 0.f, 0, kchunk, slab)
+    if (akc) {
+      if (bkc) DTFK_GS(true, true); else DTFK_GS(true, false);
+    } else {
+      if (bkc) DTFK_GS(false, true); else DTFK_GS(false, false);
+    }
+#undef DTFK_GS
+    const long long work = (long long)M * (N / 4);
+    hipLaunchKernelGGL(slab_reduce, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, stream,
+                       static_cast<const float*>(ws), split, slab, static_cast<float*>(C), ldc, M, N, bias, beta);
+    return hipGetLastError();
   }
   if (split > 1 && beta == 0.f) {
     const hipError_t e = hipMemset2DAsync(C, (size_t)ldc * sizeof(float), 0, (size_t)N * sizeof(float), M, stream);
@@ -629,9 +809,12 @@ extern "C" hipError_t dtfk_gemm_big(const void* A, int lda, int transA, const vo
 // 32-deep 5-stage ring, 128-row tiles, register staging and the two-barrier
 // loop measured slower (profiles/gemm_big_cfg_r2.jsonl)
 #define DTFK_GB(AK, BKk, OB)                                                                                      \
-  if (ph8)                                                                                                       \
-    hipLaunchKernelGGL((gemm_8ph<AK, BKk, OB>), grid, block, 0, stream, a, lda, b, ldb, C, ldc, bias, M, N, K,    \
-                       alpha, split > 1 ? 1.f : beta, act, kchunk);                                              \
+  if (ph8 && split > 1)                                                                                          \
+    hipLaunchKernelGGL((gemm_8ph<AK, BKk, false, false>), grid, block, 0, stream, a, lda, b, ldb, C, ldc, bias, M, \
+                       N, K, alpha, 1.f, act, kchunk);                                                           \
+  else if (ph8)                                                                                                  \
+    hipLaunchKernelGGL((gemm_8ph<AK, BKk, OB, true>), grid, block, 0, stream, a, lda, b, ldb, C, ldc, bias, M, N, \
+                       K, alpha, beta, act, kchunk);                                                             \
   else                                                                                                           \
     hipLaunchKernelGGL((gemm_big<256, 64, 2, AK, BKk, OB, 4>), grid, block, 0, stream, a, lda, b, ldb, C, ldc, bias, \
                        M, N, K, alpha, split > 1 ? 1.f : beta, act, kchunk)
@@ -671,9 +854,10 @@ extern "C" hipError_t dtfk_gemm_big_cfg(int cfg, const void* A, int lda, const v
     case 8: DTFK_CFG(256, 64, 2, 3); break;
     case 9: DTFK_CFG(256, 64, 2, 4); break;
     case 10:
+    case 11:   // 11: the same without the epilogue (loop-cost probe; C is not written)
       if (K % 128) return hipErrorInvalidValue;
-      hipLaunchKernelGGL((gemm_8ph<true, true, true>), dim3((M / 256) * tn, 1), dim3(NTHR), 0, stream, a, lda, b, ldb,
-                         C, ldc, nullptr, M, N, K, 1.f, 0.f, 0, K);
+      hipLaunchKernelGGL((gemm_8ph<true, true, true, true>), dim3((M / 256) * tn, 1), dim3(NTHR), 0, stream, a, lda, b, ldb,
+                         C, ldc, nullptr, M, N, K, 1.f, 0.f, cfg == 11 ? -1 : 0, K);
       break;
     default: return hipErrorInvalidValue;
   }

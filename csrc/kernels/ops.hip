@@ -561,41 +561,59 @@ namespace dtfk {
 namespace ops {
 // ---------------------------------------------------------------------------
 // DDP bucket <-> communication buffer (K16): one pass each way.
-//   pack:   comm_bf16[i] = bf16(scale * grad_f32[i])   (the 1/N average folded in)
-//   unpack: grad_f32[i]  = scale * f32(comm_bf16[i])
-// 8 elements per thread (two 16-byte fp32 loads -> one 16-byte bf16 store);
-// replaces cast + copy-back + mul_ (three full-bucket passes) around a bf16
-// all-reduce.  Round-to-nearest-even like the cast it replaces.
-__global__ void bucket_pack_bf16(const float* __restrict__ g, uint16_t* __restrict__ c, int64_t n, float scale) {
+//   pack:   comm[i] = half(scale * grad_f32[i])   (the 1/N average folded in)
+//   unpack: grad_f32[i]  = scale * f32(comm[i])
+// half = bf16 or fp16 (F16).  8 elements per thread (two 16-byte fp32 loads ->
+// one 16-byte store); replaces cast + copy-back + mul_ (three full-bucket
+// passes) around a 16-bit all-reduce.  Round-to-nearest-even like the cast it
+// replaces (fp16 overflow -> inf, as the cast).
+template <bool F16>
+__device__ __forceinline__ uint32_t pack2h(float lo, float hi) {
+  if constexpr (F16) {
+    const _Float16 a = static_cast<_Float16>(lo), b = static_cast<_Float16>(hi);
+    return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
+  } else {
+    return pack2bf(lo, hi);
+  }
+}
+template <bool F16>
+__device__ __forceinline__ float h2f(uint32_t bits) {
+  if constexpr (F16) return static_cast<float>(__builtin_bit_cast(_Float16, (uint16_t)bits));
+  else return bf2f((uint16_t)bits);
+}
+
+template <bool F16>
+__global__ void bucket_pack(const float* __restrict__ g, uint16_t* __restrict__ c, int64_t n, float scale) {
   const int64_t n8 = n >> 3;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
     const float4 a = reinterpret_cast<const float4*>(g)[2 * i];
     const float4 b = reinterpret_cast<const float4*>(g)[2 * i + 1];
     uint4 o;
-    o.x = pack2bf(a.x * scale, a.y * scale);
-    o.y = pack2bf(a.z * scale, a.w * scale);
-    o.z = pack2bf(b.x * scale, b.y * scale);
-    o.w = pack2bf(b.z * scale, b.w * scale);
+    o.x = pack2h<F16>(a.x * scale, a.y * scale);
+    o.y = pack2h<F16>(a.z * scale, a.w * scale);
+    o.z = pack2h<F16>(b.x * scale, b.y * scale);
+    o.w = pack2h<F16>(b.z * scale, b.w * scale);
     reinterpret_cast<uint4*>(c)[i] = o;
   }
   for (int64_t i = (n8 << 3) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    c[i] = f2bf(g[i] * scale);
+    c[i] = (uint16_t)(pack2h<F16>(g[i] * scale, 0.f) & 0xFFFF);
 }
 
-__global__ void bucket_unpack_bf16(const uint16_t* __restrict__ c, float* __restrict__ g, int64_t n, float scale) {
+template <bool F16>
+__global__ void bucket_unpack(const uint16_t* __restrict__ c, float* __restrict__ g, int64_t n, float scale) {
   const int64_t n8 = n >> 3;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
     const uint4 u = reinterpret_cast<const uint4*>(c)[i];
     float4 a, b;
-    a.x = bf2f(u.x & 0xFFFF) * scale; a.y = bf2f(u.x >> 16) * scale;
-    a.z = bf2f(u.y & 0xFFFF) * scale; a.w = bf2f(u.y >> 16) * scale;
-    b.x = bf2f(u.z & 0xFFFF) * scale; b.y = bf2f(u.z >> 16) * scale;
-    b.z = bf2f(u.w & 0xFFFF) * scale; b.w = bf2f(u.w >> 16) * scale;
+    a.x = h2f<F16>(u.x & 0xFFFF) * scale; a.y = h2f<F16>(u.x >> 16) * scale;
+    a.z = h2f<F16>(u.y & 0xFFFF) * scale; a.w = h2f<F16>(u.y >> 16) * scale;
+    b.x = h2f<F16>(u.z & 0xFFFF) * scale; b.y = h2f<F16>(u.z >> 16) * scale;
+    b.z = h2f<F16>(u.w & 0xFFFF) * scale; b.w = h2f<F16>(u.w >> 16) * scale;
     reinterpret_cast<float4*>(g)[2 * i] = a;
     reinterpret_cast<float4*>(g)[2 * i + 1] = b;
   }
   for (int64_t i = (n8 << 3) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    g[i] = bf2f(c[i]) * scale;
+    g[i] = h2f<F16>(c[i]) * scale;
 }
 }  // namespace ops
 }  // namespace dtfk
@@ -606,12 +624,14 @@ static int nblk(int64_t n, int per = 256, int cap = 4096) {
 }
 
 extern "C" {
-hipError_t dtfk_bucket_pack_bf16(const float* g, uint16_t* c, int64_t n, float scale, hipStream_t s) {
-  hipLaunchKernelGGL(bucket_pack_bf16, dim3(nblk((n + 7) / 8)), dim3(256), 0, s, g, c, n, scale);
+hipError_t dtfk_bucket_pack(const float* g, uint16_t* c, int64_t n, float scale, int fp16, hipStream_t s) {
+  if (fp16) hipLaunchKernelGGL(bucket_pack<true>, dim3(nblk((n + 7) / 8)), dim3(256), 0, s, g, c, n, scale);
+  else hipLaunchKernelGGL(bucket_pack<false>, dim3(nblk((n + 7) / 8)), dim3(256), 0, s, g, c, n, scale);
   return hipGetLastError();
 }
-hipError_t dtfk_bucket_unpack_bf16(const uint16_t* c, float* g, int64_t n, float scale, hipStream_t s) {
-  hipLaunchKernelGGL(bucket_unpack_bf16, dim3(nblk((n + 7) / 8)), dim3(256), 0, s, c, g, n, scale);
+hipError_t dtfk_bucket_unpack(const uint16_t* c, float* g, int64_t n, float scale, int fp16, hipStream_t s) {
+  if (fp16) hipLaunchKernelGGL(bucket_unpack<true>, dim3(nblk((n + 7) / 8)), dim3(256), 0, s, c, g, n, scale);
+  else hipLaunchKernelGGL(bucket_unpack<false>, dim3(nblk((n + 7) / 8)), dim3(256), 0, s, c, g, n, scale);
   return hipGetLastError();
 }
 hipError_t dtfk_act_backward(const float* dy, const float* y, const float* z, float* dz, int64_t n,

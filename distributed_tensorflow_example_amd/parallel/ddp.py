@@ -243,20 +243,18 @@ class DistributedDataParallel(torch.nn.Module):
             self.comm_stream.wait_event(ev)
             with torch.cuda.stream(self.comm_stream):
                 scale = 1.0 / w.world_size if self.average else 1.0
-                if self.comm_dtype == torch.bfloat16:
-                    # K16: pack + cast + 1/N in one kernel, reduce in bf16 (half the
-                    # xGMI bytes), unpack in one kernel -- two passes instead of
-                    # cast, copy-back and mul_
-                    if b.comm_buf is None:
-                        b.comm_buf = torch.empty(b.buf.numel(), dtype=torch.bfloat16, device=b.buf.device)
+                if self.comm_dtype in (torch.bfloat16, torch.float16):
+                    # K16: pack + cast + 1/N in one kernel, reduce in 16 bits (half
+                    # the xGMI bytes), unpack in one kernel -- two passes instead of
+                    # cast, copy-back and mul_; the comm buffer persists per bucket
+                    if b.comm_buf is None or b.comm_buf.dtype != self.comm_dtype:
+                        b.comm_buf = torch.empty(b.buf.numel(), dtype=self.comm_dtype, device=b.buf.device)
                     C = _native.load()
-                    C.bucket_pack_bf16(b.buf, b.comm_buf, scale)
+                    C.bucket_pack(b.buf, b.comm_buf, scale)
                     w.comm.all_reduce(b.comm_buf, "sum")
-                    C.bucket_unpack_bf16(b.comm_buf, b.buf, 1.0)
+                    C.bucket_unpack(b.comm_buf, b.buf, 1.0)
                 elif self.comm_dtype is not None and self.comm_dtype != torch.float32:
-                    b.comm_buf = b.buf.to(self.comm_dtype)
-                    w.comm.all_reduce(b.comm_buf, "avg" if self.average else "sum")
-                    b.buf.copy_(b.comm_buf)
+                    raise ValueError(f"DDP comm_dtype {self.comm_dtype}: float32, bfloat16 or float16")
                 else:
                     # RCCL's ncclAvg divides inside the reduction: no extra pass over the bucket
                     w.comm.all_reduce(b.buf, "avg" if self.average else "sum")

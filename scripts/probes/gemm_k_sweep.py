@@ -42,6 +42,7 @@ def main():
             y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
             row = {"M": M, "N": N, "K": K}
             for name, f in (("v8", lambda: C.gemm_big(x, False, w, True, y, variant=8)),
+                            ("v8_noepi", lambda: C.gemm_big_cfg(11, x, w, y)),
                             ("v4", lambda: C.gemm_big(x, False, w, True, y, variant=4)),
                             ("torch", lambda: torch.mm(x, w.t(), out=y))):
                 ms = timed(f)

@@ -368,20 +368,24 @@ def test_sparse_route_kernel_matches_torch(W):
 
 
 @pytest.mark.gpu
-def test_bucket_pack_unpack_bf16():
-    """K16: DDP bucket -> bf16 comm buffer with the 1/N scale folded in, and
-    back, against torch's round-to-nearest-even cast (incl. a ragged tail)."""
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_bucket_pack_unpack_16bit(dt):
+    """K16: DDP bucket -> bf16 / fp16 comm buffer with the 1/N scale folded in,
+    and back, against torch's round-to-nearest-even cast (incl. a ragged tail)."""
     from distributed_tensorflow_example_amd import _native
 
     C = _native.load()
     for n in (8, 1000, (1 << 20) + 5):
         g = torch.randn(n, device="cuda") * 3
-        c = torch.empty(n, dtype=torch.bfloat16, device="cuda")
-        C.bucket_pack_bf16(g, c, 0.125)
-        assert torch.equal(c, (g * 0.125).to(torch.bfloat16))
+        c = torch.empty(n, dtype=dt, device="cuda")
+        C.bucket_pack(g, c, 0.125)
+        assert torch.equal(c, (g * 0.125).to(dt))
         out = torch.empty(n, device="cuda")
-        C.bucket_unpack_bf16(c, out, 2.0)
+        C.bucket_unpack(c, out, 2.0)
         assert torch.equal(out, c.float() * 2.0)
+    if dt == torch.bfloat16:        # the round-2 names stay bound
+        C.bucket_pack_bf16(g, c, 1.0)
+        assert torch.equal(c, g.to(dt))
 
 
 @pytest.mark.gpu

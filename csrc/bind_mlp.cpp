@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -55,8 +56,9 @@ hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int n
 long long dtfk_graph_mlp_part_floats(int B, int H);
 hipError_t dtfk_graph_mlp_step(const float* x, const float* ylab, float* W1, float* b1, float* W2, float* b2,
                                float* a2buf, float* dz2buf, float* part, float* gW1, float* gb1, float* gW2,
-                               float* gb2, float* metrics, void* gstep, int gstep_kind, const float* lr_ptr, int B,
-                               int K, int H, int C, int act, int naive, int sgd, hipStream_t stream);
+                               float* gb2, float* metrics, float* host_metrics, void* gstep, int gstep_kind,
+                               const float* lr_ptr, int B, int K, int H, int C, int act, int naive, int sgd,
+                               hipStream_t stream);
 long long dtfk_mlpx_stage_rec();
 long long dtfk_mlpx_xbuf_bytes();
 long long dtfk_mlpx_ipc_bytes();
@@ -567,7 +569,7 @@ void graph_mlp_step(at::Tensor x, at::Tensor ylab, at::Tensor W1, at::Tensor b1,
   hip_check(dtfk_graph_mlp_step(x.data_ptr<float>(), ylab.data_ptr<float>(), W1.data_ptr<float>(),
                                 b1.data_ptr<float>(), W2.data_ptr<float>(), b2.data_ptr<float>(),
                                 a2buf.data_ptr<float>(), dz2buf.data_ptr<float>(), part.data_ptr<float>() + 1, gW1,
-                                gb1, gW2, gb2, metrics.data_ptr<float>(), gp, kind, part.data_ptr<float>(), B, K, H, C,
+                                gb1, gW2, gb2, metrics.data_ptr<float>(), nullptr, gp, kind, part.data_ptr<float>(), B, K, H, C,
                                 act, naive ? 1 : 0, sgd ? 1 : 0, cur_stream()),
             "graph_mlp_step");
 }
@@ -585,6 +587,8 @@ class GraphStepPlan {
       : W1_(W1), b1_(b1), W2_(W2), b2_(b2), B_(B), act_(act), naive_(naive), use_graph_(use_graph) {
     const char* df = getenv("DTF_GRAPH_STEP_DIRECT_FEED");
     direct_feed_ = df != nullptr && df[0] == '1';
+    const char* hs = getenv("DTF_GRAPH_STEP_METRICS_COPY");   // 1: copy the metrics back with a D2H op
+    host_store_ = !(hs != nullptr && hs[0] == '1');
     for (const at::Tensor* t : {&W1, &b1, &W2, &b2})
       TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous(),
                   "GraphStepPlan: fp32 contiguous device parameters expected");
@@ -643,6 +647,8 @@ class GraphStepPlan {
     {
       py::gil_scoped_release nogil;
       if (!use_graph_) {   // direct launches on the caller's stream: no cross-stream events, no replay floor
+        using clk = std::chrono::steady_clock;
+        const auto t0 = clk::now();
         hip_check(hipEventSynchronize(ev_[slot]), "GraphStepPlan: staging slot");
         float* h = stage_[slot].data_ptr<float>();
         float* d = dev_.data_ptr<float>();
@@ -658,12 +664,16 @@ class GraphStepPlan {
           std::memcpy(h, xp, sizeof(float) * nx);
           std::memcpy(h + nx, yp, sizeof(float) * ny);
           h[nx + ny] = (float)lr;
+          t_[0] += std::chrono::duration<double, std::micro>(clk::now() - t0).count();
           hip_check(hipMemcpyAsync(d, h, sizeof(float) * (nx + ny + 1), hipMemcpyHostToDevice, st),
                     "GraphStepPlan: feed copy");
         }
         hip_check(hipEventRecord(ev_[slot], st), "GraphStepPlan: event");
-        launch_step(st);
+        hip_check(launch_step(st, host_store_), "GraphStepPlan: launch");
+        const auto t2 = clk::now();
+        t_[1] += std::chrono::duration<double, std::micro>(t2 - t0).count();
         if (sync) hip_check(hipStreamSynchronize(st), "GraphStepPlan: sync");
+        t_[2] += std::chrono::duration<double, std::micro>(clk::now() - t2).count();
         ++steps_;
         return;
       }
@@ -691,18 +701,32 @@ class GraphStepPlan {
   }
   int64_t steps() const { return steps_; }
   bool use_graph() const { return use_graph_; }
+  // host-side split of the direct-launch calls so far, us per call: feed copy
+  // into the staging slot, everything up to the last enqueue, the final wait
+  py::dict timing() const {
+    py::dict d;
+    const double n = steps_ > 0 ? (double)steps_ : 1.0;
+    d["feed_memcpy_us"] = t_[0] / n;
+    d["enqueue_us"] = t_[1] / n;
+    d["sync_us"] = t_[2] / n;
+    d["calls"] = steps_;
+    return d;
+  }
 
  private:
-  // the step's three kernels + the metrics copy back, on stream st
-  hipError_t launch_step(hipStream_t st) {
+  // the step's three kernels on stream st; the metrics reach host_metrics_
+  // either from the last kernel itself (system-scope stores into the pinned
+  // buffer: direct launches) or by a copy back (captured graphs)
+  hipError_t launch_step(hipStream_t st, bool host_store) {
     const int64_t nx = (int64_t)B_ * K_, ny = (int64_t)B_ * C_;
     float* d = dev_.data_ptr<float>();
     hipError_t e = dtfk_graph_mlp_step(d, d + nx, W1_.data_ptr<float>(), b1_.data_ptr<float>(), W2_.data_ptr<float>(),
                                        b2_.data_ptr<float>(), a2_.data_ptr<float>(), dz2_.data_ptr<float>(),
                                        part_.data_ptr<float>(), nullptr, nullptr, nullptr, nullptr,
-                                       metrics_.data_ptr<float>(), gstep_.defined() ? gstep_.data_ptr() : nullptr,
-                                       gkind_, d + nx + ny, B_, K_, H_, C_, act_, naive_ ? 1 : 0, 1, st);
-    if (e == hipSuccess)
+                                       metrics_.data_ptr<float>(), host_store ? host_metrics_.data_ptr<float>() : nullptr,
+                                       gstep_.defined() ? gstep_.data_ptr() : nullptr, gkind_, d + nx + ny, B_, K_, H_,
+                                       C_, act_, naive_ ? 1 : 0, 1, st);
+    if (e == hipSuccess && !host_store)
       e = hipMemcpyAsync(host_metrics_.data_ptr<float>(), metrics_.data_ptr<float>(), 3 * sizeof(float),
                          hipMemcpyDeviceToHost, st);
     return e;
@@ -712,7 +736,7 @@ class GraphStepPlan {
     if (exec_) { (void)hipGraphExecDestroy(exec_); exec_ = nullptr; }
     if (graph_) { (void)hipGraphDestroy(graph_); graph_ = nullptr; }
     hip_check(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal), "GraphStepPlan: begin capture");
-    const hipError_t e = launch_step(st);
+    const hipError_t e = launch_step(st, false);
     hipGraph_t g = nullptr;
     const hipError_t e2 = hipStreamEndCapture(st, &g);
     hip_check(e, "GraphStepPlan: captured launches");
@@ -731,6 +755,8 @@ class GraphStepPlan {
   int B_, K_ = 0, H_ = 0, C_ = 0, HP_ = 0, act_, gkind_ = 0, slot_ = 0;
   bool naive_, use_graph_, direct_feed_ = false;
   int64_t nfeed_ = 0, steps_ = 0;
+  bool host_store_ = true;
+  double t_[3] = {0, 0, 0};
 };
 
 void init_mlp(py::module& m) {
@@ -741,7 +767,8 @@ void init_mlp(py::module& m) {
       .def("use_graph", &GraphStepPlan::use_graph)
       .def("run", &GraphStepPlan::run, py::arg("x"), py::arg("y"), py::arg("lr"), py::arg("sync"))
       .def("host_metrics", &GraphStepPlan::host_metrics)
-      .def("steps", &GraphStepPlan::steps);
+      .def("steps", &GraphStepPlan::steps)
+      .def("timing", &GraphStepPlan::timing);
   m.def("graph_mlp_step", &graph_mlp_step, py::arg("x"), py::arg("ylab"), py::arg("W1"), py::arg("b1"),
         py::arg("W2"), py::arg("b2"), py::arg("a2buf"), py::arg("dz2buf"), py::arg("grads"), py::arg("metrics"),
         py::arg("gstep"), py::arg("lr"), py::arg("act"), py::arg("naive"), py::arg("sgd"));

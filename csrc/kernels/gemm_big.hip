@@ -539,7 +539,11 @@ __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A,
     mma(1, 0);
   }
   if (!wr) raw_barrier();   // equal barrier counts for both wave rows
-  if (act < 0) return;      // probe only (dtfk_gemm_big_cfg 11): the loop without the epilogue
+  // probes only (dtfk_gemm_big_cfg 11-13): -1 the loop without the epilogue,
+  // -2 a quarter of the outputs stored, -3 every tile stored over tile (0, 0)
+  const int probe = act < 0 ? -act : 0;
+  if (probe == 1) return;
+  if (probe) act = ACT_NONE;
 
   if constexpr (!SW) {
     // split-K (fp32, linear): accumulators in MFMA layout -- lane l holds rows
@@ -581,7 +585,8 @@ __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A,
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const size_t o = (size_t)(mrow + i * 16) * ldc + ncol + j * 16;
+        if (probe == 2 && j != 0) continue;
+        const size_t o = (size_t)(mrow + i * 16) * ldc + ncol + j * 16 - (probe == 3 ? (size_t)m0 * ldc + n0 : 0);
         float z[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) z[r] = alpha * acc[i][j][r] + bv[j][r];
@@ -854,10 +859,12 @@ extern "C" hipError_t dtfk_gemm_big_cfg(int cfg, const void* A, int lda, const v
     case 8: DTFK_CFG(256, 64, 2, 3); break;
     case 9: DTFK_CFG(256, 64, 2, 4); break;
     case 10:
-    case 11:   // 11: the same without the epilogue (loop-cost probe; C is not written)
+    case 11:   // 11-13: epilogue probes (11: none, 12: a quarter of C, 13: all tiles onto tile (0, 0))
+    case 12:
+    case 13:
       if (K % 128) return hipErrorInvalidValue;
       hipLaunchKernelGGL((gemm_8ph<true, true, true, true>), dim3((M / 256) * tn, 1), dim3(NTHR), 0, stream, a, lda, b, ldb,
-                         C, ldc, nullptr, M, N, K, 1.f, 0.f, cfg == 11 ? -1 : 0, K);
+                         C, ldc, nullptr, M, N, K, 1.f, 0.f, cfg == 10 ? 0 : 10 - cfg, K);
       break;
     default: return hipErrorInvalidValue;
   }

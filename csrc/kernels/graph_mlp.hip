@@ -259,6 +259,7 @@ struct WgradArgs {
   float* gb2;
   const float* hpart;   // L2's dW2 partials + loss / correct sums
   float* metrics;       // [0] loss, [1] accuracy, [2] global_step after the step
+  float* host_metrics;  // the same three in pinned host memory (nullptr: none) -- no copy-back op
   void* gstep;          // global_step storage or nullptr
   int gstep_kind;       // 0 f32, 1 i64, 2 i32, 3 f64
   const float* lr_ptr;  // device learning rate (a captured step reads the current one)
@@ -301,6 +302,12 @@ __device__ void graph_mlp_w2_final(const WgradArgs& a, int ht) {
         default: now = (float)(*reinterpret_cast<double*>(a.gstep) += 1.0); break;
       }
       a.metrics[2] = now;                 // post-increment value, read back with the loss
+    }
+    if (a.host_metrics != nullptr) {      // system-scope vector stores over PCIe, fenced before the kernel ends
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        __hip_atomic_store(a.host_metrics + i, a.metrics[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __threadfence_system();
     }
   }
 }
@@ -377,9 +384,9 @@ extern "C" long long dtfk_graph_mlp_part_floats(int B, int H) {
 
 extern "C" hipError_t dtfk_graph_mlp_step(const float* x, const float* ylab, float* W1, float* b1, float* W2,
                                           float* b2, float* a2buf, float* dz2buf, float* part, float* gW1, float* gb1,
-                                          float* gW2, float* gb2, float* metrics, void* gstep, int gstep_kind,
-                                          const float* lr_ptr, int B, int K, int H, int C, int act, int naive, int sgd,
-                                          hipStream_t stream) {
+                                          float* gW2, float* gb2, float* metrics, float* host_metrics, void* gstep,
+                                          int gstep_kind, const float* lr_ptr, int B, int K, int H, int C, int act,
+                                          int naive, int sgd, hipStream_t stream) {
   using namespace dtfk::gmlp;
   if (B < 1 || B > MAXB || H < 1 || H > MAXH || C < 1 || C > CP || K < 1 || lr_ptr == nullptr)
     return hipErrorInvalidValue;
@@ -395,8 +402,8 @@ extern "C" hipError_t dtfk_graph_mlp_step(const float* x, const float* ylab, flo
   HeadArgs h{a2buf, ylab, W2, b2, dz2buf, part, B, H, HP, C, act, naive};
   hipLaunchKernelGGL(graph_mlp_head, dim3(BP / 16), dim3(HW * 64), 0, stream, h);
   const int tiles = ((K + 1 + 15) / 16) * (HP / 16);
-  WgradArgs wa{x, dz2buf, W1, b1, W2, b2, gW1, gb1, gW2, gb2, part, metrics, gstep, gstep_kind, lr_ptr,
-               B, K, H, HP, C, sgd, tiles};
+  WgradArgs wa{x, dz2buf, W1, b1, W2, b2, gW1, gb1, gW2, gb2, part, metrics, host_metrics, gstep, gstep_kind,
+               lr_ptr, B, K, H, HP, C, sgd, tiles};
   hipLaunchKernelGGL(graph_mlp_wgrad, dim3(tiles + HP / 16), dim3(256), 0, stream, wa);
   return hipGetLastError();
 }

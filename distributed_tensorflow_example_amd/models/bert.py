@@ -112,7 +112,13 @@ def _wgrad(gy2, x2, into=None):
     """dW[out, in] = gy2[T, out]^T @ x2[T, in] in fp32 (accumulated into `into`)."""
     T, out = gy2.shape
     if gy2.is_cuda and big_gemm.use_native("dw", out, x2.shape[1], T, gy2.device):
-        return big_gemm.linear_dw(gy2, x2, into=into)   # split-K over tokens, fp32 atomics into `into`
+        return big_gemm.linear_dw(gy2, x2, into=into)   # split-K over tokens: fp32 slabs + reduce into `into`
+    return _wgrad_torch(gy2, x2, into)
+
+
+def _wgrad_torch(gy2, x2, into=None):
+    """_wgrad on hipBLASLt: token-slab batched GEMM + slab_sum."""
+    T, out = gy2.shape
     s = _wgrad_split(T, out, x2.shape[1]) if gy2.is_cuda else 1
     if s == 1:
         if into is not None:

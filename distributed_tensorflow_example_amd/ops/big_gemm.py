@@ -19,9 +19,10 @@ import torch
 
 from .. import _native
 
-# never (default): hipBLASLt runs the model GEMMs -- on the BERT-base shapes it
-# is ~2x this kernel (profiles/gemm_big_vs_hipblaslt_r2.jsonl) and a per-shape
-# auto pick measured 3.5 % slower end to end (profiles/bert_base_b128_gemm_policy_r2.txt);
+# never (default): hipBLASLt runs the model GEMMs -- with the 8-phase schedule
+# this kernel is 0.77-0.90x of it on BERT-base's forward / input-gradient
+# shapes and 0.81-1.02x on the weight gradients (profiles/gemm_8ph_r3.txt); end
+# to end 'auto' measured 1.1 % and 'always' 12 % slower than 'never';
 # auto: time both once per shape, keep the faster; always: this kernel
 _POLICY = os.environ.get("DTF_BIG_GEMM", "never")
 _choice: dict = {}
@@ -55,11 +56,15 @@ def _candidates(role, M, N, K, dev):
         a, b = torch.randn(M, K, device=dev, dtype=bf), torch.randn(K, N, device=dev, dtype=bf)
         o = torch.empty(M, N, device=dev, dtype=bf)
         return (lambda: C.gemm_big(a, False, b, False, o)), (lambda: torch.mm(a, b, out=o))
-    # dw[M,N] += dy[K,M]^T x[K,N]
+    # dw[M,N] += dy[K,M]^T x[K,N]; the torch side is what the models run without
+    # this kernel: token-slab batched GEMM + slab_sum (models/bert.py _wgrad)
     a, b = torch.randn(K, M, device=dev, dtype=bf), torch.randn(K, N, device=dev, dtype=bf)
     o = torch.zeros(M, N, device=dev)
-    return ((lambda: C.gemm_big(a, True, b, False, o, beta=1.0, split_k=0)),
-            (lambda: torch.addmm(o, a.t(), b, out_dtype=torch.float32, out=o)))
+
+    def theirs():
+        from ..models.bert import _wgrad_torch
+        _wgrad_torch(a, b, into=o)
+    return (lambda: C.gemm_big(a, True, b, False, o, beta=1.0, split_k=0)), theirs
 
 
 def use_native(role: str, M: int, N: int, K: int, dev) -> bool:

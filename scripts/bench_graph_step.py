@@ -71,11 +71,15 @@ def main():
                 for i in range(1000):
                     cp.run(xs[i % 64], ys[i % 64], 0.0, True)
                 out["native_call_us"] = (time.perf_counter() - t0) / 1000 * 1e6
+                if hasattr(cp, "timing"):
+                    out["native_call_split_us"] = {k: round(v, 2) if isinstance(v, float) else v
+                                                   for k, v in cp.timing().items()}
         tf.reset_default_graph()
     os.environ.pop("DTF_GRAPH_LOWERING", None)
     print(json.dumps({"native_plan_runs": out.get("native_plan_runs"),
                       "native_plan_hipgraph": out.get("native_plan_hipgraph"),
                       "native_call_us": round(out.get("native_call_us", 0.0), 2),
+                      "native_call_split_us": out.get("native_call_split_us"),
                       "session_run_ms_per_step_lowered": round(out["lowered"], 4),
                       "session_run_ms_per_step_eager": round(out["eager"], 4),
                       "lowered_kernels_us_per_step": round(out["kernels_us"], 3), "batch": B, "steps": steps}))

@@ -43,6 +43,8 @@ def main():
             row = {"M": M, "N": N, "K": K}
             for name, f in (("v8", lambda: C.gemm_big(x, False, w, True, y, variant=8)),
                             ("v8_noepi", lambda: C.gemm_big_cfg(11, x, w, y)),
+                            ("v8_quarter", lambda: C.gemm_big_cfg(12, x, w, y)),
+                            ("v8_samedst", lambda: C.gemm_big_cfg(13, x, w, y)),
                             ("v4", lambda: C.gemm_big(x, False, w, True, y, variant=4)),
                             ("torch", lambda: torch.mm(x, w.t(), out=y))):
                 ms = timed(f)

@@ -27,7 +27,7 @@ def _free_port():
 
 
 class _GlooStreamComm:
-    """RcclComm's all_reduce(tensor, op) over the gloo process group."""
+    """RcclComm's all_reduce / broadcast over the gloo process group."""
 
     def all_reduce(self, t, op="sum"):
         import torch.distributed as dist
@@ -35,6 +35,11 @@ class _GlooStreamComm:
         dist.all_reduce(t)
         if op == "avg":
             t.div_(dist.get_world_size())
+
+    def broadcast(self, t, src):
+        import torch.distributed as dist
+
+        dist.broadcast(t, src)
 
 
 def _worker(rank, ws, port, q, bucket_mb, comm):
@@ -74,7 +79,7 @@ def _worker(rank, ws, port, q, bucket_mb, comm):
         q.put((rank, traceback.format_exc(), 0))
 
 
-@pytest.mark.parametrize("comm,bucket_mb", [("fp32", 0.05), ("fp32", 25.0), ("bf16", 0.05), ("fp16", 0.05)])
+@pytest.mark.parametrize("comm,bucket_mb", [("fp32", 0.001), ("fp32", 25.0), ("bf16", 0.001), ("fp16", 0.001)])
 def test_ddp_two_ranks_same_gpu_match_full_batch(comm, bucket_mb):
     ws = 2
     ctx = mp.get_context("spawn")

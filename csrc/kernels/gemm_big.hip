@@ -432,7 +432,10 @@ __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A,
                                                  float alpha, float beta, int act, int kchunk, long long slab = 0) {
   constexpr int BM = 256, BK = 64, HALF = 128 * BK * 2, BUF = 4 * HALF;   // A_q0 A_q1 B_q0 B_q1
   constexpr int NA = AKC ? 8 : 16;                                       // LDS instructions of one A-fragment set
-  __shared__ __attribute__((aligned(1024))) uint8_t smem[2 * BUF];
+  // operand buffers; after the K loop, each wave's fp32 output half-tile (64
+  // rows of EPI_ROW bytes: 256 + 16 pad) for the row-contiguous store pass
+  constexpr int EPI_ROW = 272, EPI_WAVE = 64 * EPI_ROW;
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[(2 * BUF > 8 * EPI_WAVE) ? 2 * BUF : 8 * EPI_WAVE];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
 
@@ -573,6 +576,71 @@ __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A,
   // (fp32) store per tile instead of four 2- / 4-byte ones.
   const bool vec = (ldc & 7) == 0 && (reinterpret_cast<uintptr_t>(C) & 15) == 0;
   const int mrow = m0 + wr * 128 + (lane & 15), ncol = n0 + wc * 64 + 4 * (lane >> 4);
+  if (vec && m0 + BM <= M && n0 + BN <= N && probe == 0) {
+    // Interior tile: the wave's 128 x 64 outputs go through its private LDS
+    // region (free after the loop's last barrier) in two halves of 64 rows,
+    // as fp32 (alpha acc + bias); read back as 8 consecutive columns per lane
+    // (+ beta C, activation, conversion) and stored as whole row segments:
+    // each store instruction writes 8 rows x 128 (bf16) / 256 (fp32) bytes =
+    // full cache lines, instead of 16 rows x 32 / 64 bytes.  Measured: the
+    // end-of-tile store burst was the kernel's largest cost (profiles/gemm_8ph_r3.txt).
+    uint8_t* ep = smem + wave * EPI_WAVE;
+    float bv[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bv[j][r] = bias != nullptr ? bias[ncol + j * 16 + r] : 0.f;
+    const int rsub = lane >> 3, c8 = (lane & 7) * 8;     // read-back: row rsub (+8 it), columns c8 .. c8+7
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int row = i * 16 + (lane & 15), col = j * 16 + 4 * (lane >> 4);
+          const f32x4 a4 = acc[half * 4 + i][j];
+          *reinterpret_cast<f32x4*>(ep + row * EPI_ROW + col * 4) =
+              f32x4{alpha * a4[0] + bv[j][0], alpha * a4[1] + bv[j][1], alpha * a4[2] + bv[j][2],
+                    alpha * a4[3] + bv[j][3]};
+        }
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const int lrow = it * 8 + rsub;
+        const f32x4 lo = *reinterpret_cast<const f32x4*>(ep + lrow * EPI_ROW + c8 * 4);
+        const f32x4 hi = *reinterpret_cast<const f32x4*>(ep + lrow * EPI_ROW + c8 * 4 + 16);
+        float z[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const size_t o = (size_t)(m0 + wr * 128 + half * 64 + lrow) * ldc + n0 + wc * 64 + c8;
+        if (beta != 0.f) {
+          if constexpr (OBF) {
+            const uint4 c = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(C) + o);
+            const uint32_t cw[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              z[2 * q] += beta * bf2f((uint16_t)(cw[q] & 0xffff));
+              z[2 * q + 1] += beta * bf2f((uint16_t)(cw[q] >> 16));
+            }
+          } else {
+            const float4 c0 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(C) + o);
+            const float4 c1 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(C) + o + 4);
+            z[0] += beta * c0.x; z[1] += beta * c0.y; z[2] += beta * c0.z; z[3] += beta * c0.w;
+            z[4] += beta * c1.x; z[5] += beta * c1.y; z[6] += beta * c1.z; z[7] += beta * c1.w;
+          }
+        }
+        if (act != ACT_NONE) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) z[q] = apply_act_slow(z[q], act);
+        }
+        if constexpr (OBF) {
+          *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(C) + o) =
+              make_uint4(pack2bf(z[0], z[1]), pack2bf(z[2], z[3]), pack2bf(z[4], z[5]), pack2bf(z[6], z[7]));
+        } else {
+          *reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + o) = make_float4(z[0], z[1], z[2], z[3]);
+          *reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + o + 4) = make_float4(z[4], z[5], z[6], z[7]);
+        }
+      }
+    }
+    return;
+  }
   if (vec && m0 + BM <= M && n0 + BN <= N) {
     // interior tile: no per-lane bounds, only wave-uniform branches (an
     // exec-masked branch per element costs more than the stores themselves)

@@ -46,25 +46,27 @@ def test_layouts_fp32_out(native, tA, tB, M, N, K, variant):
     assert _rel(C, ref) < 1e-5, _rel(C, ref)
 
 
+@pytest.mark.parametrize("obf", [True, False])
 @pytest.mark.parametrize("act", [0, 1, 2, 4])
-def test_bf16_out_bias_act(native, act):
+def test_out_bias_act(native, act, obf):
     M, N, K = 2048, 1024, 512
     A, B = _operands(M, N, K, False, True, act)
     bias = torch.randn(N, device="cuda")
-    C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16 if obf else torch.float32)
     assert native.gemm_big(A, False, B, True, C, bias=bias, act=act, alpha=0.5)
     ref = _ref(A, False, B, True, bias, act, 0.5)
-    assert _rel(C, ref) < 1e-2
+    assert _rel(C, ref) < (1e-2 if obf else 1e-5)
 
 
+@pytest.mark.parametrize("variant,K", [(0, 320), (8, 384)])
 @pytest.mark.parametrize("obf", [False, True])
-def test_beta_accumulate(native, obf):
-    M, N, K = 768, 1280, 320
+def test_beta_accumulate(native, obf, variant, K):
+    M, N = 768, 1280
     A, B = _operands(M, N, K, False, False, 7)
     dt = torch.bfloat16 if obf else torch.float32
     C0 = torch.randn(M, N, device="cuda").to(dt)
     C = C0.clone()
-    assert native.gemm_big(A, False, B, False, C, beta=1.0)
+    assert native.gemm_big(A, False, B, False, C, beta=1.0, variant=variant)
     ref = _ref(A, False, B, False, beta=1.0, C0=C0)
     assert _rel(C, ref) < (1e-2 if obf else 1e-5)
 

@@ -129,7 +129,8 @@ bool gemm_big(at::Tensor A, bool transA, at::Tensor B, bool transB, at::Tensor o
               int act, double alpha, double beta, int split_k, int variant) {
   gpu(A, "A"); gpu(B, "B"); gpu(out, "out");
   if (A.dim() != 2 || B.dim() != 2 || out.dim() != 2) throw std::runtime_error("gemm_big operands must be 2-D");
-  if (variant != 0 && variant != 4 && variant != 8) throw std::runtime_error("gemm_big: variant 0 (auto), 4 or 8");
+  if (variant != 0 && variant != 4 && variant != 8 && variant != 9)
+    throw std::runtime_error("gemm_big: variant 0 (auto), 4, 8 or 9");
   if (A.scalar_type() != at::kBFloat16 || B.scalar_type() != at::kBFloat16)
     throw std::runtime_error("gemm_big: bf16 operands");
   if (out.scalar_type() != at::kBFloat16 && out.scalar_type() != at::kFloat)

@@ -79,8 +79,11 @@ __device__ __forceinline__ int kc_off(int r, int c) {
 }
 // M/N-contiguous [BK][R] bf16: byte offset of (k, 16-byte chunk ch = mn/8)
 __device__ __forceinline__ int mn_swz(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
+// (the chunk XOR is masked to the row's R / 8 chunks: a no-op for R >= 128)
 template <int R>
-__device__ __forceinline__ int mn_off(int k, int ch) { return k * (2 * R) + ((ch ^ (mn_swz(k) << 1)) << 4); }
+__device__ __forceinline__ int mn_off(int k, int ch) {
+  return k * (2 * R) + ((ch ^ ((mn_swz(k) << 1) & (R / 8 - 1))) << 4);
+}
 
 // Stage one operand tile (R rows of the output dimension x BK k) into `img`.
 // KC: src element (row, k) at base[row * ld + k]; else at base[k * ld + row].
@@ -392,26 +395,35 @@ __global__ __launch_bounds__(NTHR) void gemm_big(const uint16_t* __restrict__ A,
 // staggered group passes one more barrier after the other group's wait).
 // Shape contract on top of gemm_big's: the K range of a workgroup is a
 // multiple of 128 (an even number of K tiles).
-template <bool IS_A>
-__device__ __forceinline__ int half_row(int l, int q) {   // half-tile local index -> tile row / col
-  if constexpr (IS_A) return ((l >> 6) << 7) + (q << 6) + (l & 63);
-  else return ((l >> 5) << 6) + (q << 5) + (l & 31);
+// half-tile local index -> tile row (A) / column (B).  B: WN = the wave's
+// column count (64, or 48 for 192-wide tiles); quadrant column 0 is its first
+// 32 columns, quadrant column 1 the remaining WN - 32.
+template <bool IS_A, int WN>
+__device__ __forceinline__ int half_row(int l, int q) {
+  if constexpr (IS_A) {
+    return ((l >> 6) << 7) + (q << 6) + (l & 63);
+  } else {
+    constexpr int W1 = WN - 32;
+    return q == 0 ? (l >> 5) * WN + (l & 31) : (l / W1) * WN + 32 + (l % W1);
+  }
 }
 
-template <bool IS_A, bool KC>
+// Stage one half-tile (R rows of the output dimension x 64 k, R / 64 LDS-DMA
+// instructions per thread) of K tile k0 into `img`.
+template <bool IS_A, bool KC, int R, int WN>
 __device__ __forceinline__ void stage_half(const uint16_t* __restrict__ base, int ld, int rows, int r0, int k0, int q,
                                            uint8_t* img, int wave, int lane) {
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+  for (int j = 0; j < R / 64; ++j) {
     const int wbase = (j * 8 + wave) << 10;
     const int o = wbase + (lane << 4);
     const uint16_t* src;
-    if constexpr (KC) {   // [128][64] image, kc_off<64> chunk XOR
+    if constexpr (KC) {   // [R][64] image, kc_off<64> chunk XOR
       const int rl = o >> 7, c = ((o >> 4) & 7) ^ ((rl >> 1) & 7);
-      src = base + (size_t)min(r0 + half_row<IS_A>(rl, q), rows - 1) * ld + k0 + c * 8;
-    } else {              // [64][128] image, mn_off<128>
-      const int k = o >> 8, ch = ((o & 255) >> 4) ^ (mn_swz(k) << 1);
-      src = base + (size_t)(k0 + k) * ld + min(r0 + half_row<IS_A>(ch * 8, q), rows - 8);
+      src = base + (size_t)min(r0 + half_row<IS_A, WN>(rl, q), rows - 1) * ld + k0 + c * 8;
+    } else {              // [64][R] image, mn_off<R>
+      const int k = o / (2 * R), ch = ((o % (2 * R)) >> 4) ^ ((mn_swz(k) << 1) & (R / 8 - 1));
+      src = base + (size_t)(k0 + k) * ld + min(r0 + half_row<IS_A, WN>(ch * 8, q), rows - 8);
     }
     __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(img + wbase), 16, 0, 0);
   }
@@ -425,43 +437,49 @@ __device__ __forceinline__ void raw_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <bool AKC, bool BKC, bool OBF, bool SW>
+template <bool AKC, bool BKC, bool OBF, bool SW, int BNT = 256>
 __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A, int lda,
                                                  const uint16_t* __restrict__ B, int ldb, void* __restrict__ C,
                                                  int ldc, const float* __restrict__ bias, int M, int N, int K,
                                                  float alpha, float beta, int act, int kchunk, long long slab = 0) {
-  constexpr int BM = 256, BK = 64, HALF = 128 * BK * 2, BUF = 4 * HALF;   // A_q0 A_q1 B_q0 B_q1
+  // BNT = 256, or 192 (waves 128 x 48: quadrant column 1 is one 16-wide n tile,
+  // its half-tile 64 rows / one DMA per thread) for N where 256 leaves CUs idle
+  static_assert(BNT == 256 || BNT == 192, "tile width");
+  constexpr int BM = 256, BK = 64, WN = BNT / 4, NJ = WN / 16, NQ1 = NJ - 2;
+  constexpr int HALF = 128 * BK * 2, HB1 = 4 * 16 * NQ1 * BK * 2;       // A / B_q0 halves, B_q1
+  constexpr int BUF = 3 * HALF + HB1;                                    // A_q0 A_q1 B_q0 B_q1
+  constexpr int VMC = 4 + NQ1;   // DMA ops of the 3 half-tiles in flight: B_q0 (2) + A_q0 (2) + B_q1 (NQ1)
   constexpr int NA = AKC ? 8 : 16;                                       // LDS instructions of one A-fragment set
   // operand buffers; after the K loop, each wave's fp32 output half-tile (64
-  // rows of EPI_ROW bytes: 256 + 16 pad) for the row-contiguous store pass
-  constexpr int EPI_ROW = 272, EPI_WAVE = 64 * EPI_ROW;
+  // rows of EPI_ROW bytes: WN floats + 16 pad) for the row-contiguous store pass
+  constexpr int EPI_ROW = 4 * WN + 16, EPI_WAVE = 64 * EPI_ROW;
   __shared__ __attribute__((aligned(1024))) uint8_t smem[(2 * BUF > 8 * EPI_WAVE) ? 2 * BUF : 8 * EPI_WAVE];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
 
-  const int nt_n = (N + BN - 1) / BN;
+  const int nt_n = (N + BNT - 1) / BNT;
   const int nwg = gridDim.x, orig = blockIdx.x;
   const int xcd = orig % 8, q8 = nwg / 8, rem = nwg % 8;
   const int wg = (xcd < rem ? xcd * (q8 + 1) : rem * (q8 + 1) + (xcd - rem) * q8) + orig / 8;
-  const int m0 = (wg / nt_n) * BM, n0 = (wg % nt_n) * BN;
+  const int m0 = (wg / nt_n) * BM, n0 = (wg % nt_n) * BNT;
   const int kb = blockIdx.y * kchunk, ke = min(K, kb + kchunk);
   const int nk = (ke - kb) / BK;   // even (host contract)
 
-  f32x4 acc[8][4];
+  f32x4 acc[8][NJ];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // half-tile h of K tile t: 0 B_q0, 1 A_q0, 2 B_q1, 3 A_q1 (staging order)
   auto stage = [&](int t, int h) {
     if (t >= nk) return;
     uint8_t* buf = smem + (t & 1) * BUF;
     const int k0 = kb + t * BK;
-    if (h == 0) stage_half<false, BKC>(B, ldb, N, n0, k0, 0, buf + 2 * HALF, wave, lane);
-    else if (h == 1) stage_half<true, AKC>(A, lda, M, m0, k0, 0, buf, wave, lane);
-    else if (h == 2) stage_half<false, BKC>(B, ldb, N, n0, k0, 1, buf + 3 * HALF, wave, lane);
-    else stage_half<true, AKC>(A, lda, M, m0, k0, 1, buf + HALF, wave, lane);
+    if (h == 0) stage_half<false, BKC, 128, WN>(B, ldb, N, n0, k0, 0, buf + 2 * HALF, wave, lane);
+    else if (h == 1) stage_half<true, AKC, 128, WN>(A, lda, M, m0, k0, 0, buf, wave, lane);
+    else if (h == 2) stage_half<false, BKC, 64 * NQ1, WN>(B, ldb, N, n0, k0, 1, buf + 3 * HALF, wave, lane);
+    else stage_half<true, AKC, 128, WN>(A, lda, M, m0, k0, 1, buf + HALF, wave, lane);
   };
   bf16x8 fa[2][4], fb[2][2][2];   // A: [k-sub][m-tile] of one quadrant row; B: [qn][k-sub][n-tile]
   auto read_a = [&](const uint8_t* buf, int qm) {
@@ -471,10 +489,18 @@ __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A,
       for (int i = 0; i < 4; ++i) fa[s][i] = frag<128, BK, AKC>(buf + qm * HALF, wr * 64 + i * 16, s, lane);
   };
   auto read_b = [&](const uint8_t* buf, int qn) {
+    if (qn == 0) {
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+      for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) fb[qn][s][j] = frag<128, BK, BKC>(buf + (2 + qn) * HALF, wc * 32 + j * 16, s, lane);
+        for (int j = 0; j < 2; ++j) fb[0][s][j] = frag<128, BK, BKC>(buf + 2 * HALF, wc * 32 + j * 16, s, lane);
+    } else {
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int j = 0; j < NQ1; ++j)
+          fb[1][s][j] = frag<64 * NQ1, BK, BKC>(buf + 3 * HALF, wc * 16 * NQ1 + j * 16, s, lane);
+    }
   };
   auto mma = [&](int qm, int qn) {
     raw_barrier();
@@ -486,8 +512,9 @@ __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A,
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[qm * 4 + i][qn * 2 + j] = SW ? mfma16x16x32(fb[qn][s][j], fa[s][i], acc[qm * 4 + i][qn * 2 + j])
-                                           : mfma16x16x32(fa[s][i], fb[qn][s][j], acc[qm * 4 + i][qn * 2 + j]);
+          if (qn == 0 || j < NQ1)
+            acc[qm * 4 + i][qn * 2 + j] = SW ? mfma16x16x32(fb[qn][s][j], fa[s][i], acc[qm * 4 + i][qn * 2 + j])
+                                             : mfma16x16x32(fa[s][i], fb[qn][s][j], acc[qm * 4 + i][qn * 2 + j]);
     __builtin_amdgcn_s_setprio(0);
     raw_barrier();
   };
@@ -505,7 +532,7 @@ __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A,
   for (int h = 0; h < 4; ++h) stage(0, h);
 #pragma unroll
   for (int h = 0; h < 3; ++h) stage(1, h);
-  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMC) : "memory");
   raw_barrier();
   if (wr) raw_barrier();   // the second wave row runs one barrier behind
 
@@ -525,7 +552,7 @@ __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A,
     mma(1, 1);
     stage(t + 2, 2);
     if (last) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMC) : "memory");
     mma(1, 0);
     // phases 5-8: odd buffer (K tile t+1)
     read_first(od);
@@ -538,7 +565,7 @@ __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A,
     stage(t + 3, 1);
     mma(1, 1);
     stage(t + 3, 2);
-    if (!last) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    if (!last) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMC) : "memory");
     mma(1, 0);
   }
   if (!wr) raw_barrier();   // equal barrier counts for both wave rows
@@ -553,8 +580,8 @@ __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A,
     // 4 (l >> 4) .. +3 of column (l & 15), so each atomic instruction covers
     // 16 consecutive columns of 4 rows (4 cache lines, not 16)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wc * 64 + j * 16 + (lane & 15);
+    for (int j = 0; j < NJ; ++j) {
+      const int n = n0 + wc * WN + j * 16 + (lane & 15);
       if (n >= N) continue;
       const float bv = (bias != nullptr && blockIdx.y == 0) ? bias[n] : 0.f;
 #pragma unroll
@@ -575,8 +602,8 @@ __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A,
   // 4 consecutive columns 4 (l >> 4) .. +3 -- one 8-byte (bf16) / 16-byte
   // (fp32) store per tile instead of four 2- / 4-byte ones.
   const bool vec = (ldc & 7) == 0 && (reinterpret_cast<uintptr_t>(C) & 15) == 0;
-  const int mrow = m0 + wr * 128 + (lane & 15), ncol = n0 + wc * 64 + 4 * (lane >> 4);
-  if (vec && m0 + BM <= M && n0 + BN <= N && probe == 0) {
+  const int mrow = m0 + wr * 128 + (lane & 15), ncol = n0 + wc * WN + 4 * (lane >> 4);
+  if (vec && m0 + BM <= M && n0 + BNT <= N && probe == 0) {
     // Interior tile: the wave's 128 x 64 outputs go through its private LDS
     // region (free after the loop's last barrier) in two halves of 64 rows,
     // as fp32 (alpha acc + bias); read back as 8 consecutive columns per lane
@@ -585,18 +612,21 @@ __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A,
     // full cache lines, instead of 16 rows x 32 / 64 bytes.  Measured: the
     // end-of-tile store burst was the kernel's largest cost (profiles/gemm_8ph_r3.txt).
     uint8_t* ep = smem + wave * EPI_WAVE;
-    float bv[4][4];
+    float bv[NJ][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) bv[j][r] = bias != nullptr ? bias[ncol + j * 16 + r] : 0.f;
-    const int rsub = lane >> 3, c8 = (lane & 7) * 8;     // read-back: row rsub (+8 it), columns c8 .. c8+7
+    // read-back: row rsub (+8 it), columns c8 .. c8+7; WN / 8 lanes per row (48-wide: lanes >= 48 idle)
+    constexpr int LPR = WN / 8;
+    const int rsub = lane / LPR, c8 = (lane % LPR) * 8;
+    const bool rb_on = lane < 8 * LPR;
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < NJ; ++j) {
           const int row = i * 16 + (lane & 15), col = j * 16 + 4 * (lane >> 4);
           const f32x4 a4 = acc[half * 4 + i][j];
           *reinterpret_cast<f32x4*>(ep + row * EPI_ROW + col * 4) =
@@ -605,11 +635,12 @@ __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A,
         }
 #pragma unroll
       for (int it = 0; it < 8; ++it) {
+        if (!rb_on) break;
         const int lrow = it * 8 + rsub;
         const f32x4 lo = *reinterpret_cast<const f32x4*>(ep + lrow * EPI_ROW + c8 * 4);
         const f32x4 hi = *reinterpret_cast<const f32x4*>(ep + lrow * EPI_ROW + c8 * 4 + 16);
         float z[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        const size_t o = (size_t)(m0 + wr * 128 + half * 64 + lrow) * ldc + n0 + wc * 64 + c8;
+        const size_t o = (size_t)(m0 + wr * 128 + half * 64 + lrow) * ldc + n0 + wc * WN + c8;
         if (beta != 0.f) {
           if constexpr (OBF) {
             const uint4 c = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(C) + o);
@@ -641,18 +672,18 @@ __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A,
     }
     return;
   }
-  if (vec && m0 + BM <= M && n0 + BN <= N) {
+  if (vec && m0 + BM <= M && n0 + BNT <= N) {
     // interior tile: no per-lane bounds, only wave-uniform branches (an
     // exec-masked branch per element costs more than the stores themselves)
-    float bv[4][4];
+    float bv[NJ][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) bv[j][r] = bias != nullptr ? bias[ncol + j * 16 + r] : 0.f;
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         if (probe == 2 && j != 0) continue;
         const size_t o = (size_t)(mrow + i * 16) * ldc + ncol + j * 16 - (probe == 3 ? (size_t)m0 * ldc + n0 : 0);
         float z[4];
@@ -688,8 +719,8 @@ __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A,
     const int m = m0 + wr * 128 + i * 16 + (lane & 15);
     if (m >= M) continue;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wc * 64 + j * 16 + 4 * (lane >> 4);
+    for (int j = 0; j < NJ; ++j) {
+      const int n = n0 + wc * WN + j * 16 + 4 * (lane >> 4);
       if (n >= N) continue;
       const size_t o = (size_t)m * ldc + n;
       const bool full = vec && n + 3 < N;
@@ -805,7 +836,7 @@ static SplitPlan plan_split(int M, int N, int K, int c_bf16, float beta, int act
 // Bytes of fp32 workspace dtfk_gemm_big needs for this product (0: none).
 extern "C" long long dtfk_gemm_big_workspace(int M, int N, int K, int c_bf16, float beta, int act, int split_k,
                                              int variant) {
-  const bool ph8 = variant == 8 || (variant == 0 && K % 128 == 0);
+  const bool ph8 = variant >= 8 || (variant == 0 && K % 128 == 0);
   const dtfk::gemm2::SplitPlan p = dtfk::gemm2::plan_split(M, N, K, c_bf16, beta, act, split_k, ph8);
   return p.slabs ? (long long)p.split * M * N * 4 : 0;
 }
@@ -832,8 +863,9 @@ extern "C" int dtfk_gemm_big_supported(const void* A, int lda, int transA, const
 // Returns hipErrorInvalidValue (launching nothing) when the shape contract
 // (dtfk_gemm_big_supported) does not hold.  split_k <= 0: automatic.
 // variant: 0 = automatic (the 8-phase schedule whenever every workgroup's K
-// range is a multiple of 128, else the one-barrier loop), 4 = one-barrier loop
-// (gemm_big VAR 4), 8 = 8-phase (hipErrorInvalidValue if K % 128).
+// range is a multiple of 128 -- 192-wide tiles where they fill the CUs better
+// -- else the one-barrier loop), 4 = one-barrier loop (gemm_big VAR 4), 8 =
+// 8-phase 256-wide, 9 = 8-phase 192-wide where unsplit (hipErrorInvalidValue if K % 128).
 extern "C" hipError_t dtfk_gemm_big(const void* A, int lda, int transA, const void* B, int ldb, int transB,
                                     void* C, int c_bf16, int ldc, const float* bias, int M, int N, int K,
                                     float alpha, float beta, int act, int split_k, int variant, void* ws,
@@ -842,8 +874,8 @@ extern "C" hipError_t dtfk_gemm_big(const void* A, int lda, int transA, const vo
   const bool akc = !transA, bkc = transB != 0;
   if (!dtfk_gemm_big_supported(A, lda, transA, B, ldb, transB, c_bf16, M, N, K, beta, act, split_k))
     return hipErrorInvalidValue;
-  if (variant != 0 && variant != 4 && variant != 8) return hipErrorInvalidValue;
-  const bool ph8 = variant == 8 || (variant == 0 && K % 128 == 0);
+  if (variant != 0 && variant != 4 && variant != 8 && variant != 9) return hipErrorInvalidValue;
+  const bool ph8 = variant >= 8 || (variant == 0 && K % 128 == 0);
   if (ph8 && K % 128) return hipErrorInvalidValue;
   const int tn = (N + BN - 1) / BN;
   // 256 x 256 tiles even when they leave CUs idle (N = 768: 192 tiles): measured
@@ -875,6 +907,12 @@ extern "C" hipError_t dtfk_gemm_big(const void* A, int lda, int transA, const vo
     const hipError_t e = hipMemset2DAsync(C, (size_t)ldc * sizeof(float), 0, (size_t)N * sizeof(float), M, stream);
     if (e != hipSuccess) return e;
   }
+  // 192-wide tiles when 256-wide ones leave a wave of tiles partly empty
+  // (BERT-base: N = 768 -> 192 tiles for 256 CUs, N = 2304 -> 2.25 waves)
+  const long long tiles192 = (long long)((M + 255) / 256) * ((N + 191) / 192);
+  auto fill = [](long long t) { return (double)t / (double)(((t + 255) / 256) * 256); };
+  const bool w192 = ph8 && split == 1 && (variant == 9 || (variant == 0 && fill(tiles192) > fill(tiles) + 0.1));
+  const dim3 grid192((unsigned)tiles192, 1);
   const dim3 grid((unsigned)tiles, split), block(NTHR);
   const uint16_t* a = static_cast<const uint16_t*>(A);
   const uint16_t* b = static_cast<const uint16_t*>(B);
@@ -885,6 +923,9 @@ extern "C" hipError_t dtfk_gemm_big(const void* A, int lda, int transA, const vo
   if (ph8 && split > 1)                                                                                          \
     hipLaunchKernelGGL((gemm_8ph<AK, BKk, false, false>), grid, block, 0, stream, a, lda, b, ldb, C, ldc, bias, M, \
                        N, K, alpha, 1.f, act, kchunk);                                                           \
+  else if (w192)                                                                                                 \
+    hipLaunchKernelGGL((gemm_8ph<AK, BKk, OB, true, 192>), grid192, block, 0, stream, a, lda, b, ldb, C, ldc, bias, \
+                       M, N, K, alpha, beta, act, kchunk);                                                       \
   else if (ph8)                                                                                                  \
     hipLaunchKernelGGL((gemm_8ph<AK, BKk, OB, true>), grid, block, 0, stream, a, lda, b, ldb, C, ldc, bias, M, N, \
                        K, alpha, beta, act, kchunk);                                                             \
@@ -933,6 +974,11 @@ extern "C" hipError_t dtfk_gemm_big_cfg(int cfg, const void* A, int lda, const v
       if (K % 128) return hipErrorInvalidValue;
       hipLaunchKernelGGL((gemm_8ph<true, true, true, true>), dim3((M / 256) * tn, 1), dim3(NTHR), 0, stream, a, lda, b, ldb,
                          C, ldc, nullptr, M, N, K, 1.f, 0.f, cfg == 10 ? 0 : 10 - cfg, K);
+      break;
+    case 14:   // 192-wide 8-phase tiles (N % 192 == 0)
+      if (K % 128 || N % 192) return hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_8ph<true, true, true, true, 192>), dim3((M / 256) * (N / 192), 1), dim3(NTHR), 0,
+                         stream, a, lda, b, ldb, C, ldc, nullptr, M, N, K, 1.f, 0.f, 0, K);
       break;
     default: return hipErrorInvalidValue;
   }

@@ -42,6 +42,7 @@ def main():
             y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
             row = {"M": M, "N": N, "K": K}
             for name, f in (("v8", lambda: C.gemm_big(x, False, w, True, y, variant=8)),
+                            ("v8_w192", lambda: C.gemm_big_cfg(14, x, w, y)),
                             ("v8_noepi", lambda: C.gemm_big_cfg(11, x, w, y)),
                             ("v8_quarter", lambda: C.gemm_big_cfg(12, x, w, y)),
                             ("v8_samedst", lambda: C.gemm_big_cfg(13, x, w, y)),

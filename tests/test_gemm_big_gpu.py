@@ -31,12 +31,12 @@ def _rel(x, y):
     return float((x.float() - y).norm() / y.norm().clamp_min(1e-12))
 
 
-@pytest.mark.parametrize("variant", [4, 8])
+@pytest.mark.parametrize("variant", [4, 8, 9])
 @pytest.mark.parametrize("tA,tB", [(False, True), (False, False), (True, False), (True, True)])
 @pytest.mark.parametrize("M,N,K", [(512, 512, 256), (1000, 776, 192), (4096, 768, 768), (136, 264, 64),
                                    (1000, 776, 384), (136, 264, 128)])
 def test_layouts_fp32_out(native, tA, tB, M, N, K, variant):
-    if variant == 8 and K % 128:
+    if variant >= 8 and K % 128:
         pytest.skip("8-phase schedule: K % 128 == 0")
     A, B = _operands(M, N, K, tA, tB, M + N + K)
     C = torch.full((M, N), float("nan"), device="cuda")
@@ -46,19 +46,20 @@ def test_layouts_fp32_out(native, tA, tB, M, N, K, variant):
     assert _rel(C, ref) < 1e-5, _rel(C, ref)
 
 
+@pytest.mark.parametrize("variant", [8, 9])
 @pytest.mark.parametrize("obf", [True, False])
 @pytest.mark.parametrize("act", [0, 1, 2, 4])
-def test_out_bias_act(native, act, obf):
+def test_out_bias_act(native, act, obf, variant):
     M, N, K = 2048, 1024, 512
     A, B = _operands(M, N, K, False, True, act)
     bias = torch.randn(N, device="cuda")
     C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16 if obf else torch.float32)
-    assert native.gemm_big(A, False, B, True, C, bias=bias, act=act, alpha=0.5)
+    assert native.gemm_big(A, False, B, True, C, bias=bias, act=act, alpha=0.5, variant=variant)
     ref = _ref(A, False, B, True, bias, act, 0.5)
     assert _rel(C, ref) < (1e-2 if obf else 1e-5)
 
 
-@pytest.mark.parametrize("variant,K", [(0, 320), (8, 384)])
+@pytest.mark.parametrize("variant,K", [(0, 320), (8, 384), (9, 384)])
 @pytest.mark.parametrize("obf", [False, True])
 def test_beta_accumulate(native, obf, variant, K):
     M, N = 768, 1280
@@ -107,19 +108,20 @@ def test_linear_layer_products_match_torch(native):
     assert _rel(dw, gy.float().t() @ x.float()) < 1e-5
 
 
+@pytest.mark.parametrize("variant", [8, 9])
 @pytest.mark.parametrize("tA,tB", [(False, True), (False, False), (True, False)])
 @pytest.mark.parametrize("M,N,K", [(4096, 3072, 768), (16384, 768, 3072), (2304, 768, 4096)])
-def test_8phase_race_screen(native, tA, tB, M, N, K):
+def test_8phase_race_screen(native, tA, tB, M, N, K, variant):
     """The 8-phase schedule's LDS hand-offs are placed by vmcnt / barrier count:
     a read placed one phase early passes reference checks whenever the DMA
     lands first, so every run of one shape must be bitwise identical (fixed
     summation order) and match the reference."""
     A, B = _operands(M, N, K, tA, tB, 5)
     C = torch.empty(M, N, device="cuda")
-    assert native.gemm_big(A, tA, B, tB, C, split_k=1, variant=8)
+    assert native.gemm_big(A, tA, B, tB, C, split_k=1, variant=variant)
     first = C.clone()
     assert _rel(first, _ref(A, tA, B, tB)) < 1e-5
     for _ in range(12):
         C.fill_(float("nan"))
-        native.gemm_big(A, tA, B, tB, C, split_k=1, variant=8)
+        native.gemm_big(A, tA, B, tB, C, split_k=1, variant=variant)
         assert torch.equal(C, first)

@@ -47,13 +47,17 @@ def main():
             "dx": {"ours": lambda: C.gemm_big(gy, False, w, False, gx),
                    "ours_v4": lambda: C.gemm_big(gy, False, w, False, gx, variant=4),
                    "torch": lambda: torch.mm(gy, w, out=gx)},
+            # input gradient accumulated onto a residual branch's (beta = 1), as models/bert.py runs it
+            "dx_res": {"ours": lambda: C.gemm_big(gy, False, w, False, gx, beta=1.0),
+                       "ours_v4": lambda: C.gemm_big(gy, False, w, False, gx, beta=1.0, variant=4),
+                       "torch": lambda: gx.addmm_(gy, w)},
             "dw": {"ours": lambda: C.gemm_big(gy, True, x, False, dw, beta=1.0, split_k=0),
                    "ours_v4": lambda: C.gemm_big(gy, True, x, False, dw, beta=1.0, split_k=0, variant=4),
                    "torch": lambda: torch.addmm(dw, gy.t(), x, out_dtype=torch.float32, out=dw),
                    "torch_slabs": lambda: bert._wgrad(gy, x, into=dw)},
         }
         for role, fns in roles.items():
-            M, N, K = {"fwd": (T, O, I), "dx": (T, I, O), "dw": (O, I, T)}[role]
+            M, N, K = {"fwd": (T, O, I), "dx": (T, I, O), "dx_res": (T, I, O), "dw": (O, I, T)}[role]
             flop = 2.0 * M * N * K
             times = {k: [] for k in fns}
             for f in fns.values():

@@ -7,9 +7,9 @@ GEMM (csrc/kernels/gemm_big.hip), with no transpose copies:
 
 Shapes outside the kernel's contract (K % 64, 16-byte alignment) go to
 torch's GEMM (hipBLASLt).  `use_native(role, M, N, K)` decides per product
-which engine a model runs: DTF_BIG_GEMM=never (default) / always, or auto --
-both engines timed once per shape on scratch operands, the faster one kept
-(`scripts/bench_gemm.py` prints the same comparison for the BERT shapes).
+which engine a model runs: DTF_BIG_GEMM=auto (default) -- both engines timed
+once per shape on scratch operands, the faster one kept -- never (hipBLASLt),
+or always (`scripts/bench_gemm.py` prints the same comparison for BERT's shapes).
 """
 from __future__ import annotations
 
@@ -19,12 +19,12 @@ import torch
 
 from .. import _native
 
-# never (default): hipBLASLt runs the model GEMMs -- with the 8-phase schedule
-# this kernel is 0.77-0.90x of it on BERT-base's forward / input-gradient
-# shapes and 0.81-1.02x on the weight gradients (profiles/gemm_8ph_r3.txt); end
-# to end 'auto' measured 1.1 % and 'always' 12 % slower than 'never';
-# auto: time both once per shape, keep the faster; always: this kernel
-_POLICY = os.environ.get("DTF_BIG_GEMM", "never")
+# auto (default): both engines timed once per shape (best of 3 rounds), the
+# faster one kept -- with the 8-phase schedule this kernel is 0.93-1.09x of
+# hipBLASLt on BERT-base's forward / input-gradient shapes and 0.82-1.03x on the
+# weight gradients (profiles/gemm_8ph_r3.txt); end to end 'auto' measured equal
+# to 'never' and 'always' 3 % slower;  never: hipBLASLt;  always: this kernel
+_POLICY = os.environ.get("DTF_BIG_GEMM", "auto")
 _choice: dict = {}
 _timings: dict = {}
 
@@ -33,15 +33,23 @@ def _C():
     return _native.load()
 
 
-def _time(fn, reps=5):
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+def _time(fn, reps=5, rounds=3):
+    """Best-of-`rounds` mean time (ms) of `reps` back-to-back calls."""
     fn()
-    s.record()
-    for _ in range(reps):
-        fn()
-    e.record()
-    e.synchronize()
-    return s.elapsed_time(e) / reps
+    best = float("inf")
+    for _ in range(rounds):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            fn()
+        e.record()
+        e.synchronize()
+        best = min(best, s.elapsed_time(e) / reps)
+    return best
+
+
+def policy() -> str:
+    return _POLICY
 
 
 def _candidates(role, M, N, K, dev):
@@ -71,7 +79,7 @@ def use_native(role: str, M: int, N: int, K: int, dev) -> bool:
     """True when gemm_big should run this product: the policy, the kernel's
     shape contract (K % 64), and -- under 'auto' -- a one-time timing of both
     engines on scratch operands of the shape (cached per process)."""
-    if _POLICY == "never" or K % 64:
+    if _POLICY == "never" or K % 64 or torch.device(dev).type != "cuda":
         return False
     if _POLICY == "always":
         return True

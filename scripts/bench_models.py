@@ -233,6 +233,11 @@ def dense_bench(a, w):
                "data": "synthetic", "config": cfg, "final_loss": float(loss)}
         if a.model == "bert_base":
             out["tokens_per_s"] = round(v * a.seq, 1)
+            from distributed_tensorflow_example_amd.ops import big_gemm
+            ch = big_gemm.choices()
+            out["config"]["linear_gemm_policy"] = big_gemm.policy()
+            if ch:   # which linear products ran on gemm_big.hip (auto: timed per shape)
+                out["config"]["linear_gemm_native"] = {f"{k[0]}:{k[1]}x{k[2]}x{k[3]}": v[0] for k, v in ch.items()}
         if sweep:
             out["bucket_sweep"] = sweep
         out["config"]["grad_comm_dtype"] = "bf16" if a.comm_bf16 else "fp32"

@@ -54,6 +54,7 @@ hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int n
                                 int rank, int gbf16, long long* phase_ts, int spread, int xmode, int split,
                                 hipStream_t stream);
 long long dtfk_graph_mlp_part_floats(int B, int H);
+hipError_t dtfk_graph_feed_ingest(const void* host, void* dev, long long bytes, hipStream_t stream);
 hipError_t dtfk_graph_mlp_step(const float* x, const float* ylab, float* W1, float* b1, float* W2, float* b2,
                                float* a2buf, float* dz2buf, float* part, float* gW1, float* gb1, float* gW2,
                                float* gb2, float* metrics, float* host_metrics, void* gstep, int gstep_kind,
@@ -589,6 +590,10 @@ class GraphStepPlan {
     direct_feed_ = df != nullptr && df[0] == '1';
     const char* hs = getenv("DTF_GRAPH_STEP_METRICS_COPY");   // 1: copy the metrics back with a D2H op
     host_store_ = !(hs != nullptr && hs[0] == '1');
+    // 1: the feed read over PCIe by an ingest kernel instead of the copy engine
+    // (system-scope 8-byte loads: 17 us for the 0.3 MB feed vs ~15 us by DMA -- kept off)
+    const char* fk = getenv("DTF_GRAPH_STEP_FEED_KERNEL");
+    kernel_feed_ = fk != nullptr && fk[0] == '1';
     for (const at::Tensor* t : {&W1, &b1, &W2, &b2})
       TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous(),
                   "GraphStepPlan: fp32 contiguous device parameters expected");
@@ -602,7 +607,8 @@ class GraphStepPlan {
       gkind_ = gstep_kind_of(*gstep);
       gstep_ = *gstep;
     }
-    nfeed_ = (int64_t)B_ * K_ + (int64_t)B_ * C_ + 4;   // x | y | lr (+ pad)
+    nfeed_ = ((int64_t)B_ * K_ + (int64_t)B_ * C_ + 1 + 3) / 4 * 4;   // x | y | lr, padded to 16 bytes
+    feed_bytes_ = nfeed_ * (int64_t)sizeof(float);
     auto fo = W1.options();
     dev_ = at::empty({nfeed_}, fo);
     a2_ = at::empty({(int64_t)BP * HP_}, fo);
@@ -665,8 +671,11 @@ class GraphStepPlan {
           std::memcpy(h + nx, yp, sizeof(float) * ny);
           h[nx + ny] = (float)lr;
           t_[0] += std::chrono::duration<double, std::micro>(clk::now() - t0).count();
-          hip_check(hipMemcpyAsync(d, h, sizeof(float) * (nx + ny + 1), hipMemcpyHostToDevice, st),
-                    "GraphStepPlan: feed copy");
+          if (kernel_feed_)   // workgroups read the pinned slot over PCIe (no copy-engine op)
+            hip_check(dtfk_graph_feed_ingest(h, d, feed_bytes_, st), "GraphStepPlan: feed ingest");
+          else
+            hip_check(hipMemcpyAsync(d, h, sizeof(float) * (nx + ny + 1), hipMemcpyHostToDevice, st),
+                      "GraphStepPlan: feed copy");
         }
         hip_check(hipEventRecord(ev_[slot], st), "GraphStepPlan: event");
         hip_check(launch_step(st, host_store_), "GraphStepPlan: launch");
@@ -755,7 +764,8 @@ class GraphStepPlan {
   int B_, K_ = 0, H_ = 0, C_ = 0, HP_ = 0, act_, gkind_ = 0, slot_ = 0;
   bool naive_, use_graph_, direct_feed_ = false;
   int64_t nfeed_ = 0, steps_ = 0;
-  bool host_store_ = true;
+  bool host_store_ = true, kernel_feed_ = false;
+  int64_t feed_bytes_ = 0;
   double t_[3] = {0, 0, 0};
 };
 

@@ -623,6 +623,23 @@ __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A,
     const bool rb_on = lane < 8 * LPR;
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
+      // beta != 0: this half's C chunks are loaded first, all at once (the
+      // operand-fragment registers are free after the loop), so their latency
+      // hides under the LDS round trip instead of one load per store
+      typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+      u32x4 cpre[OBF ? 8 : 16];
+      if (beta != 0.f && rb_on) {
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+          const size_t o = (size_t)(m0 + wr * 128 + half * 64 + it * 8 + rsub) * ldc + n0 + wc * WN + c8;
+          if constexpr (OBF) {
+            cpre[it] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const uint16_t*>(C) + o);
+          } else {
+            cpre[2 * it] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const float*>(C) + o);
+            cpre[2 * it + 1] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const float*>(C) + o + 4);
+          }
+        }
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -643,18 +660,17 @@ __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A,
         const size_t o = (size_t)(m0 + wr * 128 + half * 64 + lrow) * ldc + n0 + wc * WN + c8;
         if (beta != 0.f) {
           if constexpr (OBF) {
-            const uint4 c = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(C) + o);
-            const uint32_t cw[4] = {c.x, c.y, c.z, c.w};
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-              z[2 * q] += beta * bf2f((uint16_t)(cw[q] & 0xffff));
-              z[2 * q + 1] += beta * bf2f((uint16_t)(cw[q] >> 16));
+              z[2 * q] += beta * bf2f((uint16_t)(cpre[it][q] & 0xffff));
+              z[2 * q + 1] += beta * bf2f((uint16_t)(cpre[it][q] >> 16));
             }
           } else {
-            const float4 c0 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(C) + o);
-            const float4 c1 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(C) + o + 4);
-            z[0] += beta * c0.x; z[1] += beta * c0.y; z[2] += beta * c0.z; z[3] += beta * c0.w;
-            z[4] += beta * c1.x; z[5] += beta * c1.y; z[6] += beta * c1.z; z[7] += beta * c1.w;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              z[q] += beta * __uint_as_float(cpre[2 * it][q]);
+              z[4 + q] += beta * __uint_as_float(cpre[2 * it + 1][q]);
+            }
           }
         }
         if (act != ACT_NONE) {

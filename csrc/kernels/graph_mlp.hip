@@ -31,6 +31,8 @@
 // K >= 1, H <= 128, C <= 16.
 #include "common.h"
 
+#include <algorithm>
+
 namespace dtfk {
 namespace gmlp {
 
@@ -158,6 +160,14 @@ __global__ __launch_bounds__(HW * 64) void graph_mlp_head(HeadArgs a) {
   const int rt = blockIdx.x, rb = rt * 16;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
+  // wave 0's softmax operands first (labels of its 4 rows, b2): issued before
+  // the staging below so their latency is not a separate round trip later
+  float labp[4] = {0.f, 0.f, 0.f, 0.f}, b2p = 0.f;
+  if (w == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) labp[i] = pin(a.ylab[(size_t)min(rb + 4 * g + i, B - 1) * C + min(r, C - 1)]);
+    b2p = pin(a.b2[min(r, C - 1)]);
+  }
   // operands, branch-free (clamped + masked): a2 tile, W2, this lane's label / b2
   for (int i = tid; i < 16 * HP / 4; i += HW * 64)
     reinterpret_cast<float4*>(a2s)[i] = reinterpret_cast<const float4*>(a.a2 + (size_t)rb * HP)[i];
@@ -178,15 +188,14 @@ __global__ __launch_bounds__(HW * 64) void graph_mlp_head(HeadArgs a) {
     f32x4 acc = zp[0][lane];
 #pragma unroll
     for (int q = 1; q < HW; ++q) acc += zp[q][lane];
-    const float b2v = r < C ? a.b2[min(r, C - 1)] : 0.f;
+    const float b2v = r < C ? b2p : 0.f;
     float loss_part = 0.f, corr_part = 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = rb + 4 * g + i;               // row; column = r (class)
       const bool valid = m < B;
       const bool cl = r < C;
-      const float labv = a.ylab[(size_t)min(m, B - 1) * C + min(r, C - 1)];
-      const float lab = (valid && cl) ? labv : 0.f;
+      const float lab = (valid && cl) ? labp[i] : 0.f;
       const float z = cl ? acc[i] + b2v : -INFINITY;
       const float mx = row16_max(z);
       const float e = cl ? expf(z - mx) : 0.f;
@@ -373,8 +382,33 @@ __global__ __launch_bounds__(256) void graph_mlp_wgrad(WgradArgs a) {
   }
 }
 
+// Feed ingest: the step's packed feed (x | y_ | lr) read straight from the
+// pinned host staging slot over PCIe by many workgroups (16-byte loads), instead
+// of a copy-engine transfer -- for a ~0.3 MB feed the DMA's setup / completion
+// latency is most of its time.  n4: 16-byte chunks (the tail pads to a chunk).
+// The slot is rewritten by the host every other step: system-scope loads (no
+// stale cached copy of the previous use).
+__global__ __launch_bounds__(256) void feed_ingest(const uint4* __restrict__ host, uint4* __restrict__ dev,
+                                                   long long n4) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    const unsigned long long lo = ld_sys_u64(host + i), hi = ld_sys_u64(reinterpret_cast<const char*>(host + i) + 8);
+    dev[i] = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+  }
+}
+
 }  // namespace gmlp
 }  // namespace dtfk
+
+extern "C" hipError_t dtfk_graph_feed_ingest(const void* host, void* dev, long long bytes, hipStream_t stream) {
+  if (bytes <= 0) return hipSuccess;
+  if ((reinterpret_cast<uintptr_t>(host) | reinterpret_cast<uintptr_t>(dev) | (uintptr_t)bytes) & 15)
+    return hipErrorInvalidValue;
+  const long long n4 = bytes / 16;
+  const unsigned grid = (unsigned)std::min<long long>(160, (n4 + 255) / 256);
+  hipLaunchKernelGGL(dtfk::gmlp::feed_ingest, dim3(grid), dim3(256), 0, stream, static_cast<const uint4*>(host),
+                     static_cast<uint4*>(dev), n4);
+  return hipGetLastError();
+}
 
 // Device scratch (floats) the step needs besides a2 / dz2: L2's partials + loss sums.
 extern "C" long long dtfk_graph_mlp_part_floats(int B, int H) {

@@ -33,7 +33,10 @@
 //          wave 7 also: dW2 (28 MFMAs), db1, db2, metrics, update of the LDS
 //          copies of W2[block j], b1[block j], b2 -- identical in every
 //          workgroup that holds them (same inputs, same order).
-//    Two LDS barriers and two inter-workgroup edges per step; the data of
+//      P2 runs without a workgroup barrier: each 32-row batch chunk of the
+//          weight gradient starts as soon as the heads of its batch tiles have
+//          set their LDS flags; wave 7 signals the next step's stage with a flag.
+//    One LDS barrier and two inter-workgroup edges per step; the data of
 //    every edge is double-buffered by step parity and tagged with the global
 //    exchange sequence number, so buffers are never reset between launches.
 //  * x enters the MFMAs as exact integers 0..255 (v_cvt_f32_ubyte); the 1/255
@@ -183,7 +186,8 @@ struct Args {
                             // 1 two-shot (reduce-scatter by wave chunk, then all-gather of the sums)
   int dbg;                  // profiling only (DTF_PERSIST_DBG): bit 0 = never stage the next step's x (wrong
                             // numerics; what the per-step LDS-DMA stage costs the hand-offs), bit 1 = head
-                            // sub-phase stamps (slots 13-15, wave 0)
+                            // sub-phase stamps (slots 13-15, wave 0), bits 2 / 3 = stage (half) after the
+                            // first head, bit 4 = longer sleeps in the chunk polls (tuning)
 };
 
 // phase stamp ph of step st (s_memrealtime, 100 MHz) -- profiling only
@@ -745,7 +749,30 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
     const bool more = st + 1 < a.nsteps;
     // everyone's reads of this step's stage retired at barrier A: wave 7 (idle
     // until P2) stages the next step while the others run the edges and the head
-    if (w == 7 && more && !(a.dbg & 1)) stage_x(st + 1, 0, 1);
+    int* hflag = reinterpret_cast<int*>(smem + L_HFLAG);   // [0..6] head of batch tile v done; [7] stage landed
+    auto heads_done = [&]() -> unsigned {   // bit v: head of batch tile v finished this step
+      const bool ok = lane < NBT && __hip_atomic_load(hflag + (lane < NBT ? lane : 0), __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_WORKGROUP) >= st + 1;
+      return (unsigned)__ballot(ok) & ((1u << NBT) - 1u);
+    };
+    if (w == 7 && more && !(a.dbg & 1)) {
+      // DTF_PERSIST_DBG bits 2 / 3 (tuning): the whole stage / its second half only
+      // once the first head is done (its DMA then does not queue in front of this
+      // CU's E1 / E2 gather loads)
+      if (a.dbg & 8) stage_x(st + 1, 0, 2);
+      if (a.dbg & 12) {
+        while (heads_done() == 0u) __builtin_amdgcn_s_sleep(1);
+      }
+      if (a.dbg & 8) stage_x(st + 1, 1, 2);
+      else stage_x(st + 1, 0, 1);
+      // idle until the first head is done anyway: wait for the DMA here and tell the
+      // other waves the next step's operands are in LDS
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+      if (lane == 0) __hip_atomic_store(hflag + 7, st + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else if (w == 7 && more && lane == 0) {
+      __hip_atomic_store(hflag + 7, st + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
 
     // ---------------- E1 + P1 + E2 + head (wave w < 7: batch tile w)
     if (w < NBT) {
@@ -882,58 +909,13 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
                            __HIP_MEMORY_SCOPE_WORKGROUP);
       if (w == 0) { PH(9); }
     }
-    // wave 7 (idle since staging the next step): sums the 7 head waves' dW2 / db1 /
-    // db2 partials and metrics in fixed tile order (bit-identical to folding them
-    // one by one); one GPU: the W2 / b1 / b2 updates too
-    f32x4 D = {0.f, 0.f, 0.f, 0.f};      // wave 7: dW2[16j+4g+i][class r] (x B)
-    float gb = 0.f;                      // wave 7: db1 (lanes < 16) / db2 (lanes 16..25) (x B)
-    float ls = 0.f, cr = 0.f;            // wave 7: loss / correct sums of the batch
-    if (w == 7) {
-      const int* hflag = reinterpret_cast<const int*>(smem + L_HFLAG);
-      // lane < 16: db1 column `lane`; 16..25: db2 column lane - 16 (rdb2 follows rdb1 by 128 floats)
-      const float* gsrc = rdb1 + (lane < 16 ? lane : (lane < 16 + NCLS ? lane + 112 : 0));
-      for (;;) {   // lane v < 7 watches head v: all flags in one poll
-        const bool ok = lane >= NBT ||
-                        __hip_atomic_load(hflag + (lane < NBT ? lane : 0), __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_WORKGROUP) >= st + 1;
-        if (__all(ok)) break;
-        __builtin_amdgcn_s_sleep(1);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-      const f32x4* dw2p = reinterpret_cast<const f32x4*>(smem + L_DW2P);
-#pragma unroll
-      for (int v = 0; v < NBT; ++v) {
-        D += dw2p[v * 64 + lane];
-        gb += gsrc[v * 16];
-        ls += rmet[2 * v];
-        cr += rmet[2 * v + 1];
-      }
-      if (lane >= 16 + NCLS) gb = 0.f;
-      PH7(13);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next step's stage landed (long since)
-      PH7(15);
-      if constexpr (!MULTI) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (16 * j + 4 * g + i < HID && r < NCLS) w2s[(4 * g + i) * 16 + r] -= lrB * D[i];
-        if (lane < 16) {
-          if (16 * j + lane < HID) b1s[lane] -= lrB * gb;
-        } else if (lane < 16 + NCLS) {
-          b2s[lane - 16] -= lrB * gb;
-        }
-      }
-    }
-    lds_barrier();
-    if (w == 0) { PH(10); }
-    if (w == 7 && c == 0 && lane == 63) {   // after the barrier: its store is never waited for there
-      const int sl = (int)((gstep0 + st) % a.ring);
-      a.metrics[2 * sl] = ls / (float)B;
-      a.metrics[2 * sl + 1] = cr / (float)B;
-    }
-    if (*abort_flag) { aborted = true; break; }
-    if (more) read_xf();   // next step's forward operands and label (dead since P0 / the head)
-
-    // ---------------- P2: weight gradients of the wave's tiles
+    // ---------------- P2 without a workgroup barrier: a wave multiplies the weight-
+    // gradient chunk of batch rows 32cc..32cc+31 as soon as the heads of its batch
+    // tiles are done (LDS flags), chunks in order (one accumulator chain:
+    // deterministic; separate per-chunk accumulators for arrival order spill).
+    // Barrier B used to wait for the LAST head before any chunk started: ~1.2 us of
+    // every step.  Reuse of everything the heads wrote is still fenced by barrier A
+    // of the next step.
     f32x4 G[NTW];                        // dW1[16ft+4g+i][16j+r] (x 255 B)
 #pragma unroll
     for (int k = 0; k < NTW; ++k) G[k] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -942,6 +924,13 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
       // B = the dz2 pieces; an absent second tile computes a zero-weight copy (unused)
 #pragma unroll
       for (int cc = 0; cc < 4; ++cc) {
+        const unsigned need = (1u << (2 * cc)) | (2 * cc + 1 < NBT ? 1u << (2 * cc + 1) : 0u);
+        while ((heads_done() & need) != need) {
+          if (a.dbg & 16) __builtin_amdgcn_s_sleep(2);
+          else __builtin_amdgcn_s_sleep(0);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+        if (cc == 0 && w == 0) { PH(10); }
         const uint16_t* bp = dzp + r * PS + 32 * cc + 8 * g;
         const bf16x8 Bh = *reinterpret_cast<const bf16x8*>(bp);
         const bf16x8 Bm = *reinterpret_cast<const bf16x8*>(bp + 16 * PS);
@@ -962,23 +951,76 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
         }
       }
     } else {
+      // one batch tile at a time, in tile order (single accumulator chain)
+      f32x4 g0[NTW], g1[NTW];
 #pragma unroll
-    for (int k = 0; k < NTW; ++k) {
-      if (tvk(k)) {
-        f32x4 g0 = {0.f, 0.f, 0.f, 0.f}, g1 = {0.f, 0.f, 0.f, 0.f};
+      for (int k = 0; k < NTW; ++k) g0[k] = g1[k] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int s = 0; s < NBT; ++s) {
-          const f32x4 bz = *reinterpret_cast<const f32x4*>(dz2T + r * LS + 16 * s + 4 * g);
-          g0 = mfma4(ub(xt[k][s], 0), bz[0], g0);
-          g1 = mfma4(ub(xt[k][s], 1), bz[1], g1);
-          g0 = mfma4(ub(xt[k][s], 2), bz[2], g0);
-          g1 = mfma4(ub(xt[k][s], 3), bz[3], g1);
+      for (int s = 0; s < NBT; ++s) {
+        while (((heads_done() >> s) & 1u) == 0u) __builtin_amdgcn_s_sleep(0);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+        if (s == 0 && w == 0) { PH(10); }
+        const f32x4 bz = *reinterpret_cast<const f32x4*>(dz2T + r * LS + 16 * s + 4 * g);
+#pragma unroll
+        for (int k = 0; k < NTW; ++k) {
+          if (tvk(k)) {
+            g0[k] = mfma4(ub(xt[k][s], 0), bz[0], g0[k]);
+            g1[k] = mfma4(ub(xt[k][s], 1), bz[1], g1[k]);
+            g0[k] = mfma4(ub(xt[k][s], 2), bz[2], g0[k]);
+            g1[k] = mfma4(ub(xt[k][s], 3), bz[3], g1[k]);
+          }
         }
-        G[k] = g0 + g1;
+      }
+#pragma unroll
+      for (int k = 0; k < NTW; ++k) G[k] = g0[k] + g1[k];
+    }
+    // every head is done here.  Wave 7 sums the 7 head waves' dW2 / db1 / db2
+    // partials and metrics in fixed tile order (all loads in flight at once); one
+    // GPU: the W2 / b1 / b2 updates too (their readers, this step's heads, are done;
+    // the next step's read them after barrier A)
+    f32x4 D = {0.f, 0.f, 0.f, 0.f};      // wave 7: dW2[16j+4g+i][class r] (x B)
+    float gb = 0.f;                      // wave 7: db1 (lanes < 16) / db2 (lanes 16..25) (x B)
+    if (w == 7) {
+      float ls = 0.f, cr = 0.f;          // loss / correct sums of the batch
+      // lane < 16: db1 column `lane`; 16..25: db2 column lane - 16 (rdb2 follows rdb1 by 128 floats)
+      const float* gsrc = rdb1 + (lane < 16 ? lane : (lane < 16 + NCLS ? lane + 112 : 0));
+      const f32x4* dw2p = reinterpret_cast<const f32x4*>(smem + L_DW2P);
+#pragma unroll
+      for (int v = 0; v < NBT; ++v) {
+        D += dw2p[v * 64 + lane];
+        gb += gsrc[v * 16];
+        ls += rmet[2 * v];
+        cr += rmet[2 * v + 1];
+      }
+      if (lane >= 16 + NCLS) gb = 0.f;
+      PH7(13);
+      PH7(15);
+      if (c == 0 && lane == 63) {
+        const int sl = (int)((gstep0 + st) % a.ring);
+        a.metrics[2 * sl] = ls / (float)B;
+        a.metrics[2 * sl + 1] = cr / (float)B;
+      }
+      if constexpr (!MULTI) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (16 * j + 4 * g + i < HID && r < NCLS) w2s[(4 * g + i) * 16 + r] -= lrB * D[i];
+        if (lane < 16) {
+          if (16 * j + lane < HID) b1s[lane] -= lrB * gb;
+        } else if (lane < 16 + NCLS) {
+          b2s[lane - 16] -= lrB * gb;
+        }
       }
     }
+    if (*abort_flag) { aborted = true; break; }   // final for this step: every head has reported
+    if (more) {
+      // next step's operands (this step's are consumed): x rows + label once wave 7
+      // saw the stage land, x^T
+      while (__hip_atomic_load(hflag + 7, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < st + 1)
+        __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+      read_xf();
+      read_xt();
     }
-    if (more) read_xt();   // next step's weight-gradient operands (this step's are consumed)
     if (w == 0) { PH(11); }
     if constexpr (MULTI) {
       // ---- exchange of this workgroup's gradient with the same workgroup on

@@ -148,7 +148,8 @@ constexpr int PS = XTS + 8;                            // split mode: bf16 plane
 constexpr int L_DZP = L_LAB + 128;                     // split mode: [3 pieces][16 hidden][PS] dz2 bf16
 constexpr int L_HFLAG = L_DZP + 3 * 16 * PS * 2;       // [8] head-done flags (step + 1) of waves 0..6
 constexpr int L_DW2P = L_HFLAG + 64;                   // [7 batch tiles][64 lanes] f32x4 dW2 partials
-constexpr int LDS_COMPUTE = L_DW2P + NBT * 64 * 16;
+constexpr int L_RLOSS = L_DW2P + NBT * 64 * 16;        // [2][128] per-row loss / correct of the step
+constexpr int LDS_COMPUTE = L_RLOSS + 2 * 128 * 4;
 static_assert(L_XF % 1024 == 0 && L_XT % 16 == 0 && L_LAB % 16 == 0, "LDS-DMA bases");
 static_assert(L_DW2P % 16 == 0, "dW2 partials: 16-B lanes");
 constexpr int CROW = DIN + 16;                         // copier LDS row stride (800)
@@ -539,9 +540,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
   float* w2s = reinterpret_cast<float*>(smem + L_W2);
   float* b1s = reinterpret_cast<float*>(smem + L_B1);
   float* b2s = reinterpret_cast<float*>(smem + L_B2);
-  float* rdb1 = reinterpret_cast<float*>(smem + L_RDB1);
   float* rdb2 = reinterpret_cast<float*>(smem + L_RDB2);
-  float* rmet = reinterpret_cast<float*>(smem + L_RMET);
   int* abort_flag = reinterpret_cast<int*>(smem + L_FLAG);
   int* census = abort_flag + 1;
   uint16_t* dzp = reinterpret_cast<uint16_t*>(smem + L_DZP);
@@ -877,32 +876,34 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
           dz2T[(4 * g + i) * LS + bw] = d;
         }
         dz3T[(4 * g + i) * LS + bw] = dz3[i];
-        const float s1 = row16_sum(d);
-        const float s2 = row16_sum(dz3[i]);
-        if (r == 0) {
-          rdb1[w * 16 + 4 * g + i] = s1;
-          rdb2[w * 16 + 4 * g + i] = s2;
-        }
       }
       if (w == 0) { PHX(15); }
-      const float ls = row16_sum((g == 0 && bv) ? loss : 0.f);
-      const float cr = row16_sum((g == 0 && bv && (int)am == y) ? 1.f : 0.f);
-      if (lane == 0) { rmet[2 * w] = ls; rmet[2 * w + 1] = cr; }
-      // this tile's dW2 partial (a2^T dz3 over its 16 rows, from the rows this wave
-      // just wrote: LDS ops of one wave complete in order) -- folded here, in
-      // parallel over the 7 head waves, instead of by wave 7 tile after tile
-      // (7 serial folds behind the last head: ~0.7 us of every step)
+      // per-row loss / hit, summed by wave 7 (no row reductions on the head's path)
+      if (g == 0) {
+        float* rl = reinterpret_cast<float*>(smem + L_RLOSS);
+        rl[bw] = bv ? loss : 0.f;
+        rl[128 + bw] = (bv && (int)am == y) ? 1.f : 0.f;
+      }
+      // this tile's dW2 = a2^T dz3 and db2 = 1^T dz3 partials over its 16 rows (two
+      // independent f32 MFMA chains; k = batch 4g + e, from the rows this wave just
+      // wrote: LDS ops of one wave complete in order).  db1 rides along with wave
+      // 7's weight-gradient MFMAs as a ones "feature" tile.
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       {
         const f32x4 av = *reinterpret_cast<const f32x4*>(a2T + r * LS + 16 * w + 4 * g);
         const f32x4 dv = *reinterpret_cast<const f32x4*>(dz3T + r * LS + 16 * w + 4 * g);
-        f32x4 dp = {0.f, 0.f, 0.f, 0.f};
+        const float one = r == 0 ? 1.f : 0.f;   // A = rows of ones at row 0
+        f32x4 dp = {0.f, 0.f, 0.f, 0.f}, p2 = dp;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) dp = mfma4(av[e], dv[e], dp);
+        for (int e = 0; e < 4; ++e) {
+          dp = mfma4(av[e], dv[e], dp);
+          p2 = mfma4(one, dv[e], p2);
+        }
         reinterpret_cast<f32x4*>(smem + L_DW2P)[w * 64 + lane] = dp;
+        if (g == 0) rdb2[w * 16 + r] = p2[0];   // D[0][class r]
       }
-      // head of batch tile w done (its dW2 / db partials and metrics are in LDS, its
-      // reads of W2 / b1 / b2 are over): wave 7 takes it from here
+      // head of batch tile w done (dz2 / dz3 / a2 rows and the row metrics are in LDS,
+      // its reads of W2 / b1 / b2 are over)
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
       if (lane == 0)
         __hip_atomic_store(reinterpret_cast<int*>(smem + L_HFLAG) + w, st + 1, __ATOMIC_RELAXED,
@@ -910,34 +911,32 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
       if (w == 0) { PH(9); }
     }
     // ---------------- P2 without a workgroup barrier: a wave multiplies the weight-
-    // gradient chunk of batch rows 32cc..32cc+31 as soon as the heads of its batch
-    // tiles are done (LDS flags), chunks in order (one accumulator chain:
-    // deterministic; separate per-chunk accumulators for arrival order spill).
-    // Barrier B used to wait for the LAST head before any chunk started: ~1.2 us of
-    // every step.  Reuse of everything the heads wrote is still fenced by barrier A
-    // of the next step.
+    // gradient chunk of batch rows 32cc..32cc+31 (one batch tile without SPLIT) as
+    // soon as the heads of its batch tiles are done (LDS flags), chunks in order
+    // (one accumulator chain: deterministic).  Barrier B used to wait for the LAST
+    // head before any chunk started.  Reuse of everything the heads wrote is still
+    // fenced by barrier A of the next step.
     f32x4 G[NTW];                        // dW1[16ft+4g+i][16j+r] (x 255 B)
+    f32x4 G1[NTW];                       // !SPLIT: second accumulator chain
 #pragma unroll
-    for (int k = 0; k < NTW; ++k) G[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if constexpr (SPLIT) {
-      // dW1 tile = x^T dz2 over K = 128 batch rows in 4 chunks: A = x^T bytes (exact),
-      // B = the dz2 pieces; an absent second tile computes a zero-weight copy (unused)
-#pragma unroll
-      for (int cc = 0; cc < 4; ++cc) {
-        const unsigned need = (1u << (2 * cc)) | (2 * cc + 1 < NBT ? 1u << (2 * cc + 1) : 0u);
-        while ((heads_done() & need) != need) {
-          if (a.dbg & 16) __builtin_amdgcn_s_sleep(2);
-          else __builtin_amdgcn_s_sleep(0);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-        if (cc == 0 && w == 0) { PH(10); }
-        const uint16_t* bp = dzp + r * PS + 32 * cc + 8 * g;
+    for (int k = 0; k < NTW; ++k) G[k] = G1[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+    constexpr int NCH = SPLIT ? 4 : NBT;
+    auto need_of = [](int ch) -> unsigned {
+      return SPLIT ? ((1u << (2 * ch)) | (2 * ch + 1 < NBT ? 1u << (2 * ch + 1) : 0u)) : (1u << ch);
+    };
+    auto chunk = [&](int ch) {   // ch is a constant after unrolling (register operands)
+      if constexpr (SPLIT) {
+        // dW1 tile = x^T dz2 over K = 128 batch rows in 4 chunks: A = x^T bytes (exact),
+        // B = the dz2 pieces; an absent second tile computes a zero-weight copy (unused)
+        const uint16_t* bp = dzp + r * PS + 32 * ch + 8 * g;
         const bf16x8 Bh = *reinterpret_cast<const bf16x8*>(bp);
         const bf16x8 Bm = *reinterpret_cast<const bf16x8*>(bp + 16 * PS);
         const bf16x8 Bl = *reinterpret_cast<const bf16x8*>(bp + 32 * PS);
-        const bf16x8 X0 = px8(xt[0][2 * cc], xt[0][2 * cc + 1]);
-        if (tv1) {   // wave-uniform: waves without a second tile skip its MFMAs
-          const bf16x8 X1 = px8(xt[1][2 * cc], xt[1][2 * cc + 1]);
+        const bf16x8 X0 = px8(xt[0][2 * ch], xt[0][2 * ch + 1]);
+        if (tv1 || w == 7) {   // wave-uniform: waves without a second tile skip its MFMAs
+          // wave 7 (always one tile) multiplies a tile of ones instead: G[1] = db1
+          // (lane (r, g): hidden 16j + r, every i), exact like the rest
+          const bf16x8 X1 = tv1 ? px8(xt[1][2 * ch], xt[1][2 * ch + 1]) : px8(0x01010101u, 0x01010101u);
           G[0] = mfma16x16x32(X0, Bl, G[0]);
           G[1] = mfma16x16x32(X1, Bl, G[1]);
           G[0] = mfma16x16x32(X0, Bm, G[0]);
@@ -949,56 +948,80 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
           G[0] = mfma16x16x32(X0, Bm, G[0]);
           G[0] = mfma16x16x32(X0, Bh, G[0]);
         }
-      }
-    } else {
-      // one batch tile at a time, in tile order (single accumulator chain)
-      f32x4 g0[NTW], g1[NTW];
-#pragma unroll
-      for (int k = 0; k < NTW; ++k) g0[k] = g1[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < NBT; ++s) {
-        while (((heads_done() >> s) & 1u) == 0u) __builtin_amdgcn_s_sleep(0);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-        if (s == 0 && w == 0) { PH(10); }
-        const f32x4 bz = *reinterpret_cast<const f32x4*>(dz2T + r * LS + 16 * s + 4 * g);
+      } else {
+        const f32x4 bz = *reinterpret_cast<const f32x4*>(dz2T + r * LS + 16 * ch + 4 * g);
 #pragma unroll
         for (int k = 0; k < NTW; ++k) {
           if (tvk(k)) {
-            g0[k] = mfma4(ub(xt[k][s], 0), bz[0], g0[k]);
-            g1[k] = mfma4(ub(xt[k][s], 1), bz[1], g1[k]);
-            g0[k] = mfma4(ub(xt[k][s], 2), bz[2], g0[k]);
-            g1[k] = mfma4(ub(xt[k][s], 3), bz[3], g1[k]);
+            G[k] = mfma4(ub(xt[k][ch], 0), bz[0], G[k]);
+            G1[k] = mfma4(ub(xt[k][ch], 1), bz[1], G1[k]);
+            G[k] = mfma4(ub(xt[k][ch], 2), bz[2], G[k]);
+            G1[k] = mfma4(ub(xt[k][ch], 3), bz[3], G1[k]);
           }
         }
+        if (w == 7) {   // one tile: a ones tile in the second slot gives db1
+          G[1] = mfma4(1.f, bz[0], G[1]);
+          G1[1] = mfma4(1.f, bz[1], G1[1]);
+          G[1] = mfma4(1.f, bz[2], G[1]);
+          G1[1] = mfma4(1.f, bz[3], G1[1]);
+        }
       }
+    };
+    {
+      int cc = 0;   // next chunk
+      for (;;) {
+        const unsigned hm = heads_done();
+        bool did = false;
 #pragma unroll
-      for (int k = 0; k < NTW; ++k) G[k] = g0[k] + g1[k];
+        for (int ch = 0; ch < NCH; ++ch) {
+          if (ch == cc && (hm & need_of(ch)) == need_of(ch)) {   // wave-uniform
+            if (!did) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+            if (cc == 0 && w == 0) { PH(10); }
+            chunk(ch);
+            ++cc;
+            did = true;
+          }
+        }
+        if (cc == NCH) break;
+        if (!did) {
+          if (a.dbg & 16) __builtin_amdgcn_s_sleep(2);
+          else __builtin_amdgcn_s_sleep(0);
+        }
+      }
     }
-    // every head is done here.  Wave 7 sums the 7 head waves' dW2 / db1 / db2
-    // partials and metrics in fixed tile order (all loads in flight at once); one
+    if constexpr (!SPLIT) {
+#pragma unroll
+      for (int k = 0; k < NTW; ++k) G[k] = G[k] + G1[k];
+    }
+    // every head is done here.  Wave 7 sums the 7 head waves' dW2 / db2 partials
+    // and the per-row metrics in fixed order (all loads in flight at once); one
     // GPU: the W2 / b1 / b2 updates too (their readers, this step's heads, are done;
     // the next step's read them after barrier A)
     f32x4 D = {0.f, 0.f, 0.f, 0.f};      // wave 7: dW2[16j+4g+i][class r] (x B)
     float gb = 0.f;                      // wave 7: db1 (lanes < 16) / db2 (lanes 16..25) (x B)
     if (w == 7) {
-      float ls = 0.f, cr = 0.f;          // loss / correct sums of the batch
-      // lane < 16: db1 column `lane`; 16..25: db2 column lane - 16 (rdb2 follows rdb1 by 128 floats)
-      const float* gsrc = rdb1 + (lane < 16 ? lane : (lane < 16 + NCLS ? lane + 112 : 0));
+      // lanes 16..25: db2 column lane - 16 (lanes < 16 take db1 from the ones tile)
+      const float* gsrc = rdb2 + (lane >= 16 && lane < 16 + NCLS ? lane - 16 : 0);
       const f32x4* dw2p = reinterpret_cast<const f32x4*>(smem + L_DW2P);
 #pragma unroll
       for (int v = 0; v < NBT; ++v) {
         D += dw2p[v * 64 + lane];
         gb += gsrc[v * 16];
-        ls += rmet[2 * v];
-        cr += rmet[2 * v + 1];
       }
+      if (lane < 16) gb = G[1][0];   // db1 of hidden 16j + lane from the ones tile
       if (lane >= 16 + NCLS) gb = 0.f;
       PH7(13);
       PH7(15);
-      if (c == 0 && lane == 63) {
-        const int sl = (int)((gstep0 + st) % a.ring);
-        a.metrics[2 * sl] = ls / (float)B;
-        a.metrics[2 * sl + 1] = cr / (float)B;
+      if (c == 0) {   // loss / accuracy of the batch: per-row values, fixed reduction order
+        const float* rl = reinterpret_cast<const float*>(smem + L_RLOSS);
+        const bool hi = lane + 64 < BROWS;
+        const float ls = wave_sum(rl[lane] + (hi ? rl[lane + 64] : 0.f));
+        const float cr = wave_sum(rl[128 + lane] + (hi ? rl[128 + lane + 64] : 0.f));
+        if (lane == 63) {
+          const int sl = (int)((gstep0 + st) % a.ring);
+          a.metrics[2 * sl] = ls / (float)B;
+          a.metrics[2 * sl + 1] = cr / (float)B;
+        }
       }
       if constexpr (!MULTI) {
 #pragma unroll
@@ -1176,11 +1199,11 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
       }
     }
     // ---------------- updates (lr / (W B), 1/255 for the pixel scale)
-    if (hv) {
+    if (hv) {   // an absent second tile keeps its zero weights (wave 7's G[1] is db1)
 #pragma unroll
       for (int k = 0; k < NTW; ++k)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) Wt[k][i] -= lrX * G[k][i];
+        for (int i = 0; i < 4; ++i) Wt[k][i] -= (k == 0 || tv1) ? lrX * G[k][i] : 0.f;
     }
     if (w == 0) { PH(12); }
     if (MULTI && w == 7) {   // N GPUs: with the rank sums of dW2 / db1 / db2

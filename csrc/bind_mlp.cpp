@@ -565,7 +565,7 @@ void graph_mlp_step(at::Tensor x, at::Tensor ylab, at::Tensor W1, at::Tensor b1,
     gp = gstep->data_ptr();
   }
   // L2's partials + the learning rate on the device (scratch from the caching allocator)
-  at::Tensor part = at::empty({dtfk_graph_mlp_part_floats(B, H) + 1}, x.options());
+  at::Tensor part = at::zeros({dtfk_graph_mlp_part_floats(B, H) + 1}, x.options());
   part.narrow(0, 0, 1).fill_(lr);
   hip_check(dtfk_graph_mlp_step(x.data_ptr<float>(), ylab.data_ptr<float>(), W1.data_ptr<float>(),
                                 b1.data_ptr<float>(), W2.data_ptr<float>(), b2.data_ptr<float>(),
@@ -613,7 +613,7 @@ class GraphStepPlan {
     dev_ = at::empty({nfeed_}, fo);
     a2_ = at::empty({(int64_t)BP * HP_}, fo);
     dz2_ = at::empty({(int64_t)BP * HP_}, fo);
-    part_ = at::empty({dtfk_graph_mlp_part_floats(B_, H_)}, fo);
+    part_ = at::zeros({dtfk_graph_mlp_part_floats(B_, H_)}, fo);
     metrics_ = at::zeros({4}, fo);
     auto ho = at::TensorOptions().dtype(at::kFloat).pinned_memory(true);
     for (int i = 0; i < 2; ++i) stage_[i] = at::empty({nfeed_}, ho);
@@ -655,7 +655,10 @@ class GraphStepPlan {
       if (!use_graph_) {   // direct launches on the caller's stream: no cross-stream events, no replay floor
         using clk = std::chrono::steady_clock;
         const auto t0 = clk::now();
-        hip_check(hipEventSynchronize(ev_[slot]), "GraphStepPlan: staging slot");
+        // the copy that last read this staging slot: only an unsynchronized call
+        // leaves one in flight (a synchronizing call needs no event at all)
+        if (pending_[slot]) hip_check(hipEventSynchronize(ev_[slot]), "GraphStepPlan: staging slot");
+        pending_[slot] = false;
         float* h = stage_[slot].data_ptr<float>();
         float* d = dev_.data_ptr<float>();
         if (direct_feed_) {
@@ -677,16 +680,23 @@ class GraphStepPlan {
             hip_check(hipMemcpyAsync(d, h, sizeof(float) * (nx + ny + 1), hipMemcpyHostToDevice, st),
                       "GraphStepPlan: feed copy");
         }
-        hip_check(hipEventRecord(ev_[slot], st), "GraphStepPlan: event");
+        if (!sync) {
+          hip_check(hipEventRecord(ev_[slot], st), "GraphStepPlan: event");
+          pending_[slot] = true;
+        }
         hip_check(launch_step(st, host_store_), "GraphStepPlan: launch");
         const auto t2 = clk::now();
         t_[1] += std::chrono::duration<double, std::micro>(t2 - t0).count();
-        if (sync) hip_check(hipStreamSynchronize(st), "GraphStepPlan: sync");
+        if (sync) {
+          hip_check(hipStreamSynchronize(st), "GraphStepPlan: sync");
+          pending_[0] = pending_[1] = false;
+        }
         t_[2] += std::chrono::duration<double, std::micro>(clk::now() - t2).count();
         ++steps_;
         return;
       }
       hip_check(hipEventSynchronize(ev_[slot]), "GraphStepPlan: staging slot");   // its last copy is done
+      pending_[slot] = false;
       float* h = stage_[slot].data_ptr<float>();
       std::memcpy(h, xp, sizeof(float) * nx);
       std::memcpy(h + nx, yp, sizeof(float) * ny);
@@ -765,6 +775,7 @@ class GraphStepPlan {
   bool naive_, use_graph_, direct_feed_ = false;
   int64_t nfeed_ = 0, steps_ = 0;
   bool host_store_ = true, kernel_feed_ = false;
+  bool pending_[2] = {false, false};   // an event on the staging slot's copy may still be in flight
   int64_t feed_bytes_ = 0;
   double t_[3] = {0, 0, 0};
 };

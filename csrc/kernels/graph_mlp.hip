@@ -5,23 +5,23 @@
 //        | mean(softmax_cross_entropy_with_logits(y_, z3))     ("stable")
 //   train_op = GradientDescentOptimizer(lr).minimize(loss, global_step)
 //   accuracy = mean(cast(equal(argmax(y, 1), argmax(y_, 1))))
-// is matched on the deferred graph and run as three kernels instead of ~25
+// is matched on the deferred graph and run as two launches instead of ~25
 // eager ops, with every product on the exact-fp32 matrix core path
 // (v_mfma_f32_16x16x4_f32, fp32 accumulate): the numbers are the fp32 graph's,
 // only the summation order differs.
 //
-//   L1 graph_mlp_l1     a2 = act(x W1 + b1): one workgroup per 16x16 tile of
-//                       a2, its 4 waves take interleaved 16-deep K blocks
+//   L1 graph_mlp_l1h    a2 = act(x W1 + b1): one workgroup per 16x16 tile of
+//                       a2, its 8 waves take interleaved 16-deep K blocks
 //                       (lane group g holds k = 16j + 4g .. +3 as one float4
 //                       of x, so the 4 MFMAs of a block need no shuffles),
 //                       partial tiles summed through LDS; rows >= B and
-//                       columns >= H are written as 0.
-//   L2 graph_mlp_head   one 512-thread workgroup for the whole batch (B <= 256):
-//                       z3 = a2 W2 + b2 (MFMA), softmax per row with 16-lane
-//                       reductions, loss, argmax accuracy, dz3; dW2 = a2^T dz3,
-//                       db2, da2 = dz3 W2^T (MFMA), dz2 = da2 act'(a2);
-//                       SGD on W2/b2 (or gradients out), metrics, and
-//                       global_step += 1.
+//                       columns >= H are written as 0.  The LAST workgroup of
+//                       each 16-row tile to finish (arrival counter) then runs
+//                       that row tile's head (L2) in the same launch:
+//   L2 head_tile        z3 = a2 W2 + b2 (MFMA), softmax per row with 16-lane
+//                       reductions (one row element per wave), loss, argmax
+//                       accuracy, dz3; da2 = dz3 W2^T (MFMA), dz2 = da2 act'(a2);
+//                       the row tile's dW2 partial a2^T dz3 and loss sums.
 //   L3 graph_mlp_wgrad  [dW1; db1] = [x 1]^T dz2, one workgroup per 16x16
 //                       tile, batch split over its 4 waves, fused W1 -= lr dW1,
 //                       b1 -= lr db1 (or gradients out).
@@ -65,9 +65,9 @@ constexpr int L1W = 8;     // waves per a2 tile (interleaved 16-deep K blocks)
 constexpr int PF = 8;      // K blocks per wave whose loads are issued before any MFMA
 
 template <bool VEC>   // VEC: K % 4 == 0 and x 16-byte aligned -> x as float4s
-__global__ __launch_bounds__(512) void graph_mlp_l1(const float* __restrict__ x, const float* __restrict__ W1,
-                                                    const float* __restrict__ b1, float* __restrict__ a2,
-                                                    int B, int K, int H, int HP, int act) {
+__device__ __forceinline__ void l1_tile(const float* __restrict__ x, const float* __restrict__ W1,
+                                        const float* __restrict__ b1, float* __restrict__ a2,
+                                        int B, int K, int H, int HP, int act) {
   __shared__ f32x4 part[L1W][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
@@ -77,6 +77,7 @@ __global__ __launch_bounds__(512) void graph_mlp_l1(const float* __restrict__ x,
   const bool rv = row < B, cv = col < H;
   const float* xr = x + (size_t)min(row, B - 1) * K;
   const float* wc = W1 + min(col, H - 1);
+  const float bv = pin(b1[min(col, H - 1)]);   // issued with the operand loads, not after the barrier
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   const int nkb = (K + 15) / 16;
   for (int base = w; base < nkb; base += L1W * PF) {
@@ -119,11 +120,10 @@ __global__ __launch_bounds__(512) void graph_mlp_l1(const float* __restrict__ x,
     }
     // C layout: lane holds rows 4g + i, column r.  Column H carries 1 for
     // valid rows: L2's dW2 tile then yields db2 = colsum(dz3) as its row H.
-    const float bv = cv ? b1[col] : 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = r0 + 4 * g + i;
-      const float z = t[i] + bv;
+      const float z = t[i] + (cv ? bv : 0.f);
       a2[(size_t)m * HP + col] = m < B ? (cv ? act_fwd(z, act) : (col == H ? 1.f : 0.f)) : 0.f;
     }
   }
@@ -148,55 +148,74 @@ struct HeadArgs {
   int B, H, HP, C, act, naive;
 };
 
-constexpr int HW = 4;   // waves per head workgroup
+constexpr int HW = 4;   // waves of the z3 split-K and of the softmax rows
 
-__global__ __launch_bounds__(HW * 64) void graph_mlp_head(HeadArgs a) {
+// The head of batch-row tile rt, run by the LAST of L1's workgroups of that row
+// tile to finish (NW waves; every thread of the block calls it: it has barriers).
+template <int NW>
+__device__ void head_tile(const HeadArgs& a, const int rt) {
   __shared__ float a2s[16 * MAXH + 16];       // this tile's a2 rows [16][HP]
   __shared__ float w2s[(MAXH + 16) * CP];     // W2 [HP][CP], zero padded
   __shared__ float dz3s[16 * CP];             // dz3 / B of the tile [16][CP]
   __shared__ f32x4 zp[HW][64];                // split-K partials of z3
   const int B = a.B, H = a.H, HP = a.HP, C = a.C;
   const int NRT = (B + 15) / 16;
-  const int rt = blockIdx.x, rb = rt * 16;
+  const int rb = rt * 16;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
-  // wave 0's softmax operands first (labels of its 4 rows, b2): issued before
-  // the staging below so their latency is not a separate round trip later
-  float labp[4] = {0.f, 0.f, 0.f, 0.f}, b2p = 0.f;
-  if (w == 0) {
+  // the softmax operands first (waves < HW: element i = w of the lane's rows; b2):
+  // issued before the staging below so their latency is not a separate round trip
+  const float labw = pin(a.ylab[(size_t)min(rb + 4 * g + (w & 3), B - 1) * C + min(r, C - 1)]);
+  const float b2p = pin(a.b2[min(r, C - 1)]);
+  // operands, branch-free (clamped + masked): a2 tile, W2 -- every load issued
+  // before the first LDS store (a load -> store loop waits one round trip per
+  // iteration: ~1 us each)
+  constexpr int A2N = (16 * (MAXH + 16) / 4 + NW * 64 - 1) / (NW * 64);   // float4s per thread
+  constexpr int W2N = ((MAXH + 16) * CP + NW * 64 - 1) / (NW * 64);       // floats per thread
+  float4 av4[A2N];
+  float wv[W2N];
+  const float4* a2g = reinterpret_cast<const float4*>(a.a2 + (size_t)rb * HP);
+  const int na2 = 16 * HP / 4;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) labp[i] = pin(a.ylab[(size_t)min(rb + 4 * g + i, B - 1) * C + min(r, C - 1)]);
-    b2p = pin(a.b2[min(r, C - 1)]);
+  for (int j = 0; j < A2N; ++j) av4[j] = a2g[min(tid + j * NW * 64, na2 - 1)];
+#pragma unroll
+  for (int j = 0; j < W2N; ++j) {
+    const int i = tid + j * NW * 64, h = i / CP, c = i % CP;
+    wv[j] = a.W2[min(h, H - 1) * C + min(c, C - 1)];
   }
-  // operands, branch-free (clamped + masked): a2 tile, W2, this lane's label / b2
-  for (int i = tid; i < 16 * HP / 4; i += HW * 64)
-    reinterpret_cast<float4*>(a2s)[i] = reinterpret_cast<const float4*>(a.a2 + (size_t)rb * HP)[i];
-  for (int i = tid; i < HP * CP; i += HW * 64) {
-    const int h = i / CP, c = i % CP;
-    const float v = a.W2[min(h, H - 1) * C + min(c, C - 1)];
-    w2s[i] = (h < H && c < C) ? v : 0.f;
+#pragma unroll
+  for (int j = 0; j < A2N; ++j)
+    if (tid + j * NW * 64 < na2) reinterpret_cast<float4*>(a2s)[tid + j * NW * 64] = av4[j];
+#pragma unroll
+  for (int j = 0; j < W2N; ++j) {
+    const int i = tid + j * NW * 64, h = i / CP, c = i % CP;
+    if (i < HP * CP) w2s[i] = (h < H && c < C) ? wv[j] : 0.f;
   }
   __syncthreads();
-  // z3 tile, K = HP split over the waves
-  {
+  // z3 tile, K = HP split over HW waves
+  if (w < HW) {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     for (int k = 4 * w; k < HP; k += 4 * HW) acc = mfma4(a2s[r * HP + k + g], w2s[(k + g) * CP + r], acc);
     zp[w][lane] = acc;
   }
   __syncthreads();
-  if (w == 0) {
+  // softmax / loss / dz3: wave w takes element i = w of every lane's 4 rows (the
+  // 16-lane reductions of the 16 rows run on all 4 waves instead of serially on one)
+  __shared__ float lcs[HW][2];
+  if (w < HW) {
     f32x4 acc = zp[0][lane];
 #pragma unroll
     for (int q = 1; q < HW; ++q) acc += zp[q][lane];
     const float b2v = r < C ? b2p : 0.f;
     float loss_part = 0.f, corr_part = 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    {
+      const int i = w;
       const int m = rb + 4 * g + i;               // row; column = r (class)
       const bool valid = m < B;
       const bool cl = r < C;
-      const float lab = (valid && cl) ? labp[i] : 0.f;
-      const float z = cl ? acc[i] + b2v : -INFINITY;
+      const float lab = (valid && cl) ? labw : 0.f;
+      const float ai = w == 0 ? acc[0] : (w == 1 ? acc[1] : (w == 2 ? acc[2] : acc[3]));   // no dynamic index
+      const float z = cl ? ai + b2v : -INFINITY;
       const float mx = row16_max(z);
       const float e = cl ? expf(z - mx) : 0.f;
       const float s = row16_sum(e);
@@ -218,21 +237,25 @@ __global__ __launch_bounds__(HW * 64) void graph_mlp_head(HeadArgs a) {
       const float d = a.naive ? (y * lsum - lab) : (y - lab);
       dz3s[(4 * g + i) * CP + r] = (valid && cl) ? d / (float)B : 0.f;
     }
-    // (lanes with r == 0 hold the partial sums of their 4 rows)
+    // (lanes with r == 0 hold the partial sums of their row)
     loss_part += __shfl_xor(loss_part, 16, 64);
     loss_part += __shfl_xor(loss_part, 32, 64);
     corr_part += __shfl_xor(corr_part, 16, 64);
     corr_part += __shfl_xor(corr_part, 32, 64);
     if (lane == 0) {
-      float* lc = a.part + (size_t)NRT * HP * CP;
-      lc[2 * rt] = loss_part;
-      lc[2 * rt + 1] = corr_part;
+      lcs[w][0] = loss_part;
+      lcs[w][1] = corr_part;
     }
   }
   __syncthreads();
+  if (tid == 0) {   // the tile's sums in fixed wave order
+    float* lc = a.part + (size_t)NRT * HP * CP;
+    lc[2 * rt] = ((lcs[0][0] + lcs[1][0]) + lcs[2][0]) + lcs[3][0];
+    lc[2 * rt + 1] = ((lcs[0][1] + lcs[1][1]) + lcs[2][1]) + lcs[3][1];
+  }
   // per hidden tile: da2 = dz3 W2^T -> dz2 rows; dW2 partial = a2^T dz3
   const int nht = HP / 16;
-  for (int ht = w; ht < nht; ht += HW) {
+  for (int ht = w; ht < nht; ht += NW) {
     const int hb = ht * 16;
     f32x4 da = {0.f, 0.f, 0.f, 0.f}, dw = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -248,6 +271,30 @@ __global__ __launch_bounds__(HW * 64) void graph_mlp_head(HeadArgs a) {
       a.part[((size_t)rt * HP + hb + 4 * g + i) * CP + r] = dw[i];
     }
   }
+}
+
+// L1 + L2 in one launch: every workgroup computes its a2 tile; the last of the
+// row tile's HP / 16 workgroups to finish (a per-row-tile arrival counter,
+// reset by that workgroup for the next step) runs the row tile's head -- no
+// second launch and no grid-wide wait.
+template <bool VEC>
+__global__ __launch_bounds__(512) void graph_mlp_l1h(const float* __restrict__ x, const float* __restrict__ W1,
+                                                     const float* __restrict__ b1, HeadArgs h, int K, int* cnt) {
+  __shared__ int last;
+  l1_tile<VEC>(x, W1, b1, const_cast<float*>(h.a2), h.B, K, h.H, h.HP, h.act);
+  const int nct = h.HP / 16, rt = blockIdx.x / nct;
+  if (threadIdx.x < 64) {   // wave 0 stored the tile: release it, then arrive
+    __threadfence();
+    if (threadIdx.x == 0) {
+      const int old = atomicAdd(cnt + rt, 1);
+      last = old == nct - 1;
+      if (last) cnt[rt] = 0;   // nobody else touches it until the next launch
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();          // acquire: the other workgroups' a2 rows
+  head_tile<8>(h, rt);
 }
 
 // ---------------------------------------------------------------- L3
@@ -410,10 +457,11 @@ extern "C" hipError_t dtfk_graph_feed_ingest(const void* host, void* dev, long l
   return hipGetLastError();
 }
 
-// Device scratch (floats) the step needs besides a2 / dz2: L2's partials + loss sums.
+// Device scratch (floats) the step needs besides a2 / dz2: L2's partials + loss
+// sums + the per-row-tile arrival counters (int).  Must be ZERO when first used.
 extern "C" long long dtfk_graph_mlp_part_floats(int B, int H) {
   const int HP = (H + 16) & ~15, NRT = (B + 15) / 16;
-  return (long long)NRT * HP * dtfk::gmlp::CP + 2LL * NRT;
+  return (long long)NRT * HP * dtfk::gmlp::CP + 3LL * NRT;
 }
 
 extern "C" hipError_t dtfk_graph_mlp_step(const float* x, const float* ylab, float* W1, float* b1, float* W2,
@@ -427,14 +475,13 @@ extern "C" hipError_t dtfk_graph_mlp_step(const float* x, const float* ylab, flo
   const int HP = (H + 16) & ~15, BP = (B + 15) & ~15;   // >= H + 1 (ones column)
   if (BP * HP > A2_LDS) return hipErrorInvalidValue;
   const bool vec = (K & 3) == 0 && K >= 4 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
-  if (vec)
-    hipLaunchKernelGGL(graph_mlp_l1<true>, dim3((BP / 16) * (HP / 16)), dim3(512), 0, stream, x, W1, b1, a2buf, B, K,
-                       H, HP, act);
-  else
-    hipLaunchKernelGGL(graph_mlp_l1<false>, dim3((BP / 16) * (HP / 16)), dim3(512), 0, stream, x, W1, b1, a2buf, B,
-                       K, H, HP, act);
   HeadArgs h{a2buf, ylab, W2, b2, dz2buf, part, B, H, HP, C, act, naive};
-  hipLaunchKernelGGL(graph_mlp_head, dim3(BP / 16), dim3(HW * 64), 0, stream, h);
+  // per-row-tile arrival counters behind the partials (zero at allocation, reset by their last arriver)
+  int* cnt = reinterpret_cast<int*>(part + (size_t)(BP / 16) * HP * CP + 2 * (BP / 16));
+  if (vec)
+    hipLaunchKernelGGL(graph_mlp_l1h<true>, dim3((BP / 16) * (HP / 16)), dim3(512), 0, stream, x, W1, b1, h, K, cnt);
+  else
+    hipLaunchKernelGGL(graph_mlp_l1h<false>, dim3((BP / 16) * (HP / 16)), dim3(512), 0, stream, x, W1, b1, h, K, cnt);
   const int tiles = ((K + 1 + 15) / 16) * (HP / 16);
   WgradArgs wa{x, dz2buf, W1, b1, W2, b2, gW1, gb1, gW2, gb2, part, metrics, host_metrics, gstep, gstep_kind,
                lr_ptr, B, K, H, HP, C, sgd, tiles};

@@ -785,6 +785,16 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
       const auto r1 = region_rsrc(a.xbuf + E1_OFF + (long long)(par * NJ + j) * NQ * NBT * GSLOT, NQ * NBT * GSLOT);
       put_gran(r1, (q * NBT + w) * GSLOT + 32 * lane, zs, tag, l2_e1);
       if (w == 0) { PH(3); }
+      // this step's W2 / b1 / b2 operands of the lane, read from LDS while the
+      // partial is in flight (their LDS latency off the E1 -> P1 -> E2 -> head chain)
+      float w2p[4], w2d[4], b1v[4], b2v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        w2p[e] = w2s[(4 * g + e) * 16 + r];
+        w2d[e] = w2s[r * 16 + 4 * g + e];
+        b1v[e] = b1s[4 * g + e];
+        b2v[e] = b2s[4 * g + e];
+      }
       f32x4 part[NQ];
       bool ok = gather_gran<NQ>(r1, [&](int k) { return (k * NBT + w) * GSLOT; }, q, true, 63, tag, zs, part, lane, a);
       if (w == 0) { PH(4); }
@@ -797,7 +807,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int hl = 4 * g + i;
-        const float zt = z[i] * (1.f / 255.f) + b1s[hl];
+        const float zt = z[i] * (1.f / 255.f) + b1v[i];
         // v_exp_f32 / v_rcp_f32 (<= 2 ulp each, 1e-7 relative): ~20 instructions per
         // element less than IEEE expf + division on this single-wave critical path
         const float av = ACT == 0 ? __builtin_amdgcn_rcpf(1.f + __expf(-zt)) : fmaxf(zt, 0.f);
@@ -806,7 +816,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
       // partial logits^T[class][batch] of block j: A = W2^T (lane: class r), B = a2^T
       f32x4 pl = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int e = 0; e < 4; ++e) pl = mfma4(w2s[(4 * g + e) * 16 + r], a2[e], pl);
+      for (int e = 0; e < 4; ++e) pl = mfma4(w2p[e], a2[e], pl);
       // E2 region of (parity, slice q, batch tile w): [block] slots
       const auto r2 = region_rsrc(a.xbuf + E2_OFF + (long long)((par * NQ + q) * NBT + w) * NJ * GSLOT, NJ * GSLOT);
       if (g < 3) put_gran(r2, j * GSLOT + 32 * lane, pl, tag, l2_e2);
@@ -823,7 +833,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
       float m = -3.0e38f;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        float v = b2s[4 * g + i];
+        float v = b2v[i];
 #pragma unroll
         for (int jj = 0; jj < NJ; ++jj) v += lp[jj][i];
         lg[i] = v;
@@ -860,7 +870,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
       // da2^T = W2 . dz3^T (A = W2, lane: hidden r), dz2 = da2 * act'(a2)
       f32x4 da = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int e = 0; e < 4; ++e) da = mfma4(w2s[r * 16 + 4 * g + e], dz3[e], da);
+      for (int e = 0; e < 4; ++e) da = mfma4(w2d[e], dz3[e], da);
       if (w == 0) { PHX(14); }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {

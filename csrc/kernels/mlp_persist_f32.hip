@@ -546,25 +546,11 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
   uint16_t* dzp = reinterpret_cast<uint16_t*>(smem + L_DZP);
   if (tid == 0) { PRO(c, 0); }
 
-  // ---- load state
-  for (int k = tid; k < 3 * 16 * LS; k += THREADS) a2T[k] = 0.f;   // a2T, dz2T, dz3T (batch pad stays 0)
-  if constexpr (SPLIT)
-    for (int k = tid; k < 3 * 16 * PS; k += THREADS) dzp[k] = (uint16_t)0;   // dz2 planes (batch pad 0)
-  if (tid < 256) {
-    const int n = tid >> 4, cl = tid & 15;
-    const int hn = 16 * j + n;
-    w2s[tid] = (hn < HID && cl < NCLS) ? a.params[OFF_W2 + hn * NCLS + cl] : 0.f;
-  } else if (tid < 272) {
-    const int hn = 16 * j + (tid - 256);
-    b1s[tid - 256] = hn < HID ? a.params[OFF_B1 + hn] : 0.f;
-  } else if (tid < 288) {
-    const int cl = tid - 272;
-    b2s[cl] = cl < NCLS ? a.params[OFF_B2 + cl] : 0.f;
-  } else if (tid == 288) {
-    *abort_flag = 0;
-  } else if (tid >= 296 && tid < 304) {
-    reinterpret_cast<int*>(smem + L_HFLAG)[tid - 296] = 0;
-  }
+  // ---- load state: every global load of the prologue is issued first (the
+  // master weights, the small parameters into registers, the step / sequence /
+  // lr scalars); the LDS stores that consume them come after the LDS clears, so
+  // no store waits on a load before the next load is even issued (~2 us of every
+  // launch when the W2 / b loads fed LDS stores ahead of the W1 loads)
   const int hid = 16 * j + r;       // this lane's hidden unit in the W1 / dW1 layouts
   const bool hv = hid < HID;
   // wave w owns local feature tiles w and w + 8 of the slice (global tile ft[k])
@@ -580,11 +566,37 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
 #pragma unroll
     for (int e = 0; e < 4; ++e)
       Wt[k][e] = (tvk(k) && hv) ? a.params[(16 * ftk(k) + 4 * g + e) * HID + hid] : 0.f;
+  float pv = 0.f;   // this thread's W2 / b1 / b2 entry (threads < 288)
+  if (tid < 256) {
+    const int n = tid >> 4, cl = tid & 15;
+    const int hn = 16 * j + n;
+    pv = (hn < HID && cl < NCLS) ? a.params[OFF_W2 + hn * NCLS + cl] : 0.f;
+  } else if (tid < 272) {
+    const int hn = 16 * j + (tid - 256);
+    pv = hn < HID ? a.params[OFF_B1 + hn] : 0.f;
+  } else if (tid < 288) {
+    const int cl = tid - 272;
+    pv = cl < NCLS ? a.params[OFF_B2 + cl] : 0.f;
+  }
   const unsigned long long seq0 = *a.seq;
   const long long gstep0 = *a.gstep;
   const float lr = *a.lr;
   const float lrB = lr / (float)(B * (MULTI ? a.W : 1));
   const float lrX = lrB * (1.f / 255.f);
+  for (int k = tid; k < 3 * 16 * LS; k += THREADS) a2T[k] = 0.f;   // a2T, dz2T, dz3T (batch pad stays 0)
+  if constexpr (SPLIT)
+    for (int k = tid; k < 3 * 16 * PS; k += THREADS) dzp[k] = (uint16_t)0;   // dz2 planes (batch pad 0)
+  if (tid < 256) {
+    w2s[tid] = pv;
+  } else if (tid < 272) {
+    b1s[tid - 256] = pv;
+  } else if (tid < 288) {
+    b2s[tid - 272] = pv;
+  } else if (tid == 288) {
+    *abort_flag = 0;
+  } else if (tid >= 296 && tid < 304) {
+    reinterpret_cast<int*>(smem + L_HFLAG)[tid - 296] = 0;
+  }
   const bool failed_in = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
 
   // x operands of the wave's feature tiles (registers, read from the LDS stage):

@@ -40,9 +40,24 @@ __device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
   return static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
 }
 
-// Counter-based dropout hash (splitmix64 finaliser): keep(i) = hash32(seed, i)
-// >= p * 2^32.  Shared by every kernel that regenerates a mask in backward.
+// Counter-based dropout hash: keep(i) = hash32(seed, i) >= p * 2^32.  Shared by
+// every kernel that regenerates a mask in backward.  Seeds with bit 63 set (what
+// ops/transformer.py hands out by default) take a 32-bit lowbias32 finaliser of
+// the element index xor a mixed seed -- ~8 VALU ops, all 32-bit; the others the
+// splitmix64 finaliser (~30 ops incl. 64-bit multiplies: ~25 us of a BERT-base
+// attention forward at B = 128, S = 128, scripts/probes/attn_dropout_cost.py).
+// The branch is wave-uniform (the seed is a kernel argument).
 __device__ __forceinline__ uint32_t hash32(uint64_t seed, uint64_t i) {
+  if (seed >> 63) {
+    const uint32_t k = (uint32_t)seed ^ ((uint32_t)(seed >> 32) * 0x85EBCA6Bu);
+    uint32_t x = ((uint32_t)i ^ k) + (uint32_t)(i >> 32) * 0x9E3779B9u;
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+  }
   uint64_t x = seed ^ (i * 0x9E3779B97F4A7C15ull);
   x ^= x >> 30; x *= 0xBF58476D1CE4E5B9ull;
   x ^= x >> 27; x *= 0x94D049BB133111EBull;

@@ -8,6 +8,7 @@ is a counter hash of (seed, element index) regenerated in backward).
 from __future__ import annotations
 
 import itertools
+import os
 import math
 from typing import Optional
 
@@ -19,8 +20,14 @@ _seed_counter = itertools.count(1)
 _BASE_SEED = 0x5EED
 
 
+# bit 63 of a dropout seed selects the 32-bit hash in the kernels (csrc/kernels/
+# common.h hash32); DTF_DROPOUT_HASH=64 keeps the splitmix64 one.  Seeds cross
+# into C++ as int64: bit 63 set = a negative Python int (same bits).
+_FAST_HASH = -(1 << 63) if os.environ.get("DTF_DROPOUT_HASH", "32") != "64" else 0
+
+
 def next_seed() -> int:
-    return (_BASE_SEED * 1000003 + next(_seed_counter) * 0x9E3779B1) & ((1 << 62) - 1)
+    return ((_BASE_SEED * 1000003 + next(_seed_counter) * 0x9E3779B1) & ((1 << 62) - 1)) + _FAST_HASH
 
 
 def set_dropout_seed(seed: int):

@@ -70,14 +70,49 @@ __device__ __forceinline__ float keepf(uint64_t seed, uint64_t i, uint32_t thres
 
 // stage a [S][64] tile (rows of the packed projection, or of a [B,S,NH*64]
 // tensor) into a row image rows[S][KP] and, optionally, a transposed image
-// cols[64][S+8]
+// cols[64][S+8].  Two halves so a kernel issues every global load of all its
+// stages (and its per-wave fragments) before the first LDS store: a
+// load -> store loop per stage costs one memory round trip per iteration.  With
+// 512 threads a thread's 16-byte column part (ch & 7) is the same in every
+// iteration, so its 8 bias values are loaded once.
 template <int S>
-__device__ __forceinline__ void stage(const uint16_t* __restrict__ src, long long row_stride,
-                                      const float* __restrict__ bias, uint16_t* rows, uint16_t* cols) {
+struct StageRegs {
+  static constexpr int N = (S * 8 + 511) / 512;   // 16-byte chunks per thread
+  uint4 v[N];
+  float4 b0, b1;
+};
+template <int S>
+__device__ __forceinline__ void stage_load(const uint16_t* __restrict__ src, long long row_stride,
+                                           const float* __restrict__ bias, StageRegs<S>& R) {
+  const int part = threadIdx.x & 7;
+#pragma unroll
+  for (int it = 0; it < StageRegs<S>::N; ++it) {
+    const int ch = threadIdx.x + 512 * it;
+    if (ch < S * 8) R.v[it] = ld16(src + (ch >> 3) * row_stride + part * 8);
+  }
+  if (bias) {
+    R.b0 = *reinterpret_cast<const float4*>(bias + part * 8);
+    R.b1 = *reinterpret_cast<const float4*>(bias + part * 8 + 4);
+  }
+}
+template <int S>
+__device__ __forceinline__ void stage_store(const StageRegs<S>& R, bool has_bias, uint16_t* rows, uint16_t* cols) {
   constexpr int VT = S + 8;
-  for (int ch = threadIdx.x; ch < S * 8; ch += blockDim.x) {
-    const int r = ch >> 3, part = ch & 7;
-    const uint4 v = add_bias8(ld16(src + r * row_stride + part * 8), bias ? bias + part * 8 : nullptr);
+  const int part = threadIdx.x & 7;
+  const float bb[8] = {R.b0.x, R.b0.y, R.b0.z, R.b0.w, R.b1.x, R.b1.y, R.b1.z, R.b1.w};
+#pragma unroll
+  for (int it = 0; it < StageRegs<S>::N; ++it) {
+    const int ch = threadIdx.x + 512 * it;
+    if (ch >= S * 8) break;
+    const int r = ch >> 3;
+    uint4 v = R.v[it];
+    if (has_bias) {
+      uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        w[j] = pack2bf(bf2f(w[j] & 0xffff) + bb[2 * j], bf2f(w[j] >> 16) + bb[2 * j + 1]);
+      v = uint4{w[0], w[1], w[2], w[3]};
+    }
     if (rows) *reinterpret_cast<uint4*>(rows + r * KP + part * 8) = v;
     if (cols) {
       const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -106,16 +141,22 @@ __global__ __launch_bounds__(512) void attn_fwd(const uint16_t* __restrict__ qkv
   const float* bq = bias ? bias + h * D : nullptr;
   const float* bk = bias ? bias + (NH + h) * D : nullptr;
   const float* bv = bias ? bias + (2 * NH + h) * D : nullptr;
-  stage<S>(base + NH * D, RS, bk, Ks, nullptr);
-  stage<S>(base + 2 * NH * D, RS, bv, nullptr, Vt);
-  __syncthreads();
+  StageRegs<S> rk, rv;
+  stage_load<S>(base + NH * D, RS, bk, rk);
+  stage_load<S>(base + 2 * NH * D, RS, bv, rv);
   const int q = blockIdx.x * 128 + w * 16 + c;
-  if (blockIdx.x * 128 + w * 16 >= S) return;          // wave-uniform; no barrier follows
+  const bool active = blockIdx.x * 128 + w * 16 < S;   // wave-uniform
+  uint4 qraw[2];   // this wave's query fragments, in flight with the stages
+#pragma unroll
+  for (int s = 0; s < 2; ++s) qraw[s] = ld16(base + (long long)min(q, S - 1) * RS + 32 * s + 8 * g);
+  stage_store<S>(rk, bk != nullptr, Ks, nullptr);
+  stage_store<S>(rv, bv != nullptr, nullptr, Vt);
+  __syncthreads();
+  if (!active) return;                                 // no barrier follows
 
   bf16x8 bqf[2];
 #pragma unroll
-  for (int s = 0; s < 2; ++s)
-    bqf[s] = as_frag(add_bias8(ld16(base + (long long)q * RS + 32 * s + 8 * g), bq ? bq + 32 * s + 8 * g : nullptr));
+  for (int s = 0; s < 2; ++s) bqf[s] = as_frag(add_bias8(qraw[s], bq ? bq + 32 * s + 8 * g : nullptr));
   f32x4 sc[2 * NKB];
 #pragma unroll
   for (int t = 0; t < 2 * NKB; ++t) {
@@ -190,18 +231,30 @@ __global__ __launch_bounds__(512) void attn_bwd_dq(const uint16_t* __restrict__ 
   const long long RS = 3LL * NH * D, HS = (long long)NH * D;
   const uint16_t* base = qkv + (long long)b * S * RS + h * D;
   const float* bq = bias ? bias + h * D : nullptr;
-  stage<S>(base + NH * D, RS, bias ? bias + (NH + h) * D : nullptr, Ks, Kt);
-  stage<S>(base + 2 * NH * D, RS, bias ? bias + (2 * NH + h) * D : nullptr, Vs, nullptr);
-  __syncthreads();
-  const int q = blockIdx.x * 128 + w * 16 + c;
-  if (blockIdx.x * 128 + w * 16 >= S) return;
-
-  bf16x8 bqf[2], bdo[2];
+  StageRegs<S> rk, rv;
+  const float* bkp = bias ? bias + (NH + h) * D : nullptr;
+  const float* bvp = bias ? bias + (2 * NH + h) * D : nullptr;
+  stage_load<S>(base + NH * D, RS, bkp, rk);
+  stage_load<S>(base + 2 * NH * D, RS, bvp, rv);
+  const bool active = blockIdx.x * 128 + w * 16 < S;   // wave-uniform
+  const int q = min(blockIdx.x * 128 + w * 16 + c, S - 1);
   const uint16_t* dor = dctx + ((long long)b * S + q) * HS + h * D;
+  uint4 qraw[2], doraw[2];   // this wave's fragments, in flight with the stages
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    bqf[s] = as_frag(add_bias8(ld16(base + (long long)q * RS + 32 * s + 8 * g), bq ? bq + 32 * s + 8 * g : nullptr));
-    bdo[s] = as_frag(ld16(dor + 32 * s + 8 * g));
+    qraw[s] = ld16(base + (long long)q * RS + 32 * s + 8 * g);
+    doraw[s] = ld16(dor + 32 * s + 8 * g);
+  }
+  stage_store<S>(rk, bkp != nullptr, Ks, Kt);
+  stage_store<S>(rv, bvp != nullptr, Vs, nullptr);
+  __syncthreads();
+  if (!active) return;
+
+  bf16x8 bqf[2], bdo[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    bqf[s] = as_frag(add_bias8(qraw[s], bq ? bq + 32 * s + 8 * g : nullptr));
+    bdo[s] = as_frag(doraw[s]);
   }
   // D = rowsum(dO * O): lane group g covers d = 16g .. 16g+15
   const uint16_t* orow = ctx + ((long long)b * S + q) * HS + h * D + 16 * g;
@@ -274,20 +327,31 @@ __global__ __launch_bounds__(512) void attn_bwd_dkv(const uint16_t* __restrict__
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, g = l >> 4, c = l & 15;
   const long long RS = 3LL * NH * D, HS = (long long)NH * D;
   const uint16_t* base = qkv + (long long)b * S * RS + h * D;
-  stage<S>(base, RS, bias ? bias + h * D : nullptr, Qs, Qt);
-  stage<S>(dctx + (long long)b * S * HS + h * D, HS, nullptr, dOs, dOt);
-  __syncthreads();
+  StageRegs<S> rq, rd;
+  const float* bqp = bias ? bias + h * D : nullptr;
+  stage_load<S>(base, RS, bqp, rq);
+  stage_load<S>(dctx + (long long)b * S * HS + h * D, HS, nullptr, rd);
   const int k0 = blockIdx.x * 128 + w * 16;
-  if (k0 >= S) return;
-  const int key = k0 + c;
+  const bool active = k0 < S;   // wave-uniform
+  const int key = min(k0 + c, S - 1);
+  uint4 kraw[2], vraw[2];   // this wave's key / value fragments, in flight with the stages
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    kraw[s] = ld16(base + (long long)key * RS + NH * D + 32 * s + 8 * g);
+    vraw[s] = ld16(base + (long long)key * RS + 2 * NH * D + 32 * s + 8 * g);
+  }
+  stage_store<S>(rq, bqp != nullptr, Qs, Qt);
+  stage_store<S>(rd, false, dOs, dOt);
+  __syncthreads();
+  if (!active) return;
 
   const float* bk = bias ? bias + (NH + h) * D : nullptr;
   const float* bv = bias ? bias + (2 * NH + h) * D : nullptr;
   bf16x8 kf[2], vf[2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    kf[s] = as_frag(add_bias8(ld16(base + (long long)key * RS + NH * D + 32 * s + 8 * g), bk ? bk + 32 * s + 8 * g : nullptr));
-    vf[s] = as_frag(add_bias8(ld16(base + (long long)key * RS + 2 * NH * D + 32 * s + 8 * g), bv ? bv + 32 * s + 8 * g : nullptr));
+    kf[s] = as_frag(add_bias8(kraw[s], bk ? bk + 32 * s + 8 * g : nullptr));
+    vf[s] = as_frag(add_bias8(vraw[s], bv ? bv + 32 * s + 8 * g : nullptr));
   }
   const float mk = mask ? mask[(long long)b * S + key] : 0.f;
   const long long rbase = ((long long)b * NH + h) * S;

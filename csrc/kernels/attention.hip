@@ -273,8 +273,13 @@ __global__ __launch_bounds__(512) void attn_bwd_dq(const uint16_t* __restrict__ 
   if (g == 0) Dbuf[row] = dsum;
   const float L = lse[row];
   const uint64_t ebase = (uint64_t)row * S;
-  bf16x8 dsb[NKB];
+  // dQ^T accumulates key block by key block as each block's dS is formed (no
+  // [NKB] dS array: with every block's operand loads hoisted the fully unrolled
+  // form held 152 VGPRs = one workgroup per CU); same MFMA order per output
+  f32x4 acc[4];
 #pragma unroll
+  for (int u = 0; u < 4; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
   for (int kb = 0; kb < NKB; ++kb) {
     float f[8];
 #pragma unroll
@@ -297,18 +302,18 @@ __global__ __launch_bounds__(512) void attn_bwd_dq(const uint16_t* __restrict__ 
         f[4 * tt + i] = P * (dpd - dsum);
       }
     }
-    dsb[kb] = pack8(f);
+    const bf16x8 dsb = pack8(f);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint16_t* kr = Kt + (16 * u + c) * VT + 4 * g + 32 * kb;
+      acc[u] = mfma16x16x32(ld_pair(kr, kr + 16), dsb, acc[u]);
+    }
   }
   uint16_t* dq = dqkv + ((long long)b * S + q) * RS + h * D;
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    const uint16_t* kr = Kt + (16 * u + c) * VT + 4 * g;
-#pragma unroll
-    for (int kb = 0; kb < NKB; ++kb) acc = mfma16x16x32(ld_pair(kr + 32 * kb, kr + 32 * kb + 16), dsb[kb], acc);
+  for (int u = 0; u < 4; ++u)
     *reinterpret_cast<uint2*>(dq + 16 * u + 4 * g) =
-        uint2{pack2bf(acc[0] * scale, acc[1] * scale), pack2bf(acc[2] * scale, acc[3] * scale)};
-  }
+        uint2{pack2bf(acc[u][0] * scale, acc[u][1] * scale), pack2bf(acc[u][2] * scale, acc[u][3] * scale)};
 }
 
 template <int NKB>

@@ -328,6 +328,8 @@ __global__ __launch_bounds__(512) void attn_bwd_dkv(const uint16_t* __restrict__
   uint16_t* dOs = lds + S * KP;                // [S][KP]
   uint16_t* Qt = lds + 2 * S * KP;             // [64][VT]
   uint16_t* dOt = lds + 2 * S * KP + D * VT;   // [64][VT]
+  float* Ls = reinterpret_cast<float*>(lds + 2 * S * KP + 2 * D * VT);   // [S] lse of every query row
+  float* Dl = Ls + S;                                                     // [S] rowsum(dO * O)
   const int b = blockIdx.z, h = blockIdx.y;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, g = l >> 4, c = l & 15;
   const long long RS = 3LL * NH * D, HS = (long long)NH * D;
@@ -345,8 +347,20 @@ __global__ __launch_bounds__(512) void attn_bwd_dkv(const uint16_t* __restrict__
     kraw[s] = ld16(base + (long long)key * RS + NH * D + 32 * s + 8 * g);
     vraw[s] = ld16(base + (long long)key * RS + 2 * NH * D + 32 * s + 8 * g);
   }
+  const long long rbase = ((long long)b * NH + h) * S;
+  // the per-query lse / D rows go to LDS with the stages (global float4 loads in
+  // the query loop exposed their latency every iteration)
+  float lsv = 0.f, dlv = 0.f;
+  if (threadIdx.x < S) {
+    lsv = lse[rbase + threadIdx.x];
+    dlv = Dbuf[rbase + threadIdx.x];
+  }
   stage_store<S>(rq, bqp != nullptr, Qs, Qt);
   stage_store<S>(rd, false, dOs, dOt);
+  if (threadIdx.x < S) {
+    Ls[threadIdx.x] = lsv;
+    Dl[threadIdx.x] = dlv;
+  }
   __syncthreads();
   if (!active) return;
 
@@ -359,7 +373,6 @@ __global__ __launch_bounds__(512) void attn_bwd_dkv(const uint16_t* __restrict__
     vf[s] = as_frag(add_bias8(vraw[s], bv ? bv + 32 * s + 8 * g : nullptr));
   }
   const float mk = mask ? mask[(long long)b * S + key] : 0.f;
-  const long long rbase = ((long long)b * NH + h) * S;
   f32x4 dv[4], dk[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
@@ -377,13 +390,13 @@ __global__ __launch_bounds__(512) void attn_bwd_dkv(const uint16_t* __restrict__
         sv = mfma16x16x32(ld_bf16x8(Qs + (16 * t + c) * KP + 32 * s + 8 * g), kf[s], sv);
         dp = mfma16x16x32(ld_bf16x8(dOs + (16 * t + c) * KP + 32 * s + 8 * g), vf[s], dp);
       }
-      const float4 L4 = *reinterpret_cast<const float4*>(lse + rbase + 16 * t + 4 * g);
-      const float4 D4 = *reinterpret_cast<const float4*>(Dbuf + rbase + 16 * t + 4 * g);
-      const float Ls[4] = {L4.x, L4.y, L4.z, L4.w}, Ds[4] = {D4.x, D4.y, D4.z, D4.w};
+      const float4 L4 = *reinterpret_cast<const float4*>(Ls + 16 * t + 4 * g);
+      const float4 D4 = *reinterpret_cast<const float4*>(Dl + 16 * t + 4 * g);
+      const float Lq[4] = {L4.x, L4.y, L4.z, L4.w}, Ds[4] = {D4.x, D4.y, D4.z, D4.w};
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int q = 16 * t + 4 * g + i;
-        const float P = __expf(sv[i] * scale + mk - Ls[i]);
+        const float P = __expf(sv[i] * scale + mk - Lq[i]);
         const float kp = keepf(seed, (uint64_t)(rbase + q) * S + key, thresh, inv_keep);
         pd[4 * tt + i] = P * kp;
         ds[4 * tt + i] = P * (dp[i] * kp - Ds[i]);
@@ -472,7 +485,7 @@ hipError_t dtfk_attn_bwd(const void* qkv, const float* bias, const float* mask, 
   const float ik = p > 0.f ? 1.f / (1.f - p) : 1.f;
   const uint32_t th = attn_thresh(p);
   const size_t lds_q = (size_t)(2 * S * KP + D * (S + 8)) * 2;
-  const size_t lds_kv = (size_t)(2 * S * KP + 2 * D * (S + 8)) * 2;
+  const size_t lds_kv = (size_t)(2 * S * KP + 2 * D * (S + 8)) * 2 + 2 * S * sizeof(float);
 #define L_BWD(N)                                                                                                   \
   {                                                                                                                \
     static hipError_t e1 = allow_lds(attn_bwd_dq<N>, lds_q);                                                       \

@@ -124,7 +124,10 @@ __device__ __forceinline__ void l1_tile(const float* __restrict__ x, const float
     for (int i = 0; i < 4; ++i) {
       const int m = r0 + 4 * g + i;
       const float z = t[i] + (cv ? bv : 0.f);
-      a2[(size_t)m * HP + col] = m < B ? (cv ? act_fwd(z, act) : (col == H ? 1.f : 0.f)) : 0.f;
+      // write-through (sc1) store: the row tile's head (another workgroup, maybe
+      // another XCD) reads it with sc1 loads -- no L2 write-back fence needed
+      __hip_atomic_store(a2 + (size_t)m * HP + col, m < B ? (cv ? act_fwd(z, act) : (col == H ? 1.f : 0.f)) : 0.f,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -174,10 +177,14 @@ __device__ void head_tile(const HeadArgs& a, const int rt) {
   constexpr int W2N = ((MAXH + 16) * CP + NW * 64 - 1) / (NW * 64);       // floats per thread
   float4 av4[A2N];
   float wv[W2N];
-  const float4* a2g = reinterpret_cast<const float4*>(a.a2 + (size_t)rb * HP);
+  // a2 rows of the tile: written (sc1) by the other workgroups of this launch ->
+  // L1-bypassing sc1 loads through a buffer resource
+  const __amdgpu_buffer_rsrc_t a2r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.a2 + (size_t)rb * HP), 0, 16 * HP * 4, 0x00020000);
   const int na2 = 16 * HP / 4;
 #pragma unroll
-  for (int j = 0; j < A2N; ++j) av4[j] = a2g[min(tid + j * NW * 64, na2 - 1)];
+  for (int j = 0; j < A2N; ++j)
+    av4[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(a2r, 16 * min(tid + j * NW * 64, na2 - 1), 0, 16));
 #pragma unroll
   for (int j = 0; j < W2N; ++j) {
     const int i = tid + j * NW * 64, h = i / CP, c = i % CP;
@@ -283,8 +290,8 @@ __global__ __launch_bounds__(512) void graph_mlp_l1h(const float* __restrict__ x
   __shared__ int last;
   l1_tile<VEC>(x, W1, b1, const_cast<float*>(h.a2), h.B, K, h.H, h.HP, h.act);
   const int nct = h.HP / 16, rt = blockIdx.x / nct;
-  if (threadIdx.x < 64) {   // wave 0 stored the tile: release it, then arrive
-    __threadfence();
+  if (threadIdx.x < 64) {   // wave 0 stored the tile (write-through): wait for the stores, then arrive
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (threadIdx.x == 0) {
       const int old = atomicAdd(cnt + rt, 1);
       last = old == nct - 1;
@@ -293,8 +300,7 @@ __global__ __launch_bounds__(512) void graph_mlp_l1h(const float* __restrict__ x
   }
   __syncthreads();
   if (!last) return;
-  __threadfence();          // acquire: the other workgroups' a2 rows
-  head_tile<8>(h, rt);
+  head_tile<8>(h, rt);      // reads the other workgroups' a2 rows with sc1 loads
 }
 
 // ---------------------------------------------------------------- L3

@@ -365,11 +365,13 @@ __device__ void graph_mlp_w2_final(const WgradArgs& a, int ht) {
       }
       a.metrics[2] = now;                 // post-increment value, read back with the loss
     }
-    if (a.host_metrics != nullptr) {      // system-scope vector stores over PCIe, fenced before the kernel ends
+    if (a.host_metrics != nullptr) {      // system-scope (write-through) stores over PCIe
 #pragma unroll
       for (int i = 0; i < 3; ++i)
         __hip_atomic_store(a.host_metrics + i, a.metrics[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __threadfence_system();
+      // acknowledged before the wave ends (the kernel's completion signal follows);
+      // a __threadfence_system() here wrote back the whole L2 first
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
   }
 }

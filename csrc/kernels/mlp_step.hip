@@ -732,7 +732,8 @@ __global__ __launch_bounds__(256) void mlp_ipc_reduce_apply(
   if (ok && threadIdx.x < W) {
     const unsigned long long* f = reinterpret_cast<const unsigned long long*>(peer_base[threadIdx.x]);
     const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
+    // relaxed polls (an acquire load is an L2 invalidate per poll), one acquire after
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
       __builtin_amdgcn_s_sleep(1);
       if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
         atomicOr(err, 1);
@@ -740,6 +741,7 @@ __global__ __launch_bounds__(256) void mlp_ipc_reduce_apply(
         break;
       }
     }
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
   }
   __syncthreads();
   if (!ok) return;

@@ -498,39 +498,83 @@ __global__ void multi_tensor_apply(const TensorRec* __restrict__ tab, const int2
     lr_t = (float)(lr * sqrt(1.0 - pow((double)b2, st)) / (1.0 - pow((double)b1, st)));
   }
   const int64_t s = (int64_t)ch.y, e = min(t.n, s + CHUNK);
-  for (int64_t i = s + threadIdx.x; i < e; i += blockDim.x) {
-    float g = ld_grad(t.g, i, gbf) * gscale;
-    float p = t.p[i];
+  // one element: p, m, v in registers (m / v untouched by the kinds that have none)
+  auto upd = [&](float& p, float g, float& m, float& v) {
+    const float p0 = p;
+    g *= gscale;
     if (kind == 0) {
       if (wd != 0.f) g += wd * p;
       p -= lr * g;
     } else if (kind == 1) {
       if (wd != 0.f) g += wd * p;
-      const float mv = momentum * t.m[i] + g;
-      t.m[i] = mv;
+      const float mv = momentum * m + g;
+      m = mv;
       p -= lr * (nesterov ? g + momentum * mv : mv);
     } else if (kind == 4) {
       // TF ApplyAdagrad: accum += g^2; var -= lr * g / sqrt(accum)
-      const float acc = t.m[i] + g * g;
-      t.m[i] = acc;
+      const float acc = m + g * g;
+      m = acc;
       p -= lr * g / sqrtf(acc);
     } else if (kind == 5) {
       // TF ApplyRMSProp: ms = rho ms + (1 - rho) g^2; mom = mu mom + lr g / sqrt(ms + eps); var -= mom
-      const float ms = b1 * t.m[i] + (1.f - b1) * g * g;
-      const float mo = momentum * t.v[i] + lr * g / sqrtf(ms + eps);
-      t.m[i] = ms;
-      t.v[i] = mo;
+      const float ms = b1 * m + (1.f - b1) * g * g;
+      const float mo = momentum * v + lr * g / sqrtf(ms + eps);
+      m = ms;
+      v = mo;
       p -= mo;
     } else {
       if (kind == 2 && wd != 0.f) g += wd * p;
-      const float mv = b1 * t.m[i] + (1.f - b1) * g;
-      const float vv = b2 * t.v[i] + (1.f - b2) * g * g;
-      t.m[i] = mv;
-      t.v[i] = vv;
+      const float mv = b1 * m + (1.f - b1) * g;
+      const float vv = b2 * v + (1.f - b2) * g * g;
+      m = mv;
+      v = vv;
       p -= lr_t * mv / (sqrtf(vv) + eps);
-      if (kind == 3 && wd != 0.f) p -= lr * wd * t.p[i];
+      if (kind == 3 && wd != 0.f) p -= lr * wd * p0;
     }
+  };
+  const bool use_m = kind != 0, use_v = kind == 2 || kind == 3 || kind == 5;
+  // 16-byte path (4 elements per access) when every stream of this chunk is aligned:
+  // the scalar loop moved 4 B per lane per access (~4.5 TB/s on BERT-base's AdamW)
+  const bool vec = (s & 3) == 0 && (reinterpret_cast<uintptr_t>(t.p) & 15) == 0 &&
+                   (!use_m || (reinterpret_cast<uintptr_t>(t.m) & 15) == 0) &&
+                   (!use_v || (reinterpret_cast<uintptr_t>(t.v) & 15) == 0) &&
+                   (reinterpret_cast<uintptr_t>(t.g) & (gbf ? 7 : 15)) == 0 &&
+                   (t.shadow == nullptr || (reinterpret_cast<uintptr_t>(t.shadow) & 7) == 0);
+  int64_t i0 = s;
+  if (vec) {
+    const int64_t e4 = s + ((e - s) & ~(int64_t)3);
+    for (int64_t i = s + 4 * (int64_t)threadIdx.x; i < e4; i += 4 * (int64_t)blockDim.x) {
+      float4 p4 = *reinterpret_cast<const float4*>(t.p + i);
+      float4 m4 = use_m ? *reinterpret_cast<const float4*>(t.m + i) : float4{0.f, 0.f, 0.f, 0.f};
+      float4 v4 = use_v ? *reinterpret_cast<const float4*>(t.v + i) : float4{0.f, 0.f, 0.f, 0.f};
+      float g4[4];
+      if (gbf) {
+        const uint2 u = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(t.g) + i);
+        g4[0] = bf2f(u.x & 0xffff); g4[1] = bf2f(u.x >> 16); g4[2] = bf2f(u.y & 0xffff); g4[3] = bf2f(u.y >> 16);
+      } else {
+        const float4 f = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(t.g) + i);
+        g4[0] = f.x; g4[1] = f.y; g4[2] = f.z; g4[3] = f.w;
+      }
+      upd(p4.x, g4[0], m4.x, v4.x);
+      upd(p4.y, g4[1], m4.y, v4.y);
+      upd(p4.z, g4[2], m4.z, v4.z);
+      upd(p4.w, g4[3], m4.w, v4.w);
+      *reinterpret_cast<float4*>(t.p + i) = p4;
+      if (use_m) *reinterpret_cast<float4*>(t.m + i) = m4;
+      if (use_v) *reinterpret_cast<float4*>(t.v + i) = v4;
+      if (t.shadow)
+        *reinterpret_cast<uint2*>(t.shadow + i) = uint2{(uint32_t)f2bf(p4.x) | ((uint32_t)f2bf(p4.y) << 16),
+                                                         (uint32_t)f2bf(p4.z) | ((uint32_t)f2bf(p4.w) << 16)};
+    }
+    i0 = e4;
+  }
+  for (int64_t i = i0 + threadIdx.x; i < e; i += blockDim.x) {
+    float p = t.p[i];
+    float m = use_m ? t.m[i] : 0.f, v = use_v ? t.v[i] : 0.f;
+    upd(p, ld_grad(t.g, i, gbf), m, v);
     t.p[i] = p;
+    if (use_m) t.m[i] = m;
+    if (use_v) t.v[i] = v;
     if (t.shadow) t.shadow[i] = f2bf(p);
   }
 }

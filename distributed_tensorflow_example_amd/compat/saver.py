@@ -400,6 +400,9 @@ class Saver:
                 v.initialized = True
                 continue
             t = read_tensor(prefix, name)
+            if hasattr(v, "restore_from"):     # derived state (Adam's beta powers -> step counts)
+                v.restore_from(t)
+                continue
             dst = self._value(v)
             if tuple(t.shape) != tuple(dst.shape):
                 raise ValueError(f"shape mismatch for {name}: ckpt {tuple(t.shape)} vs {tuple(dst.shape)}")

@@ -356,6 +356,7 @@ class Optimizer:
         for _, pv in sparse_pairs:      # owner-side sparse rule + sharded slots (TF names var/<slot>)
             pv.table.set_optimizer(self._kind, **self._sparse_hp())
             self._register_pv_slots(pv)
+        self._register_nonslot([v for _, v in dense_pairs], [pv for _, pv in sparse_pairs])
         vars_ = [v for _, v in dense_pairs]
         gtens = [g for g, _ in dense_pairs]
         opt = self
@@ -387,10 +388,18 @@ class Optimizer:
                 fused.step(grads=[g.contiguous() for g in gs])
             lr = opt._lr_value()
             for g, pv in sparse_pairs:      # owner-side sparse update, sync average as grad_scale
-                for lctx, rows_grad in ctx.eval(g):
+                looks = ctx.eval(g)
+                # several lookups of one variable: TF sums their IndexedSlices and
+                # applies the rule once (SGD is linear, the others are not)
+                multi = len(looks) > 1
+                if multi:
+                    pv.table.begin_update()
+                for lctx, rows_grad in looks:
                     pv.table.apply_sgd(lctx, rows_grad if rows_grad is not None else
                                        torch.zeros((lctx.uniq.numel(), pv.dim), device=pv.table.device), lr,
                                        grad_scale=1.0 / ws)
+                if multi:
+                    pv.table.finish_update(lr)
             if global_step is not None:
                 with torch.no_grad():
                     global_step.value.data += 1
@@ -499,6 +508,9 @@ class Optimizer:
     def get_slot_names(self):
         return list(self._slot_names)
 
+    def _register_nonslot(self, dense_vars, pvs):
+        """TF's non-slot optimizer variables (Adam: beta1_power / beta2_power)."""
+
     def _slot_init(self, sname: str) -> float:
         """Initial value TF gives the slot (zeros unless the optimizer says otherwise)."""
         return 0.0
@@ -554,36 +566,65 @@ class AdamOptimizer(Optimizer):
     def _sparse_hp(self):
         return {"beta1": float(self.beta1), "beta2": float(self.beta2), "epsilon": float(self.epsilon)}
 
+    def _register_nonslot(self, dense_vars, pvs):
+        # TF's non-slot accumulators beta1_power / beta2_power (= beta^(t+1)),
+        # tied to the step count of the dense fused Adam and of every
+        # partitioned variable's sparse Adam (a restore sets them all)
+        steps = []
+        for pv in pvs:
+            if pv.table._adam is not None:
+                steps.append(pv.table._adam.step_t)
+        self._pending_powers = steps
+        if not dense_vars and steps:
+            self._add_powers(None)
+
     def _register_slots(self, vars_, fused):
         super()._register_slots(vars_, fused)
+        self._add_powers(fused)
+
+    def _add_powers(self, fused):
         g = get_default_graph()
-        # TF's non-slot accumulators beta1_power / beta2_power (= beta^t)
-        b1p = _PowerVariable("beta1_power", self.beta1, fused)
-        b2p = _PowerVariable("beta2_power", self.beta2, fused)
-        for v in (b1p, b2p):
-            g.add_to_collection(GLOBAL_VARIABLES, v)
+        steps = ([fused.step_t] if fused is not None else []) + list(getattr(self, "_pending_powers", []))
+        have = {v.name: v for v in g.get_collection(GLOBAL_VARIABLES)}
+        for name, beta in (("beta1_power", self.beta1), ("beta2_power", self.beta2)):
+            v = have.get(name + ":0")
+            if isinstance(v, _PowerVariable):
+                v.steps += [t for t in steps if all(t is not u for u in v.steps)]
+            else:
+                g.add_to_collection(GLOBAL_VARIABLES, _PowerVariable(name, beta, steps))
 
 
 class _PowerVariable:
-    """beta^t as a saveable variable, tied to the fused optimizer's step."""
+    """beta^(t+1) as a saveable variable, tied to the optimizers' step counts
+    (`steps`: device int64 [1] tensors advanced together)."""
 
     op_type, attrs, shape, dtype = "VariableV2", {}, (), torch.float32
 
-    def __init__(self, name, beta, fused):
+    def __init__(self, name, beta, steps):
         self.name = name + ":0"
         self.beta = beta
-        self.fused = fused
+        self.steps = list(steps)
         self.initialized = True
         self._buf = torch.zeros((), dtype=torch.float32)
 
     @property
     def value(self):
-        t = int(self.fused.step_t.item())
+        t = int(self.steps[0].item()) if self.steps else 0
         self._buf.fill_(self.beta ** (t + 1))  # TF stores beta^(t+1) after t updates
         return self._buf
 
+    def restore_from(self, t: torch.Tensor):
+        """Saver.restore: beta^(t+1) -> the step count of every tied optimizer."""
+        import math
+
+        v = float(t.reshape(-1)[0])
+        steps = max(0, int(round(math.log(v) / math.log(self.beta))) - 1) if 0.0 < v < 1.0 else 0
+        for s in self.steps:
+            s.fill_(steps)
+
     def _initialize(self):
-        pass
+        for s in self.steps:
+            s.zero_()
 
 
 class AdagradOptimizer(Optimizer):

@@ -76,12 +76,16 @@ class SparseLRTrainer(StaticStepMixin):
         offsets = offsets.to(self.device).long()
         ids = ids.to(self.device)
         vals = None if vals is None else vals.to(self.device).float()
+        self._last_empty = ids.numel() == 0
         if self.W.capacity is not None:      # fixed shapes for the captured / static step
             offsets, ids, vals = pad_to_capacity(offsets, ids, vals, self.W.capacity)
         return labels.to(self.device), offsets, ids, vals
 
     def _router(self):
         return self.W.router
+
+    def _route_table(self):
+        return self.W
 
     def train_step(self, batch) -> torch.Tensor:
         if self._bstore is not None:
@@ -163,12 +167,15 @@ class SparseLRTrainer(StaticStepMixin):
     @torch.no_grad()
     def evaluate(self, batch):
         """(mean loss, probabilities) without updating (lr2.py Test(), :307-315).
-        Lookups use the exact exchange: evaluation batches need no fixed shapes."""
+        Lookups use the exact exchange: evaluation batches need no fixed shapes.
+        Collective: first applies any voided steps of the current window."""
+        self.sync_exchange()
         logits, labels, _ = self._forward(batch, exact=True)
         return ops.sigmoid_xent(logits, labels).detach(), torch.sigmoid(logits).reshape(-1)
 
     @torch.no_grad()
     def auc_update(self, batch):
+        self.sync_exchange()
         logits, labels, _ = self._forward(batch, exact=True)
         ops.auc_histogram_(torch.sigmoid(logits).reshape(-1), labels.reshape(-1), self.auc_pos, self.auc_neg)
 
@@ -185,6 +192,9 @@ class SparseLRTrainer(StaticStepMixin):
 
     # ----------------------------------------------------------------- state
     def checkpoint_tensors(self):
+        """Collective: applies the voided steps of the current window first, so a
+        checkpoint holds every batch trained so far."""
+        self.sync_exchange()
         local = {"weights/Variable": self.W}      # saved as a TF partitioned variable
         repl = {"bias/Variable": self.b.detach(), "global_step": torch.tensor(float(self.global_step))}
         return local, repl

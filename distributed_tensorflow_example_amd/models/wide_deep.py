@@ -105,12 +105,16 @@ class WideDeep(StaticStepMixin):
         offsets = offsets.to(self.device).long()
         ids = ids.to(self.device)
         vals = None if vals is None else vals.to(self.device).float()
+        self._last_empty = ids.numel() == 0
         if self.ids_capacity is not None:    # fixed shapes for the captured / static step
             offsets, ids, vals = pad_to_capacity(offsets, ids, vals, self.ids_capacity)
         return labels.to(self.device), offsets, ids, vals
 
     def _router(self):
         return self.wide.router
+
+    def _route_table(self):
+        return self.wide          # routes both tables' ids
 
     def enable_graph(self, on: bool = True, example=None):
         """Replay each training step as ONE captured hipGraph: routing, the two
@@ -178,19 +182,76 @@ class WideDeep(StaticStepMixin):
 
     @torch.no_grad()
     def predict(self, batch) -> torch.Tensor:
+        self.sync_exchange()      # collective: the voided steps of the window are applied first
         labels, offsets, ids, vals = batch.to(self.device) if hasattr(batch, "to") else batch
         logit, _ = self.forward(labels, offsets, ids, vals, exact=True)
         return torch.sigmoid(logit).reshape(-1)
 
     def checkpoint_tensors(self):
+        """(sharded, replicated) tensors under TF names.  Collective: applies the
+        voided steps of the current window first.  Adam state is complete: the
+        tower's slots (`<var>/Adam`, `<var>/Adam_1`) and `beta1_power` /
+        `beta2_power` (TF's beta^(t+1) after t updates), and the tables' own
+        sparse-Adam powers under `sparse/`."""
+        self.sync_exchange()
         local = {self.wide.name: self.wide, self.emb.name: self.emb}   # TF partitioned variables
         for t in (self.wide, self.emb):                                 # their optimizer slots, sharded alike
             for sname in t.slots:
                 local[f"{t.name}/{sname}"] = t.slot_view(sname)
+        repl = {}
+        for name, p, i in self._dense_names():
+            repl[name] = p.detach()
+            for sname, st in (("Adam", self.opt.m[i]), ("Adam_1", self.opt.v[i])):
+                if st is not None:
+                    repl[f"{name}/{sname}"] = st.detach()
+        repl.update(self._powers("", self.opt))
+        if self.wide._adam is not None:
+            repl.update(self._powers("sparse/", self.wide._adam))
+        repl["global_step"] = torch.tensor(self.global_step, dtype=torch.int64)
+        return local, repl
+
+    def _dense_names(self):
         names = []
         for i in range(len(self.layers) // 2):
             names += [f"deep/dense_{i}/kernel", f"deep/dense_{i}/bias"]
-        repl = {n: p.detach() for n, p in zip(names, self.layers)}
-        repl["bias"] = self.bias.detach()
-        repl["global_step"] = torch.tensor(self.global_step, dtype=torch.int64)
-        return local, repl
+        names.append("bias")
+        return [(n, p, i) for i, (n, p) in enumerate(zip(names, self.dense_params))]
+
+    @staticmethod
+    def _powers(prefix, opt):
+        if opt.kind not in ("adam", "adamw"):
+            return {}
+        t = int(opt.step_t.item())
+        return {f"{prefix}beta1_power": torch.tensor(opt.b1 ** (t + 1), dtype=torch.float32),
+                f"{prefix}beta2_power": torch.tensor(opt.b2 ** (t + 1), dtype=torch.float32)}
+
+    @staticmethod
+    def _step_from_power(value: float, beta: float) -> int:
+        import math
+        return max(0, int(round(math.log(float(value)) / math.log(beta))) - 1)
+
+    def restore(self, prefix: str):
+        """Load a checkpoint written from `checkpoint_tensors` (any world size):
+        tables and slots take the rows they own, the tower, its Adam slots and
+        every optimizer's step count (from beta1_power) are restored."""
+        from ..ckpt import read_bundle_index, read_tensor, restore_sharded
+
+        local, repl = self.checkpoint_tensors()
+        idx = read_bundle_index(prefix)
+        restore_sharded(prefix, {k: v for k, v in local.items()})
+        with torch.no_grad():
+            for name, dst in repl.items():
+                if name.endswith("beta2_power") or name == "global_step":
+                    continue
+                if name.endswith("beta1_power"):
+                    opt = self.opt if name == "beta1_power" else self.wide._adam
+                    if name in idx:
+                        steps = self._step_from_power(float(read_tensor(prefix, name)), opt.b1)
+                        opts = [opt] if opt is self.opt else [self.wide._adam, self.emb._adam]
+                        for o in opts:
+                            o.step_t.fill_(steps)
+                    continue
+                if name in idx:          # dst shares storage with the parameter / slot
+                    dst.copy_(read_tensor(prefix, name).to(self.device, torch.float32).reshape(dst.shape))
+        if "global_step" in idx:
+            self.global_step = int(read_tensor(prefix, "global_step"))

@@ -182,6 +182,8 @@ class ShardedEmbedding:
         self.opt_kind, self.opt_hp, self.slots = "sgd", {}, {}
         self._gacc = None
         self._adam = None
+        self._defer = None               # pending (row index) tensors of a multi-lookup sparse update
+        self._empty = None               # device int32 [1]: this step's batch has no ids (set_batch_empty)
         n_local = (self.num_rows - self.rank + self.W - 1) // self.W if self.rank < self.num_rows else 0
         self.local = torch.empty((n_local, self.dim), dtype=torch.float32, device=self.device)
         with torch.no_grad():
@@ -228,6 +230,8 @@ class ShardedEmbedding:
         owner = uniq % self.W
         order = torch.argsort(owner, stable=True)
         uniq_sorted = uniq[order]
+        if self._empty is not None and bool(self._empty.item()):
+            uniq_sorted = torch.full_like(uniq_sorted, -1)   # padding of an empty batch: no row is touched
         send = torch.bincount(owner, minlength=self.W)
         recv = torch.empty_like(send)
         self.world.all_to_all(send, [1] * self.W, recv, [1] * self.W)
@@ -253,6 +257,15 @@ class ShardedEmbedding:
             ops.register_sorted_ids(inverse, inv_sorted, perm)
         else:
             inv_sorted, inverse, uniq, dest, send, ocnt = _route_static_torch(sids, perm, W, pc)
+        if self._empty is not None:
+            # an empty batch is all padding: no id is sent or looked up as a
+            # touched row (capturable: the flag is read on the device)
+            e = self._empty.bool()
+            uniq = uniq.masked_fill(e, -1)
+            if W > 1:
+                send = send.masked_fill(e, -1)
+                dest = dest.masked_fill(e, -1)
+                ocnt = ocnt.masked_fill(e, 0)
         if W == 1:
             return LookupCtx(uniq, inverse, None, None, None, uniq, static=True, n=N)
         router.record(ocnt, self.rank)
@@ -267,7 +280,9 @@ class ShardedEmbedding:
         if self.hogwild is not None:      # asynchronous: straight from the owners' shards, no collective
             rows, inverse, uniq = self.hogwild.lookup(ids)
             return rows, LookupCtx(uniq, inverse, None, None, None, None, hogwild=True)
-        ctx = self.route(ids)
+        # outside a training step: the exact exchange (the static one records
+        # into the router's per-step window, which only train steps advance)
+        ctx = self.route(ids, exact=True)
         return lookup_shared([self], ctx)[0], ctx
 
     def apply_sgd(self, ctx: LookupCtx, grad_rows: torch.Tensor, lr: float, grad_scale: float = 1.0):
@@ -315,15 +330,40 @@ class ShardedEmbedding:
             self._adam = optim.FusedAdam([self.local], 0.001, float(hp.get("beta1", 0.9)),
                                          float(hp.get("beta2", 0.999)), float(hp.get("epsilon", 1e-8)))
             self.slots["Adam"], self.slots["Adam_1"] = self._adam.m[0], self._adam.v[0]
+        self._empty = None if kind == "sgd" else torch.zeros(1, dtype=torch.int32, device=self.device)
         # [local rows + 1 dump row] accumulator of a step's summed gradients, zero between steps
         self._gacc = None if kind == "sgd" else torch.zeros((self.local.shape[0] + 1, self.dim),
                                                             dtype=torch.float32, device=self.device)
+
+    def set_batch_empty(self, empty: bool):
+        """Mark the next routed batch as empty (all padding).  Only matters for
+        the row-local sparse rules: TF touches no row on an empty batch, while
+        the static padding would repeat id 0 with a zero gradient (SGD: a
+        no-op, so nothing is recorded)."""
+        if self.opt_kind == "sgd" and self._empty is None:
+            return
+        if self._empty is None:
+            self._empty = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self._empty.fill_(1 if empty else 0)
+
+    def begin_update(self):
+        """Collect the sparse gradients of several lookups of this table into one
+        update (TF sums the IndexedSlices of every lookup, then applies the rule
+        once): `apply_sgd` calls only accumulate until `finish_update`."""
+        if self.opt_kind != "sgd":
+            self._defer = []
+
+    def finish_update(self, lr: float, void: Optional[torch.Tensor] = None):
+        pend, self._defer = self._defer, None
+        if pend:
+            self._apply_rule(torch.cat(pend), lr, void)
 
     def slot_view(self, slot: str) -> "ShardedEmbedding":
         """The slot as a table of the same geometry (checkpoint save / restore)."""
         v = copy.copy(self)
         v.local, v.name = self.slots[slot], f"{self.name}/{slot}"
         v.router, v.hogwild, v.slots, v.opt_kind, v._gacc, v._adam = None, None, {}, "sgd", None, None
+        v._defer, v._empty = None, None
         return v
 
     def state_tensors(self):
@@ -352,6 +392,16 @@ class ShardedEmbedding:
         nl = self.local.shape[0]
         i = torch.where(idx >= 0, idx, torch.full_like(idx, nl))
         self._gacc.index_add_(0, i, g if grad_scale == 1.0 else g * grad_scale)
+        if self._defer is not None:        # more lookups of this table follow in this step
+            self._defer.append(i)
+            return
+        self._apply_rule(i, lr, void)
+
+    @torch.no_grad()
+    def _apply_rule(self, i: torch.Tensor, lr: float, void: Optional[torch.Tensor]):
+        """The rule over the rows accumulated in _gacc (i: their local indices,
+        nl = the dump row of padding), then clear them."""
+        nl = self.local.shape[0]
         s, _ = torch.sort(i)
         hp = self.opt_hp
         if self.opt_kind == "adam":
@@ -432,7 +482,7 @@ def lookup_shared(tables, ctx: LookupCtx):
         idx = ctx.uniq.clamp_min(0) if ctx.static else ctx.uniq     # padding slots read row 0, never used
         return [t.local.index_select(0, idx) for t in tables]
     dims = [t.dim for t in tables]
-    src = ctx.recv_local.clamp_min(0) if ctx.static else ctx.recv_local
+    src = ctx.recv_local.clamp_min(0)           # -1: padding slots / an empty batch's ids, never used
     served = torch.cat([t.local.index_select(0, src) for t in tables], 1) if len(tables) > 1 else \
         t0.local.index_select(0, src)
     got = torch.empty((sum(ctx.send), sum(dims)) if ctx.static else (ctx.uniq.numel(), sum(dims)),
@@ -563,11 +613,16 @@ class StaticStepMixin:
     through the exact exchange and re-capture after a resize -- on every rank
     at the same step, so collective sequences always match.
 
-    Needs: `_router()`, `_static_batch(batch)`, `_train_step(batch, exact)`,
-    `_graphed`, `_example`, `_window`, `global_step`, `world`."""
+    Needs: `_router()`, `_route_table()`, `_static_batch(batch)` (sets
+    `_last_empty`), `_train_step(batch, exact)`, `_graphed`, `_example`,
+    `_window`, `global_step`, `world`."""
+
+    _last_empty = False
 
     def train_step(self, batch) -> torch.Tensor:
         b = self._static_batch(batch)
+        empty = bool(self._last_empty)
+        self._route_table().set_batch_empty(empty)
         g = self._graphed
         if g is not None and (g.matches(*b) or not g.strict):   # one rank: (re)capture lazily
             loss = g(*b)
@@ -577,14 +632,15 @@ class StaticStepMixin:
         r = self._router()
         if r is not None and self.world.world_size > 1:
             r.steps += 1
-            self._window.append(b)
+            self._window.append((b, empty))
             if r.due():
                 self._check_exchange()
         return loss.detach()
 
     def sync_exchange(self):
-        """Replay the voided steps of the current window now (call before
-        evaluation / checkpointing: then every batch seen so far is applied)."""
+        """Replay the voided steps of the current window now: afterwards every
+        batch seen so far is applied.  Collective (every rank at the same
+        point); evaluation, prediction, AUC and checkpoints call it first."""
         r = self._router()
         if r is not None and self.world.world_size > 1 and r.steps:
             self._check_exchange()
@@ -593,7 +649,12 @@ class StaticStepMixin:
         r = self._router()
         voided, changed = r.check()
         window, self._window = self._window, []
-        for i in voided:
-            self._train_step(window[i], exact=True)
+        t = self._route_table()
+        with torch.enable_grad():        # also reached from no_grad evaluation / prediction
+            for i in voided:
+                b, empty = window[i]
+                t.set_batch_empty(empty)
+                self._train_step(b, exact=True)
+        t.set_batch_empty(False)
         if changed and self._graphed is not None and self._graphed.strict:
             self._graphed.capture(*self._example)

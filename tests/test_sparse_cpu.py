@@ -95,7 +95,8 @@ def test_parse_parity_with_python_reference_parser():
         assert d.labels[i] == lab and list(d.ids[s:e]) == idx and np.allclose(d.vals[s:e], val)
 
 
-def _sharded_worker(rank, ws, port, q, files, steps, lr, kind="lr", peer_cap=None, sparse_opt="sgd"):
+def _sharded_worker(rank, ws, port, q, files, steps, lr, kind="lr", peer_cap=None, sparse_opt="sgd",
+                    explicit_sync=True):
     try:
         sys.path.insert(0, REPO)
         os.environ.update(RANK=str(rank), WORLD_SIZE=str(ws), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
@@ -128,10 +129,11 @@ def _sharded_worker(rank, ws, port, q, files, steps, lr, kind="lr", peer_cap=Non
             tr.train_step(data.take(mine))
         stats = None
         if router is not None and ws > 1:
-            tr.sync_exchange()                     # flush the last window (replays voided steps)
+            if explicit_sync:
+                tr.sync_exchange()                 # flush the last window (replays voided steps)
             stats = dict(peer_cap=router.peer_cap, checks=router.checks, resizes=router.resizes,
                          voided=router.voided, gstep=tr.global_step)
-        final = tr.W.full_table().numpy().copy()
+        final = tr.W.full_table().numpy().copy() if explicit_sync else None
         if kind.startswith("wd"):
             q.put((rank, init_tab, final, tr.b.detach().numpy().copy(), tr.wide.full_table().numpy().copy(), stats))
             return

@@ -33,6 +33,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import statistics
 import sys
@@ -202,6 +203,8 @@ def main(argv=None):
         fallbacks[mode] = "failed validation (exchange timeout or replica drift after warmup)"
         print(f"bench: {mode} failed validation" + (f"; trying {chain[i + 1]}" if i + 1 < len(chain) else ""),
               file=sys.stderr, flush=True)
+    # chain modes not tried yet (the loop stops once a good strategy validated)
+    remaining = [m for m in chain[chain.index(picked[-1][0]) + 1:] if m not in fallbacks] if picked else []
     if not picked:
         raise SystemExit(f"replicas diverged / exchange timed out after warmup (tried {chain})")
     tuned = {}
@@ -218,64 +221,104 @@ def main(argv=None):
             tuned[mode] = round(el * 1e6 / a.tune_steps, 3)
             if not consistent(tr_, rn_):
                 tuned[mode] = None
+                fallbacks[mode] = "failed validation during exchange tuning"
         print(f"bench: exchange tuning us/step {tuned}", file=sys.stderr, flush=True)
         picked.sort(key=lambda m: float("inf") if tuned[m[0]] is None else tuned[m[0]])
-        if tuned[picked[0][0]] is None:
-            raise SystemExit("every exchange strategy failed validation during tuning")
-    mode, trainer, runner = picked[0]
-    persistent = isinstance(runner, PersistentMLPRunner)
-    if persistent and w_final > 0:
-        runner.prepare(w_final)   # (the tuning moved the cursor: staged outside any timed region)
-        torch.cuda.synchronize()
+        picked = [m for m in picked if tuned[m[0]] is not None]
+
+    def timed_run(mode, trainer, runner):
+        """The timed region: exactly a.steps steps between barrier + synchronize
+        on both sides.  Returns None when the run fails the exchange / replica
+        check (the caller falls back to the next validated strategy)."""
+        persistent = isinstance(runner, PersistentMLPRunner)
+        if persistent and w_final > 0:
+            runner.prepare(w_final)   # (the tuning moved the cursor: staged outside any timed region)
+            torch.cuda.synchronize()
+            w.barrier()
+            runner.run(w_final, lookahead=a.steps)   # final warmup; stages the timed run's chunk
+        else:
+            runner.prepare(a.steps)   # graphs / first staged chunk for the timed plan (the tuning moved the cursor)
+            torch.cuda.synchronize()
+        step0 = trainer.global_step
+        cold0 = runner.copy_only_launches if persistent else 0
+        # tests: rank 1 goes silent (a dead peer) from timed step k on, in the first timed attempt only
+        fault = os.environ.pop("DTF_BENCH_FAULT", None)
+        if fault is not None and w.world_size > 1 and persistent:
+            os.environ["DTF_XCHG_FAULT"] = f"1:{step0 + int(fault)}"
+        # Timing events only for the 3-launch path (its per-replay p50); the
+        # persistent engine's p50 comes from device stamps, so nothing but the
+        # launch is issued inside its timed region (a first hipEventCreate + record
+        # there measured ~+30-40 us of host time in front of the kernel).
+        events = None if persistent else []
+        ev0 = None if persistent else torch.cuda.Event(enable_timing=True)
         w.barrier()
-        runner.run(w_final, lookahead=a.steps)   # final warmup; stages the timed run's chunk
-    else:
-        runner.prepare(a.steps)   # graphs / first staged chunk for the timed plan (the tuning moved the cursor)
         torch.cuda.synchronize()
-    step0 = trainer.global_step
-    cold0 = runner.copy_only_launches if persistent else 0
+        t0 = time.perf_counter()
+        if ev0 is not None:
+            ev0.record()
+        runner.run(a.steps, events=events)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        w.barrier()
+        os.environ.pop("DTF_XCHG_FAULT", None)
+        elapsed_max = w.host_all_reduce(t1 - t0, "max")
+        if not consistent(trainer, runner):
+            return None
+        if persistent:
+            # true per-step times: device stamps at every step start (100 MHz s_memrealtime)
+            per_step_ms = list(runner.step_times_ms(step0, step0 + a.steps))
+            p50_source = "per-step device timestamps (s_memrealtime at every step start)"
+        else:
+            # 3-launch path: average per step of each graph replay
+            per_step_ms = []
+            prev = ev0
+            for ev, g in events:
+                per_step_ms.append(prev.elapsed_time(ev) / g)
+                prev = ev
+            p50_source = "per-graph-replay average"
+        srt = sorted(per_step_ms)
+        p50 = statistics.median(srt) if srt else float("nan")
+        p90 = srt[min(len(srt) - 1, int(0.9 * len(srt)))] if srt else float("nan")
+        return dict(elapsed_max=elapsed_max, p50=w.host_all_reduce(p50, "max"), p90=w.host_all_reduce(p90, "max"),
+                    p50_source=p50_source, step0=step0,
+                    cold_timed=(runner.copy_only_launches - cold0) if persistent else 0)
 
-    # Timing events only for the 3-launch path (its per-replay p50); the
-    # persistent engine's p50 comes from device stamps, so nothing but the
-    # launch is issued inside its timed region (a first hipEventCreate + record
-    # there measured ~+30-40 us of host time in front of the kernel).
-    events = None if persistent else []
-    ev0 = None if persistent else torch.cuda.Event(enable_timing=True)
-    w.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    if ev0 is not None:
-        ev0.record()
-    runner.run(a.steps, events=events)
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    w.barrier()
-    elapsed = t1 - t0
-    elapsed_max = w.host_all_reduce(elapsed, "max")
-
-    if persistent:
-        # true per-step times: device stamps at every step start (100 MHz s_memrealtime)
-        per_step_ms = list(runner.step_times_ms(step0, step0 + a.steps))
-        p50_source = "per-step device timestamps (s_memrealtime at every step start)"
-    else:
-        # 3-launch path: average per step of each graph replay
-        per_step_ms = []
-        prev = ev0
-        for ev, g in events:
-            per_step_ms.append(prev.elapsed_time(ev) / g)
-            prev = ev
-        p50_source = "per-graph-replay average"
-    srt = sorted(per_step_ms)
-    p50 = statistics.median(srt) if srt else float("nan")
-    p90 = srt[min(len(srt) - 1, int(0.9 * len(srt)))] if srt else float("nan")
-    p50 = w.host_all_reduce(p50, "max")
-    p90 = w.host_all_reduce(p90, "max")
-    cold_timed = (runner.copy_only_launches - cold0) if persistent else 0
-
-    if not consistent(trainer, runner):
-        raise SystemExit("replicas diverged / IPC timeout during the timed run; result discarded")
+    # the timed run; if it fails the exchange / replica check, the next validated
+    # strategy is timed instead in this same process (then the chain's untried
+    # modes, each validated first) -- a scaling point is never lost to one bad run
+    res = None
+    while res is None:
+        if not picked:
+            if not remaining:
+                raise SystemExit(f"every exchange strategy failed (fallbacks: {fallbacks})")
+            mode = remaining.pop(0)
+            try:
+                trainer, runner = setup(mode)
+            except RuntimeError as e:
+                fallbacks[mode] = f"unavailable: {str(e)[:160]}"
+                continue
+            if not consistent(trainer, runner):
+                fallbacks[mode] = "failed validation (exchange timeout or replica drift after warmup)"
+                continue
+            picked.append((mode, trainer, runner))
+        mode, trainer, runner = picked.pop(0)
+        res = timed_run(mode, trainer, runner)
+        if res is None:
+            fallbacks[mode] = "failed the exchange / replica check in the timed run; re-timed with the next strategy"
+            print(f"bench: {mode} failed in the timed run; falling back", file=sys.stderr, flush=True)
+    persistent = isinstance(runner, PersistentMLPRunner)
+    elapsed_max, p50, p90, p50_source = res["elapsed_max"], res["p50"], res["p90"], res["p50_source"]
+    step0, cold_timed = res["step0"], res["cold_timed"]
     steps_done = trainer.global_step - step0
     m = trainer.read_metrics(trainer.global_step - 1, trainer.global_step)[0]
+    bad = 0.0 if all(math.isfinite(float(v)) for v in m) else 1.0
+    if w.world_size > 1:
+        bad = w.host_all_reduce(bad, "max")
+    if bad:
+        # a diverged run is not a measurement: no value is printed
+        print(json.dumps({"metric": METRIC, "error": "non-finite final loss / accuracy; result discarded",
+                          "final_loss": float(m[0])}), file=sys.stderr, flush=True)
+        raise SystemExit(3)
     n = w.world_size
     samples_per_s = n * a.batch * a.steps / elapsed_max
     if w.rank == 0:

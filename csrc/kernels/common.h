@@ -5,6 +5,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 namespace dtfk {
 
@@ -26,6 +27,29 @@ __device__ __forceinline__ f32x4 mfma16x16x32(bf16x8 a, bf16x8 b, f32x4 c) {
 // B[8*(l>>5)+j][l&31]; C/D[(r&3)+8*(r>>2)+4*(l>>5)][l&31] (r = 0..15).
 __device__ __forceinline__ f32x16 mfma32x32x16(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// Zero an [M, N] fp32 block of row stride ldc (the output of a split-K /
+// atomically accumulated product).  A kernel, not hipMemset2DAsync /
+// hipMemsetAsync: those memsets do not take effect when replayed from a
+// captured hipGraph on this stack (measured: a [256, 1] 2-D memset and a
+// 40-byte 1-D memset both left the previous replay's sums in place), so
+// Wide&Deep's graphed step accumulated its tower gradients across replays and
+// diverged (tests/test_graph_replay_gpu.py; DTF_ZERO_MEMSET2D=1 restores the
+// old path for that A/B).
+__global__ static __launch_bounds__(256) void zero2d_f32_kernel(float* __restrict__ C, int ldc, int M, int N) {
+  const long long n = (long long)M * N;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    C[(i / N) * ldc + i % N] = 0.f;
+}
+static inline hipError_t zero2d_f32(float* C, int ldc, int M, int N, hipStream_t s) {
+  const long long n = (long long)M * N;
+  if (n <= 0) return hipSuccess;
+  static const bool memset2d = getenv("DTF_ZERO_MEMSET2D") != nullptr;   // A/B probe of the old path
+  if (memset2d) return hipMemset2DAsync(C, (size_t)ldc * sizeof(float), 0, (size_t)N * sizeof(float), M, s);
+  const unsigned blocks = (unsigned)((n + 255) / 256 < 2048 ? (n + 255) / 256 : 2048);
+  hipLaunchKernelGGL(zero2d_f32_kernel, dim3(blocks), dim3(256), 0, s, C, ldc, M, N);
+  return hipGetLastError();
 }
 
 // fp32 -> bf16 bits, round-to-nearest-even (hardware cvt on gfx950).

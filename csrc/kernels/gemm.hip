@@ -401,7 +401,7 @@ extern "C" hipError_t dtfk_gemm(const void* A, int a_bf16, int lda, int transA, 
       const int kc = (K + gy - 1) / gy;
       gy = (K + kc - 1) / kc;
       if (beta == 0.f) {
-        const hipError_t e = hipMemset2DAsync(C, (size_t)ldc * sizeof(float), 0, sizeof(float), M, stream);
+        const hipError_t e = dtfk::zero2d_f32(Cf, ldc, M, 1, stream);
         if (e != hipSuccess) return e;
       }
       hipLaunchKernelGGL(gemv_cols_f32, dim3(bx, gy), dim3(256), 0, stream, Af, lda, Bf, ldbk, Cf, ldc, bias, M, K,
@@ -423,7 +423,7 @@ extern "C" hipError_t dtfk_gemm(const void* A, int a_bf16, int lda, int transA, 
     if (split <= 1) { split = 1; kchunk = K; }
   }
   if (split > 1 && beta == 0.f) {
-    const hipError_t e = hipMemset2DAsync(C, (size_t)ldc * sizeof(float), 0, (size_t)N * sizeof(float), M, stream);
+    const hipError_t e = dtfk::zero2d_f32(static_cast<float*>(C), ldc, M, N, stream);
     if (e != hipSuccess) return e;
   }
   const dim3 grid(tiles, split), block(256);

@@ -920,7 +920,7 @@ extern "C" hipError_t dtfk_gemm_big(const void* A, int lda, int transA, const vo
     return hipGetLastError();
   }
   if (split > 1 && beta == 0.f) {
-    const hipError_t e = hipMemset2DAsync(C, (size_t)ldc * sizeof(float), 0, (size_t)N * sizeof(float), M, stream);
+    const hipError_t e = dtfk::zero2d_f32(static_cast<float*>(C), ldc, M, N, stream);
     if (e != hipSuccess) return e;
   }
   // 192-wide tiles when 256-wide ones leave a wave of tiles partly empty

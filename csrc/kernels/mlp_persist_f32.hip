@@ -67,6 +67,7 @@
 #include "common.h"
 
 #include <cstdlib>
+#include <cstring>
 
 namespace dtfk {
 namespace mlpf {
@@ -185,6 +186,9 @@ struct Args {
                             // no / short / long s_sleep between passes (DTF_GATHER_MODE, tuning)
   int xmode;                // N GPUs: 0 one-shot (every workgroup reads its slot from every peer),
                             // 1 two-shot (reduce-scatter by wave chunk, then all-gather of the sums)
+  long long fault_step;     // fault injection (DTF_XCHG_FAULT=rank:step, tests of the bench's fallback):
+  int fault_rank;           // that rank stops publishing its exchange flag from that global step on, a dead
+                            // peer (-1: off; one skipped flag alone is absorbed: the flags are monotonic)
   int dbg;                  // profiling only (DTF_PERSIST_DBG): bit 0 = never stage the next step's x (wrong
                             // numerics; what the per-step LDS-DMA stage costs the hand-offs), bit 1 = head
                             // sub-phase stamps (slots 13-15, wave 0), bits 2 / 3 = stage (half) after the
@@ -1134,7 +1138,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
         lds_barrier();
         asm volatile("" ::: "memory");   // no peer-slot load hoisted above the flag match
       };
-      if (tid == 0)
+      if (tid == 0 && !(a.rank == a.fault_rank && gstep0 + st >= a.fault_step))
         __hip_atomic_store(reinterpret_cast<unsigned*>(flags + 64 * c), tag, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
       wait_peers(0);
@@ -1346,6 +1350,13 @@ hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int n
     a.gmode = gm ? atoi(gm) : 1;
     const char* db = getenv("DTF_PERSIST_DBG");
     a.dbg = db ? atoi(db) : 0;
+    a.fault_rank = -1;
+    a.fault_step = -1;
+    const char* fl = getenv("DTF_XCHG_FAULT");   // "rank:global_step"
+    if (fl != nullptr && strchr(fl, ':') != nullptr) {
+      a.fault_rank = atoi(fl);
+      a.fault_step = atoll(strchr(fl, ':') + 1);
+    }
   }
   constexpr size_t lds = LDS_BYTES;
   typedef void (*Kern)(Args);

@@ -692,7 +692,7 @@ hipError_t dtfk_col_sum(const float* X, float* out, int M, int N, hipStream_t s)
   const int rows_per_block = ((M + gy - 1) / gy + 15) / 16 * 16;
   gy = (M + rows_per_block - 1) / rows_per_block;
   if (gy > 1) {
-    const hipError_t e = hipMemsetAsync(out, 0, sizeof(float) * N, s);
+    const hipError_t e = dtfk::zero2d_f32(out, N, 1, N, s);   // a kernel: replays from hipGraphs (common.h)
     if (e != hipSuccess) return e;
   }
   if (vec)
@@ -777,7 +777,7 @@ hipError_t dtfk_multi_tensor_apply(const void* tab, const void* chunks, int nchu
 }
 hipError_t dtfk_multi_tensor_sumsq(const void* tab, const void* chunks, int nchunks, int gbf, float* out,
                                    hipStream_t s) {
-  (void)hipMemsetAsync(out, 0, sizeof(float), s);
+  (void)dtfk::zero2d_f32(out, 1, 1, 1, s);
   if (nchunks == 0) return hipSuccess;
   hipLaunchKernelGGL(multi_tensor_sumsq, dim3(nchunks), dim3(256), 0, s, (const TensorRec*)tab,
                      (const int2*)chunks, nchunks, gbf, out);

@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -31,6 +32,20 @@ def _exchange_stats(m):
     wr = r.wire_ratio()
     return {"peer_capacity": r.peer_cap, "checks": r.checks, "resizes": r.resizes, "voided_steps": r.voided,
             "wire_ids_over_exact": None if wr is None else round(wr, 3)}
+
+
+def refuse_diverged(w, loss, metric):
+    """A run whose final loss is not finite is not a measurement: no value line,
+    non-zero exit (collective: every rank exits alike)."""
+    bad = 0.0 if math.isfinite(float(loss)) else 1.0
+    if w.world_size > 1:
+        bad = w.host_all_reduce(bad, "max")
+    if bad:
+        if w.rank == 0:
+            print(json.dumps({"metric": metric, "error": "non-finite final loss; result discarded",
+                              "final_loss": float(loss)}), file=sys.stderr, flush=True)
+        w.shutdown()
+        raise SystemExit(3)
 
 
 def synthetic_sparse_batches(n_batches, batch, num_features, nnz, seed, device):
@@ -135,6 +150,7 @@ def main():
     w.barrier()
     dt = w.host_all_reduce(time.time() - t0, "max")
     sps = a.batch * w.world_size * a.steps / dt
+    refuse_diverged(w, loss, f"{a.model} samples/sec (whole node)")
     if w.rank == 0:
         print(json.dumps({"metric": f"{a.model} samples/sec (whole node)", "value": round(sps, 1),
                           "unit": "samples/s", "n_gpus": w.world_size, "steps": a.steps, "warmup": a.warmup,
@@ -210,6 +226,7 @@ def dense_bench(a, w):
     w.barrier()
     dt = w.host_all_reduce(time.time() - t0, "max")
     v = per * w.world_size * a.steps / dt
+    refuse_diverged(w, loss, f"{a.model} {unit} (whole node)")
     sweep = {}
     for mb in [float(x) for x in a.bucket_sweep.split(",") if x.strip()]:
         ddp.close()

@@ -294,3 +294,36 @@ def test_bench_two_ranks_same_gpu_short_run(native):
     assert res["n_gpus"] == 2 and res["steps"] == 20 and res["warmup"] == 5
     assert res["value"] > 0 and res["ms_per_step"] > 0 and res["dtype"] == "fp32"
     assert res["config"]["parallelism"] == "dp2"
+
+
+def test_bench_two_ranks_timed_run_fault_falls_back(native):
+    """A failure inside the timed run does not lose the scaling point: rank 1
+    stops publishing its exchange flag from timed step 5 on (a dead peer) (DTF_BENCH_FAULT -> the kernel's
+    DTF_XCHG_FAULT), its peer times out, the replica check fails, and bench.py
+    re-times the next validated strategy in the same process and prints one
+    contract line naming the failed mode under `fallbacks`."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(repo, "bench.py"), "--gpus", "2",
+           "--steps", "20", "--warmup", "5", "--tune-steps", "40", "--exchange-timeout", "2"]
+    env = dict(os.environ, PYTHONPATH=repo, OMP_NUM_THREADS="2", DTF_BENCH_SAME_GPU="1", DTF_BENCH_FAULT="5")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=env, cwd=repo)
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert r.returncode == 0 and len(lines) == 1, (r.stdout + r.stderr)[-3000:]
+    res = json.loads(lines[0])
+    fb = res["config"]["fallbacks"] or {}
+    failed = [m for m, why in fb.items() if "timed run" in why]
+    assert len(failed) == 1, (fb, r.stderr[-4000:])
+    assert res["config"]["exchange_mode"] != failed[0]
+    assert res["value"] > 0 and res["steps"] == 20 and res["n_gpus"] == 2
+    assert res["global_steps_timed"] == 20

@@ -22,6 +22,19 @@ accuracy of the run (pre-update, as TF evaluates them in the same run) are
 seeded into the run's memo, so summaries / cost fetches of the same run cost
 no extra kernels.
 
+and lr2.py's sparse logistic regression (lr2.py:359-396) over a partitioned
+(ps-placed, row-sharded) W:
+
+    py_x = Add(EmbeddingLookupSparse(W, SparseTensor(idx, fids), SparseTensor(idx, fvals), 'sum'), b)
+    loss = Mean(SigmoidCrossEntropyWithLogits(py_x, y))
+    train_op = GradientDescentOptimizer(lr).minimize(loss, global_step)
+
+whose train run becomes the native sparse-LR step (models/sparse_lr.py on the
+variables' own storage): the feeds are packed into one pinned buffer and
+copied once, the COO indices become CSR offsets on the host, and on one GPU
+the step -- device-resident dedup, bag, sigmoid-xent, bag backward, scatter
+SGD, bias update -- replays from a hipGraph per (batch, padded id count).
+
 A run is lowered only if nothing else it fetches reads the matched
 variables or interior nodes (those would see post-update weights); anything
 unmatched -- other shapes, CPU tensors, other fetch sets -- runs eagerly as
@@ -151,22 +164,13 @@ def _match_accuracy(g, pat) -> Optional[Tensor]:
     return None
 
 
-class MLPStepPlan:
-    """Fused execution of one matched train op."""
+class _PlanBase:
+    """fetches_ok: a lowered run is allowed only when no fetched node reads a
+    matched variable or interior node (those would see post-update values)."""
+    seeded: set
+    blocked: set
+    _fetch_ok: Dict[tuple, bool]
 
-    def __init__(self, op: Operation, pat: MLPPattern, graph):
-        info = op._lowering
-        self.op, self.pat, self.info = op, pat, info
-        self.accuracy = _match_accuracy(graph, pat)
-        order = {id(v): i for i, v in enumerate(info["vars"])}
-        self.var_index = [order[id(v)] for v in (pat.W1, pat.b1, pat.W2, pat.b2)]
-        self.seeded = {id(pat.loss), id(op)} | ({id(self.accuracy)} if self.accuracy is not None else set())
-        self.blocked = {id(t) for t in pat.interior} | {id(v) for v in (pat.W1, pat.b1, pat.W2, pat.b2)}
-        self._fetch_ok: Dict[tuple, bool] = {}
-        self.a2buf = self.dz2buf = self.metrics = None
-        self.steps = 0
-
-    # -------------------------------------------------------------- checks
     def fetches_ok(self, fetch_list) -> bool:
         key = tuple(id(f) for f in fetch_list)
         ok = self._fetch_ok.get(key)
@@ -185,6 +189,22 @@ class MLPStepPlan:
                 stack.extend(i for i in getattr(t, "inputs", ()) if isinstance(i, Tensor))
             self._fetch_ok[key] = ok
         return ok
+
+
+class MLPStepPlan(_PlanBase):
+    """Fused execution of one matched train op."""
+
+    def __init__(self, op: Operation, pat: MLPPattern, graph):
+        info = op._lowering
+        self.op, self.pat, self.info = op, pat, info
+        self.accuracy = _match_accuracy(graph, pat)
+        order = {id(v): i for i, v in enumerate(info["vars"])}
+        self.var_index = [order[id(v)] for v in (pat.W1, pat.b1, pat.W2, pat.b2)]
+        self.seeded = {id(pat.loss), id(op)} | ({id(self.accuracy)} if self.accuracy is not None else set())
+        self.blocked = {id(t) for t in pat.interior} | {id(v) for v in (pat.W1, pat.b1, pat.W2, pat.b2)}
+        self._fetch_ok: Dict[tuple, bool] = {}
+        self.a2buf = self.dz2buf = self.metrics = None
+        self.steps = 0
 
     # -------------------------------------------------------------- feeds
     @staticmethod
@@ -428,6 +448,170 @@ class MLPStepPlan:
             self._fetch_ok[key] = r
         return r
 
+class SparseLRPattern:
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+def _placeholder(t) -> bool:
+    return getattr(t, "op_type", None) == "Placeholder"
+
+
+def match_sparse_lr(loss) -> Optional[SparseLRPattern]:
+    """lr2.py:383-391 -- mean sigmoid xent of (sum-combined sparse lookup of a
+    partitioned [F, 1] W) + b, every input a placeholder."""
+    if not _is(loss, "Mean") or loss.attrs.get("axis") is not None or not loss.inputs:
+        return None
+    xent = loss.inputs[0]
+    if not _is(xent, "SigmoidCrossEntropyWithLogits") or len(xent.inputs) != 2:
+        return None
+    logits, y = xent.inputs
+    if not _is(logits, "Add", "AddV2", "BiasAdd") or len(logits.inputs) != 2:
+        return None
+    e, b = logits.inputs
+    if not _is(e, "EmbeddingLookupSparse"):
+        e, b = b, e
+    if not _is(e, "EmbeddingLookupSparse") or e.attrs.get("combiner") != "sum" or len(e.inputs) != 2:
+        return None
+    W = getattr(e, "params", None)
+    if not (getattr(W, "is_partitioned", False) and getattr(W, "dim", 0) == 1):
+        return None
+    if not (_is_plain_var(b) and b.value.numel() == 1 and b.value.dtype == torch.float32):
+        return None
+    sp_ids, sp_w = e.inputs
+    if sp_w is None or getattr(sp_ids, "indices", None) is None or getattr(sp_w, "indices", None) is not sp_ids.indices:
+        return None
+    idx, fids, fvals = sp_ids.indices, sp_ids.values, sp_w.values
+    if not all(_placeholder(t) for t in (idx, fids, fvals, y)):
+        return None
+    return SparseLRPattern(loss=loss, W=W, b=b, y=y, idx=idx, fids=fids, fvals=fvals,
+                           interior=[loss, xent, logits, e, sp_ids, sp_w])
+
+
+class SparseLRStepPlan(_PlanBase):
+    """lr2.py's train run on the native sparse-LR step over the graph's own
+    variables (W's shards, b's tensor): same synchronous semantics as the
+    op-by-op path (sum of the per-worker mean gradients / W, owner-side scatter
+    SGD), one host-to-device copy of the packed feeds, and on one GPU a
+    hipGraph replay per (batch rows, padded id count)."""
+
+    ID_BUCKET = 4096       # ids padded to a multiple of this (a handful of captured shapes)
+
+    def __init__(self, op: Operation, pat: SparseLRPattern):
+        self.op, self.pat, self.info = op, pat, op._lowering
+        self.seeded = {id(pat.loss), id(op)}
+        self.blocked = {id(t) for t in pat.interior} | {id(pat.W), id(pat.b)}
+        self._fetch_ok = {}
+        self.trainer = None
+        self._stage = None
+        self.steps = 0
+
+    @staticmethod
+    def _feed(ctx, ph):
+        for key in (ph, ph.name, ph.name[:-2]):
+            try:
+                if key in ctx.feeds:
+                    return ctx.feeds[key]
+            except TypeError:
+                continue
+        return None
+
+    def _batch(self, ctx, dev):
+        """(labels [B,1], offsets [B+1], ids, vals) on `dev` from the feeds, or
+        None (then the run goes op by op)."""
+        p = self.pat
+        fy, fi, ff, fv = (self._feed(ctx, t) for t in (p.y, p.idx, p.fids, p.fvals))
+        if any(v is None or isinstance(v, torch.Tensor) for v in (fy, fi, ff, fv)):
+            return None
+        y = np.asarray(fy, dtype=np.float32)
+        idx = np.asarray(fi)
+        ids = np.asarray(ff).astype(np.int64, copy=False).reshape(-1)
+        vals = np.asarray(fv, dtype=np.float32).reshape(-1)
+        B = y.shape[0] if y.ndim else 0
+        nnz = ids.size
+        if B == 0 or y.size != B or vals.size != nnz or (nnz and (idx.ndim != 2 or idx.shape[0] != nnz)):
+            return None
+        rows = idx[:, 0] if nnz else np.zeros(0, np.int64)
+        if nnz and (rows.min() < 0 or rows.max() >= B or (rows[1:] < rows[:-1]).any()):
+            return None            # not in canonical row order: op by op
+        offsets = np.zeros(B + 1, np.int64)
+        if nnz:
+            np.cumsum(np.bincount(rows, minlength=B), out=offsets[1:])
+        pad = 0
+        if dev.type == "cuda" and self.trainer is not None and self.trainer.world.world_size == 1 and nnz:
+            pad = -(-nnz // self.ID_BUCKET) * self.ID_BUCKET - nnz
+        n = nnz + pad
+        if dev.type != "cuda":
+            to = lambda a: torch.from_numpy(np.ascontiguousarray(a))
+            lab, off, i, v = to(y.reshape(B, 1)), to(offsets), to(ids), to(vals)
+        else:
+            # one pinned staging buffer -> one copy: [ids i64 | offsets i64 | vals f32 | labels f32]
+            sizes = [8 * n, 8 * (B + 1), 4 * n, 4 * B]
+            offs = np.cumsum([0] + [-(-s // 16) * 16 for s in sizes])
+            total = int(offs[-1])
+            if self._stage is None or self._stage[0].numel() < total:
+                cap = max(total, 1 << 20)
+                self._stage = [torch.empty(cap, dtype=torch.uint8, pin_memory=True),
+                               torch.empty(cap, dtype=torch.uint8, device=dev), None]
+            host, devb, ev = self._stage
+            if ev is not None:
+                ev.synchronize()                   # the previous copy out of the staging buffer is done
+            hb = host.numpy()
+            hv = [hb[offs[k]:offs[k] + sizes[k]] for k in range(4)]
+            hi = hv[0].view(np.int64)
+            hi[:nnz] = ids
+            hi[nnz:] = ids[0] if nnz else 0        # padding repeats the first id with weight 0 (last bag)
+            hv[1].view(np.int64)[:] = offsets
+            if pad:
+                hv[1].view(np.int64)[-1] = n
+            hf = hv[2].view(np.float32)
+            hf[:nnz] = vals
+            hf[nnz:] = 0.0
+            hv[3].view(np.float32)[:] = y.reshape(-1)
+            devb[:total].copy_(host[:total], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._stage[2] = ev
+            dv = [devb[int(offs[k]):int(offs[k]) + sizes[k]] for k in range(4)]
+            i, off = dv[0].view(torch.int64), dv[1].view(torch.int64)
+            v, lab = dv[2].view(torch.float32), dv[3].view(torch.float32).view(B, 1)
+        return lab, off, i, v
+
+    def run(self, ctx, flat) -> bool:
+        from ..models.sparse_lr import SparseLRTrainer
+        from ..utils import debug as _debug
+        from .train import GradientDescentOptimizer, _world_or_local
+
+        p, info = self.pat, self.info
+        opt, gs_var = info["opt"], info["global_step"]
+        w = _world_or_local()
+        if type(opt) is not GradientDescentOptimizer or (w.world_size > 1 and not opt.sync_replicas):
+            return False
+        table = p.W.table
+        if table.hogwild is not None:
+            return False
+        dev = table.device
+        if self.trainer is None:
+            self.trainer = SparseLRTrainer(table.num_rows, float(opt._lr_value()), w, device=dev, table=table,
+                                           bias=p.b.value)
+            if dev.type == "cuda" and w.world_size == 1:
+                self.trainer.enable_graph()        # one worker: no collectives, lazy per-shape captures
+        batch = self._batch(ctx, dev)
+        if batch is None:
+            return False
+        opt._steps += 1
+        _debug.fault_point(opt._steps, w.rank)
+        self.trainer.lr = float(opt._lr_value())
+        loss = self.trainer.train_step(batch)
+        if gs_var is not None:
+            with torch.no_grad():
+                gs_var.value.data += 1
+        ctx.memo[id(p.loss)] = loss.clone()        # pre-update loss of this run (a graph's output is reused)
+        ctx.memo[id(self.op)] = None
+        self.steps += 1
+        return True
+
+
 def _flatten(f, out: List[Any]):
     if isinstance(f, (list, tuple)):
         for x in f:
@@ -450,11 +634,17 @@ def try_lower(session, fetches, ctx) -> None:
             continue
         plan = _CACHE.get(f)
         if plan is None:
-            pat = match_mlp(getattr(f, "loss", None)) if getattr(f, "loss", None) is not None else None
+            loss = getattr(f, "loss", None)
+            pat = match_mlp(loss) if loss is not None else None
             plan = False
             if pat is not None and {id(v) for v in f._lowering["vars"]} == \
                     {id(v) for v in (pat.W1, pat.b1, pat.W2, pat.b2)}:
                 plan = MLPStepPlan(f, pat, session.graph)
+            elif loss is not None:
+                sp = match_sparse_lr(loss)
+                if sp is not None and [id(v) for v in f._lowering["vars"]] == [id(sp.b)] and \
+                        [id(pv) for _, pv in f._lowering["sparse"]] == [id(sp.W)]:
+                    plan = SparseLRStepPlan(f, sp)
             _CACHE[f] = plan
         if plan is False or id(f) in ctx.memo:
             continue
@@ -462,6 +652,6 @@ def try_lower(session, fetches, ctx) -> None:
             plan.run(ctx, flat)
 
 
-def plan_for(train_op) -> Optional[MLPStepPlan]:
+def plan_for(train_op) -> Optional[_PlanBase]:
     p = _CACHE.get(train_op)
     return p if p else None

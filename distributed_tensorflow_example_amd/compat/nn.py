@@ -95,9 +95,10 @@ def embedding_lookup_sparse(params, sp_ids, sp_weights, combiner="mean", name="e
     if _partitioned(params):
         from .partitioned import lookup_sparse
 
-        t = Tensor(None, [sp_ids, sp_weights], name)
+        t = Tensor(None, [sp_ids, sp_weights], name, op_type="EmbeddingLookupSparse", attrs={"combiner": combiner})
         t._eval = lambda ctx: lookup_sparse(ctx, params, ctx.eval(sp_ids),
                                             ctx.eval(sp_weights) if sp_weights is not None else None, combiner)
+        t.params = params              # (compat/lowering.py matches lr2.py's graph through it)
         return t
 
     def f(w, ids_sp, wts_sp):
@@ -105,7 +106,9 @@ def embedding_lookup_sparse(params, sp_ids, sp_weights, combiner="mean", name="e
         out = _ops.embedding_bag(w, ids.to(w.device), offsets.to(w.device),
                                  None if vals is None else vals.to(w.device).float(), combiner)
         return out
-    return Tensor(f, [params, sp_ids, sp_weights], name)
+    t = Tensor(f, [params, sp_ids, sp_weights], name, op_type="EmbeddingLookupSparse", attrs={"combiner": combiner})
+    t.params = params
+    return t
 
 
 def l2_loss(t, name="L2Loss"):

@@ -87,8 +87,7 @@ class Session:
         ctx = RunContext(feed_dict or {}, self.graph.device)
         ctx.session = self
         ctx.options = options
-        if ctx.device.type == "cuda":
-            _lowering.try_lower(self, fetches, ctx)     # fused kernels for matched train ops
+        _lowering.try_lower(self, fetches, ctx)         # fused steps for matched train ops
         for hook in _pre_run_hooks(fetches):           # async train ops: pull the ps variables first
             hook()
         out = self._run(fetches, ctx)

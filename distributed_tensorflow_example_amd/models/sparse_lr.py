@@ -32,16 +32,30 @@ class SparseLRTrainer(StaticStepMixin):
     def __init__(self, num_features: int, lr: float, world: Optional[World] = None, seed: int = 1,
                  init_std: float = 1.0, device=None, auc_bins: int = 200, ids_capacity: Optional[int] = None,
                  rows: int = 500, peer_capacity: Optional[int] = None, update_mode: Optional[str] = None,
-                 use_locking: bool = False):
+                 use_locking: bool = False, table: Optional[ShardedEmbedding] = None,
+                 bias: Optional[torch.Tensor] = None):
+        """`table` / `bias`: train existing storage in place instead of creating
+        it (the compat Session's lowered lr2 graph: a PartitionedVariable's
+        shards and the `bias/Variable` tensor, compat/lowering.py)."""
         self.world = world or get_world()
         self.device = torch.device(device) if device is not None else self.world.device
         self.lr = float(lr)
-        self.W = ShardedEmbedding(num_features, 1, self.world, init_std=init_std, seed=seed, device=self.device,
-                                  name="weights/Variable", capacity=ids_capacity, peer_capacity=peer_capacity)
+        if table is not None:
+            if table.dim != 1 or table.num_rows != num_features:
+                raise ValueError("table must be [num_features, 1]")
+            self.W = table
+        else:
+            self.W = ShardedEmbedding(num_features, 1, self.world, init_std=init_std, seed=seed, device=self.device,
+                                      name="weights/Variable", capacity=ids_capacity, peer_capacity=peer_capacity)
         self.rows = int(rows)              # batch rows of the captured step (lr2: batch_size)
         self._window = []                  # static steps since the router's last check (replay source)
         self._example = None
-        self.b = torch.zeros(1, dtype=torch.float32, device=self.device, requires_grad=True)
+        if bias is not None:
+            if bias.numel() != 1 or bias.dtype != torch.float32:
+                raise ValueError("bias must be one fp32 value")
+            self.b = bias if bias.requires_grad else bias.requires_grad_(True)
+        else:
+            self.b = torch.zeros(1, dtype=torch.float32, device=self.device, requires_grad=True)
         self.global_step = 0
         self._graphed = None
         # streaming_auc's num_thresholds = auc_bins -> auc_bins + 1 histogram bins

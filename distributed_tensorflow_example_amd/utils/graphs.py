@@ -9,13 +9,26 @@ input shape signature (warmup iterations on a side stream first, as capture
 requires), then each call copies the new inputs into the static buffers and
 replays the graph.  The warmup iterations really run the step, so the state
 they mutate is snapshotted before and restored after: capturing changes no
-numbers.
+numbers.  One rank keeps up to `max_graphs` signatures (e.g. the compat
+Session's lr2 step: a full batch and the epoch's last, shorter one, each at a
+few padded id capacities); the least recently used one is dropped beyond that.
+
+A replay returns the graph's static output tensor: it is overwritten by the
+next replay (copy it to keep it).
 """
 from __future__ import annotations
 
+from collections import OrderedDict
 from typing import Callable, List, Sequence
 
 import torch
+
+
+class _Captured:
+    __slots__ = ("graph", "static_in", "out")
+
+    def __init__(self, graph, static_in, out):
+        self.graph, self.static_in, self.out = graph, static_in, out
 
 
 class GraphedStep:
@@ -26,15 +39,13 @@ class GraphedStep:
     capturing again on one rank alone."""
 
     def __init__(self, step_fn: Callable, state: Callable[[], Sequence[torch.Tensor]], warmup: int = 2,
-                 strict: bool = False):
+                 strict: bool = False, max_graphs: int = 8):
         self.step_fn = step_fn
         self.state = state            # -> the tensors the step mutates (snapshotted around warmup)
         self.warmup = warmup
         self.strict = strict
-        self.key = None
-        self.graph = None
-        self.static_in: List[torch.Tensor] = []
-        self.out = None
+        self.max_graphs = 1 if strict else max(1, int(max_graphs))
+        self._graphs: "OrderedDict[tuple, _Captured]" = OrderedDict()
         self.captures = 0
         self.replays = 0
 
@@ -42,44 +53,67 @@ class GraphedStep:
     def _sig(inputs):
         return tuple((tuple(t.shape), t.dtype, t.device) for t in inputs)
 
+    # the most recent capture (tests and callers that hold one signature)
+    @property
+    def key(self):
+        return next(reversed(self._graphs)) if self._graphs else None
+
+    @property
+    def graph(self):
+        return self._graphs[self.key].graph if self._graphs else None
+
+    @property
+    def out(self):
+        return self._graphs[self.key].out if self._graphs else None
+
     def _capture(self, inputs):
-        self.graph = None
-        self.static_in = [t.detach().clone() for t in inputs]
+        sig = self._sig(inputs)
+        self._graphs.pop(sig, None)
+        static_in = [t.detach().clone() for t in inputs]
         saved = [t.detach().clone() for t in self.state()]
         cur = torch.cuda.current_stream()
         side = torch.cuda.Stream()
         side.wait_stream(cur)
         with torch.cuda.stream(side):
             for _ in range(self.warmup):
-                self.step_fn(*self.static_in)
+                self.step_fn(*static_in)
         cur.wait_stream(side)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self.out = self.step_fn(*self.static_in)
+            out = self.step_fn(*static_in)
         with torch.no_grad():
             for t, s in zip(self.state(), saved):
                 t.copy_(s)
-        self.graph = g
-        self.key = self._sig(inputs)
+        del saved
+        self._graphs[sig] = _Captured(g, static_in, out)
+        while len(self._graphs) > self.max_graphs:
+            self._graphs.popitem(last=False)
         self.captures += 1
 
     def capture(self, *inputs):
         """(Re)capture now with `inputs` as the example (state is restored after)."""
+        if self.strict:
+            self._graphs.clear()
         self._capture(inputs)
 
     def matches(self, *inputs) -> bool:
-        return self.graph is not None and self._sig(inputs) == self.key
+        return self._sig(inputs) in self._graphs
 
     def __call__(self, *inputs):
-        if self.graph is None or self._sig(inputs) != self.key:
+        sig = self._sig(inputs)
+        c = self._graphs.get(sig)
+        if c is None:
             if self.strict:
                 raise RuntimeError("captured multi-rank step called with other input shapes "
-                                   f"({self._sig(inputs)} vs {self.key}): pad inputs to the static capacity; a "
+                                   f"({sig} vs {self.key}): pad inputs to the static capacity; a "
                                    "re-capture must be collective (capture() on every rank)")
             self._capture(inputs)
+            c = self._graphs[sig]
+        else:
+            self._graphs.move_to_end(sig)
         with torch.no_grad():
-            for s, t in zip(self.static_in, inputs):
+            for s, t in zip(c.static_in, inputs):
                 s.copy_(t, non_blocking=True)
-        self.graph.replay()
+        c.graph.replay()
         self.replays += 1
-        return self.out
+        return c.out

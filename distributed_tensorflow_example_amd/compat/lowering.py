@@ -637,9 +637,9 @@ def try_lower(session, fetches, ctx) -> None:
             loss = getattr(f, "loss", None)
             pat = match_mlp(loss) if loss is not None else None
             plan = False
-            if pat is not None and {id(v) for v in f._lowering["vars"]} == \
+            if pat is not None and pat.W1.value.is_cuda and {id(v) for v in f._lowering["vars"]} == \
                     {id(v) for v in (pat.W1, pat.b1, pat.W2, pat.b2)}:
-                plan = MLPStepPlan(f, pat, session.graph)
+                plan = MLPStepPlan(f, pat, session.graph)     # (GPU kernels: CPU sessions run it op by op)
             elif loss is not None:
                 sp = match_sparse_lr(loss)
                 if sp is not None and [id(v) for v in f._lowering["vars"]] == [id(sp.b)] and \

@@ -8,8 +8,8 @@ lr 0.0005, sigmoid hidden layer, softmax cross-entropy, plain SGD.
 Default engine: the persistent fp32 kernel (csrc/kernels/mlp_persist_f32.hip)
 -- the reference's precision (example.py:77-118 is fp32 end to end): the two
 big GEMMs as exact 3-way bf16 splits of their fp32 operands (every product
-exact, fp32 accumulate), the head on f32-input MFMA, fp32 master weights.  `--precision fp16`
-selects the f16-MFMA persistent kernel (labelled as such in the output line).
+exact, fp32 accumulate), the head on f32-input MFMA, fp32 master weights.  `--precision fp32-mfma`
+runs every product on f32-input MFMA instead.
 N GPUs: gradients exchanged inside the persistent launch over IPC-mapped xGMI
 peer buffers (bf16 payload per BASELINE config #2, `--grad-dtype fp32` for
 fp32), falling back to 3 fused launches per step with an IPC or RCCL
@@ -62,11 +62,10 @@ def main(argv=None):
     ap.add_argument("--batch", type=int, default=100, help="per-GPU batch (reference: 100)")
     ap.add_argument("--lr", type=float, default=0.0005)
     ap.add_argument("--steps-per-graph", type=int, default=50, help="3-launch path: steps per captured hipGraph")
-    ap.add_argument("--precision", choices=["fp32", "fp32-mfma", "fp32-split7", "fp16"], default="fp32",
+    ap.add_argument("--precision", choices=["fp32", "fp32-mfma"], default="fp32",
                     help="persistent engine (reference precision: fp32): fp32 = the 28-workgroup engine with the "
                          "big GEMMs as exact 3-way bf16 splits of their fp32 operands (exact products, fp32 "
-                         "accumulate); fp32-mfma = every product on f32-input MFMA; fp32-split7 = the 7-workgroup "
-                         "split engine; fp16 = f16 MFMA operands (not the reference's precision)")
+                         "accumulate); fp32-mfma = every product on f32-input MFMA")
     ap.add_argument("--exchange-timeout", type=float, default=30.0,
                     help="in-kernel exchange wait bound (s); a cold multi-GPU start can skew ranks by seconds")
     ap.add_argument("--steps-per-launch", type=int, default=550,
@@ -175,7 +174,7 @@ def main(argv=None):
                  "ipc-apply": ["ipc-apply"], "rccl": ["rccl"]}[a.allreduce]
         if can_persist and a.allreduce == "auto":
             # both in-kernel exchanges are timed (the fabric decides which wins)
-            chain = ["persistent"] + (["persistent-2shot"] if a.precision in ("fp32", "fp32-mfma") else []) + chain
+            chain = ["persistent", "persistent-2shot"] + chain
     # N > 1: the first two valid candidates are timed briefly (outside the timed
     # region) and the faster one is kept -- the in-kernel exchange's per-CU peer
     # reads vs the 3-launch path's exchange spread over 347 workgroups depends on
@@ -336,7 +335,7 @@ def main(argv=None):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": (("fp32" if a.precision.startswith("fp32") else a.precision) if persistent else "bf16"),
+            "dtype": "fp32" if persistent else "bf16",
             "data": ("synthetic MNIST-shaped uint8 resident in pinned host memory, streamed per chunk over PCIe "
                      + ("by copier workgroups inside the persistent launch" if persistent else
                         "by hipMemcpyAsync inside the chunk's hipGraph") + "; random-init weights"),
@@ -360,17 +359,12 @@ def main(argv=None):
                 "input_prefetch": "in-kernel copier workgroups" if persistent else a.prefetch,
                 "activation": a.act,
                 "exchange_tuning_us_per_step": tuned or None,
-                "precision": ({"fp32-split7": "7-workgroup engine: fp32 GEMMs as exact 3-way bf16 splits (hi+mid+lo == each fp32 "
-                                             "weight / gradient, uint8 pixels exact): exact products, fp32 "
-                                             "accumulate; head on v_mfma_f32_16x16x4_f32; fp32 master weights",
-                               "fp32": "fp32 GEMMs as exact 3-way bf16 splits on the 28-workgroup engine "
+                "precision": ({"fp32": "fp32 GEMMs as exact 3-way bf16 splits on the 28-workgroup engine "
                                            "(hi+mid+lo == each fp32 weight / gradient, uint8 pixels exact): exact "
                                            "products, fp32 accumulate; head on v_mfma_f32_16x16x4_f32; fp32 master "
                                            "weights",
                                "fp32-mfma": "fp32 MFMA operands (v_mfma_f32_16x16x4_f32, exact f32 products), "
-                                       "fp32 accumulate, fp32 master weights",
-                               "fp16": "fp16 MFMA operands (pixels exact as 1024+u), fp32 accumulate, fp32 master "
-                                       "weights"}[a.precision]
+                                       "fp32 accumulate, fp32 master weights"}[a.precision]
                               if persistent else "bf16 MFMA operands, fp32 accumulate, fp32 master weights"),
             },
             "native_src_hash": _native.src_hash(),

@@ -32,17 +32,6 @@ hipError_t dtfk_mlp_ipc_reduce_apply(float* params, void* const* peer_table, int
                                      long long slot_bytes, const long long* gstep, const float* lr, float scale,
                                      void* W1T, void* W2T, void* W2N, int* err, long long timeout_ticks,
                                      hipStream_t stream);
-int dtfk_mlp_persist_gran_count();
-int dtfk_mlp_persist_xt_bytes();
-int dtfk_mlp_persist_max_batch();
-int dtfk_mlp_persist_stage_rec(int B);
-int dtfk_mlp_persist_ipc_bytes();
-hipError_t dtfk_mlp_persist(const void* xs, const void* xts, long long rec, long long rec_h, int B, int nsteps, float* params,
-                            const float* lr, float* metrics, int ring, int act, int naive, long long* gstep,
-                            unsigned long long* seq, unsigned long long* gran, int* err, long long timeout,
-                            const void* host_next, int next_steps, void* xs_next, void* xts_next,
-                            long long* ts, void* const* peer_base, int W, int rank, long long* step_ts,
-                            int ts_ring, hipStream_t stream);
 long long dtfk_mlpf_stage_rec();
 long long dtfk_mlpf_xbuf_bytes();
 long long dtfk_mlpf_ipc_bytes();
@@ -60,14 +49,6 @@ hipError_t dtfk_graph_mlp_step(const float* x, const float* ylab, float* W1, flo
                                float* gb2, float* metrics, float* host_metrics, void* gstep, int gstep_kind,
                                const float* lr_ptr, int B, int K, int H, int C, int act, int naive, int sgd,
                                hipStream_t stream);
-long long dtfk_mlpx_stage_rec();
-long long dtfk_mlpx_xbuf_bytes();
-long long dtfk_mlpx_ipc_bytes();
-hipError_t dtfk_mlp_persist_x3(const void* stage, long long rec_h, int B, int nsteps, float* params, const float* lr,
-                               float* metrics, int ring, int act, int naive, long long* gstep, unsigned long long* seq,
-                               void* xbuf, int* err, long long timeout, long long* step_ts, int ts_ring,
-                               const void* host_next, int next_steps, void* stage_next, void* const* peer_base, int W,
-                               int rank, int gbf16, long long* phase_ts, int spread, int xmode, hipStream_t stream);
 hipError_t dtfk_mlp_fwd_head(const void* x, int x_kind, int B, const void* W1T, float* z2p, const void* labels,
                              const void* W2T, const void* W2N, const float* params, void* dz2T, int BP,
                              float* partials, float inv_batch, int act, int naive_loss, int* counters,
@@ -301,74 +282,8 @@ void memcpy_h2d_async(at::Tensor dst, int64_t dst_offset, at::Tensor src, int64_
             "hipMemcpyAsync");
 }
 
-// Persistent weight-stationary MLP launch (csrc/kernels/mlp_persist.hip):
-// runs `nsteps` SGD steps of the chunk staged in (xs, xts) and, in the same
-// launch, copies `next_steps` records starting at byte `host_off` of the
-// pinned host epoch into (xs_next, xts_next).  nsteps = 0: copy only.
-void mlp_persist(at::Tensor xs, at::Tensor xts, int64_t rec, int B, int nsteps, at::Tensor params, at::Tensor lr,
-                 at::Tensor metrics, at::Tensor gstep, at::Tensor seq, at::Tensor gran, at::Tensor err,
-                 double timeout_s, int act, int naive, c10::optional<at::Tensor> host, int64_t host_off,
-                 int next_steps, c10::optional<at::Tensor> xs_next, c10::optional<at::Tensor> xts_next,
-                 c10::optional<at::Tensor> ts, int64_t ipc_table, int ipc_W, int ipc_rank,
-                 c10::optional<at::Tensor> step_ts) {
-  if (ipc_W > 1 && (ipc_table == 0 || ipc_rank < 0 || ipc_rank >= ipc_W))
-    throw std::runtime_error("mlp_persist: N-GPU exchange needs the IPC peer table");
-  if (B <= 0 || B > dtfk_mlp_persist_max_batch()) throw std::runtime_error("mlp_persist: B out of range");
-  if (rec < (int64_t)B * 785 || rec % 16 != 0) throw std::runtime_error("mlp_persist: bad record size");
-  const int64_t rec_h = rec;                        // host record (pinned epoch)
-  const int64_t rec_s = dtfk_mlp_persist_stage_rec(B);   // device stage record (permuted rows)
-  const int64_t xtb = dtfk_mlp_persist_xt_bytes();
-  need(xs, at::kByte, (int64_t)std::max(nsteps, 1) * rec_s, "xs");
-  need(xts, at::kByte, (int64_t)std::max(nsteps, 1) * xtb, "xts");
-  need(params, at::kFloat, kNParam, "params");
-  need(lr, at::kFloat, 1, "lr");
-  need(metrics, at::kFloat, 2, "metrics");
-  need(gstep, at::kLong, 1, "gstep");
-  need(seq, at::kLong, 1, "seq");
-  need(gran, at::kLong, dtfk_mlp_persist_gran_count(), "gran");
-  need(err, at::kInt, 1, "err");
-  if (((uintptr_t)xs.data_ptr() | (uintptr_t)xts.data_ptr()) % 16 != 0)
-    throw std::runtime_error("mlp_persist: stage buffers must be 16-byte aligned");
-  const void* hn = nullptr;
-  void* xn = nullptr;
-  void* xtn = nullptr;
-  if (next_steps > 0) {
-    if (!host.has_value() || !xs_next.has_value() || !xts_next.has_value())
-      throw std::runtime_error("mlp_persist: next chunk needs host, xs_next, xts_next");
-    const at::Tensor& h = *host;
-    if (h.is_cuda() || !h.is_pinned()) throw std::runtime_error("mlp_persist: host must be pinned host memory");
-    if (host_off < 0 || host_off % 16 != 0 ||
-        host_off + (int64_t)next_steps * rec_h > (int64_t)(h.numel() * h.element_size()))
-      throw std::runtime_error("mlp_persist: host range out of bounds");
-    need(*xs_next, at::kByte, (int64_t)next_steps * rec_s, "xs_next");
-    need(*xts_next, at::kByte, (int64_t)next_steps * xtb, "xts_next");
-    void* dp = nullptr;
-    char* hp = reinterpret_cast<char*>(h.data_ptr()) + host_off;
-    if (hipHostGetDevicePointer(&dp, hp, 0) != hipSuccess || dp == nullptr) {
-      (void)hipGetLastError();
-      dp = hp;   // unified addressing: the host address is device-visible
-    }
-    if (reinterpret_cast<uintptr_t>(dp) % 16 != 0) throw std::runtime_error("mlp_persist: host not aligned");
-    hn = dp;
-    xn = xs_next->data_ptr();
-    xtn = xts_next->data_ptr();
-  }
-  const long long ticks = (long long)(timeout_s * 1e8);   // s_memrealtime: 100 MHz
-  int ts_ring = 1;
-  long long* sts = step_ts_ptr(step_ts, &ts_ring);
-  hip_check(dtfk_mlp_persist(xs.data_ptr(), xts.data_ptr(), rec_s, rec_h, B, nsteps, params.data_ptr<float>(),
-                             lr.data_ptr<float>(), metrics.data_ptr<float>(), (int)(metrics.numel() / 2), act, naive,
-                             reinterpret_cast<long long*>(gstep.data_ptr<int64_t>()),
-                             reinterpret_cast<unsigned long long*>(seq.data_ptr<int64_t>()),
-                             reinterpret_cast<unsigned long long*>(gran.data_ptr<int64_t>()), err.data_ptr<int>(),
-                             ticks, hn, next_steps, xn, xtn, ts_ptr(ts, 64 * 8 * 16 + 2 * 64),
-                             reinterpret_cast<void* const*>(ipc_table), ipc_W > 1 ? ipc_W : 1, ipc_W > 1 ? ipc_rank : 0,
-                             sts, ts_ring, cur_stream()),
-            "mlp_persist");
-}
-
-// fp32 persistent engines: csrc/kernels/mlp_persist_f32.hip (f32-input MFMA) or, with
-// exact_split, csrc/kernels/mlp_persist_x3.hip (exact 3-way bf16 split): `nsteps` SGD steps of
+// The fp32 persistent engine (csrc/kernels/mlp_persist_f32.hip; mfma_split: the big
+// GEMMs as exact 3-way bf16 splits, else f32-input MFMA): `nsteps` SGD steps of
 // the chunk staged in `stage` (records of mlpf_stage_rec() bytes) and, in the same
 // launch, `next_steps` host records from byte `host_off` of the pinned epoch into
 // `stage_next`.  nsteps = 0: copy only.  xbuf: exchange buffer (zeroed once).
@@ -377,21 +292,20 @@ void mlp_persist_f32(at::Tensor stage, int64_t rec_h, int B, int nsteps, at::Ten
                      double timeout_s, int act, int naive, c10::optional<at::Tensor> host, int64_t host_off,
                      int next_steps, c10::optional<at::Tensor> stage_next, c10::optional<at::Tensor> step_ts,
                      int64_t ipc_table, int ipc_W, int ipc_rank, bool grad_bf16,
-                     c10::optional<at::Tensor> phase_ts, bool spread, bool exact_split, bool two_shot,
-                     bool mfma_split) {
+                     c10::optional<at::Tensor> phase_ts, bool spread, bool two_shot, bool mfma_split) {
   if (ipc_W > 1 && (ipc_table == 0 || ipc_rank < 0 || ipc_rank >= ipc_W || ipc_W > 64))
     throw std::runtime_error("mlp_persist_f32: N-GPU exchange needs the IPC peer table");
   if (B <= 0 || B > dtfk_mlpf_max_batch()) throw std::runtime_error("mlp_persist_f32: B out of range");
   if (rec_h < (int64_t)B * 785 || rec_h % 16 != 0) throw std::runtime_error("mlp_persist_f32: bad host record size");
   if (nsteps < 0 || next_steps < 0) throw std::runtime_error("mlp_persist_f32: negative step count");
-  const int64_t rec_s = exact_split ? dtfk_mlpx_stage_rec() : dtfk_mlpf_stage_rec();
+  const int64_t rec_s = dtfk_mlpf_stage_rec();
   need(stage, at::kByte, (int64_t)std::max(nsteps, 1) * rec_s, "stage");
   need(params, at::kFloat, kNParam, "params");
   need(lr, at::kFloat, 1, "lr");
   need(metrics, at::kFloat, 2, "metrics");
   need(gstep, at::kLong, 1, "gstep");
   need(seq, at::kLong, 1, "seq");
-  need(xbuf, at::kByte, exact_split ? dtfk_mlpx_xbuf_bytes() : dtfk_mlpf_xbuf_bytes(), "xbuf");
+  need(xbuf, at::kByte, dtfk_mlpf_xbuf_bytes(), "xbuf");
   need(err, at::kInt, 1, "err");
   if (((uintptr_t)stage.data_ptr() | (uintptr_t)xbuf.data_ptr()) % 16 != 0)
     throw std::runtime_error("mlp_persist_f32: stage / xbuf must be 16-byte aligned");
@@ -409,18 +323,8 @@ void mlp_persist_f32(at::Tensor stage, int64_t rec_h, int B, int nsteps, at::Ten
   int ts_ring = 1;
   long long* sts = step_ts_ptr(step_ts, &ts_ring);
   const long long ticks = (long long)(timeout_s * 1e8);   // s_memrealtime: 100 MHz
-  hipError_t e;
-  if (exact_split)
-    e = dtfk_mlp_persist_x3(stage.data_ptr(), rec_h, B, nsteps, params.data_ptr<float>(), lr.data_ptr<float>(),
-                            metrics.data_ptr<float>(), (int)(metrics.numel() / 2), act, naive,
-                            reinterpret_cast<long long*>(gstep.data_ptr<int64_t>()),
-                            reinterpret_cast<unsigned long long*>(seq.data_ptr<int64_t>()), xbuf.data_ptr(),
-                            err.data_ptr<int>(), ticks, sts, ts_ring, hn, next_steps, sn,
-                            reinterpret_cast<void* const*>(ipc_table), ipc_W > 1 ? ipc_W : 1,
-                            ipc_W > 1 ? ipc_rank : 0, grad_bf16 ? 1 : 0, ts_ptr(phase_ts, 64 * 64 * 16),
-                            spread ? 1 : 0, two_shot ? 1 : 0, cur_stream());
-  else
-    e = dtfk_mlp_persist_f32(stage.data_ptr(), rec_h, B, nsteps, params.data_ptr<float>(), lr.data_ptr<float>(),
+  const hipError_t e =
+      dtfk_mlp_persist_f32(stage.data_ptr(), rec_h, B, nsteps, params.data_ptr<float>(), lr.data_ptr<float>(),
                              metrics.data_ptr<float>(), (int)(metrics.numel() / 2), act, naive,
                              reinterpret_cast<long long*>(gstep.data_ptr<int64_t>()),
                              reinterpret_cast<unsigned long long*>(seq.data_ptr<int64_t>()), xbuf.data_ptr(),
@@ -793,36 +697,22 @@ void init_mlp(py::module& m) {
   m.def("graph_mlp_step", &graph_mlp_step, py::arg("x"), py::arg("ylab"), py::arg("W1"), py::arg("b1"),
         py::arg("W2"), py::arg("b2"), py::arg("a2buf"), py::arg("dz2buf"), py::arg("grads"), py::arg("metrics"),
         py::arg("gstep"), py::arg("lr"), py::arg("act"), py::arg("naive"), py::arg("sgd"));
-  m.def("mlp_persist", &mlp_persist, py::arg("xs"), py::arg("xts"), py::arg("rec"), py::arg("B"),
-        py::arg("nsteps"), py::arg("params"), py::arg("lr"), py::arg("metrics"), py::arg("gstep"), py::arg("seq"),
-        py::arg("gran"), py::arg("err"), py::arg("timeout_s"), py::arg("act"), py::arg("naive"),
-        py::arg("host") = py::none(), py::arg("host_offset") = 0, py::arg("next_steps") = 0,
-        py::arg("xs_next") = py::none(), py::arg("xts_next") = py::none(), py::arg("ts") = py::none(),
-        py::arg("ipc_table") = 0, py::arg("ipc_W") = 1, py::arg("ipc_rank") = 0, py::arg("step_ts") = py::none());
   m.def("mlp_persist_f32", &mlp_persist_f32, py::arg("stage"), py::arg("rec_h"), py::arg("B"), py::arg("nsteps"),
         py::arg("params"), py::arg("lr"), py::arg("metrics"), py::arg("gstep"), py::arg("seq"), py::arg("xbuf"),
         py::arg("err"), py::arg("timeout_s"), py::arg("act"), py::arg("naive"), py::arg("host") = py::none(),
         py::arg("host_offset") = 0, py::arg("next_steps") = 0, py::arg("stage_next") = py::none(),
         py::arg("step_ts") = py::none(), py::arg("ipc_table") = 0, py::arg("ipc_W") = 1, py::arg("ipc_rank") = 0,
         py::arg("grad_bf16") = true, py::arg("phase_ts") = py::none(), py::arg("spread") = false,
-        py::arg("exact_split") = false, py::arg("two_shot") = false, py::arg("mfma_split") = false);
+        py::arg("two_shot") = false, py::arg("mfma_split") = false);
   py::class_<PersistF32Plan>(m, "PersistF32Plan")
       .def(py::init<at::Tensor, at::Tensor, int64_t, int, at::Tensor, at::Tensor, at::Tensor, at::Tensor,
                     at::Tensor, at::Tensor, at::Tensor, double, int, int, at::Tensor, at::Tensor, int64_t, int, int,
                     bool, bool, bool, bool>())
       .def("launch", &PersistF32Plan::launch);
-  m.def("mlpx_stage_rec", &dtfk_mlpx_stage_rec);
-  m.def("mlpx_xbuf_bytes", &dtfk_mlpx_xbuf_bytes);
-  m.def("mlpx_ipc_bytes", &dtfk_mlpx_ipc_bytes);
   m.def("mlpf_stage_rec", &dtfk_mlpf_stage_rec);
   m.def("mlpf_xbuf_bytes", &dtfk_mlpf_xbuf_bytes);
   m.def("mlpf_ipc_bytes", &dtfk_mlpf_ipc_bytes);
   m.def("mlpf_max_batch", &dtfk_mlpf_max_batch);
-  m.def("mlp_persist_ipc_bytes", &dtfk_mlp_persist_ipc_bytes);
-  m.def("mlp_persist_xt_bytes", &dtfk_mlp_persist_xt_bytes);
-  m.def("mlp_persist_gran_count", &dtfk_mlp_persist_gran_count);
-  m.def("mlp_persist_max_batch", &dtfk_mlp_persist_max_batch);
-  m.def("mlp_persist_stage_rec", &dtfk_mlp_persist_stage_rec);
   m.def("mlp_ksplit", &dtfk_mlp_ksplit);
   m.def("mlp_l1_fwd", &mlp_l1_fwd, py::arg("x"), py::arg("x_offset"), py::arg("x_kind"),
         py::arg("B"), py::arg("W1T"), py::arg("z2p"), py::arg("ts") = py::none());

@@ -435,13 +435,9 @@ class PersistentMLPRunner:
     precision="fp32-mfma" -- the same engine with every product on f32-input
         MFMA (v_mfma_f32_16x16x4_f32, bitwise an fmaf chain): 1/8 of the bf16
         MFMA rate, ~2 us/step slower.
-    precision="fp32-split7" -- csrc/kernels/mlp_persist_x3.hip: 7 compute
-        workgroups (one per hidden block, the exact split on the big GEMMs):
-        one inter-workgroup edge per step instead of two, but 7 CUs carry all
-        the MFMA work.
-    precision="fp16" -- csrc/kernels/mlp_persist.hip: 7 compute workgroups on
-        f16 MFMA (pixels exact as 1024+u, weights/activations rounded to fp16),
-        57 copier workgroups.
+    (Rounds 1-3 also carried a 7-workgroup split engine -- one hand-off per
+    step but 7 CUs of MFMA work: 14.5 us/step -- and an fp16 engine; both were
+    retired in round 4: profiles/README.md.)
 
     Inside each launch the copier workgroups pull the NEXT chunk from pinned host
     memory over PCIe into the other device stage while the compute workgroups
@@ -470,21 +466,18 @@ class PersistentMLPRunner:
                  timeout_s: float = 30.0, precision: str = "fp32", grad_bf16: bool = True,
                  placement: str = "auto", exchange: str = "one-shot"):
         C = trainer.C
-        if precision not in ("fp32", "fp32-mfma", "fp32-split7", "fp16"):
-            raise ValueError("precision must be 'fp32', 'fp32-mfma', 'fp32-split7' or 'fp16'")
+        if precision not in ("fp32", "fp32-mfma"):
+            raise ValueError("precision must be 'fp32' or 'fp32-mfma'")
         self.precision = precision
-        self.f32 = precision in ("fp32", "fp32-mfma", "fp32-split7")
-        self.exact_split = precision == "fp32-split7"
+        self.f32 = True
         self.mfma_split = precision == "fp32"
         if exchange not in ("one-shot", "two-shot"):
             raise ValueError("exchange must be 'one-shot' or 'two-shot'")
-        if exchange == "two-shot" and precision not in ("fp32", "fp32-mfma"):
-            raise ValueError("the two-shot exchange exists in the fp32 engine only")
         # N GPUs: one-shot = each workgroup reads its gradient slot from every
         # peer ((W-1) slots per GPU per step); two-shot = reduce-scatter by wave
         # chunk + all-gather of the sums (2 (W-1)/W of a slot, one more hop)
         self.exchange = exchange
-        maxb = C.mlpf_max_batch() if self.f32 else C.mlp_persist_max_batch()
+        maxb = C.mlpf_max_batch()
         if trainer.B > maxb:
             raise ValueError(f"PersistentMLPRunner needs batch <= {maxb}")
         if epoch.batch_size != trainer.B:
@@ -502,17 +495,9 @@ class PersistentMLPRunner:
             raise ValueError("placement must be 'auto', 'packed' or 'spread'")
         self.placement = placement
         dev = trainer.device
-        if self.f32:
-            self.rec_s = int(C.mlpx_stage_rec() if self.exact_split else C.mlpf_stage_rec())
-            self.stages = [torch.zeros(self.g * self.rec_s, dtype=torch.uint8, device=dev) for _ in range(2)]
-            nx = C.mlpx_xbuf_bytes() if self.exact_split else C.mlpf_xbuf_bytes()
-            self.xbuf = torch.zeros(int(nx), dtype=torch.uint8, device=dev)
-        else:
-            self.rec_s = int(C.mlp_persist_stage_rec(trainer.B))   # k-step-pair interleaved rows
-            self.xtb = int(C.mlp_persist_xt_bytes())
-            self.xs = [torch.zeros(self.g * self.rec_s, dtype=torch.uint8, device=dev) for _ in range(2)]
-            self.xts = [torch.zeros(self.g * self.xtb, dtype=torch.uint8, device=dev) for _ in range(2)]
-            self.gran = torch.zeros(C.mlp_persist_gran_count(), dtype=torch.int64, device=dev)
+        self.rec_s = int(C.mlpf_stage_rec())
+        self.stages = [torch.zeros(self.g * self.rec_s, dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.xbuf = torch.zeros(int(C.mlpf_xbuf_bytes()), dtype=torch.uint8, device=dev)
         self.seq = torch.zeros(1, dtype=torch.int64, device=dev)
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
         self.step_ts = torch.zeros(self.TS_RING, dtype=torch.int64, device=dev)
@@ -531,9 +516,7 @@ class PersistentMLPRunner:
             if int(os.environ.get("LOCAL_WORLD_SIZE", w.world_size)) != w.world_size:
                 raise RuntimeError("the persistent N-GPU exchange needs all ranks on one node")
             from ..parallel.world import open_peer_buffers
-            nbytes = ((C.mlpx_ipc_bytes() if self.exact_split else C.mlpf_ipc_bytes()) if self.f32
-                      else C.mlp_persist_ipc_bytes())
-            self.ipc = open_peer_buffers(C, int(nbytes), w)
+            self.ipc = open_peer_buffers(C, int(C.mlpf_ipc_bytes()), w)
             self.W, self.rank = w.world_size, w.rank
 
     def _chunks(self, cursor: int, steps: int) -> List[Tuple[int, int]]:
@@ -552,7 +535,7 @@ class PersistentMLPRunner:
         t, ep = self.t, self.epoch
         dst = par ^ 1
         ipc = dict(ipc_table=self.ipc.table_ptr() if self.ipc is not None else 0, ipc_W=self.W, ipc_rank=self.rank)
-        if self.f32 and not self.exact_split and self.phase_ts is None:
+        if self.phase_ts is None:
             if self._plan is None:   # every pointer resolved once (host-side launch cost)
                 self._plan = t.C.PersistF32Plan(
                     self.stages[0], self.stages[1], ep.rec, t.B, t.params, t.lr, t.metrics, t.gstep, self.seq,
@@ -560,21 +543,14 @@ class PersistentMLPRunner:
                     ipc["ipc_table"], self.W, self.rank, self.grad_bf16, self.placement == "spread",
                     self.exchange == "two-shot", self.mfma_split)
             self._plan.launch(par, off if nsteps > 0 else 0, nsteps, nxt[0] * ep.rec, nxt[1])
-        elif self.f32:
+        else:   # phase stamps (profiling): the generic binding
             st = self.stages[par][off * self.rec_s:] if nsteps > 0 else self.stages[par]
             t.C.mlp_persist_f32(st, ep.rec, t.B, nsteps, t.params, t.lr, t.metrics, t.gstep, self.seq, self.xbuf,
                                 self.err, self.timeout_s, t.act, int(t.naive), host=ep.host,
                                 host_offset=nxt[0] * ep.rec, next_steps=nxt[1], stage_next=self.stages[dst],
                                 step_ts=self.step_ts, grad_bf16=self.grad_bf16, phase_ts=self.phase_ts,
-                                spread=self.placement == "spread", exact_split=self.exact_split,
-                                two_shot=self.exchange == "two-shot", mfma_split=self.mfma_split, **ipc)
-        else:
-            xs = self.xs[par][off * self.rec_s:] if nsteps > 0 else self.xs[par]
-            xts = self.xts[par][off * self.xtb:] if nsteps > 0 else self.xts[par]
-            t.C.mlp_persist(xs, xts, ep.rec, t.B, nsteps, t.params, t.lr, t.metrics, t.gstep,
-                            self.seq, self.gran, self.err, self.timeout_s, t.act, int(t.naive),
-                            host=ep.host, host_offset=nxt[0] * ep.rec, next_steps=nxt[1],
-                            xs_next=self.xs[dst], xts_next=self.xts[dst], step_ts=self.step_ts, **ipc)
+                                spread=self.placement == "spread", two_shot=self.exchange == "two-shot",
+                                mfma_split=self.mfma_split, **ipc)
         if nxt[1] > 0:
             self.staged[dst] = nxt
         self.last_prefetch_steps = nxt[1]

@@ -22,11 +22,7 @@ from distributed_tensorflow_example_amd.data.mnist import PinnedEpoch, synthetic
 from distributed_tensorflow_example_amd.models import mlp  # noqa: E402
 
 NAMES = {"fp32": ["fwd_mfma", "barrier_A", "E1_publish", "E1_wait", "E1_load_sum", "P1_logit_publish",
-                       "E2_wait", "E2_load_sum", "head", "barrier_B", "wgrad_mfma", "update"],
-         # exact-split engine (mlp_persist_x3.hip): 0 start 1 fwd 2 barA 3 E2 pub 4 E2 gathered 5 head 6 barB
-         # 7 wgrad 8 update
-         "fp32-split7": ["fwd_mfma_and_prefetch_issue", "barrier_A", "zsum_act_logits_publish", "E2_wait", "head",
-                  "barrier_B", "wgrad_mfma", "update"]}
+                       "E2_wait", "E2_load_sum", "head", "barrier_B", "wgrad_mfma", "update"]}
 
 
 def main():
@@ -112,14 +108,6 @@ def main():
             "barrier_B_exit": med(rs[:, :, 10] - rs[:, :, 0])}
     late = (r[:, :, 0] - r[:, :, 0].min(axis=1, keepdims=True)).mean(axis=0)
     out["step_start_lateness_us_by_wg"] = np.round(late, 2).tolist()
-    if prec == "fp32-split7":
-        rr = raw[1:G, :7, :].astype(np.float64) * 0.01
-        med = lambda x: round(float(np.median(x)), 3)
-        out["x3_fwd_detail_us"] = {"w0_start_to_mfma_done": med(rr[:, :, 9] - rr[:, :, 0]),
-                                   "w4_start_to_mfma_done": med(rr[:, :, 10] - rr[:, :, 12]),
-                                   "w0_mfma_done_to_pair_barrier": med(rr[:, :, 11] - rr[:, :, 9]),
-                                   "w0_pair_barrier_to_stamp1": med(rr[:, :, 1] - rr[:, :, 11]),
-                                   "w4_start_minus_w0_start": med(rr[:, :, 12] - rr[:, :, 0])}
     np.save(os.path.join(REPO, "gpurun_out", f"phase_raw_{prec}.npy"), raw[:G])
     print(json.dumps(out, indent=1))
 

@@ -1,5 +1,5 @@
-"""Persistent weight-stationary MLP kernels (csrc/kernels/mlp_persist_f32.hip,
-the fp32 default, and csrc/kernels/mlp_persist.hip, fp16 operands) vs the plain
+"""The persistent weight-stationary MLP engine (csrc/kernels/mlp_persist_f32.hip:
+exact-split bf16 MFMA "fp32" and f32-input MFMA "fp32-mfma") vs the plain
 PyTorch fp32 reference of example.py's step (models/mlp.reference_step)."""
 import numpy as np
 import pytest
@@ -24,7 +24,7 @@ def _ref_run(p0, imgs, labels, B, batches, lr, act="sigmoid"):
     return p, np.array(losses), np.array(accs)
 
 
-@pytest.mark.parametrize("engine", ["fp32", "fp32-mfma", "fp32-split7"])
+@pytest.mark.parametrize("engine", ["fp32", "fp32-mfma"])
 @pytest.mark.parametrize("B", [100, 37, 112])
 @pytest.mark.parametrize("act", ["sigmoid", "relu"])
 def test_persist_f32_one_step_gradient_fp32_exact(native, B, act, engine):
@@ -55,7 +55,7 @@ def test_persist_f32_one_step_gradient_fp32_exact(native, B, act, engine):
     assert abs(m[1] - acc.item()) < 1e-6
 
 
-@pytest.mark.parametrize("engine", ["fp32", "fp32-mfma", "fp32-split7"])
+@pytest.mark.parametrize("engine", ["fp32", "fp32-mfma"])
 def test_persist_f32_multi_step_matches_reference(native, engine):
     """11 steps over wrapping chunks (cold start, in-kernel prefetch, offsets into
     a staged chunk, epoch wrap): fp32 engine tracks fp32 SGD to ~1e-6."""
@@ -85,7 +85,7 @@ def test_persist_f32_multi_step_matches_reference(native, engine):
     assert np.allclose(m[:, 1], accs, atol=1e-6)
 
 
-@pytest.mark.parametrize("precision", ["fp32", "fp32-mfma", "fp32-split7", "fp16"])
+@pytest.mark.parametrize("precision", ["fp32", "fp32-mfma"])
 def test_persist_short_timed_run_streams_only_what_it_computes(native, precision):
     """The bench's pattern: warmup(5) primes exactly the timed run's chunk; the
     timed run(20) needs no copy-only launch and prefetches <= 20 steps; the
@@ -110,60 +110,7 @@ def test_persist_short_timed_run_streams_only_what_it_computes(native, precision
     assert dt.shape == (20,) and (dt > 0).all() and (dt < 1.0).all(), dt
 
 
-@pytest.mark.parametrize("B", [100, 37, 112])
-@pytest.mark.parametrize("act", ["sigmoid", "relu"])
-def test_persist_one_step_gradient(native, B, act):
-    imgs, labels = synthetic_mnist(B, seed=11)
-    dev = torch.device("cuda")
-    tr = mlp.FusedMLPTrainer(batch_size=B, lr=1.0, act=act, device=dev)
-    p0 = tr.get_params().clone()
-    ep = PinnedEpoch(imgs, labels, B)
-    run = mlp.PersistentMLPRunner(tr, ep, steps_per_launch=1, precision="fp16")
-    run.run(1)
-    torch.cuda.synchronize()
-    assert run.error() == 0
-    assert tr.global_step == 1
-    _, _, g = mlp.reference_loss_and_grad(p0, torch.from_numpy(imgs).float() / 255.0,
-                                          torch.from_numpy(labels), act)
-    loss, acc, _ = mlp.reference_loss_and_grad(p0, torch.from_numpy(imgs).float() / 255.0,
-                                               torch.from_numpy(labels), act)
-    g_k = p0 - tr.get_params()
-    for name, (off, shape) in mlp.PARAM_SPECS.items():
-        n = int(np.prod(shape))
-        a, b = g_k[off:off + n], g[off:off + n]
-        rel = ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
-        assert rel < (5e-3 if act == "sigmoid" else 1e-2), (name, rel)
-    m = tr.read_metrics(0, 1)[0]
-    assert abs(m[0] - loss.item()) < 2e-3 * max(1.0, abs(loss.item())), (m, loss)
-    assert abs(m[1] - acc.item()) < 1e-6
-
-
-def test_persist_chunks_wrap_and_match_reference(native):
-    B, nb = 100, 6
-    imgs, labels = synthetic_mnist(B * nb, seed=12)
-    dev = torch.device("cuda")
-    lr = 0.05
-    tr = mlp.FusedMLPTrainer(batch_size=B, lr=lr, device=dev)
-    p0 = tr.get_params().clone()
-    ep = PinnedEpoch(imgs, labels, B)
-    run = mlp.PersistentMLPRunner(tr, ep, steps_per_launch=4, precision="fp16")
-    run.run(7)     # chunks (0,4) (4,2) (0,1): copy-only cold start, in-kernel copies, epoch wrap
-    run.run(4)     # (1,3) (4,1): inside / outside the staged speculative chunk
-    torch.cuda.synchronize()
-    assert run.error() == 0
-    assert tr.global_step == 11
-    batches = [0, 1, 2, 3, 4, 5, 0, 1, 2, 3, 4]
-    p_ref, losses, accs = _ref_run(p0, imgs, labels, B, batches, lr)
-    d_k = tr.get_params() - p0
-    d_r = p_ref - p0
-    rel = ((d_k - d_r).norm() / d_r.norm()).item()
-    assert rel < 5e-3, rel
-    m = tr.read_metrics(0, 11)
-    assert np.allclose(m[:, 0], losses, rtol=2e-3, atol=2e-3), (m[:, 0], losses)
-    assert np.allclose(m[:, 1], accs, atol=1e-6)
-
-
-@pytest.mark.parametrize("precision", ["fp32", "fp32-mfma", "fp32-split7", "fp16"])
+@pytest.mark.parametrize("precision", ["fp32", "fp32-mfma"])
 def test_persist_deterministic_and_hands_over_to_step_path(native, precision):
     B = 100
     imgs, labels = synthetic_mnist(B * 4, seed=13)
@@ -190,7 +137,7 @@ def test_persist_deterministic_and_hands_over_to_step_path(native, precision):
     assert ((g_k - g).norm() / g.norm()).item() < 3e-2
 
 
-@pytest.mark.parametrize("precision", ["fp32", "fp32-mfma", "fp32-split7", "fp16"])
+@pytest.mark.parametrize("precision", ["fp32", "fp32-mfma"])
 def test_persist_long_run_learns(native, precision):
     """1000 steps on synthetic MNIST: loss goes down."""
     B = 100
@@ -209,8 +156,7 @@ def test_persist_long_run_learns(native, precision):
 
 @pytest.mark.parametrize("precision,grad,exchange", [("fp32", "bf16", "one-shot"), ("fp32", "fp32", "one-shot"),
                                                      ("fp32", "bf16", "two-shot"), ("fp32", "fp32", "two-shot"),
-                                                     ("fp32-mfma", "bf16", "one-shot"), ("fp32-mfma", "fp32", "two-shot"),
-                                                     ("fp32-split7", "fp32", "one-shot"), ("fp16", "bf16", "one-shot")])
+                                                     ("fp32-mfma", "bf16", "one-shot"), ("fp32-mfma", "fp32", "two-shot")])
 @pytest.mark.parametrize("nproc", [2, 3])
 def test_persist_multi_rank_same_gpu(native, nproc, precision, grad, exchange):
     _persist_selftest(nproc, precision, grad, exchange)

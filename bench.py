@@ -243,7 +243,7 @@ def main(argv=None):
         # tests: rank 1 goes silent (a dead peer) from timed step k on, in the first timed attempt only
         fault = os.environ.pop("DTF_BENCH_FAULT", None)
         if fault is not None and w.world_size > 1 and persistent:
-            os.environ["DTF_XCHG_FAULT"] = f"1:{step0 + int(fault)}"
+            trainer.C.mlpf_set_fault(1, step0 + int(fault))
         # Timing events only for the 3-launch path (its per-replay p50); the
         # persistent engine's p50 comes from device stamps, so nothing but the
         # launch is issued inside its timed region (a first hipEventCreate + record
@@ -259,7 +259,8 @@ def main(argv=None):
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         w.barrier()
-        os.environ.pop("DTF_XCHG_FAULT", None)
+        if fault is not None and w.world_size > 1 and persistent:
+            trainer.C.mlpf_set_fault(-1, -1)
         elapsed_max = w.host_all_reduce(t1 - t0, "max")
         if not consistent(trainer, runner):
             return None

@@ -33,6 +33,7 @@ hipError_t dtfk_mlp_ipc_reduce_apply(float* params, void* const* peer_table, int
                                      void* W1T, void* W2T, void* W2N, int* err, long long timeout_ticks,
                                      hipStream_t stream);
 long long dtfk_mlpf_stage_rec();
+void dtfk_mlpf_set_fault(int rank, long long step);
 long long dtfk_mlpf_xbuf_bytes();
 long long dtfk_mlpf_ipc_bytes();
 int dtfk_mlpf_max_batch();
@@ -713,6 +714,7 @@ void init_mlp(py::module& m) {
                     bool, bool, bool, bool, bool>())
       .def("launch", &PersistF32Plan::launch);
   m.def("mlpf_stage_rec", &dtfk_mlpf_stage_rec);
+  m.def("mlpf_set_fault", &dtfk_mlpf_set_fault, py::arg("rank"), py::arg("step"));
   m.def("mlpf_xbuf_bytes", &dtfk_mlpf_xbuf_bytes);
   m.def("mlpf_ipc_bytes", &dtfk_mlpf_ipc_bytes);
   m.def("mlpf_max_batch", &dtfk_mlpf_max_batch);

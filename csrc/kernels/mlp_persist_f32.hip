@@ -238,7 +238,7 @@ struct Args {
                             // no / short / long s_sleep between passes (DTF_GATHER_MODE, tuning)
   int xmode;                // N GPUs: 0 one-shot (every workgroup reads its slot from every peer),
                             // 1 two-shot (reduce-scatter by wave chunk, then all-gather of the sums)
-  long long fault_step;     // fault injection (DTF_XCHG_FAULT=rank:step, tests of the bench's fallback):
+  long long fault_step;     // fault injection (mlpf_set_fault(rank, step), tests of the bench's fallback):
   int fault_rank;           // that rank stops publishing its exchange flag from that global step on, a dead
                             // peer (-1: off; one skipped flag alone is absorbed: the flags are monotonic)
   int look;                 // one GPU, SPLIT: the lookahead schedule (compute_look)
@@ -1871,7 +1871,17 @@ __global__ __launch_bounds__(THREADS, 1) void mlp_persist_f32(Args a) {
 }  // namespace mlpf
 }  // namespace dtfk
 
+// fault injection (tests of the bench's in-process fallback): rank `rank` stops
+// publishing its exchange flag from global step `step` on; rank -1 = off
+static int g_fault_rank = -1;
+static long long g_fault_step = -1;
+
 extern "C" {
+
+void dtfk_mlpf_set_fault(int rank, long long step) {
+  g_fault_rank = rank;
+  g_fault_step = step;
+}
 
 long long dtfk_mlpf_stage_rec() { return dtfk::mlpf::REC; }
 long long dtfk_mlpf_xbuf_bytes() { return dtfk::mlpf::XBUF_BYTES; }
@@ -1915,17 +1925,19 @@ hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int n
   a.xmode = xmode;
   a.look = (look != 0 && W == 1 && split != 0) ? 1 : 0;
   {
-    const char* gm = getenv("DTF_GATHER_MODE");   // r3: direct loads, no sleep 8.68 / long sleep 8.72 / probe 9.56 us
-    a.gmode = gm ? atoi(gm) : 1;
-    const char* db = getenv("DTF_PERSIST_DBG");
-    a.dbg = db ? atoi(db) : 0;
-    a.fault_rank = -1;
-    a.fault_step = -1;
-    const char* fl = getenv("DTF_XCHG_FAULT");   // "rank:global_step"
-    if (fl != nullptr && strchr(fl, ':') != nullptr) {
-      a.fault_rank = atoi(fl);
-      a.fault_step = atoll(strchr(fl, ':') + 1);
-    }
+    // read once per process (a getenv per launch is host time inside a short timed run)
+    static const int gmode = [] {
+      const char* gm = getenv("DTF_GATHER_MODE");   // r3: direct loads, no sleep 8.68 / long sleep 8.72 / probe 9.56 us
+      return gm ? atoi(gm) : 1;
+    }();
+    static const int dbg = [] {
+      const char* db = getenv("DTF_PERSIST_DBG");
+      return db ? atoi(db) : 0;
+    }();
+    a.gmode = gmode;
+    a.dbg = dbg;
+    a.fault_rank = g_fault_rank;
+    a.fault_step = g_fault_step;
   }
   constexpr size_t lds = LDS_BYTES;
   typedef void (*Kern)(Args);

@@ -58,7 +58,9 @@ def _no_hook(p):
 # xGMI ring model (task spec: 7 links x ~153 GB/s per GPU; a ring is bound by
 # one link per direction).  The per-hop fixed cost is RCCL's kernel hand-off
 # plus one flag round trip over xGMI; 6 us is an estimate, not a measurement
-# (gpurun gives one GPU) -- the driver's 8-GPU run is where it gets checked.
+# (gpurun gives one GPU).  GPU worlds therefore calibrate by default
+# (measure_allreduce_cost: a tiny and a 32 MB all-reduce at construction); the
+# model is the CPU / DTF_BUCKET_MODEL=1 fallback.
 XGMI_LINK_GBPS = 153.0
 XGMI_HOP_US = 6.0
 
@@ -151,7 +153,12 @@ class DistributedDataParallel(torch.nn.Module):
         if bucket_mb in ("auto", "measure"):
             wire = 2 if comm_dtype in (torch.bfloat16, torch.float16) else 4
             n_el = sum(p.numel() for p in params)
-            if bucket_mb == "measure" and self.world.world_size > 1:
+            # on a GPU world the default calibrates too: the xGMI link model's
+            # constants are estimates, two timed all-reduces are this machine
+            # (DTF_BUCKET_MODEL=1 keeps the model)
+            calibrate = bucket_mb == "measure" or (self.device.type == "cuda"
+                                                   and os.environ.get("DTF_BUCKET_MODEL", "0") != "1")
+            if calibrate and self.world.world_size > 1:
                 # this machine's alpha / bandwidth instead of the xGMI link model
                 self.comm_cost = measure_allreduce_cost(self.world, self.device, comm_dtype or torch.float32)
             a_s, bw = self.comm_cost or (None, None)

@@ -245,7 +245,7 @@ def test_bench_two_ranks_same_gpu_short_run(native):
 def test_bench_two_ranks_timed_run_fault_falls_back(native):
     """A failure inside the timed run does not lose the scaling point: rank 1
     stops publishing its exchange flag from timed step 5 on (a dead peer) (DTF_BENCH_FAULT -> the kernel's
-    DTF_XCHG_FAULT), its peer times out, the replica check fails, and bench.py
+    mlpf_set_fault), its peer times out, the replica check fails, and bench.py
     re-times the next validated strategy in the same process and prints one
     contract line naming the failed mode under `fallbacks`."""
     import json

@@ -42,7 +42,7 @@ hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int n
                                 void* xbuf, int* err, long long timeout, long long* step_ts, int ts_ring,
                                 const void* host_next, int next_steps, void* stage_next, void* const* peer_base, int W,
                                 int rank, int gbf16, long long* phase_ts, int spread, int xmode, int split,
-                                int look, hipStream_t stream);
+                                hipStream_t stream);
 long long dtfk_graph_mlp_part_floats(int B, int H);
 hipError_t dtfk_graph_feed_ingest(const void* host, void* dev, long long bytes, hipStream_t stream);
 hipError_t dtfk_graph_mlp_step(const float* x, const float* ylab, float* W1, float* b1, float* W2, float* b2,
@@ -293,8 +293,7 @@ void mlp_persist_f32(at::Tensor stage, int64_t rec_h, int B, int nsteps, at::Ten
                      double timeout_s, int act, int naive, c10::optional<at::Tensor> host, int64_t host_off,
                      int next_steps, c10::optional<at::Tensor> stage_next, c10::optional<at::Tensor> step_ts,
                      int64_t ipc_table, int ipc_W, int ipc_rank, bool grad_bf16,
-                     c10::optional<at::Tensor> phase_ts, bool spread, bool two_shot, bool mfma_split,
-                     bool look) {
+                     c10::optional<at::Tensor> phase_ts, bool spread, bool two_shot, bool mfma_split) {
   if (ipc_W > 1 && (ipc_table == 0 || ipc_rank < 0 || ipc_rank >= ipc_W || ipc_W > 64))
     throw std::runtime_error("mlp_persist_f32: N-GPU exchange needs the IPC peer table");
   if (B <= 0 || B > dtfk_mlpf_max_batch()) throw std::runtime_error("mlp_persist_f32: B out of range");
@@ -333,7 +332,7 @@ void mlp_persist_f32(at::Tensor stage, int64_t rec_h, int B, int nsteps, at::Ten
                              err.data_ptr<int>(), ticks, sts, ts_ring, hn, next_steps, sn,
                              reinterpret_cast<void* const*>(ipc_table), ipc_W > 1 ? ipc_W : 1,
                              ipc_W > 1 ? ipc_rank : 0, grad_bf16 ? 1 : 0, ts_ptr(phase_ts, 65 * 64 * 16),
-                             spread ? 1 : 0, two_shot ? 1 : 0, mfma_split ? 1 : 0, look ? 1 : 0, cur_stream());
+                             spread ? 1 : 0, two_shot ? 1 : 0, mfma_split ? 1 : 0, cur_stream());
   hip_check(e,
             "mlp_persist_f32");
 }
@@ -347,15 +346,14 @@ struct PersistF32Plan {
   void* st[2];
   const char* host_dev = nullptr;
   int64_t host_bytes = 0, rec_h = 0, rec_s = 0;
-  int B, act, naive, ring, ts_ring = 1, W, rank, gbf16, spread, two_shot, split, look;
+  int B, act, naive, ring, ts_ring = 1, W, rank, gbf16, spread, two_shot, split;
   long long ticks;
   int64_t ipc_table;
 
   PersistF32Plan(at::Tensor s0, at::Tensor s1, int64_t rec_h_, int B_, at::Tensor params_, at::Tensor lr_,
                  at::Tensor metrics_, at::Tensor gstep_, at::Tensor seq_, at::Tensor xbuf_, at::Tensor err_,
                  double timeout_s, int act_, int naive_, at::Tensor host_, at::Tensor step_ts_, int64_t ipc_table_,
-                 int ipc_W, int ipc_rank, bool grad_bf16, bool spread_, bool two_shot_, bool mfma_split,
-                 bool look_)
+                 int ipc_W, int ipc_rank, bool grad_bf16, bool spread_, bool two_shot_, bool mfma_split)
       : stage0(s0), stage1(s1), params(params_), lr(lr_), metrics(metrics_), gstep(gstep_), seq(seq_), xbuf(xbuf_),
         err(err_), step_ts(step_ts_), host(host_) {
     if (ipc_W > 1 && (ipc_table_ == 0 || ipc_rank < 0 || ipc_rank >= ipc_W || ipc_W > 64))
@@ -393,7 +391,6 @@ struct PersistF32Plan {
     spread = spread_ ? 1 : 0;
     two_shot = two_shot_ ? 1 : 0;
     split = mfma_split ? 1 : 0;
-    look = (look_ && W == 1 && split) ? 1 : 0;
   }
 
   // nsteps steps from stage `par` at step offset `off`; next_steps host records from
@@ -419,7 +416,7 @@ struct PersistF32Plan {
                                    err.data_ptr<int>(), ticks,
                                    reinterpret_cast<long long*>(step_ts.data_ptr<int64_t>()), ts_ring, hn,
                                    next_steps, sn, reinterpret_cast<void* const*>(ipc_table), W, rank, gbf16,
-                                   nullptr, spread, two_shot, split, look, cur_stream()),
+                                   nullptr, spread, two_shot, split, cur_stream()),
               "PersistF32Plan.launch");
   }
 };
@@ -707,11 +704,11 @@ void init_mlp(py::module& m) {
         py::arg("host_offset") = 0, py::arg("next_steps") = 0, py::arg("stage_next") = py::none(),
         py::arg("step_ts") = py::none(), py::arg("ipc_table") = 0, py::arg("ipc_W") = 1, py::arg("ipc_rank") = 0,
         py::arg("grad_bf16") = true, py::arg("phase_ts") = py::none(), py::arg("spread") = false,
-        py::arg("two_shot") = false, py::arg("mfma_split") = false, py::arg("look") = false);
+        py::arg("two_shot") = false, py::arg("mfma_split") = false);
   py::class_<PersistF32Plan>(m, "PersistF32Plan")
       .def(py::init<at::Tensor, at::Tensor, int64_t, int, at::Tensor, at::Tensor, at::Tensor, at::Tensor,
                     at::Tensor, at::Tensor, at::Tensor, double, int, int, at::Tensor, at::Tensor, int64_t, int, int,
-                    bool, bool, bool, bool, bool>())
+                    bool, bool, bool, bool>())
       .def("launch", &PersistF32Plan::launch);
   m.def("mlpf_stage_rec", &dtfk_mlpf_stage_rec);
   m.def("mlpf_set_fault", &dtfk_mlpf_set_fault, py::arg("rank"), py::arg("step"));

@@ -155,59 +155,7 @@ static_assert(L_XF % 1024 == 0 && L_XT % 16 == 0 && L_LAB % 16 == 0, "LDS-DMA ba
 static_assert(L_DW2P % 16 == 0, "dW2 partials: 16-B lanes");
 constexpr int CROW = DIN + 16;                         // copier LDS row stride (800)
 constexpr int LDS_COPIER = BROWS * CROW;               // 89600
-// ------------------------------------------------------------------ lookahead engine (one GPU)
-// The same 28 workgroups, the same two hand-offs, but the step's weight update
-// leaves the critical path.  SGD gives, for the forward of step s+1,
-//
-//     z_{s+1} = x_{s+1} V_{s+1} = x_{s+1} V_s - lrX (x_{s+1} x_s^T) dz2_s
-//
-// (V_s: the weights step s ran with, dz2_s its hidden-layer gradient), so while
-// step s is between its hand-offs each wave already has x_{s+1} V_s (P0) and
-// G = x_{s+1} x_s^T of its slice (uint8 products, integer sums < 2^24: exact on
-// bf16 MFMA), and once the heads of step s are done the forward of s+1 only
-// needs G dz2_s (28 exact f32 MFMAs per wave) before its partial goes out.  The
-// weight gradient of step s (x_s^T dz2_s, exact 3-way split as before) and the
-// in-register update run in the next step's first hand-off window.  Products are
-// exact as before; z differs from x (V_s - delta) only by the rounding of the
-// stored update (fp32 ulp), the weights themselves are updated exactly as before.
-//
-//   wave w < 7 (batch tile w), per step s:
-//     corr  z = P0_s - lrX G_s dz2_{s-1}        (all heads of s-1 done)  -> E1 out
-//     P2    dW1_{s-1} tiles, W1 -= lrX dW1 (registers), W1^T pieces -> LDS
-//     E1 in, P1 (act, partial logits) -> E2 out
-//     P0_{s+1} = x_{s+1} V_s (W1^T pieces from LDS: every wave the whole slice
-//           for its batch tile -- no cross-wave partial sums) and G_{s+1}
-//     E2 in, head: softmax-xent, dz3, da2, dz2 -> LDS (parity s & 1)
-//     x_s^T fragments -> registers (the weight gradient of s, next step)
-//   wave 7: stages x_{s+1} rows / labels and x_s^T (LDS-DMA), its own weight-
-//     gradient tile + db1, sums dW2 / db2 / metrics of s-1, updates W2 / b1 / b2.
-constexpr int WPS = 232;                                  // W1^T piece row stride (bf16): 208 + zero pad
-constexpr int WP_PLANE = 16 * WPS;                        // bf16 elements per piece
-constexpr int K_WP = 0;                                   // [3 pieces][16 hidden][WPS] hi / mid / lo
-constexpr int K_XF0 = ((3 * WP_PLANE * 2 + 1023) / 1024) * 1024;
-constexpr int XFB = ((BROWS * XF_ROW + 64 + 1023) / 1024) * 1024;   // + over-read of the 7th K chunk
-constexpr int K_XT = K_XF0 + 2 * XFB;                     // [208 features][128 batch] u8, swizzled
-constexpr int K_LAB = K_XT + 13 * 16 * XTS;               // [2][128] labels
-constexpr int DZPB = 3 * 16 * PS;                         // dz2 pieces of one step (bf16 elements)
-constexpr int K_DZP = K_LAB + 256;                        // [2 parities][3][16 hidden][PS]
-constexpr int K_A2T = K_DZP + 2 * DZPB * 2;               // [16 hidden][LS] a2 (own tile rows)
-constexpr int K_DZ3T = K_A2T + 16 * LS * 4;               // [16 class][LS] dz3
-constexpr int K_W2 = K_DZ3T + 16 * LS * 4;                // [16 hidden][16 class]
-constexpr int K_B1 = K_W2 + 1024;
-constexpr int K_B2 = K_B1 + 64;
-constexpr int K_DW2P = K_B2 + 64;                         // [2][7 tiles][64 lanes] f32x4 dW2 partials
-constexpr int K_RDB2 = K_DW2P + 2 * NBT * 64 * 16;        // [2][8][16] db2 partials
-constexpr int K_RLOSS = K_RDB2 + 2 * 8 * 16 * 4;          // [2][2][128] per-row loss / hit
-constexpr int K_FLAG = K_RLOSS + 2 * 256 * 4;             // int flags
-constexpr int LDS_LOOK = K_FLAG + 256;
-static_assert(K_XF0 % 1024 == 0 && XFB % 1024 == 0 && K_XT % 1024 == 0 && K_DW2P % 16 == 0, "LDS-DMA / vector bases");
-static_assert(LDS_LOOK <= 160 * 1024, "lookahead LDS carve");
-// flag words: abort, census, head done (waves 0..6: steps done), stage landed,
-// W2 / b ready, W1^T pieces current (waves 0..7)
-constexpr int F_ABORT = 0, F_CENSUS = 1, F_HEAD = 2, F_STAGE = 9, F_PRM = 10, F_WUPD = 11;
-
-constexpr int LDS_BYTES_CC = LDS_COMPUTE > LDS_COPIER ? LDS_COMPUTE : LDS_COPIER;
-constexpr int LDS_BYTES = LDS_BYTES_CC > LDS_LOOK ? LDS_BYTES_CC : LDS_LOOK;
+constexpr int LDS_BYTES = LDS_COMPUTE > LDS_COPIER ? LDS_COMPUTE : LDS_COPIER;
 
 struct Args {
   const uint8_t* stage;     // this chunk: nsteps records of REC bytes
@@ -241,7 +189,6 @@ struct Args {
   long long fault_step;     // fault injection (mlpf_set_fault(rank, step), tests of the bench's fallback):
   int fault_rank;           // that rank stops publishing its exchange flag from that global step on, a dead
                             // peer (-1: off; one skipped flag alone is absorbed: the flags are monotonic)
-  int look;                 // one GPU, SPLIT: the lookahead schedule (compute_look)
   int dbg;                  // profiling only (DTF_PERSIST_DBG): bit 0 = never stage the next step's x (wrong
                             // numerics; what the per-step LDS-DMA stage costs the hand-offs), bit 1 = head
                             // sub-phase stamps (slots 13-15, wave 0), bits 2 / 3 = stage (half) after the
@@ -1331,523 +1278,12 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
   if (tid == 0) { PRO(c, 5); }
 }
 
-template <int ACT>
-__device__ void compute_look(const Args& a, const int j, const int q, uint8_t* smem) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int r = lane & 15, g = lane >> 4;
-  const int c = j * NQ + q;
-  const int B = a.B;
-  int* fl = reinterpret_cast<int*>(smem + K_FLAG);
-  uint16_t* wpl = reinterpret_cast<uint16_t*>(smem + K_WP);
-  uint16_t* dzpa = reinterpret_cast<uint16_t*>(smem + K_DZP);
-  float* a2T = reinterpret_cast<float*>(smem + K_A2T);
-  float* dz3T = reinterpret_cast<float*>(smem + K_DZ3T);
-  float* w2s = reinterpret_cast<float*>(smem + K_W2);
-  float* b1s = reinterpret_cast<float*>(smem + K_B1);
-  float* b2s = reinterpret_cast<float*>(smem + K_B2);
-  if (tid == 0) { PRO(c, 0); }
-
-  const int hid = 16 * j + r;
-  const bool hv = hid < HID;
-  const int nt = ntile(q);
-  const bool tv0 = w < nt, tv1 = w + 8 < nt;
-  const int ft0 = tile0(q) + w, ft1 = tile0(q) + (tv1 ? w + 8 : 0);
-  auto tvk = [=](int k) { return k ? tv1 : tv0; };
-  auto ftk = [=](int k) { return k ? ft1 : ft0; };
-  float Wt[NTW][4];
-#pragma unroll
-  for (int k = 0; k < NTW; ++k)
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-      Wt[k][e] = (tvk(k) && hv) ? a.params[(16 * ftk(k) + 4 * g + e) * HID + hid] : 0.f;
-  float pv = 0.f;
-  if (tid < 256) {
-    const int n = tid >> 4, cl = tid & 15;
-    const int hn = 16 * j + n;
-    pv = (hn < HID && cl < NCLS) ? a.params[OFF_W2 + hn * NCLS + cl] : 0.f;
-  } else if (tid < 272) {
-    const int hn = 16 * j + (tid - 256);
-    pv = hn < HID ? a.params[OFF_B1 + hn] : 0.f;
-  } else if (tid < 288) {
-    const int cl = tid - 272;
-    pv = cl < NCLS ? a.params[OFF_B2 + cl] : 0.f;
-  }
-  const unsigned long long seq0 = *a.seq;
-  const long long gstep0 = *a.gstep;
-  const float lr = *a.lr;
-  const float lrB = lr / (float)B;
-  const float lrX = lrB * (1.f / 255.f);
-  for (int k = tid; k < 2 * 16 * LS; k += THREADS) a2T[k] = 0.f;          // a2T, dz3T (batch pad stays 0)
-  for (int k = tid; k < 2 * DZPB; k += THREADS) dzpa[k] = (uint16_t)0;    // dz2 pieces, both parities
-  for (int k = tid; k < 3 * WP_PLANE; k += THREADS) wpl[k] = (uint16_t)0; // W1^T pieces (pad stays 0)
-  if (tid < 64) fl[tid] = 0;
-  if (tid < 256) {
-    w2s[tid] = pv;
-  } else if (tid < 272) {
-    b1s[tid - 256] = pv;
-  } else if (tid < 288) {
-    b2s[tid - 272] = pv;
-  }
-  const bool failed_in = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-
-  // x rows (and labels) of step st -> XF[buf] / LAB[buf]; x^T of step st -> XT
-  auto stage_rows = [&](int st, int buf, int n0, int dn) {
-    const uint8_t* rec = a.stage + (long long)st * REC;
-    const uint8_t* xr = rec + 16 * tile0(q);
-#pragma unroll 1
-    for (int n = n0; n < (XF_CHUNKS + 63) / 64; n += dn) {
-      const int k = 64 * n + lane;
-      if (k < XF_CHUNKS) glds16(xr + (k / 13) * DIN + 16 * (k % 13), smem + K_XF0 + buf * XFB + 1024 * n);
-    }
-    if (n0 == 0 && lane < 8) glds16(rec + XROW_BYTES + XT_BYTES + 16 * lane, smem + K_LAB + 128 * buf);
-  };
-  auto stage_xt = [&](int st) {
-    const uint8_t* xtb = a.stage + (long long)st * REC + XROW_BYTES + (long long)(16 * tile0(q)) * XTS;
-#pragma unroll 1
-    for (int n = 0; n < XT_CHUNKS / 64; ++n) {
-      const int f = 8 * n + (lane >> 3);
-      const int s = (lane & 7) ^ ((f >> 1) & 7);
-      if (f < 16 * nt) glds16(xtb + f * XTS + 16 * s, smem + K_XT + 1024 * n);
-    }
-  };
-  uint32_t xt[NTW][8];
-  auto tlk = [=](int k) { return k ? (tv1 ? w + 8 : 0) : w; };
-  auto read_xt = [&]() {
-#pragma unroll
-    for (int k = 0; k < NTW; ++k) {
-      const int f = 16 * tlk(k) + r;
-#pragma unroll
-      for (int cc = 0; cc < 4; ++cc) {
-        const uint2 v = *reinterpret_cast<const uint2*>(smem + K_XT + f * XTS +
-                                                         16 * ((2 * cc + (g >> 1)) ^ ((f >> 1) & 7)) + 8 * (g & 1));
-        xt[k][2 * cc] = v.x;
-        xt[k][2 * cc + 1] = v.y;
-      }
-    }
-  };
-  // this wave's master tiles -> the W1^T pieces in LDS (hi / mid / lo, 4 features per lane)
-  auto write_wp = [&]() {
-#pragma unroll
-    for (int k = 0; k < NTW; ++k) {
-      if (!tvk(k)) continue;
-      const int lt = k ? w + 8 : w;
-      uint32_t h[4], m[4], l[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) split3(Wt[k][e], h[e], m[e], l[e]);
-      uint16_t* p = wpl + r * WPS + 16 * lt + 4 * g;
-      *reinterpret_cast<uint2*>(p) = make_uint2(hi2(h[0], h[1]), hi2(h[2], h[3]));
-      *reinterpret_cast<uint2*>(p + WP_PLANE) = make_uint2(hi2(m[0], m[1]), hi2(m[2], m[3]));
-      *reinterpret_cast<uint2*>(p + 2 * WP_PLANE) = make_uint2(hi2(l[0], l[1]), hi2(l[2], l[3]));
-    }
-  };
-  // intra-workgroup waits are bounded too (a.timeout + 1 s: a head wave may itself
-  // wait a.timeout in a hand-off): false = give up, the caller aborts the launch
-  const long long lds_limit = a.timeout + 100000000LL;
-  auto wait_flag = [&](int idx, int val) -> bool {
-    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(fl + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < val) {
-      if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > lds_limit) return false;
-      __builtin_amdgcn_s_sleep(1);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-    return true;
-  };
-  auto wait_all = [&](int base, int n, int val) -> bool {   // flags base..base+n-1 all >= val
-    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-    for (;;) {
-      const bool ok = lane >= n || __hip_atomic_load(fl + base + (lane < n ? lane : 0), __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_WORKGROUP) >= val;
-      if (__all(ok)) break;
-      if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > lds_limit) return false;
-      __builtin_amdgcn_s_sleep(1);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-    return true;
-  };
-  auto give_up = [&]() {
-    if (lane == 0) {
-      atomicOr(a.err, 4);
-      __hip_atomic_store(fl + F_ABORT, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-  };
-  auto set_flag = [&](int idx, int val) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    if (lane == 0) __hip_atomic_store(fl + idx, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  };
-
-  if (tid == 0) { PRO(c, 4); }
-  // placement census (as in compute())
-  const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20) & 15u;
-  unsigned long long* hdr = reinterpret_cast<unsigned long long*>(a.xbuf + HDR_OFF);
-  const unsigned tag0 = (unsigned)(seq0 + 1ull);
-  if (tid == 0)
-    __hip_atomic_store(hdr + c, ((unsigned long long)tag0 << 32) | xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();   // LDS clears before the stage lands / the census result is written
-  if (tid < 8) fl[F_WUPD + tid] = 1;   // the pieces written below are the weights of step 0
-  stage_rows(0, 0, w, 8);
-  if (w == 0) {
-    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-    unsigned long long v = 0;
-    bool seen = lane >= NCOMP, bad = false;
-    for (;;) {
-      if (!seen) {
-        v = __hip_atomic_load(hdr + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        seen = (unsigned)(v >> 32) == tag0;
-      }
-      if (__all(seen)) break;
-      if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) {
-        if (lane == 0) atomicOr(a.err, 1);
-        bad = true;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    const bool off = lane < NCOMP && (unsigned)v != xcc;
-    const bool e1 = !__any(off && lane / NQ == j);
-    const bool e2 = !__any(off && lane % NQ == q);
-    if (lane == 0) fl[F_CENSUS] = bad ? -1 : ((e1 ? 1 : 0) | (e2 ? 2 : 0));
-  }
-  write_wp();
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // step 0's rows / labels landed
-  __syncthreads();
-  if (failed_in || fl[F_CENSUS] < 0) return;
-  const bool l2_e1 = (fl[F_CENSUS] & 1) != 0;
-  const bool l2_e2 = (fl[F_CENSUS] & 2) != 0;
-  if (tid == 0) { PRO(c, 1); }
-
-  // P0 of step st + 1 into Z (x rows of buffer nb, batch tile w, against the LDS
-  // W1^T pieces) and G^T of (x rows of buffer cb) x (x rows of nb, tile w) into GT
-  f32x4 Zp = {0.f, 0.f, 0.f, 0.f};
-  f32x4 GT[NBT];
-  auto p0g = [&](int nb, int cb, bool with_g) {
-    f32x4 Z0 = {0.f, 0.f, 0.f, 0.f}, Z1 = Z0;
-    if (with_g) {
-#pragma unroll
-      for (int t = 0; t < NBT; ++t) GT[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    const uint8_t* xn = smem + K_XF0 + nb * XFB + (16 * w + r) * XF_ROW + 8 * g;
-    const uint8_t* xc = smem + K_XF0 + cb * XFB + r * XF_ROW + 8 * g;
-    const uint16_t* wp = wpl + r * WPS + 8 * g;
-    const int nch = q == 0 ? 7 : 6;   // slice features: 208 (13 tiles) or 192
-#pragma unroll
-    for (int cc = 0; cc < 7; ++cc) {
-      if (cc >= nch) break;   // wave-uniform
-      uint2 bx = *reinterpret_cast<const uint2*>(xn + 32 * cc);
-      if (cc == 6 && g >= 2) bx = make_uint2(0u, 0u);   // features 208..223: not the slice's
-      const bf16x8 Bv = px8(bx.x, bx.y);
-      const bf16x8 Al = *reinterpret_cast<const bf16x8*>(wp + 2 * WP_PLANE + 32 * cc);
-      const bf16x8 Am = *reinterpret_cast<const bf16x8*>(wp + WP_PLANE + 32 * cc);
-      const bf16x8 Ah = *reinterpret_cast<const bf16x8*>(wp + 32 * cc);
-      Z0 = mfma16x16x32(Al, Bv, Z0);
-      Z1 = mfma16x16x32(Am, Bv, Z1);
-      Z0 = mfma16x16x32(Ah, Bv, Z0);
-      if (with_g) {
-#pragma unroll
-        for (int t = 0; t < NBT; ++t) {
-          const uint2 ax = *reinterpret_cast<const uint2*>(xc + 16 * t * XF_ROW + 32 * cc);
-          GT[t] = mfma16x16x32(px8(ax.x, ax.y), Bv, GT[t]);
-        }
-      }
-    }
-    Zp = Z0 + Z1;
-  };
-  if (w < NBT) p0g(0, 0, false);
-
-  // weight gradient of the step whose dz2 pieces are in parity pp (x^T in xt)
-  f32x4 G[NTW];
-  auto wgrad = [&](int pp) {
-#pragma unroll
-    for (int k = 0; k < NTW; ++k) G[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const uint16_t* dzp = dzpa + pp * DZPB;
-#pragma unroll
-    for (int ch = 0; ch < 4; ++ch) {
-      const uint16_t* bp = dzp + r * PS + 32 * ch + 8 * g;
-      const bf16x8 Bh = *reinterpret_cast<const bf16x8*>(bp);
-      const bf16x8 Bm = *reinterpret_cast<const bf16x8*>(bp + 16 * PS);
-      const bf16x8 Bl = *reinterpret_cast<const bf16x8*>(bp + 32 * PS);
-      const bf16x8 X0 = px8(xt[0][2 * ch], xt[0][2 * ch + 1]);
-      if (tv1 || w == 7) {
-        const bf16x8 X1 = tv1 ? px8(xt[1][2 * ch], xt[1][2 * ch + 1]) : px8(0x01010101u, 0x01010101u);
-        G[0] = mfma16x16x32(X0, Bl, G[0]);
-        G[1] = mfma16x16x32(X1, Bl, G[1]);
-        G[0] = mfma16x16x32(X0, Bm, G[0]);
-        G[1] = mfma16x16x32(X1, Bm, G[1]);
-        G[0] = mfma16x16x32(X0, Bh, G[0]);
-        G[1] = mfma16x16x32(X1, Bh, G[1]);
-      } else {
-        G[0] = mfma16x16x32(X0, Bl, G[0]);
-        G[0] = mfma16x16x32(X0, Bm, G[0]);
-        G[0] = mfma16x16x32(X0, Bh, G[0]);
-      }
-    }
-    if (hv) {   // wave 7's G[1] is db1, never a weight
-#pragma unroll
-      for (int k = 0; k < NTW; ++k)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) Wt[k][i] -= (k == 0 || tv1) ? lrX * G[k][i] : 0.f;
-    }
-    write_wp();
-  };
-  // wave 7: dW2 / db2 / db1 sums, metrics and the W2 / b1 / b2 update of step sp
-  auto small_update = [&](int sp) {
-    const int pp = sp & 1;
-    const float* rdb2 = reinterpret_cast<const float*>(smem + K_RDB2) + pp * 128;
-    const float* gsrc = rdb2 + (lane >= 16 && lane < 16 + NCLS ? lane - 16 : 0);
-    const f32x4* dw2p = reinterpret_cast<const f32x4*>(smem + K_DW2P) + pp * NBT * 64;
-    f32x4 D = {0.f, 0.f, 0.f, 0.f};
-    float gb = 0.f;
-#pragma unroll
-    for (int v = 0; v < NBT; ++v) {
-      D += dw2p[v * 64 + lane];
-      gb += gsrc[v * 16];
-    }
-    if (lane < 16) gb = G[1][0];
-    if (lane >= 16 + NCLS) gb = 0.f;
-    if (c == 0) {
-      const float* rl = reinterpret_cast<const float*>(smem + K_RLOSS) + pp * 256;
-      const bool hi = lane + 64 < BROWS;
-      const float ls = wave_sum(rl[lane] + (hi ? rl[lane + 64] : 0.f));
-      const float cr = wave_sum(rl[128 + lane] + (hi ? rl[128 + lane + 64] : 0.f));
-      if (lane == 63) {
-        const int sl = (int)((gstep0 + sp) % a.ring);
-        a.metrics[2 * sl] = ls / (float)B;
-        a.metrics[2 * sl + 1] = cr / (float)B;
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (16 * j + 4 * g + i < HID && r < NCLS) w2s[(4 * g + i) * 16 + r] -= lrB * D[i];
-    if (lane < 16) {
-      if (16 * j + lane < HID) b1s[lane] -= lrB * gb;
-    } else if (lane < 16 + NCLS) {
-      b2s[lane - 16] -= lrB * gb;
-    }
-  };
-
-  bool aborted = false;
-  for (int st = 0; st < a.nsteps; ++st) {
-    const unsigned long long sq = seq0 + (unsigned long long)st + 1ull;
-    const unsigned tag = (unsigned)sq;
-    const int par = (int)(sq & 1ull);
-    const int pp = st & 1;
-    const bool more = st + 1 < a.nsteps;
-    if (c == 0 && tid == 0 && a.step_ts != nullptr)
-      a.step_ts[(gstep0 + st) % a.ts_ring] = (long long)__builtin_amdgcn_s_memrealtime();
-    if (w == 0) { PH(0); }
-    if (st > 0) {   // every head of step st - 1 is done: its dz2 pieces, dW2 partials, x^T reads
-      if (!wait_all(F_HEAD, NBT, st)) { give_up(); aborted = true; break; }
-      if (fl[F_ABORT]) { aborted = true; break; }
-    }
-    if (w == 7) {
-      if (more) stage_rows(st + 1, (st + 1) & 1, 0, 1);
-      stage_xt(st);
-      if (st > 0) {
-        wgrad(pp ^ 1);
-        set_flag(F_WUPD + 7, st + 1);
-        small_update(st - 1);
-      }
-      set_flag(F_PRM, st + 1);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      set_flag(F_STAGE, st + 1);
-      read_xt();
-      continue;
-    }
-    // ---------------- waves 0..6: batch tile w
-    const int bw = 16 * w + r;
-    const bool bv = bw < B;
-    f32x4 zs = Zp;
-    if (st > 0) {   // z -= lrX G dz2_{st-1}: A = dz2 (lane: hidden r), B = G^T (lane: batch r)
-      const uint16_t* dz = dzpa + (pp ^ 1) * DZPB + r * PS + 4 * g;
-      f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
-#pragma unroll
-      for (int t = 0; t < NBT; ++t) {
-        const uint2 vh = *reinterpret_cast<const uint2*>(dz + 16 * t);
-        const uint2 vm = *reinterpret_cast<const uint2*>(dz + 16 * PS + 16 * t);
-        const uint2 vl = *reinterpret_cast<const uint2*>(dz + 32 * PS + 16 * t);
-        const f32x4 dh = unbf4(vh.x, vh.y), dm = unbf4(vm.x, vm.y), dl = unbf4(vl.x, vl.y);
-        const f32x4 d = (dh + dm) + dl;   // exact: the pieces of one fp32 value
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii) {
-          if ((t * 4 + ii) & 1) c1 = mfma4(d[ii], GT[t][ii], c1);
-          else c0 = mfma4(d[ii], GT[t][ii], c0);
-        }
-      }
-      zs -= lrX * (c0 + c1);
-    }
-    const auto r1 = region_rsrc(a.xbuf + E1_OFF + (long long)(par * NJ + j) * NQ * NBT * GSLOT, NQ * NBT * GSLOT);
-    put_gran(r1, (q * NBT + w) * GSLOT + 32 * lane, zs, tag, l2_e1);
-    if (w == 0) { PH(1); }
-    if (st > 0) {
-      wgrad(pp ^ 1);
-      set_flag(F_WUPD + w, st + 1);
-    }
-    if (w == 0) { PH(2); }
-    if (!wait_flag(F_PRM, st + 1)) { give_up(); aborted = true; break; }
-    float w2p[4], w2d[4], b1v[4], b2v[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      w2p[e] = w2s[(4 * g + e) * 16 + r];
-      w2d[e] = w2s[r * 16 + 4 * g + e];
-      b1v[e] = b1s[4 * g + e];
-      b2v[e] = b2s[4 * g + e];
-    }
-    const int lab = smem[K_LAB + 128 * pp + bw];
-    f32x4 part[NQ];
-    bool ok = gather_gran<NQ>(r1, [&](int k) { return (k * NBT + w) * GSLOT; }, q, true, 63, tag, zs, part, lane, a);
-    if (w == 0) { PH(3); }
-    f32x4 z = part[0];
-#pragma unroll
-    for (int qq = 1; qq < NQ; ++qq) z += part[qq];
-    float a2[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int hl = 4 * g + i;
-      const float zt = z[i] * (1.f / 255.f) + b1v[i];
-      const float av = ACT == 0 ? __builtin_amdgcn_rcpf(1.f + __expf(-zt)) : fmaxf(zt, 0.f);
-      a2[i] = (16 * j + hl < HID) ? av : 0.f;
-    }
-    f32x4 pl = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) pl = mfma4(w2p[e], a2[e], pl);
-    const auto r2 = region_rsrc(a.xbuf + E2_OFF + (long long)((par * NQ + q) * NBT + w) * NJ * GSLOT, NJ * GSLOT);
-    if (g < 3) put_gran(r2, j * GSLOT + 32 * lane, pl, tag, l2_e2);
-    if (w == 0) { PH(4); }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) a2T[(4 * g + i) * LS + bw] = a2[i];
-    // the next step's forward partial and G while the logits are in flight
-    if (more) {
-      if (!wait_flag(F_STAGE, st + 1) || !wait_all(F_WUPD, 8, st + 1)) { give_up(); aborted = true; break; }
-      p0g((st + 1) & 1, pp, true);
-    }
-    if (w == 0) { PH(5); }
-    f32x4 lp[NJ];
-    ok = gather_gran<NJ>(r2, [&](int k) { return k * GSLOT; }, j, g < 3, 47, tag, pl, lp, lane, a) && ok;
-    if (w == 0) { PH(6); }
-    if (!ok && lane == 0) fl[F_ABORT] = 1;
-    float lg[4], ex[4];
-    float m = -3.0e38f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float v = b2v[i];
-#pragma unroll
-      for (int jj = 0; jj < NJ; ++jj) v += lp[jj][i];
-      lg[i] = v;
-      if (4 * g + i < NCLS) m = fmaxf(m, v);
-    }
-    m = fmaxf(m, xor16(m));
-    m = fmaxf(m, xor32(m));
-    const int y = lab < NCLS ? lab : 0;
-    float ssum = 0.f, zy = 0.f, am = 1e9f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int cl = 4 * g + i;
-      ex[i] = cl < NCLS ? __expf(lg[i] - m) : 0.f;
-      ssum += ex[i];
-      zy += (cl == y) ? lg[i] : 0.f;
-      if (cl < NCLS && lg[i] == m) am = fminf(am, (float)cl);
-    }
-    ssum += xor16(ssum); ssum += xor32(ssum);
-    zy += xor16(zy); zy += xor32(zy);
-    am = fminf(am, xor16(am)); am = fminf(am, xor32(am));
-    const float inv = __builtin_amdgcn_rcpf(ssum);
-    float dz3[4], py = 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int cl = 4 * g + i;
-      const float p = ex[i] * inv;
-      py += (cl == y) ? p : 0.f;
-      dz3[i] = (bv && cl < NCLS) ? p - (cl == y ? 1.f : 0.f) : 0.f;
-    }
-    py += xor16(py); py += xor32(py);
-    const float loss = a.naive ? -__logf(py) : (m + __logf(ssum) - zy);
-    f32x4 da = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) da = mfma4(w2d[e], dz3[e], da);
-    uint16_t* dzo = dzpa + pp * DZPB;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float d = ACT == 0 ? da[i] * a2[i] * (1.f - a2[i]) : (a2[i] > 0.f ? da[i] : 0.f);
-      uint32_t ph, pm, pq;
-      split3(d, ph, pm, pq);
-      const int o = (4 * g + i) * PS + bw;
-      dzo[o] = (uint16_t)(ph >> 16);
-      dzo[16 * PS + o] = (uint16_t)(pm >> 16);
-      dzo[32 * PS + o] = (uint16_t)(pq >> 16);
-      dz3T[(4 * g + i) * LS + bw] = dz3[i];
-    }
-    if (g == 0) {
-      float* rl = reinterpret_cast<float*>(smem + K_RLOSS) + pp * 256;
-      rl[bw] = bv ? loss : 0.f;
-      rl[128 + bw] = (bv && (int)am == y) ? 1.f : 0.f;
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    {
-      const f32x4 av = *reinterpret_cast<const f32x4*>(a2T + r * LS + 16 * w + 4 * g);
-      const f32x4 dv = *reinterpret_cast<const f32x4*>(dz3T + r * LS + 16 * w + 4 * g);
-      const float one = r == 0 ? 1.f : 0.f;
-      f32x4 dp = {0.f, 0.f, 0.f, 0.f}, p2 = dp;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        dp = mfma4(av[e], dv[e], dp);
-        p2 = mfma4(one, dv[e], p2);
-      }
-      reinterpret_cast<f32x4*>(smem + K_DW2P)[(pp * NBT + w) * 64 + lane] = dp;
-      if (g == 0) reinterpret_cast<float*>(smem + K_RDB2)[pp * 128 + w * 16 + r] = p2[0];
-    }
-    if (w == 0) { PH(7); }
-    // x^T of this step (the weight gradient, next step) once wave 7 saw it land
-    if (!wait_flag(F_STAGE, st + 1)) { give_up(); aborted = true; break; }
-    read_xt();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    set_flag(F_HEAD + w, st + 1);
-    if (w == 0) { PH(8); }
-  }
-  if (aborted) return;
-  // ---- the last step's weight gradient, dW2 / b updates, metrics
-  if (!wait_all(F_HEAD, NBT, a.nsteps)) { give_up(); return; }
-  if (fl[F_ABORT]) return;
-  if (a.nsteps > 0) {
-    wgrad((a.nsteps - 1) & 1);
-    if (w == 7) small_update(a.nsteps - 1);
-  }
-  __syncthreads();
-  if (tid == 0) { PRO(c, 3); }
-  if (hv) {
-#pragma unroll
-    for (int k = 0; k < NTW; ++k)
-      if (tvk(k)) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) a.params[(16 * ftk(k) + 4 * g + e) * HID + hid] = Wt[k][e];
-      }
-  }
-  if (q == 0) {
-    if (tid < 256) {
-      const int n = tid >> 4, cl = tid & 15;
-      const int hn = 16 * j + n;
-      if (hn < HID && cl < NCLS) a.params[OFF_W2 + hn * NCLS + cl] = w2s[tid];
-    } else if (tid < 272) {
-      const int hn = 16 * j + (tid - 256);
-      if (hn < HID) a.params[OFF_B1 + hn] = b1s[tid - 256];
-    }
-  }
-  if (c == 0) {
-    if (tid >= 272 && tid < 272 + NCLS) a.params[OFF_B2 + (tid - 272)] = b2s[tid - 272];
-    if (tid == 300) {
-      *a.gstep = gstep0 + a.nsteps;
-      *a.seq = seq0 + (unsigned long long)a.nsteps;
-      if (a.step_ts != nullptr)
-        a.step_ts[(gstep0 + a.nsteps) % a.ts_ring] = (long long)__builtin_amdgcn_s_memrealtime();
-    }
-  }
-  if (tid == 0) { PRO(c, 5); }
-}
-
 // packed placement (a.spread == 0): compute workgroup c runs as blockIdx 8c, so
 // under the observed round-robin dispatch all 28 share ONE XCD (both edges in one
 // L2); the first NCOP other blocks copy, the rest exit.  spread (several ranks on
 // one GPU, tests): compute = blocks 0..27, copiers = 28..43.  Placement is speed
 // only: the census above decides each edge's store flavour.
-template <int ACT, int NW, bool SPLIT, bool LOOK = false>
+template <int ACT, int NW, bool SPLIT>
 __global__ __launch_bounds__(THREADS, 1) void mlp_persist_f32(Args a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int b = blockIdx.x;
@@ -1858,11 +1294,7 @@ __global__ __launch_bounds__(THREADS, 1) void mlp_persist_f32(Args a) {
     if ((b & 7) == 0) c = b >> 3; else cid = b - (b >> 3) - 1;
   }
   if (c >= 0) {
-    if constexpr (LOOK) {
-      if (a.nsteps > 0) compute_look<ACT>(a, c / NQ, c % NQ, smem);
-    } else {
-      if (a.nsteps > 0) compute<ACT, NW, SPLIT>(a, c / NQ, c % NQ, smem);
-    }
+    if (a.nsteps > 0) compute<ACT, NW, SPLIT>(a, c / NQ, c % NQ, smem);
     return;
   }
   if (cid < NCOP) copier(a, cid, smem);
@@ -1893,7 +1325,7 @@ hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int n
                                 void* xbuf, int* err, long long timeout, long long* step_ts, int ts_ring,
                                 const void* host_next, int next_steps, void* stage_next, void* const* peer_base, int W,
                                 int rank, int gbf16, long long* phase_ts, int spread, int xmode, int split,
-                                int look, hipStream_t stream) {
+                                hipStream_t stream) {
   using namespace dtfk::mlpf;
   Args a;
   a.phase_ts = phase_ts;
@@ -1923,7 +1355,6 @@ hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int n
   a.gbf16 = gbf16;
   a.spread = spread;
   a.xmode = xmode;
-  a.look = (look != 0 && W == 1 && split != 0) ? 1 : 0;
   {
     // read once per process (a getenv per launch is host time inside a short timed run)
     static const int gmode = [] {
@@ -1942,13 +1373,13 @@ hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int n
   constexpr size_t lds = LDS_BYTES;
   typedef void (*Kern)(Args);
   // NW: peer-table width the exchange is unrolled for (W rounded up to 2 / 4 / 8)
-  static const Kern kerns[18] = {
+  static const Kern kerns[16] = {
       mlp_persist_f32<0, 1, false>, mlp_persist_f32<1, 1, false>, mlp_persist_f32<0, 2, false>,
       mlp_persist_f32<1, 2, false>, mlp_persist_f32<0, 4, false>, mlp_persist_f32<1, 4, false>,
       mlp_persist_f32<0, 8, false>, mlp_persist_f32<1, 8, false>, mlp_persist_f32<0, 1, true>,
       mlp_persist_f32<1, 1, true>,  mlp_persist_f32<0, 2, true>,  mlp_persist_f32<1, 2, true>,
       mlp_persist_f32<0, 4, true>,  mlp_persist_f32<1, 4, true>,  mlp_persist_f32<0, 8, true>,
-      mlp_persist_f32<1, 8, true>,  mlp_persist_f32<0, 1, true, true>, mlp_persist_f32<1, 1, true, true>};
+      mlp_persist_f32<1, 8, true>};
   static bool attr_set = false;
   if (!attr_set) {
     for (Kern k : kerns) {
@@ -1960,7 +1391,7 @@ hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int n
   }
   if (W < 1 || W > 8 || rank < 0 || rank >= W) return hipErrorInvalidValue;
   const int nwi = W <= 1 ? 0 : (W <= 2 ? 1 : (W <= 4 ? 2 : 3));
-  const int which = a.look ? 16 + (act == 0 ? 0 : 1) : (act == 0 ? 0 : 1) + 2 * nwi + (split ? 8 : 0);
+  const int which = (act == 0 ? 0 : 1) + 2 * nwi + (split ? 8 : 0);
   const int grid = spread ? GRID_SPREAD : GRID_PACKED;
   hipLaunchKernelGGL(kerns[which], dim3(grid), dim3(THREADS), lds, stream, a);
   return hipGetLastError();

@@ -464,7 +464,7 @@ class PersistentMLPRunner:
 
     def __init__(self, trainer: FusedMLPTrainer, epoch, steps_per_launch: int = 550,
                  timeout_s: float = 30.0, precision: str = "fp32", grad_bf16: bool = True,
-                 placement: str = "auto", exchange: str = "one-shot", look: Optional[bool] = None):
+                 placement: str = "auto", exchange: str = "one-shot"):
         C = trainer.C
         if precision not in ("fp32", "fp32-mfma"):
             raise ValueError("precision must be 'fp32' or 'fp32-mfma'")
@@ -494,13 +494,6 @@ class PersistentMLPRunner:
         if placement not in ("packed", "spread"):
             raise ValueError("placement must be 'auto', 'packed' or 'spread'")
         self.placement = placement
-        # one GPU, exact-split engine: the lookahead schedule (the weight update
-        # off the step's critical path, csrc/kernels/mlp_persist_f32.hip
-        # compute_look); DTF_PERSIST_LOOK=1 selects it (off until validated on a GPU)
-        if look is None:
-            look = os.environ.get("DTF_PERSIST_LOOK", "0") != "0"
-        w0 = trainer.world
-        self.look = bool(look) and self.mfma_split and (w0 is None or w0.world_size == 1)
         dev = trainer.device
         self.rec_s = int(C.mlpf_stage_rec())
         self.stages = [torch.zeros(self.g * self.rec_s, dtype=torch.uint8, device=dev) for _ in range(2)]
@@ -548,7 +541,7 @@ class PersistentMLPRunner:
                     self.stages[0], self.stages[1], ep.rec, t.B, t.params, t.lr, t.metrics, t.gstep, self.seq,
                     self.xbuf, self.err, self.timeout_s, t.act, int(t.naive), ep.host, self.step_ts,
                     ipc["ipc_table"], self.W, self.rank, self.grad_bf16, self.placement == "spread",
-                    self.exchange == "two-shot", self.mfma_split, self.look)
+                    self.exchange == "two-shot", self.mfma_split)
             self._plan.launch(par, off if nsteps > 0 else 0, nsteps, nxt[0] * ep.rec, nxt[1])
         else:   # phase stamps (profiling): the generic binding
             st = self.stages[par][off * self.rec_s:] if nsteps > 0 else self.stages[par]
@@ -557,7 +550,7 @@ class PersistentMLPRunner:
                                 host_offset=nxt[0] * ep.rec, next_steps=nxt[1], stage_next=self.stages[dst],
                                 step_ts=self.step_ts, grad_bf16=self.grad_bf16, phase_ts=self.phase_ts,
                                 spread=self.placement == "spread", two_shot=self.exchange == "two-shot",
-                                mfma_split=self.mfma_split, look=self.look, **ipc)
+                                mfma_split=self.mfma_split, **ipc)
         if nxt[1] > 0:
             self.staged[dst] = nxt
         self.last_prefetch_steps = nxt[1]

@@ -273,37 +273,3 @@ def test_bench_two_ranks_timed_run_fault_falls_back(native):
     assert res["config"]["exchange_mode"] != failed[0]
     assert res["value"] > 0 and res["steps"] == 20 and res["n_gpus"] == 2
     assert res["global_steps_timed"] == 20
-
-
-@pytest.mark.parametrize("act", ["sigmoid", "relu"])
-def test_persist_lookahead_schedule_matches_plain(native, act):
-    """The one-GPU lookahead schedule (z_{s+1} = x_{s+1} V_s - lrX (x_{s+1} x_s^T)
-    dz2_s, the weight update off the critical path) trains like the plain
-    schedule: 60 steps over launches of 25 (launch boundaries restart the
-    lookahead), losses and parameters within fp32 rounding, and both track the
-    fp32 reference."""
-    B, nb = 100, 40
-    imgs, labels = synthetic_mnist(B * nb, seed=21)
-    dev = torch.device("cuda")
-    lr = 0.05
-    out = {}
-    for look in (True, False):
-        tr = mlp.FusedMLPTrainer(batch_size=B, lr=lr, act=act, device=dev)
-        p0 = tr.get_params().clone()
-        run = mlp.PersistentMLPRunner(tr, PinnedEpoch(imgs, labels, B), steps_per_launch=25, precision="fp32",
-                                      look=look, timeout_s=3.0)
-        assert run.look == look
-        run.run(60)
-        torch.cuda.synchronize()
-        assert run.error() == 0 and tr.global_step == 60
-        out[look] = (tr.get_params().double(), tr.read_metrics(0, 60))
-    (pl, ml), (pp, mp) = out[True], out[False]
-    d_l, d_p = pl - p0.double(), pp - p0.double()
-    rel = ((d_l - d_p).norm() / d_p.norm()).item()
-    assert rel < 2e-5, rel
-    assert np.allclose(ml[:, 0], mp[:, 0], rtol=1e-5, atol=1e-6), np.abs(ml[:, 0] - mp[:, 0]).max()
-    assert np.array_equal(ml[:, 1], mp[:, 1])
-    batches = [s % nb for s in range(60)]
-    p_ref, losses, _ = _ref_run(p0, imgs, labels, B, batches, lr, act)
-    rel_ref = ((d_l - (p_ref.double() - p0.double())).norm() / d_p.norm()).item()
-    assert rel_ref < 5e-5, rel_ref

@@ -139,6 +139,7 @@ class Server:
         return ok
 
     def _leave(self):
+        self.rdv.stop_heartbeat()
         try:
             self.rdv.store.set(f"left/{self.job_name}/{self.task_index}", b"1")
         except Exception:
@@ -167,6 +168,7 @@ class Server:
             except Exception:
                 break
             time.sleep(0.1)
+        self.rdv.stop_heartbeat()
 
     def _atexit(self):
         self.signal_done()

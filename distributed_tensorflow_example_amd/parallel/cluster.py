@@ -273,8 +273,17 @@ class Rendezvous:
                 dead.append(i)
         return dead
 
-    def close(self):
+    def stop_heartbeat(self, wait_s: float = 2.0):
+        """Stop beating and wait for the thread: a daemon thread still inside a
+        native store call while the interpreter finalises can abort the process
+        (a task that left must not beat into a store the chief is closing)."""
         self._hb_stop.set()
+        t = self._hb_thread
+        if t is not None and t.is_alive() and t is not threading.current_thread():
+            t.join(wait_s)
+
+    def close(self):
+        self.stop_heartbeat()
         try:
             self.store.close()
         except Exception:

@@ -261,10 +261,18 @@ class _EmbeddingBag(torch.autograd.Function):
 
 _SORT_PLAN = [None]   # (key, ids ref, (rows int32 sorted, occ))
 _BAG_OF = [None]      # (key, offsets ref, bag_of int32)
+# bumped around every hipGraph capture (utils/graphs.py): a plan computed
+# eagerly (e.g. by the capture's warmup on the same static input buffers) must
+# never be baked into a graph -- it would freeze the warmup batch's bag map
+_CAPTURE_EPOCH = [0]
+
+
+def bump_capture_epoch() -> None:
+    _CAPTURE_EPOCH[0] += 1
 
 
 def _tkey(t: torch.Tensor):
-    return (t.data_ptr(), t.numel(), t._version)
+    return (t.data_ptr(), t.numel(), t._version, _CAPTURE_EPOCH[0])
 
 
 def register_sorted_ids(ids: torch.Tensor, rows_sorted: torch.Tensor, occ: torch.Tensor) -> None:

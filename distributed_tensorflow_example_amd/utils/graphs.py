@@ -78,9 +78,12 @@ class GraphedStep:
             for _ in range(self.warmup):
                 self.step_fn(*static_in)
         cur.wait_stream(side)
+        from .. import ops
         g = torch.cuda.CUDAGraph()
+        ops.bump_capture_epoch()          # no eager-cached sort / bag plan inside the graph
         with torch.cuda.graph(g):
             out = self.step_fn(*static_in)
+        ops.bump_capture_epoch()          # nor a captured one in later eager calls
         with torch.no_grad():
             for t, s in zip(self.state(), saved):
                 t.copy_(s)

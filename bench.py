@@ -48,7 +48,7 @@ if REPO not in sys.path:
 from distributed_tensorflow_example_amd import _native  # noqa: E402
 from distributed_tensorflow_example_amd.data.mnist import PinnedEpoch, synthetic_mnist  # noqa: E402
 from distributed_tensorflow_example_amd.models.mlp import (  # noqa: E402
-    FusedMLPTrainer, MLPStepRunner, PersistentMLPRunner)
+    FusedMLPTrainer, GemmMLPTrainer, MLPStepRunner, PersistentMLPRunner)
 from distributed_tensorflow_example_amd.parallel import world as world_mod  # noqa: E402
 
 METRIC = "samples/sec (whole node) MNIST MLP sync-SGD at 1/2/4/8 MI355X; step-time p50"
@@ -78,9 +78,10 @@ def main(argv=None):
     ap.add_argument("--prefetch", choices=["serial", "side"], default="serial")
     ap.add_argument("--tune-steps", type=int, default=300,
                     help="N>1: steps used to time each valid exchange strategy before the timed run (0: first valid)")
-    ap.add_argument("--engine", choices=["auto", "persistent", "launches"], default="auto",
-                    help="1 GPU: persistent weight-stationary kernel, one launch per chunk (default), or "
-                         "3 fused launches per step replayed from hipGraphs")
+    ap.add_argument("--engine", choices=["auto", "persistent", "launches", "gemm"], default="auto",
+                    help="persistent weight-stationary kernel, one launch per chunk (auto for batch <= 112); "
+                         "3 fused launches per step replayed from hipGraphs; or the large-batch step on the tiled "
+                         "fp32 MFMA GEMM (auto for batch >= 256), RCCL all-reduce for N > 1")
     ap.add_argument("--allreduce", choices=["auto", "ipc-fused", "ipc-apply", "rccl"], default="auto",
                     help="N>1 gradient exchange: IPC over xGMI inside the wgrad kernel (ipc-fused, default), "
                          "IPC one-shot in a separate reduce+apply kernel (ipc-apply), or RCCL")
@@ -113,7 +114,8 @@ def main(argv=None):
     epoch = PinnedEpoch(imgs, labels, a.batch)
     gd = torch.bfloat16 if a.grad_dtype == "bf16" else torch.float32
 
-    can_persist = a.batch <= 112 and a.engine != "launches"
+    can_persist = a.batch <= 112 and a.engine in ("auto", "persistent")
+    use_gemm = a.engine == "gemm" or (a.engine == "auto" and a.batch >= 256)
     # persistent engine: the warmup is split into a validation part (setup,
     # consistency check, exchange tuning) and a final short launch issued right
     # before the timed region, so the GPU is not coming out of an idle clock
@@ -126,9 +128,12 @@ def main(argv=None):
         """mode: 'persistent' / 'persistent-2shot' (one launch per chunk, in-kernel
         N-GPU exchange: one-shot or reduce-scatter + all-gather) or the 3-launch
         path's gradient exchange ('ipc-fused' / 'ipc-apply' / 'rccl')."""
-        trainer = FusedMLPTrainer(batch_size=a.batch, lr=a.lr, act=a.act, world=w, grad_dtype=gd,
-                                  device=dev, allreduce="rccl" if mode.startswith("persistent") else mode,
-                                  ipc_timeout_s=a.exchange_timeout)
+        if mode == "gemm":
+            trainer = GemmMLPTrainer(batch_size=a.batch, lr=a.lr, act=a.act, world=w, device=dev)
+        else:
+            trainer = FusedMLPTrainer(batch_size=a.batch, lr=a.lr, act=a.act, world=w, grad_dtype=gd,
+                                      device=dev, allreduce="rccl" if mode.startswith("persistent") else mode,
+                                      ipc_timeout_s=a.exchange_timeout)
         if mode.startswith("persistent"):
             runner = PersistentMLPRunner(trainer, epoch, steps_per_launch=a.steps_per_launch,
                                          timeout_s=a.exchange_timeout, precision=a.precision,
@@ -167,7 +172,9 @@ def main(argv=None):
 
     # fallback chain: persistent (in-kernel exchange) -> 3 launches with the IPC
     # exchange inside the wgrad kernel -> separate IPC reduce+apply -> RCCL
-    if w.world_size == 1:
+    if use_gemm:
+        chain = ["gemm"]
+    elif w.world_size == 1:
         chain = ["persistent"] if can_persist else ["rccl"]
     else:
         chain = {"auto": ["ipc-fused", "ipc-apply", "rccl"], "ipc-fused": ["ipc-fused"],
@@ -336,7 +343,7 @@ def main(argv=None):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32" if persistent else "bf16",
+            "dtype": "fp32" if persistent or mode == "gemm" else "bf16",
             "data": ("synthetic MNIST-shaped uint8 resident in pinned host memory, streamed per chunk over PCIe "
                      + ("by copier workgroups inside the persistent launch" if persistent else
                         "by hipMemcpyAsync inside the chunk's hipGraph") + "; random-init weights"),
@@ -350,8 +357,8 @@ def main(argv=None):
                 "grad_allreduce": ("none" if n == 1 else
                                    f"{a.grad_dtype} in-kernel {'two-shot' if mode == 'persistent-2shot' else 'one-shot'}"
                                    " over IPC/xGMI"
-                                   if persistent else f"{a.grad_dtype} {trainer.allreduce}"),
-                "engine": f"persistent-{a.precision}" if persistent else "launches",
+                                   if persistent else f"{'fp32' if mode == 'gemm' else a.grad_dtype} {trainer.allreduce}"),
+                "engine": f"persistent-{a.precision}" if persistent else ("gemm" if mode == "gemm" else "launches"),
                 "exchange_mode": mode,
                 "fallbacks": fallbacks or None,
                 "copy_only_launches_in_timed_run": cold_timed,
@@ -366,7 +373,9 @@ def main(argv=None):
                                            "weights",
                                "fp32-mfma": "fp32 MFMA operands (v_mfma_f32_16x16x4_f32, exact f32 products), "
                                        "fp32 accumulate, fp32 master weights"}[a.precision]
-                              if persistent else "bf16 MFMA operands, fp32 accumulate, fp32 master weights"),
+                              if persistent else
+                              "fp32 MFMA operands (v_mfma_f32_16x16x4_f32), fp32 accumulate, fp32 master weights"
+                              if mode == "gemm" else "bf16 MFMA operands, fp32 accumulate, fp32 master weights"),
             },
             "native_src_hash": _native.src_hash(),
             "final_loss": round(float(m[0]), 5),

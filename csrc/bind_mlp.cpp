@@ -28,6 +28,14 @@ hipError_t dtfk_mlp_wgrad(const void* x, int x_kind, const void* dz2T, int BP, i
 hipError_t dtfk_mlp_apply_flat(float* params, const void* grads, int grad_kind, const float* lr,
                                float scale, void* W1T, void* W2T, void* W2N, hipStream_t stream);
 int dtfk_mlp_ipc_flag_bytes();
+int dtfk_mlpg_p1_floats();
+void dtfk_mlpg_set_stop(int s);
+hipError_t dtfk_mlpg_fwd(const void* x, const void* labels, int B, int BP, const void* W1S, const float* params,
+                         float* P1, void* dz2S, int act, int naive, float gscale, hipStream_t s);
+hipError_t dtfk_mlpg_wgrad(const void* x, int B, int BP, const void* dz2S, float* P2, int nchunk, hipStream_t s);
+hipError_t dtfk_mlpg_apply(float* params, const float* P1, int n1, const float* P2, int n2, const float* gin,
+                           float* gout, const float* lr, float scale, void* W1S, float* metrics, int ring,
+                           long long* gstep, int B, int mode, hipStream_t s);
 hipError_t dtfk_mlp_ipc_reduce_apply(float* params, void* const* peer_table, int W, int rank, int parity,
                                      long long slot_bytes, const long long* gstep, const float* lr, float scale,
                                      void* W1T, void* W2T, void* W2N, int* err, long long timeout_ticks,
@@ -266,6 +274,66 @@ void mlp_apply_flat(at::Tensor params, c10::optional<at::Tensor> grads, at::Tens
                                 (float)scale, W1T.data_ptr(), W2T.data_ptr(), W2N.data_ptr(),
                                 cur_stream()),
             "mlp_apply_flat");
+}
+
+// ---- large-batch GEMM step (kernels/mlp_gemm.hip); x / labels: u8 stage at a byte offset
+static const uint8_t* stage_ptr(const at::Tensor& st, int64_t off, int64_t nbytes, const char* name) {
+  need(st, at::kByte, -1, name);
+  if (off < 0 || off + nbytes > st.numel()) throw std::runtime_error(std::string(name) + ": offset out of range");
+  return st.data_ptr<uint8_t>() + off;
+}
+
+static int64_t mlpg_bp(int B) { return ((int64_t)B + 63) / 64 * 64; }
+
+void mlpg_fwd(at::Tensor x, int64_t x_off, at::Tensor labels, int64_t labels_off, int B, at::Tensor W1S,
+              at::Tensor params, at::Tensor P1, at::Tensor dz2S, int act, bool naive, double gscale) {
+  const int64_t BP = mlpg_bp(B);
+  if (B < 1) throw std::runtime_error("mlpg_fwd: B >= 1");
+  const uint8_t* px = stage_ptr(x, x_off, (int64_t)B * 784, "x");
+  if (reinterpret_cast<uintptr_t>(px) & 15) throw std::runtime_error("mlpg_fwd: x must be 16-byte aligned");
+  const uint8_t* pl = stage_ptr(labels, labels_off, B, "labels");
+  need(W1S, at::kBFloat16, 3 * 112 * 800, "W1S");
+  need(params, at::kFloat, kNParam, "params");
+  need(P1, at::kFloat, BP / 64 * dtfk_mlpg_p1_floats(), "P1");
+  need(dz2S, at::kBFloat16, 3 * 112 * BP, "dz2S");
+  hip_check(dtfk_mlpg_fwd(px, pl, B, (int)BP, W1S.data_ptr(), params.data_ptr<float>(), P1.data_ptr<float>(),
+                          dz2S.data_ptr(), act, naive ? 1 : 0, (float)gscale, cur_stream()),
+            "mlpg_fwd");
+}
+
+void mlpg_wgrad(at::Tensor x, int64_t x_off, int B, at::Tensor dz2S, at::Tensor P2, int nchunk) {
+  const int64_t BP = mlpg_bp(B);
+  const uint8_t* px = stage_ptr(x, x_off, (int64_t)B * 784, "x");
+  if (reinterpret_cast<uintptr_t>(px) & 15) throw std::runtime_error("mlpg_wgrad: x must be 16-byte aligned");
+  if (nchunk < 1 || (BP / 32) % nchunk) throw std::runtime_error("mlpg_wgrad: nchunk must divide ceil64(B)/32");
+  need(dz2S, at::kBFloat16, 3 * 112 * BP, "dz2S");
+  need(P2, at::kFloat, (int64_t)nchunk * 78400, "P2");
+  hip_check(dtfk_mlpg_wgrad(px, B, (int)BP, dz2S.data_ptr(), P2.data_ptr<float>(), nchunk, cur_stream()),
+            "mlpg_wgrad");
+}
+
+void mlpg_apply(at::Tensor params, at::Tensor P1, at::Tensor P2, int nchunk, c10::optional<at::Tensor> gin,
+                c10::optional<at::Tensor> gout, at::Tensor lr, double scale, at::Tensor W1S, at::Tensor metrics,
+                at::Tensor gstep, int B, int mode) {
+  const int64_t BP = mlpg_bp(B);
+  if (mode < 0 || mode > 3) throw std::runtime_error("mlpg_apply: mode 0..3");
+  need(params, at::kFloat, kNParam, "params");
+  need(P1, at::kFloat, BP / 64 * dtfk_mlpg_p1_floats(), "P1");
+  need(P2, at::kFloat, (int64_t)nchunk * 78400, "P2");
+  if (mode == 2 && !gin.has_value()) throw std::runtime_error("mlpg_apply: mode 2 needs gin");
+  if (mode == 1 && !gout.has_value()) throw std::runtime_error("mlpg_apply: mode 1 needs gout");
+  if (gin.has_value()) need(*gin, at::kFloat, kNParam, "gin");
+  if (gout.has_value()) need(*gout, at::kFloat, kNParam, "gout");
+  need(lr, at::kFloat, 1, "lr");
+  need(W1S, at::kBFloat16, 3 * 112 * 800, "W1S");
+  need(metrics, at::kFloat, 2, "metrics");
+  need(gstep, at::kLong, 1, "gstep");
+  hip_check(dtfk_mlpg_apply(params.data_ptr<float>(), P1.data_ptr<float>(), (int)(BP / 64), P2.data_ptr<float>(),
+                            nchunk, gin.has_value() ? gin->data_ptr<float>() : nullptr,
+                            gout.has_value() ? gout->data_ptr<float>() : nullptr, lr.data_ptr<float>(), (float)scale,
+                            W1S.data_ptr(), metrics.data_ptr<float>(), (int)(metrics.numel() / 2),
+                            reinterpret_cast<long long*>(gstep.data_ptr<int64_t>()), B, mode, cur_stream()),
+            "mlpg_apply");
 }
 
 // hipMemcpyAsync host(pinned) -> device on the *current* stream (graph-capturable).
@@ -734,6 +802,16 @@ void init_mlp(py::module& m) {
   m.def("mlp_ipc_reduce_apply", &mlp_ipc_reduce_apply);
   m.def("mlp_ipc_flag_bytes", &dtfk_mlp_ipc_flag_bytes);
   m.def("memcpy_h2d_async", &memcpy_h2d_async);
+  m.def("mlpg_fwd", &mlpg_fwd, py::arg("x"), py::arg("x_offset"), py::arg("labels"), py::arg("labels_offset"),
+        py::arg("B"), py::arg("W1S"), py::arg("params"), py::arg("P1"), py::arg("dz2S"), py::arg("act"),
+        py::arg("naive"), py::arg("gscale"));
+  m.def("mlpg_wgrad", &mlpg_wgrad, py::arg("x"), py::arg("x_offset"), py::arg("B"), py::arg("dz2S"), py::arg("P2"),
+        py::arg("nchunk"));
+  m.def("mlpg_apply", &mlpg_apply, py::arg("params"), py::arg("P1"), py::arg("P2"), py::arg("nchunk"),
+        py::arg("gin"), py::arg("gout"), py::arg("lr"), py::arg("scale"), py::arg("W1S"), py::arg("metrics"),
+        py::arg("gstep"), py::arg("B"), py::arg("mode"));
+  m.def("mlpg_p1_floats", &dtfk_mlpg_p1_floats);
+  m.def("mlpg_set_stop", &dtfk_mlpg_set_stop);
 }
 
 }  // namespace dtf

@@ -285,6 +285,111 @@ class FusedMLPTrainer:
         self.enqueue_step(x.contiguous(), 0, kind, labels.to(torch.uint8).contiguous(), 0)
 
 
+class GemmMLPTrainer:
+    """Large-batch step of the same model (csrc/kernels/mlp_gemm.hip), 3
+    launches: `mlpg_fwd` (one workgroup per 64 rows: the hidden layer on bf16
+    MFMA with W1 as an exact 3-way bf16 split, then act, logits, softmax-xent,
+    dz2 and this block's dW2/db1/db2 partials without leaving the workgroup),
+    `mlpg_wgrad` (dW1 = x^T dz2 over a pixel-block x batch-chunk grid, dz2 as
+    its exact split) and `mlpg_apply` (fixed-order slab reduction, SGD, W1 split
+    refresh, metrics).  The fused engines contract the batch serially inside
+    one wave per weight tile: right at B=100, 4x too slow at B=4096.  All three
+    launches are graph-capturable, so `MLPStepRunner` replays them exactly like
+    the fused trainer's.  N > 1: the apply kernel first writes the reduced flat
+    fp32 gradient, one RCCL all-reduce, then the apply.
+
+    Same interface as `FusedMLPTrainer` (params / metrics ring / global step)."""
+
+    def __init__(self, batch_size: int = 4096, lr: float = 0.0005, act: str = "sigmoid", world=None,
+                 naive_loss: bool = False, metrics_ring: int = 8192, seed: int = 1, device=None,
+                 wgrad_chunks: Optional[int] = None, **_ignored):
+        self.C = _native.load()
+        self.world = world
+        self.world_size = 1 if world is None else world.world_size
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        dev = self.device
+        B = self.B = int(batch_size)
+        self.BP = (B + 63) // 64 * 64
+        self.act = ACTS[act]
+        self.act_name = act
+        self.naive = bool(naive_loss)
+        f32 = torch.float32
+        # dW1 batch chunks: enough (pixel block x chunk) workgroups to cover the
+        # 256 CUs, each chunk a multiple of 32 rows dividing the padded batch
+        units = self.BP // 32
+        want = int(wgrad_chunks or os.environ.get("DTF_MLPG_CHUNKS", 0) or max(1, min(units, 24)))
+        self.nchunk = max(c for c in range(1, min(want, units) + 1) if units % c == 0)
+        self.params = torch.zeros(NPARAM, dtype=f32, device=dev)
+        self.W1S = torch.zeros(3 * 112 * 800, dtype=torch.bfloat16, device=dev)
+        self.dz2S = torch.zeros(3 * 112 * self.BP, dtype=torch.bfloat16, device=dev)
+        self.P1 = torch.zeros(self.BP // 64 * self.C.mlpg_p1_floats(), dtype=f32, device=dev)
+        self.P2 = torch.zeros(self.nchunk * 78400, dtype=f32, device=dev)
+        self.grads = torch.zeros(NPARAM, dtype=f32, device=dev) if self.world_size > 1 else None
+        self.lr = torch.tensor([lr], dtype=f32, device=dev)
+        self.ring = int(metrics_ring)
+        self.metrics = torch.zeros(self.ring * 2, dtype=f32, device=dev)
+        self.gstep = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.allreduce = "rccl" if self.world_size > 1 else "none"
+        self.ipc_parity = 0
+        self.shadows_stale = False
+        self.set_params(init_params(seed))
+
+    def ipc_error(self) -> int:
+        return 0
+
+    def _apply(self, mode: int, gin=None, gout=None, scale: float = 1.0):
+        self.C.mlpg_apply(self.params, self.P1, self.P2, self.nchunk, gin, gout, self.lr, scale, self.W1S,
+                          self.metrics, self.gstep, self.B, mode)
+
+    def set_params(self, flat_cpu: torch.Tensor, broadcast: bool = True):
+        self.params.copy_(flat_cpu.to(self.device, torch.float32))
+        if broadcast and self.world is not None and self.world_size > 1:
+            self.world.broadcast(self.params, 0)
+        self.refresh_shadows()
+
+    def refresh_shadows(self):
+        self._apply(3)
+
+    def get_params(self) -> torch.Tensor:
+        return self.params.detach().cpu()
+
+    def set_lr(self, lr: float):
+        self.lr.fill_(lr)
+
+    @property
+    def global_step(self) -> int:
+        return int(self.gstep.item())
+
+    def set_global_step(self, v: int):
+        self.gstep.fill_(int(v))
+
+    def read_metrics(self, first_step: int, last_step: int) -> np.ndarray:
+        m = self.metrics.view(self.ring, 2).cpu().numpy()
+        return m[np.arange(first_step, last_step) % self.ring]
+
+    def enqueue_step(self, x: torch.Tensor, x_off: int, x_kind: int, labels: torch.Tensor,
+                     labels_off: int, ipc_parity: Optional[int] = None):
+        """x: u8 stage holding B rows of 784 pixels at byte offset x_off; labels: u8 class ids."""
+        if x_kind != 0:
+            raise ValueError("GemmMLPTrainer reads uint8 pixel records (x_kind 0)")
+        C, B = self.C, self.B
+        C.mlpg_fwd(x, x_off, labels, labels_off, B, self.W1S, self.params, self.P1, self.dz2S, self.act,
+                   self.naive, 1.0 / B)
+        C.mlpg_wgrad(x, x_off, B, self.dz2S, self.P2, self.nchunk)
+        if self.world_size == 1:
+            self._apply(0)
+        else:
+            self._apply(1, gout=self.grads)
+            self.world.comm.all_reduce(self.grads, "sum")
+            self._apply(2, gin=self.grads, scale=1.0 / self.world_size)
+
+    def step_tensors(self, x: torch.Tensor, labels: torch.Tensor):
+        """Eager step on device tensors (x: uint8 [B,784], labels [B])."""
+        if x.dtype != torch.uint8:
+            raise ValueError("GemmMLPTrainer.step_tensors takes uint8 pixels")
+        self.enqueue_step(x.contiguous().view(-1), 0, 0, labels.to(torch.uint8).contiguous(), 0)
+
+
 class MLPStepRunner:
     """Drives `FusedMLPTrainer` over a pinned-host epoch.
 

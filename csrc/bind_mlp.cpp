@@ -32,7 +32,9 @@ int dtfk_mlpg_p1_floats();
 void dtfk_mlpg_set_stop(int s);
 hipError_t dtfk_mlpg_fwd(const void* x, const void* labels, int B, int BP, const void* W1S, const float* params,
                          float* P1, void* dz2S, int act, int naive, float gscale, hipStream_t s);
-hipError_t dtfk_mlpg_wgrad(const void* x, int B, int BP, const void* dz2S, float* P2, int nchunk, hipStream_t s);
+hipError_t dtfk_mlpg_wgrad(const void* x, int B, const void* dz2F, float* P2, int nchunk, hipStream_t s);
+int dtfk_mlpg_wchunk();
+int dtfk_mlpg_p2_floats();
 hipError_t dtfk_mlpg_apply(float* params, const float* P1, int n1, const float* P2, int n2, const float* gin,
                            float* gout, const float* lr, float scale, void* W1S, float* metrics, int ring,
                            long long* gstep, int B, int mode, hipStream_t s);
@@ -284,6 +286,11 @@ static const uint8_t* stage_ptr(const at::Tensor& st, int64_t off, int64_t nbyte
 }
 
 static int64_t mlpg_bp(int B) { return ((int64_t)B + 63) / 64 * 64; }
+static int64_t mlpg_bp2(int B) {
+  const int64_t c = dtfk_mlpg_wchunk();
+  return ((int64_t)B + c - 1) / c * c;
+}
+
 
 void mlpg_fwd(at::Tensor x, int64_t x_off, at::Tensor labels, int64_t labels_off, int B, at::Tensor W1S,
               at::Tensor params, at::Tensor P1, at::Tensor dz2S, int act, bool naive, double gscale) {
@@ -295,21 +302,20 @@ void mlpg_fwd(at::Tensor x, int64_t x_off, at::Tensor labels, int64_t labels_off
   need(W1S, at::kBFloat16, 3 * 112 * 800, "W1S");
   need(params, at::kFloat, kNParam, "params");
   need(P1, at::kFloat, BP / 64 * dtfk_mlpg_p1_floats(), "P1");
-  need(dz2S, at::kBFloat16, 3 * 112 * BP, "dz2S");
+  need(dz2S, at::kBFloat16, 3 * 112 * mlpg_bp2(B), "dz2S");
   hip_check(dtfk_mlpg_fwd(px, pl, B, (int)BP, W1S.data_ptr(), params.data_ptr<float>(), P1.data_ptr<float>(),
                           dz2S.data_ptr(), act, naive ? 1 : 0, (float)gscale, cur_stream()),
             "mlpg_fwd");
 }
 
-void mlpg_wgrad(at::Tensor x, int64_t x_off, int B, at::Tensor dz2S, at::Tensor P2, int nchunk) {
-  const int64_t BP = mlpg_bp(B);
+void mlpg_wgrad(at::Tensor x, int64_t x_off, int B, at::Tensor dz2F, at::Tensor P2, int nchunk) {
+  const int64_t BP2 = mlpg_bp2(B);
   const uint8_t* px = stage_ptr(x, x_off, (int64_t)B * 784, "x");
   if (reinterpret_cast<uintptr_t>(px) & 15) throw std::runtime_error("mlpg_wgrad: x must be 16-byte aligned");
-  if (nchunk < 1 || (BP / 32) % nchunk) throw std::runtime_error("mlpg_wgrad: nchunk must divide ceil64(B)/32");
-  need(dz2S, at::kBFloat16, 3 * 112 * BP, "dz2S");
-  need(P2, at::kFloat, (int64_t)nchunk * 78400, "P2");
-  hip_check(dtfk_mlpg_wgrad(px, B, (int)BP, dz2S.data_ptr(), P2.data_ptr<float>(), nchunk, cur_stream()),
-            "mlpg_wgrad");
+  if (nchunk != BP2 / dtfk_mlpg_wchunk()) throw std::runtime_error("mlpg_wgrad: nchunk must be ceil(B / chunk)");
+  need(dz2F, at::kBFloat16, 3 * 112 * BP2, "dz2F");
+  need(P2, at::kFloat, (int64_t)nchunk * dtfk_mlpg_p2_floats(), "P2");
+  hip_check(dtfk_mlpg_wgrad(px, B, dz2F.data_ptr(), P2.data_ptr<float>(), nchunk, cur_stream()), "mlpg_wgrad");
 }
 
 void mlpg_apply(at::Tensor params, at::Tensor P1, at::Tensor P2, int nchunk, c10::optional<at::Tensor> gin,
@@ -319,7 +325,7 @@ void mlpg_apply(at::Tensor params, at::Tensor P1, at::Tensor P2, int nchunk, c10
   if (mode < 0 || mode > 3) throw std::runtime_error("mlpg_apply: mode 0..3");
   need(params, at::kFloat, kNParam, "params");
   need(P1, at::kFloat, BP / 64 * dtfk_mlpg_p1_floats(), "P1");
-  need(P2, at::kFloat, (int64_t)nchunk * 78400, "P2");
+  need(P2, at::kFloat, (int64_t)nchunk * dtfk_mlpg_p2_floats(), "P2");
   if (mode == 2 && !gin.has_value()) throw std::runtime_error("mlpg_apply: mode 2 needs gin");
   if (mode == 1 && !gout.has_value()) throw std::runtime_error("mlpg_apply: mode 1 needs gout");
   if (gin.has_value()) need(*gin, at::kFloat, kNParam, "gin");
@@ -811,6 +817,8 @@ void init_mlp(py::module& m) {
         py::arg("gin"), py::arg("gout"), py::arg("lr"), py::arg("scale"), py::arg("W1S"), py::arg("metrics"),
         py::arg("gstep"), py::arg("B"), py::arg("mode"));
   m.def("mlpg_p1_floats", &dtfk_mlpg_p1_floats);
+  m.def("mlpg_wchunk", &dtfk_mlpg_wchunk);
+  m.def("mlpg_p2_floats", &dtfk_mlpg_p2_floats);
   m.def("mlpg_set_stop", &dtfk_mlpg_set_stop);
 }
 

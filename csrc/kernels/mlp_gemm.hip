@@ -7,24 +7,30 @@
 // better here: [B,784]x[784,100] has 2*ceil(B/64) 64x64 tiles, i.e. 32 f32-MFMA
 // workgroups at B=1024 (57 us, rocprofv3).  This step is shaped for the batch:
 //
-//   mlpg_fwd    one workgroup per 64 rows (4 waves x 16 rows x all 112 hidden
-//               columns): z = x W1 on bf16 MFMA with W1 as an exact 3-way bf16
-//               split (hi + mid + lo == the fp32 weight; uint8 pixels are exact
-//               in bf16) -> exact products, fp32 accumulate; then, per row and
-//               without leaving the workgroup, a2 = act(z/255 + b1), logits,
-//               softmax-xent, dlog, dz2 = (dlog W2^T) act'(a2), and this block's
-//               partial dW2 / db1 / db2 / loss / correct (slab P1).  dz2 leaves
-//               as its exact 3-way split, hidden-major [3][112][BP] bf16.
-//   mlpg_wgrad  dW1 = x^T dz2 / 255 over a (pixel block x batch chunk) grid:
-//               x tiles transposed into LDS as bf16, dz2 split from LDS,
-//               3 MFMAs per tile and k-step; one fp32 slab per batch chunk (P2).
+//   mlpg_fwd    one workgroup per 64 rows; its 4 waves split the 25 k-steps
+//               and each covers all 64 x 112 outputs, so every operand is
+//               loaded once per workgroup straight into MFMA fragments (W1 is
+//               kept as a fragment image, 1 KB coalesced loads), with the next
+//               k-step's loads in flight under 84 MFMAs and no barrier in the
+//               K loop.  W1 rides as an exact 3-way bf16 split (hi + mid + lo
+//               == the fp32 weight; uint8 pixels are exact in bf16): exact
+//               products, fp32 accumulate.  Partials meet in LDS, then per
+//               row: a2 = act(z/255 + b1), logits, softmax-xent, dlog,
+//               dz2 = (dlog W2^T) act'(a2) and this block's [dW2; db2] on
+//               exact-f32 MFMA.  dz2 leaves as its exact split, in the
+//               weight-gradient kernel's fragment order.
+//   mlpg_wgrad  [dW1; db1] = [x | 255]^T dz2 / 255 per (64-pixel block,
+//               256-row chunk): waves split the chunk, x tiles transposed
+//               through wave-private LDS, dz2 straight from its fragment
+//               image; one fp32 slab per chunk.
 //   mlpg_apply  sums the slabs in a fixed order (deterministic), SGD, refreshes
-//               the W1 split, metrics ring + global step.  N > 1: the same
-//               kernel first writes the reduced gradient (RCCL all-reduce), then
-//               applies it.
+//               the W1 fragment image, metrics ring + global step.  N > 1: the
+//               same kernel first writes the reduced gradient (RCCL
+//               all-reduce), then applies it.
 //
-// Every staged operand goes global -> registers (one k-step ahead) -> LDS
-// (double-buffered, one barrier per k-step).
+// Measured (scripts/probes/mlpg_stages.py) -- the first cut staged operands
+// through LDS with one barrier per k-step and paid a full load latency per
+// k-step (a load under a branch, and a HIP uint4 array kept in scratch).
 #include "common.h"
 
 namespace dtfk {
@@ -33,24 +39,23 @@ namespace mlpg {
 constexpr int DIN = 784, DINP = 800, HID = 100, HIDP = 112, NCLS = 10;
 constexpr int OFF_W2 = 78400, OFF_B1 = 79400, OFF_B2 = 79500, NPARAM = 79510;
 constexpr int KSTEPS = DINP / 32;          // 25
-constexpr int BLD = 40;                    // LDS row stride (bf16) of a staged 32-wide k slice
-constexpr int SLICE = 3 * HIDP * BLD;      // one staged [3][112][32] slice
-constexpr int SLICE_CHUNKS = 3 * HIDP * 4; // 16-byte chunks per slice (1344)
 constexpr int R1 = 64;                     // rows per mlpg_fwd block
-constexpr int ALD = 101;                   // LDS row stride (fp32) of a2 / dz2 (odd: row-varying reads conflict-free)
-constexpr int P1N = 1112;                  // [dW2 1000 | db1 100 | db2 10 | loss | correct]
+constexpr int P1N = 1112;                  // [dW2 1000 | (unused 100) | db2 10 | loss | correct]
 constexpr int XTLD = 40;                   // LDS row stride (bf16) of a transposed x tile [64 px][32 batch]
+// register staging in native vectors (an array of HIP's struct uint4 stayed in scratch memory)
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ bf16x8 u8x8_to_bf16(uint2 w) {
+__device__ __forceinline__ bf16x8 u8x8_to_bf16(u32x2 w) {
   // integers 0..255 are exact in bf16
   uint32_t p[4];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    const uint32_t v = j == 0 ? w.x : w.y;
+    const uint32_t v = w[j];
     p[2 * j] = pack2bf((float)(v & 255u), (float)((v >> 8) & 255u));
     p[2 * j + 1] = pack2bf((float)((v >> 16) & 255u), (float)(v >> 24));
   }
-  return __builtin_bit_cast(bf16x8, make_uint4(p[0], p[1], p[2], p[3]));
+  return __builtin_bit_cast(bf16x8, u32x4{p[0], p[1], p[2], p[3]});
 }
 
 // fp32 -> hi + mid + lo bf16, exact for normal values (8 + 8 + 8 mantissa bits)
@@ -61,205 +66,318 @@ __device__ __forceinline__ void split3(float v, uint16_t& h, uint16_t& m, uint16
   l = f2bf(r1 - bf2f(m));
 }
 
-// [3][112][ld] bf16 operand, 32-wide k slice at column k0 -> registers
-__device__ __forceinline__ void load_slice(const uint16_t* __restrict__ src, long long ld, int k0, uint4 (&v)[6]) {
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    const int c = threadIdx.x + 256 * i;
-    if (c < SLICE_CHUNKS) {
-      const int row = c >> 2, q = c & 3;   // row = s * 112 + n
-      v[i] = *reinterpret_cast<const uint4*>(src + (size_t)row * ld + k0 + 8 * q);
-    }
-  }
-}
-__device__ __forceinline__ void store_slice(uint16_t* dst, const uint4 (&v)[6]) {
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    const int c = threadIdx.x + 256 * i;
-    if (c < SLICE_CHUNKS) *reinterpret_cast<uint4*>(dst + (c >> 2) * BLD + 8 * (c & 3)) = v[i];
-  }
+// W1 as MFMA B fragments: [ks 25][split 3][col tile 7][lane 64][8] bf16, so each
+// (k-step, split, col tile) fragment is one coalesced 1 KB wave load.  Pads
+// (hidden >= 100, pixel >= 784) stay zero.
+__device__ __forceinline__ size_t w1f_index(int k, int n, int s) {
+  const int ks = k >> 5, kk = k & 31;
+  const int lane = (kk >> 3) * 16 + (n & 15);
+  return ((((size_t)ks * 3 + s) * 7 + (n >> 4)) * 64 + lane) * 8 + (kk & 7);
 }
 
-__global__ __launch_bounds__(256) void mlpg_fwd(const uint8_t* __restrict__ x, const uint8_t* __restrict__ labels,
-                                                int B, int BP, const uint16_t* __restrict__ W1S,
-                                                const float* __restrict__ params, float* __restrict__ P1,
-                                                uint16_t* __restrict__ dz2S, int act, int naive, float gscale,
-                                                int stop) {
-  __shared__ __attribute__((aligned(16))) uint16_t bs[2 * SLICE];   // 53.8 KB; a2 / dz2 after the K loop
-  __shared__ float w2[HID * NCLS], b2[NCLS], lg[R1][NCLS + 1], dl[R1][NCLS + 1], red[2][R1];
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+__device__ __forceinline__ f32x4 mfma16x16x4f32(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+constexpr int NW = 4;            // waves per mlpg_fwd block: they split K, each covers all 64 x 112 outputs
+constexpr int NT = 28;           // 4 row tiles x 7 col tiles
+constexpr int ZLD = 113;         // LDS row stride (fp32) of a2 / dz2 after the reduction
+
+// One block per 64 rows.  Wave w contracts k-steps w, w+4, ... for every
+// output tile, B fragments straight from the fragment image (no LDS staging,
+// no barrier in the K loop), next k-step's loads in flight under this one's 84
+// MFMAs.  The 4 partial sums meet in LDS (each tile summed by one owner wave in
+// wave order: deterministic), then the head runs on exact-f32 MFMA.
+__global__ __launch_bounds__(256, 1) void mlpg_fwd(const uint8_t* __restrict__ x, const uint8_t* __restrict__ labels,
+                                                   int B, int BP, const uint16_t* __restrict__ W1F,
+                                                   const float* __restrict__ params, float* __restrict__ P1,
+                                                   uint16_t* __restrict__ dz2S, int act, int naive, float gscale,
+                                                   int stop) {
+  __shared__ __attribute__((aligned(16))) float zred[NW * NT * 256];   // 112 KB; a2 / dz2 after the reduction
+  __shared__ float w2[HID * NCLS], b2[16], b1[HIDP], dls[R1][16], lred[2][NW];
+  __shared__ int lab[R1];
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int lr = lane & 15, lg4 = lane >> 4;
   const int r0 = blockIdx.x * R1;
-  const int row = r0 + wave * 16 + (lane & 15);
-  const int kq = 8 * (lane >> 4);
-  const uint8_t* xr = x + (size_t)min(row, B - 1) * DIN;
-  for (int i = t; i < HID * NCLS; i += 256) w2[i] = params[OFF_W2 + i];
-  if (t < NCLS) b2[t] = params[OFF_B2 + t];
+  // small operands into registers now, into LDS after the K loop (a load
+  // waited for here would stall the K loop's start)
+  float pw[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) pw[k] = params[OFF_W2 + min(t + 256 * k, HID * NCLS - 1)];
+  const float pb1 = params[OFF_B1 + min(t, HID - 1)];
+  const float pb2 = params[OFF_B2 + min(t, NCLS - 1)];
+  const int plab = labels[min(r0 + (t & 63), B - 1)];
 
-  f32x4 acc[7];
+  const uint8_t* xr[4];
 #pragma unroll
-  for (int j = 0; j < 7; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  uint4 v[6];
-  uint2 xa = make_uint2(0u, 0u);
-  load_slice(W1S, DINP, 0, v);
-  if (row < B) xa = *reinterpret_cast<const uint2*>(xr + kq);
-  for (int ks = 0; ks < KSTEPS; ++ks) {
-    uint16_t* cur = bs + (ks & 1) * SLICE;
-    store_slice(cur, v);
-    const bf16x8 a = u8x8_to_bf16(xa);
-    __syncthreads();
-    if (ks + 1 < KSTEPS) {
-      load_slice(W1S, DINP, (ks + 1) * 32, v);
-      const int k = (ks + 1) * 32 + kq;
-      xa = (row < B && k < DIN) ? *reinterpret_cast<const uint2*>(xr + k) : make_uint2(0u, 0u);
+  for (int rt = 0; rt < 4; ++rt) xr[rt] = x + (size_t)min(r0 + 16 * rt + lr, B - 1) * DIN;   // rows >= B: grads zeroed
+  const bf16x8* wf = reinterpret_cast<const bf16x8*>(W1F) + lane;
+  f32x4 acc[4][7];
+#pragma unroll
+  for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+    for (int ct = 0; ct < 7; ++ct) acc[rt][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // 7 k-steps per wave, fully unrolled, the next k-step's loads in flight
+  // under this one's MFMAs; waves 1-3 run a 7th, all-zero step (ks >= 25
+  // re-reads step 24 and multiplies a zero x fragment) -- no branch around a
+  // load, so the compiler's waits stay counted (a conditional load made it
+  // wait for the just-issued next step at every join).  Loading two steps
+  // ahead (3 register sets) measured slower: 15.1 vs 13.0 us (VGPRs spill
+  // into AGPR copies).
+  bf16x8 bq[2][21];
+  u32x2 xq[2][4];
+  auto load = [&](int ks, bf16x8 (&b)[21], u32x2 (&xv)[4]) {
+    const int kc = min(ks, KSTEPS - 1);
+#pragma unroll
+    for (int i = 0; i < 21; ++i) b[i] = wf[((size_t)kc * 21 + i) * 64];   // i = s * 7 + ct
+    // pixels >= 784 re-read 776.. (times W1's zero padding)
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt) xv[rt] = *reinterpret_cast<const u32x2*>(xr[rt] + min(kc * 32 + 8 * lg4, DIN - 8));
+  };
+  auto compute = [&](int ks, const bf16x8 (&b)[21], const u32x2 (&xv)[4]) {
+    const bool live = ks < KSTEPS;
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt) {
+      const bf16x8 a = u8x8_to_bf16(live ? xv[rt] : u32x2{0u, 0u});
+#pragma unroll
+      for (int s = 0; s < 3; ++s)
+#pragma unroll
+        for (int ct = 0; ct < 7; ++ct) acc[rt][ct] = mfma16x16x32(a, b[s * 7 + ct], acc[rt][ct]);
     }
-    const uint16_t* bl = cur + (lane & 15) * BLD + kq;
+  };
+  constexpr int KPW = (KSTEPS + NW - 1) / NW;   // 7
+  load(wave, bq[0], xq[0]);
 #pragma unroll
-    for (int j = 0; j < 7; ++j) {
-#pragma unroll
-      for (int s = 0; s < 3; ++s) acc[j] = mfma16x16x32(a, ld_bf16x8(bl + (s * HIDP + j * 16) * BLD), acc[j]);
-    }
+  for (int i = 0; i < KPW; ++i) {
+    if (i + 1 < KPW) load(wave + NW * (i + 1), bq[(i + 1) & 1], xq[(i + 1) & 1]);
+    __builtin_amdgcn_sched_barrier(0);   // the next step's loads go out before this step's MFMAs
+    compute(wave + NW * i, bq[i & 1], xq[i & 1]);
   }
-  __syncthreads();   // the slices are dead: a2 / dz2 reuse the LDS
-  float* a2s = reinterpret_cast<float*>(bs);
-  float* dzs = a2s + R1 * ALD;
 #pragma unroll
-  for (int j = 0; j < 7; ++j) {
-    const int h = j * 16 + (lane & 15);
-    if (h < HID) {
-      const float bb = params[OFF_B1 + h];
+  for (int k = 0; k < 4; ++k)
+    if (t + 256 * k < HID * NCLS) w2[t + 256 * k] = pw[k];
+  if (t < 16) b2[t] = t < NCLS ? pb2 : 0.f;
+  if (t < HIDP) b1[t] = t < HID ? pb1 : 0.f;
+  if (t < R1) lab[t] = plab;
+  // partial sums -> LDS [wave][tile][lane][4]
+  f32x4* zr = reinterpret_cast<f32x4*>(zred);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float z = acc[j][i] * (1.f / 255.f) + bb;
-        a2s[(wave * 16 + 4 * (lane >> 4) + i) * ALD + h] = act == 0 ? sigmoidf_(z) : fmaxf(z, 0.f);
-      }
+  for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+    for (int ct = 0; ct < 7; ++ct) zr[(wave * NT + rt * 7 + ct) * 64 + lane] = acc[rt][ct];
+  __syncthreads();
+  float av[7][4];
+#pragma unroll
+  for (int m = 0; m < 7; ++m) {   // owned tiles: wave + 4m
+    const int tile = wave + NW * m, rt = tile / 7, ct = tile % 7;
+    f32x4 z = zr[tile * 64 + lane];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) z += zr[(w * NT + tile) * 64 + lane];
+    const int h = 16 * ct + lr;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float zz = z[i] * (1.f / 255.f) + b1[h];
+      const float a = act == 0 ? sigmoidf_(zz) : fmaxf(zz, 0.f);
+      av[m][i] = h < HID ? a : (h == HID ? 1.f : 0.f);   // column 100 = 1: db2 rides dW2's product
     }
+    (void)rt;
+  }
+  __syncthreads();   // every partial read: a2 / dz2 reuse the LDS
+  float* a2s = zred;
+  float* dzs = zred + R1 * ZLD;
+#pragma unroll
+  for (int m = 0; m < 7; ++m) {
+    const int tile = wave + NW * m, rt = tile / 7, ct = tile % 7;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a2s[(16 * rt + 4 * lg4 + i) * ZLD + 16 * ct + lr] = av[m][i];
   }
   __syncthreads();
   if (stop == 1) return;
-  for (int o = t; o < R1 * NCLS; o += 256) {   // logits
-    const int r = o / NCLS, c = o % NCLS;
-    float s = b2[c];
-#pragma unroll 10
-    for (int h = 0; h < HID; ++h) s = fmaf(a2s[r * ALD + h], w2[h * NCLS + c], s);
-    lg[r][c] = s;
+  // logits of row tile `wave`: [16 x 100] x [100 x 10] on f32 MFMA (exact products)
+  f32x4 lgt = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 5
+  for (int s = 0; s < HID / 4; ++s) {
+    const int k = 4 * s + lg4;
+    lgt = mfma16x16x4f32(a2s[(16 * wave + lr) * ZLD + k], lr < NCLS ? w2[k * NCLS + lr] : 0.f, lgt);
   }
-  __syncthreads();
-  if (t < R1) {   // softmax-xent of row t
-    float loss = 0.f, corr = 0.f;
-    if (r0 + t < B) {
-      const int y = labels[r0 + t];
-      float m = lg[t][0];
-      int am = 0;
-      for (int c = 1; c < NCLS; ++c)
-        if (lg[t][c] > m) { m = lg[t][c]; am = c; }
-      float s = 0.f;
-      for (int c = 0; c < NCLS; ++c) s += __expf(lg[t][c] - m);
-      const float inv = 1.f / s;
-      loss = naive ? -__logf(__expf(lg[t][y] - m) * inv) : (m + __logf(s)) - lg[t][y];
-      corr = am == y ? 1.f : 0.f;
-      for (int c = 0; c < NCLS; ++c) dl[t][c] = (__expf(lg[t][c] - m) * inv - (c == y ? 1.f : 0.f)) * gscale;
-    } else {
-      for (int c = 0; c < NCLS; ++c) dl[t][c] = 0.f;
+  float lsum = 0.f, csum = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {   // rows 16*wave + 4*lg4 + i, class lr (16-lane DPP rows)
+    const int rl = 16 * wave + 4 * lg4 + i, row = r0 + rl;
+    const bool cv = lr < NCLS;
+    const float z = cv ? lgt[i] + b2[lr] : -INFINITY;
+    const float m = row16_max(z);
+    const float e = cv ? __expf(z - m) : 0.f;
+    const float se = row16_sum(e);
+    float g = 0.f;
+    if (row < B) {
+      const int y = lab[rl];
+      const float zy = row16_sum(lr == y ? z : 0.f);
+      const float ey = row16_sum(lr == y ? e : 0.f);
+      const float am = row16_min(cv && z == m ? (float)lr : 16.f);
+      const float loss = naive ? -__logf(ey / se) : (m + __logf(se)) - zy;
+      if (lr == 0) {
+        lsum += loss;
+        csum += (int)am == y ? 1.f : 0.f;
+      }
+      g = cv ? (e / se - (lr == y ? 1.f : 0.f)) * gscale : 0.f;
     }
-    red[0][t] = loss;
-    red[1][t] = corr;
+    dls[rl][lr] = g;
+  }
+  lsum = wave_sum(lsum);
+  csum = wave_sum(csum);
+  if (lane == 0) {
+    lred[0][wave] = lsum;
+    lred[1][wave] = csum;
   }
   __syncthreads();
   if (stop == 2) return;
-  for (int o = t; o < R1 * HID; o += 256) {   // dz2 (rows fastest: coalesced split stores)
-    const int r = o % R1, h = o / R1;
-    float d = 0.f;
+  // dz2 of row tile `wave` = dl [16 x 10] x W2^T [10 x 100] (K padded to 12), times act'(a2)
 #pragma unroll
-    for (int c = 0; c < NCLS; ++c) d = fmaf(dl[r][c], w2[h * NCLS + c], d);
-    const float av = a2s[r * ALD + h];
-    const float dz = act == 0 ? d * av * (1.f - av) : (av > 0.f ? d : 0.f);
-    dzs[r * ALD + h] = dz;
-    uint16_t hi, mi, lo;
-    split3(dz, hi, mi, lo);
-    const size_t col = (size_t)r0 + r;
-    dz2S[(size_t)h * BP + col] = hi;
-    dz2S[(size_t)(HIDP + h) * BP + col] = mi;
-    dz2S[(size_t)(2 * HIDP + h) * BP + col] = lo;
+  for (int ct = 0; ct < 7; ++ct) {
+    f32x4 d = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int h = 16 * ct + lr;
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const int c = 4 * s + lg4;
+      d = mfma16x16x4f32(dls[16 * wave + lr][c], (c < NCLS && h < HID) ? w2[h * NCLS + c] : 0.f, d);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rl = 16 * wave + 4 * lg4 + i;
+      const float a = a2s[rl * ZLD + h];
+      dzs[rl * ZLD + h] = h < HID ? (act == 0 ? d[i] * a * (1.f - a) : (a > 0.f ? d[i] : 0.f)) : 0.f;
+    }
   }
   __syncthreads();
-  if (stop == 3) return;
-  float* p1 = P1 + (size_t)blockIdx.x * P1N;
-  for (int o = t; o < P1N; o += 256) {   // this block's partial sums
-    float s = 0.f;
-    if (o < HID * NCLS) {
-      const int h = o / NCLS, c = o % NCLS;
-      for (int r = 0; r < R1; ++r) s = fmaf(a2s[r * ALD + h], dl[r][c], s);
-    } else if (o < HID * NCLS + HID) {
-      const int h = o - HID * NCLS;
-      for (int r = 0; r < R1; ++r) s += dzs[r * ALD + h];
-    } else if (o < HID * NCLS + HID + NCLS) {
-      const int c = o - HID * NCLS - HID;
-      for (int r = 0; r < R1; ++r) s += dl[r][c];
-    } else {
-      const int k = o - (HID * NCLS + HID + NCLS);
-      for (int r = 0; r < R1; ++r) s += red[k][r];
+  // dz2 as its exact split in the wgrad's B-fragment image (dz2F: [row/32][split][col tile][lane][8]):
+  // one task = 8 consecutive rows of one hidden unit -> three 16-byte stores
+  for (int task = t; task < (R1 / 8) * HID; task += 256) {
+    const int h = task % HID, rg = task / HID;
+    u32x4 hv, mv, lv;
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+      uint16_t h0, m0, l0, h1, m1, l1;
+      split3(dzs[(8 * rg + e) * ZLD + h], h0, m0, l0);
+      split3(dzs[(8 * rg + e + 1) * ZLD + h], h1, m1, l1);
+      hv[e / 2] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+      mv[e / 2] = (uint32_t)m0 | ((uint32_t)m1 << 16);
+      lv[e / 2] = (uint32_t)l0 | ((uint32_t)l1 << 16);
     }
-    p1[o] = s;
+    const int row = r0 + 8 * rg;
+    const size_t base = (((size_t)(row >> 5) * 3) * 7 + (h >> 4)) * 64 + ((row & 31) >> 3) * 16 + (h & 15);
+    u32x4* dst = reinterpret_cast<u32x4*>(dz2S);
+    dst[base] = hv;
+    dst[base + 7 * 64] = mv;
+    dst[base + 14 * 64] = lv;
+  }
+  if (stop == 3) return;
+  // this block's [dW2; db2] = [a2 | 1]^T dl on f32 MFMA: hidden tiles ct = wave, wave + 4
+  float* p1 = P1 + (size_t)blockIdx.x * P1N;
+  for (int ct = wave; ct < 7; ct += NW) {
+    f32x4 d = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+    for (int s = 0; s < R1 / 4; ++s) {
+      const int r = 4 * s + lg4;
+      d = mfma16x16x4f32(a2s[r * ZLD + 16 * ct + lr], dls[r][lr], d);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int h = 16 * ct + 4 * lg4 + i;
+      if (lr < NCLS) {
+        if (h < HID) p1[h * NCLS + lr] = d[i];
+        else if (h == HID) p1[HID * NCLS + HID + lr] = d[i];
+      }
+    }
+  }
+  if (t == 0) {   // (db1 rides the weight gradient: pixel column 784 == 255 in mlpg_wgrad)
+    float ls = 0.f, cs = 0.f;
+    for (int w = 0; w < NW; ++w) { ls += lred[0][w]; cs += lred[1][w]; }
+    p1[P1N - 2] = ls;
+    p1[P1N - 1] = cs;
   }
 }
 
-// grid (13 pixel blocks of 64, nchunk batch chunks of kchunk rows)
-__global__ __launch_bounds__(256) void mlpg_wgrad(const uint8_t* __restrict__ x, int B, int BP,
-                                                  const uint16_t* __restrict__ dz2S, float* __restrict__ P2,
-                                                  int kchunk) {
-  __shared__ __attribute__((aligned(16))) uint16_t ds[2 * SLICE];
-  __shared__ __attribute__((aligned(16))) uint16_t xs[2 * 64 * XTLD];
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+constexpr int WKPW = 2;                 // mlpg_wgrad: 32-row k-steps per wave (chunk = 4 waves x 2 x 32 = 256 rows)
+constexpr int WCHUNK = NW * WKPW * 32;
+constexpr int P2N = (DIN + 1) * HID;     // one dW1 slab: 784 pixel rows + the db1 row
+
+// [dW1; db1] partial of one 256-row batch chunk for 64 pixels (+ the constant
+// pixel 784 = 255 in the last block: db1 = sum(255 dz2) / 255).  Wave w
+// contracts k-steps w and w+4 for all 4 x 7 output tiles: x rows go through
+// a wave-private LDS tile transposed to [pixel][batch] bf16 (A fragments),
+// dz2 comes straight from its fragment image (B), no block barrier until
+// the 4 partials meet in LDS (owner wave per tile, wave order).
+__global__ __launch_bounds__(256, 1) void mlpg_wgrad(const uint8_t* __restrict__ x, int B,
+                                                     const uint16_t* __restrict__ dz2F, float* __restrict__ P2) {
+  __shared__ __attribute__((aligned(16))) float zred[NW * NT * 256];   // 112 KB (x tiles before the reduction)
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int lr = lane & 15, lg4 = lane >> 4;
   const int p0 = blockIdx.x * 64;
-  const int b0 = blockIdx.y * kchunk, b1 = min(BP, b0 + kchunk);
-  const int kq = 8 * (lane >> 4);
-  // x staging: threads 0..127 load 16 pixels of one batch row
-  const int xb = t >> 2, xq = t & 3;
-  const bool xload = t < 128 && p0 + 16 * xq < DIN;
-  f32x4 acc[7];
+  const int c0 = blockIdx.y * WCHUNK;
+  uint16_t* xt = reinterpret_cast<uint16_t*>(zred) + wave * (WKPW * 64 * XTLD);   // [step][64 px][XTLD]
+  // x: lane -> batch row (lane & 31) of the step, pixels p0 + 32 * (lane >> 5) .. + 32
+  const int xb = lane & 31, xh = lane >> 5;
+  u32x4 xv[WKPW][2];
+  bf16x8 bq[WKPW][21];
+  const bf16x8* df = reinterpret_cast<const bf16x8*>(dz2F) + lane;
 #pragma unroll
-  for (int j = 0; j < 7; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  uint4 v[6];
-  uint4 xv = make_uint4(0u, 0u, 0u, 0u);
-  auto load_x = [&](int k0) {
-    const int r = min(k0 + xb, B - 1);   // rows >= B: dz2 is 0 there
-    xv = xload ? *reinterpret_cast<const uint4*>(x + (size_t)r * DIN + p0 + 16 * xq) : make_uint4(0u, 0u, 0u, 0u);
-  };
-  load_slice(dz2S, BP, b0, v);
-  load_x(b0);
-  for (int k0 = b0; k0 < b1; k0 += 32) {
-    const int par = ((k0 - b0) >> 5) & 1;
-    uint16_t* cur = ds + par * SLICE;
-    uint16_t* xc = xs + par * 64 * XTLD;
-    store_slice(cur, v);
-    if (t < 128) {
-      const uint32_t w[4] = {xv.x, xv.y, xv.z, xv.w};
+  for (int st = 0; st < WKPW; ++st) {
+    const int kb = (c0 >> 5) + wave + NW * st;   // global 32-row k-step
+    const int r = min(32 * kb + xb, B - 1);      // rows >= B: dz2 is 0 there
 #pragma unroll
-      for (int j = 0; j < 16; ++j)
-        xc[(16 * xq + j) * XTLD + xb] = f2bf((float)((w[j >> 2] >> (8 * (j & 3))) & 255u));
-    }
-    __syncthreads();
-    if (k0 + 32 < b1) {
-      load_slice(dz2S, BP, k0 + 32, v);
-      load_x(k0 + 32);
-    }
-    const bf16x8 a = ld_bf16x8(xc + (wave * 16 + (lane & 15)) * XTLD + kq);
-    const uint16_t* bl = cur + (lane & 15) * BLD + kq;
+    for (int q = 0; q < 2; ++q)
+      xv[st][q] = *reinterpret_cast<const u32x4*>(x + (size_t)r * DIN + min(p0 + 32 * xh + 16 * q, DIN - 16));
 #pragma unroll
-    for (int j = 0; j < 7; ++j) {
+    for (int i = 0; i < 21; ++i) bq[st][i] = df[((size_t)kb * 21 + i) * 64];
+  }
 #pragma unroll
-      for (int s = 0; s < 3; ++s) acc[j] = mfma16x16x32(a, ld_bf16x8(bl + (s * HIDP + j * 16) * BLD), acc[j]);
+  for (int st = 0; st < WKPW; ++st) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int pl = 32 * xh + 16 * q + j, p = p0 + pl;
+        const float v = p < DIN ? (float)((xv[st][q][j >> 2] >> (8 * (j & 3))) & 255u) : (p == DIN ? 255.f : 0.f);
+        xt[(st * 64 + pl) * XTLD + xb] = f2bf(v);
+      }
     }
   }
-  float* p2 = P2 + (size_t)blockIdx.y * OFF_W2;
+  f32x4 acc[4][7];
 #pragma unroll
-  for (int j = 0; j < 7; ++j) {
-    const int h = j * 16 + (lane & 15);
-    if (h >= HID) continue;
+  for (int pt = 0; pt < 4; ++pt)
+#pragma unroll
+    for (int ct = 0; ct < 7; ++ct) acc[pt][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int st = 0; st < WKPW; ++st) {
+#pragma unroll
+    for (int pt = 0; pt < 4; ++pt) {
+      const bf16x8 a = ld_bf16x8(xt + (st * 64 + 16 * pt + lr) * XTLD + 8 * lg4);
+#pragma unroll
+      for (int sp = 0; sp < 3; ++sp)
+#pragma unroll
+        for (int ct = 0; ct < 7; ++ct) acc[pt][ct] = mfma16x16x32(a, bq[st][sp * 7 + ct], acc[pt][ct]);
+    }
+  }
+  __syncthreads();   // every wave's x tiles read: the partials reuse the LDS
+  f32x4* zr = reinterpret_cast<f32x4*>(zred);
+#pragma unroll
+  for (int pt = 0; pt < 4; ++pt)
+#pragma unroll
+    for (int ct = 0; ct < 7; ++ct) zr[(wave * NT + pt * 7 + ct) * 64 + lane] = acc[pt][ct];
+  __syncthreads();
+  float* p2 = P2 + (size_t)blockIdx.y * P2N;
+#pragma unroll
+  for (int m = 0; m < 7; ++m) {
+    const int tile = wave + NW * m, pt = tile / 7, ct = tile % 7;
+    f32x4 z = zr[tile * 64 + lane];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) z += zr[(w * NT + tile) * 64 + lane];
+    const int h = 16 * ct + lr;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int p = p0 + wave * 16 + 4 * (lane >> 4) + i;
-      if (p < DIN) p2[(size_t)p * HID + h] = acc[j][i];
+      const int p = p0 + 16 * pt + 4 * lg4 + i;
+      if (h < HID && p <= DIN) p2[(size_t)p * HID + h] = z[i];
     }
   }
 }
@@ -295,9 +413,11 @@ __global__ __launch_bounds__(256) void mlpg_apply(float* __restrict__ params, co
     if (mode == 2) {
       g = gin[i];
     } else if (i < OFF_W2) {
-      g = sum_strided(P2 + i, OFF_W2, n2) * (1.f / 255.f);
+      g = sum_strided(P2 + i, P2N, n2) * (1.f / 255.f);
+    } else if (i >= OFF_B1 && i < OFF_B2) {
+      g = sum_strided(P2 + OFF_W2 + (i - OFF_B1), P2N, n2) * (1.f / 255.f);   // db1 = the pixel-784 row
     } else {
-      const int j = i < OFF_B1 ? i - OFF_W2 : (i < OFF_B2 ? HID * NCLS + (i - OFF_B1) : HID * NCLS + HID + (i - OFF_B2));
+      const int j = i < OFF_B1 ? i - OFF_W2 : HID * NCLS + HID + (i - OFF_B2);
       g = sum_strided(P1 + j, P1N, n1);
     }
     if (mode == 1) gout[i] = g;
@@ -307,9 +427,9 @@ __global__ __launch_bounds__(256) void mlpg_apply(float* __restrict__ params, co
     uint16_t hi, mi, lo;
     split3(params[i], hi, mi, lo);
     const int k = i / HID, n = i % HID;
-    W1S[(size_t)n * DINP + k] = hi;
-    W1S[(size_t)(HIDP + n) * DINP + k] = mi;
-    W1S[(size_t)(2 * HIDP + n) * DINP + k] = lo;
+    W1S[w1f_index(k, n, 0)] = hi;
+    W1S[w1f_index(k, n, 1)] = mi;
+    W1S[w1f_index(k, n, 2)] = lo;
   }
   if (blockIdx.x == 0 && threadIdx.x < 64 && (mode == 0 || mode == 1)) {
     // wave 0 of block 0: lanes over the row blocks, fixed-order wave sum
@@ -348,11 +468,13 @@ hipError_t dtfk_mlpg_fwd(const void* x, const void* labels, int B, int BP, const
   return hipGetLastError();
 }
 
-hipError_t dtfk_mlpg_wgrad(const void* x, int B, int BP, const void* dz2S, float* P2, int nchunk, hipStream_t s) {
+int dtfk_mlpg_wchunk() { return dtfk::mlpg::WCHUNK; }
+int dtfk_mlpg_p2_floats() { return dtfk::mlpg::P2N; }
+
+hipError_t dtfk_mlpg_wgrad(const void* x, int B, const void* dz2F, float* P2, int nchunk, hipStream_t s) {
   using namespace dtfk::mlpg;
-  const int kchunk = BP / nchunk;
-  hipLaunchKernelGGL(mlpg_wgrad, dim3((DIN + 63) / 64, nchunk), dim3(256), 0, s, (const uint8_t*)x, B, BP,
-                     (const uint16_t*)dz2S, P2, kchunk);
+  hipLaunchKernelGGL(mlpg_wgrad, dim3((DIN + 64) / 64, nchunk), dim3(256), 0, s, (const uint8_t*)x, B,
+                     (const uint16_t*)dz2F, P2);
   return hipGetLastError();
 }
 

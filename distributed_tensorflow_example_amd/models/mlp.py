@@ -289,10 +289,10 @@ class GemmMLPTrainer:
     """Large-batch step of the same model (csrc/kernels/mlp_gemm.hip), 3
     launches: `mlpg_fwd` (one workgroup per 64 rows: the hidden layer on bf16
     MFMA with W1 as an exact 3-way bf16 split, then act, logits, softmax-xent,
-    dz2 and this block's dW2/db1/db2 partials without leaving the workgroup),
-    `mlpg_wgrad` (dW1 = x^T dz2 over a pixel-block x batch-chunk grid, dz2 as
-    its exact split) and `mlpg_apply` (fixed-order slab reduction, SGD, W1 split
-    refresh, metrics).  The fused engines contract the batch serially inside
+    dz2 and this block's dW2/db2 partials without leaving the workgroup),
+    `mlpg_wgrad` ([dW1; db1] over a 64-pixel-block x 256-row-chunk grid, dz2 as
+    its exact split) and `mlpg_apply` (fixed-order slab reduction, SGD, W1
+    fragment-image refresh, metrics).  The fused engines contract the batch serially inside
     one wave per weight tile: right at B=100, 4x too slow at B=4096.  All three
     launches are graph-capturable, so `MLPStepRunner` replays them exactly like
     the fused trainer's.  N > 1: the apply kernel first writes the reduced flat
@@ -302,7 +302,7 @@ class GemmMLPTrainer:
 
     def __init__(self, batch_size: int = 4096, lr: float = 0.0005, act: str = "sigmoid", world=None,
                  naive_loss: bool = False, metrics_ring: int = 8192, seed: int = 1, device=None,
-                 wgrad_chunks: Optional[int] = None, **_ignored):
+                 **_ignored):
         self.C = _native.load()
         self.world = world
         self.world_size = 1 if world is None else world.world_size
@@ -314,16 +314,15 @@ class GemmMLPTrainer:
         self.act_name = act
         self.naive = bool(naive_loss)
         f32 = torch.float32
-        # dW1 batch chunks: enough (pixel block x chunk) workgroups to cover the
-        # 256 CUs, each chunk a multiple of 32 rows dividing the padded batch
-        units = self.BP // 32
-        want = int(wgrad_chunks or os.environ.get("DTF_MLPG_CHUNKS", 0) or max(1, min(units, 24)))
-        self.nchunk = max(c for c in range(1, min(want, units) + 1) if units % c == 0)
+        # dW1: one workgroup per (64-pixel block, 256-row batch chunk); the
+        # B-fragment image of dz2 is padded (with zeros) to whole chunks
+        wc = self.C.mlpg_wchunk()
+        self.nchunk = (B + wc - 1) // wc
         self.params = torch.zeros(NPARAM, dtype=f32, device=dev)
         self.W1S = torch.zeros(3 * 112 * 800, dtype=torch.bfloat16, device=dev)
-        self.dz2S = torch.zeros(3 * 112 * self.BP, dtype=torch.bfloat16, device=dev)
+        self.dz2S = torch.zeros(3 * 112 * self.nchunk * wc, dtype=torch.bfloat16, device=dev)
         self.P1 = torch.zeros(self.BP // 64 * self.C.mlpg_p1_floats(), dtype=f32, device=dev)
-        self.P2 = torch.zeros(self.nchunk * 78400, dtype=f32, device=dev)
+        self.P2 = torch.zeros(self.nchunk * self.C.mlpg_p2_floats(), dtype=f32, device=dev)
         self.grads = torch.zeros(NPARAM, dtype=f32, device=dev) if self.world_size > 1 else None
         self.lr = torch.tensor([lr], dtype=f32, device=dev)
         self.ring = int(metrics_ring)

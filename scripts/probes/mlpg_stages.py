@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-kernel / per-stage timing of the large-batch MLP step (mlp_gemm.hip):
 mlpg_fwd ended after its K loop (stop=1), after softmax (2), after dz2 (3),
-full (0); mlpg_wgrad at several batch-chunk counts; mlpg_apply.  One JSON line
+full (0); mlpg_wgrad; mlpg_apply.  One JSON line
 per (B, item): us per launch over back-to-back launches (events)."""
 import json
 import os
@@ -42,10 +42,7 @@ def main():
             out[f"fwd_stop{stop}_us"] = round(timeit(lambda: C.mlpg_fwd(x, 0, y, 0, B, tr.W1S, tr.params, tr.P1,
                                                                       tr.dz2S, tr.act, False, 1.0 / B)), 2)
         C.mlpg_set_stop(0)
-        units = tr.BP // 32
-        for nc in sorted({c for c in (1, 2, 4, 8, 16, 32, 64) if units % c == 0}):
-            P2 = torch.zeros(nc * 78400, dtype=torch.float32, device=dev)
-            out[f"wgrad_n{nc}_us"] = round(timeit(lambda: C.mlpg_wgrad(x, 0, B, tr.dz2S, P2, nc)), 2)
+        out["wgrad_us"] = round(timeit(lambda: C.mlpg_wgrad(x, 0, B, tr.dz2S, tr.P2, tr.nchunk)), 2)
         out["apply_us"] = round(timeit(lambda: tr._apply(0)), 2)
         out["step_us"] = round(timeit(lambda: tr.enqueue_step(x, 0, 0, y, 0)), 2)
         print(json.dumps(out), flush=True)

@@ -151,12 +151,13 @@ def main(argv=None):
             runner.run(w_val, lookahead=w_final if w_final > 0 else a.steps)
             torch.cuda.synchronize()
             return trainer, runner
+        graphs = not a.eager and getattr(trainer, "graph_safe", True)
         runner = MLPStepRunner(trainer, epoch, steps_per_graph=a.steps_per_graph,
-                               use_graph=not a.eager, prefetch=a.prefetch)
+                               use_graph=graphs, prefetch=a.prefetch)
         # warmup: eager first (module load), then the graphs the warmup itself needs
         runner.use_graph = False
         runner.run(min(2, a.warmup))
-        runner.use_graph = not a.eager
+        runner.use_graph = graphs
         if a.warmup > 2:
             runner.prepare(a.warmup - 2)
             runner.run(a.warmup - 2)
@@ -368,7 +369,7 @@ def main(argv=None):
                 "fallbacks": fallbacks or None,
                 "copy_only_launches_in_timed_run": cold_timed,
                 "steps_per_launch": runner.g if persistent else 1,
-                "hipgraph_steps": 0 if (a.eager or persistent) else a.steps_per_graph,
+                "hipgraph_steps": 0 if (persistent or not runner.use_graph) else a.steps_per_graph,
                 "input_prefetch": "in-kernel copier workgroups" if persistent else a.prefetch,
                 "activation": a.act,
                 "exchange_tuning_us_per_step": tuned or None,

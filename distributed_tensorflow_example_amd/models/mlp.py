@@ -328,7 +328,12 @@ class GemmMLPTrainer:
         self.ring = int(metrics_ring)
         self.metrics = torch.zeros(self.ring * 2, dtype=f32, device=dev)
         self.gstep = torch.zeros(1, dtype=torch.int64, device=dev)
-        self.allreduce = "rccl" if self.world_size > 1 else "none"
+        self.allreduce = "none"
+        if self.world_size > 1:
+            self.allreduce = "rccl" if world.comm is not None else world.backend
+        # RCCL calls capture into hipGraphs; a gloo all-reduce (ranks sharing
+        # one GPU in tests) does not
+        self.graph_safe = self.world_size == 1 or world.comm is not None
         self.ipc_parity = 0
         self.shadows_stale = False
         self.set_params(init_params(seed))
@@ -379,7 +384,7 @@ class GemmMLPTrainer:
             self._apply(0)
         else:
             self._apply(1, gout=self.grads)
-            self.world.comm.all_reduce(self.grads, "sum")
+            self.world.all_reduce(self.grads, "sum")
             self._apply(2, gin=self.grads, scale=1.0 / self.world_size)
 
     def step_tensors(self, x: torch.Tensor, labels: torch.Tensor):

@@ -57,3 +57,33 @@ def test_gemm_runner_trains_and_matches_reference_run(native):
     assert rel < 1e-5, rel
     m = tr.read_metrics(0, steps)
     assert np.all(np.isfinite(m)) and tr.global_step == steps
+
+
+def test_gemm_engine_two_ranks_same_gpu(native):
+    """bench.py's large-batch engine under torch.distributed.run with 2 ranks
+    sharing cuda:0 (DTF_BENCH_SAME_GPU=1: gloo all-reduce of the flat fp32
+    gradient between the slab reduce and the apply, eager launches): replicas
+    must stay bit-identical (bench's consistency check) and one contract line
+    comes out.  Timings are not multi-GPU numbers."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(repo, "bench.py"), "--gpus", "2",
+           "--batch", "512", "--steps", "10", "--warmup", "3", "--train-examples", "8192"]
+    env = dict(os.environ, PYTHONPATH=repo, OMP_NUM_THREADS="2", DTF_BENCH_SAME_GPU="1")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=env, cwd=repo)
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert r.returncode == 0 and len(lines) == 1, (r.stdout + r.stderr)[-3000:]
+    res = json.loads(lines[0])
+    assert res["config"]["engine"] == "gemm" and res["config"]["parallelism"] == "dp2"
+    assert res["global_steps_timed"] == 10 and res["value"] > 0
+    assert res["config"]["global_batch"] == 1024

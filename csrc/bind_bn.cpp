@@ -17,6 +17,10 @@ hipError_t dtfk_bn_bwd(const void* dy, const void* x, const void* res, const flo
                        const float* invstd, const float* scale, const float* shift, float* part, float* coef,
                        void* dx, void* dres, float* dgamma, float* dbeta, int M, int C, int relu, int accum,
                        hipStream_t st);
+hipError_t dtfk_maxpool_fwd(const void* x, void* y, void* idx, int N, int H, int W, int C, int Ho, int Wo, int k,
+                            int s, int p, hipStream_t st);
+hipError_t dtfk_maxpool_bwd(const void* dy, const void* idx, void* dx, int N, int H, int W, int C, int Ho, int Wo,
+                            int k, int s, int p, hipStream_t st);
 }
 
 namespace dtf {
@@ -39,6 +43,40 @@ void f32(const at::Tensor& t, int64_t n, const char* w) {
 }
 float* optf(const c10::optional<at::Tensor>& t) { return t.has_value() ? t->data_ptr<float>() : nullptr; }
 }  // namespace
+
+// ---- NHWC bf16 max pooling (kernels/pool.hip); idx: uint8 window position of each output's max
+static void pool_check(const at::Tensor& t, const char* w) {
+  if (!t.is_cuda() || t.scalar_type() != at::kBFloat16 || t.dim() != 4 ||
+      !t.is_contiguous(at::MemoryFormat::ChannelsLast) || t.size(1) % 8)
+    throw std::runtime_error(std::string("maxpool: ") + w + " must be channels_last bf16 [N, C % 8 == 0, H, W]");
+}
+
+void maxpool_fwd(at::Tensor x, at::Tensor y, at::Tensor idx, int64_t k, int64_t s, int64_t p) {
+  pool_check(x, "x");
+  pool_check(y, "y");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), Ho = y.size(2), Wo = y.size(3);
+  if (y.size(0) != N || y.size(1) != C || Ho != (H + 2 * p - k) / s + 1 || Wo != (W + 2 * p - k) / s + 1)
+    throw std::runtime_error("maxpool_fwd: output shape");
+  if (k < 1 || k * k > 255 || s < 1 || p < 0 || 2 * p > k) throw std::runtime_error("maxpool_fwd: window");
+  if (!idx.is_cuda() || idx.scalar_type() != at::kByte || idx.numel() != y.numel())
+    throw std::runtime_error("maxpool_fwd: idx must be a uint8 GPU tensor like y");
+  ck(dtfk_maxpool_fwd(x.data_ptr(), y.data_ptr(), idx.data_ptr(), (int)N, (int)H, (int)W, (int)C, (int)Ho, (int)Wo,
+                      (int)k, (int)s, (int)p, cs()),
+     "maxpool_fwd");
+}
+
+void maxpool_bwd(at::Tensor dy, at::Tensor idx, at::Tensor dx, int64_t k, int64_t s, int64_t p) {
+  pool_check(dy, "dy");
+  pool_check(dx, "dx");
+  const int64_t N = dx.size(0), C = dx.size(1), H = dx.size(2), W = dx.size(3), Ho = dy.size(2), Wo = dy.size(3);
+  if (dy.size(0) != N || dy.size(1) != C || Ho != (H + 2 * p - k) / s + 1 || Wo != (W + 2 * p - k) / s + 1)
+    throw std::runtime_error("maxpool_bwd: shapes");
+  if (!idx.is_cuda() || idx.scalar_type() != at::kByte || idx.numel() != dy.numel())
+    throw std::runtime_error("maxpool_bwd: idx must be a uint8 GPU tensor like dy");
+  ck(dtfk_maxpool_bwd(dy.data_ptr(), idx.data_ptr(), dx.data_ptr(), (int)N, (int)H, (int)W, (int)C, (int)Ho, (int)Wo,
+                      (int)k, (int)s, (int)p, cs()),
+     "maxpool_bwd");
+}
 
 int64_t bn_partial_rows(int64_t M, int64_t C) { return dtfk_bn_partial_rows((int)M, (int)C); }
 
@@ -86,6 +124,8 @@ void bn_bwd(at::Tensor dy, at::Tensor x, c10::optional<at::Tensor> res, at::Tens
 
 void init_bn(pybind11::module& m) {
   m.def("bn_partial_rows", &bn_partial_rows);
+  m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("maxpool_bwd", &maxpool_bwd);
   m.def("bn_fwd", &bn_fwd);
   m.def("bn_apply", &bn_apply);
   m.def("bn_bwd", &bn_bwd);

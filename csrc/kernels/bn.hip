@@ -38,15 +38,23 @@ __device__ __forceinline__ void st8(uint16_t* p, const float* f) {
 // rows in flight per thread.  The 32 row lanes are combined in LDS and written
 // as part[pass][p][c] (pass 0 / 1 = the two sums), so P stays small enough for
 // the finalize to read the partials in a few microseconds.
+//
+// f is called as f(NR, rows) with NR = 4 (four valid rows, the main loop) or
+// NR = 1 (the tail): both forms load unconditionally.  With a validity test
+// around each row's load (the first version) the compiler waited for every
+// load inside its branch, i.e. four serialized memory latencies per iteration.
+template <int NR>
+struct Rows {
+  static constexpr int n = NR;
+  int r[4];
+};
 template <typename F>
 __device__ __forceinline__ void bn_tile_rows(int M, int P, F&& f) {
   const int tr = threadIdx.x >> 3;
   const int stride = 32 * P;
   int r = blockIdx.y * 32 + tr;
-  for (; r + 3 * stride < M; r += 4 * stride) {
-    f(r, r + stride, r + 2 * stride, r + 3 * stride);
-  }
-  for (; r < M; r += stride) f(r, -1, -1, -1);
+  for (; r + 3 * stride < M; r += 4 * stride) f(Rows<4>{{r, r + stride, r + 2 * stride, r + 3 * stride}});
+  for (; r < M; r += stride) f(Rows<1>{{r, r, r, r}});
 }
 
 __device__ __forceinline__ void bn_tile_store(const float* s, const float* q, float* __restrict__ part, int P, int C,
@@ -72,17 +80,15 @@ __global__ __launch_bounds__(256) void bn_partials(const uint16_t* __restrict__ 
   const int cc = c0 + (threadIdx.x & 7) * 8;
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (cc < C)
-    bn_tile_rows(M, P, [&](int r0, int r1, int r2, int r3) {
+    bn_tile_rows(M, P, [&](auto rows) {
+      constexpr int NR = decltype(rows)::n;
       float v[4][8];
-      const int rs[4] = {r0, r1, r2, r3};
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (rs[k] >= 0) ld8(x + (size_t)rs[k] * C + cc, v[k]);
+      for (int k = 0; k < NR; ++k) ld8(x + (size_t)rows.r[k] * C + cc, v[k]);
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (rs[k] >= 0)
+      for (int k = 0; k < NR; ++k)
 #pragma unroll
-          for (int j = 0; j < 8; ++j) { s[j] += v[k][j]; q[j] += v[k][j] * v[k][j]; }
+        for (int j = 0; j < 8; ++j) { s[j] += v[k][j]; q[j] += v[k][j] * v[k][j]; }
     });
   bn_tile_store(s, q, part, P, C, c0);
 }
@@ -194,20 +200,18 @@ __global__ __launch_bounds__(256) void bn_bwd_partials(const uint16_t* __restric
     *reinterpret_cast<float4*>(sc + 4) = *reinterpret_cast<const float4*>(scale + cc + 4);
     *reinterpret_cast<float4*>(sh) = *reinterpret_cast<const float4*>(shift + cc);
     *reinterpret_cast<float4*>(sh + 4) = *reinterpret_cast<const float4*>(shift + cc + 4);
-    bn_tile_rows(M, P, [&](int r0, int r1, int r2, int r3) {
-      const int rs[4] = {r0, r1, r2, r3};
+    bn_tile_rows(M, P, [&](auto rows) {
+      constexpr int NR = decltype(rows)::n;
       float d[4][8], v[4][8], rr[4][8];
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (rs[k] >= 0) {
-          const size_t e = (size_t)rs[k] * C + cc;
-          ld8(dy + e, d[k]);
-          ld8(x + e, v[k]);
-          if constexpr (RES) ld8(res + e, rr[k]);
-        }
+      for (int k = 0; k < NR; ++k) {
+        const size_t e = (size_t)rows.r[k] * C + cc;
+        ld8(dy + e, d[k]);
+        ld8(x + e, v[k]);
+        if constexpr (RES) ld8(res + e, rr[k]);
+      }
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (rs[k] >= 0)
+      for (int k = 0; k < NR; ++k)
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             float g = d[k][j];

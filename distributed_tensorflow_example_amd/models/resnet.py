@@ -15,6 +15,7 @@ import torch.nn.functional as F
 from .. import ops
 from ..ops.bn import FusedBatchNorm2d
 from ..ops.conv import ShadowConv2d, attach_shadows as _attach_conv_shadows
+from ..ops.pool import max_pool2d
 
 
 class Bottleneck(nn.Module):
@@ -59,7 +60,7 @@ class ResNet(nn.Module):
     def forward(self, x):
         with torch.autocast(device_type="cuda", dtype=torch.bfloat16, enabled=x.is_cuda):
             x = self.bn1(self.conv1(x), relu=True)
-            x = F.max_pool2d(x, 3, 2, 1)
+            x = max_pool2d(x, 3, 2, 1)
             x = self.blocks(x)
             x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
             return self.fc(x)

@@ -1,0 +1,63 @@
+"""ResNet-side kernels against plain PyTorch fp32 references: the NHWC bf16
+max pool (csrc/kernels/pool.hip) and the 1x1 convolution weight gradient on
+the in-tree GEMM (ops/conv.py)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("shape,k,s,p", [((4, 64, 112, 112), 3, 2, 1), ((2, 16, 9, 11), 3, 2, 1),
+                                         ((2, 8, 10, 10), 2, 2, 0), ((1, 24, 7, 7), 3, 1, 1)])
+def test_maxpool_nhwc_matches_fp32(native, shape, k, s, p):
+    from distributed_tensorflow_example_amd.ops.pool import max_pool2d
+
+    torch.manual_seed(0)
+    x = torch.randn(shape, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    y = max_pool2d(x, k, s, p)
+    xr = x.detach().float().requires_grad_(True)
+    yr = F.max_pool2d(xr, k, s, p)
+    assert y.shape == yr.shape
+    assert torch.equal(y.float(), yr)                       # a max of bf16 values is exact
+    g = torch.randn_like(yr)
+    y.backward(g.to(torch.bfloat16))
+    yr.backward(g.to(torch.bfloat16).float())
+    # random inputs: no ties, so every gradient lands on the same input as torch's
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=1e-2, atol=1e-2)
+
+
+def test_maxpool_ties_take_first_and_nan_propagates(native):
+    from distributed_tensorflow_example_amd.ops.pool import max_pool2d
+
+    x = torch.zeros(1, 8, 4, 4, device="cuda", dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x[0, 0, 1, 1] = float("nan")
+    x.requires_grad_(True)
+    y = max_pool2d(x, 2, 2, 0)
+    assert torch.isnan(y[0, 0, 0, 0]) and torch.all(y[0, 1:] == 0)
+    y.backward(torch.ones_like(y))
+    # all-zero windows: the first position (0, 0) of each window gets the gradient
+    assert x.grad[0, 1, 0, 0] == 1 and x.grad[0, 1, 0, 1] == 0 and x.grad[0, 1, 1, 0] == 0
+
+
+@pytest.mark.parametrize("n,cin,cout,hw", [(8, 64, 256, 28), (4, 256, 64, 14), (16, 512, 128, 7)])
+def test_conv1x1_gemm_wgrad_matches_fp32(native, n, cin, cout, hw, monkeypatch):
+    from distributed_tensorflow_example_amd.ops import conv
+
+    monkeypatch.setattr(conv, "_DW_POLICY", "always")
+    torch.manual_seed(1)
+    m = conv.ShadowConv2d(cin, cout, 1, bias=False).cuda().to(memory_format=torch.channels_last)
+    conv.attach_shadows(m)
+    x = torch.randn(n, cin, hw, hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    y = m(x)
+    g = torch.randn_like(y.float()).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y.backward(g)
+    xr = x.detach().float()
+    wr = m.weight.detach().to(torch.bfloat16).float()
+    gr = g.float()
+    dw_ref = torch.einsum("nohw,nihw->oi", gr, xr).view_as(m.weight)
+    dx_ref = torch.einsum("nohw,oi->nihw", gr, wr.view(cout, cin))
+    torch.testing.assert_close(m.weight.grad, dw_ref, rtol=2e-3, atol=2e-3 * dw_ref.abs().max().item())
+    torch.testing.assert_close(x.grad.float(), dx_ref, rtol=2e-2, atol=2e-2 * dx_ref.abs().max().item())

@@ -29,9 +29,8 @@ hipError_t dtfk_mlp_apply_flat(float* params, const void* grads, int grad_kind, 
                                float scale, void* W1T, void* W2T, void* W2N, hipStream_t stream);
 int dtfk_mlp_ipc_flag_bytes();
 int dtfk_mlpg_p1_floats();
-void dtfk_mlpg_set_stop(int s);
-hipError_t dtfk_mlpg_fwd(const void* x, const void* labels, int B, int BP, const void* W1S, const float* params,
-                         float* P1, void* dz2S, int act, int naive, float gscale, hipStream_t s);
+hipError_t dtfk_mlpg_fwd(const void* x, const void* labels, int B, int BP, const void* W1F, const float* params,
+                         float* a2g, float* P1, void* dz2F, int act, int naive, float gscale, hipStream_t s);
 hipError_t dtfk_mlpg_wgrad(const void* x, int B, const void* dz2F, float* P2, int nchunk, hipStream_t s);
 int dtfk_mlpg_wchunk();
 int dtfk_mlpg_p2_floats();
@@ -292,19 +291,20 @@ static int64_t mlpg_bp2(int B) {
 }
 
 
-void mlpg_fwd(at::Tensor x, int64_t x_off, at::Tensor labels, int64_t labels_off, int B, at::Tensor W1S,
-              at::Tensor params, at::Tensor P1, at::Tensor dz2S, int act, bool naive, double gscale) {
+void mlpg_fwd(at::Tensor x, int64_t x_off, at::Tensor labels, int64_t labels_off, int B, at::Tensor W1F,
+              at::Tensor params, at::Tensor a2, at::Tensor P1, at::Tensor dz2F, int act, bool naive, double gscale) {
   const int64_t BP = mlpg_bp(B);
   if (B < 1) throw std::runtime_error("mlpg_fwd: B >= 1");
   const uint8_t* px = stage_ptr(x, x_off, (int64_t)B * 784, "x");
   if (reinterpret_cast<uintptr_t>(px) & 15) throw std::runtime_error("mlpg_fwd: x must be 16-byte aligned");
   const uint8_t* pl = stage_ptr(labels, labels_off, B, "labels");
-  need(W1S, at::kBFloat16, 3 * 112 * 800, "W1S");
+  need(W1F, at::kBFloat16, 3 * 112 * 800, "W1F");
   need(params, at::kFloat, kNParam, "params");
-  need(P1, at::kFloat, BP / 64 * dtfk_mlpg_p1_floats(), "P1");
-  need(dz2S, at::kBFloat16, 3 * 112 * mlpg_bp2(B), "dz2S");
-  hip_check(dtfk_mlpg_fwd(px, pl, B, (int)BP, W1S.data_ptr(), params.data_ptr<float>(), P1.data_ptr<float>(),
-                          dz2S.data_ptr(), act, naive ? 1 : 0, (float)gscale, cur_stream()),
+  need(a2, at::kFloat, BP * 112, "a2");
+  need(P1, at::kFloat, BP / 16 * dtfk_mlpg_p1_floats(), "P1");
+  need(dz2F, at::kBFloat16, 3 * 112 * mlpg_bp2(B), "dz2F");
+  hip_check(dtfk_mlpg_fwd(px, pl, B, (int)BP, W1F.data_ptr(), params.data_ptr<float>(), a2.data_ptr<float>(),
+                          P1.data_ptr<float>(), dz2F.data_ptr(), act, naive ? 1 : 0, (float)gscale, cur_stream()),
             "mlpg_fwd");
 }
 
@@ -324,7 +324,7 @@ void mlpg_apply(at::Tensor params, at::Tensor P1, at::Tensor P2, int nchunk, c10
   const int64_t BP = mlpg_bp(B);
   if (mode < 0 || mode > 3) throw std::runtime_error("mlpg_apply: mode 0..3");
   need(params, at::kFloat, kNParam, "params");
-  need(P1, at::kFloat, BP / 64 * dtfk_mlpg_p1_floats(), "P1");
+  need(P1, at::kFloat, BP / 16 * dtfk_mlpg_p1_floats(), "P1");
   need(P2, at::kFloat, (int64_t)nchunk * dtfk_mlpg_p2_floats(), "P2");
   if (mode == 2 && !gin.has_value()) throw std::runtime_error("mlpg_apply: mode 2 needs gin");
   if (mode == 1 && !gout.has_value()) throw std::runtime_error("mlpg_apply: mode 1 needs gout");
@@ -334,7 +334,7 @@ void mlpg_apply(at::Tensor params, at::Tensor P1, at::Tensor P2, int nchunk, c10
   need(W1S, at::kBFloat16, 3 * 112 * 800, "W1S");
   need(metrics, at::kFloat, 2, "metrics");
   need(gstep, at::kLong, 1, "gstep");
-  hip_check(dtfk_mlpg_apply(params.data_ptr<float>(), P1.data_ptr<float>(), (int)(BP / 64), P2.data_ptr<float>(),
+  hip_check(dtfk_mlpg_apply(params.data_ptr<float>(), P1.data_ptr<float>(), (int)(BP / 16), P2.data_ptr<float>(),
                             nchunk, gin.has_value() ? gin->data_ptr<float>() : nullptr,
                             gout.has_value() ? gout->data_ptr<float>() : nullptr, lr.data_ptr<float>(), (float)scale,
                             W1S.data_ptr(), metrics.data_ptr<float>(), (int)(metrics.numel() / 2),
@@ -809,7 +809,7 @@ void init_mlp(py::module& m) {
   m.def("mlp_ipc_flag_bytes", &dtfk_mlp_ipc_flag_bytes);
   m.def("memcpy_h2d_async", &memcpy_h2d_async);
   m.def("mlpg_fwd", &mlpg_fwd, py::arg("x"), py::arg("x_offset"), py::arg("labels"), py::arg("labels_offset"),
-        py::arg("B"), py::arg("W1S"), py::arg("params"), py::arg("P1"), py::arg("dz2S"), py::arg("act"),
+        py::arg("B"), py::arg("W1F"), py::arg("params"), py::arg("a2"), py::arg("P1"), py::arg("dz2F"), py::arg("act"),
         py::arg("naive"), py::arg("gscale"));
   m.def("mlpg_wgrad", &mlpg_wgrad, py::arg("x"), py::arg("x_offset"), py::arg("B"), py::arg("dz2S"), py::arg("P2"),
         py::arg("nchunk"));
@@ -819,7 +819,6 @@ void init_mlp(py::module& m) {
   m.def("mlpg_p1_floats", &dtfk_mlpg_p1_floats);
   m.def("mlpg_wchunk", &dtfk_mlpg_wchunk);
   m.def("mlpg_p2_floats", &dtfk_mlpg_p2_floats);
-  m.def("mlpg_set_stop", &dtfk_mlpg_set_stop);
 }
 
 }  // namespace dtf

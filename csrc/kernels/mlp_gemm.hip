@@ -39,7 +39,6 @@ namespace mlpg {
 constexpr int DIN = 784, DINP = 800, HID = 100, HIDP = 112, NCLS = 10;
 constexpr int OFF_W2 = 78400, OFF_B1 = 79400, OFF_B2 = 79500, NPARAM = 79510;
 constexpr int KSTEPS = DINP / 32;          // 25
-constexpr int R1 = 64;                     // rows per mlpg_fwd block
 constexpr int P1N = 1112;                  // [dW2 1000 | (unused 100) | db2 10 | loss | correct]
 constexpr int XTLD = 40;                   // LDS row stride (bf16) of a transposed x tile [64 px][32 batch]
 // register staging in native vectors (an array of HIP's struct uint4 stayed in scratch memory)
@@ -79,222 +78,188 @@ __device__ __forceinline__ f32x4 mfma16x16x4f32(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-constexpr int NW = 4;            // waves per mlpg_fwd block: they split K, each covers all 64 x 112 outputs
-constexpr int NT = 28;           // 4 row tiles x 7 col tiles
-constexpr int ZLD = 113;         // LDS row stride (fp32) of a2 / dz2 after the reduction
+constexpr int NW = 4;            // waves per block (mlpg_l1 / mlpg_wgrad split K over them)
+constexpr int NT = 28;           // mlpg_wgrad: 4 pixel tiles x 7 hidden tiles
+constexpr int ALD = 112;         // row stride (fp32) of the a2 buffer [BP][112]: col 100 = 1 (db2's column)
+constexpr int KPW = (KSTEPS + NW - 1) / NW;   // 7 k-steps per wave
 
-// One block per 64 rows.  Wave w contracts k-steps w, w+4, ... for every
-// output tile, B fragments straight from the fragment image (no LDS staging,
-// no barrier in the K loop), next k-step's loads in flight under this one's 84
-// MFMAs.  The 4 partial sums meet in LDS (each tile summed by one owner wave in
-// wave order: deterministic), then the head runs on exact-f32 MFMA.
-__global__ __launch_bounds__(256, 1) void mlpg_fwd(const uint8_t* __restrict__ x, const uint8_t* __restrict__ labels,
-                                                   int B, int BP, const uint16_t* __restrict__ W1F,
-                                                   const float* __restrict__ params, float* __restrict__ P1,
-                                                   uint16_t* __restrict__ dz2S, int act, int naive, float gscale,
-                                                   int stop) {
-  __shared__ __attribute__((aligned(16))) float zred[NW * NT * 256];   // 112 KB; a2 / dz2 after the reduction
-  __shared__ float w2[HID * NCLS], b2[16], b1[HIDP], dls[R1][16], lred[2][NW];
-  __shared__ int lab[R1];
+// Hidden layer: one workgroup per (64 rows, 16 hidden units).  Its 4 waves
+// split the 25 k-steps (7 each; waves 1-3 run a 7th, all-zero step) and each
+// covers the 4 row tiles of the column tile, so a wave's whole operand set --
+// 7 x 3 W1 fragments from the fragment image and 7 x 4 x fragments, ~140
+// VGPRs -- is requested up front: ONE memory latency, then 84 back-to-back
+// MFMAs.  (Covering all 112 hidden units per workgroup streamed the whole
+// 537 KB W1 image through every workgroup in 7 dependent rounds: 13 us.)
+// Partials meet in LDS (tile rt summed by wave rt, wave order), then
+// a2 = act(z / 255 + b1) goes to global fp32 [BP][112].
+__global__ __launch_bounds__(256) void mlpg_l1(const uint8_t* __restrict__ x, int B, const uint16_t* __restrict__ W1F,
+                                               const float* __restrict__ params, float* __restrict__ a2g, int act) {
+  __shared__ __attribute__((aligned(16))) f32x4 red[NW][4][64];
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int lr = lane & 15, lg4 = lane >> 4;
-  const int r0 = blockIdx.x * R1;
-  // small operands into registers now, into LDS after the K loop (a load
-  // waited for here would stall the K loop's start)
-  float pw[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) pw[k] = params[OFF_W2 + min(t + 256 * k, HID * NCLS - 1)];
-  const float pb1 = params[OFF_B1 + min(t, HID - 1)];
-  const float pb2 = params[OFF_B2 + min(t, NCLS - 1)];
-  const int plab = labels[min(r0 + (t & 63), B - 1)];
-
+  const int r0 = blockIdx.x * 64, ct = blockIdx.y;
+  const int h = 16 * ct + lr;
+  const float bb = params[OFF_B1 + min(h, HID - 1)];
+  const bf16x8* wf = reinterpret_cast<const bf16x8*>(W1F) + lane;
   const uint8_t* xr[4];
 #pragma unroll
-  for (int rt = 0; rt < 4; ++rt) xr[rt] = x + (size_t)min(r0 + 16 * rt + lr, B - 1) * DIN;   // rows >= B: grads zeroed
-  const bf16x8* wf = reinterpret_cast<const bf16x8*>(W1F) + lane;
-  f32x4 acc[4][7];
-#pragma unroll
-  for (int rt = 0; rt < 4; ++rt)
-#pragma unroll
-    for (int ct = 0; ct < 7; ++ct) acc[rt][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // 7 k-steps per wave, fully unrolled, the next k-step's loads in flight
-  // under this one's MFMAs; waves 1-3 run a 7th, all-zero step (ks >= 25
-  // re-reads step 24 and multiplies a zero x fragment) -- no branch around a
-  // load, so the compiler's waits stay counted (a conditional load made it
-  // wait for the just-issued next step at every join).  Loading two steps
-  // ahead (3 register sets) measured slower: 15.1 vs 13.0 us (VGPRs spill
-  // into AGPR copies).
-  bf16x8 bq[2][21];
-  u32x2 xq[2][4];
-  auto load = [&](int ks, bf16x8 (&b)[21], u32x2 (&xv)[4]) {
-    const int kc = min(ks, KSTEPS - 1);
-#pragma unroll
-    for (int i = 0; i < 21; ++i) b[i] = wf[((size_t)kc * 21 + i) * 64];   // i = s * 7 + ct
-    // pixels >= 784 re-read 776.. (times W1's zero padding)
-#pragma unroll
-    for (int rt = 0; rt < 4; ++rt) xv[rt] = *reinterpret_cast<const u32x2*>(xr[rt] + min(kc * 32 + 8 * lg4, DIN - 8));
-  };
-  auto compute = [&](int ks, const bf16x8 (&b)[21], const u32x2 (&xv)[4]) {
-    const bool live = ks < KSTEPS;
-#pragma unroll
-    for (int rt = 0; rt < 4; ++rt) {
-      const bf16x8 a = u8x8_to_bf16(live ? xv[rt] : u32x2{0u, 0u});
-#pragma unroll
-      for (int s = 0; s < 3; ++s)
-#pragma unroll
-        for (int ct = 0; ct < 7; ++ct) acc[rt][ct] = mfma16x16x32(a, b[s * 7 + ct], acc[rt][ct]);
-    }
-  };
-  constexpr int KPW = (KSTEPS + NW - 1) / NW;   // 7
-  load(wave, bq[0], xq[0]);
+  for (int rt = 0; rt < 4; ++rt) xr[rt] = x + (size_t)min(r0 + 16 * rt + lr, B - 1) * DIN;   // rows >= B: zeroed later
+  bf16x8 bq[KPW][3];
+  u32x2 xq[KPW][4];
 #pragma unroll
   for (int i = 0; i < KPW; ++i) {
-    if (i + 1 < KPW) load(wave + NW * (i + 1), bq[(i + 1) & 1], xq[(i + 1) & 1]);
-    __builtin_amdgcn_sched_barrier(0);   // the next step's loads go out before this step's MFMAs
-    compute(wave + NW * i, bq[i & 1], xq[i & 1]);
+    const int kc = min(wave + NW * i, KSTEPS - 1);
+#pragma unroll
+    for (int sp = 0; sp < 3; ++sp) bq[i][sp] = wf[((size_t)(kc * 3 + sp) * 7 + ct) * 64];
+    // pixels >= 784 re-read 776.. (times W1's zero padding)
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt) xq[i][rt] = *reinterpret_cast<const u32x2*>(xr[rt] + min(kc * 32 + 8 * lg4, DIN - 8));
   }
+  f32x4 acc[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k)
-    if (t + 256 * k < HID * NCLS) w2[t + 256 * k] = pw[k];
-  if (t < 16) b2[t] = t < NCLS ? pb2 : 0.f;
-  if (t < HIDP) b1[t] = t < HID ? pb1 : 0.f;
-  if (t < R1) lab[t] = plab;
-  // partial sums -> LDS [wave][tile][lane][4]
-  f32x4* zr = reinterpret_cast<f32x4*>(zred);
+  for (int rt = 0; rt < 4; ++rt) acc[rt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int rt = 0; rt < 4; ++rt)
+  for (int i = 0; i < KPW; ++i) {
+    const bool live = wave + NW * i < KSTEPS;
 #pragma unroll
-    for (int ct = 0; ct < 7; ++ct) zr[(wave * NT + rt * 7 + ct) * 64 + lane] = acc[rt][ct];
-  __syncthreads();
-  float av[7][4];
+    for (int rt = 0; rt < 4; ++rt) {
+      const bf16x8 a = u8x8_to_bf16(live ? xq[i][rt] : u32x2{0u, 0u});
 #pragma unroll
-  for (int m = 0; m < 7; ++m) {   // owned tiles: wave + 4m
-    const int tile = wave + NW * m, rt = tile / 7, ct = tile % 7;
-    f32x4 z = zr[tile * 64 + lane];
-#pragma unroll
-    for (int w = 1; w < NW; ++w) z += zr[(w * NT + tile) * 64 + lane];
-    const int h = 16 * ct + lr;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float zz = z[i] * (1.f / 255.f) + b1[h];
-      const float a = act == 0 ? sigmoidf_(zz) : fmaxf(zz, 0.f);
-      av[m][i] = h < HID ? a : (h == HID ? 1.f : 0.f);   // column 100 = 1: db2 rides dW2's product
+      for (int sp = 0; sp < 3; ++sp) acc[rt] = mfma16x16x32(a, bq[i][sp], acc[rt]);
     }
-    (void)rt;
   }
-  __syncthreads();   // every partial read: a2 / dz2 reuse the LDS
-  float* a2s = zred;
-  float* dzs = zred + R1 * ZLD;
 #pragma unroll
-  for (int m = 0; m < 7; ++m) {
-    const int tile = wave + NW * m, rt = tile / 7, ct = tile % 7;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) a2s[(16 * rt + 4 * lg4 + i) * ZLD + 16 * ct + lr] = av[m][i];
-  }
+  for (int rt = 0; rt < 4; ++rt) red[wave][rt][lane] = acc[rt];
   __syncthreads();
-  if (stop == 1) return;
-  // logits of row tile `wave`: [16 x 100] x [100 x 10] on f32 MFMA (exact products)
-  f32x4 lgt = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 5
+  f32x4 z = red[0][wave][lane];
+#pragma unroll
+  for (int w = 1; w < NW; ++w) z += red[w][wave][lane];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float zz = z[i] * (1.f / 255.f) + bb;
+    const float av = act == 0 ? sigmoidf_(zz) : fmaxf(zz, 0.f);
+    a2g[(size_t)(r0 + 16 * wave + 4 * lg4 + i) * ALD + h] = h < HID ? av : (h == HID ? 1.f : 0.f);
+  }
+}
+
+// Head: one workgroup per 16 rows, no block barrier.  Every wave computes the
+// rows' logits and softmax-xent (the cheap, serial part: 25 dependent f32
+// MFMAs and DPP row reductions) and then its share of the 7 hidden tiles --
+// wave w takes tiles w and w + 4 -- for dz2 = (dlog W2^T) act'(a2) (stored as
+// its exact split in mlpg_wgrad's fragment order) and [dW2; db2] = [a2 | 1]^T
+// dlog (a2's column 100 is 1) into the tile's P1 slab.  All operands are
+// requested up front (one memory latency), on exact-f32 MFMA throughout.
+__global__ __launch_bounds__(256) void mlpg_head(const float* __restrict__ a2g, const uint8_t* __restrict__ labels,
+                                                 int B, const float* __restrict__ params, float* __restrict__ P1,
+                                                 uint16_t* __restrict__ dz2F, int act, int naive, float gscale) {
+  __shared__ float dlx[NW][16][17];
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int lr = lane & 15, lg4 = lane >> 4;
+  const int r0 = 16 * blockIdx.x;
+  const float* W2 = params + OFF_W2;
+  // ---- operands, all in flight at once
+  float la[HID / 4], lw[HID / 4];              // logits: A = a2[row lr][k], B = W2[k][class lr]
+#pragma unroll
   for (int s = 0; s < HID / 4; ++s) {
     const int k = 4 * s + lg4;
-    lgt = mfma16x16x4f32(a2s[(16 * wave + lr) * ZLD + k], lr < NCLS ? w2[k * NCLS + lr] : 0.f, lgt);
+    la[s] = a2g[(size_t)(r0 + lr) * ALD + k];
+    lw[s] = W2[k * NCLS + min(lr, NCLS - 1)];
   }
-  float lsum = 0.f, csum = 0.f;
+  float ad[2][4], aw[2][4], w2t[2][3];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {   // rows 16*wave + 4*lg4 + i, class lr (16-lane DPP rows)
-    const int rl = 16 * wave + 4 * lg4 + i, row = r0 + rl;
-    const bool cv = lr < NCLS;
-    const float z = cv ? lgt[i] + b2[lr] : -INFINITY;
+  for (int m = 0; m < 2; ++m) {
+    const int ct = min(wave + NW * m, 6), h = 16 * ct + lr;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ad[m][i] = a2g[(size_t)(r0 + 4 * lg4 + i) * ALD + h];   // D layout: act' of dz2
+      aw[m][i] = a2g[(size_t)(r0 + 4 * i + lg4) * ALD + h];   // dW2's A operand: [h][row 4i + lg4]
+    }
+#pragma unroll
+    for (int s = 0; s < 3; ++s) w2t[m][s] = W2[min(h, HID - 1) * NCLS + min(4 * s + lg4, NCLS - 1)];
+  }
+  const float b2v = params[OFF_B2 + min(lr, NCLS - 1)];
+  int yl[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) yl[i] = labels[min(r0 + 4 * lg4 + i, B - 1)];
+  // ---- logits [16 x 10] = a2 [16 x 100] W2 [100 x 10]
+  f32x4 lgt = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < HID / 4; ++s) lgt = mfma16x16x4f32(la[s], lr < NCLS ? lw[s] : 0.f, lgt);
+  // ---- softmax-xent per row (rows 4*lg4 + i, class lr: one 16-lane DPP row per lane group)
+  float lsum = 0.f, csum = 0.f;
+  const bool cv = lr < NCLS;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int rl = 4 * lg4 + i, row = r0 + rl;
+    const float z = cv ? lgt[i] + b2v : -INFINITY;
     const float m = row16_max(z);
     const float e = cv ? __expf(z - m) : 0.f;
     const float se = row16_sum(e);
+    const int y = yl[i];
+    const float zy = row16_sum(lr == y ? z : 0.f);
+    const float ey = row16_sum(lr == y ? e : 0.f);
+    const float am = row16_min(cv && z == m ? (float)lr : 16.f);
     float g = 0.f;
     if (row < B) {
-      const int y = lab[rl];
-      const float zy = row16_sum(lr == y ? z : 0.f);
-      const float ey = row16_sum(lr == y ? e : 0.f);
-      const float am = row16_min(cv && z == m ? (float)lr : 16.f);
-      const float loss = naive ? -__logf(ey / se) : (m + __logf(se)) - zy;
       if (lr == 0) {
-        lsum += loss;
+        lsum += naive ? -__logf(ey / se) : (m + __logf(se)) - zy;
         csum += (int)am == y ? 1.f : 0.f;
       }
       g = cv ? (e / se - (lr == y ? 1.f : 0.f)) * gscale : 0.f;
     }
-    dls[rl][lr] = g;
+    dlx[wave][rl][lr] = g;                      // transposed through wave-private LDS
   }
-  lsum = wave_sum(lsum);
-  csum = wave_sum(csum);
-  if (lane == 0) {
-    lred[0][wave] = lsum;
-    lred[1][wave] = csum;
-  }
-  __syncthreads();
-  if (stop == 2) return;
-  // dz2 of row tile `wave` = dl [16 x 10] x W2^T [10 x 100] (K padded to 12), times act'(a2)
+  float dlk[3];                                 // dz2's A operand: dl[row lr][class 4s + lg4]
 #pragma unroll
-  for (int ct = 0; ct < 7; ++ct) {
-    f32x4 d = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int h = 16 * ct + lr;
+  for (int s = 0; s < 3; ++s) dlk[s] = dlx[wave][lr][4 * s + lg4];
+  float dlr[4];                                 // dW2's B operand: dl[row 4i + lg4][class lr]
 #pragma unroll
-    for (int s = 0; s < 3; ++s) {
-      const int c = 4 * s + lg4;
-      d = mfma16x16x4f32(dls[16 * wave + lr][c], (c < NCLS && h < HID) ? w2[h * NCLS + c] : 0.f, d);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int rl = 16 * wave + 4 * lg4 + i;
-      const float a = a2s[rl * ZLD + h];
-      dzs[rl * ZLD + h] = h < HID ? (act == 0 ? d[i] * a * (1.f - a) : (a > 0.f ? d[i] : 0.f)) : 0.f;
-    }
-  }
-  __syncthreads();
-  // dz2 as its exact split in the wgrad's B-fragment image (dz2F: [row/32][split][col tile][lane][8]):
-  // one task = 8 consecutive rows of one hidden unit -> three 16-byte stores
-  for (int task = t; task < (R1 / 8) * HID; task += 256) {
-    const int h = task % HID, rg = task / HID;
-    u32x4 hv, mv, lv;
-#pragma unroll
-    for (int e = 0; e < 8; e += 2) {
-      uint16_t h0, m0, l0, h1, m1, l1;
-      split3(dzs[(8 * rg + e) * ZLD + h], h0, m0, l0);
-      split3(dzs[(8 * rg + e + 1) * ZLD + h], h1, m1, l1);
-      hv[e / 2] = (uint32_t)h0 | ((uint32_t)h1 << 16);
-      mv[e / 2] = (uint32_t)m0 | ((uint32_t)m1 << 16);
-      lv[e / 2] = (uint32_t)l0 | ((uint32_t)l1 << 16);
-    }
-    const int row = r0 + 8 * rg;
-    const size_t base = (((size_t)(row >> 5) * 3) * 7 + (h >> 4)) * 64 + ((row & 31) >> 3) * 16 + (h & 15);
-    u32x4* dst = reinterpret_cast<u32x4*>(dz2S);
-    dst[base] = hv;
-    dst[base + 7 * 64] = mv;
-    dst[base + 14 * 64] = lv;
-  }
-  if (stop == 3) return;
-  // this block's [dW2; db2] = [a2 | 1]^T dl on f32 MFMA: hidden tiles ct = wave, wave + 4
+  for (int i = 0; i < 4; ++i) dlr[i] = dlx[wave][4 * i + lg4][lr];
   float* p1 = P1 + (size_t)blockIdx.x * P1N;
-  for (int ct = wave; ct < 7; ct += NW) {
+  // ---- this wave's hidden tiles: dz2 -> the B-fragment image of mlpg_wgrad
+  //      [row / 32][split][col tile][lane ((row % 32) / 8) * 16 + h % 16][row % 8], and [dW2; db2]
+  const int R = r0 + 4 * lg4;                   // this lane's 4 rows R .. R+3 (one 8-byte run of e)
+  uint16_t* dbase = dz2F + (((size_t)(R >> 5) * 3) * 7) * 512 + (size_t)(((R & 31) >> 3) * 16 + lr) * 8 + (R & 7);
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    const int ct = wave + NW * m;
+    if (ct >= 7) break;
+    const int h = 16 * ct + lr;
     f32x4 d = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-    for (int s = 0; s < R1 / 4; ++s) {
-      const int r = 4 * s + lg4;
-      d = mfma16x16x4f32(a2s[r * ZLD + 16 * ct + lr], dls[r][lr], d);
-    }
+#pragma unroll
+    for (int s = 0; s < 3; ++s) d = mfma16x16x4f32(dlk[s], (4 * s + lg4 < NCLS && h < HID) ? w2t[m][s] : 0.f, d);
+    uint16_t hv[4], mv[4], lv[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int h = 16 * ct + 4 * lg4 + i;
+      const float av = ad[m][i];
+      const float dz = h < HID ? (act == 0 ? d[i] * av * (1.f - av) : (av > 0.f ? d[i] : 0.f)) : 0.f;
+      split3(dz, hv[i], mv[i], lv[i]);
+    }
+#pragma unroll
+    for (int sp = 0; sp < 3; ++sp) {
+      const uint16_t* v = sp == 0 ? hv : (sp == 1 ? mv : lv);
+      *reinterpret_cast<u32x2*>(dbase + (size_t)(sp * 7 + ct) * 512) =
+          u32x2{(uint32_t)v[0] | ((uint32_t)v[1] << 16), (uint32_t)v[2] | ((uint32_t)v[3] << 16)};
+    }
+    f32x4 w = f32x4{0.f, 0.f, 0.f, 0.f};        // [dW2; db2] tile: M = hidden, N = class, K = 16 rows
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w = mfma16x16x4f32(aw[m][i], dlr[i], w);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int hh = 16 * ct + 4 * lg4 + i;
       if (lr < NCLS) {
-        if (h < HID) p1[h * NCLS + lr] = d[i];
-        else if (h == HID) p1[HID * NCLS + HID + lr] = d[i];
+        if (hh < HID) p1[hh * NCLS + lr] = w[i];
+        else if (hh == HID) p1[HID * NCLS + HID + lr] = w[i];
       }
     }
   }
-  if (t == 0) {   // (db1 rides the weight gradient: pixel column 784 == 255 in mlpg_wgrad)
-    float ls = 0.f, cs = 0.f;
-    for (int w = 0; w < NW; ++w) { ls += lred[0][w]; cs += lred[1][w]; }
-    p1[P1N - 2] = ls;
-    p1[P1N - 1] = cs;
+  if (wave == 0) {
+    lsum = wave_sum(lsum);
+    csum = wave_sum(csum);
+    if (lane == 0) {
+      p1[P1N - 2] = lsum;
+      p1[P1N - 1] = csum;
+    }
   }
 }
 
@@ -397,42 +362,62 @@ __device__ __forceinline__ float sum_strided(const float* __restrict__ p, size_t
   return s;
 }
 
-// mode 0: reduce the slabs + SGD + W1 split refresh + metrics (1 GPU)
+// mode 0: reduce the slabs + SGD + W1 fragment-image refresh + metrics (1 GPU)
 // mode 1: reduce the slabs into gout (TF flat layout) + metrics (before the all-reduce)
-// mode 2: SGD from gin (all-reduced, x scale) + W1 split refresh
-// mode 3: W1 split refresh only (after set_params)
+// mode 2: SGD from gin (all-reduced, x scale) + W1 refresh
+// mode 3: W1 refresh only (after set_params)
+// Blocks [0, NB2): one thread per W1 / b1 parameter (P2 slabs: n2 batch chunks).
+// Blocks [NB2, ..): one WAVE per W2 / b2 parameter: the P1 slabs (one per 16
+// batch rows, hundreds at large B) summed lane-strided + a fixed-order wave sum.
+constexpr int NP2 = OFF_W2 + HID;                 // W1 + b1
+constexpr int NB2 = (NP2 + 255) / 256;
+constexpr int NP1 = HID * NCLS + NCLS;            // W2 + b2
+__device__ __forceinline__ void apply_one(float* params, int i, float g, const float* gin, float* gout,
+                                          const float* lr_ptr, float scale, int mode) {
+  if (mode == 2) g = gin[i];
+  if (mode == 1) gout[i] = g;
+  else params[i] -= (*lr_ptr) * scale * g;
+}
+
 __global__ __launch_bounds__(256) void mlpg_apply(float* __restrict__ params, const float* __restrict__ P1, int n1,
                                                   const float* __restrict__ P2, int n2, const float* __restrict__ gin,
                                                   float* __restrict__ gout, const float* __restrict__ lr_ptr,
                                                   float scale, uint16_t* __restrict__ W1S,
                                                   float* __restrict__ metrics, int ring,
                                                   long long* __restrict__ gstep, float inv_b, int mode) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < NPARAM && mode != 3) {
+  if (blockIdx.x >= NB2) {
+    if (mode == 3) return;
+    const int pi = (blockIdx.x - NB2) * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (pi >= NP1) return;
+    const int i = pi < HID * NCLS ? OFF_W2 + pi : OFF_B2 + (pi - HID * NCLS);
+    const int j = pi < HID * NCLS ? pi : HID * NCLS + HID + (pi - HID * NCLS);
     float g = 0.f;
-    if (mode == 2) {
-      g = gin[i];
-    } else if (i < OFF_W2) {
-      g = sum_strided(P2 + i, P2N, n2) * (1.f / 255.f);
-    } else if (i >= OFF_B1 && i < OFF_B2) {
-      g = sum_strided(P2 + OFF_W2 + (i - OFF_B1), P2N, n2) * (1.f / 255.f);   // db1 = the pixel-784 row
-    } else {
-      const int j = i < OFF_B1 ? i - OFF_W2 : HID * NCLS + HID + (i - OFF_B2);
-      g = sum_strided(P1 + j, P1N, n1);
+    if (mode != 2) {
+      for (int b = lane; b < n1; b += 64) g += P1[(size_t)b * P1N + j];
+      g = wave_sum(g);
     }
-    if (mode == 1) gout[i] = g;
-    else params[i] -= (*lr_ptr) * scale * g;
+    if (lane == 0) apply_one(params, i, g, gin, gout, lr_ptr, scale, mode);
+    return;
   }
-  if (i < OFF_W2 && mode != 1) {
-    uint16_t hi, mi, lo;
-    split3(params[i], hi, mi, lo);
-    const int k = i / HID, n = i % HID;
-    W1S[w1f_index(k, n, 0)] = hi;
-    W1S[w1f_index(k, n, 1)] = mi;
-    W1S[w1f_index(k, n, 2)] = lo;
+  const int il = blockIdx.x * blockDim.x + threadIdx.x;
+  if (il < NP2) {
+    const int i = il < OFF_W2 ? il : OFF_B1 + (il - OFF_W2);
+    if (mode != 3) {
+      // db1 = the pixel-784 row of the slabs
+      const float g = mode == 2 ? 0.f : sum_strided(P2 + il, P2N, n2) * (1.f / 255.f);
+      apply_one(params, i, g, gin, gout, lr_ptr, scale, mode);
+    }
+    if (il < OFF_W2 && mode != 1) {
+      uint16_t hi, mi, lo;
+      split3(params[i], hi, mi, lo);
+      const int k = i / HID, n = i % HID;
+      W1S[w1f_index(k, n, 0)] = hi;
+      W1S[w1f_index(k, n, 1)] = mi;
+      W1S[w1f_index(k, n, 2)] = lo;
+    }
   }
   if (blockIdx.x == 0 && threadIdx.x < 64 && (mode == 0 || mode == 1)) {
-    // wave 0 of block 0: lanes over the row blocks, fixed-order wave sum
+    // wave 0 of block 0: lanes over the row tiles, fixed-order wave sum
     float ls = 0.f, cs = 0.f;
     for (int b = threadIdx.x; b < n1; b += 64) {
       ls += P1[(size_t)b * P1N + P1N - 2];
@@ -452,19 +437,18 @@ __global__ __launch_bounds__(256) void mlpg_apply(float* __restrict__ params, co
 }  // namespace mlpg
 }  // namespace dtfk
 
-static int g_stop = 0;   // probe knob (scripts/probes/mlpg_stages.py): end mlpg_fwd after stage 1/2/3
-
 extern "C" {
-
-void dtfk_mlpg_set_stop(int s) { g_stop = s; }
 
 int dtfk_mlpg_p1_floats() { return dtfk::mlpg::P1N; }
 
-hipError_t dtfk_mlpg_fwd(const void* x, const void* labels, int B, int BP, const void* W1S, const float* params,
-                         float* P1, void* dz2S, int act, int naive, float gscale, hipStream_t s) {
+hipError_t dtfk_mlpg_fwd(const void* x, const void* labels, int B, int BP, const void* W1F, const float* params,
+                         float* a2g, float* P1, void* dz2F, int act, int naive, float gscale, hipStream_t s) {
   using namespace dtfk::mlpg;
-  hipLaunchKernelGGL(mlpg_fwd, dim3(BP / R1), dim3(256), 0, s, (const uint8_t*)x, (const uint8_t*)labels, B, BP,
-                     (const uint16_t*)W1S, params, P1, (uint16_t*)dz2S, act, naive, gscale, g_stop);
+  if (BP % 64) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(mlpg_l1, dim3(BP / 64, 7), dim3(256), 0, s, (const uint8_t*)x, B, (const uint16_t*)W1F, params,
+                     a2g, act);
+  hipLaunchKernelGGL(mlpg_head, dim3(BP / 16), dim3(256), 0, s, a2g, (const uint8_t*)labels, B, params, P1,
+                     (uint16_t*)dz2F, act, naive, gscale);
   return hipGetLastError();
 }
 
@@ -482,7 +466,7 @@ hipError_t dtfk_mlpg_apply(float* params, const float* P1, int n1, const float* 
                            float* gout, const float* lr, float scale, void* W1S, float* metrics, int ring,
                            long long* gstep, int B, int mode, hipStream_t s) {
   using namespace dtfk::mlpg;
-  hipLaunchKernelGGL(mlpg_apply, dim3((NPARAM + 255) / 256), dim3(256), 0, s, params, P1, n1, P2, n2, gin, gout, lr,
+  hipLaunchKernelGGL(mlpg_apply, dim3(NB2 + (NP1 + 3) / 4), dim3(256), 0, s, params, P1, n1, P2, n2, gin, gout, lr,
                      scale, (uint16_t*)W1S, metrics, ring, gstep, 1.f / (float)B, mode);
   return hipGetLastError();
 }

@@ -286,10 +286,11 @@ class FusedMLPTrainer:
 
 
 class GemmMLPTrainer:
-    """Large-batch step of the same model (csrc/kernels/mlp_gemm.hip), 3
-    launches: `mlpg_fwd` (one workgroup per 64 rows: the hidden layer on bf16
-    MFMA with W1 as an exact 3-way bf16 split, then act, logits, softmax-xent,
-    dz2 and this block's dW2/db2 partials without leaving the workgroup),
+    """Large-batch step of the same model (csrc/kernels/mlp_gemm.hip), 4
+    launches: `mlpg_l1` (one workgroup per 64 rows x 16 hidden units: the
+    hidden layer on bf16 MFMA with W1 as an exact 3-way bf16 split) and
+    `mlpg_head` (one workgroup per 16 rows, its waves splitting the hidden
+    tiles: logits, softmax-xent, dz2 and the dW2/db2 partials on exact-f32 MFMA),
     `mlpg_wgrad` ([dW1; db1] over a 64-pixel-block x 256-row-chunk grid, dz2 as
     its exact split) and `mlpg_apply` (fixed-order slab reduction, SGD, W1
     fragment-image refresh, metrics).  The fused engines contract the batch serially inside
@@ -321,7 +322,8 @@ class GemmMLPTrainer:
         self.params = torch.zeros(NPARAM, dtype=f32, device=dev)
         self.W1S = torch.zeros(3 * 112 * 800, dtype=torch.bfloat16, device=dev)
         self.dz2S = torch.zeros(3 * 112 * self.nchunk * wc, dtype=torch.bfloat16, device=dev)
-        self.P1 = torch.zeros(self.BP // 64 * self.C.mlpg_p1_floats(), dtype=f32, device=dev)
+        self.a2 = torch.zeros(self.BP * 112, dtype=f32, device=dev)
+        self.P1 = torch.zeros(self.BP // 16 * self.C.mlpg_p1_floats(), dtype=f32, device=dev)
         self.P2 = torch.zeros(self.nchunk * self.C.mlpg_p2_floats(), dtype=f32, device=dev)
         self.grads = torch.zeros(NPARAM, dtype=f32, device=dev) if self.world_size > 1 else None
         self.lr = torch.tensor([lr], dtype=f32, device=dev)
@@ -377,7 +379,7 @@ class GemmMLPTrainer:
         if x_kind != 0:
             raise ValueError("GemmMLPTrainer reads uint8 pixel records (x_kind 0)")
         C, B = self.C, self.B
-        C.mlpg_fwd(x, x_off, labels, labels_off, B, self.W1S, self.params, self.P1, self.dz2S, self.act,
+        C.mlpg_fwd(x, x_off, labels, labels_off, B, self.W1S, self.params, self.a2, self.P1, self.dz2S, self.act,
                    self.naive, 1.0 / B)
         C.mlpg_wgrad(x, x_off, B, self.dz2S, self.P2, self.nchunk)
         if self.world_size == 1:

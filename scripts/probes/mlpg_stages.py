@@ -1,7 +1,6 @@
 #!/usr/bin/env python3
-"""Per-kernel / per-stage timing of the large-batch MLP step (mlp_gemm.hip):
-mlpg_fwd ended after its K loop (stop=1), after softmax (2), after dz2 (3),
-full (0); mlpg_wgrad; mlpg_apply.  One JSON line
+"""Per-launch timing of the large-batch MLP step (mlp_gemm.hip): the forward
+(mlpg_l1 + mlpg_head), mlpg_wgrad, mlpg_apply and the whole step.  One JSON line
 per (B, item): us per launch over back-to-back launches (events)."""
 import json
 import os
@@ -37,11 +36,8 @@ def main():
         tr = mlp.GemmMLPTrainer(batch_size=B, device=dev)
         C = tr.C
         out = {"B": B, "nchunk": tr.nchunk}
-        for stop in (1, 2, 3, 0):
-            C.mlpg_set_stop(stop)
-            out[f"fwd_stop{stop}_us"] = round(timeit(lambda: C.mlpg_fwd(x, 0, y, 0, B, tr.W1S, tr.params, tr.P1,
-                                                                      tr.dz2S, tr.act, False, 1.0 / B)), 2)
-        C.mlpg_set_stop(0)
+        out["fwd_us"] = round(timeit(lambda: C.mlpg_fwd(x, 0, y, 0, B, tr.W1S, tr.params, tr.a2, tr.P1, tr.dz2S,
+                                                       tr.act, False, 1.0 / B)), 2)
         out["wgrad_us"] = round(timeit(lambda: C.mlpg_wgrad(x, 0, B, tr.dz2S, tr.P2, tr.nchunk)), 2)
         out["apply_us"] = round(timeit(lambda: tr._apply(0)), 2)
         out["step_us"] = round(timeit(lambda: tr.enqueue_step(x, 0, 0, y, 0)), 2)

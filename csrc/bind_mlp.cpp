@@ -32,7 +32,7 @@ int dtfk_mlpg_p1_floats();
 hipError_t dtfk_mlpg_fwd(const void* x, const void* labels, int B, int BP, const void* W1F, const float* params,
                          float* a2g, float* P1, void* dz2F, int act, int naive, float gscale, hipStream_t s);
 hipError_t dtfk_mlpg_wgrad(const void* x, int B, const void* dz2F, float* P2, int nchunk, hipStream_t s);
-int dtfk_mlpg_wchunk();
+int dtfk_mlpg_wchunk(int B);
 int dtfk_mlpg_p2_floats();
 hipError_t dtfk_mlpg_apply(float* params, const float* P1, int n1, const float* P2, int n2, const float* gin,
                            float* gout, const float* lr, float scale, void* W1S, float* metrics, int ring,
@@ -286,7 +286,7 @@ static const uint8_t* stage_ptr(const at::Tensor& st, int64_t off, int64_t nbyte
 
 static int64_t mlpg_bp(int B) { return ((int64_t)B + 63) / 64 * 64; }
 static int64_t mlpg_bp2(int B) {
-  const int64_t c = dtfk_mlpg_wchunk();
+  const int64_t c = dtfk_mlpg_wchunk(B);
   return ((int64_t)B + c - 1) / c * c;
 }
 
@@ -312,7 +312,7 @@ void mlpg_wgrad(at::Tensor x, int64_t x_off, int B, at::Tensor dz2F, at::Tensor 
   const int64_t BP2 = mlpg_bp2(B);
   const uint8_t* px = stage_ptr(x, x_off, (int64_t)B * 784, "x");
   if (reinterpret_cast<uintptr_t>(px) & 15) throw std::runtime_error("mlpg_wgrad: x must be 16-byte aligned");
-  if (nchunk != BP2 / dtfk_mlpg_wchunk()) throw std::runtime_error("mlpg_wgrad: nchunk must be ceil(B / chunk)");
+  if (nchunk != BP2 / dtfk_mlpg_wchunk(B)) throw std::runtime_error("mlpg_wgrad: nchunk must be ceil(B / chunk)");
   need(dz2F, at::kBFloat16, 3 * 112 * BP2, "dz2F");
   need(P2, at::kFloat, (int64_t)nchunk * dtfk_mlpg_p2_floats(), "P2");
   hip_check(dtfk_mlpg_wgrad(px, B, dz2F.data_ptr(), P2.data_ptr<float>(), nchunk, cur_stream()), "mlpg_wgrad");

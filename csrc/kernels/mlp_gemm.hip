@@ -1,4 +1,4 @@
-// Large-batch MLP step (784-100-10, example.py:69-128): three launches.
+// Large-batch MLP step (784-100-10, example.py:69-128): four launches.
 //
 // The fused / persistent engines (mlp_step.hip, mlp_persist_f32.hip) are
 // latency engines for the reference's batch of 100: one wave owns a 16x16
@@ -7,20 +7,19 @@
 // better here: [B,784]x[784,100] has 2*ceil(B/64) 64x64 tiles, i.e. 32 f32-MFMA
 // workgroups at B=1024 (57 us, rocprofv3).  This step is shaped for the batch:
 //
-//   mlpg_fwd    one workgroup per 64 rows; its 4 waves split the 25 k-steps
-//               and each covers all 64 x 112 outputs, so every operand is
-//               loaded once per workgroup straight into MFMA fragments (W1 is
-//               kept as a fragment image, 1 KB coalesced loads), with the next
-//               k-step's loads in flight under 84 MFMAs and no barrier in the
-//               K loop.  W1 rides as an exact 3-way bf16 split (hi + mid + lo
-//               == the fp32 weight; uint8 pixels are exact in bf16): exact
-//               products, fp32 accumulate.  Partials meet in LDS, then per
-//               row: a2 = act(z/255 + b1), logits, softmax-xent, dlog,
-//               dz2 = (dlog W2^T) act'(a2) and this block's [dW2; db2] on
-//               exact-f32 MFMA.  dz2 leaves as its exact split, in the
-//               weight-gradient kernel's fragment order.
+//   mlpg_l1     one workgroup per (64 rows, 16 hidden units): its 4 waves
+//               split the 25 k-steps and request their whole operand slice in
+//               one shot -- W1 kept as a fragment image of its exact 3-way
+//               bf16 split (hi + mid + lo == the fp32 weight; uint8 pixels are
+//               exact in bf16: exact products, fp32 accumulate), 1 KB coalesced
+//               fragment loads -- partials meet in LDS, a2 = act(z/255 + b1).
+//   mlpg_head   one workgroup per 16 rows: logits, softmax-xent, dlog,
+//               dz2 = (dlog W2^T) act'(a2) and the [dW2; db2] partials on
+//               exact-f32 MFMA, the waves splitting the hidden tiles; dz2
+//               leaves as its exact split in the weight-gradient kernel's
+//               fragment order.
 //   mlpg_wgrad  [dW1; db1] = [x | 255]^T dz2 / 255 per (64-pixel block,
-//               256-row chunk): waves split the chunk, x tiles transposed
+//               128- or 256-row chunk): waves split the chunk, x tiles transposed
 //               through wave-private LDS, dz2 straight from its fragment
 //               image; one fp32 slab per chunk.
 //   mlpg_apply  sums the slabs in a fixed order (deterministic), SGD, refreshes
@@ -28,9 +27,11 @@
 //               same kernel first writes the reduced gradient (RCCL
 //               all-reduce), then applies it.
 //
-// Measured (scripts/probes/mlpg_stages.py) -- the first cut staged operands
-// through LDS with one barrier per k-step and paid a full load latency per
-// k-step (a load under a branch, and a HIP uint4 array kept in scratch).
+// Measured (scripts/probes/mlpg_stages.py, profiles/mlp_large_batch_r4.md) --
+// the first cut staged operands through LDS with one barrier per k-step and
+// paid a full load latency per k-step (a load under a branch, and a HIP uint4
+// array kept in scratch); a fused forward streaming all of W1 through every
+// workgroup was latency-chained over 7 k-step rounds.
 #include "common.h"
 
 namespace dtfk {
@@ -263,8 +264,10 @@ __global__ __launch_bounds__(256) void mlpg_head(const float* __restrict__ a2g, 
   }
 }
 
-constexpr int WKPW = 2;                 // mlpg_wgrad: 32-row k-steps per wave (chunk = 4 waves x 2 x 32 = 256 rows)
-constexpr int WCHUNK = NW * WKPW * 32;
+// mlpg_wgrad: WKPW 32-row k-steps per wave, chunk = 4 waves x WKPW x 32 rows:
+// 128 (WKPW 1) up to B = 2048 -- more workgroups for a small batch -- else 256
+__host__ __device__ constexpr int wchunk_of(int wkpw) { return NW * wkpw * 32; }
+inline int wkpw_for(int B) { return B <= 2048 ? 1 : 2; }
 constexpr int P2N = (DIN + 1) * HID;     // one dW1 slab: 784 pixel rows + the db1 row
 
 // [dW1; db1] partial of one 256-row batch chunk for 64 pixels (+ the constant
@@ -273,13 +276,14 @@ constexpr int P2N = (DIN + 1) * HID;     // one dW1 slab: 784 pixel rows + the d
 // a wave-private LDS tile transposed to [pixel][batch] bf16 (A fragments),
 // dz2 comes straight from its fragment image (B), no block barrier until
 // the 4 partials meet in LDS (owner wave per tile, wave order).
+template <int WKPW>
 __global__ __launch_bounds__(256, 1) void mlpg_wgrad(const uint8_t* __restrict__ x, int B,
                                                      const uint16_t* __restrict__ dz2F, float* __restrict__ P2) {
   __shared__ __attribute__((aligned(16))) float zred[NW * NT * 256];   // 112 KB (x tiles before the reduction)
   const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int lr = lane & 15, lg4 = lane >> 4;
   const int p0 = blockIdx.x * 64;
-  const int c0 = blockIdx.y * WCHUNK;
+  const int c0 = blockIdx.y * wchunk_of(WKPW);
   uint16_t* xt = reinterpret_cast<uint16_t*>(zred) + wave * (WKPW * 64 * XTLD);   // [step][64 px][XTLD]
   // x: lane -> batch row (lane & 31) of the step, pixels p0 + 32 * (lane >> 5) .. + 32
   const int xb = lane & 31, xh = lane >> 5;
@@ -452,13 +456,17 @@ hipError_t dtfk_mlpg_fwd(const void* x, const void* labels, int B, int BP, const
   return hipGetLastError();
 }
 
-int dtfk_mlpg_wchunk() { return dtfk::mlpg::WCHUNK; }
+int dtfk_mlpg_wchunk(int B) { return dtfk::mlpg::wchunk_of(dtfk::mlpg::wkpw_for(B)); }
 int dtfk_mlpg_p2_floats() { return dtfk::mlpg::P2N; }
 
 hipError_t dtfk_mlpg_wgrad(const void* x, int B, const void* dz2F, float* P2, int nchunk, hipStream_t s) {
   using namespace dtfk::mlpg;
-  hipLaunchKernelGGL(mlpg_wgrad, dim3((DIN + 64) / 64, nchunk), dim3(256), 0, s, (const uint8_t*)x, B,
-                     (const uint16_t*)dz2F, P2);
+  if (wkpw_for(B) == 1)
+    hipLaunchKernelGGL(mlpg_wgrad<1>, dim3((DIN + 64) / 64, nchunk), dim3(256), 0, s, (const uint8_t*)x, B,
+                       (const uint16_t*)dz2F, P2);
+  else
+    hipLaunchKernelGGL(mlpg_wgrad<2>, dim3((DIN + 64) / 64, nchunk), dim3(256), 0, s, (const uint8_t*)x, B,
+                       (const uint16_t*)dz2F, P2);
   return hipGetLastError();
 }
 

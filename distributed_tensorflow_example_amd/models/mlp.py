@@ -315,9 +315,9 @@ class GemmMLPTrainer:
         self.act_name = act
         self.naive = bool(naive_loss)
         f32 = torch.float32
-        # dW1: one workgroup per (64-pixel block, 256-row batch chunk); the
+        # dW1: one workgroup per (64-pixel block, 128- or 256-row batch chunk); the
         # B-fragment image of dz2 is padded (with zeros) to whole chunks
-        wc = self.C.mlpg_wchunk()
+        wc = self.C.mlpg_wchunk(B)
         self.nchunk = (B + wc - 1) // wc
         self.params = torch.zeros(NPARAM, dtype=f32, device=dev)
         self.W1S = torch.zeros(3 * 112 * 800, dtype=torch.bfloat16, device=dev)
@@ -421,7 +421,10 @@ class MLPStepRunner:
             raise ValueError("prefetch must be 'serial' or 'side'")
         self.t = trainer
         self.epoch = epoch
-        self.g = int(min(steps_per_graph, epoch.num_batches))
+        # a chunk may run across the epoch boundary (its records are copied in two
+        # pieces): at large batch an epoch is only ~13 steps, and the side-stream
+        # prefetch pays its cross-queue synchronisation once per chunk
+        self.g = int(max(1, steps_per_graph))
         self.use_graph = use_graph
         self.prefetch = prefetch
         self.side = torch.cuda.Stream(device=trainer.device)
@@ -436,7 +439,13 @@ class MLPStepRunner:
 
     def _copy_chunk(self, dst: torch.Tensor, b0: int, g: int):
         ep = self.epoch
-        self.t.C.memcpy_h2d_async(dst, 0, ep.host, b0 * ep.rec, g * ep.rec)
+        nb, off = ep.num_batches, 0
+        while g > 0:   # batches b0 .. b0+g-1 of the epoch, wrapping at its end
+            n = min(g, nb - b0)
+            self.t.C.memcpy_h2d_async(dst, off, ep.host, b0 * ep.rec, n * ep.rec)
+            off += n * ep.rec
+            b0 = (b0 + n) % nb
+            g -= n
 
     def _emit_steps(self, g: int, buf: torch.Tensor, ipar: int):
         t = self.t
@@ -471,7 +480,7 @@ class MLPStepRunner:
         nb = self.epoch.num_batches
         while left > 0:
             b0 = cursor % nb
-            g = min(self.g, left, nb - b0)
+            g = min(self.g, left)
             out.append((b0, g))
             cursor += g
             left -= g
@@ -635,7 +644,7 @@ class PersistentMLPRunner:
         nb = self.epoch.num_batches
         while left > 0:
             b0 = cursor % nb
-            g = min(self.g, left, nb - b0)
+            g = min(self.g, left)
             out.append((b0, g))
             cursor += g
             left -= g

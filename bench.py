@@ -77,8 +77,8 @@ def main(argv=None):
     ap.add_argument("--train-examples", type=int, default=55000)
     ap.add_argument("--prefetch", choices=["auto", "serial", "side"], default="auto",
                     help="3-launch / gemm engines: input chunk copy at the head of each chunk graph (serial) or on a "
-                         "side stream under the previous chunk (side); auto = side for batch >= 2048 (the copy is "
-                         "then longer than the step: 41.9M vs 64.5M samples/s at B=4096), else serial")
+                         "side stream under the previous chunk (side); auto = side on the large-batch engine "
+                         "(B=1024: 33.3M vs 25.8M samples/s, B=4096: 71.0M vs 44.5M), serial on the 3-launch path")
     ap.add_argument("--tune-steps", type=int, default=300,
                     help="N>1: steps used to time each valid exchange strategy before the timed run (0: first valid)")
     ap.add_argument("--engine", choices=["auto", "persistent", "launches", "gemm"], default="auto",
@@ -120,7 +120,7 @@ def main(argv=None):
     can_persist = a.batch <= 112 and a.engine in ("auto", "persistent")
     use_gemm = a.engine == "gemm" or (a.engine == "auto" and a.batch >= 256)
     if a.prefetch == "auto":
-        a.prefetch = "side" if a.batch >= 2048 else "serial"
+        a.prefetch = "side" if use_gemm else "serial"
     # persistent engine: the warmup is split into a validation part (setup,
     # consistency check, exchange tuning) and a final short launch issued right
     # before the timed region, so the GPU is not coming out of an idle clock

@@ -644,7 +644,7 @@ class PersistentMLPRunner:
         nb = self.epoch.num_batches
         while left > 0:
             b0 = cursor % nb
-            g = min(self.g, left)
+            g = min(self.g, left, nb - b0)
             out.append((b0, g))
             cursor += g
             left -= g

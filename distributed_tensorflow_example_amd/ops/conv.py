@@ -11,13 +11,16 @@ this removes is the glue around them in a bf16-compute / fp32-master step:
   when the weight is managed by DDP (ops.grad_sink), folds the bf16 dW into
   the fp32 bucket view with one mixed-dtype add -- no bf16->fp32 cast pass and
   no separate AccumulateGrad add;
-* a 1x1 / stride-1 convolution's weight gradient is a plain GEMM over the
-  NHWC rows, dW[cout, cin] = dy[NHW, cout]^T x[NHW, cin]: it can run on the
-  in-tree GEMM (gemm_big.hip, split-K over the rows, fp32 out accumulated
-  straight into the bucket) instead of MIOpen's atomic wrw solver, whose
-  zero-fill + scale + fp32->bf16 cast passes and our bf16->fp32 add cost more
-  than the GEMM itself (ResNet-50, profiles/resnet50_r4.md).  Both routes are
-  timed once per shape (`DTF_CONV_GEMM_DW`: auto / never / always).
+* a 1x1 / stride-1 convolution on NHWC activations is a plain GEMM over the
+  rows: y[NHW, cout] = x[NHW, cin] W^T, dx = dy W, dW = dy^T x.  Each of the
+  three products picks, per shape and once (timed on the layer's own
+  operands), between MIOpen and the GEMM engines: hipBLASLt (`torch.mm`) or
+  the in-tree `gemm_big.hip` for y / dx, and for dW the in-tree GEMM with
+  split-K accumulated straight into the fp32 bucket (MIOpen's atomic wrw
+  solver adds zero-fill, scale and fp32 -> bf16 cast passes, then our bf16 ->
+  fp32 add).  MIOpen keeps the early layers' forwards; the GEMMs win most
+  input gradients (ResNet-50 B=128: 20-60 % per layer,
+  profiles/resnet50_r4.md).  `DTF_CONV_GEMM`: auto (default) / never.
 Any other case (CPU, no shadow, eval under a different dtype) is plain
 `nn.Conv2d`.
 """
@@ -30,16 +33,16 @@ import torch.nn.functional as F
 
 from . import grad_sink
 
-_DW_POLICY = os.environ.get("DTF_CONV_GEMM_DW", "auto")
-_dw_choice: dict = {}
-_dw_timings: dict = {}
+_POLICY = os.environ.get("DTF_CONV_GEMM", "auto")
+_choice: dict = {}
+_timings: dict = {}
 
 
-def _gemm_dw_ok(x, dy, w16, stride, padding, dilation, groups) -> bool:
+def _gemm_ok(x, w16, stride, padding, dilation, groups) -> bool:
+    """A 1x1 / stride-1 / unpadded / ungrouped conv on channels_last bf16 rows."""
     return (w16.shape[2] == 1 and w16.shape[3] == 1 and tuple(stride) == (1, 1) and tuple(padding) == (0, 0)
-            and groups == 1 and x.is_cuda and x.dtype == torch.bfloat16 and dy.dtype == torch.bfloat16
+            and groups == 1 and x.is_cuda and x.dtype == torch.bfloat16
             and x.is_contiguous(memory_format=torch.channels_last)
-            and dy.is_contiguous(memory_format=torch.channels_last)
             and (x.shape[0] * x.shape[2] * x.shape[3]) % 64 == 0)
 
 
@@ -48,38 +51,92 @@ def _rows(t):
     return t.permute(0, 2, 3, 1).reshape(-1, t.shape[1])
 
 
-def _use_gemm_dw(x, dy, w16) -> bool:
-    """Per shape: the in-tree GEMM (accumulating into an fp32 target) vs MIOpen's
-    weight gradient + the bf16 -> fp32 add, each timed once on these operands."""
-    if _DW_POLICY == "never":
-        return False
-    if _DW_POLICY == "always":
-        return True
-    key = (tuple(x.shape), w16.shape[0])
-    hit = _dw_choice.get(key)
+def _cl_empty(n, c, h, w, like):
+    return torch.empty((n, c, h, w), device=like.device, dtype=like.dtype, memory_format=torch.channels_last)
+
+
+def _fwd_gemm(engine, x, w16):
+    y = _cl_empty(x.shape[0], w16.shape[0], x.shape[2], x.shape[3], x)
+    x2, w2, y2 = _rows(x), w16.view(w16.shape[0], w16.shape[1]), _rows(y)
+    if engine != "gemm_big" or not _C().gemm_big(x2, False, w2, True, y2):
+        torch.mm(x2, w2.t(), out=y2)
+    return y
+
+
+def _dx_gemm(engine, dy, w16, x_shape):
+    dx = _cl_empty(x_shape[0], x_shape[1], x_shape[2], x_shape[3], dy)
+    dy2, w2, dx2 = _rows(dy), w16.view(w16.shape[0], w16.shape[1]), _rows(dx)
+    if engine != "gemm_big" or not _C().gemm_big(dy2, False, w2, False, dx2):
+        torch.mm(dy2, w2, out=dx2)
+    return dx
+
+
+def _C():
+    from .. import _native
+    return _native.load()
+
+
+def _pick(role, key, cands) -> str:
+    """Fastest of `cands` {name: fn} for (role, key), timed once (MIOpen first)."""
+    k = (role,) + key
+    hit = _choice.get(k)
     if hit is None:
-        if torch.cuda.is_current_stream_capturing():
-            return False
+        if _POLICY == "never" or torch.cuda.is_current_stream_capturing():
+            return "miopen"
+        from . import big_gemm
+        t = {name: big_gemm._time(fn, reps=3) for name, fn in cands.items()}
+        hit = _choice[k] = min(t, key=t.get)
+        _timings[k] = {n: round(v, 4) for n, v in t.items()}
+    return hit
+
+
+def _fwd_engine(x, w16) -> str:
+    if _POLICY == "never":
+        return "miopen"
+    key = (tuple(x.shape), w16.shape[0])
+    if ("fwd",) + key not in _choice:
+        cands = {"miopen": lambda: F.conv2d(x, w16),
+                 "hipblaslt": lambda: _fwd_gemm("hipblaslt", x, w16),
+                 "gemm_big": lambda: _fwd_gemm("gemm_big", x, w16)}
+        return _pick("fwd", key, cands)
+    return _choice[("fwd",) + key]
+
+
+def _dx_engine(dy, x, w16) -> str:
+    if _POLICY == "never":
+        return "miopen"
+    key = (tuple(x.shape), w16.shape[0])
+    if ("dx",) + key not in _choice:
+        cands = {"miopen": lambda: torch.ops.aten.convolution_backward(
+                     dy, x, w16, None, (1, 1), (0, 0), (1, 1), False, [0, 0], 1, [True, False, False]),
+                 "hipblaslt": lambda: _dx_gemm("hipblaslt", dy, w16, x.shape),
+                 "gemm_big": lambda: _dx_gemm("gemm_big", dy, w16, x.shape)}
+        return _pick("dx", key, cands)
+    return _choice[("dx",) + key]
+
+
+def _dw_engine(dy, x, w16) -> str:
+    """The in-tree GEMM accumulating into an fp32 target vs MIOpen's weight
+    gradient + the bf16 -> fp32 add."""
+    if _POLICY == "never":
+        return "miopen"
+    key = (tuple(x.shape), w16.shape[0])
+    if ("dw",) + key not in _choice:
         from . import big_gemm
         acc = torch.zeros(w16.shape[0], w16.shape[1], device=x.device, dtype=torch.float32)
         x2, dy2 = _rows(x), _rows(dy)
-
-        def ours():
-            big_gemm.linear_dw(dy2, x2, into=acc)
 
         def miopen():
             dw = torch.ops.aten.convolution_backward(dy, x, w16, None, (1, 1), (0, 0), (1, 1), False, [0, 0], 1,
                                                      [False, True, False])[1]
             acc.add_(dw.view(acc.shape))
-        t_ours, t_theirs = big_gemm._time(ours, reps=3), big_gemm._time(miopen, reps=3)
-        hit = _dw_choice[key] = t_ours <= t_theirs
-        _dw_timings[key] = (round(t_ours, 4), round(t_theirs, 4))
-    return hit
+        return _pick("dw", key, {"miopen": miopen, "gemm_big": lambda: big_gemm.linear_dw(dy2, x2, into=acc)})
+    return _choice[("dw",) + key]
 
 
-def dw_choices() -> dict:
-    """{(x shape, cout): (gemm chosen, (gemm ms, miopen ms))}"""
-    return {k: (v, _dw_timings.get(k)) for k, v in _dw_choice.items()}
+def choices() -> dict:
+    """{(role, x shape, cout): (engine, {engine: ms})}"""
+    return {k: (v, _timings.get(k)) for k, v in _choice.items()}
 
 
 class _ShadowConv(torch.autograd.Function):
@@ -88,6 +145,11 @@ class _ShadowConv(torch.autograd.Function):
         ctx.save_for_backward(x, w16)
         ctx.conf = (stride, padding, dilation, groups)
         ctx.w = w
+        ctx.gemm = _gemm_ok(x, w16, stride, padding, dilation, groups)
+        if ctx.gemm:
+            eng = _fwd_engine(x, w16)
+            if eng != "miopen":
+                return _fwd_gemm(eng, x, w16)
         return F.conv2d(x, w16, None, stride, padding, dilation, groups)
 
     @staticmethod
@@ -98,25 +160,33 @@ class _ShadowConv(torch.autograd.Function):
         need_w = ctx.needs_input_grad[1]
         dy = dy.to(w16.dtype)
         w = ctx.w
-        if need_w and _gemm_dw_ok(x, dy, w16, stride, padding, dilation, groups) and _use_gemm_dw(x, dy, w16):
+        gemm = ctx.gemm and dy.is_contiguous(memory_format=torch.channels_last)
+        dx_eng = _dx_engine(dy, x, w16) if gemm and need_x else "miopen"
+        dw_eng = _dw_engine(dy, x, w16) if gemm and need_w else "miopen"
+        # MIOpen's share: one convolution_backward call for whatever stays on it
+        mx, mw = need_x and dx_eng == "miopen", need_w and dw_eng == "miopen"
+        dx = dw = None
+        if mx or mw:
+            dx, dw, _ = torch.ops.aten.convolution_backward(dy, x, w16, None, stride, padding, dilation, False,
+                                                            [0, 0], groups, [mx, mw, False])
+        if need_x and not mx:
+            dx = _dx_gemm(dx_eng, dy, w16, x.shape)
+        if not need_w:
+            return dx, None, None, None, None, None, None
+        sink = grad_sink.enabled(w) and (w.grad is None or w.grad.is_contiguous())
+        if not mw:
             from . import big_gemm
-            dx = (torch.ops.aten.convolution_backward(dy, x, w16, None, stride, padding, dilation, False, [0, 0],
-                                                      groups, [True, False, False])[0] if need_x else None)
-            sink = grad_sink.enabled(w) and (w.grad is None or w.grad.is_contiguous())
             if sink:
                 g = grad_sink.target(w)
                 big_gemm.linear_dw(_rows(dy), _rows(x), into=g.view(g.shape[0], g.shape[1]))
                 grad_sink.done(w)
                 return dx, None, None, None, None, None, None
-            dw = big_gemm.linear_dw(_rows(dy), _rows(x)).view(w.shape)
-            return dx, dw.to(w.dtype), None, None, None, None, None
-        dx, dw, _ = torch.ops.aten.convolution_backward(dy, x, w16, None, stride, padding, dilation, False,
-                                                        [0, 0], groups, [need_x, need_w, False])
-        if need_w and grad_sink.enabled(w):
+            return dx, big_gemm.linear_dw(_rows(dy), _rows(x)).view(w.shape).to(w.dtype), None, None, None, None, None
+        if sink:
             grad_sink.target(w).add_(dw)
             grad_sink.done(w)
             return dx, None, None, None, None, None, None
-        return dx, (dw.to(w.dtype) if need_w else None), None, None, None, None, None
+        return dx, dw.to(w.dtype), None, None, None, None, None
 
 
 class ShadowConv2d(torch.nn.Conv2d):

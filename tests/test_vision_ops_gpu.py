@@ -41,23 +41,36 @@ def test_maxpool_ties_take_first_and_nan_propagates(native):
     assert x.grad[0, 1, 0, 0] == 1 and x.grad[0, 1, 0, 1] == 0 and x.grad[0, 1, 1, 0] == 0
 
 
+@pytest.mark.parametrize("engines", [("hipblaslt", "hipblaslt", "gemm_big"), ("gemm_big", "gemm_big", "gemm_big"),
+                                     ("miopen", "miopen", "miopen"), ("miopen", "hipblaslt", "miopen")])
 @pytest.mark.parametrize("n,cin,cout,hw", [(8, 64, 256, 28), (4, 256, 64, 14), (16, 512, 128, 7)])
-def test_conv1x1_gemm_wgrad_matches_fp32(native, n, cin, cout, hw, monkeypatch):
+def test_conv1x1_engines_match_fp32(native, n, cin, cout, hw, engines):
+    """Every engine choice of the 1x1 convolution's three products (ops/conv.py)
+    against an fp32 einsum reference."""
     from distributed_tensorflow_example_amd.ops import conv
 
-    monkeypatch.setattr(conv, "_DW_POLICY", "always")
     torch.manual_seed(1)
     m = conv.ShadowConv2d(cin, cout, 1, bias=False).cuda().to(memory_format=torch.channels_last)
     conv.attach_shadows(m)
     x = torch.randn(n, cin, hw, hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    x.requires_grad_(True)
-    y = m(x)
-    g = torch.randn_like(y.float()).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    y.backward(g)
+    key = (tuple(x.shape), cout)
+    for role, eng in zip(("fwd", "dx", "dw"), engines):
+        conv._choice[(role,) + key] = eng
+    try:
+        x.requires_grad_(True)
+        y = m(x)
+        assert y.is_contiguous(memory_format=torch.channels_last)
+        g = torch.randn_like(y.float()).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        y.backward(g)
+    finally:
+        for role in ("fwd", "dx", "dw"):
+            conv._choice.pop((role,) + key, None)
     xr = x.detach().float()
-    wr = m.weight.detach().to(torch.bfloat16).float()
+    wr = m.weight.detach().to(torch.bfloat16).float().view(cout, cin)
     gr = g.float()
+    y_ref = torch.einsum("nihw,oi->nohw", xr, wr)
     dw_ref = torch.einsum("nohw,nihw->oi", gr, xr).view_as(m.weight)
-    dx_ref = torch.einsum("nohw,oi->nihw", gr, wr.view(cout, cin))
+    dx_ref = torch.einsum("nohw,oi->nihw", gr, wr)
+    torch.testing.assert_close(y.float(), y_ref, rtol=2e-2, atol=2e-2 * y_ref.abs().max().item())
     torch.testing.assert_close(m.weight.grad, dw_ref, rtol=2e-3, atol=2e-3 * dw_ref.abs().max().item())
     torch.testing.assert_close(x.grad.float(), dx_ref, rtol=2e-2, atol=2e-2 * dx_ref.abs().max().item())

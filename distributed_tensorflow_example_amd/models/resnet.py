@@ -8,6 +8,8 @@ DDP all-reduce overlapped with backward (parallel.ddp).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -16,10 +18,13 @@ from .. import ops
 from ..ops.bn import FusedBatchNorm2d
 from ..ops.conv import ShadowConv2d, attach_shadows as _attach_conv_shadows
 from ..ops.pool import max_pool2d
+from ..ops.transformer import GradSlot
 
 
 class Bottleneck(nn.Module):
     expansion = 4
+    # identity blocks: conv1's dx GEMM accumulates the residual gradient (DTF_RES_FOLD=0: autograd adds)
+    fold_residual_grad = os.environ.get("DTF_RES_FOLD", "1") != "0"
 
     def __init__(self, cin, width, stride=1, down=False):
         super().__init__()
@@ -36,9 +41,13 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         idt = self.down_bn(self.down_conv(x)) if self.down_conv is not None else x
-        y = self.bn1(self.conv1(x), relu=True)           # BN + ReLU: one fused pass
+        # identity path: bn3's residual gradient is accumulated by conv1's input-
+        # gradient GEMM (beta = 1) instead of autograd adding the two branches
+        slot = (GradSlot() if self.fold_residual_grad and self.down_conv is None and x.is_cuda and self.training
+                else None)
+        y = self.bn1(self.conv1(x, grad_slot=slot), relu=True)   # BN + ReLU: one fused pass
         y = self.bn2(self.conv2(y), relu=True)
-        return self.bn3(self.conv3(y), residual=idt, relu=True)   # BN + residual add + ReLU
+        return self.bn3(self.conv3(y), residual=idt, relu=True, residual_slot=slot)   # BN + residual add + ReLU
 
 
 class ResNet(nn.Module):

@@ -32,7 +32,7 @@ _ENABLED = os.environ.get("DTF_FUSED_BN", "1") != "0"
 
 class _FusedBN(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, res, running_mean, running_var, momentum, eps, relu, sink):
+    def forward(ctx, x, gamma, beta, res, running_mean, running_var, momentum, eps, relu, sink, res_slot=None):
         C = _C()
         ch = gamma.numel()
         M = x.numel() // ch
@@ -43,6 +43,7 @@ class _FusedBN(torch.autograd.Function):
         ctx.save_for_backward(x, res if res is not None else torch.empty(0, device=x.device), gamma, stats)
         ctx.has_res, ctx.relu = res is not None, relu
         ctx.sink = sink           # (weight, bias) whose .grad the finalize kernel accumulates into, or None
+        ctx.res_slot = res_slot   # GradSlot: the residual's gradient goes to the GEMM that consumes it
         return y
 
     @staticmethod
@@ -63,11 +64,15 @@ class _FusedBN(torch.autograd.Function):
         part = torch.empty(2 * C.bn_partial_rows(M, ch) * ch, dtype=torch.float32, device=x.device)
         C.bn_bwd(dy, x, res if ctx.has_res else None, gamma, stats, part, coef, dx, dres, dgamma, dbeta, ctx.relu,
                  ctx.sink is not None)
+        if dres is not None and ctx.res_slot is not None and not ctx.res_slot.consumed:
+            # folded into the residual source's other consumer: the 1x1 conv's dx GEMM
+            # accumulates it (beta = 1) instead of autograd adding the two branches
+            ctx.res_slot.g, dres = dres, None
         if ctx.sink is not None:
             grad_sink.done(ctx.sink[0])
             grad_sink.done(ctx.sink[1])
-            return dx, None, None, dres, None, None, None, None, None, None
-        return dx, dgamma, dbeta, dres, None, None, None, None, None, None
+            return dx, None, None, dres, None, None, None, None, None, None, None
+        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None
 
 
 class FusedBatchNorm2d(torch.nn.BatchNorm2d):
@@ -97,7 +102,11 @@ class FusedBatchNorm2d(torch.nn.BatchNorm2d):
         self._flush_batches()
         super()._save_to_state_dict(destination, prefix, keep_vars)
 
-    def forward(self, x, residual: Optional[torch.Tensor] = None, relu: bool = False):  # noqa: D401
+    def forward(self, x, residual: Optional[torch.Tensor] = None, relu: bool = False,
+                residual_slot=None):  # noqa: D401
+        """`residual_slot` (ops.transformer.GradSlot, fused path only): the
+        residual's gradient is handed to the slot's consumer instead of being
+        returned through autograd."""
         fused_ok = (_ENABLED and self.training and x.is_cuda and x.dtype == torch.bfloat16 and _nhwc(x)
                     and self.affine and x.shape[1] % 8 == 0 and self.momentum is not None
                     and (residual is None or (residual.dtype == torch.bfloat16 and _nhwc(residual))))
@@ -107,7 +116,7 @@ class FusedBatchNorm2d(torch.nn.BatchNorm2d):
             mom = self.momentum
             return _FusedBN.apply(x, self.weight, self.bias, residual, self.running_mean if self.track_running_stats
                                   else None, self.running_var if self.track_running_stats else None, float(mom),
-                                  float(self.eps), bool(relu), self._sink())
+                                  float(self.eps), bool(relu), self._sink(), residual_slot)
         self._flush_batches()
         y = super().forward(x)
         if residual is not None:

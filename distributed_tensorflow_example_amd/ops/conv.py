@@ -63,11 +63,19 @@ def _fwd_gemm(engine, x, w16):
     return y
 
 
-def _dx_gemm(engine, dy, w16, x_shape):
-    dx = _cl_empty(x_shape[0], x_shape[1], x_shape[2], x_shape[3], dy)
+def _dx_gemm(engine, dy, w16, x_shape, into=None):
+    """dx = dy W; with `into` (a channels_last bf16 gradient of x from another
+    branch) accumulated in place: dx = into + dy W, one GEMM with beta = 1."""
+    acc = into is not None and into.dtype == dy.dtype and into.is_contiguous(memory_format=torch.channels_last)
+    dx = into if acc else _cl_empty(x_shape[0], x_shape[1], x_shape[2], x_shape[3], dy)
     dy2, w2, dx2 = _rows(dy), w16.view(w16.shape[0], w16.shape[1]), _rows(dx)
-    if engine != "gemm_big" or not _C().gemm_big(dy2, False, w2, False, dx2):
-        torch.mm(dy2, w2, out=dx2)
+    if engine != "gemm_big" or not _C().gemm_big(dy2, False, w2, False, dx2, beta=1.0 if acc else 0.0):
+        if acc:
+            dx2.addmm_(dy2, w2)
+        else:
+            torch.mm(dy2, w2, out=dx2)
+    if into is not None and not acc:
+        dx = dx + into
     return dx
 
 
@@ -141,10 +149,11 @@ def choices() -> dict:
 
 class _ShadowConv(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, w16, stride, padding, dilation, groups):
+    def forward(ctx, x, w, w16, stride, padding, dilation, groups, slot=None):
         ctx.save_for_backward(x, w16)
         ctx.conf = (stride, padding, dilation, groups)
         ctx.w = w
+        ctx.slot = slot
         ctx.gemm = _gemm_ok(x, w16, stride, padding, dilation, groups)
         if ctx.gemm:
             eng = _fwd_engine(x, w16)
@@ -169,10 +178,13 @@ class _ShadowConv(torch.autograd.Function):
         if mx or mw:
             dx, dw, _ = torch.ops.aten.convolution_backward(dy, x, w16, None, stride, padding, dilation, False,
                                                             [0, 0], groups, [mx, mw, False])
+        extra = ctx.slot.take() if ctx.slot is not None else None   # a residual branch's gradient of x
         if need_x and not mx:
-            dx = _dx_gemm(dx_eng, dy, w16, x.shape)
+            dx = _dx_gemm(dx_eng, dy, w16, x.shape, into=extra)
+        elif need_x and extra is not None:
+            dx = dx + extra
         if not need_w:
-            return dx, None, None, None, None, None, None
+            return dx, None, None, None, None, None, None, None
         sink = grad_sink.enabled(w) and (w.grad is None or w.grad.is_contiguous())
         if not mw:
             from . import big_gemm
@@ -180,25 +192,31 @@ class _ShadowConv(torch.autograd.Function):
                 g = grad_sink.target(w)
                 big_gemm.linear_dw(_rows(dy), _rows(x), into=g.view(g.shape[0], g.shape[1]))
                 grad_sink.done(w)
-                return dx, None, None, None, None, None, None
-            return dx, big_gemm.linear_dw(_rows(dy), _rows(x)).view(w.shape).to(w.dtype), None, None, None, None, None
+                return dx, None, None, None, None, None, None, None
+            return (dx, big_gemm.linear_dw(_rows(dy), _rows(x)).view(w.shape).to(w.dtype), None, None, None, None,
+                    None, None)
         if sink:
             grad_sink.target(w).add_(dw)
             grad_sink.done(w)
-            return dx, None, None, None, None, None, None
-        return dx, dw.to(w.dtype), None, None, None, None, None
+            return dx, None, None, None, None, None, None, None
+        return dx, dw.to(w.dtype), None, None, None, None, None, None
 
 
 class ShadowConv2d(torch.nn.Conv2d):
     """nn.Conv2d that computes with `weight._shadow` when one is attached."""
 
-    def forward(self, x):
+    def forward(self, x, grad_slot=None):
+        """`grad_slot` (ops.transformer.GradSlot): another branch's gradient of x,
+        deposited by its producer during backward, is accumulated into this
+        conv's input gradient (the residual add of a bottleneck's identity path)."""
         w16 = getattr(self.weight, "_shadow", None)
         if (w16 is not None and x.is_cuda and self.bias is None and self.padding_mode == "zeros"
                 and isinstance(self.padding, tuple)):
             if x.dtype != w16.dtype:
                 x = x.to(w16.dtype)
-            return _ShadowConv.apply(x, self.weight, w16, self.stride, self.padding, self.dilation, self.groups)
+                grad_slot = None     # the cast node, not x, would receive this conv's gradient
+            return _ShadowConv.apply(x, self.weight, w16, self.stride, self.padding, self.dilation, self.groups,
+                                     grad_slot)
         return super().forward(x)
 
 

@@ -74,3 +74,34 @@ def test_conv1x1_engines_match_fp32(native, n, cin, cout, hw, engines):
     torch.testing.assert_close(y.float(), y_ref, rtol=2e-2, atol=2e-2 * y_ref.abs().max().item())
     torch.testing.assert_close(m.weight.grad, dw_ref, rtol=2e-3, atol=2e-3 * dw_ref.abs().max().item())
     torch.testing.assert_close(x.grad.float(), dx_ref, rtol=2e-2, atol=2e-2 * dx_ref.abs().max().item())
+
+
+@pytest.mark.parametrize("dx_engine", ["hipblaslt", "gemm_big", "miopen"])
+def test_bottleneck_residual_grad_fold(native, dx_engine):
+    """An identity bottleneck's residual gradient accumulated by conv1's dx GEMM
+    (beta = 1, models/resnet.py) equals autograd's two-branch sum."""
+    from distributed_tensorflow_example_amd.models.resnet import Bottleneck
+    from distributed_tensorflow_example_amd.ops import conv
+
+    torch.manual_seed(3)
+    blk = Bottleneck(256, 64).cuda().to(memory_format=torch.channels_last).train()
+    conv.attach_shadows(blk)
+    x0 = torch.randn(8, 256, 14, 14, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    g = torch.randn(8, 256, 14, 14, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    key = ("dx", tuple(x0.shape), 64)
+    conv._choice[key] = dx_engine
+    grads = []
+    try:
+        for fold in (True, False):
+            blk.fold_residual_grad = fold
+            blk.zero_grad(set_to_none=True)
+            x = x0.clone().requires_grad_(True)
+            blk(x).backward(g)
+            grads.append((x.grad.float(), blk.conv1.weight.grad.clone()))
+    finally:
+        conv._choice.pop(key, None)
+        blk.fold_residual_grad = True
+    (a, wa), (b, wb) = grads
+    # one bf16 rounding of (dy W + dres) vs two (dy W, then the add)
+    torch.testing.assert_close(a, b, rtol=1e-2, atol=1e-2 * b.abs().max().item())
+    torch.testing.assert_close(wa, wb)

@@ -37,6 +37,10 @@ hipError_t dtfk_gemm_big(const void* A, int lda, int transA, const void* B, int 
 long long dtfk_gemm_big_workspace(int M, int N, int K, int c_bf16, float beta, int act, int split_k, int variant);
 int dtfk_gemm_big_supported(const void* A, int lda, int transA, const void* B, int ldb, int transB, int c_bf16, int M,
                             int N, int K, float beta, int act, int split_k);
+hipError_t dtfk_gemm_dgelu(const void* A, int lda, int transA, const void* B, int ldb, int transB, void* C, int ldc,
+                           const void* aux, const float* bias, float* colpart, int M, int N, int K, hipStream_t stream);
+hipError_t dtfk_colsum_partials_multi(const float* const* parts, float* const* outs, int nbuf, int P, int H,
+                                      int accumulate, hipStream_t st);
 hipError_t dtfk_gemm_big_cfg(int cfg, const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N,
                              int K, hipStream_t stream);
 hipError_t dtfk_act_backward(const float* dy, const float* y, const float* z, float* dz, int64_t n, int act,
@@ -157,6 +161,38 @@ bool gemm_big(at::Tensor A, bool transA, at::Tensor B, bool transB, at::Tensor o
                    (int)out.stride(0), opt_ptr<float>(bias), M, N, K, (float)alpha, (float)beta, act, split_k, variant,
                    wsb > 0 ? ws.data_ptr() : nullptr, cs()),
      "gemm_big");   // any launch error is a real error
+  return true;
+}
+
+// Input gradient of a linear layer fed by bias + GELU, with the GELU backward
+// in the GEMM epilogue (gemm_big.hip dtfk_gemm_dgelu): out = (op(A) op(B)) *
+// gelu'(aux + bias) in bf16, and dbias (fp32) = (or +=, accumulate) the column
+// sums, via the kernel's [M/128, N] partials in `colpart`.  False (nothing
+// launched) outside the kernel's contract.
+bool gemm_dgelu(at::Tensor A, bool transA, at::Tensor B, bool transB, at::Tensor out, at::Tensor aux,
+                at::Tensor bias, at::Tensor colpart, at::Tensor dbias, bool accumulate) {
+  gpu(A, "A"); gpu(B, "B"); gpu(out, "out"); gpu(aux, "aux");
+  f32c(bias, "bias"); f32c(colpart, "colpart"); f32c(dbias, "dbias");
+  if (A.dim() != 2 || B.dim() != 2 || out.dim() != 2 || aux.dim() != 2) throw std::runtime_error("gemm_dgelu: 2-D");
+  for (const at::Tensor* t : {&A, &B, &out, &aux})
+    if (t->scalar_type() != at::kBFloat16 || t->stride(1) != 1) throw std::runtime_error("gemm_dgelu: bf16, unit inner stride");
+  const int M = (int)(transA ? A.size(1) : A.size(0));
+  const int K = (int)(transA ? A.size(0) : A.size(1));
+  const int N = (int)(transB ? B.size(0) : B.size(1));
+  if ((transB ? B.size(1) : B.size(0)) != K) throw std::runtime_error("gemm_dgelu inner dimensions differ");
+  if (out.size(0) != M || out.size(1) != N || aux.size(0) != M || aux.size(1) != N || aux.stride(0) != out.stride(0))
+    throw std::runtime_error("gemm_dgelu: out / aux shape or leading dimension");
+  if (bias.numel() != N || dbias.numel() != N || !dbias.is_contiguous()) throw std::runtime_error("gemm_dgelu: bias size");
+  if (M % 256 || N % 256 || K % 128) return false;
+  if (colpart.numel() < (int64_t)(M / 128) * N) throw std::runtime_error("gemm_dgelu: colpart needs M/128 * N floats");
+  const hipError_t e = dtfk_gemm_dgelu(A.data_ptr(), (int)A.stride(0), transA, B.data_ptr(), (int)B.stride(0), transB,
+                                       out.data_ptr(), (int)out.stride(0), aux.data_ptr(), bias.data_ptr<float>(),
+                                       colpart.data_ptr<float>(), M, N, K, cs());
+  if (e == hipErrorInvalidValue) { (void)hipGetLastError(); return false; }   // alignment contract
+  ck(e, "gemm_dgelu");
+  const float* pp[1] = {colpart.data_ptr<float>()};
+  float* po[1] = {dbias.data_ptr<float>()};
+  ck(dtfk_colsum_partials_multi(pp, po, 1, M / 128, N, accumulate ? 1 : 0, cs()), "gemm_dgelu colsum");
   return true;
 }
 
@@ -491,6 +527,8 @@ void init_ops(py::module& m) {
         py::arg("bias") = py::none(), py::arg("act") = 0, py::arg("alpha") = 1.0, py::arg("beta") = 0.0,
         py::arg("split_k") = 0, py::arg("variant") = 0);
   m.def("gemm_big_cfg", &gemm_big_cfg);
+  m.def("gemm_dgelu", &gemm_dgelu, py::arg("A"), py::arg("transA"), py::arg("B"), py::arg("transB"), py::arg("out"),
+        py::arg("aux"), py::arg("bias"), py::arg("colpart"), py::arg("dbias"), py::arg("accumulate") = false);
   m.def("act_backward", &act_backward);
   m.def("col_sum", &col_sum);
   m.def("softmax_xent", &softmax_xent);

@@ -182,6 +182,19 @@ __device__ __forceinline__ f32x4 ld_sys_f32x4(const void* p) {
                __uint_as_float((uint32_t)(b >> 32))};
 }
 
+// GELU (erf form) cdf and pdf with the A&S 7.1.26 erfc polynomial: libm erff
+// made the [tokens, 3072] GELU passes VALU-bound (shared by transformer.hip's
+// elementwise kernels and gemm_big.hip's fused GELU-backward epilogue).
+__device__ __forceinline__ void gelu_cdf_pdf(float z, float& cdf, float& pdf) {
+  const float x = fabsf(z) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, x, 1.f));
+  const float poly = t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f),
+                                      -0.284496736f), 0.254829592f);
+  const float e = __expf(-0.5f * z * z);
+  const float tail = 0.5f * poly * e;           // 0.5 * (1 - erf(|z| / sqrt2))
+  cdf = z >= 0.f ? 1.f - tail : tail;
+  pdf = 0.3989422804014327f * e;
+}
 }  // namespace dtfk
 
 #define DTFK_CHECK_LAUNCH() (hipGetLastError())

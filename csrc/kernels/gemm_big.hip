@@ -66,6 +66,11 @@ __device__ __attribute__((noinline)) float apply_act_slow(float z, int act) {
     default: return z;
   }
 }
+__device__ __forceinline__ float gelu_grad_f(float z) {
+  float cdf, pdf;
+  gelu_cdf_pdf(z, cdf, pdf);
+  return fmaf(z, pdf, cdf);
+}
 __device__ __forceinline__ float apply_act(float z, int act) { return act == ACT_NONE ? z : apply_act_slow(z, act); }
 
 // ---- LDS images ----------------------------------------------------------
@@ -437,11 +442,19 @@ __device__ __forceinline__ void raw_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <bool AKC, bool BKC, bool OBF, bool SW, int BNT = 256>
+// DG (GELU backward, interior tiles of a bf16 256-wide product only -- host
+// contract in dtfk_gemm_dgelu): C = (A' B') * gelu'(aux + bias), aux the saved
+// pre-activation (bf16, ld = ldc), and the per-column sums of that fp32 product
+// over each wave row's 128 rows to colpart[M / 128][N] (the bias gradient's
+// partials, reduced by colsum_partials).
+template <bool AKC, bool BKC, bool OBF, bool SW, int BNT = 256, bool DG = false>
 __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A, int lda,
                                                  const uint16_t* __restrict__ B, int ldb, void* __restrict__ C,
                                                  int ldc, const float* __restrict__ bias, int M, int N, int K,
-                                                 float alpha, float beta, int act, int kchunk, long long slab = 0) {
+                                                 float alpha, float beta, int act, int kchunk, long long slab = 0,
+                                                 const uint16_t* __restrict__ aux = nullptr,
+                                                 float* __restrict__ colpart = nullptr) {
+  static_assert(!DG || (OBF && SW && BNT == 256), "GELU-backward epilogue: bf16 out, 256-wide tiles");
   // BNT = 256, or 192 (waves 128 x 48: quadrant column 1 is one 16-wide n tile,
   // its half-tile 64 rows / one DMA per thread) for N where 256 leaves CUs idle
   static_assert(BNT == 256 || BNT == 192, "tile width");
@@ -616,11 +629,16 @@ __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A,
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) bv[j][r] = bias != nullptr ? bias[ncol + j * 16 + r] : 0.f;
+      for (int r = 0; r < 4; ++r) bv[j][r] = (bias != nullptr && !DG) ? bias[ncol + j * 16 + r] : 0.f;
     // read-back: row rsub (+8 it), columns c8 .. c8+7; WN / 8 lanes per row (48-wide: lanes >= 48 idle)
     constexpr int LPR = WN / 8;
     const int rsub = lane / LPR, c8 = (lane % LPR) * 8;
     const bool rb_on = lane < 8 * LPR;
+    float ab[8], cs[8];   // DG: the pre-activation's bias for this lane's 8 columns; their column sums
+    if constexpr (DG) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) { ab[q] = bias[n0 + wc * WN + c8 + q]; cs[q] = 0.f; }
+    }
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
       // beta != 0: this half's C chunks are loaded first, all at once (the
@@ -628,11 +646,13 @@ __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A,
       // hides under the LDS round trip instead of one load per store
       typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
       u32x4 cpre[OBF ? 8 : 16];
-      if (beta != 0.f && rb_on) {
+      if (DG || (beta != 0.f && rb_on)) {
 #pragma unroll
         for (int it = 0; it < 8; ++it) {
           const size_t o = (size_t)(m0 + wr * 128 + half * 64 + it * 8 + rsub) * ldc + n0 + wc * WN + c8;
-          if constexpr (OBF) {
+          if constexpr (DG) {   // the saved pre-activation instead of C (beta is 0)
+            cpre[it] = *reinterpret_cast<const u32x4*>(aux + o);
+          } else if constexpr (OBF) {
             cpre[it] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const uint16_t*>(C) + o);
           } else {
             cpre[2 * it] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const float*>(C) + o);
@@ -658,7 +678,15 @@ __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A,
         const f32x4 hi = *reinterpret_cast<const f32x4*>(ep + lrow * EPI_ROW + c8 * 4 + 16);
         float z[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         const size_t o = (size_t)(m0 + wr * 128 + half * 64 + lrow) * ldc + n0 + wc * WN + c8;
-        if (beta != 0.f) {
+        if constexpr (DG) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            z[2 * q] *= gelu_grad_f(bf2f((uint16_t)(cpre[it][q] & 0xffff)) + ab[2 * q]);
+            z[2 * q + 1] *= gelu_grad_f(bf2f((uint16_t)(cpre[it][q] >> 16)) + ab[2 * q + 1]);
+          }
+#pragma unroll
+          for (int q = 0; q < 8; ++q) cs[q] += z[q];
+        } else if (beta != 0.f) {
           if constexpr (OBF) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -684,6 +712,21 @@ __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A,
           *reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + o) = make_float4(z[0], z[1], z[2], z[3]);
           *reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + o + 4) = make_float4(z[4], z[5], z[6], z[7]);
         }
+      }
+    }
+    if constexpr (DG) {
+      // lanes of one column group (lane % 8) hold 8 rows each of the 16 x 8 it/half rows: butterfly over the
+      // row index, then the rsub == 0 lanes store the wave row's 128-row column sums
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        cs[q] += __shfl_xor(cs[q], 8);
+        cs[q] += __shfl_xor(cs[q], 16);
+        cs[q] += __shfl_xor(cs[q], 32);
+      }
+      if (rsub == 0) {
+        float* p = colpart + (size_t)((m0 >> 7) + wr) * N + n0 + wc * WN + c8;
+        *reinterpret_cast<float4*>(p) = make_float4(cs[0], cs[1], cs[2], cs[3]);
+        *reinterpret_cast<float4*>(p + 4) = make_float4(cs[4], cs[5], cs[6], cs[7]);
       }
     }
     return;
@@ -956,6 +999,37 @@ extern "C" hipError_t dtfk_gemm_big(const void* A, int lda, int transA, const vo
 #undef DTFK_GB_B
 #undef DTFK_GB_O
 #undef DTFK_GB
+  return hipGetLastError();
+}
+
+// dU[M,N] = (A' B') * gelu'(aux + bias) in bf16 and colpart[M/128][N] = its
+// fp32 column sums per 128 rows: the input gradient of a linear layer fed by
+// bias + GELU (BERT's FFN-down dX) with the GELU backward and the bias
+// gradient's first reduction in the epilogue.  Contract (else
+// hipErrorInvalidValue, nothing launched): M % 256 == 0, N % 256 == 0,
+// K % 128 == 0, 16-byte aligned bases / leading dims, aux with ld = ldc.
+extern "C" hipError_t dtfk_gemm_dgelu(const void* A, int lda, int transA, const void* B, int ldb, int transB,
+                                      void* C, int ldc, const void* aux, const float* bias, float* colpart, int M,
+                                      int N, int K, hipStream_t stream) {
+  using namespace dtfk::gemm2;
+  if (M % 256 || N % 256 || K % 128 || ldc % 8 || (reinterpret_cast<uintptr_t>(C) & 15) ||
+      (reinterpret_cast<uintptr_t>(aux) & 15) || (reinterpret_cast<uintptr_t>(colpart) & 15) || bias == nullptr ||
+      !dtfk_gemm_big_supported(A, lda, transA, B, ldb, transB, 1, M, N, K, 0.f, 0, 1))
+    return hipErrorInvalidValue;
+  const dim3 grid((unsigned)((M / 256) * (N / BN)), 1), block(NTHR);
+  const uint16_t* a = static_cast<const uint16_t*>(A);
+  const uint16_t* b = static_cast<const uint16_t*>(B);
+  const uint16_t* x = static_cast<const uint16_t*>(aux);
+#define DTFK_DG(AK, BKk)                                                                                          \
+  hipLaunchKernelGGL((gemm_8ph<AK, BKk, true, true, 256, true>), grid, block, 0, stream, a, lda, b, ldb, C, ldc, \
+                     bias, M, N, K, 1.f, 0.f, 0, K, 0LL, x, colpart)
+  const bool akc = !transA, bkc = transB != 0;
+  if (akc) {
+    if (bkc) DTFK_DG(true, true); else DTFK_DG(true, false);
+  } else {
+    if (bkc) DTFK_DG(false, true); else DTFK_DG(false, false);
+  }
+#undef DTFK_DG
   return hipGetLastError();
 }
 

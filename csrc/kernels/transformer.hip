@@ -232,16 +232,6 @@ __global__ __launch_bounds__(256) void ln_fwd_f32in(
 // exp(-z^2/2), which is also the normal pdf's, so gelu' costs one more FMA.
 // The bf16 [tokens, 3072] GELU tensors are large enough that libm erff made
 // these elementwise kernels VALU-bound rather than HBM-bound.
-__device__ __forceinline__ void gelu_cdf_pdf(float z, float& cdf, float& pdf) {
-  const float x = fabsf(z) * 0.70710678118654752f;
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, x, 1.f));
-  const float poly = t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f),
-                                      -0.284496736f), 0.254829592f);
-  const float e = __expf(-0.5f * z * z);
-  const float tail = 0.5f * poly * e;           // 0.5 * (1 - erf(|z| / sqrt2))
-  cdf = z >= 0.f ? 1.f - tail : tail;
-  pdf = 0.3989422804014327f * e;
-}
 __device__ __forceinline__ float gelu_f(float z) {
   float cdf, pdf;
   gelu_cdf_pdf(z, cdf, pdf);

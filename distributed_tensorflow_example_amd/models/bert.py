@@ -95,6 +95,66 @@ class _ShadowLinear(torch.autograd.Function):
         return gx, _wgrad(gy2, x2), None, None
 
 
+class _GeluShadowLinear(torch.autograd.Function):
+    """y = gelu(u + b) @ w16^T: BERT's FFN-down projection fused with the bias +
+    GELU that feeds it.  Backward computes dU = (gy W) * gelu'(u + b) as ONE
+    gemm_big launch with the GELU backward and the bias gradient's partial
+    column sums in its epilogue (gemm_big.hip gemm_8ph<DG>, ops.big_gemm
+    use_dgelu) -- the dH tensor is never written or re-read -- or, where the
+    per-shape timing says otherwise, the dX GEMM + the bias_gelu_bwd pass."""
+
+    @staticmethod
+    def forward(ctx, u, b, w, w16):
+        u = u.contiguous()
+        h = torch.empty_like(u)
+        T._C().bias_gelu_fwd(u, b, h)
+        ctx.save_for_backward(u, h, w16, b)
+        ctx.w, ctx.b = w, b
+        h2 = h.reshape(-1, h.shape[-1])
+        if big_gemm.use_native("fwd", h2.shape[0], w16.shape[0], h2.shape[1], h.device):
+            return big_gemm.linear_fwd(h2, w16).view(*h.shape[:-1], w16.shape[0])
+        return F.linear(h, w16)
+
+    @staticmethod
+    def backward(ctx, gy):
+        u, h, w16, b = ctx.saved_tensors
+        gy2 = gy.to(w16.dtype).reshape(-1, gy.shape[-1])
+        u2, h2 = u.reshape(-1, u.shape[-1]), h.reshape(-1, h.shape[-1])
+        M, N, K = u2.shape[0], u2.shape[1], gy2.shape[1]
+        w = ctx.w
+        if grad_sink.enabled(w) and (w.grad is None or w.grad.is_contiguous()):
+            _wgrad(gy2, h2, into=grad_sink.target(w))
+            grad_sink.done(w)
+            gw = None
+        else:
+            gw = _wgrad(gy2, h2)
+        C = T._C()
+        pb = ctx.b
+        sink = grad_sink.all_enabled(pb)
+        db = grad_sink.target(pb) if sink else torch.empty(N, dtype=torch.float32, device=u.device)
+        du = torch.empty_like(u2)
+        fused = False
+        if big_gemm.use_dgelu(M, N, K, u.device):
+            colpart = torch.empty((M // 128) * N, dtype=torch.float32, device=u.device)
+            fused = C.gemm_dgelu(gy2, False, w16, False, du, u2, b, colpart, db, accumulate=sink)
+        if not fused:
+            dh = big_gemm.linear_dx(gy2, w16) if big_gemm.use_native("dx", M, N, K, u.device) else gy2 @ w16
+            part = torch.empty(big_gemm.gelu_bwd_slices(M) * N, dtype=torch.float32, device=u.device)
+            C.bias_gelu_bwd(dh, u2, b, du, part, db, accumulate=sink)
+        if sink:
+            grad_sink.done(pb)
+            db = None
+        return du.view(u.shape), db, gw, None
+
+
+def _gelu_mm(u, b, w):
+    """gelu(u + b) @ w^T, fused with its backward on the bf16-shadow path."""
+    w16 = getattr(w, "_shadow", None)
+    if w16 is not None and u.is_cuda and u.dtype == w16.dtype:
+        return _GeluShadowLinear.apply(u, b, w, w16)
+    return _mm(T.bias_gelu(u, b), w)
+
+
 def _wgrad_split(T: int, out: int, inp: int) -> int:
     """Token-slab count for the weight-gradient GEMM.  dW = gy^T x has a long
     reduction (T = B*S tokens) and few output tiles (36-144 of 128x128 for
@@ -199,8 +259,8 @@ class BertLayer(torch.nn.Module):
         a = T.bias_dropout_residual_layernorm(_mm(ctx, self.w_o), self.b_o, x, self.ln1_g, self.ln1_b,
                                               c.dropout, c.ln_eps, self.training, residual_slot=slot_x)
         slot_a = _slot_for(a, self.w_1)        # LN2's residual grad of a -> W1 GEMM's dX
-        hmid = T.bias_gelu(_mm(a, self.w_1, slot_a), self.b_1)
-        out = T.bias_dropout_residual_layernorm(_mm(hmid, self.w_2), self.b_2, a, self.ln2_g, self.ln2_b,
+        pre = _gelu_mm(_mm(a, self.w_1, slot_a), self.b_1, self.w_2)
+        out = T.bias_dropout_residual_layernorm(pre, self.b_2, a, self.ln2_g, self.ln2_b,
                                                 c.dropout, c.ln_eps, self.training, residual_slot=slot_a)
         return out
 

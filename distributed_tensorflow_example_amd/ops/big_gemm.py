@@ -25,6 +25,7 @@ from .. import _native
 # weight gradients (profiles/gemm_8ph_r3.txt); end to end 'auto' measured equal
 # to 'never' and 'always' 3 % slower;  never: hipBLASLt;  always: this kernel
 _POLICY = os.environ.get("DTF_BIG_GEMM", "auto")
+_DGELU = os.environ.get("DTF_GEMM_DGELU", "1") != "0"   # fused GELU-backward epilogue (use_dgelu)
 _choice: dict = {}
 _timings: dict = {}
 
@@ -90,6 +91,49 @@ def use_native(role: str, M: int, N: int, K: int, dev) -> bool:
             return False
         ours, theirs = _candidates(role, M, N, K, dev)
         t_ours, t_theirs = _time(ours), _time(theirs)
+        hit = _choice[key] = t_ours <= t_theirs
+        _timings[key] = (round(t_ours, 4), round(t_theirs, 4))
+    return hit
+
+
+def gelu_bwd_slices(M: int) -> int:
+    """Row slices of the standalone bias + GELU backward (ops.transformer)."""
+    return max(1, min(512, M // 32))
+
+
+def use_dgelu(M: int, N: int, K: int, dev) -> bool:
+    """True when the input gradient of a linear layer fed by bias + GELU should
+    run as ONE gemm_big launch with the GELU backward and the bias-gradient
+    partials in its epilogue (gemm_dgelu) instead of the dX GEMM (whichever
+    engine use_native picks) + the bias_gelu_bwd pass; timed once per shape
+    under 'auto'."""
+    if (_POLICY == "never" or not _DGELU or M % 256 or N % 256 or K % 128
+            or torch.device(dev).type != "cuda"):
+        return False
+    if _POLICY == "always":
+        return True
+    key = ("dgelu", M, N, K)
+    hit = _choice.get(key)
+    if hit is None:
+        if torch.cuda.is_current_stream_capturing():
+            return False
+        C = _C()
+        bf = torch.bfloat16
+        a, b = torch.randn(M, K, device=dev, dtype=bf), torch.randn(K, N, device=dev, dtype=bf)
+        aux, out = torch.randn(M, N, device=dev, dtype=bf), torch.empty(M, N, device=dev, dtype=bf)
+        bias, db = torch.randn(N, device=dev), torch.empty(N, device=dev)
+        colpart = torch.empty((M // 128) * N, device=dev)
+        part = torch.empty(gelu_bwd_slices(M) * N, device=dev)
+        if not C.gemm_dgelu(a, False, b, False, out, aux, bias, colpart, db):
+            _choice[key] = False
+            return False
+        native_dx = use_native("dx", M, N, K, dev)
+
+        def theirs():
+            dh = linear_dx(a, b) if native_dx else torch.mm(a, b)
+            C.bias_gelu_bwd(dh, aux, bias, out, part, db, accumulate=False)
+        t_ours = _time(lambda: C.gemm_dgelu(a, False, b, False, out, aux, bias, colpart, db))
+        t_theirs = _time(theirs)
         hit = _choice[key] = t_ours <= t_theirs
         _timings[key] = (round(t_ours, 4), round(t_theirs, 4))
     return hit

@@ -39,6 +39,8 @@ int dtfk_gemm_big_supported(const void* A, int lda, int transA, const void* B, i
                             int N, int K, float beta, int act, int split_k);
 hipError_t dtfk_gemm_dgelu(const void* A, int lda, int transA, const void* B, int ldb, int transB, void* C, int ldc,
                            const void* aux, const float* bias, float* colpart, int M, int N, int K, hipStream_t stream);
+hipError_t dtfk_gemm_gelu_aux(const void* A, int lda, int transA, const void* B, int ldb, int transB, void* C,
+                              int ldc, void* aux, const float* bias, int M, int N, int K, hipStream_t stream);
 hipError_t dtfk_colsum_partials_multi(const float* const* parts, float* const* outs, int nbuf, int P, int H,
                                       int accumulate, hipStream_t st);
 hipError_t dtfk_gemm_big_cfg(int cfg, const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N,
@@ -170,9 +172,10 @@ bool gemm_big(at::Tensor A, bool transA, at::Tensor B, bool transB, at::Tensor o
 // sums, via the kernel's [M/128, N] partials in `colpart`.  False (nothing
 // launched) outside the kernel's contract.
 bool gemm_dgelu(at::Tensor A, bool transA, at::Tensor B, bool transB, at::Tensor out, at::Tensor aux,
-                at::Tensor bias, at::Tensor colpart, at::Tensor dbias, bool accumulate) {
+                c10::optional<at::Tensor> bias, at::Tensor colpart, at::Tensor dbias, bool accumulate) {
   gpu(A, "A"); gpu(B, "B"); gpu(out, "out"); gpu(aux, "aux");
-  f32c(bias, "bias"); f32c(colpart, "colpart"); f32c(dbias, "dbias");
+  if (bias.has_value()) f32c(*bias, "bias");
+  f32c(colpart, "colpart"); f32c(dbias, "dbias");
   if (A.dim() != 2 || B.dim() != 2 || out.dim() != 2 || aux.dim() != 2) throw std::runtime_error("gemm_dgelu: 2-D");
   for (const at::Tensor* t : {&A, &B, &out, &aux})
     if (t->scalar_type() != at::kBFloat16 || t->stride(1) != 1) throw std::runtime_error("gemm_dgelu: bf16, unit inner stride");
@@ -182,17 +185,44 @@ bool gemm_dgelu(at::Tensor A, bool transA, at::Tensor B, bool transB, at::Tensor
   if ((transB ? B.size(1) : B.size(0)) != K) throw std::runtime_error("gemm_dgelu inner dimensions differ");
   if (out.size(0) != M || out.size(1) != N || aux.size(0) != M || aux.size(1) != N || aux.stride(0) != out.stride(0))
     throw std::runtime_error("gemm_dgelu: out / aux shape or leading dimension");
-  if (bias.numel() != N || dbias.numel() != N || !dbias.is_contiguous()) throw std::runtime_error("gemm_dgelu: bias size");
+  if ((bias.has_value() && bias->numel() != N) || dbias.numel() != N || !dbias.is_contiguous())
+    throw std::runtime_error("gemm_dgelu: bias size");
   if (M % 256 || N % 256 || K % 128) return false;
   if (colpart.numel() < (int64_t)(M / 128) * N) throw std::runtime_error("gemm_dgelu: colpart needs M/128 * N floats");
   const hipError_t e = dtfk_gemm_dgelu(A.data_ptr(), (int)A.stride(0), transA, B.data_ptr(), (int)B.stride(0), transB,
-                                       out.data_ptr(), (int)out.stride(0), aux.data_ptr(), bias.data_ptr<float>(),
+                                       out.data_ptr(), (int)out.stride(0), aux.data_ptr(), opt_ptr<float>(bias),
                                        colpart.data_ptr<float>(), M, N, K, cs());
   if (e == hipErrorInvalidValue) { (void)hipGetLastError(); return false; }   // alignment contract
   ck(e, "gemm_dgelu");
   const float* pp[1] = {colpart.data_ptr<float>()};
   float* po[1] = {dbias.data_ptr<float>()};
   ck(dtfk_colsum_partials_multi(pp, po, 1, M / 128, N, accumulate ? 1 : 0, cs()), "gemm_dgelu colsum");
+  return true;
+}
+
+// Forward of a linear layer followed by bias + GELU (gemm_big.hip
+// dtfk_gemm_gelu_aux): aux = op(A) op(B) + bias (the pre-activation, bf16) and
+// out = gelu(aux) (bf16) from one epilogue.  False outside the contract.
+bool gemm_gelu_aux(at::Tensor A, bool transA, at::Tensor B, bool transB, at::Tensor out, at::Tensor aux,
+                   at::Tensor bias) {
+  gpu(A, "A"); gpu(B, "B"); gpu(out, "out"); gpu(aux, "aux"); f32c(bias, "bias");
+  if (A.dim() != 2 || B.dim() != 2 || out.dim() != 2 || aux.dim() != 2) throw std::runtime_error("gemm_gelu_aux: 2-D");
+  for (const at::Tensor* t : {&A, &B, &out, &aux})
+    if (t->scalar_type() != at::kBFloat16 || t->stride(1) != 1)
+      throw std::runtime_error("gemm_gelu_aux: bf16, unit inner stride");
+  const int M = (int)(transA ? A.size(1) : A.size(0));
+  const int K = (int)(transA ? A.size(0) : A.size(1));
+  const int N = (int)(transB ? B.size(0) : B.size(1));
+  if ((transB ? B.size(1) : B.size(0)) != K) throw std::runtime_error("gemm_gelu_aux inner dimensions differ");
+  if (out.size(0) != M || out.size(1) != N || aux.size(0) != M || aux.size(1) != N || aux.stride(0) != out.stride(0))
+    throw std::runtime_error("gemm_gelu_aux: out / aux shape or leading dimension");
+  if (bias.numel() != N) throw std::runtime_error("gemm_gelu_aux: bias size");
+  if (M % 256 || N % 256 || K % 128) return false;
+  const hipError_t e = dtfk_gemm_gelu_aux(A.data_ptr(), (int)A.stride(0), transA, B.data_ptr(), (int)B.stride(0),
+                                          transB, out.data_ptr(), (int)out.stride(0), aux.data_ptr(),
+                                          bias.data_ptr<float>(), M, N, K, cs());
+  if (e == hipErrorInvalidValue) { (void)hipGetLastError(); return false; }
+  ck(e, "gemm_gelu_aux");
   return true;
 }
 
@@ -529,6 +559,8 @@ void init_ops(py::module& m) {
   m.def("gemm_big_cfg", &gemm_big_cfg);
   m.def("gemm_dgelu", &gemm_dgelu, py::arg("A"), py::arg("transA"), py::arg("B"), py::arg("transB"), py::arg("out"),
         py::arg("aux"), py::arg("bias"), py::arg("colpart"), py::arg("dbias"), py::arg("accumulate") = false);
+  m.def("gemm_gelu_aux", &gemm_gelu_aux, py::arg("A"), py::arg("transA"), py::arg("B"), py::arg("transB"),
+        py::arg("out"), py::arg("aux"), py::arg("bias"));
   m.def("act_backward", &act_backward);
   m.def("col_sum", &col_sum);
   m.def("softmax_xent", &softmax_xent);

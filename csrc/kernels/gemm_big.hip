@@ -66,6 +66,11 @@ __device__ __attribute__((noinline)) float apply_act_slow(float z, int act) {
     default: return z;
   }
 }
+__device__ __forceinline__ float gelu_fwd_f(float z) {
+  float cdf, pdf;
+  gelu_cdf_pdf(z, cdf, pdf);
+  return z * cdf;
+}
 __device__ __forceinline__ float gelu_grad_f(float z) {
   float cdf, pdf;
   gelu_cdf_pdf(z, cdf, pdf);
@@ -442,19 +447,25 @@ __device__ __forceinline__ void raw_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// DG (GELU backward, interior tiles of a bf16 256-wide product only -- host
-// contract in dtfk_gemm_dgelu): C = (A' B') * gelu'(aux + bias), aux the saved
-// pre-activation (bf16, ld = ldc), and the per-column sums of that fp32 product
-// over each wave row's 128 rows to colpart[M / 128][N] (the bias gradient's
-// partials, reduced by colsum_partials).
-template <bool AKC, bool BKC, bool OBF, bool SW, int BNT = 256, bool DG = false>
+// Fused GELU epilogues (interior tiles of a bf16 256-wide product only -- host
+// contracts in dtfk_gemm_dgelu / dtfk_gemm_gelu_aux), EP:
+//   EP_DGELU     C = (A' B') * gelu'(aux + bias), aux the saved pre-activation
+//                (bf16, ld = ldc; bias may be null), and the per-column sums of
+//                that fp32 product over each wave row's 128 rows to
+//                colpart[M / 128][N] (the bias gradient's partials, reduced by
+//                colsum_partials);
+//   EP_GELU_AUX  aux = A' B' + bias (the pre-activation the backward needs) and
+//                C = gelu(A' B' + bias), both bf16 with ld = ldc.
+enum Epi { EP_PLAIN = 0, EP_DGELU = 1, EP_GELU_AUX = 2 };
+template <bool AKC, bool BKC, bool OBF, bool SW, int BNT = 256, int EP = EP_PLAIN>
 __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A, int lda,
                                                  const uint16_t* __restrict__ B, int ldb, void* __restrict__ C,
                                                  int ldc, const float* __restrict__ bias, int M, int N, int K,
                                                  float alpha, float beta, int act, int kchunk, long long slab = 0,
-                                                 const uint16_t* __restrict__ aux = nullptr,
+                                                 uint16_t* __restrict__ aux = nullptr,
                                                  float* __restrict__ colpart = nullptr) {
-  static_assert(!DG || (OBF && SW && BNT == 256), "GELU-backward epilogue: bf16 out, 256-wide tiles");
+  constexpr bool DG = EP == EP_DGELU, GA = EP == EP_GELU_AUX;
+  static_assert(EP == EP_PLAIN || (OBF && SW && BNT == 256), "GELU epilogues: bf16 out, 256-wide tiles");
   // BNT = 256, or 192 (waves 128 x 48: quadrant column 1 is one 16-wide n tile,
   // its half-tile 64 rows / one DMA per thread) for N where 256 leaves CUs idle
   static_assert(BNT == 256 || BNT == 192, "tile width");
@@ -637,7 +648,7 @@ __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A,
     float ab[8], cs[8];   // DG: the pre-activation's bias for this lane's 8 columns; their column sums
     if constexpr (DG) {
 #pragma unroll
-      for (int q = 0; q < 8; ++q) { ab[q] = bias[n0 + wc * WN + c8 + q]; cs[q] = 0.f; }
+      for (int q = 0; q < 8; ++q) { ab[q] = bias != nullptr ? bias[n0 + wc * WN + c8 + q] : 0.f; cs[q] = 0.f; }
     }
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
@@ -700,6 +711,12 @@ __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A,
               z[4 + q] += beta * __uint_as_float(cpre[2 * it + 1][q]);
             }
           }
+        }
+        if constexpr (GA) {
+          *reinterpret_cast<uint4*>(aux + o) =
+              make_uint4(pack2bf(z[0], z[1]), pack2bf(z[2], z[3]), pack2bf(z[4], z[5]), pack2bf(z[6], z[7]));
+#pragma unroll
+          for (int q = 0; q < 8; ++q) z[q] = gelu_fwd_f(z[q]);
         }
         if (act != ACT_NONE) {
 #pragma unroll
@@ -1013,16 +1030,16 @@ extern "C" hipError_t dtfk_gemm_dgelu(const void* A, int lda, int transA, const 
                                       int N, int K, hipStream_t stream) {
   using namespace dtfk::gemm2;
   if (M % 256 || N % 256 || K % 128 || ldc % 8 || (reinterpret_cast<uintptr_t>(C) & 15) ||
-      (reinterpret_cast<uintptr_t>(aux) & 15) || (reinterpret_cast<uintptr_t>(colpart) & 15) || bias == nullptr ||
+      (reinterpret_cast<uintptr_t>(aux) & 15) || (reinterpret_cast<uintptr_t>(colpart) & 15) ||
       !dtfk_gemm_big_supported(A, lda, transA, B, ldb, transB, 1, M, N, K, 0.f, 0, 1))
     return hipErrorInvalidValue;
   const dim3 grid((unsigned)((M / 256) * (N / BN)), 1), block(NTHR);
   const uint16_t* a = static_cast<const uint16_t*>(A);
   const uint16_t* b = static_cast<const uint16_t*>(B);
-  const uint16_t* x = static_cast<const uint16_t*>(aux);
+  uint16_t* x = const_cast<uint16_t*>(static_cast<const uint16_t*>(aux));   // read only (EP_DGELU)
 #define DTFK_DG(AK, BKk)                                                                                          \
-  hipLaunchKernelGGL((gemm_8ph<AK, BKk, true, true, 256, true>), grid, block, 0, stream, a, lda, b, ldb, C, ldc, \
-                     bias, M, N, K, 1.f, 0.f, 0, K, 0LL, x, colpart)
+  hipLaunchKernelGGL((gemm_8ph<AK, BKk, true, true, 256, EP_DGELU>), grid, block, 0, stream, a, lda, b, ldb, C,  \
+                     ldc, bias, M, N, K, 1.f, 0.f, 0, K, 0LL, x, colpart)
   const bool akc = !transA, bkc = transB != 0;
   if (akc) {
     if (bkc) DTFK_DG(true, true); else DTFK_DG(true, false);
@@ -1030,6 +1047,35 @@ extern "C" hipError_t dtfk_gemm_dgelu(const void* A, int lda, int transA, const 
     if (bkc) DTFK_DG(false, true); else DTFK_DG(false, false);
   }
 #undef DTFK_DG
+  return hipGetLastError();
+}
+
+// aux = A' B' + bias and C = gelu(aux), bf16 [M,N] with ld = ldc: the forward of
+// a linear layer followed by bias + GELU (BERT's FFN-up) writing the saved
+// pre-activation and the activation in one epilogue.  Contract as
+// dtfk_gemm_dgelu (else hipErrorInvalidValue, nothing launched).
+extern "C" hipError_t dtfk_gemm_gelu_aux(const void* A, int lda, int transA, const void* B, int ldb, int transB,
+                                         void* C, int ldc, void* aux, const float* bias, int M, int N, int K,
+                                         hipStream_t stream) {
+  using namespace dtfk::gemm2;
+  if (M % 256 || N % 256 || K % 128 || ldc % 8 || (reinterpret_cast<uintptr_t>(C) & 15) ||
+      (reinterpret_cast<uintptr_t>(aux) & 15) ||
+      !dtfk_gemm_big_supported(A, lda, transA, B, ldb, transB, 1, M, N, K, 0.f, 0, 1))
+    return hipErrorInvalidValue;
+  const dim3 grid((unsigned)((M / 256) * (N / BN)), 1), block(NTHR);
+  const uint16_t* a = static_cast<const uint16_t*>(A);
+  const uint16_t* b = static_cast<const uint16_t*>(B);
+  uint16_t* x = static_cast<uint16_t*>(aux);
+#define DTFK_GA(AK, BKk)                                                                                         \
+  hipLaunchKernelGGL((gemm_8ph<AK, BKk, true, true, 256, EP_GELU_AUX>), grid, block, 0, stream, a, lda, b, ldb, \
+                     C, ldc, bias, M, N, K, 1.f, 0.f, 0, K, 0LL, x, nullptr)
+  const bool akc = !transA, bkc = transB != 0;
+  if (akc) {
+    if (bkc) DTFK_GA(true, true); else DTFK_GA(true, false);
+  } else {
+    if (bkc) DTFK_GA(false, true); else DTFK_GA(false, false);
+  }
+#undef DTFK_GA
   return hipGetLastError();
 }
 

@@ -95,64 +95,92 @@ class _ShadowLinear(torch.autograd.Function):
         return gx, _wgrad(gy2, x2), None, None
 
 
-class _GeluShadowLinear(torch.autograd.Function):
-    """y = gelu(u + b) @ w16^T: BERT's FFN-down projection fused with the bias +
-    GELU that feeds it.  Backward computes dU = (gy W) * gelu'(u + b) as ONE
-    gemm_big launch with the GELU backward and the bias gradient's partial
-    column sums in its epilogue (gemm_big.hip gemm_8ph<DG>, ops.big_gemm
-    use_dgelu) -- the dH tensor is never written or re-read -- or, where the
-    per-shape timing says otherwise, the dX GEMM + the bias_gelu_bwd pass."""
+def _linear_dx(gy2, w16, extra=None):
+    """dX = gy2 @ w16 on the engine use_native picks; `extra` (a residual
+    branch's gradient of X) accumulated in place as the GEMM's beta = 1 term."""
+    native = big_gemm.use_native("dx", gy2.shape[0], w16.shape[1], gy2.shape[1], gy2.device)
+    if extra is not None:
+        return big_gemm.linear_dx(gy2, w16, extra=extra) if native else extra.addmm_(gy2, w16)
+    return big_gemm.linear_dx(gy2, w16) if native else gy2 @ w16
+
+
+def _linear_dw(gy2, x2, w):
+    """dW = gy2^T x2: sunk into the DDP bucket (returns None) or returned."""
+    if grad_sink.enabled(w) and (w.grad is None or w.grad.is_contiguous()):
+        _wgrad(gy2, x2, into=grad_sink.target(w))
+        grad_sink.done(w)
+        return None
+    return _wgrad(gy2, x2)
+
+
+class _FFN(torch.autograd.Function):
+    """y = gelu(x W1^T + b1) W2^T: BERT's feed-forward block on the bf16 weight
+    shadows, with GELU in the GEMM epilogues (gemm_big.hip gemm_8ph<EP>):
+      forward   FFN-up writes the pre-activation u = x W1^T + b1 AND h = gelu(u)
+                from one epilogue (gemm_gelu_aux), or hipBLASLt + bias_gelu_fwd;
+      backward  dU = (gy W2) * gelu'(u) with the b1-gradient partial column sums
+                in one epilogue (gemm_dgelu), or the dH GEMM + bias_gelu_bwd;
+    each fused path only where the per-shape timing (ops.big_gemm use_gelu_aux /
+    use_dgelu) beats the separate passes.  `slot`: LN2's residual gradient of x,
+    accumulated by the dX GEMM (beta = 1)."""
 
     @staticmethod
-    def forward(ctx, u, b, w, w16):
-        u = u.contiguous()
+    def forward(ctx, x, w1, w1_16, b1, w2, w2_16, slot):
+        x2 = x.reshape(-1, x.shape[-1])
+        M, F_, H = x2.shape[0], w1_16.shape[0], x2.shape[1]
+        u = torch.empty(M, F_, device=x.device, dtype=x.dtype)
         h = torch.empty_like(u)
-        T._C().bias_gelu_fwd(u, b, h)
-        ctx.save_for_backward(u, h, w16, b)
-        ctx.w, ctx.b = w, b
-        h2 = h.reshape(-1, h.shape[-1])
-        if big_gemm.use_native("fwd", h2.shape[0], w16.shape[0], h2.shape[1], h.device):
-            return big_gemm.linear_fwd(h2, w16).view(*h.shape[:-1], w16.shape[0])
-        return F.linear(h, w16)
+        ctx.biased = big_gemm.use_gelu_aux(M, F_, H, x.device) and T._C().gemm_gelu_aux(x2, False, w1_16, True,
+                                                                                        h, u, b1)
+        if not ctx.biased:      # u without b1; bias_gelu adds it
+            if big_gemm.use_native("fwd", M, F_, H, x.device):
+                big_gemm.linear_fwd(x2, w1_16, out=u)
+            else:
+                torch.mm(x2, w1_16.t(), out=u)
+            T._C().bias_gelu_fwd(u, b1, h)
+        ctx.save_for_backward(x2, u, h, w1_16, w2_16, b1)
+        ctx.w1, ctx.b1, ctx.w2, ctx.slot, ctx.xshape = w1, b1, w2, slot, x.shape
+        if big_gemm.use_native("fwd", M, w2_16.shape[0], F_, x.device):
+            y = big_gemm.linear_fwd(h, w2_16)
+        else:
+            y = torch.mm(h, w2_16.t())
+        return y.view(*x.shape[:-1], w2_16.shape[0])
 
     @staticmethod
     def backward(ctx, gy):
-        u, h, w16, b = ctx.saved_tensors
-        gy2 = gy.to(w16.dtype).reshape(-1, gy.shape[-1])
-        u2, h2 = u.reshape(-1, u.shape[-1]), h.reshape(-1, h.shape[-1])
-        M, N, K = u2.shape[0], u2.shape[1], gy2.shape[1]
-        w = ctx.w
-        if grad_sink.enabled(w) and (w.grad is None or w.grad.is_contiguous()):
-            _wgrad(gy2, h2, into=grad_sink.target(w))
-            grad_sink.done(w)
-            gw = None
-        else:
-            gw = _wgrad(gy2, h2)
+        x2, u, h, w1_16, w2_16, b1 = ctx.saved_tensors
+        gy2 = gy.to(w2_16.dtype).reshape(-1, gy.shape[-1])
+        M, F_, K = u.shape[0], u.shape[1], gy2.shape[1]
+        gw2 = _linear_dw(gy2, h, ctx.w2)
         C = T._C()
-        pb = ctx.b
+        pb = ctx.b1
         sink = grad_sink.all_enabled(pb)
-        db = grad_sink.target(pb) if sink else torch.empty(N, dtype=torch.float32, device=u.device)
-        du = torch.empty_like(u2)
+        db = grad_sink.target(pb) if sink else torch.empty(F_, dtype=torch.float32, device=u.device)
+        ub = None if ctx.biased else b1           # the bias still to add to the saved u
+        du = torch.empty_like(u)
         fused = False
-        if big_gemm.use_dgelu(M, N, K, u.device):
-            colpart = torch.empty((M // 128) * N, dtype=torch.float32, device=u.device)
-            fused = C.gemm_dgelu(gy2, False, w16, False, du, u2, b, colpart, db, accumulate=sink)
+        if big_gemm.use_dgelu(M, F_, K, u.device):
+            colpart = torch.empty((M // 128) * F_, dtype=torch.float32, device=u.device)
+            fused = C.gemm_dgelu(gy2, False, w2_16, False, du, u, ub, colpart, db, accumulate=sink)
         if not fused:
-            dh = big_gemm.linear_dx(gy2, w16) if big_gemm.use_native("dx", M, N, K, u.device) else gy2 @ w16
-            part = torch.empty(big_gemm.gelu_bwd_slices(M) * N, dtype=torch.float32, device=u.device)
-            C.bias_gelu_bwd(dh, u2, b, du, part, db, accumulate=sink)
+            dh = _linear_dx(gy2, w2_16)
+            part = torch.empty(big_gemm.gelu_bwd_slices(M) * F_, dtype=torch.float32, device=u.device)
+            C.bias_gelu_bwd(dh, u, ub if ub is not None else torch.zeros_like(b1), du, part, db, accumulate=sink)
         if sink:
             grad_sink.done(pb)
             db = None
-        return du.view(u.shape), db, gw, None
+        extra = ctx.slot.take() if ctx.slot is not None else None
+        gx = _linear_dx(du, w1_16, extra.reshape(-1, x2.shape[1]) if extra is not None else None)
+        gw1 = _linear_dw(du, x2, ctx.w1)
+        return gx.view(ctx.xshape), gw1, None, db, gw2, None, None
 
 
-def _gelu_mm(u, b, w):
-    """gelu(u + b) @ w^T, fused with its backward on the bf16-shadow path."""
-    w16 = getattr(w, "_shadow", None)
-    if w16 is not None and u.is_cuda and u.dtype == w16.dtype:
-        return _GeluShadowLinear.apply(u, b, w, w16)
-    return _mm(T.bias_gelu(u, b), w)
+def _ffn(x, w1, b1, w2, slot=None):
+    """gelu(x W1^T + b1) W2^T, fused on the bf16-shadow path."""
+    w1_16, w2_16 = getattr(w1, "_shadow", None), getattr(w2, "_shadow", None)
+    if w1_16 is not None and w2_16 is not None and x.is_cuda and x.dtype == w1_16.dtype:
+        return _FFN.apply(x, w1, w1_16, b1, w2, w2_16, slot)
+    return _mm(T.bias_gelu(_mm(x, w1, slot), b1), w2)
 
 
 def _wgrad_split(T: int, out: int, inp: int) -> int:
@@ -259,7 +287,7 @@ class BertLayer(torch.nn.Module):
         a = T.bias_dropout_residual_layernorm(_mm(ctx, self.w_o), self.b_o, x, self.ln1_g, self.ln1_b,
                                               c.dropout, c.ln_eps, self.training, residual_slot=slot_x)
         slot_a = _slot_for(a, self.w_1)        # LN2's residual grad of a -> W1 GEMM's dX
-        pre = _gelu_mm(_mm(a, self.w_1, slot_a), self.b_1, self.w_2)
+        pre = _ffn(a, self.w_1, self.b_1, self.w_2, slot_a)
         out = T.bias_dropout_residual_layernorm(pre, self.b_2, a, self.ln2_g, self.ln2_b,
                                                 c.dropout, c.ln_eps, self.training, residual_slot=slot_a)
         return out

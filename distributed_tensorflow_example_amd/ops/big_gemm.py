@@ -25,7 +25,10 @@ from .. import _native
 # weight gradients (profiles/gemm_8ph_r3.txt); end to end 'auto' measured equal
 # to 'never' and 'always' 3 % slower;  never: hipBLASLt;  always: this kernel
 _POLICY = os.environ.get("DTF_BIG_GEMM", "auto")
-_DGELU = os.environ.get("DTF_GEMM_DGELU", "1") != "0"   # fused GELU-backward epilogue (use_dgelu)
+# fused GELU epilogues: 1 both (use_gelu_aux, use_dgelu), bwd only the backward one, 0 none
+_GELU_EPI = os.environ.get("DTF_GEMM_DGELU", "1")
+_DGELU = _GELU_EPI != "0"
+_GELU_AUX = _GELU_EPI not in ("0", "bwd")
 _choice: dict = {}
 _timings: dict = {}
 
@@ -133,6 +136,44 @@ def use_dgelu(M: int, N: int, K: int, dev) -> bool:
             dh = linear_dx(a, b) if native_dx else torch.mm(a, b)
             C.bias_gelu_bwd(dh, aux, bias, out, part, db, accumulate=False)
         t_ours = _time(lambda: C.gemm_dgelu(a, False, b, False, out, aux, bias, colpart, db))
+        t_theirs = _time(theirs)
+        hit = _choice[key] = t_ours <= t_theirs
+        _timings[key] = (round(t_ours, 4), round(t_theirs, 4))
+    return hit
+
+
+def use_gelu_aux(M: int, N: int, K: int, dev) -> bool:
+    """True when the forward of a linear layer followed by bias + GELU should
+    run as ONE gemm_big launch writing the pre-activation and the activation
+    (gemm_gelu_aux) instead of the GEMM (whichever engine use_native picks) +
+    the bias_gelu_fwd pass; timed once per shape under 'auto'."""
+    if (_POLICY == "never" or not _GELU_AUX or M % 256 or N % 256 or K % 128
+            or torch.device(dev).type != "cuda"):
+        return False
+    if _POLICY == "always":
+        return True
+    key = ("gelu_aux", M, N, K)
+    hit = _choice.get(key)
+    if hit is None:
+        if torch.cuda.is_current_stream_capturing():
+            return False
+        C = _C()
+        bf = torch.bfloat16
+        a, b = torch.randn(M, K, device=dev, dtype=bf), torch.randn(N, K, device=dev, dtype=bf)
+        u, h = torch.empty(M, N, device=dev, dtype=bf), torch.empty(M, N, device=dev, dtype=bf)
+        bias = torch.randn(N, device=dev)
+        if not C.gemm_gelu_aux(a, False, b, True, h, u, bias):
+            _choice[key] = False
+            return False
+        native = use_native("fwd", M, N, K, dev)
+
+        def theirs():
+            if native:
+                linear_fwd(a, b, out=u)
+            else:
+                torch.mm(a, b.t(), out=u)
+            C.bias_gelu_fwd(u, bias, h)
+        t_ours = _time(lambda: C.gemm_gelu_aux(a, False, b, True, h, u, bias))
         t_theirs = _time(theirs)
         hit = _choice[key] = t_ours <= t_theirs
         _timings[key] = (round(t_ours, 4), round(t_theirs, 4))

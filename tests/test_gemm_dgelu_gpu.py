@@ -46,29 +46,60 @@ def test_gemm_dgelu_refuses_off_contract(native):
     assert not native.gemm_dgelu(dy, False, w, False, du, u, b, torch.empty(3 * 512, device="cuda"), db)
 
 
+@pytest.mark.parametrize("M,N,K", [(512, 512, 256), (2048, 3072, 768)])
+def test_gemm_gelu_aux_matches_fp32(native, M, N, K):
+    torch.manual_seed(2)
+    bf = torch.bfloat16
+    x = torch.randn(M, K, device="cuda").to(bf)
+    w = (torch.randn(N, K, device="cuda") * K ** -0.5).to(bf)
+    b = torch.randn(N, device="cuda") * 0.1
+    u, h = torch.empty(M, N, device="cuda", dtype=bf), torch.empty(M, N, device="cuda", dtype=bf)
+    assert native.gemm_gelu_aux(x, False, w, True, h, u, b)
+    ur = x.float() @ w.float().t() + b
+    torch.testing.assert_close(u.float(), ur, rtol=1e-2, atol=1e-2 * ur.abs().max().item())
+    hr = gelu_ref(ur)
+    torch.testing.assert_close(h.float(), hr, rtol=1e-2, atol=1e-2 * hr.abs().max().item())
+
+
+def test_gemm_dgelu_without_bias(native):
+    torch.manual_seed(3)
+    bf = torch.bfloat16
+    dy = torch.randn(512, 256, device="cuda").to(bf)
+    w = (torch.randn(256, 512, device="cuda") * 0.0625).to(bf)
+    u = torch.randn(512, 512, device="cuda").to(bf)
+    du, db = torch.empty_like(u), torch.empty(512, device="cuda")
+    assert native.gemm_dgelu(dy, False, w, False, du, u, None, torch.empty(4 * 512, device="cuda"), db)
+    ref = (dy.float() @ w.float()) * _gelu_grad_ref(u.float())
+    torch.testing.assert_close(du.float(), ref, rtol=1e-2, atol=1e-2 * ref.abs().max().item())
+    torch.testing.assert_close(db, ref.sum(0), rtol=1e-3, atol=1e-3 * ref.abs().sum(0).max().item())
+
+
 @pytest.mark.parametrize("policy", ["always", "never"])
-def test_bert_fused_ffn_down_matches_unfused(native, monkeypatch, policy):
-    """_GeluShadowLinear (fused epilogue or fallback) vs bias_gelu + linear in
-    fp32 autograd: input, bias and weight gradients."""
+def test_bert_fused_ffn_matches_fp32(native, monkeypatch, policy):
+    """models/bert.py _FFN (fused GELU epilogues under 'always', the separate
+    passes under 'never') vs gelu(x W1^T + b1) W2^T in fp32 autograd: the
+    output and the x, W1, b1, W2 gradients."""
     from distributed_tensorflow_example_amd.models import bert
     from distributed_tensorflow_example_amd.ops import big_gemm
 
     monkeypatch.setattr(big_gemm, "_POLICY", policy)
     torch.manual_seed(1)
-    M, H, O = 1024, 512, 256
-    u = torch.randn(M, H, device="cuda").to(torch.bfloat16).requires_grad_(True)
-    b = (torch.randn(H, device="cuda") * 0.1).requires_grad_(True)
-    w = (torch.randn(O, H, device="cuda") * H ** -0.5).requires_grad_(True)
-    w._shadow = w.detach().to(torch.bfloat16)
-    y = bert._gelu_mm(u, b, w)
-    g = torch.randn(M, O, device="cuda").to(torch.bfloat16)
+    M, D, F_ = 1024, 256, 512
+    x = torch.randn(M, D, device="cuda").to(torch.bfloat16).requires_grad_(True)
+    w1 = (torch.randn(F_, D, device="cuda") * D ** -0.5).requires_grad_(True)
+    b1 = (torch.randn(F_, device="cuda") * 0.1).requires_grad_(True)
+    w2 = (torch.randn(D, F_, device="cuda") * F_ ** -0.5).requires_grad_(True)
+    for w in (w1, w2):
+        w._shadow = w.detach().to(torch.bfloat16)
+    y = bert._ffn(x, w1, b1, w2)
+    g = torch.randn(M, D, device="cuda").to(torch.bfloat16)
     y.backward(g)
-    ur = u.detach().float().requires_grad_(True)
-    br = b.detach().clone().requires_grad_(True)
-    wr = w._shadow.float().requires_grad_(True)
-    yr = gelu_ref(ur + br) @ wr.t()
+    xr = x.detach().float().requires_grad_(True)
+    w1r = w1._shadow.float().requires_grad_(True)
+    b1r = b1.detach().clone().requires_grad_(True)
+    w2r = w2._shadow.float().requires_grad_(True)
+    yr = gelu_ref(xr @ w1r.t() + b1r) @ w2r.t()
     yr.backward(g.float())
-    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=2e-2 * yr.abs().max().item())
-    torch.testing.assert_close(u.grad.float(), ur.grad, rtol=2e-2, atol=2e-2 * ur.grad.abs().max().item())
-    torch.testing.assert_close(b.grad, br.grad, rtol=2e-2, atol=2e-2 * br.grad.abs().max().item())
-    torch.testing.assert_close(w.grad, wr.grad, rtol=2e-2, atol=2e-2 * wr.grad.abs().max().item())
+    for got, ref in ((y.float(), yr), (x.grad.float(), xr.grad), (w1.grad, w1r.grad), (b1.grad, b1r.grad),
+                     (w2.grad, w2r.grad)):
+        torch.testing.assert_close(got, ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item())

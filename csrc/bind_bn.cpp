@@ -3,6 +3,8 @@
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <stdexcept>
 #include <string>
 
@@ -16,7 +18,7 @@ hipError_t dtfk_bn_apply(const void* x, const void* res, const float* scale, con
 hipError_t dtfk_bn_bwd(const void* dy, const void* x, const void* res, const float* gamma, const float* mean,
                        const float* invstd, const float* scale, const float* shift, float* part, float* coef,
                        void* dx, void* dres, float* dgamma, float* dbeta, int M, int C, int relu, int accum,
-                       hipStream_t st);
+                       int write_g, hipStream_t st);
 hipError_t dtfk_maxpool_fwd(const void* x, void* y, void* idx, int N, int H, int W, int C, int Ho, int Wo, int k,
                             int s, int p, hipStream_t st);
 hipError_t dtfk_maxpool_bwd(const void* dy, const void* idx, void* dx, int N, int H, int W, int C, int Ho, int Wo,
@@ -115,10 +117,16 @@ void bn_bwd(at::Tensor dy, at::Tensor x, c10::optional<at::Tensor> res, at::Tens
   f32(stats, 4 * C, "stats"); f32(coef, 3 * C, "coef"); f32(dgamma, C, "dgamma"); f32(dbeta, C, "dbeta");
   f32(part, 2 * (int64_t)dtfk_bn_partial_rows((int)M, (int)C) * C, "part");
   const float* s = stats.data_ptr<float>();
+  // residual + ReLU blocks: the partials pass stores g = dres and the apply pass reads
+  // (g, x) -- one tensor pass fewer (DTF_BN_WRITE_G=0: recompute g from dy, x, res twice)
+  static const bool write_g = [] {
+    const char* e = getenv("DTF_BN_WRITE_G");
+    return e == nullptr || e[0] != '0';
+  }();
   ck(dtfk_bn_bwd(dy.data_ptr(), x.data_ptr(), res.has_value() ? res->data_ptr() : nullptr, gamma.data_ptr<float>(),
                  s, s + C, s + 2 * C, s + 3 * C, part.data_ptr<float>(), coef.data_ptr<float>(), dx.data_ptr(),
                  dres.has_value() ? dres->data_ptr() : nullptr, dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
-                 (int)M, (int)C, relu ? 1 : 0, accum ? 1 : 0, cs()),
+                 (int)M, (int)C, relu ? 1 : 0, accum ? 1 : 0, write_g ? 1 : 0, cs()),
      "bn_bwd");
 }
 

@@ -178,14 +178,18 @@ __global__ __launch_bounds__(256) void bn_apply(const uint16_t* __restrict__ x, 
 }
 
 // g = dy * relu'(y) with y recomputed from x (and res); partial sums of g and g*x_hat.
-template <bool RES, bool RELU>
+// WG (residual + ReLU blocks): g is also stored (it IS the residual branch's
+// gradient, exact in bf16: dy or 0), and the apply pass then reads g and x
+// only -- 7 tensor passes instead of 8 (dy, x, res read twice; dx, dres written).
+template <bool RES, bool RELU, bool WG = false>
 __global__ __launch_bounds__(256) void bn_bwd_partials(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
                                                        const uint16_t* __restrict__ res,
                                                        const float* __restrict__ mean,
                                                        const float* __restrict__ invstd,
                                                        const float* __restrict__ scale,
                                                        const float* __restrict__ shift, float* __restrict__ part,
-                                                       int M, int C) {
+                                                       int M, int C, uint16_t* __restrict__ gout = nullptr) {
+  static_assert(!WG || (RES && RELU), "g is only worth storing for residual + ReLU blocks");
   const int P = gridDim.y;
   const int c0 = blockIdx.x * 64;
   const int cc = c0 + (threadIdx.x & 7) * 8;
@@ -211,7 +215,7 @@ __global__ __launch_bounds__(256) void bn_bwd_partials(const uint16_t* __restric
         if constexpr (RES) ld8(res + e, rr[k]);
       }
 #pragma unroll
-      for (int k = 0; k < NR; ++k)
+      for (int k = 0; k < NR; ++k) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             float g = d[k][j];
@@ -220,9 +224,12 @@ __global__ __launch_bounds__(256) void bn_bwd_partials(const uint16_t* __restric
               if constexpr (RES) o += rr[k][j];
               g = o > 0.f ? g : 0.f;
             }
+            d[k][j] = g;
             sg[j] += g;
             sgx[j] += g * (v[k][j] - mu[j]) * is[j];
           }
+        if constexpr (WG) st8(gout + (size_t)rows.r[k] * C + cc, d[k]);
+      }
     });
   }
   bn_tile_store(sg, sgx, part, P, C, c0);
@@ -353,22 +360,33 @@ hipError_t dtfk_bn_apply(const void* x, const void* res, const float* scale, con
 }
 
 // backward.  coef: [3, C] scratch; part: [2 * P, C]
+// write_g (residual + ReLU only): the partials pass stores g into dres and the
+// apply pass reads (g, x) instead of (dy, x, res).
 hipError_t dtfk_bn_bwd(const void* dy, const void* x, const void* res, const float* gamma, const float* mean,
                        const float* invstd, const float* scale, const float* shift, float* part, float* coef,
                        void* dx, void* dres, float* dgamma, float* dbeta, int M, int C, int relu, int accum,
-                       hipStream_t st) {
+                       int write_g, hipStream_t st) {
   if (C % 8) return hipErrorInvalidValue;
   const int P = bn_grid(M, C);
   const uint16_t* dyp = (const uint16_t*)dy;
   const uint16_t* xp = (const uint16_t*)x;
   const uint16_t* rp = (const uint16_t*)res;
-#define DTFK_BNP(R, L) hipLaunchKernelGGL((bn_bwd_partials<R, L>), dim3((C + 63) / 64, P), dim3(256), 0, st, dyp, xp, rp, mean, invstd, scale, shift, part, M, C)
+  const long long n8 = (long long)M * C / 8;
+  if (res && relu && write_g && dres) {
+    hipLaunchKernelGGL((bn_bwd_partials<true, true, true>), dim3((C + 63) / 64, P), dim3(256), 0, st, dyp, xp, rp,
+                       mean, invstd, scale, shift, part, M, C, (uint16_t*)dres);
+    hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + 63) / 64), dim3(1024), 0, st, part, P, M, C, gamma, mean, invstd,
+                       dgamma, dbeta, coef, accum);
+    hipLaunchKernelGGL((bn_bwd_apply<false, false>), dim3(ew_grid(n8)), dim3(256), 0, st, (const uint16_t*)dres, xp,
+                       nullptr, scale, shift, coef, (uint16_t*)dx, nullptr, n8, C);
+    return hipGetLastError();
+  }
+#define DTFK_BNP(R, L) hipLaunchKernelGGL((bn_bwd_partials<R, L>), dim3((C + 63) / 64, P), dim3(256), 0, st, dyp, xp, rp, mean, invstd, scale, shift, part, M, C, nullptr)
   if (res && relu) DTFK_BNP(true, true); else if (res) DTFK_BNP(true, false);
   else if (relu) DTFK_BNP(false, true); else DTFK_BNP(false, false);
 #undef DTFK_BNP
   hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + 63) / 64), dim3(1024), 0, st, part, P, M, C, gamma, mean, invstd,
                      dgamma, dbeta, coef, accum);
-  const long long n8 = (long long)M * C / 8;
 #define DTFK_BNA(R, L) hipLaunchKernelGGL((bn_bwd_apply<R, L>), dim3(ew_grid(n8)), dim3(256), 0, st, dyp, xp, rp, scale, shift, coef, (uint16_t*)dx, (uint16_t*)dres, n8, C)
   if (res && relu) DTFK_BNA(true, true); else if (res) DTFK_BNA(true, false);
   else if (relu) DTFK_BNA(false, true); else DTFK_BNA(false, false);

@@ -93,24 +93,27 @@ __global__ __launch_bounds__(256) void bn_partials(const uint16_t* __restrict__ 
   bn_tile_store(s, q, part, P, C, c0);
 }
 
-// Column sums of the [2P, C] partials: 1024 threads = 64 channels x 16 row
-// groups (coalesced), LDS tree.  Returns (sum of pass 0, sum of pass 1) to the
-// g == 0 threads.
+// Column sums of the [2P, C] partials: 1024 threads = 16 channels x 64 row
+// groups, so each thread reads only P / 64 rows per pass (the finalize
+// kernels are latency-bound: ~2 memory round trips instead of ~8 with 64
+// channels x 16 groups), then an LDS tree over the groups (fixed order,
+// deterministic).  Returns (sum of pass 0, sum of pass 1) to the g == 0 threads.
+constexpr int FIN_C = 16, FIN_G = 64;
 __device__ __forceinline__ void sum_partials(const float* __restrict__ part, int P, int C, int c, int lane, int g,
                                              double& s0, double& s1) {
-  __shared__ double red[2][16][64];
+  __shared__ double red[2][FIN_G][FIN_C];
   double a = 0.0, b = 0.0;
   if (c < C) {
     int p = g;
-    for (; p + 48 < P; p += 64) {      // four independent loads per sum in flight
-      float x0 = part[(size_t)p * C + c], x1 = part[(size_t)(p + 16) * C + c];
-      float x2 = part[(size_t)(p + 32) * C + c], x3 = part[(size_t)(p + 48) * C + c];
-      float y0 = part[((size_t)P + p) * C + c], y1 = part[((size_t)P + p + 16) * C + c];
-      float y2 = part[((size_t)P + p + 32) * C + c], y3 = part[((size_t)P + p + 48) * C + c];
+    for (; p + 3 * FIN_G < P; p += 4 * FIN_G) {      // four independent loads per sum in flight
+      float x0 = part[(size_t)p * C + c], x1 = part[(size_t)(p + FIN_G) * C + c];
+      float x2 = part[(size_t)(p + 2 * FIN_G) * C + c], x3 = part[(size_t)(p + 3 * FIN_G) * C + c];
+      float y0 = part[((size_t)P + p) * C + c], y1 = part[((size_t)P + p + FIN_G) * C + c];
+      float y2 = part[((size_t)P + p + 2 * FIN_G) * C + c], y3 = part[((size_t)P + p + 3 * FIN_G) * C + c];
       a += ((double)x0 + x1) + ((double)x2 + x3);
       b += ((double)y0 + y1) + ((double)y2 + y3);
     }
-    for (; p < P; p += 16) {
+    for (; p < P; p += FIN_G) {
       a += part[(size_t)p * C + c];
       b += part[((size_t)P + p) * C + c];
     }
@@ -118,10 +121,16 @@ __device__ __forceinline__ void sum_partials(const float* __restrict__ part, int
   red[0][g][lane] = a;
   red[1][g][lane] = b;
   __syncthreads();
-  s0 = s1 = 0.0;
-  if (g == 0)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) { s0 += red[0][i][lane]; s1 += red[1][i][lane]; }
+  for (int st = FIN_G / 2; st > 0; st >>= 1) {
+    if (g < st) {
+      red[0][g][lane] += red[0][g + st][lane];
+      red[1][g][lane] += red[1][g + st][lane];
+    }
+    __syncthreads();
+  }
+  s0 = red[0][0][lane];
+  s1 = red[1][0][lane];
 }
 
 // mean/var (double), running stats, scale = gamma*invstd, shift = beta - mean*scale.
@@ -131,8 +140,8 @@ __global__ __launch_bounds__(1024) void bn_finalize(const float* __restrict__ pa
                                                     float* __restrict__ scale, float* __restrict__ shift,
                                                     float* __restrict__ run_mean, float* __restrict__ run_var,
                                                     float momentum, float eps) {
-  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
+  const int lane = threadIdx.x % FIN_C, g = threadIdx.x / FIN_C;
+  const int c = blockIdx.x * FIN_C + lane;
   double s, q;
   sum_partials(part, P, C, c, lane, g, s, q);
   if (g != 0 || c >= C) return;
@@ -243,8 +252,8 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize(const float* __restrict_
                                                         const float* __restrict__ invstd, float* __restrict__ dgamma,
                                                         float* __restrict__ dbeta, float* __restrict__ coef,
                                                         int accum) {
-  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
+  const int lane = threadIdx.x % FIN_C, g = threadIdx.x / FIN_C;
+  const int c = blockIdx.x * FIN_C + lane;
   double sgd, sgxd;
   sum_partials(part, P, C, c, lane, g, sgd, sgxd);
   if (g != 0 || c >= C) return;
@@ -331,7 +340,7 @@ hipError_t dtfk_bn_fwd(const void* x, const void* res, const float* gamma, const
   if (C % 8) return hipErrorInvalidValue;
   const int P = bn_grid(M, C);
   hipLaunchKernelGGL(bn_partials, dim3((C + 63) / 64, P), dim3(256), 0, st, (const uint16_t*)x, part, M, C);
-  hipLaunchKernelGGL(bn_finalize, dim3((C + 63) / 64), dim3(1024), 0, st, part, P, M, C, gamma, beta, mean, invstd,
+  hipLaunchKernelGGL(bn_finalize, dim3((C + FIN_C - 1) / FIN_C), dim3(1024), 0, st, part, P, M, C, gamma, beta, mean, invstd,
                      scale, shift, run_mean, run_var, momentum, eps);
   const long long n8 = (long long)M * C / 8;
   const uint16_t* xp = (const uint16_t*)x;
@@ -375,7 +384,7 @@ hipError_t dtfk_bn_bwd(const void* dy, const void* x, const void* res, const flo
   if (res && relu && write_g && dres) {
     hipLaunchKernelGGL((bn_bwd_partials<true, true, true>), dim3((C + 63) / 64, P), dim3(256), 0, st, dyp, xp, rp,
                        mean, invstd, scale, shift, part, M, C, (uint16_t*)dres);
-    hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + 63) / 64), dim3(1024), 0, st, part, P, M, C, gamma, mean, invstd,
+    hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + FIN_C - 1) / FIN_C), dim3(1024), 0, st, part, P, M, C, gamma, mean, invstd,
                        dgamma, dbeta, coef, accum);
     hipLaunchKernelGGL((bn_bwd_apply<false, false>), dim3(ew_grid(n8)), dim3(256), 0, st, (const uint16_t*)dres, xp,
                        nullptr, scale, shift, coef, (uint16_t*)dx, nullptr, n8, C);
@@ -385,7 +394,7 @@ hipError_t dtfk_bn_bwd(const void* dy, const void* x, const void* res, const flo
   if (res && relu) DTFK_BNP(true, true); else if (res) DTFK_BNP(true, false);
   else if (relu) DTFK_BNP(false, true); else DTFK_BNP(false, false);
 #undef DTFK_BNP
-  hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + 63) / 64), dim3(1024), 0, st, part, P, M, C, gamma, mean, invstd,
+  hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + FIN_C - 1) / FIN_C), dim3(1024), 0, st, part, P, M, C, gamma, mean, invstd,
                      dgamma, dbeta, coef, accum);
 #define DTFK_BNA(R, L) hipLaunchKernelGGL((bn_bwd_apply<R, L>), dim3(ew_grid(n8)), dim3(256), 0, st, dyp, xp, rp, scale, shift, coef, (uint16_t*)dx, (uint16_t*)dres, n8, C)
   if (res && relu) DTFK_BNA(true, true); else if (res) DTFK_BNA(true, false);

@@ -363,30 +363,35 @@ struct ColsumArgs {
   const float* part[3];
   float* out[3];
 };
+// 1024 threads = 16 consecutive columns x 64 row groups: a thread sums only
+// P / 64 partial rows (4 loads in flight), so the few-microsecond latency of
+// this launch-bound pass is ~2 memory round trips instead of ~8 with 64-wide
+// column tiles; LDS tree over the groups, fixed order (deterministic).
+constexpr int CS_COLS = 16, CS_GROUPS = 64;
 __global__ __launch_bounds__(1024) void colsum_partials(ColsumArgs a, int P, int H, int accumulate) {
-  __shared__ float red[16][64];
+  __shared__ float red[CS_GROUPS][CS_COLS];
   const float* __restrict__ part = a.part[blockIdx.y];
   float* __restrict__ out = a.out[blockIdx.y];
-  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
-  // 4 independent accumulators: 4 loads in flight per thread (the partial
-  // buffers have up to 1024 rows, and this grid is only H/64 blocks wide);
-  // the summation order is still fixed, so the result stays deterministic
+  const int lane = threadIdx.x % CS_COLS, g = threadIdx.x / CS_COLS;
+  const int c = blockIdx.x * CS_COLS + lane;
   float s[4] = {0.f, 0.f, 0.f, 0.f};
   if (c < H) {
     int p = g;
-    for (; p + 48 < P; p += 64) {
+    for (; p + 3 * CS_GROUPS < P; p += 4 * CS_GROUPS) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) s[u] += part[(size_t)(p + 16 * u) * H + c];
+      for (int u = 0; u < 4; ++u) s[u] += part[(size_t)(p + CS_GROUPS * u) * H + c];
     }
-    for (; p < P; p += 16) s[0] += part[(size_t)p * H + c];
+    for (; p < P; p += CS_GROUPS) s[0] += part[(size_t)p * H + c];
   }
   red[g][lane] = (s[0] + s[1]) + (s[2] + s[3]);
   __syncthreads();
-  if (g == 0 && c < H) {
-    float t = 0.f;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) t += red[i][lane];
+  for (int st = CS_GROUPS / 2; st > 0; st >>= 1) {
+    if (g < st) red[g][lane] += red[g + st][lane];
+    __syncthreads();
+  }
+  if (g == 0 && c < H) {
+    const float t = red[0][lane];
     out[c] = accumulate ? out[c] + t : t;
   }
 }
@@ -615,7 +620,7 @@ hipError_t dtfk_ln_bwd(const void* dy, const void* s, const float* mean, const f
 
 hipError_t dtfk_colsum_partials(const float* part, float* out, int P, int H, hipStream_t st) {
   dtfk::tfm::ColsumArgs a = {{part, nullptr, nullptr}, {out, nullptr, nullptr}};
-  hipLaunchKernelGGL(colsum_partials, dim3((H + 63) / 64, 1), dim3(1024), 0, st, a, P, H, 0);
+  hipLaunchKernelGGL(colsum_partials, dim3((H + CS_COLS - 1) / CS_COLS, 1), dim3(1024), 0, st, a, P, H, 0);
   return hipGetLastError();
 }
 
@@ -624,7 +629,7 @@ hipError_t dtfk_colsum_partials_multi(const float* const* parts, float* const* o
                                       int accumulate, hipStream_t st) {
   dtfk::tfm::ColsumArgs a = {{nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr}};
   for (int k = 0; k < nbuf; ++k) { a.part[k] = parts[k]; a.out[k] = outs[k]; }
-  hipLaunchKernelGGL(colsum_partials, dim3((H + 63) / 64, nbuf), dim3(1024), 0, st, a, P, H, accumulate);
+  hipLaunchKernelGGL(colsum_partials, dim3((H + CS_COLS - 1) / CS_COLS, nbuf), dim3(1024), 0, st, a, P, H, accumulate);
   return hipGetLastError();
 }
 
@@ -634,7 +639,7 @@ hipError_t dtfk_colsum_bf16(const void* x, float* part, float* out, int N, int H
   hipLaunchKernelGGL(colsum_bf16_partials, dim3((H + 511) / 512, P), dim3(256), 0, st,
                      static_cast<const uint16_t*>(x), part, N, H);
   dtfk::tfm::ColsumArgs a = {{part, nullptr, nullptr}, {out, nullptr, nullptr}};
-  hipLaunchKernelGGL(colsum_partials, dim3((H + 63) / 64, 1), dim3(1024), 0, st, a, P, H, accumulate);
+  hipLaunchKernelGGL(colsum_partials, dim3((H + CS_COLS - 1) / CS_COLS, 1), dim3(1024), 0, st, a, P, H, accumulate);
   return hipGetLastError();
 }
 

@@ -54,7 +54,8 @@ hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int n
                                 hipStream_t stream);
 long long dtfk_graph_mlp_part_floats(int B, int H);
 hipError_t dtfk_graph_feed_ingest(const void* host, void* dev, long long bytes, hipStream_t stream);
-hipError_t dtfk_graph_mlp_step(const float* x, const float* ylab, float* W1, float* b1, float* W2, float* b2,
+hipError_t dtfk_graph_mlp_step(const float* x, const uint8_t* xu, const float* ylab, float* W1, float* b1, float* W2,
+                               float* b2,
                                float* a2buf, float* dz2buf, float* part, float* gW1, float* gb1, float* gW2,
                                float* gb2, float* metrics, float* host_metrics, void* gstep, int gstep_kind,
                                const float* lr_ptr, int B, int K, int H, int C, int act, int naive, int sgd,
@@ -546,7 +547,7 @@ void graph_mlp_step(at::Tensor x, at::Tensor ylab, at::Tensor W1, at::Tensor b1,
   // L2's partials + the learning rate on the device (scratch from the caching allocator)
   at::Tensor part = at::zeros({dtfk_graph_mlp_part_floats(B, H) + 1}, x.options());
   part.narrow(0, 0, 1).fill_(lr);
-  hip_check(dtfk_graph_mlp_step(x.data_ptr<float>(), ylab.data_ptr<float>(), W1.data_ptr<float>(),
+  hip_check(dtfk_graph_mlp_step(x.data_ptr<float>(), nullptr, ylab.data_ptr<float>(), W1.data_ptr<float>(),
                                 b1.data_ptr<float>(), W2.data_ptr<float>(), b2.data_ptr<float>(),
                                 a2buf.data_ptr<float>(), dz2buf.data_ptr<float>(), part.data_ptr<float>() + 1, gW1,
                                 gb1, gW2, gb2, metrics.data_ptr<float>(), nullptr, gp, kind, part.data_ptr<float>(), B, K, H, C,
@@ -697,6 +698,52 @@ class GraphStepPlan {
     }
     ++steps_;
   }
+  // The same step fed uint8 pixels (the MNIST loader's source bytes of a float
+  // batch x = u8 / 255, data/mnist.py): a 4x smaller staging copy and transfer;
+  // the kernels convert with the loader's exact float32 division, so the step is
+  // bit-identical to run() with that float batch.  Direct launches only.
+  void run_u8(py::array xu8, py::array y, double lr, bool sync) {
+    const int64_t nx = (int64_t)B_ * K_, ny = (int64_t)B_ * C_;
+    TORCH_CHECK(!use_graph_, "GraphStepPlan.run_u8: direct-launch plans only");
+    TORCH_CHECK(xu8.dtype().is(py::dtype::of<uint8_t>()) && y.dtype().is(py::dtype::of<float>()),
+                "GraphStepPlan.run_u8: uint8 x and float32 y_ expected");
+    TORCH_CHECK((xu8.flags() & py::array::c_style) && (y.flags() & py::array::c_style),
+                "GraphStepPlan.run_u8: C-contiguous feeds expected");
+    TORCH_CHECK(xu8.size() == nx && y.size() == ny, "GraphStepPlan.run_u8: feed shapes differ from the plan's");
+    TORCH_CHECK(K_ % 4 == 0, "GraphStepPlan.run_u8: K % 4 == 0 expected");
+    const uint8_t* xp = static_cast<const uint8_t*>(xu8.data());
+    const float* yp = static_cast<const float*>(y.data());
+    hipStream_t st = cur_stream();
+    const int slot = slot_ ^= 1;
+    const int64_t xf = u8_x_floats();
+    {
+      py::gil_scoped_release nogil;
+      using clk = std::chrono::steady_clock;
+      const auto t0 = clk::now();
+      if (pending_[slot]) hip_check(hipEventSynchronize(ev_[slot]), "GraphStepPlan: staging slot");
+      pending_[slot] = false;
+      float* h = stage_[slot].data_ptr<float>();
+      std::memcpy(h, xp, (size_t)nx);
+      std::memcpy(h + xf, yp, sizeof(float) * ny);
+      h[xf + ny] = (float)lr;
+      t_[0] += std::chrono::duration<double, std::micro>(clk::now() - t0).count();
+      hip_check(hipMemcpyAsync(dev_.data_ptr<float>(), h, sizeof(float) * (xf + ny + 1), hipMemcpyHostToDevice, st),
+                "GraphStepPlan: feed copy");
+      if (!sync) {
+        hip_check(hipEventRecord(ev_[slot], st), "GraphStepPlan: event");
+        pending_[slot] = true;
+      }
+      hip_check(launch_step(st, host_store_, true), "GraphStepPlan: launch");
+      const auto t2 = clk::now();
+      t_[1] += std::chrono::duration<double, std::micro>(t2 - t0).count();
+      if (sync) {
+        hip_check(hipStreamSynchronize(st), "GraphStepPlan: sync");
+        pending_[0] = pending_[1] = false;
+      }
+      t_[2] += std::chrono::duration<double, std::micro>(clk::now() - t2).count();
+      ++steps_;
+    }
+  }
   int64_t steps() const { return steps_; }
   bool use_graph() const { return use_graph_; }
   // host-side split of the direct-launch calls so far, us per call: feed copy
@@ -715,14 +762,17 @@ class GraphStepPlan {
   // the step's three kernels on stream st; the metrics reach host_metrics_
   // either from the last kernel itself (system-scope stores into the pinned
   // buffer: direct launches) or by a copy back (captured graphs)
-  hipError_t launch_step(hipStream_t st, bool host_store) {
+  hipError_t launch_step(hipStream_t st, bool host_store, bool u8 = false) {
     const int64_t nx = (int64_t)B_ * K_, ny = (int64_t)B_ * C_;
     float* d = dev_.data_ptr<float>();
-    hipError_t e = dtfk_graph_mlp_step(d, d + nx, W1_.data_ptr<float>(), b1_.data_ptr<float>(), W2_.data_ptr<float>(),
+    // uint8 feed: [x bytes padded to 16 | y_ | lr] in the same device buffer
+    const uint8_t* xu = u8 ? reinterpret_cast<const uint8_t*>(d) : nullptr;
+    float* yd = u8 ? d + u8_x_floats() : d + nx;
+    hipError_t e = dtfk_graph_mlp_step(u8 ? nullptr : d, xu, yd, W1_.data_ptr<float>(), b1_.data_ptr<float>(), W2_.data_ptr<float>(),
                                        b2_.data_ptr<float>(), a2_.data_ptr<float>(), dz2_.data_ptr<float>(),
                                        part_.data_ptr<float>(), nullptr, nullptr, nullptr, nullptr,
                                        metrics_.data_ptr<float>(), host_store ? host_metrics_.data_ptr<float>() : nullptr,
-                                       gstep_.defined() ? gstep_.data_ptr() : nullptr, gkind_, d + nx + ny, B_, K_, H_,
+                                       gstep_.defined() ? gstep_.data_ptr() : nullptr, gkind_, yd + ny, B_, K_, H_,
                                        C_, act_, naive_ ? 1 : 0, 1, st);
     if (e == hipSuccess && !host_store)
       e = hipMemcpyAsync(host_metrics_.data_ptr<float>(), metrics_.data_ptr<float>(), 3 * sizeof(float),
@@ -742,6 +792,9 @@ class GraphStepPlan {
     graph_ = g;
     hip_check(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0), "GraphStepPlan: instantiate");
   }
+
+  // floats the uint8 x occupies at the front of the feed buffer (16-byte padded)
+  int64_t u8_x_floats() const { return ((int64_t)B_ * K_ + 15) / 16 * 4; }
 
   at::Tensor W1_, b1_, W2_, b2_, gstep_, dev_, a2_, dz2_, part_, metrics_, host_metrics_;
   at::Tensor stage_[2];
@@ -766,6 +819,7 @@ void init_mlp(py::module& m) {
            py::arg("naive"), py::arg("use_graph") = false)
       .def("use_graph", &GraphStepPlan::use_graph)
       .def("run", &GraphStepPlan::run, py::arg("x"), py::arg("y"), py::arg("lr"), py::arg("sync"))
+      .def("run_u8", &GraphStepPlan::run_u8, py::arg("xu8"), py::arg("y"), py::arg("lr"), py::arg("sync"))
       .def("host_metrics", &GraphStepPlan::host_metrics)
       .def("steps", &GraphStepPlan::steps)
       .def("timing", &GraphStepPlan::timing);

@@ -64,8 +64,16 @@ __device__ __forceinline__ float act_bwd(float a, int act) {
 constexpr int L1W = 8;     // waves per a2 tile (interleaved 16-deep K blocks)
 constexpr int PF = 8;      // K blocks per wave whose loads are issued before any MFMA
 
-template <bool VEC>   // VEC: K % 4 == 0 and x 16-byte aligned -> x as float4s
-__device__ __forceinline__ void l1_tile(const float* __restrict__ x, const float* __restrict__ W1,
+// A uint8 pixel as the float32 the MNIST loader feeds: k / 255 correctly rounded
+// (numpy's float32 division; data/mnist.py), so a uint8 feed is bit-identical to
+// the float one.
+__device__ __forceinline__ float px255(uint32_t k) { return __fdiv_rn((float)k, 255.f); }
+
+// VEC: K % 4 == 0 and x 16-byte aligned -> x as float4s.  U8: x is uint8 pixels
+// (xu, 4-byte aligned rows, K % 4 == 0), 4 per 32-bit load, converted by px255.
+template <bool VEC, bool U8 = false>
+__device__ __forceinline__ void l1_tile(const float* __restrict__ x, const uint8_t* __restrict__ xu,
+                                        const float* __restrict__ W1,
                                         const float* __restrict__ b1, float* __restrict__ a2,
                                         int B, int K, int H, int HP, int act) {
   __shared__ f32x4 part[L1W][64];
@@ -76,6 +84,7 @@ __device__ __forceinline__ void l1_tile(const float* __restrict__ x, const float
   const int row = r0 + r, col = c0 + r;
   const bool rv = row < B, cv = col < H;
   const float* xr = x + (size_t)min(row, B - 1) * K;
+  const uint8_t* xur = xu + (size_t)min(row, B - 1) * K;
   const float* wc = W1 + min(col, H - 1);
   const float bv = pin(b1[min(col, H - 1)]);   // issued with the operand loads, not after the barrier
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -87,7 +96,12 @@ __device__ __forceinline__ void l1_tile(const float* __restrict__ x, const float
 #pragma unroll
     for (int j = 0; j < PF; ++j) {
       const int k = (base + j * L1W) * 16 + 4 * g;
-      if constexpr (VEC) {
+      if constexpr (U8) {
+        const uint32_t v = *reinterpret_cast<const uint32_t*>(xur + min(k, K - 4));
+        const bool ok = k < K;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) xa[j][s] = ok ? px255((v >> (8 * s)) & 255u) : 0.f;
+      } else if constexpr (VEC) {
         const float4 v = *reinterpret_cast<const float4*>(xr + min(k, K - 4));
         const bool ok = k < K;                     // K % 4 == 0: the float4 is all in or all out
         xa[j][0] = ok ? v.x : 0.f; xa[j][1] = ok ? v.y : 0.f; xa[j][2] = ok ? v.z : 0.f; xa[j][3] = ok ? v.w : 0.f;
@@ -284,11 +298,12 @@ __device__ void head_tile(const HeadArgs& a, const int rt) {
 // row tile's HP / 16 workgroups to finish (a per-row-tile arrival counter,
 // reset by that workgroup for the next step) runs the row tile's head -- no
 // second launch and no grid-wide wait.
-template <bool VEC>
-__global__ __launch_bounds__(512) void graph_mlp_l1h(const float* __restrict__ x, const float* __restrict__ W1,
+template <bool VEC, bool U8 = false>
+__global__ __launch_bounds__(512) void graph_mlp_l1h(const float* __restrict__ x, const uint8_t* __restrict__ xu,
+                                                     const float* __restrict__ W1,
                                                      const float* __restrict__ b1, HeadArgs h, int K, int* cnt) {
   __shared__ int last;
-  l1_tile<VEC>(x, W1, b1, const_cast<float*>(h.a2), h.B, K, h.H, h.HP, h.act);
+  l1_tile<VEC, U8>(x, xu, W1, b1, const_cast<float*>(h.a2), h.B, K, h.H, h.HP, h.act);
   const int nct = h.HP / 16, rt = blockIdx.x / nct;
   if (threadIdx.x < 64) {   // wave 0 stored the tile (write-through): wait for the stores, then arrive
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -310,6 +325,7 @@ __global__ __launch_bounds__(512) void graph_mlp_l1h(const float* __restrict__ x
 constexpr int L3PF = 16;
 struct WgradArgs {
   const float* x;
+  const uint8_t* xu;    // uint8 pixels instead of x (px255), or null
   const float* dz2;
   float* W1;
   float* b1;
@@ -402,7 +418,7 @@ __global__ __launch_bounds__(256) void graph_mlp_wgrad(WgradArgs a) {
   for (int t = 0; t < L3PF; ++t) {
     const int m = (w + 4 * t) * 4 + g;             // batch row supplied by this lane
     const int mc = min(m, B - 1);
-    const float xr = x[(size_t)mc * K + kc];
+    const float xr = a.xu != nullptr ? px255(a.xu[(size_t)mc * K + kc]) : x[(size_t)mc * K + kc];
     const float d = dz2[(size_t)min(m, nbb * 4 - 1) * HP + h0 + r];   // rows >= B are 0
     const bool ok = m < B && (w + 4 * t) < nbb;
     xv[t] = ok ? (kk < K ? xr : (kk == K ? 1.f : 0.f)) : 0.f;
@@ -472,7 +488,9 @@ extern "C" long long dtfk_graph_mlp_part_floats(int B, int H) {
   return (long long)NRT * HP * dtfk::gmlp::CP + 3LL * NRT;
 }
 
-extern "C" hipError_t dtfk_graph_mlp_step(const float* x, const float* ylab, float* W1, float* b1, float* W2,
+// xu (uint8 pixels, K % 4 == 0, 4-byte aligned) replaces x when non-null.
+extern "C" hipError_t dtfk_graph_mlp_step(const float* x, const uint8_t* xu, const float* ylab, float* W1, float* b1,
+                                          float* W2,
                                           float* b2, float* a2buf, float* dz2buf, float* part, float* gW1, float* gb1,
                                           float* gW2, float* gb2, float* metrics, float* host_metrics, void* gstep,
                                           int gstep_kind, const float* lr_ptr, int B, int K, int H, int C, int act,
@@ -482,16 +500,20 @@ extern "C" hipError_t dtfk_graph_mlp_step(const float* x, const float* ylab, flo
     return hipErrorInvalidValue;
   const int HP = (H + 16) & ~15, BP = (B + 15) & ~15;   // >= H + 1 (ones column)
   if (BP * HP > A2_LDS) return hipErrorInvalidValue;
+  if (xu != nullptr && ((K & 3) || (reinterpret_cast<uintptr_t>(xu) & 3))) return hipErrorInvalidValue;
   const bool vec = (K & 3) == 0 && K >= 4 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
   HeadArgs h{a2buf, ylab, W2, b2, dz2buf, part, B, H, HP, C, act, naive};
   // per-row-tile arrival counters behind the partials (zero at allocation, reset by their last arriver)
   int* cnt = reinterpret_cast<int*>(part + (size_t)(BP / 16) * HP * CP + 2 * (BP / 16));
-  if (vec)
-    hipLaunchKernelGGL(graph_mlp_l1h<true>, dim3((BP / 16) * (HP / 16)), dim3(512), 0, stream, x, W1, b1, h, K, cnt);
+  const dim3 g1((BP / 16) * (HP / 16));
+  if (xu != nullptr)
+    hipLaunchKernelGGL((graph_mlp_l1h<true, true>), g1, dim3(512), 0, stream, x, xu, W1, b1, h, K, cnt);
+  else if (vec)
+    hipLaunchKernelGGL((graph_mlp_l1h<true, false>), g1, dim3(512), 0, stream, x, xu, W1, b1, h, K, cnt);
   else
-    hipLaunchKernelGGL(graph_mlp_l1h<false>, dim3((BP / 16) * (HP / 16)), dim3(512), 0, stream, x, W1, b1, h, K, cnt);
+    hipLaunchKernelGGL((graph_mlp_l1h<false, false>), g1, dim3(512), 0, stream, x, xu, W1, b1, h, K, cnt);
   const int tiles = ((K + 1 + 15) / 16) * (HP / 16);
-  WgradArgs wa{x, dz2buf, W1, b1, W2, b2, gW1, gb1, gW2, gb2, part, metrics, host_metrics, gstep, gstep_kind,
+  WgradArgs wa{x, xu, dz2buf, W1, b1, W2, b2, gW1, gb1, gW2, gb2, part, metrics, host_metrics, gstep, gstep_kind,
                lr_ptr, B, K, H, HP, C, sgd, tiles};
   hipLaunchKernelGGL(graph_mlp_wgrad, dim3(tiles + HP / 16), dim3(256), 0, stream, wa);
   return hipGetLastError();

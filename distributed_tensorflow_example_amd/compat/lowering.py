@@ -370,9 +370,15 @@ class MLPStepPlan(_PlanBase):
         opt._steps += 1
         _debug.fault_point(opt._steps, w.rank)
         needs, gs_seed, scalars = self._needs(flat, gs_var, self._gstep)
-        self._cplan.run(fx if fx.flags.c_contiguous else np.ascontiguousarray(fx),
-                        (fy if fy.flags.c_contiguous else np.ascontiguousarray(fy)).reshape(B, C),
-                        float(opt._lr_value()), bool(needs))
+        fy2 = (fy if fy.flags.c_contiguous else np.ascontiguousarray(fy)).reshape(B, C)
+        u8 = getattr(fx, "u8", None)
+        if (u8 is not None and not fx.flags.writeable and u8.shape == fx.shape and u8.dtype == np.uint8
+                and fx.shape[1] % 4 == 0):
+            # data/mnist.py PixelBatch: ship the uint8 source (bit-identical, 4x fewer bytes)
+            self._cplan.run_u8(u8, fy2, float(opt._lr_value()), bool(needs))
+        else:
+            self._cplan.run(fx if fx.flags.c_contiguous else np.ascontiguousarray(fx), fy2,
+                            float(opt._lr_value()), bool(needs))
         # pinned host metrics [loss, accuracy, global_step]: numpy view -> float32
         # scalar copies, or 0-d tensors when another node of the run consumes them
         m = self._hm_np if scalars else self._cplan.host_metrics().clone()

@@ -165,7 +165,31 @@ class DataSet:
                 self._perm = self._rng.permutation(self.num_examples)
         idx = self._perm[self._pos:self._pos + batch_size]
         self._pos += batch_size
-        return self.images_u8[idx].astype(np.float32) / 255.0, one_hot(self.labels_u8[idx])
+        return PixelBatch.of(self.images_u8[idx]), one_hot(self.labels_u8[idx])
+
+
+class PixelBatch(np.ndarray):
+    """A read-only float32 image batch x = u8 / 255 that keeps its uint8 source
+    in `.u8`.  Everywhere it is an ordinary float32 array; the lowered Session
+    step (compat/lowering.py) ships the 4x smaller uint8 batch instead and the
+    kernel converts with the same correctly rounded float32 division, so the
+    step is bit-identical.  Arrays derived from it (slices, arithmetic) carry no
+    source."""
+
+    u8 = None
+
+    @staticmethod
+    def of(u8: np.ndarray) -> "PixelBatch":
+        x = (u8.astype(np.float32) / np.float32(255.0)).view(PixelBatch)
+        x.u8 = np.ascontiguousarray(u8)
+        x.flags.writeable = False
+        return x
+
+    def __array_finalize__(self, obj):
+        self.u8 = None
+
+    def __reduce__(self):   # pickles as a plain float32 array
+        return np.asarray(self).copy().__reduce__()
 
 
 class Datasets:

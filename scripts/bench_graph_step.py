@@ -26,23 +26,36 @@ def main():
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 2000
     rng = np.random.default_rng(0)
     B = 100
-    xs = (rng.integers(0, 256, (64, B, 784)) / 255.0).astype(np.float32)
+    from distributed_tensorflow_example_amd.data.mnist import PixelBatch
+
+    u8s = rng.integers(0, 256, (64, B, 784), dtype=np.uint8)
+    pbs = [PixelBatch.of(u) for u in u8s]           # what the MNIST loader's next_batch returns
+    xs = np.stack([np.asarray(p) for p in pbs])     # the same values as plain float32 arrays
     ys = np.eye(10, dtype=np.float32)[rng.integers(0, 10, (64, B))]
     out = {}
-    for mode in ("1", "0"):
-        os.environ["DTF_GRAPH_LOWERING"] = mode
+    for mode in ("u8", "1", "0"):
+        os.environ["DTF_GRAPH_LOWERING"] = "0" if mode == "0" else "1"
+        feeds = pbs if mode == "u8" else xs
         g = _graph(tf)
         with tf.Session() as sess:
             sess.run(tf.global_variables_initializer())
             fetch = [g["train"], g["ce"], g["gs"]]
             for i in range(20):
-                sess.run(fetch, feed_dict={g["x"]: xs[i % 64], g["y_"]: ys[i % 64]})
+                sess.run(fetch, feed_dict={g["x"]: feeds[i % 64], g["y_"]: ys[i % 64]})
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for i in range(steps):
-                sess.run(fetch, feed_dict={g["x"]: xs[i % 64], g["y_"]: ys[i % 64]})
+                sess.run(fetch, feed_dict={g["x"]: feeds[i % 64], g["y_"]: ys[i % 64]})
             torch.cuda.synchronize()
-            out["lowered" if mode == "1" else "eager"] = (time.perf_counter() - t0) / steps * 1e3
+            out[{"u8": "lowered_u8", "1": "lowered", "0": "eager"}[mode]] = (time.perf_counter() - t0) / steps * 1e3
+            if mode == "u8":
+                cp = L.plan_for(g["train"])._cplan
+                t0 = time.perf_counter()
+                for i in range(1000):
+                    cp.run_u8(u8s[i % 64], ys[i % 64], 0.0, True)
+                out["native_call_u8_us"] = (time.perf_counter() - t0) / 1000 * 1e6
+                out["native_call_u8_split_us"] = {k: round(v, 2) if isinstance(v, float) else v
+                                                  for k, v in cp.timing().items()}
             if mode == "1":
                 plan = L.plan_for(g["train"])
                 assert plan is not None and plan.steps >= steps
@@ -80,6 +93,9 @@ def main():
                       "native_plan_hipgraph": out.get("native_plan_hipgraph"),
                       "native_call_us": round(out.get("native_call_us", 0.0), 2),
                       "native_call_split_us": out.get("native_call_split_us"),
+                      "native_call_u8_us": round(out.get("native_call_u8_us", 0.0), 2),
+                      "native_call_u8_split_us": out.get("native_call_u8_split_us"),
+                      "session_run_ms_per_step_lowered_loader_batches": round(out["lowered_u8"], 4),
                       "session_run_ms_per_step_lowered": round(out["lowered"], 4),
                       "session_run_ms_per_step_eager": round(out["eager"], 4),
                       "lowered_kernels_us_per_step": round(out["kernels_us"], 3), "batch": B, "steps": steps}))

@@ -178,3 +178,57 @@ def test_lr2_graph_lowered_matches_op_by_op(monkeypatch):
     np.testing.assert_allclose(ll, le, rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(wl, we, rtol=1e-5, atol=1e-5)
     assert abs(bl - be) < 1e-5
+
+
+def test_uint8_feed_is_bit_identical(native):
+    """GraphStepPlan.run_u8 (the MNIST loader's uint8 source of a PixelBatch,
+    converted on the GPU with the loader's float32 division) vs run() with the
+    float32 batch: identical metrics and parameters, bit for bit."""
+    from distributed_tensorflow_example_amd.data.mnist import PixelBatch
+
+    K, H, C, B = 784, 100, 10, 100
+    g = torch.Generator(device="cpu").manual_seed(0)
+    p0 = [torch.randn(K, H, generator=g) * 0.05, torch.zeros(H), torch.randn(H, C, generator=g) * 0.1, torch.zeros(C)]
+    pa = [t.cuda().contiguous() for t in p0]
+    pb = [t.cuda().contiguous() for t in p0]
+    plan_f = native.GraphStepPlan(*pa, None, B, 0, True, False)
+    plan_u = native.GraphStepPlan(*pb, None, B, 0, True, False)
+    rng = np.random.default_rng(1)
+    for _ in range(5):
+        u8 = rng.integers(0, 256, (B, K), dtype=np.uint8)
+        x = PixelBatch.of(u8)
+        y = np.eye(C, dtype=np.float32)[rng.integers(0, C, B)]
+        plan_f.run(np.asarray(x), y, 0.5, True)
+        plan_u.run_u8(x.u8, y, 0.5, True)
+        assert np.array_equal(plan_f.host_metrics().numpy(), plan_u.host_metrics().numpy())
+    for a, b in zip(pa, pb):
+        assert torch.equal(a, b)
+
+
+def test_session_uses_uint8_feed_for_loader_batches():
+    """examples/mnist_example.py's graph fed by the MNIST loader: the lowered
+    plan takes the uint8 path and matches a float-fed session bit for bit."""
+    import distributed_tensorflow_example_amd.compat as tf
+    from distributed_tensorflow_example_amd.compat import lowering as L
+    from distributed_tensorflow_example_amd.data.mnist import PixelBatch
+
+    rng = np.random.default_rng(3)
+    batches = [(PixelBatch.of(rng.integers(0, 256, (100, 784), dtype=np.uint8)),
+                np.eye(10, dtype=np.float32)[rng.integers(0, 10, 100)]) for _ in range(3)]
+    finals = []
+    for use_u8 in (True, False):
+        g = _graph(tf)
+        with tf.Session() as sess:
+            sess.run(tf.global_variables_initializer())
+            init = [v.numpy().copy() for v in g["W"]]
+            if finals:
+                for v, w in zip(g["W"], finals[0][0]):
+                    v.load(w, sess)
+            for bx, by in batches:
+                sess.run([g["train"], g["ce"]], feed_dict={g["x"]: bx if use_u8 else np.array(bx), g["y_"]: by})
+            plan = L.plan_for(g["train"])
+            assert plan is not None and plan._cplan.steps() == 3
+            finals.append((init, [v.numpy().copy() for v in g["W"]]))
+        tf.reset_default_graph()
+    for a, b in zip(finals[0][1], finals[1][1]):
+        assert np.array_equal(a, b)

@@ -76,6 +76,25 @@ __device__ __forceinline__ float gelu_grad_f(float z) {
   gelu_cdf_pdf(z, cdf, pdf);
   return fmaf(z, pdf, cdf);
 }
+// gelu'(z) for two values at once: the polynomial / scaling work as packed
+// fp32 (v_pk_fma_f32 / v_pk_mul_f32 on float2), the rcp / exp per value --
+// the fused GELU-backward epilogue is VALU-bound on this math
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 gelu_grad2(f32x2 z) {
+  const f32x2 x = f32x2{fabsf(z.x), fabsf(z.y)} * 0.70710678118654752f;
+  const f32x2 d = x * 0.3275911f + 1.f;
+  const f32x2 t = f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  f32x2 poly = t * 0.5f * 1.061405429f + 0.5f * -1.453152027f;
+  poly = t * poly + 0.5f * 1.421413741f;
+  poly = t * poly + 0.5f * -0.284496736f;
+  poly = t * poly + 0.5f * 0.254829592f;
+  poly = t * poly;                                   // 0.5 * (1 - erf(|z| / sqrt2)) / exp(-z^2 / 2)
+  const f32x2 a = z * z * -0.5f;
+  const f32x2 e = f32x2{__expf(a.x), __expf(a.y)};
+  const f32x2 tail = poly * e;
+  const f32x2 cdf = f32x2{z.x >= 0.f ? 1.f - tail.x : tail.x, z.y >= 0.f ? 1.f - tail.y : tail.y};
+  return z * (e * 0.3989422804014327f) + cdf;
+}
 __device__ __forceinline__ float apply_act(float z, int act) { return act == ACT_NONE ? z : apply_act_slow(z, act); }
 
 // ---- LDS images ----------------------------------------------------------
@@ -650,20 +669,27 @@ __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A,
 #pragma unroll
       for (int q = 0; q < 8; ++q) { ab[q] = bias != nullptr ? bias[n0 + wc * WN + c8 + q] : 0.f; cs[q] = 0.f; }
     }
+    typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+    // DG: the saved pre-activation of BOTH halves requested up front (16 loads
+    // in flight; the operand-fragment registers are free after the loop)
+    u32x4 apre[DG ? 16 : 1];
+    if constexpr (DG) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        apre[q] = *reinterpret_cast<const u32x4*>(
+            aux + (size_t)(m0 + wr * 128 + (q >> 3) * 64 + (q & 7) * 8 + rsub) * ldc + n0 + wc * WN + c8);
+    }
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
       // beta != 0: this half's C chunks are loaded first, all at once (the
       // operand-fragment registers are free after the loop), so their latency
       // hides under the LDS round trip instead of one load per store
-      typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
       u32x4 cpre[OBF ? 8 : 16];
-      if (DG || (beta != 0.f && rb_on)) {
+      if (!DG && beta != 0.f && rb_on) {
 #pragma unroll
         for (int it = 0; it < 8; ++it) {
           const size_t o = (size_t)(m0 + wr * 128 + half * 64 + it * 8 + rsub) * ldc + n0 + wc * WN + c8;
-          if constexpr (DG) {   // the saved pre-activation instead of C (beta is 0)
-            cpre[it] = *reinterpret_cast<const u32x4*>(aux + o);
-          } else if constexpr (OBF) {
+          if constexpr (OBF) {
             cpre[it] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const uint16_t*>(C) + o);
           } else {
             cpre[2 * it] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const float*>(C) + o);
@@ -692,8 +718,11 @@ __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A,
         if constexpr (DG) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            z[2 * q] *= gelu_grad_f(bf2f((uint16_t)(cpre[it][q] & 0xffff)) + ab[2 * q]);
-            z[2 * q + 1] *= gelu_grad_f(bf2f((uint16_t)(cpre[it][q] >> 16)) + ab[2 * q + 1]);
+            const uint32_t u2 = apre[half * 8 + it][q];
+            const f32x2 g2 = gelu_grad2(f32x2{bf2f((uint16_t)(u2 & 0xffff)), bf2f((uint16_t)(u2 >> 16))} +
+                                        f32x2{ab[2 * q], ab[2 * q + 1]});
+            z[2 * q] *= g2.x;
+            z[2 * q + 1] *= g2.y;
           }
 #pragma unroll
           for (int q = 0; q < 8; ++q) cs[q] += z[q];

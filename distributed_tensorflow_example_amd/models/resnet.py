@@ -39,12 +39,19 @@ class Bottleneck(nn.Module):
         self.down_conv = ShadowConv2d(cin, cout, 1, stride, bias=False) if down else None
         self.down_bn = FusedBatchNorm2d(cout) if down else None
 
+    def _fold_ok(self, x) -> bool:
+        """The fold needs conv1 on its bf16-shadow path, the only one that takes the
+        slot: a gradient bn3 deposited for any other path would be lost.  (A bn3
+        off its fused path ignores the slot and returns the gradient itself.)"""
+        w16 = getattr(self.conv1.weight, "_shadow", None)
+        return (self.fold_residual_grad and self.down_conv is None and self.training and x.is_cuda
+                and w16 is not None and x.dtype == w16.dtype and self.conv1.bias is None)
+
     def forward(self, x):
         idt = self.down_bn(self.down_conv(x)) if self.down_conv is not None else x
         # identity path: bn3's residual gradient is accumulated by conv1's input-
         # gradient GEMM (beta = 1) instead of autograd adding the two branches
-        slot = (GradSlot() if self.fold_residual_grad and self.down_conv is None and x.is_cuda and self.training
-                else None)
+        slot = GradSlot() if self._fold_ok(x) else None
         y = self.bn1(self.conv1(x, grad_slot=slot), relu=True)   # BN + ReLU: one fused pass
         y = self.bn2(self.conv2(y), relu=True)
         return self.bn3(self.conv3(y), residual=idt, relu=True, residual_slot=slot)   # BN + residual add + ReLU

@@ -105,3 +105,23 @@ def test_bottleneck_residual_grad_fold(native, dx_engine):
     # one bf16 rounding of (dy W + dres) vs two (dy W, then the add)
     torch.testing.assert_close(a, b, rtol=1e-2, atol=1e-2 * b.abs().max().item())
     torch.testing.assert_close(wa, wb)
+
+
+def test_bottleneck_fold_off_without_shadows(native):
+    """Without bf16 shadows conv1 runs as plain nn.Conv2d and cannot take the
+    residual gradient, so no slot is created: gradients match the unfolded block."""
+    from distributed_tensorflow_example_amd.models.resnet import Bottleneck
+
+    torch.manual_seed(4)
+    blk = Bottleneck(64, 16).cuda().to(memory_format=torch.channels_last).train()
+    x = torch.randn(2, 64, 8, 8, device="cuda").contiguous(memory_format=torch.channels_last)
+    assert not blk._fold_ok(x)
+    xr = x.clone().requires_grad_(True)
+    blk(xr).float().sum().backward()
+    grads = xr.grad.clone()
+    blk.fold_residual_grad = False
+    xr2 = x.clone().requires_grad_(True)
+    blk.zero_grad(set_to_none=True)
+    blk(xr2).float().sum().backward()
+    blk.fold_residual_grad = True
+    assert torch.equal(grads, xr2.grad)

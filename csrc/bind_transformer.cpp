@@ -35,7 +35,7 @@ hipError_t dtfk_attn_fwd(const void* qkv, const float* bias, const float* mask, 
                          int NH, float scale, float p, unsigned long long seed, hipStream_t st);
 hipError_t dtfk_attn_bwd(const void* qkv, const float* bias, const float* mask, const void* ctx, const void* dctx,
                          const float* lse, float* Dbuf, void* dqkv, int B, int S, int NH, float scale, float p,
-                         unsigned long long seed, hipStream_t st);
+                         unsigned long long seed, float* bpart, hipStream_t st);
 }
 
 namespace dtf {
@@ -219,9 +219,12 @@ void attn_fwd(at::Tensor qkv, c10::optional<at::Tensor> bias, c10::optional<at::
      "attn_fwd");
 }
 
+// dbias (optional, with bpart [B * S / 16, 3 * NH * 64] fp32 scratch): the qkv
+// bias gradient = column sums of dqkv, from per-wave partial sums the backward
+// kernels write (no pass over dqkv); accumulate: dbias +=.
 void attn_bwd(at::Tensor qkv, c10::optional<at::Tensor> bias, c10::optional<at::Tensor> mask, at::Tensor ctx,
               at::Tensor dctx, at::Tensor lse, at::Tensor Dbuf, at::Tensor dqkv, int64_t NH, double scale, double p,
-              int64_t seed) {
+              int64_t seed, c10::optional<at::Tensor> bpart, c10::optional<at::Tensor> dbias, bool accumulate) {
   attn_check(qkv, bias, mask, NH);
   const int64_t B = qkv.size(0), S = qkv.size(1);
   req(ctx, at::kBFloat16, "ctx"); req(dctx, at::kBFloat16, "dctx"); req(dqkv, at::kBFloat16, "dqkv");
@@ -229,16 +232,30 @@ void attn_bwd(at::Tensor qkv, c10::optional<at::Tensor> bias, c10::optional<at::
   if (ctx.numel() != B * S * NH * 64 || dctx.numel() != ctx.numel() || dqkv.numel() != qkv.numel() ||
       lse.numel() != B * NH * S || Dbuf.numel() != lse.numel())
     throw std::runtime_error("attn_bwd: sizes");
+  const int64_t H3 = 3 * NH * 64, P = B * S / 16;
+  if (bpart.has_value() != dbias.has_value()) throw std::runtime_error("attn_bwd: bpart and dbias go together");
+  if (bpart.has_value()) {
+    req(*bpart, at::kFloat, "bpart"); req(*dbias, at::kFloat, "dbias");
+    if (bpart->numel() < P * H3 || dbias->numel() != H3 || !dbias->is_contiguous())
+      throw std::runtime_error("attn_bwd: bpart needs B*S/16 x 3*NH*64 floats, dbias 3*NH*64");
+  }
   ck(dtfk_attn_bwd(qkv.data_ptr(), optf(bias), optf(mask), ctx.data_ptr(), dctx.data_ptr(), lse.data_ptr<float>(),
                    Dbuf.data_ptr<float>(), dqkv.data_ptr(), (int)B, (int)S, (int)NH, (float)scale, (float)p,
-                   (unsigned long long)seed, cs()),
+                   (unsigned long long)seed, bpart.has_value() ? bpart->data_ptr<float>() : nullptr, cs()),
      "attn_bwd");
+  if (bpart.has_value()) {
+    const float* pp[1] = {bpart->data_ptr<float>()};
+    float* po[1] = {dbias->data_ptr<float>()};
+    ck(dtfk_colsum_partials_multi(pp, po, 1, (int)P, (int)H3, accumulate ? 1 : 0, cs()), "attn_bwd dbias");
+  }
 }
 
 void init_transformer(pybind11::module& m) {
   m.def("attn_supported", [](int64_t S, int64_t d) { return dtfk_attn_supported((int)S, (int)d) != 0; });
   m.def("attn_fwd", &attn_fwd);
-  m.def("attn_bwd", &attn_bwd);
+  m.def("attn_bwd", &attn_bwd, py::arg("qkv"), py::arg("bias"), py::arg("mask"), py::arg("ctx"), py::arg("dctx"),
+        py::arg("lse"), py::arg("Dbuf"), py::arg("dqkv"), py::arg("NH"), py::arg("scale"), py::arg("p"),
+        py::arg("seed"), py::arg("bpart") = py::none(), py::arg("dbias") = py::none(), py::arg("accumulate") = false);
   m.def("bdrln_fwd", &bdrln_fwd);
   m.def("ln_fwd_f32in", &ln_fwd_f32in);
   m.def("ln_bwd", &ln_bwd, py::arg("dy"), py::arg("s"), py::arg("mean"), py::arg("rstd"), py::arg("gamma"),

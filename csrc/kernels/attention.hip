@@ -220,7 +220,8 @@ __global__ __launch_bounds__(512) void attn_bwd_dq(const uint16_t* __restrict__ 
                                                    const float* __restrict__ mask, const uint16_t* __restrict__ ctx,
                                                    const uint16_t* __restrict__ dctx, const float* __restrict__ lse,
                                                    float* __restrict__ Dbuf, uint16_t* __restrict__ dqkv, int NH,
-                                                   float scale, uint32_t thresh, float inv_keep, uint64_t seed) {
+                                                   float scale, uint32_t thresh, float inv_keep, uint64_t seed,
+                                                   float* __restrict__ bpart) {
   constexpr int S = 32 * NKB, VT = S + 8;
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
   uint16_t* Ks = lds;                    // [S][KP]
@@ -314,6 +315,28 @@ __global__ __launch_bounds__(512) void attn_bwd_dq(const uint16_t* __restrict__ 
   for (int u = 0; u < 4; ++u)
     *reinterpret_cast<uint2*>(dq + 16 * u + 4 * g) =
         uint2{pack2bf(acc[u][0] * scale, acc[u][1] * scale), pack2bf(acc[u][2] * scale, acc[u][3] * scale)};
+  if (bpart != nullptr) {
+    // q-bias gradient partials: this wave's 16 queries summed per dimension
+    // (lanes c = 0..15 of a group hold the 16 queries) -> bpart[b * S/16 + wave row][h * 64 + d]
+    float cs[16];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float v = acc[u][j] * scale;
+        v += __shfl_xor(v, 1, 64);
+        v += __shfl_xor(v, 2, 64);
+        v += __shfl_xor(v, 4, 64);
+        v += __shfl_xor(v, 8, 64);
+        cs[4 * u + j] = v;
+      }
+    if (c == 0) {
+      float* pr = bpart + ((long long)b * (S / 16) + blockIdx.x * 8 + w) * RS + h * D;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        *reinterpret_cast<float4*>(pr + 16 * u + 4 * g) = float4{cs[4 * u], cs[4 * u + 1], cs[4 * u + 2], cs[4 * u + 3]};
+    }
+  }
 }
 
 template <int NKB>
@@ -321,7 +344,7 @@ __global__ __launch_bounds__(512) void attn_bwd_dkv(const uint16_t* __restrict__
                                                     const float* __restrict__ mask, const uint16_t* __restrict__ dctx,
                                                     const float* __restrict__ lse, const float* __restrict__ Dbuf,
                                                     uint16_t* __restrict__ dqkv, int NH, float scale, uint32_t thresh,
-                                                    float inv_keep, uint64_t seed) {
+                                                    float inv_keep, uint64_t seed, float* __restrict__ bpart) {
   constexpr int S = 32 * NKB, VT = S + 8;
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
   uint16_t* Qs = lds;                          // [S][KP]
@@ -421,6 +444,24 @@ __global__ __launch_bounds__(512) void attn_bwd_dkv(const uint16_t* __restrict__
       rowp[2 * NH * D + 16 * u] = f2bf(dv[u][i]);
     }
   }
+  if (bpart != nullptr) {
+    // k / v-bias gradient partials: this wave's 16 keys (4 per lane x the 4 lane
+    // groups g) summed per dimension d = 16u + c
+    float* pr = bpart + ((long long)b * (S / 16) + k0 / 16) * RS + h * D + c;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      float sk = (dk[u][0] + dk[u][1]) + (dk[u][2] + dk[u][3]);
+      float sv = (dv[u][0] + dv[u][1]) + (dv[u][2] + dv[u][3]);
+      sk += __shfl_xor(sk, 16, 64);
+      sk += __shfl_xor(sk, 32, 64);
+      sv += __shfl_xor(sv, 16, 64);
+      sv += __shfl_xor(sv, 32, 64);
+      if (g == 0) {
+        pr[NH * D + 16 * u] = sk * scale;
+        pr[2 * NH * D + 16 * u] = sv;
+      }
+    }
+  }
 }
 
 }  // namespace attn
@@ -479,7 +520,9 @@ hipError_t dtfk_attn_fwd(const void* qkv, const float* bias, const float* mask, 
 // dqkv [B, S, 3, NH, 64] is fully written; Dbuf [B, NH, S] fp32 scratch
 hipError_t dtfk_attn_bwd(const void* qkv, const float* bias, const float* mask, const void* ctx, const void* dctx,
                          const float* lse, float* Dbuf, void* dqkv, int B, int S, int NH, float scale, float p,
-                         unsigned long long seed, hipStream_t st) {
+                         unsigned long long seed, float* bpart, hipStream_t st) {
+  // bpart (optional): [B * S / 16, 3 * NH * 64] fp32 partial column sums of dqkv
+  // (the qkv bias gradient before its colsum_partials reduction)
   if (!dtfk_attn_supported(S, D)) return hipErrorInvalidValue;
   const dim3 grid((S + 127) / 128, NH, B);
   const float ik = p > 0.f ? 1.f / (1.f - p) : 1.f;
@@ -494,9 +537,9 @@ hipError_t dtfk_attn_bwd(const void* qkv, const float* bias, const float* mask, 
     if (e2 != hipSuccess) return e2;                                                                               \
     hipLaunchKernelGGL(attn_bwd_dq<N>, grid, dim3(512), lds_q, st, (const uint16_t*)qkv, bias, mask,               \
                        (const uint16_t*)ctx, (const uint16_t*)dctx, lse, Dbuf, (uint16_t*)dqkv, NH, scale, th, ik, \
-                       (uint64_t)seed);                                                                            \
+                       (uint64_t)seed, bpart);                                                                     \
     hipLaunchKernelGGL(attn_bwd_dkv<N>, grid, dim3(512), lds_kv, st, (const uint16_t*)qkv, bias, mask,             \
-                       (const uint16_t*)dctx, lse, Dbuf, (uint16_t*)dqkv, NH, scale, th, ik, (uint64_t)seed);      \
+                       (const uint16_t*)dctx, lse, Dbuf, (uint16_t*)dqkv, NH, scale, th, ik, (uint64_t)seed, bpart); \
   }
   DTFK_ATTN_DISPATCH(S, L_BWD)
 #undef L_BWD

@@ -26,6 +26,11 @@ _BASE_SEED = 0x5EED
 _FAST_HASH = -(1 << 63) if os.environ.get("DTF_DROPOUT_HASH", "32") != "64" else 0
 
 
+# qkv bias gradient from the attention backward kernels' own partial sums (1), or
+# a separate column-sum pass over dqkv (0, A/B)
+_ATTN_BIAS_PARTIALS = os.environ.get("DTF_ATTN_BIAS_PARTIALS", "1") != "0"
+
+
 def next_seed() -> int:
     return ((_BASE_SEED * 1000003 + next(_seed_counter) * 0x9E3779B1) & ((1 << 62) - 1)) + _FAST_HASH
 
@@ -295,20 +300,36 @@ class _FusedAttention(torch.autograd.Function):
         qkv, bias, mask, out, lse = ctx.saved_tensors
         dqkv = torch.empty_like(qkv)
         Dbuf = torch.empty_like(lse)
-        C.attn_bwd(qkv, bias if ctx.has_bias else None, mask if ctx.has_mask else None, out,
-                   dout.to(torch.bfloat16).contiguous(), lse, Dbuf, dqkv, ctx.nh, ctx.scale, ctx.p, ctx.seed)
-        dbias = None
-        if ctx.has_bias:
+        dbias = bpart = None
+        sink = False
+        if ctx.has_bias and not _ATTN_BIAS_PARTIALS:   # A/B only: column sums re-read from dqkv
+            C.attn_bwd(qkv, bias, mask if ctx.has_mask else None, out, dout.to(torch.bfloat16).contiguous(), lse,
+                       Dbuf, dqkv, ctx.nh, ctx.scale, ctx.p, ctx.seed)
             H3 = dqkv.shape[-1]
-            N = dqkv.numel() // H3
-            part = torch.empty(max(1, min(256, N // 64)) * H3, dtype=torch.float32, device=dqkv.device)
+            part = torch.empty(max(1, min(256, dqkv.numel() // H3 // 64)) * H3, dtype=torch.float32,
+                               device=dqkv.device)
             pb = ctx.bias_param
             sink = grad_sink.all_enabled(pb)
             dbias = grad_sink.target(pb) if sink else torch.empty(H3, dtype=torch.float32, device=dqkv.device)
-            C.colsum_bf16(dqkv.view(-1, H3), part, dbias, accumulate=sink)   # bias grad = column sums of dqkv
+            C.colsum_bf16(dqkv.view(-1, H3), part, dbias, accumulate=sink)
             if sink:
                 grad_sink.done(pb)
                 dbias = None
+            return dqkv, dbias, None, None, None, None
+        if ctx.has_bias:
+            # bias grad = column sums of dqkv: per-wave partials written by the
+            # backward kernels themselves, reduced by one small pass (no re-read of dqkv)
+            B, S, H3 = qkv.shape
+            bpart = torch.empty(B * S // 16 * H3, dtype=torch.float32, device=qkv.device)
+            pb = ctx.bias_param
+            sink = grad_sink.all_enabled(pb)
+            dbias = grad_sink.target(pb) if sink else torch.empty(H3, dtype=torch.float32, device=qkv.device)
+        C.attn_bwd(qkv, bias if ctx.has_bias else None, mask if ctx.has_mask else None, out,
+                   dout.to(torch.bfloat16).contiguous(), lse, Dbuf, dqkv, ctx.nh, ctx.scale, ctx.p, ctx.seed,
+                   bpart, dbias, accumulate=sink)
+        if sink:
+            grad_sink.done(ctx.bias_param)
+            dbias = None
         return dqkv, dbias, None, None, None, None
 
 

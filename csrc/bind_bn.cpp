@@ -19,6 +19,8 @@ hipError_t dtfk_bn_bwd(const void* dy, const void* x, const void* res, const flo
                        const float* invstd, const float* scale, const float* shift, float* part, float* coef,
                        void* dx, void* dres, float* dgamma, float* dbeta, int M, int C, int relu, int accum,
                        int write_g, hipStream_t st);
+hipError_t dtfk_strided_add(void* full, const void* comp, int N, int H, int W, int C, int Ho, int Wo, int s,
+                            hipStream_t st);
 hipError_t dtfk_maxpool_fwd(const void* x, void* y, void* idx, int N, int H, int W, int C, int Ho, int Wo, int k,
                             int s, int p, hipStream_t st);
 hipError_t dtfk_maxpool_bwd(const void* dy, const void* idx, void* dx, int N, int H, int W, int C, int Ho, int Wo,
@@ -130,7 +132,20 @@ void bn_bwd(at::Tensor dy, at::Tensor x, c10::optional<at::Tensor> res, at::Tens
      "bn_bwd");
 }
 
+// full[:, :, s*i, s*j] += comp (channels_last bf16 [N, C, H, W] and [N, C, Ho, Wo])
+void strided_add(at::Tensor full, at::Tensor comp, int64_t s) {
+  for (const at::Tensor* t : {&full, &comp})
+    if (!t->is_cuda() || t->scalar_type() != at::kBFloat16 || t->dim() != 4 ||
+        !t->is_contiguous(at::MemoryFormat::ChannelsLast))
+      throw std::runtime_error("strided_add: channels_last bf16 4-D CUDA tensors");
+  if (full.size(0) != comp.size(0) || full.size(1) != comp.size(1)) throw std::runtime_error("strided_add: N / C differ");
+  ck(dtfk_strided_add(full.data_ptr(), comp.data_ptr(), (int)full.size(0), (int)full.size(2), (int)full.size(3),
+                      (int)full.size(1), (int)comp.size(2), (int)comp.size(3), (int)s, cs()),
+     "strided_add");
+}
+
 void init_bn(pybind11::module& m) {
+  m.def("strided_add", &strided_add);
   m.def("bn_partial_rows", &bn_partial_rows);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);

@@ -110,6 +110,30 @@ __global__ __launch_bounds__(256) void maxpool_bwd(const uint16_t* __restrict__ 
   *reinterpret_cast<u32x4*>(dx + (((size_t)n * H + h) * W + w) * C + 8 * c8) = o;
 }
 
+// full[n, s*i, s*j, :] += comp[n, i, j, :] (NHWC bf16, fp32 add, one rounding):
+// the input gradient of a 1x1 / stride-s / unpadded convolution (a GEMM over
+// the strided pixels) folded into the other branch's full-size gradient of the
+// same input, instead of a zero-filled full-size dx and an add pass over it.
+__global__ __launch_bounds__(256) void strided_add(uint16_t* __restrict__ full, const uint16_t* __restrict__ comp,
+                                                   int N, int H, int W, int C, int Ho, int Wo, int s) {
+  const int C8 = C >> 3;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)N * Ho * Wo * C8) return;
+  const int c8 = (int)(i % C8);
+  long long r = i / C8;
+  const int wo = (int)(r % Wo);
+  r /= Wo;
+  const int ho = (int)(r % Ho);
+  const int n = (int)(r / Ho);
+  uint16_t* f = full + (((size_t)n * H + (size_t)ho * s) * W + (size_t)wo * s) * C + 8 * c8;
+  const u32x4 a = *reinterpret_cast<const u32x4*>(f);
+  const u32x4 b = *reinterpret_cast<const u32x4*>(comp + (size_t)i * 8);
+  u32x4 o;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) o[q] = pack2bf(lo16(a[q]) + lo16(b[q]), hi16(a[q]) + hi16(b[q]));
+  *reinterpret_cast<u32x4*>(f) = o;
+}
+
 }  // namespace pool
 }  // namespace dtfk
 
@@ -128,5 +152,15 @@ extern "C" hipError_t dtfk_maxpool_bwd(const void* dy, const void* idx, void* dx
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(dtfk::pool::maxpool_bwd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
                      (const uint16_t*)dy, (const uint8_t*)idx, (uint16_t*)dx, N, H, W, C, Ho, Wo, k, s, p);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t dtfk_strided_add(void* full, const void* comp, int N, int H, int W, int C, int Ho, int Wo, int s,
+                                       hipStream_t st) {
+  if (C % 8 || s < 1 || (long long)(Ho - 1) * s >= H || (long long)(Wo - 1) * s >= W) return hipErrorInvalidValue;
+  const long long n = (long long)N * Ho * Wo * (C / 8);
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(dtfk::pool::strided_add, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, (uint16_t*)full,
+                     (const uint16_t*)comp, N, H, W, C, Ho, Wo, s);
   return hipGetLastError();
 }

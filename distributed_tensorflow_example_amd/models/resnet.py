@@ -16,7 +16,7 @@ import torch.nn.functional as F
 
 from .. import ops
 from ..ops.bn import FusedBatchNorm2d
-from ..ops.conv import ShadowConv2d, attach_shadows as _attach_conv_shadows
+from ..ops.conv import ShadowConv2d, XGradShare, attach_shadows as _attach_conv_shadows
 from ..ops.pool import max_pool2d
 from ..ops.transformer import GradSlot
 
@@ -25,6 +25,8 @@ class Bottleneck(nn.Module):
     expansion = 4
     # identity blocks: conv1's dx GEMM accumulates the residual gradient (DTF_RES_FOLD=0: autograd adds)
     fold_residual_grad = os.environ.get("DTF_RES_FOLD", "1") != "0"
+    # downsampling blocks: conv1 / projection input gradients folded into one tensor (DTF_X_SHARE=0: autograd adds)
+    share_input_grad = os.environ.get("DTF_X_SHARE", "1") != "0"
 
     def __init__(self, cin, width, stride=1, down=False):
         super().__init__()
@@ -43,16 +45,25 @@ class Bottleneck(nn.Module):
         """The fold needs conv1 on its bf16-shadow path, the only one that takes the
         slot: a gradient bn3 deposited for any other path would be lost.  (A bn3
         off its fused path ignores the slot and returns the gradient itself.)"""
-        w16 = getattr(self.conv1.weight, "_shadow", None)
-        return (self.fold_residual_grad and self.down_conv is None and self.training and x.is_cuda
-                and w16 is not None and x.dtype == w16.dtype and self.conv1.bias is None)
+        return (self.fold_residual_grad and self.down_conv is None and self.training
+                and self.conv1.on_shadow_path(x))
+
+    def _share_ok(self, x) -> bool:
+        """Downsampling blocks: conv1 and the projection both read x and both take
+        the shared input-gradient fold (each must be on its shadow path)."""
+        return (self.share_input_grad and self.down_conv is not None and self.training and x.requires_grad
+                and self.conv1.on_shadow_path(x) and self.down_conv.on_shadow_path(x))
 
     def forward(self, x):
-        idt = self.down_bn(self.down_conv(x)) if self.down_conv is not None else x
+        # downsampling blocks: the projection's and conv1's input gradients meet
+        # in one tensor (GEMM beta = 1, or the stride-2 projection's strided
+        # pixels added in place) instead of MIOpen's zero-filled dx + an add
+        share = XGradShare() if self._share_ok(x) else None
+        idt = self.down_bn(self.down_conv(x, share=share)) if self.down_conv is not None else x
         # identity path: bn3's residual gradient is accumulated by conv1's input-
         # gradient GEMM (beta = 1) instead of autograd adding the two branches
         slot = GradSlot() if self._fold_ok(x) else None
-        y = self.bn1(self.conv1(x, grad_slot=slot), relu=True)   # BN + ReLU: one fused pass
+        y = self.bn1(self.conv1(x, grad_slot=slot, share=share), relu=True)   # BN + ReLU: one fused pass
         y = self.bn2(self.conv2(y), relu=True)
         return self.bn3(self.conv3(y), residual=idt, relu=True, residual_slot=slot)   # BN + residual add + ReLU
 

@@ -147,13 +147,39 @@ def choices() -> dict:
     return {k: (v, _timings.get(k)) for k, v in _choice.items()}
 
 
+class XGradShare:
+    """Two 1x1 convolutions reading the same input (a downsampling bottleneck's
+    conv1 and projection): whichever backward runs first deposits its input
+    gradient, the second folds its own in and returns the sum -- a GEMM with
+    beta = 1, or, for the stride-2 projection, its compact gradient added onto
+    the strided pixels (strided_add), instead of a zero-filled full-size dx from
+    MIOpen plus an autograd add."""
+    __slots__ = ("part",)
+
+    def __init__(self):
+        self.part = None   # ("full", dx) or ("strided", compact dx, stride)
+
+    def take(self):
+        p, self.part = self.part, None
+        return p
+
+
+def _strided_ok(x, w16, stride, padding, dilation, groups) -> bool:
+    """A 1x1 / stride-s / unpadded conv whose input gradient is a GEMM over the
+    strided pixels."""
+    return (w16.shape[2] == 1 and w16.shape[3] == 1 and tuple(padding) == (0, 0) and groups == 1
+            and stride[0] == stride[1] and stride[0] > 1 and x.is_cuda and x.dtype == torch.bfloat16
+            and x.is_contiguous(memory_format=torch.channels_last) and x.shape[1] % 8 == 0)
+
+
 class _ShadowConv(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, w16, stride, padding, dilation, groups, slot=None):
+    def forward(ctx, x, w, w16, stride, padding, dilation, groups, slot=None, share=None):
         ctx.save_for_backward(x, w16)
         ctx.conf = (stride, padding, dilation, groups)
         ctx.w = w
         ctx.slot = slot
+        ctx.share = share
         ctx.gemm = _gemm_ok(x, w16, stride, padding, dilation, groups)
         if ctx.gemm:
             eng = _fwd_engine(x, w16)
@@ -170,21 +196,41 @@ class _ShadowConv(torch.autograd.Function):
         dy = dy.to(w16.dtype)
         w = ctx.w
         gemm = ctx.gemm and dy.is_contiguous(memory_format=torch.channels_last)
+        share = ctx.share if need_x else None
+        other = share.take() if share is not None else None    # what the pair's first backward deposited
+        first = share is not None and other is None
+        strided = (share is not None and dy.is_contiguous(memory_format=torch.channels_last)
+                   and _strided_ok(x, w16, stride, padding, dilation, groups))
         dx_eng = _dx_engine(dy, x, w16) if gemm and need_x else "miopen"
         dw_eng = _dw_engine(dy, x, w16) if gemm and need_w else "miopen"
         # MIOpen's share: one convolution_backward call for whatever stays on it
-        mx, mw = need_x and dx_eng == "miopen", need_w and dw_eng == "miopen"
+        mx, mw = need_x and dx_eng == "miopen" and not strided, need_w and dw_eng == "miopen"
         dx = dw = None
         if mx or mw:
             dx, dw, _ = torch.ops.aten.convolution_backward(dy, x, w16, None, stride, padding, dilation, False,
                                                             [0, 0], groups, [mx, mw, False])
         extra = ctx.slot.take() if ctx.slot is not None else None   # a residual branch's gradient of x
-        if need_x and not mx:
+        if other is not None and other[0] == "full":    # the pair's full-size gradient of x
+            extra = other[1] if extra is None else extra.add_(other[1])
+        if strided:
+            # the input gradient lives on the strided pixels only: [N*Ho*Wo, Cin] = dy W
+            comp = _cl_empty(x.shape[0], x.shape[1], dy.shape[2], dy.shape[3], dy)
+            torch.mm(_rows(dy), w16.view(w16.shape[0], w16.shape[1]), out=_rows(comp))
+            if extra is None:            # first of the pair: the other conv adds its gradient onto this later
+                share.part = ("strided", comp, stride[0])
+            else:
+                _C().strided_add(extra, comp, stride[0])
+                dx = extra
+        elif need_x and not mx:
             dx = _dx_gemm(dx_eng, dy, w16, x.shape, into=extra)
         elif need_x and extra is not None:
             dx = dx + extra
+        if other is not None and other[0] == "strided":
+            _C().strided_add(dx, other[1], other[2])
+        if first and not strided:        # first of the pair: hand the full gradient to the second
+            share.part, dx = ("full", dx), None
         if not need_w:
-            return dx, None, None, None, None, None, None, None
+            return dx, None, None, None, None, None, None, None, None
         sink = grad_sink.enabled(w) and (w.grad is None or w.grad.is_contiguous())
         if not mw:
             from . import big_gemm
@@ -192,32 +238,41 @@ class _ShadowConv(torch.autograd.Function):
                 g = grad_sink.target(w)
                 big_gemm.linear_dw(_rows(dy), _rows(x), into=g.view(g.shape[0], g.shape[1]))
                 grad_sink.done(w)
-                return dx, None, None, None, None, None, None, None
+                return dx, None, None, None, None, None, None, None, None
             return (dx, big_gemm.linear_dw(_rows(dy), _rows(x)).view(w.shape).to(w.dtype), None, None, None, None,
-                    None, None)
+                    None, None, None)
         if sink:
             grad_sink.target(w).add_(dw)
             grad_sink.done(w)
-            return dx, None, None, None, None, None, None, None
-        return dx, dw.to(w.dtype), None, None, None, None, None, None
+            return dx, None, None, None, None, None, None, None, None
+        return dx, dw.to(w.dtype), None, None, None, None, None, None, None
 
 
 class ShadowConv2d(torch.nn.Conv2d):
     """nn.Conv2d that computes with `weight._shadow` when one is attached."""
 
-    def forward(self, x, grad_slot=None):
+    def forward(self, x, grad_slot=None, share=None):
         """`grad_slot` (ops.transformer.GradSlot): another branch's gradient of x,
         deposited by its producer during backward, is accumulated into this
-        conv's input gradient (the residual add of a bottleneck's identity path)."""
+        conv's input gradient (the residual add of a bottleneck's identity path).
+        `share` (XGradShare): this conv and one other read the same x and fold
+        their input gradients into one tensor.  Both only take effect on the
+        shadow path, which the caller must ensure (`on_shadow_path`)."""
+        if self.on_shadow_path(x):
+            return _ShadowConv.apply(x, self.weight, self.weight._shadow, self.stride, self.padding, self.dilation,
+                                     self.groups, grad_slot, share)
         w16 = getattr(self.weight, "_shadow", None)
         if (w16 is not None and x.is_cuda and self.bias is None and self.padding_mode == "zeros"
                 and isinstance(self.padding, tuple)):
-            if x.dtype != w16.dtype:
-                x = x.to(w16.dtype)
-                grad_slot = None     # the cast node, not x, would receive this conv's gradient
-            return _ShadowConv.apply(x, self.weight, w16, self.stride, self.padding, self.dilation, self.groups,
-                                     grad_slot)
+            return _ShadowConv.apply(x.to(w16.dtype), self.weight, w16, self.stride, self.padding, self.dilation,
+                                     self.groups)
         return super().forward(x)
+
+    def on_shadow_path(self, x) -> bool:
+        """x goes straight into _ShadowConv (the path that honours grad_slot / share)."""
+        w16 = getattr(self.weight, "_shadow", None)
+        return (w16 is not None and x.is_cuda and x.dtype == w16.dtype and self.bias is None
+                and self.padding_mode == "zeros" and isinstance(self.padding, tuple))
 
 
 def attach_shadows(module: torch.nn.Module, optimizer=None, dtype=torch.bfloat16):

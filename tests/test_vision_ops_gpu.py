@@ -125,3 +125,43 @@ def test_bottleneck_fold_off_without_shadows(native):
     blk(xr2).float().sum().backward()
     blk.fold_residual_grad = True
     assert torch.equal(grads, xr2.grad)
+
+
+@pytest.mark.parametrize("stride,cin,hw", [(2, 256, 28), (1, 64, 28), (2, 512, 15)])
+def test_downsample_block_input_grad_share(native, stride, cin, hw):
+    """A downsampling bottleneck's conv1 / projection input gradients folded into
+    one tensor (ops/conv.py XGradShare: GEMM beta = 1, or the stride-2
+    projection's strided pixels via strided_add) equal autograd's sum."""
+    from distributed_tensorflow_example_amd.models.resnet import Bottleneck
+    from distributed_tensorflow_example_amd.ops import conv
+
+    torch.manual_seed(5)
+    blk = Bottleneck(cin, 64, stride=stride, down=True).cuda().to(memory_format=torch.channels_last).train()
+    conv.attach_shadows(blk)
+    x0 = torch.randn(4, cin, hw, hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    grads = []
+    for fold in (True, False):
+        blk.share_input_grad = fold
+        blk.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        assert blk._share_ok(x) == fold
+        y = blk(x)
+        y.backward(torch.ones_like(y) * 0.01)
+        grads.append((x.grad.float(), blk.conv1.weight.grad.clone(), blk.down_conv.weight.grad.clone()))
+    blk.share_input_grad = True
+    (a, w1a, wda), (b, w1b, wdb) = grads
+    torch.testing.assert_close(a, b, rtol=1e-2, atol=1e-2 * b.abs().max().item())
+    # weight gradients: same kernels, but MIOpen's split-K weight-gradient solvers
+    # accumulate with atomics (bf16 results may differ by an ulp run to run)
+    torch.testing.assert_close(w1a, w1b, rtol=1e-2, atol=1e-2 * w1b.abs().max().item())
+    torch.testing.assert_close(wda, wdb, rtol=1e-2, atol=1e-2 * wdb.abs().max().item())
+
+
+def test_strided_add_matches_torch(native):
+    torch.manual_seed(6)
+    full = torch.randn(2, 16, 9, 9, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    comp = torch.randn(2, 16, 5, 5, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    ref = full.float().clone()
+    ref[:, :, ::2, ::2] += comp.float()
+    native.strided_add(full, comp, 2)
+    torch.testing.assert_close(full.float(), ref.bfloat16().float())

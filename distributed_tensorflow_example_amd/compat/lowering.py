@@ -54,6 +54,26 @@ from .graph import Operation, Tensor
 _CACHE: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()   # train_op -> plan | False
 
 
+_MODS = {}
+
+
+def _train_mod():
+    """compat.train (imported lazily: it imports this module)."""
+    m = _MODS.get("train")
+    if m is None:
+        from . import train as m
+        _MODS["train"] = m
+    return m
+
+
+def _debug_mod():
+    m = _MODS.get("debug")
+    if m is None:
+        from ..utils import debug as m
+        _MODS["debug"] = m
+    return m
+
+
 def enabled() -> bool:
     return os.environ.get("DTF_GRAPH_LOWERING", "1") != "0"
 
@@ -281,8 +301,9 @@ class MLPStepPlan(_PlanBase):
             self.metrics = torch.zeros(3, dtype=torch.float32, device=x.device)
             self.host_metrics = torch.zeros(3, dtype=torch.float32, pin_memory=True)
         opt, fused, sync, gs_var = info["opt"], info["fused"], info["sync"], info["global_step"]
-        from .train import GradientDescentOptimizer, _world_or_local
-        from ..utils import debug as _debug
+        _tr = _train_mod()
+        GradientDescentOptimizer, _world_or_local = _tr.GradientDescentOptimizer, _tr._world_or_local
+        _debug = _debug_mod()
 
         w = _world_or_local()
         opt._steps += 1
@@ -348,8 +369,9 @@ class MLPStepPlan(_PlanBase):
         objects or the feed shapes change; the fetched values are seeded as numpy
         scalars read from the pinned buffer (no tensor indexing / .cpu() per
         fetch).  False: not applicable."""
-        from .train import GradientDescentOptimizer, _world_or_local
-        from ..utils import debug as _debug
+        _tr = _train_mod()
+        GradientDescentOptimizer, _world_or_local = _tr.GradientDescentOptimizer, _tr._world_or_local
+        _debug = _debug_mod()
 
         pat, info = self.pat, self.info
         opt, gs_var = info["opt"], info["global_step"]
@@ -585,8 +607,9 @@ class SparseLRStepPlan(_PlanBase):
 
     def run(self, ctx, flat) -> bool:
         from ..models.sparse_lr import SparseLRTrainer
-        from ..utils import debug as _debug
-        from .train import GradientDescentOptimizer, _world_or_local
+        _debug = _debug_mod()
+        _tr = _train_mod()
+        GradientDescentOptimizer, _world_or_local = _tr.GradientDescentOptimizer, _tr._world_or_local
 
         p, info = self.pat, self.info
         opt, gs_var = info["opt"], info["global_step"]
@@ -632,7 +655,8 @@ def _flatten(f, out: List[Any]):
 
 def try_lower(session, fetches, ctx) -> None:
     """Run lowered plans for train ops in `fetches`, seeding ctx.memo."""
-    if not enabled():
+    lower = getattr(session, "_lower", None)          # read once per Session (compat/session.py)
+    if not (enabled() if lower is None else lower):
         return
     flat = _flatten(fetches, [])
     for f in flat:

@@ -79,6 +79,7 @@ class Session:
         self._ctx_stack = []
         self._post_run = []
         self._in_post = False
+        self._lower = _lowering.enabled()   # DTF_GRAPH_LOWERING, read once per session (not per run)
 
     # ---------------------------------------------------------------- run
     def run(self, fetches, feed_dict=None, options: RunOptions = None, run_metadata=None):

@@ -15,7 +15,9 @@ from test_lowering_cpu import _graph  # noqa: E402
 
 rng = np.random.default_rng(0)
 B = 100
-xs = (rng.integers(0, 256, (64, B, 784)) / 255.0).astype(np.float32)
+from distributed_tensorflow_example_amd.data.mnist import PixelBatch  # noqa: E402
+
+xs = [PixelBatch.of(u) for u in rng.integers(0, 256, (64, B, 784), dtype=np.uint8)]   # loader-shaped batches
 ys = np.eye(10, dtype=np.float32)[rng.integers(0, 10, (64, B))]
 g = _graph(tf)
 with tf.Session() as sess:

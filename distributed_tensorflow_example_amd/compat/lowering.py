@@ -394,8 +394,8 @@ class MLPStepPlan(_PlanBase):
         needs, gs_seed, scalars = self._needs(flat, gs_var, self._gstep)
         fy2 = (fy if fy.flags.c_contiguous else np.ascontiguousarray(fy)).reshape(B, C)
         u8 = getattr(fx, "u8", None)
-        if (u8 is not None and not fx.flags.writeable and u8.shape == fx.shape and u8.dtype == np.uint8
-                and fx.shape[1] % 4 == 0):
+        if (u8 is not None and self._cplan_u8 and not fx.flags.writeable and u8.shape == fx.shape
+                and u8.dtype == np.uint8 and fx.shape[1] % 4 == 0):
             # data/mnist.py PixelBatch: ship the uint8 source (bit-identical, 4x fewer bytes)
             self._cplan.run_u8(u8, fy2, float(opt._lr_value()), bool(needs))
         else:
@@ -441,6 +441,8 @@ class MLPStepPlan(_PlanBase):
                                                        os.environ.get("DTF_GRAPH_STEP_HIPGRAPH", "0") == "1")
             self._cplan_key = key
             self._hm_np = self._cplan.host_metrics().numpy()
+            # the captured-graph plan takes float32 feeds only (run_u8 is direct-launch)
+            self._cplan_u8 = not self._cplan.use_graph()
         self._cplan_BC = (B, C)
         self._gstep = gstep
         return True
@@ -560,8 +562,15 @@ class SparseLRStepPlan(_PlanBase):
         if B == 0 or y.size != B or vals.size != nnz or (nnz and (idx.ndim != 2 or idx.shape[0] != nnz)):
             return None
         rows = idx[:, 0] if nnz else np.zeros(0, np.int64)
-        if nnz and (rows.min() < 0 or rows.max() >= B or (rows[1:] < rows[:-1]).any()):
-            return None            # not in canonical row order: op by op
+        if nnz and (rows.min() < 0 or rows.max() >= B):
+            return None
+        if nnz and (rows[1:] < rows[:-1]).any():
+            # not in canonical row order: a stable sort by row gives the same bags
+            # (sum combiner), so every rank lowers -- the decision must not depend on
+            # one rank's data (ranks that lowered and ranks that went op by op would
+            # issue different collectives)
+            order = np.argsort(rows, kind="stable")
+            rows, ids, vals = rows[order], ids[order], vals[order]
         offsets = np.zeros(B + 1, np.int64)
         if nnz:
             np.cumsum(np.bincount(rows, minlength=B), out=offsets[1:])
@@ -627,6 +636,12 @@ class SparseLRStepPlan(_PlanBase):
                 self.trainer.enable_graph()        # one worker: no collectives, lazy per-shape captures
         batch = self._batch(ctx, dev)
         if batch is None:
+            if w.world_size > 1:
+                # falling back on this rank alone would desynchronise the collectives
+                # of the lowered step (all-to-all / all-reduce) from its peers'
+                raise RuntimeError("lowered sparse-LR step: this worker's feeds do not match the graph (tensor "
+                                   "feeds, label / index size mismatch or out-of-range rows); synchronous workers "
+                                   "cannot fall back op by op one rank at a time")
             return False
         opt._steps += 1
         _debug.fault_point(opt._steps, w.rank)

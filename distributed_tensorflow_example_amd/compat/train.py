@@ -594,6 +594,12 @@ class AdamOptimizer(Optimizer):
                 v.steps += [t for t in steps if all(t is not u for u in v.steps)]
             else:
                 g.add_to_collection(GLOBAL_VARIABLES, _PowerVariable(name, beta, steps))
+        p1, p2 = have.get("beta1_power:0"), have.get("beta2_power:0")
+        if p1 is None or p2 is None:
+            cur = {v.name: v for v in g.get_collection(GLOBAL_VARIABLES)}
+            p1, p2 = cur.get("beta1_power:0"), cur.get("beta2_power:0")
+        if isinstance(p1, _PowerVariable) and isinstance(p2, _PowerVariable):
+            p1.sibling, p2.sibling = p2, p1
 
 
 class _PowerVariable:
@@ -608,6 +614,8 @@ class _PowerVariable:
         self.steps = list(steps)
         self.initialized = True
         self._buf = torch.zeros((), dtype=torch.float32)
+        self.sibling = None      # the other power of the same optimizer (beta1 <-> beta2)
+        self._restored = None    # value read by the last restore
 
     @property
     def value(self):
@@ -616,11 +624,17 @@ class _PowerVariable:
         return self._buf
 
     def restore_from(self, t: torch.Tensor):
-        """Saver.restore: beta^(t+1) -> the step count of every tied optimizer."""
-        import math
+        """Saver.restore: beta^(t+1) -> the step count of every tied optimizer.
 
-        v = float(t.reshape(-1)[0])
-        steps = max(0, int(round(math.log(v) / math.log(self.beta))) - 1) if 0.0 < v < 1.0 else 0
+        Uses both powers whichever order they are restored in: a power that
+        underflowed (subnormal / 0 in float32) only bounds the count, the other
+        one pins it (`optim.adam_steps_from_powers`)."""
+        from ..optim import adam_steps_from_powers
+
+        self._restored = float(t.reshape(-1)[0])
+        sib = self.sibling
+        other = (sib._restored, sib.beta) if sib is not None and sib._restored is not None else (None, None)
+        steps = adam_steps_from_powers(self._restored, self.beta, *other)
         for s in self.steps:
             s.fill_(steps)
 

@@ -24,6 +24,7 @@ import gzip
 import os
 import struct
 import sys
+from typing import Optional
 
 import numpy as np
 import torch
@@ -134,9 +135,17 @@ def one_hot(labels: np.ndarray, n: int = NUM_CLASSES) -> np.ndarray:
 
 class DataSet:
     """Minimal stand-in for `mnist.train` / `mnist.test` (next_batch, epochs,
-    float images in [0,1] and one-hot labels as the reference feeds them)."""
+    float images in [0,1] and one-hot labels as the reference feeds them).
 
-    def __init__(self, images_u8: np.ndarray, labels_u8: np.ndarray, seed: int = 0, shuffle: bool = True):
+    `next_batch` returns ordinary writeable float32 arrays, like TF's loader
+    (callers may normalise / shuffle / augment a batch in place).  With
+    `pixel_batches=True` (opt-in: `read_data_sets(..., pixel_batches=True)` or
+    DTF_MNIST_PIXEL_BATCHES=1) it returns read-only `PixelBatch`es instead, which
+    the lowered Session step ships as their 4x smaller uint8 source."""
+
+    def __init__(self, images_u8: np.ndarray, labels_u8: np.ndarray, seed: int = 0, shuffle: bool = True,
+                 pixel_batches: bool = False):
+        self.pixel_batches = bool(pixel_batches)
         self.images_u8 = images_u8
         self.labels_u8 = labels_u8
         self._rng = np.random.default_rng(seed)
@@ -165,12 +174,16 @@ class DataSet:
                 self._perm = self._rng.permutation(self.num_examples)
         idx = self._perm[self._pos:self._pos + batch_size]
         self._pos += batch_size
-        return PixelBatch.of(self.images_u8[idx]), one_hot(self.labels_u8[idx])
+        u8 = self.images_u8[idx]
+        if self.pixel_batches:
+            return PixelBatch.of(u8), one_hot(self.labels_u8[idx])
+        return u8.astype(np.float32) / np.float32(255.0), one_hot(self.labels_u8[idx])
 
 
 class PixelBatch(np.ndarray):
     """A read-only float32 image batch x = u8 / 255 that keeps its uint8 source
-    in `.u8`.  Everywhere it is an ordinary float32 array; the lowered Session
+    in `.u8` (the loader's opt-in `pixel_batches` mode: read-only, so the source
+    provably still matches the floats).  Everywhere it is an ordinary float32 array; the lowered Session
     step (compat/lowering.py) ships the 4x smaller uint8 batch instead and the
     kernel converts with the same correctly rounded float32 division, so the
     step is bit-identical.  Arrays derived from it (slices, arithmetic) carry no
@@ -210,7 +223,8 @@ def idx_files(train_dir: str):
 
 def read_data_sets(train_dir: str = "", one_hot: bool = True, seed: int = 0,
                    train_size: int = TRAIN_EXAMPLES, test_size: int = TEST_EXAMPLES,
-                   validation_size: int = VALIDATION_SIZE, synthetic_fallback: bool = True) -> Datasets:
+                   validation_size: int = VALIDATION_SIZE, synthetic_fallback: bool = True,
+                   pixel_batches: Optional[bool] = None) -> Datasets:
     """Drop-in for tensorflow.examples.tutorials.mnist.input_data.read_data_sets.
 
     Real data: the IDX files in `train_dir`; the first `validation_size` training
@@ -218,8 +232,13 @@ def read_data_sets(train_dir: str = "", one_hot: bool = True, seed: int = 0,
     `train_size` / `test_size` only size the synthetic fallback, which has the
     same three splits.  `one_hot` is accepted for signature parity: `labels`
     are always one-hot float32 (what example.py feeds), `labels_u8` the ids.
+    `pixel_batches`: next_batch returns read-only `PixelBatch`es (see DataSet);
+    None reads DTF_MNIST_PIXEL_BATCHES (default off: writeable float32 batches).
     """
     del one_hot
+    if pixel_batches is None:
+        pixel_batches = os.environ.get("DTF_MNIST_PIXEL_BATCHES", "0") == "1"
+    pb = {"pixel_batches": bool(pixel_batches)}
     paths = idx_files(train_dir)
     if paths is not None:
         xi, yi = read_idx_images(paths[0]), read_idx_labels(paths[1])
@@ -228,9 +247,9 @@ def read_data_sets(train_dir: str = "", one_hot: bool = True, seed: int = 0,
             raise ValueError(f"{train_dir}: image / label counts differ ({len(xi)}/{len(yi)}, {len(xt)}/{len(yt)})")
         if not 0 <= validation_size <= len(xi):
             raise ValueError(f"validation size should be between 0 and {len(xi)}; received {validation_size}")
-        return Datasets(DataSet(xi[validation_size:], yi[validation_size:], seed=seed),
-                        DataSet(xt, yt, seed=seed, shuffle=False),
-                        DataSet(xi[:validation_size], yi[:validation_size], seed=seed, shuffle=False),
+        return Datasets(DataSet(xi[validation_size:], yi[validation_size:], seed=seed, **pb),
+                        DataSet(xt, yt, seed=seed, shuffle=False, **pb),
+                        DataSet(xi[:validation_size], yi[:validation_size], seed=seed, shuffle=False, **pb),
                         source=f"idx:{os.path.abspath(train_dir)}")
     if not synthetic_fallback:
         raise FileNotFoundError(f"MNIST IDX files not found in {train_dir!r} (no network to download them)")
@@ -240,8 +259,8 @@ def read_data_sets(train_dir: str = "", one_hot: bool = True, seed: int = 0,
     xi, yi = synthetic_mnist(train_size, seed=seed)
     xv, yv = synthetic_mnist(validation_size, seed=seed + 104729) if validation_size > 0 else (xi[:0], yi[:0])
     xt, yt = synthetic_mnist(test_size, seed=seed + 7919)
-    return Datasets(DataSet(xi, yi, seed=seed), DataSet(xt, yt, seed=seed, shuffle=False),
-                    DataSet(xv, yv, seed=seed, shuffle=False), source="synthetic")
+    return Datasets(DataSet(xi, yi, seed=seed, **pb), DataSet(xt, yt, seed=seed, shuffle=False, **pb),
+                    DataSet(xv, yv, seed=seed, shuffle=False, **pb), source="synthetic")
 
 
 def record_bytes(batch_size: int) -> int:

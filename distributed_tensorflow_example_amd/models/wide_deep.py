@@ -222,34 +222,40 @@ class WideDeep(StaticStepMixin):
         if opt.kind not in ("adam", "adamw"):
             return {}
         t = int(opt.step_t.item())
+        # the integer count itself rides along (`adam_step`): the float32 powers
+        # underflow (beta1 = 0.9: 0.0 after ~990 steps) and cannot pin it alone
         return {f"{prefix}beta1_power": torch.tensor(opt.b1 ** (t + 1), dtype=torch.float32),
-                f"{prefix}beta2_power": torch.tensor(opt.b2 ** (t + 1), dtype=torch.float32)}
-
-    @staticmethod
-    def _step_from_power(value: float, beta: float) -> int:
-        import math
-        return max(0, int(round(math.log(float(value)) / math.log(beta))) - 1)
+                f"{prefix}beta2_power": torch.tensor(opt.b2 ** (t + 1), dtype=torch.float32),
+                f"{prefix}adam_step": torch.tensor(t, dtype=torch.int64)}
 
     def restore(self, prefix: str):
         """Load a checkpoint written from `checkpoint_tensors` (any world size):
         tables and slots take the rows they own, the tower, its Adam slots and
-        every optimizer's step count (from beta1_power) are restored."""
+        every optimizer's step count (the saved `adam_step`; a checkpoint without
+        it: from both beta powers, `optim.adam_steps_from_powers`) are restored."""
         from ..ckpt import read_bundle_index, read_tensor, restore_sharded
+        from ..optim import adam_steps_from_powers
 
         local, repl = self.checkpoint_tensors()
         idx = read_bundle_index(prefix)
         restore_sharded(prefix, {k: v for k, v in local.items()})
         with torch.no_grad():
             for name, dst in repl.items():
-                if name.endswith("beta2_power") or name == "global_step":
+                if name.endswith(("beta2_power", "adam_step")) or name == "global_step":
                     continue
                 if name.endswith("beta1_power"):
-                    opt = self.opt if name == "beta1_power" else self.wide._adam
-                    if name in idx:
-                        steps = self._step_from_power(float(read_tensor(prefix, name)), opt.b1)
-                        opts = [opt] if opt is self.opt else [self.wide._adam, self.emb._adam]
-                        for o in opts:
-                            o.step_t.fill_(steps)
+                    pre = name[: -len("beta1_power")]
+                    opt = self.opt if pre == "" else self.wide._adam
+                    if pre + "adam_step" in idx:
+                        steps = int(read_tensor(prefix, pre + "adam_step"))
+                    elif name in idx:
+                        b2 = float(read_tensor(prefix, pre + "beta2_power")) if pre + "beta2_power" in idx else None
+                        steps = adam_steps_from_powers(float(read_tensor(prefix, name)), opt.b1, b2, opt.b2)
+                    else:
+                        continue
+                    opts = [opt] if opt is self.opt else [self.wide._adam, self.emb._adam]
+                    for o in opts:
+                        o.step_t.fill_(steps)
                     continue
                 if name in idx:          # dst shares storage with the parameter / slot
                     dst.copy_(read_tensor(prefix, name).to(self.device, torch.float32).reshape(dst.shape))

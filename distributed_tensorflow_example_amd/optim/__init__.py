@@ -29,6 +29,41 @@ from .. import _native
 KINDS = {"sgd": 0, "momentum": 1, "adam": 2, "adamw": 3, "adagrad": 4, "rmsprop": 5}
 
 
+_F32_TINY = 1.1754943508222875e-38   # smallest normal float32
+_F32_ZERO_BELOW = 2.0 ** -150         # a float32 power this small rounds to 0.0
+
+
+def adam_steps_from_powers(beta1_power: Optional[float], beta1: float,
+                           beta2_power: Optional[float] = None, beta2: Optional[float] = None) -> int:
+    """Adam's update count t from TF's saved non-slot accumulators beta^(t+1).
+
+    The powers are float32: beta1 = 0.9 turns subnormal near t = 830 and 0.0
+    near t = 990; beta2 = 0.999 stays normal to t ~ 87,000 and reaches 0.0
+    near t ~ 103,000.  The step comes from whichever power is still a normal
+    float (those are exact to far below one step); a subnormal power is too
+    coarse and only bounds t from below.  When every power has underflowed the
+    bias correction is 1 to float precision (TF keeps the power at 0), so the
+    count saturates at the first step where every power is 0.0 -- never at 0,
+    which would restart the bias correction (lr ~0.3x for thousands of steps)."""
+    import math
+
+    best, bound = None, 0
+    for v, beta in ((beta1_power, beta1), (beta2_power, beta2)):
+        if v is None or beta is None or not (0.0 < beta < 1.0):
+            continue
+        v = float(v)
+        if _F32_TINY <= v < 1.0:
+            best = max(0, int(round(math.log(v) / math.log(beta))) - 1)
+            break
+        if 0.0 < v < _F32_TINY:       # subnormal: t + 1 >= log(tiny) / log(beta)
+            bound = max(bound, int(math.floor(math.log(v) / math.log(beta))) - 1)
+        elif v <= 0.0:                # underflowed: t + 1 > log(2^-150) / log(beta)
+            bound = max(bound, int(math.ceil(math.log(_F32_ZERO_BELOW) / math.log(beta))))
+    if best is not None:
+        return best
+    return max(0, bound)
+
+
 def _dense(t: torch.Tensor) -> bool:
     """Non-overlapping dense storage (row-major or channels_last): the kernels
     walk params/grads/slots as flat arrays, so only identical layouts matter."""

@@ -105,8 +105,13 @@ def main(_):
         supervisor = tf.train.Supervisor(is_chief=is_chief, init_op=init, global_step=global_step)
         config = tf.ConfigProto(allow_soft_placement=True)
 
+    # tests: this worker feeds its COO entries in reverse (non-canonical) order
+    permute = os.environ.get("DTF_LR2_PERMUTE_COO_TASK") == str(FLAGS.task_index)
+
     def feed(batch):
         labels, fids, fvals, sp_indices, batch_size = batch.as_tf_feed()
+        if permute:
+            fids, fvals, sp_indices = fids[::-1], fvals[::-1], sp_indices[::-1]
         return {y: labels, x_shape: [num_features, batch_size], x_indices: sp_indices, x_fids: fids,
                 x_fvals: fvals}
 

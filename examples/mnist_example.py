@@ -263,7 +263,9 @@ def main(_argv):
         return 0
     print(f"worker {FLAGS.task_index} start ...", flush=True)
     data_dir = FLAGS.data_dir or f"MNIST_data/{FLAGS.job_name}_{FLAGS.task_index}"
-    mnist = mnist_data.read_data_sets(data_dir, one_hot=True, seed=FLAGS.task_index, train_size=FLAGS.train_size)
+    # the loop below feeds batches unmodified: read-only pixel batches, shipped as uint8 by the lowered step
+    mnist = mnist_data.read_data_sets(data_dir, one_hot=True, seed=FLAGS.task_index, train_size=FLAGS.train_size,
+                                      pixel_batches=True)
     print(f"MNIST source: {mnist.source} (train {mnist.train.num_examples}, validation "
           f"{mnist.validation.num_examples}, test {mnist.test.num_examples})", flush=True)
     if FLAGS.fused:

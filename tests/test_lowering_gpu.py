@@ -232,3 +232,30 @@ def test_session_uses_uint8_feed_for_loader_batches():
         tf.reset_default_graph()
     for a, b in zip(finals[0][1], finals[1][1]):
         assert np.array_equal(a, b)
+
+
+def test_loader_batches_with_captured_graph_plan(monkeypatch):
+    """DTF_GRAPH_STEP_HIPGRAPH=1 builds the captured-graph plan, which takes
+    float32 feeds only: loader PixelBatches must take its float path (not
+    run_u8, which that plan refuses) and still train like the fp64 graph."""
+    monkeypatch.setenv("DTF_GRAPH_STEP_HIPGRAPH", "1")
+    import distributed_tensorflow_example_amd.compat as tf
+    from distributed_tensorflow_example_amd.compat import lowering as L
+    from distributed_tensorflow_example_amd.data.mnist import PixelBatch
+
+    rng = np.random.default_rng(4)
+    g = _graph(tf)
+    with tf.Session() as sess:
+        sess.run(tf.global_variables_initializer())
+        params = [v.numpy().astype(np.float64) for v in g["W"]]
+        for s in range(3):
+            bx = PixelBatch.of(rng.integers(0, 256, (100, 784), dtype=np.uint8))
+            by = np.eye(10, dtype=np.float32)[rng.integers(0, 10, 100)]
+            params, ref_ce, _ = _ref_step(params, np.asarray(bx), by, 0.5, "sigmoid", False)
+            _, ce = sess.run([g["train"], g["ce"]], feed_dict={g["x"]: bx, g["y_"]: by})
+            assert abs(ce - ref_ce) <= 1e-5 * abs(ref_ce)
+        plan = L.plan_for(g["train"])
+        assert plan is not None and plan._cplan.use_graph() and plan._cplan.steps() == 3
+        for got, want in zip(g["W"], params):
+            assert _rel(got.numpy(), want) < 1e-5
+    tf.reset_default_graph()

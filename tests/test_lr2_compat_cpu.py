@@ -90,3 +90,23 @@ def test_lr2_compat_lowered_matches_native_and_op_by_op(svm, tmp_path):
     assert np.allclose(w_low, w_nat, atol=1e-5), np.abs(w_low - w_nat).max()
     assert abs(low[0]["b"] - native[0]["b"]) < 1e-5
     assert abs(low[0]["loss"] - eager[0]["loss"]) < 1e-4
+
+
+def test_lr2_compat_one_worker_non_canonical_coo_still_lowers(svm, tmp_path):
+    """Worker 1 feeds its COO entries in reverse order: the lower / fall-back
+    decision must not differ between ranks (mismatched collectives would hang),
+    so that worker's batch is re-sorted by row and both workers lower; the
+    result equals the canonical-order run."""
+    d, tr, te = svm
+    common = [f"--train={','.join(tr)}", f"--test={','.join(te)}", "--features=3000", "--num_epochs=1",
+              "--learning_rate=0.5", "--batch_size=100", "--trace_step_interval=4"]
+    (tmp_path / "canon").mkdir()
+    (tmp_path / "perm").mkdir()
+    canon, _ = _cluster(tmp_path / "canon", "lr2_compat.py", common)
+    perm, _ = _cluster(tmp_path / "perm", "lr2_compat.py", common, {"DTF_LR2_PERMUTE_COO_TASK": "1"})
+    for r in perm:
+        assert r["lowered_steps"] == 10 and r["global_step"] == 10
+    w_c = np.load(str(tmp_path / "canon" / "w0.json") + ".W.npy")
+    w_p = np.load(str(tmp_path / "perm" / "w0.json") + ".W.npy")
+    assert np.array_equal(w_p, np.load(str(tmp_path / "perm" / "w1.json") + ".W.npy"))
+    assert np.allclose(w_c, w_p, atol=1e-6), np.abs(w_c - w_p).max()

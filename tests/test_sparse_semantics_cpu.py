@@ -203,3 +203,64 @@ def test_wide_deep_checkpoint_restores_adam_state(tmp_path):
     assert torch.allclose(c.emb.local, a.emb.local, atol=1e-7) and torch.allclose(c.wide.local, a.wide.local, atol=1e-7)
     for p, q in zip(c.dense_params, a.dense_params):
         assert torch.allclose(p, q, atol=1e-7)
+
+
+def test_adam_steps_from_powers_survives_underflow():
+    """beta1 = 0.9 underflows float32 near t = 990 and beta2 = 0.999 near
+    t ~ 103k: the count comes from whichever power is still normal, and a fully
+    underflowed pair saturates (bias correction 1) instead of restarting at 0."""
+    from distributed_tensorflow_example_amd.optim import adam_steps_from_powers
+
+    def f32(x):
+        return float(np.float32(x))
+
+    for t in (0, 3, 500, 829, 900, 990, 1200, 5000, 60000):
+        b1, b2 = f32(0.9 ** (t + 1)), f32(0.999 ** (t + 1))
+        assert adam_steps_from_powers(b1, 0.9, b2, 0.999) == t
+        assert adam_steps_from_powers(b2, 0.999, b1, 0.9) == t
+    # beta1's power alone, still normal
+    assert adam_steps_from_powers(f32(0.9 ** 501), 0.9) == 500
+    # beta1's alone once it underflowed: a lower bound past the underflow, never 0
+    assert adam_steps_from_powers(0.0, 0.9) >= 986
+    # both underflowed: saturated at a count where both float32 powers are 0
+    t = adam_steps_from_powers(0.0, 0.9, 0.0, 0.999)
+    assert f32(0.9 ** (t + 1)) == 0.0 and f32(0.999 ** (t + 1)) == 0.0
+
+
+def test_wide_deep_restore_after_1000_adam_steps(tmp_path):
+    from distributed_tensorflow_example_amd import ckpt
+    from distributed_tensorflow_example_amd.models.wide_deep import WideDeep
+    from distributed_tensorflow_example_amd.parallel.world import World
+
+    def make(seed):
+        return WideDeep(400, emb_dim=4, hidden=(8,), lr=0.1, dense_opt="adam", dense_lr=0.01,
+                        world=World(device="cpu"), device="cpu", seed=seed, sparse_opt="adam")
+    a = make(1)
+    for o in (a.opt, a.wide._adam, a.emb._adam):
+        o.step_t.fill_(1234)          # past beta1_power's float32 underflow
+    local, repl = a.checkpoint_tensors()
+    assert float(repl["beta1_power"]) == 0.0 and int(repl["adam_step"]) == 1234
+    prefix = ckpt.save_sharded(str(tmp_path / "wd"), local, repl, World(device="cpu"), global_step=1234)
+    c = make(7)
+    c.restore(prefix)
+    assert int(c.opt.step_t.item()) == 1234 and int(c.wide._adam.step_t.item()) == 1234
+    assert int(c.emb._adam.step_t.item()) == 1234
+
+
+def test_compat_power_restore_any_order_past_underflow():
+    """Saver.restore feeds beta1_power / beta2_power one at a time: the tied
+    step count must come out right in either order once beta1's power is 0."""
+    import distributed_tensorflow_example_amd.compat as tf
+    from distributed_tensorflow_example_amd.compat.train import _PowerVariable
+
+    for order in ((0, 1), (1, 0)):
+        step = torch.zeros(1, dtype=torch.int64)
+        p1, p2 = _PowerVariable("beta1_power", 0.9, [step]), _PowerVariable("beta2_power", 0.999, [step])
+        p1.sibling, p2.sibling = p2, p1
+        vals = (torch.tensor(np.float32(0.9 ** 2001)), torch.tensor(np.float32(0.999 ** 2001)))
+        assert float(vals[0]) == 0.0
+        pv = (p1, p2)
+        for i in order:
+            pv[i].restore_from(vals[i])
+        assert int(step.item()) == 2000, order
+    assert tf is not None

@@ -25,7 +25,8 @@ device timestamps (s_memrealtime at every step start) on the persistent
 engines.
 
     python bench.py --gpus N --steps K --warmup W
-    (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+    (N>1: either under python -m torch.distributed.run --nproc-per-node N ...,
+     or plain: bench.py then starts the N rank processes itself)
 
 Rank 0 prints ONE JSON line.
 """
@@ -36,10 +37,76 @@ import json
 import math
 import os
 import statistics
+import subprocess
 import sys
 import time
 
-import torch
+
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(argv, gpus: int, grace_s: float = 60.0, script: str = None) -> int:
+    """`bench.py --gpus N` started as ONE plain process (no torchrun env): start
+    the N rank processes here -- fresh children with RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* set, this same command line -- and return the worst
+    child exit code.  The reference launches every task as a plain process by
+    hand (README.md:11-16, example.py:24-40); this keeps that shape working.
+
+    Runs before anything in this process touches the GPU (no torch import
+    yet), and starts children rather than exec'ing.  Rank 0's stdout is
+    inherited (its one JSON line is the output); the other ranks' stdout goes to
+    stderr.  When a rank fails, the rest get `grace_s` to finish, then are
+    terminated, so a dead rank cannot leave the job hanging."""
+    port = _free_port()
+    procs = []
+    for r in range(gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(gpus), LOCAL_WORLD_SIZE=str(gpus),
+                   GROUP_RANK="0", MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"), MASTER_PORT=str(port),
+                   DTF_BENCH_SELF_LAUNCHED="1")
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=None if r == 0 else sys.stderr))
+    rcs = [None] * gpus
+    first_fail = None
+    try:
+        while any(rc is None for rc in rcs):
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    rcs[i] = p.poll()
+                    if rcs[i] not in (None, 0) and first_fail is None:
+                        first_fail = time.monotonic()
+                        print(f"bench: rank {i} exited with {rcs[i]}", file=sys.stderr, flush=True)
+            if first_fail is not None and time.monotonic() - first_fail > grace_s:
+                break
+            time.sleep(0.05)
+    finally:
+        for i, p in enumerate(procs):
+            if p.poll() is None:
+                p.terminate()
+                try:
+                    p.wait(10)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            rcs[i] = p.returncode
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+if __name__ == "__main__" and "WORLD_SIZE" not in os.environ:
+    _ap = argparse.ArgumentParser(add_help=False)
+    _ap.add_argument("--gpus", type=int, default=1)
+    _n = _ap.parse_known_args(sys.argv[1:])[0].gpus
+    if _n > 1:
+        sys.exit(self_launch(sys.argv[1:], _n))
+
+import torch  # noqa: E402
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 if REPO not in sys.path:
@@ -88,12 +155,16 @@ def main(argv=None):
     ap.add_argument("--allreduce", choices=["auto", "ipc-fused", "ipc-apply", "rccl"], default="auto",
                     help="N>1 gradient exchange: IPC over xGMI inside the wgrad kernel (ipc-fused, default), "
                          "IPC one-shot in a separate reduce+apply kernel (ipc-apply), or RCCL")
+    ap.add_argument("--rccl-timeout", type=float, default=120.0,
+                    help="N>1: bound on RCCL communicator creation (s); a failure is recorded in the fallbacks")
     a = ap.parse_args(argv)
 
     world_size_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.gpus > 1 and world_size_env == 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(self_launch(sys.argv[1:] if argv is None else list(argv), a.gpus))
     if world_size_env != a.gpus:
-        if a.gpus > 1 and world_size_env == 1:
-            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
+        print(f"bench: --gpus {a.gpus} but WORLD_SIZE={world_size_env}; measuring the launched world",
+              file=sys.stderr, flush=True)
     if os.environ.get("DTF_BENCH_SAME_GPU") == "1" and world_size_env > 1:
         # test mode: all ranks share cuda:0 (gloo control plane, IPC data plane only);
         # validates the multi-rank IPC path + graphs on a 1-GPU box, timings not meaningful
@@ -109,7 +180,9 @@ def main(argv=None):
                             backend="gloo", pg_initialized=True)
         world_mod._WORLD = w
     else:
-        w = world_mod.init(backend="rccl")
+        # RCCL is created lazily (World.ensure_comm), only when an RCCL strategy is
+        # set up, and bounded: the in-kernel IPC exchange never depends on it
+        w = world_mod.init(backend="rccl", rccl="lazy", rccl_timeout_s=a.rccl_timeout)
     dev = w.device
     torch.manual_seed(1234 + w.rank)
 
@@ -137,7 +210,7 @@ def main(argv=None):
             trainer = GemmMLPTrainer(batch_size=a.batch, lr=a.lr, act=a.act, world=w, device=dev)
         else:
             trainer = FusedMLPTrainer(batch_size=a.batch, lr=a.lr, act=a.act, world=w, grad_dtype=gd,
-                                      device=dev, allreduce="rccl" if mode.startswith("persistent") else mode,
+                                      device=dev, allreduce="external" if mode.startswith("persistent") else mode,
                                       ipc_timeout_s=a.exchange_timeout)
         if mode.startswith("persistent"):
             runner = PersistentMLPRunner(trainer, epoch, steps_per_launch=a.steps_per_launch,
@@ -188,6 +261,8 @@ def main(argv=None):
         if can_persist and a.allreduce == "auto":
             # both in-kernel exchanges are timed (the fabric decides which wins)
             chain = ["persistent", "persistent-2shot"] + chain
+    if os.environ.get("DTF_BENCH_CHAIN"):   # tests: an explicit strategy order
+        chain = [m.strip() for m in os.environ["DTF_BENCH_CHAIN"].split(",") if m.strip()]
     # N > 1: the first two valid candidates are timed briefly (outside the timed
     # region) and the faster one is kept -- the in-kernel exchange's per-CU peer
     # reads vs the 3-launch path's exchange spread over 347 workgroups depends on
@@ -367,6 +442,10 @@ def main(argv=None):
                 "engine": f"persistent-{a.precision}" if persistent else ("gemm" if mode == "gemm" else "launches"),
                 "exchange_mode": mode,
                 "fallbacks": fallbacks or None,
+                "rccl_comm": (None if n == 1 else w.comm_error if w.comm_error is not None else
+                              "created" if w.comm is not None else "not created (not needed by the exchange)"),
+                "launch": ("self-launched rank processes" if os.environ.get("DTF_BENCH_SELF_LAUNCHED") == "1"
+                           else "torch.distributed.run" if n > 1 else "single process"),
                 "copy_only_launches_in_timed_run": cold_timed,
                 "steps_per_launch": runner.g if persistent else 1,
                 "hipgraph_steps": 0 if (persistent or not runner.use_graph) else a.steps_per_graph,

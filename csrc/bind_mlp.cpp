@@ -6,7 +6,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <thread>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -52,6 +54,13 @@ hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int n
                                 const void* host_next, int next_steps, void* stage_next, void* const* peer_base, int W,
                                 int rank, int gbf16, long long* phase_ts, int spread, int xmode, int split,
                                 hipStream_t stream);
+hipError_t dtfk_mlp_persist_f32_resident(void* stage, int B, float* W1, float* W2, float* b1, float* b2, const float* lr,
+                                         float* metrics, int ring, int act, int naive, long long* gstep,
+                                         unsigned long long* seq, void* xbuf, int* err, long long timeout,
+                                         const long long* door, const void* host_recs, long long rec_h,
+                                         const float* host_lr, float* host_out, long long* host_done,
+                                         long long* host_state, long long launch_id, long long run0, long long idle,
+                                         void* gvar, int gvar_kind, unsigned* dctr, hipStream_t stream);
 long long dtfk_graph_mlp_part_floats(int B, int H);
 hipError_t dtfk_graph_feed_ingest(const void* host, void* dev, long long bytes, hipStream_t stream);
 hipError_t dtfk_graph_mlp_step(const float* x, const uint8_t* xu, const float* ylab, float* W1, float* b1, float* W2,
@@ -812,7 +821,237 @@ class GraphStepPlan {
   double t_[3] = {0, 0, 0};
 };
 
+// The resident Session engine (compat/resident.py): the persistent fp32 kernel
+// (csrc/kernels/mlp_persist_f32.hip, RES) stays launched across Session.run
+// calls of the reference's training graph and is driven through pinned host
+// memory -- per run the host writes the uint8 batch, its labels and lr into a
+// record slot and bumps a doorbell; the kernel stages, trains one step on the
+// graph's own W1 / b1 / W2 / b2 (written through every step, so other readers
+// see current values), bumps global_step and stores loss / accuracy /
+// global_step and a done count back into pinned memory.  No launch, no
+// completion, no copy-engine op per run.  The launch exits by itself after
+// `idle_s` without a doorbell (relaunched on the next run) or when stop() rings
+// door = -1; either way every wave reaches the exit.
+class ResidentMLPPlan {
+ public:
+  ResidentMLPPlan(at::Tensor W1, at::Tensor b1, at::Tensor W2, at::Tensor b2, c10::optional<at::Tensor> gstep, int B,
+                  int act, bool naive, double idle_s, double timeout_s)
+      : W1_(W1), b1_(b1), W2_(W2), b2_(b2), B_(B), act_(act), naive_(naive) {
+    for (const at::Tensor* t : {&W1, &b1, &W2, &b2})
+      TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous(),
+                  "ResidentMLPPlan: fp32 contiguous device parameters expected");
+    TORCH_CHECK(W1.dim() == 2 && W1.size(0) == 784 && W1.size(1) == 100 && b1.numel() == 100 && W2.dim() == 2 &&
+                    W2.size(0) == 100 && W2.size(1) == 10 && b2.numel() == 10,
+                "ResidentMLPPlan: the reference's 784-100-10 shapes expected");
+    TORCH_CHECK(B >= 1 && B <= dtfk_mlpf_max_batch(), "ResidentMLPPlan: batch must be in [1, ",
+                dtfk_mlpf_max_batch(), "]");
+    if (gstep.has_value()) {
+      const int k = gstep_kind_of(*gstep);   // 0 f32, 1 i64, 2 i32, 3 f64
+      gkind_ = k + 1;
+      gstep_ = *gstep;
+    }
+    rec_h_ = ((int64_t)B * 785 + 15) / 16 * 16;
+    const size_t bytes = 512 + 2 * (size_t)rec_h_;
+    hip_check(hipHostMalloc(&mail_, bytes, hipHostMallocMapped | hipHostMallocCoherent), "ResidentMLPPlan: mailbox");
+    std::memset(mail_, 0, bytes);
+    char* m = static_cast<char*>(mail_);
+    door_ = reinterpret_cast<long long*>(m);
+    done_ = reinterpret_cast<long long*>(m + 64);
+    state_ = reinterpret_cast<long long*>(m + 128);
+    out_ = reinterpret_cast<float*>(m + 192);
+    lr_ = reinterpret_cast<float*>(m + 256);
+    recs_ = reinterpret_cast<uint8_t*>(m + 512);
+    void* dp = nullptr;   // device-visible alias of the mailbox (unified addressing: the same address)
+    if (hipHostGetDevicePointer(&dp, mail_, 0) != hipSuccess || dp == nullptr) {
+      (void)hipGetLastError();
+      dp = mail_;
+    }
+    dmail_ = static_cast<char*>(dp);
+    auto o8 = W1.options().dtype(at::kByte);
+    stage_ = at::zeros({2 * dtfk_mlpf_stage_rec()}, o8);
+    xbuf_ = at::zeros({dtfk_mlpf_xbuf_bytes()}, o8);
+    seq_ = at::zeros({1}, W1.options().dtype(at::kLong));
+    kgstep_ = at::zeros({1}, W1.options().dtype(at::kLong));
+    err_ = at::zeros({1}, W1.options().dtype(at::kInt));
+    lrdev_ = at::zeros({1}, W1.options());
+    metrics_ = at::zeros({2 * kRing}, W1.options());
+    dctr_ = at::zeros({64}, W1.options().dtype(at::kInt));
+    idle_ = (long long)(idle_s * 1e8);            // s_memrealtime: 100 MHz
+    timeout_ = (long long)(timeout_s * 1e8);
+    wait_s_ = std::max(5.0, 4.0 * idle_s + timeout_s);
+    hip_check(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking), "hipStreamCreate");
+    hip_check(hipEventCreateWithFlags(&ev_, hipEventDisableTiming), "hipEventCreate");
+  }
+  ~ResidentMLPPlan() {
+    try {
+      stop();
+    } catch (...) {
+    }
+    if (ev_) (void)hipEventDestroy(ev_);
+    if (st_) (void)hipStreamDestroy(st_);
+    if (mail_) (void)hipHostFree(mail_);
+  }
+
+  // One training step from the MNIST loader's uint8 batch [B, 784] and one-hot
+  // float32 labels [B, 10].  False (nothing ran) when y_ is not exactly one-hot:
+  // the caller takes the general plan.  Returns after the step; host_metrics()
+  // then holds loss, accuracy, global_step (pre-update loss / accuracy, as the
+  // graph evaluates them in the same run).
+  bool run_u8(py::array xu8, py::array y, double lr) {
+    TORCH_CHECK(xu8.dtype().is(py::dtype::of<uint8_t>()) && y.dtype().is(py::dtype::of<float>()),
+                "ResidentMLPPlan.run_u8: uint8 x and float32 y_ expected");
+    TORCH_CHECK((xu8.flags() & py::array::c_style) && (y.flags() & py::array::c_style),
+                "ResidentMLPPlan.run_u8: C-contiguous feeds expected");
+    TORCH_CHECK(xu8.size() == (int64_t)B_ * 784 && y.size() == (int64_t)B_ * 10,
+                "ResidentMLPPlan.run_u8: feed shapes differ from the plan's");
+    const uint8_t* xp = static_cast<const uint8_t*>(xu8.data());
+    const float* yp = static_cast<const float*>(y.data());
+    uint8_t lab[128];
+    for (int b = 0; b < B_; ++b) {   // class ids; anything but an exact one-hot row -> general plan
+      int hot = -1;
+      for (int c = 0; c < 10; ++c) {
+        const float v = yp[b * 10 + c];
+        if (v == 1.0f && hot < 0) hot = c;
+        else if (v != 0.0f) return false;
+      }
+      if (hot < 0) return false;
+      lab[b] = (uint8_t)hot;
+    }
+    {
+      py::gil_scoped_release nogil;
+      using clk = std::chrono::steady_clock;
+      const auto t0 = clk::now();
+      if (alive_ && __atomic_load_n(state_, __ATOMIC_ACQUIRE) == launch_id_) reap();   // exited while idle
+      if (!alive_) launch();
+      const int slot = (int)(runs_ & 1);
+      uint8_t* rec = recs_ + slot * rec_h_;
+      std::memcpy(rec, xp, (size_t)B_ * 784);
+      std::memcpy(rec + (size_t)B_ * 784, lab, (size_t)B_);
+      lr_[slot] = (float)lr;
+      std::atomic_thread_fence(std::memory_order_seq_cst);
+      __atomic_store_n(door_, runs_ + 1, __ATOMIC_RELEASE);
+      const auto t1 = clk::now();
+      t_[0] += std::chrono::duration<double, std::micro>(t1 - t0).count();
+      long long spins = 0;
+      while (__atomic_load_n(done_, __ATOMIC_ACQUIRE) < runs_ + 1) {
+        if ((++spins & 1023) == 0) {
+          if (__atomic_load_n(state_, __ATOMIC_ACQUIRE) == launch_id_ &&
+              __atomic_load_n(done_, __ATOMIC_ACQUIRE) < runs_ + 1) {
+            // the launch stopped (idle) without taking this run: start another
+            reap();
+            launch();
+          }
+          if (std::chrono::duration<double>(clk::now() - t1).count() > wait_s_) {
+            dead_ = true;
+            throw std::runtime_error("ResidentMLPPlan: no completion within the wait bound");
+          }
+        }
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+      }
+      ++runs_;
+      t_[1] += std::chrono::duration<double, std::micro>(clk::now() - t1).count();
+    }
+    return true;
+  }
+
+  // door = -1, then wait for the launch to finish (the variables hold the
+  // trained values either way: every step writes them through)
+  void stop() {
+    if (!alive_) return;
+    __atomic_store_n(door_, -1LL, __ATOMIC_RELEASE);
+    reap();
+  }
+
+  bool alive() const { return alive_; }
+  int64_t runs() const { return runs_; }
+  int64_t launches() const { return launch_id_; }
+  at::Tensor host_metrics() const {
+    return at::from_blob(out_, {3}, at::TensorOptions().dtype(at::kFloat));
+  }
+  py::dict timing() const {
+    py::dict d;
+    const double n = runs_ > 0 ? (double)runs_ : 1.0;
+    d["feed_us"] = t_[0] / n;
+    d["wait_us"] = t_[1] / n;
+    d["runs"] = runs_;
+    d["launches"] = launch_id_;
+    return d;
+  }
+
+ private:
+  static constexpr int kRing = 64;
+
+  void reap() {
+    const hipError_t e = hipStreamSynchronize(st_);
+    alive_ = false;
+    hip_check(e, "ResidentMLPPlan: launch");
+    int err = 0;
+    hip_check(hipMemcpy(&err, err_.data_ptr(), sizeof(int), hipMemcpyDeviceToHost), "ResidentMLPPlan: err");
+    if (err != 0) {
+      dead_ = true;
+      throw std::runtime_error("ResidentMLPPlan: the resident kernel reported error " + std::to_string(err));
+    }
+  }
+
+  void launch() {
+    TORCH_CHECK(!dead_, "ResidentMLPPlan: failed earlier");
+    // whatever the caller's stream queued (initialisation, restores) lands first
+    hip_check(hipEventRecord(ev_, cur_stream()), "ResidentMLPPlan: event");
+    hip_check(hipStreamWaitEvent(st_, ev_, 0), "ResidentMLPPlan: wait");
+    hip_check(hipMemsetAsync(dctr_.data_ptr(), 0, dctr_.numel() * sizeof(int), st_), "ResidentMLPPlan: counters");
+    if (__atomic_load_n(door_, __ATOMIC_ACQUIRE) < 0) __atomic_store_n(door_, runs_, __ATOMIC_RELEASE);   // after stop()
+    ++launch_id_;
+    hip_check(dtfk_mlp_persist_f32_resident(
+                  stage_.data_ptr(), B_, W1_.data_ptr<float>(), W2_.data_ptr<float>(), b1_.data_ptr<float>(),
+                  b2_.data_ptr<float>(), lrdev_.data_ptr<float>(), metrics_.data_ptr<float>(), kRing, act_,
+                  naive_ ? 1 : 0, reinterpret_cast<long long*>(kgstep_.data_ptr<int64_t>()),
+                  reinterpret_cast<unsigned long long*>(seq_.data_ptr<int64_t>()), xbuf_.data_ptr(),
+                  err_.data_ptr<int>(), timeout_, reinterpret_cast<const long long*>(dmail_),
+                  dmail_ + 512, rec_h_, reinterpret_cast<const float*>(dmail_ + 256),
+                  reinterpret_cast<float*>(dmail_ + 192), reinterpret_cast<long long*>(dmail_ + 64),
+                  reinterpret_cast<long long*>(dmail_ + 128), launch_id_, runs_, idle_,
+                  gkind_ ? gstep_.data_ptr() : nullptr, gkind_, reinterpret_cast<unsigned*>(dctr_.data_ptr<int>()),
+                  st_),
+              "ResidentMLPPlan: launch");
+    alive_ = true;
+  }
+
+  at::Tensor W1_, b1_, W2_, b2_, gstep_, stage_, xbuf_, seq_, kgstep_, err_, lrdev_, metrics_, dctr_;
+  int B_, act_, gkind_ = 0;
+  bool naive_;
+  int64_t rec_h_ = 0;
+  void* mail_ = nullptr;
+  char* dmail_ = nullptr;
+  long long* door_ = nullptr;
+  long long* done_ = nullptr;
+  long long* state_ = nullptr;
+  float* out_ = nullptr;
+  float* lr_ = nullptr;
+  uint8_t* recs_ = nullptr;
+  long long idle_ = 0, timeout_ = 0;
+  double wait_s_ = 5.0;
+  hipStream_t st_ = nullptr;
+  hipEvent_t ev_ = nullptr;
+  bool alive_ = false, dead_ = false;
+  long long runs_ = 0, launch_id_ = 0;
+  double t_[2] = {0, 0};
+};
+
 void init_mlp(py::module& m) {
+  py::class_<ResidentMLPPlan>(m, "ResidentMLPPlan")
+      .def(py::init<at::Tensor, at::Tensor, at::Tensor, at::Tensor, c10::optional<at::Tensor>, int, int, bool, double,
+                    double>(),
+           py::arg("W1"), py::arg("b1"), py::arg("W2"), py::arg("b2"), py::arg("gstep"), py::arg("B"), py::arg("act"),
+           py::arg("naive"), py::arg("idle_s") = 0.1, py::arg("timeout_s") = 10.0)
+      .def("run_u8", &ResidentMLPPlan::run_u8, py::arg("xu8"), py::arg("y"), py::arg("lr"))
+      .def("stop", &ResidentMLPPlan::stop)
+      .def("alive", &ResidentMLPPlan::alive)
+      .def("runs", &ResidentMLPPlan::runs)
+      .def("launches", &ResidentMLPPlan::launches)
+      .def("host_metrics", &ResidentMLPPlan::host_metrics)
+      .def("timing", &ResidentMLPPlan::timing);
   py::class_<GraphStepPlan>(m, "GraphStepPlan")
       .def(py::init<at::Tensor, at::Tensor, at::Tensor, at::Tensor, c10::optional<at::Tensor>, int, int, bool, bool>(),
            py::arg("W1"), py::arg("b1"), py::arg("W2"), py::arg("b2"), py::arg("gstep"), py::arg("B"), py::arg("act"),

@@ -10,8 +10,10 @@
 #include <c10/hip/HIPStream.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace dtf {
@@ -19,6 +21,17 @@ namespace dtf {
 #define RCCL_CHECK(cmd)                                                              \
   do {                                                                               \
     ncclResult_t r_ = (cmd);                                                         \
+    if (r_ != ncclSuccess)                                                           \
+      throw std::runtime_error(std::string("RCCL error ") + ncclGetErrorString(r_) + \
+                               " at " #cmd);                                         \
+  } while (0)
+
+// calls on a non-blocking communicator may return ncclInProgress: wait for the
+// communicator to settle (bounded by the init timeout)
+#define RCCL_CALL(cmd)                                                               \
+  do {                                                                               \
+    ncclResult_t r_ = (cmd);                                                         \
+    if (r_ == ncclInProgress && nonblocking_) r_ = poll_(timeout_s_);                \
     if (r_ != ncclSuccess)                                                           \
       throw std::runtime_error(std::string("RCCL error ") + ncclGetErrorString(r_) + \
                                " at " #cmd);                                         \
@@ -63,12 +76,36 @@ int rccl_version() {
 
 class RcclComm {
  public:
-  RcclComm(py::bytes uid, int nranks, int rank) : nranks_(nranks), rank_(rank) {
+  // timeout_s > 0: non-blocking init (ncclCommInitRankConfig, blocking = 0)
+  // polled until it completes, aborted after timeout_s -- a peer that never
+  // arrives or a fabric that never comes up ends in an exception, not a hang.
+  // The communicator then stays non-blocking: every call is followed by wait_()
+  // (a call may return ncclInProgress while RCCL finishes its host-side work).
+  RcclComm(py::bytes uid, int nranks, int rank, double timeout_s = 0.0) : nranks_(nranks), rank_(rank) {
     std::string s = uid;
     if (s.size() != sizeof(ncclUniqueId)) throw std::runtime_error("bad unique id size");
     ncclUniqueId id;
     memcpy(&id, s.data(), sizeof(id));
-    RCCL_CHECK(ncclCommInitRank(&comm_, nranks, id, rank));
+    if (timeout_s <= 0.0) {
+      RCCL_CHECK(ncclCommInitRank(&comm_, nranks, id, rank));
+      return;
+    }
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    nonblocking_ = true;
+    timeout_s_ = timeout_s;
+    ncclResult_t r;
+    {
+      py::gil_scoped_release nogil;
+      r = ncclCommInitRankConfig(&comm_, nranks, id, rank, &cfg);
+      if (r == ncclInProgress || (r == ncclSuccess && comm_ != nullptr)) r = poll_(timeout_s);
+    }
+    if (r != ncclSuccess) {
+      if (comm_) ncclCommAbort(comm_);
+      comm_ = nullptr;
+      throw std::runtime_error(std::string("RCCL init failed: ") +
+                               (r == ncclInProgress ? "timed out" : ncclGetErrorString(r)));
+    }
   }
   ~RcclComm() {
     if (comm_) ncclCommDestroy(comm_);
@@ -78,31 +115,31 @@ class RcclComm {
 
   void all_reduce(at::Tensor t, const std::string& op) {
     check(t);
-    RCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()),
+    RCCL_CALL(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()),
                              to_op(op), comm_, cur_stream()));
   }
   void all_reduce_out(at::Tensor src, at::Tensor dst, const std::string& op) {
     check(src); check(dst);
-    RCCL_CHECK(ncclAllReduce(src.data_ptr(), dst.data_ptr(), src.numel(),
+    RCCL_CALL(ncclAllReduce(src.data_ptr(), dst.data_ptr(), src.numel(),
                              to_nccl(src.scalar_type()), to_op(op), comm_, cur_stream()));
   }
   void broadcast(at::Tensor t, int root) {
     check(t);
-    RCCL_CHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), root,
+    RCCL_CALL(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), root,
                              comm_, cur_stream()));
   }
   // dst holds nranks * src.numel() elements
   void all_gather(at::Tensor src, at::Tensor dst) {
     check(src); check(dst);
     if (dst.numel() != src.numel() * nranks_) throw std::runtime_error("all_gather size mismatch");
-    RCCL_CHECK(ncclAllGather(src.data_ptr(), dst.data_ptr(), src.numel(),
+    RCCL_CALL(ncclAllGather(src.data_ptr(), dst.data_ptr(), src.numel(),
                              to_nccl(src.scalar_type()), comm_, cur_stream()));
   }
   // src holds nranks * dst.numel() elements
   void reduce_scatter(at::Tensor src, at::Tensor dst, const std::string& op) {
     check(src); check(dst);
     if (src.numel() != dst.numel() * nranks_) throw std::runtime_error("reduce_scatter size mismatch");
-    RCCL_CHECK(ncclReduceScatter(src.data_ptr(), dst.data_ptr(), dst.numel(),
+    RCCL_CALL(ncclReduceScatter(src.data_ptr(), dst.data_ptr(), dst.numel(),
                                  to_nccl(src.scalar_type()), to_op(op), comm_, cur_stream()));
   }
   // Variable-split all-to-all over grouped point-to-point (each xGMI peer link
@@ -118,23 +155,24 @@ class RcclComm {
     char* d = reinterpret_cast<char*>(dst.data_ptr());
     int64_t so = 0, ro = 0;
     hipStream_t st = cur_stream();
-    RCCL_CHECK(ncclGroupStart());
+    RCCL_CALL(ncclGroupStart());
     for (int p = 0; p < nranks_; ++p) {
-      if (send_counts[p] > 0) RCCL_CHECK(ncclSend(s + so * es, send_counts[p], dt, p, comm_, st));
-      if (recv_counts[p] > 0) RCCL_CHECK(ncclRecv(d + ro * es, recv_counts[p], dt, p, comm_, st));
+      if (send_counts[p] > 0) RCCL_CALL(ncclSend(s + so * es, send_counts[p], dt, p, comm_, st));
+      if (recv_counts[p] > 0) RCCL_CALL(ncclRecv(d + ro * es, recv_counts[p], dt, p, comm_, st));
       so += send_counts[p];
       ro += recv_counts[p];
     }
-    RCCL_CHECK(ncclGroupEnd());
+    RCCL_CALL(ncclGroupEnd());
   }
   void send(at::Tensor t, int peer) {
     check(t);
-    RCCL_CHECK(ncclSend(t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), peer, comm_, cur_stream()));
+    RCCL_CALL(ncclSend(t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), peer, comm_, cur_stream()));
   }
   void recv(at::Tensor t, int peer) {
     check(t);
-    RCCL_CHECK(ncclRecv(t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), peer, comm_, cur_stream()));
+    RCCL_CALL(ncclRecv(t.data_ptr(), t.numel(), to_nccl(t.scalar_type()), peer, comm_, cur_stream()));
   }
+  bool nonblocking() const { return nonblocking_; }
   void abort() {
     if (comm_) {
       ncclCommAbort(comm_);
@@ -154,15 +192,33 @@ class RcclComm {
     if (!t.is_cuda()) throw std::runtime_error("RCCL tensors must live on the GPU");
     if (!t.is_contiguous()) throw std::runtime_error("RCCL tensors must be contiguous");
   }
+  // wait until the communicator's pending host-side work settled: ncclSuccess,
+  // an error, or ncclInProgress after timeout_s
+  ncclResult_t poll_(double timeout_s) const {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+      ncclResult_t r = ncclSuccess;
+      const ncclResult_t q = ncclCommGetAsyncError(comm_, &r);
+      if (q != ncclSuccess) return q;
+      if (r != ncclInProgress) return r;
+      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s)
+        return ncclInProgress;
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+  }
   ncclComm_t comm_ = nullptr;
   int nranks_, rank_;
+  bool nonblocking_ = false;
+  double timeout_s_ = 0.0;
 };
 
 void init_comm(py::module& m) {
   m.def("rccl_unique_id", &rccl_unique_id);
   m.def("rccl_version", &rccl_version);
   py::class_<RcclComm>(m, "RcclComm")
-      .def(py::init<py::bytes, int, int>())
+      .def(py::init<py::bytes, int, int, double>(), py::arg("uid"), py::arg("nranks"), py::arg("rank"),
+           py::arg("timeout_s") = 0.0)
+      .def("nonblocking", &RcclComm::nonblocking)
       .def("rank", &RcclComm::rank)
       .def("size", &RcclComm::size)
       .def("all_reduce", &RcclComm::all_reduce)

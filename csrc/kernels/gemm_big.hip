@@ -23,11 +23,13 @@
 //    counted `s_waitcnt vmcnt(N)` and a raw s_barrier, so the prefetch
 //    survives the barrier (a workgroup LDS fence would drain it: the DMA is a
 //    pending LDS write on the vector-memory counter).
-//  * Measured (rocprofv3 PMC, 16384x3072x768): ~8 B/clk/CU of LDS-DMA fill
-//    with a 77 % L2 hit rate bounds the loop at ~25 % MFMA utilisation -- the
-//    operand delivery, not the MFMA issue, is this kernel's limit; hipBLASLt
-//    stays ~2x faster on the large forward/backward shapes, so models pick
-//    per shape (ops/big_gemm.py: use_native) and this kernel runs where it wins.
+//  * Measured: the round-2 single-phase loop (rocprofv3 PMC, 16384x3072x768:
+//    ~8 B/clk/CU of LDS-DMA fill, 77 % L2 hit rate, ~25 % MFMA utilisation) was
+//    operand-delivery bound at ~0.5x hipBLASLt; the 8-phase schedule (gemm_8ph)
+//    runs BERT-base's forward / input-gradient shapes at 0.93-1.09x hipBLASLt
+//    and its weight gradients at 0.82-1.03x (profiles/gemm_8ph_r3.txt).  Models
+//    pick per shape with hysteresis (ops/big_gemm.py: use_native keeps this
+//    kernel unless hipBLASLt wins by more than DTF_BIG_GEMM_MARGIN).
 //  * K-contiguous images are [rows][BK] with a 16-byte chunk XOR that puts the
 //    16 lanes of a ds_read_b128 group on 16 distinct slots of a bank row.
 //  * M/N-contiguous images are [BK k][rows] and are read with the hardware

@@ -85,6 +85,8 @@ constexpr int XTS = 128;           // x^T row stride (batch padded)
 constexpr int NCOMP = NJ * NQ;     // 28 compute workgroups: one XCD
 constexpr int THREADS = 512;
 constexpr int NCOP = 16;           // copier workgroups
+constexpr int NCOPR = 14;          // RES: copiers of one record (8 batch rows each)
+constexpr int RES_LR_BYTE = 124;   // RES: the run's lr rides in the record's label area (B <= 112)
 constexpr int GRID_PACKED = 8 * NCOMP;
 constexpr int GRID_SPREAD = NCOMP + NCOP;
 __host__ __device__ constexpr int tile0(int q) { return q == 0 ? 0 : 13 + 12 * (q - 1); }
@@ -189,6 +191,26 @@ struct Args {
   long long fault_step;     // fault injection (mlpf_set_fault(rank, step), tests of the bench's fallback):
   int fault_rank;           // that rank stops publishing its exchange flag from that global step on, a dead
                             // peer (-1: off; one skipped flag alone is absorbed: the flags are monotonic)
+  // flat master layout: W1 at params[0..78400); W2 / b1 / b2 through their own
+  // pointers (params + OFF_* for the flat trainer; a graph's own variables for the
+  // resident Session engine)
+  float* p_w2;
+  float* p_b1;
+  float* p_b2;
+  // RESIDENT (Session engine, compat/resident.py): one launch serves many
+  // Session.run calls.  Host -> device: a doorbell and 2 pinned record slots;
+  // device -> host: metrics + a done count in pinned memory.  Exits by itself
+  // after `idle` ticks without a doorbell (or on door < 0).
+  const long long* door;    // pinned: runs made ready (run k ready when door > k); < 0: stop
+  const uint8_t* host_recs; // pinned: 2 slots of rec_h bytes (B x 784 pixels, B labels)
+  const float* host_lr;     // pinned: lr of each slot
+  float* host_out;          // pinned: [loss, accuracy, global step] of the last run
+  long long* host_done;     // pinned: runs completed
+  long long* host_state;    // pinned: id of the launch that exited
+  long long launch_id, run0, idle;
+  void* gvar;               // the graph's global_step variable (kind 0 none, 1 f32, 2 i64, 3 i32, 4 f64)
+  int gvar_kind;
+  unsigned* dctr;           // device: [0] records staged, [8] runs released, [16] stop, [32] steps done
   int dbg;                  // profiling only (DTF_PERSIST_DBG): bit 0 = never stage the next step's x (wrong
                             // numerics; what the per-step LDS-DMA stage costs the hand-offs), bit 1 = head
                             // sub-phase stamps (slots 13-15, wave 0), bits 2 / 3 = stage (half) after the
@@ -524,13 +546,113 @@ __device__ void copier(const Args& a, int cid, uint8_t* smem) {
   if (tid == 0) { PRO(NCOMP + cid, 1); }
 }
 
+// RES copier: copier 0 watches the doorbell (system-scope loads of pinned host
+// memory) and releases run k to the others, or stops the launch after `idle`
+// ticks without one (or on door < 0) and reports that to the host; copiers
+// 0..13 each move 8 batch rows of the run's pinned record into device stage
+// slot (st & 1): row-major image, the x^T bytes of those rows (4x4 v_perm
+// transposes), labels + lr (copier 0); every store write-through (sc1), then
+// every wave's vmcnt(0), the barrier and one agent add to the staged count.
+__device__ void copier_res(const Args& a, int cid, uint8_t* smem) {
+  if (cid >= NCOPR) return;
+  const int tid = threadIdx.x;
+  constexpr int RR = 8;                                   // rows per copier
+  int* dec = reinterpret_cast<int*>(smem + RR * CROW);
+  const int B = a.B;
+  const int hb = (int)(2 * a.rec_h);
+  const auto hrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.host_recs), 0, hb, 0x00020000);
+  for (int st = 0;; ++st) {
+    const long long k = a.run0 + st;
+    if (tid == 0) {
+      int d = 1;
+      const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+      if (cid == 0) {
+        for (;;) {
+          const long long v = __hip_atomic_load(a.door, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          if (v < 0) { d = 0; break; }
+          if (v > k) break;
+          if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > a.idle) { d = 0; break; }
+          __builtin_amdgcn_s_sleep(2);
+        }
+        if (d) __hip_atomic_store(a.dctr + 8, (unsigned)(st + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else __hip_atomic_store(a.dctr + 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        for (;;) {
+          if (__hip_atomic_load(a.dctr + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)(st + 1)) break;
+          if (__hip_atomic_load(a.dctr + 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) { d = 0; break; }
+          if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > a.idle + a.timeout) { d = 0; break; }
+          __builtin_amdgcn_s_sleep(2);
+        }
+      }
+      *dec = d;
+    }
+    __syncthreads();
+    if (*dec == 0) break;
+    const int slot = (int)(k & 1);
+    const int hbase = slot * (int)a.rec_h;
+    const int r0 = RR * cid;
+    uint8_t* dst = const_cast<uint8_t*>(a.stage) + (long long)(st & 1) * REC;
+    constexpr int C16 = DIN / 16;   // 49
+    // pinned rows -> LDS (rows >= B zero): one 16-B system-scope load per thread
+    for (int t = tid; t < RR * C16; t += THREADS) {
+      const int rr = t / C16, cc = t % C16;
+      const int row = r0 + rr;
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(hrs, row < B ? hbase + row * DIN + 16 * cc : OOB_OFF,
+                                                            0, SYS);
+      *reinterpret_cast<u32x4*>(smem + rr * CROW + 16 * cc) = v;
+    }
+    __syncthreads();
+    for (int t = tid; t < RR * C16; t += THREADS) {
+      const int rr = t / C16, cc = t % C16;
+      const u32x4 v = *reinterpret_cast<const u32x4*>(smem + rr * CROW + 16 * cc);
+      __builtin_amdgcn_raw_buffer_store_b128(v, region_rsrc(dst, (int)REC), (r0 + rr) * DIN + 16 * cc, 0, 16);
+    }
+    // x^T: feature quad fq x row quad rq (2 per copier) -> 4 dwords of 4 batch bytes
+    for (int t = tid; t < (DIN / 4) * (RR / 4); t += THREADS) {
+      const int fq = t >> 1, rq = t & 1;
+      const uint8_t* p = smem + 4 * rq * CROW + 4 * fq;
+      const uint32_t q0 = *reinterpret_cast<const uint32_t*>(p);
+      const uint32_t q1 = *reinterpret_cast<const uint32_t*>(p + CROW);
+      const uint32_t q2 = *reinterpret_cast<const uint32_t*>(p + 2 * CROW);
+      const uint32_t q3 = *reinterpret_cast<const uint32_t*>(p + 3 * CROW);
+      const uint32_t t01 = __builtin_amdgcn_perm(q1, q0, 0x05010400u);
+      const uint32_t t23 = __builtin_amdgcn_perm(q3, q2, 0x05010400u);
+      const uint32_t u01 = __builtin_amdgcn_perm(q1, q0, 0x07030602u);
+      const uint32_t u23 = __builtin_amdgcn_perm(q3, q2, 0x07030602u);
+      const auto rs = region_rsrc(dst, (int)REC);
+      const int o = (int)XROW_BYTES + (4 * fq) * XTS + r0 + 4 * rq;
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_perm(t23, t01, 0x05040100u), rs, o, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_perm(t23, t01, 0x07060302u), rs, o + XTS, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_perm(u23, u01, 0x05040100u), rs, o + 2 * XTS, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_perm(u23, u01, 0x07060302u), rs, o + 3 * XTS, 0, 16);
+    }
+    if (cid == 0 && tid < 32) {   // labels (dwords 0..27) and the run's lr (byte RES_LR_BYTE)
+      uint32_t v;
+      if (4 * tid == RES_LR_BYTE) {
+        v = __float_as_uint(__hip_atomic_load(a.host_lr + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+      } else {
+        v = __builtin_amdgcn_raw_buffer_load_b32(hrs, 4 * tid < B ? hbase + B * DIN + 4 * tid : OOB_OFF, 0, SYS);
+        const int nv = B - 4 * tid;   // valid label bytes in this dword
+        if (nv < 4) v = nv <= 0 ? 0u : (v & ((1u << (8 * nv)) - 1u));
+      }
+      __builtin_amdgcn_raw_buffer_store_b32(v, region_rsrc(dst, (int)REC), (int)(XROW_BYTES + XT_BYTES) + 4 * tid, 0,
+                                            16);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(a.dctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (cid == 0 && tid == 0)   // no further run is taken by this launch
+    __hip_atomic_store(a.host_state, a.launch_id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // ------------------------------------------------------------------ compute
 // ACT 0 sigmoid, 1 relu; MULTI: N-GPU gradient exchange; SPLIT: the two big
 // GEMMs (forward x W1, weight gradient x^T dz2) on bf16 MFMA through the exact
 // three-way split of their fp32 operand (pixels are exact in bf16), so every
 // product is exact and accumulates in fp32 -- 16x16x32 bf16 MFMAs at 8x the
 // f32-MFMA rate; the head stays on f32-input MFMA
-template <int ACT, int NW, bool SPLIT>
+template <int ACT, int NW, bool SPLIT, bool RES>
 __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) {
   constexpr bool MULTI = NW > 1;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -574,19 +696,19 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
   if (tid < 256) {
     const int n = tid >> 4, cl = tid & 15;
     const int hn = 16 * j + n;
-    pv = (hn < HID && cl < NCLS) ? a.params[OFF_W2 + hn * NCLS + cl] : 0.f;
+    pv = (hn < HID && cl < NCLS) ? a.p_w2[hn * NCLS + cl] : 0.f;
   } else if (tid < 272) {
     const int hn = 16 * j + (tid - 256);
-    pv = hn < HID ? a.params[OFF_B1 + hn] : 0.f;
+    pv = hn < HID ? a.p_b1[hn] : 0.f;
   } else if (tid < 288) {
     const int cl = tid - 272;
-    pv = cl < NCLS ? a.params[OFF_B2 + cl] : 0.f;
+    pv = cl < NCLS ? a.p_b2[cl] : 0.f;
   }
   const unsigned long long seq0 = *a.seq;
   const long long gstep0 = *a.gstep;
   const float lr = *a.lr;
-  const float lrB = lr / (float)(B * (MULTI ? a.W : 1));
-  const float lrX = lrB * (1.f / 255.f);
+  float lrB = lr / (float)(B * (MULTI ? a.W : 1));   // RES: per run (the record's lr)
+  float lrX = lrB * (1.f / 255.f);
   for (int k = tid; k < 3 * 16 * LS; k += THREADS) a2T[k] = 0.f;   // a2T, dz2T, dz3T (batch pad stays 0)
   if constexpr (SPLIT)
     for (int k = tid; k < 3 * 16 * PS; k += THREADS) dzp[k] = (uint16_t)0;   // dz2 planes (batch pad 0)
@@ -675,7 +797,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
   const unsigned tag0 = (unsigned)(seq0 + 1ull);
   if (tid == 0)
     __hip_atomic_store(hdr + c, ((unsigned long long)tag0 << 32) | xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  stage_x(0, w, 8);   // the first step's stage: every wave a share
+  if constexpr (!RES) stage_x(0, w, 8);   // the first step's stage: every wave a share (RES: per run)
   if (w == 0) {   // lane cc watches workgroup cc's entry: all 28 polls in flight at once
     const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
     unsigned long long v = 0;
@@ -706,13 +828,103 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
   const bool l2_e1 = (*census & 1) != 0;
   const bool l2_e2 = (*census & 2) != 0;
   if (tid == 0) { PRO(c, 1); }
-  read_xf();
-  read_xt();
+  if constexpr (!RES) {
+    read_xf();
+    read_xt();
+  }
   if (tid == 0) { PRO(c, 2); }
+
+  // RES: the run's record -> LDS at the top of every step.  The copiers stored it
+  // write-through (sc1) and each added to the staged count after its waves'
+  // vmcnt(0) + barrier; one lane polls that count with sc1 loads, the workgroup
+  // barrier follows, and every load of the record is an sc1 load to registers
+  // (MI355X_MICROARCH.md "Valid forms", first table row) -> the LDS layout of
+  // stage_x (x^T chunks XOR-swizzled).  false: stop (idle / door < 0 / error).
+  auto res_stage = [&](int st) -> bool {
+    int* rflag = abort_flag + 2;
+    if (tid == 0) {
+      const unsigned need = (unsigned)NCOPR * (unsigned)(st + 1);
+      const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+      int v = 1;
+      for (;;) {
+        if (__hip_atomic_load(a.dctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need) break;
+        if (__hip_atomic_load(a.dctr + 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) { v = 0; break; }
+        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > a.idle + a.timeout) {   // copiers gone: bounded
+          atomicOr(a.err, 4);
+          v = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      *rflag = v;
+    }
+    __syncthreads();
+    if (*rflag == 0) return false;
+    const auto rs = region_rsrc(a.stage + (long long)(st & 1) * REC, (int)REC);
+    const int xr0 = 16 * tile0(q);
+#pragma unroll 4
+    for (int k = tid; k < XF_CHUNKS; k += THREADS) {
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (k / 13) * DIN + 16 * (k % 13) + xr0, 0, 16);
+      *reinterpret_cast<u32x4*>(smem + L_XF + 16 * k) = v;
+    }
+    const int xt0 = (int)XROW_BYTES + 16 * tile0(q) * XTS;
+#pragma unroll 4
+    for (int k = tid; k < XT_CHUNKS; k += THREADS) {
+      const int f = k >> 3;
+      if (f < 16 * nt) {
+        const int sw = (k & 7) ^ ((f >> 1) & 7);
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, xt0 + f * XTS + 16 * sw, 0, 16);
+        *reinterpret_cast<u32x4*>(smem + L_XT + 16 * k) = v;
+      }
+    }
+    if (tid < 8) {
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(XROW_BYTES + XT_BYTES) + 16 * tid, 0, 16);
+      *reinterpret_cast<u32x4*>(smem + L_LAB + 16 * tid) = v;
+    }
+    __syncthreads();
+    read_xf();
+    read_xt();
+    const float lr_run = *reinterpret_cast<const float*>(smem + L_LAB + RES_LR_BYTE);
+    lrB = lr_run / (float)B;
+    lrX = lrB * (1.f / 255.f);
+    return true;
+  };
+  int st_done = 0;
+  // fp32 master -> memory: W1 entries of this lane; W2 / b1 / b2 of block j from
+  // the q == 0 workgroups, b2 from workgroup 0.  wt: write-through (sc1) stores
+  // (RES: every step, read by torch kernels / copies between runs)
+  auto write_params = [&](bool wt) {
+    auto put = [wt](float* p, float v) {
+      if (wt) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else *p = v;
+    };
+    if (hv) {
+#pragma unroll
+      for (int k = 0; k < NTW; ++k)
+        if (tvk(k)) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) put(a.params + (16 * ftk(k) + 4 * g + e) * HID + hid, Wt[k][e]);
+        }
+    }
+    if (q == 0) {
+      if (tid < 256) {
+        const int n = tid >> 4, cl = tid & 15;
+        const int hn = 16 * j + n;
+        if (hn < HID && cl < NCLS) put(a.p_w2 + hn * NCLS + cl, w2s[tid]);
+      } else if (tid < 272) {
+        const int hn = 16 * j + (tid - 256);
+        if (hn < HID) put(a.p_b1 + hn, b1s[tid - 256]);
+      }
+    }
+    if (c == 0 && tid >= 272 && tid < 272 + NCLS) put(a.p_b2 + (tid - 272), b2s[tid - 272]);
+  };
 
   const PeerRs<NW> prs = peer_rsrcs<NW>(a.peer_base, MULTI ? a.W : 1);
   bool aborted = false;
   for (int st = 0; st < a.nsteps; ++st) {
+    if constexpr (RES) {
+      if (!res_stage(st)) break;
+    }
     const unsigned long long sq = seq0 + (unsigned long long)st + 1ull;
     const unsigned tag = (unsigned)sq;
     const int par = (int)(sq & 1ull);
@@ -761,7 +973,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
     if (w == 0) { PH(1); }
     lds_barrier();
     if (w == 0) { PH(2); }
-    const bool more = st + 1 < a.nsteps;
+    const bool more = !RES && st + 1 < a.nsteps;   // RES: the next run's record is staged at its top
     // everyone's reads of this step's stage retired at barrier A: wave 7 (idle
     // until P2) stages the next step while the others run the edges and the head
     int* hflag = reinterpret_cast<int*>(smem + L_HFLAG);   // [0..6] head of batch tile v done; [7] stage landed
@@ -1045,8 +1257,13 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
         const float cr = wave_sum(rl[128 + lane] + (hi ? rl[128 + lane + 64] : 0.f));
         if (lane == 63) {
           const int sl = (int)((gstep0 + st) % a.ring);
-          a.metrics[2 * sl] = ls / (float)B;
-          a.metrics[2 * sl + 1] = cr / (float)B;
+          if constexpr (RES) {   // read by the step's last arriver (sc1 hand-off)
+            __hip_atomic_store(a.metrics + 2 * sl, ls / (float)B, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.metrics + 2 * sl + 1, cr / (float)B, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          } else {
+            a.metrics[2 * sl] = ls / (float)B;
+            a.metrics[2 * sl + 1] = cr / (float)B;
+          }
         }
       }
       if constexpr (!MULTI) {
@@ -1242,38 +1459,64 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
         b2s[lane - 16] -= lrB * gb;
       }
     }
+    st_done = st + 1;
+    if constexpr (RES) {
+      // the run is complete once every compute workgroup's parameters are in
+      // memory: write-through stores, every wave's vmcnt(0), barrier, one agent add;
+      // the last arriver (its add's return value says so) publishes the metrics,
+      // global_step and the done count to pinned host memory
+      __syncthreads();   // wave 7's LDS updates of W2 / b1 / b2
+      write_params(true);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        const unsigned old = __hip_atomic_fetch_add(a.dctr + 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == (unsigned)NCOMP * (unsigned)(st + 1) - 1u) {
+          const int sl = (int)((gstep0 + st) % a.ring);
+          const float ls = __hip_atomic_load(a.metrics + 2 * sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const float ac = __hip_atomic_load(a.metrics + 2 * sl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          float gs = (float)(gstep0 + st + 1);
+          if (a.gvar_kind == 1) {
+            float* gp = static_cast<float*>(a.gvar);
+            gs = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1.f;
+            __hip_atomic_store(gp, gs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          } else if (a.gvar_kind == 2) {
+            long long* gp = static_cast<long long*>(a.gvar);
+            const long long v = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+            __hip_atomic_store(gp, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            gs = (float)v;
+          } else if (a.gvar_kind == 3) {
+            int* gp = static_cast<int*>(a.gvar);
+            const int v = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+            __hip_atomic_store(gp, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            gs = (float)v;
+          } else if (a.gvar_kind == 4) {
+            double* gp = static_cast<double*>(a.gvar);
+            const double v = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1.0;
+            __hip_atomic_store(gp, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            gs = (float)v;
+          }
+          __hip_atomic_store(a.host_out, ls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(a.host_out + 1, ac, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(a.host_out + 2, gs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __hip_atomic_store(a.host_done, a.run0 + st + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      }
+    }
   }
   if (aborted) return;
   __syncthreads();   // wave 7's last small-parameter update
   if (tid == 0) { PRO(c, 3); }
 
   // ---- write back (fp32 master), global step, exchange sequence, end stamp
-  if (hv) {
-#pragma unroll
-    for (int k = 0; k < NTW; ++k)
-      if (tvk(k)) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) a.params[(16 * ftk(k) + 4 * g + e) * HID + hid] = Wt[k][e];
-      }
-  }
-  if (q == 0) {
-    if (tid < 256) {
-      const int n = tid >> 4, cl = tid & 15;
-      const int hn = 16 * j + n;
-      if (hn < HID && cl < NCLS) a.params[OFF_W2 + hn * NCLS + cl] = w2s[tid];
-    } else if (tid < 272) {
-      const int hn = 16 * j + (tid - 256);
-      if (hn < HID) a.params[OFF_B1 + hn] = b1s[tid - 256];
-    }
-  }
-  if (c == 0) {
-    if (tid >= 272 && tid < 272 + NCLS) a.params[OFF_B2 + (tid - 272)] = b2s[tid - 272];
-    if (tid == 300) {
-      *a.gstep = gstep0 + a.nsteps;
-      *a.seq = seq0 + (unsigned long long)a.nsteps;
-      if (a.step_ts != nullptr)
-        a.step_ts[(gstep0 + a.nsteps) % a.ts_ring] = (long long)__builtin_amdgcn_s_memrealtime();
-    }
+  // (RES: the steps that ran -- the sequence never falls behind the tags in use)
+  write_params(false);
+  if (c == 0 && tid == 300) {
+    *a.gstep = gstep0 + st_done;
+    *a.seq = seq0 + (unsigned long long)st_done;
+    if (a.step_ts != nullptr)
+      a.step_ts[(gstep0 + st_done) % a.ts_ring] = (long long)__builtin_amdgcn_s_memrealtime();
   }
   if (tid == 0) { PRO(c, 5); }
 }
@@ -1283,7 +1526,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
 // L2); the first NCOP other blocks copy, the rest exit.  spread (several ranks on
 // one GPU, tests): compute = blocks 0..27, copiers = 28..43.  Placement is speed
 // only: the census above decides each edge's store flavour.
-template <int ACT, int NW, bool SPLIT>
+template <int ACT, int NW, bool SPLIT, bool RES = false>
 __global__ __launch_bounds__(THREADS, 1) void mlp_persist_f32(Args a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int b = blockIdx.x;
@@ -1294,10 +1537,11 @@ __global__ __launch_bounds__(THREADS, 1) void mlp_persist_f32(Args a) {
     if ((b & 7) == 0) c = b >> 3; else cid = b - (b >> 3) - 1;
   }
   if (c >= 0) {
-    if (a.nsteps > 0) compute<ACT, NW, SPLIT>(a, c / NQ, c % NQ, smem);
+    if (a.nsteps > 0) compute<ACT, NW, SPLIT, RES>(a, c / NQ, c % NQ, smem);
     return;
   }
-  if (cid < NCOP) copier(a, cid, smem);
+  if constexpr (RES) copier_res(a, cid, smem);
+  else if (cid < NCOP) copier(a, cid, smem);
 }
 
 }  // namespace mlpf
@@ -1334,6 +1578,19 @@ hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int n
   a.B = B;
   a.nsteps = nsteps;
   a.params = params;
+  a.p_w2 = params + OFF_W2;
+  a.p_b1 = params + OFF_B1;
+  a.p_b2 = params + OFF_B2;
+  a.door = nullptr;
+  a.host_recs = nullptr;
+  a.host_lr = nullptr;
+  a.host_out = nullptr;
+  a.host_done = nullptr;
+  a.host_state = nullptr;
+  a.launch_id = a.run0 = a.idle = 0;
+  a.gvar = nullptr;
+  a.gvar_kind = 0;
+  a.dctr = nullptr;
   a.lr = lr;
   a.metrics = metrics;
   a.ring = ring;
@@ -1394,6 +1651,75 @@ hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int n
   const int which = (act == 0 ? 0 : 1) + 2 * nwi + (split ? 8 : 0);
   const int grid = spread ? GRID_SPREAD : GRID_PACKED;
   hipLaunchKernelGGL(kerns[which], dim3(grid), dim3(THREADS), lds, stream, a);
+  return hipGetLastError();
+}
+
+// The resident Session engine (compat/resident.py, csrc/bind_mlp.cpp
+// ResidentMLPPlan): ONE launch serves Session.run calls until `idle` ticks pass
+// without a doorbell or the host writes door < 0.  One GPU, the reference's
+// precision (SPLIT), packed placement; the graph's own W1 / W2 / b1 / b2 tensors
+// and global_step variable are read at launch and written through every step.
+hipError_t dtfk_mlp_persist_f32_resident(void* stage, int B, float* W1, float* W2, float* b1, float* b2, const float* lr,
+                                         float* metrics, int ring, int act, int naive, long long* gstep,
+                                         unsigned long long* seq, void* xbuf, int* err, long long timeout,
+                                         const long long* door, const void* host_recs, long long rec_h,
+                                         const float* host_lr, float* host_out, long long* host_done,
+                                         long long* host_state, long long launch_id, long long run0, long long idle,
+                                         void* gvar, int gvar_kind, unsigned* dctr, hipStream_t stream) {
+  using namespace dtfk::mlpf;
+  if (B < 1 || B > BROWS || rec_h < (long long)B * (DIN + 1) || gvar_kind < 0 || gvar_kind > 4 ||
+      (gvar_kind != 0 && gvar == nullptr))
+    return hipErrorInvalidValue;
+  Args a;
+  std::memset(&a, 0, sizeof(a));
+  a.stage = static_cast<const uint8_t*>(stage);
+  a.rec_h = rec_h;
+  a.B = B;
+  a.nsteps = 0x7fffffff;   // bounded by the doorbell / idle exit
+  a.params = W1;
+  a.p_w2 = W2;
+  a.p_b1 = b1;
+  a.p_b2 = b2;
+  a.lr = lr;
+  a.metrics = metrics;
+  a.ring = ring;
+  a.act = act;
+  a.naive = naive;
+  a.gstep = gstep;
+  a.seq = seq;
+  a.xbuf = static_cast<uint8_t*>(xbuf);
+  a.err = err;
+  a.timeout = timeout;
+  a.ts_ring = 1;
+  a.W = 1;
+  a.gmode = 1;
+  a.fault_rank = -1;
+  a.fault_step = -1;
+  a.door = door;
+  a.host_recs = static_cast<const uint8_t*>(host_recs);
+  a.host_lr = host_lr;
+  a.host_out = host_out;
+  a.host_done = host_done;
+  a.host_state = host_state;
+  a.launch_id = launch_id;
+  a.run0 = run0;
+  a.idle = idle;
+  a.gvar = gvar;
+  a.gvar_kind = gvar_kind;
+  a.dctr = dctr;
+  constexpr size_t lds = LDS_BYTES;
+  typedef void (*Kern)(Args);
+  static const Kern kerns[2] = {mlp_persist_f32<0, 1, true, true>, mlp_persist_f32<1, 1, true, true>};
+  static bool attr_set = false;
+  if (!attr_set) {
+    for (Kern k : kerns) {
+      const hipError_t e =
+          hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+    }
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kerns[act == 0 ? 0 : 1], dim3(GRID_PACKED), dim3(THREADS), lds, stream, a);
   return hipGetLastError();
 }
 

@@ -463,6 +463,8 @@ class Variable(Tensor):
         return Operation(f, [self, delta], self.op_name + "/AssignAdd", op_type="AssignAdd")
 
     def load(self, value, session=None):
+        from . import resident
+        resident.quiesce_all()         # a resident engine holds this graph's weights in registers
         with torch.no_grad():
             self.value.data.copy_(torch.as_tensor(np.asarray(value)).to(self.value.device, self.value.dtype))
 

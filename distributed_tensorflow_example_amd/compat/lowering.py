@@ -66,6 +66,14 @@ def _train_mod():
     return m
 
 
+def _resident_mod():
+    m = _MODS.get("resident")
+    if m is None:
+        from . import resident as m
+        _MODS["resident"] = m
+    return m
+
+
 def _debug_mod():
     m = _MODS.get("debug")
     if m is None:
@@ -225,6 +233,8 @@ class MLPStepPlan(_PlanBase):
         self._fetch_ok: Dict[tuple, bool] = {}
         self.a2buf = self.dz2buf = self.metrics = None
         self.steps = 0
+        self._rplan = None           # compat/resident.py handle (one worker, uint8 loader batches)
+        self.resident_steps = 0
 
     # -------------------------------------------------------------- feeds
     @staticmethod
@@ -280,6 +290,7 @@ class MLPStepPlan(_PlanBase):
             return False
         if self._run_native_plan(ctx, flat, W1, b1, W2, b2):
             return True
+        _resident_mod().quiesce_all()   # the kernels below update the variables a resident engine holds
         xy = self._packed_feeds(ctx, W1.device)
         x, y = xy if xy is not None else (ctx.eval(pat.x), ctx.eval(pat.ylab))
         if not (isinstance(x, torch.Tensor) and isinstance(y, torch.Tensor) and x.is_cuda):
@@ -384,7 +395,7 @@ class MLPStepPlan(_PlanBase):
         gv = getattr(gs_var, "value", None) if gs_var is not None else None
         fast = (id(W1), id(b1), id(W2), id(b2), id(gv), fx.shape, fy.size)
         if getattr(self, "_fast_key", None) != fast:
-            if not self._build_native_plan(fx, fy, W1, b1, W2, b2, gs_var, gv):
+            if not self._build_native_plan(fx, fy, W1, b1, W2, b2, gs_var, gv, w):
                 self._fast_key = None
                 return False
             self._fast_key = fast
@@ -394,8 +405,26 @@ class MLPStepPlan(_PlanBase):
         needs, gs_seed, scalars = self._needs(flat, gs_var, self._gstep)
         fy2 = (fy if fy.flags.c_contiguous else np.ascontiguousarray(fy)).reshape(B, C)
         u8 = getattr(fx, "u8", None)
-        if (u8 is not None and self._cplan_u8 and not fx.flags.writeable and u8.shape == fx.shape
-                and u8.dtype == np.uint8 and fx.shape[1] % 4 == 0):
+        u8_ok = (u8 is not None and self._cplan_u8 and not fx.flags.writeable and u8.shape == fx.shape
+                 and u8.dtype == np.uint8 and fx.shape[1] % 4 == 0)
+        res = _resident_mod()
+        if u8_ok and self._rplan is not None and self._rplan.run_u8(u8, fy2, float(opt._lr_value())):
+            # the resident engine (compat/resident.py): no launch / completion per run
+            ctx.resident_ran = True
+            m = self._rplan.out if scalars else torch.from_numpy(self._rplan.out.copy())
+            memo = ctx.memo
+            memo[id(pat.loss)] = m[0]
+            if self.accuracy is not None:
+                memo[id(self.accuracy)] = m[1]
+            if gs_seed:
+                memo[id(gs_var)] = self._rplan.out[2]
+            memo[id(self.op)] = None
+            self.steps += 1
+            self.resident_steps = getattr(self, "resident_steps", 0) + 1
+            return True
+        if res.any_live():
+            res.quiesce_all()           # the launched plans below write the same variables
+        if u8_ok:
             # data/mnist.py PixelBatch: ship the uint8 source (bit-identical, 4x fewer bytes)
             self._cplan.run_u8(u8, fy2, float(opt._lr_value()), bool(needs))
         else:
@@ -414,7 +443,7 @@ class MLPStepPlan(_PlanBase):
         self.steps += 1
         return True
 
-    def _build_native_plan(self, fx, fy, W1, b1, W2, b2, gs_var, gv) -> bool:
+    def _build_native_plan(self, fx, fy, W1, b1, W2, b2, gs_var, gv, w=None) -> bool:
         from .. import _native
 
         pat = self.pat
@@ -443,6 +472,18 @@ class MLPStepPlan(_PlanBase):
             self._hm_np = self._cplan.host_metrics().numpy()
             # the captured-graph plan takes float32 feeds only (run_u8 is direct-launch)
             self._cplan_u8 = not self._cplan.use_graph()
+            # the resident engine: one worker, the reference's shapes, uint8 loader batches
+            # (compat/resident.py; the persistent kernel takes batches <= its max)
+            old = getattr(self, "_rplan", None)
+            if old is not None:
+                old.stop()
+            self._rplan = None
+            res = _resident_mod()
+            C_ = _native.load()
+            if (res.enabled() and self._cplan_u8 and (w is None or w.world_size == 1) and K == 784 and H == 100
+                    and C == 10 and B <= C_.mlpf_max_batch()):
+                self._rplan = res.ResidentHandle(C_.ResidentMLPPlan(
+                    W1.data, b1.data, W2.data, b2.data, gstep, B, pat.act, bool(pat.naive), res.idle_s()))
         self._cplan_BC = (B, C)
         self._gstep = gstep
         return True
@@ -625,6 +666,7 @@ class SparseLRStepPlan(_PlanBase):
         w = _world_or_local()
         if type(opt) is not GradientDescentOptimizer or (w.world_size > 1 and not opt.sync_replicas):
             return False
+        _resident_mod().quiesce_all()
         table = p.W.table
         if table.hogwild is not None:
             return False

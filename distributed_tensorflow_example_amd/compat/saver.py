@@ -368,6 +368,8 @@ class Saver:
         return prefix
 
     def restore(self, sess=None, save_path: str = None):
+        from . import resident
+        resident.quiesce_all()         # restored values must not be overwritten by a resident engine
         prefix = _resolve(save_path)
         idx = read_bundle_index(prefix)
         missing = []

@@ -17,6 +17,7 @@ import numpy as np
 import torch
 
 from . import lowering as _lowering
+from . import resident as _resident
 from .graph import Operation, RunContext, Tensor, get_default_graph
 
 _tls = threading.local()
@@ -89,6 +90,8 @@ class Session:
         ctx.session = self
         ctx.options = options
         _lowering.try_lower(self, fetches, ctx)         # fused steps for matched train ops
+        if _resident._LIVE and not getattr(ctx, "resident_ran", False):
+            _resident.quiesce_all()      # this run may write variables a resident engine holds
         for hook in _pre_run_hooks(fetches):           # async train ops: pull the ps variables first
             hook()
         out = self._run(fetches, ctx)
@@ -129,6 +132,7 @@ class Session:
 
     # ---------------------------------------------------------------- lifecycle
     def close(self):
+        _resident.quiesce_all()
         self._closed = True
 
     @property

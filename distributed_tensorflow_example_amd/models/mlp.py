@@ -165,7 +165,11 @@ class FusedMLPTrainer:
         self.ipc_parity = 0
         self.ipc_mode = None
         self.ipc_timeout_s = float(ipc_timeout_s)
-        if self.world_size > 1:
+        if self.world_size > 1 and allreduce == "external":
+            # the caller owns the gradient exchange (PersistentMLPRunner: in-kernel
+            # over IPC): no exchange buffers, no RCCL communicator
+            self.allreduce = "external"
+        elif self.world_size > 1:
             self.allreduce = "rccl"
             if allreduce in ("ipc", "ipc-fused", "ipc-apply", "auto"):
                 try:
@@ -178,6 +182,14 @@ class FusedMLPTrainer:
                     import warnings
 
                     warnings.warn(f"IPC all-reduce unavailable ({e}); using RCCL")
+            if self.allreduce == "rccl":
+                # created here, collectively, only when this trainer's exchange is RCCL
+                # (RuntimeError if it cannot come up: the caller falls back)
+                world.ensure_comm()
+        # RCCL and the IPC kernels capture into hipGraphs; a gloo all-reduce (ranks
+        # sharing one GPU in tests) does not
+        self.graph_safe = (self.world_size == 1 or self.allreduce.startswith("ipc")
+                           or (world is not None and world.comm is not None))
         self.shadows_stale = False   # set by PersistentMLPRunner (it updates only the fp32 master)
         self.set_params(init_params(seed))
 
@@ -275,7 +287,7 @@ class FusedMLPTrainer:
             kind = 1 if self.grad_dtype == torch.float32 else 2
             C.mlp_wgrad(x, x_off, x_kind, self.dz2T, B, self.partials, self.params, self.W1T,
                         self.W2T, self.W2N, self.grads, kind, self.lr, self.metrics, self.gstep)
-            self.world.comm.all_reduce(self.grads, "sum")
+            self.world.all_reduce(self.grads, "sum")
             C.mlp_apply_flat(self.params, self.grads, self.lr, 1.0 / self.world_size, self.W1T,
                              self.W2T, self.W2N)
 
@@ -332,6 +344,7 @@ class GemmMLPTrainer:
         self.gstep = torch.zeros(1, dtype=torch.int64, device=dev)
         self.allreduce = "none"
         if self.world_size > 1:
+            world.ensure_comm()    # collective; None on gloo worlds
             self.allreduce = "rccl" if world.comm is not None else world.backend
         # RCCL calls capture into hipGraphs; a gloo all-reduce (ranks sharing
         # one GPU in tests) does not

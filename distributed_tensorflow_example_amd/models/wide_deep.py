@@ -79,6 +79,8 @@ class WideDeep(StaticStepMixin):
                 for p in self.dense_params:
                     self.world.broadcast(p.data, 0)
         self.comm_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        if self.device.type == "cuda":
+            self.world.ensure_comm()   # collective: a lazy world's RCCL communicator, before any bucket
         self.global_step = 0
         self._graphed = None
 

@@ -191,6 +191,8 @@ class DistributedDataParallel(torch.nn.Module):
         for p in params:
             grad_sink.install(p, self._on_grad if overlap else _no_hook)
         self.comm_stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
+        if self.device.type == "cuda":
+            self.world.ensure_comm()   # collective: a lazy world's RCCL communicator, before any bucket
         if broadcast_params and self.world.world_size > 1:
             with torch.no_grad():
                 for p in params:

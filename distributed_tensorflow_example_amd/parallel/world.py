@@ -34,8 +34,11 @@ class World:
     local_rank: int = 0
     device: torch.device = field(default_factory=lambda: torch.device("cpu"))
     backend: str = "none"          # "rccl" | "gloo" | "none"
-    comm: Any = None               # native RcclComm (GPU data plane)
+    comm: Any = None               # native RcclComm (GPU data plane); None until ensure_comm() when lazy
     pg_initialized: bool = False
+    comm_error: Optional[str] = None   # why the RCCL communicator could not be created (all ranks agree)
+    rccl_timeout_s: float = 120.0
+    _uid_source: Any = None        # callable(rank) -> RCCL unique id of rank 0 (store- or gloo-based)
 
     @property
     def is_chief(self) -> bool:
@@ -73,9 +76,56 @@ class World:
         return out
 
     # --------------------------------------------------------------- data plane
+    def ensure_comm(self):
+        """Create the RCCL communicator now if this world wants one and has none.
+
+        COLLECTIVE over the world's ranks (every rank must call it at the same
+        point: the data-plane methods below do, and so do trainers that issue
+        RCCL calls themselves).  Bounded: RCCL's init runs non-blocking and is
+        aborted after `rccl_timeout_s`; the ranks agree on the outcome over the
+        gloo control plane, so either every rank has a communicator or every rank
+        raises RuntimeError (recorded in `comm_error`; later calls re-raise it
+        without another attempt).  Returns the communicator, or None for worlds
+        without an RCCL data plane (one rank, gloo, CPU).  DTF_FAULT_RCCL_INIT=1
+        injects an init failure (tests of the fallback paths)."""
+        if self.comm is not None:
+            return self.comm
+        if self.comm_error is not None:
+            raise RuntimeError(self.comm_error)
+        fault = os.environ.get("DTF_FAULT_RCCL_INIT", "0") == "1"
+        if self.world_size == 1 or not self.pg_initialized or (self.backend != "rccl" and not fault):
+            return None
+        err = "RCCL init fault injected (DTF_FAULT_RCCL_INIT=1)" if fault else None
+        comm = None
+        if err is None:
+            try:
+                from .. import _native
+
+                C = _native.load()
+                uid = self._uid_source(self) if self._uid_source is not None else self._gloo_uid(C)
+                comm = C.RcclComm(uid, self.world_size, self.rank, float(self.rccl_timeout_s))
+            except Exception as e:  # noqa: BLE001
+                err = f"RCCL init failed on rank {self.rank}: {e}"
+        ok = self.host_all_reduce(0.0 if err is not None else 1.0, "min")
+        if ok < 1.0:
+            if comm is not None:
+                try:
+                    comm.abort()
+                except Exception:  # noqa: BLE001
+                    pass
+            self.comm_error = err or "RCCL init failed on a peer rank"
+            raise RuntimeError(self.comm_error)
+        self.comm = comm
+        return comm
+
+    def _gloo_uid(self, C):
+        return self.broadcast_object(C.rccl_unique_id() if self.rank == 0 else None, 0)
+
     def all_reduce(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
         if self.world_size == 1:
             return t
+        if t.is_cuda and self.backend == "rccl":
+            self.ensure_comm()
         if t.is_cuda and self.comm is not None:
             self.comm.all_reduce(t, op)
         else:
@@ -90,6 +140,8 @@ class World:
     def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if self.world_size == 1:
             return t
+        if t.is_cuda and self.backend == "rccl":
+            self.ensure_comm()
         if t.is_cuda and self.comm is not None:
             self.comm.broadcast(t, src)
         else:
@@ -100,6 +152,8 @@ class World:
         if self.world_size == 1:
             dst.copy_(src.reshape(dst.shape))
             return dst
+        if src.is_cuda and self.backend == "rccl":
+            self.ensure_comm()
         if src.is_cuda and self.comm is not None:
             self.comm.all_gather(src, dst)
         else:
@@ -110,6 +164,8 @@ class World:
         if self.world_size == 1:
             dst.copy_(src.reshape(dst.shape))
             return dst
+        if src.is_cuda and self.backend == "rccl":
+            self.ensure_comm()
         if src.is_cuda and self.comm is not None:
             self.comm.reduce_scatter(src, dst, op)
         else:
@@ -123,6 +179,8 @@ class World:
         if self.world_size == 1:
             dst[: recv_counts[0]].copy_(src[: send_counts[0]])
             return dst
+        if src.is_cuda and self.backend == "rccl":
+            self.ensure_comm()
         if src.is_cuda and self.comm is not None:
             inner = math.prod(src.shape[1:])   # counts are in rows; RCCL wants elements
             self.comm.all_to_all(src, [c * inner for c in send_counts], dst, [c * inner for c in recv_counts])
@@ -160,10 +218,15 @@ def _env_int(name: str, default: int) -> int:
 def init(rank: Optional[int] = None, world_size: Optional[int] = None,
          local_rank: Optional[int] = None, master_addr: Optional[str] = None,
          master_port: Optional[int] = None, backend: str = "auto",
-         timeout_s: float = 600.0) -> World:
+         timeout_s: float = 600.0, rccl: str = "eager", rccl_timeout_s: float = 120.0) -> World:
     """Initialise (idempotently) the process world.
 
     backend: "auto" -> "rccl" when a GPU is visible, else "gloo".
+    rccl: "eager" creates the RCCL communicator here; "lazy" leaves it to the
+    first `World.ensure_comm()` (the data-plane methods call it), so a program
+    whose data plane is something else (the persistent engine's in-kernel IPC
+    exchange) never depends on RCCL coming up.  Either way the init is bounded
+    by `rccl_timeout_s` and failures are agreed on by every rank.
     """
     global _WORLD
     if _WORLD is not None:
@@ -185,7 +248,8 @@ def init(rank: Optional[int] = None, world_size: Optional[int] = None,
         device = torch.device("cpu")
 
     w = World(rank=rank, world_size=world_size, local_rank=local_rank, device=device,
-              backend=backend if world_size > 1 else ("rccl" if device.type == "cuda" else "none"))
+              backend=backend if world_size > 1 else ("rccl" if device.type == "cuda" else "none"),
+              rccl_timeout_s=float(rccl_timeout_s))
     if device.type == "cpu":
         _cpu_threads(_env_int("LOCAL_WORLD_SIZE", world_size))
     if world_size > 1:
@@ -198,13 +262,8 @@ def init(rank: Optional[int] = None, world_size: Optional[int] = None,
             dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world_size,
                                     timeout=datetime.timedelta(seconds=timeout_s))
         w.pg_initialized = True
-        if backend == "rccl":
-            from .. import _native
-
-            C = _native.load()
-            uid = C.rccl_unique_id() if rank == 0 else None
-            uid = w.broadcast_object(uid, 0)
-            w.comm = C.RcclComm(uid, world_size, rank)
+        if backend == "rccl" and rccl == "eager":
+            w.ensure_comm()
     _WORLD = w
     return w
 
@@ -245,13 +304,16 @@ def init_from_rendezvous(rdv, backend: str = "auto", timeout_s: float = 600.0) -
                                 timeout=datetime.timedelta(seconds=timeout_s))
         w.pg_initialized = True
         if backend == "rccl":
-            from .. import _native
+            def uid_from_store(world, _n=[0]):
+                from .. import _native
 
-            C = _native.load()
-            if rank == 0:
-                rdv.store.set("rccl_uid", C.rccl_unique_id())
-            uid = rdv.store.get("rccl_uid", timeout_s)
-            w.comm = C.RcclComm(uid, world_size, rank)
+                key = f"rccl_uid/{_n[0]}"     # one key per attempt
+                _n[0] += 1
+                if world.rank == 0:
+                    rdv.store.set(key, _native.load().rccl_unique_id())
+                return rdv.store.get(key, timeout_s)
+            w._uid_source = uid_from_store
+            w.ensure_comm()
     _WORLD = w
     return w
 

@@ -1,7 +1,9 @@
 """Per-step cost of the compat graph path (examples/mnist_example.py's graph,
-no --fused): Session.run wall time per step with the lowered kernels vs the
-eager op-by-op path (DTF_GRAPH_LOWERING=0), plus device time of the three
-lowered kernels alone (CUDA events around graph_mlp_step).
+no --fused): Session.run wall time per step on the resident engine (MNIST
+loader batches, compat/resident.py), on the launched lowered kernels
+(DTF_RESIDENT_SESSION=0; loader batches and plain float32 feeds) and on the
+eager op-by-op path (DTF_GRAPH_LOWERING=0), plus device time of the lowered
+kernels alone (CUDA events around graph_mlp_step).
 
     python scripts/bench_graph_step.py [steps]
 """
@@ -33,9 +35,12 @@ def main():
     xs = np.stack([np.asarray(p) for p in pbs])     # the same values as plain float32 arrays
     ys = np.eye(10, dtype=np.float32)[rng.integers(0, 10, (64, B))]
     out = {}
-    for mode in ("u8", "1", "0"):
+    from distributed_tensorflow_example_amd.compat import resident as R
+
+    for mode in ("resident", "u8", "1", "0"):
         os.environ["DTF_GRAPH_LOWERING"] = "0" if mode == "0" else "1"
-        feeds = pbs if mode == "u8" else xs
+        os.environ["DTF_RESIDENT_SESSION"] = "1" if mode == "resident" else "0"
+        feeds = pbs if mode in ("resident", "u8") else xs
         g = _graph(tf)
         with tf.Session() as sess:
             sess.run(tf.global_variables_initializer())
@@ -47,7 +52,15 @@ def main():
             for i in range(steps):
                 sess.run(fetch, feed_dict={g["x"]: feeds[i % 64], g["y_"]: ys[i % 64]})
             torch.cuda.synchronize()
-            out[{"u8": "lowered_u8", "1": "lowered", "0": "eager"}[mode]] = (time.perf_counter() - t0) / steps * 1e3
+            out[{"resident": "resident", "u8": "lowered_u8", "1": "lowered", "0": "eager"}[mode]] = \
+                (time.perf_counter() - t0) / steps * 1e3
+            if mode == "resident":
+                plan = L.plan_for(g["train"])
+                out["resident_steps"] = int(plan.resident_steps)
+                rp = plan._rplan.plan
+                out["resident_split_us"] = {k: round(v, 2) if isinstance(v, float) else v
+                                            for k, v in rp.timing().items()}
+                R.quiesce_all()
             if mode == "u8":
                 cp = L.plan_for(g["train"])._cplan
                 t0 = time.perf_counter()
@@ -89,7 +102,11 @@ def main():
                                                    for k, v in cp.timing().items()}
         tf.reset_default_graph()
     os.environ.pop("DTF_GRAPH_LOWERING", None)
-    print(json.dumps({"native_plan_runs": out.get("native_plan_runs"),
+    os.environ.pop("DTF_RESIDENT_SESSION", None)
+    print(json.dumps({"session_run_ms_per_step_resident_loader_batches": round(out["resident"], 4),
+                      "resident_steps": out.get("resident_steps"),
+                      "resident_split_us": out.get("resident_split_us"),
+                      "native_plan_runs": out.get("native_plan_runs"),
                       "native_plan_hipgraph": out.get("native_plan_hipgraph"),
                       "native_call_us": round(out.get("native_call_us", 0.0), 2),
                       "native_call_split_us": out.get("native_call_split_us"),

@@ -205,9 +205,12 @@ def test_uint8_feed_is_bit_identical(native):
         assert torch.equal(a, b)
 
 
-def test_session_uses_uint8_feed_for_loader_batches():
+def test_session_uses_uint8_feed_for_loader_batches(monkeypatch):
     """examples/mnist_example.py's graph fed by the MNIST loader: the lowered
-    plan takes the uint8 path and matches a float-fed session bit for bit."""
+    plan takes the uint8 path and matches a float-fed session bit for bit
+    (the launched plan's uint8 path: the resident engine is off here, it has
+    tests of its own in test_resident_gpu.py)."""
+    monkeypatch.setenv("DTF_RESIDENT_SESSION", "0")
     import distributed_tensorflow_example_amd.compat as tf
     from distributed_tensorflow_example_amd.compat import lowering as L
     from distributed_tensorflow_example_amd.data.mnist import PixelBatch

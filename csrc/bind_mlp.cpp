@@ -1044,7 +1044,7 @@ void init_mlp(py::module& m) {
       .def(py::init<at::Tensor, at::Tensor, at::Tensor, at::Tensor, c10::optional<at::Tensor>, int, int, bool, double,
                     double>(),
            py::arg("W1"), py::arg("b1"), py::arg("W2"), py::arg("b2"), py::arg("gstep"), py::arg("B"), py::arg("act"),
-           py::arg("naive"), py::arg("idle_s") = 0.1, py::arg("timeout_s") = 10.0)
+           py::arg("naive"), py::arg("idle_s") = 0.002, py::arg("timeout_s") = 10.0)
       .def("run_u8", &ResidentMLPPlan::run_u8, py::arg("xu8"), py::arg("y"), py::arg("lr"))
       .def("stop", &ResidentMLPPlan::stop)
       .def("alive", &ResidentMLPPlan::alive)

@@ -1,0 +1,215 @@
+// The one-GPU sparse logistic-regression step of lr2.py as ONE host call
+// (csrc/kernels/sparse_lr.hip).  SparseLRPlan.run takes lr2.py's own feed
+// arrays -- labels y [B, 1], SparseTensor indices [nnz, 2] (row, column),
+// feature ids [nnz], values [nnz] (lr2.py:440-446) -- builds the CSR row
+// offsets (a stable counting sort when the COO entries are not in row order),
+// packs ids | offsets | values | labels into a pinned staging slot with the GIL
+// released, issues ONE host-to-device copy and the two step kernels on the
+// caller's stream, and returns without waiting (staging slots are double
+// buffered behind events).  SparseLRPlan.step runs the same kernels on device
+// tensors (models/sparse_lr.py, one worker).
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <pybind11/numpy.h>
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+extern "C" {
+hipError_t dtfk_slr_step(float* W, long long F, const long long* ids, const long long* offsets, const float* vals,
+                         const float* labels, float* bias, int B, const float* lr_ptr, float lr_val, float* dz,
+                         float* lrow, float* loss_out, int* bad, void* gvar, int gkind, hipStream_t stream);
+}
+
+namespace dtf {
+
+static void hck(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+static int64_t align16(int64_t v) { return (v + 15) / 16 * 16; }
+
+class SparseLRPlan {
+ public:
+  SparseLRPlan(at::Tensor W, at::Tensor bias, c10::optional<at::Tensor> gstep) : W_(W), bias_(bias) {
+    TORCH_CHECK(W.is_cuda() && W.scalar_type() == at::kFloat && W.is_contiguous() &&
+                    (W.dim() == 1 || (W.dim() == 2 && W.size(1) == 1)),
+                "SparseLRPlan: W must be a contiguous fp32 [F, 1] GPU table");
+    TORCH_CHECK(bias.is_cuda() && bias.scalar_type() == at::kFloat && bias.numel() == 1 && bias.is_contiguous(),
+                "SparseLRPlan: bias must be one fp32 GPU value");
+    F_ = W.size(0);
+    if (gstep.has_value()) {
+      const at::Tensor& g = *gstep;
+      TORCH_CHECK(g.is_cuda() && g.numel() == 1, "SparseLRPlan: device scalar global_step");
+      switch (g.scalar_type()) {
+        case at::kFloat: gkind_ = 1; break;
+        case at::kLong: gkind_ = 2; break;
+        case at::kInt: gkind_ = 3; break;
+        case at::kDouble: gkind_ = 4; break;
+        default: TORCH_CHECK(false, "SparseLRPlan: unsupported global_step dtype");
+      }
+      gstep_ = g;
+    }
+    auto fo = W.options();
+    loss_ = at::zeros({1}, fo);
+    bad_ = at::zeros({1}, fo.dtype(at::kInt));
+    for (int i = 0; i < 2; ++i) hck(hipEventCreateWithFlags(&ev_[i], hipEventDisableTiming), "hipEventCreate");
+  }
+  ~SparseLRPlan() {
+    for (auto& e : ev_)
+      if (e) (void)hipEventDestroy(e);
+  }
+
+  // lr2.py's feeds (numpy).  False: not applicable (dtypes, shapes, a row index
+  // outside [0, B)) -- nothing ran, the caller takes the general path.
+  bool run(py::array y, py::array idx, py::array ids, py::array vals, double lr) {
+    if (!y.dtype().is(py::dtype::of<float>()) || !idx.dtype().is(py::dtype::of<int64_t>()) ||
+        !ids.dtype().is(py::dtype::of<int64_t>()) || !vals.dtype().is(py::dtype::of<float>()))
+      return false;
+    const int64_t B = y.size(), n = ids.size();
+    if (B < 1 || B > (1 << 30) || vals.size() != n || (n > 0 && (idx.ndim() != 2 || idx.shape(0) != n || idx.shape(1) < 2)))
+      return false;
+    // strided views are fine: read through the numpy strides
+    const char* yb = static_cast<const char*>(y.data());
+    const char* ib = static_cast<const char*>(idx.data());
+    const char* fb = static_cast<const char*>(ids.data());
+    const char* vb = static_cast<const char*>(vals.data());
+    const int64_t ys = y.ndim() >= 1 ? y.strides(0) : 4;
+    const int64_t is0 = n > 0 ? idx.strides(0) : 0;
+    const int64_t fs = ids.ndim() >= 1 ? ids.strides(0) : 8, vs = vals.ndim() >= 1 ? vals.strides(0) : 4;
+    if (y.ndim() > 2 || ids.ndim() > 1 || vals.ndim() > 1 || (y.ndim() == 2 && y.shape(1) != 1 && y.shape(0) != 1))
+      return false;
+    const int64_t ys_el = (y.ndim() == 2 && y.shape(0) == 1) ? y.strides(1) : ys;
+    const int64_t o_ids = 0, o_off = align16(8 * n), o_val = o_off + align16(8 * (B + 1)),
+                  o_lab = o_val + align16(4 * n), total = o_lab + align16(4 * B);
+    const int slot = slot_ ^= 1;
+    bool ok = true;
+    {
+      py::gil_scoped_release nogil;
+      if (pending_[slot]) hck(hipEventSynchronize(ev_[slot]), "SparseLRPlan: staging slot");
+      pending_[slot] = false;
+      if (host_[slot].numel() < total) {
+        host_[slot] = at::empty({std::max<int64_t>(total, 1 << 20)}, at::TensorOptions().dtype(at::kByte).pinned_memory(true));
+      }
+      char* h = static_cast<char*>(host_[slot].data_ptr());
+      int64_t* hid = reinterpret_cast<int64_t*>(h + o_ids);
+      int64_t* hoff = reinterpret_cast<int64_t*>(h + o_off);
+      float* hval = reinterpret_cast<float*>(h + o_val);
+      float* hlab = reinterpret_cast<float*>(h + o_lab);
+      // rows -> CSR offsets (counting); in row order: copy straight through, else a
+      // stable counting sort by row (the same bags: the 'sum' combiner)
+      std::vector<int64_t>& cnt = cnt_;
+      cnt.assign((size_t)B + 1, 0);
+      bool sorted = true;
+      int64_t prev = 0;
+      for (int64_t j = 0; j < n; ++j) {
+        const int64_t r = *reinterpret_cast<const int64_t*>(ib + j * is0);
+        if (r < 0 || r >= B) {
+          ok = false;
+          break;
+        }
+        sorted = sorted && r >= prev;
+        prev = r;
+        ++cnt[(size_t)r + 1];
+      }
+      if (ok) {
+        for (int64_t b = 0; b < B; ++b) cnt[(size_t)b + 1] += cnt[(size_t)b];
+        std::memcpy(hoff, cnt.data(), sizeof(int64_t) * (size_t)(B + 1));
+        if (sorted) {
+          if (fs == 8) std::memcpy(hid, fb, 8 * (size_t)n);
+          else for (int64_t j = 0; j < n; ++j) hid[j] = *reinterpret_cast<const int64_t*>(fb + j * fs);
+          if (vs == 4) std::memcpy(hval, vb, 4 * (size_t)n);
+          else for (int64_t j = 0; j < n; ++j) hval[j] = *reinterpret_cast<const float*>(vb + j * vs);
+        } else {
+          for (int64_t j = 0; j < n; ++j) {
+            const int64_t r = *reinterpret_cast<const int64_t*>(ib + j * is0);
+            const int64_t d = cnt[(size_t)r]++;
+            hid[d] = *reinterpret_cast<const int64_t*>(fb + j * fs);
+            hval[d] = *reinterpret_cast<const float*>(vb + j * vs);
+          }
+        }
+        for (int64_t b = 0; b < B; ++b) hlab[b] = *reinterpret_cast<const float*>(yb + b * ys_el);
+      }
+    }
+    if (!ok) return false;
+    if (dev_.numel() < total) dev_ = at::empty({std::max<int64_t>(total, 1 << 20)}, W_.options().dtype(at::kByte));
+    if (dz_.numel() < B) {
+      dz_ = at::empty({std::max<int64_t>(B, 1024)}, W_.options());
+      lrow_ = at::empty({std::max<int64_t>(B, 1024)}, W_.options());
+    }
+    hipStream_t st = c10::hip::getCurrentHIPStream().stream();
+    char* d = static_cast<char*>(dev_.data_ptr());
+    {
+      py::gil_scoped_release nogil;
+      hck(hipMemcpyAsync(d, host_[slot].data_ptr(), (size_t)total, hipMemcpyHostToDevice, st), "SparseLRPlan: feed copy");
+      hck(hipEventRecord(ev_[slot], st), "SparseLRPlan: event");
+      pending_[slot] = true;
+      launch(reinterpret_cast<const long long*>(d + o_ids), reinterpret_cast<const long long*>(d + o_off),
+             reinterpret_cast<const float*>(d + o_val), reinterpret_cast<const float*>(d + o_lab), (int)B, (float)lr, st);
+    }
+    ++runs_;
+    return true;
+  }
+
+  // device tensors (labels [B] / [B,1] f32, offsets [B+1] i64, ids [nnz] i64, vals [nnz] f32 or None)
+  at::Tensor step(at::Tensor labels, at::Tensor offsets, at::Tensor ids, c10::optional<at::Tensor> vals, double lr) {
+    TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == at::kFloat && labels.is_contiguous(), "labels");
+    TORCH_CHECK(offsets.is_cuda() && offsets.scalar_type() == at::kLong && offsets.is_contiguous(), "offsets");
+    TORCH_CHECK(ids.is_cuda() && ids.scalar_type() == at::kLong && ids.is_contiguous(), "ids");
+    const int64_t B = labels.numel();
+    TORCH_CHECK(offsets.numel() == B + 1, "SparseLRPlan.step: offsets must hold B + 1 entries");
+    const float* vp = nullptr;
+    if (vals.has_value()) {
+      TORCH_CHECK(vals->is_cuda() && vals->scalar_type() == at::kFloat && vals->is_contiguous() &&
+                      vals->numel() == ids.numel(), "vals");
+      vp = vals->data_ptr<float>();
+    }
+    if (dz_.numel() < B) {
+      dz_ = at::empty({std::max<int64_t>(B, 1024)}, W_.options());
+      lrow_ = at::empty({std::max<int64_t>(B, 1024)}, W_.options());
+    }
+    launch(reinterpret_cast<const long long*>(ids.data_ptr<int64_t>()),
+           reinterpret_cast<const long long*>(offsets.data_ptr<int64_t>()), vp, labels.data_ptr<float>(), (int)B,
+           (float)lr, c10::hip::getCurrentHIPStream().stream());
+    ++runs_;
+    return loss();
+  }
+
+  at::Tensor loss() const { return loss_.select(0, 0); }   // the last run's mean loss (0-d, device)
+  int64_t runs() const { return runs_; }
+  int64_t bad_ids() const { return bad_.item<int>(); }
+
+ private:
+  void launch(const long long* ids, const long long* offs, const float* vals, const float* labels, int B, float lr,
+              hipStream_t st) {
+    hck(dtfk_slr_step(W_.data_ptr<float>(), (long long)F_, ids, offs, vals, labels, bias_.data_ptr<float>(), B, nullptr,
+                      lr, dz_.data_ptr<float>(), lrow_.data_ptr<float>(), loss_.data_ptr<float>(),
+                      bad_.data_ptr<int>(), gkind_ ? gstep_.data_ptr() : nullptr, gkind_, st),
+        "SparseLRPlan: step");
+  }
+
+  at::Tensor W_, bias_, gstep_, loss_, bad_, dev_, dz_, lrow_;
+  at::Tensor host_[2];
+  std::vector<int64_t> cnt_;
+  hipEvent_t ev_[2] = {nullptr, nullptr};
+  bool pending_[2] = {false, false};
+  int slot_ = 0, gkind_ = 0;
+  int64_t F_ = 0, runs_ = 0;
+};
+
+void init_sparse(py::module& m) {
+  py::class_<SparseLRPlan>(m, "SparseLRPlan")
+      .def(py::init<at::Tensor, at::Tensor, c10::optional<at::Tensor>>(), py::arg("W"), py::arg("bias"),
+           py::arg("gstep") = py::none())
+      .def("run", &SparseLRPlan::run, py::arg("y"), py::arg("indices"), py::arg("ids"), py::arg("vals"), py::arg("lr"))
+      .def("step", &SparseLRPlan::step, py::arg("labels"), py::arg("offsets"), py::arg("ids"), py::arg("vals"),
+           py::arg("lr"))
+      .def("loss", &SparseLRPlan::loss)
+      .def("runs", &SparseLRPlan::runs)
+      .def("bad_ids", &SparseLRPlan::bad_ids);
+}
+
+}  // namespace dtf

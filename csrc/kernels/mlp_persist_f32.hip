@@ -564,26 +564,21 @@ __device__ void copier_res(const Args& a, int cid, uint8_t* smem) {
   for (int st = 0;; ++st) {
     const long long k = a.run0 + st;
     if (tid == 0) {
+      // every copier watches the doorbell (no second hop through a device flag);
+      // copier 0 alone may stop the launch: its rows complete every record, so a
+      // run it did not take never reaches the compute workgroups' staged count
       int d = 1;
       const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-      if (cid == 0) {
-        for (;;) {
-          const long long v = __hip_atomic_load(a.door, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          if (v < 0) { d = 0; break; }
-          if (v > k) break;
-          if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > a.idle) { d = 0; break; }
-          __builtin_amdgcn_s_sleep(2);
-        }
-        if (d) __hip_atomic_store(a.dctr + 8, (unsigned)(st + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else __hip_atomic_store(a.dctr + 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        for (;;) {
-          if (__hip_atomic_load(a.dctr + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)(st + 1)) break;
-          if (__hip_atomic_load(a.dctr + 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) { d = 0; break; }
-          if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > a.idle + a.timeout) { d = 0; break; }
-          __builtin_amdgcn_s_sleep(2);
-        }
+      const long long lim = cid == 0 ? a.idle : a.idle + a.timeout;
+      for (;;) {
+        const long long v = __hip_atomic_load(a.door, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (v < 0) { d = 0; break; }
+        if (v > k) break;
+        if (cid != 0 && __hip_atomic_load(a.dctr + 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) { d = 0; break; }
+        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > lim) { d = 0; break; }
+        __builtin_amdgcn_s_sleep(1);
       }
+      if (cid == 0 && !d) __hip_atomic_store(a.dctr + 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       *dec = d;
     }
     __syncthreads();
@@ -706,6 +701,14 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
   }
   const unsigned long long seq0 = *a.seq;
   const long long gstep0 = *a.gstep;
+  double gvar0 = 0.0;   // RES: the graph's global_step at launch
+  if constexpr (RES) {
+    if (a.gvar_kind == 1) gvar0 = *static_cast<const float*>(a.gvar);
+    else if (a.gvar_kind == 2) gvar0 = (double)*static_cast<const long long*>(a.gvar);
+    else if (a.gvar_kind == 3) gvar0 = *static_cast<const int*>(a.gvar);
+    else if (a.gvar_kind == 4) gvar0 = *static_cast<const double*>(a.gvar);
+    else gvar0 = (double)gstep0;
+  }
   const float lr = *a.lr;
   float lrB = lr / (float)(B * (MULTI ? a.W : 1));   // RES: per run (the record's lr)
   float lrX = lrB * (1.f / 255.f);
@@ -1257,7 +1260,9 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
         const float cr = wave_sum(rl[128 + lane] + (hi ? rl[128 + lane + 64] : 0.f));
         if (lane == 63) {
           const int sl = (int)((gstep0 + st) % a.ring);
-          if constexpr (RES) {   // read by the step's last arriver (sc1 hand-off)
+          if constexpr (RES) {   // workgroup 0 publishes them (LDS), the ring keeps them too
+            reinterpret_cast<float*>(abort_flag)[4] = ls / (float)B;
+            reinterpret_cast<float*>(abort_flag)[5] = cr / (float)B;
             __hip_atomic_store(a.metrics + 2 * sl, ls / (float)B, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(a.metrics + 2 * sl + 1, cr / (float)B, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           } else {
@@ -1465,40 +1470,35 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
       // memory: write-through stores, every wave's vmcnt(0), barrier, one agent add;
       // the last arriver (its add's return value says so) publishes the metrics,
       // global_step and the done count to pinned host memory
-      __syncthreads();   // wave 7's LDS updates of W2 / b1 / b2
+      __syncthreads();   // wave 7's LDS updates of W2 / b1 / b2 (and workgroup 0's metrics)
       write_params(true);
+      // the graph's global_step: counted here (anything else that writes it stops
+      // the engine first), stored write-through by workgroup 0
+      const double gsv = gvar0 + (double)(st + 1);
+      if (c == 0 && tid == 0) {
+        if (a.gvar_kind == 1) __hip_atomic_store(static_cast<float*>(a.gvar), (float)gsv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else if (a.gvar_kind == 2) __hip_atomic_store(static_cast<long long*>(a.gvar), (long long)gsv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else if (a.gvar_kind == 3) __hip_atomic_store(static_cast<int*>(a.gvar), (int)gsv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else if (a.gvar_kind == 4) __hip_atomic_store(static_cast<double*>(a.gvar), gsv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) {
-        const unsigned old = __hip_atomic_fetch_add(a.dctr + 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old == (unsigned)NCOMP * (unsigned)(st + 1) - 1u) {
-          const int sl = (int)((gstep0 + st) % a.ring);
-          const float ls = __hip_atomic_load(a.metrics + 2 * sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const float ac = __hip_atomic_load(a.metrics + 2 * sl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          float gs = (float)(gstep0 + st + 1);
-          if (a.gvar_kind == 1) {
-            float* gp = static_cast<float*>(a.gvar);
-            gs = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1.f;
-            __hip_atomic_store(gp, gs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          } else if (a.gvar_kind == 2) {
-            long long* gp = static_cast<long long*>(a.gvar);
-            const long long v = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-            __hip_atomic_store(gp, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            gs = (float)v;
-          } else if (a.gvar_kind == 3) {
-            int* gp = static_cast<int*>(a.gvar);
-            const int v = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-            __hip_atomic_store(gp, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            gs = (float)v;
-          } else if (a.gvar_kind == 4) {
-            double* gp = static_cast<double*>(a.gvar);
-            const double v = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1.0;
-            __hip_atomic_store(gp, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            gs = (float)v;
+        __hip_atomic_fetch_add(a.dctr + 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (c == 0) {
+          // workgroup 0 (it holds the metrics) publishes once all 28 have arrived
+          const unsigned need = (unsigned)NCOMP * (unsigned)(st + 1);
+          const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+          while (__hip_atomic_load(a.dctr + 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+            if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > a.timeout) {
+              atomicOr(a.err, 8);
+              break;
+            }
           }
-          __hip_atomic_store(a.host_out, ls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          __hip_atomic_store(a.host_out + 1, ac, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          __hip_atomic_store(a.host_out + 2, gs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          const float* mf = reinterpret_cast<const float*>(abort_flag);
+          __hip_atomic_store(a.host_out, mf[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(a.host_out + 1, mf[5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(a.host_out + 2, (float)gsv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           __hip_atomic_store(a.host_done, a.run0 + st + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }

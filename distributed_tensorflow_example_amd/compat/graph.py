@@ -261,6 +261,8 @@ class Tensor:
     """Deferred value: fn(*inputs) evaluated inside Session.run."""
 
     _is_op = False
+    _pre_run = None      # async train ops: a hook pulling the ps variables (compat/train.py)
+    _lowering = None     # train ops: what compat/lowering.py may replace
 
     def __init__(self, fn: Callable, inputs: Sequence[Any] = (), name: str = "Tensor", dtype=None,
                  shape=None, op_type: Optional[str] = None, attrs: Optional[Dict[str, Any]] = None):

@@ -200,7 +200,7 @@ class _PlanBase:
     _fetch_ok: Dict[tuple, bool]
 
     def fetches_ok(self, fetch_list) -> bool:
-        key = tuple(id(f) for f in fetch_list)
+        key = tuple(map(id, fetch_list))
         ok = self._fetch_ok.get(key)
         if ok is None:
             ok = True
@@ -282,14 +282,13 @@ class MLPStepPlan(_PlanBase):
 
     # -------------------------------------------------------------- run
     def run(self, ctx, flat) -> bool:
-        from .. import _native
-
         pat, info = self.pat, self.info
-        W1, b1, W2, b2 = (v.value for v in (pat.W1, pat.b1, pat.W2, pat.b2))
+        W1, b1, W2, b2 = pat.W1.value, pat.b1.value, pat.W2.value, pat.b2.value
         if not W1.is_cuda:
             return False
         if self._run_native_plan(ctx, flat, W1, b1, W2, b2):
             return True
+        from .. import _native
         _resident_mod().quiesce_all()   # the kernels below update the variables a resident engine holds
         xy = self._packed_feeds(ctx, W1.device)
         x, y = xy if xy is not None else (ctx.eval(pat.x), ctx.eval(pat.ylab))
@@ -490,7 +489,7 @@ class MLPStepPlan(_PlanBase):
 
     def _needs(self, flat, gs_var, gstep):
         """(fetches read the loss/accuracy, global_step may be seeded)."""
-        key = ("needs",) + tuple(id(f) for f in flat)
+        key = ("needs",) + tuple(map(id, flat))
         r = self._fetch_ok.get(key)
         if r is None:
             targets = {id(self.pat.loss)} | ({id(self.accuracy)} if self.accuracy is not None else set())
@@ -575,6 +574,8 @@ class SparseLRStepPlan(_PlanBase):
         self._fetch_ok = {}
         self.trainer = None
         self._stage = None
+        self._nplan = None            # one worker: csrc/bind_sparse.cpp SparseLRPlan
+        self._fused_env = os.environ.get("DTF_SLR_FUSED", "1") != "0"
         self.steps = 0
 
     @staticmethod
@@ -655,6 +656,36 @@ class SparseLRStepPlan(_PlanBase):
             v, lab = dv[2].view(torch.float32), dv[3].view(torch.float32).view(B, 1)
         return lab, off, i, v
 
+    def _native_run(self, ctx, opt, gs_var, table) -> bool:
+        """One worker: the whole run as ONE native call on lr2.py's own feed
+        arrays (csrc/bind_sparse.cpp SparseLRPlan: CSR build + packing with the
+        GIL released, one copy, two kernels -- no dedup or routing needed when
+        every row of W is local).  False: feeds it does not take (tensors, other
+        dtypes, a row outside the batch)."""
+        p = self.pat
+        fy, fi, ff, fv = (self._feed(ctx, t) for t in (p.y, p.idx, p.fids, p.fvals))
+        if not all(isinstance(v, np.ndarray) for v in (fy, fi, ff, fv)):
+            return False
+        if self._nplan is None:
+            from .. import _native
+
+            gv = getattr(gs_var, "value", None) if gs_var is not None else None
+            gst = gv.data if (isinstance(gv, torch.Tensor) and gv.is_cuda and gv.numel() == 1 and gv.dtype in (
+                torch.float32, torch.int64, torch.int32, torch.float64)) else None
+            self._nplan = _native.load().SparseLRPlan(table.local, p.b.value.data, gst)
+            self._nplan_gs = gst is not None
+        if not self._nplan.run(fy, fi, ff, fv, float(opt._lr_value())):
+            return False
+        opt._steps += 1
+        _debug_mod().fault_point(opt._steps, 0)
+        if gs_var is not None and not self._nplan_gs:
+            with torch.no_grad():
+                gs_var.value.data += 1
+        ctx.memo[id(p.loss)] = self._nplan.loss()   # this run's loss (a device scalar, read before the next run)
+        ctx.memo[id(self.op)] = None
+        self.steps += 1
+        return True
+
     def run(self, ctx, flat) -> bool:
         from ..models.sparse_lr import SparseLRTrainer
         _debug = _debug_mod()
@@ -671,6 +702,8 @@ class SparseLRStepPlan(_PlanBase):
         if table.hogwild is not None:
             return False
         dev = table.device
+        if dev.type == "cuda" and w.world_size == 1 and self._fused_env and self._native_run(ctx, opt, gs_var, table):
+            return True
         if self.trainer is None:
             self.trainer = SparseLRTrainer(table.num_rows, float(opt._lr_value()), w, device=dev, table=table,
                                            bias=p.b.value)
@@ -710,16 +743,19 @@ def _flatten(f, out: List[Any]):
     return out
 
 
-def try_lower(session, fetches, ctx) -> None:
+def try_lower(session, fetches, ctx, flat=None) -> None:
     """Run lowered plans for train ops in `fetches`, seeding ctx.memo."""
     lower = getattr(session, "_lower", None)          # read once per Session (compat/session.py)
     if not (enabled() if lower is None else lower):
         return
-    flat = _flatten(fetches, [])
+    if flat is None:
+        flat = _flatten(fetches, [])
     for f in flat:
-        if not (isinstance(f, Operation) and getattr(f, "_lowering", None) is not None):
+        if getattr(f, "_lowering", None) is None or not isinstance(f, Operation):
             continue
-        plan = _CACHE.get(f)
+        plan = f.__dict__.get("_dtf_plan")
+        if plan is None:
+            plan = _CACHE.get(f)
         if plan is None:
             loss = getattr(f, "loss", None)
             pat = match_mlp(loss) if loss is not None else None
@@ -733,6 +769,7 @@ def try_lower(session, fetches, ctx) -> None:
                         [id(pv) for _, pv in f._lowering["sparse"]] == [id(sp.W)]:
                     plan = SparseLRStepPlan(f, sp)
             _CACHE[f] = plan
+            f._dtf_plan = plan
         if plan is False or id(f) in ctx.memo:
             continue
         if plan.fetches_ok(flat):

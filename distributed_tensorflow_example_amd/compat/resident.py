@@ -13,8 +13,10 @@ WRITES the graph's variables must stop it first: every Session.run that does
 not take the resident path, `Variable.load`, `Saver.restore` and
 `Session.close` call `quiesce_all()` (the kernel writes the variables through
 every step, so reads need nothing).  A launch also exits by itself after
-`DTF_RESIDENT_IDLE_S` (default 0.1 s) without a run -- the next run relaunches
-it -- and at interpreter exit.  Direct torch writes to a variable's tensor
+`DTF_RESIDENT_IDLE_S` (default 2 ms) without a run -- the next run relaunches
+it (~20 us) -- and at interpreter exit.  The idle bound is short on purpose: a
+device-wide `torch.cuda.synchronize()` waits for the resident launch too, so
+it returns at most that long after the last run.  Direct torch writes to a variable's tensor
 while an engine is live are not seen by it (call `quiesce_all()` first).
 DTF_RESIDENT_SESSION=0 disables the engine.
 """
@@ -22,9 +24,8 @@ from __future__ import annotations
 
 import atexit
 import os
-import weakref
 
-_LIVE: "weakref.WeakSet" = weakref.WeakSet()
+_LIVE: list = []     # handles whose launch may be live (a plain list: its truth test is free per run)
 
 
 def enabled() -> bool:
@@ -32,7 +33,7 @@ def enabled() -> bool:
 
 
 def idle_s() -> float:
-    return float(os.environ.get("DTF_RESIDENT_IDLE_S", "0.1"))
+    return float(os.environ.get("DTF_RESIDENT_IDLE_S", "0.002"))
 
 
 class ResidentHandle:
@@ -41,20 +42,24 @@ class ResidentHandle:
     def __init__(self, native_plan):
         self.plan = native_plan
         self.out = native_plan.host_metrics().numpy()     # pinned [loss, accuracy, global_step]
+        self.live = False
 
     def run_u8(self, u8, y, lr) -> bool:
         ok = self.plan.run_u8(u8, y, lr)
-        if ok:
-            _LIVE.add(self)
+        if ok and not self.live:
+            self.live = True
+            _LIVE.append(self)
         return ok
 
     def stop(self):
-        _LIVE.discard(self)
+        if self.live:
+            self.live = False
+            _LIVE.remove(self)
         self.plan.stop()
 
 
 def any_live() -> bool:
-    return len(_LIVE) > 0
+    return bool(_LIVE)
 
 
 def quiesce_all():

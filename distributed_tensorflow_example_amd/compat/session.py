@@ -44,6 +44,9 @@ class RunMetadata:
         self.step_stats = None
 
 
+_SCALARS = (np.float32, np.float64, np.int64, np.int32)   # seeded fetch values, returned as they are
+
+
 def _to_numpy(v):
     if v is None:
         return None
@@ -58,17 +61,10 @@ def _to_numpy(v):
     return v
 
 
-def _pre_run_hooks(fetches) -> list:
-    out, stack = [], [fetches]
-    while stack:
-        f = stack.pop()
-        if isinstance(f, (list, tuple)):
-            stack.extend(f)
-        elif isinstance(f, dict):
-            stack.extend(f.values())
-        elif getattr(f, "_pre_run", None) is not None:
-            out.append(f._pre_run)
-    return out
+def _flat(fetches) -> list:
+    if type(fetches) is list and all(isinstance(f, Tensor) for f in fetches):
+        return fetches                      # the common shape: a flat list of graph nodes
+    return _lowering._flatten(fetches, [])
 
 
 class Session:
@@ -89,12 +85,21 @@ class Session:
         ctx = RunContext(feed_dict or {}, self.graph.device)
         ctx.session = self
         ctx.options = options
-        _lowering.try_lower(self, fetches, ctx)         # fused steps for matched train ops
+        flat = _flat(fetches)
+        _lowering.try_lower(self, fetches, ctx, flat)   # fused steps for matched train ops
         if _resident._LIVE and not getattr(ctx, "resident_ran", False):
             _resident.quiesce_all()      # this run may write variables a resident engine holds
-        for hook in _pre_run_hooks(fetches):           # async train ops: pull the ps variables first
-            hook()
-        out = self._run(fetches, ctx)
+        for f in flat:                   # async train ops: pull the ps variables first
+            hook = getattr(f, "_pre_run", None)
+            if hook is not None:
+                hook()
+        if flat is fetches:              # flat list of graph nodes: no per-fetch dispatch
+            memo, out = ctx.memo, []
+            for f in fetches:
+                v = memo[id(f)] if id(f) in memo else ctx.eval(f)
+                out.append(None if f._is_op else (v if type(v) in _SCALARS else _to_numpy(v)))
+        else:
+            out = self._run(fetches, ctx)
         if self._post_run and not self._in_post:
             # step-boundary services (Supervisor checkpoints): run in the training
             # thread between steps, never concurrently with a train op

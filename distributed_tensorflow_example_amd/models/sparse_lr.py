@@ -104,7 +104,34 @@ class SparseLRTrainer(StaticStepMixin):
     def train_step(self, batch) -> torch.Tensor:
         if self._bstore is not None:
             return self._train_step_async(batch)
+        if self._fused_ok():
+            return self._train_step_fused(batch)
         return StaticStepMixin.train_step(self, batch)
+
+    def _fused_ok(self) -> bool:
+        """One worker on a GPU: every row of W is local, so the step is the two
+        kernels of csrc/kernels/sparse_lr.hip (no dedup / routing / exchange).
+        DTF_SLR_FUSED=0 keeps the general sharded path."""
+        ok = getattr(self, "_fused", None)
+        if ok is None:
+            import os
+            ok = self._fused = (self.world.world_size == 1 and self.device.type == "cuda" and self.W.dim == 1
+                                and self.W.hogwild is None and self.W.router is None
+                                and os.environ.get("DTF_SLR_FUSED", "1") != "0")
+        return ok
+
+    def _train_step_fused(self, batch) -> torch.Tensor:
+        labels, offsets, ids, vals = batch.to(self.device) if hasattr(batch, "to") else batch
+        plan = getattr(self, "_plan", None)
+        if plan is None:
+            from .. import _native
+            plan = self._plan = _native.load().SparseLRPlan(self.W.local, self.b.data, None)
+        dev = self.device
+        loss = plan.step(labels.to(dev, torch.float32).contiguous(), offsets.to(dev, torch.int64).contiguous(),
+                         ids.to(dev, torch.int64).contiguous(),
+                         None if vals is None else vals.to(dev, torch.float32).contiguous(), self.lr)
+        self.global_step += 1
+        return loss
 
     def _train_step_async(self, batch) -> torch.Tensor:
         """One Hogwild step: pull b, rows straight from their owners, scatter-SGD

@@ -82,11 +82,14 @@ def test_mnist_example_single_worker_gpu(tmp_path):
         assert res["accuracy"] > 0.5, res
 
 
-def test_sparse_lr_graphed_step_matches_eager():
+def test_sparse_lr_graphed_step_matches_eager(monkeypatch):
     """The device-resident sparse LR step captured in one hipGraph
     (utils/graphs.GraphedStep) trains like the launch-by-launch step:
-    capture warmups leave no trace, replays see the new batches."""
+    capture warmups leave no trace, replays see the new batches.  (The
+    general sharded path: one worker otherwise takes the fused kernels.)"""
     import numpy as np
+
+    monkeypatch.setenv("DTF_SLR_FUSED", "0")
 
     from distributed_tensorflow_example_amd.models.sparse_lr import SparseLRTrainer
     from distributed_tensorflow_example_amd.parallel import world as W
@@ -145,3 +148,38 @@ def test_wide_deep_graphed_step_matches_eager(native):
     assert torch.allclose(eager.wide.local, graphed.wide.local, atol=1e-5)
     for a, b in zip(eager.dense_params, graphed.dense_params):
         assert torch.allclose(a, b, atol=1e-5)
+
+
+def test_sparse_lr_fused_step_matches_general(monkeypatch):
+    """One worker: the two-kernel step (csrc/kernels/sparse_lr.hip: no dedup,
+    atomic scatter-SGD) trains like the general sharded path (radix-sort dedup,
+    bag backward, owner-side apply) over 12 Zipf batches with hot ids."""
+    import numpy as np
+
+    from distributed_tensorflow_example_amd.models.sparse_lr import SparseLRTrainer
+    from distributed_tensorflow_example_amd.parallel import world as W
+
+    w = W.get_world() if W._WORLD is not None else W.init()
+    rng = np.random.default_rng(4)
+    B, F = 500, 1_000_000
+    batches = []
+    for _ in range(6):
+        k = rng.integers(20, 61, B)
+        offs = np.zeros(B + 1, np.int64)
+        np.cumsum(k, out=offs[1:])
+        ids = torch.from_numpy(((rng.zipf(1.1, int(offs[-1])) - 1) % F).astype(np.int64)).cuda()
+        batches.append(((torch.rand(B, 1, device="cuda") < 0.3).float(), torch.from_numpy(offs).cuda(), ids,
+                        torch.rand(int(offs[-1]), device="cuda")))
+    monkeypatch.setenv("DTF_SLR_FUSED", "0")
+    general = SparseLRTrainer(F, 1.0, w, seed=3)
+    assert not general._fused_ok()
+    monkeypatch.setenv("DTF_SLR_FUSED", "1")
+    fused = SparseLRTrainer(F, 1.0, w, seed=3)
+    assert fused._fused_ok()
+    for i in range(12):
+        lg = general.train_step(batches[i % 6])
+        lf = fused.train_step(batches[i % 6])
+        assert abs(float(lg) - float(lf)) < 1e-5, i
+    assert fused.global_step == general.global_step == 12
+    assert torch.allclose(general.W.local, fused.W.local, atol=1e-5)
+    assert torch.allclose(general.b, fused.b, atol=1e-6)

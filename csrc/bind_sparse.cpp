@@ -19,9 +19,9 @@
 #include <vector>
 
 extern "C" {
-hipError_t dtfk_slr_step(float* W, long long F, const long long* ids, const long long* offsets, const float* vals,
-                         const float* labels, float* bias, int B, const float* lr_ptr, float lr_val, float* dz,
-                         float* lrow, float* loss_out, int* bad, void* gvar, int gkind, hipStream_t stream);
+hipError_t dtfk_slr_step(float* W, long long F, const void* ids, int ids32, const long long* offsets,
+                         const float* vals, const float* labels, float* bias, int B, const float* lr_ptr, float lr_val,
+                         float* dz, float* lrow, float* loss_out, int* bad, void* gvar, int gkind, hipStream_t stream);
 }
 
 namespace dtf {
@@ -83,7 +83,10 @@ class SparseLRPlan {
     if (y.ndim() > 2 || ids.ndim() > 1 || vals.ndim() > 1 || (y.ndim() == 2 && y.shape(1) != 1 && y.shape(0) != 1))
       return false;
     const int64_t ys_el = (y.ndim() == 2 && y.shape(0) == 1) ? y.strides(1) : ys;
-    const int64_t o_ids = 0, o_off = align16(8 * n), o_val = o_off + align16(8 * (B + 1)),
+    // ids travel as int32 when the table has < 2^31 rows (lr2's F = 1e9 does): half the bytes
+    const bool i32 = F_ < (1LL << 31);
+    const int64_t isz = i32 ? 4 : 8;
+    const int64_t o_ids = 0, o_off = align16(isz * n), o_val = o_off + align16(8 * (B + 1)),
                   o_lab = o_val + align16(4 * n), total = o_lab + align16(4 * B);
     const int slot = slot_ ^= 1;
     bool ok = true;
@@ -96,6 +99,7 @@ class SparseLRPlan {
       }
       char* h = static_cast<char*>(host_[slot].data_ptr());
       int64_t* hid = reinterpret_cast<int64_t*>(h + o_ids);
+      int32_t* hid32 = reinterpret_cast<int32_t*>(h + o_ids);
       int64_t* hoff = reinterpret_cast<int64_t*>(h + o_off);
       float* hval = reinterpret_cast<float*>(h + o_val);
       float* hlab = reinterpret_cast<float*>(h + o_lab);
@@ -118,16 +122,22 @@ class SparseLRPlan {
       if (ok) {
         for (int64_t b = 0; b < B; ++b) cnt[(size_t)b + 1] += cnt[(size_t)b];
         std::memcpy(hoff, cnt.data(), sizeof(int64_t) * (size_t)(B + 1));
+        // out-of-range ids are kept as such (the kernels count and skip them): in int32
+        // form anything outside [0, F) becomes -1
+        auto put = [&](int64_t d, int64_t id) {
+          if (i32) hid32[d] = (id >= 0 && id < F_) ? (int32_t)id : -1;
+          else hid[d] = id;
+        };
         if (sorted) {
-          if (fs == 8) std::memcpy(hid, fb, 8 * (size_t)n);
-          else for (int64_t j = 0; j < n; ++j) hid[j] = *reinterpret_cast<const int64_t*>(fb + j * fs);
+          if (!i32 && fs == 8) std::memcpy(hid, fb, 8 * (size_t)n);
+          else for (int64_t j = 0; j < n; ++j) put(j, *reinterpret_cast<const int64_t*>(fb + j * fs));
           if (vs == 4) std::memcpy(hval, vb, 4 * (size_t)n);
           else for (int64_t j = 0; j < n; ++j) hval[j] = *reinterpret_cast<const float*>(vb + j * vs);
         } else {
           for (int64_t j = 0; j < n; ++j) {
             const int64_t r = *reinterpret_cast<const int64_t*>(ib + j * is0);
             const int64_t d = cnt[(size_t)r]++;
-            hid[d] = *reinterpret_cast<const int64_t*>(fb + j * fs);
+            put(d, *reinterpret_cast<const int64_t*>(fb + j * fs));
             hval[d] = *reinterpret_cast<const float*>(vb + j * vs);
           }
         }
@@ -147,8 +157,8 @@ class SparseLRPlan {
       hck(hipMemcpyAsync(d, host_[slot].data_ptr(), (size_t)total, hipMemcpyHostToDevice, st), "SparseLRPlan: feed copy");
       hck(hipEventRecord(ev_[slot], st), "SparseLRPlan: event");
       pending_[slot] = true;
-      launch(reinterpret_cast<const long long*>(d + o_ids), reinterpret_cast<const long long*>(d + o_off),
-             reinterpret_cast<const float*>(d + o_val), reinterpret_cast<const float*>(d + o_lab), (int)B, (float)lr, st);
+      launch(d + o_ids, i32, reinterpret_cast<const long long*>(d + o_off), reinterpret_cast<const float*>(d + o_val),
+             reinterpret_cast<const float*>(d + o_lab), (int)B, (float)lr, st);
     }
     ++runs_;
     return true;
@@ -171,9 +181,8 @@ class SparseLRPlan {
       dz_ = at::empty({std::max<int64_t>(B, 1024)}, W_.options());
       lrow_ = at::empty({std::max<int64_t>(B, 1024)}, W_.options());
     }
-    launch(reinterpret_cast<const long long*>(ids.data_ptr<int64_t>()),
-           reinterpret_cast<const long long*>(offsets.data_ptr<int64_t>()), vp, labels.data_ptr<float>(), (int)B,
-           (float)lr, c10::hip::getCurrentHIPStream().stream());
+    launch(ids.data_ptr(), false, reinterpret_cast<const long long*>(offsets.data_ptr<int64_t>()), vp,
+           labels.data_ptr<float>(), (int)B, (float)lr, c10::hip::getCurrentHIPStream().stream());
     ++runs_;
     return loss();
   }
@@ -183,9 +192,9 @@ class SparseLRPlan {
   int64_t bad_ids() const { return bad_.item<int>(); }
 
  private:
-  void launch(const long long* ids, const long long* offs, const float* vals, const float* labels, int B, float lr,
-              hipStream_t st) {
-    hck(dtfk_slr_step(W_.data_ptr<float>(), (long long)F_, ids, offs, vals, labels, bias_.data_ptr<float>(), B, nullptr,
+  void launch(const void* ids, bool i32, const long long* offs, const float* vals, const float* labels, int B,
+              float lr, hipStream_t st) {
+    hck(dtfk_slr_step(W_.data_ptr<float>(), (long long)F_, ids, i32 ? 1 : 0, offs, vals, labels, bias_.data_ptr<float>(), B, nullptr,
                       lr, dz_.data_ptr<float>(), lrow_.data_ptr<float>(), loss_.data_ptr<float>(),
                       bad_.data_ptr<int>(), gkind_ ? gstep_.data_ptr() : nullptr, gkind_, st),
         "SparseLRPlan: step");

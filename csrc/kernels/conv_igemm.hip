@@ -1,0 +1,504 @@
+// 3x3 convolution (pad 1, stride 1 or 2) on NHWC bf16 activations as an
+// implicit GEMM on the gfx950 matrix cores, with an optional BatchNorm
+// statistics epilogue (ResNet-50, BASELINE.json configs[2]).
+//
+//   y[p][k] = sum_{r,s,c} x[n, ho*st + r - 1, wo*st + s - 1, c] * w[k][r][s][c]
+//
+// GEMM view: M = N*Ho*Wo output pixels (rows), N = K output channels, the
+// reduction runs over (r, s, 64-channel chunk) steps: no im2col buffer -- each
+// step's A tile is 128 pixels x 64 channels gathered straight from x (one
+// 128-byte channel run per pixel, zero for padding pixels via out-of-range
+// buffer loads), its B tile the matching [BN][64] slice of w (KRSC =
+// channels_last [K, C, 3, 3]).
+//
+//  * 256 threads = 4 waves in a 2 x 2 grid over the BM x BN tile (BM = 128,
+//    BN = 128 or 64): each wave owns (BM/2) x (BN/2) of the output as 16x16
+//    v_mfma_f32_16x16x32_bf16 tiles, fp32 accumulate.
+//  * Global -> registers (16-B buffer loads, 4 + BN/32 per thread per step) ->
+//    LDS: two register sets and two LDS buffers, a step's loads issued two
+//    steps before its MFMAs (the first version's one-step lookahead left every
+//    step waiting ~1 us on HBM: per-step time was the load latency).  LDS rows are 128 B with the 16-B chunk XOR
+//    (chunk ^ ((row >> 1) & 7)) that puts the 16 lanes of a ds_read_b128 group
+//    on 16 distinct slots of a bank row (MI355X_MICROARCH.md).
+//  * Epilogue through LDS: the bf16 tile is written back as whole 16-B row
+//    segments; with `part` the workgroup also writes per-channel sums of y and
+//    y^2 over its valid rows -- the [2, P, K] partials bn_finalize
+//    (csrc/kernels/bn.hip) reduces, so the BatchNorm after this conv skips its
+//    statistics pass over y.
+//
+// The input gradient of a stride-1 3x3 conv is the same convolution of dy with
+// the flipped, channel-transposed filter (conv_igemm_wflip builds it).
+#include "common.h"
+
+#include <type_traits>
+
+namespace dtfk {
+namespace cig {
+
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+
+constexpr int BM = 128, BK = 64, NTHR = 256;
+constexpr int OOB = 0x7ffffff0;
+
+__device__ __forceinline__ int swz(int row, int ch) { return ch ^ ((row >> 1) & 7); }
+
+template <int BN, bool STATS>
+__global__ __launch_bounds__(NTHR, 2) void conv3x3_fwd(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
+                                                       uint16_t* __restrict__ y, float* __restrict__ part, int N,
+                                                       int H, int W, int C, int K, int Ho, int Wo, int stride,
+                                                       long long xbytes) {
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, BUF = A_BYTES + B_BYTES;
+  constexpr int WM = BM / 2, WN = BN / 2;          // per-wave output block
+  constexpr int TM = WM / 16, TN = WN / 16;        // 16x16 tiles per wave
+  constexpr int NB = BN * 8 / NTHR;                // B chunks per thread per step
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * BUF];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wm = wv >> 1, wn = wv & 1;
+  const long long M = (long long)N * Ho * Wo;
+  const long long m0 = (long long)blockIdx.x * BM;
+  const int k0 = blockIdx.y * BN;
+
+  // this thread's 4 A rows (pixel coordinates fixed over the K loop) and chunk
+  const int ach = tid & 7;
+  int an[4], aho[4], awo[4];
+  bool arow[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const long long m = m0 + (tid >> 3) + 32 * i;
+    arow[i] = m < M;
+    const long long mm = arow[i] ? m : 0;
+    awo[i] = (int)(mm % Wo);
+    const long long t = mm / Wo;
+    aho[i] = (int)(t % Ho);
+    an[i] = (int)(t / Ho);
+  }
+  const auto xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(x), 0, (int)(xbytes > 0x7ffffff0 ? 0x7ffffff0 : xbytes), 0x00020000);
+  const long long wbytes = (long long)K * 9 * C * 2;
+  const auto wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(w), 0, (int)wbytes, 0x00020000);
+  const int ncc = C / BK;
+  const int nsteps = 9 * ncc;
+
+  // two register sets: a step's operands are loaded two steps ahead (issued
+  // while the step before it is multiplied), so one HBM round trip hides
+  // behind two steps of MFMAs instead of one
+  u32x4 ra[2][4], rb[2][NB];
+  auto load = [&](int step, auto pc) {
+    constexpr int P = decltype(pc)::value;
+    const int rs = step / ncc, c0 = (step % ncc) * BK;
+    const int r = rs / 3, s = rs % 3;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int hi = aho[i] * stride + r - 1, wi = awo[i] * stride + s - 1;
+      const bool ok = arow[i] && hi >= 0 && hi < H && wi >= 0 && wi < W;
+      const long long off = ((((long long)an[i] * H + hi) * W + wi) * C + c0 + 8 * ach) * 2;
+      ra[P][i] = __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? (int)off : OOB, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int row = (tid >> 3) + 32 * i;   // output channel within the tile
+      const long long off = (((long long)(k0 + row) * 9 + rs) * C + c0 + 8 * ach) * 2;
+      rb[P][i] = __builtin_amdgcn_raw_buffer_load_b128(wr, (int)off, 0, 0);
+    }
+  };
+  auto store = [&](auto pc) {   // register set P -> LDS buffer P
+    constexpr int P = decltype(pc)::value;
+    uint8_t* A = smem + P * BUF;
+    uint8_t* Bs = A + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = (tid >> 3) + 32 * i;
+      *reinterpret_cast<u32x4*>(A + row * 128 + 16 * swz(row, ach)) = ra[P][i];
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int row = (tid >> 3) + 32 * i;
+      *reinterpret_cast<u32x4*>(Bs + row * 128 + 16 * swz(row, ach)) = rb[P][i];
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  load(0, I0{});
+  if (nsteps > 1) load(1, I1{});
+  store(I0{});
+  __syncthreads();
+  const int fr = lane & 15, fk = lane >> 4;   // fragment row / k-chunk of this lane
+  // step s: its operands sit in LDS buffer s & 1; first the next step's operands
+  // go from their registers into the other buffer (free since the last
+  // barrier), then the step after that is loaded into the registers just freed
+  auto body = [&](int step, auto pc) {
+    constexpr int P = decltype(pc)::value;
+    using Q = std::integral_constant<int, P ^ 1>;
+    if (step + 1 < nsteps) store(Q{});
+    if (step + 2 < nsteps) load(step + 2, pc);
+    const uint8_t* A = smem + P * BUF;
+    const uint8_t* Bs = A + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {   // two 32-deep k halves of the 64-channel step
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * WM + 16 * i + fr;
+        af[i] = *reinterpret_cast<const bf16x8*>(A + row * 128 + 16 * swz(row, 4 * kk + fk));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * WN + 16 * j + fr;
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + row * 128 + 16 * swz(row, 4 * kk + fk));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(af[i], bfr[j], acc[i][j]);
+    }
+    __syncthreads();
+  };
+  for (int step = 0; step < nsteps; step += 2) {
+    body(step, I0{});
+    if (step + 1 < nsteps) body(step + 1, I1{});
+  }
+
+  // ---- epilogue: bf16 tile through LDS [BM][BN] (row pitch BN*2 + 16 B)
+  constexpr int PITCH = BN * 2 + 16;
+  static_assert(BM * PITCH <= 2 * BUF, "epilogue tile fits the operand buffers");
+  uint8_t* E = smem;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = wm * WM + 16 * i + 4 * fk + e;   // C[4*(l>>4)+e][l&15]
+        const int col = wn * WN + 16 * j + fr;
+        *reinterpret_cast<uint16_t*>(E + row * PITCH + 2 * col) = f2bf(acc[i][j][e]);
+      }
+  __syncthreads();
+  constexpr int CPR = BN / 8;   // 16-B chunks per output row
+  for (int t = tid; t < BM * CPR; t += NTHR) {
+    const int row = t / CPR, ch = t % CPR;
+    const long long m = m0 + row;
+    if (m < M)
+      *reinterpret_cast<u32x4*>(y + m * K + k0 + 8 * ch) = *reinterpret_cast<const u32x4*>(E + row * PITCH + 16 * ch);
+  }
+  if constexpr (STATS) {
+    // per-channel sum / sum of squares of the bf16 outputs over the valid rows
+    const int rows = (int)(M - m0 < BM ? M - m0 : BM);
+    constexpr int RG = NTHR / BN;   // row groups
+    const int col = tid % BN, g = tid / BN;
+    float s = 0.f, q = 0.f;
+    for (int row = g; row < rows; row += RG) {
+      const float v = bf2f(*reinterpret_cast<const uint16_t*>(E + row * PITCH + 2 * col));
+      s += v;
+      q += v * v;
+    }
+    float* red = reinterpret_cast<float*>(smem + ((BM * PITCH + 15) & ~15));   // behind the tile
+    static_assert(((BM * PITCH + 15) & ~15) + 2 * NTHR * 4 <= 2 * BUF, "stats scratch fits");
+    red[tid] = s;
+    red[NTHR + tid] = q;
+    __syncthreads();
+    if (g == 0) {
+#pragma unroll
+      for (int k = 1; k < RG; ++k) {
+        s += red[k * BN + col];
+        q += red[NTHR + k * BN + col];
+      }
+      const int P = gridDim.x;
+      part[((size_t)0 * P + blockIdx.x) * K + k0 + col] = s;
+      part[((size_t)1 * P + blockIdx.x) * K + k0 + col] = q;
+    }
+  }
+}
+
+// ---- weight gradient -------------------------------------------------------
+//   dW[k][r][s][c] += sum_p dy[p][k] * x[n, ho*st + r - 1, wo*st + s - 1, c]
+// GEMM: M = K (output channels), N = 9 C (filter columns (r, s, c) -- the KRSC
+// layout), reduction over the P = N*Ho*Wo output pixels, split over gridDim.z
+// (each split's fp32 tile is added into dW with float atomics: dW is the fp32
+// gradient buffer, so accumulation into an existing gradient is free).  Both
+// operands arrive pixel-major -- dy rows [P][K], x rows [.][C] -- so the LDS
+// images are [64 pixels][BM] and [64 pixels][BN] ("M/N-contiguous") and the MFMA
+// fragments are read with the gfx950 transposed LDS read ds_read_b64_tr_b16
+// (4 x 16-bit down a column per lane, two per 8-deep fragment).  Pixel rows
+// advance 64 per step by a carried (n, ho, wo) counter, no divisions in the loop.
+__device__ __forceinline__ int mn_swz(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
+template <int R>
+__device__ __forceinline__ int mn_off(int k, int ch) {   // byte offset of (k, 16-byte chunk ch) in [64][R]
+  return k * (2 * R) + ((ch ^ ((mn_swz(k) << 1) & (R / 8 - 1))) << 4);
+}
+typedef __attribute__((ext_vector_type(4))) short v4s;
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+// MFMA 16x16x32 fragment of rows [rb, rb+16), k-sub s of a [64][R] image
+template <int R>
+__device__ __forceinline__ bf16x8 frag_tr(const uint8_t* img, int rb, int s, int lane) {
+  const int k = s * 32 + 8 * (lane >> 4) + ((lane & 15) >> 2);
+  const int mn = rb + 4 * (lane & 3);
+  const int off = mn_off<R>(k, mn >> 3) + ((mn & 7) << 1);
+  const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(img + off));
+  const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(img + off + 4 * 2 * R));
+  typedef __attribute__((ext_vector_type(8))) short v8s;
+  const v8s v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+template <int BMW, int BNW>
+__global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
+                                                         float* __restrict__ dw, int N, int H, int W, int C, int K,
+                                                         int Ho, int Wo, int stride, long long xbytes,
+                                                         int steps_per_split, int kcrs) {
+  constexpr int PK = 64;                                        // pixels per step
+  constexpr int A_BYTES = PK * BMW * 2, B_BYTES = PK * BNW * 2, BUF = A_BYTES + B_BYTES;
+  constexpr int ACPR = BMW / 8, BCPR = BNW / 8;                 // 16-B chunks per image row
+  constexpr int NA = PK * ACPR / NTHR, NB = PK * BCPR / NTHR;   // chunks per thread per step
+  constexpr int WM = BMW / 2, WN = BNW / 2, TM = WM / 16, TN = WN / 16;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * BUF];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wm = wv >> 1, wn = wv & 1;
+  const long long P = (long long)N * Ho * Wo;
+  const int m0 = blockIdx.x * BMW;            // output-channel tile
+  const int n0 = blockIdx.y * BNW;            // filter-column tile over (r, s, c)
+  const int NC = 9 * C;
+  const long long pb = (long long)blockIdx.z * steps_per_split * PK;
+  long long pe = pb + (long long)steps_per_split * PK;
+  if (pe > P) pe = P;
+  const int nsteps = pb < pe ? (int)((pe - pb + PK - 1) / PK) : 0;
+  const auto dyr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(dy), 0,
+                                                     (int)((P * K * 2) > 0x7ffffff0LL ? 0x7ffffff0LL : P * K * 2), 0x00020000);
+  const auto xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(x), 0,
+                                                    (int)(xbytes > 0x7ffffff0LL ? 0x7ffffff0LL : xbytes), 0x00020000);
+  // A: thread's chunk column and pixel rows (fixed), B: chunk column -> (r, s, c) and pixel rows
+  const int ach = tid % ACPR, arow0 = tid / ACPR;               // rows arow0 + (NTHR/ACPR) i
+  const int bch = tid % BCPR, brow0 = tid / BCPR;
+  constexpr int ARS = NTHR / ACPR, BRS = NTHR / BCPR;           // row strides between a thread's chunks
+  // the B chunk's physical (swizzled) column and its filter column
+  int bphys[NB], br[NB], bs[NB], bc[NB];
+  bool bval[NB];
+  // carried pixel coordinates of each B row (advanced by PK per step)
+  int bn_[NB], bho[NB], bwo[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int row = brow0 + BRS * i;
+    const int lch = bch ^ ((mn_swz(row) << 1) & (BNW / 8 - 1));   // logical chunk stored at this slot
+    bphys[i] = bch;
+    const int col = n0 + 8 * lch;
+    bval[i] = col < NC;
+    const int rs = bval[i] ? col / C : 0;
+    bc[i] = bval[i] ? col % C : 0;
+    br[i] = rs / 3;
+    bs[i] = rs % 3;
+    const long long p = pb + row;
+    const long long pp = p < P ? p : 0;
+    bwo[i] = (int)(pp % Wo);
+    const long long t = pp / Wo;
+    bho[i] = (int)(t % Ho);
+    bn_[i] = (int)(t / Ho);
+  }
+  int alch[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int row = arow0 + ARS * i;
+    alch[i] = ach ^ ((mn_swz(row) << 1) & (BMW / 8 - 1));
+  }
+  const int dq = PK / Wo, dr = PK % Wo;
+  auto advance = [&]() {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      bwo[i] += dr;
+      bho[i] += dq;
+      if (bwo[i] >= Wo) { bwo[i] -= Wo; bho[i] += 1; }
+      while (bho[i] >= Ho) { bho[i] -= Ho; bn_[i] += 1; }
+    }
+  };
+  u32x4 ra[2][NA], rb[2][NB];
+  auto load = [&](int step, auto pc) {
+    constexpr int Q = decltype(pc)::value;
+    const long long p0 = pb + (long long)step * PK;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const long long p = p0 + arow0 + ARS * i;
+      const bool ok = p < pe;
+      ra[Q][i] = __builtin_amdgcn_raw_buffer_load_b128(dyr, ok ? (int)((p * K + m0 + 8 * alch[i]) * 2) : OOB, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const long long p = p0 + brow0 + BRS * i;
+      const int hi = bho[i] * stride + br[i] - 1, wi = bwo[i] * stride + bs[i] - 1;
+      const bool ok = bval[i] && p < pe && hi >= 0 && hi < H && wi >= 0 && wi < W;
+      const long long off = ((((long long)bn_[i] * H + hi) * W + wi) * C + bc[i]) * 2;
+      rb[Q][i] = __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? (int)off : OOB, 0, 0);
+    }
+    advance();
+  };
+  auto store = [&](auto pc) {
+    constexpr int Q = decltype(pc)::value;
+    uint8_t* A = smem + Q * BUF;
+    uint8_t* Bs = A + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < NA; ++i)
+      *reinterpret_cast<u32x4*>(A + (arow0 + ARS * i) * (2 * BMW) + 16 * ach) = ra[Q][i];
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+      *reinterpret_cast<u32x4*>(Bs + (brow0 + BRS * i) * (2 * BNW) + 16 * bphys[i]) = rb[Q][i];
+  };
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  if (nsteps > 0) {
+    load(0, I0{});
+    if (nsteps > 1) load(1, I1{});
+    store(I0{});
+  }
+  __syncthreads();
+  auto body = [&](int step, auto pc) {
+    constexpr int Q = decltype(pc)::value;
+    using Q1 = std::integral_constant<int, Q ^ 1>;
+    if (step + 1 < nsteps) store(Q1{});
+    if (step + 2 < nsteps) load(step + 2, pc);
+    const uint8_t* A = smem + Q * BUF;
+    const uint8_t* Bs = A + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = frag_tr<BMW>(A, wm * WM + 16 * i, kk, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = frag_tr<BNW>(Bs, wn * WN + 16 * j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(af[i], bfr[j], acc[i][j]);
+    }
+    __syncthreads();
+  };
+  for (int step = 0; step < nsteps; step += 2) {
+    body(step, I0{});
+    if (step + 1 < nsteps) body(step + 1, I1{});
+  }
+  if (nsteps == 0) return;
+  const int fr = lane & 15, fk = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + wn * WN + 16 * j + fr;
+      if (col >= NC) continue;
+      // KRSC (channels_last) or KCRS (contiguous) gradient layout
+      const int cidx = kcrs ? (col % C) * 9 + col / C : col;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = m0 + wm * WM + 16 * i + 4 * fk + e;
+        __hip_atomic_fetch_add(dw + (long long)row * NC + cidx, acc[i][j][e], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+}
+
+// w' [C][3][3][K] = w [K][2-r][2-s][C]: the filter of the stride-1 input gradient
+__global__ void wflip(const uint16_t* __restrict__ w, uint16_t* __restrict__ wt, int K, int C) {
+  const long long n = (long long)K * 9 * C;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    // i indexes wt = [c][rs'][k]
+    const int k = (int)(i % K);
+    const long long t = i / K;
+    const int rs = (int)(t % 9), c = (int)(t / 9);
+    const int r = 2 - rs / 3, s = 2 - rs % 3;
+    wt[i] = w[((long long)k * 9 + r * 3 + s) * C + c];
+  }
+}
+
+}  // namespace cig
+}  // namespace dtfk
+
+extern "C" {
+
+// 0: ok; invalid shapes return hipErrorInvalidValue (the caller uses MIOpen)
+int dtfk_conv3x3_supported(int N, int H, int W, int C, int K, int stride) {
+  if (N < 1 || H < 1 || W < 1 || (stride != 1 && stride != 2)) return 0;
+  if (C % 64 != 0 || K % 64 != 0) return 0;
+  const long long xbytes = (long long)N * H * W * C * 2;
+  if (xbytes >= 0x7ffffff0LL || (long long)K * 9 * C * 2 >= 0x7ffffff0LL) return 0;   // 32-bit buffer offsets
+  return 1;
+}
+
+hipError_t dtfk_conv3x3_fwd(const void* x, const void* w, void* y, float* part, int N, int H, int W, int C, int K,
+                            int stride, int bn, hipStream_t stream) {
+  using namespace dtfk::cig;
+  if (!dtfk_conv3x3_supported(N, H, W, C, K, stride)) return hipErrorInvalidValue;
+  const int Ho = (H + 2 - 3) / stride + 1, Wo = (W + 2 - 3) / stride + 1;
+  const long long M = (long long)N * Ho * Wo;
+  if (bn != 64 && bn != 128) {
+    // 128-wide channel tiles unless that leaves fewer than two workgroups per CU
+    // (2 fit per CU) -- the late stages (7x7 / 14x14, 512 channels) have few pixels
+    const long long t128 = (M + BM - 1) / BM * (K / 128);
+    bn = (K % 128 == 0 && t128 >= 512) ? 128 : 64;
+  }
+  if (K % bn) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)((M + BM - 1) / BM), (unsigned)(K / bn));
+  const long long xbytes = (long long)N * H * W * C * 2;
+  auto xs = static_cast<const uint16_t*>(x);
+  auto ws = static_cast<const uint16_t*>(w);
+  auto ys = static_cast<uint16_t*>(y);
+  if (bn == 128) {
+    if (part) hipLaunchKernelGGL((conv3x3_fwd<128, true>), grid, dim3(NTHR), 0, stream, xs, ws, ys, part, N, H, W, C, K, Ho, Wo, stride, xbytes);
+    else hipLaunchKernelGGL((conv3x3_fwd<128, false>), grid, dim3(NTHR), 0, stream, xs, ws, ys, part, N, H, W, C, K, Ho, Wo, stride, xbytes);
+  } else {
+    if (part) hipLaunchKernelGGL((conv3x3_fwd<64, true>), grid, dim3(NTHR), 0, stream, xs, ws, ys, part, N, H, W, C, K, Ho, Wo, stride, xbytes);
+    else hipLaunchKernelGGL((conv3x3_fwd<64, false>), grid, dim3(NTHR), 0, stream, xs, ws, ys, part, N, H, W, C, K, Ho, Wo, stride, xbytes);
+  }
+  return hipGetLastError();
+}
+
+long long dtfk_conv3x3_tiles(int N, int H, int W, int stride) {
+  const int Ho = (H + 2 - 3) / stride + 1, Wo = (W + 2 - 3) / stride + 1;
+  return ((long long)N * Ho * Wo + dtfk::cig::BM - 1) / dtfk::cig::BM;
+}
+
+hipError_t dtfk_conv3x3_wflip(const void* w, void* wt, int K, int C, hipStream_t stream) {
+  const long long n = (long long)K * 9 * C;
+  const unsigned blocks = (unsigned)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+  hipLaunchKernelGGL(dtfk::cig::wflip, dim3(blocks), dim3(256), 0, stream, static_cast<const uint16_t*>(w),
+                     static_cast<uint16_t*>(wt), K, C);
+  return hipGetLastError();
+}
+
+
+// dW (fp32 [K][3][3][C], accumulated into) of y = conv3x3(x, w, stride); dy is y's gradient
+hipError_t dtfk_conv3x3_wgrad(const void* dy, const void* x, float* dw, int N, int H, int W, int C, int K, int stride,
+                              int kcrs, hipStream_t stream) {
+  using namespace dtfk::cig;
+  if (!dtfk_conv3x3_supported(N, H, W, C, K, stride)) return hipErrorInvalidValue;
+  const int Ho = (H + 2 - 3) / stride + 1, Wo = (W + 2 - 3) / stride + 1;
+  const long long P = (long long)N * Ho * Wo;
+  if (P * K * 2 >= 0x7ffffff0LL) return hipErrorInvalidValue;
+  const int NC = 9 * C;
+  const int bm = K % 128 == 0 ? 128 : 64;
+  const int bnw = NC % 128 == 0 ? 128 : 64;
+  const long long tiles = (long long)(K / bm) * ((NC + bnw - 1) / bnw);
+  const long long steps = (P + 63) / 64;
+  // about 4 workgroups per CU in total (2 resident at a time), at least 8 steps per split
+  long long splits = (1024 + tiles - 1) / tiles;
+  if (splits > steps / 8) splits = steps / 8;
+  if (splits < 1) splits = 1;
+  const int sps = (int)((steps + splits - 1) / splits);
+  splits = (steps + sps - 1) / sps;
+  const dim3 grid((unsigned)(K / bm), (unsigned)((NC + bnw - 1) / bnw), (unsigned)splits);
+  const long long xbytes = (long long)N * H * W * C * 2;
+  auto d = static_cast<const uint16_t*>(dy);
+  auto xs = static_cast<const uint16_t*>(x);
+  if (bm == 128 && bnw == 128) hipLaunchKernelGGL((conv3x3_wgrad<128, 128>), grid, dim3(NTHR), 0, stream, d, xs, dw, N, H, W, C, K, Ho, Wo, stride, xbytes, sps, kcrs);
+  else if (bm == 128) hipLaunchKernelGGL((conv3x3_wgrad<128, 64>), grid, dim3(NTHR), 0, stream, d, xs, dw, N, H, W, C, K, Ho, Wo, stride, xbytes, sps, kcrs);
+  else if (bnw == 128) hipLaunchKernelGGL((conv3x3_wgrad<64, 128>), grid, dim3(NTHR), 0, stream, d, xs, dw, N, H, W, C, K, Ho, Wo, stride, xbytes, sps, kcrs);
+  else hipLaunchKernelGGL((conv3x3_wgrad<64, 64>), grid, dim3(NTHR), 0, stream, d, xs, dw, N, H, W, C, K, Ho, Wo, stride, xbytes, sps, kcrs);
+  return hipGetLastError();
+}
+
+}  // extern "C"

@@ -61,9 +61,17 @@
 // L2 (plain stores); spread (several ranks on one GPU: tests) runs them as
 // blocks 0..27.  A per-launch census of HW_REG_XCC_ID picks each edge's store
 // flavour (plain if L2-local, write-through otherwise): speed only, never
-// correctness.  Measured on MI355X (profiles/): ~13 us/step; the per-step
-// critical path is the two hops (~1.3 and ~1.9 us after the last producer)
-// plus producer skew, not the MFMA phases (~1.6 + 1.8 us).
+// correctness.  Measured on MI355X (profiles/mlp_persist_f32_phases_r3_prologue.json,
+// BENCH_r04.json): ~8.1 us/step; the per-step critical path is the two hops
+// (~1.3 and ~1.9 us after the last producer) plus producer skew, not the MFMA
+// phases (~0.5 forward + ~1.1 weight gradient).
+//
+// RES (the resident Session engine, compat/resident.py): ONE launch serves
+// Session.run calls -- per run the copiers wait on a pinned-host doorbell, stage
+// the run's record, and the compute workgroups stage it at the top of the step
+// (no in-step prefetch: the next run's data does not exist yet); after the step
+// the weights are written through to the graph's own variables and workgroup 0
+// publishes loss / accuracy / global_step and a done count to pinned memory.
 #include "common.h"
 
 #include <cstdlib>

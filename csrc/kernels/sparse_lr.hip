@@ -13,11 +13,11 @@
 //   slr_fwd    one wave per batch row: z = b + sum_j W[id_j] val_j (lanes stride
 //              the row's ids, DPP wave sum), the row's sigmoid cross-entropy and
 //              dz = (sigmoid(z) - y) / B;
-//   slr_apply  one wave per batch row: W[id_j] -= lr dz val_j by float atomics
-//              at the memory side (TF's ScatterSub on the ps: duplicates combine,
-//              hot Zipf ids included); workgroup 0 also sums dz and the row losses
-//              in a fixed order -> b -= lr sum(dz), the batch's mean loss, and the
-//              graph's global_step += 1.
+//   slr_apply  W[id_j] -= lr dz val_j (TF's ScatterSub on the ps: duplicates
+//              combine): each workgroup sums its 32 rows' updates per id in an LDS
+//              hash table, then one float atomic per distinct id; workgroup 0 also
+//              sums dz and the row losses in a fixed order -> b -= lr sum(dz), the
+//              batch's mean loss, and the graph's global_step += 1.
 //
 // The kernel boundary orders every read of W / b (forward) before any update.
 #include "common.h"
@@ -29,8 +29,9 @@ constexpr int THREADS = 256;   // 4 waves = 4 batch rows per workgroup
 
 __device__ __forceinline__ float xent(float v, float y) { return fmaxf(v, 0.f) - v * y + log1pf(__expf(-fabsf(v))); }
 
+template <typename ID>
 __global__ __launch_bounds__(THREADS) void slr_fwd(const float* __restrict__ W, long long F,
-                                                   const long long* __restrict__ ids,
+                                                   const ID* __restrict__ ids,
                                                    const long long* __restrict__ offsets,
                                                    const float* __restrict__ vals, const float* __restrict__ labels,
                                                    const float* __restrict__ bias, int B, float* __restrict__ dz,
@@ -41,7 +42,7 @@ __global__ __launch_bounds__(THREADS) void slr_fwd(const float* __restrict__ W, 
   const long long s = offsets[b], e = offsets[b + 1];
   float acc = 0.f;
   for (long long j = s + lane; j < e; j += 64) {
-    const long long id = ids[j];
+    const long long id = (long long)ids[j];
     if (id < 0 || id >= F) {   // TF raises on an out-of-range id; counted, skipped
       atomicAdd(bad, 1);
       continue;
@@ -57,24 +58,63 @@ __global__ __launch_bounds__(THREADS) void slr_fwd(const float* __restrict__ W, 
   }
 }
 
-__global__ __launch_bounds__(THREADS) void slr_apply(float* __restrict__ W, long long F,
-                                                     const long long* __restrict__ ids,
+// Scatter-SGD with the updates of a workgroup's rows combined in LDS first:
+// Zipf-distributed ids put the same hot rows of W in most bags, and float
+// atomics on one address serialize at the memory side (32 us per step at
+// B = 500 / 20 k ids with one atomic per entry).  Each workgroup takes RPW
+// consecutive batch rows; every entry's update goes into an LDS open-addressing
+// table (64-bit key CAS, float add), then each occupied slot makes ONE global
+// atomic.  An entry that finds no slot within MAXP probes goes straight to
+// memory.  Workgroup 0 also sums dz and the row losses in a fixed order.
+constexpr int RPW = 32;              // batch rows per workgroup
+constexpr int HSLOTS = 4096;         // LDS table: 32 KB keys + 16 KB values
+constexpr int MAXP = 16;
+constexpr unsigned long long EMPTY = ~0ull;
+
+template <typename ID>
+__global__ __launch_bounds__(THREADS) void slr_apply(float* __restrict__ W, long long F, const ID* __restrict__ ids,
                                                      const long long* __restrict__ offsets,
                                                      const float* __restrict__ vals, const float* __restrict__ dz,
                                                      const float* __restrict__ lrow, const float* __restrict__ lr_ptr,
                                                      float lr_val, float* __restrict__ bias, int B,
                                                      float* __restrict__ loss_out, void* gvar, int gkind) {
+  __shared__ unsigned long long hkey[HSLOTS];
+  __shared__ float hval[HSLOTS];
   const float lr = lr_ptr != nullptr ? *lr_ptr : lr_val;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int b = blockIdx.x * (THREADS / 64) + wv;
-  if (b < B) {
+  for (int i = threadIdx.x; i < HSLOTS; i += THREADS) {
+    hkey[i] = EMPTY;
+    hval[i] = 0.f;
+  }
+  __syncthreads();
+  const int r0 = blockIdx.x * RPW;
+  for (int b = r0 + wv; b < B && b < r0 + RPW; b += THREADS / 64) {
     const float g = -lr * dz[b];
     const long long s = offsets[b], e = offsets[b + 1];
     for (long long j = s + lane; j < e; j += 64) {
-      const long long id = ids[j];
+      const long long id = (long long)ids[j];
       const float v = vals != nullptr ? vals[j] : 1.f;
-      if (id >= 0 && id < F && v != 0.f) atomicAdd(W + id, g * v);   // padding (val 0) touches nothing
+      if (id < 0 || id >= F || v == 0.f) continue;   // padding (val 0) touches nothing
+      const float u = g * v;
+      const unsigned long long key = (unsigned long long)id;
+      unsigned h = (unsigned)(key * 0x9E3779B97F4A7C15ull >> 52) & (HSLOTS - 1);
+      bool done = false;
+      for (int p = 0; p < MAXP; ++p) {
+        const unsigned long long cur = atomicCAS(&hkey[h], EMPTY, key);
+        if (cur == EMPTY || cur == key) {
+          atomicAdd(&hval[h], u);
+          done = true;
+          break;
+        }
+        h = (h + 1) & (HSLOTS - 1);
+      }
+      if (!done) atomicAdd(W + id, u);
     }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < HSLOTS; i += THREADS) {
+    const unsigned long long k = hkey[i];
+    if (k != EMPTY) atomicAdd(W + (long long)k, hval[i]);
   }
   if (blockIdx.x == 0) {   // fixed-order sums of dz and the row losses
     __shared__ float red[2][THREADS / 64];
@@ -111,17 +151,28 @@ __global__ __launch_bounds__(THREADS) void slr_apply(float* __restrict__ W, long
 
 extern "C" {
 
-// gkind: 0 none, 1 f32, 2 i64, 3 i32, 4 f64 (the graph's global_step variable)
-hipError_t dtfk_slr_step(float* W, long long F, const long long* ids, const long long* offsets, const float* vals,
-                         const float* labels, float* bias, int B, const float* lr_ptr, float lr_val, float* dz,
-                         float* lrow, float* loss_out, int* bad, void* gvar, int gkind, hipStream_t stream) {
+// gkind: 0 none, 1 f32, 2 i64, 3 i32, 4 f64 (the graph's global_step variable);
+// ids32: ids are int32 (the packed Session feed when every id < 2^31), else int64
+hipError_t dtfk_slr_step(float* W, long long F, const void* ids, int ids32, const long long* offsets,
+                         const float* vals, const float* labels, float* bias, int B, const float* lr_ptr, float lr_val,
+                         float* dz, float* lrow, float* loss_out, int* bad, void* gvar, int gkind, hipStream_t stream) {
   using namespace dtfk::slr;
   if (B < 1 || gkind < 0 || gkind > 4 || (gkind != 0 && gvar == nullptr)) return hipErrorInvalidValue;
   const int grid = (B + THREADS / 64 - 1) / (THREADS / 64);
-  hipLaunchKernelGGL(slr_fwd, dim3(grid), dim3(THREADS), 0, stream, W, F, ids, offsets, vals, labels, bias, B, dz,
-                     lrow, bad);
-  hipLaunchKernelGGL(slr_apply, dim3(grid), dim3(THREADS), 0, stream, W, F, ids, offsets, vals, dz, lrow, lr_ptr,
-                     lr_val, bias, B, loss_out, gvar, gkind);
+  const int agrid = (B + RPW - 1) / RPW;
+  if (ids32) {
+    auto id = static_cast<const int*>(ids);
+    hipLaunchKernelGGL(slr_fwd<int>, dim3(grid), dim3(THREADS), 0, stream, W, F, id, offsets, vals, labels, bias, B,
+                       dz, lrow, bad);
+    hipLaunchKernelGGL(slr_apply<int>, dim3(agrid), dim3(THREADS), 0, stream, W, F, id, offsets, vals, dz, lrow,
+                       lr_ptr, lr_val, bias, B, loss_out, gvar, gkind);
+  } else {
+    auto id = static_cast<const long long*>(ids);
+    hipLaunchKernelGGL(slr_fwd<long long>, dim3(grid), dim3(THREADS), 0, stream, W, F, id, offsets, vals, labels,
+                       bias, B, dz, lrow, bad);
+    hipLaunchKernelGGL(slr_apply<long long>, dim3(agrid), dim3(THREADS), 0, stream, W, F, id, offsets, vals, dz, lrow,
+                       lr_ptr, lr_val, bias, B, loss_out, gvar, gkind);
+  }
   return hipGetLastError();
 }
 

@@ -21,6 +21,13 @@ this removes is the glue around them in a bf16-compute / fp32-master step:
   fp32 add).  MIOpen keeps the early layers' forwards; the GEMMs win most
   input gradients (ResNet-50 B=128: 20-60 % per layer,
   profiles/resnet50_r4.md).  `DTF_CONV_GEMM`: auto (default) / never.
+* a 3x3 / pad-1 / stride-1-or-2 convolution with 64-multiple channel counts
+  may run on the in-tree implicit-GEMM kernel (`csrc/kernels/conv_igemm.hip`,
+  MFMA, no im2col buffer): its forward, and for stride 1 its input gradient
+  (the same convolution of dy with the flipped, channel-transposed filter),
+  each chosen per shape against MIOpen by the same one-time timing.  The
+  kernel can also emit the BatchNorm statistics partials of its output
+  (`conv3x3(..., stats=)`).  `DTF_CONV_IGEMM`: auto (default) / never / always.
 Any other case (CPU, no shadow, eval under a different dtype) is plain
 `nn.Conv2d`.
 """
@@ -34,6 +41,7 @@ import torch.nn.functional as F
 from . import grad_sink
 
 _POLICY = os.environ.get("DTF_CONV_GEMM", "auto")
+_IGEMM = os.environ.get("DTF_CONV_IGEMM", "auto")
 _choice: dict = {}
 _timings: dict = {}
 
@@ -82,6 +90,94 @@ def _dx_gemm(engine, dy, w16, x_shape, into=None):
 def _C():
     from .. import _native
     return _native.load()
+
+
+def igemm_ok(x, w16, stride, padding, dilation, groups) -> bool:
+    """A 3x3 / pad 1 / stride 1 or 2 conv the in-tree implicit GEMM takes."""
+    return (_IGEMM != "never" and w16.dim() == 4 and w16.shape[2] == 3 and w16.shape[3] == 3
+            and tuple(padding) == (1, 1) and tuple(dilation) == (1, 1) and groups == 1
+            and stride[0] == stride[1] and stride[0] in (1, 2) and x.is_cuda and x.dtype == torch.bfloat16
+            and w16.dtype == torch.bfloat16 and x.is_contiguous(memory_format=torch.channels_last)
+            and w16.is_contiguous(memory_format=torch.channels_last)
+            and bool(_C().conv3x3_supported(x, w16, int(stride[0]))))
+
+
+def conv3x3(x, w16, stride: int = 1, stats=None, out=None):
+    """y = conv2d(x, w16, stride, padding=1) on the in-tree implicit GEMM
+    (channels_last bf16).  `stats`: an fp32 [2, P, Cout] buffer (P =
+    `conv3x3_stat_rows`) that receives per-channel sums of y and y^2 per
+    128-row tile -- the partials csrc/kernels/bn.hip's finalize reduces."""
+    N, _, H, W = x.shape
+    Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+    y = _cl_empty(N, w16.shape[0], Ho, Wo, x) if out is None else out
+    _C().conv3x3_fwd(x, w16, y, stats, stride, 0)
+    return y
+
+
+def conv3x3_stat_rows(x, stride: int = 1) -> int:
+    return int(_C().conv3x3_tiles(x.shape[0], x.shape[2], x.shape[3], stride))
+
+
+def conv3x3_dx(dy, w16, x_shape):
+    """Input gradient of a stride-1 3x3 conv: conv3x3 of dy with the flipped,
+    channel-transposed filter."""
+    wt = torch.empty((w16.shape[1], w16.shape[0], 3, 3), device=w16.device, dtype=w16.dtype,
+                     memory_format=torch.channels_last)
+    _C().conv3x3_wflip(w16, wt)
+    dx = _cl_empty(x_shape[0], x_shape[1], x_shape[2], x_shape[3], dy)
+    return conv3x3(dy, wt, 1, out=dx)
+
+
+def conv3x3_dw(dy, x, stride: int, into=None):
+    """fp32 weight gradient of y = conv3x3(x, w, stride) for y's gradient dy,
+    accumulated into `into` (an fp32 [Cout, Cin, 3, 3] tensor, contiguous or
+    channels_last) or into a fresh zeroed one."""
+    if into is None:
+        into = torch.zeros((dy.shape[1], x.shape[1], 3, 3), device=dy.device, dtype=torch.float32)
+    _C().conv3x3_wgrad(dy, x, into, stride)
+    return into
+
+
+def _dw3_engine(dy, x, w16, stride: int) -> str:
+    if _IGEMM == "always":
+        return "igemm"
+    key = (tuple(x.shape), w16.shape[0], stride)
+    if ("dw3",) + key not in _choice:
+        if _POLICY == "never":
+            return "miopen"
+        acc = torch.zeros((w16.shape[0], w16.shape[1], 3, 3), device=x.device, dtype=torch.float32)
+
+        def miopen():
+            dw = torch.ops.aten.convolution_backward(dy, x, w16, None, (stride, stride), (1, 1), (1, 1), False,
+                                                     [0, 0], 1, [False, True, False])[1]
+            acc.add_(dw)
+        return _pick("dw3", key, {"miopen": miopen, "igemm": lambda: conv3x3_dw(dy, x, stride, into=acc)})
+    return _choice[("dw3",) + key]
+
+
+def _fwd3_engine(x, w16, stride: int) -> str:
+    if _IGEMM == "always":
+        return "igemm"
+    key = (tuple(x.shape), w16.shape[0], stride)
+    if ("fwd3",) + key not in _choice:
+        if _POLICY == "never":
+            return "miopen"
+        return _pick("fwd3", key, {"miopen": lambda: F.conv2d(x, w16, None, stride, 1),
+                                   "igemm": lambda: conv3x3(x, w16, stride)})
+    return _choice[("fwd3",) + key]
+
+
+def _dx3_engine(dy, x, w16) -> str:
+    if _IGEMM == "always":
+        return "igemm"
+    key = (tuple(x.shape), w16.shape[0], 1)
+    if ("dx3",) + key not in _choice:
+        if _POLICY == "never":
+            return "miopen"
+        return _pick("dx3", key, {"miopen": lambda: torch.ops.aten.convolution_backward(
+                         dy, x, w16, None, (1, 1), (1, 1), (1, 1), False, [0, 0], 1, [True, False, False]),
+                     "igemm": lambda: conv3x3_dx(dy, w16, x.shape)})
+    return _choice[("dx3",) + key]
 
 
 def _pick(role, key, cands) -> str:
@@ -185,6 +281,9 @@ class _ShadowConv(torch.autograd.Function):
             eng = _fwd_engine(x, w16)
             if eng != "miopen":
                 return _fwd_gemm(eng, x, w16)
+        ctx.igemm = igemm_ok(x, w16, stride, padding, dilation, groups)
+        if ctx.igemm and _fwd3_engine(x, w16, int(stride[0])) == "igemm":
+            return conv3x3(x, w16, int(stride[0]))
         return F.conv2d(x, w16, None, stride, padding, dilation, groups)
 
     @staticmethod
@@ -203,8 +302,13 @@ class _ShadowConv(torch.autograd.Function):
                    and _strided_ok(x, w16, stride, padding, dilation, groups))
         dx_eng = _dx_engine(dy, x, w16) if gemm and need_x else "miopen"
         dw_eng = _dw_engine(dy, x, w16) if gemm and need_w else "miopen"
+        dx3 = (_dx3_engine(dy, x, w16) if need_x and getattr(ctx, "igemm", False) and tuple(stride) == (1, 1)
+               and dy.is_contiguous(memory_format=torch.channels_last) else "miopen")
+        dw3 = (_dw3_engine(dy, x, w16, int(stride[0])) if need_w and getattr(ctx, "igemm", False)
+               and dy.is_contiguous(memory_format=torch.channels_last) else "miopen")
         # MIOpen's share: one convolution_backward call for whatever stays on it
-        mx, mw = need_x and dx_eng == "miopen" and not strided, need_w and dw_eng == "miopen"
+        mx = need_x and dx_eng == "miopen" and not strided and dx3 == "miopen"
+        mw = need_w and dw_eng == "miopen" and dw3 == "miopen"
         dx = dw = None
         if mx or mw:
             dx, dw, _ = torch.ops.aten.convolution_backward(dy, x, w16, None, stride, padding, dilation, False,
@@ -221,6 +325,10 @@ class _ShadowConv(torch.autograd.Function):
             else:
                 _C().strided_add(extra, comp, stride[0])
                 dx = extra
+        elif need_x and dx3 == "igemm":
+            dx = conv3x3_dx(dy, w16, x.shape)
+            if extra is not None:
+                dx = dx.add_(extra)
         elif need_x and not mx:
             dx = _dx_gemm(dx_eng, dy, w16, x.shape, into=extra)
         elif need_x and extra is not None:
@@ -232,6 +340,12 @@ class _ShadowConv(torch.autograd.Function):
         if not need_w:
             return dx, None, None, None, None, None, None, None, None
         sink = grad_sink.enabled(w) and (w.grad is None or w.grad.is_contiguous())
+        if dw3 == "igemm":      # the in-tree weight gradient accumulates straight into fp32
+            if sink:
+                conv3x3_dw(dy, x, int(stride[0]), into=grad_sink.target(w))
+                grad_sink.done(w)
+                return dx, None, None, None, None, None, None, None, None
+            return dx, conv3x3_dw(dy, x, int(stride[0])).to(w.dtype), None, None, None, None, None, None, None
         if not mw:
             from . import big_gemm
             if sink:

@@ -1,0 +1,10 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests/test_conv_igemm_gpu.py tests/test_bn_gpu.py tests/test_vision_ops_gpu.py -x -q --timeout 150 --timeout-method thread > gpurun_out/r5e_tests.log 2>&1 || { tail -n 40 gpurun_out/r5e_tests.log; exit 1; }
+tail -n 2 gpurun_out/r5e_tests.log
+for mode in auto never; do
+  DTF_CONV_IGEMM=$mode timeout -k 10 400 python scripts/bench_models.py --model resnet50 --steps 30 --warmup 10 > gpurun_out/r5e_resnet_$mode.log 2>&1 || { tail -n 20 gpurun_out/r5e_resnet_$mode.log; exit 1; }
+  grep '^{' gpurun_out/r5e_resnet_$mode.log | tail -n 1
+done
+echo done

@@ -1,0 +1,96 @@
+"""In-tree 3x3 implicit-GEMM convolution (csrc/kernels/conv_igemm.hip) against
+torch's fp32 conv2d of the same bf16 operands: forward at stride 1 / 2 (odd
+spatial sizes, partial last tile, both channel tilings), the BatchNorm
+statistics partials of its output, and the stride-1 input gradient through
+the flipped filter; the ShadowConv2d autograd path on it."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _cl(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+def _close(got, ref, tol=1e-2):
+    err = (got.float() - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    assert err <= tol * scale + 1e-3, (err, scale)
+
+
+@pytest.mark.parametrize("N,C,H,W,K,s", [(2, 64, 14, 14, 64, 1), (3, 128, 9, 7, 192, 1), (2, 64, 15, 13, 128, 2),
+                                         (1, 256, 7, 7, 256, 1), (4, 64, 8, 8, 64, 2)])
+def test_conv3x3_forward_matches_fp32(N, C, H, W, K, s):
+    from distributed_tensorflow_example_amd.ops import conv
+
+    g = torch.Generator(device="cuda").manual_seed(N * 1000 + C + K + s)
+    x = _cl(torch.randn(N, C, H, W, device="cuda", generator=g).bfloat16())
+    w = _cl((torch.randn(K, C, 3, 3, device="cuda", generator=g) * (2.0 / (9 * C)) ** 0.5).bfloat16())
+    assert conv.igemm_ok(x, w, (s, s), (1, 1), (1, 1), 1)
+    P = conv.conv3x3_stat_rows(x, s)
+    part = torch.full((2, P, K), float("nan"), device="cuda")
+    y = conv.conv3x3(x, w, s, stats=part)
+    ref = F.conv2d(x.float(), w.float(), None, s, 1)
+    assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
+    _close(y, ref)
+    # BN statistics of the bf16 output, per channel
+    yf = y.float().permute(0, 2, 3, 1).reshape(-1, K)
+    torch.testing.assert_close(part[0].sum(0), yf.sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(part[1].sum(0), (yf * yf).sum(0), rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("N,C,H,W,K", [(2, 64, 12, 10, 128), (2, 128, 7, 7, 64)])
+def test_conv3x3_input_gradient_matches_fp32(N, C, H, W, K):
+    from distributed_tensorflow_example_amd.ops import conv
+
+    g = torch.Generator(device="cuda").manual_seed(7 + C + K)
+    x = _cl(torch.randn(N, C, H, W, device="cuda", generator=g).bfloat16())
+    w = _cl((torch.randn(K, C, 3, 3, device="cuda", generator=g) * 0.05).bfloat16())
+    dy = _cl(torch.randn(N, K, H, W, device="cuda", generator=g).bfloat16())
+    dx = conv.conv3x3_dx(dy, w, x.shape)
+    xr = x.float().requires_grad_(True)
+    F.conv2d(xr, w.float(), None, 1, 1).backward(dy.float())
+    _close(dx, xr.grad)
+
+
+def test_shadow_conv_on_igemm_trains_like_miopen(monkeypatch):
+    """ShadowConv2d (3x3, stride 1) forced onto the in-tree kernel: output and
+    both gradients match the MIOpen path of the same module."""
+    from distributed_tensorflow_example_amd.ops import conv
+
+    torch.manual_seed(0)
+    res = {}
+    for mode in ("always", "never"):
+        monkeypatch.setattr(conv, "_IGEMM", mode)
+        m = conv.ShadowConv2d(64, 64, 3, 1, 1, bias=False).cuda().to(memory_format=torch.channels_last)
+        with torch.no_grad():
+            m.weight.copy_(torch.linspace(-0.05, 0.05, m.weight.numel(), device="cuda").view_as(m.weight))
+        conv.attach_shadows(m)
+        x = _cl(torch.linspace(-1, 1, 2 * 64 * 10 * 10, device="cuda").view(2, 64, 10, 10).sin().bfloat16())
+        x.requires_grad_(True)
+        y = m(x)
+        y.float().square().sum().backward()
+        res[mode] = (y.float(), x.grad.float(), m.weight.grad.float())
+    for a, b in zip(res["always"], res["never"]):
+        _close(a, b, 2e-2)
+
+
+@pytest.mark.parametrize("N,C,H,W,K,s,cl", [(2, 64, 12, 10, 64, 1, True), (2, 128, 9, 7, 192, 1, False),
+                                            (3, 64, 15, 13, 128, 2, True), (2, 256, 7, 7, 128, 1, False)])
+def test_conv3x3_weight_gradient_matches_fp32(N, C, H, W, K, s, cl):
+    """Split-K weight gradient accumulated into an fp32 buffer (channels_last or
+    contiguous) that already holds a gradient."""
+    from distributed_tensorflow_example_amd.ops import conv
+
+    g = torch.Generator(device="cuda").manual_seed(11 + C + K + s)
+    x = _cl(torch.randn(N, C, H, W, device="cuda", generator=g).bfloat16())
+    Ho, Wo = (H - 1) // s + 1, (W - 1) // s + 1
+    dy = _cl(torch.randn(N, K, Ho, Wo, device="cuda", generator=g).bfloat16())
+    w = torch.zeros(K, C, 3, 3, device="cuda", requires_grad=True)
+    F.conv2d(x.float(), w, None, s, 1).backward(dy.float())
+    prior = torch.randn(K, C, 3, 3, device="cuda", generator=g)
+    into = prior.clone().contiguous(memory_format=torch.channels_last if cl else torch.contiguous_format)
+    conv.conv3x3_dw(dy, x, s, into=into)
+    _close(into - prior, w.grad, 2e-3)

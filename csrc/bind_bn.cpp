@@ -32,6 +32,10 @@ long long dtfk_conv3x3_tiles(int N, int H, int W, int stride);
 hipError_t dtfk_conv3x3_wflip(const void* w, void* wt, int K, int C, hipStream_t stream);
 hipError_t dtfk_conv3x3_wgrad(const void* dy, const void* x, float* dw, int N, int H, int W, int C, int K, int stride,
                               int kcrs, hipStream_t stream);
+hipError_t dtfk_bn_fwd_parts(const void* x, const void* res, const float* gamma, const float* beta, void* y,
+                             const float* part, int P, float* mean, float* invstd, float* scale, float* shift,
+                             float* run_mean, float* run_var, int M, int C, float momentum, float eps, int relu,
+                             hipStream_t st);
 }
 
 namespace dtf {
@@ -105,6 +109,23 @@ void bn_fwd(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor gamma, at::T
                  beta.data_ptr<float>(), y.data_ptr(), part.data_ptr<float>(), s, s + C, s + 2 * C, s + 3 * C,
                  optf(run_mean), optf(run_var), (int)M, (int)C, (float)momentum, (float)eps, relu ? 1 : 0, cs()),
      "bn_fwd");
+}
+
+// bn_fwd with the statistics partials [2, P, C] supplied by the producer of x
+void bn_fwd_parts(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor gamma, at::Tensor beta, at::Tensor y,
+                  at::Tensor part, int64_t P, at::Tensor stats, c10::optional<at::Tensor> run_mean,
+                  c10::optional<at::Tensor> run_var, double momentum, double eps, bool relu) {
+  const int64_t C = gamma.numel();
+  const int64_t M = rows_of(x, C);
+  if (rows_of(y, C) != M) throw std::runtime_error("bn_fwd_parts: y shape");
+  if (res.has_value() && rows_of(*res, C) != M) throw std::runtime_error("bn_fwd_parts: residual shape");
+  f32(gamma, C, "gamma"); f32(beta, C, "beta"); f32(stats, 4 * C, "stats"); f32(part, 2 * P * C, "part");
+  float* s = stats.data_ptr<float>();
+  ck(dtfk_bn_fwd_parts(x.data_ptr(), res.has_value() ? res->data_ptr() : nullptr, gamma.data_ptr<float>(),
+                       beta.data_ptr<float>(), y.data_ptr(), part.data_ptr<float>(), (int)P, s, s + C, s + 2 * C,
+                       s + 3 * C, optf(run_mean), optf(run_var), (int)M, (int)C, (float)momentum, (float)eps,
+                       relu ? 1 : 0, cs()),
+     "bn_fwd_parts");
 }
 
 void bn_apply(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor scale, at::Tensor shift, at::Tensor y,
@@ -219,6 +240,7 @@ void conv3x3_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t stride) {
 
 void init_bn(pybind11::module& m) {
   m.def("conv3x3_wgrad", &conv3x3_wgrad);
+  m.def("bn_fwd_parts", &bn_fwd_parts);
   m.def("conv3x3_supported", &conv3x3_supported);
   m.def("conv3x3_tiles", &conv3x3_tiles);
   m.def("conv3x3_fwd", &conv3x3_fwd, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("part") = py::none(),

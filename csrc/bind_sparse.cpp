@@ -13,6 +13,7 @@
 #include <pybind11/numpy.h>
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -90,76 +91,103 @@ class SparseLRPlan {
                   o_lab = o_val + align16(4 * n), total = o_lab + align16(4 * B);
     const int slot = slot_ ^= 1;
     bool ok = true;
+    if (dz_.numel() < B) {
+      dz_ = at::empty({std::max<int64_t>(B, 1024)}, W_.options());
+      lrow_ = at::empty({std::max<int64_t>(B, 1024)}, W_.options());
+    }
+    if (dev_.numel() < total) dev_ = at::empty({std::max<int64_t>(total, 1 << 20)}, W_.options().dtype(at::kByte));
+    if (host_[slot].numel() < total)
+      host_[slot] = at::empty({std::max<int64_t>(total, 1 << 20)}, at::TensorOptions().dtype(at::kByte).pinned_memory(true));
+    hipStream_t st = c10::hip::getCurrentHIPStream().stream();
+    char* d = static_cast<char*>(dev_.data_ptr());
     {
       py::gil_scoped_release nogil;
+      using clk = std::chrono::steady_clock;
+      const auto t0 = clk::now();
       if (pending_[slot]) hck(hipEventSynchronize(ev_[slot]), "SparseLRPlan: staging slot");
       pending_[slot] = false;
-      if (host_[slot].numel() < total) {
-        host_[slot] = at::empty({std::max<int64_t>(total, 1 << 20)}, at::TensorOptions().dtype(at::kByte).pinned_memory(true));
-      }
       char* h = static_cast<char*>(host_[slot].data_ptr());
       int64_t* hid = reinterpret_cast<int64_t*>(h + o_ids);
       int32_t* hid32 = reinterpret_cast<int32_t*>(h + o_ids);
       int64_t* hoff = reinterpret_cast<int64_t*>(h + o_off);
       float* hval = reinterpret_cast<float*>(h + o_val);
       float* hlab = reinterpret_cast<float*>(h + o_lab);
-      // rows -> CSR offsets (counting); in row order: copy straight through, else a
-      // stable counting sort by row (the same bags: the 'sum' combiner)
-      std::vector<int64_t>& cnt = cnt_;
-      cnt.assign((size_t)B + 1, 0);
+      // rows -> CSR offsets: in row order (lr2.py's own feeds, as_tf_feed) the
+      // offsets are the row boundaries, found in one pass; otherwise a stable
+      // counting sort by row (the same bags: the 'sum' combiner)
       bool sorted = true;
-      int64_t prev = 0;
-      for (int64_t j = 0; j < n; ++j) {
-        const int64_t r = *reinterpret_cast<const int64_t*>(ib + j * is0);
-        if (r < 0 || r >= B) {
-          ok = false;
-          break;
+      if (n > 0 && is0 == 16) {   // contiguous [nnz, 2] indices: rows at even int64s
+        const int64_t* rp = reinterpret_cast<const int64_t*>(ib);
+        int64_t bad = 0, down = 0;
+        for (int64_t j = 0; j < n; ++j) bad |= (rp[2 * j] < 0) | (rp[2 * j] >= B);
+        for (int64_t j = 1; j < n; ++j) down |= rp[2 * j] < rp[2 * j - 2];
+        ok = bad == 0;
+        sorted = down == 0;
+      } else {
+        int64_t prev = 0;
+        for (int64_t j = 0; j < n && ok; ++j) {
+          const int64_t r = *reinterpret_cast<const int64_t*>(ib + j * is0);
+          ok = r >= 0 && r < B;
+          sorted = sorted && r >= prev;
+          prev = r;
         }
-        sorted = sorted && r >= prev;
-        prev = r;
-        ++cnt[(size_t)r + 1];
       }
       if (ok) {
-        for (int64_t b = 0; b < B; ++b) cnt[(size_t)b + 1] += cnt[(size_t)b];
-        std::memcpy(hoff, cnt.data(), sizeof(int64_t) * (size_t)(B + 1));
-        // out-of-range ids are kept as such (the kernels count and skip them): in int32
-        // form anything outside [0, F) becomes -1
-        auto put = [&](int64_t d, int64_t id) {
-          if (i32) hid32[d] = (id >= 0 && id < F_) ? (int32_t)id : -1;
-          else hid[d] = id;
-        };
+        auto row = [&](int64_t j) { return *reinterpret_cast<const int64_t*>(ib + j * is0); };
         if (sorted) {
-          if (!i32 && fs == 8) std::memcpy(hid, fb, 8 * (size_t)n);
-          else for (int64_t j = 0; j < n; ++j) put(j, *reinterpret_cast<const int64_t*>(fb + j * fs));
+          int64_t j = 0;
+          for (int64_t b = 0; b < B; ++b) {   // boundary search: rows are non-decreasing
+            hoff[b] = j;
+            while (j < n && row(j) == b) ++j;
+          }
+          hoff[B] = n;
+        } else {
+          std::vector<int64_t>& cnt = cnt_;
+          cnt.assign((size_t)B + 1, 0);
+          for (int64_t j = 0; j < n; ++j) ++cnt[(size_t)row(j) + 1];
+          for (int64_t b = 0; b < B; ++b) cnt[(size_t)b + 1] += cnt[(size_t)b];
+          std::memcpy(hoff, cnt.data(), sizeof(int64_t) * (size_t)(B + 1));
+        }
+        // out-of-range ids are kept as such (the kernels count and skip them): in
+        // int32 form anything outside [0, F) becomes -1
+        const int64_t F = F_;
+        if (sorted) {
+          if (i32 && fs == 8) {
+            const int64_t* f = reinterpret_cast<const int64_t*>(fb);
+            for (int64_t j = 0; j < n; ++j) hid32[j] = ((uint64_t)f[j] < (uint64_t)F) ? (int32_t)f[j] : -1;
+          } else if (!i32 && fs == 8) {
+            std::memcpy(hid, fb, 8 * (size_t)n);
+          } else {
+            for (int64_t j = 0; j < n; ++j) {
+              const int64_t id = *reinterpret_cast<const int64_t*>(fb + j * fs);
+              if (i32) hid32[j] = ((uint64_t)id < (uint64_t)F) ? (int32_t)id : -1;
+              else hid[j] = id;
+            }
+          }
           if (vs == 4) std::memcpy(hval, vb, 4 * (size_t)n);
           else for (int64_t j = 0; j < n; ++j) hval[j] = *reinterpret_cast<const float*>(vb + j * vs);
         } else {
+          std::vector<int64_t>& cnt = cnt_;
           for (int64_t j = 0; j < n; ++j) {
-            const int64_t r = *reinterpret_cast<const int64_t*>(ib + j * is0);
-            const int64_t d = cnt[(size_t)r]++;
-            put(d, *reinterpret_cast<const int64_t*>(fb + j * fs));
-            hval[d] = *reinterpret_cast<const float*>(vb + j * vs);
+            const int64_t dd = cnt[(size_t)row(j)]++;
+            const int64_t id = *reinterpret_cast<const int64_t*>(fb + j * fs);
+            if (i32) hid32[dd] = ((uint64_t)id < (uint64_t)F) ? (int32_t)id : -1;
+            else hid[dd] = id;
+            hval[dd] = *reinterpret_cast<const float*>(vb + j * vs);
           }
         }
         for (int64_t b = 0; b < B; ++b) hlab[b] = *reinterpret_cast<const float*>(yb + b * ys_el);
+        const auto t1 = clk::now();
+        hck(hipMemcpyAsync(d, h, (size_t)total, hipMemcpyHostToDevice, st), "SparseLRPlan: feed copy");
+        hck(hipEventRecord(ev_[slot], st), "SparseLRPlan: event");
+        pending_[slot] = true;
+        launch(d + o_ids, i32, reinterpret_cast<const long long*>(d + o_off), reinterpret_cast<const float*>(d + o_val),
+               reinterpret_cast<const float*>(d + o_lab), (int)B, (float)lr, st);
+        t_[0] += std::chrono::duration<double, std::micro>(t1 - t0).count();
+        t_[1] += std::chrono::duration<double, std::micro>(clk::now() - t1).count();
       }
     }
     if (!ok) return false;
-    if (dev_.numel() < total) dev_ = at::empty({std::max<int64_t>(total, 1 << 20)}, W_.options().dtype(at::kByte));
-    if (dz_.numel() < B) {
-      dz_ = at::empty({std::max<int64_t>(B, 1024)}, W_.options());
-      lrow_ = at::empty({std::max<int64_t>(B, 1024)}, W_.options());
-    }
-    hipStream_t st = c10::hip::getCurrentHIPStream().stream();
-    char* d = static_cast<char*>(dev_.data_ptr());
-    {
-      py::gil_scoped_release nogil;
-      hck(hipMemcpyAsync(d, host_[slot].data_ptr(), (size_t)total, hipMemcpyHostToDevice, st), "SparseLRPlan: feed copy");
-      hck(hipEventRecord(ev_[slot], st), "SparseLRPlan: event");
-      pending_[slot] = true;
-      launch(d + o_ids, i32, reinterpret_cast<const long long*>(d + o_off), reinterpret_cast<const float*>(d + o_val),
-             reinterpret_cast<const float*>(d + o_lab), (int)B, (float)lr, st);
-    }
     ++runs_;
     return true;
   }
@@ -188,6 +216,16 @@ class SparseLRPlan {
   }
 
   at::Tensor loss() const { return loss_.select(0, 0); }   // the last run's mean loss (0-d, device)
+  // host time per run() call, us: feed packing (CSR build + copies into the pinned
+  // slot), then the copy + two launches
+  py::dict timing() const {
+    py::dict dd;
+    const double k = runs_ > 0 ? (double)runs_ : 1.0;
+    dd["pack_us"] = t_[0] / k;
+    dd["enqueue_us"] = t_[1] / k;
+    dd["runs"] = runs_;
+    return dd;
+  }
   int64_t runs() const { return runs_; }
   int64_t bad_ids() const { return bad_.item<int>(); }
 
@@ -207,6 +245,7 @@ class SparseLRPlan {
   bool pending_[2] = {false, false};
   int slot_ = 0, gkind_ = 0;
   int64_t F_ = 0, runs_ = 0;
+  double t_[2] = {0, 0};
 };
 
 void init_sparse(py::module& m) {
@@ -218,6 +257,7 @@ void init_sparse(py::module& m) {
            py::arg("lr"))
       .def("loss", &SparseLRPlan::loss)
       .def("runs", &SparseLRPlan::runs)
+      .def("timing", &SparseLRPlan::timing)
       .def("bad_ids", &SparseLRPlan::bad_ids);
 }
 

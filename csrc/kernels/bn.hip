@@ -353,6 +353,27 @@ hipError_t dtfk_bn_fwd(const void* x, const void* res, const float* gamma, const
   return hipGetLastError();
 }
 
+// the same forward when the per-channel sums of x and x^2 already exist as [2, P, C]
+// partials (written by the producing convolution's epilogue, csrc/kernels/conv_igemm.hip):
+// finalize + apply, no statistics pass over x
+hipError_t dtfk_bn_fwd_parts(const void* x, const void* res, const float* gamma, const float* beta, void* y,
+                             const float* part, int P, float* mean, float* invstd, float* scale, float* shift,
+                             float* run_mean, float* run_var, int M, int C, float momentum, float eps, int relu,
+                             hipStream_t st) {
+  if (C % 8 || P < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_finalize, dim3((C + FIN_C - 1) / FIN_C), dim3(1024), 0, st, part, P, M, C, gamma, beta, mean, invstd,
+                     scale, shift, run_mean, run_var, momentum, eps);
+  const long long n8 = (long long)M * C / 8;
+  const uint16_t* xp = (const uint16_t*)x;
+  const uint16_t* rp = (const uint16_t*)res;
+  uint16_t* yp = (uint16_t*)y;
+  if (res && relu) hipLaunchKernelGGL((bn_apply<true, true>), dim3(ew_grid(n8)), dim3(256), 0, st, xp, rp, scale, shift, yp, n8, C);
+  else if (res) hipLaunchKernelGGL((bn_apply<true, false>), dim3(ew_grid(n8)), dim3(256), 0, st, xp, rp, scale, shift, yp, n8, C);
+  else if (relu) hipLaunchKernelGGL((bn_apply<false, true>), dim3(ew_grid(n8)), dim3(256), 0, st, xp, rp, scale, shift, yp, n8, C);
+  else hipLaunchKernelGGL((bn_apply<false, false>), dim3(ew_grid(n8)), dim3(256), 0, st, xp, rp, scale, shift, yp, n8, C);
+  return hipGetLastError();
+}
+
 // eval-mode / inference apply with given scale/shift
 hipError_t dtfk_bn_apply(const void* x, const void* res, const float* scale, const float* shift, void* y, int M, int C,
                          int relu, hipStream_t st) {

@@ -12,9 +12,14 @@ Matched today -- the headline graph (example.py:93-118):
     train_op = <Optimizer>.minimize(loss, global_step)
     accuracy = Mean(Cast(Equal(ArgMax(Softmax(z3), 1), ArgMax(y_, 1))))   (optional)
 
-A run that fetches train_op executes three exact-fp32 MFMA kernels
-(csrc/kernels/graph_mlp.hip): forward, head + backward of layer 2, and the
-layer-1 weight gradient.  With GradientDescentOptimizer on one worker the
+On one GPU with the MNIST loader's batches (uint8 source, one-hot labels) and
+the reference's 784-100-10 shapes, a run that fetches train_op goes to the
+RESIDENT engine (compat/resident.py): the persistent fp32 kernel
+(csrc/kernels/mlp_persist_f32.hip) stays launched across runs and each run is
+a pinned-memory doorbell -- no launch, no completion round trip.  Every other
+case (float feeds, other shapes or optimizers, several workers) is the
+launched fallback: three exact-fp32 MFMA kernels (csrc/kernels/graph_mlp.hip):
+forward, head + backward of layer 2, and the layer-1 weight gradient.  With GradientDescentOptimizer on one worker the
 SGD update and global_step += 1 happen inside those kernels; otherwise the
 kernels write the four gradients straight into the optimizer's all-reduce
 bucket and the usual sync + fused optimizer step follows.  The loss and
@@ -29,11 +34,13 @@ and lr2.py's sparse logistic regression (lr2.py:359-396) over a partitioned
     loss = Mean(SigmoidCrossEntropyWithLogits(py_x, y))
     train_op = GradientDescentOptimizer(lr).minimize(loss, global_step)
 
-whose train run becomes the native sparse-LR step (models/sparse_lr.py on the
-variables' own storage): the feeds are packed into one pinned buffer and
-copied once, the COO indices become CSR offsets on the host, and on one GPU
-the step -- device-resident dedup, bag, sigmoid-xent, bag backward, scatter
-SGD, bias update -- replays from a hipGraph per (batch, padded id count).
+whose train run becomes the native sparse-LR step on the variables' own
+storage: on one GPU ONE native call (csrc/bind_sparse.cpp SparseLRPlan) packs
+lr2.py's feed arrays (COO indices -> CSR offsets, int32 ids) into a pinned
+slot with the GIL released, copies it once and runs the two kernels of
+csrc/kernels/sparse_lr.hip (bag + sigmoid-xent, LDS-aggregated scatter SGD +
+bias); with several workers, models/sparse_lr.py's sharded step (dedup,
+routing, all-to-all) on packed feeds.
 
 A run is lowered only if nothing else it fetches reads the matched
 variables or interior nodes (those would see post-update weights); anything

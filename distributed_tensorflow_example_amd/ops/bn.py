@@ -32,14 +32,20 @@ _ENABLED = os.environ.get("DTF_FUSED_BN", "1") != "0"
 
 class _FusedBN(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, res, running_mean, running_var, momentum, eps, relu, sink, res_slot=None):
+    def forward(ctx, x, gamma, beta, res, running_mean, running_var, momentum, eps, relu, sink, res_slot=None,
+                pre=None):
         C = _C()
         ch = gamma.numel()
         M = x.numel() // ch
         y = torch.empty_like(x)
         stats = torch.empty(4 * ch, dtype=torch.float32, device=x.device)
-        part = torch.empty(2 * C.bn_partial_rows(M, ch) * ch, dtype=torch.float32, device=x.device)
-        C.bn_fwd(x, res, gamma, beta, y, part, stats, running_mean, running_var, momentum, eps, relu)
+        if pre is not None:
+            # x's producer (a 3x3 conv on the in-tree kernel) wrote the statistics partials
+            part, P = pre
+            C.bn_fwd_parts(x, res, gamma, beta, y, part, P, stats, running_mean, running_var, momentum, eps, relu)
+        else:
+            part = torch.empty(2 * C.bn_partial_rows(M, ch) * ch, dtype=torch.float32, device=x.device)
+            C.bn_fwd(x, res, gamma, beta, y, part, stats, running_mean, running_var, momentum, eps, relu)
         ctx.save_for_backward(x, res if res is not None else torch.empty(0, device=x.device), gamma, stats)
         ctx.has_res, ctx.relu = res is not None, relu
         ctx.sink = sink           # (weight, bias) whose .grad the finalize kernel accumulates into, or None
@@ -71,8 +77,8 @@ class _FusedBN(torch.autograd.Function):
         if ctx.sink is not None:
             grad_sink.done(ctx.sink[0])
             grad_sink.done(ctx.sink[1])
-            return dx, None, None, dres, None, None, None, None, None, None, None
-        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None
+            return dx, None, None, dres, None, None, None, None, None, None, None, None
+        return dx, dgamma, dbeta, dres, None, None, None, None, None, None, None, None
 
 
 class FusedBatchNorm2d(torch.nn.BatchNorm2d):
@@ -114,9 +120,12 @@ class FusedBatchNorm2d(torch.nn.BatchNorm2d):
             if self.track_running_stats:
                 self._pending_batches += 1
             mom = self.momentum
+            pre = getattr(x, "_dtf_bn_part", None)
+            if pre is not None and (pre[0].dim() != 3 or pre[0].shape[2] != x.shape[1]):
+                pre = None
             return _FusedBN.apply(x, self.weight, self.bias, residual, self.running_mean if self.track_running_stats
                                   else None, self.running_var if self.track_running_stats else None, float(mom),
-                                  float(self.eps), bool(relu), self._sink(), residual_slot)
+                                  float(self.eps), bool(relu), self._sink(), residual_slot, pre)
         self._flush_batches()
         y = super().forward(x)
         if residual is not None:

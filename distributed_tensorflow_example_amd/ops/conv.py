@@ -42,6 +42,10 @@ from . import grad_sink
 
 _POLICY = os.environ.get("DTF_CONV_GEMM", "auto")
 _IGEMM = os.environ.get("DTF_CONV_IGEMM", "auto")
+# a 3x3 forward on the in-tree kernel also writes its output's BatchNorm statistics
+# partials; the FusedBatchNorm2d reading that output then skips its statistics pass
+_BN_STATS = os.environ.get("DTF_CONV_BN_STATS", "1") != "0"
+_handoff = {}   # id(conv output) -> (partials, P): from _ShadowConv.forward to ShadowConv2d.forward
 _choice: dict = {}
 _timings: dict = {}
 
@@ -283,6 +287,13 @@ class _ShadowConv(torch.autograd.Function):
                 return _fwd_gemm(eng, x, w16)
         ctx.igemm = igemm_ok(x, w16, stride, padding, dilation, groups)
         if ctx.igemm and _fwd3_engine(x, w16, int(stride[0])) == "igemm":
+            if _BN_STATS:
+                s = int(stride[0])
+                P = conv3x3_stat_rows(x, s)
+                part = torch.empty((2, P, w16.shape[0]), device=x.device, dtype=torch.float32)
+                y = conv3x3(x, w16, s, stats=part)
+                _handoff[id(y)] = (part, P)
+                return y
             return conv3x3(x, w16, int(stride[0]))
         return F.conv2d(x, w16, None, stride, padding, dilation, groups)
 
@@ -373,8 +384,14 @@ class ShadowConv2d(torch.nn.Conv2d):
         their input gradients into one tensor.  Both only take effect on the
         shadow path, which the caller must ensure (`on_shadow_path`)."""
         if self.on_shadow_path(x):
-            return _ShadowConv.apply(x, self.weight, self.weight._shadow, self.stride, self.padding, self.dilation,
-                                     self.groups, grad_slot, share)
+            y = _ShadowConv.apply(x, self.weight, self.weight._shadow, self.stride, self.padding, self.dilation,
+                                  self.groups, grad_slot, share)
+            if _handoff:
+                st = _handoff.pop(id(y), None)
+                _handoff.clear()
+                if st is not None:
+                    y._dtf_bn_part = st     # read by the FusedBatchNorm2d that consumes y
+            return y
         w16 = getattr(self.weight, "_shadow", None)
         if (w16 is not None and x.is_cuda and self.bias is None and self.padding_mode == "zeros"
                 and isinstance(self.padding, tuple)):

@@ -90,6 +90,9 @@ def main():
     sess_ms = (time.perf_counter() - t0) / a.steps * 1e3
     plan = lowering.plan_for(train_op)
     lowered = plan.steps if plan is not None else 0
+    nplan = getattr(plan, "_nplan", None) if plan is not None else None
+    native_split = {k: (round(v, 2) if isinstance(v, float) else v) for k, v in nplan.timing().items()} \
+        if nplan is not None else None
     loss_c = float(sess.run(cross_entropy, feed_dict=feeds[0]))
     del sess
 
@@ -117,6 +120,8 @@ def main():
                       "session_run_ms": round(sess_ms, 4), "native_step_ms": round(nat_ms, 4),
                       "ratio": round(sess_ms / nat_ms, 3), "lowered_runs": lowered,
                       "session_samples_per_s": round(a.batch / sess_ms * 1e3, 1),
+                      "session_native_call_split_us": native_split,
+                      "native_samples_per_s": round(a.batch / nat_ms * 1e3, 1),
                       "loss_after_compat_run": round(loss_c, 5)}), flush=True)
 
 

@@ -94,3 +94,29 @@ def test_conv3x3_weight_gradient_matches_fp32(N, C, H, W, K, s, cl):
     into = prior.clone().contiguous(memory_format=torch.channels_last if cl else torch.contiguous_format)
     conv.conv3x3_dw(dy, x, s, into=into)
     _close(into - prior, w.grad, 2e-3)
+
+
+def test_conv_bn_statistics_handoff(monkeypatch):
+    """3x3 conv on the in-tree kernel -> FusedBatchNorm2d(relu): the BN takes the
+    statistics partials from the conv's epilogue (no statistics pass) and gives
+    the same output, running stats and gradients as the plain path."""
+    from distributed_tensorflow_example_amd.ops import conv
+    from distributed_tensorflow_example_amd.ops.bn import FusedBatchNorm2d
+
+    monkeypatch.setattr(conv, "_IGEMM", "always")
+    res = {}
+    for stats in (True, False):
+        monkeypatch.setattr(conv, "_BN_STATS", stats)
+        torch.manual_seed(3)
+        m = conv.ShadowConv2d(64, 128, 3, 2, 1, bias=False).cuda().to(memory_format=torch.channels_last)
+        bn = FusedBatchNorm2d(128).cuda()
+        conv.attach_shadows(m)
+        x = _cl(torch.randn(4, 64, 15, 15, device="cuda").bfloat16()).requires_grad_(True)
+        y = m(x)
+        assert hasattr(y, "_dtf_bn_part") == stats
+        out = bn(y, relu=True)
+        out.float().square().sum().backward()
+        res[stats] = (out.float(), bn.running_mean.clone(), bn.running_var.clone(), x.grad.float(),
+                      m.weight.grad.float(), bn.weight.grad.float())
+    for a, b in zip(res[True], res[False]):
+        _close(a, b, 1e-2)

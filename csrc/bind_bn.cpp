@@ -30,8 +30,10 @@ hipError_t dtfk_conv3x3_fwd(const void* x, const void* w, void* y, float* part, 
                             int stride, int bn, hipStream_t stream);
 long long dtfk_conv3x3_tiles(int N, int H, int W, int stride);
 hipError_t dtfk_conv3x3_wflip(const void* w, void* wt, int K, int C, hipStream_t stream);
-hipError_t dtfk_conv3x3_wgrad(const void* dy, const void* x, float* dw, int N, int H, int W, int C, int K, int stride,
-                              int kcrs, hipStream_t stream);
+hipError_t dtfk_conv3x3_wgrad(const void* dy, const void* x, float* dw, float* ws, int N, int H, int W, int C, int K,
+                              int stride, int kcrs, hipStream_t stream);
+long long dtfk_conv3x3_wgrad_plan(int N, int H, int W, int C, int K, int stride, int* splits_out, int* sps_out);
+hipError_t dtfk_bn_stat_partials(const void* x, float* part, int M, int C, hipStream_t st);
 hipError_t dtfk_bn_fwd_parts(const void* x, const void* res, const float* gamma, const float* beta, void* y,
                              const float* part, int P, float* mean, float* invstd, float* scale, float* shift,
                              float* run_mean, float* run_var, int M, int C, float momentum, float eps, int relu,
@@ -234,11 +236,30 @@ void conv3x3_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t stride) {
   const int Ho = (H - 1) / (int)stride + 1, Wo = (W - 1) / (int)stride + 1;
   if (dw.size(0) != K || dw.size(1) != C || dy.size(0) != N || dy.size(2) != Ho || dy.size(3) != Wo)
     throw std::runtime_error("conv3x3_wgrad: shapes");
-  ck(dtfk_conv3x3_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), N, H, W, C, K, (int)stride, kcrs, cs()),
+  // split slabs from the caching allocator (freed back to it on return; the
+  // stream-ordered reuse is safe)
+  const long long wsn = dtfk_conv3x3_wgrad_plan(N, H, W, C, K, (int)stride, nullptr, nullptr);
+  at::Tensor ws;
+  if (wsn > 0) ws = at::empty({wsn}, dw.options());
+  ck(dtfk_conv3x3_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), wsn > 0 ? ws.data_ptr<float>() : nullptr, N,
+                        H, W, C, K, (int)stride, kcrs, cs()),
      "conv3x3_wgrad");
 }
 
+// BatchNorm statistics partials of x alone ([2, P, C], P = bn_partial_rows(M, C));
+// returns P.  The convolution engine choice prices a conv without a statistics
+// epilogue with this pass (ops/conv.py).
+int64_t bn_stat_partials(at::Tensor x, at::Tensor part) {
+  const int64_t C = x.dim() == 4 ? x.size(1) : x.size(1);
+  const int64_t M = rows_of(x, C);
+  const int P = dtfk_bn_partial_rows((int)M, (int)C);
+  f32(part, 2LL * P * C, "part");
+  ck(dtfk_bn_stat_partials(x.data_ptr(), part.data_ptr<float>(), (int)M, (int)C, cs()), "bn_stat_partials");
+  return P;
+}
+
 void init_bn(pybind11::module& m) {
+  m.def("bn_stat_partials", &bn_stat_partials);
   m.def("conv3x3_wgrad", &conv3x3_wgrad);
   m.def("bn_fwd_parts", &bn_fwd_parts);
   m.def("conv3x3_supported", &conv3x3_supported);

@@ -879,7 +879,29 @@ class ResidentMLPPlan {
     idle_ = (long long)(idle_s * 1e8);            // s_memrealtime: 100 MHz
     timeout_ = (long long)(timeout_s * 1e8);
     wait_s_ = std::max(5.0, 4.0 * idle_s + timeout_s);
-    hip_check(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking), "hipStreamCreate");
+    // The launch stays resident between runs, so its stream must own a hardware
+    // queue: HIP maps streams onto GPU_MAX_HW_QUEUES (4) queues round-robin, and
+    // any stream sharing the resident kernel's queue (e.g. torch's, reading a
+    // variable) would wait behind it until the idle exit.  A CU mask is a queue
+    // property, so a CU-masked stream (all CUs) gets a queue of its own; a
+    // high-priority stream is the fallback.
+    int ncu = 0;
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, W1.get_device());
+    std::vector<uint32_t> mask((size_t)std::max(1, (ncu + 31) / 32), 0xffffffffu);
+    if (ncu > 0 && hipExtStreamCreateWithCUMask(&st_, (uint32_t)mask.size(), mask.data()) == hipSuccess) {
+      stream_kind_ = "own queue (CU-masked stream)";
+    } else {
+      (void)hipGetLastError();
+      int lo = 0, hi = 0;
+      if (hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess &&
+          hipStreamCreateWithPriority(&st_, hipStreamNonBlocking, hi) == hipSuccess) {
+        stream_kind_ = "high-priority stream";
+      } else {
+        (void)hipGetLastError();
+        hip_check(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking), "hipStreamCreate");
+        stream_kind_ = "plain stream";
+      }
+    }
     hip_check(hipEventCreateWithFlags(&ev_, hipEventDisableTiming), "hipEventCreate");
   }
   ~ResidentMLPPlan() {
@@ -977,6 +999,7 @@ class ResidentMLPPlan {
     d["wait_us"] = t_[1] / n;
     d["runs"] = runs_;
     d["launches"] = launch_id_;
+    d["stream"] = stream_kind_;
     return d;
   }
 
@@ -1022,6 +1045,7 @@ class ResidentMLPPlan {
   int B_, act_, gkind_ = 0;
   bool naive_;
   int64_t rec_h_ = 0;
+  const char* stream_kind_ = "";
   void* mail_ = nullptr;
   char* dmail_ = nullptr;
   long long* door_ = nullptr;

@@ -37,6 +37,9 @@ hipError_t dtfk_gemm_big(const void* A, int lda, int transA, const void* B, int 
 long long dtfk_gemm_big_workspace(int M, int N, int K, int c_bf16, float beta, int act, int split_k, int variant);
 int dtfk_gemm_big_supported(const void* A, int lda, int transA, const void* B, int ldb, int transB, int c_bf16, int M,
                             int N, int K, float beta, int act, int split_k);
+hipError_t dtfk_gemm_bn_stats(const void* A, int lda, int transA, const void* B, int ldb, int transB, void* C, int ldc,
+                              float* colpart, int M, int N, int K, hipStream_t stream);
+int dtfk_gemm_bn_stat_rows(int M);
 hipError_t dtfk_gemm_dgelu(const void* A, int lda, int transA, const void* B, int ldb, int transB, void* C, int ldc,
                            const void* aux, const float* bias, float* colpart, int M, int N, int K, hipStream_t stream);
 hipError_t dtfk_gemm_gelu_aux(const void* A, int lda, int transA, const void* B, int ldb, int transB, void* C,
@@ -163,6 +166,32 @@ bool gemm_big(at::Tensor A, bool transA, at::Tensor B, bool transB, at::Tensor o
                    (int)out.stride(0), opt_ptr<float>(bias), M, N, K, (float)alpha, (float)beta, act, split_k, variant,
                    wsb > 0 ? ws.data_ptr() : nullptr, cs()),
      "gemm_big");   // any launch error is a real error
+  return true;
+}
+
+// out = op(A) op(B) in bf16 plus the BatchNorm statistics partials of out in
+// colpart ([2, ceil(M/128), N] fp32: per-column sums and sums of squares of the
+// stored values per 128 rows) -- a 1x1 convolution feeding a BatchNorm
+// (gemm_big.hip dtfk_gemm_bn_stats).  False (nothing launched) outside the
+// kernel's contract.
+bool gemm_bn_stats(at::Tensor A, bool transA, at::Tensor B, bool transB, at::Tensor out, at::Tensor colpart) {
+  gpu(A, "A"); gpu(B, "B"); gpu(out, "out"); f32c(colpart, "colpart");
+  if (A.dim() != 2 || B.dim() != 2 || out.dim() != 2) throw std::runtime_error("gemm_bn_stats: 2-D");
+  for (const at::Tensor* t : {&A, &B, &out})
+    if (t->scalar_type() != at::kBFloat16 || t->stride(1) != 1)
+      throw std::runtime_error("gemm_bn_stats: bf16, unit inner stride");
+  const int M = (int)(transA ? A.size(1) : A.size(0));
+  const int K = (int)(transA ? A.size(0) : A.size(1));
+  const int N = (int)(transB ? B.size(0) : B.size(1));
+  if ((transB ? B.size(1) : B.size(0)) != K) throw std::runtime_error("gemm_bn_stats inner dimensions differ");
+  if (out.size(0) != M || out.size(1) != N) throw std::runtime_error("gemm_bn_stats: out shape");
+  if (colpart.numel() < 2LL * dtfk_gemm_bn_stat_rows(M) * N)
+    throw std::runtime_error("gemm_bn_stats: colpart needs 2 * ceil(M/128) * N floats");
+  const hipError_t e = dtfk_gemm_bn_stats(A.data_ptr(), (int)A.stride(0), transA, B.data_ptr(), (int)B.stride(0),
+                                          transB, out.data_ptr(), (int)out.stride(0), colpart.data_ptr<float>(), M, N,
+                                          K, cs());
+  if (e == hipErrorInvalidValue) { (void)hipGetLastError(); return false; }   // shape / alignment contract
+  ck(e, "gemm_bn_stats");
   return true;
 }
 
@@ -557,6 +586,9 @@ void init_ops(py::module& m) {
         py::arg("bias") = py::none(), py::arg("act") = 0, py::arg("alpha") = 1.0, py::arg("beta") = 0.0,
         py::arg("split_k") = 0, py::arg("variant") = 0);
   m.def("gemm_big_cfg", &gemm_big_cfg);
+  m.def("gemm_bn_stats", &gemm_bn_stats, py::arg("A"), py::arg("transA"), py::arg("B"), py::arg("transB"),
+        py::arg("out"), py::arg("colpart"));
+  m.def("gemm_bn_stat_rows", [](int64_t M) { return dtfk_gemm_bn_stat_rows((int)M); });
   m.def("gemm_dgelu", &gemm_dgelu, py::arg("A"), py::arg("transA"), py::arg("B"), py::arg("transB"), py::arg("out"),
         py::arg("aux"), py::arg("bias"), py::arg("colpart"), py::arg("dbias"), py::arg("accumulate") = false);
   m.def("gemm_gelu_aux", &gemm_gelu_aux, py::arg("A"), py::arg("transA"), py::arg("B"), py::arg("transB"),

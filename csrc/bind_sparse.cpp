@@ -3,10 +3,14 @@
 // arrays -- labels y [B, 1], SparseTensor indices [nnz, 2] (row, column),
 // feature ids [nnz], values [nnz] (lr2.py:440-446) -- builds the CSR row
 // offsets (a stable counting sort when the COO entries are not in row order),
-// packs ids | offsets | values | labels into a pinned staging slot with the GIL
-// released, issues ONE host-to-device copy and the two step kernels on the
-// caller's stream, and returns without waiting (staging slots are double
-// buffered behind events).  SparseLRPlan.step runs the same kernels on device
+// packs ids | offsets | values | labels into a pinned staging slot (mapped,
+// coherent host memory) with the GIL released and issues the two step kernels
+// on the caller's stream: the forward kernel reads the slot in place and leaves
+// device copies of ids / offsets / values for the apply kernel (DTF_SLR_FEED=
+// stage: a staging kernel copies the slot first; =dma: an SDMA hipMemcpyAsync,
+// which ran as a 36 us blit and cost ~40 us of host time per call on MI355X --
+// profiles/lr2_compat_r5.json).  Returns without waiting (staging slots are
+// double buffered behind events).  SparseLRPlan.step runs the same kernels on device
 // tensors (models/sparse_lr.py, one worker).
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
@@ -14,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -23,6 +28,11 @@ extern "C" {
 hipError_t dtfk_slr_step(float* W, long long F, const void* ids, int ids32, const long long* offsets,
                          const float* vals, const float* labels, float* bias, int B, const float* lr_ptr, float lr_val,
                          float* dz, float* lrow, float* loss_out, int* bad, void* gvar, int gkind, hipStream_t stream);
+hipError_t dtfk_slr_stage(const void* src, void* dst, long long bytes, hipStream_t stream);
+hipError_t dtfk_slr_step_direct(float* W, long long F, const void* hids, int ids32, const long long* hoffsets,
+                                const float* hvals, const float* hlabels, void* ids_d, long long* off_d, float* vals_d,
+                                float* bias, int B, float lr_val, float* dz, float* lrow, float* loss_out, int* bad,
+                                void* gvar, int gkind, hipStream_t stream);
 }
 
 namespace dtf {
@@ -58,10 +68,16 @@ class SparseLRPlan {
     loss_ = at::zeros({1}, fo);
     bad_ = at::zeros({1}, fo.dtype(at::kInt));
     for (int i = 0; i < 2; ++i) hck(hipEventCreateWithFlags(&ev_[i], hipEventDisableTiming), "hipEventCreate");
+    const char* fe = std::getenv("DTF_SLR_FEED");
+    const std::string f = fe != nullptr ? fe : "direct";
+    feed_ = f == "dma" ? 2 : (f == "stage" ? 1 : 0);
   }
   ~SparseLRPlan() {
-    for (auto& e : ev_)
-      if (e) (void)hipEventDestroy(e);
+    for (int i = 0; i < 2; ++i) {
+      if (pending_[i]) (void)hipEventSynchronize(ev_[i]);
+      if (ev_[i]) (void)hipEventDestroy(ev_[i]);
+      if (hbuf_[i]) (void)hipHostFree(hbuf_[i]);
+    }
   }
 
   // lr2.py's feeds (numpy).  False: not applicable (dtypes, shapes, a row index
@@ -84,38 +100,11 @@ class SparseLRPlan {
     if (y.ndim() > 2 || ids.ndim() > 1 || vals.ndim() > 1 || (y.ndim() == 2 && y.shape(1) != 1 && y.shape(0) != 1))
       return false;
     const int64_t ys_el = (y.ndim() == 2 && y.shape(0) == 1) ? y.strides(1) : ys;
-    // ids travel as int32 when the table has < 2^31 rows (lr2's F = 1e9 does): half the bytes
-    const bool i32 = F_ < (1LL << 31);
-    const int64_t isz = i32 ? 4 : 8;
-    const int64_t o_ids = 0, o_off = align16(isz * n), o_val = o_off + align16(8 * (B + 1)),
-                  o_lab = o_val + align16(4 * n), total = o_lab + align16(4 * B);
-    const int slot = slot_ ^= 1;
-    bool ok = true;
-    if (dz_.numel() < B) {
-      dz_ = at::empty({std::max<int64_t>(B, 1024)}, W_.options());
-      lrow_ = at::empty({std::max<int64_t>(B, 1024)}, W_.options());
-    }
-    if (dev_.numel() < total) dev_ = at::empty({std::max<int64_t>(total, 1 << 20)}, W_.options().dtype(at::kByte));
-    if (host_[slot].numel() < total)
-      host_[slot] = at::empty({std::max<int64_t>(total, 1 << 20)}, at::TensorOptions().dtype(at::kByte).pinned_memory(true));
-    hipStream_t st = c10::hip::getCurrentHIPStream().stream();
-    char* d = static_cast<char*>(dev_.data_ptr());
-    {
-      py::gil_scoped_release nogil;
-      using clk = std::chrono::steady_clock;
-      const auto t0 = clk::now();
-      if (pending_[slot]) hck(hipEventSynchronize(ev_[slot]), "SparseLRPlan: staging slot");
-      pending_[slot] = false;
-      char* h = static_cast<char*>(host_[slot].data_ptr());
-      int64_t* hid = reinterpret_cast<int64_t*>(h + o_ids);
-      int32_t* hid32 = reinterpret_cast<int32_t*>(h + o_ids);
-      int64_t* hoff = reinterpret_cast<int64_t*>(h + o_off);
-      float* hval = reinterpret_cast<float*>(h + o_val);
-      float* hlab = reinterpret_cast<float*>(h + o_lab);
+    return submit_(B, n, lr, [&](int64_t* hoff, int64_t* hid, int32_t* hid32, float* hval, float* hlab, bool i32) {
       // rows -> CSR offsets: in row order (lr2.py's own feeds, as_tf_feed) the
       // offsets are the row boundaries, found in one pass; otherwise a stable
       // counting sort by row (the same bags: the 'sum' combiner)
-      bool sorted = true;
+      bool ok = true, sorted = true;
       if (n > 0 && is0 == 16) {   // contiguous [nnz, 2] indices: rows at even int64s
         const int64_t* rp = reinterpret_cast<const int64_t*>(ib);
         int64_t bad = 0, down = 0;
@@ -132,58 +121,167 @@ class SparseLRPlan {
           prev = r;
         }
       }
-      if (ok) {
-        auto row = [&](int64_t j) { return *reinterpret_cast<const int64_t*>(ib + j * is0); };
-        if (sorted) {
-          int64_t j = 0;
-          for (int64_t b = 0; b < B; ++b) {   // boundary search: rows are non-decreasing
-            hoff[b] = j;
-            while (j < n && row(j) == b) ++j;
+      if (!ok) return false;
+      auto row = [&](int64_t j) { return *reinterpret_cast<const int64_t*>(ib + j * is0); };
+      if (sorted) {
+        // row boundaries of the non-decreasing row column: one pass with a rarely
+        // taken branch (a per-row `while (row(j) == b)` scan was ~25 us at 20 k ids)
+        int64_t prev = n > 0 ? row(0) : B;
+        for (int64_t b = 0; b <= prev && b <= B; ++b) hoff[b] = 0;
+        for (int64_t j = 1; j < n; ++j) {
+          const int64_t r = row(j);
+          if (r != prev) {
+            for (int64_t b = prev + 1; b <= r; ++b) hoff[b] = j;
+            prev = r;
           }
-          hoff[B] = n;
-        } else {
-          std::vector<int64_t>& cnt = cnt_;
-          cnt.assign((size_t)B + 1, 0);
-          for (int64_t j = 0; j < n; ++j) ++cnt[(size_t)row(j) + 1];
-          for (int64_t b = 0; b < B; ++b) cnt[(size_t)b + 1] += cnt[(size_t)b];
-          std::memcpy(hoff, cnt.data(), sizeof(int64_t) * (size_t)(B + 1));
         }
-        // out-of-range ids are kept as such (the kernels count and skip them): in
-        // int32 form anything outside [0, F) becomes -1
+        for (int64_t b = prev + 1; b <= B; ++b) hoff[b] = n;
+        pack_ids_(hid, hid32, i32, fb, fs, n);
+        if (vs == 4) std::memcpy(hval, vb, 4 * (size_t)n);
+        else for (int64_t j = 0; j < n; ++j) hval[j] = *reinterpret_cast<const float*>(vb + j * vs);
+      } else {
+        std::vector<int64_t>& cnt = cnt_;
+        cnt.assign((size_t)B + 1, 0);
+        for (int64_t j = 0; j < n; ++j) ++cnt[(size_t)row(j) + 1];
+        for (int64_t b = 0; b < B; ++b) cnt[(size_t)b + 1] += cnt[(size_t)b];
+        std::memcpy(hoff, cnt.data(), sizeof(int64_t) * (size_t)(B + 1));
         const int64_t F = F_;
-        if (sorted) {
-          if (i32 && fs == 8) {
-            const int64_t* f = reinterpret_cast<const int64_t*>(fb);
-            for (int64_t j = 0; j < n; ++j) hid32[j] = ((uint64_t)f[j] < (uint64_t)F) ? (int32_t)f[j] : -1;
-          } else if (!i32 && fs == 8) {
-            std::memcpy(hid, fb, 8 * (size_t)n);
-          } else {
-            for (int64_t j = 0; j < n; ++j) {
-              const int64_t id = *reinterpret_cast<const int64_t*>(fb + j * fs);
-              if (i32) hid32[j] = ((uint64_t)id < (uint64_t)F) ? (int32_t)id : -1;
-              else hid[j] = id;
-            }
-          }
-          if (vs == 4) std::memcpy(hval, vb, 4 * (size_t)n);
-          else for (int64_t j = 0; j < n; ++j) hval[j] = *reinterpret_cast<const float*>(vb + j * vs);
-        } else {
-          std::vector<int64_t>& cnt = cnt_;
-          for (int64_t j = 0; j < n; ++j) {
-            const int64_t dd = cnt[(size_t)row(j)]++;
-            const int64_t id = *reinterpret_cast<const int64_t*>(fb + j * fs);
-            if (i32) hid32[dd] = ((uint64_t)id < (uint64_t)F) ? (int32_t)id : -1;
-            else hid[dd] = id;
-            hval[dd] = *reinterpret_cast<const float*>(vb + j * vs);
-          }
+        for (int64_t j = 0; j < n; ++j) {
+          const int64_t dd = cnt[(size_t)row(j)]++;
+          const int64_t id = *reinterpret_cast<const int64_t*>(fb + j * fs);
+          if (i32) hid32[dd] = ((uint64_t)id < (uint64_t)F) ? (int32_t)id : -1;
+          else hid[dd] = id;
+          hval[dd] = *reinterpret_cast<const float*>(vb + j * vs);
         }
-        for (int64_t b = 0; b < B; ++b) hlab[b] = *reinterpret_cast<const float*>(yb + b * ys_el);
+      }
+      for (int64_t b = 0; b < B; ++b) hlab[b] = *reinterpret_cast<const float*>(yb + b * ys_el);
+      return true;
+    });
+  }
+
+  // A host CSR batch (the native trainer's own layout: labels [B] / [B, 1] f32,
+  // offsets [B + 1] i64, ids [nnz] i64, vals [nnz] f32 or None) through the same
+  // packed feed.  False: not applicable (dtypes / shapes / offsets not a CSR of nnz).
+  bool run_csr(py::array y, py::array offsets, py::array ids, py::object vals_o, double lr) {
+    if (!y.dtype().is(py::dtype::of<float>()) || !offsets.dtype().is(py::dtype::of<int64_t>()) ||
+        !ids.dtype().is(py::dtype::of<int64_t>()))
+      return false;
+    py::array vals;
+    const bool has_v = !vals_o.is_none();
+    if (has_v) {
+      vals = py::array::ensure(vals_o);
+      if (!vals || !vals.dtype().is(py::dtype::of<float>()) || vals.ndim() != 1 || vals.size() != ids.size()) return false;
+    }
+    const int64_t B = y.size(), n = ids.size();
+    if (B < 1 || B > (1 << 30) || offsets.ndim() != 1 || offsets.size() != B + 1 || ids.ndim() != 1) return false;
+    const char* yb = static_cast<const char*>(y.data());
+    const char* ob = static_cast<const char*>(offsets.data());
+    const char* fb = static_cast<const char*>(ids.data());
+    const char* vb = has_v ? static_cast<const char*>(vals.data()) : nullptr;
+    const int64_t ys = (y.ndim() == 2 && y.shape(0) == 1) ? y.strides(1) : (y.ndim() >= 1 ? y.strides(0) : 4);
+    const int64_t os = offsets.strides(0), fs = ids.strides(0), vs = has_v ? vals.strides(0) : 4;
+    if (y.ndim() > 2 || (y.ndim() == 2 && y.shape(1) != 1 && y.shape(0) != 1)) return false;
+    return submit_(B, n, lr, [&](int64_t* hoff, int64_t* hid, int32_t* hid32, float* hval, float* hlab, bool i32) {
+      int64_t prev = 0;
+      for (int64_t b = 0; b <= B; ++b) {
+        const int64_t o = *reinterpret_cast<const int64_t*>(ob + b * os);
+        if (o < prev || o > n || (b == 0 && o != 0)) return false;
+        hoff[b] = prev = o;
+      }
+      if (hoff[B] != n) return false;
+      pack_ids_(hid, hid32, i32, fb, fs, n);
+      if (!has_v) for (int64_t j = 0; j < n; ++j) hval[j] = 1.f;
+      else if (vs == 4) std::memcpy(hval, vb, 4 * (size_t)n);
+      else for (int64_t j = 0; j < n; ++j) hval[j] = *reinterpret_cast<const float*>(vb + j * vs);
+      for (int64_t b = 0; b < B; ++b) hlab[b] = *reinterpret_cast<const float*>(yb + b * ys);
+      return true;
+    });
+  }
+
+ private:
+  // out-of-range ids are kept as such (the kernels count and skip them): in
+  // int32 form anything outside [0, F) becomes -1
+  void pack_ids_(int64_t* hid, int32_t* hid32, bool i32, const char* fb, int64_t fs, int64_t n) const {
+    const int64_t F = F_;
+    if (i32 && fs == 8) {
+      const int64_t* f = reinterpret_cast<const int64_t*>(fb);
+      for (int64_t j = 0; j < n; ++j) hid32[j] = ((uint64_t)f[j] < (uint64_t)F) ? (int32_t)f[j] : -1;
+    } else if (!i32 && fs == 8) {
+      std::memcpy(hid, fb, 8 * (size_t)n);
+    } else {
+      for (int64_t j = 0; j < n; ++j) {
+        const int64_t id = *reinterpret_cast<const int64_t*>(fb + j * fs);
+        if (i32) hid32[j] = ((uint64_t)id < (uint64_t)F) ? (int32_t)id : -1;
+        else hid[j] = id;
+      }
+    }
+  }
+
+  // Packs one batch (fill writes the CSR offsets, ids, values and labels into
+  // the pinned slot) with the GIL released, moves it to the device and launches
+  // the step.  False when fill refused the batch (nothing was launched).
+  template <typename Fill>
+  bool submit_(int64_t B, int64_t n, double lr, Fill&& fill) {
+    // ids travel as int32 when the table has < 2^31 rows (lr2's F = 1e9 does): half the bytes
+    const bool i32 = F_ < (1LL << 31);
+    const int64_t isz = i32 ? 4 : 8;
+    const int64_t o_ids = 0, o_off = align16(isz * n), o_val = o_off + align16(8 * (B + 1)),
+                  o_lab = o_val + align16(4 * n), total = o_lab + align16(4 * B);
+    const int slot = slot_ ^ 1;
+    bool ok = true;
+    if (dz_.numel() < B) {
+      dz_ = at::empty({std::max<int64_t>(B, 1024)}, W_.options());
+      lrow_ = at::empty({std::max<int64_t>(B, 1024)}, W_.options());
+    }
+    if (dev_.numel() < total) dev_ = at::empty({std::max<int64_t>(total, 1 << 20)}, W_.options().dtype(at::kByte));
+    hipStream_t st = c10::hip::getCurrentHIPStream().stream();
+    char* d = static_cast<char*>(dev_.data_ptr());
+    {
+      py::gil_scoped_release nogil;
+      using clk = std::chrono::steady_clock;
+      const auto t0 = clk::now();
+      if (pending_[slot]) hck(hipEventSynchronize(ev_[slot]), "SparseLRPlan: staging slot");
+      pending_[slot] = false;
+      if (hcap_[slot] < total) {   // mapped + coherent: the staging kernel reads it in place
+        if (hbuf_[slot]) hck(hipHostFree(hbuf_[slot]), "hipHostFree");
+        hbuf_[slot] = nullptr;
+        const int64_t cap = std::max<int64_t>(total, 1 << 20);
+        hck(hipHostMalloc(&hbuf_[slot], (size_t)cap, hipHostMallocMapped | hipHostMallocCoherent),
+            "SparseLRPlan: pinned staging slot");
+        hck(hipHostGetDevicePointer(&hdev_[slot], hbuf_[slot], 0), "SparseLRPlan: staging slot device view");
+        hcap_[slot] = cap;
+      }
+      const auto tw = clk::now();   // slot wait (+ first-use allocation) | packing
+      char* h = static_cast<char*>(hbuf_[slot]);
+      ok = fill(reinterpret_cast<int64_t*>(h + o_off), reinterpret_cast<int64_t*>(h + o_ids),
+                reinterpret_cast<int32_t*>(h + o_ids), reinterpret_cast<float*>(h + o_val),
+                reinterpret_cast<float*>(h + o_lab), i32);
+      if (ok) {
+        slot_ = slot;
         const auto t1 = clk::now();
-        hck(hipMemcpyAsync(d, h, (size_t)total, hipMemcpyHostToDevice, st), "SparseLRPlan: feed copy");
-        hck(hipEventRecord(ev_[slot], st), "SparseLRPlan: event");
-        pending_[slot] = true;
-        launch(d + o_ids, i32, reinterpret_cast<const long long*>(d + o_off), reinterpret_cast<const float*>(d + o_val),
-               reinterpret_cast<const float*>(d + o_lab), (int)B, (float)lr, st);
-        t_[0] += std::chrono::duration<double, std::micro>(t1 - t0).count();
+        if (feed_ == 0) {
+          // the forward kernel reads the slot in place and leaves device copies for the apply
+          const char* hd = static_cast<const char*>(hdev_[slot]);
+          hck(dtfk_slr_step_direct(W_.data_ptr<float>(), (long long)F_, hd + o_ids, i32 ? 1 : 0,
+                                   reinterpret_cast<const long long*>(hd + o_off),
+                                   reinterpret_cast<const float*>(hd + o_val), reinterpret_cast<const float*>(hd + o_lab),
+                                   d + o_ids, reinterpret_cast<long long*>(d + o_off), reinterpret_cast<float*>(d + o_val),
+                                   bias_.data_ptr<float>(), (int)B, (float)lr, dz_.data_ptr<float>(),
+                                   lrow_.data_ptr<float>(), loss_.data_ptr<float>(), bad_.data_ptr<int>(),
+                                   gkind_ ? gstep_.data_ptr() : nullptr, gkind_, st),
+              "SparseLRPlan: step");
+          hck(hipEventRecord(ev_[slot], st), "SparseLRPlan: event");
+          pending_[slot] = true;
+        } else {
+          if (feed_ == 2) hck(hipMemcpyAsync(d, h, (size_t)total, hipMemcpyHostToDevice, st), "SparseLRPlan: feed copy");
+          else hck(dtfk_slr_stage(hdev_[slot], d, total, st), "SparseLRPlan: feed staging");
+          hck(hipEventRecord(ev_[slot], st), "SparseLRPlan: event");
+          pending_[slot] = true;
+          launch(d + o_ids, i32, reinterpret_cast<const long long*>(d + o_off), reinterpret_cast<const float*>(d + o_val),
+                 reinterpret_cast<const float*>(d + o_lab), (int)B, (float)lr, st);
+        }
+        t_[2] += std::chrono::duration<double, std::micro>(tw - t0).count();
+        t_[0] += std::chrono::duration<double, std::micro>(t1 - tw).count();
         t_[1] += std::chrono::duration<double, std::micro>(clk::now() - t1).count();
       }
     }
@@ -192,6 +290,7 @@ class SparseLRPlan {
     return true;
   }
 
+ public:
   // device tensors (labels [B] / [B,1] f32, offsets [B+1] i64, ids [nnz] i64, vals [nnz] f32 or None)
   at::Tensor step(at::Tensor labels, at::Tensor offsets, at::Tensor ids, c10::optional<at::Tensor> vals, double lr) {
     TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == at::kFloat && labels.is_contiguous(), "labels");
@@ -216,14 +315,17 @@ class SparseLRPlan {
   }
 
   at::Tensor loss() const { return loss_.select(0, 0); }   // the last run's mean loss (0-d, device)
-  // host time per run() call, us: feed packing (CSR build + copies into the pinned
-  // slot), then the copy + two launches
+  // host time per run() call, us: waiting for the staging slot (the GPU two
+  // steps behind), feed packing (CSR build + copies into the pinned slot), then
+  // the feed transfer + two launches
   py::dict timing() const {
     py::dict dd;
     const double k = runs_ > 0 ? (double)runs_ : 1.0;
     dd["pack_us"] = t_[0] / k;
     dd["enqueue_us"] = t_[1] / k;
+    dd["slot_wait_us"] = t_[2] / k;
     dd["runs"] = runs_;
+    dd["feed"] = feed_ == 2 ? "dma" : (feed_ == 1 ? "staging kernel" : "direct");
     return dd;
   }
   int64_t runs() const { return runs_; }
@@ -239,13 +341,16 @@ class SparseLRPlan {
   }
 
   at::Tensor W_, bias_, gstep_, loss_, bad_, dev_, dz_, lrow_;
-  at::Tensor host_[2];
+  void* hbuf_[2] = {nullptr, nullptr};
+  void* hdev_[2] = {nullptr, nullptr};
+  int64_t hcap_[2] = {0, 0};
+  int feed_ = 0;   // 0 direct (the forward reads the pinned slot), 1 staging kernel, 2 SDMA copy
   std::vector<int64_t> cnt_;
   hipEvent_t ev_[2] = {nullptr, nullptr};
   bool pending_[2] = {false, false};
   int slot_ = 0, gkind_ = 0;
   int64_t F_ = 0, runs_ = 0;
-  double t_[2] = {0, 0};
+  double t_[3] = {0, 0, 0};
 };
 
 void init_sparse(py::module& m) {
@@ -253,6 +358,8 @@ void init_sparse(py::module& m) {
       .def(py::init<at::Tensor, at::Tensor, c10::optional<at::Tensor>>(), py::arg("W"), py::arg("bias"),
            py::arg("gstep") = py::none())
       .def("run", &SparseLRPlan::run, py::arg("y"), py::arg("indices"), py::arg("ids"), py::arg("vals"), py::arg("lr"))
+      .def("run_csr", &SparseLRPlan::run_csr, py::arg("y"), py::arg("offsets"), py::arg("ids"), py::arg("vals"),
+           py::arg("lr"))
       .def("step", &SparseLRPlan::step, py::arg("labels"), py::arg("offsets"), py::arg("ids"), py::arg("vals"),
            py::arg("lr"))
       .def("loss", &SparseLRPlan::loss)

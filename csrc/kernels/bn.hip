@@ -93,27 +93,29 @@ __global__ __launch_bounds__(256) void bn_partials(const uint16_t* __restrict__ 
   bn_tile_store(s, q, part, P, C, c0);
 }
 
-// Column sums of the [2P, C] partials: 1024 threads = 16 channels x 64 row
-// groups, so each thread reads only P / 64 rows per pass (the finalize
-// kernels are latency-bound: ~2 memory round trips instead of ~8 with 64
-// channels x 16 groups), then an LDS tree over the groups (fixed order,
-// deterministic).  Returns (sum of pass 0, sum of pass 1) to the g == 0 threads.
-constexpr int FIN_C = 16, FIN_G = 64;
+// Column sums of the [2P, C] partials: 1024 threads = FC channels x (1024 / FC)
+// row groups, then an LDS tree over the groups (fixed order, deterministic).
+// The finalize kernels are latency-bound chains of partial-row loads: FC = 4
+// for narrow layers (C < 512: 4x the blocks and a quarter of the rows per thread
+// of FC = 16 -- a 64-channel 3x3 conv at 56x56 hands over P = 3136 partial rows),
+// 8 / 16 for wide ones.  Returns (sum of pass 0, sum of pass 1) to the g == 0 threads.
+template <int FC>
 __device__ __forceinline__ void sum_partials(const float* __restrict__ part, int P, int C, int c, int lane, int g,
                                              double& s0, double& s1) {
-  __shared__ double red[2][FIN_G][FIN_C];
+  constexpr int FG = 1024 / FC;
+  __shared__ double red[2][FG][FC];
   double a = 0.0, b = 0.0;
   if (c < C) {
     int p = g;
-    for (; p + 3 * FIN_G < P; p += 4 * FIN_G) {      // four independent loads per sum in flight
-      float x0 = part[(size_t)p * C + c], x1 = part[(size_t)(p + FIN_G) * C + c];
-      float x2 = part[(size_t)(p + 2 * FIN_G) * C + c], x3 = part[(size_t)(p + 3 * FIN_G) * C + c];
-      float y0 = part[((size_t)P + p) * C + c], y1 = part[((size_t)P + p + FIN_G) * C + c];
-      float y2 = part[((size_t)P + p + 2 * FIN_G) * C + c], y3 = part[((size_t)P + p + 3 * FIN_G) * C + c];
+    for (; p + 3 * FG < P; p += 4 * FG) {      // four independent loads per sum in flight
+      float x0 = part[(size_t)p * C + c], x1 = part[(size_t)(p + FG) * C + c];
+      float x2 = part[(size_t)(p + 2 * FG) * C + c], x3 = part[(size_t)(p + 3 * FG) * C + c];
+      float y0 = part[((size_t)P + p) * C + c], y1 = part[((size_t)P + p + FG) * C + c];
+      float y2 = part[((size_t)P + p + 2 * FG) * C + c], y3 = part[((size_t)P + p + 3 * FG) * C + c];
       a += ((double)x0 + x1) + ((double)x2 + x3);
       b += ((double)y0 + y1) + ((double)y2 + y3);
     }
-    for (; p < P; p += FIN_G) {
+    for (; p < P; p += FG) {
       a += part[(size_t)p * C + c];
       b += part[((size_t)P + p) * C + c];
     }
@@ -122,7 +124,7 @@ __device__ __forceinline__ void sum_partials(const float* __restrict__ part, int
   red[1][g][lane] = b;
   __syncthreads();
 #pragma unroll
-  for (int st = FIN_G / 2; st > 0; st >>= 1) {
+  for (int st = FG / 2; st > 0; st >>= 1) {
     if (g < st) {
       red[0][g][lane] += red[0][g + st][lane];
       red[1][g][lane] += red[1][g + st][lane];
@@ -134,16 +136,17 @@ __device__ __forceinline__ void sum_partials(const float* __restrict__ part, int
 }
 
 // mean/var (double), running stats, scale = gamma*invstd, shift = beta - mean*scale.
+template <int FC>
 __global__ __launch_bounds__(1024) void bn_finalize(const float* __restrict__ part, int P, int M, int C,
                                                     const float* __restrict__ gamma, const float* __restrict__ beta,
                                                     float* __restrict__ mean, float* __restrict__ invstd,
                                                     float* __restrict__ scale, float* __restrict__ shift,
                                                     float* __restrict__ run_mean, float* __restrict__ run_var,
                                                     float momentum, float eps) {
-  const int lane = threadIdx.x % FIN_C, g = threadIdx.x / FIN_C;
-  const int c = blockIdx.x * FIN_C + lane;
+  const int lane = threadIdx.x % FC, g = threadIdx.x / FC;
+  const int c = blockIdx.x * FC + lane;
   double s, q;
-  sum_partials(part, P, C, c, lane, g, s, q);
+  sum_partials<FC>(part, P, C, c, lane, g, s, q);
   if (g != 0 || c >= C) return;
   const double mu = s / M;
   double var = q / M - mu * mu;
@@ -246,16 +249,17 @@ __global__ __launch_bounds__(256) void bn_bwd_partials(const uint16_t* __restric
 
 // dbeta = sum g, dgamma = sum g*x_hat; dx = gamma*is*(g - dbeta/M - x_hat*dgamma/M)
 //   = A*g + B*x + Cc with A = gamma*is, B = -gamma*is^2*dgamma/M, Cc = -A*dbeta/M - B*mean
+template <int FC>
 __global__ __launch_bounds__(1024) void bn_bwd_finalize(const float* __restrict__ part, int P, int M, int C,
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ mean,
                                                         const float* __restrict__ invstd, float* __restrict__ dgamma,
                                                         float* __restrict__ dbeta, float* __restrict__ coef,
                                                         int accum) {
-  const int lane = threadIdx.x % FIN_C, g = threadIdx.x / FIN_C;
-  const int c = blockIdx.x * FIN_C + lane;
+  const int lane = threadIdx.x % FC, g = threadIdx.x / FC;
+  const int c = blockIdx.x * FC + lane;
   double sgd, sgxd;
-  sum_partials(part, P, C, c, lane, g, sgd, sgxd);
+  sum_partials<FC>(part, P, C, c, lane, g, sgd, sgxd);
   if (g != 0 || c >= C) return;
   const float sg = (float)sgd, sgx = (float)sgxd;
   // accum: dgamma/dbeta are the parameters' .grad (e.g. DDP bucket views) and
@@ -324,6 +328,24 @@ static int bn_grid(int M, int C) {
   if (g > 512) g = 512;
   return g < 1 ? 1 : g;
 }
+// the finalize kernels' channels per block (sum_partials)
+static void launch_finalize(const float* part, int P, int M, int C, const float* gamma, const float* beta, float* mean,
+                            float* invstd, float* scale, float* shift, float* run_mean, float* run_var, float momentum,
+                            float eps, hipStream_t st) {
+#define DTFK_FIN(FC)                                                                                                \
+  hipLaunchKernelGGL((bn_finalize<FC>), dim3((C + FC - 1) / FC), dim3(1024), 0, st, part, P, M, C, gamma, beta, mean, \
+                     invstd, scale, shift, run_mean, run_var, momentum, eps)
+  if (C >= 1024) DTFK_FIN(16); else if (C >= 512) DTFK_FIN(8); else DTFK_FIN(4);
+#undef DTFK_FIN
+}
+static void launch_bwd_finalize(const float* part, int P, int M, int C, const float* gamma, const float* mean,
+                                const float* invstd, float* dgamma, float* dbeta, float* coef, int accum, hipStream_t st) {
+#define DTFK_FIN(FC)                                                                                                   \
+  hipLaunchKernelGGL((bn_bwd_finalize<FC>), dim3((C + FC - 1) / FC), dim3(1024), 0, st, part, P, M, C, gamma, mean, \
+                     invstd, dgamma, dbeta, coef, accum)
+  if (C >= 1024) DTFK_FIN(16); else if (C >= 512) DTFK_FIN(8); else DTFK_FIN(4);
+#undef DTFK_FIN
+}
 static unsigned ew_grid(long long n8) {
   long long g = (n8 + 255) / 256;
   return (unsigned)(g > 16384 ? 16384 : (g < 1 ? 1 : g));
@@ -340,8 +362,7 @@ hipError_t dtfk_bn_fwd(const void* x, const void* res, const float* gamma, const
   if (C % 8) return hipErrorInvalidValue;
   const int P = bn_grid(M, C);
   hipLaunchKernelGGL(bn_partials, dim3((C + 63) / 64, P), dim3(256), 0, st, (const uint16_t*)x, part, M, C);
-  hipLaunchKernelGGL(bn_finalize, dim3((C + FIN_C - 1) / FIN_C), dim3(1024), 0, st, part, P, M, C, gamma, beta, mean, invstd,
-                     scale, shift, run_mean, run_var, momentum, eps);
+  launch_finalize(part, P, M, C, gamma, beta, mean, invstd, scale, shift, run_mean, run_var, momentum, eps, st);
   const long long n8 = (long long)M * C / 8;
   const uint16_t* xp = (const uint16_t*)x;
   const uint16_t* rp = (const uint16_t*)res;
@@ -353,6 +374,14 @@ hipError_t dtfk_bn_fwd(const void* x, const void* res, const float* gamma, const
   return hipGetLastError();
 }
 
+// the statistics pass alone: part [2, P, C] (P = dtfk_bn_partial_rows) -- the
+// cost a convolution without a statistics epilogue leaves to its BatchNorm
+hipError_t dtfk_bn_stat_partials(const void* x, float* part, int M, int C, hipStream_t st) {
+  if (C % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_partials, dim3((C + 63) / 64, bn_grid(M, C)), dim3(256), 0, st, (const uint16_t*)x, part, M, C);
+  return hipGetLastError();
+}
+
 // the same forward when the per-channel sums of x and x^2 already exist as [2, P, C]
 // partials (written by the producing convolution's epilogue, csrc/kernels/conv_igemm.hip):
 // finalize + apply, no statistics pass over x
@@ -361,8 +390,7 @@ hipError_t dtfk_bn_fwd_parts(const void* x, const void* res, const float* gamma,
                              float* run_mean, float* run_var, int M, int C, float momentum, float eps, int relu,
                              hipStream_t st) {
   if (C % 8 || P < 1) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(bn_finalize, dim3((C + FIN_C - 1) / FIN_C), dim3(1024), 0, st, part, P, M, C, gamma, beta, mean, invstd,
-                     scale, shift, run_mean, run_var, momentum, eps);
+  launch_finalize(part, P, M, C, gamma, beta, mean, invstd, scale, shift, run_mean, run_var, momentum, eps, st);
   const long long n8 = (long long)M * C / 8;
   const uint16_t* xp = (const uint16_t*)x;
   const uint16_t* rp = (const uint16_t*)res;
@@ -405,8 +433,7 @@ hipError_t dtfk_bn_bwd(const void* dy, const void* x, const void* res, const flo
   if (res && relu && write_g && dres) {
     hipLaunchKernelGGL((bn_bwd_partials<true, true, true>), dim3((C + 63) / 64, P), dim3(256), 0, st, dyp, xp, rp,
                        mean, invstd, scale, shift, part, M, C, (uint16_t*)dres);
-    hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + FIN_C - 1) / FIN_C), dim3(1024), 0, st, part, P, M, C, gamma, mean, invstd,
-                       dgamma, dbeta, coef, accum);
+    launch_bwd_finalize(part, P, M, C, gamma, mean, invstd, dgamma, dbeta, coef, accum, st);
     hipLaunchKernelGGL((bn_bwd_apply<false, false>), dim3(ew_grid(n8)), dim3(256), 0, st, (const uint16_t*)dres, xp,
                        nullptr, scale, shift, coef, (uint16_t*)dx, nullptr, n8, C);
     return hipGetLastError();
@@ -415,8 +442,7 @@ hipError_t dtfk_bn_bwd(const void* dy, const void* x, const void* res, const flo
   if (res && relu) DTFK_BNP(true, true); else if (res) DTFK_BNP(true, false);
   else if (relu) DTFK_BNP(false, true); else DTFK_BNP(false, false);
 #undef DTFK_BNP
-  hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + FIN_C - 1) / FIN_C), dim3(1024), 0, st, part, P, M, C, gamma, mean, invstd,
-                     dgamma, dbeta, coef, accum);
+  launch_bwd_finalize(part, P, M, C, gamma, mean, invstd, dgamma, dbeta, coef, accum, st);
 #define DTFK_BNA(R, L) hipLaunchKernelGGL((bn_bwd_apply<R, L>), dim3(ew_grid(n8)), dim3(256), 0, st, dyp, xp, rp, scale, shift, coef, (uint16_t*)dx, (uint16_t*)dres, n8, C)
   if (res && relu) DTFK_BNA(true, true); else if (res) DTFK_BNA(true, false);
   else if (relu) DTFK_BNA(false, true); else DTFK_BNA(false, false);

@@ -218,9 +218,13 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_fwd(const uint16_t* __restric
 // ---- weight gradient -------------------------------------------------------
 //   dW[k][r][s][c] += sum_p dy[p][k] * x[n, ho*st + r - 1, wo*st + s - 1, c]
 // GEMM: M = K (output channels), N = 9 C (filter columns (r, s, c) -- the KRSC
-// layout), reduction over the P = N*Ho*Wo output pixels, split over gridDim.z
-// (each split's fp32 tile is added into dW with float atomics: dW is the fp32
-// gradient buffer, so accumulation into an existing gradient is free).  Both
+// layout), reduction over the P = N*Ho*Wo output pixels, split over gridDim.z.
+// Each split writes its fp32 tile as a plain slab (fragment order, 16-byte
+// stores) and wgrad_reduce adds the slabs into dW in split order -- the
+// gradient is deterministic and accumulates into an existing fp32 gradient.
+// (The first version added every split's tile with float atomics: ~16M
+// atomics per call, 5x slower than MIOpen -- profiles/conv3x3_paths_r5.jsonl.)
+// With one split the workgroup adds its tile into dW directly.  Both
 // operands arrive pixel-major -- dy rows [P][K], x rows [.][C] -- so the LDS
 // images are [64 pixels][BM] and [64 pixels][BN] ("M/N-contiguous") and the MFMA
 // fragments are read with the gfx950 transposed LDS read ds_read_b64_tr_b16
@@ -250,7 +254,8 @@ template <int BMW, int BNW>
 __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
                                                          float* __restrict__ dw, int N, int H, int W, int C, int K,
                                                          int Ho, int Wo, int stride, long long xbytes,
-                                                         int steps_per_split, int kcrs) {
+                                                         int steps_per_split, int kcrs, float* __restrict__ ws,
+                                                         long long slab) {
   constexpr int PK = 64;                                        // pixels per step
   constexpr int A_BYTES = PK * BMW * 2, B_BYTES = PK * BNW * 2, BUF = A_BYTES + B_BYTES;
   constexpr int ACPR = BMW / 8, BCPR = BNW / 8;                 // 16-B chunks per image row
@@ -383,8 +388,18 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad(const uint16_t* __restr
     body(step, I0{});
     if (step + 1 < nsteps) body(step + 1, I1{});
   }
-  if (nsteps == 0) return;
   const int fr = lane & 15, fk = lane >> 4;
+  if (ws != nullptr) {
+    // slab of split z, tile (x, y): [wave][TM][TN][64 lanes] f32x4 (zeros for an empty split)
+    float* sl = ws + blockIdx.z * slab + ((long long)blockIdx.y * gridDim.x + blockIdx.x) * (BMW * BNW);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        *reinterpret_cast<f32x4*>(sl + (((wv * TM + i) * TN + j) * 64 + lane) * 4) = acc[i][j];
+    return;
+  }
+  if (nsteps == 0) return;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -396,10 +411,34 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad(const uint16_t* __restr
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int row = m0 + wm * WM + 16 * i + 4 * fk + e;
-        __hip_atomic_fetch_add(dw + (long long)row * NC + cidx, acc[i][j][e], __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+        dw[(long long)row * NC + cidx] += acc[i][j][e];
       }
     }
+}
+
+// dW += sum_z slab_z, in split order: one thread per f32x4 of the fragment-order
+// tiles (the wgrad epilogue's layout), mapped back to (output channel, filter column)
+template <int BMW, int BNW>
+__global__ __launch_bounds__(256) void wgrad_reduce(const float* __restrict__ ws, int S, long long slab,
+                                                    float* __restrict__ dw, int C, int tiles_x, int kcrs) {
+  constexpr int WM = BMW / 2, WN = BNW / 2, TM = WM / 16, TN = WN / 16;
+  constexpr int Q = BMW * BNW / 4;                      // f32x4 per tile
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e * 4 >= slab) return;
+  const int tile = (int)(e / Q), q = (int)(e - (long long)tile * Q);
+  const int lane = q & 63, f = q >> 6;                  // f = (wave * TM + i) * TN + j
+  const int j = f % TN, i = (f / TN) % TM, wv = f / (TN * TM);
+  const int wm = wv >> 1, wn = wv & 1;
+  const int NC = 9 * C;
+  const int col = (tile / tiles_x) * BNW + wn * WN + 16 * j + (lane & 15);
+  if (col >= NC) return;
+  const int row0 = (tile % tiles_x) * BMW + wm * WM + 16 * i + 4 * (lane >> 4);
+  const float* src = ws + e * 4;
+  f32x4 z = *reinterpret_cast<const f32x4*>(src);
+  for (int s = 1; s < S; ++s) z += *reinterpret_cast<const f32x4*>(src + s * slab);
+  const int cidx = kcrs ? (col % C) * 9 + col / C : col;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) dw[(long long)(row0 + r) * NC + cidx] += z[r];
 }
 
 // w' [C][3][3][K] = w [K][2-r][2-s][C]: the filter of the stride-1 input gradient
@@ -439,7 +478,7 @@ hipError_t dtfk_conv3x3_fwd(const void* x, const void* w, void* y, float* part, 
     // 128-wide channel tiles unless that leaves fewer than two workgroups per CU
     // (2 fit per CU) -- the late stages (7x7 / 14x14, 512 channels) have few pixels
     const long long t128 = (M + BM - 1) / BM * (K / 128);
-    bn = (K % 128 == 0 && t128 >= 512) ? 128 : 64;
+    bn = (K % 128 == 0 && t128 >= 256) ? 128 : 64;
   }
   if (K % bn) return hipErrorInvalidValue;
   const dim3 grid((unsigned)((M + BM - 1) / BM), (unsigned)(K / bn));
@@ -471,9 +510,33 @@ hipError_t dtfk_conv3x3_wflip(const void* w, void* wt, int K, int C, hipStream_t
 }
 
 
-// dW (fp32 [K][3][3][C], accumulated into) of y = conv3x3(x, w, stride); dy is y's gradient
-hipError_t dtfk_conv3x3_wgrad(const void* dy, const void* x, float* dw, int N, int H, int W, int C, int K, int stride,
-                              int kcrs, hipStream_t stream) {
+// Split plan of the weight gradient: the number of pixel splits (gridDim.z)
+// and the fp32 workspace (floats) its slabs need (0 with one split).  About two
+// workgroups per CU in total (both resident at once) and at least 8 steps of 64
+// pixels per split: each extra split costs a 64 KB slab write + read.
+long long dtfk_conv3x3_wgrad_plan(int N, int H, int W, int C, int K, int stride, int* splits_out, int* sps_out) {
+  using namespace dtfk::cig;
+  const int Ho = (H + 2 - 3) / stride + 1, Wo = (W + 2 - 3) / stride + 1;
+  const long long P = (long long)N * Ho * Wo;
+  const int NC = 9 * C;
+  const int bm = K % 128 == 0 ? 128 : 64;
+  const int bnw = NC % 128 == 0 ? 128 : 64;
+  const long long tiles = (long long)(K / bm) * ((NC + bnw - 1) / bnw);
+  const long long steps = (P + 63) / 64;
+  long long splits = (512 + tiles - 1) / tiles;
+  if (splits > steps / 8) splits = steps / 8;
+  if (splits < 1) splits = 1;
+  const int sps = (int)((steps + splits - 1) / splits);
+  splits = (steps + sps - 1) / sps;
+  if (splits_out) *splits_out = (int)splits;
+  if (sps_out) *sps_out = sps;
+  return splits > 1 ? splits * tiles * bm * bnw : 0;
+}
+
+// dW (fp32 [K][3][3][C], accumulated into) of y = conv3x3(x, w, stride); dy is
+// y's gradient; ws: dtfk_conv3x3_wgrad_plan's workspace (may be null when it is 0)
+hipError_t dtfk_conv3x3_wgrad(const void* dy, const void* x, float* dw, float* ws, int N, int H, int W, int C, int K,
+                              int stride, int kcrs, hipStream_t stream) {
   using namespace dtfk::cig;
   if (!dtfk_conv3x3_supported(N, H, W, C, K, stride)) return hipErrorInvalidValue;
   const int Ho = (H + 2 - 3) / stride + 1, Wo = (W + 2 - 3) / stride + 1;
@@ -482,22 +545,28 @@ hipError_t dtfk_conv3x3_wgrad(const void* dy, const void* x, float* dw, int N, i
   const int NC = 9 * C;
   const int bm = K % 128 == 0 ? 128 : 64;
   const int bnw = NC % 128 == 0 ? 128 : 64;
-  const long long tiles = (long long)(K / bm) * ((NC + bnw - 1) / bnw);
-  const long long steps = (P + 63) / 64;
-  // about 4 workgroups per CU in total (2 resident at a time), at least 8 steps per split
-  long long splits = (1024 + tiles - 1) / tiles;
-  if (splits > steps / 8) splits = steps / 8;
-  if (splits < 1) splits = 1;
-  const int sps = (int)((steps + splits - 1) / splits);
-  splits = (steps + sps - 1) / sps;
+  int splits = 1, sps = 1;
+  const long long wsn = dtfk_conv3x3_wgrad_plan(N, H, W, C, K, stride, &splits, &sps);
+  if (wsn > 0 && ws == nullptr) return hipErrorInvalidValue;
+  float* wsp = wsn > 0 ? ws : nullptr;
+  const long long slab = wsn > 0 ? wsn / splits : 0;
   const dim3 grid((unsigned)(K / bm), (unsigned)((NC + bnw - 1) / bnw), (unsigned)splits);
   const long long xbytes = (long long)N * H * W * C * 2;
   auto d = static_cast<const uint16_t*>(dy);
   auto xs = static_cast<const uint16_t*>(x);
-  if (bm == 128 && bnw == 128) hipLaunchKernelGGL((conv3x3_wgrad<128, 128>), grid, dim3(NTHR), 0, stream, d, xs, dw, N, H, W, C, K, Ho, Wo, stride, xbytes, sps, kcrs);
-  else if (bm == 128) hipLaunchKernelGGL((conv3x3_wgrad<128, 64>), grid, dim3(NTHR), 0, stream, d, xs, dw, N, H, W, C, K, Ho, Wo, stride, xbytes, sps, kcrs);
-  else if (bnw == 128) hipLaunchKernelGGL((conv3x3_wgrad<64, 128>), grid, dim3(NTHR), 0, stream, d, xs, dw, N, H, W, C, K, Ho, Wo, stride, xbytes, sps, kcrs);
-  else hipLaunchKernelGGL((conv3x3_wgrad<64, 64>), grid, dim3(NTHR), 0, stream, d, xs, dw, N, H, W, C, K, Ho, Wo, stride, xbytes, sps, kcrs);
+#define DTFK_WG(A, B)                                                                                              \
+  do {                                                                                                             \
+    hipLaunchKernelGGL((conv3x3_wgrad<A, B>), grid, dim3(NTHR), 0, stream, d, xs, dw, N, H, W, C, K, Ho, Wo, stride, \
+                       xbytes, sps, kcrs, wsp, slab);                                                              \
+    if (wsp)                                                                                                       \
+      hipLaunchKernelGGL((wgrad_reduce<A, B>), dim3((unsigned)((slab / 4 + 255) / 256)), dim3(256), 0, stream, wsp, \
+                         splits, slab, dw, C, (int)grid.x, kcrs);                                                  \
+  } while (0)
+  if (bm == 128 && bnw == 128) DTFK_WG(128, 128);
+  else if (bm == 128) DTFK_WG(128, 64);
+  else if (bnw == 128) DTFK_WG(64, 128);
+  else DTFK_WG(64, 64);
+#undef DTFK_WG
   return hipGetLastError();
 }
 

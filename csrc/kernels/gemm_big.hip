@@ -476,8 +476,13 @@ __device__ __forceinline__ void raw_barrier() {
 //                colpart[M / 128][N] (the bias gradient's partials, reduced by
 //                colsum_partials);
 //   EP_GELU_AUX  aux = A' B' + bias (the pre-activation the backward needs) and
-//                C = gelu(A' B' + bias), both bf16 with ld = ldc.
-enum Epi { EP_PLAIN = 0, EP_DGELU = 1, EP_GELU_AUX = 2 };
+//                C = gelu(A' B' + bias), both bf16 with ld = ldc;
+//   EP_STATS     C = A' B' (bf16) and, per column, the sum and the sum of
+//                squares of the STORED (bf16-rounded) values over each wave
+//                row's 128 rows to colpart[2][P][N], P = ceil(M / 128): the
+//                BatchNorm statistics partials of a 1x1 convolution's output
+//                (csrc/kernels/bn.hip bn_fwd_parts), edge tiles included.
+enum Epi { EP_PLAIN = 0, EP_DGELU = 1, EP_GELU_AUX = 2, EP_STATS = 3 };
 template <bool AKC, bool BKC, bool OBF, bool SW, int BNT = 256, int EP = EP_PLAIN>
 __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A, int lda,
                                                  const uint16_t* __restrict__ B, int ldb, void* __restrict__ C,
@@ -485,7 +490,7 @@ __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A,
                                                  float alpha, float beta, int act, int kchunk, long long slab = 0,
                                                  uint16_t* __restrict__ aux = nullptr,
                                                  float* __restrict__ colpart = nullptr) {
-  constexpr bool DG = EP == EP_DGELU, GA = EP == EP_GELU_AUX;
+  constexpr bool DG = EP == EP_DGELU, GA = EP == EP_GELU_AUX, ST = EP == EP_STATS;
   static_assert(EP == EP_PLAIN || (OBF && SW && BNT == 256), "GELU epilogues: bf16 out, 256-wide tiles");
   // BNT = 256, or 192 (waves 128 x 48: quadrant column 1 is one 16-wide n tile,
   // its half-tile 64 rows / one DMA per thread) for N where 256 leaves CUs idle
@@ -666,10 +671,16 @@ __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A,
     constexpr int LPR = WN / 8;
     const int rsub = lane / LPR, c8 = (lane % LPR) * 8;
     const bool rb_on = lane < 8 * LPR;
-    float ab[8], cs[8];   // DG: the pre-activation's bias for this lane's 8 columns; their column sums
+    // DG: the pre-activation's bias for this lane's 8 columns; their column sums
+    // (ST: the column sums and sums of squares of the stored values)
+    float ab[8], cs[8], cq[8];
     if constexpr (DG) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) { ab[q] = bias != nullptr ? bias[n0 + wc * WN + c8 + q] : 0.f; cs[q] = 0.f; }
+    }
+    if constexpr (ST) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) { cs[q] = 0.f; cq[q] = 0.f; }
     }
     typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
     // DG: the saved pre-activation of BOTH halves requested up front (16 loads
@@ -753,6 +764,14 @@ __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A,
 #pragma unroll
           for (int q = 0; q < 8; ++q) z[q] = apply_act_slow(z[q], act);
         }
+        if constexpr (ST) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const float r = bf2f(f2bf(z[q]));
+            cs[q] += r;
+            cq[q] += r * r;
+          }
+        }
         if constexpr (OBF) {
           *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(C) + o) =
               make_uint4(pack2bf(z[0], z[1]), pack2bf(z[2], z[3]), pack2bf(z[4], z[5]), pack2bf(z[6], z[7]));
@@ -777,6 +796,70 @@ __global__ __launch_bounds__(NTHR) void gemm_8ph(const uint16_t* __restrict__ A,
         *reinterpret_cast<float4*>(p + 4) = make_float4(cs[4], cs[5], cs[6], cs[7]);
       }
     }
+    if constexpr (ST) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        cs[q] += __shfl_xor(cs[q], 8);
+        cs[q] += __shfl_xor(cs[q], 16);
+        cs[q] += __shfl_xor(cs[q], 32);
+        cq[q] += __shfl_xor(cq[q], 8);
+        cq[q] += __shfl_xor(cq[q], 16);
+        cq[q] += __shfl_xor(cq[q], 32);
+      }
+      if (rsub == 0) {
+        const size_t P = (size_t)((M + 127) >> 7);
+        float* p = colpart + (size_t)((m0 >> 7) + wr) * N + n0 + wc * WN + c8;
+        *reinterpret_cast<float4*>(p) = make_float4(cs[0], cs[1], cs[2], cs[3]);
+        *reinterpret_cast<float4*>(p + 4) = make_float4(cs[4], cs[5], cs[6], cs[7]);
+        *reinterpret_cast<float4*>(p + P * N) = make_float4(cq[0], cq[1], cq[2], cq[3]);
+        *reinterpret_cast<float4*>(p + P * N + 4) = make_float4(cq[4], cq[5], cq[6], cq[7]);
+      }
+    }
+    return;
+  }
+  if constexpr (ST) {
+    // edge tile (rows past M or columns past N): bf16 stores with bounds, and the
+    // per-column partials of this wave row's 128 rows -- each lane sums its 4
+    // columns over its rows, then a butterfly over the 16 row lanes
+    float ps[NJ][4], pq[NJ][4];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { ps[j][r] = 0.f; pq[j][r] = 0.f; }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = m0 + wr * 128 + i * 16 + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int n = n0 + wc * WN + j * 16 + 4 * (lane >> 4);
+        if (m >= M || n >= N) continue;
+        const size_t o = (size_t)m * ldc + n;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (n + r >= N) continue;
+          const uint16_t h = f2bf(alpha * acc[i][j][r]);
+          reinterpret_cast<uint16_t*>(C)[o + r] = h;
+          const float v = bf2f(h);
+          ps[j][r] += v;
+          pq[j][r] += v * v;
+        }
+      }
+    }
+    const size_t P = (size_t)((M + 127) >> 7);
+    const int prow = (m0 >> 7) + wr;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float a = ps[j][r], b = pq[j][r];
+        a += __shfl_xor(a, 1); a += __shfl_xor(a, 2); a += __shfl_xor(a, 4); a += __shfl_xor(a, 8);
+        b += __shfl_xor(b, 1); b += __shfl_xor(b, 2); b += __shfl_xor(b, 4); b += __shfl_xor(b, 8);
+        const int n = n0 + wc * WN + j * 16 + 4 * (lane >> 4) + r;
+        if ((lane & 15) == 0 && n < N && prow < (int)P) {
+          colpart[(size_t)prow * N + n] = a;
+          colpart[(P + prow) * N + n] = b;
+        }
+      }
     return;
   }
   if (vec && m0 + BM <= M && n0 + BNT <= N) {
@@ -1107,6 +1190,37 @@ extern "C" hipError_t dtfk_gemm_gelu_aux(const void* A, int lda, int transA, con
     if (bkc) DTFK_GA(false, true); else DTFK_GA(false, false);
   }
 #undef DTFK_GA
+  return hipGetLastError();
+}
+
+// Partial rows of dtfk_gemm_bn_stats' colpart: [2][P][N] floats
+extern "C" int dtfk_gemm_bn_stat_rows(int M) { return (M + 127) / 128; }
+
+// C = op(A) op(B) in bf16 (ld = ldc) and the BatchNorm statistics partials of C
+// (per-column sums and sums of squares of the stored values per 128 rows) in
+// colpart[2][ceil(M / 128)][N]: a 1x1 convolution's forward whose output feeds
+// a BatchNorm (csrc/kernels/bn.hip bn_fwd_parts finalizes them).  Contract
+// (else hipErrorInvalidValue, nothing launched): dtfk_gemm_big_supported for a
+// bf16 output, K % 128 == 0, N % 8 == 0, ldc % 8 == 0, 16-byte aligned colpart.
+extern "C" hipError_t dtfk_gemm_bn_stats(const void* A, int lda, int transA, const void* B, int ldb, int transB,
+                                         void* C, int ldc, float* colpart, int M, int N, int K, hipStream_t stream) {
+  using namespace dtfk::gemm2;
+  if (K % 128 || N % 8 || ldc % 8 || (reinterpret_cast<uintptr_t>(colpart) & 15) ||
+      !dtfk_gemm_big_supported(A, lda, transA, B, ldb, transB, 1, M, N, K, 0.f, 0, 1))
+    return hipErrorInvalidValue;
+  const dim3 grid((unsigned)(((M + 255) / 256) * ((N + BN - 1) / BN)), 1), block(NTHR);
+  const uint16_t* a = static_cast<const uint16_t*>(A);
+  const uint16_t* b = static_cast<const uint16_t*>(B);
+#define DTFK_ST(AK, BKk)                                                                                         \
+  hipLaunchKernelGGL((gemm_8ph<AK, BKk, true, true, 256, EP_STATS>), grid, block, 0, stream, a, lda, b, ldb, C, \
+                     ldc, nullptr, M, N, K, 1.f, 0.f, 0, K, 0LL, nullptr, colpart)
+  const bool akc = !transA, bkc = transB != 0;
+  if (akc) {
+    if (bkc) DTFK_ST(true, true); else DTFK_ST(true, false);
+  } else {
+    if (bkc) DTFK_ST(false, true); else DTFK_ST(false, false);
+  }
+#undef DTFK_ST
   return hipGetLastError();
 }
 

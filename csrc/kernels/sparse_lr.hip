@@ -29,25 +29,42 @@ constexpr int THREADS = 256;   // 4 waves = 4 batch rows per workgroup
 
 __device__ __forceinline__ float xent(float v, float y) { return fmaxf(v, 0.f) - v * y + log1pf(__expf(-fabsf(v))); }
 
-template <typename ID>
+// COPY: ids / offsets / values / labels are read straight from the packed
+// feed in mapped pinned host memory (one pass, no staging copy in front of the
+// step) and the ids, offsets and values are written to device buffers for
+// slr_apply.
+template <typename ID, bool COPY = false>
 __global__ __launch_bounds__(THREADS) void slr_fwd(const float* __restrict__ W, long long F,
                                                    const ID* __restrict__ ids,
                                                    const long long* __restrict__ offsets,
                                                    const float* __restrict__ vals, const float* __restrict__ labels,
                                                    const float* __restrict__ bias, int B, float* __restrict__ dz,
-                                                   float* __restrict__ lrow, int* __restrict__ bad) {
+                                                   float* __restrict__ lrow, int* __restrict__ bad,
+                                                   ID* __restrict__ ids_out = nullptr,
+                                                   long long* __restrict__ off_out = nullptr,
+                                                   float* __restrict__ vals_out = nullptr) {
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.x * (THREADS / 64) + (threadIdx.x >> 6);
   if (b >= B) return;
   const long long s = offsets[b], e = offsets[b + 1];
+  if constexpr (COPY) {
+    if (lane == 0) off_out[b] = s;
+    if (lane == 1 && b == B - 1) off_out[B] = e;
+  }
   float acc = 0.f;
   for (long long j = s + lane; j < e; j += 64) {
-    const long long id = (long long)ids[j];
+    const ID idr = ids[j];
+    const float v = vals != nullptr ? vals[j] : 1.f;
+    if constexpr (COPY) {
+      ids_out[j] = idr;
+      vals_out[j] = v;
+    }
+    const long long id = (long long)idr;
     if (id < 0 || id >= F) {   // TF raises on an out-of-range id; counted, skipped
       atomicAdd(bad, 1);
       continue;
     }
-    acc += W[id] * (vals != nullptr ? vals[j] : 1.f);
+    acc += W[id] * v;
   }
   acc = wave_sum(acc);
   if (lane == 0) {
@@ -146,10 +163,56 @@ __global__ __launch_bounds__(THREADS) void slr_apply(float* __restrict__ W, long
   }
 }
 
+// The packed Session feed (ids | offsets | values | labels) from mapped, coherent
+// pinned host memory into device memory: one 16-byte load + store per thread.  A
+// kernel on the step's own queue instead of an SDMA copy -- no copy-engine
+// dispatch and no cross-engine wait in front of slr_fwd.
+__global__ __launch_bounds__(256) void slr_stage(const uint4* __restrict__ src, uint4* __restrict__ dst, long long n16) {
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n16; i += (long long)gridDim.x * 256) dst[i] = src[i];
+}
+
 }  // namespace slr
 }  // namespace dtfk
 
 extern "C" {
+
+// The step with its feed read in place from mapped pinned host memory (hids,
+// hoffsets, hvals, hlabels: device views): slr_fwd<COPY> copies ids / offsets /
+// values into ids_d / off_d / vals_d on the way, slr_apply reads those.
+hipError_t dtfk_slr_step_direct(float* W, long long F, const void* hids, int ids32, const long long* hoffsets,
+                                const float* hvals, const float* hlabels, void* ids_d, long long* off_d, float* vals_d,
+                                float* bias, int B, float lr_val, float* dz, float* lrow, float* loss_out, int* bad,
+                                void* gvar, int gkind, hipStream_t stream) {
+  using namespace dtfk::slr;
+  if (B < 1 || gkind < 0 || gkind > 4 || (gkind != 0 && gvar == nullptr) || hvals == nullptr) return hipErrorInvalidValue;
+  const int grid = (B + THREADS / 64 - 1) / (THREADS / 64);
+  const int agrid = (B + RPW - 1) / RPW;
+  if (ids32) {
+    hipLaunchKernelGGL((slr_fwd<int, true>), dim3(grid), dim3(THREADS), 0, stream, W, F, static_cast<const int*>(hids),
+                       hoffsets, hvals, hlabels, bias, B, dz, lrow, bad, static_cast<int*>(ids_d), off_d, vals_d);
+    hipLaunchKernelGGL(slr_apply<int>, dim3(agrid), dim3(THREADS), 0, stream, W, F, static_cast<const int*>(ids_d),
+                       off_d, vals_d, dz, lrow, nullptr, lr_val, bias, B, loss_out, gvar, gkind);
+  } else {
+    hipLaunchKernelGGL((slr_fwd<long long, true>), dim3(grid), dim3(THREADS), 0, stream, W, F,
+                       static_cast<const long long*>(hids), hoffsets, hvals, hlabels, bias, B, dz, lrow, bad,
+                       static_cast<long long*>(ids_d), off_d, vals_d);
+    hipLaunchKernelGGL(slr_apply<long long>, dim3(agrid), dim3(THREADS), 0, stream, W, F,
+                       static_cast<const long long*>(ids_d), off_d, vals_d, dz, lrow, nullptr, lr_val, bias, B,
+                       loss_out, gvar, gkind);
+  }
+  return hipGetLastError();
+}
+
+// bytes: a multiple of 16; src: the device view of mapped pinned host memory
+hipError_t dtfk_slr_stage(const void* src, void* dst, long long bytes, hipStream_t stream) {
+  if (bytes <= 0 || (bytes & 15)) return hipErrorInvalidValue;
+  const long long n16 = bytes / 16;
+  long long g = (n16 + 255) / 256;
+  if (g > 1024) g = 1024;
+  hipLaunchKernelGGL(dtfk::slr::slr_stage, dim3((unsigned)g), dim3(256), 0, stream, static_cast<const uint4*>(src),
+                     static_cast<uint4*>(dst), n16);
+  return hipGetLastError();
+}
 
 // gkind: 0 none, 1 f32, 2 i64, 3 i32, 4 f64 (the graph's global_step variable);
 // ids32: ids are int32 (the packed Session feed when every id < 2^31), else int64

@@ -225,6 +225,10 @@ class _PlanBase:
             self._fetch_ok[key] = ok
         return ok
 
+    def fast_runner(self, flat):
+        """A direct runner for this flat fetch list (Session._fast), or None."""
+        return None
+
 
 class MLPStepPlan(_PlanBase):
     """Fused execution of one matched train op."""
@@ -693,6 +697,38 @@ class SparseLRStepPlan(_PlanBase):
         self.steps += 1
         return True
 
+    def fast_runner(self, flat):
+        """The one-GPU native step without the Session's per-run machinery: once a
+        run of exactly these fetches went through _native_run, the next runs call
+        SparseLRPlan.run on the four feeds straight from the feed dict (keyed by
+        the placeholders themselves).  Taken only when nothing per-run can differ:
+        a constant learning rate, global_step advanced on the device, no fault
+        injection; the fetches are the train op and / or the loss.  Any other
+        feed shape returns None and the run takes the full path."""
+        if self._nplan is None or (self.info["global_step"] is not None and not self._nplan_gs):
+            return None
+        opt = self.info["opt"]
+        if isinstance(opt.learning_rate, Tensor) or os.environ.get("DTF_FAULT_STEP") is not None:
+            return None
+        if not all(f is self.op or f is self.pat.loss for f in flat):
+            return None
+        lr = float(opt.learning_rate)
+        p, nplan, res = self.pat, self._nplan, _resident_mod()
+        y, idx, fids, fvals = p.y, p.idx, p.fids, p.fvals
+        want_loss = [f is p.loss for f in flat]
+        nd = np.ndarray
+
+        def fast(feed):
+            fy, fi, ff, fv = feed.get(y), feed.get(idx), feed.get(fids), feed.get(fvals)
+            if type(fy) is not nd or type(fi) is not nd or type(ff) is not nd or type(fv) is not nd or res._LIVE:
+                return None
+            if not nplan.run(fy, fi, ff, fv, lr):
+                return None
+            opt._steps += 1
+            self.steps += 1
+            return [nplan.loss().cpu().numpy() if wl else None for wl in want_loss]
+        return fast
+
     def run(self, ctx, flat) -> bool:
         from ..models.sparse_lr import SparseLRTrainer
         _debug = _debug_mod()
@@ -779,8 +815,13 @@ def try_lower(session, fetches, ctx, flat=None) -> None:
             f._dtf_plan = plan
         if plan is False or id(f) in ctx.memo:
             continue
-        if plan.fetches_ok(flat):
-            plan.run(ctx, flat)
+        if plan.fetches_ok(flat) and plan.run(ctx, flat) and flat is fetches and \
+                isinstance(getattr(session, "_fast", None), dict):
+            fk = tuple(map(id, flat))
+            if fk not in session._fast:
+                runner = plan.fast_runner(flat)
+                if runner is not None:
+                    session._fast[fk] = runner
 
 
 def plan_for(train_op) -> Optional[_PlanBase]:

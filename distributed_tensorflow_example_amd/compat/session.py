@@ -77,11 +77,24 @@ class Session:
         self._post_run = []
         self._in_post = False
         self._lower = _lowering.enabled()   # DTF_GRAPH_LOWERING, read once per session (not per run)
+        # {fetch ids: runner}: lowered plans' direct runners for a flat fetch list
+        # (compat/lowering.py _PlanBase.fast_runner) -- feed dict in, outputs out,
+        # None = not this run (then the full path runs)
+        self._fast = {}
 
     # ---------------------------------------------------------------- run
     def run(self, fetches, feed_dict=None, options: RunOptions = None, run_metadata=None):
         if self._closed:
             raise RuntimeError("Attempted to use a closed Session.")
+        if self._fast and type(fetches) is list and options is None and feed_dict is not None:
+            fk = tuple(map(id, fetches))
+            fast = self._fast.get(fk)
+            if fast is not None:
+                out = fast(feed_dict)
+                if out is not None:
+                    if self._post_run and not self._in_post:
+                        self._post_hooks()
+                    return out
         ctx = RunContext(feed_dict or {}, self.graph.device)
         ctx.session = self
         ctx.options = options
@@ -101,15 +114,18 @@ class Session:
         else:
             out = self._run(fetches, ctx)
         if self._post_run and not self._in_post:
-            # step-boundary services (Supervisor checkpoints): run in the training
-            # thread between steps, never concurrently with a train op
-            self._in_post = True
-            try:
-                for cb in list(self._post_run):
-                    cb(self)
-            finally:
-                self._in_post = False
+            self._post_hooks()
         return out
+
+    def _post_hooks(self):
+        # step-boundary services (Supervisor checkpoints): run in the training
+        # thread between steps, never concurrently with a train op
+        self._in_post = True
+        try:
+            for cb in list(self._post_run):
+                cb(self)
+        finally:
+            self._in_post = False
 
     def _run(self, f, ctx):
         if f is None:

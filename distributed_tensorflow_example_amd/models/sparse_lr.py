@@ -121,15 +121,22 @@ class SparseLRTrainer(StaticStepMixin):
         return ok
 
     def _train_step_fused(self, batch) -> torch.Tensor:
+        """Host batches (numpy arrays or CPU tensors) go through the plan's packed
+        feed: one CSR pack into a pinned slot, one staging kernel, the two step
+        kernels (SparseLRPlan.run_csr); device batches straight to the kernels."""
         labels, offsets, ids, vals = batch.to(self.device) if hasattr(batch, "to") else batch
         plan = getattr(self, "_plan", None)
         if plan is None:
             from .. import _native
             plan = self._plan = _native.load().SparseLRPlan(self.W.local, self.b.data, None)
+        host = _host_arrays(labels, offsets, ids, vals)
+        if host is not None and plan.run_csr(*host, self.lr):
+            self.global_step += 1
+            return plan.loss()
         dev = self.device
-        loss = plan.step(labels.to(dev, torch.float32).contiguous(), offsets.to(dev, torch.int64).contiguous(),
-                         ids.to(dev, torch.int64).contiguous(),
-                         None if vals is None else vals.to(dev, torch.float32).contiguous(), self.lr)
+        loss = plan.step(_dev(labels, dev, torch.float32), _dev(offsets, dev, torch.int64),
+                         _dev(ids, dev, torch.int64), None if vals is None else _dev(vals, dev, torch.float32),
+                         self.lr)
         self.global_step += 1
         return loss
 
@@ -262,3 +269,26 @@ def steps_per_epoch(world: World, local_batches: int) -> int:
 
 def np_sigmoid(x):
     return 1.0 / (1.0 + np.exp(-x))
+
+
+def _dev(t, dev, dtype):
+    if not torch.is_tensor(t):
+        t = torch.as_tensor(t)
+    return t.to(dev, dtype).contiguous()
+
+
+def _host_arrays(labels, offsets, ids, vals):
+    """numpy views (float32 labels / values, int64 offsets / ids) of a host
+    batch, or None when any part is on a GPU."""
+    out = []
+    for t, dt in ((labels, np.float32), (offsets, np.int64), (ids, np.int64), (vals, np.float32)):
+        if t is None:
+            out.append(None)
+            continue
+        if torch.is_tensor(t):
+            if t.device.type != "cpu":
+                return None
+            t = t.detach().numpy()
+        out.append(np.asarray(t, dtype=dt))
+    return out
+

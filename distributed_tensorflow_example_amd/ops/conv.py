@@ -28,6 +28,12 @@ this removes is the glue around them in a bf16-compute / fp32-master step:
   each chosen per shape against MIOpen by the same one-time timing.  The
   kernel can also emit the BatchNorm statistics partials of its output
   (`conv3x3(..., stats=)`).  `DTF_CONV_IGEMM`: auto (default) / never / always.
+* BatchNorm statistics hand-off (`DTF_CONV_BN_STATS`, default on): the 3x3
+  kernel and the 1x1 gemm_big forward (`dtfk_gemm_bn_stats`) write the
+  per-channel sum / sum-of-squares partials of their output in the epilogue;
+  the FusedBatchNorm2d consuming that output finalizes them instead of
+  re-reading it.  Engine timing charges the engines without the epilogue
+  (MIOpen, hipBLASLt) with that statistics pass.
 Any other case (CPU, no shadow, eval under a different dtype) is plain
 `nn.Conv2d`.
 """
@@ -75,6 +81,27 @@ def _fwd_gemm(engine, x, w16):
     return y
 
 
+def _fwd_gemm_stats(x, w16):
+    """1x1 forward on gemm_big with the BatchNorm statistics partials of y in
+    the epilogue: (y, part [2, P, cout], P), or None outside the kernel's contract."""
+    y = _cl_empty(x.shape[0], w16.shape[0], x.shape[2], x.shape[3], x)
+    x2, w2, y2 = _rows(x), w16.view(w16.shape[0], w16.shape[1]), _rows(y)
+    P = int(_C().gemm_bn_stat_rows(x2.shape[0]))
+    part = torch.empty((2, P, w16.shape[0]), device=x.device, dtype=torch.float32)
+    if not _C().gemm_bn_stats(x2, False, w2, True, y2, part):
+        return None
+    return y, part, P
+
+
+def _stat_pass(y):
+    """The statistics pass a BatchNorm runs over a conv output that came without
+    partials (what the engine timing charges the engines without an epilogue)."""
+    C = _C()
+    part = torch.empty(2 * C.bn_partial_rows(y.numel() // y.shape[1], y.shape[1]) * y.shape[1],
+                       device=y.device, dtype=torch.float32)
+    C.bn_stat_partials(y, part)
+
+
 def _dx_gemm(engine, dy, w16, x_shape, into=None):
     """dx = dy W; with `into` (a channels_last bf16 gradient of x from another
     branch) accumulated in place: dx = into + dy W, one GEMM with beta = 1."""
@@ -106,15 +133,16 @@ def igemm_ok(x, w16, stride, padding, dilation, groups) -> bool:
             and bool(_C().conv3x3_supported(x, w16, int(stride[0]))))
 
 
-def conv3x3(x, w16, stride: int = 1, stats=None, out=None):
+def conv3x3(x, w16, stride: int = 1, stats=None, out=None, bn: int = 0):
     """y = conv2d(x, w16, stride, padding=1) on the in-tree implicit GEMM
     (channels_last bf16).  `stats`: an fp32 [2, P, Cout] buffer (P =
     `conv3x3_stat_rows`) that receives per-channel sums of y and y^2 per
-    128-row tile -- the partials csrc/kernels/bn.hip's finalize reduces."""
+    128-row tile -- the partials csrc/kernels/bn.hip's finalize reduces.
+    `bn`: output-channel tile width (64 / 128; 0 = the kernel's choice)."""
     N, _, H, W = x.shape
     Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
     y = _cl_empty(N, w16.shape[0], Ho, Wo, x) if out is None else out
-    _C().conv3x3_fwd(x, w16, y, stats, stride, 0)
+    _C().conv3x3_fwd(x, w16, y, stats, stride, bn)
     return y
 
 
@@ -166,6 +194,11 @@ def _fwd3_engine(x, w16, stride: int) -> str:
     if ("fwd3",) + key not in _choice:
         if _POLICY == "never":
             return "miopen"
+        if _BN_STATS:   # the igemm epilogue writes the BatchNorm partials MIOpen's output needs a pass for
+            P = conv3x3_stat_rows(x, stride)
+            part = torch.empty((2, P, w16.shape[0]), device=x.device, dtype=torch.float32)
+            return _pick("fwd3", key, {"miopen": lambda: _stat_pass(F.conv2d(x, w16, None, stride, 1)),
+                                       "igemm": lambda: conv3x3(x, w16, stride, stats=part)})
         return _pick("fwd3", key, {"miopen": lambda: F.conv2d(x, w16, None, stride, 1),
                                    "igemm": lambda: conv3x3(x, w16, stride)})
     return _choice[("fwd3",) + key]
@@ -203,9 +236,15 @@ def _fwd_engine(x, w16) -> str:
         return "miopen"
     key = (tuple(x.shape), w16.shape[0])
     if ("fwd",) + key not in _choice:
-        cands = {"miopen": lambda: F.conv2d(x, w16),
-                 "hipblaslt": lambda: _fwd_gemm("hipblaslt", x, w16),
-                 "gemm_big": lambda: _fwd_gemm("gemm_big", x, w16)}
+        if _BN_STATS and _fwd_gemm_stats(x, w16) is not None:
+            # gemm_big hands its output's BatchNorm partials over; the others leave a statistics pass
+            cands = {"miopen": lambda: _stat_pass(F.conv2d(x, w16)),
+                     "hipblaslt": lambda: _stat_pass(_fwd_gemm("hipblaslt", x, w16)),
+                     "gemm_big": lambda: _fwd_gemm_stats(x, w16)}
+        else:
+            cands = {"miopen": lambda: F.conv2d(x, w16),
+                     "hipblaslt": lambda: _fwd_gemm("hipblaslt", x, w16),
+                     "gemm_big": lambda: _fwd_gemm("gemm_big", x, w16)}
         return _pick("fwd", key, cands)
     return _choice[("fwd",) + key]
 
@@ -283,6 +322,11 @@ class _ShadowConv(torch.autograd.Function):
         ctx.gemm = _gemm_ok(x, w16, stride, padding, dilation, groups)
         if ctx.gemm:
             eng = _fwd_engine(x, w16)
+            if eng == "gemm_big" and _BN_STATS:
+                r = _fwd_gemm_stats(x, w16)
+                if r is not None:
+                    _handoff[id(r[0])] = (r[1], r[2])
+                    return r[0]
             if eng != "miopen":
                 return _fwd_gemm(eng, x, w16)
         ctx.igemm = igemm_ok(x, w16, stride, padding, dilation, groups)

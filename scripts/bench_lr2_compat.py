@@ -3,7 +3,8 @@
 graph: replica_device_setter, SparseTensor feeds, embedding_lookup_sparse,
 sigmoid xent, GradientDescentOptimizer) vs the native SparseLRTrainer step on
 the same data -- the lowered Session.run (compat/lowering.py SparseLRStepPlan)
-should cost within 2x of the native step.
+vs the native step on device-resident batches and on the same host (numpy)
+batches the Session is fed.
 
     python scripts/bench_lr2_compat.py [--features 1e9] [--batch 500] [--nnz 40] [--steps 200]
 
@@ -115,10 +116,23 @@ def main():
         tr.train_step(dev_batches[i % 16])
     torch.cuda.synchronize()
     nat_ms = (time.perf_counter() - t0) / a.steps * 1e3
+    # native, host-fed: the same numpy CSR batches each step (the compat Session's
+    # situation -- its feeds are host arrays): SparseLRPlan.run_csr
+    for i in range(a.warmup):
+        tr.train_step(data[i % 16])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        tr.train_step(data[i % 16])
+    torch.cuda.synchronize()
+    host_ms = (time.perf_counter() - t0) / a.steps * 1e3
+    host_split = {k: (round(v, 2) if isinstance(v, float) else v) for k, v in tr._plan.timing().items()}
     print(json.dumps({"metric": "lr2 compat Session.run vs native sparse-LR step (ms)", "features": F,
                       "batch": a.batch, "nnz_per_sample": a.nnz, "steps": a.steps,
                       "session_run_ms": round(sess_ms, 4), "native_step_ms": round(nat_ms, 4),
-                      "ratio": round(sess_ms / nat_ms, 3), "lowered_runs": lowered,
+                      "ratio": round(sess_ms / nat_ms, 3), "native_host_fed_step_ms": round(host_ms, 4),
+                      "ratio_vs_host_fed": round(sess_ms / host_ms, 3), "native_host_fed_split_us": host_split,
+                      "lowered_runs": lowered,
                       "session_samples_per_s": round(a.batch / sess_ms * 1e3, 1),
                       "session_native_call_split_us": native_split,
                       "native_samples_per_s": round(a.batch / nat_ms * 1e3, 1),

@@ -30,6 +30,8 @@ def main():
         r = {"C": C, "H": H, "K": K, "stride": s}
         r["fwd_miopen_us"] = round(big_gemm._time(lambda: F.conv2d(x, w, None, s, 1), reps=10) * 1e3, 1)
         r["fwd_igemm_us"] = round(big_gemm._time(lambda: conv.conv3x3(x, w, s), reps=10) * 1e3, 1)
+        for bn in ((64, 128) if K % 128 == 0 else (64,)):
+            r[f"fwd_igemm_bn{bn}_us"] = round(big_gemm._time(lambda: conv.conv3x3(x, w, s, bn=bn), reps=10) * 1e3, 1)
         P = conv.conv3x3_stat_rows(x, s)
         part = torch.empty(2, P, K, device="cuda")
         r["fwd_igemm_stats_us"] = round(big_gemm._time(lambda: conv.conv3x3(x, w, s, stats=part), reps=10) * 1e3, 1)

@@ -120,3 +120,55 @@ def test_conv_bn_statistics_handoff(monkeypatch):
                       m.weight.grad.float(), bn.weight.grad.float())
     for a, b in zip(res[True], res[False]):
         _close(a, b, 1e-2)
+
+
+@pytest.mark.parametrize("M,K,N", [(2 * 256, 256, 512), (6272, 512, 2048), (3136 // 2, 256, 64), (200, 128, 136)])
+def test_gemm_bn_stats_epilogue(M, K, N):
+    """gemm_big's statistics epilogue (dtfk_gemm_bn_stats): y = x W^T in bf16 and
+    the per-128-row column sums / sums of squares of the STORED y, interior and
+    edge tiles (M % 256 != 0, N % 256 != 0), against fp32 sums of y itself."""
+    from distributed_tensorflow_example_amd import _native
+
+    C = _native.load()
+    torch.manual_seed(M + N)
+    x = torch.randn(M, K, device="cuda").bfloat16()
+    w = (torch.randn(N, K, device="cuda") * 0.05).bfloat16()
+    y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    P = int(C.gemm_bn_stat_rows(M))
+    part = torch.full((2, P, N), float("nan"), device="cuda")
+    assert C.gemm_bn_stats(x, False, w, True, y, part)
+    ref = x.float() @ w.float().t()
+    _close(y.float(), ref, 1e-2)
+    yf = y.float()
+    pad = torch.zeros(P * 128 - M, N, device="cuda")
+    yb = torch.cat([yf, pad]).view(P, 128, N)
+    torch.testing.assert_close(part[0], yb.sum(1), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(part[1], yb.square().sum(1), rtol=1e-4, atol=1e-3)
+
+
+def test_conv1x1_bn_statistics_handoff(monkeypatch):
+    """1x1 conv on gemm_big with the statistics epilogue -> FusedBatchNorm2d(relu):
+    same output, running stats and gradients as the plain path (stats pass in the BN)."""
+    from distributed_tensorflow_example_amd.ops import conv
+    from distributed_tensorflow_example_amd.ops.bn import FusedBatchNorm2d
+
+    res = {}
+    for stats in (True, False):
+        monkeypatch.setattr(conv, "_BN_STATS", stats)
+        conv._choice.clear()
+        torch.manual_seed(5)
+        m = conv.ShadowConv2d(256, 128, 1, 1, 0, bias=False).cuda().to(memory_format=torch.channels_last)
+        bn = FusedBatchNorm2d(128).cuda()
+        conv.attach_shadows(m)
+        x = _cl(torch.randn(4, 256, 14, 14, device="cuda").bfloat16()).requires_grad_(True)
+        key = ("fwd", tuple(x.shape), 128)
+        conv._choice[key] = "gemm_big"
+        y = m(x)
+        assert hasattr(y, "_dtf_bn_part") == stats
+        out = bn(y, relu=True)
+        out.float().square().sum().backward()
+        res[stats] = (out.float(), bn.running_mean.clone(), bn.running_var.clone(), x.grad.float(),
+                      m.weight.grad.float(), bn.weight.grad.float())
+    conv._choice.clear()
+    for a, b in zip(res[True], res[False]):
+        _close(a, b, 1e-2)

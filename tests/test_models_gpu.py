@@ -183,3 +183,37 @@ def test_sparse_lr_fused_step_matches_general(monkeypatch):
     assert fused.global_step == general.global_step == 12
     assert torch.allclose(general.W.local, fused.W.local, atol=1e-5)
     assert torch.allclose(general.b, fused.b, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_sparse_lr_fused_host_batches_match_device_batches():
+    """Host (numpy / CPU tensor) batches take SparseLRPlan.run_csr -- one pinned
+    pack + staging kernel -- and train exactly like the same batches on the GPU."""
+    import numpy as np
+
+    from distributed_tensorflow_example_amd.models.sparse_lr import SparseLRTrainer
+    from distributed_tensorflow_example_amd.parallel import world as W
+
+    w = W.get_world() if W._WORLD is not None else W.init()
+    rng = np.random.default_rng(5)
+    B, F = 300, 200_000
+    host = []
+    for _ in range(5):
+        k = rng.integers(0, 50, B)
+        offs = np.zeros(B + 1, np.int64)
+        np.cumsum(k, out=offs[1:])
+        ids = ((rng.zipf(1.2, int(offs[-1])) - 1) % F).astype(np.int64)
+        host.append(((rng.random((B, 1)) < 0.4).astype(np.float32), offs, ids,
+                     rng.random(int(offs[-1])).astype(np.float32)))
+    dev = [tuple(torch.from_numpy(a).cuda() for a in b) for b in host]
+    a = SparseLRTrainer(F, 0.5, w, seed=7)
+    c = SparseLRTrainer(F, 0.5, w, seed=7)
+    assert a._fused_ok()
+    for i in range(10):
+        hb = host[i % 5] if i % 2 == 0 else tuple(torch.from_numpy(x) for x in host[i % 5])
+        la = float(a.train_step(hb))
+        lc = float(c.train_step(dev[i % 5]))
+        assert abs(la - lc) < 1e-6, i
+    assert a._plan.timing()["runs"] == 10
+    assert torch.equal(a.W.local, c.W.local) or torch.allclose(a.W.local, c.W.local, atol=1e-6)
+    assert torch.allclose(a.b, c.b, atol=1e-7)

@@ -879,28 +879,34 @@ class ResidentMLPPlan {
     idle_ = (long long)(idle_s * 1e8);            // s_memrealtime: 100 MHz
     timeout_ = (long long)(timeout_s * 1e8);
     wait_s_ = std::max(5.0, 4.0 * idle_s + timeout_s);
-    // The launch stays resident between runs, so its stream must own a hardware
-    // queue: HIP maps streams onto GPU_MAX_HW_QUEUES (4) queues round-robin, and
-    // any stream sharing the resident kernel's queue (e.g. torch's, reading a
-    // variable) would wait behind it until the idle exit.  A CU mask is a queue
-    // property, so a CU-masked stream (all CUs) gets a queue of its own; a
-    // high-priority stream is the fallback.
-    int ncu = 0;
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, W1.get_device());
-    std::vector<uint32_t> mask((size_t)std::max(1, (ncu + 31) / 32), 0xffffffffu);
-    if (ncu > 0 && hipExtStreamCreateWithCUMask(&st_, (uint32_t)mask.size(), mask.data()) == hipSuccess) {
-      stream_kind_ = "own queue (CU-masked stream)";
-    } else {
-      (void)hipGetLastError();
+    // The launch stays resident between runs, so no other work may queue behind
+    // it: HIP maps streams onto GPU_MAX_HW_QUEUES (4) hardware queues round-robin,
+    // and a stream sharing the resident kernel's queue (e.g. torch's, reading a
+    // variable) waits until the idle exit.  DTF_RESIDENT_STREAM: "priority"
+    // (default: a non-blocking high-priority stream -- its own queue as long as no
+    // other high-priority stream exists), "cumask" (a CU-masked stream: its own
+    // queue, but BLOCKING -- legacy-default-stream work waits for it; measured:
+    // every variable read waited out the idle bound,
+    // scripts/probes/resident_relaunch.py) or "plain".
+    const char* sk = std::getenv("DTF_RESIDENT_STREAM");
+    const std::string want = sk != nullptr ? sk : "priority";
+    bool made = false;
+    if (want == "cumask") {
+      int ncu = 0;
+      (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, W1.get_device());
+      std::vector<uint32_t> mask((size_t)std::max(1, (ncu + 31) / 32), 0xffffffffu);
+      made = ncu > 0 && hipExtStreamCreateWithCUMask(&st_, (uint32_t)mask.size(), mask.data()) == hipSuccess;
+      if (made) stream_kind_ = "CU-masked (blocking) stream";
+    } else if (want != "plain") {
       int lo = 0, hi = 0;
-      if (hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess &&
-          hipStreamCreateWithPriority(&st_, hipStreamNonBlocking, hi) == hipSuccess) {
-        stream_kind_ = "high-priority stream";
-      } else {
-        (void)hipGetLastError();
-        hip_check(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking), "hipStreamCreate");
-        stream_kind_ = "plain stream";
-      }
+      made = hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess &&
+             hipStreamCreateWithPriority(&st_, hipStreamNonBlocking, hi) == hipSuccess;
+      if (made) stream_kind_ = "high-priority non-blocking stream";
+    }
+    if (!made) {
+      (void)hipGetLastError();
+      hip_check(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking), "hipStreamCreate");
+      stream_kind_ = "plain non-blocking stream";
     }
     hip_check(hipEventCreateWithFlags(&ev_, hipEventDisableTiming), "hipEventCreate");
   }
@@ -943,7 +949,10 @@ class ResidentMLPPlan {
       py::gil_scoped_release nogil;
       using clk = std::chrono::steady_clock;
       const auto t0 = clk::now();
-      if (alive_ && __atomic_load_n(state_, __ATOMIC_ACQUIRE) == launch_id_) reap();   // exited while idle
+      if (alive_ && __atomic_load_n(state_, __ATOMIC_ACQUIRE) == launch_id_) {   // exited while idle
+        reap();
+        ++idle_exits_;
+      }
       if (!alive_) launch();
       const int slot = (int)(runs_ & 1);
       uint8_t* rec = recs_ + slot * rec_h_;
@@ -961,6 +970,7 @@ class ResidentMLPPlan {
               __atomic_load_n(done_, __ATOMIC_ACQUIRE) < runs_ + 1) {
             // the launch stopped (idle) without taking this run: start another
             reap();
+            ++idle_exits_;
             launch();
           }
           if (std::chrono::duration<double>(clk::now() - t1).count() > wait_s_) {
@@ -982,6 +992,7 @@ class ResidentMLPPlan {
   // trained values either way: every step writes them through)
   void stop() {
     if (!alive_) return;
+    ++stops_;
     __atomic_store_n(door_, -1LL, __ATOMIC_RELEASE);
     reap();
   }
@@ -1000,6 +1011,8 @@ class ResidentMLPPlan {
     d["runs"] = runs_;
     d["launches"] = launch_id_;
     d["stream"] = stream_kind_;
+    d["stops"] = stops_;             // host-requested (quiesce / close)
+    d["idle_exits"] = idle_exits_;   // the launch left by itself (idle bound)
     return d;
   }
 
@@ -1046,6 +1059,7 @@ class ResidentMLPPlan {
   bool naive_;
   int64_t rec_h_ = 0;
   const char* stream_kind_ = "";
+  int64_t stops_ = 0, idle_exits_ = 0;
   void* mail_ = nullptr;
   char* dmail_ = nullptr;
   long long* door_ = nullptr;

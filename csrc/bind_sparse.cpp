@@ -29,6 +29,7 @@ hipError_t dtfk_slr_step(float* W, long long F, const void* ids, int ids32, cons
                          const float* vals, const float* labels, float* bias, int B, const float* lr_ptr, float lr_val,
                          float* dz, float* lrow, float* loss_out, int* bad, void* gvar, int gkind, hipStream_t stream);
 hipError_t dtfk_slr_stage(const void* src, void* dst, long long bytes, hipStream_t stream);
+void dtfk_slr_set_rows_per_wg(int rpw);
 hipError_t dtfk_slr_step_direct(float* W, long long F, const void* hids, int ids32, const long long* hoffsets,
                                 const float* hvals, const float* hlabels, void* ids_d, long long* off_d, float* vals_d,
                                 float* bias, int B, float lr_val, float* dz, float* lrow, float* loss_out, int* bad,
@@ -70,14 +71,31 @@ class SparseLRPlan {
     for (int i = 0; i < 2; ++i) hck(hipEventCreateWithFlags(&ev_[i], hipEventDisableTiming), "hipEventCreate");
     const char* fe = std::getenv("DTF_SLR_FEED");
     const std::string f = fe != nullptr ? fe : "direct";
-    feed_ = f == "dma" ? 2 : (f == "stage" ? 1 : 0);
+    feed_ = f == "dma" ? 2 : (f == "stage" ? 1 : (f == "overlap" ? 3 : 0));
+    const char* rp = std::getenv("DTF_SLR_RPW");
+    dtfk_slr_set_rows_per_wg(rp != nullptr ? std::atoi(rp) : 32);
+    if (feed_ == 3) {
+      // the next batch's staging copy runs on a queue of its own, under the
+      // current step's kernels (a CU mask is a queue property: a CU-masked stream
+      // does not share a hardware queue with the compute stream)
+      int ncu = 0;
+      (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, W.get_device());
+      std::vector<uint32_t> mask((size_t)std::max(1, (ncu + 31) / 32), 0xffffffffu);
+      if (ncu <= 0 || hipExtStreamCreateWithCUMask(&side_, (uint32_t)mask.size(), mask.data()) != hipSuccess) {
+        (void)hipGetLastError();
+        hck(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking), "SparseLRPlan: side stream");
+      }
+      for (int i = 0; i < 2; ++i) hck(hipEventCreateWithFlags(&evs_[i], hipEventDisableTiming), "hipEventCreate");
+    }
   }
   ~SparseLRPlan() {
     for (int i = 0; i < 2; ++i) {
       if (pending_[i]) (void)hipEventSynchronize(ev_[i]);
       if (ev_[i]) (void)hipEventDestroy(ev_[i]);
       if (hbuf_[i]) (void)hipHostFree(hbuf_[i]);
+      if (evs_[i]) (void)hipEventDestroy(evs_[i]);
     }
+    if (side_) (void)hipStreamDestroy(side_);
   }
 
   // lr2.py's feeds (numpy).  False: not applicable (dtypes, shapes, a row index
@@ -105,37 +123,34 @@ class SparseLRPlan {
       // offsets are the row boundaries, found in one pass; otherwise a stable
       // counting sort by row (the same bags: the 'sum' combiner)
       bool ok = true, sorted = true;
-      if (n > 0 && is0 == 16) {   // contiguous [nnz, 2] indices: rows at even int64s
-        const int64_t* rp = reinterpret_cast<const int64_t*>(ib);
-        int64_t bad = 0, down = 0;
-        for (int64_t j = 0; j < n; ++j) bad |= (rp[2 * j] < 0) | (rp[2 * j] >= B);
-        for (int64_t j = 1; j < n; ++j) down |= rp[2 * j] < rp[2 * j - 2];
-        ok = bad == 0;
-        sorted = down == 0;
-      } else {
-        int64_t prev = 0;
-        for (int64_t j = 0; j < n && ok; ++j) {
-          const int64_t r = *reinterpret_cast<const int64_t*>(ib + j * is0);
-          ok = r >= 0 && r < B;
-          sorted = sorted && r >= prev;
+      auto row = [&](int64_t j) { return *reinterpret_cast<const int64_t*>(ib + j * is0); };
+      // one pass: row range, order and (in order) the CSR boundaries -- the
+      // common case, lr2.py's own row-major feeds (as_tf_feed); a row out of
+      // order sends the batch to the stable counting sort below
+      int64_t prev = n > 0 ? row(0) : B;
+      if (n > 0 && (prev < 0 || prev >= B)) return false;
+      for (int64_t b = 0; b <= prev && b <= B; ++b) hoff[b] = 0;
+      for (int64_t j = 1; j < n; ++j) {
+        const int64_t r = row(j);
+        if (r != prev) {
+          if (r < prev || r >= B) {
+            sorted = false;
+            break;
+          }
+          for (int64_t b = prev + 1; b <= r; ++b) hoff[b] = j;
           prev = r;
         }
       }
-      if (!ok) return false;
-      auto row = [&](int64_t j) { return *reinterpret_cast<const int64_t*>(ib + j * is0); };
       if (sorted) {
-        // row boundaries of the non-decreasing row column: one pass with a rarely
-        // taken branch (a per-row `while (row(j) == b)` scan was ~25 us at 20 k ids)
-        int64_t prev = n > 0 ? row(0) : B;
-        for (int64_t b = 0; b <= prev && b <= B; ++b) hoff[b] = 0;
-        for (int64_t j = 1; j < n; ++j) {
-          const int64_t r = row(j);
-          if (r != prev) {
-            for (int64_t b = prev + 1; b <= r; ++b) hoff[b] = j;
-            prev = r;
-          }
-        }
         for (int64_t b = prev + 1; b <= B; ++b) hoff[b] = n;
+      } else {
+        for (int64_t j = 0; j < n && ok; ++j) {
+          const int64_t r = row(j);
+          ok = r >= 0 && r < B;
+        }
+      }
+      if (!ok) return false;
+      if (sorted) {
         pack_ids_(hid, hid32, i32, fb, fs, n);
         if (vs == 4) std::memcpy(hval, vb, 4 * (size_t)n);
         else for (int64_t j = 0; j < n; ++j) hval[j] = *reinterpret_cast<const float*>(vb + j * vs);
@@ -233,9 +248,10 @@ class SparseLRPlan {
       dz_ = at::empty({std::max<int64_t>(B, 1024)}, W_.options());
       lrow_ = at::empty({std::max<int64_t>(B, 1024)}, W_.options());
     }
-    if (dev_.numel() < total) dev_ = at::empty({std::max<int64_t>(total, 1 << 20)}, W_.options().dtype(at::kByte));
+    at::Tensor& dvb = feed_ == 3 ? dev2_[slot] : dev_;   // overlap: one device copy per slot
+    if (dvb.numel() < total) dvb = at::empty({std::max<int64_t>(total, 1 << 20)}, W_.options().dtype(at::kByte));
     hipStream_t st = c10::hip::getCurrentHIPStream().stream();
-    char* d = static_cast<char*>(dev_.data_ptr());
+    char* d = static_cast<char*>(dvb.data_ptr());
     {
       py::gil_scoped_release nogil;
       using clk = std::chrono::steady_clock;
@@ -271,6 +287,14 @@ class SparseLRPlan {
                                    gkind_ ? gstep_.data_ptr() : nullptr, gkind_, st),
               "SparseLRPlan: step");
           hck(hipEventRecord(ev_[slot], st), "SparseLRPlan: event");
+          pending_[slot] = true;
+        } else if (feed_ == 3) {
+          hck(dtfk_slr_stage(hdev_[slot], d, total, side_), "SparseLRPlan: feed staging");
+          hck(hipEventRecord(evs_[slot], side_), "SparseLRPlan: event");
+          hck(hipStreamWaitEvent(st, evs_[slot], 0), "SparseLRPlan: wait staging");
+          launch(d + o_ids, i32, reinterpret_cast<const long long*>(d + o_off), reinterpret_cast<const float*>(d + o_val),
+                 reinterpret_cast<const float*>(d + o_lab), (int)B, (float)lr, st);
+          hck(hipEventRecord(ev_[slot], st), "SparseLRPlan: event");   // host + device slot free after the step
           pending_[slot] = true;
         } else {
           if (feed_ == 2) hck(hipMemcpyAsync(d, h, (size_t)total, hipMemcpyHostToDevice, st), "SparseLRPlan: feed copy");
@@ -325,7 +349,7 @@ class SparseLRPlan {
     dd["enqueue_us"] = t_[1] / k;
     dd["slot_wait_us"] = t_[2] / k;
     dd["runs"] = runs_;
-    dd["feed"] = feed_ == 2 ? "dma" : (feed_ == 1 ? "staging kernel" : "direct");
+    dd["feed"] = feed_ == 2 ? "dma" : (feed_ == 1 ? "staging kernel" : (feed_ == 3 ? "overlapped staging" : "direct"));
     return dd;
   }
   int64_t runs() const { return runs_; }
@@ -344,7 +368,10 @@ class SparseLRPlan {
   void* hbuf_[2] = {nullptr, nullptr};
   void* hdev_[2] = {nullptr, nullptr};
   int64_t hcap_[2] = {0, 0};
-  int feed_ = 0;   // 0 direct (the forward reads the pinned slot), 1 staging kernel, 2 SDMA copy
+  int feed_ = 0;   // 0 direct (the forward reads the pinned slot), 1 staging kernel, 2 SDMA copy, 3 staging on a side queue
+  hipStream_t side_ = nullptr;
+  hipEvent_t evs_[2] = {nullptr, nullptr};
+  at::Tensor dev2_[2];
   std::vector<int64_t> cnt_;
   hipEvent_t ev_[2] = {nullptr, nullptr};
   bool pending_[2] = {false, false};

@@ -21,15 +21,19 @@
 // sums over keys, i.e. over the accumulator's row index, so P^T feeds the
 // B operand straight from registers: the k-slot (g, j) of a 32-key block is
 // key 4g+j (j < 4) or 16+4g+(j-4) (j >= 4), and the A operand (V^T) is read
-// from an LDS image of V^T with the same key permutation (two 8-byte reads).
-// The backward products follow the same rule (dQ^T = K^T dS^T; dV = Pd^T dO,
-// dK = dS^T Q in the key-major kernel), using transposed LDS images of K, Q
-// and dO written once per workgroup.
+// from the row-major LDS image of V with the same key permutation by two
+// transposed LDS reads (ds_read_b64_tr_b16, ld_tr_pair).  The backward products
+// follow the same rule (dQ^T = K^T dS^T; dV = Pd^T dO, dK = dS^T Q in the
+// key-major kernel), reading the row images of K, Q and dO transposed -- no
+// second, transposed image is written.
 //
 // Dropout keep(i) = hash32(seed, i) >= p * 2^32 with i the element index of
 // the [B, NH, S, S] probability tensor -- the same convention as the unfused
 // softmax kernel (transformer.hip), so both paths drop the same elements.
 #include "common.h"
+
+#include <cstdlib>
+#include <string>
 
 namespace dtfk {
 namespace attn {
@@ -53,11 +57,24 @@ __device__ __forceinline__ uint4 ld16(const uint16_t* p) { return *reinterpret_c
 
 __device__ __forceinline__ bf16x8 as_frag(uint4 u) { return __builtin_bit_cast(bf16x8, u); }
 
-// two 4-element (8-byte) runs -> one 8-element fragment
-__device__ __forceinline__ bf16x8 ld_pair(const uint16_t* p0, const uint16_t* p1) {
-  const uint2 a = *reinterpret_cast<const uint2*>(p0);
-  const uint2 b = *reinterpret_cast<const uint2*>(p1);
-  return as_frag(uint4{a.x, a.y, b.x, b.y});
+// The permuted 32-key fragment of a TRANSPOSED operand straight from a
+// row-major [S][KP] image with the gfx950 transposed LDS read
+// (ds_read_b64_tr_b16: per 16-lane group, lane 4q+p addresses row q, columns
+// 4p..4p+3 of a 4 x 16 block; lane i receives column i): lane (g, c) gets
+// column col0 + c of rows row0 + 4g + 0..3 (elements 0..3) and row0 + 16 + 4g +
+// 0..3 (elements 4..7) -- the k-slot order of the score accumulators.  Replaces
+// a second, transposed LDS image written with 2-byte scatter stores.  EXEC must
+// be full (wave-uniform control flow only).
+typedef __attribute__((ext_vector_type(4))) short v4s_t;
+typedef __attribute__((address_space(3))) v4s_t lds_v4s_t;
+__device__ __forceinline__ bf16x8 ld_tr_pair(const uint16_t* img, int row0, int col0, int l) {
+  const int g = l >> 4, q = (l >> 2) & 3, p = l & 3;
+  const uint16_t* a = img + (row0 + 4 * g + q) * KP + col0 + 4 * p;
+  const v4s_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t*)(a));
+  const v4s_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t*)(a + 16 * KP));
+  typedef __attribute__((ext_vector_type(8))) short v8s_t;
+  const v8s_t v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
 }
 
 __device__ __forceinline__ bf16x8 pack8(const float* f) {
@@ -69,8 +86,8 @@ __device__ __forceinline__ float keepf(uint64_t seed, uint64_t i, uint32_t thres
 }
 
 // stage a [S][64] tile (rows of the packed projection, or of a [B,S,NH*64]
-// tensor) into a row image rows[S][KP] and, optionally, a transposed image
-// cols[64][S+8].  Two halves so a kernel issues every global load of all its
+// tensor) into a row image rows[S][KP] (the products that need it transposed
+// read it with ld_tr_pair).  Two halves so a kernel issues every global load of all its
 // stages (and its per-wave fragments) before the first LDS store: a
 // load -> store loop per stage costs one memory round trip per iteration.  With
 // 512 threads a thread's 16-byte column part (ch & 7) is the same in every
@@ -96,8 +113,7 @@ __device__ __forceinline__ void stage_load(const uint16_t* __restrict__ src, lon
   }
 }
 template <int S>
-__device__ __forceinline__ void stage_store(const StageRegs<S>& R, bool has_bias, uint16_t* rows, uint16_t* cols) {
-  constexpr int VT = S + 8;
+__device__ __forceinline__ void stage_store(const StageRegs<S>& R, bool has_bias, uint16_t* rows) {
   const int part = threadIdx.x & 7;
   const float bb[8] = {R.b0.x, R.b0.y, R.b0.z, R.b0.w, R.b1.x, R.b1.y, R.b1.z, R.b1.w};
 #pragma unroll
@@ -113,15 +129,7 @@ __device__ __forceinline__ void stage_store(const StageRegs<S>& R, bool has_bias
         w[j] = pack2bf(bf2f(w[j] & 0xffff) + bb[2 * j], bf2f(w[j] >> 16) + bb[2 * j + 1]);
       v = uint4{w[0], w[1], w[2], w[3]};
     }
-    if (rows) *reinterpret_cast<uint4*>(rows + r * KP + part * 8) = v;
-    if (cols) {
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        cols[(part * 8 + 2 * j) * VT + r] = (uint16_t)(w[j] & 0xffff);
-        cols[(part * 8 + 2 * j + 1) * VT + r] = (uint16_t)(w[j] >> 16);
-      }
-    }
+    *reinterpret_cast<uint4*>(rows + r * KP + part * 8) = v;
   }
 }
 
@@ -130,10 +138,10 @@ __global__ __launch_bounds__(512) void attn_fwd(const uint16_t* __restrict__ qkv
                                                 const float* __restrict__ mask, uint16_t* __restrict__ ctx,
                                                 float* __restrict__ lse, int NH, float scale, uint32_t thresh,
                                                 float inv_keep, uint64_t seed) {
-  constexpr int S = 32 * NKB, VT = S + 8;
+  constexpr int S = 32 * NKB;
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
   uint16_t* Ks = lds;                 // [S][KP]
-  uint16_t* Vt = lds + S * KP;        // [64][VT]
+  uint16_t* Vs = lds + S * KP;        // [S][KP] (read transposed: ld_tr_pair)
   const int b = blockIdx.z, h = blockIdx.y;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, g = l >> 4, c = l & 15;
   const long long RS = 3LL * NH * D;
@@ -149,8 +157,8 @@ __global__ __launch_bounds__(512) void attn_fwd(const uint16_t* __restrict__ qkv
   uint4 qraw[2];   // this wave's query fragments, in flight with the stages
 #pragma unroll
   for (int s = 0; s < 2; ++s) qraw[s] = ld16(base + (long long)min(q, S - 1) * RS + 32 * s + 8 * g);
-  stage_store<S>(rk, bk != nullptr, Ks, nullptr);
-  stage_store<S>(rv, bv != nullptr, nullptr, Vt);
+  stage_store<S>(rk, bk != nullptr, Ks);
+  stage_store<S>(rv, bv != nullptr, Vs);
   __syncthreads();
   if (!active) return;                                 // no barrier follows
 
@@ -208,9 +216,8 @@ __global__ __launch_bounds__(512) void attn_fwd(const uint16_t* __restrict__ qkv
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     f32x4 o = {0.f, 0.f, 0.f, 0.f};
-    const uint16_t* vr = Vt + (16 * u + c) * VT + 4 * g;
 #pragma unroll
-    for (int kb = 0; kb < NKB; ++kb) o = mfma16x16x32(ld_pair(vr + 32 * kb, vr + 32 * kb + 16), pb[kb], o);
+    for (int kb = 0; kb < NKB; ++kb) o = mfma16x16x32(ld_tr_pair(Vs, 32 * kb, 16 * u, l), pb[kb], o);
     *reinterpret_cast<uint2*>(out + 16 * u + 4 * g) = uint2{pack2bf(o[0], o[1]), pack2bf(o[2], o[3])};
   }
 }
@@ -222,11 +229,10 @@ __global__ __launch_bounds__(512) void attn_bwd_dq(const uint16_t* __restrict__ 
                                                    float* __restrict__ Dbuf, uint16_t* __restrict__ dqkv, int NH,
                                                    float scale, uint32_t thresh, float inv_keep, uint64_t seed,
                                                    float* __restrict__ bpart) {
-  constexpr int S = 32 * NKB, VT = S + 8;
+  constexpr int S = 32 * NKB;
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
-  uint16_t* Ks = lds;                    // [S][KP]
+  uint16_t* Ks = lds;                    // [S][KP] (also read transposed: ld_tr_pair)
   uint16_t* Vs = lds + S * KP;           // [S][KP]
-  uint16_t* Kt = lds + 2 * S * KP;       // [64][VT]
   const int b = blockIdx.z, h = blockIdx.y;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, g = l >> 4, c = l & 15;
   const long long RS = 3LL * NH * D, HS = (long long)NH * D;
@@ -246,8 +252,8 @@ __global__ __launch_bounds__(512) void attn_bwd_dq(const uint16_t* __restrict__ 
     qraw[s] = ld16(base + (long long)q * RS + 32 * s + 8 * g);
     doraw[s] = ld16(dor + 32 * s + 8 * g);
   }
-  stage_store<S>(rk, bkp != nullptr, Ks, Kt);
-  stage_store<S>(rv, bvp != nullptr, Vs, nullptr);
+  stage_store<S>(rk, bkp != nullptr, Ks);
+  stage_store<S>(rv, bvp != nullptr, Vs);
   __syncthreads();
   if (!active) return;
 
@@ -305,10 +311,7 @@ __global__ __launch_bounds__(512) void attn_bwd_dq(const uint16_t* __restrict__ 
     }
     const bf16x8 dsb = pack8(f);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const uint16_t* kr = Kt + (16 * u + c) * VT + 4 * g + 32 * kb;
-      acc[u] = mfma16x16x32(ld_pair(kr, kr + 16), dsb, acc[u]);
-    }
+    for (int u = 0; u < 4; ++u) acc[u] = mfma16x16x32(ld_tr_pair(Ks, 32 * kb, 16 * u, l), dsb, acc[u]);
   }
   uint16_t* dq = dqkv + ((long long)b * S + q) * RS + h * D;
 #pragma unroll
@@ -345,13 +348,11 @@ __global__ __launch_bounds__(512) void attn_bwd_dkv(const uint16_t* __restrict__
                                                     const float* __restrict__ lse, const float* __restrict__ Dbuf,
                                                     uint16_t* __restrict__ dqkv, int NH, float scale, uint32_t thresh,
                                                     float inv_keep, uint64_t seed, float* __restrict__ bpart) {
-  constexpr int S = 32 * NKB, VT = S + 8;
+  constexpr int S = 32 * NKB;
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
-  uint16_t* Qs = lds;                          // [S][KP]
-  uint16_t* dOs = lds + S * KP;                // [S][KP]
-  uint16_t* Qt = lds + 2 * S * KP;             // [64][VT]
-  uint16_t* dOt = lds + 2 * S * KP + D * VT;   // [64][VT]
-  float* Ls = reinterpret_cast<float*>(lds + 2 * S * KP + 2 * D * VT);   // [S] lse of every query row
+  uint16_t* Qs = lds;                          // [S][KP] (also read transposed: ld_tr_pair)
+  uint16_t* dOs = lds + S * KP;                // [S][KP] (likewise)
+  float* Ls = reinterpret_cast<float*>(lds + 2 * S * KP);   // [S] lse of every query row
   float* Dl = Ls + S;                                                     // [S] rowsum(dO * O)
   const int b = blockIdx.z, h = blockIdx.y;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, g = l >> 4, c = l & 15;
@@ -378,8 +379,8 @@ __global__ __launch_bounds__(512) void attn_bwd_dkv(const uint16_t* __restrict__
     lsv = lse[rbase + threadIdx.x];
     dlv = Dbuf[rbase + threadIdx.x];
   }
-  stage_store<S>(rq, bqp != nullptr, Qs, Qt);
-  stage_store<S>(rd, false, dOs, dOt);
+  stage_store<S>(rq, bqp != nullptr, Qs);
+  stage_store<S>(rd, false, dOs);
   if (threadIdx.x < S) {
     Ls[threadIdx.x] = lsv;
     Dl[threadIdx.x] = dlv;
@@ -428,10 +429,8 @@ __global__ __launch_bounds__(512) void attn_bwd_dkv(const uint16_t* __restrict__
     const bf16x8 ap = pack8(pd), as = pack8(ds);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const uint16_t* dr = dOt + (16 * u + c) * VT + 32 * qb + 4 * g;
-      const uint16_t* qr = Qt + (16 * u + c) * VT + 32 * qb + 4 * g;
-      dv[u] = mfma16x16x32(ap, ld_pair(dr, dr + 16), dv[u]);
-      dk[u] = mfma16x16x32(as, ld_pair(qr, qr + 16), dk[u]);
+      dv[u] = mfma16x16x32(ap, ld_tr_pair(dOs, 32 * qb, 16 * u, l), dv[u]);
+      dk[u] = mfma16x16x32(as, ld_tr_pair(Qs, 32 * qb, 16 * u, l), dk[u]);
     }
   }
   // lane holds dV/dK[key k0 + 4g + i][d 16u + c]
@@ -447,6 +446,209 @@ __global__ __launch_bounds__(512) void attn_bwd_dkv(const uint16_t* __restrict__
   if (bpart != nullptr) {
     // k / v-bias gradient partials: this wave's 16 keys (4 per lane x the 4 lane
     // groups g) summed per dimension d = 16u + c
+    float* pr = bpart + ((long long)b * (S / 16) + k0 / 16) * RS + h * D + c;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      float sk = (dk[u][0] + dk[u][1]) + (dk[u][2] + dk[u][3]);
+      float sv = (dv[u][0] + dv[u][1]) + (dv[u][2] + dv[u][3]);
+      sk += __shfl_xor(sk, 16, 64);
+      sk += __shfl_xor(sk, 32, 64);
+      sv += __shfl_xor(sv, 16, 64);
+      sv += __shfl_xor(sv, 32, 64);
+      if (g == 0) {
+        pr[NH * D + 16 * u] = sk * scale;
+        pr[2 * NH * D + 16 * u] = sv;
+      }
+    }
+  }
+}
+
+// S <= 128: the whole backward of one (batch, head) in ONE workgroup -- phase 1
+// is attn_bwd_dq's work (wave w: queries 16w..16w+15; D and lse of every query
+// go to LDS instead of a global round trip), phase 2 attn_bwd_dkv's (wave w:
+// keys 16w..16w+15) on the Q / dO / K / V images phase 1 already staged: one
+// staging pass and one launch instead of two of each.  Same MFMA order per
+// output as the two-kernel path.
+template <int NKB>
+__global__ __launch_bounds__(512) void attn_bwd_fused(const uint16_t* __restrict__ qkv, const float* __restrict__ bias,
+                                                      const float* __restrict__ mask, const uint16_t* __restrict__ ctx,
+                                                      const uint16_t* __restrict__ dctx, const float* __restrict__ lse,
+                                                      uint16_t* __restrict__ dqkv, int NH, float scale, uint32_t thresh,
+                                                      float inv_keep, uint64_t seed, float* __restrict__ bpart) {
+  constexpr int S = 32 * NKB;
+  static_assert(S <= 128, "one workgroup per (batch, head)");
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  uint16_t* Ks = lds;                    // [S][KP] each; all four also read transposed (ld_tr_pair)
+  uint16_t* Vs = lds + S * KP;
+  uint16_t* Qs = lds + 2 * S * KP;
+  uint16_t* dOs = lds + 3 * S * KP;
+  float* Ls = reinterpret_cast<float*>(lds + 4 * S * KP);   // [S] lse of every query row
+  float* Dl = Ls + S;                                        // [S] rowsum(dO * O)
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, g = l >> 4, c = l & 15;
+  const long long RS = 3LL * NH * D, HS = (long long)NH * D;
+  const uint16_t* base = qkv + (long long)b * S * RS + h * D;
+  const float* bq = bias ? bias + h * D : nullptr;
+  const float* bkp = bias ? bias + (NH + h) * D : nullptr;
+  const float* bvp = bias ? bias + (2 * NH + h) * D : nullptr;
+  StageRegs<S> rk, rv, rq, rd;
+  stage_load<S>(base + NH * D, RS, bkp, rk);
+  stage_load<S>(base + 2 * NH * D, RS, bvp, rv);
+  stage_load<S>(base, RS, bq, rq);
+  stage_load<S>(dctx + (long long)b * S * HS + h * D, HS, nullptr, rd);
+  const bool active = w * 16 < S;   // wave-uniform
+  const int q = min(w * 16 + c, S - 1);
+  const long long rbase = ((long long)b * NH + h) * S;
+  // O rows for D = rowsum(dO * O), lse: in flight with the stages
+  const uint16_t* orow = ctx + ((long long)b * S + q) * HS + h * D + 16 * g;
+  const uint4 ov0 = ld16(orow), ov1 = ld16(orow + 8);
+  const float L = lse[rbase + q];
+  stage_store<S>(rk, bkp != nullptr, Ks);
+  stage_store<S>(rv, bvp != nullptr, Vs);
+  stage_store<S>(rq, bq != nullptr, Qs);
+  stage_store<S>(rd, false, dOs);
+  __syncthreads();
+
+  // ---- phase 1: dQ of this wave's 16 queries, D and lse to LDS
+  if (active) {
+    bf16x8 bqf[2], bdo[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bqf[s] = ld_bf16x8(Qs + q * KP + 32 * s + 8 * g);
+      bdo[s] = ld_bf16x8(dOs + q * KP + 32 * s + 8 * g);
+    }
+    float dsum = 0.f;
+    {
+      const uint4 dv0 = *reinterpret_cast<const uint4*>(dOs + q * KP + 16 * g);
+      const uint4 dv1 = *reinterpret_cast<const uint4*>(dOs + q * KP + 16 * g + 8);
+      const uint32_t a[8] = {ov0.x, ov0.y, ov0.z, ov0.w, ov1.x, ov1.y, ov1.z, ov1.w};
+      const uint32_t d8[8] = {dv0.x, dv0.y, dv0.z, dv0.w, dv1.x, dv1.y, dv1.z, dv1.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        dsum += bf2f(a[j] & 0xffff) * bf2f(d8[j] & 0xffff) + bf2f(a[j] >> 16) * bf2f(d8[j] >> 16);
+    }
+    dsum += __shfl_xor(dsum, 16, 64);
+    dsum += __shfl_xor(dsum, 32, 64);
+    if (g == 0) {
+      Dl[q] = dsum;
+      Ls[q] = L;
+    }
+    const uint64_t ebase = (uint64_t)(rbase + q) * S;
+    f32x4 acc[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+    for (int kb = 0; kb < NKB; ++kb) {
+      float f[8];
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        const int t = 2 * kb + tt;
+        f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          sv = mfma16x16x32(ld_bf16x8(Ks + (16 * t + c) * KP + 32 * s + 8 * g), bqf[s], sv);
+          dp = mfma16x16x32(ld_bf16x8(Vs + (16 * t + c) * KP + 32 * s + 8 * g), bdo[s], dp);
+        }
+        float4 mk = mask ? *reinterpret_cast<const float4*>(mask + (long long)b * S + 16 * t + 4 * g)
+                         : float4{0.f, 0.f, 0.f, 0.f};
+        const float m4[4] = {mk.x, mk.y, mk.z, mk.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int key = 16 * t + 4 * g + i;
+          const float P = __expf(sv[i] * scale + m4[i] - L);
+          const float dpd = dp[i] * keepf(seed, ebase + key, thresh, inv_keep);
+          f[4 * tt + i] = P * (dpd - dsum);
+        }
+      }
+      const bf16x8 dsb = pack8(f);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] = mfma16x16x32(ld_tr_pair(Ks, 32 * kb, 16 * u, l), dsb, acc[u]);
+    }
+    uint16_t* dq = dqkv + ((long long)b * S + q) * RS + h * D;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      *reinterpret_cast<uint2*>(dq + 16 * u + 4 * g) =
+          uint2{pack2bf(acc[u][0] * scale, acc[u][1] * scale), pack2bf(acc[u][2] * scale, acc[u][3] * scale)};
+    if (bpart != nullptr) {
+      float cs[16];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float v = acc[u][j] * scale;
+          v += __shfl_xor(v, 1, 64);
+          v += __shfl_xor(v, 2, 64);
+          v += __shfl_xor(v, 4, 64);
+          v += __shfl_xor(v, 8, 64);
+          cs[4 * u + j] = v;
+        }
+      if (c == 0) {
+        float* pr = bpart + ((long long)b * (S / 16) + w) * RS + h * D;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          *reinterpret_cast<float4*>(pr + 16 * u + 4 * g) = float4{cs[4 * u], cs[4 * u + 1], cs[4 * u + 2], cs[4 * u + 3]};
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- phase 2: dK, dV of this wave's 16 keys over every query
+  if (!active) return;
+  const int k0 = w * 16;
+  const int key = k0 + c;
+  bf16x8 kf[2], vf[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    kf[s] = ld_bf16x8(Ks + key * KP + 32 * s + 8 * g);
+    vf[s] = ld_bf16x8(Vs + key * KP + 32 * s + 8 * g);
+  }
+  const float mk = mask ? mask[(long long)b * S + key] : 0.f;
+  f32x4 dv[4], dk[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    dv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    dk[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  for (int qb = 0; qb < NKB; ++qb) {
+    float pd[8], ds[8];
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      const int t = 2 * qb + tt;
+      f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        sv = mfma16x16x32(ld_bf16x8(Qs + (16 * t + c) * KP + 32 * s + 8 * g), kf[s], sv);
+        dp = mfma16x16x32(ld_bf16x8(dOs + (16 * t + c) * KP + 32 * s + 8 * g), vf[s], dp);
+      }
+      const float4 L4 = *reinterpret_cast<const float4*>(Ls + 16 * t + 4 * g);
+      const float4 D4 = *reinterpret_cast<const float4*>(Dl + 16 * t + 4 * g);
+      const float Lq[4] = {L4.x, L4.y, L4.z, L4.w}, Ds[4] = {D4.x, D4.y, D4.z, D4.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int qq = 16 * t + 4 * g + i;
+        const float P = __expf(sv[i] * scale + mk - Lq[i]);
+        const float kp = keepf(seed, (uint64_t)(rbase + qq) * S + key, thresh, inv_keep);
+        pd[4 * tt + i] = P * kp;
+        ds[4 * tt + i] = P * (dp[i] * kp - Ds[i]);
+      }
+    }
+    const bf16x8 ap = pack8(pd), as = pack8(ds);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      dv[u] = mfma16x16x32(ap, ld_tr_pair(dOs, 32 * qb, 16 * u, l), dv[u]);
+      dk[u] = mfma16x16x32(as, ld_tr_pair(Qs, 32 * qb, 16 * u, l), dk[u]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    uint16_t* rowp = dqkv + ((long long)b * S + k0 + 4 * g + i) * RS + h * D + c;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      rowp[NH * D + 16 * u] = f2bf(dk[u][i] * scale);
+      rowp[2 * NH * D + 16 * u] = f2bf(dv[u][i]);
+    }
+  }
+  if (bpart != nullptr) {
     float* pr = bpart + ((long long)b * (S / 16) + k0 / 16) * RS + h * D + c;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -504,7 +706,7 @@ hipError_t dtfk_attn_fwd(const void* qkv, const float* bias, const float* mask, 
   if (!dtfk_attn_supported(S, D)) return hipErrorInvalidValue;
   const dim3 grid((S + 127) / 128, NH, B);
   const float ik = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  const size_t lds = (size_t)(S * KP + D * (S + 8)) * 2;
+  const size_t lds = (size_t)(2 * S * KP) * 2;
 #define L_FWD(N)                                                                                                \
   {                                                                                                             \
     static hipError_t e = allow_lds(attn_fwd<N>, lds);                                                          \
@@ -527,8 +729,32 @@ hipError_t dtfk_attn_bwd(const void* qkv, const float* bias, const float* mask, 
   const dim3 grid((S + 127) / 128, NH, B);
   const float ik = p > 0.f ? 1.f / (1.f - p) : 1.f;
   const uint32_t th = attn_thresh(p);
-  const size_t lds_q = (size_t)(2 * S * KP + D * (S + 8)) * 2;
-  const size_t lds_kv = (size_t)(2 * S * KP + 2 * D * (S + 8)) * 2 + 2 * S * sizeof(float);
+  const size_t lds_q = (size_t)(2 * S * KP) * 2;
+  const size_t lds_kv = (size_t)(2 * S * KP) * 2 + 2 * S * sizeof(float);
+  static const bool fused_ok = [] {
+    const char* e = std::getenv("DTF_ATTN_BWD_FUSED");
+    return e == nullptr || std::string(e) != "0";
+  }();
+  if (fused_ok && S <= 128) {
+    const size_t lds_f = (size_t)(4 * S * KP) * 2 + 2 * S * sizeof(float);
+    const dim3 gridf(1, NH, B);
+#define L_BWDF(N)                                                                                                  \
+  {                                                                                                                \
+    static hipError_t e = allow_lds(attn_bwd_fused<N>, lds_f);                                                     \
+    if (e != hipSuccess) return e;                                                                                 \
+    hipLaunchKernelGGL(attn_bwd_fused<N>, gridf, dim3(512), lds_f, st, (const uint16_t*)qkv, bias, mask,           \
+                       (const uint16_t*)ctx, (const uint16_t*)dctx, lse, (uint16_t*)dqkv, NH, scale, th, ik,       \
+                       (uint64_t)seed, bpart);                                                                     \
+  }
+    switch (S / 32) {
+      case 1: L_BWDF(1); break;
+      case 2: L_BWDF(2); break;
+      case 4: L_BWDF(4); break;
+      default: return hipErrorInvalidValue;
+    }
+#undef L_BWDF
+    return hipGetLastError();
+  }
 #define L_BWD(N)                                                                                                   \
   {                                                                                                                \
     static hipError_t e1 = allow_lds(attn_bwd_dq<N>, lds_q);                                                       \

@@ -83,12 +83,12 @@ __global__ __launch_bounds__(THREADS) void slr_fwd(const float* __restrict__ W, 
 // table (64-bit key CAS, float add), then each occupied slot makes ONE global
 // atomic.  An entry that finds no slot within MAXP probes goes straight to
 // memory.  Workgroup 0 also sums dz and the row losses in a fixed order.
-constexpr int RPW = 32;              // batch rows per workgroup
-constexpr int HSLOTS = 4096;         // LDS table: 32 KB keys + 16 KB values
+// RPW batch rows per workgroup, an LDS table of HS slots (RPW 32: 4096 slots =
+// 32 KB keys + 16 KB values); dtfk_slr_set_rows_per_wg picks 8 / 16 / 32
 constexpr int MAXP = 16;
 constexpr unsigned long long EMPTY = ~0ull;
 
-template <typename ID>
+template <typename ID, int RPW = 32, int HSLOTS = 4096>
 __global__ __launch_bounds__(THREADS) void slr_apply(float* __restrict__ W, long long F, const ID* __restrict__ ids,
                                                      const long long* __restrict__ offsets,
                                                      const float* __restrict__ vals, const float* __restrict__ dz,
@@ -97,22 +97,49 @@ __global__ __launch_bounds__(THREADS) void slr_apply(float* __restrict__ W, long
                                                      float* __restrict__ loss_out, void* gvar, int gkind) {
   __shared__ unsigned long long hkey[HSLOTS];
   __shared__ float hval[HSLOTS];
+  __shared__ long long soff[RPW + 1];   // the workgroup's row offsets
+  __shared__ float sgr[RPW];            // -lr * dz of its rows
   const float lr = lr_ptr != nullptr ? *lr_ptr : lr_val;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int r0 = blockIdx.x * RPW;
+  const int nr = min(RPW, B - r0);
+  if ((int)threadIdx.x <= nr) soff[threadIdx.x] = offsets[r0 + threadIdx.x];
+  if ((int)threadIdx.x < nr) sgr[threadIdx.x] = -lr * dz[r0 + threadIdx.x];
   for (int i = threadIdx.x; i < HSLOTS; i += THREADS) {
     hkey[i] = EMPTY;
     hval[i] = 0.f;
   }
   __syncthreads();
-  const int r0 = blockIdx.x * RPW;
-  for (int b = r0 + wv; b < B && b < r0 + RPW; b += THREADS / 64) {
-    const float g = -lr * dz[b];
-    const long long s = offsets[b], e = offsets[b + 1];
-    for (long long j = s + lane; j < e; j += 64) {
-      const long long id = (long long)ids[j];
-      const float v = vals != nullptr ? vals[j] : 1.f;
-      if (id < 0 || id >= F || v == 0.f) continue;   // padding (val 0) touches nothing
-      const float u = g * v;
+  // The rows' entries are one contiguous CSR range: the threads stride it flat,
+  // U entries each with every id / value load in flight before the first use
+  // (a wave-per-row loop put ~3 dependent memory round trips per row in series:
+  // 15 us at B = 500 / 20 k ids), and find an entry's row by a binary search of
+  // the LDS offsets.
+  constexpr int U = 4;
+  const long long s0 = soff[0], e0 = soff[nr];
+  for (long long base = s0; base < e0; base += (long long)U * THREADS) {
+    long long idv[U];
+    float vv[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const long long j = base + threadIdx.x + (long long)k * THREADS;
+      const bool in = j < e0;
+      idv[k] = in ? (long long)ids[j] : -1;
+      vv[k] = in ? (vals != nullptr ? vals[j] : 1.f) : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const long long j = base + threadIdx.x + (long long)k * THREADS;
+      const long long id = idv[k];
+      const float v = vv[k];
+      if (j >= e0 || id < 0 || id >= F || v == 0.f) continue;   // padding (val 0) touches nothing
+      int lo = 0, hi = nr;   // the row: largest r with soff[r] <= j (soff[nr] > j)
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (soff[mid] <= j) lo = mid;
+        else hi = mid;
+      }
+      const float u = sgr[lo] * v;
       const unsigned long long key = (unsigned long long)id;
       unsigned h = (unsigned)(key * 0x9E3779B97F4A7C15ull >> 52) & (HSLOTS - 1);
       bool done = false;
@@ -174,7 +201,27 @@ __global__ __launch_bounds__(256) void slr_stage(const uint4* __restrict__ src, 
 }  // namespace slr
 }  // namespace dtfk
 
+static int g_rpw = 32;
+
+template <typename ID>
+static void launch_apply(int B, hipStream_t stream, float* W, long long F, const ID* ids, const long long* offsets,
+                         const float* vals, const float* dz, const float* lrow, const float* lr_ptr, float lr_val,
+                         float* bias, float* loss_out, void* gvar, int gkind) {
+  using namespace dtfk::slr;
+#define DTFK_AP(R, H)                                                                                             \
+  hipLaunchKernelGGL((slr_apply<ID, R, H>), dim3((B + R - 1) / R), dim3(THREADS), 0, stream, W, F, ids, offsets, \
+                     vals, dz, lrow, lr_ptr, lr_val, bias, B, loss_out, gvar, gkind)
+  if (g_rpw == 8) DTFK_AP(8, 1024);
+  else if (g_rpw == 16) DTFK_AP(16, 2048);
+  else DTFK_AP(32, 4096);
+#undef DTFK_AP
+}
+
 extern "C" {
+
+// batch rows per slr_apply workgroup (8, 16 or 32; else 32): more workgroups
+// vs more cross-workgroup atomics on hot ids
+void dtfk_slr_set_rows_per_wg(int rpw) { g_rpw = (rpw == 8 || rpw == 16) ? rpw : 32; }
 
 // The step with its feed read in place from mapped pinned host memory (hids,
 // hoffsets, hvals, hlabels: device views): slr_fwd<COPY> copies ids / offsets /
@@ -186,19 +233,17 @@ hipError_t dtfk_slr_step_direct(float* W, long long F, const void* hids, int ids
   using namespace dtfk::slr;
   if (B < 1 || gkind < 0 || gkind > 4 || (gkind != 0 && gvar == nullptr) || hvals == nullptr) return hipErrorInvalidValue;
   const int grid = (B + THREADS / 64 - 1) / (THREADS / 64);
-  const int agrid = (B + RPW - 1) / RPW;
   if (ids32) {
     hipLaunchKernelGGL((slr_fwd<int, true>), dim3(grid), dim3(THREADS), 0, stream, W, F, static_cast<const int*>(hids),
                        hoffsets, hvals, hlabels, bias, B, dz, lrow, bad, static_cast<int*>(ids_d), off_d, vals_d);
-    hipLaunchKernelGGL(slr_apply<int>, dim3(agrid), dim3(THREADS), 0, stream, W, F, static_cast<const int*>(ids_d),
-                       off_d, vals_d, dz, lrow, nullptr, lr_val, bias, B, loss_out, gvar, gkind);
+    launch_apply<int>(B, stream, W, F, static_cast<const int*>(ids_d), off_d, vals_d, dz, lrow, nullptr, lr_val, bias,
+                      loss_out, gvar, gkind);
   } else {
     hipLaunchKernelGGL((slr_fwd<long long, true>), dim3(grid), dim3(THREADS), 0, stream, W, F,
                        static_cast<const long long*>(hids), hoffsets, hvals, hlabels, bias, B, dz, lrow, bad,
                        static_cast<long long*>(ids_d), off_d, vals_d);
-    hipLaunchKernelGGL(slr_apply<long long>, dim3(agrid), dim3(THREADS), 0, stream, W, F,
-                       static_cast<const long long*>(ids_d), off_d, vals_d, dz, lrow, nullptr, lr_val, bias, B,
-                       loss_out, gvar, gkind);
+    launch_apply<long long>(B, stream, W, F, static_cast<const long long*>(ids_d), off_d, vals_d, dz, lrow, nullptr,
+                            lr_val, bias, loss_out, gvar, gkind);
   }
   return hipGetLastError();
 }
@@ -222,19 +267,16 @@ hipError_t dtfk_slr_step(float* W, long long F, const void* ids, int ids32, cons
   using namespace dtfk::slr;
   if (B < 1 || gkind < 0 || gkind > 4 || (gkind != 0 && gvar == nullptr)) return hipErrorInvalidValue;
   const int grid = (B + THREADS / 64 - 1) / (THREADS / 64);
-  const int agrid = (B + RPW - 1) / RPW;
   if (ids32) {
     auto id = static_cast<const int*>(ids);
     hipLaunchKernelGGL(slr_fwd<int>, dim3(grid), dim3(THREADS), 0, stream, W, F, id, offsets, vals, labels, bias, B,
                        dz, lrow, bad);
-    hipLaunchKernelGGL(slr_apply<int>, dim3(agrid), dim3(THREADS), 0, stream, W, F, id, offsets, vals, dz, lrow,
-                       lr_ptr, lr_val, bias, B, loss_out, gvar, gkind);
+    launch_apply<int>(B, stream, W, F, id, offsets, vals, dz, lrow, lr_ptr, lr_val, bias, loss_out, gvar, gkind);
   } else {
     auto id = static_cast<const long long*>(ids);
     hipLaunchKernelGGL(slr_fwd<long long>, dim3(grid), dim3(THREADS), 0, stream, W, F, id, offsets, vals, labels,
                        bias, B, dz, lrow, bad);
-    hipLaunchKernelGGL(slr_apply<long long>, dim3(agrid), dim3(THREADS), 0, stream, W, F, id, offsets, vals, dz, lrow,
-                       lr_ptr, lr_val, bias, B, loss_out, gvar, gkind);
+    launch_apply<long long>(B, stream, W, F, id, offsets, vals, dz, lrow, lr_ptr, lr_val, bias, loss_out, gvar, gkind);
   }
   return hipGetLastError();
 }

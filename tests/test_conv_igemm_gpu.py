@@ -160,7 +160,7 @@ def test_conv1x1_bn_statistics_handoff(monkeypatch):
         m = conv.ShadowConv2d(256, 128, 1, 1, 0, bias=False).cuda().to(memory_format=torch.channels_last)
         bn = FusedBatchNorm2d(128).cuda()
         conv.attach_shadows(m)
-        x = _cl(torch.randn(4, 256, 14, 14, device="cuda").bfloat16()).requires_grad_(True)
+        x = _cl(torch.randn(4, 256, 16, 16, device="cuda").bfloat16()).requires_grad_(True)
         key = ("fwd", tuple(x.shape), 128)
         conv._choice[key] = "gemm_big"
         y = m(x)

@@ -311,6 +311,12 @@ def _strided_ok(x, w16, stride, padding, dilation, groups) -> bool:
             and x.is_contiguous(memory_format=torch.channels_last) and x.shape[1] % 8 == 0)
 
 
+def _s2_ok(x, w16, stride, padding, dilation, groups) -> bool:
+    """A strided 1x1 conv (unpadded, ungrouped) whose forward / weight gradient
+    may run as GEMMs over the gathered strided pixels (DTF_CONV_GEMM=never: off)."""
+    return _POLICY != "never" and _strided_ok(x, w16, stride, padding, dilation, groups) and tuple(dilation) == (1, 1)
+
+
 class _ShadowConv(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, w16, stride, padding, dilation, groups, slot=None, share=None):
@@ -320,6 +326,23 @@ class _ShadowConv(torch.autograd.Function):
         ctx.slot = slot
         ctx.share = share
         ctx.gemm = _gemm_ok(x, w16, stride, padding, dilation, groups)
+        ctx.xs = None
+        if not ctx.gemm and _s2_ok(x, w16, stride, padding, dilation, groups):
+            # strided 1x1 (ResNet's downsampling projection): gather the strided
+            # pixels once; forward and weight gradient are then plain GEMMs over
+            # them (the input gradient keeps the strided-GEMM / MIOpen path)
+            xs = x[:, :, ::stride[0], ::stride[1]].contiguous(memory_format=torch.channels_last)
+            if _gemm_ok(xs, w16, (1, 1), (0, 0), dilation, groups):
+                ctx.xs = xs
+                eng = _fwd_engine(xs, w16)
+                if eng == "gemm_big" and _BN_STATS:
+                    r = _fwd_gemm_stats(xs, w16)
+                    if r is not None:
+                        _handoff[id(r[0])] = (r[1], r[2])
+                        return r[0]
+                if eng != "miopen":
+                    return _fwd_gemm(eng, xs, w16)
+                return F.conv2d(xs, w16)
         if ctx.gemm:
             eng = _fwd_engine(x, w16)
             if eng == "gemm_big" and _BN_STATS:
@@ -355,8 +378,11 @@ class _ShadowConv(torch.autograd.Function):
         first = share is not None and other is None
         strided = (share is not None and dy.is_contiguous(memory_format=torch.channels_last)
                    and _strided_ok(x, w16, stride, padding, dilation, groups))
+        xs = getattr(ctx, "xs", None)     # the strided 1x1's gathered pixels (its weight gradient is a GEMM over them)
+        xw = xs if xs is not None else x
+        gw = (ctx.gemm or xs is not None) and dy.is_contiguous(memory_format=torch.channels_last)
         dx_eng = _dx_engine(dy, x, w16) if gemm and need_x else "miopen"
-        dw_eng = _dw_engine(dy, x, w16) if gemm and need_w else "miopen"
+        dw_eng = _dw_engine(dy, xw, w16) if gw and need_w else "miopen"
         dx3 = (_dx3_engine(dy, x, w16) if need_x and getattr(ctx, "igemm", False) and tuple(stride) == (1, 1)
                and dy.is_contiguous(memory_format=torch.channels_last) else "miopen")
         dw3 = (_dw3_engine(dy, x, w16, int(stride[0])) if need_w and getattr(ctx, "igemm", False)
@@ -405,10 +431,10 @@ class _ShadowConv(torch.autograd.Function):
             from . import big_gemm
             if sink:
                 g = grad_sink.target(w)
-                big_gemm.linear_dw(_rows(dy), _rows(x), into=g.view(g.shape[0], g.shape[1]))
+                big_gemm.linear_dw(_rows(dy), _rows(xw), into=g.view(g.shape[0], g.shape[1]))
                 grad_sink.done(w)
                 return dx, None, None, None, None, None, None, None, None
-            return (dx, big_gemm.linear_dw(_rows(dy), _rows(x)).view(w.shape).to(w.dtype), None, None, None, None,
+            return (dx, big_gemm.linear_dw(_rows(dy), _rows(xw)).view(w.shape).to(w.dtype), None, None, None, None,
                     None, None, None)
         if sink:
             grad_sink.target(w).add_(dw)

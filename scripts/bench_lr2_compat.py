@@ -129,13 +129,20 @@ def main():
     host_split = {k: (round(v, 2) if isinstance(v, float) else v) for k, v in tr._plan.timing().items()}
     print(json.dumps({"metric": "lr2 compat Session.run vs native sparse-LR step (ms)", "features": F,
                       "batch": a.batch, "nnz_per_sample": a.nnz, "steps": a.steps,
-                      "session_run_ms": round(sess_ms, 4), "native_step_ms": round(nat_ms, 4),
-                      "ratio": round(sess_ms / nat_ms, 3), "native_host_fed_step_ms": round(host_ms, 4),
-                      "ratio_vs_host_fed": round(sess_ms / host_ms, 3), "native_host_fed_split_us": host_split,
+                      "session_run_ms": round(sess_ms, 4),
+                      # the Session's compat overhead: the native trainer fed the SAME host (numpy)
+                      # batches every step, as the Session is (lr2.py's feed_dict)
+                      "native_host_fed_step_ms": round(host_ms, 4),
+                      "ratio": round(sess_ms / host_ms, 3),
+                      "ratio_basis": "native SparseLRTrainer step on the same host numpy batches",
+                      # and against a native step whose batches already sit on the GPU (no host feed at all)
+                      "native_device_batches_step_ms": round(nat_ms, 4),
+                      "ratio_vs_device_resident_batches": round(sess_ms / nat_ms, 3),
+                      "native_host_fed_split_us": host_split,
                       "lowered_runs": lowered,
                       "session_samples_per_s": round(a.batch / sess_ms * 1e3, 1),
                       "session_native_call_split_us": native_split,
-                      "native_samples_per_s": round(a.batch / nat_ms * 1e3, 1),
+                      "native_host_fed_samples_per_s": round(a.batch / host_ms * 1e3, 1),
                       "loss_after_compat_run": round(loss_c, 5)}), flush=True)
 
 

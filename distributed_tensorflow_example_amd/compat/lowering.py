@@ -536,20 +536,21 @@ class MLPStepPlan(_PlanBase):
         self.resident_steps = getattr(self, "resident_steps", 0)
         shape = (B, 784)
 
+        prun, out, u8t, f32t, n = rp.plan.run_u8, rp.out, np.dtype(np.uint8), np.dtype(np.float32), B * C
+
         def fast(feed):
             fx, fy = feed.get(xph), feed.get(yph)
             u8 = getattr(fx, "u8", None)
             if (u8 is None or not isinstance(fx, nd) or fx.flags.writeable or fx.shape != shape
-                    or type(u8) is not nd or u8.dtype != np.uint8 or u8.shape != shape
-                    or type(fy) is not nd or fy.dtype != np.float32 or fy.size != B * C
-                    or not fy.flags.c_contiguous):
+                    or type(u8) is not nd or u8.dtype != u8t or u8.shape != shape
+                    or type(fy) is not nd or fy.dtype != f32t or fy.size != n or not fy.flags.c_contiguous):
                 return None
-            if not rp.run_u8(u8, fy.reshape(B, C), lr):
+            # (a run that registers the engine as live goes through the handle)
+            if not (prun(u8, fy, lr) if rp.live else rp.run_u8(u8, fy, lr)):
                 return None
             opt._steps += 1
             self.steps += 1
             self.resident_steps += 1
-            out = rp.out
             return [None if k < 0 else out[k] for k in kinds]
         return fast
 

@@ -74,6 +74,8 @@
 // publishes loss / accuracy / global_step and a done count to pinned memory.
 #include "common.h"
 
+#include <atomic>
+
 #include <cstdlib>
 #include <cstring>
 
@@ -216,6 +218,7 @@ struct Args {
   long long* host_done;     // pinned: runs completed
   long long* host_state;    // pinned: id of the launch that exited
   long long launch_id, run0, idle;
+  unsigned census_tag;      // per-launch placement-census tag from the host (no device load in front of the census)
   void* gvar;               // the graph's global_step variable (kind 0 none, 1 f32, 2 i64, 3 i32, 4 f64)
   int gvar_kind;
   unsigned* dctr;           // device: [0] records staged, [8] runs released, [16] stop, [32] steps done
@@ -718,22 +721,18 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
     else gvar0 = (double)gstep0;
   }
   const float lr = *a.lr;
-  float lrB = lr / (float)(B * (MULTI ? a.W : 1));   // RES: per run (the record's lr)
-  float lrX = lrB * (1.f / 255.f);
+  // the placement-census entry goes out before anything waits on a load: its
+  // tag is the host's per-launch tag, not the device sequence counter (whose
+  // load, with the lr / parameter waits ahead of the LDS stores, held every
+  // workgroup's entry back ~2 us per launch)
+  const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20) & 15u;
+  unsigned long long* hdr = reinterpret_cast<unsigned long long*>(a.xbuf + HDR_OFF);
+  const unsigned tag0 = a.census_tag;
+  if (tid == 0)
+    __hip_atomic_store(hdr + c, ((unsigned long long)tag0 << 32) | xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   for (int k = tid; k < 3 * 16 * LS; k += THREADS) a2T[k] = 0.f;   // a2T, dz2T, dz3T (batch pad stays 0)
   if constexpr (SPLIT)
     for (int k = tid; k < 3 * 16 * PS; k += THREADS) dzp[k] = (uint16_t)0;   // dz2 planes (batch pad 0)
-  if (tid < 256) {
-    w2s[tid] = pv;
-  } else if (tid < 272) {
-    b1s[tid - 256] = pv;
-  } else if (tid < 288) {
-    b2s[tid - 272] = pv;
-  } else if (tid == 288) {
-    *abort_flag = 0;
-  } else if (tid >= 296 && tid < 304) {
-    reinterpret_cast<int*>(smem + L_HFLAG)[tid - 296] = 0;
-  }
   const bool failed_in = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
 
   // x operands of the wave's feature tiles (registers, read from the LDS stage):
@@ -803,11 +802,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
   // ---- placement census: E1 group (the NQ slices of block j) and E2 group (the
   // NJ blocks of slice q) each on this workgroup's XCD -> that edge stays in one
   // L2 (plain stores).  Decided per launch from HW_REG_XCC_ID, never assumed.
-  const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20) & 15u;
-  unsigned long long* hdr = reinterpret_cast<unsigned long long*>(a.xbuf + HDR_OFF);
-  const unsigned tag0 = (unsigned)(seq0 + 1ull);
-  if (tid == 0)
-    __hip_atomic_store(hdr + c, ((unsigned long long)tag0 << 32) | xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // (this workgroup's entry was stored above, right after the loads were issued)
   if constexpr (!RES) stage_x(0, w, 8);   // the first step's stage: every wave a share (RES: per run)
   if (w == 0) {   // lane cc watches workgroup cc's entry: all 28 polls in flight at once
     const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
@@ -831,8 +826,23 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
     const bool e2 = !__any(off && lane % NQ == q);
     if (lane == 0) *census = bad ? -1 : ((e1 ? 1 : 0) | (e2 ? 2 : 0));
   }
+  // the small parameters' LDS stores wait for their loads: placed after the
+  // census entry and the stage DMA are out
+  if (tid < 256) {
+    w2s[tid] = pv;
+  } else if (tid < 272) {
+    b1s[tid - 256] = pv;
+  } else if (tid < 288) {
+    b2s[tid - 272] = pv;
+  } else if (tid == 288) {
+    *abort_flag = 0;
+  } else if (tid >= 296 && tid < 304) {
+    reinterpret_cast<int*>(smem + L_HFLAG)[tid - 296] = 0;
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // parameter loads + the first stage landed
   __syncthreads();
+  float lrB = lr / (float)(B * (MULTI ? a.W : 1));   // RES: per run (the record's lr)
+  float lrX = lrB * (1.f / 255.f);
   // an earlier launch failed (err set): nothing runs.  Checked only here, so the
   // wait for that load does not serialize the parameter loads behind it
   if (failed_in || *census < 0) return;
@@ -1560,6 +1570,14 @@ __global__ __launch_bounds__(THREADS, 1) void mlp_persist_f32(Args a) {
 static int g_fault_rank = -1;
 static long long g_fault_step = -1;
 
+// Placement-census tags: unique per launch within the process (the census
+// buffer lives in a runner's exchange buffer, zeroed once; tag 0 never matches)
+static unsigned next_census_tag() {
+  static std::atomic<unsigned> ctr{0};
+  unsigned t = ctr.fetch_add(1u, std::memory_order_relaxed) + 1u;
+  return t == 0u ? ctr.fetch_add(1u, std::memory_order_relaxed) + 1u : t;
+}
+
 extern "C" {
 
 void dtfk_mlpf_set_fault(int rank, long long step) {
@@ -1596,6 +1614,7 @@ hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int n
   a.host_done = nullptr;
   a.host_state = nullptr;
   a.launch_id = a.run0 = a.idle = 0;
+  a.census_tag = next_census_tag();
   a.gvar = nullptr;
   a.gvar_kind = 0;
   a.dctr = nullptr;
@@ -1710,6 +1729,7 @@ hipError_t dtfk_mlp_persist_f32_resident(void* stage, int B, float* W1, float* W
   a.host_done = host_done;
   a.host_state = host_state;
   a.launch_id = launch_id;
+  a.census_tag = next_census_tag();
   a.run0 = run0;
   a.idle = idle;
   a.gvar = gvar;

@@ -1,0 +1,6 @@
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -k 10 300 python scripts/prof_persist_f32.py fp32 > gpurun_out/r5r_phases.log 2>&1 || { tail -n 30 gpurun_out/r5r_phases.log; exit 1; }
+grep -A12 launch_stamps gpurun_out/r5r_phases.log | head -14
+grep -A4 '"launch_20"' gpurun_out/r5r_phases.log
+echo done

@@ -599,13 +599,30 @@ __device__ void copier_res(const Args& a, int cid, uint8_t* smem) {
     const int r0 = RR * cid;
     uint8_t* dst = const_cast<uint8_t*>(a.stage) + (long long)(st & 1) * REC;
     constexpr int C16 = DIN / 16;   // 49
-    // pinned rows -> LDS (rows >= B zero): one 16-B system-scope load per thread
-    for (int t = tid; t < RR * C16; t += THREADS) {
+    // pinned rows -> LDS (rows >= B zero): 16-B system-scope loads, a thread's
+    // NLD loads all issued before the first LDS store (one host-memory round
+    // trip, not NLD of them in series)
+    constexpr int NLD = (RR * C16 + THREADS - 1) / THREADS;
+    u32x4 hv[NLD];
+    uint32_t lv = 0;   // copier 0, threads < 32: a label dword or the run's lr
+    if (cid == 0 && tid < 32) {
+      if (4 * tid == RES_LR_BYTE)
+        lv = __float_as_uint(__hip_atomic_load(a.host_lr + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+      else
+        lv = __builtin_amdgcn_raw_buffer_load_b32(hrs, 4 * tid < B ? hbase + B * DIN + 4 * tid : OOB_OFF, 0, SYS);
+    }
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int t = tid + i * THREADS;
       const int rr = t / C16, cc = t % C16;
       const int row = r0 + rr;
-      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(hrs, row < B ? hbase + row * DIN + 16 * cc : OOB_OFF,
-                                                            0, SYS);
-      *reinterpret_cast<u32x4*>(smem + rr * CROW + 16 * cc) = v;
+      hv[i] = __builtin_amdgcn_raw_buffer_load_b128(hrs, (t < RR * C16 && row < B) ? hbase + row * DIN + 16 * cc : OOB_OFF,
+                                                    0, SYS);
+    }
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int t = tid + i * THREADS;
+      if (t < RR * C16) *reinterpret_cast<u32x4*>(smem + (t / C16) * CROW + 16 * (t % C16)) = hv[i];
     }
     __syncthreads();
     for (int t = tid; t < RR * C16; t += THREADS) {
@@ -632,12 +649,9 @@ __device__ void copier_res(const Args& a, int cid, uint8_t* smem) {
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_perm(u23, u01, 0x05040100u), rs, o + 2 * XTS, 0, 16);
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_perm(u23, u01, 0x07060302u), rs, o + 3 * XTS, 0, 16);
     }
-    if (cid == 0 && tid < 32) {   // labels (dwords 0..27) and the run's lr (byte RES_LR_BYTE)
-      uint32_t v;
-      if (4 * tid == RES_LR_BYTE) {
-        v = __float_as_uint(__hip_atomic_load(a.host_lr + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-      } else {
-        v = __builtin_amdgcn_raw_buffer_load_b32(hrs, 4 * tid < B ? hbase + B * DIN + 4 * tid : OOB_OFF, 0, SYS);
+    if (cid == 0 && tid < 32) {   // labels (dwords 0..27) and the run's lr (byte RES_LR_BYTE), loaded with the rows
+      uint32_t v = lv;
+      if (4 * tid != RES_LR_BYTE) {
         const int nv = B - 4 * tid;   // valid label bytes in this dword
         if (nv < 4) v = nv <= 0 ? 0u : (v & ((1u << (8 * nv)) - 1u));
       }

@@ -33,6 +33,14 @@ hipError_t dtfk_conv3x3_wflip(const void* w, void* wt, int K, int C, hipStream_t
 hipError_t dtfk_conv3x3_wgrad(const void* dy, const void* x, float* dw, float* ws, int N, int H, int W, int C, int K,
                               int stride, int kcrs, hipStream_t stream);
 long long dtfk_conv3x3_wgrad_plan(int N, int H, int W, int C, int K, int stride, int* splits_out, int* sps_out);
+int dtfk_conv_supported(int N, int H, int W, int C, int K, int stride, int ks);
+hipError_t dtfk_conv_fwd(const void* x, const void* w, void* y, float* part, int N, int H, int W, int C, int K,
+                         int stride, int bn, int ks, int accum, hipStream_t stream);
+long long dtfk_conv_tiles(int N, int H, int W, int stride, int ks);
+hipError_t dtfk_conv_wflip(const void* w, void* wt, int K, int C, int ks, hipStream_t stream);
+long long dtfk_conv_wgrad_plan(int N, int H, int W, int C, int K, int stride, int ks, int* splits_out, int* sps_out);
+hipError_t dtfk_conv_wgrad(const void* dy, const void* x, float* dw, float* ws, int N, int H, int W, int C, int K,
+                           int stride, int ks, int kcrs, hipStream_t stream);
 hipError_t dtfk_bn_stat_partials(const void* x, float* part, int M, int C, hipStream_t st);
 hipError_t dtfk_bn_fwd_parts(const void* x, const void* res, const float* gamma, const float* beta, void* y,
                              const float* part, int P, float* mean, float* invstd, float* scale, float* shift,
@@ -174,76 +182,87 @@ void strided_add(at::Tensor full, at::Tensor comp, int64_t s) {
      "strided_add");
 }
 
-// 3x3 / pad 1 / stride 1 or 2 convolution on channels_last bf16 tensors as an
-// in-tree implicit GEMM (csrc/kernels/conv_igemm.hip); `part` [2, P, K] fp32
-// receives the BatchNorm statistics partials of y (P = conv3x3_tiles).
+// 3x3 (pad 1) or 1x1 (pad 0), stride 1 or 2 convolution on channels_last bf16
+// tensors as an in-tree implicit GEMM (csrc/kernels/conv_igemm.hip; the filter
+// size comes from w); `part` [2, P, K] fp32 receives the BatchNorm statistics
+// partials of y (P = conv3x3_tiles).
 static void cl_bf16(const at::Tensor& t, const char* what) {
   if (!t.is_cuda() || t.scalar_type() != at::kBFloat16 || t.dim() != 4 || !t.is_contiguous(at::MemoryFormat::ChannelsLast))
     throw std::runtime_error(std::string(what) + ": channels_last bf16 4-D CUDA tensor expected");
 }
+static int ksize(const at::Tensor& w) {
+  if (w.dim() != 4 || w.size(2) != w.size(3) || (w.size(2) != 1 && w.size(2) != 3)) return 0;
+  return (int)w.size(2);
+}
 
 bool conv3x3_supported(at::Tensor x, at::Tensor w, int64_t stride) {
-  if (x.dim() != 4 || w.dim() != 4 || w.size(2) != 3 || w.size(3) != 3 || w.size(1) != x.size(1)) return false;
-  return dtfk_conv3x3_supported((int)x.size(0), (int)x.size(2), (int)x.size(3), (int)x.size(1), (int)w.size(0),
-                                (int)stride) != 0;
+  const int ks = ksize(w);
+  if (x.dim() != 4 || ks == 0 || w.size(1) != x.size(1)) return false;
+  return dtfk_conv_supported((int)x.size(0), (int)x.size(2), (int)x.size(3), (int)x.size(1), (int)w.size(0),
+                             (int)stride, ks) != 0;
 }
 
 int64_t conv3x3_tiles(int64_t N, int64_t H, int64_t W, int64_t stride) {
-  return dtfk_conv3x3_tiles((int)N, (int)H, (int)W, (int)stride);
+  return dtfk_conv_tiles((int)N, (int)H, (int)W, (int)stride, 3);   // same rows for 1x1 / pad 0
 }
 
 void conv3x3_fwd(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tensor> part, int64_t stride,
-                 int64_t bn) {
-  cl_bf16(x, "conv3x3_fwd x");
-  cl_bf16(w, "conv3x3_fwd w");
-  cl_bf16(y, "conv3x3_fwd y");
+                 int64_t bn, bool accumulate) {
+  cl_bf16(x, "conv_fwd x");
+  cl_bf16(w, "conv_fwd w");
+  cl_bf16(y, "conv_fwd y");
+  const int ks = ksize(w);
   const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3), K = (int)w.size(0);
   const int Ho = (H - 1) / (int)stride + 1, Wo = (W - 1) / (int)stride + 1;
-  if (w.size(1) != C || w.size(2) != 3 || w.size(3) != 3 || y.size(0) != N || y.size(1) != K || y.size(2) != Ho ||
-      y.size(3) != Wo)
-    throw std::runtime_error("conv3x3_fwd: shapes");
+  if (ks == 0 || w.size(1) != C || y.size(0) != N || y.size(1) != K || y.size(2) != Ho || y.size(3) != Wo)
+    throw std::runtime_error("conv_fwd: shapes");
   float* pp = nullptr;
   if (part.has_value()) {
-    const int64_t P = dtfk_conv3x3_tiles(N, H, W, (int)stride);
+    const int64_t P = dtfk_conv_tiles(N, H, W, (int)stride, ks);
     if (!part->is_cuda() || part->scalar_type() != at::kFloat || !part->is_contiguous() || part->numel() < 2 * P * K)
-      throw std::runtime_error("conv3x3_fwd: part must hold [2, P, K] fp32");
+      throw std::runtime_error("conv_fwd: part must hold [2, P, K] fp32");
     pp = part->data_ptr<float>();
   }
-  ck(dtfk_conv3x3_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), pp, N, H, W, C, K, (int)stride, (int)bn, cs()),
-     "conv3x3_fwd");
+  ck(dtfk_conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), pp, N, H, W, C, K, (int)stride, (int)bn, ks,
+                   accumulate ? 1 : 0, cs()),
+     "conv_fwd");
 }
 
-// wt [C, K, 3, 3] channels_last = the flipped, transposed filter of the stride-1 input gradient
+// wt [C, K, ks, ks] channels_last = the flipped, transposed filter of the stride-1 input gradient
 void conv3x3_wflip(at::Tensor w, at::Tensor wt) {
-  cl_bf16(w, "conv3x3_wflip w");
-  cl_bf16(wt, "conv3x3_wflip wt");
-  if (wt.size(0) != w.size(1) || wt.size(1) != w.size(0)) throw std::runtime_error("conv3x3_wflip: shapes");
-  ck(dtfk_conv3x3_wflip(w.data_ptr(), wt.data_ptr(), (int)w.size(0), (int)w.size(1), cs()), "conv3x3_wflip");
+  cl_bf16(w, "conv_wflip w");
+  cl_bf16(wt, "conv_wflip wt");
+  const int ks = ksize(w);
+  if (ks == 0 || wt.size(0) != w.size(1) || wt.size(1) != w.size(0) || wt.size(2) != ks || wt.size(3) != ks)
+    throw std::runtime_error("conv_wflip: shapes");
+  ck(dtfk_conv_wflip(w.data_ptr(), wt.data_ptr(), (int)w.size(0), (int)w.size(1), ks, cs()), "conv_wflip");
 }
 
-// dw (fp32 [K, C, 3, 3], channels_last or contiguous) += the weight gradient of
-// y = conv3x3(x, w, stride) for y's gradient dy
+// dw (fp32 [K, C, ks, ks], channels_last or contiguous) += the weight gradient of
+// y = conv(x, w, stride) for y's gradient dy
 void conv3x3_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t stride) {
-  cl_bf16(dy, "conv3x3_wgrad dy");
-  cl_bf16(x, "conv3x3_wgrad x");
-  if (!dw.is_cuda() || dw.scalar_type() != at::kFloat || dw.dim() != 4 || dw.size(2) != 3 || dw.size(3) != 3)
-    throw std::runtime_error("conv3x3_wgrad: dw must be an fp32 [K, C, 3, 3] CUDA tensor");
+  cl_bf16(dy, "conv_wgrad dy");
+  cl_bf16(x, "conv_wgrad x");
+  if (!dw.is_cuda() || dw.scalar_type() != at::kFloat || dw.dim() != 4 || dw.size(2) != dw.size(3) ||
+      (dw.size(2) != 3 && dw.size(2) != 1))
+    throw std::runtime_error("conv_wgrad: dw must be an fp32 [K, C, ks, ks] CUDA tensor, ks 1 or 3");
+  const int ks = (int)dw.size(2);
   int kcrs;
   if (dw.is_contiguous()) kcrs = 1;
   else if (dw.is_contiguous(at::MemoryFormat::ChannelsLast)) kcrs = 0;
-  else throw std::runtime_error("conv3x3_wgrad: dw must be contiguous or channels_last");
+  else throw std::runtime_error("conv_wgrad: dw must be contiguous or channels_last");
   const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3), K = (int)dy.size(1);
   const int Ho = (H - 1) / (int)stride + 1, Wo = (W - 1) / (int)stride + 1;
   if (dw.size(0) != K || dw.size(1) != C || dy.size(0) != N || dy.size(2) != Ho || dy.size(3) != Wo)
-    throw std::runtime_error("conv3x3_wgrad: shapes");
+    throw std::runtime_error("conv_wgrad: shapes");
   // split slabs from the caching allocator (freed back to it on return; the
   // stream-ordered reuse is safe)
-  const long long wsn = dtfk_conv3x3_wgrad_plan(N, H, W, C, K, (int)stride, nullptr, nullptr);
+  const long long wsn = dtfk_conv_wgrad_plan(N, H, W, C, K, (int)stride, ks, nullptr, nullptr);
   at::Tensor ws;
   if (wsn > 0) ws = at::empty({wsn}, dw.options());
-  ck(dtfk_conv3x3_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), wsn > 0 ? ws.data_ptr<float>() : nullptr, N,
-                        H, W, C, K, (int)stride, kcrs, cs()),
-     "conv3x3_wgrad");
+  ck(dtfk_conv_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), wsn > 0 ? ws.data_ptr<float>() : nullptr, N,
+                     H, W, C, K, (int)stride, ks, kcrs, cs()),
+     "conv_wgrad");
 }
 
 // BatchNorm statistics partials of x alone ([2, P, C], P = bn_partial_rows(M, C));
@@ -265,7 +284,7 @@ void init_bn(pybind11::module& m) {
   m.def("conv3x3_supported", &conv3x3_supported);
   m.def("conv3x3_tiles", &conv3x3_tiles);
   m.def("conv3x3_fwd", &conv3x3_fwd, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("part") = py::none(),
-        py::arg("stride") = 1, py::arg("bn") = 0);
+        py::arg("stride") = 1, py::arg("bn") = 0, py::arg("accumulate") = false);
   m.def("conv3x3_wflip", &conv3x3_wflip);
   m.def("strided_add", &strided_add);
   m.def("bn_partial_rows", &bn_partial_rows);

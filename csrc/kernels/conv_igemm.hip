@@ -1,6 +1,7 @@
-// 3x3 convolution (pad 1, stride 1 or 2) on NHWC bf16 activations as an
-// implicit GEMM on the gfx950 matrix cores, with an optional BatchNorm
-// statistics epilogue (ResNet-50, BASELINE.json configs[2]).
+// 3x3 (pad 1) and 1x1 (pad 0) convolutions, stride 1 or 2, on NHWC bf16
+// activations as implicit GEMMs on the gfx950 matrix cores, with an optional
+// BatchNorm statistics epilogue (ResNet-50, BASELINE.json configs[2]).  KS is
+// the filter size (template): 9 or 1 taps per 64-channel chunk.
 //
 //   y[p][k] = sum_{r,s,c} x[n, ho*st + r - 1, wo*st + s - 1, c] * w[k][r][s][c]
 //
@@ -42,11 +43,12 @@ constexpr int OOB = 0x7ffffff0;
 
 __device__ __forceinline__ int swz(int row, int ch) { return ch ^ ((row >> 1) & 7); }
 
-template <int BN, bool STATS>
-__global__ __launch_bounds__(NTHR, 2) void conv3x3_fwd(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
-                                                       uint16_t* __restrict__ y, float* __restrict__ part, int N,
-                                                       int H, int W, int C, int K, int Ho, int Wo, int stride,
-                                                       long long xbytes) {
+template <int KS, int BN, bool STATS>
+__global__ __launch_bounds__(NTHR, 2) void conv_fwd(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
+                                                    uint16_t* __restrict__ y, float* __restrict__ part, int N,
+                                                    int H, int W, int C, int K, int Ho, int Wo, int stride,
+                                                    long long xbytes, int accum) {
+  constexpr int PAD = KS / 2, TAPS = KS * KS;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, BUF = A_BYTES + B_BYTES;
   constexpr int WM = BM / 2, WN = BN / 2;          // per-wave output block
   constexpr int TM = WM / 16, TN = WN / 16;        // 16x16 tiles per wave
@@ -73,10 +75,10 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_fwd(const uint16_t* __restric
     an[i] = (int)(t / Ho);
   }
   const auto xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(x), 0, (int)(xbytes > 0x7ffffff0 ? 0x7ffffff0 : xbytes), 0x00020000);
-  const long long wbytes = (long long)K * 9 * C * 2;
+  const long long wbytes = (long long)K * TAPS * C * 2;
   const auto wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(w), 0, (int)wbytes, 0x00020000);
   const int ncc = C / BK;
-  const int nsteps = 9 * ncc;
+  const int nsteps = TAPS * ncc;
 
   // two register sets: a step's operands are loaded two steps ahead (issued
   // while the step before it is multiplied), so one HBM round trip hides
@@ -85,10 +87,10 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_fwd(const uint16_t* __restric
   auto load = [&](int step, auto pc) {
     constexpr int P = decltype(pc)::value;
     const int rs = step / ncc, c0 = (step % ncc) * BK;
-    const int r = rs / 3, s = rs % 3;
+    const int r = rs / KS, s = rs % KS;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int hi = aho[i] * stride + r - 1, wi = awo[i] * stride + s - 1;
+      const int hi = aho[i] * stride + r - PAD, wi = awo[i] * stride + s - PAD;
       const bool ok = arow[i] && hi >= 0 && hi < H && wi >= 0 && wi < W;
       const long long off = ((((long long)an[i] * H + hi) * W + wi) * C + c0 + 8 * ach) * 2;
       ra[P][i] = __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? (int)off : OOB, 0, 0);
@@ -96,7 +98,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_fwd(const uint16_t* __restric
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       const int row = (tid >> 3) + 32 * i;   // output channel within the tile
-      const long long off = (((long long)(k0 + row) * 9 + rs) * C + c0 + 8 * ach) * 2;
+      const long long off = (((long long)(k0 + row) * TAPS + rs) * C + c0 + 8 * ach) * 2;
       rb[P][i] = __builtin_amdgcn_raw_buffer_load_b128(wr, (int)off, 0, 0);
     }
   };
@@ -183,8 +185,16 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_fwd(const uint16_t* __restric
   for (int t = tid; t < BM * CPR; t += NTHR) {
     const int row = t / CPR, ch = t % CPR;
     const long long m = m0 + row;
-    if (m < M)
-      *reinterpret_cast<u32x4*>(y + m * K + k0 + 8 * ch) = *reinterpret_cast<const u32x4*>(E + row * PITCH + 16 * ch);
+    if (m < M) {
+      u32x4 v = *reinterpret_cast<const u32x4*>(E + row * PITCH + 16 * ch);
+      if (accum) {   // y += conv (an input gradient folded into an existing one)
+        const u32x4 o = *reinterpret_cast<const u32x4*>(y + m * K + k0 + 8 * ch);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          v[q] = pack2bf(bf2f(v[q] & 0xffff) + bf2f(o[q] & 0xffff), bf2f(v[q] >> 16) + bf2f(o[q] >> 16));
+      }
+      *reinterpret_cast<u32x4*>(y + m * K + k0 + 8 * ch) = v;
+    }
   }
   if constexpr (STATS) {
     // per-channel sum / sum of squares of the bf16 outputs over the valid rows
@@ -250,12 +260,13 @@ __device__ __forceinline__ bf16x8 frag_tr(const uint8_t* img, int rb, int s, int
   return __builtin_bit_cast(bf16x8, v);
 }
 
-template <int BMW, int BNW>
-__global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
+template <int KS, int BMW, int BNW>
+__global__ __launch_bounds__(NTHR, 2) void conv_wgrad(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
                                                          float* __restrict__ dw, int N, int H, int W, int C, int K,
                                                          int Ho, int Wo, int stride, long long xbytes,
                                                          int steps_per_split, int kcrs, float* __restrict__ ws,
                                                          long long slab) {
+  constexpr int PAD = KS / 2, TAPS = KS * KS;
   constexpr int PK = 64;                                        // pixels per step
   constexpr int A_BYTES = PK * BMW * 2, B_BYTES = PK * BNW * 2, BUF = A_BYTES + B_BYTES;
   constexpr int ACPR = BMW / 8, BCPR = BNW / 8;                 // 16-B chunks per image row
@@ -267,7 +278,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad(const uint16_t* __restr
   const long long P = (long long)N * Ho * Wo;
   const int m0 = blockIdx.x * BMW;            // output-channel tile
   const int n0 = blockIdx.y * BNW;            // filter-column tile over (r, s, c)
-  const int NC = 9 * C;
+  const int NC = TAPS * C;
   const long long pb = (long long)blockIdx.z * steps_per_split * PK;
   long long pe = pb + (long long)steps_per_split * PK;
   if (pe > P) pe = P;
@@ -294,8 +305,8 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad(const uint16_t* __restr
     bval[i] = col < NC;
     const int rs = bval[i] ? col / C : 0;
     bc[i] = bval[i] ? col % C : 0;
-    br[i] = rs / 3;
-    bs[i] = rs % 3;
+    br[i] = rs / KS;
+    bs[i] = rs % KS;
     const long long p = pb + row;
     const long long pp = p < P ? p : 0;
     bwo[i] = (int)(pp % Wo);
@@ -332,7 +343,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad(const uint16_t* __restr
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       const long long p = p0 + brow0 + BRS * i;
-      const int hi = bho[i] * stride + br[i] - 1, wi = bwo[i] * stride + bs[i] - 1;
+      const int hi = bho[i] * stride + br[i] - PAD, wi = bwo[i] * stride + bs[i] - PAD;
       const bool ok = bval[i] && p < pe && hi >= 0 && hi < H && wi >= 0 && wi < W;
       const long long off = ((((long long)bn_[i] * H + hi) * W + wi) * C + bc[i]) * 2;
       rb[Q][i] = __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? (int)off : OOB, 0, 0);
@@ -407,7 +418,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad(const uint16_t* __restr
       const int col = n0 + wn * WN + 16 * j + fr;
       if (col >= NC) continue;
       // KRSC (channels_last) or KCRS (contiguous) gradient layout
-      const int cidx = kcrs ? (col % C) * 9 + col / C : col;
+      const int cidx = kcrs ? (col % C) * TAPS + col / C : col;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int row = m0 + wm * WM + 16 * i + 4 * fk + e;
@@ -418,7 +429,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad(const uint16_t* __restr
 
 // dW += sum_z slab_z, in split order: one thread per f32x4 of the fragment-order
 // tiles (the wgrad epilogue's layout), mapped back to (output channel, filter column)
-template <int BMW, int BNW>
+template <int KS, int BMW, int BNW>
 __global__ __launch_bounds__(256) void wgrad_reduce(const float* __restrict__ ws, int S, long long slab,
                                                     float* __restrict__ dw, int C, int tiles_x, int kcrs) {
   constexpr int WM = BMW / 2, WN = BNW / 2, TM = WM / 16, TN = WN / 16;
@@ -429,28 +440,31 @@ __global__ __launch_bounds__(256) void wgrad_reduce(const float* __restrict__ ws
   const int lane = q & 63, f = q >> 6;                  // f = (wave * TM + i) * TN + j
   const int j = f % TN, i = (f / TN) % TM, wv = f / (TN * TM);
   const int wm = wv >> 1, wn = wv & 1;
-  const int NC = 9 * C;
+  const int NC = KS * KS * C;
   const int col = (tile / tiles_x) * BNW + wn * WN + 16 * j + (lane & 15);
   if (col >= NC) return;
   const int row0 = (tile % tiles_x) * BMW + wm * WM + 16 * i + 4 * (lane >> 4);
   const float* src = ws + e * 4;
   f32x4 z = *reinterpret_cast<const f32x4*>(src);
   for (int s = 1; s < S; ++s) z += *reinterpret_cast<const f32x4*>(src + s * slab);
-  const int cidx = kcrs ? (col % C) * 9 + col / C : col;
+  const int cidx = kcrs ? (col % C) * (KS * KS) + col / C : col;
 #pragma unroll
   for (int r = 0; r < 4; ++r) dw[(long long)(row0 + r) * NC + cidx] += z[r];
 }
 
-// w' [C][3][3][K] = w [K][2-r][2-s][C]: the filter of the stride-1 input gradient
+// w' [C][KS][KS][K] = w [K][KS-1-r][KS-1-s][C]: the filter of the stride-1
+// input gradient (KS = 1: the channel transpose)
+template <int KS>
 __global__ void wflip(const uint16_t* __restrict__ w, uint16_t* __restrict__ wt, int K, int C) {
-  const long long n = (long long)K * 9 * C;
+  constexpr int TAPS = KS * KS;
+  const long long n = (long long)K * TAPS * C;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
     // i indexes wt = [c][rs'][k]
     const int k = (int)(i % K);
     const long long t = i / K;
-    const int rs = (int)(t % 9), c = (int)(t / 9);
-    const int r = 2 - rs / 3, s = 2 - rs % 3;
-    wt[i] = w[((long long)k * 9 + r * 3 + s) * C + c];
+    const int rs = (int)(t % TAPS), c = (int)(t / TAPS);
+    const int r = KS - 1 - rs / KS, s = KS - 1 - rs % KS;
+    wt[i] = w[((long long)k * TAPS + r * KS + s) * C + c];
   }
 }
 
@@ -459,24 +473,31 @@ __global__ void wflip(const uint16_t* __restrict__ w, uint16_t* __restrict__ wt,
 
 extern "C" {
 
-// 0: ok; invalid shapes return hipErrorInvalidValue (the caller uses MIOpen)
-int dtfk_conv3x3_supported(int N, int H, int W, int C, int K, int stride) {
-  if (N < 1 || H < 1 || W < 1 || (stride != 1 && stride != 2)) return 0;
+// 0: ok; invalid shapes return hipErrorInvalidValue (the caller uses MIOpen).
+// ks: 3 (pad 1) or 1 (pad 0)
+int dtfk_conv_supported(int N, int H, int W, int C, int K, int stride, int ks) {
+  if (N < 1 || H < 1 || W < 1 || (stride != 1 && stride != 2) || (ks != 1 && ks != 3)) return 0;
   if (C % 64 != 0 || K % 64 != 0) return 0;
   const long long xbytes = (long long)N * H * W * C * 2;
-  if (xbytes >= 0x7ffffff0LL || (long long)K * 9 * C * 2 >= 0x7ffffff0LL) return 0;   // 32-bit buffer offsets
+  if (xbytes >= 0x7ffffff0LL || (long long)K * ks * ks * C * 2 >= 0x7ffffff0LL) return 0;   // 32-bit buffer offsets
   return 1;
 }
+int dtfk_conv3x3_supported(int N, int H, int W, int C, int K, int stride) {
+  return dtfk_conv_supported(N, H, W, C, K, stride, 3);
+}
 
-hipError_t dtfk_conv3x3_fwd(const void* x, const void* w, void* y, float* part, int N, int H, int W, int C, int K,
-                            int stride, int bn, hipStream_t stream) {
+static inline int conv_out(int H, int stride, int ks) { return (H + 2 * (ks / 2) - ks) / stride + 1; }
+
+// y = conv(x, w) (+ y when accum); part (optional): the output's BN statistics partials
+hipError_t dtfk_conv_fwd(const void* x, const void* w, void* y, float* part, int N, int H, int W, int C, int K,
+                         int stride, int bn, int ks, int accum, hipStream_t stream) {
   using namespace dtfk::cig;
-  if (!dtfk_conv3x3_supported(N, H, W, C, K, stride)) return hipErrorInvalidValue;
-  const int Ho = (H + 2 - 3) / stride + 1, Wo = (W + 2 - 3) / stride + 1;
+  if (!dtfk_conv_supported(N, H, W, C, K, stride, ks)) return hipErrorInvalidValue;
+  const int Ho = conv_out(H, stride, ks), Wo = conv_out(W, stride, ks);
   const long long M = (long long)N * Ho * Wo;
   if (bn != 64 && bn != 128) {
-    // 128-wide channel tiles unless that leaves fewer than two workgroups per CU
-    // (2 fit per CU) -- the late stages (7x7 / 14x14, 512 channels) have few pixels
+    // 128-wide channel tiles unless that leaves fewer than one workgroup per CU
+    // -- the late stages (7x7 / 14x14, 512 channels) have few pixels
     const long long t128 = (M + BM - 1) / BM * (K / 128);
     bn = (K % 128 == 0 && t128 >= 256) ? 128 : 64;
   }
@@ -486,39 +507,55 @@ hipError_t dtfk_conv3x3_fwd(const void* x, const void* w, void* y, float* part, 
   auto xs = static_cast<const uint16_t*>(x);
   auto ws = static_cast<const uint16_t*>(w);
   auto ys = static_cast<uint16_t*>(y);
-  if (bn == 128) {
-    if (part) hipLaunchKernelGGL((conv3x3_fwd<128, true>), grid, dim3(NTHR), 0, stream, xs, ws, ys, part, N, H, W, C, K, Ho, Wo, stride, xbytes);
-    else hipLaunchKernelGGL((conv3x3_fwd<128, false>), grid, dim3(NTHR), 0, stream, xs, ws, ys, part, N, H, W, C, K, Ho, Wo, stride, xbytes);
-  } else {
-    if (part) hipLaunchKernelGGL((conv3x3_fwd<64, true>), grid, dim3(NTHR), 0, stream, xs, ws, ys, part, N, H, W, C, K, Ho, Wo, stride, xbytes);
-    else hipLaunchKernelGGL((conv3x3_fwd<64, false>), grid, dim3(NTHR), 0, stream, xs, ws, ys, part, N, H, W, C, K, Ho, Wo, stride, xbytes);
+#define DTFK_CF(KSV, BNV, ST)                                                                                     \
+  hipLaunchKernelGGL((conv_fwd<KSV, BNV, ST>), grid, dim3(NTHR), 0, stream, xs, ws, ys, part, N, H, W, C, K, Ho, Wo, \
+                     stride, xbytes, accum)
+#define DTFK_CF_BN(KSV)                                                   \
+  if (bn == 128) {                                                        \
+    if (part) DTFK_CF(KSV, 128, true); else DTFK_CF(KSV, 128, false);     \
+  } else {                                                                \
+    if (part) DTFK_CF(KSV, 64, true); else DTFK_CF(KSV, 64, false);       \
   }
+  if (ks == 3) { DTFK_CF_BN(3) } else { DTFK_CF_BN(1) }
+#undef DTFK_CF_BN
+#undef DTFK_CF
   return hipGetLastError();
 }
-
-long long dtfk_conv3x3_tiles(int N, int H, int W, int stride) {
-  const int Ho = (H + 2 - 3) / stride + 1, Wo = (W + 2 - 3) / stride + 1;
-  return ((long long)N * Ho * Wo + dtfk::cig::BM - 1) / dtfk::cig::BM;
+hipError_t dtfk_conv3x3_fwd(const void* x, const void* w, void* y, float* part, int N, int H, int W, int C, int K,
+                            int stride, int bn, hipStream_t stream) {
+  return dtfk_conv_fwd(x, w, y, part, N, H, W, C, K, stride, bn, 3, 0, stream);
 }
 
-hipError_t dtfk_conv3x3_wflip(const void* w, void* wt, int K, int C, hipStream_t stream) {
-  const long long n = (long long)K * 9 * C;
+long long dtfk_conv_tiles(int N, int H, int W, int stride, int ks) {
+  return ((long long)N * conv_out(H, stride, ks) * conv_out(W, stride, ks) + dtfk::cig::BM - 1) / dtfk::cig::BM;
+}
+long long dtfk_conv3x3_tiles(int N, int H, int W, int stride) { return dtfk_conv_tiles(N, H, W, stride, 3); }
+
+hipError_t dtfk_conv_wflip(const void* w, void* wt, int K, int C, int ks, hipStream_t stream) {
+  const long long n = (long long)K * ks * ks * C;
   const unsigned blocks = (unsigned)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
-  hipLaunchKernelGGL(dtfk::cig::wflip, dim3(blocks), dim3(256), 0, stream, static_cast<const uint16_t*>(w),
-                     static_cast<uint16_t*>(wt), K, C);
+  if (ks == 3)
+    hipLaunchKernelGGL(dtfk::cig::wflip<3>, dim3(blocks), dim3(256), 0, stream, static_cast<const uint16_t*>(w),
+                       static_cast<uint16_t*>(wt), K, C);
+  else if (ks == 1)
+    hipLaunchKernelGGL(dtfk::cig::wflip<1>, dim3(blocks), dim3(256), 0, stream, static_cast<const uint16_t*>(w),
+                       static_cast<uint16_t*>(wt), K, C);
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }
-
+hipError_t dtfk_conv3x3_wflip(const void* w, void* wt, int K, int C, hipStream_t stream) {
+  return dtfk_conv_wflip(w, wt, K, C, 3, stream);
+}
 
 // Split plan of the weight gradient: the number of pixel splits (gridDim.z)
 // and the fp32 workspace (floats) its slabs need (0 with one split).  About two
 // workgroups per CU in total (both resident at once) and at least 8 steps of 64
 // pixels per split: each extra split costs a 64 KB slab write + read.
-long long dtfk_conv3x3_wgrad_plan(int N, int H, int W, int C, int K, int stride, int* splits_out, int* sps_out) {
+long long dtfk_conv_wgrad_plan(int N, int H, int W, int C, int K, int stride, int ks, int* splits_out, int* sps_out) {
   using namespace dtfk::cig;
-  const int Ho = (H + 2 - 3) / stride + 1, Wo = (W + 2 - 3) / stride + 1;
-  const long long P = (long long)N * Ho * Wo;
-  const int NC = 9 * C;
+  const long long P = (long long)N * conv_out(H, stride, ks) * conv_out(W, stride, ks);
+  const int NC = ks * ks * C;
   const int bm = K % 128 == 0 ? 128 : 64;
   const int bnw = NC % 128 == 0 ? 128 : 64;
   const long long tiles = (long long)(K / bm) * ((NC + bnw - 1) / bnw);
@@ -532,21 +569,25 @@ long long dtfk_conv3x3_wgrad_plan(int N, int H, int W, int C, int K, int stride,
   if (sps_out) *sps_out = sps;
   return splits > 1 ? splits * tiles * bm * bnw : 0;
 }
+long long dtfk_conv3x3_wgrad_plan(int N, int H, int W, int C, int K, int stride, int* splits_out, int* sps_out) {
+  return dtfk_conv_wgrad_plan(N, H, W, C, K, stride, 3, splits_out, sps_out);
+}
 
-// dW (fp32 [K][3][3][C], accumulated into) of y = conv3x3(x, w, stride); dy is
-// y's gradient; ws: dtfk_conv3x3_wgrad_plan's workspace (may be null when it is 0)
-hipError_t dtfk_conv3x3_wgrad(const void* dy, const void* x, float* dw, float* ws, int N, int H, int W, int C, int K,
-                              int stride, int kcrs, hipStream_t stream) {
+// dW (fp32 [K][ks][ks][C] channels_last or [K][C][ks][ks] with kcrs, accumulated
+// into) of y = conv(x, w, stride); dy is y's gradient; ws: dtfk_conv_wgrad_plan's
+// workspace (may be null when it is 0)
+hipError_t dtfk_conv_wgrad(const void* dy, const void* x, float* dw, float* ws, int N, int H, int W, int C, int K,
+                           int stride, int ks, int kcrs, hipStream_t stream) {
   using namespace dtfk::cig;
-  if (!dtfk_conv3x3_supported(N, H, W, C, K, stride)) return hipErrorInvalidValue;
-  const int Ho = (H + 2 - 3) / stride + 1, Wo = (W + 2 - 3) / stride + 1;
+  if (!dtfk_conv_supported(N, H, W, C, K, stride, ks)) return hipErrorInvalidValue;
+  const int Ho = conv_out(H, stride, ks), Wo = conv_out(W, stride, ks);
   const long long P = (long long)N * Ho * Wo;
   if (P * K * 2 >= 0x7ffffff0LL) return hipErrorInvalidValue;
-  const int NC = 9 * C;
+  const int NC = ks * ks * C;
   const int bm = K % 128 == 0 ? 128 : 64;
   const int bnw = NC % 128 == 0 ? 128 : 64;
   int splits = 1, sps = 1;
-  const long long wsn = dtfk_conv3x3_wgrad_plan(N, H, W, C, K, stride, &splits, &sps);
+  const long long wsn = dtfk_conv_wgrad_plan(N, H, W, C, K, stride, ks, &splits, &sps);
   if (wsn > 0 && ws == nullptr) return hipErrorInvalidValue;
   float* wsp = wsn > 0 ? ws : nullptr;
   const long long slab = wsn > 0 ? wsn / splits : 0;
@@ -554,20 +595,27 @@ hipError_t dtfk_conv3x3_wgrad(const void* dy, const void* x, float* dw, float* w
   const long long xbytes = (long long)N * H * W * C * 2;
   auto d = static_cast<const uint16_t*>(dy);
   auto xs = static_cast<const uint16_t*>(x);
-#define DTFK_WG(A, B)                                                                                              \
+#define DTFK_WG(KSV, A, B)                                                                                         \
   do {                                                                                                             \
-    hipLaunchKernelGGL((conv3x3_wgrad<A, B>), grid, dim3(NTHR), 0, stream, d, xs, dw, N, H, W, C, K, Ho, Wo, stride, \
-                       xbytes, sps, kcrs, wsp, slab);                                                              \
+    hipLaunchKernelGGL((conv_wgrad<KSV, A, B>), grid, dim3(NTHR), 0, stream, d, xs, dw, N, H, W, C, K, Ho, Wo,     \
+                       stride, xbytes, sps, kcrs, wsp, slab);                                                      \
     if (wsp)                                                                                                       \
-      hipLaunchKernelGGL((wgrad_reduce<A, B>), dim3((unsigned)((slab / 4 + 255) / 256)), dim3(256), 0, stream, wsp, \
-                         splits, slab, dw, C, (int)grid.x, kcrs);                                                  \
+      hipLaunchKernelGGL((wgrad_reduce<KSV, A, B>), dim3((unsigned)((slab / 4 + 255) / 256)), dim3(256), 0, stream, \
+                         wsp, splits, slab, dw, C, (int)grid.x, kcrs);                                             \
   } while (0)
-  if (bm == 128 && bnw == 128) DTFK_WG(128, 128);
-  else if (bm == 128) DTFK_WG(128, 64);
-  else if (bnw == 128) DTFK_WG(64, 128);
-  else DTFK_WG(64, 64);
+#define DTFK_WG_T(KSV)                                 \
+  if (bm == 128 && bnw == 128) DTFK_WG(KSV, 128, 128); \
+  else if (bm == 128) DTFK_WG(KSV, 128, 64);           \
+  else if (bnw == 128) DTFK_WG(KSV, 64, 128);          \
+  else DTFK_WG(KSV, 64, 64);
+  if (ks == 3) { DTFK_WG_T(3) } else { DTFK_WG_T(1) }
+#undef DTFK_WG_T
 #undef DTFK_WG
   return hipGetLastError();
+}
+hipError_t dtfk_conv3x3_wgrad(const void* dy, const void* x, float* dw, float* ws, int N, int H, int W, int C, int K,
+                              int stride, int kcrs, hipStream_t stream) {
+  return dtfk_conv_wgrad(dy, x, dw, ws, N, H, W, C, K, stride, 3, kcrs, stream);
 }
 
 }  // extern "C"

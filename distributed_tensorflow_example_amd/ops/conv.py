@@ -106,6 +106,9 @@ def _dx_gemm(engine, dy, w16, x_shape, into=None):
     """dx = dy W; with `into` (a channels_last bf16 gradient of x from another
     branch) accumulated in place: dx = into + dy W, one GEMM with beta = 1."""
     acc = into is not None and into.dtype == dy.dtype and into.is_contiguous(memory_format=torch.channels_last)
+    if engine == "igemm":     # the in-tree implicit GEMM (1x1: dy times the transposed filter), accumulating
+        return conv3x3_dx(dy, w16, x_shape, into=into if acc else None) if acc or into is None else \
+            conv3x3_dx(dy, w16, x_shape) + into
     dx = into if acc else _cl_empty(x_shape[0], x_shape[1], x_shape[2], x_shape[3], dy)
     dy2, w2, dx2 = _rows(dy), w16.view(w16.shape[0], w16.shape[1]), _rows(dx)
     if engine != "gemm_big" or not _C().gemm_big(dy2, False, w2, False, dx2, beta=1.0 if acc else 0.0):
@@ -133,16 +136,23 @@ def igemm_ok(x, w16, stride, padding, dilation, groups) -> bool:
             and bool(_C().conv3x3_supported(x, w16, int(stride[0]))))
 
 
-def conv3x3(x, w16, stride: int = 1, stats=None, out=None, bn: int = 0):
-    """y = conv2d(x, w16, stride, padding=1) on the in-tree implicit GEMM
-    (channels_last bf16).  `stats`: an fp32 [2, P, Cout] buffer (P =
-    `conv3x3_stat_rows`) that receives per-channel sums of y and y^2 per
-    128-row tile -- the partials csrc/kernels/bn.hip's finalize reduces.
-    `bn`: output-channel tile width (64 / 128; 0 = the kernel's choice)."""
+def igemm1_ok(x, w16) -> bool:
+    """A 1x1 / stride-1 conv (the GEMM path's shapes) the in-tree implicit GEMM takes."""
+    return (_IGEMM != "never" and w16.dim() == 4 and w16.shape[2] == 1 and w16.shape[3] == 1
+            and w16.is_contiguous(memory_format=torch.channels_last) and bool(_C().conv3x3_supported(x, w16, 1)))
+
+
+def conv3x3(x, w16, stride: int = 1, stats=None, out=None, bn: int = 0, accumulate: bool = False):
+    """y = conv2d(x, w16, stride, padding=k//2) on the in-tree implicit GEMM
+    (channels_last bf16; w16 3x3 or 1x1).  `stats`: an fp32 [2, P, Cout]
+    buffer (P = `conv3x3_stat_rows`) that receives per-channel sums of y and
+    y^2 per 128-row tile -- the partials csrc/kernels/bn.hip's finalize
+    reduces.  `bn`: output-channel tile width (64 / 128; 0 = the kernel's
+    choice).  `accumulate`: out += the convolution."""
     N, _, H, W = x.shape
     Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
     y = _cl_empty(N, w16.shape[0], Ho, Wo, x) if out is None else out
-    _C().conv3x3_fwd(x, w16, y, stats, stride, bn)
+    _C().conv3x3_fwd(x, w16, y, stats, stride, bn, accumulate)
     return y
 
 
@@ -150,22 +160,27 @@ def conv3x3_stat_rows(x, stride: int = 1) -> int:
     return int(_C().conv3x3_tiles(x.shape[0], x.shape[2], x.shape[3], stride))
 
 
-def conv3x3_dx(dy, w16, x_shape):
-    """Input gradient of a stride-1 3x3 conv: conv3x3 of dy with the flipped,
-    channel-transposed filter."""
-    wt = torch.empty((w16.shape[1], w16.shape[0], 3, 3), device=w16.device, dtype=w16.dtype,
+def conv3x3_dx(dy, w16, x_shape, into=None):
+    """Input gradient of a stride-1 3x3 (or 1x1) conv: the same convolution of
+    dy with the flipped, channel-transposed filter; `into` (a channels_last bf16
+    gradient of x from another branch) is accumulated in the epilogue."""
+    ks = w16.shape[2]
+    wt = torch.empty((w16.shape[1], w16.shape[0], ks, ks), device=w16.device, dtype=w16.dtype,
                      memory_format=torch.channels_last)
     _C().conv3x3_wflip(w16, wt)
+    if into is not None:
+        return conv3x3(dy, wt, 1, out=into, accumulate=True)
     dx = _cl_empty(x_shape[0], x_shape[1], x_shape[2], x_shape[3], dy)
     return conv3x3(dy, wt, 1, out=dx)
 
 
-def conv3x3_dw(dy, x, stride: int, into=None):
+def conv3x3_dw(dy, x, stride: int, into=None, ks=None):
     """fp32 weight gradient of y = conv3x3(x, w, stride) for y's gradient dy,
     accumulated into `into` (an fp32 [Cout, Cin, 3, 3] tensor, contiguous or
     channels_last) or into a fresh zeroed one."""
     if into is None:
-        into = torch.zeros((dy.shape[1], x.shape[1], 3, 3), device=dy.device, dtype=torch.float32)
+        ks = 3 if ks is None else ks
+        into = torch.zeros((dy.shape[1], x.shape[1], ks, ks), device=dy.device, dtype=torch.float32)
     _C().conv3x3_wgrad(dy, x, into, stride)
     return into
 
@@ -237,14 +252,20 @@ def _fwd_engine(x, w16) -> str:
     key = (tuple(x.shape), w16.shape[0])
     if ("fwd",) + key not in _choice:
         if _BN_STATS and _fwd_gemm_stats(x, w16) is not None:
-            # gemm_big hands its output's BatchNorm partials over; the others leave a statistics pass
+            # gemm_big / the implicit GEMM hand their output's BatchNorm partials over;
+            # the others leave a statistics pass
             cands = {"miopen": lambda: _stat_pass(F.conv2d(x, w16)),
                      "hipblaslt": lambda: _stat_pass(_fwd_gemm("hipblaslt", x, w16)),
                      "gemm_big": lambda: _fwd_gemm_stats(x, w16)}
+            if igemm1_ok(x, w16):
+                part = torch.empty((2, conv3x3_stat_rows(x, 1), w16.shape[0]), device=x.device, dtype=torch.float32)
+                cands["igemm"] = lambda: conv3x3(x, w16, 1, stats=part)
         else:
             cands = {"miopen": lambda: F.conv2d(x, w16),
                      "hipblaslt": lambda: _fwd_gemm("hipblaslt", x, w16),
                      "gemm_big": lambda: _fwd_gemm("gemm_big", x, w16)}
+            if igemm1_ok(x, w16):
+                cands["igemm"] = lambda: conv3x3(x, w16, 1)
         return _pick("fwd", key, cands)
     return _choice[("fwd",) + key]
 
@@ -258,6 +279,8 @@ def _dx_engine(dy, x, w16) -> str:
                      dy, x, w16, None, (1, 1), (0, 0), (1, 1), False, [0, 0], 1, [True, False, False]),
                  "hipblaslt": lambda: _dx_gemm("hipblaslt", dy, w16, x.shape),
                  "gemm_big": lambda: _dx_gemm("gemm_big", dy, w16, x.shape)}
+        if igemm1_ok(x, w16) and dy.is_contiguous(memory_format=torch.channels_last):
+            cands["igemm"] = lambda: _dx_gemm("igemm", dy, w16, x.shape)
         return _pick("dx", key, cands)
     return _choice[("dx",) + key]
 
@@ -277,7 +300,11 @@ def _dw_engine(dy, x, w16) -> str:
             dw = torch.ops.aten.convolution_backward(dy, x, w16, None, (1, 1), (0, 0), (1, 1), False, [0, 0], 1,
                                                      [False, True, False])[1]
             acc.add_(dw.view(acc.shape))
-        return _pick("dw", key, {"miopen": miopen, "gemm_big": lambda: big_gemm.linear_dw(dy2, x2, into=acc)})
+        cands = {"miopen": miopen, "gemm_big": lambda: big_gemm.linear_dw(dy2, x2, into=acc)}
+        if igemm1_ok(x, w16):
+            acc4 = acc.view(w16.shape[0], w16.shape[1], 1, 1)
+            cands["igemm"] = lambda: conv3x3_dw(dy, x, 1, into=acc4)
+        return _pick("dw", key, cands)
     return _choice[("dw",) + key]
 
 
@@ -317,6 +344,17 @@ def _s2_ok(x, w16, stride, padding, dilation, groups) -> bool:
     return _POLICY != "never" and _strided_ok(x, w16, stride, padding, dilation, groups) and tuple(dilation) == (1, 1)
 
 
+def _fwd_igemm1(x, w16):
+    """1x1 forward on the implicit GEMM, with the BatchNorm partials hand-off."""
+    if _BN_STATS:
+        P = conv3x3_stat_rows(x, 1)
+        part = torch.empty((2, P, w16.shape[0]), device=x.device, dtype=torch.float32)
+        y = conv3x3(x, w16, 1, stats=part)
+        _handoff[id(y)] = (part, P)
+        return y
+    return conv3x3(x, w16, 1)
+
+
 class _ShadowConv(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, w16, stride, padding, dilation, groups, slot=None, share=None):
@@ -335,6 +373,8 @@ class _ShadowConv(torch.autograd.Function):
             if _gemm_ok(xs, w16, (1, 1), (0, 0), dilation, groups):
                 ctx.xs = xs
                 eng = _fwd_engine(xs, w16)
+                if eng == "igemm":
+                    return _fwd_igemm1(xs, w16)
                 if eng == "gemm_big" and _BN_STATS:
                     r = _fwd_gemm_stats(xs, w16)
                     if r is not None:
@@ -345,6 +385,8 @@ class _ShadowConv(torch.autograd.Function):
                 return F.conv2d(xs, w16)
         if ctx.gemm:
             eng = _fwd_engine(x, w16)
+            if eng == "igemm":
+                return _fwd_igemm1(x, w16)
             if eng == "gemm_big" and _BN_STATS:
                 r = _fwd_gemm_stats(x, w16)
                 if r is not None:
@@ -427,6 +469,12 @@ class _ShadowConv(torch.autograd.Function):
                 grad_sink.done(w)
                 return dx, None, None, None, None, None, None, None, None
             return dx, conv3x3_dw(dy, x, int(stride[0])).to(w.dtype), None, None, None, None, None, None, None
+        if not mw and dw_eng == "igemm":     # the 1x1 implicit GEMM's weight gradient, straight into fp32
+            if sink:
+                conv3x3_dw(dy, xw, 1, into=grad_sink.target(w))
+                grad_sink.done(w)
+                return dx, None, None, None, None, None, None, None, None
+            return dx, conv3x3_dw(dy, xw, 1, ks=1).to(w.dtype), None, None, None, None, None, None, None
         if not mw:
             from . import big_gemm
             if sink:

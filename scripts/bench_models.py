@@ -248,6 +248,11 @@ def dense_bench(a, w):
                "n_gpus": w.world_size, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 3),
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
                "data": "synthetic", "config": cfg, "final_loss": float(loss)}
+        if a.model == "resnet50":
+            from distributed_tensorflow_example_amd.ops import conv as conv_ops
+            # which engine each conv product runs on (per-shape timing), with the timed ms
+            out["conv_engines"] = {f"{k[0]}:{'x'.join(map(str, k[1]))}->{k[2]}" + (f"/s{k[3]}" if len(k) > 3 else ""):
+                                   [e, t] for k, (e, t) in conv_ops.choices().items()}
         if a.model == "bert_base":
             out["tokens_per_s"] = round(v * a.seq, 1)
             from distributed_tensorflow_example_amd.ops import big_gemm

@@ -13,10 +13,11 @@ import sys
 
 GROUPS = [
     ("hipBLASLt", lambda k: k.startswith("Cijk_")),
-    ("MIOpen/CK conv", lambda k: k.startswith(("igemm_", "naive_conv", "MIOpen")) or "ck::" in k or k.startswith("_ZN2ck")
-     or "conv_fwd" in k or "conv_bwd" in k or "gridwise_convolution" in k),
+    ("MIOpen/CK conv", lambda k: "dtfk::" not in k and (
+        k.startswith(("igemm_", "naive_conv", "MIOpen")) or "ck::" in k or k.startswith("_ZN2ck")
+        or "conv_fwd" in k or "conv_bwd" in k or "gridwise_convolution" in k)),
     ("in-tree gemm_big", lambda k: "dtfk::gemm2::" in k),
-    ("in-tree conv3x3", lambda k: "dtfk::cig::" in k),
+    ("in-tree conv (implicit GEMM)", lambda k: "dtfk::cig::" in k),
     ("in-tree BN", lambda k: "dtfk::bn::" in k),
     ("other in-tree", lambda k: "dtfk::" in k),
     ("other (torch / MIOpen glue)", lambda k: True),

@@ -201,3 +201,62 @@ def test_strided_1x1_conv_gathered_gemms_match_conv2d(monkeypatch):
     _close(y, ref)
     _close(x.grad, xr.grad)
     _close(m.weight.grad, w.grad)
+
+
+@pytest.mark.parametrize("N,C,H,W,K", [(2, 64, 14, 14, 256), (3, 256, 9, 7, 64), (2, 128, 7, 7, 128)])
+def test_conv1x1_implicit_gemm_matches_fp32(N, C, H, W, K):
+    """The implicit-GEMM kernels with a 1x1 filter: forward (+ BN statistics),
+    input gradient accumulated into an existing gradient, weight gradient into
+    an fp32 buffer that already holds one -- against fp32 conv2d."""
+    from distributed_tensorflow_example_amd.ops import conv
+
+    g = torch.Generator(device="cuda").manual_seed(31 + C + K)
+    x = _cl(torch.randn(N, C, H, W, device="cuda", generator=g).bfloat16())
+    w = _cl((torch.randn(K, C, 1, 1, device="cuda", generator=g) * 0.05).bfloat16())
+    assert conv.igemm1_ok(x, w)
+    P = conv.conv3x3_stat_rows(x, 1)
+    part = torch.full((2, P, K), float("nan"), device="cuda")
+    y = conv.conv3x3(x, w, 1, stats=part)
+    ref = F.conv2d(x.float(), w.float())
+    _close(y, ref)
+    yf = y.float().permute(0, 2, 3, 1).reshape(-1, K)
+    torch.testing.assert_close(part[0].sum(0), yf.sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(part[1].sum(0), (yf * yf).sum(0), rtol=1e-4, atol=1e-2)
+    dy = _cl(torch.randn(N, K, H, W, device="cuda", generator=g).bfloat16())
+    prior = _cl(torch.randn(N, C, H, W, device="cuda", generator=g).bfloat16())
+    dx = conv.conv3x3_dx(dy, w, x.shape, into=prior.clone())
+    xr = x.float().requires_grad_(True)
+    wr = w.float().requires_grad_(True)
+    F.conv2d(xr, wr).backward(dy.float())
+    _close(dx, xr.grad + prior.float(), 2e-2)
+    into = torch.randn(K, C, 1, 1, device="cuda", generator=g)
+    base = into.clone()
+    conv.conv3x3_dw(dy, x, 1, into=into)
+    _close(into - base, wr.grad, 2e-3)
+
+
+def test_shadow_conv1x1_on_igemm_trains_like_miopen(monkeypatch):
+    """A 1x1 ShadowConv2d with every product forced onto the implicit GEMM
+    (forward with the BN hand-off, input gradient, weight gradient) matches the
+    MIOpen path of the same module."""
+    from distributed_tensorflow_example_amd.ops import conv
+
+    res = {}
+    for eng in ("igemm", "miopen"):
+        torch.manual_seed(2)
+        m = conv.ShadowConv2d(128, 256, 1, 1, 0, bias=False).cuda().to(memory_format=torch.channels_last)
+        conv.attach_shadows(m)
+        x = _cl(torch.randn(2, 128, 16, 16, device="cuda").bfloat16()).requires_grad_(True)
+        key = (tuple(x.shape), 256)
+        conv._choice.clear()
+        for role in ("fwd", "dx", "dw"):
+            conv._choice[(role,) + key] = eng
+        try:
+            y = m(x)
+            y.float().square().sum().backward()
+        finally:
+            conv._choice.clear()
+            conv._handoff.clear()
+        res[eng] = (y.float(), x.grad.float(), m.weight.grad.float())
+    for a, b in zip(res["igemm"], res["miopen"]):
+        _close(a, b, 2e-2)

@@ -35,7 +35,11 @@ hipError_t dtfk_conv3x3_wgrad(const void* dy, const void* x, float* dw, float* w
 long long dtfk_conv3x3_wgrad_plan(int N, int H, int W, int C, int K, int stride, int* splits_out, int* sps_out);
 int dtfk_conv_supported(int N, int H, int W, int C, int K, int stride, int ks);
 hipError_t dtfk_conv_fwd(const void* x, const void* w, void* y, float* part, int N, int H, int W, int C, int K,
-                         int stride, int bn, int ks, int accum, hipStream_t stream);
+                         int stride, int bn, int ks, int accum, const void* bnx, const float* bnst,
+                         const void* bnres, hipStream_t stream);
+hipError_t dtfk_bn_bwd_parts(const void* g, const void* x, const float* gamma, const float* mean, const float* invstd,
+                             const float* part, int P, float* coef, void* dx, float* dgamma, float* dbeta, int M, int C,
+                             int accum, hipStream_t st);
 long long dtfk_conv_tiles(int N, int H, int W, int stride, int ks);
 hipError_t dtfk_conv_wflip(const void* w, void* wt, int K, int C, int ks, hipStream_t stream);
 long long dtfk_conv_wgrad_plan(int N, int H, int W, int C, int K, int stride, int ks, int* splits_out, int* sps_out);
@@ -206,8 +210,15 @@ int64_t conv3x3_tiles(int64_t N, int64_t H, int64_t W, int64_t stride) {
   return dtfk_conv_tiles((int)N, (int)H, (int)W, (int)stride, 3);   // same rows for 1x1 / pad 0
 }
 
+// bn_x / bn_stats (EPI 2): y is the output gradient of a BatchNorm(+ReLU) whose
+// input was bn_x ([N, K, Ho, Wo]) with statistics bn_stats [4, K] -- y is stored as
+// the ReLU-masked g and part receives the BN backward's [2, P, K] partials.
+// bn_res (EPI 3, with accumulate): that BN also added a residual (mask from
+// bn_x * scale + shift + bn_res) and y already holds the residual branch's
+// gradient, so g is formed from y + the convolution.
 void conv3x3_fwd(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Tensor> part, int64_t stride,
-                 int64_t bn, bool accumulate) {
+                 int64_t bn, bool accumulate, c10::optional<at::Tensor> bn_x, c10::optional<at::Tensor> bn_stats,
+                 c10::optional<at::Tensor> bn_res) {
   cl_bf16(x, "conv_fwd x");
   cl_bf16(w, "conv_fwd w");
   cl_bf16(y, "conv_fwd y");
@@ -223,8 +234,26 @@ void conv3x3_fwd(at::Tensor x, at::Tensor w, at::Tensor y, c10::optional<at::Ten
       throw std::runtime_error("conv_fwd: part must hold [2, P, K] fp32");
     pp = part->data_ptr<float>();
   }
+  const void* bx = nullptr;
+  const void* br = nullptr;
+  const float* bst = nullptr;
+  if (bn_x.has_value()) {
+    cl_bf16(*bn_x, "conv_fwd bn_x");
+    if (!bn_stats.has_value() || pp == nullptr || accumulate != bn_res.has_value() || bn_x->sizes() != y.sizes())
+      throw std::runtime_error("conv_fwd: bn_x needs bn_stats, part, y's shape, and accumulate iff bn_res");
+    f32(*bn_stats, 4LL * K, "bn_stats");
+    bx = bn_x->data_ptr();
+    bst = bn_stats->data_ptr<float>();
+    if (bn_res.has_value()) {
+      cl_bf16(*bn_res, "conv_fwd bn_res");
+      if (bn_res->sizes() != y.sizes()) throw std::runtime_error("conv_fwd: bn_res must have y's shape");
+      br = bn_res->data_ptr();
+    }
+  } else if (bn_res.has_value()) {
+    throw std::runtime_error("conv_fwd: bn_res needs bn_x");
+  }
   ck(dtfk_conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), pp, N, H, W, C, K, (int)stride, (int)bn, ks,
-                   accumulate ? 1 : 0, cs()),
+                   accumulate ? 1 : 0, bx, bst, br, cs()),
      "conv_fwd");
 }
 
@@ -265,6 +294,23 @@ void conv3x3_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t stride) {
      "conv_wgrad");
 }
 
+// BatchNorm backward when its output gradient arrived already ReLU-masked as g
+// together with the [2, P, C] partials (sum g, sum g x_hat) -- written by the
+// producing convolution's epilogue (conv3x3_fwd bn_x): finalize + apply only.
+void bn_bwd_parts(at::Tensor g, at::Tensor x, at::Tensor gamma, at::Tensor stats, at::Tensor part, int64_t P,
+                  at::Tensor coef, at::Tensor dx, at::Tensor dgamma, at::Tensor dbeta, bool accum) {
+  const int64_t C = gamma.numel();
+  const int64_t M = rows_of(x, C);
+  if (rows_of(g, C) != M || rows_of(dx, C) != M) throw std::runtime_error("bn_bwd_parts: shapes");
+  f32(stats, 4 * C, "stats"); f32(coef, 3 * C, "coef"); f32(dgamma, C, "dgamma"); f32(dbeta, C, "dbeta");
+  f32(part, 2 * P * C, "part");
+  const float* s = stats.data_ptr<float>();
+  ck(dtfk_bn_bwd_parts(g.data_ptr(), x.data_ptr(), gamma.data_ptr<float>(), s, s + C, part.data_ptr<float>(), (int)P,
+                       coef.data_ptr<float>(), dx.data_ptr(), dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
+                       (int)M, (int)C, accum ? 1 : 0, cs()),
+     "bn_bwd_parts");
+}
+
 // BatchNorm statistics partials of x alone ([2, P, C], P = bn_partial_rows(M, C));
 // returns P.  The convolution engine choice prices a conv without a statistics
 // epilogue with this pass (ops/conv.py).
@@ -279,12 +325,14 @@ int64_t bn_stat_partials(at::Tensor x, at::Tensor part) {
 
 void init_bn(pybind11::module& m) {
   m.def("bn_stat_partials", &bn_stat_partials);
+  m.def("bn_bwd_parts", &bn_bwd_parts);
   m.def("conv3x3_wgrad", &conv3x3_wgrad);
   m.def("bn_fwd_parts", &bn_fwd_parts);
   m.def("conv3x3_supported", &conv3x3_supported);
   m.def("conv3x3_tiles", &conv3x3_tiles);
   m.def("conv3x3_fwd", &conv3x3_fwd, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("part") = py::none(),
-        py::arg("stride") = 1, py::arg("bn") = 0, py::arg("accumulate") = false);
+        py::arg("stride") = 1, py::arg("bn") = 0, py::arg("accumulate") = false, py::arg("bn_x") = py::none(),
+        py::arg("bn_stats") = py::none(), py::arg("bn_res") = py::none());
   m.def("conv3x3_wflip", &conv3x3_wflip);
   m.def("strided_add", &strided_add);
   m.def("bn_partial_rows", &bn_partial_rows);

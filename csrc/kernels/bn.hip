@@ -417,6 +417,20 @@ hipError_t dtfk_bn_apply(const void* x, const void* res, const float* scale, con
   return hipGetLastError();
 }
 
+// backward with the partials (sum g, sum g x_hat) [2, P, C] and the ReLU-masked
+// output gradient g supplied by its producer (conv_igemm.hip conv_fwd EPI 2):
+// finalize + apply, no partials pass over dy / x
+hipError_t dtfk_bn_bwd_parts(const void* g, const void* x, const float* gamma, const float* mean, const float* invstd,
+                             const float* part, int P, float* coef, void* dx, float* dgamma, float* dbeta, int M, int C,
+                             int accum, hipStream_t st) {
+  if (C % 8 || P < 1) return hipErrorInvalidValue;
+  launch_bwd_finalize(part, P, M, C, gamma, mean, invstd, dgamma, dbeta, coef, accum, st);
+  const long long n8 = (long long)M * C / 8;
+  hipLaunchKernelGGL((bn_bwd_apply<false, false>), dim3(ew_grid(n8)), dim3(256), 0, st, (const uint16_t*)g,
+                     (const uint16_t*)x, nullptr, nullptr, nullptr, coef, (uint16_t*)dx, nullptr, n8, C);
+  return hipGetLastError();
+}
+
 // backward.  coef: [3, C] scratch; part: [2 * P, C]
 // write_g (residual + ReLU only): the partials pass stores g into dres and the
 // apply pass reads (g, x) instead of (dy, x, res).

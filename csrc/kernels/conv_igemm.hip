@@ -43,11 +43,23 @@ constexpr int OOB = 0x7ffffff0;
 
 __device__ __forceinline__ int swz(int row, int ch) { return ch ^ ((row >> 1) & 7); }
 
-template <int KS, int BN, bool STATS>
+// EPI: 0 plain, 1 BN statistics of y (forward), 2 BN backward of the BatchNorm
+// whose OUTPUT gradient y is (an input gradient feeding BN(+ReLU)'s backward):
+// y is stored as g = y * relu'(bn(bnx)) and part receives the per-channel sums
+// of g and g * x_hat (bnst = [mean, invstd, scale, shift] of that BN) -- the
+// partials pass of csrc/kernels/bn.hip bn_bwd, done in this epilogue.
+// EPI 3: the same for a BatchNorm + residual add + ReLU (mask from
+// bnx * scale + shift + bnres), with accum: the output gradient is the
+// convolution plus the residual branch's gradient already in y (the fold of
+// ops/conv.py), so g is formed from the complete gradient.
+template <int KS, int BN, int EPI>
 __global__ __launch_bounds__(NTHR, 2) void conv_fwd(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
                                                     uint16_t* __restrict__ y, float* __restrict__ part, int N,
                                                     int H, int W, int C, int K, int Ho, int Wo, int stride,
-                                                    long long xbytes, int accum) {
+                                                    long long xbytes, int accum, const uint16_t* __restrict__ bnx,
+                                                    const float* __restrict__ bnst,
+                                                    const uint16_t* __restrict__ bnres) {
+  constexpr bool STATS = EPI == 1, BNB = EPI >= 2, BNR = EPI == 3;
   constexpr int PAD = KS / 2, TAPS = KS * KS;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, BUF = A_BYTES + B_BYTES;
   constexpr int WM = BM / 2, WN = BN / 2;          // per-wave output block
@@ -124,10 +136,42 @@ __global__ __launch_bounds__(NTHR, 2) void conv_fwd(const uint16_t* __restrict__
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // epilogue operands read from HBM (BNB: the BN input x; accum: the gradient
+  // added onto) are loaded at the start of the last K step, so their latency
+  // hides behind its MFMAs instead of stalling the store loop
+  constexpr int CPR = BN / 8;                 // 16-B chunks per output row
+  constexpr int EIT = BM * CPR / NTHR;        // store-loop iterations per thread
+  static_assert(NTHR % CPR == 0, "a thread's chunk column is fixed over the store loop");
+  // EPI 3 on 64-wide tiles also prefetches the folded gradient and the residual
+  // (on 128-wide tiles those registers would spill: loaded in the store loop)
+  constexpr bool PRE3 = BNR && BN == 64;
+  u32x4 pre[EIT], pre_y[PRE3 ? EIT : 1], pre_r[PRE3 ? EIT : 1];
+  auto prefetch = [&]() {
+    if (!(BNB || accum)) return;
+    const uint16_t* src = BNB ? bnx : y;
+#pragma unroll
+    for (int it = 0; it < EIT; ++it) {
+      const int t = tid + it * NTHR;
+      const long long m = m0 + t / CPR;
+      if (m < M) {
+        const long long e = m * K + k0 + 8 * (t % CPR);
+        pre[it] = *reinterpret_cast<const u32x4*>(src + e);
+        if constexpr (PRE3) {
+          pre_y[it] = *reinterpret_cast<const u32x4*>(y + e);
+          pre_r[it] = *reinterpret_cast<const u32x4*>(bnres + e);
+        }
+      }
+    }
+  };
+  // with one or two K steps (a 1x1 over 64 / 128 channels: the epilogue's HBM
+  // traffic dominates) the epilogue loads go out with the operands' first loads
+  const bool early = nsteps <= 2;
+
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
   load(0, I0{});
   if (nsteps > 1) load(1, I1{});
+  if (early) prefetch();
   store(I0{});
   __syncthreads();
   const int fr = lane & 15, fk = lane >> 4;   // fragment row / k-chunk of this lane
@@ -139,6 +183,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv_fwd(const uint16_t* __restrict__
     using Q = std::integral_constant<int, P ^ 1>;
     if (step + 1 < nsteps) store(Q{});
     if (step + 2 < nsteps) load(step + 2, pc);
+    if (step + 1 == nsteps && !early) prefetch();
     const uint8_t* A = smem + P * BUF;
     const uint8_t* Bs = A + A_BYTES;
 #pragma unroll
@@ -180,20 +225,81 @@ __global__ __launch_bounds__(NTHR, 2) void conv_fwd(const uint16_t* __restrict__
         const int col = wn * WN + 16 * j + fr;
         *reinterpret_cast<uint16_t*>(E + row * PITCH + 2 * col) = f2bf(acc[i][j][e]);
       }
+  float bmu[8], bis[8], bsc[8], bsh[8];      // BNB: the BN's statistics for this thread's 8 channels
+  if constexpr (BNB) {
+    const int c8 = k0 + 8 * (tid % CPR);
+#pragma unroll
+    for (int q = 0; q < 8; q += 4) {
+      *reinterpret_cast<f32x4*>(bmu + q) = *reinterpret_cast<const f32x4*>(bnst + c8 + q);
+      *reinterpret_cast<f32x4*>(bis + q) = *reinterpret_cast<const f32x4*>(bnst + K + c8 + q);
+      *reinterpret_cast<f32x4*>(bsc + q) = *reinterpret_cast<const f32x4*>(bnst + 2 * K + c8 + q);
+      *reinterpret_cast<f32x4*>(bsh + q) = *reinterpret_cast<const f32x4*>(bnst + 3 * K + c8 + q);
+    }
+  }
   __syncthreads();
-  constexpr int CPR = BN / 8;   // 16-B chunks per output row
-  for (int t = tid; t < BM * CPR; t += NTHR) {
+  float sg[8], sgx[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) sg[q] = sgx[q] = 0.f;
+#pragma unroll
+  for (int it = 0; it < EIT; ++it) {
+    const int t = tid + it * NTHR;
     const int row = t / CPR, ch = t % CPR;
     const long long m = m0 + row;
     if (m < M) {
       u32x4 v = *reinterpret_cast<const u32x4*>(E + row * PITCH + 16 * ch);
-      if (accum) {   // y += conv (an input gradient folded into an existing one)
-        const u32x4 o = *reinterpret_cast<const u32x4*>(y + m * K + k0 + 8 * ch);
+      if constexpr (BNB) {
+        // g = dy * relu'(x * scale + shift) with the BN input x; sums of g and g * x_hat
+        const u32x4 xo = pre[it];
+        u32x4 ro = {0u, 0u, 0u, 0u};
+        if constexpr (BNR) {   // the complete gradient: conv + the folded residual gradient (rounded as stored)
+          const long long e = m * K + k0 + 8 * ch;
+          const u32x4 o = PRE3 ? pre_y[PRE3 ? it : 0] : *reinterpret_cast<const u32x4*>(y + e);
+          ro = PRE3 ? pre_r[PRE3 ? it : 0] : *reinterpret_cast<const u32x4*>(bnres + e);
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            v[q] = pack2bf(bf2f(v[q] & 0xffff) + bf2f(o[q] & 0xffff), bf2f(v[q] >> 16) + bf2f(o[q] >> 16));
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float x0 = bf2f(xo[q] & 0xffff), x1 = bf2f(xo[q] >> 16);
+          const float r0 = BNR ? bf2f(ro[q] & 0xffff) : 0.f, r1 = BNR ? bf2f(ro[q] >> 16) : 0.f;
+          const float g0 = x0 * bsc[2 * q] + bsh[2 * q] + r0 > 0.f ? bf2f(v[q] & 0xffff) : 0.f;
+          const float g1 = x1 * bsc[2 * q + 1] + bsh[2 * q + 1] + r1 > 0.f ? bf2f(v[q] >> 16) : 0.f;
+          sg[2 * q] += g0;
+          sg[2 * q + 1] += g1;
+          sgx[2 * q] += g0 * (x0 - bmu[2 * q]) * bis[2 * q];
+          sgx[2 * q + 1] += g1 * (x1 - bmu[2 * q + 1]) * bis[2 * q + 1];
+          v[q] = pack2bf(g0, g1);
+        }
+      } else if (accum) {   // y += conv (an input gradient folded into an existing one)
+        const u32x4 o = pre[it];
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           v[q] = pack2bf(bf2f(v[q] & 0xffff) + bf2f(o[q] & 0xffff), bf2f(v[q] >> 16) + bf2f(o[q] >> 16));
       }
       *reinterpret_cast<u32x4*>(y + m * K + k0 + 8 * ch) = v;
+    }
+  }
+  if constexpr (BNB) {
+    // the NTHR / CPR threads of each chunk column -> per-channel tile sums (fixed order)
+    float* red = reinterpret_cast<float*>(smem + ((BM * PITCH + 15) & ~15));   // behind the tile
+    static_assert(((BM * PITCH + 15) & ~15) + NTHR * 16 * 4 <= 2 * BUF, "BN-backward scratch fits");
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      red[tid * 16 + q] = sg[q];
+      red[tid * 16 + 8 + q] = sgx[q];
+    }
+    __syncthreads();
+    if (tid < BN) {
+      const int ch = tid / 8, q = tid % 8;
+      float a = 0.f, b = 0.f;
+      for (int j = ch; j < NTHR; j += CPR) {
+        a += red[j * 16 + q];
+        b += red[j * 16 + 8 + q];
+      }
+      const int P = gridDim.x;
+      part[((size_t)0 * P + blockIdx.x) * K + k0 + tid] = a;
+      part[((size_t)1 * P + blockIdx.x) * K + k0 + tid] = b;
     }
   }
   if constexpr (STATS) {
@@ -490,7 +596,8 @@ static inline int conv_out(int H, int stride, int ks) { return (H + 2 * (ks / 2)
 
 // y = conv(x, w) (+ y when accum); part (optional): the output's BN statistics partials
 hipError_t dtfk_conv_fwd(const void* x, const void* w, void* y, float* part, int N, int H, int W, int C, int K,
-                         int stride, int bn, int ks, int accum, hipStream_t stream) {
+                         int stride, int bn, int ks, int accum, const void* bnx, const float* bnst, const void* bnres,
+                         hipStream_t stream) {
   using namespace dtfk::cig;
   if (!dtfk_conv_supported(N, H, W, C, K, stride, ks)) return hipErrorInvalidValue;
   const int Ho = conv_out(H, stride, ks), Wo = conv_out(W, stride, ks);
@@ -507,23 +614,38 @@ hipError_t dtfk_conv_fwd(const void* x, const void* w, void* y, float* part, int
   auto xs = static_cast<const uint16_t*>(x);
   auto ws = static_cast<const uint16_t*>(w);
   auto ys = static_cast<uint16_t*>(y);
-#define DTFK_CF(KSV, BNV, ST)                                                                                     \
-  hipLaunchKernelGGL((conv_fwd<KSV, BNV, ST>), grid, dim3(NTHR), 0, stream, xs, ws, ys, part, N, H, W, C, K, Ho, Wo, \
-                     stride, xbytes, accum)
-#define DTFK_CF_BN(KSV)                                                   \
-  if (bn == 128) {                                                        \
-    if (part) DTFK_CF(KSV, 128, true); else DTFK_CF(KSV, 128, false);     \
-  } else {                                                                \
-    if (part) DTFK_CF(KSV, 64, true); else DTFK_CF(KSV, 64, false);       \
+  // EPI 2 (BN backward) overwrites y; EPI 3 (BN + residual backward) needs the folded gradient in y
+  if (bnx != nullptr && (part == nullptr || bnst == nullptr || (bnres != nullptr) != (accum != 0)))
+    return hipErrorInvalidValue;
+  if (bnx == nullptr && bnres != nullptr) return hipErrorInvalidValue;
+  const int epi = bnx != nullptr ? (bnres != nullptr ? 3 : 2) : (part != nullptr ? 1 : 0);
+  auto bx = static_cast<const uint16_t*>(bnx);
+  auto br = static_cast<const uint16_t*>(bnres);
+#define DTFK_CF(KSV, BNV, EP)                                                                                     \
+  hipLaunchKernelGGL((conv_fwd<KSV, BNV, EP>), grid, dim3(NTHR), 0, stream, xs, ws, ys, part, N, H, W, C, K, Ho, Wo, \
+                     stride, xbytes, accum, bx, bnst, br)
+#define DTFK_CF_EPI(KSV, BNV)                                                                               \
+  switch (epi) {                                                                                            \
+    case 3: DTFK_CF(KSV, BNV, 3); break;                                                                    \
+    case 2: DTFK_CF(KSV, BNV, 2); break;                                                                    \
+    case 1: DTFK_CF(KSV, BNV, 1); break;                                                                    \
+    default: DTFK_CF(KSV, BNV, 0);                                                                          \
+  }
+#define DTFK_CF_BN(KSV)                                                                      \
+  if (bn == 128) {                                                                           \
+    DTFK_CF_EPI(KSV, 128)                                                                    \
+  } else {                                                                                   \
+    DTFK_CF_EPI(KSV, 64)                                                                     \
   }
   if (ks == 3) { DTFK_CF_BN(3) } else { DTFK_CF_BN(1) }
 #undef DTFK_CF_BN
+#undef DTFK_CF_EPI
 #undef DTFK_CF
   return hipGetLastError();
 }
 hipError_t dtfk_conv3x3_fwd(const void* x, const void* w, void* y, float* part, int N, int H, int W, int C, int K,
                             int stride, int bn, hipStream_t stream) {
-  return dtfk_conv_fwd(x, w, y, part, N, H, W, C, K, stride, bn, 3, 0, stream);
+  return dtfk_conv_fwd(x, w, y, part, N, H, W, C, K, stride, bn, 3, 0, nullptr, nullptr, nullptr, stream);
 }
 
 long long dtfk_conv_tiles(int N, int H, int W, int stride, int ks) {

@@ -28,6 +28,33 @@ def _nhwc(x: torch.Tensor) -> bool:
 
 # DTF_FUSED_BN=0 routes every layer through MIOpen's BN + separate add/ReLU (A/B runs)
 _ENABLED = os.environ.get("DTF_FUSED_BN", "1") != "0"
+# DTF_BN_BWD_EPILOGUE=0: no BN-backward partials from the consuming convolution's
+# input-gradient epilogue (A/B runs)
+_BWD_EPI = os.environ.get("DTF_BN_BWD_EPILOGUE", "1") != "0"
+_bwd_handoff = {}   # id(BN output) -> BwdSlot: from _FusedBN.forward to FusedBatchNorm2d.forward
+
+
+class BwdSlot:
+    """A BatchNorm (+ residual) + ReLU whose output's gradient may be produced
+    by the consuming convolution's input-gradient kernel together with this BN's
+    backward partials (ops/conv.py: the in-tree implicit GEMM's EPI 2 / 3
+    epilogue masks the gradient with the ReLU and sums g and g * x_hat; with a
+    residual the conv's gradient is first added onto the residual branch's).
+    The conv's backward fills `part`, `g` and `g_version`; the BN's backward
+    uses them when its incoming gradient is exactly that tensor, unmodified."""
+    __slots__ = ("x", "stats", "res", "part", "g", "g_version")
+
+    def __init__(self, x, stats, res=None):
+        self.x, self.stats, self.res = x, stats, res
+        self.part = self.g = self.g_version = None
+
+    def take(self, dy):
+        """(part, P) when dy is the conv's masked gradient, untouched since; else None."""
+        part, g, ver = self.part, self.g, self.g_version
+        self.part = self.g = self.g_version = None
+        if part is None or g is None or dy.data_ptr() != g.data_ptr() or dy._version != ver or dy.shape != g.shape:
+            return None
+        return part
 
 
 class _FusedBN(torch.autograd.Function):
@@ -50,6 +77,10 @@ class _FusedBN(torch.autograd.Function):
         ctx.has_res, ctx.relu = res is not None, relu
         ctx.sink = sink           # (weight, bias) whose .grad the finalize kernel accumulates into, or None
         ctx.res_slot = res_slot   # GradSlot: the residual's gradient goes to the GEMM that consumes it
+        ctx.bwd_slot = None
+        if _BWD_EPI and relu:
+            ctx.bwd_slot = BwdSlot(x, stats, res)
+            _bwd_handoff[id(y)] = ctx.bwd_slot
         return y
 
     @staticmethod
@@ -60,16 +91,23 @@ class _FusedBN(torch.autograd.Function):
         M = x.numel() // ch
         dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         dx = torch.empty_like(x)
-        dres = torch.empty_like(res) if ctx.has_res else None
         if ctx.sink is not None:
             dgamma, dbeta = grad_sink.target(ctx.sink[0]), grad_sink.target(ctx.sink[1])
         else:
             dgamma = torch.empty(ch, dtype=torch.float32, device=x.device)
             dbeta = torch.empty_like(dgamma)
         coef = torch.empty(3 * ch, dtype=torch.float32, device=x.device)
-        part = torch.empty(2 * C.bn_partial_rows(M, ch) * ch, dtype=torch.float32, device=x.device)
-        C.bn_bwd(dy, x, res if ctx.has_res else None, gamma, stats, part, coef, dx, dres, dgamma, dbeta, ctx.relu,
-                 ctx.sink is not None)
+        pre = ctx.bwd_slot.take(dy) if ctx.bwd_slot is not None else None
+        if pre is not None:
+            # dy is already relu-masked and its partials came from the conv's epilogue;
+            # the masked gradient is also the residual's gradient
+            C.bn_bwd_parts(dy, x, gamma, stats, pre[0], pre[1], coef, dx, dgamma, dbeta, ctx.sink is not None)
+            dres = dy if ctx.has_res else None
+        else:
+            dres = torch.empty_like(res) if ctx.has_res else None
+            part = torch.empty(2 * C.bn_partial_rows(M, ch) * ch, dtype=torch.float32, device=x.device)
+            C.bn_bwd(dy, x, res if ctx.has_res else None, gamma, stats, part, coef, dx, dres, dgamma, dbeta,
+                     ctx.relu, ctx.sink is not None)
         if dres is not None and ctx.res_slot is not None and not ctx.res_slot.consumed:
             # folded into the residual source's other consumer: the 1x1 conv's dx GEMM
             # accumulates it (beta = 1) instead of autograd adding the two branches
@@ -123,9 +161,15 @@ class FusedBatchNorm2d(torch.nn.BatchNorm2d):
             pre = getattr(x, "_dtf_bn_part", None)
             if pre is not None and (pre[0].dim() != 3 or pre[0].shape[2] != x.shape[1]):
                 pre = None
-            return _FusedBN.apply(x, self.weight, self.bias, residual, self.running_mean if self.track_running_stats
-                                  else None, self.running_var if self.track_running_stats else None, float(mom),
-                                  float(self.eps), bool(relu), self._sink(), residual_slot, pre)
+            y = _FusedBN.apply(x, self.weight, self.bias, residual, self.running_mean if self.track_running_stats
+                               else None, self.running_var if self.track_running_stats else None, float(mom),
+                               float(self.eps), bool(relu), self._sink(), residual_slot, pre)
+            if _bwd_handoff:
+                slot = _bwd_handoff.pop(id(y), None)
+                _bwd_handoff.clear()
+                if slot is not None:
+                    y._dtf_bn_bwd = slot     # read by the ShadowConv2d that consumes y
+            return y
         self._flush_batches()
         y = super().forward(x)
         if residual is not None:

@@ -142,17 +142,23 @@ def igemm1_ok(x, w16) -> bool:
             and w16.is_contiguous(memory_format=torch.channels_last) and bool(_C().conv3x3_supported(x, w16, 1)))
 
 
-def conv3x3(x, w16, stride: int = 1, stats=None, out=None, bn: int = 0, accumulate: bool = False):
+def conv3x3(x, w16, stride: int = 1, stats=None, out=None, bn: int = 0, accumulate: bool = False,
+            bn_x=None, bn_stats=None, bn_res=None):
     """y = conv2d(x, w16, stride, padding=k//2) on the in-tree implicit GEMM
     (channels_last bf16; w16 3x3 or 1x1).  `stats`: an fp32 [2, P, Cout]
     buffer (P = `conv3x3_stat_rows`) that receives per-channel sums of y and
     y^2 per 128-row tile -- the partials csrc/kernels/bn.hip's finalize
     reduces.  `bn`: output-channel tile width (64 / 128; 0 = the kernel's
-    choice).  `accumulate`: out += the convolution."""
+    choice).  `accumulate`: out += the convolution.  `bn_x` / `bn_stats`: y is
+    the output gradient of a BatchNorm + ReLU whose input was bn_x (stats
+    [4, Cout]); y is stored ReLU-masked and `stats` receives that BN
+    backward's partials (sum g, sum g * x_hat) instead.  `bn_res` (with
+    accumulate): that BN added this residual before the ReLU, and `out` holds
+    the residual branch's gradient the convolution is added onto first."""
     N, _, H, W = x.shape
     Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
     y = _cl_empty(N, w16.shape[0], Ho, Wo, x) if out is None else out
-    _C().conv3x3_fwd(x, w16, y, stats, stride, bn, accumulate)
+    _C().conv3x3_fwd(x, w16, y, stats, stride, bn, accumulate, bn_x, bn_stats, bn_res)
     return y
 
 
@@ -160,18 +166,57 @@ def conv3x3_stat_rows(x, stride: int = 1) -> int:
     return int(_C().conv3x3_tiles(x.shape[0], x.shape[2], x.shape[3], stride))
 
 
-def conv3x3_dx(dy, w16, x_shape, into=None):
+def _bnb_fits(bnb, into, x_shape) -> bool:
+    """The BN-backward epilogue applies: the BN's tensors have x's shape, and a
+    residual BN comes with the residual branch's gradient to add onto (a plain
+    one without)."""
+    if bnb is None or tuple(bnb.x.shape) != tuple(x_shape) or bnb.stats.numel() != 4 * x_shape[1]:
+        return False
+    if bnb.res is None:
+        return into is None
+    return (into is not None and tuple(bnb.res.shape) == tuple(x_shape) and tuple(into.shape) == tuple(x_shape)
+            and into.dtype == torch.bfloat16 and into.is_contiguous(memory_format=torch.channels_last)
+            and bnb.res.is_contiguous(memory_format=torch.channels_last))
+
+
+def conv3x3_dx(dy, w16, x_shape, into=None, bnb=None):
     """Input gradient of a stride-1 3x3 (or 1x1) conv: the same convolution of
     dy with the flipped, channel-transposed filter; `into` (a channels_last bf16
-    gradient of x from another branch) is accumulated in the epilogue."""
+    gradient of x from another branch) is accumulated in the epilogue.  `bnb`
+    (ops.bn.BwdSlot of the BatchNorm (+ residual) + ReLU that produced x): dx
+    is returned ReLU-masked and the epilogue writes that BN backward's partials
+    into the slot, so the BN's backward skips its own pass over the gradient
+    (with a residual BN, `into` must be the residual branch's gradient)."""
     ks = w16.shape[2]
     wt = torch.empty((w16.shape[1], w16.shape[0], ks, ks), device=w16.device, dtype=w16.dtype,
                      memory_format=torch.channels_last)
     _C().conv3x3_wflip(w16, wt)
+    if _bnb_fits(bnb, into, x_shape):
+        P = conv3x3_stat_rows(dy, 1)
+        part = torch.empty((2, P, x_shape[1]), device=dy.device, dtype=torch.float32)
+        dx = into if into is not None else _cl_empty(x_shape[0], x_shape[1], x_shape[2], x_shape[3], dy)
+        conv3x3(dy, wt, 1, stats=part, out=dx, accumulate=into is not None, bn_x=bnb.x, bn_stats=bnb.stats,
+                bn_res=bnb.res)
+        bnb.part, bnb.g, bnb.g_version = (part, P), dx, dx._version
+        return dx
     if into is not None:
         return conv3x3(dy, wt, 1, out=into, accumulate=True)
     dx = _cl_empty(x_shape[0], x_shape[1], x_shape[2], x_shape[3], dy)
     return conv3x3(dy, wt, 1, out=dx)
+
+
+def _fuse_bnb(bnb, dx_eng, key, x) -> bool:
+    """Route a 1x1 input gradient onto the implicit GEMM for the BN-backward
+    epilogue: when it is the chosen engine, or when its measured deficit is
+    below the HBM passes the epilogue saves (one over x for a plain BN, two
+    with a residual: the partials pass re-reads dy, x (and res) and writes g)."""
+    if dx_eng == "igemm":
+        return True
+    t = _timings.get(("dx",) + key)
+    if not t or "igemm" not in t:
+        return False
+    passes = 2 if bnb.res is not None else 1
+    return t["igemm"] - min(t.values()) <= passes * x.numel() * 2 / 5e9   # ms at ~5 TB/s
 
 
 def conv3x3_dw(dy, x, stride: int, into=None, ks=None):
@@ -357,12 +402,13 @@ def _fwd_igemm1(x, w16):
 
 class _ShadowConv(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, w16, stride, padding, dilation, groups, slot=None, share=None):
+    def forward(ctx, x, w, w16, stride, padding, dilation, groups, slot=None, share=None, bnb=None):
         ctx.save_for_backward(x, w16)
         ctx.conf = (stride, padding, dilation, groups)
         ctx.w = w
         ctx.slot = slot
         ctx.share = share
+        ctx.bnb = bnb     # ops.bn.BwdSlot of the BatchNorm + ReLU that produced x
         ctx.gemm = _gemm_ok(x, w16, stride, padding, dilation, groups)
         ctx.xs = None
         if not ctx.gemm and _s2_ok(x, w16, stride, padding, dilation, groups):
@@ -429,16 +475,23 @@ class _ShadowConv(torch.autograd.Function):
                and dy.is_contiguous(memory_format=torch.channels_last) else "miopen")
         dw3 = (_dw3_engine(dy, x, w16, int(stride[0])) if need_w and getattr(ctx, "igemm", False)
                and dy.is_contiguous(memory_format=torch.channels_last) else "miopen")
+        extra = ctx.slot.take() if ctx.slot is not None else None   # a residual branch's gradient of x
+        if other is not None and other[0] == "full":    # the pair's full-size gradient of x
+            extra = other[1] if extra is None else extra.add_(other[1])
+        # the BatchNorm (+ residual) + ReLU that produced x takes its backward
+        # partials from this input gradient's epilogue (not for a shared x: the
+        # pair's other gradient would be missing from the mask's input)
+        bnb = ctx.bnb if share is None else None
+        bnb_ok = need_x and bnb is not None and not strided and _bnb_fits(bnb, extra, x.shape)
+        fuse1 = (bnb_ok and dx3 != "igemm" and gemm and igemm1_ok(x, w16)
+                 and _fuse_bnb(bnb, dx_eng, (tuple(x.shape), w16.shape[0]), x))
         # MIOpen's share: one convolution_backward call for whatever stays on it
-        mx = need_x and dx_eng == "miopen" and not strided and dx3 == "miopen"
+        mx = need_x and dx_eng == "miopen" and not strided and dx3 == "miopen" and not fuse1
         mw = need_w and dw_eng == "miopen" and dw3 == "miopen"
         dx = dw = None
         if mx or mw:
             dx, dw, _ = torch.ops.aten.convolution_backward(dy, x, w16, None, stride, padding, dilation, False,
                                                             [0, 0], groups, [mx, mw, False])
-        extra = ctx.slot.take() if ctx.slot is not None else None   # a residual branch's gradient of x
-        if other is not None and other[0] == "full":    # the pair's full-size gradient of x
-            extra = other[1] if extra is None else extra.add_(other[1])
         if strided:
             # the input gradient lives on the strided pixels only: [N*Ho*Wo, Cin] = dy W
             comp = _cl_empty(x.shape[0], x.shape[1], dy.shape[2], dy.shape[3], dy)
@@ -448,10 +501,14 @@ class _ShadowConv(torch.autograd.Function):
             else:
                 _C().strided_add(extra, comp, stride[0])
                 dx = extra
+        elif need_x and dx3 == "igemm" and bnb_ok:
+            dx = conv3x3_dx(dy, w16, x.shape, into=extra, bnb=bnb)
         elif need_x and dx3 == "igemm":
             dx = conv3x3_dx(dy, w16, x.shape)
             if extra is not None:
                 dx = dx.add_(extra)
+        elif fuse1:
+            dx = conv3x3_dx(dy, w16, x.shape, into=extra, bnb=bnb)
         elif need_x and not mx:
             dx = _dx_gemm(dx_eng, dy, w16, x.shape, into=extra)
         elif need_x and extra is not None:
@@ -461,34 +518,34 @@ class _ShadowConv(torch.autograd.Function):
         if first and not strided:        # first of the pair: hand the full gradient to the second
             share.part, dx = ("full", dx), None
         if not need_w:
-            return dx, None, None, None, None, None, None, None, None
+            return dx, None, None, None, None, None, None, None, None, None
         sink = grad_sink.enabled(w) and (w.grad is None or w.grad.is_contiguous())
         if dw3 == "igemm":      # the in-tree weight gradient accumulates straight into fp32
             if sink:
                 conv3x3_dw(dy, x, int(stride[0]), into=grad_sink.target(w))
                 grad_sink.done(w)
-                return dx, None, None, None, None, None, None, None, None
-            return dx, conv3x3_dw(dy, x, int(stride[0])).to(w.dtype), None, None, None, None, None, None, None
+                return dx, None, None, None, None, None, None, None, None, None
+            return dx, conv3x3_dw(dy, x, int(stride[0])).to(w.dtype), None, None, None, None, None, None, None, None
         if not mw and dw_eng == "igemm":     # the 1x1 implicit GEMM's weight gradient, straight into fp32
             if sink:
                 conv3x3_dw(dy, xw, 1, into=grad_sink.target(w))
                 grad_sink.done(w)
-                return dx, None, None, None, None, None, None, None, None
-            return dx, conv3x3_dw(dy, xw, 1, ks=1).to(w.dtype), None, None, None, None, None, None, None
+                return dx, None, None, None, None, None, None, None, None, None
+            return dx, conv3x3_dw(dy, xw, 1, ks=1).to(w.dtype), None, None, None, None, None, None, None, None
         if not mw:
             from . import big_gemm
             if sink:
                 g = grad_sink.target(w)
                 big_gemm.linear_dw(_rows(dy), _rows(xw), into=g.view(g.shape[0], g.shape[1]))
                 grad_sink.done(w)
-                return dx, None, None, None, None, None, None, None, None
+                return dx, None, None, None, None, None, None, None, None, None
             return (dx, big_gemm.linear_dw(_rows(dy), _rows(xw)).view(w.shape).to(w.dtype), None, None, None, None,
-                    None, None, None)
+                    None, None, None, None)
         if sink:
             grad_sink.target(w).add_(dw)
             grad_sink.done(w)
-            return dx, None, None, None, None, None, None, None, None
-        return dx, dw.to(w.dtype), None, None, None, None, None, None, None
+            return dx, None, None, None, None, None, None, None, None, None
+        return dx, dw.to(w.dtype), None, None, None, None, None, None, None, None
 
 
 class ShadowConv2d(torch.nn.Conv2d):
@@ -503,7 +560,7 @@ class ShadowConv2d(torch.nn.Conv2d):
         shadow path, which the caller must ensure (`on_shadow_path`)."""
         if self.on_shadow_path(x):
             y = _ShadowConv.apply(x, self.weight, self.weight._shadow, self.stride, self.padding, self.dilation,
-                                  self.groups, grad_slot, share)
+                                  self.groups, grad_slot, share, getattr(x, "_dtf_bn_bwd", None))
             if _handoff:
                 st = _handoff.pop(id(y), None)
                 _handoff.clear()

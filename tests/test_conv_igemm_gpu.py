@@ -122,6 +122,108 @@ def test_conv_bn_statistics_handoff(monkeypatch):
         _close(a, b, 1e-2)
 
 
+@pytest.mark.parametrize("ks,two_consumers", [(3, False), (1, False), (3, True)])
+def test_bn_backward_partials_from_conv_input_gradient(monkeypatch, ks, two_consumers):
+    """FusedBatchNorm2d(relu) -> conv (3x3 or 1x1, in-tree implicit GEMM): the
+    conv's input-gradient epilogue masks the gradient with the ReLU and writes
+    the BN backward's partials, and the BN finalizes from them.  Output and all
+    gradients match the unfused path; with a second consumer of the BN output
+    (autograd sums into the gradient) the BN falls back to its own pass."""
+    from distributed_tensorflow_example_amd.ops import bn as bn_mod
+    from distributed_tensorflow_example_amd.ops import conv
+    from distributed_tensorflow_example_amd.ops.bn import FusedBatchNorm2d
+
+    monkeypatch.setattr(conv, "_IGEMM", "always")
+    N, C, H, W, K = 4, 64, 16, 16, 128
+    key = ((N, C, H, W), K)
+    monkeypatch.setattr(conv, "_choice", {("fwd",) + key: "igemm", ("dx",) + key: "igemm", ("dw",) + key: "igemm"})
+    taken = []
+    orig = bn_mod.BwdSlot.take
+
+    def spy(self, dy):
+        r = orig(self, dy)
+        taken.append(r is not None)
+        return r
+    monkeypatch.setattr(bn_mod.BwdSlot, "take", spy)
+    res = {}
+    for fused in (True, False):
+        monkeypatch.setattr(bn_mod, "_BWD_EPI", fused)
+        taken.clear()
+        torch.manual_seed(5)
+        bn = FusedBatchNorm2d(C).cuda()
+        with torch.no_grad():
+            bn.weight.uniform_(0.5, 1.5)
+            bn.bias.uniform_(-0.3, 0.3)
+        m = conv.ShadowConv2d(C, K, ks, 1, ks // 2, bias=False).cuda().to(memory_format=torch.channels_last)
+        conv.attach_shadows(m)
+        x = _cl(torch.randn(N, C, H, W, device="cuda").bfloat16()).requires_grad_(True)
+        h = bn(x, relu=True)
+        assert hasattr(h, "_dtf_bn_bwd") == fused
+        y = m(h)
+        loss = y.float().square().sum()
+        if two_consumers:
+            loss = loss + (h.float() * torch.linspace(-1, 1, W, device="cuda")).sum()
+        loss.backward()
+        if fused:
+            assert taken == [not two_consumers], taken
+        res[fused] = (y.float(), x.grad.float(), bn.weight.grad.float(), bn.bias.grad.float(), m.weight.grad.float())
+    for a, b in zip(res[True], res[False]):
+        _close(a, b, 1.5e-2)
+
+
+def test_bottleneck_chain_bn_backward_epilogues(monkeypatch):
+    """Three identity bottlenecks (models/resnet.py) with every conv on the
+    implicit GEMM: bn1 / bn2 take their backward partials from conv2 / conv3's
+    input-gradient epilogue, and each block's bn3 (residual + ReLU) from the
+    next block's conv1, whose input gradient is added onto the folded residual
+    gradient first.  Output, input gradient and every parameter gradient match
+    the unfused path."""
+    from distributed_tensorflow_example_amd.models.resnet import Bottleneck
+    from distributed_tensorflow_example_amd.ops import bn as bn_mod
+    from distributed_tensorflow_example_amd.ops import conv
+
+    monkeypatch.setattr(conv, "_IGEMM", "always")
+    N, H = 4, 16
+    ch = {}
+    for cin, cout in ((256, 64), (64, 256)):
+        key = ((N, cin, H, H), cout)
+        for role in ("fwd", "dx", "dw"):
+            ch[(role,) + key] = "igemm"
+    monkeypatch.setattr(conv, "_choice", ch)
+    taken = []
+    orig = bn_mod.BwdSlot.take
+
+    def spy(self, dy):
+        r = orig(self, dy)
+        taken.append((self.res is not None, r is not None))
+        return r
+    monkeypatch.setattr(bn_mod.BwdSlot, "take", spy)
+    res = {}
+    for fused in (True, False):
+        monkeypatch.setattr(bn_mod, "_BWD_EPI", fused)
+        taken.clear()
+        torch.manual_seed(9)
+        net = torch.nn.Sequential(*[Bottleneck(256, 64) for _ in range(3)]).cuda().to(
+            memory_format=torch.channels_last)
+        for m in net.modules():
+            if isinstance(m, bn_mod.FusedBatchNorm2d):
+                with torch.no_grad():
+                    m.weight.uniform_(0.5, 1.5)
+                    m.bias.uniform_(-0.2, 0.2)
+        conv.attach_shadows(net)
+        x = _cl(torch.randn(N, 256, H, H, device="cuda").bfloat16()).requires_grad_(True)
+        y = net(x)
+        (y.float() * torch.linspace(-1, 1, H, device="cuda")).square().sum().backward()
+        if fused:
+            # 3 blocks x (bn1, bn2) plain + bn3 of blocks 0 and 1 through the next conv1
+            assert sum(1 for r, t in taken if t and not r) == 6, taken
+            assert sum(1 for r, t in taken if t and r) == 2, taken
+        grads = [p.grad.float().clone() for p in net.parameters()]
+        res[fused] = [y.float(), x.grad.float()] + grads
+    for a, b in zip(res[True], res[False]):
+        _close(a, b, 2e-2)
+
+
 @pytest.mark.parametrize("M,K,N", [(2 * 256, 256, 512), (6272, 512, 2048), (3136 // 2, 256, 64), (200, 128, 136)])
 def test_gemm_bn_stats_epilogue(M, K, N):
     """gemm_big's statistics epilogue (dtfk_gemm_bn_stats): y = x W^T in bf16 and

@@ -42,6 +42,7 @@ hipError_t dtfk_bn_bwd_parts(const void* g, const void* x, const float* gamma, c
                              int accum, hipStream_t st);
 long long dtfk_conv_tiles(int N, int H, int W, int stride, int ks);
 hipError_t dtfk_conv_wflip(const void* w, void* wt, int K, int C, int ks, hipStream_t stream);
+hipError_t dtfk_conv_wflip_multi(const long long* tab, const int* tiles, int ntiles, hipStream_t stream);
 long long dtfk_conv_wgrad_plan(int N, int H, int W, int C, int K, int stride, int ks, int* splits_out, int* sps_out);
 hipError_t dtfk_conv_wgrad(const void* dy, const void* x, float* dw, float* ws, int N, int H, int W, int C, int K,
                            int stride, int ks, int kcrs, hipStream_t stream);
@@ -267,6 +268,20 @@ void conv3x3_wflip(at::Tensor w, at::Tensor wt) {
   ck(dtfk_conv_wflip(w.data_ptr(), wt.data_ptr(), (int)w.size(0), (int)w.size(1), ks, cs()), "conv_wflip");
 }
 
+// Several filters flipped in one launch.  tab: int64 [n, 5] rows {w, wt, K, C, ks}
+// (device pointers of channels_last bf16 filters, checked by the caller:
+// ops/conv.py _flipped), tiles: int32 [m, 4] (row, tap, k0, c0) per 64 x 64
+// tile, both on the device.
+void conv_wflip_multi(at::Tensor tab, at::Tensor tiles) {
+  if (!tab.is_cuda() || tab.scalar_type() != at::kLong || tab.dim() != 2 || tab.size(1) != 5 || !tab.is_contiguous() ||
+      !tiles.is_cuda() || tiles.scalar_type() != at::kInt || tiles.dim() != 2 || tiles.size(1) != 4 ||
+      !tiles.is_contiguous())
+    throw std::runtime_error("conv_wflip_multi: tab int64 [n, 5], tiles int32 [m, 4] on the device");
+  ck(dtfk_conv_wflip_multi(reinterpret_cast<const long long*>(tab.data_ptr<int64_t>()), tiles.data_ptr<int>(),
+                           (int)tiles.size(0), cs()),
+     "conv_wflip_multi");
+}
+
 // dw (fp32 [K, C, ks, ks], channels_last or contiguous) += the weight gradient of
 // y = conv(x, w, stride) for y's gradient dy
 void conv3x3_wgrad(at::Tensor dy, at::Tensor x, at::Tensor dw, int64_t stride) {
@@ -334,6 +349,7 @@ void init_bn(pybind11::module& m) {
         py::arg("stride") = 1, py::arg("bn") = 0, py::arg("accumulate") = false, py::arg("bn_x") = py::none(),
         py::arg("bn_stats") = py::none(), py::arg("bn_res") = py::none());
   m.def("conv3x3_wflip", &conv3x3_wflip);
+  m.def("conv_wflip_multi", &conv_wflip_multi);
   m.def("strided_add", &strided_add);
   m.def("bn_partial_rows", &bn_partial_rows);
   m.def("maxpool_fwd", &maxpool_fwd);

@@ -574,10 +574,51 @@ __global__ void wflip(const uint16_t* __restrict__ w, uint16_t* __restrict__ wt,
   }
 }
 
+// Every conv's flipped filter in one launch, as LDS-tiled transposes: for
+// each tap rs, w[k][rs][c] -> wt[c][TAPS-1-rs][k].  Rows of `tab` are
+// {w, wt, K, C, ks} (int64); `tiles` lists (row, rs, k0, c0) per 64 x 64 tile.
+// Once per optimizer step instead of one wflip launch per conv backward.
+__global__ __launch_bounds__(256) void wflip_multi(const long long* __restrict__ tab, const int4* __restrict__ tiles) {
+  __shared__ uint16_t t[64][66];
+  const int4 d = tiles[blockIdx.x];
+  const long long* r = tab + 5LL * d.x;
+  const uint16_t* __restrict__ w = reinterpret_cast<const uint16_t*>(r[0]);
+  uint16_t* __restrict__ wt = reinterpret_cast<uint16_t*>(r[1]);
+  const int K = (int)r[2], C = (int)r[3], KS = (int)r[4], TAPS = KS * KS;
+  const int rs = d.y, k0 = d.z, c0 = d.w;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  for (int kk = ty; kk < 64; kk += 16) {      // read 64 k rows x 64 c (c contiguous)
+    const int k = k0 + kk;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = c0 + 4 * tx + j;
+      t[kk][4 * tx + j] = (k < K && c < C) ? w[((long long)k * TAPS + rs) * C + c] : (uint16_t)0;
+    }
+  }
+  __syncthreads();
+  const int rsf = TAPS - 1 - rs;
+  for (int cc = ty; cc < 64; cc += 16) {      // write 64 c rows x 64 k (k contiguous)
+    const int c = c0 + cc;
+    if (c >= C) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = k0 + 4 * tx + j;
+      if (k < K) wt[((long long)c * TAPS + rsf) * K + k] = t[4 * tx + j][cc];
+    }
+  }
+}
+
 }  // namespace cig
 }  // namespace dtfk
 
 extern "C" {
+
+hipError_t dtfk_conv_wflip_multi(const long long* tab, const int* tiles, int ntiles, hipStream_t stream) {
+  if (ntiles <= 0) return hipSuccess;
+  hipLaunchKernelGGL(dtfk::cig::wflip_multi, dim3((unsigned)ntiles), dim3(256), 0, stream, tab,
+                     reinterpret_cast<const int4*>(tiles));
+  return hipGetLastError();
+}
 
 // 0: ok; invalid shapes return hipErrorInvalidValue (the caller uses MIOpen).
 // ks: 3 (pad 1) or 1 (pad 0)

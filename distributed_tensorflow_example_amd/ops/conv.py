@@ -40,6 +40,7 @@ Any other case (CPU, no shadow, eval under a different dtype) is plain
 from __future__ import annotations
 
 import os
+import weakref
 
 import torch
 import torch.nn.functional as F
@@ -166,6 +167,59 @@ def conv3x3_stat_rows(x, stride: int = 1) -> int:
     return int(_C().conv3x3_tiles(x.shape[0], x.shape[2], x.shape[3], stride))
 
 
+# flipped filters of the input gradients: id(w16) -> [weakref(w16), wt, w16._version at the flip].
+# The fused optimizer rewrites a shadow in place and bumps its version
+# (optim.FusedOptimizer.step), so after a step the first input gradient
+# re-flips every registered filter in ONE launch (conv_wflip_multi) instead
+# of one wflip launch per conv backward (~5 us each, 40 per ResNet-50 step).
+_FLIP_CACHE = os.environ.get("DTF_CONV_FLIP_CACHE", "1") != "0"
+_flips: dict = {}
+_flip_tab: dict = {"key": None}
+
+
+def _flipped(w16):
+    ks = w16.shape[2]
+    if not _FLIP_CACHE:
+        wt = torch.empty((w16.shape[1], w16.shape[0], ks, ks), device=w16.device, dtype=w16.dtype,
+                         memory_format=torch.channels_last)
+        _C().conv3x3_wflip(w16, wt)
+        return wt
+    ent = _flips.get(id(w16))
+    if ent is None or ent[0]() is not w16:
+        wt = torch.empty((w16.shape[1], w16.shape[0], ks, ks), device=w16.device, dtype=w16.dtype,
+                         memory_format=torch.channels_last)
+        ent = _flips[id(w16)] = [weakref.ref(w16), wt, None]
+    if ent[2] == w16._version:
+        return ent[1]
+    stale = []
+    for k, e in list(_flips.items()):
+        w = e[0]()
+        if w is None:
+            del _flips[k]
+        elif e[2] != w._version and w.device == w16.device:
+            stale.append((w, e))
+    key = tuple((w.data_ptr(), e[1].data_ptr()) for w, e in stale)
+    if _flip_tab["key"] != key and torch.cuda.is_current_stream_capturing():
+        # no host-built table inside a capture: this filter alone
+        _C().conv3x3_wflip(w16, ent[1])
+        ent[2] = w16._version
+        return ent[1]
+    if _flip_tab["key"] != key:
+        rows, tiles = [], []
+        for i, (w, e) in enumerate(stale):
+            K_, C_, ks_ = w.shape[0], w.shape[1], w.shape[2]
+            rows.append([w.data_ptr(), e[1].data_ptr(), K_, C_, ks_])
+            tiles.extend([i, rs, k0, c0] for rs in range(ks_ * ks_) for k0 in range(0, K_, 64)
+                         for c0 in range(0, C_, 64))
+        _flip_tab.update(key=key, tab=torch.tensor(rows, dtype=torch.int64).to(w16.device),
+                         tiles=torch.tensor(tiles, dtype=torch.int32).reshape(-1, 4).to(w16.device),
+                         refs=[e[1] for _, e in stale])
+    _C().conv_wflip_multi(_flip_tab["tab"], _flip_tab["tiles"])
+    for w, e in stale:
+        e[2] = w._version
+    return ent[1]
+
+
 def _bnb_fits(bnb, into, x_shape) -> bool:
     """The BN-backward epilogue applies: the BN's tensors have x's shape, and a
     residual BN comes with the residual branch's gradient to add onto (a plain
@@ -187,10 +241,7 @@ def conv3x3_dx(dy, w16, x_shape, into=None, bnb=None):
     is returned ReLU-masked and the epilogue writes that BN backward's partials
     into the slot, so the BN's backward skips its own pass over the gradient
     (with a residual BN, `into` must be the residual branch's gradient)."""
-    ks = w16.shape[2]
-    wt = torch.empty((w16.shape[1], w16.shape[0], ks, ks), device=w16.device, dtype=w16.dtype,
-                     memory_format=torch.channels_last)
-    _C().conv3x3_wflip(w16, wt)
+    wt = _flipped(w16)
     if _bnb_fits(bnb, into, x_shape):
         P = conv3x3_stat_rows(dy, 1)
         part = torch.empty((2, P, x_shape[1]), device=dy.device, dtype=torch.float32)
@@ -519,7 +570,11 @@ class _ShadowConv(torch.autograd.Function):
             share.part, dx = ("full", dx), None
         if not need_w:
             return dx, None, None, None, None, None, None, None, None, None
-        sink = grad_sink.enabled(w) and (w.grad is None or w.grad.is_contiguous())
+        # every weight-gradient path below accumulates into a contiguous or a
+        # channels_last fp32 .grad (the DDP bucket view mirrors the weight's layout:
+        # channels_last 3x3 filters included)
+        sink = grad_sink.enabled(w) and (w.grad is None or w.grad.is_contiguous()
+                                         or w.grad.is_contiguous(memory_format=torch.channels_last))
         if dw3 == "igemm":      # the in-tree weight gradient accumulates straight into fp32
             if sink:
                 conv3x3_dw(dy, x, int(stride[0]), into=grad_sink.target(w))

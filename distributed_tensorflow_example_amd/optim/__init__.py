@@ -26,6 +26,8 @@ import torch
 
 from .. import _native
 
+_bump_version = torch.autograd.graph.increment_version
+
 KINDS = {"sgd": 0, "momentum": 1, "adam": 2, "adamw": 3, "adagrad": 4, "rmsprop": 5}
 
 
@@ -197,6 +199,11 @@ class _FusedBase:
                                           float(grad_scale), self.wd, self.b1, self.b2, self.eps,
                                           self.momentum, self.nesterov, self.step_t,
                                           None if skip is None else skip.reshape(-1)[:1].to(torch.int32))
+        # the kernel rewrote the bf16 shadows in place: bump their version counters as
+        # an in-place torch op would (caches keyed on them, e.g. ops/conv.py's flipped
+        # filters, see the change; a graph still holding an old shadow raises as usual)
+        for sh in self.shadows.values():
+            _bump_version(sh)
 
     def _step_cpu(self, grads, gs):
         self._step_cpu_math(grads, gs)

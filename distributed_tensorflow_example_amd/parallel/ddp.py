@@ -109,10 +109,11 @@ def measure_allreduce_cost(world: World, device: torch.device, dtype=torch.float
 
 
 class _Bucket:
-    def __init__(self, params: List[torch.nn.Parameter], dtype, device):
+    def __init__(self, params: List[torch.nn.Parameter], dtype, device, buf: Optional[torch.Tensor] = None):
         self.params = params
         n = sum(p.numel() for p in params)
-        self.buf = torch.zeros(n, dtype=dtype, device=device)
+        # buf: this bucket's slice of the model's one flat gradient buffer
+        self.buf = torch.zeros(n, dtype=dtype, device=device) if buf is None else buf
         self.views = []
         off = 0
         for p in params:
@@ -176,7 +177,16 @@ class DistributedDataParallel(torch.nn.Module):
                 cur, cur_bytes = [], 0
         if cur:
             buckets.append(cur)
-        self.buckets = [_Bucket(b, torch.float32, self.device) for b in buckets]
+        # every bucket is a slice of ONE flat fp32 buffer (each slice 256-byte aligned):
+        # zero_grad is a single fill instead of one per bucket
+        sizes = [sum(p.numel() for p in b) for b in buckets]
+        offs, tot = [], 0
+        for n in sizes:
+            offs.append(tot)
+            tot += (n + 63) // 64 * 64
+        self._flat = torch.zeros(tot, dtype=torch.float32, device=self.device)
+        self.buckets = [_Bucket(b, torch.float32, self.device, self._flat[o:o + n])
+                        for b, o, n in zip(buckets, offs, sizes)]
         self._param_bucket = {}
         for bi, b in enumerate(self.buckets):
             for idx, (p, v) in enumerate(zip(b.params, b.views)):
@@ -290,8 +300,7 @@ class DistributedDataParallel(torch.nn.Module):
         self.reset_step()
 
     def zero_grad(self):
-        for b in self.buckets:
-            b.buf.zero_()
+        self._flat.zero_()
 
     def grads(self) -> List[torch.Tensor]:
         return [p.grad for p in self.module.parameters() if p.requires_grad]

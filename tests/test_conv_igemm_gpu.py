@@ -362,3 +362,49 @@ def test_shadow_conv1x1_on_igemm_trains_like_miopen(monkeypatch):
         res[eng] = (y.float(), x.grad.float(), m.weight.grad.float())
     for a, b in zip(res["igemm"], res["miopen"]):
         _close(a, b, 2e-2)
+
+
+def test_flipped_filter_cache_follows_optimizer_steps(monkeypatch):
+    """The input gradient's flipped filters are cached per shadow version and
+    re-flipped in one batched launch after a fused optimizer step: three
+    momentum steps of two stacked convs (3x3 then 1x1, both on the implicit
+    GEMM) match the uncached run, and the batched flip equals per-filter flips."""
+    from distributed_tensorflow_example_amd import _native, optim
+    from distributed_tensorflow_example_amd.ops import conv
+
+    monkeypatch.setattr(conv, "_IGEMM", "always")
+    N, C, H = 4, 64, 16
+    key = ((N, C, H, H), C)
+    monkeypatch.setattr(conv, "_choice", {("fwd",) + key: "igemm", ("dx",) + key: "igemm", ("dw",) + key: "igemm"})
+    res = {}
+    for cache in (True, False):
+        monkeypatch.setattr(conv, "_FLIP_CACHE", cache)
+        torch.manual_seed(4)
+        net = torch.nn.Sequential(conv.ShadowConv2d(C, C, 3, 1, 1, bias=False),
+                                  conv.ShadowConv2d(C, C, 1, bias=False)).cuda().to(memory_format=torch.channels_last)
+        opt = optim.FusedMomentum(list(net.parameters()), 0.05, 0.9)
+        conv.attach_shadows(net, opt)
+        x = _cl(torch.randn(N, C, H, H, device="cuda").bfloat16()).requires_grad_(True)
+        for _ in range(3):
+            for p in net.parameters():
+                p.grad = None
+            x.grad = None
+            net(x).float().square().mean().backward()
+            opt.step()
+        res[cache] = [p.detach().clone() for p in net.parameters()] + [x.grad.float()]
+    for a, b in zip(res[True], res[False]):
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
+    C_ = _native.load()
+    ws = [_cl(torch.randn(96, 64, k, k, device="cuda").bfloat16()) for k in (1, 3, 3)]
+    outs = [torch.empty((w.shape[1], w.shape[0], w.shape[2], w.shape[3]), device="cuda", dtype=torch.bfloat16,
+                        memory_format=torch.channels_last) for w in ws]
+    tab = torch.tensor([[w.data_ptr(), o.data_ptr(), w.shape[0], w.shape[1], w.shape[2]] for w, o in zip(ws, outs)],
+                       dtype=torch.int64).cuda()
+    tiles = torch.tensor([[i, rs, k0, c0] for i, w in enumerate(ws) for rs in range(w.shape[2] ** 2)
+                          for k0 in range(0, w.shape[0], 64) for c0 in range(0, w.shape[1], 64)],
+                         dtype=torch.int32).cuda()
+    C_.conv_wflip_multi(tab, tiles)
+    for w, o in zip(ws, outs):
+        ref = torch.empty_like(o)
+        C_.conv3x3_wflip(w, ref)
+        assert torch.equal(o, ref)

@@ -30,6 +30,7 @@
 // The input gradient of a stride-1 3x3 conv is the same convolution of dy with
 // the flipped, channel-transposed filter (conv_igemm_wflip builds it).
 #include "common.h"
+#include <cstdlib>
 
 #include <type_traits>
 
@@ -533,26 +534,40 @@ __global__ __launch_bounds__(NTHR, 2) void conv_wgrad(const uint16_t* __restrict
     }
 }
 
-// dW += sum_z slab_z, in split order: one thread per f32x4 of the fragment-order
-// tiles (the wgrad epilogue's layout), mapped back to (output channel, filter column)
+// dW += sum_z slab_z: G threads per f32x4 of the fragment-order tiles (the
+// wgrad epilogue's layout), thread g summing slabs g, g + G, ... in order and
+// the G partials then combined in LDS in g order -- a fixed summation order
+// (deterministic).  With one thread per output (the first version) a 2-tile
+// 1x1 weight gradient at 56x56 (256 slabs) ran 16 workgroups of 256-long
+// serial load chains.  Each output is mapped back to (output channel, filter
+// column) and added into dW once.
 template <int KS, int BMW, int BNW>
 __global__ __launch_bounds__(256) void wgrad_reduce(const float* __restrict__ ws, int S, long long slab,
-                                                    float* __restrict__ dw, int C, int tiles_x, int kcrs) {
+                                                    float* __restrict__ dw, int C, int tiles_x, int kcrs, int G) {
   constexpr int WM = BMW / 2, WN = BNW / 2, TM = WM / 16, TN = WN / 16;
   constexpr int Q = BMW * BNW / 4;                      // f32x4 per tile
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e * 4 >= slab) return;
-  const int tile = (int)(e / Q), q = (int)(e - (long long)tile * Q);
-  const int lane = q & 63, f = q >> 6;                  // f = (wave * TM + i) * TN + j
+  __shared__ f32x4 red[256];
+  const int OPB = 256 / G;                              // outputs per block
+  const int lo = threadIdx.x % OPB, g = threadIdx.x / OPB;
+  const long long e = (long long)blockIdx.x * OPB + lo;
+  const bool valid = e * 4 < slab;
+  f32x4 z = {0.f, 0.f, 0.f, 0.f};
+  if (valid) {
+    const float* src = ws + e * 4;
+    for (int s = g; s < S; s += G) z += *reinterpret_cast<const f32x4*>(src + s * slab);
+  }
+  red[threadIdx.x] = z;
+  __syncthreads();
+  if (g != 0 || !valid) return;
+  for (int q = 1; q < G; ++q) z += red[q * OPB + lo];
+  const int tile = (int)(e / Q), qq = (int)(e - (long long)tile * Q);
+  const int lane = qq & 63, f = qq >> 6;                // f = (wave * TM + i) * TN + j
   const int j = f % TN, i = (f / TN) % TM, wv = f / (TN * TM);
   const int wm = wv >> 1, wn = wv & 1;
   const int NC = KS * KS * C;
   const int col = (tile / tiles_x) * BNW + wn * WN + 16 * j + (lane & 15);
   if (col >= NC) return;
   const int row0 = (tile % tiles_x) * BMW + wm * WM + 16 * i + 4 * (lane >> 4);
-  const float* src = ws + e * 4;
-  f32x4 z = *reinterpret_cast<const f32x4*>(src);
-  for (int s = 1; s < S; ++s) z += *reinterpret_cast<const f32x4*>(src + s * slab);
   const int cidx = kcrs ? (col % C) * (KS * KS) + col / C : col;
 #pragma unroll
   for (int r = 0; r < 4; ++r) dw[(long long)(row0 + r) * NC + cidx] += z[r];
@@ -723,8 +738,22 @@ long long dtfk_conv_wgrad_plan(int N, int H, int W, int C, int K, int stride, in
   const int bnw = NC % 128 == 0 ? 128 : 64;
   const long long tiles = (long long)(K / bm) * ((NC + bnw - 1) / bnw);
   const long long steps = (P + 63) / 64;
-  long long splits = (512 + tiles - 1) / tiles;
-  if (splits > steps / 8) splits = steps / 8;
+  // target workgroups: 512 (two per CU); 256 for the few-tile 1x1 gradients
+  // (56x56 / 28x28: fewer, longer splits), 1024 for the many-tile 3x3 ones
+  // (profiles/conv_wgrad_sweep_r5.txt; DTF_CONV_WGRAD_WGS overrides), and the
+  // minimum 64-pixel steps per split (DTF_CONV_WGRAD_MINSTEPS, default 8)
+  static const long long env_target = [] {
+    const char* e = getenv("DTF_CONV_WGRAD_WGS");
+    return e ? atoll(e) : 0LL;
+  }();
+  const long long target = env_target > 0 ? env_target
+                                          : (ks == 1 ? (tiles <= 4 ? 256 : 512) : (tiles >= 32 ? 1024 : 512));
+  static const long long minsteps = [] {
+    const char* e = getenv("DTF_CONV_WGRAD_MINSTEPS");
+    return e ? atoll(e) : 8LL;
+  }();
+  long long splits = (target + tiles - 1) / tiles;
+  if (splits > steps / minsteps) splits = steps / minsteps;
   if (splits < 1) splits = 1;
   const int sps = (int)((steps + splits - 1) / splits);
   splits = (steps + sps - 1) / sps;
@@ -756,6 +785,9 @@ hipError_t dtfk_conv_wgrad(const void* dy, const void* x, float* dw, float* ws, 
   const long long slab = wsn > 0 ? wsn / splits : 0;
   const dim3 grid((unsigned)(K / bm), (unsigned)((NC + bnw - 1) / bnw), (unsigned)splits);
   const long long xbytes = (long long)N * H * W * C * 2;
+  // reduce threads per output: up to 16, ~128K threads in all
+  int G = 1;
+  while (G < 16 && 2 * G <= splits && (slab / 4) * G < 131072) G *= 2;
   auto d = static_cast<const uint16_t*>(dy);
   auto xs = static_cast<const uint16_t*>(x);
 #define DTFK_WG(KSV, A, B)                                                                                         \
@@ -763,8 +795,8 @@ hipError_t dtfk_conv_wgrad(const void* dy, const void* x, float* dw, float* ws, 
     hipLaunchKernelGGL((conv_wgrad<KSV, A, B>), grid, dim3(NTHR), 0, stream, d, xs, dw, N, H, W, C, K, Ho, Wo,     \
                        stride, xbytes, sps, kcrs, wsp, slab);                                                      \
     if (wsp)                                                                                                       \
-      hipLaunchKernelGGL((wgrad_reduce<KSV, A, B>), dim3((unsigned)((slab / 4 + 255) / 256)), dim3(256), 0, stream, \
-                         wsp, splits, slab, dw, C, (int)grid.x, kcrs);                                             \
+      hipLaunchKernelGGL((wgrad_reduce<KSV, A, B>), dim3((unsigned)((slab / 4 + 256 / G - 1) / (256 / G))),        \
+                         dim3(256), 0, stream, wsp, splits, slab, dw, C, (int)grid.x, kcrs, G);                    \
   } while (0)
 #define DTFK_WG_T(KSV)                                 \
   if (bm == 128 && bnw == 128) DTFK_WG(KSV, 128, 128); \

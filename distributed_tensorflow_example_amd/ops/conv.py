@@ -288,12 +288,15 @@ def _dw3_engine(dy, x, w16, stride: int) -> str:
     if ("dw3",) + key not in _choice:
         if _POLICY == "never":
             return "miopen"
-        acc = torch.zeros((w16.shape[0], w16.shape[1], 3, 3), device=x.device, dtype=torch.float32)
+        # the accumulator in the layout of the .grad it stands for (the weight's)
+        fmt = torch.channels_last if w16.is_contiguous(memory_format=torch.channels_last) else torch.contiguous_format
+        acc = torch.zeros((w16.shape[0], w16.shape[1], 3, 3), device=x.device, dtype=torch.float32).contiguous(
+            memory_format=fmt)
 
         def miopen():
             dw = torch.ops.aten.convolution_backward(dy, x, w16, None, (stride, stride), (1, 1), (1, 1), False,
                                                      [0, 0], 1, [False, True, False])[1]
-            acc.add_(dw)
+            acc.add_(dw.float())
         return _pick("dw3", key, {"miopen": miopen, "igemm": lambda: conv3x3_dw(dy, x, stride, into=acc)})
     return _choice[("dw3",) + key]
 
@@ -395,7 +398,7 @@ def _dw_engine(dy, x, w16) -> str:
         def miopen():
             dw = torch.ops.aten.convolution_backward(dy, x, w16, None, (1, 1), (0, 0), (1, 1), False, [0, 0], 1,
                                                      [False, True, False])[1]
-            acc.add_(dw.view(acc.shape))
+            acc.add_(dw.view(acc.shape).float())
         cands = {"miopen": miopen, "gemm_big": lambda: big_gemm.linear_dw(dy2, x2, into=acc)}
         if igemm1_ok(x, w16):
             acc4 = acc.view(w16.shape[0], w16.shape[1], 1, 1)
@@ -597,7 +600,10 @@ class _ShadowConv(torch.autograd.Function):
             return (dx, big_gemm.linear_dw(_rows(dy), _rows(xw)).view(w.shape).to(w.dtype), None, None, None, None,
                     None, None, None, None)
         if sink:
-            grad_sink.target(w).add_(dw)
+            # bf16 -> fp32 first: a mixed-dtype add_ into the fp32 .grad runs PyTorch's
+            # vectorized_templated kernel at ~45 us for a 9-37K element filter on this
+            # stack (3.9 us as a copy + same-dtype add; profiles/resnet50_sink_add_r5.txt)
+            grad_sink.target(w).add_(dw.float())
             grad_sink.done(w)
             return dx, None, None, None, None, None, None, None, None, None
         return dx, dw.to(w.dtype), None, None, None, None, None, None, None, None

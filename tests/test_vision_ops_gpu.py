@@ -9,7 +9,8 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("shape,k,s,p", [((4, 64, 112, 112), 3, 2, 1), ((2, 16, 9, 11), 3, 2, 1),
-                                         ((2, 8, 10, 10), 2, 2, 0), ((1, 24, 7, 7), 3, 1, 1)])
+                                         ((2, 8, 10, 10), 2, 2, 0), ((1, 24, 7, 7), 3, 1, 1),
+                                         ((2, 8, 9, 12), 3, 2, 0)])
 def test_maxpool_nhwc_matches_fp32(native, shape, k, s, p):
     from distributed_tensorflow_example_amd.ops.pool import max_pool2d
 
@@ -39,6 +40,24 @@ def test_maxpool_ties_take_first_and_nan_propagates(native):
     y.backward(torch.ones_like(y))
     # all-zero windows: the first position (0, 0) of each window gets the gradient
     assert x.grad[0, 1, 0, 0] == 1 and x.grad[0, 1, 0, 1] == 0 and x.grad[0, 1, 1, 0] == 0
+
+
+def test_maxpool_3x3_stride2_ties_match_torch(native):
+    """The specialized 3x3 / stride-2 kernels on tie-heavy input (all zeros with a
+    NaN): torch's first-maximum rule, forward values and the gradient routing."""
+    from distributed_tensorflow_example_amd.ops.pool import max_pool2d
+
+    x = torch.zeros(2, 16, 11, 13, device="cuda", dtype=torch.bfloat16)
+    x[1, 3, 4, 5] = float("nan")
+    x = x.contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    y = max_pool2d(x, 3, 2, 1)
+    xr = x.detach().float().requires_grad_(True)
+    yr = F.max_pool2d(xr, 3, 2, 1)
+    torch.testing.assert_close(y.float(), yr, equal_nan=True, rtol=0, atol=0)
+    g = torch.arange(yr.numel(), device="cuda", dtype=torch.float32).reshape(yr.shape).remainder(7).bfloat16()
+    y.backward(g.contiguous(memory_format=torch.channels_last))
+    yr.backward(g.float())
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=0, atol=0)
 
 
 @pytest.mark.parametrize("engines", [("hipblaslt", "hipblaslt", "gemm_big"), ("gemm_big", "gemm_big", "gemm_big"),

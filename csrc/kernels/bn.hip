@@ -106,18 +106,22 @@ __device__ __forceinline__ void sum_partials(const float* __restrict__ part, int
   __shared__ double red[2][FG][FC];
   double a = 0.0, b = 0.0;
   if (c < C) {
-    int p = g;
-    for (; p + 3 * FG < P; p += 4 * FG) {      // four independent loads per sum in flight
-      float x0 = part[(size_t)p * C + c], x1 = part[(size_t)(p + FG) * C + c];
-      float x2 = part[(size_t)(p + 2 * FG) * C + c], x3 = part[(size_t)(p + 3 * FG) * C + c];
-      float y0 = part[((size_t)P + p) * C + c], y1 = part[((size_t)P + p + FG) * C + c];
-      float y2 = part[((size_t)P + p + 2 * FG) * C + c], y3 = part[((size_t)P + p + 3 * FG) * C + c];
-      a += ((double)x0 + x1) + ((double)x2 + x3);
-      b += ((double)y0 + y1) + ((double)y2 + y3);
-    }
-    for (; p < P; p += FG) {
-      a += part[(size_t)p * C + c];
-      b += part[((size_t)P + p) * C + c];
+    // four rows per trip, all eight loads issued unconditionally (rows past P
+    // re-read row p and are masked out): one round of loads per four rows
+    for (int p = g; p < P; p += 4 * FG) {
+      float xv[4], yv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int q = p + j * FG < P ? p + j * FG : p;
+        xv[j] = part[(size_t)q * C + c];
+        yv[j] = part[((size_t)P + q) * C + c];
+      }
+#pragma unroll
+      for (int j = 1; j < 4; ++j) {
+        if (p + j * FG >= P) xv[j] = yv[j] = 0.f;
+      }
+      a += ((double)xv[0] + xv[1]) + ((double)xv[2] + xv[3]);
+      b += ((double)yv[0] + yv[1]) + ((double)yv[2] + yv[3]);
     }
   }
   red[0][g][lane] = a;
@@ -328,14 +332,25 @@ static int bn_grid(int M, int C) {
   if (g > 512) g = 512;
   return g < 1 ? 1 : g;
 }
-// the finalize kernels' channels per block (sum_partials)
+// the finalize kernels' channels per block (sum_partials): 16 for C >= 1024,
+// 8 for >= 512, else 4.  Fewer channels per block for the long (P = 3136)
+// partials of the 56x56 convolutions measured slower: FC = 1 took 11-13 us
+// against 6-8 us (1024-deep LDS tree, one float per row per lane;
+// profiles/resnet50_b128_steps_r5_fc1.txt)
+static int finalize_fc(int /*P*/, int C) { return C >= 1024 ? 16 : (C >= 512 ? 8 : 4); }
 static void launch_finalize(const float* part, int P, int M, int C, const float* gamma, const float* beta, float* mean,
                             float* invstd, float* scale, float* shift, float* run_mean, float* run_var, float momentum,
                             float eps, hipStream_t st) {
 #define DTFK_FIN(FC)                                                                                                \
   hipLaunchKernelGGL((bn_finalize<FC>), dim3((C + FC - 1) / FC), dim3(1024), 0, st, part, P, M, C, gamma, beta, mean, \
                      invstd, scale, shift, run_mean, run_var, momentum, eps)
-  if (C >= 1024) DTFK_FIN(16); else if (C >= 512) DTFK_FIN(8); else DTFK_FIN(4);
+  switch (finalize_fc(P, C)) {
+    case 16: DTFK_FIN(16); break;
+    case 8: DTFK_FIN(8); break;
+    case 4: DTFK_FIN(4); break;
+    case 2: DTFK_FIN(2); break;
+    default: DTFK_FIN(1);
+  }
 #undef DTFK_FIN
 }
 static void launch_bwd_finalize(const float* part, int P, int M, int C, const float* gamma, const float* mean,
@@ -343,7 +358,13 @@ static void launch_bwd_finalize(const float* part, int P, int M, int C, const fl
 #define DTFK_FIN(FC)                                                                                                   \
   hipLaunchKernelGGL((bn_bwd_finalize<FC>), dim3((C + FC - 1) / FC), dim3(1024), 0, st, part, P, M, C, gamma, mean, \
                      invstd, dgamma, dbeta, coef, accum)
-  if (C >= 1024) DTFK_FIN(16); else if (C >= 512) DTFK_FIN(8); else DTFK_FIN(4);
+  switch (finalize_fc(P, C)) {
+    case 16: DTFK_FIN(16); break;
+    case 8: DTFK_FIN(8); break;
+    case 4: DTFK_FIN(4); break;
+    case 2: DTFK_FIN(2); break;
+    default: DTFK_FIN(1);
+  }
 #undef DTFK_FIN
 }
 static unsigned ew_grid(long long n8) {

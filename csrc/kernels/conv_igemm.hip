@@ -22,13 +22,23 @@
 //    (chunk ^ ((row >> 1) & 7)) that puts the 16 lanes of a ds_read_b128 group
 //    on 16 distinct slots of a bank row (MI355X_MICROARCH.md).
 //  * Epilogue through LDS: the bf16 tile is written back as whole 16-B row
-//    segments; with `part` the workgroup also writes per-channel sums of y and
+//    segments.  EPI 1: the workgroup also writes per-channel sums of y and
 //    y^2 over its valid rows -- the [2, P, K] partials bn_finalize
 //    (csrc/kernels/bn.hip) reduces, so the BatchNorm after this conv skips its
-//    statistics pass over y.
+//    statistics pass over y.  EPI 2 / 3 (this conv computes an input gradient
+//    that feeds a BatchNorm (+ residual) + ReLU backward): y is stored
+//    ReLU-masked and the partials are that BN backward's sums of g and
+//    g * x_hat (EPI 3 first adds the residual branch's gradient already in y).
+//    The HBM operands of the epilogue are loaded while the last K step
+//    multiplies (with the operands' first loads for <= 2 steps).
+//  * ONE (a 1x1 over 64 channels: a single K step): one operand buffer and the
+//    LDS sized for the epilogue -- three workgroups per CU instead of two.
 //
-// The input gradient of a stride-1 3x3 conv is the same convolution of dy with
-// the flipped, channel-transposed filter (conv_igemm_wflip builds it).
+// The input gradient of a stride-1 conv is the same convolution of dy with the
+// flipped, channel-transposed filter (wflip; wflip_multi re-flips every conv's
+// filter in one launch after an optimizer step, ops/conv.py _flipped).  The
+// weight gradient (conv_wgrad) is split over pixels into fp32 slabs summed in
+// split order by wgrad_reduce (profiles/conv_wgrad_sweep_r5.txt).
 #include "common.h"
 #include <cstdlib>
 
@@ -53,8 +63,17 @@ __device__ __forceinline__ int swz(int row, int ch) { return ch ^ ((row >> 1) & 
 // bnx * scale + shift + bnres), with accum: the output gradient is the
 // convolution plus the residual branch's gradient already in y (the fold of
 // ops/conv.py), so g is formed from the complete gradient.
+// ONE: a single 64-channel K step (1x1 over C = 64): one operand buffer, the
+// LDS sized for the epilogue, three workgroups per CU instead of two -- the
+// load -> MFMA -> epilogue chain of such a tile is latency bound.
 template <int KS, int BN, int EPI>
-__global__ __launch_bounds__(NTHR, 2) void conv_fwd(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
+constexpr int fwd_lds_bytes(bool one) {
+  constexpr int BUF = BM * BK * 2 + BN * BK * 2, PITCH = BN * 2 + 16;
+  constexpr int EPI_B = ((BM * PITCH + 15) & ~15) + (EPI >= 2 ? NTHR * 16 * 4 : (EPI == 1 ? 2 * NTHR * 4 : 0));
+  return one ? (BUF > EPI_B ? BUF : EPI_B) : 2 * BUF;
+}
+template <int KS, int BN, int EPI, bool ONE = false>
+__global__ __launch_bounds__(NTHR, ONE ? 3 : 2) void conv_fwd(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
                                                     uint16_t* __restrict__ y, float* __restrict__ part, int N,
                                                     int H, int W, int C, int K, int Ho, int Wo, int stride,
                                                     long long xbytes, int accum, const uint16_t* __restrict__ bnx,
@@ -66,7 +85,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv_fwd(const uint16_t* __restrict__
   constexpr int WM = BM / 2, WN = BN / 2;          // per-wave output block
   constexpr int TM = WM / 16, TN = WN / 16;        // 16x16 tiles per wave
   constexpr int NB = BN * 8 / NTHR;                // B chunks per thread per step
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * BUF];
+  __shared__ __attribute__((aligned(16))) uint8_t smem[fwd_lds_bytes<KS, BN, EPI>(ONE)];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wm = wv >> 1, wn = wv & 1;
   const long long M = (long long)N * Ho * Wo;
@@ -171,7 +190,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv_fwd(const uint16_t* __restrict__
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
   load(0, I0{});
-  if (nsteps > 1) load(1, I1{});
+  if (!ONE && nsteps > 1) load(1, I1{});
   if (early) prefetch();
   store(I0{});
   __syncthreads();
@@ -182,8 +201,8 @@ __global__ __launch_bounds__(NTHR, 2) void conv_fwd(const uint16_t* __restrict__
   auto body = [&](int step, auto pc) {
     constexpr int P = decltype(pc)::value;
     using Q = std::integral_constant<int, P ^ 1>;
-    if (step + 1 < nsteps) store(Q{});
-    if (step + 2 < nsteps) load(step + 2, pc);
+    if (!ONE && step + 1 < nsteps) store(Q{});
+    if (!ONE && step + 2 < nsteps) load(step + 2, pc);
     if (step + 1 == nsteps && !early) prefetch();
     const uint8_t* A = smem + P * BUF;
     const uint8_t* Bs = A + A_BYTES;
@@ -207,14 +226,16 @@ __global__ __launch_bounds__(NTHR, 2) void conv_fwd(const uint16_t* __restrict__
     }
     __syncthreads();
   };
-  for (int step = 0; step < nsteps; step += 2) {
+  if constexpr (ONE) {
+    body(0, I0{});
+  } else for (int step = 0; step < nsteps; step += 2) {
     body(step, I0{});
     if (step + 1 < nsteps) body(step + 1, I1{});
   }
 
   // ---- epilogue: bf16 tile through LDS [BM][BN] (row pitch BN*2 + 16 B)
   constexpr int PITCH = BN * 2 + 16;
-  static_assert(BM * PITCH <= 2 * BUF, "epilogue tile fits the operand buffers");
+  static_assert(BM * PITCH <= (int)sizeof(smem), "epilogue tile fits the operand buffers");
   uint8_t* E = smem;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -284,7 +305,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv_fwd(const uint16_t* __restrict__
   if constexpr (BNB) {
     // the NTHR / CPR threads of each chunk column -> per-channel tile sums (fixed order)
     float* red = reinterpret_cast<float*>(smem + ((BM * PITCH + 15) & ~15));   // behind the tile
-    static_assert(((BM * PITCH + 15) & ~15) + NTHR * 16 * 4 <= 2 * BUF, "BN-backward scratch fits");
+    static_assert(((BM * PITCH + 15) & ~15) + NTHR * 16 * 4 <= (int)sizeof(smem), "BN-backward scratch fits");
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       red[tid * 16 + q] = sg[q];
@@ -315,7 +336,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv_fwd(const uint16_t* __restrict__
       q += v * v;
     }
     float* red = reinterpret_cast<float*>(smem + ((BM * PITCH + 15) & ~15));   // behind the tile
-    static_assert(((BM * PITCH + 15) & ~15) + 2 * NTHR * 4 <= 2 * BUF, "stats scratch fits");
+    static_assert(((BM * PITCH + 15) & ~15) + 2 * NTHR * 4 <= (int)sizeof(smem), "stats scratch fits");
     red[tid] = s;
     red[NTHR + tid] = q;
     __syncthreads();
@@ -677,9 +698,20 @@ hipError_t dtfk_conv_fwd(const void* x, const void* w, void* y, float* part, int
   const int epi = bnx != nullptr ? (bnres != nullptr ? 3 : 2) : (part != nullptr ? 1 : 0);
   auto bx = static_cast<const uint16_t*>(bnx);
   auto br = static_cast<const uint16_t*>(bnres);
-#define DTFK_CF(KSV, BNV, EP)                                                                                     \
-  hipLaunchKernelGGL((conv_fwd<KSV, BNV, EP>), grid, dim3(NTHR), 0, stream, xs, ws, ys, part, N, H, W, C, K, Ho, Wo, \
-                     stride, xbytes, accum, bx, bnst, br)
+  // one 64-channel K step: the single-buffer, three-workgroups-per-CU variant
+  const bool one = ks == 1 && C == BK;
+#define DTFK_CF(KSV, BNV, EP)                                                                                        \
+  if constexpr (KSV == 1) {                                                                                         \
+    if (one)                                                                                                        \
+      hipLaunchKernelGGL((conv_fwd<KSV, BNV, EP, true>), grid, dim3(NTHR), 0, stream, xs, ws, ys, part, N, H, W, C,  \
+                         K, Ho, Wo, stride, xbytes, accum, bx, bnst, br);                                           \
+    else                                                                                                            \
+      hipLaunchKernelGGL((conv_fwd<KSV, BNV, EP>), grid, dim3(NTHR), 0, stream, xs, ws, ys, part, N, H, W, C, K, Ho, \
+                         Wo, stride, xbytes, accum, bx, bnst, br);                                                  \
+  } else {                                                                                                          \
+    hipLaunchKernelGGL((conv_fwd<KSV, BNV, EP>), grid, dim3(NTHR), 0, stream, xs, ws, ys, part, N, H, W, C, K, Ho,   \
+                       Wo, stride, xbytes, accum, bx, bnst, br);                                                    \
+  }
 #define DTFK_CF_EPI(KSV, BNV)                                                                               \
   switch (epi) {                                                                                            \
     case 3: DTFK_CF(KSV, BNV, 3); break;                                                                    \
@@ -730,12 +762,20 @@ hipError_t dtfk_conv3x3_wflip(const void* w, void* wt, int K, int C, hipStream_t
 // and the fp32 workspace (floats) its slabs need (0 with one split).  About two
 // workgroups per CU in total (both resident at once) and at least 8 steps of 64
 // pixels per split: each extra split costs a 64 KB slab write + read.
+// filter-column tile of the weight gradient: 128 wide when it divides 9C / C,
+// or when the last, partial tile wastes at most 1/8 (3x3 over 64 channels:
+// 576 columns = 4.5 tiles -- the 64-wide tiling ran 1.2x MIOpen's time)
+static int wgrad_bnw(int NC) {
+  if (NC % 128 == 0) return 128;
+  return (NC >= 512 && ((NC + 127) / 128) * 128 - NC <= NC / 8) ? 128 : 64;
+}
+
 long long dtfk_conv_wgrad_plan(int N, int H, int W, int C, int K, int stride, int ks, int* splits_out, int* sps_out) {
   using namespace dtfk::cig;
   const long long P = (long long)N * conv_out(H, stride, ks) * conv_out(W, stride, ks);
   const int NC = ks * ks * C;
   const int bm = K % 128 == 0 ? 128 : 64;
-  const int bnw = NC % 128 == 0 ? 128 : 64;
+  const int bnw = wgrad_bnw(NC);
   const long long tiles = (long long)(K / bm) * ((NC + bnw - 1) / bnw);
   const long long steps = (P + 63) / 64;
   // target workgroups: 512 (two per CU); 256 for the few-tile 1x1 gradients
@@ -777,7 +817,7 @@ hipError_t dtfk_conv_wgrad(const void* dy, const void* x, float* dw, float* ws, 
   if (P * K * 2 >= 0x7ffffff0LL) return hipErrorInvalidValue;
   const int NC = ks * ks * C;
   const int bm = K % 128 == 0 ? 128 : 64;
-  const int bnw = NC % 128 == 0 ? 128 : 64;
+  const int bnw = wgrad_bnw(NC);
   int splits = 1, sps = 1;
   const long long wsn = dtfk_conv_wgrad_plan(N, H, W, C, K, stride, ks, &splits, &sps);
   if (wsn > 0 && ws == nullptr) return hipErrorInvalidValue;

@@ -165,7 +165,11 @@ __global__ __launch_bounds__(NTHR, ONE ? 3 : 2) void conv_fwd(const uint16_t* __
   // EPI 3 on 64-wide tiles also prefetches the folded gradient and the residual
   // (on 128-wide tiles those registers would spill: loaded in the store loop)
   constexpr bool PRE3 = BNR && BN == 64;
-  u32x4 pre[EIT], pre_y[PRE3 ? EIT : 1], pre_r[PRE3 ? EIT : 1];
+  // ... and on 128-wide tiles right after the K loop (the operand registers are
+  // dead by then), ahead of the accumulator write-out and its barrier
+  // (not in the single-step variant: its 3-workgroup register budget spills)
+  constexpr bool POST3 = BNR && !PRE3 && !ONE;
+  u32x4 pre[EIT], pre_y[PRE3 || POST3 ? EIT : 1], pre_r[PRE3 || POST3 ? EIT : 1];
   auto prefetch = [&]() {
     if (!(BNB || accum)) return;
     const uint16_t* src = BNB ? bnx : y;
@@ -233,6 +237,19 @@ __global__ __launch_bounds__(NTHR, ONE ? 3 : 2) void conv_fwd(const uint16_t* __
     if (step + 1 < nsteps) body(step + 1, I1{});
   }
 
+  if constexpr (POST3) {
+#pragma unroll
+    for (int it = 0; it < EIT; ++it) {
+      const int t = tid + it * NTHR;
+      const long long m = m0 + t / CPR;
+      if (m < M) {
+        const long long e = m * K + k0 + 8 * (t % CPR);
+        pre_y[it] = *reinterpret_cast<const u32x4*>(y + e);
+        pre_r[it] = *reinterpret_cast<const u32x4*>(bnres + e);
+      }
+    }
+  }
+
   // ---- epilogue: bf16 tile through LDS [BM][BN] (row pitch BN*2 + 16 B)
   constexpr int PITCH = BN * 2 + 16;
   static_assert(BM * PITCH <= (int)sizeof(smem), "epilogue tile fits the operand buffers");
@@ -275,8 +292,9 @@ __global__ __launch_bounds__(NTHR, ONE ? 3 : 2) void conv_fwd(const uint16_t* __
         u32x4 ro = {0u, 0u, 0u, 0u};
         if constexpr (BNR) {   // the complete gradient: conv + the folded residual gradient (rounded as stored)
           const long long e = m * K + k0 + 8 * ch;
-          const u32x4 o = PRE3 ? pre_y[PRE3 ? it : 0] : *reinterpret_cast<const u32x4*>(y + e);
-          ro = PRE3 ? pre_r[PRE3 ? it : 0] : *reinterpret_cast<const u32x4*>(bnres + e);
+          constexpr bool HELD = PRE3 || POST3;
+          const u32x4 o = HELD ? pre_y[HELD ? it : 0] : *reinterpret_cast<const u32x4*>(y + e);
+          ro = HELD ? pre_r[HELD ? it : 0] : *reinterpret_cast<const u32x4*>(bnres + e);
 #pragma unroll
           for (int q = 0; q < 4; ++q)
             v[q] = pack2bf(bf2f(v[q] & 0xffff) + bf2f(o[q] & 0xffff), bf2f(v[q] >> 16) + bf2f(o[q] >> 16));

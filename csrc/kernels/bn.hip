@@ -103,7 +103,8 @@ template <int FC>
 __device__ __forceinline__ void sum_partials(const float* __restrict__ part, int P, int C, int c, int lane, int g,
                                              double& s0, double& s1) {
   constexpr int FG = 1024 / FC;
-  __shared__ double red[2][FG][FC];
+  static_assert(FC <= 64 && 64 % FC == 0, "channels per block divide a wave");
+  __shared__ double red[2][16][FC];
   double a = 0.0, b = 0.0;
   if (c < C) {
     // four rows per trip, all eight loads issued unconditionally (rows past P
@@ -124,19 +125,30 @@ __device__ __forceinline__ void sum_partials(const float* __restrict__ part, int
       b += ((double)yv[0] + yv[1]) + ((double)yv[2] + yv[3]);
     }
   }
-  red[0][g][lane] = a;
-  red[1][g][lane] = b;
-  __syncthreads();
+  // row groups of a wave combined with xor shuffles (fixed pairing), then the
+  // 16 waves' sums in wave order through LDS: one barrier instead of a
+  // log2(FG)-level LDS tree (deterministic either way)
 #pragma unroll
-  for (int st = FG / 2; st > 0; st >>= 1) {
-    if (g < st) {
-      red[0][g][lane] += red[0][g + st][lane];
-      red[1][g][lane] += red[1][g + st][lane];
-    }
-    __syncthreads();
+  for (int m = FC; m < 64; m <<= 1) {
+    a += __shfl_xor(a, m);
+    b += __shfl_xor(b, m);
   }
-  s0 = red[0][0][lane];
-  s1 = red[1][0][lane];
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) < FC) {
+    red[0][wave][lane] = a;
+    red[1][wave][lane] = b;
+  }
+  __syncthreads();
+  double x = 0.0, y = 0.0;
+  if (g == 0) {
+#pragma unroll
+    for (int w = 0; w < 16; ++w) {
+      x += red[0][w][lane];
+      y += red[1][w][lane];
+    }
+  }
+  s0 = x;
+  s1 = y;
 }
 
 // mean/var (double), running stats, scale = gamma*invstd, shift = beta - mean*scale.

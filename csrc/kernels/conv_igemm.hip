@@ -78,7 +78,7 @@ __global__ __launch_bounds__(NTHR, ONE ? 3 : 2) void conv_fwd(const uint16_t* __
                                                     int H, int W, int C, int K, int Ho, int Wo, int stride,
                                                     long long xbytes, int accum, const uint16_t* __restrict__ bnx,
                                                     const float* __restrict__ bnst,
-                                                    const uint16_t* __restrict__ bnres) {
+                                                    const uint16_t* __restrict__ bnres, int xcd) {
   constexpr bool STATS = EPI == 1, BNB = EPI >= 2, BNR = EPI == 3;
   constexpr int PAD = KS / 2, TAPS = KS * KS;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, BUF = A_BYTES + B_BYTES;
@@ -89,8 +89,20 @@ __global__ __launch_bounds__(NTHR, ONE ? 3 : 2) void conv_fwd(const uint16_t* __
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wm = wv >> 1, wn = wv & 1;
   const long long M = (long long)N * Ho * Wo;
-  const long long m0 = (long long)blockIdx.x * BM;
-  const int k0 = blockIdx.y * BN;
+  // xcd: the channel tiles of one pixel tile (they share its A rows) on one XCD,
+  // consecutive pixel tiles dealt over the 8 XCDs (1-D grid, ids round robin)
+  int bx, by;
+  if (xcd) {
+    const int nt = K / BN, L = blockIdx.x, i = L >> 3;
+    bx = (i / nt) * 8 + (L & 7);
+    by = i % nt;
+    if ((long long)bx * BM >= (long long)N * Ho * Wo) return;   // grid rounded up to 8 pixel tiles
+  } else {
+    bx = blockIdx.x;
+    by = blockIdx.y;
+  }
+  const long long m0 = (long long)bx * BM;
+  const int k0 = by * BN;
 
   // this thread's 4 A rows (pixel coordinates fixed over the K loop) and chunk
   const int ach = tid & 7;
@@ -337,9 +349,9 @@ __global__ __launch_bounds__(NTHR, ONE ? 3 : 2) void conv_fwd(const uint16_t* __
         a += red[j * 16 + q];
         b += red[j * 16 + 8 + q];
       }
-      const int P = gridDim.x;
-      part[((size_t)0 * P + blockIdx.x) * K + k0 + tid] = a;
-      part[((size_t)1 * P + blockIdx.x) * K + k0 + tid] = b;
+      const int P = (int)((M + BM - 1) / BM);
+      part[((size_t)0 * P + bx) * K + k0 + tid] = a;
+      part[((size_t)1 * P + bx) * K + k0 + tid] = b;
     }
   }
   if constexpr (STATS) {
@@ -364,9 +376,9 @@ __global__ __launch_bounds__(NTHR, ONE ? 3 : 2) void conv_fwd(const uint16_t* __
         s += red[k * BN + col];
         q += red[NTHR + k * BN + col];
       }
-      const int P = gridDim.x;
-      part[((size_t)0 * P + blockIdx.x) * K + k0 + col] = s;
-      part[((size_t)1 * P + blockIdx.x) * K + k0 + col] = q;
+      const int P = (int)((M + BM - 1) / BM);
+      part[((size_t)0 * P + bx) * K + k0 + col] = s;
+      part[((size_t)1 * P + bx) * K + k0 + col] = q;
     }
   }
 }
@@ -411,7 +423,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv_wgrad(const uint16_t* __restrict
                                                          float* __restrict__ dw, int N, int H, int W, int C, int K,
                                                          int Ho, int Wo, int stride, long long xbytes,
                                                          int steps_per_split, int kcrs, float* __restrict__ ws,
-                                                         long long slab) {
+                                                         long long slab, int tiles_x, int tiles_y, int xcd) {
   constexpr int PAD = KS / 2, TAPS = KS * KS;
   constexpr int PK = 64;                                        // pixels per step
   constexpr int A_BYTES = PK * BMW * 2, B_BYTES = PK * BNW * 2, BUF = A_BYTES + B_BYTES;
@@ -422,10 +434,22 @@ __global__ __launch_bounds__(NTHR, 2) void conv_wgrad(const uint16_t* __restrict
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wm = wv >> 1, wn = wv & 1;
   const long long P = (long long)N * Ho * Wo;
-  const int m0 = blockIdx.x * BMW;            // output-channel tile
-  const int n0 = blockIdx.y * BNW;            // filter-column tile over (r, s, c)
+  // 1-D grid of splits x tiles.  xcd: the tiles of one pixel split share its dy / x
+  // rows, so every workgroup of split z runs on XCD z % 8 (workgroups are dealt to
+  // the XCDs round robin by id) and those rows come from one L2
+  int bx, by, bz;
+  {
+    const int T = tiles_x * tiles_y, L = blockIdx.x;
+    const int logical = xcd ? ((L >> 3) / T * 8 + (L & 7)) * T + (L >> 3) % T : L;
+    bz = logical / T;
+    const int t = logical - bz * T;
+    bx = t % tiles_x;
+    by = t / tiles_x;
+  }
+  const int m0 = bx * BMW;                    // output-channel tile
+  const int n0 = by * BNW;                    // filter-column tile over (r, s, c)
   const int NC = TAPS * C;
-  const long long pb = (long long)blockIdx.z * steps_per_split * PK;
+  const long long pb = (long long)bz * steps_per_split * PK;
   long long pe = pb + (long long)steps_per_split * PK;
   if (pe > P) pe = P;
   const int nsteps = pb < pe ? (int)((pe - pb + PK - 1) / PK) : 0;
@@ -548,7 +572,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv_wgrad(const uint16_t* __restrict
   const int fr = lane & 15, fk = lane >> 4;
   if (ws != nullptr) {
     // slab of split z, tile (x, y): [wave][TM][TN][64 lanes] f32x4 (zeros for an empty split)
-    float* sl = ws + blockIdx.z * slab + ((long long)blockIdx.y * gridDim.x + blockIdx.x) * (BMW * BNW);
+    float* sl = ws + bz * slab + ((long long)by * tiles_x + bx) * (BMW * BNW);
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -704,7 +728,14 @@ hipError_t dtfk_conv_fwd(const void* x, const void* w, void* y, float* part, int
     bn = (K % 128 == 0 && t128 >= 256) ? 128 : 64;
   }
   if (K % bn) return hipErrorInvalidValue;
-  const dim3 grid((unsigned)((M + BM - 1) / BM), (unsigned)(K / bn));
+  // DTF_CONV_FWD_XCD=1: the channel tiles of a pixel tile on one XCD (measured
+  // neutral on ResNet-50: 9,275 vs 9,250-9,280 img/s; profiles/conv_wgrad_xcd_r5.txt)
+  static const int fwd_xcd = [] {
+    const char* e = getenv("DTF_CONV_FWD_XCD");
+    return (e && e[0] == '1') ? 1 : 0;
+  }();
+  const long long mt = (M + BM - 1) / BM;
+  const dim3 grid = fwd_xcd ? dim3((unsigned)((mt + 7) / 8 * 8 * (K / bn))) : dim3((unsigned)mt, (unsigned)(K / bn));
   const long long xbytes = (long long)N * H * W * C * 2;
   auto xs = static_cast<const uint16_t*>(x);
   auto ws = static_cast<const uint16_t*>(w);
@@ -722,13 +753,13 @@ hipError_t dtfk_conv_fwd(const void* x, const void* w, void* y, float* part, int
   if constexpr (KSV == 1) {                                                                                         \
     if (one)                                                                                                        \
       hipLaunchKernelGGL((conv_fwd<KSV, BNV, EP, true>), grid, dim3(NTHR), 0, stream, xs, ws, ys, part, N, H, W, C,  \
-                         K, Ho, Wo, stride, xbytes, accum, bx, bnst, br);                                           \
+                         K, Ho, Wo, stride, xbytes, accum, bx, bnst, br, fwd_xcd);                                  \
     else                                                                                                            \
       hipLaunchKernelGGL((conv_fwd<KSV, BNV, EP>), grid, dim3(NTHR), 0, stream, xs, ws, ys, part, N, H, W, C, K, Ho, \
-                         Wo, stride, xbytes, accum, bx, bnst, br);                                                  \
+                         Wo, stride, xbytes, accum, bx, bnst, br, fwd_xcd);                                         \
   } else {                                                                                                          \
     hipLaunchKernelGGL((conv_fwd<KSV, BNV, EP>), grid, dim3(NTHR), 0, stream, xs, ws, ys, part, N, H, W, C, K, Ho,   \
-                       Wo, stride, xbytes, accum, bx, bnst, br);                                                    \
+                       Wo, stride, xbytes, accum, bx, bnst, br, fwd_xcd);                                           \
   }
 #define DTFK_CF_EPI(KSV, BNV)                                                                               \
   switch (epi) {                                                                                            \
@@ -780,6 +811,19 @@ hipError_t dtfk_conv3x3_wflip(const void* w, void* wt, int K, int C, hipStream_t
 // and the fp32 workspace (floats) its slabs need (0 with one split).  About two
 // workgroups per CU in total (both resident at once) and at least 8 steps of 64
 // pixels per split: each extra split costs a 64 KB slab write + read.
+// XCD-aware weight-gradient dispatch for 8-16 tiles per split (3x3 over 128
+// channels: 73 -> 55 us; 1x1 at 14x14: 37 -> 35 us); with fewer tiles the
+// rounded-up split count, with more the one-XCD-per-split concentration lost
+// (3x3 over 256 / 512 channels: 61 -> 75 us; profiles/conv_wgrad_xcd_r5.txt).
+// DTF_CONV_XCD=0: plain split-major order everywhere.
+static bool wgrad_xcd(long long tiles) {
+  static const bool on = [] {
+    const char* e = getenv("DTF_CONV_XCD");
+    return !(e && e[0] == '0');
+  }();
+  return on && tiles >= 8 && tiles <= 16;
+}
+
 // filter-column tile of the weight gradient: 128 wide when it divides 9C / C,
 // or when the last, partial tile wastes at most 1/8 (3x3 over 64 channels:
 // 576 columns = 4.5 tiles -- the 64-wide tiling ran 1.2x MIOpen's time)
@@ -813,8 +857,14 @@ long long dtfk_conv_wgrad_plan(int N, int H, int W, int C, int K, int stride, in
   long long splits = (target + tiles - 1) / tiles;
   if (splits > steps / minsteps) splits = steps / minsteps;
   if (splits < 1) splits = 1;
-  const int sps = (int)((steps + splits - 1) / splits);
+  int sps = (int)((steps + splits - 1) / splits);
   splits = (steps + sps - 1) / sps;
+  // XCD-aware dispatch (conv_wgrad): a multiple of 8 splits, each XCD its own
+  // splits (trailing splits may be empty: they write zero slabs)
+  if (wgrad_xcd(tiles) && splits >= 8) {
+    splits = (splits + 7) / 8 * 8;
+    sps = (int)((steps + splits - 1) / splits);
+  }
   if (splits_out) *splits_out = (int)splits;
   if (sps_out) *sps_out = sps;
   return splits > 1 ? splits * tiles * bm * bnw : 0;
@@ -841,7 +891,9 @@ hipError_t dtfk_conv_wgrad(const void* dy, const void* x, float* dw, float* ws, 
   if (wsn > 0 && ws == nullptr) return hipErrorInvalidValue;
   float* wsp = wsn > 0 ? ws : nullptr;
   const long long slab = wsn > 0 ? wsn / splits : 0;
-  const dim3 grid((unsigned)(K / bm), (unsigned)((NC + bnw - 1) / bnw), (unsigned)splits);
+  const int tiles_x = K / bm, tiles_y = (NC + bnw - 1) / bnw;
+  const dim3 grid((unsigned)(tiles_x * tiles_y * splits));
+  const int xcd = (wgrad_xcd((long long)tiles_x * tiles_y) && splits >= 8 && splits % 8 == 0) ? 1 : 0;
   const long long xbytes = (long long)N * H * W * C * 2;
   // reduce threads per output: up to 16, ~128K threads in all
   int G = 1;
@@ -851,10 +903,10 @@ hipError_t dtfk_conv_wgrad(const void* dy, const void* x, float* dw, float* ws, 
 #define DTFK_WG(KSV, A, B)                                                                                         \
   do {                                                                                                             \
     hipLaunchKernelGGL((conv_wgrad<KSV, A, B>), grid, dim3(NTHR), 0, stream, d, xs, dw, N, H, W, C, K, Ho, Wo,     \
-                       stride, xbytes, sps, kcrs, wsp, slab);                                                      \
+                       stride, xbytes, sps, kcrs, wsp, slab, tiles_x, tiles_y, xcd);                               \
     if (wsp)                                                                                                       \
       hipLaunchKernelGGL((wgrad_reduce<KSV, A, B>), dim3((unsigned)((slab / 4 + 256 / G - 1) / (256 / G))),        \
-                         dim3(256), 0, stream, wsp, splits, slab, dw, C, (int)grid.x, kcrs, G);                    \
+                         dim3(256), 0, stream, wsp, splits, slab, dw, C, tiles_x, kcrs, G);                        \
   } while (0)
 #define DTFK_WG_T(KSV)                                 \
   if (bm == 128 && bnw == 128) DTFK_WG(KSV, 128, 128); \

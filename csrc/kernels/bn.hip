@@ -16,6 +16,7 @@
 // bf16x8 accesses), C % 8 == 0.  Partial buffers are [P, C] fp32 and are
 // reduced in a fixed order (deterministic).
 #include "common.h"
+#include <cstdlib>
 
 namespace dtfk {
 namespace bn {
@@ -379,9 +380,15 @@ static void launch_bwd_finalize(const float* part, int P, int M, int C, const fl
   }
 #undef DTFK_FIN
 }
+// grid of the elementwise passes: one 8-channel chunk per thread, capped at
+// DTF_BN_EW_CAP blocks (default 16384; beyond it the threads grid-stride)
 static unsigned ew_grid(long long n8) {
+  static const long long cap = [] {
+    const char* e = getenv("DTF_BN_EW_CAP");
+    return e ? atoll(e) : 16384LL;
+  }();
   long long g = (n8 + 255) / 256;
-  return (unsigned)(g > 16384 ? 16384 : (g < 1 ? 1 : g));
+  return (unsigned)(g > cap ? cap : (g < 1 ? 1 : g));
 }
 
 extern "C" {

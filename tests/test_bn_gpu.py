@@ -71,3 +71,41 @@ def test_resnet50_fused_bn_step_trains(native):
         losses.append(float(l))
     assert all(l == l for l in losses)          # no NaN
     assert losses[-1] < losses[0]
+
+
+def test_bn_bwd_parts_fused_launch_many_shapes(native):
+    """bn_bwd_parts (finalize + apply in one launch, blocks synchronised by a
+    rotating pool of 256 monotonic counters) called 600 times with channel
+    counts alternating 64 / 256 / 2048 -- every slot of the pool is reused with a
+    different number of finalize blocks -- against the fp32 formula."""
+    C_ = native
+    cl = torch.channels_last
+    cases = []
+    for C in (64, 256, 2048):
+        g = torch.Generator(device="cuda").manual_seed(C)
+        N, H = 2, 8
+        M = N * H * H
+        x = torch.randn(N, C, H, H, device="cuda", generator=g).bfloat16().contiguous(memory_format=cl)
+        gin = torch.randn(N, C, H, H, device="cuda", generator=g).bfloat16().contiguous(memory_format=cl)
+        gamma = torch.rand(C, device="cuda", generator=g) + 0.5
+        xf = x.float().permute(0, 2, 3, 1).reshape(M, C)
+        gf = gin.float().permute(0, 2, 3, 1).reshape(M, C)
+        mean, var = xf.mean(0), xf.var(0, unbiased=False)
+        invstd = (var + 1e-5).rsqrt()
+        stats = torch.cat([mean, invstd, gamma * invstd, -mean * gamma * invstd])
+        xhat = (xf - mean) * invstd
+        part = torch.stack([gf.sum(0), (gf * xhat).sum(0)]).reshape(2, 1, C).contiguous()
+        dbeta, dgamma = gf.sum(0), (gf * xhat).sum(0)
+        ref = gamma * invstd * (gf - dbeta / M - xhat * dgamma / M)
+        cases.append((C, x, gin, gamma, stats, part, ref, dgamma, dbeta, M))
+    for it in range(600):
+        C, x, gin, gamma, stats, part, ref, rdg, rdb, M = cases[it % 3]
+        dx = torch.empty_like(x)
+        coef = torch.empty(3 * C, device="cuda")
+        dg, db = torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
+        C_.bn_bwd_parts(gin, x, gamma, stats, part, 1, coef, dx, dg, db, False)
+        if it % 97 == 0 or it >= 597:
+            got = dx.float().permute(0, 2, 3, 1).reshape(M, C)
+            torch.testing.assert_close(got, ref, rtol=2e-2, atol=2e-2)
+            torch.testing.assert_close(dg, rdg, rtol=1e-4, atol=1e-3)
+            torch.testing.assert_close(db, rdb, rtol=1e-4, atol=1e-3)

@@ -36,6 +36,28 @@ _DGELU = _GELU_EPI != "0"
 _GELU_AUX = _GELU_EPI not in ("0", "bwd")
 _choice: dict = {}
 _timings: dict = {}
+# Fixed per-shape engine table for BERT-base at B = 128, S = 128 (T = 16384
+# token rows; DTF_BIG_GEMM_TABLE=0: time every shape): the choice set of the
+# fastest measured run (8,370-8,393 seq/s, profiles/bert_gemm_margin_ab_r5.txt).
+# The one-time timing flips the near-tie products from box to box (FFN2 weight
+# gradient, QKV / FFN1 input gradients: in-tree within 5 % on the microbench,
+# slower in the step), and the step with them moved ran 7,869-8,096 seq/s
+# (profiles/bert_base_b128_r5_*.json).  Shapes not listed are timed.
+_TABLE_ON = os.environ.get("DTF_BIG_GEMM_TABLE", "1") != "0"
+_TABLE = {
+    ("fwd", 16384, 2304, 768): True, ("fwd", 16384, 768, 768): True, ("fwd", 16384, 3072, 768): True,
+    ("gelu_aux", 16384, 3072, 768): True, ("dgelu", 16384, 3072, 768): True,
+    ("dx", 16384, 768, 768): True, ("dw", 768, 3072, 16384): True, ("dw", 2304, 768, 16384): True,
+    ("fwd", 16384, 768, 3072): False, ("dx", 16384, 3072, 768): False, ("dx", 16384, 768, 3072): False,
+    ("dx", 16384, 768, 2304): False, ("dw", 3072, 768, 16384): False, ("dw", 768, 768, 16384): False,
+}
+
+
+def _fixed(key):
+    """The table's engine for `key` under 'auto' (None: not listed / table off)."""
+    if not _TABLE_ON or _POLICY != "auto":
+        return None
+    return _TABLE.get(key)
 
 
 def _C():
@@ -94,6 +116,8 @@ def use_native(role: str, M: int, N: int, K: int, dev) -> bool:
         return True
     key = (role, M, N, K)
     hit = _choice.get(key)
+    if hit is None and _fixed(key) is not None:
+        hit = _choice[key] = _fixed(key)
     if hit is None:
         if torch.cuda.is_current_stream_capturing():
             return False
@@ -122,6 +146,8 @@ def use_dgelu(M: int, N: int, K: int, dev) -> bool:
         return True
     key = ("dgelu", M, N, K)
     hit = _choice.get(key)
+    if hit is None and _fixed(key) is not None:
+        hit = _choice[key] = _fixed(key)
     if hit is None:
         if torch.cuda.is_current_stream_capturing():
             return False
@@ -159,6 +185,8 @@ def use_gelu_aux(M: int, N: int, K: int, dev) -> bool:
         return True
     key = ("gelu_aux", M, N, K)
     hit = _choice.get(key)
+    if hit is None and _fixed(key) is not None:
+        hit = _choice[key] = _fixed(key)
     if hit is None:
         if torch.cuda.is_current_stream_capturing():
             return False

@@ -537,8 +537,15 @@ class MLPStepPlan(_PlanBase):
         shape = (B, 784)
 
         prun, out, u8t, f32t, n = rp.plan.run_u8, rp.out, np.dtype(np.uint8), np.dtype(np.float32), B * C
+        live = _resident_mod()._LIVE
 
         def fast(feed):
+            # this runner belongs to ONE resident handle: once the plan was rebuilt
+            # (another batch shape stopped `rp` and made a new engine) or any other
+            # engine is live, take the full path -- relaunching `rp` next to a live
+            # engine would train the same variables from two register copies
+            if self._rplan is not rp or (live and (len(live) > 1 or live[0] is not rp)):
+                return None
             fx, fy = feed.get(xph), feed.get(yph)
             u8 = getattr(fx, "u8", None)
             if (u8 is None or not isinstance(fx, nd) or fx.flags.writeable or fx.shape != shape
@@ -552,6 +559,7 @@ class MLPStepPlan(_PlanBase):
             self.steps += 1
             self.resident_steps += 1
             return [None if k < 0 else out[k] for k in kinds]
+        fast.stale = lambda: self._rplan is not rp       # try_lower replaces a stale runner
         return fast
 
     def _needs(self, flat, gs_var, gstep):
@@ -643,6 +651,10 @@ class SparseLRStepPlan(_PlanBase):
         self._stage = None
         self._nplan = None            # one worker: csrc/bind_sparse.cpp SparseLRPlan
         self._fused_env = os.environ.get("DTF_SLR_FUSED", "1") != "0"
+        # the one-GPU kernels skip (and count) feature ids outside [0, F); TF's
+        # gather raises InvalidArgument.  The count is read back every
+        # DTF_SPARSE_ID_CHECK runs (0: never) and a nonzero count raises here.
+        self._id_check = int(os.environ.get("DTF_SPARSE_ID_CHECK", "256"))
         self.steps = 0
 
     @staticmethod
@@ -744,6 +756,8 @@ class SparseLRStepPlan(_PlanBase):
         if not self._nplan.run(fy, fi, ff, fv, float(opt._lr_value())):
             return False
         opt._steps += 1
+        if self._id_check and opt._steps % self._id_check == 0:
+            self.check_ids()
         _debug_mod().fault_point(opt._steps, 0)
         if gs_var is not None and not self._nplan_gs:
             with torch.no_grad():
@@ -752,6 +766,18 @@ class SparseLRStepPlan(_PlanBase):
         ctx.memo[id(self.op)] = None
         self.steps += 1
         return True
+
+    def check_ids(self):
+        """Raise InvalidArgumentError (ValueError) if any run since the plan was
+        built fed a feature id outside [0, F) (those ids were skipped: their bags
+        trained truncated, where TF's embedding gather would have failed the run)."""
+        if self._nplan is None:
+            return
+        n = int(self._nplan.bad_ids())
+        if n:
+            raise ValueError(f"embedding_lookup_sparse: {n} feature id(s) outside [0, {self.pat.W.table.num_rows}) "
+                             f"were fed to the sparse-LR step (skipped on the device; TF raises "
+                             f"InvalidArgument)")
 
     def fast_runner(self, flat):
         """The one-GPU native step without the Session's per-run machinery: once a
@@ -772,7 +798,7 @@ class SparseLRStepPlan(_PlanBase):
         p, nplan, res = self.pat, self._nplan, _resident_mod()
         y, idx, fids, fvals = p.y, p.idx, p.fids, p.fvals
         want_loss = [f is p.loss for f in flat]
-        nd = np.ndarray
+        nd, check = np.ndarray, self._id_check
 
         def fast(feed):
             fy, fi, ff, fv = feed.get(y), feed.get(idx), feed.get(fids), feed.get(fvals)
@@ -782,6 +808,8 @@ class SparseLRStepPlan(_PlanBase):
                 return None
             opt._steps += 1
             self.steps += 1
+            if check and opt._steps % check == 0:
+                self.check_ids()
             return [nplan.loss().cpu().numpy() if wl else None for wl in want_loss]
         return fast
 
@@ -808,13 +836,18 @@ class SparseLRStepPlan(_PlanBase):
                                            bias=p.b.value)
             if dev.type == "cuda" and w.world_size == 1:
                 self.trainer.enable_graph()        # one worker: no collectives, lazy per-shape captures
+        if any(v is None or isinstance(v, torch.Tensor)
+               for v in (self._feed(ctx, t) for t in (p.y, p.idx, p.fids, p.fvals))):
+            # feed KINDS are the same on every rank (the graph's placeholders fed the
+            # same way): every rank goes op by op together
+            return False
         batch = self._batch(ctx, dev)
         if batch is None:
             if w.world_size > 1:
                 # falling back on this rank alone would desynchronise the collectives
                 # of the lowered step (all-to-all / all-reduce) from its peers'
-                raise RuntimeError("lowered sparse-LR step: this worker's feeds do not match the graph (tensor "
-                                   "feeds, label / index size mismatch or out-of-range rows); synchronous workers "
+                raise RuntimeError("lowered sparse-LR step: this worker's feeds do not match the graph (label / "
+                                   "index size mismatch or out-of-range rows); synchronous workers "
                                    "cannot fall back op by op one rank at a time")
             return False
         opt._steps += 1
@@ -874,7 +907,9 @@ def try_lower(session, fetches, ctx, flat=None) -> None:
         if plan.fetches_ok(flat) and plan.run(ctx, flat) and flat is fetches and \
                 isinstance(getattr(session, "_fast", None), dict):
             fk = tuple(map(id, flat))
-            if fk not in session._fast:
+            old = session._fast.get(fk)
+            if old is None or (getattr(old, "stale", None) is not None and old.stale()):
+                session._fast.pop(fk, None)
                 runner = plan.fast_runner(flat)
                 if runner is not None:
                     session._fast[fk] = runner

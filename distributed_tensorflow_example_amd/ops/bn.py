@@ -159,8 +159,10 @@ class FusedBatchNorm2d(torch.nn.BatchNorm2d):
                 self._pending_batches += 1
             mom = self.momentum
             pre = getattr(x, "_dtf_bn_part", None)
-            if pre is not None and (pre[0].dim() != 3 or pre[0].shape[2] != x.shape[1]):
-                pre = None
+            if pre is not None:
+                pre, ver = pre
+                if ver != x._version or pre[0].dim() != 3 or pre[0].shape[2] != x.shape[1]:
+                    pre = None          # y changed in place after the conv, or another layout
             y = _FusedBN.apply(x, self.weight, self.bias, residual, self.running_mean if self.track_running_stats
                                else None, self.running_var if self.track_running_stats else None, float(mom),
                                float(self.eps), bool(relu), self._sink(), residual_slot, pre)

@@ -626,7 +626,10 @@ class ShadowConv2d(torch.nn.Conv2d):
                 st = _handoff.pop(id(y), None)
                 _handoff.clear()
                 if st is not None:
-                    y._dtf_bn_part = st     # read by the FusedBatchNorm2d that consumes y
+                    # read by the FusedBatchNorm2d that consumes y, only while y is
+                    # unmodified (an in-place op between the conv and the BN bumps
+                    # _version and the BN recomputes its statistics)
+                    y._dtf_bn_part = (st, y._version)
             return y
         w16 = getattr(self.weight, "_shadow", None)
         if (w16 is not None and x.is_cuda and self.bias is None and self.padding_mode == "zeros"

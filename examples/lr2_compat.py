@@ -107,11 +107,18 @@ def main(_):
 
     # tests: this worker feeds its COO entries in reverse (non-canonical) order
     permute = os.environ.get("DTF_LR2_PERMUTE_COO_TASK") == str(FLAGS.task_index)
+    # tests: every worker feeds torch tensors (the lowered step takes numpy feeds;
+    # all ranks then run op by op together)
+    tensor_feeds = os.environ.get("DTF_LR2_TENSOR_FEEDS") == "1"
 
     def feed(batch):
         labels, fids, fvals, sp_indices, batch_size = batch.as_tf_feed()
         if permute:
             fids, fvals, sp_indices = fids[::-1], fvals[::-1], sp_indices[::-1]
+        if tensor_feeds:
+            import torch
+            labels, fids, fvals, sp_indices = (torch.from_numpy(np.ascontiguousarray(a))
+                                               for a in (labels, fids, fvals, sp_indices))
         return {y: labels, x_shape: [num_features, batch_size], x_indices: sp_indices, x_fids: fids,
                 x_fvals: fvals}
 

@@ -122,6 +122,32 @@ def test_conv_bn_statistics_handoff(monkeypatch):
         _close(a, b, 1e-2)
 
 
+def test_conv_bn_statistics_handoff_ignored_after_inplace_write(monkeypatch):
+    """An in-place write to the conv output between the conv and the BN (y += r)
+    bumps its version: the BN must not use the conv epilogue's statistics of the
+    old values -- it recomputes them and matches the plain BN of the new y."""
+    from distributed_tensorflow_example_amd.ops import conv
+    from distributed_tensorflow_example_amd.ops.bn import FusedBatchNorm2d
+
+    monkeypatch.setattr(conv, "_IGEMM", "always")
+    monkeypatch.setattr(conv, "_BN_STATS", True)
+    torch.manual_seed(5)
+    m = conv.ShadowConv2d(64, 128, 3, 1, 1, bias=False).cuda().to(memory_format=torch.channels_last)
+    conv.attach_shadows(m)
+    x = _cl(torch.randn(4, 64, 12, 12, device="cuda").bfloat16())
+    r = _cl(torch.randn(4, 128, 12, 12, device="cuda").bfloat16()) * 3 + 1
+    with torch.no_grad():
+        y = m(x)
+        assert hasattr(y, "_dtf_bn_part")
+        y += r
+        out = FusedBatchNorm2d(128).cuda()(y, relu=True)
+        yf = y.float()
+        mu = yf.mean(dim=(0, 2, 3), keepdim=True)
+        var = yf.var(dim=(0, 2, 3), unbiased=False, keepdim=True)
+        ref = torch.relu((yf - mu) / torch.sqrt(var + 1e-5))
+    _close(out.float(), ref, 2e-2)
+
+
 @pytest.mark.parametrize("ks,two_consumers", [(3, False), (1, False), (3, True)])
 def test_bn_backward_partials_from_conv_input_gradient(monkeypatch, ks, two_consumers):
     """FusedBatchNorm2d(relu) -> conv (3x3 or 1x1, in-tree implicit GEMM): the

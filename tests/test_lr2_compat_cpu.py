@@ -110,3 +110,22 @@ def test_lr2_compat_one_worker_non_canonical_coo_still_lowers(svm, tmp_path):
     w_p = np.load(str(tmp_path / "perm" / "w0.json") + ".W.npy")
     assert np.array_equal(w_p, np.load(str(tmp_path / "perm" / "w1.json") + ".W.npy"))
     assert np.allclose(w_c, w_p, atol=1e-6), np.abs(w_c - w_p).max()
+
+
+def test_lr2_compat_tensor_feeds_go_op_by_op_on_every_worker(svm, tmp_path):
+    """Both workers feed torch tensors: the lowered step takes numpy feeds only,
+    and since feed kinds are rank-independent every worker runs op by op (no
+    raise, no desynchronised collectives); the result equals the lowered run."""
+    d, tr, te = svm
+    common = [f"--train={','.join(tr)}", f"--test={','.join(te)}", "--features=3000", "--num_epochs=1",
+              "--learning_rate=0.5", "--batch_size=100", "--trace_step_interval=4"]
+    (tmp_path / "canon").mkdir()
+    (tmp_path / "tens").mkdir()
+    canon, _ = _cluster(tmp_path / "canon", "lr2_compat.py", common)
+    tens, _ = _cluster(tmp_path / "tens", "lr2_compat.py", common, {"DTF_LR2_TENSOR_FEEDS": "1"})
+    for r in tens:
+        assert r["lowered_steps"] == 0 and r["global_step"] == 10
+    w_c = np.load(str(tmp_path / "canon" / "w0.json") + ".W.npy")
+    w_t = np.load(str(tmp_path / "tens" / "w0.json") + ".W.npy")
+    assert np.array_equal(w_t, np.load(str(tmp_path / "tens" / "w1.json") + ".W.npy"))
+    assert np.allclose(w_c, w_t, atol=1e-5), np.abs(w_c - w_t).max()

@@ -146,3 +146,24 @@ def test_global_step_dtypes(dtype):
             _, step = sess.run([train, gs], feed_dict={x: bx, y_: by})
         assert int(step) == 3 and int(gs.numpy()) == 3
     tf.reset_default_graph()
+
+
+def test_resident_alternating_batch_sizes(monkeypatch):
+    """Alternating two batch sizes rebuilds the resident plan each time: the
+    direct runner of the first size must not relaunch its stopped engine next to
+    the live one (two persistent kernels on the same variables would lose
+    updates).  Every step matches the fp64 evaluation."""
+    monkeypatch.setenv("DTF_RESIDENT_IDLE_S", "2.0")
+    import distributed_tensorflow_example_amd.compat as tf
+    from distributed_tensorflow_example_amd.compat import resident
+
+    g = _graph(tf)
+    b100, b64 = _batches(4, 100, 21), _batches(4, 64, 22)
+    order = [b100[0], b100[1], b64[0], b100[2], b64[1], b64[2], b100[3], b64[3]]
+    with tf.Session() as sess:
+        sess.run(tf.global_variables_initializer())
+        params = [v.numpy().astype(np.float64) for v in g["W"]]
+        for s, b in enumerate(order):
+            params = _check_steps(tf, sess, g, params, [b], 0.5, step0=s)
+            assert len(resident._LIVE) <= 1
+    tf.reset_default_graph()

@@ -5,6 +5,8 @@
 #include <pybind11/numpy.h>
 #include <hip/hip_runtime.h>
 
+#include "comm/ipc_coll_host.h"
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -625,6 +627,22 @@ class GraphStepPlan {
 
   at::Tensor host_metrics() const { return host_metrics_; }
 
+  // Synchronous data parallelism over the node's IPC data plane: the step's
+  // kernels write this worker's gradients (flat [W1 | b1 | W2 | b2], fp32) and
+  // ONE more kernel all-reduces them with every worker's in rank order, applies
+  // p -= lr / W * sum on the graph's variables and bumps global_step
+  // (csrc/kernels/ipc_coll.hip reduce_sgd_k) -- no RCCL, no host round trip.
+  // Direct launches only (the collective's sequence number lives on the device,
+  // but the plan's own graph capture is single-worker).
+  void attach_ipc(py::object coll) {
+    TORCH_CHECK(!use_graph_, "GraphStepPlan.attach_ipc: direct-launch plans only");
+    ipc_obj_ = coll;
+    ipc_ = coll.cast<IpcColl*>();
+    const int64_t n = (int64_t)K_ * H_ + H_ + (int64_t)H_ * C_ + C_;
+    grad_ = at::zeros({(n + 1) & ~1LL}, W1_.options());
+  }
+  bool has_ipc() const { return ipc_ != nullptr; }
+
   // One training step.  x, y: C-contiguous float32 numpy arrays of the plan's
   // shapes.  Returns after the step when `sync` (host_metrics() then holds
   // loss, accuracy, global_step after the step).
@@ -777,12 +795,29 @@ class GraphStepPlan {
     // uint8 feed: [x bytes padded to 16 | y_ | lr] in the same device buffer
     const uint8_t* xu = u8 ? reinterpret_cast<const uint8_t*>(d) : nullptr;
     float* yd = u8 ? d + u8_x_floats() : d + nx;
+    float* gW1 = nullptr, *gb1 = nullptr, *gW2 = nullptr, *gb2 = nullptr;
+    if (ipc_ != nullptr) {     // gradients out (flat, variable order), then the IPC reduce + SGD
+      gW1 = grad_.data_ptr<float>();
+      gb1 = gW1 + (int64_t)K_ * H_;
+      gW2 = gb1 + H_;
+      gb2 = gW2 + (int64_t)H_ * C_;
+    }
     hipError_t e = dtfk_graph_mlp_step(u8 ? nullptr : d, xu, yd, W1_.data_ptr<float>(), b1_.data_ptr<float>(), W2_.data_ptr<float>(),
                                        b2_.data_ptr<float>(), a2_.data_ptr<float>(), dz2_.data_ptr<float>(),
-                                       part_.data_ptr<float>(), nullptr, nullptr, nullptr, nullptr,
+                                       part_.data_ptr<float>(), gW1, gb1, gW2, gb2,
                                        metrics_.data_ptr<float>(), host_store ? host_metrics_.data_ptr<float>() : nullptr,
-                                       gstep_.defined() ? gstep_.data_ptr() : nullptr, gkind_, yd + ny, B_, K_, H_,
-                                       C_, act_, naive_ ? 1 : 0, 1, st);
+                                       ipc_ == nullptr && gstep_.defined() ? gstep_.data_ptr() : nullptr, gkind_,
+                                       yd + ny, B_, K_, H_, C_, act_, naive_ ? 1 : 0, ipc_ == nullptr ? 1 : 0, st);
+    if (e == hipSuccess && ipc_ != nullptr) {
+      {   // (throws on a failed earlier collective; chains streams like every IPC call)
+        (void)ipc_->begin();
+        ipc_->reduce_sgd_raw(grad_.data_ptr<float>(), (int64_t)K_ * H_ + H_ + (int64_t)H_ * C_ + C_,
+                             {W1_.data_ptr<float>(), b1_.data_ptr<float>(), W2_.data_ptr<float>(), b2_.data_ptr<float>()},
+                             {(int64_t)K_ * H_, (int64_t)H_, (int64_t)H_ * C_, (int64_t)C_}, yd + ny, 0.f,
+                             1.f / (float)ipc_->world_size(), gstep_.defined() ? gstep_.data_ptr() : nullptr, gkind_,
+                             metrics_.data_ptr<float>(), host_store ? host_metrics_.data_ptr<float>() : nullptr, st);
+      }
+    }
     if (e == hipSuccess && !host_store)
       e = hipMemcpyAsync(host_metrics_.data_ptr<float>(), metrics_.data_ptr<float>(), 3 * sizeof(float),
                          hipMemcpyDeviceToHost, st);
@@ -805,8 +840,10 @@ class GraphStepPlan {
   // floats the uint8 x occupies at the front of the feed buffer (16-byte padded)
   int64_t u8_x_floats() const { return ((int64_t)B_ * K_ + 15) / 16 * 4; }
 
-  at::Tensor W1_, b1_, W2_, b2_, gstep_, dev_, a2_, dz2_, part_, metrics_, host_metrics_;
+  at::Tensor W1_, b1_, W2_, b2_, gstep_, dev_, a2_, dz2_, part_, metrics_, host_metrics_, grad_;
   at::Tensor stage_[2];
+  py::object ipc_obj_;
+  IpcColl* ipc_ = nullptr;
   hipEvent_t ev_[2] = {nullptr, nullptr};
   hipEvent_t in_ev_ = nullptr, out_ev_ = nullptr;
   hipGraph_t graph_ = nullptr;
@@ -1098,6 +1135,8 @@ void init_mlp(py::module& m) {
       .def("run", &GraphStepPlan::run, py::arg("x"), py::arg("y"), py::arg("lr"), py::arg("sync"))
       .def("run_u8", &GraphStepPlan::run_u8, py::arg("xu8"), py::arg("y"), py::arg("lr"), py::arg("sync"))
       .def("host_metrics", &GraphStepPlan::host_metrics)
+      .def("attach_ipc", &GraphStepPlan::attach_ipc)
+      .def("has_ipc", &GraphStepPlan::has_ipc)
       .def("steps", &GraphStepPlan::steps)
       .def("timing", &GraphStepPlan::timing);
   m.def("graph_mlp_step", &graph_mlp_step, py::arg("x"), py::arg("ylab"), py::arg("W1"), py::arg("b1"),

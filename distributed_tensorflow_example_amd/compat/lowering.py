@@ -345,6 +345,9 @@ class MLPStepPlan(_PlanBase):
                 with torch.no_grad():
                     gs_var.value.data += 1
         else:
+            # gradients straight into the sync bucket's views (no copies), then one
+            # synchronous update: the IPC all-reduce + SGD kernel for plain SGD,
+            # else the all-reduce (IPC / RCCL) and the fused optimizer
             views = sync.views
             grads = [views[i] for i in self.var_index]
             C_.graph_mlp_step(x, y, W1.data, b1.data, W2.data, b2.data, self.a2buf, self.dz2buf, grads,
@@ -352,13 +355,16 @@ class MLPStepPlan(_PlanBase):
             gl = [None] * len(info["vars"])
             for i, g in zip(self.var_index, grads):
                 gl[i] = g
-            if opt.sync_replicas:
-                gl = sync(gl)
-            if fused is not None:
-                if isinstance(opt.learning_rate, Tensor):
-                    fused.set_lr(lr)
-                fused.step(grads=[g.contiguous() for g in gl])
-            if gs_var is not None:
+            done = sync.sgd(gl, lr, gs_var) if (type(opt) is GradientDescentOptimizer and opt.sync_replicas) \
+                else None
+            if done is None:
+                if opt.sync_replicas:
+                    gl = sync(gl)
+                if fused is not None:
+                    if isinstance(opt.learning_rate, Tensor):
+                        fused.set_lr(lr)
+                    fused.step(grads=[g.contiguous() for g in gl])
+            if gs_var is not None and not done:
                 with torch.no_grad():
                     gs_var.value.data += 1
         # loss / accuracy (/ global_step) of this run: one device-to-host copy
@@ -397,8 +403,10 @@ class MLPStepPlan(_PlanBase):
         pat, info = self.pat, self.info
         opt, gs_var = info["opt"], info["global_step"]
         w = _world_or_local()
-        if type(opt) is not GradientDescentOptimizer or info["sparse"] or (w.world_size > 1 and opt.sync_replicas):
+        if type(opt) is not GradientDescentOptimizer or info["sparse"]:
             return False
+        if w.world_size > 1 and opt.sync_replicas and self._sync_ipc(w) is None:
+            return False       # several synchronous workers: only over the IPC data plane
         fx, fy = self._feed_of(ctx, pat.x), self._feed_of(ctx, pat.ylab)
         if fx is None or fy is None or fx.ndim != 2:
             return False
@@ -453,6 +461,16 @@ class MLPStepPlan(_PlanBase):
         self.steps += 1
         return True
 
+    def _sync_ipc(self, w):
+        """The IpcColl the native plan's synchronous step reduces over, or None.
+        COLLECTIVE on the first call (every worker's first lowered run): the
+        node's IPC data plane comes up (or is refused) on all ranks alike."""
+        if not hasattr(self, "_ipc"):
+            coll = w.gpu_coll(4 * sum(v.value.numel() for v in self.info["vars"]))
+            self._ipc = coll if (coll is not None and coll is w.ipc and self.info["sync"] is not None
+                                 and self.info["sync"].comm_dtype in (None, torch.float32)) else None
+        return self._ipc
+
     def _build_native_plan(self, fx, fy, W1, b1, W2, b2, gs_var, gv, w=None) -> bool:
         from .. import _native
 
@@ -473,12 +491,18 @@ class MLPStepPlan(_PlanBase):
         key = (B, K, W1.data_ptr(), b1.data_ptr(), W2.data_ptr(), b2.data_ptr(),
                None if gstep is None else gstep.data_ptr(), pat.act, pat.naive)
         if getattr(self, "_cplan_key", None) != key:
+            multi = w is not None and w.world_size > 1 and self.info["opt"].sync_replicas
             # direct launches by default (measured: a hipGraph replay's fixed host cost
             # exceeds three direct launches here); DTF_GRAPH_STEP_HIPGRAPH=1 replays one
+            # (one worker only)
             self._cplan = _native.load().GraphStepPlan(W1.data, b1.data, W2.data, b2.data, gstep, B, pat.act,
                                                        bool(pat.naive),
-                                                       os.environ.get("DTF_GRAPH_STEP_HIPGRAPH", "0") == "1")
+                                                       os.environ.get("DTF_GRAPH_STEP_HIPGRAPH", "0") == "1"
+                                                       and not multi)
             self._cplan_key = key
+            if multi:
+                # several workers: the plan's step ends with the IPC all-reduce + SGD kernel
+                self._cplan.attach_ipc(self._sync_ipc(w))
             self._hm_np = self._cplan.host_metrics().numpy()
             # the captured-graph plan takes float32 feeds only (run_u8 is direct-launch)
             self._cplan_u8 = not self._cplan.use_graph()

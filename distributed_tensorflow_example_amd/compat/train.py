@@ -255,36 +255,81 @@ def _is_pv(v) -> bool:
 
 
 class _GradSync:
-    """Flat-bucket all-reduce (average) of a var_list's gradients across workers."""
+    """Flat-bucket all-reduce (average) of a var_list's gradients across workers.
+
+    The bucket is one flat fp32 buffer; gradients already written into its
+    views (the lowered step's kernels write there directly) are not copied.
+    A bf16/fp16 `comm_dtype` goes through the K16 pack + cast + 1/N kernel into
+    a persistent 16-bit buffer and back (parallel/ddp.py's bucket kernels).
+    With plain SGD on the node's IPC data plane the all-reduce and the update
+    are ONE kernel (`sgd`, csrc/kernels/ipc_coll.hip reduce_sgd_k)."""
 
     def __init__(self, params: List[torch.Tensor], comm_dtype=None):
         self.params = params
         self.sizes = [p.numel() for p in params]
-        self.flat = torch.zeros(sum(self.sizes), dtype=torch.float32, device=params[0].device)
+        self.n = sum(self.sizes)
+        # even allocation: the IPC kernels move 8-byte packets
+        self.flat = torch.zeros(self.n + (self.n & 1), dtype=torch.float32, device=params[0].device)
         self.views = []
         off = 0
         for p, n in zip(params, self.sizes):
             self.views.append(self.flat[off:off + n].view_as(p))
             off += n
         self.comm_dtype = comm_dtype
+        self.comm_buf = None
+
+    def pack(self, grads: List[Optional[torch.Tensor]]):
+        for v, g in zip(self.views, grads):
+            if g is None:
+                v.zero_()
+            elif g is v or (g.data_ptr() == v.data_ptr() and g.shape == v.shape and g.stride() == v.stride()):
+                continue                                  # written in place by the producer
+            else:
+                v.copy_(g)
 
     def __call__(self, grads: List[Optional[torch.Tensor]]) -> List[torch.Tensor]:
         with torch.no_grad():
-            for v, g in zip(self.views, grads):
-                if g is None:
-                    v.zero_()
-                else:
-                    v.copy_(g)
+            self.pack(grads)
             w = _world_or_local()
             if w.world_size > 1:
-                if self.comm_dtype is not None and self.flat.is_cuda:
-                    buf = self.flat.to(self.comm_dtype)
-                    w.all_reduce(buf, "sum")
-                    self.flat.copy_(buf)
+                flat = self.flat[:self.n]
+                if self.comm_dtype in (torch.bfloat16, torch.float16) and flat.is_cuda:
+                    from .. import _native
+                    C = _native.load()
+                    if self.comm_buf is None:
+                        self.comm_buf = torch.empty(self.n, dtype=self.comm_dtype, device=flat.device)
+                    C.bucket_pack(flat, self.comm_buf, 1.0 / w.world_size)     # K16: 1/N + cast in one pass
+                    w.all_reduce(self.comm_buf, "sum")
+                    C.bucket_unpack(self.comm_buf, flat, 1.0)
+                elif flat.is_cuda:
+                    w.all_reduce(flat, "avg")             # mean inside the collective: no extra pass
                 else:
-                    w.all_reduce(self.flat, "sum")
-                self.flat.mul_(1.0 / w.world_size)      # mean over workers == global-batch gradient
+                    w.all_reduce(flat, "sum")
+                    flat.mul_(1.0 / w.world_size)         # mean over workers == global-batch gradient
         return self.views
+
+    def sgd(self, grads: List[Optional[torch.Tensor]], lr: float, global_step=None) -> Optional[bool]:
+        """Synchronous SGD step as ONE kernel on the IPC data plane: every worker
+        sums the W gradients in rank order (bit-identical replicas) and applies
+        p -= lr / W * sum to its parameters; global_step += 1 inside it when the
+        variable is a GPU scalar.  Returns None when not applicable (one worker,
+        CPU, a 16-bit comm dtype, a plane other than IPC) -- a decision every
+        rank makes alike; else whether global_step was advanced."""
+        w = _world_or_local()
+        if (w.world_size == 1 or not self.flat.is_cuda or self.comm_dtype not in (None, torch.float32)
+                or len(self.params) > 8 or not all(p.dtype == torch.float32 and p.is_contiguous()
+                                                   for p in self.params)):
+            return None
+        coll = w.gpu_coll(self.n * 4)               # collective on first use
+        if coll is None or coll is not w.ipc or self.n * 4 > coll.capacity():
+            return None
+        with torch.no_grad():
+            self.pack(grads)
+            gv = getattr(global_step, "value", None) if global_step is not None else None
+            gs = gv.data if (isinstance(gv, torch.Tensor) and gv.is_cuda and gv.numel() == 1 and gv.is_contiguous()
+                             and gv.dtype in (torch.float32, torch.int64, torch.int32, torch.float64)) else None
+            coll.reduce_sgd(self.flat, [p.data for p in self.params], lr_val=float(lr), gstep=gs)
+        return gs is not None
 
 
 # ======================================================================= optimizers
@@ -377,17 +422,23 @@ class Optimizer:
             ws = w.world_size
             opt._steps += 1
             _debug.fault_point(opt._steps, w.rank)
+            gs_done = False
+            fused_sgd = fused is not None and type(opt) is GradientDescentOptimizer and opt.sync_replicas
             if fused is not None:
                 with _prof.range("compute_gradients"):
                     gs = [ctx.eval(g) if g is not None else None for g in gtens]
-                if opt.sync_replicas:
+                done = sync.sgd(gs, opt._lr_value(), global_step) if fused_sgd else None
+                if done is not None:
+                    gs_done = done                  # all-reduce + update in one IPC kernel
+                elif opt.sync_replicas:
                     with _prof.range("allreduce"):
                         gs = sync(gs)
                 else:
                     gs = [g if g is not None else torch.zeros_like(p) for g, p in zip(gs, params)]
-                if isinstance(opt.learning_rate, Tensor):
-                    fused.set_lr(opt._lr_value())
-                fused.step(grads=[g.contiguous() for g in gs])
+                if done is None:
+                    if isinstance(opt.learning_rate, Tensor):
+                        fused.set_lr(opt._lr_value())
+                    fused.step(grads=[g.contiguous() for g in gs])
             lr = opt._lr_value()
             for g, pv in sparse_pairs:      # owner-side sparse update, sync average as grad_scale
                 looks = ctx.eval(g)
@@ -402,7 +453,7 @@ class Optimizer:
                                        grad_scale=1.0 / ws)
                 if multi:
                     pv.table.finish_update(lr)
-            if global_step is not None:
+            if global_step is not None and not gs_done:
                 with torch.no_grad():
                     global_step.value.data += 1
             n = _debug.check_every()

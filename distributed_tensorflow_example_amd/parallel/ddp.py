@@ -202,7 +202,10 @@ class DistributedDataParallel(torch.nn.Module):
             grad_sink.install(p, self._on_grad if overlap else _no_hook)
         self.comm_stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
         if self.device.type == "cuda":
-            self.world.ensure_comm()   # collective: a lazy world's RCCL communicator, before any bucket
+            # collective: every data plane a bucket will use (IPC for the small ones,
+            # RCCL for large ones when it comes up), set up before any bucket fires
+            for b in self.buckets:
+                self.world.gpu_coll(b.buf.numel() * b.buf.element_size())
         if broadcast_params and self.world.world_size > 1:
             with torch.no_grad():
                 for p in params:
@@ -256,7 +259,8 @@ class DistributedDataParallel(torch.nn.Module):
         w = self.world
         if w.world_size == 1:
             return
-        if self.device.type == "cuda" and w.comm is not None:
+        coll = w.gpu_coll(b.buf.numel() * b.buf.element_size()) if self.device.type == "cuda" else None
+        if coll is not None:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream())
             self.comm_stream.wait_event(ev)
@@ -270,13 +274,16 @@ class DistributedDataParallel(torch.nn.Module):
                         b.comm_buf = torch.empty(b.buf.numel(), dtype=self.comm_dtype, device=b.buf.device)
                     C = _native.load()
                     C.bucket_pack(b.buf, b.comm_buf, scale)
-                    w.comm.all_reduce(b.comm_buf, "sum")
+                    if b.comm_buf.dtype == torch.float16 and coll is w.ipc:
+                        w.all_reduce(b.comm_buf, "sum")      # IPC reduces fp16 through fp32
+                    else:
+                        coll.all_reduce(b.comm_buf, "sum")
                     C.bucket_unpack(b.comm_buf, b.buf, 1.0)
                 elif self.comm_dtype is not None and self.comm_dtype != torch.float32:
                     raise ValueError(f"DDP comm_dtype {self.comm_dtype}: float32, bfloat16 or float16")
                 else:
                     # RCCL's ncclAvg divides inside the reduction: no extra pass over the bucket
-                    w.comm.all_reduce(b.buf, "avg" if self.average else "sum")
+                    coll.all_reduce(b.buf, "avg" if self.average else "sum")
             b.event = torch.cuda.Event()
             b.event.record(self.comm_stream)
         else:

@@ -63,6 +63,8 @@ flags.DEFINE_string("checkpoint_dir", "", "Supervisor logdir: restore on start, 
 flags.DEFINE_integer("save_model_secs", 600, "checkpoint period (chief, seconds)")
 flags.DEFINE_integer("save_model_steps", 0, "checkpoint every N global steps (all ranks agree; overrides secs)")
 flags.DEFINE_string("metrics_jsonl", "", "append JSON-lines step metrics here")
+flags.DEFINE_string("dump_dir", "", "tests: save this worker's initial / final parameters and the batches it fed "
+                    "(worker_<task>.npz) and the data-plane facts (which step ran, which collectives)")
 flags.DEFINE_string("update_mode", "sync", "sync: every train_op run all-reduces the workers' gradients (default); "
                     "async: the reference's Hogwild ps updates -- each worker applies its own gradient to the "
                     "shared variables without waiting (parallel/async_ps.py), global_step counts every worker's step")
@@ -124,8 +126,12 @@ def run_graph_worker(server, mnist, logs_path):
     cost = float("nan")
     steps = 0
     mw = MetricsWriter(FLAGS.metrics_jsonl) if FLAGS.metrics_jsonl else None
+    dump = {} if FLAGS.dump_dir else None
     with sv.prepare_or_wait_for_session(server.target) as sess:
         start_gstep = int(sess.run(g["global_step"]))
+        if dump is not None:
+            dump.update({f"init{k}": np.asarray(sess.run(v)) for k, v in enumerate(g["W"])})
+            xs, ys = [], []
         if start_gstep:
             print(f"restored from checkpoint at global step {start_gstep}", flush=True)
         writer = tf.summary.FileWriter(logs_path, graph=tf.get_default_graph())
@@ -136,10 +142,15 @@ def run_graph_worker(server, mnist, logs_path):
             count = 0
             for i in range(batch_count):
                 bx, by = mnist.train.next_batch(FLAGS.batch_size)
+                if dump is not None:
+                    xs.append(np.array(bx, dtype=np.float32))
+                    ys.append(np.asarray(by).copy())
                 _, cost, summary, step = sess.run([g["train_op"], g["cross_entropy"], g["summary_op"],
                                                    g["global_step"]], feed_dict={g["x"]: bx, g["y_"]: by})
                 writer.add_summary(summary, int(step))
                 steps += 1
+                if steps == 20:
+                    t_steady = time.perf_counter()      # per-run cost past the warm-up (dump_dir)
                 count += 1
                 if mw is not None:
                     mw.write("step", int(step), cost=float(cost))
@@ -154,6 +165,7 @@ def run_graph_worker(server, mnist, logs_path):
                     break
             if done:
                 break
+        steady_ms = (time.perf_counter() - t_steady) / (steps - 20) * 1e3 if steps > 20 else None
         acc = float(sess.run(g["accuracy"], feed_dict={g["x"]: mnist.test.images, g["y_"]: mnist.test.labels}))
         if mw is not None:
             mw.write("final", int(sess.run(g["global_step"])), accuracy=acc, cost=float(cost))
@@ -161,6 +173,25 @@ def run_graph_worker(server, mnist, logs_path):
         params = [np.asarray(sess.run(v)) for v in g["W"]]
         gstep = int(sess.run(g["global_step"]))
         writer.close()
+        if dump is not None:
+            from distributed_tensorflow_example_amd.compat import lowering
+
+            plan = lowering.plan_for(g["train_op"])
+            cplan = getattr(plan, "_cplan", None)
+            w = server.world
+            dump.update({f"final{k}": p for k, p in enumerate(params)})
+            dump.update(xs=np.stack(xs), ys=np.stack(ys))
+            os.makedirs(FLAGS.dump_dir, exist_ok=True)
+            np.savez(os.path.join(FLAGS.dump_dir, f"worker_{FLAGS.task_index}.npz"), **dump)
+            with open(os.path.join(FLAGS.dump_dir, f"worker_{FLAGS.task_index}.json"), "w") as f:
+                json.dump({"lowered_steps": getattr(plan, "steps", 0) if plan else 0,
+                           "native_plan_steps": int(cplan.steps()) if cplan is not None else 0,
+                           "native_plan_ipc": bool(cplan.has_ipc()) if cplan is not None else False,
+                           "rccl_comm": w is not None and w.comm is not None,
+                           "ipc_calls": int(w.ipc.calls()) if w is not None and w.ipc is not None else 0,
+                           "ipc_error": w.ipc_error if w is not None else None,
+                           "world_size": w.world_size if w is not None else 1,
+                           "steps": steps, "session_loop_ms_per_step_after_20": steady_ms}, f)
     sv.stop()
     return acc, float(cost), time.time() - begin, params, gstep
 

@@ -6,6 +6,7 @@ eager op-by-op path (DTF_GRAPH_LOWERING=0), plus device time of the lowered
 kernels alone (CUDA events around graph_mlp_step).
 
     python scripts/bench_graph_step.py [steps]
+    python scripts/bench_graph_step.py --workers 2 [steps]   # 1 ps + 2 sync workers (IPC plane)
 """
 import json
 import os
@@ -19,7 +20,35 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
 
 
+def main_workers(workers: int, steps: int):
+    """examples/mnist_example.py as 1 ps + `workers` synchronous workers (all on
+    the visible GPU(s); on a 1-GPU box they share cuda:0 -- a rehearsal of the
+    protocol, not a scaling number): per-Session.run time of the reference's
+    loop past its first 20 runs, per worker, with the data-plane facts."""
+    import tempfile
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
+    from test_compat_ipc_gpu import run_cluster
+
+    with tempfile.TemporaryDirectory() as tmp:
+        _, facts, _ = run_cluster(tmp, workers, steps, extra=["--train_size=20000"], timeout=600)
+    ms = [f["session_loop_ms_per_step_after_20"] for f in facts]
+    print(json.dumps({"workers": workers, "steps": steps,
+                      "session_run_ms_per_step_workers": [round(m, 4) for m in ms],
+                      "session_run_ms_per_step_max": round(max(ms), 4),
+                      "native_plan_ipc": all(f["native_plan_ipc"] for f in facts),
+                      "native_plan_steps": [f["native_plan_steps"] for f in facts],
+                      "rccl_comm": any(f["rccl_comm"] for f in facts),
+                      "ipc_calls": [f["ipc_calls"] for f in facts],
+                      "same_gpu": torch.cuda.device_count() < workers}))
+
+
 def main():
+    if "--workers" in sys.argv:
+        i = sys.argv.index("--workers")
+        workers = int(sys.argv[i + 1])
+        rest = [a for j, a in enumerate(sys.argv[1:], 1) if j not in (i, i + 1)]
+        return main_workers(workers, int(rest[0]) if rest else 1000)
     import distributed_tensorflow_example_amd.compat as tf
     from distributed_tensorflow_example_amd import _native
     from distributed_tensorflow_example_amd.compat import lowering as L

@@ -27,6 +27,10 @@
 #                 hipBLASLt (scripts/bench_gemm.py)
 #   gemm_sweep    gemm_big schedules vs hipBLASLt over K (fixed vs per-K-tile cost)
 #   sparse        sparse LR / Wide&Deep / sparse-optimizer GPU tests + benches
+#   ipc           IPC data-plane tests: collectives with 2-4 ranks on cuda:0, the
+#                 compat example as 1 ps + 2 / 4 sync workers, then the per-run time
+#                 of 1 ps + 2 workers (scripts/bench_graph_step.py --workers 2)
+#   tests         the GPU tests named in $TESTS (pytest node ids / files)
 # Env: STEP_ARGS_<step> adds arguments to that step's main command.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -95,6 +99,10 @@ for step in "$@"; do
       run sparse_tests 500 $PYT -x tests/test_models_gpu.py tests/test_async_ps_gpu.py tests/test_sparse_optim_gpu.py $extra
       run bench_lr2 300 python scripts/bench_models.py --model sparse_lr --graph
       run bench_wd 300 python scripts/bench_models.py --model wide_deep --graph ;;
+    ipc)
+      run ipc_tests 700 $PYT -x tests/test_ipc_coll_gpu.py tests/test_compat_ipc_gpu.py $extra
+      run bench_workers2 400 python scripts/bench_graph_step.py --workers 2 1000 ;;
+    tests) run tests 900 $PYT -x $TESTS $extra ;;
     *) echo "unknown step: $step"; exit 2 ;;
   esac
 done

@@ -100,7 +100,7 @@ class IpcColl {
   // dtype: 0 f32, 1 bf16, 2 f64, 3 i32, 4 i64; op 0 sum, 1 max, 2 min
   void all_reduce_raw(const void* in, void* out, int64_t n, int dtype, int op, float scale, hipStream_t s) {
     const int es = dtype == 1 ? 2 : (dtype == 0 || dtype == 3) ? 4 : 8;
-    if (((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 7) || (n * es) % 4)
+    if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 7)
       throw std::runtime_error("IpcColl.all_reduce: 8-byte aligned buffers expected");
     const int64_t chunk = cap_ / 8 * 8 / es;         // whole packets per chunk
     for (int64_t off = 0; off < n; off += chunk) {

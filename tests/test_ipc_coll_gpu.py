@@ -28,7 +28,8 @@ def _run(nproc, *args, env_extra=None, timeout=200):
     cmd = [sys.executable, "-m", "torch.distributed.run", f"--nproc-per-node={nproc}", "--master-addr=127.0.0.1",
            f"--master-port={_port()}", os.path.join(REPO, "scripts", "ipc_coll_selftest.py")] + list(args)
     env = dict(os.environ, PYTHONPATH=REPO, OMP_NUM_THREADS="2", DTF_DATA_PLANE="ipc", DTF_IPC_SLOT_MB="1",
-               DTF_IPC_TIMEOUT_S="20", **(env_extra or {}))
+               DTF_IPC_TIMEOUT_S="20")
+    env.update(env_extra or {})
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env)
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     out = r.stdout + r.stderr

@@ -344,11 +344,12 @@ class GemmMLPTrainer:
         self.gstep = torch.zeros(1, dtype=torch.int64, device=dev)
         self.allreduce = "none"
         if self.world_size > 1:
-            world.ensure_comm()    # collective; None on gloo worlds
-            self.allreduce = "rccl" if world.comm is not None else world.backend
-        # RCCL calls capture into hipGraphs; a gloo all-reduce (ranks sharing
-        # one GPU in tests) does not
-        self.graph_safe = self.world_size == 1 or world.comm is not None
+            coll = world.gpu_coll(NPARAM * 4)    # collective: IPC on one node, else RCCL; None on gloo worlds
+            self.allreduce = "ipc" if (coll is not None and coll is world.ipc) else \
+                ("rccl" if world.comm is not None else world.backend)
+        # RCCL and the IPC collectives capture into hipGraphs (the IPC sequence
+        # numbers live on the device); a gloo all-reduce does not
+        self.graph_safe = self.world_size == 1 or self.allreduce in ("rccl", "ipc")
         self.ipc_parity = 0
         self.shadows_stale = False
         self.set_params(init_params(seed))

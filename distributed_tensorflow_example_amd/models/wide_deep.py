@@ -79,8 +79,10 @@ class WideDeep(StaticStepMixin):
                 for p in self.dense_params:
                     self.world.broadcast(p.data, 0)
         self.comm_stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
-        if self.device.type == "cuda":
-            self.world.ensure_comm()   # collective: a lazy world's RCCL communicator, before any bucket
+        if self.device.type == "cuda" and self.world.world_size > 1:
+            # collective: the data plane of the tower's flat all-reduce (IPC on one
+            # node, RCCL when it comes up for large towers), before the first step
+            self.world.gpu_coll(self.flat_grad.numel() * self.flat_grad.element_size())
         self.global_step = 0
         self._graphed = None
 
@@ -165,7 +167,10 @@ class WideDeep(StaticStepMixin):
         # dense tower: one flat all-reduce, overlapped with the sparse exchanges
         ev = None
         if ws > 1:
-            if self.comm_stream is not None and self.world.comm is not None:
+            coll = self.world.gpu_coll(self.flat_grad.numel() * self.flat_grad.element_size())
+            if self.comm_stream is not None and coll is not None and coll is self.world.comm:
+                # (RCCL: overlapped with the sparse exchanges on a side stream; the IPC
+                # collectives keep one stream order, so they stay on this stream)
                 self.comm_stream.wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(self.comm_stream):
                     self.world.all_reduce(self.flat_grad)

@@ -159,6 +159,8 @@ def main():
                           "config": cfg, "final_loss": float(loss), "init_s": round(init_s, 3),
                           "init_peak_mem_gib": None if init_mem is None else round(init_mem, 3),
                           "sparse_exchange": _exchange_stats(m),
+                          "data_plane": {"ipc_calls": int(w.ipc.calls()) if w.ipc is not None else 0,
+                                         "rccl_comm": w.comm is not None},
                           "peak_mem_gib": round(torch.cuda.max_memory_allocated() / 2 ** 30, 3)
                           if dev.type == "cuda" else None}), flush=True)
     w.shutdown()

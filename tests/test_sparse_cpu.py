@@ -95,6 +95,11 @@ def test_parse_parity_with_python_reference_parser():
         assert d.labels[i] == lab and list(d.ids[s:e]) == idx and np.allclose(d.vals[s:e], val)
 
 
+def plane(w):
+    """Which GPU data planes this rank's world created (IPC calls, RCCL communicator)."""
+    return {"ipc_calls": int(w.ipc.calls()) if w.ipc is not None else 0, "rccl": w.comm is not None}
+
+
 def _sharded_worker(rank, ws, port, q, files, steps, lr, kind="lr", peer_cap=None, sparse_opt="sgd",
                     explicit_sync=True):
     try:
@@ -106,7 +111,9 @@ def _sharded_worker(rank, ws, port, q, files, steps, lr, kind="lr", peer_cap=Non
         from distributed_tensorflow_example_amd.models import sparse_lr
         from distributed_tensorflow_example_amd.parallel import world as W
 
-        w = W.init(backend="gloo")
+        # (tests/test_sharded_ipc_gpu.py: "rccl" = every rank on the visible GPU, the
+        # sharded exchanges on World's GPU data plane -- IPC when the ranks share a node)
+        w = W.init(backend=os.environ.get("DTF_TEST_BACKEND", "gloo"))
         data = libsvm.load_files(files, 2)
         cap = 200 * 64 if kind.endswith("-static") else None     # ids-per-batch bound: static routing
         if kind.startswith("wd"):
@@ -121,7 +128,7 @@ def _sharded_worker(rank, ws, port, q, files, steps, lr, kind="lr", peer_cap=Non
             tr = sparse_lr.SparseLRTrainer(3000, lr, w, seed=5, ids_capacity=cap, rows=200 // ws,
                                            peer_capacity=peer_cap)
             router = tr.W.router
-        init_tab = tr.W.full_table().numpy().copy()
+        init_tab = tr.W.full_table().cpu().numpy().copy()
         B = 200
         for s in range(steps):
             rows = np.arange(s * B, (s + 1) * B)
@@ -133,14 +140,15 @@ def _sharded_worker(rank, ws, port, q, files, steps, lr, kind="lr", peer_cap=Non
                 tr.sync_exchange()                 # flush the last window (replays voided steps)
             stats = dict(peer_cap=router.peer_cap, checks=router.checks, resizes=router.resizes,
                          voided=router.voided, gstep=tr.global_step)
-        final = tr.W.full_table().numpy().copy() if explicit_sync else None
+        final = tr.W.full_table().cpu().numpy().copy() if explicit_sync else None
         if kind.startswith("wd"):
-            q.put((rank, init_tab, final, tr.b.detach().numpy().copy(), tr.wide.full_table().numpy().copy(), stats))
+            q.put((rank, init_tab, final, tr.b.detach().cpu().numpy().copy(), tr.wide.full_table().cpu().numpy().copy(),
+                   stats, plane(w)))
             return
         local, repl = tr.checkpoint_tensors()
         prefix = ckpt.save_sharded(os.path.join(os.path.dirname(files[0]), f"ck{ws}", "lr"), local, repl, w,
                                    global_step=tr.global_step)
-        q.put((rank, init_tab, final, float(tr.b.detach()[0]), prefix, stats))
+        q.put((rank, init_tab, final, float(tr.b.detach()[0]), prefix, stats, plane(w)))
     except Exception:
         import traceback
 
@@ -353,7 +361,9 @@ def _zipf_worker(rank, ws, port, q, steps):
         from distributed_tensorflow_example_amd.models import sparse_lr
         from distributed_tensorflow_example_amd.parallel import world as W
 
-        w = W.init(backend="gloo")
+        # (tests/test_sharded_ipc_gpu.py: "rccl" = every rank on the visible GPU, the
+        # sharded exchanges on World's GPU data plane -- IPC when the ranks share a node)
+        w = W.init(backend=os.environ.get("DTF_TEST_BACKEND", "gloo"))
         B, nnz, F = 512, 32, 100_000_000          # scripts/bench_models.py's id law (Zipf 1.1), smaller batch
         tr = sparse_lr.SparseLRTrainer(F // 1000, 0.1, w, seed=5, ids_capacity=B * nnz, rows=B)
         rng = np.random.default_rng(1234 + rank)

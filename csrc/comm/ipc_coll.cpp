@@ -84,7 +84,7 @@ void all_to_all(IpcColl& c, at::Tensor src, std::vector<int64_t> send_counts, at
   c.all_to_all_raw(src.data_ptr(), sb, dst.data_ptr(), rb, s);
 }
 
-// grad: flat fp32 gradient of `params` (in order; even-size allocation);
+// grad: flat fp32 gradient of `params` (in order, 16-byte aligned);
 // every rank applies p -= lr / W * sum of the W gradients, global_step += 1
 void reduce_sgd(IpcColl& c, at::Tensor grad, std::vector<at::Tensor> params, c10::optional<at::Tensor> lr,
                 double lr_val, c10::optional<at::Tensor> gstep, c10::optional<at::Tensor> host_metrics) {
@@ -100,7 +100,7 @@ void reduce_sgd(IpcColl& c, at::Tensor grad, std::vector<at::Tensor> params, c10
     ns.push_back(p.numel());
     n += p.numel();
   }
-  if (grad.numel() < ((n + 1) & ~1LL)) throw std::runtime_error("IpcColl.reduce_sgd: gradient allocation too small");
+  if (grad.numel() < n) throw std::runtime_error("IpcColl.reduce_sgd: gradient smaller than the parameters");
   void* gs = nullptr;
   int gk = 0;
   if (gstep.has_value()) {

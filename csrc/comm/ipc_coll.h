@@ -28,6 +28,7 @@ struct Coll {
   int* err;                      // device error word: later collectives fail fast
   int* err_host;                 // pinned host error word: the host raises on its next call
   long long timeout;             // s_memrealtime ticks (100 MHz) a wait may take before it reports
+  int wide;                      // 1: 16-byte system-coherent buffer loads of peer slots; 0: 8-byte atomics (A/B)
 };
 
 struct SgdArgs {                 // fused all-reduce-mean + SGD over up to 8 fp32 parameters (flat order)

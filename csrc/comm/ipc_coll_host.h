@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -43,6 +44,8 @@ class IpcColl {
     err_ = at::zeros({1}, dev.dtype(at::kInt));
     err_host_ = at::zeros({2}, at::TensorOptions().dtype(at::kInt).pinned_memory(true));
     timeout_ = (long long)(std::max(0.001, timeout_s) * 1e8);   // s_memrealtime: 100 MHz
+    const char* nw = std::getenv("DTF_IPC_NARROW");                // A/B probe: 8-byte peer loads
+    wide_ = (nw != nullptr && nw[0] == '1') ? 0 : 1;
     ck(hipEventCreateWithFlags(&ev_, hipEventDisableTiming), "hipEventCreate");
   }
   ~IpcColl() {
@@ -67,6 +70,7 @@ class IpcColl {
     c.err = err_.data_ptr<int>();
     c.err_host = err_host_.data_ptr<int>();
     c.timeout = timeout_;
+    c.wide = wide_;
     return c;
   }
 
@@ -100,9 +104,9 @@ class IpcColl {
   // dtype: 0 f32, 1 bf16, 2 f64, 3 i32, 4 i64; op 0 sum, 1 max, 2 min
   void all_reduce_raw(const void* in, void* out, int64_t n, int dtype, int op, float scale, hipStream_t s) {
     const int es = dtype == 1 ? 2 : (dtype == 0 || dtype == 3) ? 4 : 8;
-    if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 7)
-      throw std::runtime_error("IpcColl.all_reduce: 8-byte aligned buffers expected");
-    const int64_t chunk = cap_ / 8 * 8 / es;         // whole packets per chunk
+    if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15)
+      throw std::runtime_error("IpcColl.all_reduce: 16-byte aligned buffers expected");
+    const int64_t chunk = cap_ / 16 * 16 / es;       // whole 16-byte packets per chunk
     for (int64_t off = 0; off < n; off += chunk) {
       const int64_t m = std::min(chunk, n - off);
       const int two = (W_ > 2 && m * es >= two_shot_) ? 1 : 0;
@@ -112,14 +116,15 @@ class IpcColl {
     }
   }
 
-  // fused all-reduce mean + SGD: grad (fp32, n values, even-size allocation)
+  // fused all-reduce mean + SGD: grad (fp32, n values, 16-byte aligned)
   void reduce_sgd_raw(const float* grad, int64_t n, const std::vector<float*>& params,
                       const std::vector<int64_t>& numels, const float* lr_ptr, float lr_val, float scale, void* gstep,
                       int gkind, float* metrics, float* host_metrics, hipStream_t s) {
     if (params.empty() || params.size() > 8 || params.size() != numels.size())
       throw std::runtime_error("IpcColl.reduce_sgd: 1..8 parameters expected");
     if (n * 4 > cap_) throw std::runtime_error("IpcColl.reduce_sgd: gradient larger than the IPC slot");
-    if (reinterpret_cast<uintptr_t>(grad) & 7) throw std::runtime_error("IpcColl.reduce_sgd: 8-byte aligned gradient");
+    if (reinterpret_cast<uintptr_t>(grad) & 15)
+      throw std::runtime_error("IpcColl.reduce_sgd: 16-byte aligned gradient");
     dtfk::ipcc::SgdArgs a{};
     int64_t e = 0;
     for (size_t i = 0; i < params.size(); ++i) {
@@ -142,7 +147,7 @@ class IpcColl {
   void broadcast_raw(void* buf, int64_t nbytes, int src, hipStream_t s) {
     if ((reinterpret_cast<uintptr_t>(buf) & 3) || (nbytes & 3))
       throw std::runtime_error("IpcColl.broadcast: 4-byte aligned buffer and size expected");
-    const int64_t chunk = cap_ / 8 * 8;
+    const int64_t chunk = cap_ / 16 * 16;
     for (int64_t off = 0; off < nbytes; off += chunk) {
       const int64_t m = std::min(chunk, nbytes - off);
       char* p = static_cast<char*>(buf) + off;
@@ -153,7 +158,7 @@ class IpcColl {
   void all_gather_raw(const void* in, void* out, int64_t nbytes, hipStream_t s) {
     if (((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 3) || (nbytes & 3))
       throw std::runtime_error("IpcColl.all_gather: 4-byte aligned buffers and size expected");
-    const int64_t chunk = cap_ / 8 * 8;
+    const int64_t chunk = cap_ / 16 * 16;
     for (int64_t off = 0; off < nbytes; off += chunk) {
       const int64_t m = std::min(chunk, nbytes - off);
       ck(dtfk_ipcc_allgather(static_cast<const char*>(in) + off, static_cast<char*>(out) + off, m, nbytes, coll(),
@@ -200,6 +205,7 @@ class IpcColl {
   int64_t cap_, two_shot_;
   int max_grid_;
   long long timeout_ = 0;
+  int wide_ = 1;
   at::Tensor words_, err_, err_host_;
   hipEvent_t ev_ = nullptr;
   hipStream_t last_ = nullptr;

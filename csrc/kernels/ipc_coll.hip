@@ -100,51 +100,93 @@ __device__ bool wait_peers(const Coll& c, int ph, u64 s) {
   return ok != 0;
 }
 
+// ---------------------------------------------------------------- peer access
+// Peer slots are read 16 bytes per lane with system-coherent (sc0 sc1) buffer
+// loads -- never served from a cache line of this GPU -- several in flight per
+// lane; Coll::wide == 0 (DTF_IPC_NARROW=1, A/B probe) reads 8-byte relaxed
+// system-scope atomics instead.
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+constexpr int SYS = 1 | 16;   // sc0 | sc1
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)(bytes < 0x7fffffffLL ? bytes : 0x7fffffffLL),
+                                           0x00020000);
+}
+__device__ __forceinline__ u32x4 ld_peer16(const Coll& c, const char* base, long long off) {
+  if (c.wide) return __builtin_amdgcn_raw_buffer_load_b128(rsrc(base, 2 * c.cap), (int)off, 0, SYS);
+  const u64 a = ld_sys_u64(base + off), b = ld_sys_u64(base + off + 8);
+  return u32x4{(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
+}
+
 // ---------------------------------------------------------------- element types
-// 8-byte packets of N elements; reductions in Acc (fp32 for bf16 storage).
+// 16-byte packets of N elements; reductions in A (fp32 for bf16 storage).
 template <typename T> struct Ty;
 template <> struct Ty<float> {
-  typedef float A; static constexpr int N = 2;
-  __device__ static void unpack(u64 u, A* v) { v[0] = __uint_as_float((uint32_t)u); v[1] = __uint_as_float((uint32_t)(u >> 32)); }
-  __device__ static u64 pack(const A* v) { return (u64)__float_as_uint(v[0]) | ((u64)__float_as_uint(v[1]) << 32); }
+  typedef float A; static constexpr int N = 4;
+  __device__ static void unpack(u32x4 u, A* v) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = __uint_as_float(u[i]);
+  }
+  __device__ static u32x4 pack(const A* v) {
+    return u32x4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+  }
   __device__ static A ld1(const void* p) { return ld_sys_f32(p); }
   __device__ static A get(float v) { return v; }
   __device__ static float put(A v) { return v; }
 };
 struct bf16_t { uint16_t b; };
 template <> struct Ty<bf16_t> {
-  typedef float A; static constexpr int N = 4;
-  __device__ static void unpack(u64 u, A* v) {
+  typedef float A; static constexpr int N = 8;
+  __device__ static void unpack(u32x4 u, A* v) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = bf2f((uint16_t)(u >> (16 * i)));
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = bf2f((uint16_t)(u[i] & 0xFFFFu));
+      v[2 * i + 1] = bf2f((uint16_t)(u[i] >> 16));
+    }
   }
-  __device__ static u64 pack(const A* v) {
-    u64 u = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) u |= (u64)f2bf(v[i]) << (16 * i);
-    return u;
+  __device__ static u32x4 pack(const A* v) {
+    return u32x4{pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7])};
   }
   __device__ static A ld1(const void* p) { return bf2f(ld_sys_u16(p)); }
   __device__ static A get(bf16_t v) { return bf2f(v.b); }
   __device__ static bf16_t put(A v) { return bf16_t{f2bf(v)}; }
 };
 template <> struct Ty<double> {
-  typedef double A; static constexpr int N = 1;
-  __device__ static void unpack(u64 u, A* v) { v[0] = __longlong_as_double((long long)u); }
-  __device__ static u64 pack(const A* v) { return (u64)__double_as_longlong(v[0]); }
+  typedef double A; static constexpr int N = 2;
+  __device__ static void unpack(u32x4 u, A* v) {
+    v[0] = __longlong_as_double((long long)((u64)u[0] | ((u64)u[1] << 32)));
+    v[1] = __longlong_as_double((long long)((u64)u[2] | ((u64)u[3] << 32)));
+  }
+  __device__ static u32x4 pack(const A* v) {
+    const u64 a = (u64)__double_as_longlong(v[0]), b = (u64)__double_as_longlong(v[1]);
+    return u32x4{(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
+  }
+  __device__ static A ld1(const void* p) { return __longlong_as_double((long long)ld_sys_u64(p)); }
+  __device__ static A get(double v) { return v; }
+  __device__ static double put(A v) { return v; }
 };
 template <> struct Ty<int> {
-  typedef int A; static constexpr int N = 2;
-  __device__ static void unpack(u64 u, A* v) { v[0] = (int)(uint32_t)u; v[1] = (int)(uint32_t)(u >> 32); }
-  __device__ static u64 pack(const A* v) { return (u64)(uint32_t)v[0] | ((u64)(uint32_t)v[1] << 32); }
+  typedef int A; static constexpr int N = 4;
+  __device__ static void unpack(u32x4 u, A* v) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = (int)u[i];
+  }
+  __device__ static u32x4 pack(const A* v) { return u32x4{(uint32_t)v[0], (uint32_t)v[1], (uint32_t)v[2], (uint32_t)v[3]}; }
   __device__ static A ld1(const void* p) { return (int)ld_sys_u32(p); }
   __device__ static A get(int v) { return v; }
   __device__ static int put(A v) { return v; }
 };
 template <> struct Ty<long long> {
-  typedef long long A; static constexpr int N = 1;
-  __device__ static void unpack(u64 u, A* v) { v[0] = (long long)u; }
-  __device__ static u64 pack(const A* v) { return (u64)v[0]; }
+  typedef long long A; static constexpr int N = 2;
+  __device__ static void unpack(u32x4 u, A* v) {
+    v[0] = (long long)((u64)u[0] | ((u64)u[1] << 32));
+    v[1] = (long long)((u64)u[2] | ((u64)u[3] << 32));
+  }
+  __device__ static u32x4 pack(const A* v) {
+    return u32x4{(uint32_t)v[0], (uint32_t)((u64)v[0] >> 32), (uint32_t)v[1], (uint32_t)((u64)v[1] >> 32)};
+  }
+  __device__ static A ld1(const void* p) { return (long long)ld_sys_u64(p); }
+  __device__ static A get(long long v) { return v; }
+  __device__ static long long put(A v) { return v; }
 };
 
 template <int OP, typename A>
@@ -154,41 +196,38 @@ __device__ __forceinline__ A combine(A a, A b) {
   return a < b ? a : b;
 }
 
-// Copy nbytes (multiple of 4; pointers 4-byte aligned, 8-byte packets where
-// both are 8-byte aligned) between local buffers, grid-stride.
-__device__ __forceinline__ void copy_local(void* dst, const void* src, long long nbytes, long long tid, long long nth) {
-  if (((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 7) == 0) {
-    const long long np = nbytes >> 3;
-    u64* d = static_cast<u64*>(dst);
-    const u64* q = static_cast<const u64*>(src);
-    for (long long j = tid; j < np; j += nth) d[j] = q[j];
-    if ((nbytes & 4) && tid == 0)
-      static_cast<uint32_t*>(dst)[nbytes / 4 - 1] = static_cast<const uint32_t*>(src)[nbytes / 4 - 1];
-  } else {
-    uint32_t* d = static_cast<uint32_t*>(dst);
-    const uint32_t* q = static_cast<const uint32_t*>(src);
-    for (long long j = tid; j < (nbytes >> 2); j += nth) d[j] = q[j];
-  }
-}
-// The same from a peer's slot (system-scope loads).
-__device__ __forceinline__ void copy_peer(void* dst, const void* src, long long nbytes, long long tid, long long nth) {
-  if (((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 7) == 0) {
-    const long long np = nbytes >> 3;
-    u64* d = static_cast<u64*>(dst);
-    const u64* q = static_cast<const u64*>(src);
+// Copy nbytes (a multiple of 4; pointers 4-byte aligned) grid-stride: 16-byte
+// packets where dst, src and nbytes allow, else 8-, else 4-byte words.
+// PEER: src is a peer's slot (system-coherent loads, four in flight per lane).
+template <bool PEER>
+__device__ void copy_bytes(const Coll& c, void* dst, const void* src, long long nbytes, long long tid, long long nth) {
+  const uintptr_t al = reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src) | (uintptr_t)nbytes;
+  char* d = static_cast<char*>(dst);
+  const char* q = static_cast<const char*>(src);
+  if ((al & 15) == 0) {
+    const long long np = nbytes >> 4;
     long long j = tid;
-    for (; j + 3 * nth < np; j += 4 * nth) {   // four loads in flight per lane
-      const u64 a = ld_sys_u64(q + j), b = ld_sys_u64(q + j + nth), e = ld_sys_u64(q + j + 2 * nth),
-                f = ld_sys_u64(q + j + 3 * nth);
-      d[j] = a; d[j + nth] = b; d[j + 2 * nth] = e; d[j + 3 * nth] = f;
+    if (PEER) {
+      for (; j + 3 * nth < np; j += 4 * nth) {
+        const u32x4 a = ld_peer16(c, q, 16 * j), b = ld_peer16(c, q, 16 * (j + nth)),
+                    e = ld_peer16(c, q, 16 * (j + 2 * nth)), f = ld_peer16(c, q, 16 * (j + 3 * nth));
+        reinterpret_cast<u32x4*>(d)[j] = a;
+        reinterpret_cast<u32x4*>(d)[j + nth] = b;
+        reinterpret_cast<u32x4*>(d)[j + 2 * nth] = e;
+        reinterpret_cast<u32x4*>(d)[j + 3 * nth] = f;
+      }
+      for (; j < np; j += nth) reinterpret_cast<u32x4*>(d)[j] = ld_peer16(c, q, 16 * j);
+    } else {
+      for (; j < np; j += nth) reinterpret_cast<u32x4*>(d)[j] = reinterpret_cast<const u32x4*>(q)[j];
     }
-    for (; j < np; j += nth) d[j] = ld_sys_u64(q + j);
-    if ((nbytes & 4) && tid == 0)
-      static_cast<uint32_t*>(dst)[nbytes / 4 - 1] = ld_sys_u32(static_cast<const uint32_t*>(src) + nbytes / 4 - 1);
+  } else if ((al & 7) == 0) {
+    const long long np = nbytes >> 3;
+    for (long long j = tid; j < np; j += nth)
+      reinterpret_cast<u64*>(d)[j] = PEER ? ld_sys_u64(q + 8 * j) : reinterpret_cast<const u64*>(q)[j];
   } else {
-    uint32_t* d = static_cast<uint32_t*>(dst);
-    const uint32_t* q = static_cast<const uint32_t*>(src);
-    for (long long j = tid; j < (nbytes >> 2); j += nth) d[j] = ld_sys_u32(q + j);
+    const long long np = nbytes >> 2;
+    for (long long j = tid; j < np; j += nth)
+      reinterpret_cast<uint32_t*>(d)[j] = PEER ? ld_sys_u32(q + 4 * j) : reinterpret_cast<const uint32_t*>(q)[j];
   }
 }
 
@@ -197,22 +236,20 @@ __device__ __forceinline__ void copy_peer(void* dst, const void* src, long long 
 template <typename T, int OP>
 __device__ void tail_reduce(const T* in, T* out, long long n, const Coll& c, u64 s, float scale) {
   typedef Ty<T> Y;
-  if constexpr (Y::N > 1) {
-    for (long long i = n / Y::N * Y::N; i < n; ++i) {
-      typename Y::A acc = 0;
-      for (int r = 0; r < c.W; ++r) {
-        const typename Y::A v = r == c.rank ? Y::get(in[i]) : Y::ld1(reinterpret_cast<const T*>(slot_in(c, r, s)) + i);
-        acc = r == 0 ? v : combine<OP>(acc, v);
-      }
-      if (OP == 0 && scale != 1.f) acc = (typename Y::A)(acc * scale);
-      out[i] = Y::put(acc);
+  for (long long i = n / Y::N * Y::N; i < n; ++i) {
+    typename Y::A acc = 0;
+    for (int r = 0; r < c.W; ++r) {
+      const typename Y::A v = r == c.rank ? Y::get(in[i]) : Y::ld1(reinterpret_cast<const T*>(slot_in(c, r, s)) + i);
+      acc = r == 0 ? v : combine<OP>(acc, v);
     }
+    if (OP == 0 && scale != 1.f) acc = (typename Y::A)(acc * scale);
+    out[i] = Y::put(acc);
   }
 }
 
 // ---------------------------------------------------------------- all-reduce
-// in / out 8-byte aligned; n * sizeof(T) a multiple of 4 (elements past the
-// last 8-byte packet go through tail_reduce).
+// in / out 16-byte aligned (elements past the last 16-byte packet go through
+// tail_reduce).
 template <typename T, int OP>
 __global__ __launch_bounds__(256) void allreduce_k(const T* __restrict__ in, T* __restrict__ out, long long n, Coll c,
                                                    float scale, int two_shot) {
@@ -222,9 +259,9 @@ __global__ __launch_bounds__(256) void allreduce_k(const T* __restrict__ in, T* 
   const u64 s = seq_of(c);
   const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x, nth = (long long)gridDim.x * blockDim.x;
   const long long np = n / N;
-  const u64* inp = reinterpret_cast<const u64*>(in);
-  u64* outp = reinterpret_cast<u64*>(out);
-  u64* mine = reinterpret_cast<u64*>(slot_in(c, c.rank, s));
+  const u32x4* inp = reinterpret_cast<const u32x4*>(in);
+  u32x4* outp = reinterpret_cast<u32x4*>(out);
+  u32x4* mine = reinterpret_cast<u32x4*>(slot_in(c, c.rank, s));
   for (long long j = tid; j < np; j += nth) mine[j] = inp[j];
   if (tid == 0)
     for (long long i = np * N; i < n; ++i) reinterpret_cast<T*>(mine)[i] = in[i];
@@ -232,12 +269,12 @@ __global__ __launch_bounds__(256) void allreduce_k(const T* __restrict__ in, T* 
   if (!wait_peers(c, 0, s)) return;
   if (tid == 0) tail_reduce<T, OP>(in, out, n, c, s, scale);
   const long long j0 = two_shot ? np * c.rank / c.W : 0, j1 = two_shot ? np * (c.rank + 1) / c.W : np;
-  u64* red = reinterpret_cast<u64*>(slot_red(c, c.rank, s));
+  u32x4* red = reinterpret_cast<u32x4*>(slot_red(c, c.rank, s));
   for (long long j = j0 + tid; j < j1; j += nth) {
-    u64 u[WMAX];
+    u32x4 u[WMAX];
 #pragma unroll
     for (int r = 0; r < WMAX; ++r)     // every peer's packet in flight before the combine
-      if (r < c.W) u[r] = r == c.rank ? inp[j] : ld_sys_u64(reinterpret_cast<const u64*>(slot_in(c, r, s)) + j);
+      if (r < c.W) u[r] = r == c.rank ? inp[j] : ld_peer16(c, slot_in(c, r, s), 16 * j);
     A acc[N], v[N];
     Y::unpack(u[0], acc);
 #pragma unroll
@@ -252,7 +289,7 @@ __global__ __launch_bounds__(256) void allreduce_k(const T* __restrict__ in, T* 
 #pragma unroll
       for (int i = 0; i < N; ++i) acc[i] = (A)(acc[i] * scale);
     }
-    const u64 pk = Y::pack(acc);
+    const u32x4 pk = Y::pack(acc);
     outp[j] = pk;
     if (two_shot) red[j] = pk;
   }
@@ -262,46 +299,54 @@ __global__ __launch_bounds__(256) void allreduce_k(const T* __restrict__ in, T* 
   for (int r = 0; r < c.W; ++r) {
     if (r == c.rank) continue;
     const long long a0 = np * r / c.W, a1 = np * (r + 1) / c.W;
-    copy_peer(outp + a0, reinterpret_cast<const u64*>(slot_red(c, r, s)) + a0, (a1 - a0) * 8, tid, nth);
+    copy_bytes<true>(c, outp + a0, slot_red(c, r, s) + 16 * a0, (a1 - a0) * 16, tid, nth);
   }
 }
 
 // ---------------------------------------------------------------- all-reduce mean + SGD
-// grad: this rank's flat fp32 gradient (n values, 8-byte aligned); every rank
+// grad: this rank's flat fp32 gradient (n values, 16-byte aligned); every rank
 // sums the W gradients in rank order, p -= lr * scale * sum in place, and bumps
 // global_step once.
+__device__ __forceinline__ void sgd_apply(const SgdArgs& a, long long i, float step, float g) {
+  int t = 0;
+  while (t < a.np - 1 && i >= a.end[t]) ++t;
+  const long long st = t == 0 ? 0 : a.end[t - 1];
+  float* p = a.p[t] + (i - st);
+  *p = *p - step * g;
+}
 __global__ __launch_bounds__(256) void reduce_sgd_k(const float* __restrict__ grad, long long n, Coll c, SgdArgs a) {
   const u64 s = seq_of(c);
   const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x, nth = (long long)gridDim.x * blockDim.x;
-  const long long np = (n + 1) / 2;    // the host pads the gradient to an even count
-  const u64* gp = reinterpret_cast<const u64*>(grad);
-  u64* mine = reinterpret_cast<u64*>(slot_in(c, c.rank, s));
+  const long long np = n / 4;
+  const u32x4* gp = reinterpret_cast<const u32x4*>(grad);
+  u32x4* mine = reinterpret_cast<u32x4*>(slot_in(c, c.rank, s));
   for (long long j = tid; j < np; j += nth) mine[j] = gp[j];
+  if (tid == 0)
+    for (long long i = 4 * np; i < n; ++i) reinterpret_cast<float*>(mine)[i] = grad[i];
   arrive(c, 0, s);
   if (!wait_peers(c, 0, s)) return;
   const float step = (a.lr_ptr != nullptr ? *a.lr_ptr : a.lr_val) * a.scale;
   for (long long j = tid; j < np; j += nth) {
-    u64 u[WMAX];
+    u32x4 u[WMAX];
 #pragma unroll
     for (int r = 0; r < WMAX; ++r)
-      if (r < c.W) u[r] = r == c.rank ? gp[j] : ld_sys_u64(reinterpret_cast<const u64*>(slot_in(c, r, s)) + j);
-    float g0 = 0.f, g1 = 0.f;
+      if (r < c.W) u[r] = r == c.rank ? gp[j] : ld_peer16(c, slot_in(c, r, s), 16 * j);
+    float g[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int r = 0; r < WMAX; ++r) {
       if (r < c.W) {
-        g0 += __uint_as_float((uint32_t)u[r]);
-        g1 += __uint_as_float((uint32_t)(u[r] >> 32));
+#pragma unroll
+        for (int h = 0; h < 4; ++h) g[h] += __uint_as_float(u[r][h]);
       }
     }
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const long long i = 2 * j + h;
-      if (i >= n) break;
-      int t = 0;
-      while (t < a.np - 1 && i >= a.end[t]) ++t;
-      const long long st = t == 0 ? 0 : a.end[t - 1];
-      float* p = a.p[t] + (i - st);
-      *p = *p - step * (h == 0 ? g0 : g1);
+    for (int h = 0; h < 4; ++h) sgd_apply(a, 4 * j + h, step, g[h]);
+  }
+  if (tid == 0) {
+    for (long long i = 4 * np; i < n; ++i) {
+      float g = 0.f;
+      for (int r = 0; r < c.W; ++r) g += r == c.rank ? grad[i] : ld_sys_f32(reinterpret_cast<const float*>(slot_in(c, r, s)) + i);
+      sgd_apply(a, i, step, g);
     }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0 && a.gstep != nullptr) {
@@ -325,12 +370,12 @@ __global__ __launch_bounds__(256) void broadcast_k(const void* in, void* out, lo
   const u64 s = seq_of(c);
   const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x, nth = (long long)gridDim.x * blockDim.x;
   if (c.rank == src) {
-    copy_local(slot_in(c, c.rank, s), in, nbytes, tid, nth);
-    if (out != in) copy_local(out, in, nbytes, tid, nth);
+    copy_bytes<false>(c, slot_in(c, c.rank, s), in, nbytes, tid, nth);
+    if (out != in) copy_bytes<false>(c, out, in, nbytes, tid, nth);
   }
   arrive(c, 0, s);
   if (!wait_peers(c, 0, s)) return;
-  if (c.rank != src) copy_peer(out, slot_in(c, src, s), nbytes, tid, nth);
+  if (c.rank != src) copy_bytes<true>(c, out, slot_in(c, src, s), nbytes, tid, nth);
 }
 
 // out + r * stride receives rank r's nbytes (stride = the whole per-rank size
@@ -339,12 +384,12 @@ __global__ __launch_bounds__(256) void allgather_k(const void* in, void* out, lo
                                                    Coll c) {
   const u64 s = seq_of(c);
   const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x, nth = (long long)gridDim.x * blockDim.x;
-  copy_local(slot_in(c, c.rank, s), in, nbytes, tid, nth);
-  copy_local(static_cast<char*>(out) + c.rank * stride, in, nbytes, tid, nth);
+  copy_bytes<false>(c, slot_in(c, c.rank, s), in, nbytes, tid, nth);
+  copy_bytes<false>(c, static_cast<char*>(out) + c.rank * stride, in, nbytes, tid, nth);
   arrive(c, 0, s);
   if (!wait_peers(c, 0, s)) return;
   for (int r = 0; r < c.W; ++r)
-    if (r != c.rank) copy_peer(static_cast<char*>(out) + r * stride, slot_in(c, r, s), nbytes, tid, nth);
+    if (r != c.rank) copy_bytes<true>(c, static_cast<char*>(out) + r * stride, slot_in(c, r, s), nbytes, tid, nth);
 }
 
 // ---------------------------------------------------------------- all-to-all
@@ -356,7 +401,7 @@ __global__ __launch_bounds__(256) void alltoall_k(const char* in, char* out, A2A
   const u64 s = seq_of(c);
   const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x, nth = (long long)gridDim.x * blockDim.x;
   const int par = (int)(s & 1);
-  if (!a.overflow) copy_local(slot_in(c, c.rank, s), in, a.send_total, tid, nth);
+  if (!a.overflow) copy_bytes<false>(c, slot_in(c, c.rank, s), in, a.send_total, tid, nth);
   if (blockIdx.x == 0 && threadIdx.x < WMAX) {
     ctl(c, c.rank, OFFS)[par * WMAX + threadIdx.x] = (u64)a.send_off[threadIdx.x];
     if (threadIdx.x == 0) ctl(c, c.rank, STAT)[par] = a.overflow ? 1ull : 0ull;
@@ -376,9 +421,9 @@ __global__ __launch_bounds__(256) void alltoall_k(const char* in, char* out, A2A
     }
     if (a.recv_bytes[r] == 0) continue;
     if (r == c.rank)
-      copy_local(out + a.recv_off[r], in + src_off[r], a.recv_bytes[r], tid, nth);
+      copy_bytes<false>(c, out + a.recv_off[r], in + src_off[r], a.recv_bytes[r], tid, nth);
     else
-      copy_peer(out + a.recv_off[r], slot_in(c, r, s) + src_off[r], a.recv_bytes[r], tid, nth);
+      copy_bytes<true>(c, out + a.recv_off[r], slot_in(c, r, s) + src_off[r], a.recv_bytes[r], tid, nth);
   }
 }
 

@@ -268,8 +268,7 @@ class _GradSync:
         self.params = params
         self.sizes = [p.numel() for p in params]
         self.n = sum(self.sizes)
-        # even allocation: the IPC kernels move 8-byte packets
-        self.flat = torch.zeros(self.n + (self.n & 1), dtype=torch.float32, device=params[0].device)
+        self.flat = torch.zeros(self.n, dtype=torch.float32, device=params[0].device)
         self.views = []
         off = 0
         for p, n in zip(params, self.sizes):

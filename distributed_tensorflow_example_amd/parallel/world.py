@@ -206,7 +206,7 @@ class World:
 
     @staticmethod
     def _aligned(t: torch.Tensor) -> bool:
-        return t.is_contiguous() and t.data_ptr() % 8 == 0
+        return t.is_contiguous() and t.data_ptr() % 16 == 0
 
     def all_reduce(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
         if self.world_size == 1:
@@ -235,10 +235,10 @@ class World:
 
     @staticmethod
     def _bytes_view(t: torch.Tensor):
-        """(contiguous, 8-byte aligned byte tensor padded to whole 4-byte words,
+        """(contiguous, 16-byte aligned byte tensor padded to whole 4-byte words,
         needs copy-back) for the IPC byte-copy collectives."""
         nb = t.numel() * t.element_size()
-        if t.is_contiguous() and t.data_ptr() % 8 == 0 and nb % 4 == 0:
+        if t.is_contiguous() and t.data_ptr() % 16 == 0 and nb % 4 == 0:
             return t.view(-1).view(torch.uint8) if t.dim() else t.reshape(1).view(torch.uint8), False
         tmp = torch.zeros(-(-nb // 4) * 4, dtype=torch.uint8, device=t.device)
         tmp[:nb].copy_(t.contiguous().reshape(-1).view(torch.uint8))

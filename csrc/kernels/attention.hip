@@ -1,3 +1,4 @@
+// Reached by: models/bert.py (BERT-base: bench_models.py --model bert_base); tests/test_transformer_gpu.py
 // Fused multi-head self-attention for BERT-shaped layers (head dim 64,
 // S <= 256, S % 32 == 0) on CDNA4 MFMA -- forward and backward.
 //

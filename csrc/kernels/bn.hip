@@ -1,3 +1,4 @@
+// Reached by: ops/bn.py FusedBatchNorm2d (ResNet-50: bench_models.py --model resnet50); tests/test_bn_gpu.py
 // Fused BatchNorm(+residual)(+ReLU) for NHWC (channels_last) bf16 activations
 // -- the ResNet-50 path (BASELINE config #3).  MIOpen's BN needs three
 // kernels forward/backward plus separate add / ReLU / ReLU-backward passes;

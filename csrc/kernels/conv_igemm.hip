@@ -1,3 +1,4 @@
+// Reached by: ops/conv.py ShadowConv2d (ResNet-50 convolutions); tests/test_conv_igemm_gpu.py
 // 3x3 (pad 1) and 1x1 (pad 0) convolutions, stride 1 or 2, on NHWC bf16
 // activations as implicit GEMMs on the gfx950 matrix cores, with an optional
 // BatchNorm statistics epilogue (ResNet-50, BASELINE.json configs[2]).  KS is

@@ -1,3 +1,4 @@
+// Reached by: ops.linear_act / ops.matmul (Wide&Deep tower, compat MatMul); tests/test_ops_gpu.py
 // Generic MFMA GEMM with a fused epilogue: C = act(alpha * op(A) op(B) + bias).
 // bf16 (or mixed) operands: 16x16x32 bf16 MFMA below; fp32 x fp32 with an fp32
 // output: the exact-f32 MFMA kernel at the end (no silent bf16 rounding).

@@ -1,3 +1,4 @@
+// Reached by: ops/big_gemm.py (BERT-base linears, ResNet-50 1x1 convs); tests/test_gemm_big_gpu.py
 // Large-tile bf16 MFMA GEMM for the transformer-size products (BERT-base:
 // T = B*S = 16384 token rows, 768 / 2304 / 3072 wide):
 //

@@ -1,3 +1,4 @@
+// Reached by: compat Session's lowered MLP step (compat/lowering.py GraphStepPlan: float feeds, other shapes, and N synchronous workers with the IPC reduce-SGD); tests/test_lowering_gpu.py, test_compat_ipc_gpu.py
 // fp32 lowering of the reference graph's training step, for the compat
 // Session (compat/lowering.py): the graph
 //   a2 = act(x W1 + b1); y = softmax(a2 W2 + b2)

@@ -1,3 +1,4 @@
+// Reached by: asynchronous (Hogwild) ps mode (parallel/async_ps.py, --update_mode=async); tests/test_async_ps_gpu.py
 // Asynchronous (Hogwild) parameter-server updates: the reference's default
 // update rule (example.py:64-118, between-graph replication with a plain
 // GradientDescentOptimizer and no SyncReplicasOptimizer: every worker reads the

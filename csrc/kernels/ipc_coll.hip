@@ -1,3 +1,4 @@
+// Reached by: parallel/world.py World GPU data plane (every collective on one node), compat N-worker MLP step; tests/test_ipc_coll_gpu.py, test_compat_ipc_gpu.py, test_sharded_ipc_gpu.py
 // Collectives over IPC-mapped peer buffers: the node's data plane without RCCL.
 //
 // Every rank exports ONE uncached (fine-grained) device buffer

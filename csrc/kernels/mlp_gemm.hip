@@ -1,3 +1,4 @@
+// Reached by: bench.py at per-GPU batch >= 256 (models/mlp.py GemmMLPTrainer); tests/test_mlp_gemm_gpu.py
 // Large-batch MLP step (784-100-10, example.py:69-128): four launches.
 //
 // The fused / persistent engines (mlp_step.hip, mlp_persist_f32.hip) are

@@ -1,3 +1,4 @@
+// Reached by: bench.py headline engine (PersistentMLPRunner), the resident Session engine (compat/resident.py), smoke(); tests/test_mlp_persist_gpu.py, test_resident_gpu.py
 // Persistent, weight-stationary training kernel for the reference's 784-100-10
 // MLP at the reference's precision: every product is an fp32 x fp32 MFMA
 // (v_mfma_f32_16x16x4_f32, bitwise an fmaf chain), fp32 accumulate, fp32

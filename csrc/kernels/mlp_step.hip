@@ -1,3 +1,4 @@
+// Reached by: models/mlp.py FusedMLPTrainer (bench.py 3-launch fallback chain, examples --fused, smoke()); tests/test_mlp_fused_gpu.py, test_ipc_gpu.py
 // Fused training step for the reference's 784-100-10 MLP
 // (reference: example.py:84-118 -- x*W1+b1 -> sigmoid -> *W2+b2 -> softmax ->
 // -sum(y log y_hat) mean -> GradientDescentOptimizer.minimize).

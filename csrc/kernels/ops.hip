@@ -1,3 +1,4 @@
+// Reached by: ops/__init__.py and optim/ (every model: xent, embedding bags, AUC, fused optimizers, DDP buckets); tests/test_ops_gpu.py
 // Fused elementwise / reduction / sparse kernels behind `distributed_tensorflow_example_amd.ops`
 // and `.optim`:
 //   act_backward      dZ = dY * act'(.)                    (SigmoidGrad / ReluGrad ...)

@@ -1,3 +1,4 @@
+// Reached by: ops/pool.py (ResNet-50 stem max pool); tests/test_vision_ops_gpu.py
 // Max pooling on NHWC bf16 activations (ResNet-50's 3x3 / stride-2 stem pool).
 //
 // torch's NHWC max-pool ran 125 us forward + 308 us backward per ResNet-50 step

@@ -1,3 +1,4 @@
+// Reached by: ops.philox_normal_ (sharded tables, compat random_normal init); tests/test_ops_gpu.py
 // Counter-based normal initialisation: tf.random_normal for device-resident
 // tables (reference: W = tf.Variable(tf.random_normal([F, 1])), lr2.py:384;
 // example.py:84-85).

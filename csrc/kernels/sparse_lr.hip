@@ -1,3 +1,4 @@
+// Reached by: one-GPU sparse LR step (csrc/bind_sparse.cpp SparseLRPlan: models/sparse_lr.py, the lr2 compat Session); tests/test_models_gpu.py, test_lowering_gpu.py
 // lr2.py's training step on ONE GPU as two kernels:
 //
 //   py_x  = embedding_lookup_sparse(W, ids, vals, 'sum') + b      (lr2.py:383-390)

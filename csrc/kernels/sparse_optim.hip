@@ -1,3 +1,4 @@
+// Reached by: sharded-table sparse optimizers (Wide&Deep sparse_opt=adagrad/rmsprop/momentum); tests/test_sparse_optim_gpu.py
 // Row-sparse optimizer updates of a sharded embedding table, on its owner
 // (parallel/sharded_embedding.py: ShardedEmbedding.set_optimizer).
 //

@@ -1,3 +1,4 @@
+// Reached by: sharded-table static routing (parallel/sharded_embedding.py _route_static); tests/test_models_gpu.py, test_sharded_ipc_gpu.py
 // Device-resident dedup + owner routing for the row-sharded tables
 // (parallel/sharded_embedding.py; reference: embedding_lookup_sparse on a
 // ps-placed W, lr2.py:383-390 -- the worker sends the batch's unique ids to

@@ -1,3 +1,4 @@
+// Reached by: ops/transformer.py (BERT-base elementwise / layernorm / softmax); tests/test_transformer_gpu.py
 // Fused transformer-block kernels for the BERT path (BASELINE config #4),
 // written for CDNA4: one wave64 per row, 8-byte bf16x4 vector accesses,
 // fp32 statistics, no LDS round-trips for row reductions.

@@ -18,11 +18,18 @@ RESIDENT engine (compat/resident.py): the persistent fp32 kernel
 (csrc/kernels/mlp_persist_f32.hip) stays launched across runs and each run is
 a pinned-memory doorbell -- no launch, no completion round trip.  Every other
 case (float feeds, other shapes or optimizers, several workers) is the
-launched fallback: three exact-fp32 MFMA kernels (csrc/kernels/graph_mlp.hip):
-forward, head + backward of layer 2, and the layer-1 weight gradient.  With GradientDescentOptimizer on one worker the
-SGD update and global_step += 1 happen inside those kernels; otherwise the
-kernels write the four gradients straight into the optimizer's all-reduce
-bucket and the usual sync + fused optimizer step follows.  The loss and
+launched plan: the exact-fp32 MFMA kernels of csrc/kernels/graph_mlp.hip
+(forward + head + backward of layer 2 in one launch, the layer-1 weight
+gradient in the second).  With GradientDescentOptimizer on one worker the
+SGD update and global_step += 1 happen inside those kernels.  With N
+synchronous workers on one node (example.py's ps/worker program as sync DP)
+the kernels write this worker's gradients and ONE more kernel all-reduces
+them with every worker's over the IPC data plane, in rank order, and applies
+SGD + global_step on the graph's variables (csrc/bind_mlp.cpp
+GraphStepPlan.attach_ipc, csrc/kernels/ipc_coll.hip reduce_sgd_k): no RCCL,
+no host round trip, bit-identical replicas.  Other optimizers write the
+gradients straight into the sync bucket (no copies) and the all-reduce +
+fused optimizer step follow.  The loss and
 accuracy of the run (pre-update, as TF evaluates them in the same run) are
 seeded into the run's memo, so summaries / cost fetches of the same run cost
 no extra kernels.

@@ -11,7 +11,8 @@ Cluster: `--ps_hosts/--worker_hosts` (comma lists) or `--cluster_conf` JSON
 
 What differs from the reference (README "semantics"):
 * workers train *synchronously* by default: every train_op run averages the
-  gradients of all workers (RCCL all-reduce on MI355X, gloo on CPU) -- the
+  gradients of all workers (on one MI355X node the IPC data plane: the lowered
+  step's last kernel all-reduces over xGMI and applies SGD; gloo on CPU) -- the
   SyncReplicasOptimizer path the reference left commented out
   (example.py:109-123); global_step counts sync steps.  `--update_mode=async`
   runs the reference's own asynchronous rule instead (Hogwild updates of shared

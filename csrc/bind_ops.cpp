@@ -451,21 +451,25 @@ std::vector<at::Tensor> sparse_route(at::Tensor sids, at::Tensor perm, int W, in
   at::Tensor dest = at::empty({W > 1 ? N : 0}, o32), send = at::empty({W > 1 ? (int64_t)W * cap : 0}, o64);
   at::Tensor count = at::empty({1}, o32);
   const int ids32 = sids.scalar_type() == at::kInt ? 1 : 0;
-  at::Tensor flag = at::empty({N}, o32);
-  at::Tensor onehot = at::empty({W > 1 ? N : 0, W}, o32);
-  ck(dtfk_route_flags(sids.data_ptr(), ids32, (int)N, W, flag.data_ptr<int>(), W > 1 ? onehot.data_ptr<int>() : nullptr,
+  // [flags | owner one-hot rows (W > 1)], owner-major, scanned flat in ONE pass
+  const int64_t nrow = W > 1 ? W + 1 : 1;
+  at::Tensor fl = at::empty({nrow * N}, o32);
+  ck(dtfk_route_flags(sids.data_ptr(), ids32, (int)N, W, fl.data_ptr<int>(), W > 1 ? fl.data_ptr<int>() + N : nullptr,
                       cs()),
      "route_flags");
-  at::Tensor incl = at::cumsum(flag, 0, at::kInt);                 // dedup index + 1
-  at::Tensor owncum = W > 1 ? at::cumsum(onehot, 0, at::kInt) : onehot;   // position among the owner's ids + 1
-  ck(dtfk_route_scatter(sids.data_ptr(), ids32, perm.data_ptr<int64_t>(), incl.data_ptr<int>(),
-                        W > 1 ? owncum.data_ptr<int>() : nullptr, (int)N, W, (int)cap, inv.data_ptr<int>(),
+  at::Tensor scan = at::cumsum(fl, 0, at::kInt);
+  ck(dtfk_route_scatter(sids.data_ptr(), ids32, perm.data_ptr<int64_t>(), scan.data_ptr<int>(),
+                        W > 1 ? scan.data_ptr<int>() + N : nullptr, (int)N, W, (int)cap, inv.data_ptr<int>(),
                         inverse.data_ptr<int64_t>(), uniq.data_ptr<int64_t>(), W > 1 ? dest.data_ptr<int>() : nullptr,
                         W > 1 ? send.data_ptr<int64_t>() : nullptr, count.data_ptr<int>(), cs()),
      "route_scatter");
-  // unique ids per owner (the last row of the per-owner inclusive scan): the
+  // unique ids per owner (differences of the scan at the row ends): the
   // caller's overflow test (> cap) and capacity adaptation, no host read-back
-  at::Tensor ocnt = W > 1 ? owncum.select(0, N - 1).contiguous() : count;
+  at::Tensor ocnt = count;
+  if (W > 1) {
+    at::Tensor ends = scan.view({nrow, N}).select(1, N - 1);
+    ocnt = (ends.slice(0, 1, nrow) - ends.slice(0, 0, nrow - 1)).contiguous();
+  }
   return {inv, inverse, uniq, dest, send, count, ocnt};
 }
 

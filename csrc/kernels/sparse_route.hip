@@ -39,10 +39,9 @@ __global__ __launch_bounds__(256) void route_flags(const ID* __restrict__ sids, 
   const ID v = sids[i];
   const int f = (i == 0 || v != sids[max(i - 1, 0)]) ? 1 : 0;
   flag[i] = f;
-  if (W > 1) {
+  if (W > 1) {   // owner-major rows [W][N] behind the flags: one flat scan covers them all
     const int o = (int)((int64_t)v % W);
-    int* row = onehot + (size_t)i * W;
-    for (int q = 0; q < W; ++q) row[q] = (f && q == o) ? 1 : 0;
+    for (int q = 0; q < W; ++q) onehot[(size_t)q * N + i] = (f && q == o) ? 1 : 0;
   }
 }
 
@@ -65,7 +64,9 @@ __global__ __launch_bounds__(256) void route_scatter(const ID* __restrict__ sids
     uniq[k] = (int64_t)v;
     if (W > 1) {
       const int o = (int)((int64_t)v % W);
-      const int pos = owncum[(size_t)i * W + o] - 1;     // rank among owner o's unique ids
+      // rank among owner o's unique ids: the flat inclusive scan of [flags | owner
+      // rows] minus the scan's value at the end of the previous row
+      const int pos = owncum[(long long)o * N + i] - owncum[(long long)o * N - 1] - 1;
       if (pos < cap) {
         const int d = o * cap + pos;
         dest[k] = d;
@@ -92,7 +93,7 @@ __global__ void fill_i64(int64_t* __restrict__ p, long long n, int64_t v) {
 
 extern "C" int dtfk_route_max_world() { return dtfk::route::MAXW; }
 
-// Pass 1: first-occurrence flags (+ owner one-hot rows [N][W] when W > 1).
+// Pass 1: first-occurrence flags (+ owner one-hot rows [W][N] when W > 1).
 extern "C" hipError_t dtfk_route_flags(const void* sids, int ids32, int N, int W, int* flag, int* onehot,
                                        hipStream_t stream) {
   using namespace dtfk::route;
@@ -106,7 +107,10 @@ extern "C" hipError_t dtfk_route_flags(const void* sids, int ids32, int N, int W
   return hipGetLastError();
 }
 
-// Pass 2 (after the inclusive scans incl = cumsum(flag), owncum = cumsum(onehot, 0)).
+// Pass 2 (after ONE flat inclusive scan of [flag (N) | owner rows (W x N)]:
+// incl = its first N values, owncum = the scan from the owner rows on -- a
+// per-column scan of an [N, W] one-hot (torch's outer-dimension scan) took
+// 15 ms at N = 131072, W = 2).
 extern "C" hipError_t dtfk_route_scatter(const void* sids, int ids32, const int64_t* perm, const int* incl,
                                          const int* owncum, int N, int W, int cap, int* inv_sorted, int64_t* inverse,
                                          int64_t* uniq, int* dest, int64_t* send, int* count, hipStream_t stream) {

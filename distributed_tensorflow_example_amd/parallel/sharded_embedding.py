@@ -535,9 +535,14 @@ def apply_sgd_shared(tables, ctx: LookupCtx, grads, lrs, grad_scale: float = 1.0
     if t0.W > 1:
         g = torch.cat(gs, 1) if len(gs) > 1 else gs[0]
         if ctx.static:
-            valid = (ctx.order >= 0).unsqueeze(1).to(g.dtype)
-            g_sorted = torch.zeros((sum(ctx.send), g.shape[1]), dtype=torch.float32, device=t0.device)
-            g_sorted.index_add_(0, ctx.order.clamp_min(0), g * valid)   # padding adds 0
+            # each live row has its own send slot (order = dest, unique), padding and
+            # overflowed rows (-1) go to a dump row past the end: a plain scatter
+            # copy (an atomic index_add_ of the [U, D] rows took 2.1 ms at B = 4096)
+            n_send = sum(ctx.send)
+            g_sorted = torch.zeros((n_send + 1, g.shape[1]), dtype=torch.float32, device=t0.device)
+            dump = torch.full_like(ctx.order, n_send)
+            g_sorted.index_copy_(0, torch.where(ctx.order >= 0, ctx.order, dump), g)
+            g_sorted = g_sorted[:n_send]
         else:
             g_sorted = g[ctx.order].contiguous()
         recv_g = torch.empty((sum(ctx.recv), g.shape[1]), dtype=torch.float32, device=t0.device)

@@ -47,6 +47,7 @@ hipError_t dtfk_mlp_ipc_reduce_apply(float* params, void* const* peer_table, int
                                      hipStream_t stream);
 long long dtfk_mlpf_stage_rec();
 void dtfk_mlpf_set_fault(int rank, long long step);
+void dtfk_mlpf_set_res_ts(long long* p);
 long long dtfk_mlpf_xbuf_bytes();
 long long dtfk_mlpf_ipc_bytes();
 int dtfk_mlpf_max_batch();
@@ -913,6 +914,8 @@ class ResidentMLPPlan {
     lrdev_ = at::zeros({1}, W1.options());
     metrics_ = at::zeros({2 * kRing}, W1.options());
     dctr_ = at::zeros({64}, W1.options().dtype(at::kInt));
+    const char* rs = std::getenv("DTF_RESIDENT_STAMPS");   // profiling: per-run device stamps
+    if (rs != nullptr && rs[0] == '1') res_ts_ = at::zeros({64 * 8}, W1.options().dtype(at::kLong));
     idle_ = (long long)(idle_s * 1e8);            // s_memrealtime: 100 MHz
     timeout_ = (long long)(timeout_s * 1e8);
     wait_s_ = std::max(5.0, 4.0 * idle_s + timeout_s);
@@ -1019,8 +1022,10 @@ class ResidentMLPPlan {
         __builtin_ia32_pause();
 #endif
       }
+      const double waited = std::chrono::duration<double, std::micro>(clk::now() - t1).count();
+      host_wait_[runs_ & 63] = waited;
       ++runs_;
-      t_[1] += std::chrono::duration<double, std::micro>(clk::now() - t1).count();
+      t_[1] += waited;
     }
     return true;
   }
@@ -1037,6 +1042,13 @@ class ResidentMLPPlan {
   bool alive() const { return alive_; }
   int64_t runs() const { return runs_; }
   int64_t launches() const { return launch_id_; }
+  // profiling (DTF_RESIDENT_STAMPS=1): device stamps [run % 64][8] and the host's
+  // door -> done wait of the same runs (us)
+  py::object stamps() const {
+    if (!res_ts_.defined()) return py::none();
+    return py::make_tuple(res_ts_.cpu(), at::from_blob(const_cast<double*>(host_wait_), {64},
+                                                       at::TensorOptions().dtype(at::kDouble)).clone());
+  }
   at::Tensor host_metrics() const {
     return at::from_blob(out_, {3}, at::TensorOptions().dtype(at::kFloat));
   }
@@ -1076,6 +1088,7 @@ class ResidentMLPPlan {
     hip_check(hipMemsetAsync(dctr_.data_ptr(), 0, dctr_.numel() * sizeof(int), st_), "ResidentMLPPlan: counters");
     if (__atomic_load_n(door_, __ATOMIC_ACQUIRE) < 0) __atomic_store_n(door_, runs_, __ATOMIC_RELEASE);   // after stop()
     ++launch_id_;
+    dtfk_mlpf_set_res_ts(res_ts_.defined() ? reinterpret_cast<long long*>(res_ts_.data_ptr<int64_t>()) : nullptr);
     hip_check(dtfk_mlp_persist_f32_resident(
                   stage_.data_ptr(), B_, W1_.data_ptr<float>(), W2_.data_ptr<float>(), b1_.data_ptr<float>(),
                   b2_.data_ptr<float>(), lrdev_.data_ptr<float>(), metrics_.data_ptr<float>(), kRing, act_,
@@ -1091,7 +1104,8 @@ class ResidentMLPPlan {
     alive_ = true;
   }
 
-  at::Tensor W1_, b1_, W2_, b2_, gstep_, stage_, xbuf_, seq_, kgstep_, err_, lrdev_, metrics_, dctr_;
+  at::Tensor W1_, b1_, W2_, b2_, gstep_, stage_, xbuf_, seq_, kgstep_, err_, lrdev_, metrics_, dctr_, res_ts_;
+  double host_wait_[64] = {0};
   int B_, act_, gkind_ = 0;
   bool naive_;
   int64_t rec_h_ = 0;
@@ -1126,7 +1140,8 @@ void init_mlp(py::module& m) {
       .def("runs", &ResidentMLPPlan::runs)
       .def("launches", &ResidentMLPPlan::launches)
       .def("host_metrics", &ResidentMLPPlan::host_metrics)
-      .def("timing", &ResidentMLPPlan::timing);
+      .def("timing", &ResidentMLPPlan::timing)
+      .def("stamps", &ResidentMLPPlan::stamps);
   py::class_<GraphStepPlan>(m, "GraphStepPlan")
       .def(py::init<at::Tensor, at::Tensor, at::Tensor, at::Tensor, c10::optional<at::Tensor>, int, int, bool, bool>(),
            py::arg("W1"), py::arg("b1"), py::arg("W2"), py::arg("b2"), py::arg("gstep"), py::arg("B"), py::arg("act"),

@@ -223,12 +223,19 @@ struct Args {
   void* gvar;               // the graph's global_step variable (kind 0 none, 1 f32, 2 i64, 3 i32, 4 f64)
   int gvar_kind;
   unsigned* dctr;           // device: [0] records staged, [8] runs released, [16] stop, [32] steps done
+  long long* res_ts;        // profiling only (DTF_RESIDENT_STAMPS): [run % 64][8] resident per-run stamps
   int dbg;                  // profiling only (DTF_PERSIST_DBG): bit 0 = never stage the next step's x (wrong
                             // numerics; what the per-step LDS-DMA stage costs the hand-offs), bit 1 = head
                             // sub-phase stamps (slots 13-15, wave 0), bits 2 / 3 = stage (half) after the
                             // first head, bit 4 = longer sleeps in the chunk polls (tuning)
 };
 
+// resident per-run stamp (s_memrealtime, 100 MHz) -- profiling only: 0 copier 0
+// saw the doorbell, 1 copier 0 staged its rows, 2 compute workgroup 0 saw the
+// whole record staged, 3 record in LDS / registers, 4 step math done, 5
+// variables written through, 6 every workgroup arrived, 7 done count published
+#define RTS(k, slot)                                                                             \
+  if (a.res_ts != nullptr) a.res_ts[((k) & 63) * 8 + (slot)] = (long long)__builtin_amdgcn_s_memrealtime();
 // phase stamp ph of step st (s_memrealtime, 100 MHz) -- profiling only
 #define PH(ph)                                                                                 \
   if (a.phase_ts != nullptr && lane == 0 && st < 64)                                         \
@@ -591,6 +598,7 @@ __device__ void copier_res(const Args& a, int cid, uint8_t* smem) {
         __builtin_amdgcn_s_sleep(1);
       }
       if (cid == 0 && !d) __hip_atomic_store(a.dctr + 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (cid == 0 && d) { RTS(k, 0); }
       *dec = d;
     }
     __syncthreads();
@@ -661,7 +669,10 @@ __device__ void copier_res(const Args& a, int cid, uint8_t* smem) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add(a.dctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) {
+      __hip_atomic_fetch_add(a.dctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (cid == 0) { RTS(k, 1); }
+    }
   }
   if (cid == 0 && tid == 0)   // no further run is taken by this launch
     __hip_atomic_store(a.host_state, a.launch_id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -896,6 +907,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
     }
     __syncthreads();
     if (*rflag == 0) return false;
+    if (c == 0 && tid == 0) { RTS(a.run0 + st, 2); }
     const auto rs = region_rsrc(a.stage + (long long)(st & 1) * REC, (int)REC);
     const int xr0 = 16 * tile0(q);
 #pragma unroll 4
@@ -920,6 +932,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
     __syncthreads();
     read_xf();
     read_xt();
+    if (c == 0 && tid == 0) { RTS(a.run0 + st, 3); }
     const float lr_run = *reinterpret_cast<const float*>(smem + L_LAB + RES_LR_BYTE);
     lrB = lr_run / (float)B;
     lrX = lrB * (1.f / 255.f);
@@ -1504,6 +1517,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
       // the last arriver (its add's return value says so) publishes the metrics,
       // global_step and the done count to pinned host memory
       __syncthreads();   // wave 7's LDS updates of W2 / b1 / b2 (and workgroup 0's metrics)
+      if (c == 0 && tid == 0) { RTS(a.run0 + st, 4); }
       write_params(true);
       // the graph's global_step: counted here (anything else that writes it stops
       // the engine first), stored write-through by workgroup 0
@@ -1517,6 +1531,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) {
+        if (c == 0) { RTS(a.run0 + st, 5); }
         __hip_atomic_fetch_add(a.dctr + 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (c == 0) {
           // workgroup 0 (it holds the metrics) publishes once all 28 have arrived
@@ -1528,12 +1543,14 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
               break;
             }
           }
+          RTS(a.run0 + st, 6);
           const float* mf = reinterpret_cast<const float*>(abort_flag);
           __hip_atomic_store(a.host_out, mf[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           __hip_atomic_store(a.host_out + 1, mf[5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           __hip_atomic_store(a.host_out + 2, (float)gsv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           __hip_atomic_store(a.host_done, a.run0 + st + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          RTS(a.run0 + st, 7);
         }
       }
     }
@@ -1600,6 +1617,10 @@ void dtfk_mlpf_set_fault(int rank, long long step) {
   g_fault_step = step;
 }
 
+// profiling only: the resident launches' per-run stamp ring (nullptr: off)
+static long long* g_res_ts = nullptr;
+void dtfk_mlpf_set_res_ts(long long* p) { g_res_ts = p; }
+
 long long dtfk_mlpf_stage_rec() { return dtfk::mlpf::REC; }
 long long dtfk_mlpf_xbuf_bytes() { return dtfk::mlpf::XBUF_BYTES; }
 long long dtfk_mlpf_ipc_bytes() { return dtfk::mlpf::IPC_BYTES; }
@@ -1614,6 +1635,7 @@ hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int n
   using namespace dtfk::mlpf;
   Args a;
   a.phase_ts = phase_ts;
+  a.res_ts = nullptr;
   a.stage = static_cast<const uint8_t*>(stage);
   a.rec_h = rec_h;
   a.B = B;
@@ -1750,6 +1772,7 @@ hipError_t dtfk_mlp_persist_f32_resident(void* stage, int B, float* W1, float* W
   a.gvar = gvar;
   a.gvar_kind = gvar_kind;
   a.dctr = dctr;
+  a.res_ts = g_res_ts;
   constexpr size_t lds = LDS_BYTES;
   typedef void (*Kern)(Args);
   static const Kern kerns[2] = {mlp_persist_f32<0, 1, true, true>, mlp_persist_f32<1, 1, true, true>};

@@ -16,12 +16,16 @@ ap.add_argument("trace")
 ap.add_argument("--steps", type=int, required=True, help="steps in the kept window (per-step averages)")
 ap.add_argument("--after-last", default="")
 ap.add_argument("--top", type=int, default=30)
+ap.add_argument("--tail-ms", type=float, default=0.0,
+                help="keep only kernels starting in the last T ms of the trace (a run's timed steps at its end)")
 a = ap.parse_args()
 rows = list(csv.DictReader(open(a.trace)))
 cut = 0
 if a.after_last:
     ends = [int(r["End_Timestamp"]) for r in rows if a.after_last in r["Kernel_Name"]]
     cut = max(ends) if ends else 0
+if a.tail_ms > 0 and rows:
+    cut = max(cut, max(int(r["End_Timestamp"]) for r in rows) - int(a.tail_ms * 1e6))
 tot, cnt = defaultdict(float), defaultdict(int)
 t0, t1 = None, 0
 for r in rows:

@@ -23,4 +23,11 @@ step prof_wd2b 500 rocprofv3 --kernel-trace --output-format csv -d $OUT/prof_wd2
 for f in $(find $OUT/prof_wd2b -name "*kernel_trace.csv"); do
   echo "== $f"; python3 scripts/prof_summary.py "$f" --steps 45 --top 25 | tee -a $OUT/prof_wd2b_summary.txt | head -14
 done
+rm -rf $OUT/prof_wd1b
+step prof_wd1b 400 rocprofv3 --kernel-trace --output-format csv -d $OUT/prof_wd1b -o run -- \
+  python3 scripts/bench_models.py --model wide_deep --graph --steps 200 --warmup 10
+f=$(find $OUT/prof_wd1b -name "*kernel_trace.csv" | head -n 1)
+python3 scripts/prof_summary.py "$f" --steps 150 --tail-ms 75 --top 45 > $OUT/prof_wd1b_summary.txt; head -50 $OUT/prof_wd1b_summary.txt
+step prof_resident 300 python scripts/prof_resident.py 2000
+step resident_tests 300 $PYT -x tests/test_resident_gpu.py
 exit 0

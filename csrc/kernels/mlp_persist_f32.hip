@@ -718,12 +718,30 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
   const int ft0 = tile0(q) + w, ft1 = tile0(q) + (tv1 ? w + 8 : 0);
   auto tvk = [=](int k) { return k ? tv1 : tv0; };
   auto ftk = [=](int k) { return k ? ft1 : ft0; };
+  // W1 slice: 16-byte loads of 4 consecutive hidden units of one feature row
+  // (the 16 lanes of a lane group cover a 4-row x 16-unit block: 4 cache lines
+  // per load), transposed across those lanes after the prologue's drain so lane
+  // (r, g) holds unit 16j + r of rows 4g..4g+3 -- the accumulator layout of dW1.
+  // (4-byte column loads touched 64 lines per wave instruction: ~2 us of issue
+  // at the top of every launch.)
+  // (RES keeps the column loads: the transposes' registers spill there, and its
+  // prologue runs once per idle period, not once per timed launch)
   float Wt[NTW][4];
+  f32x4 wld[NTW];
+  if constexpr (RES) {
 #pragma unroll
-  for (int k = 0; k < NTW; ++k)
+    for (int k = 0; k < NTW; ++k)
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
-      Wt[k][e] = (tvk(k) && hv) ? a.params[(16 * ftk(k) + 4 * g + e) * HID + hid] : 0.f;
+      for (int e = 0; e < 4; ++e)
+        Wt[k][e] = (tvk(k) && hv) ? a.params[(16 * ftk(k) + 4 * g + e) * HID + hid] : 0.f;
+  } else {
+    const int u0 = 16 * j + 4 * (r & 3);           // units 4(r&3)..+3 of block j, row 4g + (r >> 2)
+#pragma unroll
+    for (int k = 0; k < NTW; ++k)
+      wld[k] = (tvk(k) && u0 < HID)
+                   ? *reinterpret_cast<const f32x4*>(a.params + (16 * ftk(k) + 4 * g + (r >> 2)) * HID + u0)
+                   : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   float pv = 0.f;   // this thread's W2 / b1 / b2 entry (threads < 288)
   if (tid < 256) {
     const int n = tid >> 4, cl = tid & 15;
@@ -866,6 +884,24 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
     reinterpret_cast<int*>(smem + L_HFLAG)[tid - 296] = 0;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // parameter loads + the first stage landed
+  // the 4x4 transposes of the W1 blocks in 4 rounds of one lane permute:
+  // in round t the lane that loaded row e_s offers component (e_s + t) & 3, and
+  // lane r (unit 4b + m) takes row (m - t) & 3 from lane 4((m - t) & 3) + b --
+  // which offers exactly component m
+#pragma unroll
+  for (int k = 0; k < NTW && !RES; ++k) {
+    const int m = r & 3, b = r >> 2;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int cs = (b + t) & 3;          // as a source: this lane loaded row b (= r >> 2)
+      const float v = cs == 0 ? wld[k][0] : (cs == 1 ? wld[k][1] : (cs == 2 ? wld[k][2] : wld[k][3]));
+      const int e = (m - t) & 3;
+      const float got = __shfl(v, 16 * g + 4 * e + b);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (q == e) Wt[k][q] = got;
+    }
+  }
   __syncthreads();
   float lrB = lr / (float)(B * (MULTI ? a.W : 1));   // RES: per run (the record's lr)
   float lrX = lrB * (1.f / 255.f);

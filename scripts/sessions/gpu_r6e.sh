@@ -30,4 +30,7 @@ f=$(find $OUT/prof_wd1b -name "*kernel_trace.csv" | head -n 1)
 python3 scripts/prof_summary.py "$f" --steps 150 --tail-ms 75 --top 45 > $OUT/prof_wd1b_summary.txt; head -50 $OUT/prof_wd1b_summary.txt
 step prof_resident 300 python scripts/prof_resident.py 2000
 step resident_tests 300 $PYT -x tests/test_resident_gpu.py
+step persist_tests 600 $PYT -x tests/test_mlp_persist_gpu.py -k "not same_gpu and not two_ranks and not eight and not five_six"
+step phases 300 python scripts/prof_persist_f32.py fp32
+for i in 1 2 3; do step bench20_$i 180 python bench.py --gpus 1 --steps 20 --warmup 5; done
 exit 0

@@ -50,7 +50,12 @@ hipError_t dtfk_gemm_big_cfg(int cfg, const void* A, int lda, const void* B, int
                              int K, hipStream_t stream);
 hipError_t dtfk_act_backward(const float* dy, const float* y, const float* z, float* dz, int64_t n, int act,
                              hipStream_t s);
-hipError_t dtfk_col_sum(const float* X, float* out, int M, int N, hipStream_t s);
+hipError_t dtfk_col_sum(const float* X, float* out, int M, int N, int accum, hipStream_t s);
+hipError_t dtfk_logit3_xent(const float* a, const float* b, const float* bias, const float* t, float* loss,
+                            float* dz, int n, hipStream_t s);
+hipError_t dtfk_logit3_xent_bwd(const float* dz, const float* g, float* d, float* gbias, int accum, int n,
+                                hipStream_t s);
+hipError_t dtfk_multi_copy(const void* const* src, void* const* dst, const long long* bytes, int n, hipStream_t s);
 hipError_t dtfk_softmax_xent(const float* logits, const int64_t* labels, const float* ydense, float* loss_rows,
                              float* grad, int64_t* correct, int B, int C, float grad_scale, int naive,
                              hipStream_t s);
@@ -277,11 +282,46 @@ void act_backward(at::Tensor dy, c10::optional<at::Tensor> y, c10::optional<at::
      "act_backward");
 }
 
-void col_sum(at::Tensor X, at::Tensor out) {
+// Wide&Deep head (fused): loss[0] = mean xent(a + b + bias[0], t), dz
+void logit3_xent(at::Tensor a, at::Tensor b, at::Tensor bias, at::Tensor t, at::Tensor loss, at::Tensor dz) {
+  f32c(a, "a"); f32c(b, "b"); f32c(bias, "bias"); f32c(t, "t"); f32c(loss, "loss"); f32c(dz, "dz");
+  const int64_t n = a.numel();
+  if (b.numel() != n || t.numel() != n || dz.numel() != n || bias.numel() < 1 || loss.numel() < 1)
+    throw std::runtime_error("logit3_xent: size mismatch");
+  ck(dtfk_logit3_xent(a.data_ptr<float>(), b.data_ptr<float>(), bias.data_ptr<float>(), t.data_ptr<float>(),
+                      loss.data_ptr<float>(), dz.data_ptr<float>(), (int)n, cs()),
+     "logit3_xent");
+}
+void logit3_xent_bwd(at::Tensor dz, at::Tensor g, at::Tensor d, c10::optional<at::Tensor> gbias, bool accumulate) {
+  f32c(dz, "dz"); f32c(g, "g"); f32c(d, "d");
+  if (gbias.has_value()) f32c(*gbias, "gbias");
+  ck(dtfk_logit3_xent_bwd(dz.data_ptr<float>(), g.data_ptr<float>(), d.data_ptr<float>(),
+                          gbias.has_value() ? gbias->data_ptr<float>() : nullptr, accumulate ? 1 : 0, (int)dz.numel(), cs()),
+     "logit3_xent_bwd");
+}
+// dst[i].copy_(src[i]) for up to 8 contiguous same-size pairs in one launch
+void multi_copy(std::vector<at::Tensor> dst, std::vector<at::Tensor> src) {
+  if (dst.size() != src.size() || dst.empty() || dst.size() > 8) throw std::runtime_error("multi_copy: 1..8 pairs");
+  const void* sp[8];
+  void* dp[8];
+  long long nb[8];
+  for (size_t i = 0; i < dst.size(); ++i) {
+    gpu(dst[i], "dst"); gpu(src[i], "src");
+    if (!dst[i].is_contiguous() || !src[i].is_contiguous() || dst[i].scalar_type() != src[i].scalar_type() ||
+        dst[i].numel() != src[i].numel())
+      throw std::runtime_error("multi_copy: contiguous pairs of one dtype and size expected");
+    sp[i] = src[i].data_ptr();
+    dp[i] = dst[i].data_ptr();
+    nb[i] = (long long)(src[i].numel() * src[i].element_size());
+  }
+  ck(dtfk_multi_copy(sp, dp, nb, (int)dst.size(), cs()), "multi_copy");
+}
+
+void col_sum(at::Tensor X, at::Tensor out, bool accumulate) {
   f32c(X, "X"); f32c(out, "out");
   const int N = (int)X.size(-1);
   const int M = (int)(X.numel() / std::max<int64_t>(1, N));
-  ck(dtfk_col_sum(X.data_ptr<float>(), out.data_ptr<float>(), M, N, cs()), "col_sum");
+  ck(dtfk_col_sum(X.data_ptr<float>(), out.data_ptr<float>(), M, N, accumulate ? 1 : 0, cs()), "col_sum");
 }
 
 static void bf16xent_check(const at::Tensor& logits, const c10::optional<at::Tensor>& bias, const at::Tensor& labels) {
@@ -598,7 +638,10 @@ void init_ops(py::module& m) {
   m.def("gemm_gelu_aux", &gemm_gelu_aux, py::arg("A"), py::arg("transA"), py::arg("B"), py::arg("transB"),
         py::arg("out"), py::arg("aux"), py::arg("bias"));
   m.def("act_backward", &act_backward);
-  m.def("col_sum", &col_sum);
+  m.def("col_sum", &col_sum, py::arg("X"), py::arg("out"), py::arg("accumulate") = false);
+  m.def("logit3_xent", &logit3_xent);
+  m.def("logit3_xent_bwd", &logit3_xent_bwd);
+  m.def("multi_copy", &multi_copy);
   m.def("softmax_xent", &softmax_xent);
   m.def("xent_fwd_bf16", &xent_fwd_bf16);
   m.def("xent_bwd_bf16", &xent_bwd_bf16);

@@ -41,7 +41,7 @@ __global__ void act_backward(const float* __restrict__ dy, const float* __restri
 // out[n] = sum_m X[m, n] (X row-major [M, N]); block = 256 threads covers 64
 // columns x 4 row-groups, grid.y splits rows, partials atomically added.
 __global__ void col_sum(const float* __restrict__ X, float* __restrict__ out, int M, int N,
-                        int rows_per_block) {
+                        int rows_per_block, int accum) {
   __shared__ float red[4][64];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int g = threadIdx.x >> 6;
@@ -53,7 +53,7 @@ __global__ void col_sum(const float* __restrict__ X, float* __restrict__ out, in
   __syncthreads();
   if (g == 0 && c < N) {
     const float t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-    if (gridDim.y == 1) out[c] = t;
+    if (gridDim.y == 1) out[c] = accum ? out[c] + t : t;
     else atomicAdd(&out[c], t);
   }
 }
@@ -64,7 +64,7 @@ __global__ void col_sum(const float* __restrict__ X, float* __restrict__ out, in
 // scalar loads was 15 us latency-bound; 256 row chunks of atomics on the same
 // 512 addresses, 26 us contention-bound).
 __global__ void col_sum4(const float4* __restrict__ X, float* __restrict__ out, int M, int N4,
-                         int rows_per_block) {
+                         int rows_per_block, int accum) {
   __shared__ float4 red[16][16];
   const int cl = threadIdx.x & 15, g = threadIdx.x >> 4;
   const int c = blockIdx.x * 16 + cl;
@@ -95,6 +95,10 @@ __global__ void col_sum4(const float4* __restrict__ X, float* __restrict__ out, 
     }
     float* o = out + 4 * c;
     if (gridDim.y == 1) {
+      if (accum) {
+        const float4 p = *reinterpret_cast<const float4*>(o);
+        t.x += p.x; t.y += p.y; t.z += p.z; t.w += p.w;
+      }
       *reinterpret_cast<float4*>(o) = t;
     } else {
       atomicAdd(o, t.x); atomicAdd(o + 1, t.y); atomicAdd(o + 2, t.z); atomicAdd(o + 3, t.w);
@@ -243,6 +247,66 @@ __global__ void sigmoid_xent(const float* __restrict__ x, const float* __restric
     const float v = x[i], z = t[i];
     loss[i] = fmaxf(v, 0.f) - v * z + log1pf(__expf(-fabsf(v)));
     if (grad) grad[i] = (1.f / (1.f + __expf(-v)) - z) * grad_scale;
+  }
+}
+
+// Wide&Deep head, one workgroup: z = a[i] + b[i] + bias[0] (the wide part, the
+// tower's output, the shared bias), loss = mean sigmoid-xent(z, t) and
+// dz = (sigmoid(z) - t) / B -- the two adds, the xent and its mean of the
+// unfused graph in one launch.
+__global__ __launch_bounds__(1024) void logit3_xent(const float* __restrict__ a, const float* __restrict__ b,
+                                                    const float* __restrict__ bias, const float* __restrict__ t,
+                                                    float* __restrict__ loss, float* __restrict__ dz, int n) {
+  __shared__ float scratch[16];
+  const float c = bias[0], inv = 1.f / (float)n;
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const float v = a[i] + b[i] + c, z = t[i];
+    s += fmaxf(v, 0.f) - v * z + log1pf(__expf(-fabsf(v)));
+    dz[i] = (1.f / (1.f + __expf(-v)) - z) * inv;
+  }
+  s = block_sum(s, scratch);
+  if (threadIdx.x == 0) loss[0] = s * inv;
+}
+// its backward: d = dz * g (the gradient of both summands) and the bias
+// gradient sum(d), stored or added to the bias's .grad (accum)
+__global__ __launch_bounds__(1024) void logit3_xent_bwd(const float* __restrict__ dz, const float* __restrict__ g,
+                                                        float* __restrict__ d, float* __restrict__ gbias, int accum,
+                                                        int n) {
+  __shared__ float scratch[16];
+  const float gs = g[0];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const float v = dz[i] * gs;
+    d[i] = v;
+    s += v;
+  }
+  s = block_sum(s, scratch);
+  if (threadIdx.x == 0 && gbias != nullptr) gbias[0] = accum ? gbias[0] + s : s;
+}
+
+// Up to 8 device-to-device copies in one launch (a captured step's input
+// refresh: one kernel instead of a copy-engine blit per input).
+struct CopyList {
+  const char* src[8];
+  char* dst[8];
+  long long bytes[8];
+  int n;
+};
+__global__ __launch_bounds__(256) void multi_copy(CopyList c) {
+  const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x, nth = (long long)gridDim.x * blockDim.x;
+  for (int k = 0; k < c.n; ++k) {
+    const char* s = c.src[k];
+    char* d = c.dst[k];
+    const long long nb = c.bytes[k];
+    if (((reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(d)) & 15) == 0) {
+      const long long n16 = nb >> 4;
+      for (long long j = tid; j < n16; j += nth)
+        reinterpret_cast<uint4*>(d)[j] = reinterpret_cast<const uint4*>(s)[j];
+      for (long long j = (n16 << 4) + tid; j < nb; j += nth) d[j] = s[j];
+    } else {
+      for (long long j = tid; j < nb; j += nth) d[j] = s[j];
+    }
   }
 }
 
@@ -684,7 +748,8 @@ hipError_t dtfk_act_backward(const float* dy, const float* y, const float* z, fl
   hipLaunchKernelGGL(act_backward, dim3(nblk(n)), dim3(256), 0, s, dy, y, z, dz, n, act);
   return hipGetLastError();
 }
-hipError_t dtfk_col_sum(const float* X, float* out, int M, int N, hipStream_t s) {
+// accum: out += the column sums (a gradient sunk into .grad) instead of out =
+hipError_t dtfk_col_sum(const float* X, float* out, int M, int N, int accum, hipStream_t s) {
   if (M <= 0 || N <= 0) return hipSuccess;
   const bool vec = N % 4 == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0;
   const int bx = vec ? (N / 4 + 15) / 16 : (N + 63) / 64;
@@ -692,15 +757,15 @@ hipError_t dtfk_col_sum(const float* X, float* out, int M, int N, hipStream_t s)
   int gy = std::max(1, std::min(std::min(32, (M + 63) / 64), 256 / bx));
   const int rows_per_block = ((M + gy - 1) / gy + 15) / 16 * 16;
   gy = (M + rows_per_block - 1) / rows_per_block;
-  if (gy > 1) {
+  if (gy > 1 && !accum) {
     const hipError_t e = dtfk::zero2d_f32(out, N, 1, N, s);   // a kernel: replays from hipGraphs (common.h)
     if (e != hipSuccess) return e;
   }
   if (vec)
     hipLaunchKernelGGL(col_sum4, dim3(bx, gy), dim3(256), 0, s, reinterpret_cast<const float4*>(X), out, M, N / 4,
-                       rows_per_block);
+                       rows_per_block, accum);
   else
-    hipLaunchKernelGGL(col_sum, dim3(bx, gy), dim3(256), 0, s, X, out, M, N, rows_per_block);
+    hipLaunchKernelGGL(col_sum, dim3(bx, gy), dim3(256), 0, s, X, out, M, N, rows_per_block, accum);
   return hipGetLastError();
 }
 hipError_t dtfk_softmax_xent(const float* logits, const int64_t* labels, const float* ydense, float* loss_rows,
@@ -722,6 +787,31 @@ hipError_t dtfk_xent_bwd_bf16(const void* logits, const float* bias, const int64
   if (C % 2) return hipErrorInvalidValue;
   hipLaunchKernelGGL(xent_bwd_bf16, dim3(B), dim3(256), 0, s, (const uint16_t*)logits, bias, labels, lse_rows, dloss,
                      (uint16_t*)grad, C, scale);
+  return hipGetLastError();
+}
+hipError_t dtfk_logit3_xent(const float* a, const float* b, const float* bias, const float* t, float* loss,
+                            float* dz, int n, hipStream_t s) {
+  hipLaunchKernelGGL(logit3_xent, dim3(1), dim3(1024), 0, s, a, b, bias, t, loss, dz, n);
+  return hipGetLastError();
+}
+hipError_t dtfk_logit3_xent_bwd(const float* dz, const float* g, float* d, float* gbias, int accum, int n,
+                                hipStream_t s) {
+  hipLaunchKernelGGL(logit3_xent_bwd, dim3(1), dim3(1024), 0, s, dz, g, d, gbias, accum, n);
+  return hipGetLastError();
+}
+hipError_t dtfk_multi_copy(const void* const* src, void* const* dst, const long long* bytes, int n, hipStream_t s) {
+  if (n < 1 || n > 8) return hipErrorInvalidValue;
+  CopyList c{};
+  long long most = 0;
+  for (int k = 0; k < n; ++k) {
+    c.src[k] = static_cast<const char*>(src[k]);
+    c.dst[k] = static_cast<char*>(dst[k]);
+    c.bytes[k] = bytes[k];
+    most = bytes[k] > most ? bytes[k] : most;
+  }
+  c.n = n;
+  const long long blocks = (most / 16 + 255) / 256;
+  hipLaunchKernelGGL(multi_copy, dim3((unsigned)(blocks < 1 ? 1 : (blocks > 1024 ? 1024 : blocks))), dim3(256), 0, s, c);
   return hipGetLastError();
 }
 hipError_t dtfk_sigmoid_xent(const float* x, const float* t, float* loss, float* grad, int64_t n,

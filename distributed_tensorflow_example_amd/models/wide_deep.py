@@ -31,6 +31,10 @@ from ..parallel.sharded_embedding import (ShardedEmbedding, StaticStepMixin, app
 from ..parallel.world import World, get_world
 
 
+def _no_sink_hook(p):
+    """grad_sink's readiness callback: the tower's bucket is reduced after backward."""
+
+
 class WideDeep(StaticStepMixin):
     def __init__(self, num_features: int, emb_dim: int = 64, hidden: Sequence[int] = (256, 128),
                  lr: float = 0.05, dense_lr: Optional[float] = None, dense_opt: str = "sgd", combiner: str = "sum",
@@ -70,6 +74,10 @@ class WideDeep(StaticStepMixin):
         off = 0
         for p in self.dense_params:                   # grads are views of one bucket
             p.grad = self.flat_grad[off:off + p.numel()].view_as(p)
+            # the tower's backward kernels accumulate straight into these views
+            # (ops/grad_sink.py: no zeroed temporaries, no AccumulateGrad adds);
+            # flat_grad is zeroed once per step
+            p._dtf_sink_hook = _no_sink_hook
             off += p.numel()
         dl = self.lr if dense_lr is None else float(dense_lr)
         self.opt = optim.FusedAdam(self.dense_params, dl) if dense_opt == "adam" else \
@@ -87,6 +95,12 @@ class WideDeep(StaticStepMixin):
         self._graphed = None
 
     def forward(self, labels, offsets, ids, vals, exact: bool = False):
+        wide, h, extras = self.forward_parts(labels, offsets, ids, vals, exact)
+        return wide + h + self.bias, extras
+
+    def forward_parts(self, labels, offsets, ids, vals, exact: bool = False):
+        """(wide part, tower output, (rows, rows, routing)) -- the logit is their
+        sum + the shared bias."""
         # both tables read the same ids over the same row partition: one
         # dedup + id exchange, one row exchange carrying [U, 1 + D]
         ctx = self.wide.route(ids, capacity=self.ids_capacity, exact=exact)
@@ -101,8 +115,7 @@ class WideDeep(StaticStepMixin):
         nl = len(self.layers) // 2
         for i in range(nl):
             h = ops.linear_act(h, self.layers[2 * i], self.layers[2 * i + 1], "relu" if i < nl - 1 else "none")
-        logit = wide + h + self.bias
-        return logit, (wrows, erows, ctx)
+        return wide, h, (wrows, erows, ctx)
 
     def _static_batch(self, batch):
         labels, offsets, ids, vals = batch.to(self.device) if hasattr(batch, "to") else batch
@@ -160,8 +173,8 @@ class WideDeep(StaticStepMixin):
     def _train_step(self, batch, exact: bool = False) -> torch.Tensor:
         labels, offsets, ids, vals = batch.to(self.device) if hasattr(batch, "to") else batch
         self.flat_grad.zero_()
-        logit, (wrows, erows, lctx) = self.forward(labels, offsets, ids, vals, exact)
-        loss = ops.sigmoid_xent(logit, labels)
+        wide, h, (wrows, erows, lctx) = self.forward_parts(labels, offsets, ids, vals, exact)
+        loss = ops.logit3_xent(wide, h, self.bias, labels)      # the head's adds + xent + mean: one kernel
         loss.backward()
         ws = self.world.world_size
         # dense tower: one flat all-reduce, overlapped with the sparse exchanges

@@ -73,6 +73,7 @@ class _LinearAct(torch.autograd.Function):
         ctx.save_for_backward(x2, w, y if z is None else z)
         ctx.act = ACT[act]
         ctx.has_b = b is not None
+        ctx.b = b
         ctx.xshape = x.shape
         return y.reshape(*x.shape[:-1], N)
 
@@ -94,12 +95,24 @@ class _LinearAct(torch.autograd.Function):
             gx = torch.empty((dz.shape[0], w.shape[0]), dtype=torch.float32, device=dz.device)
             C.gemm(dz, False, w.contiguous(), True, gx, None, 0, 1.0, 0.0, None)   # dZ W^T
             gx = gx.reshape(ctx.xshape)
+        from . import grad_sink
         if ctx.needs_input_grad[1]:
-            gw = torch.empty_like(w, dtype=torch.float32)
-            C.gemm(x2, True, dz, False, gw, None, 0, 1.0, 0.0, None)                # X^T dZ
+            if grad_sink.all_enabled(w):
+                # sunk: X^T dZ accumulated straight into w.grad (beta = 1: no zeroed
+                # temporary, no AccumulateGrad add)
+                C.gemm(x2, True, dz, False, grad_sink.target(w), None, 0, 1.0, 1.0, None)
+                grad_sink.done(w)
+            else:
+                gw = torch.empty_like(w, dtype=torch.float32)
+                C.gemm(x2, True, dz, False, gw, None, 0, 1.0, 0.0, None)                # X^T dZ
         if ctx.has_b and ctx.needs_input_grad[2]:
-            gb = torch.empty(w.shape[1], dtype=torch.float32, device=dz.device)
-            C.col_sum(dz, gb)
+            b = ctx.b
+            if grad_sink.all_enabled(b):
+                C.col_sum(dz, grad_sink.target(b), True)
+                grad_sink.done(b)
+            else:
+                gb = torch.empty(w.shape[1], dtype=torch.float32, device=dz.device)
+                C.col_sum(dz, gb)
         return gx, gw, gb, None
 
 
@@ -214,6 +227,59 @@ class _SigmoidXent(torch.autograd.Function):
     def backward(ctx, g):
         (grad,) = ctx.saved_tensors
         return grad * g, None, None
+
+
+class _Logit3Xent(torch.autograd.Function):
+    """mean sigmoid-xent(a + b + bias, t) in one kernel, backward in one more
+    (the bias gradient stored, or sunk into bias.grad: ops/grad_sink.py)."""
+
+    @staticmethod
+    def forward(ctx, a, b, bias, t):
+        C = _C()
+        af, bf = a.contiguous().float().reshape(-1), b.contiguous().float().reshape(-1)
+        loss = torch.empty(1, dtype=torch.float32, device=a.device)
+        dz = torch.empty_like(af)
+        C.logit3_xent(af, bf, bias.contiguous().float().reshape(-1), t.contiguous().float().reshape(-1), loss, dz)
+        ctx.save_for_backward(dz)
+        ctx.bias = bias
+        ctx.shapes = (a.shape, b.shape)
+        return loss.reshape(())
+
+    @staticmethod
+    def backward(ctx, g):
+        from . import grad_sink
+        (dz,) = ctx.saved_tensors
+        d = torch.empty_like(dz)
+        bias = ctx.bias
+        sink = ctx.needs_input_grad[2] and grad_sink.all_enabled(bias)
+        gb = None
+        if sink:
+            _C().logit3_xent_bwd(dz, g.contiguous().float().reshape(1), d, grad_sink.target(bias), True)
+            grad_sink.done(bias)
+        else:
+            gb = torch.empty(1, dtype=torch.float32, device=dz.device) if ctx.needs_input_grad[2] else None
+            _C().logit3_xent_bwd(dz, g.contiguous().float().reshape(1), d, gb, False)
+            gb = None if gb is None else gb.reshape(bias.shape)
+        return d.view(ctx.shapes[0]), d.view(ctx.shapes[1]), gb, None
+
+
+def logit3_xent(a, b, bias, targets):
+    """mean(sigmoid_cross_entropy_with_logits(a + b + bias, targets)) -- the
+    Wide&Deep head (wide part + tower output + shared bias) fused."""
+    if not a.is_cuda:
+        return sigmoid_xent(a + b + bias, targets)
+    return _Logit3Xent.apply(a, b, bias, targets)
+
+
+def multi_copy_(dsts, srcs):
+    """dst.copy_(src) for every pair, one kernel on the GPU (contiguous pairs of
+    one dtype / size, at most 8); elementwise copies otherwise."""
+    if (dsts and all(d.is_cuda and s.is_cuda and d.is_contiguous() and s.is_contiguous() and d.dtype == s.dtype
+                     and d.numel() == s.numel() for d, s in zip(dsts, srcs)) and len(dsts) <= 8):
+        _C().multi_copy(list(dsts), list(srcs))
+        return
+    for d, s in zip(dsts, srcs):
+        d.copy_(s, non_blocking=True)
 
 
 def sigmoid_xent(logits, targets, reduction: str = "mean"):

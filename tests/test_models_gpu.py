@@ -150,6 +150,37 @@ def test_wide_deep_graphed_step_matches_eager(native):
         assert torch.allclose(a, b, atol=1e-5)
 
 
+def test_wide_deep_gpu_step_matches_cpu_reference(native):
+    """The GPU step -- fused head (wide + tower + bias, xent, mean: one kernel
+    forward, one backward), tower weight / bias gradients accumulated straight
+    into the flat gradient bucket, sparse SGD of both tables, fused Adam --
+    against the same model on the CPU (plain torch autograd and ops), same
+    Philox / generator initialisation, 4 steps."""
+    from distributed_tensorflow_example_amd.models.wide_deep import WideDeep
+    from distributed_tensorflow_example_amd.parallel.world import World
+
+    F, B, nnz = 20_000, 128, 6
+    gen = torch.Generator().manual_seed(7)
+    batches = []
+    for _ in range(4):
+        ids = torch.randint(0, F, (B * nnz,), generator=gen)
+        offs = torch.arange(0, B * nnz + 1, nnz)
+        vals = torch.rand(B * nnz, generator=gen)
+        lab = (torch.rand(B, 1, generator=gen) < 0.3).float()
+        batches.append((lab, offs, ids, vals))
+    mk = lambda dev: WideDeep(F, emb_dim=16, hidden=(64, 32), lr=0.3, dense_opt="adam", dense_lr=0.01,
+                              world=World(device=torch.device(dev)), seed=4, device=dev)
+    cpu, gpu = mk("cpu"), mk("cuda")
+    for i, bt in enumerate(batches):
+        lc = float(cpu.train_step(bt))
+        lg = float(gpu.train_step(tuple(t.cuda() for t in bt)))
+        assert abs(lc - lg) <= 1e-5 * max(1.0, abs(lc)), (i, lc, lg)
+    for a, b in zip(cpu.dense_params, gpu.dense_params):
+        assert torch.allclose(a, b.cpu(), atol=2e-5, rtol=1e-4)
+    assert torch.allclose(cpu.emb.local, gpu.emb.local.cpu(), atol=2e-5)
+    assert torch.allclose(cpu.wide.local, gpu.wide.local.cpu(), atol=2e-5)
+
+
 def test_sparse_lr_fused_step_matches_general(monkeypatch):
     """One worker: the two-kernel step (csrc/kernels/sparse_lr.hip: no dedup,
     atomic scatter-SGD) trains like the general sharded path (radix-sort dedup,

@@ -66,7 +66,7 @@ hipError_t dtfk_xent_fwd_bf16(const void* logits, const float* bias, const int64
 hipError_t dtfk_xent_bwd_bf16(const void* logits, const float* bias, const int64_t* labels, const float* lse_rows,
                               const float* dloss, void* grad, int B, int C, float scale, hipStream_t s);
 hipError_t dtfk_embedding_bag_fwd(const float* W, int64_t V, int D, const int64_t* ids, const int64_t* offsets,
-                                  const float* psw, int B, int mode, float* out, int64_t* bad, hipStream_t s);
+                                  const float* psw, int B, int mode, float* out, int64_t* bad, const int64_t* remap, hipStream_t s);
 hipError_t dtfk_embedding_bag_bwd(float* target, int64_t V, int D, const int64_t* ids, const int64_t* offsets,
                                   const float* psw, const float* dout, int B, int mode, float lr,
                                   hipStream_t s);
@@ -384,15 +384,16 @@ void sigmoid_xent(at::Tensor x, at::Tensor t, at::Tensor loss, c10::optional<at:
 }
 
 void embedding_bag_fwd(at::Tensor W, at::Tensor ids, at::Tensor offsets, c10::optional<at::Tensor> psw, int mode,
-                       at::Tensor out, c10::optional<at::Tensor> bad) {
+                       at::Tensor out, c10::optional<at::Tensor> bad, c10::optional<at::Tensor> remap) {
   f32c(W, "weight"); i64c(ids, "ids"); i64c(offsets, "offsets"); f32c(out, "out");
   if (psw.has_value()) f32c(*psw, "per_sample_weights");
   if (bad.has_value()) i64c(*bad, "bad");
+  if (remap.has_value()) i64c(*remap, "remap");
   const int B = (int)offsets.numel() - 1;
   const int D = W.dim() == 1 ? 1 : (int)W.size(1);
   ck(dtfk_embedding_bag_fwd(W.data_ptr<float>(), W.size(0), D, ids.data_ptr<int64_t>(),
                             offsets.data_ptr<int64_t>(), opt_ptr<float>(psw), B, mode, out.data_ptr<float>(),
-                            opt_ptr<int64_t>(bad), cs()),
+                            opt_ptr<int64_t>(bad), opt_ptr<int64_t>(remap), cs()),
      "embedding_bag_fwd");
 }
 
@@ -646,7 +647,8 @@ void init_ops(py::module& m) {
   m.def("xent_fwd_bf16", &xent_fwd_bf16);
   m.def("xent_bwd_bf16", &xent_bwd_bf16);
   m.def("sigmoid_xent", &sigmoid_xent);
-  m.def("embedding_bag_fwd", &embedding_bag_fwd);
+  m.def("embedding_bag_fwd", &embedding_bag_fwd, py::arg("W"), py::arg("ids"), py::arg("offsets"), py::arg("psw"),
+        py::arg("mode"), py::arg("out"), py::arg("bad") = py::none(), py::arg("remap") = py::none());
   m.def("embedding_bag_bwd", &embedding_bag_bwd);
   m.def("embedding_bag_bwd_sorted", &embedding_bag_bwd_sorted);
   m.def("argmax_correct", &argmax_correct);

@@ -313,10 +313,14 @@ __global__ __launch_bounds__(256) void multi_copy(CopyList c) {
 // out[b, :] = combine_{j in bag b} w_j * W[ids_j, :]   (mode 0 sum, 1 mean, 2 sqrtn)
 // One wave per bag; lanes stride the embedding dim (D >= 64) or, for narrow
 // tables (D < 64, e.g. the LR weight D = 1), lanes stride the bag's ids.
+// remap (optional): ids index remap[] and remap[id] is the table row (a one-GPU
+// sharded table reads its rows in place: W = the table, ids = the dedup
+// inverse, remap = the unique ids -- no gathered [U, D] rows tensor)
 __global__ void embedding_bag_fwd(const float* __restrict__ W, int64_t V, int D,
                                   const int64_t* __restrict__ ids, const int64_t* __restrict__ offsets,
                                   const float* __restrict__ psw, int Bn, int mode,
-                                  float* __restrict__ out, int64_t* __restrict__ bad_ids) {
+                                  float* __restrict__ out, int64_t* __restrict__ bad_ids,
+                                  const int64_t* __restrict__ remap) {
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (b >= Bn) return;
@@ -327,6 +331,7 @@ __global__ void embedding_bag_fwd(const float* __restrict__ W, int64_t V, int D,
       float acc = 0.f, ws = 0.f;
       for (int64_t j = s + lane; j < e; j += 64) {
         int64_t id = ids[j];
+        if (remap != nullptr) id = remap[id];
         const float w = psw ? psw[j] : 1.f;
         if (id < 0 || id >= V) { if (bad_ids && d == 0) atomicAdd((unsigned long long*)bad_ids, 1ull); continue; }
         acc += w * W[id * D + d];
@@ -347,7 +352,7 @@ __global__ void embedding_bag_fwd(const float* __restrict__ W, int64_t V, int D,
     const int d = d0 + lane;
     float acc = 0.f, ws = 0.f;
     for (int64_t j = s; j < e; ++j) {
-      const int64_t id = ids[j];
+      const int64_t id = remap != nullptr ? remap[ids[j]] : ids[j];
       const float w = psw ? psw[j] : 1.f;
       if (id < 0 || id >= V) continue;
       if (d < D) acc += w * W[id * D + d];
@@ -820,10 +825,11 @@ hipError_t dtfk_sigmoid_xent(const float* x, const float* t, float* loss, float*
   return hipGetLastError();
 }
 hipError_t dtfk_embedding_bag_fwd(const float* W, int64_t V, int D, const int64_t* ids, const int64_t* offsets,
-                                  const float* psw, int B, int mode, float* out, int64_t* bad, hipStream_t s) {
+                                  const float* psw, int B, int mode, float* out, int64_t* bad, const int64_t* remap,
+                                  hipStream_t s) {
   hipLaunchKernelGGL(embedding_bag_fwd, dim3((B + 3) / 4, D < 64 ? 1 : (D + 63) / 64), dim3(256), 0, s, W, V, D,
                      ids, offsets, psw, B,
-                     mode, out, bad);
+                     mode, out, bad, remap);
   return hipGetLastError();
 }
 hipError_t dtfk_embedding_bag_bwd(float* target, int64_t V, int D, const int64_t* ids, const int64_t* offsets,

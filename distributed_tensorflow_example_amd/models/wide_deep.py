@@ -93,6 +93,7 @@ class WideDeep(StaticStepMixin):
             self.world.gpu_coll(self.flat_grad.numel() * self.flat_grad.element_size())
         self.global_step = 0
         self._graphed = None
+        self._one = None
 
     def forward(self, labels, offsets, ids, vals, exact: bool = False):
         wide, h, extras = self.forward_parts(labels, offsets, ids, vals, exact)
@@ -104,13 +105,23 @@ class WideDeep(StaticStepMixin):
         # both tables read the same ids over the same row partition: one
         # dedup + id exchange, one row exchange carrying [U, 1 + D]
         ctx = self.wide.route(ids, capacity=self.ids_capacity, exact=exact)
-        wrows, erows = lookup_shared([self.wide, self.emb], ctx)
-        wrows = wrows.detach().requires_grad_(True)
-        erows = erows.detach().requires_grad_(True)
         offsets = offsets.to(self.device).long()
         vals = None if vals is None else vals.to(self.device).float()
-        wide = ops.embedding_bag(wrows, ctx.inverse, offsets, vals, "sum")
-        emb = ops.embedding_bag(erows, ctx.inverse, offsets, vals, self.combiner)
+        if self.wide.W == 1 and self.device.type == "cuda" and not ctx.hogwild:
+            # one GPU: the bags read the table rows in place (table[uniq[inverse]]); the
+            # [U, D] row tensors are only the gradient targets (never gathered)
+            U = ctx.uniq.numel()
+            wrows = torch.empty((U, 1), device=self.device).requires_grad_(True)
+            erows = torch.empty((U, self.emb.dim), device=self.device).requires_grad_(True)
+            wide = ops.embedding_bag(wrows, ctx.inverse, offsets, vals, "sum", table=self.wide.local, remap=ctx.uniq)
+            emb = ops.embedding_bag(erows, ctx.inverse, offsets, vals, self.combiner, table=self.emb.local,
+                                    remap=ctx.uniq)
+        else:
+            wrows, erows = lookup_shared([self.wide, self.emb], ctx)
+            wrows = wrows.detach().requires_grad_(True)
+            erows = erows.detach().requires_grad_(True)
+            wide = ops.embedding_bag(wrows, ctx.inverse, offsets, vals, "sum")
+            emb = ops.embedding_bag(erows, ctx.inverse, offsets, vals, self.combiner)
         h = emb
         nl = len(self.layers) // 2
         for i in range(nl):
@@ -175,7 +186,9 @@ class WideDeep(StaticStepMixin):
         self.flat_grad.zero_()
         wide, h, (wrows, erows, lctx) = self.forward_parts(labels, offsets, ids, vals, exact)
         loss = ops.logit3_xent(wide, h, self.bias, labels)      # the head's adds + xent + mean: one kernel
-        loss.backward()
+        if self._one is None or self._one.device != loss.device:
+            self._one = torch.ones((), device=loss.device)       # backward's seed, not a fill per step
+        loss.backward(self._one)
         ws = self.world.world_size
         # dense tower: one flat all-reduce, overlapped with the sparse exchanges
         ev = None

@@ -298,12 +298,18 @@ def sigmoid_xent(logits, targets, reduction: str = "mean"):
 # --------------------------------------------------------------------------- embeddings
 class _EmbeddingBag(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, weight, ids, offsets, psw, mode):
+    def forward(ctx, weight, ids, offsets, psw, mode, table=None, remap=None):
+        """table / remap (one-GPU sharded tables): the rows are read in place as
+        table[remap[ids]]; `weight` is then only the [U, D] gradient target
+        (never read -- an uninitialised tensor is fine)."""
         C = _C()
         B = offsets.numel() - 1
         D = 1 if weight.dim() == 1 else weight.shape[1]
         out = torch.empty((B, D), dtype=torch.float32, device=weight.device)
-        C.embedding_bag_fwd(weight.contiguous(), ids, offsets, psw, EMB_MODE[mode], out, None)
+        if table is not None:
+            C.embedding_bag_fwd(table, ids, offsets, psw, EMB_MODE[mode], out, None, remap)
+        else:
+            C.embedding_bag_fwd(weight.contiguous(), ids, offsets, psw, EMB_MODE[mode], out, None)
         ctx.save_for_backward(ids, offsets, psw if psw is not None else torch.empty(0))
         ctx.has_psw = psw is not None
         ctx.mode = mode
@@ -322,7 +328,7 @@ class _EmbeddingBag(torch.autograd.Function):
                                        .contiguous().float())
         else:
             C.embedding_bag_bwd(gw, ids, offsets, psw, gout.contiguous().float(), EMB_MODE[ctx.mode], 0.0)
-        return gw, None, None, None, None
+        return gw, None, None, None, None, None, None
 
 
 _SORT_PLAN = [None]   # (key, ids ref, (rows int32 sorted, occ))
@@ -369,13 +375,18 @@ def _bag_plan(ids: torch.Tensor, offsets: torch.Tensor):
     return c[2][0], c[2][1], b[2]
 
 
-def embedding_bag(weight, ids, offsets, per_sample_weights=None, mode: str = "sum"):
+def embedding_bag(weight, ids, offsets, per_sample_weights=None, mode: str = "sum", table=None, remap=None):
     """Bag-combine rows of `weight` [V, D] for CSR bags (offsets [B+1]).
 
     == tf.nn.embedding_lookup_sparse(W, sp_ids, sp_weights, combiner=mode).
+    table / remap (GPU): read row table[remap[id]] in place of weight[id] --
+    `weight` ([len(remap), D]) is then only where the gradient goes.
     """
     ids = ids.long()
     offsets = offsets.long()
+    if table is not None and not weight.is_cuda:
+        weight = table.index_select(0, remap.clamp_min(0)).requires_grad_(weight.requires_grad)
+        table = remap = None
     if not weight.is_cuda:
         W = weight if weight.dim() == 2 else weight.reshape(-1, 1)
         out = torch.nn.functional.embedding_bag(ids, W, offsets[:-1], mode="sum",
@@ -389,6 +400,10 @@ def embedding_bag(weight, ids, offsets, per_sample_weights=None, mode: str = "su
             out = out / den.clamp_min(1e-30).unsqueeze(1)
         return out
     psw = per_sample_weights.contiguous().float() if per_sample_weights is not None else None
+    if table is not None:
+        t = table if table.dim() == 2 else table.reshape(-1, 1)
+        return _EmbeddingBag.apply(weight, ids.contiguous(), offsets.contiguous(), psw, mode, t.contiguous(),
+                                   remap.long().contiguous())
     return _EmbeddingBag.apply(weight, ids.contiguous(), offsets.contiguous(), psw, mode)
 
 

@@ -56,6 +56,7 @@ hipError_t dtfk_logit3_xent(const float* a, const float* b, const float* bias, c
 hipError_t dtfk_logit3_xent_bwd(const float* dz, const float* g, float* d, float* gbias, int accum, int n,
                                 hipStream_t s);
 hipError_t dtfk_multi_copy(const void* const* src, void* const* dst, const long long* bytes, int n, hipStream_t s);
+hipError_t dtfk_bag_index(const int64_t* offsets, int B, int* bag_of, int64_t N, hipStream_t s);
 hipError_t dtfk_softmax_xent(const float* logits, const int64_t* labels, const float* ydense, float* loss_rows,
                              float* grad, int64_t* correct, int B, int C, float grad_scale, int naive,
                              hipStream_t s);
@@ -397,16 +398,26 @@ void embedding_bag_fwd(at::Tensor W, at::Tensor ids, at::Tensor offsets, c10::op
      "embedding_bag_fwd");
 }
 
-void embedding_bag_bwd(at::Tensor target, at::Tensor ids, at::Tensor offsets, c10::optional<at::Tensor> psw,
-                       at::Tensor dout, int mode, double lr) {
-  f32c(target, "target"); i64c(ids, "ids"); i64c(offsets, "offsets"); f32c(dout, "dout");
+// offsets None: one id per bag (B = ids.numel())
+void embedding_bag_bwd(at::Tensor target, at::Tensor ids, c10::optional<at::Tensor> offsets,
+                       c10::optional<at::Tensor> psw, at::Tensor dout, int mode, double lr) {
+  f32c(target, "target"); i64c(ids, "ids"); f32c(dout, "dout");
+  if (offsets.has_value()) i64c(*offsets, "offsets");
   if (psw.has_value()) f32c(*psw, "per_sample_weights");
-  const int B = (int)offsets.numel() - 1;
+  const int B = offsets.has_value() ? (int)offsets->numel() - 1 : (int)ids.numel();
   const int D = target.dim() == 1 ? 1 : (int)target.size(1);
   ck(dtfk_embedding_bag_bwd(target.data_ptr<float>(), target.size(0), D, ids.data_ptr<int64_t>(),
-                            offsets.data_ptr<int64_t>(), opt_ptr<float>(psw), dout.data_ptr<float>(), B, mode,
+                            opt_ptr<int64_t>(offsets), opt_ptr<float>(psw), dout.data_ptr<float>(), B, mode,
                             (float)lr, cs()),
      "embedding_bag_bwd");
+}
+void bag_index(at::Tensor offsets, at::Tensor bag_of) {
+  i64c(offsets, "offsets");
+  gpu(bag_of, "bag_of");
+  if (bag_of.scalar_type() != at::kInt || !bag_of.is_contiguous()) throw std::runtime_error("bag_index: int32 out");
+  ck(dtfk_bag_index(offsets.data_ptr<int64_t>(), (int)offsets.numel() - 1, bag_of.data_ptr<int>(), bag_of.numel(),
+                    cs()),
+     "bag_index");
 }
 
 void embedding_bag_bwd_sorted(at::Tensor target, at::Tensor rows, at::Tensor occ, at::Tensor bag_of,
@@ -643,6 +654,7 @@ void init_ops(py::module& m) {
   m.def("logit3_xent", &logit3_xent);
   m.def("logit3_xent_bwd", &logit3_xent_bwd);
   m.def("multi_copy", &multi_copy);
+  m.def("bag_index", &bag_index);
   m.def("softmax_xent", &softmax_xent);
   m.def("xent_fwd_bf16", &xent_fwd_bf16);
   m.def("xent_bwd_bf16", &xent_bwd_bf16);

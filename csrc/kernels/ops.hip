@@ -376,7 +376,9 @@ __global__ void embedding_bag_bwd(float* __restrict__ target, int64_t V, int D,
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (b >= Bn) return;
-  const int64_t s = offsets[b], e = offsets[b + 1];
+  // offsets == nullptr: one id per bag (a row-wise scatter, e.g. the owner-side
+  // sparse SGD of gradient rows) -- no arange offsets tensor to build
+  const int64_t s = offsets != nullptr ? offsets[b] : b, e = offsets != nullptr ? offsets[b + 1] : b + 1;
   float ws = 0.f;
   if (mode != 0) {
     for (int64_t j = s + lane; j < e; j += 64) {
@@ -403,6 +405,20 @@ __global__ void embedding_bag_bwd(float* __restrict__ target, int64_t V, int D,
     if (id < 0 || id >= V) continue;
     const float w = (psw ? psw[j] : 1.f) * mul;
     for (int d = lane; d < D; d += 64) atomicAdd(&target[id * D + d], w * dout[(size_t)b * D + d]);
+  }
+}
+
+// bag_of[j] = the bag of CSR position j (offsets [B + 1], non-decreasing): one
+// binary search per position -- one kernel instead of repeat_interleave's five
+__global__ __launch_bounds__(256) void bag_index(const int64_t* __restrict__ offsets, int B, int* __restrict__ bag_of,
+                                                 int64_t N) {
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < N; j += (int64_t)gridDim.x * blockDim.x) {
+    int lo = 0, hi = B;            // last b with offsets[b] <= j
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (offsets[mid] <= j) lo = mid; else hi = mid;
+    }
+    bag_of[j] = lo;
   }
 }
 
@@ -802,6 +818,12 @@ hipError_t dtfk_logit3_xent(const float* a, const float* b, const float* bias, c
 hipError_t dtfk_logit3_xent_bwd(const float* dz, const float* g, float* d, float* gbias, int accum, int n,
                                 hipStream_t s) {
   hipLaunchKernelGGL(logit3_xent_bwd, dim3(1), dim3(1024), 0, s, dz, g, d, gbias, accum, n);
+  return hipGetLastError();
+}
+hipError_t dtfk_bag_index(const int64_t* offsets, int B, int* bag_of, int64_t N, hipStream_t s) {
+  if (N <= 0) return hipSuccess;
+  const long long blocks = (N + 255) / 256;
+  hipLaunchKernelGGL(bag_index, dim3((unsigned)(blocks > 4096 ? 4096 : blocks)), dim3(256), 0, s, offsets, B, bag_of, N);
   return hipGetLastError();
 }
 hipError_t dtfk_multi_copy(const void* const* src, void* const* dst, const long long* bytes, int n, hipStream_t s) {

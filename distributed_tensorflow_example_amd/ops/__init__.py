@@ -367,10 +367,9 @@ def _bag_plan(ids: torch.Tensor, offsets: torch.Tensor):
         _SORT_PLAN[0] = c
     b = _BAG_OF[0]
     if b is None or b[0] != _tkey(offsets):
-        B = offsets.numel() - 1
-        bag_of = torch.repeat_interleave(torch.arange(B, dtype=torch.int32, device=ids.device),
-                                         offsets[1:] - offsets[:-1], output_size=ids.numel())
-        b = (_tkey(offsets), offsets, bag_of.contiguous())
+        bag_of = torch.empty(ids.numel(), dtype=torch.int32, device=ids.device)
+        _C().bag_index(offsets.long().contiguous(), bag_of)       # one kernel (repeat_interleave: five)
+        b = (_tkey(offsets), offsets, bag_of)
         _BAG_OF[0] = b
     return c[2][0], c[2][1], b[2]
 
@@ -408,8 +407,11 @@ def embedding_bag(weight, ids, offsets, per_sample_weights=None, mode: str = "su
 
 
 def embedding_bag_sgd_(weight, ids, offsets, per_sample_weights, grad_out, lr: float, mode: str = "sum"):
-    """Fused sparse SGD: weight[ids] -= lr * w * grad_out[bag]  (ScatterSub apply)."""
+    """Fused sparse SGD: weight[ids] -= lr * w * grad_out[bag]  (ScatterSub apply).
+    offsets None: one id per bag (row i of grad_out goes to weight[ids[i]])."""
     if not weight.is_cuda:
+        if offsets is None:
+            offsets = torch.arange(ids.numel() + 1, device=ids.device)
         seg = torch.repeat_interleave(torch.arange(offsets.numel() - 1), offsets[1:] - offsets[:-1])
         w = per_sample_weights if per_sample_weights is not None else torch.ones(ids.numel())
         W = weight if weight.dim() == 2 else weight.view(-1, 1)
@@ -417,7 +419,7 @@ def embedding_bag_sgd_(weight, ids, offsets, per_sample_weights, grad_out, lr: f
         W.index_add_(0, ids.long().clamp(0, max(W.shape[0] - 1, 0)),
                      -lr * (w * ok).unsqueeze(1) * grad_out[seg])
         return weight
-    _C().embedding_bag_bwd(weight, ids.long().contiguous(), offsets.long().contiguous(),
+    _C().embedding_bag_bwd(weight, ids.long().contiguous(), None if offsets is None else offsets.long().contiguous(),
                            per_sample_weights.contiguous().float() if per_sample_weights is not None else None,
                            grad_out.contiguous().float(), EMB_MODE[mode], float(lr))
     return weight

@@ -379,9 +379,8 @@ class ShardedEmbedding:
         if self.opt_kind != "sgd":
             self._apply_local(ctx.recv_local, g, lr, grad_scale, void)
             return
-        offs = torch.arange(n + 1, dtype=torch.int64, device=self.device)
-        with torch.no_grad():
-            ops.embedding_bag_sgd_(self.local, ctx.recv_local, offs, None, g, float(lr) * grad_scale)
+        with torch.no_grad():      # one gradient row per id: no offsets tensor
+            ops.embedding_bag_sgd_(self.local, ctx.recv_local, None, None, g, float(lr) * grad_scale)
 
     @torch.no_grad()
     def _apply_local(self, idx: torch.Tensor, g: torch.Tensor, lr: float, grad_scale: float,

@@ -210,6 +210,32 @@ def test_embedding_bag_sgd_scatter(native):
     assert torch.allclose(got.cpu(), ref, atol=1e-5)
 
 
+def test_bag_index_with_empty_bags(native):
+    """bag_index (one binary search per CSR position) == repeat_interleave, empty bags included."""
+    for seed, maxlen in ((1, 5), (2, 0), (3, 40)):
+        ids, offsets, _ = _bags(300, 100, maxlen, seed)
+        if ids.numel() == 0:
+            offsets[-1] = 0
+        ref = torch.repeat_interleave(torch.arange(300, dtype=torch.int32), offsets[1:] - offsets[:-1])
+        out = torch.empty(ids.numel(), dtype=torch.int32, device="cuda")
+        native.bag_index(offsets.cuda(), out)
+        assert torch.equal(out.cpu(), ref)
+
+
+def test_embedding_bag_sgd_identity_offsets(native):
+    """offsets None: row i of the gradient goes to weight[ids[i]] (repeated ids accumulate)."""
+    from distributed_tensorflow_example_amd import ops
+    torch.manual_seed(4)
+    V, D, n = 500, 24, 3000
+    ids = torch.randint(0, V, (n,))
+    g = torch.randn(n, D)
+    W = torch.randn(V, D)
+    ref = W.clone().index_add_(0, ids, g, alpha=-0.25)
+    got = ops.embedding_bag_sgd_(W.clone().cuda(), ids.cuda(), None, None, g.cuda(), 0.25)
+    assert torch.allclose(got.cpu(), ref, atol=1e-5)
+    assert torch.allclose(ops.embedding_bag_sgd_(W.clone(), ids, None, None, g, 0.25), ref, atol=1e-5)
+
+
 def test_argmax_correct(native):
     from distributed_tensorflow_example_amd import ops
     z = torch.randn(10000, 10)

@@ -684,8 +684,16 @@ __device__ void copier_res(const Args& a, int cid, uint8_t* smem) {
 // three-way split of their fp32 operand (pixels are exact in bf16), so every
 // product is exact and accumulates in fp32 -- 16x16x32 bf16 MFMAs at 8x the
 // f32-MFMA rate; the head stays on f32-input MFMA
-template <int ACT, int NW, bool SPLIT, bool RES>
+// EXP (timing experiment only, never the production instantiations; DTF_PERSIST_EXP,
+// scripts/probes/decomposition_sim.sh): the per-workgroup work of the 14- (EXP 2)
+// and 7-workgroup (EXP 4) decompositions on this 28-workgroup engine -- every
+// forward / weight-gradient MFMA chain and the next-step stage DMA run EXP times
+// (a 2x / 4x wider feature slice), E1 gathers 2 slices (EXP 2) or disappears
+// (EXP 4).  The sums are rescaled, so training still runs, but the numerics are
+// not the reference's: stamps and step times only.
+template <int ACT, int NW, bool SPLIT, bool RES, int EXP = 0>
 __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) {
+  constexpr int XR = EXP > 1 ? EXP : 1;
   constexpr bool MULTI = NW > 1;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
@@ -1036,11 +1044,18 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
 #pragma unroll
         for (int b = 0; b < NBT; ++b) X[b] = px8(xf[0][b], xf[1][b]);
 #pragma unroll
-        for (int b = 0; b < NBT; ++b) acc[b] = mfma16x16x32(Al, X[b], acc[b]);
+        for (int xr = 0; xr < XR; ++xr) {
 #pragma unroll
-        for (int b = 0; b < NBT; ++b) acc[b] = mfma16x16x32(Am, X[b], acc[b]);
+          for (int b = 0; b < NBT; ++b) acc[b] = mfma16x16x32(Al, X[b], acc[b]);
 #pragma unroll
-        for (int b = 0; b < NBT; ++b) acc[b] = mfma16x16x32(Ah, X[b], acc[b]);
+          for (int b = 0; b < NBT; ++b) acc[b] = mfma16x16x32(Am, X[b], acc[b]);
+#pragma unroll
+          for (int b = 0; b < NBT; ++b) acc[b] = mfma16x16x32(Ah, X[b], acc[b]);
+        }
+        if constexpr (XR > 1) {
+#pragma unroll
+          for (int b = 0; b < NBT; ++b) acc[b] *= 1.f / (float)XR;
+        }
       } else {
 #pragma unroll
         for (int k = 0; k < NTW; ++k) {
@@ -1076,7 +1091,8 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
         while (heads_done() == 0u) __builtin_amdgcn_s_sleep(1);
       }
       if (a.dbg & 8) stage_x(st + 1, 1, 2);
-      else stage_x(st + 1, 0, 1);
+      else
+        for (int xr = 0; xr < XR; ++xr) stage_x(st + 1, 0, 1);
       // idle until the first head is done anyway: wait for the DMA here and tell the
       // other waves the next step's operands are in LDS
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1096,7 +1112,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
       // publish the slice partial of (j, batch tile w) as granules; gather the others
       // E1 region of (parity, block j): [slice][batch tile] slots
       const auto r1 = region_rsrc(a.xbuf + E1_OFF + (long long)(par * NJ + j) * NQ * NBT * GSLOT, NQ * NBT * GSLOT);
-      put_gran(r1, (q * NBT + w) * GSLOT + 32 * lane, zs, tag, l2_e1);
+      if constexpr (EXP != 4) put_gran(r1, (q * NBT + w) * GSLOT + 32 * lane, zs, tag, l2_e1);
       if (w == 0) { PH(3); }
       // this step's W2 / b1 / b2 operands of the lane, read from LDS while the
       // partial is in flight (their LDS latency off the E1 -> P1 -> E2 -> head chain)
@@ -1108,12 +1124,23 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
         b1v[e] = b1s[4 * g + e];
         b2v[e] = b2s[4 * g + e];
       }
-      f32x4 part[NQ];
-      bool ok = gather_gran<NQ>(r1, [&](int k) { return (k * NBT + w) * GSLOT; }, q, true, 63, tag, zs, part, lane, a);
-      if (w == 0) { PH(4); }
-      f32x4 z = part[0];
+      f32x4 z;
+      bool ok = true;
+      if constexpr (EXP == 4) {
+        z = zs * 4.f;
+      } else if constexpr (EXP == 2) {
+        f32x4 part[2];
+        ok = gather_gran<2>(r1, [&](int k) { return (((q & 2) + k) * NBT + w) * GSLOT; }, q & 1, true, 63, tag, zs, part,
+                            lane, a);
+        z = (part[0] + part[1]) * 2.f;
+      } else {
+        f32x4 part[NQ];
+        ok = gather_gran<NQ>(r1, [&](int k) { return (k * NBT + w) * GSLOT; }, q, true, 63, tag, zs, part, lane, a);
+        z = part[0];
 #pragma unroll
-      for (int qq = 1; qq < NQ; ++qq) z += part[qq];
+        for (int qq = 1; qq < NQ; ++qq) z += part[qq];
+      }
+      if (w == 0) { PH(4); }
       if (w == 0) { PH(5); }
       // lane (batch r, g): hidden 16j+4g+i
       float a2[4];
@@ -1300,7 +1327,8 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
           if (ch == cc && (hm & need_of(ch)) == need_of(ch)) {   // wave-uniform
             if (!did) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
             if (cc == 0 && w == 0) { PH(10); }
-            chunk(ch);
+#pragma unroll
+            for (int xr = 0; xr < XR; ++xr) chunk(ch);
             ++cc;
             did = true;
           }
@@ -1315,6 +1343,10 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
     if constexpr (!SPLIT) {
 #pragma unroll
       for (int k = 0; k < NTW; ++k) G[k] = G[k] + G1[k];
+    }
+    if constexpr (XR > 1) {
+#pragma unroll
+      for (int k = 0; k < NTW; ++k) G[k] *= 1.f / (float)XR;
     }
     // every head is done here.  Wave 7 sums the 7 head waves' dW2 / db2 partials
     // and the per-row metrics in fixed order (all loads in flight at once); one
@@ -1612,7 +1644,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
 // L2); the first NCOP other blocks copy, the rest exit.  spread (several ranks on
 // one GPU, tests): compute = blocks 0..27, copiers = 28..43.  Placement is speed
 // only: the census above decides each edge's store flavour.
-template <int ACT, int NW, bool SPLIT, bool RES = false>
+template <int ACT, int NW, bool SPLIT, bool RES = false, int EXP = 0>
 __global__ __launch_bounds__(THREADS, 1) void mlp_persist_f32(Args a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int b = blockIdx.x;
@@ -1623,7 +1655,7 @@ __global__ __launch_bounds__(THREADS, 1) void mlp_persist_f32(Args a) {
     if ((b & 7) == 0) c = b >> 3; else cid = b - (b >> 3) - 1;
   }
   if (c >= 0) {
-    if (a.nsteps > 0) compute<ACT, NW, SPLIT, RES>(a, c / NQ, c % NQ, smem);
+    if (a.nsteps > 0) compute<ACT, NW, SPLIT, RES, EXP>(a, c / NQ, c % NQ, smem);
     return;
   }
   if constexpr (RES) copier_res(a, cid, smem);
@@ -1662,6 +1694,7 @@ long long dtfk_mlpf_xbuf_bytes() { return dtfk::mlpf::XBUF_BYTES; }
 long long dtfk_mlpf_ipc_bytes() { return dtfk::mlpf::IPC_BYTES; }
 int dtfk_mlpf_max_batch() { return dtfk::mlpf::BROWS; }
 
+typedef void (*Kern2)(dtfk::mlpf::Args);
 hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int nsteps, float* params, const float* lr,
                                 float* metrics, int ring, int act, int naive, long long* gstep, unsigned long long* seq,
                                 void* xbuf, int* err, long long timeout, long long* step_ts, int ts_ring,
@@ -1724,6 +1757,28 @@ hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int n
     }();
     a.gmode = gmode;
     a.dbg = dbg;
+    // timing experiment only (see compute's EXP): 2 / 4 = the 14- / 7-workgroup
+    // decompositions' per-workgroup work, sigmoid one-GPU split engine only
+    static const int exper = [] {
+      const char* e = getenv("DTF_PERSIST_EXP");
+      return e ? atoi(e) : 0;
+    }();
+    if (exper == 2 || exper == 4) {
+      if (act != 0 || W != 1 || !split || spread) return hipErrorInvalidValue;
+      static const Kern2 xk[2] = {mlp_persist_f32<0, 1, true, false, 2>, mlp_persist_f32<0, 1, true, false, 4>};
+      const Kern2 k = xk[exper == 2 ? 0 : 1];
+      static bool xattr = false;
+      if (!xattr) {
+        for (Kern2 kk : xk) {
+          const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kk),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_BYTES);
+          if (e != hipSuccess) return e;
+        }
+        xattr = true;
+      }
+      hipLaunchKernelGGL(k, dim3(GRID_PACKED), dim3(THREADS), LDS_BYTES, stream, a);
+      return hipGetLastError();
+    }
     a.fault_rank = g_fault_rank;
     a.fault_step = g_fault_step;
   }

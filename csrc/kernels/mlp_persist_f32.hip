@@ -742,37 +742,59 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
 #pragma unroll
       for (int e = 0; e < 4; ++e)
         Wt[k][e] = (tvk(k) && hv) ? a.params[(16 * ftk(k) + 4 * g + e) * HID + hid] : 0.f;
-  } else {
-    const int u0 = 16 * j + 4 * (r & 3);           // units 4(r&3)..+3 of block j, row 4g + (r >> 2)
+  } else if constexpr (MULTI) {   // (N GPUs: the branchy loads -- the unconditional ones below spill there)
+    const int u0 = 16 * j + 4 * (r & 3);
 #pragma unroll
     for (int k = 0; k < NTW; ++k)
       wld[k] = (tvk(k) && u0 < HID)
                    ? *reinterpret_cast<const f32x4*>(a.params + (16 * ftk(k) + 4 * g + (r >> 2)) * HID + u0)
                    : f32x4{0.f, 0.f, 0.f, 0.f};
+  } else {
+    // unconditional buffer loads (an absent tile / padding unit reads past the
+    // range: zero, no branch) -- a conditional load's result merged at the branch
+    // end cost a vmcnt(0) right behind it, one serial HBM round trip per launch
+    const int u0 = 16 * j + 4 * (r & 3);           // units 4(r&3)..+3 of block j, row 4g + (r >> 2)
+    const auto rw1 = __builtin_amdgcn_make_buffer_rsrc(a.params, 0, DIN * HID * 4, 0x00020000);
+#pragma unroll
+    for (int k = 0; k < NTW; ++k)
+      wld[k] = __builtin_bit_cast(
+          f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                     rw1, (tvk(k) && u0 < HID) ? ((16 * ftk(k) + 4 * g + (r >> 2)) * HID + u0) * 4 : OOB_OFF, 0, 0));
   }
-  float pv = 0.f;   // this thread's W2 / b1 / b2 entry (threads < 288)
-  if (tid < 256) {
-    const int n = tid >> 4, cl = tid & 15;
-    const int hn = 16 * j + n;
-    pv = (hn < HID && cl < NCLS) ? a.p_w2[hn * NCLS + cl] : 0.f;
-  } else if (tid < 272) {
-    const int hn = 16 * j + (tid - 256);
-    pv = hn < HID ? a.p_b1[hn] : 0.f;
-  } else if (tid < 288) {
-    const int cl = tid - 272;
-    pv = cl < NCLS ? a.p_b2[cl] : 0.f;
+  // this thread's W2 / b1 / b2 entry (threads < 288): three unconditional loads,
+  // at most one in range, OR-ed (the others read zero)
+  float pv = 0.f;
+  if constexpr (MULTI) {
+    if (tid < 256) {
+      const int n = tid >> 4, cl = tid & 15;
+      const int hn = 16 * j + n;
+      pv = (hn < HID && cl < NCLS) ? a.p_w2[hn * NCLS + cl] : 0.f;
+    } else if (tid < 272) {
+      const int hn = 16 * j + (tid - 256);
+      pv = hn < HID ? a.p_b1[hn] : 0.f;
+    } else if (tid < 288) {
+      const int cl = tid - 272;
+      pv = cl < NCLS ? a.p_b2[cl] : 0.f;
+    }
+  } else {
+    const int n = tid >> 4, cl = tid & 15, hn = 16 * j + n, hb = 16 * j + (tid - 256), c2 = tid - 272;
+    const auto rw2 = __builtin_amdgcn_make_buffer_rsrc(a.p_w2, 0, HID * NCLS * 4, 0x00020000);
+    const auto rb1 = __builtin_amdgcn_make_buffer_rsrc(a.p_b1, 0, HID * 4, 0x00020000);
+    const auto rb2 = __builtin_amdgcn_make_buffer_rsrc(a.p_b2, 0, NCLS * 4, 0x00020000);
+    const uint32_t v0 =
+        __builtin_amdgcn_raw_buffer_load_b32(rw2, (tid < 256 && hn < HID && cl < NCLS) ? (hn * NCLS + cl) * 4 : OOB_OFF, 0, 0);
+    const uint32_t v1 =
+        __builtin_amdgcn_raw_buffer_load_b32(rb1, (tid >= 256 && tid < 272 && hb < HID) ? hb * 4 : OOB_OFF, 0, 0);
+    const uint32_t v2 =
+        __builtin_amdgcn_raw_buffer_load_b32(rb2, (tid >= 272 && tid < 288 && c2 < NCLS) ? c2 * 4 : OOB_OFF, 0, 0);
+    pv = __uint_as_float(v0 | v1 | v2);
   }
-  const unsigned long long seq0 = *a.seq;
-  const long long gstep0 = *a.gstep;
-  double gvar0 = 0.0;   // RES: the graph's global_step at launch
-  if constexpr (RES) {
-    if (a.gvar_kind == 1) gvar0 = *static_cast<const float*>(a.gvar);
-    else if (a.gvar_kind == 2) gvar0 = (double)*static_cast<const long long*>(a.gvar);
-    else if (a.gvar_kind == 3) gvar0 = *static_cast<const int*>(a.gvar);
-    else if (a.gvar_kind == 4) gvar0 = *static_cast<const double*>(a.gvar);
-    else gvar0 = (double)gstep0;
-  }
-  const float lr = *a.lr;
+  // the step / sequence / lr scalars stay in VGPRs until the prologue's drain
+  // (converted to SGPRs there): a readfirstlane right behind each load waited
+  // for it, another serial round trip in front of the stage and census
+  unsigned long long seq0 = *a.seq;
+  long long gstep0 = *a.gstep;
+  float lr = *a.lr;
   // the placement-census entry goes out before anything waits on a load: its
   // tag is the host's per-launch tag, not the device sequence counter (whose
   // load, with the lr / parameter waits ahead of the LDS stores, held every
@@ -892,6 +914,22 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
     reinterpret_cast<int*>(smem + L_HFLAG)[tid - 296] = 0;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // parameter loads + the first stage landed
+  if constexpr (!MULTI) {
+    asm volatile("" : "+v"(seq0), "+v"(gstep0), "+v"(lr));
+    seq0 = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(seq0 >> 32)) << 32) |
+           __builtin_amdgcn_readfirstlane((unsigned)seq0);
+    gstep0 = (long long)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)((unsigned long long)gstep0 >> 32))
+                          << 32) |
+                         __builtin_amdgcn_readfirstlane((unsigned)gstep0));
+  }
+  double gvar0 = 0.0;   // RES: the graph's global_step at launch
+  if constexpr (RES) {
+    if (a.gvar_kind == 1) gvar0 = *static_cast<const float*>(a.gvar);
+    else if (a.gvar_kind == 2) gvar0 = (double)*static_cast<const long long*>(a.gvar);
+    else if (a.gvar_kind == 3) gvar0 = *static_cast<const int*>(a.gvar);
+    else if (a.gvar_kind == 4) gvar0 = *static_cast<const double*>(a.gvar);
+    else gvar0 = (double)gstep0;
+  }
   // the 4x4 transposes of the W1 blocks in 4 rounds of one lane permute:
   // in round t the lane that loaded row e_s offers component (e_s + t) & 3, and
   // lane r (unit 4b + m) takes row (m - t) & 3 from lane 4((m - t) & 3) + b --

@@ -399,10 +399,17 @@ __global__ __launch_bounds__(NTHR, ONE ? 3 : 2) void conv_fwd(const uint16_t* __
 // fragments are read with the gfx950 transposed LDS read ds_read_b64_tr_b16
 // (4 x 16-bit down a column per lane, two per 8-deep fragment).  Pixel rows
 // advance 64 per step by a carried (n, ho, wo) counter, no divisions in the loop.
+// chunk XOR of pixel row k (as gemm_big.hip mn_sw: R = 64 rows are 128 B, two
+// per bank row, so k bit 0 picks the half and the XOR takes bits 1 and 3)
 __device__ __forceinline__ int mn_swz(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
 template <int R>
+__device__ __forceinline__ int mn_sw(int k) {
+  if constexpr (R == 64) return (((k >> 1) & 1) | (((k >> 3) & 1) << 1)) << 1;
+  else return (mn_swz(k) << 1) & (R / 8 - 1);
+}
+template <int R>
 __device__ __forceinline__ int mn_off(int k, int ch) {   // byte offset of (k, 16-byte chunk ch) in [64][R]
-  return k * (2 * R) + ((ch ^ ((mn_swz(k) << 1) & (R / 8 - 1))) << 4);
+  return k * (2 * R) + ((ch ^ mn_sw<R>(k)) << 4);
 }
 typedef __attribute__((ext_vector_type(4))) short v4s;
 typedef __attribute__((address_space(3))) v4s lds_v4s;
@@ -470,7 +477,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv_wgrad(const uint16_t* __restrict
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
     const int row = brow0 + BRS * i;
-    const int lch = bch ^ ((mn_swz(row) << 1) & (BNW / 8 - 1));   // logical chunk stored at this slot
+    const int lch = bch ^ mn_sw<BNW>(row);   // logical chunk stored at this slot
     bphys[i] = bch;
     const int col = n0 + 8 * lch;
     bval[i] = col < NC;
@@ -489,7 +496,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv_wgrad(const uint16_t* __restrict
 #pragma unroll
   for (int i = 0; i < NA; ++i) {
     const int row = arow0 + ARS * i;
-    alch[i] = ach ^ ((mn_swz(row) << 1) & (BMW / 8 - 1));
+    alch[i] = ach ^ mn_sw<BMW>(row);
   }
   const int dq = PK / Wo, dr = PK % Wo;
   auto advance = [&]() {

@@ -109,12 +109,24 @@ __device__ __forceinline__ int kc_off(int r, int c) {
   constexpr int CPR = BK / 8;
   return r * (BK * 2) + ((c ^ ((r / (16 / CPR)) & (CPR - 1))) << 4);
 }
-// M/N-contiguous [BK][R] bf16: byte offset of (k, 16-byte chunk ch = mn/8)
+// M/N-contiguous [BK][R] bf16: byte offset of (k, 16-byte chunk ch = mn/8).
+// A transposed fragment read (frag, ds_read_b64_tr_b16) takes a 32-byte
+// segment from each of 16 k-rows (k = 32 s + {0..3, 8..11, 16..19, 24..27});
+// the chunk XOR spreads them over the bank row.  R >= 128 (rows >= 256 B):
+// k bits 0, 1, 3 pick one of 8 segments.  R = 64 (128-byte rows, two per
+// 256-byte bank row): k bit 0 already picks the half, so the XOR takes bits 1
+// and 3 -- the masked R >= 128 XOR there (2 (k & 3)) collided with bit 0 and
+// left half the banks unused: 2x the LDS cycles of every B read of a 192-wide
+// tile's second quadrant column (SQ_LDS_BANK_CONFLICT 5x, profiles/gemm_layout_ab_r6.txt).
 __device__ __forceinline__ int mn_swz(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
-// (the chunk XOR is masked to the row's R / 8 chunks: a no-op for R >= 128)
+template <int R>
+__device__ __forceinline__ int mn_sw(int k) {
+  if constexpr (R == 64) return (((k >> 1) & 1) | (((k >> 3) & 1) << 1)) << 1;
+  else return (mn_swz(k) << 1) & (R / 8 - 1);
+}
 template <int R>
 __device__ __forceinline__ int mn_off(int k, int ch) {
-  return k * (2 * R) + ((ch ^ ((mn_swz(k) << 1) & (R / 8 - 1))) << 4);
+  return k * (2 * R) + ((ch ^ mn_sw<R>(k)) << 4);
 }
 
 // Stage one operand tile (R rows of the output dimension x BK k) into `img`.
@@ -132,7 +144,7 @@ __device__ __forceinline__ void stage(const uint16_t* __restrict__ base, int ld,
       const int r = o / (BK * 2), c = ((o >> 4) % CPR) ^ ((r / (16 / CPR)) & (CPR - 1));
       src = base + (size_t)min(r0 + r, rows - 1) * ld + k0 + c * 8;
     } else {
-      const int k = o / (2 * R), ch = ((o % (2 * R)) >> 4) ^ (mn_swz(k) << 1);
+      const int k = o / (2 * R), ch = ((o % (2 * R)) >> 4) ^ mn_sw<R>(k);
       src = base + (size_t)(k0 + k) * ld + min(r0 + ch * 8, rows - 8);
     }
     __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(img + wbase), 16, 0, 0);
@@ -153,7 +165,7 @@ __device__ __forceinline__ void gload(const uint16_t* __restrict__ base, int ld,
       const int r = o / (BK * 2), c = ((o >> 4) % CPR) ^ ((r / (16 / CPR)) & (CPR - 1));
       src = base + (size_t)min(r0 + r, rows - 1) * ld + k0 + c * 8;
     } else {
-      const int k = o / (2 * R), ch = ((o % (2 * R)) >> 4) ^ (mn_swz(k) << 1);
+      const int k = o / (2 * R), ch = ((o % (2 * R)) >> 4) ^ mn_sw<R>(k);
       src = base + (size_t)(k0 + k) * ld + min(r0 + ch * 8, rows - 8);
     }
     v[j] = *reinterpret_cast<const uint4*>(src);
@@ -454,7 +466,7 @@ __device__ __forceinline__ void stage_half(const uint16_t* __restrict__ base, in
       const int rl = o >> 7, c = ((o >> 4) & 7) ^ ((rl >> 1) & 7);
       src = base + (size_t)min(r0 + half_row<IS_A, WN>(rl, q), rows - 1) * ld + k0 + c * 8;
     } else {              // [64][R] image, mn_off<R>
-      const int k = o / (2 * R), ch = ((o % (2 * R)) >> 4) ^ ((mn_swz(k) << 1) & (R / 8 - 1));
+      const int k = o / (2 * R), ch = ((o % (2 * R)) >> 4) ^ mn_sw<R>(k);
       src = base + (size_t)(k0 + k) * ld + min(r0 + half_row<IS_A, WN>(ch * 8, q), rows - 8);
     }
     __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(img + wbase), 16, 0, 0);

@@ -236,15 +236,18 @@ struct Args {
 // variables written through, 6 every workgroup arrived, 7 done count published
 #define RTS(k, slot)                                                                             \
   if (a.res_ts != nullptr) a.res_ts[((k) & 63) * 8 + (slot)] = (long long)__builtin_amdgcn_s_memrealtime();
-// phase stamp ph of step st (s_memrealtime, 100 MHz) -- profiling only
-#define PH(ph)                                                                                 \
-  if (a.phase_ts != nullptr && lane == 0 && st < 64)                                         \
-    a.phase_ts[((long long)st * 64 + c) * 16 + (ph)] = (long long)__builtin_amdgcn_s_memrealtime();
+// phase stamp ph of step st (s_memrealtime, 100 MHz) -- profiling only: compiled
+// into the instrumented instantiations (INS) alone, absent from production code
+#define PH(ph)                                                                                   \
+  if constexpr (INS) {                                                                           \
+    if (a.phase_ts != nullptr && lane == 0 && st < 64)                                           \
+      a.phase_ts[((long long)st * 64 + c) * 16 + (ph)] = (long long)__builtin_amdgcn_s_memrealtime(); \
+  }
 // DTF_PERSIST_DBG bit 1: wave 0 stamps the head's sub-phases into slots 13-15 (wave 7's stamps off)
 #define PHX(ph) \
-  if ((a.dbg & 2) != 0) { PH(ph); }
+  if ((dbg & 2) != 0) { PH(ph); }
 #define PH7(ph) \
-  if ((a.dbg & 2) == 0) { PH(ph); }
+  if ((dbg & 2) == 0) { PH(ph); }
 
 // The exact three-way split v = hi + mid + lo by truncation, as fp32 bit
 // patterns whose low 16 bits are zero: hi keeps v's top 8 significant bits, the
@@ -291,6 +294,9 @@ __device__ __forceinline__ bf16x8 px8(uint32_t w0, uint32_t w1) {
 #define PRO(wg, k)                                                                             \
   if (a.phase_ts != nullptr)                                                                   \
     a.phase_ts[((long long)64 * 64 + (wg)) * 16 + (k)] = (long long)__builtin_amdgcn_s_memrealtime();
+// the same in compute: instrumented instantiations only
+#define PROC(wg, k) \
+  if constexpr (INS) { PRO(wg, k); }
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -359,9 +365,12 @@ __device__ __forceinline__ float xor32(float v) {
 // few that were not there yet (no order between a producer's lanes).  A sweep
 // of every lane over every slot per poll was ~5 MB of L2 traffic per round.
 // false on timeout / error.
-template <int N, typename SlotOff>
+// (gm: the poll mode -- 1, direct loads without sleeps, in production; the
+// instrumented instantiations take DTF_GATHER_MODE)
+template <int N, bool INS, typename SlotOff>
 __device__ __forceinline__ bool gather_gran(__amdgpu_buffer_rsrc_t rs, SlotOff slot, int skip, bool need, int probe,
                                             unsigned tag, f32x4 own, f32x4 (&part)[N], int lane, const Args& a) {
+  const int gm = INS ? a.gmode : 1;
   bool have[N];
 #pragma unroll
   for (int k = 0; k < N; ++k) {
@@ -369,7 +378,7 @@ __device__ __forceinline__ bool gather_gran(__amdgpu_buffer_rsrc_t rs, SlotOff s
     part[k] = (k == skip) ? own : f32x4{0.f, 0.f, 0.f, 0.f};
   }
   const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-  bool seen = lane >= N || lane == skip || a.gmode != 0;
+  bool seen = lane >= N || lane == skip || gm != 0;
   for (;;) {
     asm volatile("" ::: "memory");   // re-load every pass (no loop-invariant hoisting)
     if (!seen) {
@@ -392,8 +401,8 @@ __device__ __forceinline__ bool gather_gran(__amdgpu_buffer_rsrc_t rs, SlotOff s
       all = all && have[k];
     }
     if (__all(all)) return true;
-    if (a.gmode == 2) __builtin_amdgcn_s_sleep(2);
-    else if (a.gmode == 3) __builtin_amdgcn_s_sleep(8);
+    if (gm == 2) __builtin_amdgcn_s_sleep(2);
+    else if (gm == 3) __builtin_amdgcn_s_sleep(8);
     if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > a.timeout ||
         __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
       if (lane == 0) atomicOr(a.err, 1);
@@ -691,9 +700,12 @@ __device__ void copier_res(const Args& a, int cid, uint8_t* smem) {
 // (a 2x / 4x wider feature slice), E1 gathers 2 slices (EXP 2) or disappears
 // (EXP 4).  The sums are rescaled, so training still runs, but the numerics are
 // not the reference's: stamps and step times only.
-template <int ACT, int NW, bool SPLIT, bool RES, int EXP = 0>
+// INS: the instrumented build (phase stamps, DTF_PERSIST_DBG / DTF_GATHER_MODE
+// knobs) -- production instantiations carry none of that code
+template <int ACT, int NW, bool SPLIT, bool RES, int EXP = 0, bool INS = false>
 __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) {
   constexpr int XR = EXP > 1 ? EXP : 1;
+  const int dbg = INS ? a.dbg : 0;
   constexpr bool MULTI = NW > 1;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
@@ -710,7 +722,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
   int* abort_flag = reinterpret_cast<int*>(smem + L_FLAG);
   int* census = abort_flag + 1;
   uint16_t* dzp = reinterpret_cast<uint16_t*>(smem + L_DZP);
-  if (tid == 0) { PRO(c, 0); }
+  if (tid == 0) { PROC(c, 0); }
 
   // ---- load state: every global load of the prologue is issued first (the
   // master weights, the small parameters into registers, the step / sequence /
@@ -872,7 +884,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
   // launch): the census entry goes out first, the first step's x stage is
   // issued (LDS-DMA) while the parameter loads above are still in flight, and
   // wave 0 polls the census meanwhile; one drain + barrier then covers all three.
-  if (tid == 0) { PRO(c, 4); }
+  if (tid == 0) { PROC(c, 4); }
   // ---- placement census: E1 group (the NQ slices of block j) and E2 group (the
   // NJ blocks of slice q) each on this workgroup's XCD -> that edge stays in one
   // L2 (plain stores).  Decided per launch from HW_REG_XCC_ID, never assumed.
@@ -956,12 +968,12 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
   if (failed_in || *census < 0) return;
   const bool l2_e1 = (*census & 1) != 0;
   const bool l2_e2 = (*census & 2) != 0;
-  if (tid == 0) { PRO(c, 1); }
+  if (tid == 0) { PROC(c, 1); }
   if constexpr (!RES) {
     read_xf();
     read_xt();
   }
-  if (tid == 0) { PRO(c, 2); }
+  if (tid == 0) { PROC(c, 2); }
 
   // RES: the run's record -> LDS at the top of every step.  The copiers stored it
   // write-through (sc1) and each added to the staged count after its waves'
@@ -1120,15 +1132,15 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
                                                       __HIP_MEMORY_SCOPE_WORKGROUP) >= st + 1;
       return (unsigned)__ballot(ok) & ((1u << NBT) - 1u);
     };
-    if (w == 7 && more && !(a.dbg & 1)) {
+    if (w == 7 && more && !(dbg & 1)) {
       // DTF_PERSIST_DBG bits 2 / 3 (tuning): the whole stage / its second half only
       // once the first head is done (its DMA then does not queue in front of this
       // CU's E1 / E2 gather loads)
-      if (a.dbg & 8) stage_x(st + 1, 0, 2);
-      if (a.dbg & 12) {
+      if (dbg & 8) stage_x(st + 1, 0, 2);
+      if (dbg & 12) {
         while (heads_done() == 0u) __builtin_amdgcn_s_sleep(1);
       }
-      if (a.dbg & 8) stage_x(st + 1, 1, 2);
+      if (dbg & 8) stage_x(st + 1, 1, 2);
       else
         for (int xr = 0; xr < XR; ++xr) stage_x(st + 1, 0, 1);
       // idle until the first head is done anyway: wait for the DMA here and tell the
@@ -1168,12 +1180,12 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
         z = zs * 4.f;
       } else if constexpr (EXP == 2) {
         f32x4 part[2];
-        ok = gather_gran<2>(r1, [&](int k) { return (((q & 2) + k) * NBT + w) * GSLOT; }, q & 1, true, 63, tag, zs, part,
+        ok = gather_gran<2, INS>(r1, [&](int k) { return (((q & 2) + k) * NBT + w) * GSLOT; }, q & 1, true, 63, tag, zs, part,
                             lane, a);
         z = (part[0] + part[1]) * 2.f;
       } else {
         f32x4 part[NQ];
-        ok = gather_gran<NQ>(r1, [&](int k) { return (k * NBT + w) * GSLOT; }, q, true, 63, tag, zs, part, lane, a);
+        ok = gather_gran<NQ, INS>(r1, [&](int k) { return (k * NBT + w) * GSLOT; }, q, true, 63, tag, zs, part, lane, a);
         z = part[0];
 #pragma unroll
         for (int qq = 1; qq < NQ; ++qq) z += part[qq];
@@ -1203,7 +1215,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
 #pragma unroll
       for (int i = 0; i < 4; ++i) a2T[(4 * g + i) * LS + bw] = a2[i];
       f32x4 lp[NJ];
-      ok = gather_gran<NJ>(r2, [&](int k) { return k * GSLOT; }, j, g < 3, 47, tag, pl, lp, lane, a) && ok;
+      ok = gather_gran<NJ, INS>(r2, [&](int k) { return k * GSLOT; }, j, g < 3, 47, tag, pl, lp, lane, a) && ok;
       if (w == 0) { PH(7); }
       if (!ok && lane == 0) *abort_flag = 1;
       // logits, softmax cross-entropy, accuracy -- identical in every workgroup
@@ -1373,7 +1385,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
         }
         if (cc == NCH) break;
         if (!did) {
-          if (a.dbg & 16) __builtin_amdgcn_s_sleep(2);
+          if (dbg & 16) __builtin_amdgcn_s_sleep(2);
           else __builtin_amdgcn_s_sleep(0);
         }
       }
@@ -1663,7 +1675,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
   }
   if (aborted) return;
   __syncthreads();   // wave 7's last small-parameter update
-  if (tid == 0) { PRO(c, 3); }
+  if (tid == 0) { PROC(c, 3); }
 
   // ---- write back (fp32 master), global step, exchange sequence, end stamp
   // (RES: the steps that ran -- the sequence never falls behind the tags in use)
@@ -1674,7 +1686,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
     if (a.step_ts != nullptr)
       a.step_ts[(gstep0 + st_done) % a.ts_ring] = (long long)__builtin_amdgcn_s_memrealtime();
   }
-  if (tid == 0) { PRO(c, 5); }
+  if (tid == 0) { PROC(c, 5); }
 }
 
 // packed placement (a.spread == 0): compute workgroup c runs as blockIdx 8c, so
@@ -1682,7 +1694,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
 // L2); the first NCOP other blocks copy, the rest exit.  spread (several ranks on
 // one GPU, tests): compute = blocks 0..27, copiers = 28..43.  Placement is speed
 // only: the census above decides each edge's store flavour.
-template <int ACT, int NW, bool SPLIT, bool RES = false, int EXP = 0>
+template <int ACT, int NW, bool SPLIT, bool RES = false, int EXP = 0, bool INS = false>
 __global__ __launch_bounds__(THREADS, 1) void mlp_persist_f32(Args a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int b = blockIdx.x;
@@ -1693,7 +1705,7 @@ __global__ __launch_bounds__(THREADS, 1) void mlp_persist_f32(Args a) {
     if ((b & 7) == 0) c = b >> 3; else cid = b - (b >> 3) - 1;
   }
   if (c >= 0) {
-    if (a.nsteps > 0) compute<ACT, NW, SPLIT, RES, EXP>(a, c / NQ, c % NQ, smem);
+    if (a.nsteps > 0) compute<ACT, NW, SPLIT, RES, EXP, INS>(a, c / NQ, c % NQ, smem);
     return;
   }
   if constexpr (RES) copier_res(a, cid, smem);
@@ -1803,7 +1815,8 @@ hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int n
     }();
     if (exper == 2 || exper == 4) {
       if (act != 0 || W != 1 || !split || spread) return hipErrorInvalidValue;
-      static const Kern2 xk[2] = {mlp_persist_f32<0, 1, true, false, 2>, mlp_persist_f32<0, 1, true, false, 4>};
+      static const Kern2 xk[2] = {mlp_persist_f32<0, 1, true, false, 2, true>,
+                                  mlp_persist_f32<0, 1, true, false, 4, true>};
       const Kern2 k = xk[exper == 2 ? 0 : 1];
       static bool xattr = false;
       if (!xattr) {
@@ -1843,6 +1856,23 @@ hipError_t dtfk_mlp_persist_f32(const void* stage, long long rec_h, int B, int n
   const int nwi = W <= 1 ? 0 : (W <= 2 ? 1 : (W <= 4 ? 2 : 3));
   const int which = (act == 0 ? 0 : 1) + 2 * nwi + (split ? 8 : 0);
   const int grid = spread ? GRID_SPREAD : GRID_PACKED;
+  if (phase_ts != nullptr || a.dbg != 0 || a.gmode != 1) {
+    // profiling / tuning: the instrumented build (one GPU only)
+    if (W != 1) return hipErrorInvalidValue;
+    static const Kern ik[4] = {mlp_persist_f32<0, 1, false, false, 0, true>, mlp_persist_f32<1, 1, false, false, 0, true>,
+                               mlp_persist_f32<0, 1, true, false, 0, true>, mlp_persist_f32<1, 1, true, false, 0, true>};
+    static bool iattr = false;
+    if (!iattr) {
+      for (Kern k : ik) {
+        const hipError_t e =
+            hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+      }
+      iattr = true;
+    }
+    hipLaunchKernelGGL(ik[(act == 0 ? 0 : 1) + (split ? 2 : 0)], dim3(grid), dim3(THREADS), lds, stream, a);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(kerns[which], dim3(grid), dim3(THREADS), lds, stream, a);
   return hipGetLastError();
 }

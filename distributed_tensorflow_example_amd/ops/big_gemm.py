@@ -53,8 +53,19 @@ _TABLE = {
 }
 
 
+# A/B runs: DTF_BIG_GEMM_SET="dx:16384:768:3072=1,fwd:16384:768:3072=0" overrides
+# single table entries (1 = gemm_big, 0 = hipBLASLt)
+_OVERRIDE = {}
+for _item in filter(None, os.environ.get("DTF_BIG_GEMM_SET", "").split(",")):
+    _k, _v = _item.split("=")
+    _r, _m, _n, _kk = _k.split(":")
+    _OVERRIDE[(_r, int(_m), int(_n), int(_kk))] = _v.strip() == "1"
+
+
 def _fixed(key):
     """The table's engine for `key` under 'auto' (None: not listed / table off)."""
+    if key in _OVERRIDE:
+        return _OVERRIDE[key]
     if not _TABLE_ON or _POLICY != "auto":
         return None
     return _TABLE.get(key)

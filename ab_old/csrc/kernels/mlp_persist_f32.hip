@@ -392,9 +392,7 @@ __device__ __forceinline__ bool gather_gran(__amdgpu_buffer_rsrc_t rs, SlotOff s
       return false;
     }
   }
-  // the clock and the error word are checked every 8th pass only: a pass is one
-  // L2 round trip, and the consumer CU's memory queue is what a hand-off waits on
-  for (int it = 1;; ++it) {
+  for (;;) {
     asm volatile("" ::: "memory");
     bool all = true;
 #pragma unroll
@@ -405,8 +403,8 @@ __device__ __forceinline__ bool gather_gran(__amdgpu_buffer_rsrc_t rs, SlotOff s
     if (__all(all)) return true;
     if (gm == 2) __builtin_amdgcn_s_sleep(2);
     else if (gm == 3) __builtin_amdgcn_s_sleep(8);
-    if ((it & 7) == 0 && ((long long)__builtin_amdgcn_s_memrealtime() - t0 > a.timeout ||
-                          __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)) {
+    if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > a.timeout ||
+        __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
       if (lane == 0) atomicOr(a.err, 1);
       return false;
     }

@@ -1,0 +1,728 @@
+// Reached by: ops/transformer.py (BERT-base elementwise / layernorm / softmax); tests/test_transformer_gpu.py
+// Fused transformer-block kernels for the BERT path (BASELINE config #4),
+// written for CDNA4: one wave64 per row, 8-byte bf16x4 vector accesses,
+// fp32 statistics, no LDS round-trips for row reductions.
+//
+//   bdrln_fwd   y = LayerNorm(dropout(x + bias) + residual) * gamma + beta
+//               (the attention-output / FFN-output epilogue of every layer;
+//               saves s = dropout(x+bias)+residual and mean/rstd for bwd)
+//   ln_bwd      ds = LN'(dy), dx_branch = ds * mask/keep, per-slice
+//               dgamma/dbeta partials (deterministic 2-pass column sums)
+//   bias_gelu   y = gelu(x + bias) fwd / dx = dy * gelu'(x + bias) bwd
+//   softmax     P = softmax(scale * S + mask[b, key]) with attention-prob
+//               dropout fused (mask regenerated from a counter hash in bwd)
+//
+// Dropout masks are never stored: keep(i) = hash(seed, i) >= p * 2^32 is
+// recomputed in the backward pass from the same (seed, element index).
+#include "common.h"
+
+namespace dtfk {
+namespace tfm {
+
+
+__device__ __forceinline__ bool keep_elem(uint64_t seed, uint64_t i, uint32_t thresh) {
+  return thresh == 0u || hash32(seed, i) >= thresh;
+}
+
+struct bf4 { uint16_t v[4]; };
+__device__ __forceinline__ void ld4(const uint16_t* p, float* f) {
+  const uint2 u = *reinterpret_cast<const uint2*>(p);
+  f[0] = bf2f(u.x & 0xFFFF); f[1] = bf2f(u.x >> 16); f[2] = bf2f(u.y & 0xFFFF); f[3] = bf2f(u.y >> 16);
+}
+__device__ __forceinline__ void st4(uint16_t* p, const float* f) {
+  uint2 u;
+  u.x = pack2bf(f[0], f[1]);
+  u.y = pack2bf(f[2], f[3]);
+  *reinterpret_cast<uint2*>(p) = u;
+}
+__device__ __forceinline__ void ld4f(const float* p, float* f) {
+  const float4 u = *reinterpret_cast<const float4*>(p);
+  f[0] = u.x; f[1] = u.y; f[2] = u.z; f[3] = u.w;
+}
+
+// ---------------------------------------------------------------- fused bias+dropout+residual+LN
+template <int NC>
+__global__ __launch_bounds__(256) void bdrln_fwd(
+    const uint16_t* __restrict__ x, const float* __restrict__ bias, const uint16_t* __restrict__ res,
+    const float* __restrict__ gamma, const float* __restrict__ beta, uint16_t* __restrict__ y,
+    uint16_t* __restrict__ s_out, float* __restrict__ mean_out, float* __restrict__ rstd_out, int N, int H,
+    float eps, uint32_t thresh, float inv_keep, uint64_t seed) {
+  const int lane = threadIdx.x & 63;
+  for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < N; row += gridDim.x * 4) {
+    const size_t base = (size_t)row * H;
+    float v[NC][4];
+    float sum = 0.f;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      if (k < NC) {
+        const int c = (k * 64 + lane) * 4;
+        float xv[4], bv[4], rv[4];
+        ld4(x + base + c, xv);
+        ld4f(bias + c, bv);
+        if (res) ld4(res + base + c, rv); else rv[0] = rv[1] = rv[2] = rv[3] = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float t = xv[j] + bv[j];
+          if (thresh) t = keep_elem(seed, base + c + j, thresh) ? t * inv_keep : 0.f;
+          v[k][j] = t + rv[j];
+          sum += v[k][j];
+        }
+      }
+    }
+    const float mean = wave_sum(sum) / H;
+    float var = 0.f;
+#pragma unroll
+    for (int k = 0; k < NC; ++k)
+      if (k < NC)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { const float d = v[k][j] - mean; var += d * d; }
+    const float rstd = rsqrtf(wave_sum(var) / H + eps);
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      if (k < NC) {
+        const int c = (k * 64 + lane) * 4;
+        float g[4], b[4], o[4];
+        ld4f(gamma + c, g);
+        ld4f(beta + c, b);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = (v[k][j] - mean) * rstd * g[j] + b[j];
+        st4(y + base + c, o);
+        if (s_out) st4(s_out + base + c, v[k]);
+      }
+    }
+    if (lane == 0) {
+      mean_out[row] = mean;
+      rstd_out[row] = rstd;
+    }
+  }
+}
+
+// LN backward.  s: the normalised input (bf16), dy: upstream grad (bf16).
+// Outputs ds (bf16, grad wrt s == grad for the residual branch), optionally
+// dxb = ds * keep/keep_prob (grad wrt x+bias of the dropout branch, bf16),
+// and per-block partial column sums of dgamma, dbeta, dbias (fp32 [grid, H]).
+template <int NC>
+__global__ __launch_bounds__(256) void ln_bwd(
+    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ s, const float* __restrict__ mean_in,
+    const float* __restrict__ rstd_in, const float* __restrict__ gamma, uint16_t* __restrict__ ds_out,
+    uint16_t* __restrict__ dxb_out, float* __restrict__ part_g, float* __restrict__ part_b,
+    float* __restrict__ part_bias, int N, int H, uint32_t thresh, float inv_keep, uint64_t seed) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float accg[NC][4], accb[NC][4], accx[NC][4];
+#pragma unroll
+  for (int k = 0; k < NC; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) accg[k][j] = accb[k][j] = accx[k][j] = 0.f;
+
+  for (int row = blockIdx.x * 4 + wid; row < N; row += gridDim.x * 4) {
+    const size_t base = (size_t)row * H;
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float xh[NC][4], gdy[NC][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      if (k < NC) {
+        const int c = (k * 64 + lane) * 4;
+        float sv[4], dv[4], g[4];
+        ld4(s + base + c, sv);
+        ld4(dy + base + c, dv);
+        ld4f(gamma + c, g);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          xh[k][j] = (sv[j] - mean) * rstd;
+          gdy[k][j] = dv[j] * g[j];
+          s1 += gdy[k][j];
+          s2 += gdy[k][j] * xh[k][j];
+          accg[k][j] += dv[j] * xh[k][j];
+          accb[k][j] += dv[j];
+        }
+      }
+    }
+    s1 = wave_sum(s1) / H;
+    s2 = wave_sum(s2) / H;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      if (k < NC) {
+        const int c = (k * 64 + lane) * 4;
+        float d[4], dx[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          d[j] = rstd * (gdy[k][j] - s1 - xh[k][j] * s2);
+          dx[j] = thresh ? (keep_elem(seed, base + c + j, thresh) ? d[j] * inv_keep : 0.f) : d[j];
+          accx[k][j] += dx[j];
+        }
+        st4(ds_out + base + c, d);
+        if (dxb_out) st4(dxb_out + base + c, dx);
+      }
+    }
+  }
+  // block-level column partials: 4 waves -> LDS -> one row per block
+  __shared__ float red[4][64 * 4];
+  float* outs[3] = {part_g, part_b, part_bias};
+#pragma unroll
+  for (int which = 0; which < 3; ++which) {
+    float* out = outs[which];
+    if (!out) continue;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        red[wid][lane * 4 + j] = which == 0 ? accg[k][j] : (which == 1 ? accb[k][j] : accx[k][j]);
+      __syncthreads();
+      if (wid == 0)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int i = lane * 4 + j;
+          out[(size_t)blockIdx.x * H + (k * 64 + lane) * 4 + j] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+        }
+      __syncthreads();
+    }
+  }
+}
+
+// Plain LayerNorm forward (fp32 or bf16 input via template) for embeddings.
+// (bdrln_fwd with bias = 0, no residual, no dropout covers it; kept separate
+// only to accept fp32 inputs.)
+template <int NC>
+__global__ __launch_bounds__(256) void ln_fwd_f32in(
+    const float* __restrict__ x, const float* __restrict__ gamma, const float* __restrict__ beta,
+    uint16_t* __restrict__ y, uint16_t* __restrict__ s_out, float* __restrict__ mean_out,
+    float* __restrict__ rstd_out, int N, int H, float eps, uint32_t thresh, float inv_keep, uint64_t seed) {
+  const int lane = threadIdx.x & 63;
+  for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < N; row += gridDim.x * 4) {
+    const size_t base = (size_t)row * H;
+    float v[NC][4];
+    float sum = 0.f;
+#pragma unroll
+    for (int k = 0; k < NC; ++k)
+      if (k < NC) {
+        ld4f(x + base + (k * 64 + lane) * 4, v[k]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sum += v[k][j];
+      }
+    const float mean = wave_sum(sum) / H;
+    float var = 0.f;
+#pragma unroll
+    for (int k = 0; k < NC; ++k)
+      if (k < NC)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { const float d = v[k][j] - mean; var += d * d; }
+    const float rstd = rsqrtf(wave_sum(var) / H + eps);
+#pragma unroll
+    for (int k = 0; k < NC; ++k)
+      if (k < NC) {
+        const int c = (k * 64 + lane) * 4;
+        float g[4], b[4], o[4];
+        ld4f(gamma + c, g);
+        ld4f(beta + c, b);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          o[j] = (v[k][j] - mean) * rstd * g[j] + b[j];
+          if (thresh) o[j] = keep_elem(seed, base + c + j, thresh) ? o[j] * inv_keep : 0.f;
+        }
+        st4(y + base + c, o);
+        if (s_out) st4(s_out + base + c, v[k]);
+      }
+    if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
+  }
+}
+
+// ---------------------------------------------------------------- bias + GELU (erf form)
+// Exact-GELU normal CDF via Abramowitz-Stegun 7.1.26 (|erf error| <= 1.5e-7,
+// far below bf16's 4e-3): one rcp, one exp, a 5-term polynomial.  The exp is
+// exp(-z^2/2), which is also the normal pdf's, so gelu' costs one more FMA.
+// The bf16 [tokens, 3072] GELU tensors are large enough that libm erff made
+// these elementwise kernels VALU-bound rather than HBM-bound.
+__device__ __forceinline__ float gelu_f(float z) {
+  float cdf, pdf;
+  gelu_cdf_pdf(z, cdf, pdf);
+  return z * cdf;
+}
+__device__ __forceinline__ float gelu_grad(float z) {
+  float cdf, pdf;
+  gelu_cdf_pdf(z, cdf, pdf);
+  return fmaf(z, pdf, cdf);
+}
+
+__global__ __launch_bounds__(256) void bias_gelu_fwd(const uint16_t* __restrict__ x, const float* __restrict__ bias,
+                                                     uint16_t* __restrict__ y, int64_t n4, int H) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = i * 4;
+    const int c = (int)(e % H);
+    float xv[4], bv[4], o[4];
+    ld4(x + e, xv);
+    ld4f(bias + c, bv);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = gelu_f(xv[j] + bv[j]);
+    st4(y + e, o);
+  }
+}
+
+// dx = dy * gelu'(x + b) (bf16), plus per-block column partials of dx (dbias).
+// Block = 256 threads covers one 1024-column strip (H % 1024 handled by rows
+// of strips); grid.x = column strips, grid.y = row slices.
+__global__ __launch_bounds__(256) void bias_gelu_bwd(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
+                                                     const float* __restrict__ bias, uint16_t* __restrict__ dx,
+                                                     float* __restrict__ part, int N, int H, int rows_per) {
+  const int c = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (c >= H) return;
+  const int r0 = blockIdx.y * rows_per, r1 = min(N, r0 + rows_per);
+  float bv[4], acc[4] = {0.f, 0.f, 0.f, 0.f};
+  ld4f(bias + c, bv);
+  for (int r = r0; r < r1; ++r) {
+    const size_t e = (size_t)r * H + c;
+    float dv[4], xv[4], o[4];
+    ld4(dy + e, dv);
+    ld4(x + e, xv);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      o[j] = dv[j] * gelu_grad(xv[j] + bv[j]);
+      acc[j] += o[j];
+    }
+    st4(dx + e, o);
+  }
+  float* p = part + (size_t)blockIdx.y * H + c;
+  p[0] = acc[0]; p[1] = acc[1]; p[2] = acc[2]; p[3] = acc[3];
+}
+
+// 8-wide forms (H % 8 == 0): 16-byte accesses, four rows in flight per thread.
+__device__ __forceinline__ void ld8v(const uint16_t* p, float* f) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { f[2 * j] = bf2f(w[j] & 0xffff); f[2 * j + 1] = bf2f(w[j] >> 16); }
+}
+__device__ __forceinline__ void st8v(uint16_t* p, const float* f) {
+  *reinterpret_cast<uint4*>(p) = uint4{pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]), pack2bf(f[6], f[7])};
+}
+
+__global__ __launch_bounds__(256) void bias_gelu_fwd8(const uint16_t* __restrict__ x, const float* __restrict__ bias,
+                                                      uint16_t* __restrict__ y, int64_t n8, int H) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)((i * 8) % H);
+    float xv[8], bv[8], o[8];
+    ld8v(x + i * 8, xv);
+    ld4f(bias + c, bv);
+    ld4f(bias + c + 4, bv + 4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = gelu_f(xv[j] + bv[j]);
+    st8v(y + i * 8, o);
+  }
+}
+
+// Block = 128 threads x 8 columns (a 1024-column strip); grid = (strips, row slices)
+__global__ __launch_bounds__(128) void bias_gelu_bwd8(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
+                                                      const float* __restrict__ bias, uint16_t* __restrict__ dx,
+                                                      float* __restrict__ part, int N, int H, int rows_per) {
+  const int c = (blockIdx.x * 128 + threadIdx.x) * 8;
+  if (c >= H) return;
+  const int r0 = blockIdx.y * rows_per, r1 = min(N, r0 + rows_per);
+  float bv[8], acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  ld4f(bias + c, bv);
+  ld4f(bias + c + 4, bv + 4);
+  int r = r0;
+  for (; r + 3 < r1; r += 4) {
+    float dv[4][8], xv[4][8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      ld8v(dy + (size_t)(r + k) * H + c, dv[k]);
+      ld8v(x + (size_t)(r + k) * H + c, xv[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        o[j] = dv[k][j] * gelu_grad(xv[k][j] + bv[j]);
+        acc[j] += o[j];
+      }
+      st8v(dx + (size_t)(r + k) * H + c, o);
+    }
+  }
+  for (; r < r1; ++r) {
+    float dv[8], xv[8], o[8];
+    ld8v(dy + (size_t)r * H + c, dv);
+    ld8v(x + (size_t)r * H + c, xv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      o[j] = dv[j] * gelu_grad(xv[j] + bv[j]);
+      acc[j] += o[j];
+    }
+    st8v(dx + (size_t)r * H + c, o);
+  }
+  float* p = part + (size_t)blockIdx.y * H + c;
+  *reinterpret_cast<float4*>(p) = float4{acc[0], acc[1], acc[2], acc[3]};
+  *reinterpret_cast<float4*>(p + 4) = float4{acc[4], acc[5], acc[6], acc[7]};
+}
+
+// column sums of up to 3 [P, H] fp32 partial buffers -> out_k[H] (deterministic;
+// blockIdx.y picks the buffer).  accumulate: out_k += sum (a gradient sunk into
+// the parameter's .grad) instead of out_k = sum.  1024 threads = 64 consecutive
+// columns x 16 row groups (coalesced 256 B rows), LDS tree over the groups;
+// grid = (ceil(H / 64), nbuf).
+struct ColsumArgs {
+  const float* part[3];
+  float* out[3];
+};
+// 1024 threads = 16 consecutive columns x 64 row groups: a thread sums only
+// P / 64 partial rows (4 loads in flight), so the few-microsecond latency of
+// this launch-bound pass is ~2 memory round trips instead of ~8 with 64-wide
+// column tiles; LDS tree over the groups, fixed order (deterministic).
+constexpr int CS_COLS = 16, CS_GROUPS = 64;
+__global__ __launch_bounds__(1024) void colsum_partials(ColsumArgs a, int P, int H, int accumulate) {
+  __shared__ float red[CS_GROUPS][CS_COLS];
+  const float* __restrict__ part = a.part[blockIdx.y];
+  float* __restrict__ out = a.out[blockIdx.y];
+  const int lane = threadIdx.x % CS_COLS, g = threadIdx.x / CS_COLS;
+  const int c = blockIdx.x * CS_COLS + lane;
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  if (c < H) {
+    int p = g;
+    for (; p + 3 * CS_GROUPS < P; p += 4 * CS_GROUPS) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s[u] += part[(size_t)(p + CS_GROUPS * u) * H + c];
+    }
+    for (; p < P; p += CS_GROUPS) s[0] += part[(size_t)p * H + c];
+  }
+  red[g][lane] = (s[0] + s[1]) + (s[2] + s[3]);
+  __syncthreads();
+#pragma unroll
+  for (int st = CS_GROUPS / 2; st > 0; st >>= 1) {
+    if (g < st) red[g][lane] += red[g + st][lane];
+    __syncthreads();
+  }
+  if (g == 0 && c < H) {
+    const float t = red[0][lane];
+    out[c] = accumulate ? out[c] + t : t;
+  }
+}
+
+// per-slice column sums of a bf16 [N, H] matrix -> part[P][H] fp32 (first stage of
+// a bias gradient; colsum_partials finishes it).  grid = (ceil(H / 512), P), block
+// 256 = 64 lanes x 8 columns each (16-byte loads) x 4 row groups; slice p covers
+// rows [p*N/P, (p+1)*N/P).  H % 8 == 0.
+__global__ __launch_bounds__(256) void colsum_bf16_partials(const uint16_t* __restrict__ x, float* __restrict__ part,
+                                                            int N, int H) {
+  __shared__ float red[4][512];
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c0 = blockIdx.x * 512 + 8 * lane;
+  const int P = gridDim.y;
+  const int r0 = (int)((long long)N * blockIdx.y / P), r1 = (int)((long long)N * (blockIdx.y + 1) / P);
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c0 < H)
+    for (int r = r0 + g; r < r1; r += 4) {
+      const uint4 v = *reinterpret_cast<const uint4*>(x + (size_t)r * H + c0);
+      const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { s[2 * k] += bf2f(wv[k] & 0xffff); s[2 * k + 1] += bf2f(wv[k] >> 16); }
+    }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[g][8 * lane + k] = s[k];
+  __syncthreads();
+  for (int c = threadIdx.x; c < 512; c += 256)
+    if (blockIdx.x * 512 + c < H)
+      part[(size_t)blockIdx.y * H + blockIdx.x * 512 + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+}
+
+// out[i] (+)= sum_s slabs[s][i]: the split-K weight-gradient slabs folded into
+// the gradient (sink) in one pass; fp32, n % 4 == 0.
+__global__ __launch_bounds__(256) void slab_sum(const float* __restrict__ slabs, float* __restrict__ out, int S,
+                                                long long n4, int accumulate) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  const float4* sl = reinterpret_cast<const float4*>(slabs);
+  float4 t = sl[i];
+  for (int k = 1; k < S; ++k) {
+    const float4 v = sl[(long long)k * n4 + i];
+    t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+  }
+  float4* o = reinterpret_cast<float4*>(out);
+  if (accumulate) {
+    const float4 v = o[i];
+    t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+  }
+  o[i] = t;
+}
+
+// ---------------------------------------------------------------- attention softmax
+// scores: [B*heads*Sq, Sk] bf16 (raw Q.K^T); mask: [B, Sk] fp32 additive.
+// P = softmax(scale*scores + mask) (bf16, saved for bwd); Pd = dropout(P).
+// One wave per row; Sk <= 4096, Sk % 4 == 0.
+template <int NC>
+__global__ __launch_bounds__(256) void softmax_fwd(const uint16_t* __restrict__ S, const float* __restrict__ mask,
+                                                   uint16_t* __restrict__ P, uint16_t* __restrict__ Pd, int rows,
+                                                   int Sk, int rows_per_batch, float scale, uint32_t thresh,
+                                                   float inv_keep, uint64_t seed) {
+  const int lane = threadIdx.x & 63;
+  for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += gridDim.x * 4) {
+    const size_t base = (size_t)row * Sk;
+    const float* m = mask ? mask + (size_t)(row / rows_per_batch) * Sk : nullptr;
+    float v[NC][4];
+    float mx = -3.0e38f;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      if (k < NC) {
+        const int c = (k * 64 + lane) * 4;
+        if (c < Sk) {
+          float sv[4], mv[4] = {0.f, 0.f, 0.f, 0.f};
+          ld4(S + base + c, sv);
+          if (m) ld4f(m + c, mv);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { v[k][j] = sv[j] * scale + mv[j]; mx = fmaxf(mx, v[k][j]); }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[k][j] = -3.0e38f;
+        }
+      }
+    }
+    mx = wave_max(mx);
+    float sum = 0.f;
+#pragma unroll
+    for (int k = 0; k < NC; ++k)
+      if (k < NC)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { v[k][j] = __expf(v[k][j] - mx); sum += v[k][j]; }
+    const float inv = 1.f / wave_sum(sum);
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      if (k < NC) {
+        const int c = (k * 64 + lane) * 4;
+        if (c < Sk) {
+          float p[4], pd[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            p[j] = v[k][j] * inv;
+            pd[j] = thresh ? (keep_elem(seed, base + c + j, thresh) ? p[j] * inv_keep : 0.f) : p[j];
+          }
+          st4(P + base + c, p);
+          if (Pd) st4(Pd + base + c, pd);
+        }
+      }
+    }
+  }
+}
+
+// dS = scale * P * (dP - sum(dP * P)), dP = dPd * keep / keep_prob.
+template <int NC>
+__global__ __launch_bounds__(256) void softmax_bwd(const uint16_t* __restrict__ dPd, const uint16_t* __restrict__ P,
+                                                   uint16_t* __restrict__ dS, int rows, int Sk, float scale,
+                                                   uint32_t thresh, float inv_keep, uint64_t seed) {
+  const int lane = threadIdx.x & 63;
+  for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += gridDim.x * 4) {
+    const size_t base = (size_t)row * Sk;
+    float pv[NC][4], dp[NC][4];
+    float dot = 0.f;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      if (k < NC) {
+        const int c = (k * 64 + lane) * 4;
+        if (c < Sk) {
+          ld4(P + base + c, pv[k]);
+          ld4(dPd + base + c, dp[k]);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (thresh) dp[k][j] = keep_elem(seed, base + c + j, thresh) ? dp[k][j] * inv_keep : 0.f;
+            dot += dp[k][j] * pv[k][j];
+          }
+        }
+      }
+    }
+    dot = wave_sum(dot);
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      if (k < NC) {
+        const int c = (k * 64 + lane) * 4;
+        if (c < Sk) {
+          float o[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = scale * pv[k][j] * (dp[k][j] - dot);
+          st4(dS + base + c, o);
+        }
+      }
+    }
+  }
+}
+
+// Generic dropout on bf16 (embedding output etc.): y = x * keep / keep_prob; bwd identical.
+__global__ __launch_bounds__(256) void dropout_bf16(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, int64_t n4,
+                                                    uint32_t thresh, float inv_keep, uint64_t seed) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = i * 4;
+    float v[4];
+    ld4(x + e, v);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = keep_elem(seed, e + j, thresh) ? v[j] * inv_keep : 0.f;
+    st4(y + e, v);
+  }
+}
+
+}  // namespace tfm
+}  // namespace dtfk
+
+using namespace dtfk::tfm;
+
+#define DTFK_NC_DISPATCH(ncval, LAUNCH)                                   \
+  switch (ncval) {                                                       \
+    case 1: { constexpr int NCv = 1; LAUNCH; break; }                    \
+    case 2: { constexpr int NCv = 2; LAUNCH; break; }                    \
+    case 3: { constexpr int NCv = 3; LAUNCH; break; }                    \
+    case 4: { constexpr int NCv = 4; LAUNCH; break; }                    \
+    case 6: { constexpr int NCv = 6; LAUNCH; break; }                    \
+    case 8: { constexpr int NCv = 8; LAUNCH; break; }                    \
+    case 12: { constexpr int NCv = 12; LAUNCH; break; }                  \
+    case 16: { constexpr int NCv = 16; LAUNCH; break; }                  \
+    default: return hipErrorInvalidValue;                                \
+  }
+
+static inline int row_grid(int rows) {
+  const int g = (rows + 3) / 4;
+  return g < 8192 ? (g > 0 ? g : 1) : 8192;
+}
+static inline uint32_t thresh_of(float p) {
+  if (p <= 0.f) return 0u;
+  double t = (double)p * 4294967296.0;
+  return t >= 4294967295.0 ? 4294967295u : (uint32_t)t;
+}
+
+extern "C" {
+
+hipError_t dtfk_bdrln_fwd(const void* x, const float* bias, const void* res, const float* gamma, const float* beta,
+                          void* y, void* s_out, float* mean, float* rstd, int N, int H, float eps, float p,
+                          unsigned long long seed, hipStream_t st) {
+  const float ik = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  if (H % 256) return hipErrorInvalidValue;
+  DTFK_NC_DISPATCH(H / 256, hipLaunchKernelGGL(bdrln_fwd<NCv>, dim3(row_grid(N)), dim3(256), 0, st,
+                     (const uint16_t*)x, bias, (const uint16_t*)res, gamma, beta, (uint16_t*)y, (uint16_t*)s_out,
+                     mean, rstd, N, H, eps, thresh_of(p), ik, (uint64_t)seed));
+  return hipGetLastError();
+}
+
+hipError_t dtfk_ln_fwd_f32in(const float* x, const float* gamma, const float* beta, void* y, void* s_out,
+                             float* mean, float* rstd, int N, int H, float eps, float p, unsigned long long seed,
+                             hipStream_t st) {
+  const float ik = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  if (H % 256) return hipErrorInvalidValue;
+  DTFK_NC_DISPATCH(H / 256, hipLaunchKernelGGL(ln_fwd_f32in<NCv>, dim3(row_grid(N)), dim3(256), 0, st, x, gamma,
+                     beta, (uint16_t*)y, (uint16_t*)s_out, mean, rstd, N, H, eps, thresh_of(p), ik, (uint64_t)seed));
+  return hipGetLastError();
+}
+
+// grid for ln_bwd is fixed by the caller (partial buffers are [grid, H]).
+hipError_t dtfk_ln_bwd(const void* dy, const void* s, const float* mean, const float* rstd, const float* gamma,
+                       void* ds, void* dxb, float* part_g, float* part_b, float* part_bias, int grid, int N, int H,
+                       float p, unsigned long long seed, hipStream_t st) {
+  const float ik = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  if (H % 256) return hipErrorInvalidValue;
+  DTFK_NC_DISPATCH(H / 256, hipLaunchKernelGGL(ln_bwd<NCv>, dim3(grid), dim3(256), 0, st, (const uint16_t*)dy,
+                     (const uint16_t*)s, mean, rstd, gamma, (uint16_t*)ds, (uint16_t*)dxb, part_g, part_b, part_bias,
+                     N, H, thresh_of(p), ik, (uint64_t)seed));
+  return hipGetLastError();
+}
+
+hipError_t dtfk_colsum_partials(const float* part, float* out, int P, int H, hipStream_t st) {
+  dtfk::tfm::ColsumArgs a = {{part, nullptr, nullptr}, {out, nullptr, nullptr}};
+  hipLaunchKernelGGL(colsum_partials, dim3((H + CS_COLS - 1) / CS_COLS, 1), dim3(1024), 0, st, a, P, H, 0);
+  return hipGetLastError();
+}
+
+// nbuf (<= 3) partial buffers -> outputs in ONE launch; accumulate: out += sum
+hipError_t dtfk_colsum_partials_multi(const float* const* parts, float* const* outs, int nbuf, int P, int H,
+                                      int accumulate, hipStream_t st) {
+  dtfk::tfm::ColsumArgs a = {{nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr}};
+  for (int k = 0; k < nbuf; ++k) { a.part[k] = parts[k]; a.out[k] = outs[k]; }
+  hipLaunchKernelGGL(colsum_partials, dim3((H + CS_COLS - 1) / CS_COLS, nbuf), dim3(1024), 0, st, a, P, H, accumulate);
+  return hipGetLastError();
+}
+
+hipError_t dtfk_colsum_bf16(const void* x, float* part, float* out, int N, int H, int P, int accumulate,
+                            hipStream_t st) {
+  if (H % 8 || ((uintptr_t)x % 16)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(colsum_bf16_partials, dim3((H + 511) / 512, P), dim3(256), 0, st,
+                     static_cast<const uint16_t*>(x), part, N, H);
+  dtfk::tfm::ColsumArgs a = {{part, nullptr, nullptr}, {out, nullptr, nullptr}};
+  hipLaunchKernelGGL(colsum_partials, dim3((H + CS_COLS - 1) / CS_COLS, 1), dim3(1024), 0, st, a, P, H, accumulate);
+  return hipGetLastError();
+}
+
+// scalar form for views that are not 16-byte aligned (DDP bucket offsets)
+__global__ __launch_bounds__(256) void slab_sum1(const float* __restrict__ slabs, float* __restrict__ out, int S,
+                                                 long long n, int accumulate) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float t = slabs[i];
+  for (int k = 1; k < S; ++k) t += slabs[(long long)k * n + i];
+  out[i] = accumulate ? out[i] + t : t;
+}
+
+hipError_t dtfk_slab_sum(const float* slabs, float* out, int S, long long n, int accumulate, hipStream_t st) {
+  if ((n % 4) || (((uintptr_t)slabs | (uintptr_t)out) % 16)) {
+    hipLaunchKernelGGL(slab_sum1, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, slabs, out, S, n, accumulate);
+    return hipGetLastError();
+  }
+  const long long n4 = n / 4;
+  hipLaunchKernelGGL(slab_sum, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, slabs, out, S, n4, accumulate);
+  return hipGetLastError();
+}
+
+hipError_t dtfk_bias_gelu_fwd(const void* x, const float* bias, void* y, long long n, int H, hipStream_t st) {
+  if (H % 8 == 0) {
+    const long long n8 = n / 8;
+    long long g8 = (n8 + 255) / 256;
+    if (g8 > 32768) g8 = 32768;
+    hipLaunchKernelGGL(bias_gelu_fwd8, dim3((unsigned)g8), dim3(256), 0, st, (const uint16_t*)x, bias,
+                       (uint16_t*)y, (int64_t)n8, H);
+    return hipGetLastError();
+  }
+  const long long n4 = n / 4;
+  long long g = (n4 + 255) / 256;
+  if (g > 65536) g = 65536;
+  hipLaunchKernelGGL(bias_gelu_fwd, dim3((unsigned)g), dim3(256), 0, st, (const uint16_t*)x, bias, (uint16_t*)y,
+                     (int64_t)n4, H);
+  return hipGetLastError();
+}
+
+hipError_t dtfk_bias_gelu_bwd(const void* dy, const void* x, const float* bias, void* dx, float* part, int N, int H,
+                              int row_slices, hipStream_t st) {
+  const int rows_per = (N + row_slices - 1) / row_slices;
+  if (H % 8 == 0)
+    hipLaunchKernelGGL(bias_gelu_bwd8, dim3((H / 8 + 127) / 128, row_slices), dim3(128), 0, st, (const uint16_t*)dy,
+                       (const uint16_t*)x, bias, (uint16_t*)dx, part, N, H, rows_per);
+  else
+    hipLaunchKernelGGL(bias_gelu_bwd, dim3((H / 4 + 255) / 256, row_slices), dim3(256), 0, st, (const uint16_t*)dy,
+                       (const uint16_t*)x, bias, (uint16_t*)dx, part, N, H, rows_per);
+  return hipGetLastError();
+}
+
+hipError_t dtfk_softmax_fwd(const void* S, const float* mask, void* P, void* Pd, int rows, int Sk, int rows_per_batch,
+                            float scale, float p, unsigned long long seed, hipStream_t st) {
+  const float ik = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  if (Sk % 4) return hipErrorInvalidValue;
+  const int nc = Sk <= 256 ? 1 : Sk <= 512 ? 2 : Sk <= 1024 ? 4 : Sk <= 2048 ? 8 : Sk <= 4096 ? 16 : 0;
+  DTFK_NC_DISPATCH(nc, hipLaunchKernelGGL(softmax_fwd<NCv>, dim3(row_grid(rows)), dim3(256), 0, st,
+                     (const uint16_t*)S, mask, (uint16_t*)P, (uint16_t*)Pd, rows, Sk, rows_per_batch, scale,
+                     thresh_of(p), ik, (uint64_t)seed));
+  return hipGetLastError();
+}
+
+hipError_t dtfk_softmax_bwd(const void* dPd, const void* P, void* dS, int rows, int Sk, float scale, float p,
+                            unsigned long long seed, hipStream_t st) {
+  const float ik = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  if (Sk % 4) return hipErrorInvalidValue;
+  const int nc = Sk <= 256 ? 1 : Sk <= 512 ? 2 : Sk <= 1024 ? 4 : Sk <= 2048 ? 8 : Sk <= 4096 ? 16 : 0;
+  DTFK_NC_DISPATCH(nc, hipLaunchKernelGGL(softmax_bwd<NCv>, dim3(row_grid(rows)), dim3(256), 0, st,
+                     (const uint16_t*)dPd, (const uint16_t*)P, (uint16_t*)dS, rows, Sk, scale, thresh_of(p), ik,
+                     (uint64_t)seed));
+  return hipGetLastError();
+}
+
+hipError_t dtfk_dropout_bf16(const void* x, void* y, long long n, float p, unsigned long long seed, hipStream_t st) {
+  const float ik = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const long long n4 = n / 4;
+  long long g = (n4 + 255) / 256;
+  if (g > 65536) g = 65536;
+  hipLaunchKernelGGL(dropout_bf16, dim3((unsigned)g), dim3(256), 0, st, (const uint16_t*)x, (uint16_t*)y,
+                     (int64_t)n4, thresh_of(p), ik, (uint64_t)seed);
+  return hipGetLastError();
+}
+
+}  // extern "C"

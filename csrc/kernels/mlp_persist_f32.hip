@@ -236,6 +236,9 @@ struct Args {
 // variables written through, 6 every workgroup arrived, 7 done count published
 #define RTS(k, slot)                                                                             \
   if (a.res_ts != nullptr) a.res_ts[((k) & 63) * 8 + (slot)] = (long long)__builtin_amdgcn_s_memrealtime();
+// the same in compute: instrumented instantiations only
+#define RTSC(k, slot) \
+  if constexpr (INS) { RTS(k, slot); }
 // phase stamp ph of step st (s_memrealtime, 100 MHz) -- profiling only: compiled
 // into the instrumented instantiations (INS) alone, absent from production code
 #define PH(ph)                                                                                   \
@@ -1003,7 +1006,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
     }
     __syncthreads();
     if (*rflag == 0) return false;
-    if (c == 0 && tid == 0) { RTS(a.run0 + st, 2); }
+    if (c == 0 && tid == 0) { RTSC(a.run0 + st, 2); }
     const auto rs = region_rsrc(a.stage + (long long)(st & 1) * REC, (int)REC);
     const int xr0 = 16 * tile0(q);
 #pragma unroll 4
@@ -1028,7 +1031,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
     __syncthreads();
     read_xf();
     read_xt();
-    if (c == 0 && tid == 0) { RTS(a.run0 + st, 3); }
+    if (c == 0 && tid == 0) { RTSC(a.run0 + st, 3); }
     const float lr_run = *reinterpret_cast<const float*>(smem + L_LAB + RES_LR_BYTE);
     lrB = lr_run / (float)B;
     lrX = lrB * (1.f / 255.f);
@@ -1637,7 +1640,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
       // the last arriver (its add's return value says so) publishes the metrics,
       // global_step and the done count to pinned host memory
       __syncthreads();   // wave 7's LDS updates of W2 / b1 / b2 (and workgroup 0's metrics)
-      if (c == 0 && tid == 0) { RTS(a.run0 + st, 4); }
+      if (c == 0 && tid == 0) { RTSC(a.run0 + st, 4); }
       write_params(true);
       // the graph's global_step: counted here (anything else that writes it stops
       // the engine first), stored write-through by workgroup 0
@@ -1651,7 +1654,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) {
-        if (c == 0) { RTS(a.run0 + st, 5); }
+        if (c == 0) { RTSC(a.run0 + st, 5); }
         __hip_atomic_fetch_add(a.dctr + 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (c == 0) {
           // workgroup 0 (it holds the metrics) publishes once all 28 have arrived
@@ -1663,14 +1666,14 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
               break;
             }
           }
-          RTS(a.run0 + st, 6);
+          RTSC(a.run0 + st, 6);
           const float* mf = reinterpret_cast<const float*>(abort_flag);
           __hip_atomic_store(a.host_out, mf[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           __hip_atomic_store(a.host_out + 1, mf[5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           __hip_atomic_store(a.host_out + 2, (float)gsv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           __hip_atomic_store(a.host_done, a.run0 + st + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          RTS(a.run0 + st, 7);
+          RTSC(a.run0 + st, 7);
         }
       }
     }
@@ -1936,7 +1939,9 @@ hipError_t dtfk_mlp_persist_f32_resident(void* stage, int B, float* W1, float* W
   a.res_ts = g_res_ts;
   constexpr size_t lds = LDS_BYTES;
   typedef void (*Kern)(Args);
-  static const Kern kerns[2] = {mlp_persist_f32<0, 1, true, true>, mlp_persist_f32<1, 1, true, true>};
+  // per-run stamps (DTF_RESIDENT_STAMPS): the instrumented build
+  static const Kern kerns[4] = {mlp_persist_f32<0, 1, true, true>, mlp_persist_f32<1, 1, true, true>,
+                                mlp_persist_f32<0, 1, true, true, 0, true>, mlp_persist_f32<1, 1, true, true, 0, true>};
   static bool attr_set = false;
   if (!attr_set) {
     for (Kern k : kerns) {
@@ -1946,7 +1951,8 @@ hipError_t dtfk_mlp_persist_f32_resident(void* stage, int B, float* W1, float* W
     }
     attr_set = true;
   }
-  hipLaunchKernelGGL(kerns[act == 0 ? 0 : 1], dim3(GRID_PACKED), dim3(THREADS), lds, stream, a);
+  hipLaunchKernelGGL(kerns[(act == 0 ? 0 : 1) + (a.res_ts != nullptr ? 2 : 0)], dim3(GRID_PACKED), dim3(THREADS), lds,
+                     stream, a);
   return hipGetLastError();
 }
 

@@ -1073,6 +1073,11 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
     if constexpr (RES) {
       if (!res_stage(st)) break;
     }
+    // this workgroup's block / slice as opaque values per step: the gathers'
+    // slot selects (k == skip) would otherwise be hoisted out of the step loop as
+    // ten 64-bit lane masks held across it (SGPR spills, a v_readlane per use)
+    int jq[2] = {j, q};
+    asm volatile("" : "+s"(jq[0]), "+s"(jq[1]));
     const unsigned long long sq = seq0 + (unsigned long long)st + 1ull;
     const unsigned tag = (unsigned)sq;
     const int par = (int)(sq & 1ull);
@@ -1190,7 +1195,8 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
         z = (part[0] + part[1]) * 2.f;
       } else {
         f32x4 part[NQ];
-        ok = gather_gran<NQ, INS>(r1, [&](int k) { return (k * NBT + w) * GSLOT; }, q, true, 63, tag, zs, part, lane, a);
+        ok = gather_gran<NQ, INS>(r1, [&](int k) { return (k * NBT + w) * GSLOT; }, jq[1], true, 63, tag, zs, part, lane,
+                                  a);
         z = part[0];
 #pragma unroll
         for (int qq = 1; qq < NQ; ++qq) z += part[qq];
@@ -1220,7 +1226,7 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
 #pragma unroll
       for (int i = 0; i < 4; ++i) a2T[(4 * g + i) * LS + bw] = a2[i];
       f32x4 lp[NJ];
-      ok = gather_gran<NJ, INS>(r2, [&](int k) { return k * GSLOT; }, j, g < 3, 47, tag, pl, lp, lane, a) && ok;
+      ok = gather_gran<NJ, INS>(r2, [&](int k) { return k * GSLOT; }, jq[0], g < 3, 47, tag, pl, lp, lane, a) && ok;
       if (w == 0) { PH(7); }
       if (!ok && lane == 0) *abort_flag = 1;
       // logits, softmax cross-entropy, accuracy -- identical in every workgroup

@@ -57,8 +57,6 @@ hipError_t dtfk_logit3_xent_bwd(const float* dz, const float* g, float* d, float
                                 hipStream_t s);
 hipError_t dtfk_multi_copy(const void* const* src, void* const* dst, const long long* bytes, int n, hipStream_t s);
 hipError_t dtfk_bag_index(const int64_t* offsets, int B, int* bag_of, int64_t N, hipStream_t s);
-hipError_t dtfk_sort_ids(const void* ids, int ids64, int* keys_out, int64_t* perm_out, int n, int end_bit, void* temp,
-                         size_t* temp_bytes, hipStream_t stream);
 hipError_t dtfk_softmax_xent(const float* logits, const int64_t* labels, const float* ydense, float* loss_rows,
                              float* grad, int64_t* correct, int B, int C, float grad_scale, int naive,
                              hipStream_t s);
@@ -413,28 +411,6 @@ void embedding_bag_bwd(at::Tensor target, at::Tensor ids, c10::optional<at::Tens
                             (float)lr, cs()),
      "embedding_bag_bwd");
 }
-// (int32 sorted ids, int64 positions) of non-negative ids < 2^end_bit (int64 or int32)
-std::vector<at::Tensor> sort_ids(at::Tensor ids, int64_t end_bit) {
-  gpu(ids, "ids");
-  if (!ids.is_contiguous() || (ids.scalar_type() != at::kLong && ids.scalar_type() != at::kInt))
-    throw std::runtime_error("sort_ids: contiguous int64 / int32 ids");
-  if (end_bit < 1 || end_bit > 31) throw std::runtime_error("sort_ids: end_bit in [1, 31]");
-  const int64_t n = ids.numel();
-  if (n > 0x7fffffff) throw std::runtime_error("sort_ids: too many ids");
-  auto keys = at::empty({n}, ids.options().dtype(at::kInt));
-  auto perm = at::empty({n}, ids.options().dtype(at::kLong));
-  if (n == 0) return {keys, perm};
-  const int i64 = ids.scalar_type() == at::kLong ? 1 : 0;
-  size_t tb = 0;
-  ck(dtfk_sort_ids(ids.data_ptr(), i64, keys.data_ptr<int>(), perm.data_ptr<int64_t>(), (int)n, (int)end_bit, nullptr,
-                   &tb, cs()),
-     "sort_ids (size)");
-  auto temp = at::empty({(int64_t)std::max<size_t>(tb, 1)}, ids.options().dtype(at::kByte));
-  ck(dtfk_sort_ids(ids.data_ptr(), i64, keys.data_ptr<int>(), perm.data_ptr<int64_t>(), (int)n, (int)end_bit,
-                   temp.data_ptr(), &tb, cs()),
-     "sort_ids");
-  return {keys, perm};
-}
 void bag_index(at::Tensor offsets, at::Tensor bag_of) {
   i64c(offsets, "offsets");
   gpu(bag_of, "bag_of");
@@ -679,7 +655,6 @@ void init_ops(py::module& m) {
   m.def("logit3_xent_bwd", &logit3_xent_bwd);
   m.def("multi_copy", &multi_copy);
   m.def("bag_index", &bag_index);
-  m.def("sort_ids", &sort_ids);
   m.def("softmax_xent", &softmax_xent);
   m.def("xent_fwd_bf16", &xent_fwd_bf16);
   m.def("xent_bwd_bf16", &xent_bwd_bf16);

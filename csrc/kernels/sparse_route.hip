@@ -26,10 +26,6 @@
 // output in one pass (threads i >= U also write the -1 padding of slot i).
 #include "common.h"
 
-#include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/iterator/counting_iterator.hpp>
-#include <rocprim/iterator/transform_iterator.hpp>
-
 namespace dtfk {
 namespace route {
 
@@ -134,32 +130,4 @@ extern "C" hipError_t dtfk_route_scatter(const void* sids, int ids32, const int6
     hipLaunchKernelGGL(route_scatter<int64_t>, g, b, 0, stream, static_cast<const int64_t*>(sids), perm, incl, owncum,
                        N, W, cap, inv_sorted, inverse, uniq, dest, send, count);
   return hipGetLastError();
-}
-
-// The batch's id sort (router dedup + the sorted-segment bag backward): a
-// radix sort of the ids as int32 keys (read straight from int64 ids through a
-// narrowing iterator: no conversion pass) with their positions as values
-// (a counting iterator: no iota pass), over bits [0, end_bit) only.  Onesweep
-// at every size: torch.sort's default below 1 M keys is rocprim's merge sort
-// (a block sort + 7 merge passes at 131,072 ids, ~55 us of a 0.4 ms
-// Wide&Deep step).  Ids must be non-negative and < 2^end_bit.
-namespace dtfk {
-namespace route {
-struct NarrowI32 {
-  __host__ __device__ int operator()(int64_t v) const { return (int)v; }
-};
-}  // namespace route
-}  // namespace dtfk
-
-extern "C" hipError_t dtfk_sort_ids(const void* ids, int ids64, int* keys_out, int64_t* perm_out, int n, int end_bit,
-                                    void* temp, size_t* temp_bytes, hipStream_t stream) {
-  using cfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, rocprim::default_config, 0>;
-  rocprim::counting_iterator<int64_t> pos(0);
-  if (ids64) {
-    auto keys = rocprim::make_transform_iterator(static_cast<const int64_t*>(ids), dtfk::route::NarrowI32());
-    return rocprim::radix_sort_pairs<cfg>(temp, *temp_bytes, keys, keys_out, pos, perm_out, (size_t)n, 0, end_bit,
-                                          stream);
-  }
-  return rocprim::radix_sort_pairs<cfg>(temp, *temp_bytes, static_cast<const int*>(ids), keys_out, pos, perm_out,
-                                        (size_t)n, 0, end_bit, stream);
 }

@@ -347,16 +347,6 @@ def _tkey(t: torch.Tensor):
     return (t.data_ptr(), t.numel(), t._version, _CAPTURE_EPOCH[0])
 
 
-def sort_ids(ids: torch.Tensor, bound: int = 2 ** 31):
-    """(ids as sorted int32, their positions int64) for non-negative ids < bound
-    < 2^31: on the GPU one onesweep radix sort over the ids' bits only, reading
-    int64 ids in place (csrc/kernels/sparse_route.hip dtfk_sort_ids); else torch.sort."""
-    if ids.is_cuda and ids.dtype in (torch.int64, torch.int32) and bound <= 2 ** 31:
-        return tuple(_C().sort_ids(ids.contiguous(), max(1, int(bound - 1).bit_length())))
-    s, p = torch.sort(ids.to(torch.int32))
-    return s, p
-
-
 def register_sorted_ids(ids: torch.Tensor, rows_sorted: torch.Tensor, occ: torch.Tensor) -> None:
     """Hand the bag backward a sort of `ids` that the caller already has (the
     sharded-table router sorts ids to dedup them; the dedup inverse it produces
@@ -372,7 +362,7 @@ def _bag_plan(ids: torch.Tensor, offsets: torch.Tensor):
     one sort, which the router usually supplied already."""
     c = _SORT_PLAN[0]
     if c is None or c[0] != _tkey(ids):
-        rows, occ = sort_ids(ids)
+        rows, occ = torch.sort(ids.to(torch.int32))
         c = (_tkey(ids), ids, (rows.contiguous(), occ.contiguous()))
         _SORT_PLAN[0] = c
     b = _BAG_OF[0]

@@ -217,7 +217,7 @@ class ShardedEmbedding:
         if ids.is_cuda and 0 < N and self.num_rows < 2 ** 31:
             # one int32 radix sort serves both the dedup and (handed over to
             # ops) the sorted-segment backward of every bag over these ids
-            sids, perm = ops.sort_ids(ids)
+            sids, perm = torch.sort(ids.to(torch.int32))
             uniq32, inv_sorted = torch.unique_consecutive(sids, return_inverse=True)
             uniq = uniq32.long()
             inverse = torch.empty_like(ids)
@@ -247,7 +247,7 @@ class ShardedEmbedding:
         overflow voids the step on every rank (StaticRouter)."""
         N, W = ids.numel(), self.W
         small = self.num_rows < 2 ** 31
-        sids, perm = ops.sort_ids(ids) if small else torch.sort(ids)
+        sids, perm = torch.sort(ids.to(torch.int32) if small else ids)
         router = self.router
         if W > 1 and router is None:
             router = self.router = StaticRouter(self.world, self.device, cap)

@@ -712,7 +712,10 @@ __device__ void compute(const Args& a, const int j, const int q, uint8_t* smem) 
   constexpr int XR = EXP > 1 ? EXP : 1;
   const int dbg = INS ? a.dbg : 0;
   constexpr bool MULTI = NW > 1;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // w through readfirstlane: the compiler then knows it is wave-uniform, so the
+  // per-wave conditions (w == 7, w < NBT, the tile-valid flags) are scalar
+  // branches, not 64-bit lane masks hoisted out of the step loop
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 15, g = lane >> 4;
   const int c = j * NQ + q;
   const int B = a.B;

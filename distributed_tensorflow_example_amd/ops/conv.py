@@ -52,6 +52,11 @@ _IGEMM = os.environ.get("DTF_CONV_IGEMM", "auto")
 # a 3x3 forward on the in-tree kernel also writes its output's BatchNorm statistics
 # partials; the FusedBatchNorm2d reading that output then skips its statistics pass
 _BN_STATS = os.environ.get("DTF_CONV_BN_STATS", "1") != "0"
+# strided 1x1 projections: forward / weight gradient on the implicit GEMM's
+# strided loads, chosen per shape against MIOpen (0, default: no gathered copy;
+# ResNet-50 9,391-9,413 vs 9,258-9,302 img/s same box, scripts/sessions/gpu_r6q.sh),
+# or gather the strided pixels once and run them as GEMMs over the copy (1)
+_S2_GATHER = os.environ.get("DTF_CONV_S2_GATHER", "0") != "0"
 _handoff = {}   # id(conv output) -> (partials, P): from _ShadowConv.forward to ShadowConv2d.forward
 _choice: dict = {}
 _timings: dict = {}
@@ -128,10 +133,17 @@ def _C():
 
 
 def igemm_ok(x, w16, stride, padding, dilation, groups) -> bool:
-    """A 3x3 / pad 1 / stride 1 or 2 conv the in-tree implicit GEMM takes."""
-    return (_IGEMM != "never" and w16.dim() == 4 and w16.shape[2] == 3 and w16.shape[3] == 3
-            and tuple(padding) == (1, 1) and tuple(dilation) == (1, 1) and groups == 1
-            and stride[0] == stride[1] and stride[0] in (1, 2) and x.is_cuda and x.dtype == torch.bfloat16
+    """A 3x3 / pad 1 / stride 1 or 2 conv the in-tree implicit GEMM takes -- or,
+    without the strided-pixel gather (DTF_CONV_S2_GATHER=0), a 1x1 / pad 0 /
+    stride 2 projection (its strided loads gather the pixels in place)."""
+    if w16.dim() != 4 or w16.shape[2] != w16.shape[3]:
+        return False
+    k = w16.shape[2]
+    shape_ok = ((k == 3 and tuple(padding) == (1, 1) and stride[0] in (1, 2))
+                or (k == 1 and not _S2_GATHER and tuple(padding) == (0, 0) and stride[0] == 2))
+    return (_IGEMM != "never" and shape_ok
+            and tuple(dilation) == (1, 1) and groups == 1
+            and stride[0] == stride[1] and x.is_cuda and x.dtype == torch.bfloat16
             and w16.dtype == torch.bfloat16 and x.is_contiguous(memory_format=torch.channels_last)
             and w16.is_contiguous(memory_format=torch.channels_last)
             and bool(_C().conv3x3_supported(x, w16, int(stride[0]))))
@@ -284,17 +296,18 @@ def conv3x3_dw(dy, x, stride: int, into=None, ks=None):
 def _dw3_engine(dy, x, w16, stride: int) -> str:
     if _IGEMM == "always":
         return "igemm"
-    key = (tuple(x.shape), w16.shape[0], stride)
+    key = (tuple(x.shape), w16.shape[0], stride, w16.shape[2])
     if ("dw3",) + key not in _choice:
         if _POLICY == "never":
             return "miopen"
         # the accumulator in the layout of the .grad it stands for (the weight's)
         fmt = torch.channels_last if w16.is_contiguous(memory_format=torch.channels_last) else torch.contiguous_format
-        acc = torch.zeros((w16.shape[0], w16.shape[1], 3, 3), device=x.device, dtype=torch.float32).contiguous(
+        k, pad = w16.shape[2], w16.shape[2] // 2
+        acc = torch.zeros((w16.shape[0], w16.shape[1], k, k), device=x.device, dtype=torch.float32).contiguous(
             memory_format=fmt)
 
         def miopen():
-            dw = torch.ops.aten.convolution_backward(dy, x, w16, None, (stride, stride), (1, 1), (1, 1), False,
+            dw = torch.ops.aten.convolution_backward(dy, x, w16, None, (stride, stride), (pad, pad), (1, 1), False,
                                                      [0, 0], 1, [False, True, False])[1]
             acc.add_(dw.float())
         return _pick("dw3", key, {"miopen": miopen, "igemm": lambda: conv3x3_dw(dy, x, stride, into=acc)})
@@ -304,16 +317,17 @@ def _dw3_engine(dy, x, w16, stride: int) -> str:
 def _fwd3_engine(x, w16, stride: int) -> str:
     if _IGEMM == "always":
         return "igemm"
-    key = (tuple(x.shape), w16.shape[0], stride)
+    key = (tuple(x.shape), w16.shape[0], stride, w16.shape[2])
+    pad = w16.shape[2] // 2
     if ("fwd3",) + key not in _choice:
         if _POLICY == "never":
             return "miopen"
         if _BN_STATS:   # the igemm epilogue writes the BatchNorm partials MIOpen's output needs a pass for
             P = conv3x3_stat_rows(x, stride)
             part = torch.empty((2, P, w16.shape[0]), device=x.device, dtype=torch.float32)
-            return _pick("fwd3", key, {"miopen": lambda: _stat_pass(F.conv2d(x, w16, None, stride, 1)),
+            return _pick("fwd3", key, {"miopen": lambda: _stat_pass(F.conv2d(x, w16, None, stride, pad)),
                                        "igemm": lambda: conv3x3(x, w16, stride, stats=part)})
-        return _pick("fwd3", key, {"miopen": lambda: F.conv2d(x, w16, None, stride, 1),
+        return _pick("fwd3", key, {"miopen": lambda: F.conv2d(x, w16, None, stride, pad),
                                    "igemm": lambda: conv3x3(x, w16, stride)})
     return _choice[("fwd3",) + key]
 
@@ -440,7 +454,8 @@ def _strided_ok(x, w16, stride, padding, dilation, groups) -> bool:
 def _s2_ok(x, w16, stride, padding, dilation, groups) -> bool:
     """A strided 1x1 conv (unpadded, ungrouped) whose forward / weight gradient
     may run as GEMMs over the gathered strided pixels (DTF_CONV_GEMM=never: off)."""
-    return _POLICY != "never" and _strided_ok(x, w16, stride, padding, dilation, groups) and tuple(dilation) == (1, 1)
+    return (_S2_GATHER and _POLICY != "never" and _strided_ok(x, w16, stride, padding, dilation, groups)
+            and tuple(dilation) == (1, 1))
 
 
 def _fwd_igemm1(x, w16):
@@ -583,7 +598,8 @@ class _ShadowConv(torch.autograd.Function):
                 conv3x3_dw(dy, x, int(stride[0]), into=grad_sink.target(w))
                 grad_sink.done(w)
                 return dx, None, None, None, None, None, None, None, None, None
-            return dx, conv3x3_dw(dy, x, int(stride[0])).to(w.dtype), None, None, None, None, None, None, None, None
+            return (dx, conv3x3_dw(dy, x, int(stride[0]), ks=w16.shape[2]).to(w.dtype), None, None, None, None, None,
+                    None, None, None)
         if not mw and dw_eng == "igemm":     # the 1x1 implicit GEMM's weight gradient, straight into fp32
             if sink:
                 conv3x3_dw(dy, xw, 1, into=grad_sink.target(w))

@@ -308,6 +308,7 @@ def test_strided_1x1_conv_gathered_gemms_match_conv2d(monkeypatch):
     and weight gradients match nn.functional.conv2d in fp32."""
     from distributed_tensorflow_example_amd.ops import conv
 
+    monkeypatch.setattr(conv, "_S2_GATHER", True)
     torch.manual_seed(9)
     m = conv.ShadowConv2d(128, 256, 1, 2, 0, bias=False).cuda().to(memory_format=torch.channels_last)
     conv.attach_shadows(m)
@@ -322,6 +323,39 @@ def test_strided_1x1_conv_gathered_gemms_match_conv2d(monkeypatch):
         y.backward(dy)
     finally:
         conv._choice.clear()
+    w = m.weight._shadow.float().detach().requires_grad_(True)
+    xr = x.detach().float().requires_grad_(True)
+    ref = F.conv2d(xr, w, None, 2)
+    ref.backward(dy.float())
+    _close(y, ref)
+    _close(x.grad, xr.grad)
+    _close(m.weight.grad, w.grad)
+
+
+@pytest.mark.parametrize("H,W", [(16, 16), (15, 13)])
+def test_strided_1x1_conv_on_implicit_gemm_matches_conv2d(monkeypatch, H, W):
+    """DTF_CONV_S2_GATHER=0: the stride-2 1x1 projection runs its forward (+ the BN
+    statistics hand-off) and weight gradient on the implicit GEMM's strided loads
+    (no gathered copy); output and both gradients match fp32 conv2d."""
+    from distributed_tensorflow_example_amd.ops import conv
+
+    monkeypatch.setattr(conv, "_S2_GATHER", False)
+    torch.manual_seed(13)
+    m = conv.ShadowConv2d(128, 256, 1, 2, 0, bias=False).cuda().to(memory_format=torch.channels_last)
+    conv.attach_shadows(m)
+    x = _cl(torch.randn(4, 128, H, W, device="cuda").bfloat16()).requires_grad_(True)
+    assert conv.igemm_ok(x, m.weight._shadow, (2, 2), (0, 0), (1, 1), 1)
+    conv._choice.clear()
+    key = (tuple(x.shape), 256, 2, 1)
+    conv._choice[("fwd3",) + key] = "igemm"
+    conv._choice[("dw3",) + key] = "igemm"
+    try:
+        y = m(x)
+        dy = _cl(torch.randn_like(y.float()).bfloat16())
+        y.backward(dy)
+    finally:
+        conv._choice.clear()
+        conv._handoff.clear()
     w = m.weight._shadow.float().detach().requires_grad_(True)
     xr = x.detach().float().requires_grad_(True)
     ref = F.conv2d(xr, w, None, 2)

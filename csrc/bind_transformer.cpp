@@ -10,6 +10,12 @@ extern "C" {
 hipError_t dtfk_bdrln_fwd(const void* x, const float* bias, const void* res, const float* gamma, const float* beta,
                           void* y, void* s_out, float* mean, float* rstd, int N, int H, float eps, float p,
                           unsigned long long seed, hipStream_t st);
+hipError_t dtfk_emb_ln_fwd(const float* word, const int64_t* ids, const float* typ, const int64_t* tt,
+                           const float* pos, int S, const float* gamma, const float* beta, void* y, void* s_out,
+                           float* mean, float* rstd, int N, int H, float eps, float p, unsigned long long seed,
+                           hipStream_t st);
+hipError_t dtfk_emb_bwd_aux(const void* ds, const int64_t* tt, int B, int S, int H, float* pos_grad, float* part,
+                            int accumulate, hipStream_t st);
 hipError_t dtfk_ln_fwd_f32in(const float* x, const float* gamma, const float* beta, void* y, void* s_out,
                              float* mean, float* rstd, int N, int H, float eps, float p, unsigned long long seed,
                              hipStream_t st);
@@ -82,6 +88,44 @@ void ln_fwd_f32in(at::Tensor x, at::Tensor gamma, at::Tensor beta, at::Tensor y,
                        mean.data_ptr<float>(), rstd.data_ptr<float>(), N, H, (float)eps, (float)p,
                        (unsigned long long)seed, cs()),
      "ln_fwd_f32in");
+}
+
+// BERT embedding block: y = dropout(LN(word[ids] + typ[tt] + pos[t % S])), s = bf16 of the sum
+void emb_ln_fwd(at::Tensor word, at::Tensor ids, at::Tensor typ, at::Tensor tt, at::Tensor pos, int64_t S,
+                at::Tensor gamma, at::Tensor beta, at::Tensor y, at::Tensor s, at::Tensor mean, at::Tensor rstd,
+                double eps, double p, int64_t seed) {
+  const int H = (int)word.size(-1);
+  req(word, at::kFloat, "word"); req(typ, at::kFloat, "typ"); req(pos, at::kFloat, "pos");
+  req(gamma, at::kFloat, "gamma"); req(beta, at::kFloat, "beta");
+  req(y, at::kBFloat16, "y"); req(s, at::kBFloat16, "s"); req(mean, at::kFloat, "mean"); req(rstd, at::kFloat, "rstd");
+  req(ids, at::kLong, "ids"); req(tt, at::kLong, "tt");
+  const int64_t N = ids.numel();
+  if (tt.numel() != N || y.numel() != N * H || s.numel() != N * H || mean.numel() < N || rstd.numel() < N ||
+      typ.size(-1) != H || pos.size(-1) != H || pos.size(0) < S || S < 1 || N % S)
+    throw std::runtime_error("emb_ln_fwd shapes");
+  ck(dtfk_emb_ln_fwd(word.data_ptr<float>(), ids.data_ptr<int64_t>(), typ.data_ptr<float>(), tt.data_ptr<int64_t>(),
+                     pos.data_ptr<float>(), (int)S, gamma.data_ptr<float>(), beta.data_ptr<float>(), y.data_ptr(),
+                     s.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(), (int)N, H, (float)eps, (float)p,
+                     (unsigned long long)seed, cs()),
+     "emb_ln_fwd");
+}
+// position / 2-row token-type gradients of the embedding block from ds [B*S, H] bf16:
+// pos_grad rows [0, S) (+)= sum over b; typ_grad [2, H] (+)= per-type sums
+void emb_bwd_aux(at::Tensor ds, at::Tensor tt, int64_t S, at::Tensor pos_grad, at::Tensor typ_grad, at::Tensor part,
+                 bool accumulate) {
+  const int H = (int)ds.size(-1);
+  req(ds, at::kBFloat16, "ds"); req(tt, at::kLong, "tt"); req(pos_grad, at::kFloat, "pos_grad");
+  req(typ_grad, at::kFloat, "typ_grad"); req(part, at::kFloat, "part");
+  const int64_t N = tt.numel();
+  if (S < 1 || N % S || ds.numel() != N * H || pos_grad.numel() < S * H || typ_grad.numel() < 2 * H ||
+      part.numel() < 2 * S * H)
+    throw std::runtime_error("emb_bwd_aux shapes");
+  ck(dtfk_emb_bwd_aux(ds.data_ptr(), tt.data_ptr<int64_t>(), (int)(N / S), (int)S, H, pos_grad.data_ptr<float>(),
+                      part.data_ptr<float>(), accumulate ? 1 : 0, cs()),
+     "emb_bwd_aux");
+  const float* parts[2] = {part.data_ptr<float>(), part.data_ptr<float>() + S * H};
+  float* outs[2] = {typ_grad.data_ptr<float>(), typ_grad.data_ptr<float>() + H};
+  ck(dtfk_colsum_partials_multi(parts, outs, 2, (int)S, H, accumulate ? 1 : 0, cs()), "emb_bwd_aux colsum");
 }
 
 // returns nothing; dgamma/dbeta/dbias (fp32 [H]) written if given
@@ -258,6 +302,8 @@ void init_transformer(pybind11::module& m) {
         py::arg("seed"), py::arg("bpart") = py::none(), py::arg("dbias") = py::none(), py::arg("accumulate") = false);
   m.def("bdrln_fwd", &bdrln_fwd);
   m.def("ln_fwd_f32in", &ln_fwd_f32in);
+  m.def("emb_ln_fwd", &emb_ln_fwd);
+  m.def("emb_bwd_aux", &emb_bwd_aux);
   m.def("ln_bwd", &ln_bwd, py::arg("dy"), py::arg("s"), py::arg("mean"), py::arg("rstd"), py::arg("gamma"),
         py::arg("ds"), py::arg("dxb"), py::arg("part"), py::arg("dgamma"), py::arg("dbeta"), py::arg("dbias"),
         py::arg("p"), py::arg("seed"), py::arg("accumulate") = false);

@@ -227,6 +227,111 @@ __global__ __launch_bounds__(256) void ln_fwd_f32in(
   }
 }
 
+// BERT embedding block forward: x = word[ids] + typ[tt] + pos[row % S] (fp32
+// tables, gathered here -- no fp32 [tokens, H] sum tensor), then LayerNorm +
+// dropout as ln_fwd_f32in (bf16 y, bf16 copy s of x for ln_bwd, mean / rstd).
+template <int NC>
+__global__ __launch_bounds__(256) void emb_ln_fwd(
+    const float* __restrict__ word, const int64_t* __restrict__ ids, const float* __restrict__ typ,
+    const int64_t* __restrict__ tt, const float* __restrict__ pos, int S, const float* __restrict__ gamma,
+    const float* __restrict__ beta, uint16_t* __restrict__ y, uint16_t* __restrict__ s_out,
+    float* __restrict__ mean_out, float* __restrict__ rstd_out, int N, int H, float eps, uint32_t thresh,
+    float inv_keep, uint64_t seed) {
+  const int lane = threadIdx.x & 63;
+  for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < N; row += gridDim.x * 4) {
+    const size_t base = (size_t)row * H;
+    const float* wr = word + (size_t)ids[row] * H;
+    const float* tr = typ + (size_t)tt[row] * H;
+    const float* pr = pos + (size_t)(row % S) * H;
+    float v[NC][4];
+    float sum = 0.f;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      const int c = (k * 64 + lane) * 4;
+      float a[4], b[4], d[4];
+      ld4f(wr + c, a);
+      ld4f(tr + c, b);
+      ld4f(pr + c, d);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[k][j] = a[j] + b[j] + d[j];
+        sum += v[k][j];
+      }
+    }
+    const float mean = wave_sum(sum) / H;
+    float var = 0.f;
+#pragma unroll
+    for (int k = 0; k < NC; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { const float dd = v[k][j] - mean; var += dd * dd; }
+    const float rstd = rsqrtf(wave_sum(var) / H + eps);
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      const int c = (k * 64 + lane) * 4;
+      float g[4], b[4], o[4];
+      ld4f(gamma + c, g);
+      ld4f(beta + c, b);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        o[j] = (v[k][j] - mean) * rstd * g[j] + b[j];
+        if (thresh) o[j] = keep_elem(seed, base + c + j, thresh) ? o[j] * inv_keep : 0.f;
+      }
+      st4(y + base + c, o);
+      st4(s_out + base + c, v[k]);
+    }
+    if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
+  }
+}
+
+// BERT embedding block backward, position / token-type part: block s (one per
+// position) sums ds [B*S, H] (bf16, the LN input gradient) over the batch rows
+// b*S + s into pos_grad[s] (+= when accumulate) and writes the token-type
+// partial sums of that position to part[t][s][H] (t = 0, 1; colsum_partials
+// finishes them into the 2-row table's gradient).  Fixed order: deterministic.
+template <int NC>
+__global__ __launch_bounds__(256) void emb_bwd_aux(const uint16_t* __restrict__ ds, const int64_t* __restrict__ tt,
+                                                   int B, int S, int H, float* __restrict__ pos_grad,
+                                                   float* __restrict__ part, int accumulate) {
+  __shared__ float red[2][4][NC * 256];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int s = blockIdx.x;
+  float a0[NC][4], a1[NC][4];
+#pragma unroll
+  for (int k = 0; k < NC; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a0[k][j] = a1[k][j] = 0.f;
+  for (int b = w; b < B; b += 4) {
+    const size_t row = (size_t)b * S + s;
+    const bool one = tt[row] != 0;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      float d[4];
+      ld4(ds + row * H + (k * 64 + lane) * 4, d);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (one) a1[k][j] += d[j];
+        else a0[k][j] += d[j];
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NC; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      red[0][w][(k * 64 + lane) * 4 + j] = a0[k][j];
+      red[1][w][(k * 64 + lane) * 4 + j] = a1[k][j];
+    }
+  __syncthreads();
+  for (int c = threadIdx.x; c < H; c += 256) {
+    const float t0 = (red[0][0][c] + red[0][1][c]) + (red[0][2][c] + red[0][3][c]);
+    const float t1 = (red[1][0][c] + red[1][1][c]) + (red[1][2][c] + red[1][3][c]);
+    float* pg = pos_grad + (size_t)s * H + c;
+    *pg = accumulate ? *pg + (t0 + t1) : (t0 + t1);
+    part[(size_t)s * H + c] = t0;
+    part[(size_t)(S + s) * H + c] = t1;
+  }
+}
+
 // ---------------------------------------------------------------- bias + GELU (erf form)
 // Exact-GELU normal CDF via Abramowitz-Stegun 7.1.26 (|erf error| <= 1.5e-7,
 // far below bf16's 4e-3): one rcp, one exp, a 5-term polynomial.  The exp is
@@ -394,6 +499,37 @@ __global__ __launch_bounds__(1024) void colsum_partials(ColsumArgs a, int P, int
   if (g == 0 && c < H) {
     const float t = red[0][lane];
     out[c] = accumulate ? out[c] + t : t;
+  }
+}
+
+// the same for an even H whose rows are only 4-byte aligned (the MLM decoder's
+// [M, 30522] logits gradient): 256 threads = 64 lanes x 2 columns x 4 row
+// groups, grid = (ceil(H / 128), P)
+__global__ __launch_bounds__(256) void colsum_bf16x2_partials(const uint16_t* __restrict__ x, float* __restrict__ part,
+                                                              int N, int H) {
+  __shared__ float red[4][128];
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c0 = blockIdx.x * 128 + 2 * lane;
+  const int P = gridDim.y;
+  const int r0 = (int)((long long)N * blockIdx.y / P), r1 = (int)((long long)N * (blockIdx.y + 1) / P);
+  float s0 = 0.f, s1 = 0.f;
+  if (c0 < H)
+    for (int r = r0 + g; r < r1; r += 4) {
+      const uint32_t v = *reinterpret_cast<const uint32_t*>(x + (size_t)r * H + c0);
+      s0 += bf2f(v & 0xffff);
+      s1 += bf2f(v >> 16);
+    }
+  red[g][2 * lane] = s0;
+  red[g][2 * lane + 1] = s1;
+  __syncthreads();
+  if (g == 0) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int c = c0 + k;
+      if (c < H)
+        part[(size_t)blockIdx.y * H + c] =
+            (red[0][2 * lane + k] + red[1][2 * lane + k]) + (red[2][2 * lane + k] + red[3][2 * lane + k]);
+    }
   }
 }
 
@@ -597,6 +733,30 @@ hipError_t dtfk_bdrln_fwd(const void* x, const float* bias, const void* res, con
   return hipGetLastError();
 }
 
+hipError_t dtfk_emb_ln_fwd(const float* word, const int64_t* ids, const float* typ, const int64_t* tt,
+                           const float* pos, int S, const float* gamma, const float* beta, void* y, void* s_out,
+                           float* mean, float* rstd, int N, int H, float eps, float p, unsigned long long seed,
+                           hipStream_t st) {
+  if (H % 256 || N < 1 || S < 1) return hipErrorInvalidValue;
+  const uint32_t thresh = thresh_of(p);
+  const float inv_keep = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  DTFK_NC_DISPATCH(H / 256, hipLaunchKernelGGL(emb_ln_fwd<NCv>, dim3(row_grid(N)), dim3(256), 0, st, word, ids, typ,
+                                               tt, pos, S, gamma, beta, (uint16_t*)y, (uint16_t*)s_out, mean, rstd, N,
+                                               H, eps, thresh, inv_keep, (uint64_t)seed));
+  return hipGetLastError();
+}
+hipError_t dtfk_emb_bwd_aux(const void* ds, const int64_t* tt, int B, int S, int H, float* pos_grad, float* part,
+                            int accumulate, hipStream_t st) {
+  if (H % 256 || H > 1024 || B < 1 || S < 1) return hipErrorInvalidValue;
+  switch (H / 256) {
+    case 1: hipLaunchKernelGGL(emb_bwd_aux<1>, dim3(S), dim3(256), 0, st, (const uint16_t*)ds, tt, B, S, H, pos_grad, part, accumulate); break;
+    case 2: hipLaunchKernelGGL(emb_bwd_aux<2>, dim3(S), dim3(256), 0, st, (const uint16_t*)ds, tt, B, S, H, pos_grad, part, accumulate); break;
+    case 3: hipLaunchKernelGGL(emb_bwd_aux<3>, dim3(S), dim3(256), 0, st, (const uint16_t*)ds, tt, B, S, H, pos_grad, part, accumulate); break;
+    case 4: hipLaunchKernelGGL(emb_bwd_aux<4>, dim3(S), dim3(256), 0, st, (const uint16_t*)ds, tt, B, S, H, pos_grad, part, accumulate); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
 hipError_t dtfk_ln_fwd_f32in(const float* x, const float* gamma, const float* beta, void* y, void* s_out,
                              float* mean, float* rstd, int N, int H, float eps, float p, unsigned long long seed,
                              hipStream_t st) {
@@ -636,9 +796,15 @@ hipError_t dtfk_colsum_partials_multi(const float* const* parts, float* const* o
 
 hipError_t dtfk_colsum_bf16(const void* x, float* part, float* out, int N, int H, int P, int accumulate,
                             hipStream_t st) {
-  if (H % 8 || ((uintptr_t)x % 16)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(colsum_bf16_partials, dim3((H + 511) / 512, P), dim3(256), 0, st,
-                     static_cast<const uint16_t*>(x), part, N, H);
+  if (H % 8 == 0 && (uintptr_t)x % 16 == 0) {
+    hipLaunchKernelGGL(colsum_bf16_partials, dim3((H + 511) / 512, P), dim3(256), 0, st,
+                       static_cast<const uint16_t*>(x), part, N, H);
+  } else if (H % 2 == 0 && (uintptr_t)x % 4 == 0) {
+    hipLaunchKernelGGL(colsum_bf16x2_partials, dim3((H + 127) / 128, P), dim3(256), 0, st,
+                       static_cast<const uint16_t*>(x), part, N, H);
+  } else {
+    return hipErrorInvalidValue;
+  }
   dtfk::tfm::ColsumArgs a = {{part, nullptr, nullptr}, {out, nullptr, nullptr}};
   hipLaunchKernelGGL(colsum_partials, dim3((H + CS_COLS - 1) / CS_COLS, 1), dim3(1024), 0, st, a, P, H, accumulate);
   return hipGetLastError();

@@ -21,6 +21,8 @@ from __future__ import annotations
 import math
 from dataclasses import dataclass
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -340,12 +342,18 @@ class BertForMLM(torch.nn.Module):
         mlm_positions [M] flat indices into B*S; mlm_labels [M] int64."""
         c = self.c
         B, S = input_ids.shape
-        if c.type_vocab == 2:       # 2-row table: a lerp (reduction backward) beats contended scatter-adds
-            typ = self.typ[0] + token_type.reshape(-1, 1).to(self.typ.dtype) * (self.typ[1] - self.typ[0])
+        if input_ids.is_cuda and c.type_vocab == 2 and os.environ.get("DTF_BERT_EMB_FUSED", "1") != "0":
+            # gather + sum + LayerNorm + dropout in one kernel, its backward in three
+            # (ops/transformer.py _BertEmbed)
+            x = T.bert_embed(self.word, self.typ, self.pos, self.emb_g, self.emb_b, input_ids, token_type,
+                             c.dropout, c.ln_eps, self.training)
         else:
-            typ = _lookup(self.typ, token_type)
-        emb = (_lookup(self.word, input_ids) + typ).view(B, S, c.hidden) + self.pos[:S].unsqueeze(0)
-        x = T.layernorm_dropout(emb, self.emb_g, self.emb_b, c.dropout, c.ln_eps, self.training)
+            if c.type_vocab == 2:   # 2-row table: a lerp (reduction backward) beats contended scatter-adds
+                typ = self.typ[0] + token_type.reshape(-1, 1).to(self.typ.dtype) * (self.typ[1] - self.typ[0])
+            else:
+                typ = _lookup(self.typ, token_type)
+            emb = (_lookup(self.word, input_ids) + typ).view(B, S, c.hidden) + self.pos[:S].unsqueeze(0)
+            x = T.layernorm_dropout(emb, self.emb_g, self.emb_b, c.dropout, c.ln_eps, self.training)
         act = torch.bfloat16 if x.is_cuda else torch.float32
         x = x.to(act)
         add_mask = (1.0 - attn_mask.float()) * -10000.0

@@ -174,6 +174,7 @@ class _XentBF16(torch.autograd.Function):
         C.xent_fwd_bf16(logits, bias, labels, lse, loss_rows)
         ctx.save_for_backward(logits, bias if bias is not None else torch.empty(0, device=logits.device), labels, lse)
         ctx.has_bias = bias is not None
+        ctx.bias_param = bias
         return loss_rows.mean()
 
     @staticmethod
@@ -183,7 +184,25 @@ class _XentBF16(torch.autograd.Function):
         grad = torch.empty_like(logits)
         C.xent_bwd_bf16(logits, bias if ctx.has_bias else None, labels, lse, g.float().reshape(1).contiguous(), grad,
                         1.0 / logits.shape[0])
-        dbias = grad.sum(0, dtype=torch.float32) if ctx.has_bias else None
+        dbias = None
+        if ctx.has_bias:
+            from . import grad_sink
+            # column sums on the in-tree two-stage kernel (torch's bf16 sum over the
+            # [M, vocab] gradient was ~90 us of a BERT-base step); sunk into
+            # .grad when the bias carries a DDP sink
+            V = grad.shape[-1]
+            rows = grad.numel() // V
+            if V % 2 or grad.data_ptr() % 4:
+                return grad, grad.sum(0, dtype=torch.float32).reshape(bias.shape), None
+            part = torch.empty(max(1, min(256, rows // 64)) * V, dtype=torch.float32, device=grad.device)
+            pb = ctx.bias_param
+            sink = pb is not None and grad_sink.all_enabled(pb)
+            out = grad_sink.target(pb) if sink else torch.empty(V, dtype=torch.float32, device=grad.device)
+            C.colsum_bf16(grad.reshape(rows, V), part, out, accumulate=sink)
+            if sink:
+                grad_sink.done(pb)
+            else:
+                dbias = out.reshape(bias.shape)
         return grad, dbias, None
 
 

@@ -193,6 +193,103 @@ class _EmbLN(torch.autograd.Function):
         return ds.float().view(ctx.shape), dgamma, dbeta, None, None
 
 
+class _BertEmbed(torch.autograd.Function):
+    """y = dropout(LayerNorm(word[ids] + typ[tt] + pos[:S])) (bf16) in one kernel
+    that gathers the fp32 rows itself (csrc/kernels/transformer.hip emb_ln_fwd);
+    backward: ln_bwd -> ds, then the position and 2-row token-type gradients
+    from ds in one pass (emb_bwd_aux + one finishing colsum) and the word rows
+    through the sorted-segment scatter.  Replaces the fp32 [tokens, H] sum, its
+    lerp / adds and torch's reductions over the batch."""
+
+    @staticmethod
+    def forward(ctx, word, typ, pos, gamma, beta, ids, tt, p, eps):
+        C = _C()
+        B, S = ids.shape
+        H = word.shape[-1]
+        N = B * S
+        y = torch.empty((N, H), dtype=torch.bfloat16, device=word.device)
+        s = torch.empty_like(y)
+        mean = torch.empty(N, dtype=torch.float32, device=word.device)
+        rstd = torch.empty_like(mean)
+        seed = next_seed() if p > 0 else 0
+        idf, ttf = ids.reshape(-1).contiguous(), tt.reshape(-1).contiguous()
+        C.emb_ln_fwd(word, idf, typ, ttf, pos, S, gamma, beta, y, s, mean, rstd, eps, p, seed)
+        ctx.save_for_backward(s, mean, rstd, gamma, idf, ttf)
+        ctx.params = (gamma, beta, pos, typ)
+        ctx.p, ctx.seed, ctx.B, ctx.S, ctx.wshape = p, seed, B, S, word.shape
+        return y.view(B, S, H)
+
+    @staticmethod
+    def backward(ctx, dy):
+        from . import _bag_plan
+        C = _C()
+        s, mean, rstd, gamma, idf, ttf = ctx.saved_tensors
+        H = s.shape[-1]
+        dy2 = dy.reshape(-1, H).to(torch.bfloat16).contiguous()
+        if ctx.p > 0:
+            dyd = torch.empty_like(dy2)
+            C.dropout_bf16(dy2, dyd, ctx.p, ctx.seed)
+            dy2 = dyd
+        N = dy2.shape[0]
+        ds = torch.empty_like(dy2)
+        pg, pb, ppos, ptyp = ctx.params
+        sink = grad_sink.all_enabled(pg, pb)
+        if sink:
+            dgamma, dbeta = grad_sink.target(pg), grad_sink.target(pb)
+        else:
+            dgamma = torch.empty(H, dtype=torch.float32, device=dy.device)
+            dbeta = torch.empty_like(dgamma)
+        C.ln_bwd(dy2, s, mean, rstd, gamma, ds, None, _ln_part(N, H, dy.device), dgamma, dbeta, None, 0.0, 0,
+                 accumulate=sink)
+        # position + token-type gradients: one pass over ds
+        sink2 = grad_sink.all_enabled(ppos, ptyp)
+        if sink2:
+            dpos, dtyp = grad_sink.target(ppos), grad_sink.target(ptyp)
+        else:
+            dpos = torch.zeros_like(ppos)
+            dtyp = torch.empty_like(ptyp)
+        part = torch.empty(2 * ctx.S * H, dtype=torch.float32, device=dy.device)
+        C.emb_bwd_aux(ds, ttf, ctx.S, dpos, dtyp, part, sink2)
+        # word rows: the sorted-segment scatter (one bag per token)
+        gw = torch.zeros(ctx.wshape, dtype=torch.float32, device=dy.device)
+        offs = _identity_offsets(N, dy.device)
+        rows, occ, bag_of = _bag_plan(idf, offs)
+        C.embedding_bag_bwd_sorted(gw, rows, occ, bag_of, None, ds.float())
+        if sink:
+            grad_sink.done(pg)
+            grad_sink.done(pb)
+            dgamma = dbeta = None
+        if sink2:
+            grad_sink.done(ppos)
+            grad_sink.done(ptyp)
+            dpos = dtyp = None
+        return gw, dtyp, dpos, dgamma, dbeta, None, None, None, None
+
+
+_IDOFFS: dict = {}
+
+
+def _identity_offsets(n: int, device) -> torch.Tensor:
+    """arange(n + 1) on `device`, cached (one bag per token)."""
+    key = (n, str(device))
+    t = _IDOFFS.get(key)
+    if t is None:
+        t = _IDOFFS[key] = torch.arange(n + 1, device=device)
+    return t
+
+
+def bert_embed(word, typ, pos, gamma, beta, ids, tt, p: float = 0.0, eps: float = 1e-12, training: bool = True):
+    """dropout(LayerNorm(word[ids] + typ[tt] + pos[:S])) for [B, S] ids; bf16 out
+    on the GPU (fused), the plain composition elsewhere."""
+    p = p if training else 0.0
+    S = ids.shape[1]
+    if (not word.is_cuda or typ.shape[0] != 2 or word.shape[-1] % 256 or word.shape[-1] > 1024
+            or ids.dtype != torch.int64 or tt.dtype != torch.int64):
+        x = word[ids] + typ[tt] + pos[:S].unsqueeze(0)
+        return layernorm_dropout(x, gamma, beta, p, eps, training)
+    return _BertEmbed.apply(word, typ, pos, gamma, beta, ids, tt, float(p), float(eps))
+
+
 def layernorm_dropout(x, gamma, beta, p: float = 0.0, eps: float = 1e-12, training: bool = True):
     p = p if training else 0.0
     if not x.is_cuda:

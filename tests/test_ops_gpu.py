@@ -335,11 +335,13 @@ def test_compat_mnist_graph_trains_on_gpu(native):
     assert c < first and a > 0.4
 
 
-@pytest.mark.parametrize("C", [30522, 10, 1002])
-def test_bf16_vocab_xent_with_bias(native, C):
+@pytest.mark.parametrize("C,B", [(30522, 37), (10, 37), (1002, 37), (1001, 37), (30522, 300)])
+def test_bf16_vocab_xent_with_bias(native, C, B):
+    """bf16 vocab cross-entropy with the fused bias; its gradient from the in-tree
+    column sums (16-byte / 4-byte row variants, several row slices) or torch's sum
+    (odd vocab)."""
     from distributed_tensorflow_example_amd import ops
     torch.manual_seed(C)
-    B = 37
     logits = (torch.randn(B, C) * 3).bfloat16()
     bias = torch.randn(C) * 0.5
     labels = torch.randint(0, C, (B,))

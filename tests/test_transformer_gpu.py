@@ -283,3 +283,52 @@ def test_slab_sum_matches_torch(native, S, n):
     assert torch.allclose(out, ref, rtol=1e-5, atol=1e-5)
     native.slab_sum(slabs, out, accumulate=False)
     assert torch.allclose(out, slabs.sum(0), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("H", [256, 768])
+def test_bert_embed_fused_matches_reference(native, H):
+    """The fused embedding block (gather word / type / position rows + LayerNorm,
+    one kernel; position and 2-row type gradients in one pass, word rows by the
+    sorted scatter) against the fp32 composition: output and every gradient."""
+    from distributed_tensorflow_example_amd.ops import transformer as T
+    torch.manual_seed(H)
+    B, S, V = 4, 16, 1000
+    word, typ, pos = torch.randn(V, H) * 0.1, torch.randn(2, H) * 0.1, torch.randn(64, H) * 0.1
+    gamma, beta = 1 + 0.1 * torch.randn(H), 0.1 * torch.randn(H)
+    ids = torch.randint(0, V, (B, S))
+    ids[0, :4] = 7                                 # repeated rows in the scatter
+    tt = torch.randint(0, 2, (B, S))
+    ref_p = [t.clone().requires_grad_() for t in (word, typ, pos, gamma, beta)]
+    x = ref_p[0][ids] + ref_p[1][tt] + ref_p[2][:S].unsqueeze(0)
+    ref = torch.nn.functional.layer_norm(x, (H,), ref_p[3], ref_p[4], 1e-12)
+    gy = torch.randn_like(ref)
+    ref.backward(gy)
+    got_p = [t.cuda().requires_grad_() for t in (word, typ, pos, gamma, beta)]
+    out = T.bert_embed(*got_p, ids.cuda(), tt.cuda(), 0.0, 1e-12, True)
+    assert out.dtype == torch.bfloat16 and out.shape == (B, S, H)
+    out.backward(gy.cuda().bfloat16())
+    assert (out.float().cpu() - ref.detach()).abs().max() < 3e-2
+    for g, r in zip(got_p, ref_p):
+        err = float((g.grad.float().cpu() - r.grad).norm() / r.grad.norm().clamp_min(1e-12))
+        assert err < 2e-2, err
+
+
+def test_bert_embed_fused_dropout_consistent(native):
+    """p > 0: the forward's dropped elements are exactly the ones the backward
+    masks (same hash), and about p of them are dropped."""
+    from distributed_tensorflow_example_amd.ops import transformer as T
+    torch.manual_seed(1)
+    B, S, H, V, p = 8, 32, 256, 500, 0.25
+    ps = [t.cuda().requires_grad_() for t in (torch.randn(V, H), torch.randn(2, H), torch.randn(S, H),
+                                             torch.ones(H), torch.zeros(H))]
+    ids, tt = torch.randint(0, V, (B, S)).cuda(), torch.randint(0, 2, (B, S)).cuda()
+    out = T.bert_embed(*ps, ids, tt, p, 1e-12, True)
+    dropped = out.float() == 0
+    frac = float(dropped.float().mean())
+    assert abs(frac - p) < 0.03, frac
+    out.float().sum().backward()
+    assert torch.isfinite(ps[0].grad).all() and torch.isfinite(ps[2].grad).all()
+    # beta's gradient counts the kept elements only (each kept output scales by
+    # 1/(1-p); the backward's dropout rescale is bf16: 1.3359 for 1/0.75)
+    kept = (~dropped).float().sum(dim=(0, 1)) / (1 - p)
+    assert torch.allclose(ps[4].grad, kept, rtol=5e-3, atol=1e-2)

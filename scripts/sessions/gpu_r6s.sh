@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 6, session s: BERT-base fused embedding block + in-tree decoder-bias
+# round 6, session s (and v): BERT-base fused embedding block + in-tree decoder-bias
 # column sums: transformer / op / model tests, then same-box A/B vs ab_old/ (HEAD)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 ROOT=$PWD; OUT=$ROOT/gpurun_out; mkdir -p $OUT

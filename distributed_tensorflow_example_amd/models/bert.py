@@ -94,7 +94,15 @@ class _ShadowLinear(torch.autograd.Function):
             _wgrad(gy2, x2, into=grad_sink.target(w))
             grad_sink.done(w)
             return gx, None, None, None
-        return gx, _wgrad(gy2, x2), None, None
+        dw = _wgrad(gy2, x2)
+        epoch = getattr(w, "_dtf_tied_epoch", None) if getattr(w, "_dtf_tied", False) else None
+        if epoch is not None:
+            # a tied weight (BERT's word embedding / MLM decoder) whose fused
+            # embedding forward tagged it: that embedding's backward, which runs
+            # after this one, scatters its rows into this same tensor instead of
+            # a zeroed one that autograd would then add (ops/transformer.py _BertEmbed)
+            w._dtf_tied_dw = (epoch, dw)
+        return gx, dw, None, None
 
 
 def _linear_dx(gy2, w16, extra=None):

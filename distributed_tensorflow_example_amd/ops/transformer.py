@@ -217,6 +217,9 @@ class _BertEmbed(torch.autograd.Function):
         ctx.save_for_backward(s, mean, rstd, gamma, idf, ttf)
         ctx.params = (gamma, beta, pos, typ)
         ctx.p, ctx.seed, ctx.B, ctx.S, ctx.wshape = p, seed, B, S, word.shape
+        # tied word table (MLM decoder): this forward's token, see backward
+        ctx.word = word
+        ctx.epoch = word._dtf_tied_epoch = object() if getattr(word, "_dtf_tied", False) else None
         return y.view(B, S, H)
 
     @staticmethod
@@ -250,11 +253,23 @@ class _BertEmbed(torch.autograd.Function):
             dtyp = torch.empty_like(ptyp)
         part = torch.empty(2 * ctx.S * H, dtype=torch.float32, device=dy.device)
         C.emb_bwd_aux(ds, ttf, ctx.S, dpos, dtyp, part, sink2)
-        # word rows: the sorted-segment scatter (one bag per token)
-        gw = torch.zeros(ctx.wshape, dtype=torch.float32, device=dy.device)
+        # word rows: the sorted-segment scatter (one bag per token).  A tied table
+        # whose decoder gradient of THIS forward is parked on the parameter takes
+        # the rows straight into that tensor (autograd then has nothing to add)
+        gw, ret = None, True
+        if ctx.epoch is not None:
+            tied = getattr(ctx.word, "_dtf_tied_dw", None)
+            ctx.word._dtf_tied_dw = None
+            if (tied is not None and tied[0] is ctx.epoch and tied[1].dtype == torch.float32
+                    and tied[1].shape == ctx.wshape and tied[1].is_contiguous()):
+                gw, ret = tied[1], False
+        if gw is None:
+            gw = torch.zeros(ctx.wshape, dtype=torch.float32, device=dy.device)
         offs = _identity_offsets(N, dy.device)
         rows, occ, bag_of = _bag_plan(idf, offs)
         C.embedding_bag_bwd_sorted(gw, rows, occ, bag_of, None, ds.float())
+        if not ret:
+            gw = None
         if sink:
             grad_sink.done(pg)
             grad_sink.done(pb)

@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 6, session t: ResNet-50 kernel trace after the no-gather projections (what glue is left)
+# round 6, session u: ResNet-50 kernel trace after the no-gather projections (what glue is left)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out; mkdir -p $OUT

@@ -332,3 +332,38 @@ def test_bert_embed_fused_dropout_consistent(native):
     # 1/(1-p); the backward's dropout rescale is bf16: 1.3359 for 1/0.75)
     kept = (~dropped).float().sum(dim=(0, 1)) / (1 - p)
     assert torch.allclose(ps[4].grad, kept, rtol=5e-3, atol=1e-2)
+
+
+def test_bert_tied_word_grad_fused_matches_composed(native, monkeypatch):
+    """BertForMLM's tied word table: the fused embedding's backward scatters its
+    rows straight into the MLM decoder's dW (no zeroed table, no autograd add);
+    the summed gradient must equal the composed path's (DTF_BERT_EMB_FUSED=0),
+    over two steps (a stale decoder dW from an earlier step is never reused)."""
+    from distributed_tensorflow_example_amd.models import bert
+    c = bert.BertConfig.tiny()
+    c.dropout = 0.0
+    B, S = 4, 32
+    g = torch.Generator().manual_seed(3)
+    ids = torch.randint(0, c.vocab_size, (B, S), generator=g).cuda()
+    tt = torch.randint(0, 2, (B, S), generator=g).cuda()
+    mask = torch.ones(B, S, dtype=torch.int64).cuda()
+    pos = torch.arange(0, B * S, 5).cuda()
+    lab = torch.randint(0, c.vocab_size, (pos.numel(),), generator=g).cuda()
+
+    def grads(fused):
+        monkeypatch.setenv("DTF_BERT_EMB_FUSED", "1" if fused else "0")
+        m = bert.BertForMLM(c, seed=0).cuda()
+        m.attach_shadows()
+        out = []
+        for _ in range(2):
+            m.zero_grad(set_to_none=True)
+            m(ids, tt, mask, pos, lab).backward()
+            out.append([p.grad.detach().clone() for p in (m.word, m.pos, m.typ)])
+        if fused:
+            assert getattr(m.word, "_dtf_tied_dw", "absent") is None   # parked, then consumed
+        return out
+
+    for a, b in zip(grads(True), grads(False)):
+        for x, y in zip(a, b):
+            err = float((x - y).norm() / y.norm().clamp_min(1e-12))
+            assert err < 2e-2, err

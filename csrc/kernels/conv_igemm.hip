@@ -426,7 +426,10 @@ __device__ __forceinline__ bf16x8 frag_tr(const uint8_t* img, int rb, int s, int
   return __builtin_bit_cast(bf16x8, v);
 }
 
-template <int KS, int BMW, int BNW>
+// DEPTH: register sets of operands in flight -- a step's loads go out DEPTH
+// steps ahead (2: the original two-ahead prefetch; 3: one more set, which the
+// 128x128 tile's 220 VGPRs leave room for at the same two workgroups per CU)
+template <int KS, int BMW, int BNW, int DEPTH = 2>
 __global__ __launch_bounds__(NTHR, 2) void conv_wgrad(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
                                                          float* __restrict__ dw, int N, int H, int W, int C, int K,
                                                          int Ho, int Wo, int stride, long long xbytes,
@@ -508,7 +511,8 @@ __global__ __launch_bounds__(NTHR, 2) void conv_wgrad(const uint16_t* __restrict
       while (bho[i] >= Ho) { bho[i] -= Ho; bn_[i] += 1; }
     }
   };
-  u32x4 ra[2][NA], rb[2][NB];
+  static_assert(DEPTH == 2 || DEPTH == 3, "two or three operand sets in flight");
+  u32x4 ra[DEPTH][NA], rb[DEPTH][NB];
   auto load = [&](int step, auto pc) {
     constexpr int Q = decltype(pc)::value;
     const long long p0 = pb + (long long)step * PK;
@@ -528,16 +532,16 @@ __global__ __launch_bounds__(NTHR, 2) void conv_wgrad(const uint16_t* __restrict
     }
     advance();
   };
-  auto store = [&](auto pc) {
-    constexpr int Q = decltype(pc)::value;
-    uint8_t* A = smem + Q * BUF;
+  auto store = [&](auto pr, auto pl) {   // register set R -> LDS buffer L
+    constexpr int R = decltype(pr)::value, L = decltype(pl)::value;
+    uint8_t* A = smem + L * BUF;
     uint8_t* Bs = A + A_BYTES;
 #pragma unroll
     for (int i = 0; i < NA; ++i)
-      *reinterpret_cast<u32x4*>(A + (arow0 + ARS * i) * (2 * BMW) + 16 * ach) = ra[Q][i];
+      *reinterpret_cast<u32x4*>(A + (arow0 + ARS * i) * (2 * BMW) + 16 * ach) = ra[R][i];
 #pragma unroll
     for (int i = 0; i < NB; ++i)
-      *reinterpret_cast<u32x4*>(Bs + (brow0 + BRS * i) * (2 * BNW) + 16 * bphys[i]) = rb[Q][i];
+      *reinterpret_cast<u32x4*>(Bs + (brow0 + BRS * i) * (2 * BNW) + 16 * bphys[i]) = rb[R][i];
   };
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -546,18 +550,26 @@ __global__ __launch_bounds__(NTHR, 2) void conv_wgrad(const uint16_t* __restrict
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
   if (nsteps > 0) {
     load(0, I0{});
     if (nsteps > 1) load(1, I1{});
-    store(I0{});
+    if constexpr (DEPTH == 3) {
+      if (nsteps > 2) load(2, I2{});
+    }
+    store(I0{}, I0{});
   }
   __syncthreads();
-  auto body = [&](int step, auto pc) {
-    constexpr int Q = decltype(pc)::value;
-    using Q1 = std::integral_constant<int, Q ^ 1>;
-    if (step + 1 < nsteps) store(Q1{});
-    if (step + 2 < nsteps) load(step + 2, pc);
-    const uint8_t* A = smem + Q * BUF;
+  // step s: its operands sit in LDS buffer s & 1 and came from register set
+  // s % DEPTH; first step s + 1's set goes into the other buffer (free since the
+  // last barrier), then step s + DEPTH is loaded into set s % DEPTH (stored already)
+  auto body = [&](int step, auto pr, auto pl) {
+    constexpr int R = decltype(pr)::value, L = decltype(pl)::value;
+    using Rn = std::integral_constant<int, (R + 1) % DEPTH>;
+    using Ln = std::integral_constant<int, L ^ 1>;
+    if (step + 1 < nsteps) store(Rn{}, Ln{});
+    if (step + DEPTH < nsteps) load(step + DEPTH, pr);
+    const uint8_t* A = smem + L * BUF;
     const uint8_t* Bs = A + A_BYTES;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -573,9 +585,20 @@ __global__ __launch_bounds__(NTHR, 2) void conv_wgrad(const uint16_t* __restrict
     }
     __syncthreads();
   };
-  for (int step = 0; step < nsteps; step += 2) {
-    body(step, I0{});
-    if (step + 1 < nsteps) body(step + 1, I1{});
+  if constexpr (DEPTH == 2) {
+    for (int step = 0; step < nsteps; step += 2) {
+      body(step, I0{}, I0{});
+      if (step + 1 < nsteps) body(step + 1, I1{}, I1{});
+    }
+  } else {
+    for (int step = 0; step < nsteps; step += 6) {   // (set, buffer) repeats every 6 steps
+      body(step, I0{}, I0{});
+      if (step + 1 < nsteps) body(step + 1, I1{}, I1{});
+      if (step + 2 < nsteps) body(step + 2, I2{}, I0{});
+      if (step + 3 < nsteps) body(step + 3, I0{}, I1{});
+      if (step + 4 < nsteps) body(step + 4, I1{}, I0{});
+      if (step + 5 < nsteps) body(step + 5, I2{}, I1{});
+    }
   }
   const int fr = lane & 15, fk = lane >> 4;
   if (ws != nullptr) {
@@ -908,10 +931,19 @@ hipError_t dtfk_conv_wgrad(const void* dy, const void* x, float* dw, float* ws, 
   while (G < 16 && 2 * G <= splits && (slab / 4) * G < 131072) G *= 2;
   auto d = static_cast<const uint16_t*>(dy);
   auto xs = static_cast<const uint16_t*>(x);
+  // operand sets in flight (DTF_CONV_WGRAD_DEPTH: 2 or 3; 3 where it keeps the occupancy)
+  static const int depth = [] {
+    const char* e = getenv("DTF_CONV_WGRAD_DEPTH");
+    return e && atoi(e) == 2 ? 2 : 3;
+  }();
 #define DTFK_WG(KSV, A, B)                                                                                         \
   do {                                                                                                             \
-    hipLaunchKernelGGL((conv_wgrad<KSV, A, B>), grid, dim3(NTHR), 0, stream, d, xs, dw, N, H, W, C, K, Ho, Wo,     \
-                       stride, xbytes, sps, kcrs, wsp, slab, tiles_x, tiles_y, xcd);                               \
+    if (depth == 3 && !(A == 64 && B == 128)) /* 64x128: 192 VGPRs at depth 3, one wave/SIMD less */              \
+      hipLaunchKernelGGL((conv_wgrad<KSV, A, B, 3>), grid, dim3(NTHR), 0, stream, d, xs, dw, N, H, W, C, K, Ho,    \
+                         Wo, stride, xbytes, sps, kcrs, wsp, slab, tiles_x, tiles_y, xcd);                         \
+    else                                                                                                           \
+      hipLaunchKernelGGL((conv_wgrad<KSV, A, B, 2>), grid, dim3(NTHR), 0, stream, d, xs, dw, N, H, W, C, K, Ho,    \
+                         Wo, stride, xbytes, sps, kcrs, wsp, slab, tiles_x, tiles_y, xcd);                         \
     if (wsp)                                                                                                       \
       hipLaunchKernelGGL((wgrad_reduce<KSV, A, B>), dim3((unsigned)((slab / 4 + 256 / G - 1) / (256 / G))),        \
                          dim3(256), 0, stream, wsp, splits, slab, dw, C, tiles_x, kcrs, G);                        \

@@ -25,7 +25,7 @@ def main():
               (1, 512, 2048, 7, 1), (1, 2048, 512, 7, 1),
               (3, 64, 64, 56, 1), (3, 128, 128, 56, 2), (3, 128, 128, 28, 1), (3, 256, 256, 28, 2),
               (3, 256, 256, 14, 1), (3, 512, 512, 14, 2), (3, 512, 512, 7, 1)]
-    tag = {"wgs": os.environ.get("DTF_CONV_WGRAD_WGS", "512"),
+    tag = {"wgs": os.environ.get("DTF_CONV_WGRAD_WGS", "512"), "depth": os.environ.get("DTF_CONV_WGRAD_DEPTH", "3"),
            "minsteps": os.environ.get("DTF_CONV_WGRAD_MINSTEPS", "8")}
     for ks, C, K, H, s in shapes:
         x = torch.randn(B, C, H, H, device="cuda").bfloat16().contiguous(memory_format=cl)

@@ -53,6 +53,31 @@ def test_bdrln_dropout_mask_consistency(native):
     assert abs(zero_grad - p) < 0.02
 
 
+@pytest.mark.parametrize("N", [512, 333])
+def test_bdrln_forward_mask_is_backward_mask(native, N):
+    """The dropped elements of the forward's saved s (bdrln_fwd, 16-byte half-wave
+    rows) are exactly the ones ln_bwd's dropout-branch gradient zeroes (same
+    element indices), odd row counts included."""
+    from distributed_tensorflow_example_amd.ops import transformer as T
+    C = T._C()
+    H, p, seed = 768, 0.25, -(1 << 63) + 977
+    torch.manual_seed(5)
+    x = torch.randn(N, H, device="cuda").bfloat16() + 4.0     # no exact zeros before dropout
+    bias, g, b = torch.zeros(H, device="cuda"), torch.ones(H, device="cuda"), torch.zeros(H, device="cuda")
+    y, s = torch.empty_like(x), torch.empty_like(x)
+    mean, rstd = torch.empty(N, device="cuda"), torch.empty(N, device="cuda")
+    C.bdrln_fwd(x, bias, None, g, b, y, s, mean, rstd, 1e-12, p, seed)
+    dy = torch.randn_like(x)
+    ds, dxb = torch.empty_like(x), torch.empty_like(x)
+    dg, db, dbias = (torch.empty(H, device="cuda") for _ in range(3))
+    C.ln_bwd(dy, s, mean, rstd, g, ds, dxb, T._ln_part(N, H, x.device), dg, db, dbias, p, seed, False)
+    dropped_f, dropped_b = s == 0, (dxb == 0) & (ds != 0)
+    assert abs(float(dropped_f.float().mean()) - p) < 0.02
+    assert int((dropped_f & (ds != 0) != dropped_b).sum()) == 0
+    ref = torch.nn.functional.layer_norm(s.float(), (H,), eps=1e-12)
+    assert rel(y, ref) < 1e-2
+
+
 def test_layernorm_dropout_embeddings(native):
     from distributed_tensorflow_example_amd.ops import transformer as T
     N, H = 200, 768

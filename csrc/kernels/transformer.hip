@@ -472,92 +472,6 @@ __global__ __launch_bounds__(256) void bdrln_fwd16(
   }
 }
 
-// ln_bwd in the same half-wave-row form (bdrln_fwd16's layout): two rows per
-// wave per trip, 16-byte accesses; the halves' column partials are combined
-// with one lane^32 exchange before the block's LDS sum (the same [grid, H] output)
-template <int NC>
-__global__ __launch_bounds__(256) void ln_bwd16(
-    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ s, const float* __restrict__ mean_in,
-    const float* __restrict__ rstd_in, const float* __restrict__ gamma, uint16_t* __restrict__ ds_out,
-    uint16_t* __restrict__ dxb_out, float* __restrict__ part_g, float* __restrict__ part_b,
-    float* __restrict__ part_bias, int N, int H, uint32_t thresh, float inv_keep, uint64_t seed) {
-  const int lane = threadIdx.x & 63, hl = lane & 31, half = lane >> 5, wid = threadIdx.x >> 6;
-  float accg[NC][8], accb[NC][8], accx[NC][8];
-#pragma unroll
-  for (int k = 0; k < NC; ++k)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) accg[k][j] = accb[k][j] = accx[k][j] = 0.f;
-  for (int pr = blockIdx.x * 4 + wid; 2 * pr < N; pr += gridDim.x * 4) {
-    const int row = 2 * pr + half;
-    const bool valid = row < N;   // the odd tail row's half runs on zeros
-    const int rr = valid ? row : N - 1;
-    const size_t base = (size_t)rr * H;
-    const float mean = mean_in[rr], rstd = rstd_in[rr];
-    float xh[NC][8], gdy[NC][8];
-    float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int k = 0; k < NC; ++k) {
-      const int c = (k * 32 + hl) * 8;
-      float sv[8], dv[8], g[8];
-      ld8v(s + base + c, sv);
-      ld8v(dy + base + c, dv);
-      *reinterpret_cast<float4*>(g) = *reinterpret_cast<const float4*>(gamma + c);
-      *reinterpret_cast<float4*>(g + 4) = *reinterpret_cast<const float4*>(gamma + c + 4);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float d = valid ? dv[j] : 0.f;
-        xh[k][j] = (sv[j] - mean) * rstd;
-        gdy[k][j] = d * g[j];
-        s1 += gdy[k][j];
-        s2 += gdy[k][j] * xh[k][j];
-        accg[k][j] += d * xh[k][j];
-        accb[k][j] += d;
-      }
-    }
-    s1 = half_sum(s1) / H;
-    s2 = half_sum(s2) / H;
-#pragma unroll
-    for (int k = 0; k < NC; ++k) {
-      const int c = (k * 32 + hl) * 8;
-      float d[8], dx[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        d[j] = rstd * (gdy[k][j] - s1 - xh[k][j] * s2);
-        dx[j] = thresh ? (keep_elem(seed, base + c + j, thresh) ? d[j] * inv_keep : 0.f) : d[j];
-        accx[k][j] += dx[j];
-      }
-      if (valid) {
-        st8v(ds_out + base + c, d);
-        if (dxb_out) st8v(dxb_out + base + c, dx);
-      }
-    }
-  }
-  __shared__ float red[4][256];
-  float* outs[3] = {part_g, part_b, part_bias};
-#pragma unroll
-  for (int which = 0; which < 3; ++which) {
-    float* out = outs[which];
-    if (!out) continue;
-#pragma unroll
-    for (int k = 0; k < NC; ++k) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float v = which == 0 ? accg[k][j] : (which == 1 ? accb[k][j] : accx[k][j]);
-        v += __shfl_xor(v, 32, 64);
-        if (half == 0) red[wid][hl * 8 + j] = v;
-      }
-      __syncthreads();
-      if (wid == 0)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int i = lane * 4 + j;
-          out[(size_t)blockIdx.x * H + k * 256 + i] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
-        }
-      __syncthreads();
-    }
-  }
-}
-
 __global__ __launch_bounds__(256) void bias_gelu_fwd8(const uint16_t* __restrict__ x, const float* __restrict__ bias,
                                                       uint16_t* __restrict__ y, int64_t n8, int H) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
@@ -877,18 +791,15 @@ static inline uint32_t thresh_of(float p) {
   return t >= 4294967295.0 ? 4294967295u : (uint32_t)t;
 }
 
-// DTF_LN16=0: the 8-byte, one-row-per-wave LayerNorm forward (the 16-byte form
-// is the default); DTF_LN16_BWD=1: the 16-byte LayerNorm backward (not the default)
-static bool env_flag(const char* name, bool dflt) {
-  const char* e = getenv(name);
-  return e && e[0] ? e[0] != '0' : dflt;
-}
+// DTF_LN16=0: the 8-byte, one-row-per-wave LayerNorm forward (the 16-byte form is
+// the default; the backward stays 8-byte: its 16-byte form holds 3 x 24 column
+// partials per lane, 232 VGPRs, half the occupancy -- 26 -> 38 us, measured and removed,
+// profiles/bdrln_fwd16_r6.txt)
 static bool use_ln16() {
-  static const bool v = env_flag("DTF_LN16", true);
-  return v;
-}
-static bool use_ln16_bwd() {
-  static const bool v = env_flag("DTF_LN16_BWD", false);
+  static const bool v = [] {
+    const char* e = getenv("DTF_LN16");
+    return !(e && e[0] == '0');
+  }();
   return v;
 }
 
@@ -951,13 +862,6 @@ hipError_t dtfk_ln_bwd(const void* dy, const void* s, const float* mean, const f
                        float p, unsigned long long seed, hipStream_t st) {
   const float ik = p > 0.f ? 1.f / (1.f - p) : 1.f;
   if (H % 256) return hipErrorInvalidValue;
-  // (H <= 1024: the 16-byte form's column partials fit in registers)
-  if (use_ln16_bwd() && H <= 1024) {
-    DTFK_NC_DISPATCH(H / 256, hipLaunchKernelGGL(ln_bwd16<NCv>, dim3(grid), dim3(256), 0, st, (const uint16_t*)dy,
-                       (const uint16_t*)s, mean, rstd, gamma, (uint16_t*)ds, (uint16_t*)dxb, part_g, part_b, part_bias,
-                       N, H, thresh_of(p), ik, (uint64_t)seed));
-    return hipGetLastError();
-  }
   DTFK_NC_DISPATCH(H / 256, hipLaunchKernelGGL(ln_bwd<NCv>, dim3(grid), dim3(256), 0, st, (const uint16_t*)dy,
                      (const uint16_t*)s, mean, rstd, gamma, (uint16_t*)ds, (uint16_t*)dxb, part_g, part_b, part_bias,
                      N, H, thresh_of(p), ik, (uint64_t)seed));

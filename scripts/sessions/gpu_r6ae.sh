@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 6, session ae: ln_bwd with 16-byte accesses, half a wave per row
-# (DTF_LN16_BWD=1) vs the 8-byte kernel (DTF_LN16_BWD=0), forward 16-byte in both: LN / BERT
+# (DTF_LN16_BWD=1, a knob of that build; kernel since removed) vs the 8-byte kernel: LN / BERT
 # tests, isolated kernel times, then same-box BERT-base alternating
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 ROOT=$PWD; OUT=$ROOT/gpurun_out; mkdir -p $OUT

@@ -45,6 +45,8 @@
 // Row/column tails are clamped (their products only reach unstored outputs).
 #include "common.h"
 
+#include <cstdlib>
+
 namespace dtfk {
 namespace gemm2 {
 
@@ -1025,7 +1027,14 @@ static SplitPlan plan_split(int M, int N, int K, int c_bf16, float beta, int act
   SplitPlan p{1, K, 0};
   if (!(split_k > 1 || (split_k <= 0 && linear && tiles < 256 && K >= 2048))) return p;
   const bool slabs = ph8 && linear && N % 4 == 0;
-  int split = split_k > 1 ? split_k : (slabs ? (int)max(2LL, 256 / tiles) : (int)((512 + tiles - 1) / tiles));
+  // slab mode's workgroup target (DTF_GEMM_SLAB_WGS, default 256: ~one per CU);
+  // fewer means fewer, longer splits and less fp32 slab traffic
+  static const long long slab_wgs = [] {
+    const char* e = getenv("DTF_GEMM_SLAB_WGS");
+    const long long v = e ? atoll(e) : 0LL;
+    return v > 0 ? v : 256LL;
+  }();
+  int split = split_k > 1 ? split_k : (slabs ? (int)max(2LL, slab_wgs / tiles) : (int)((512 + tiles - 1) / tiles));
   split = min(split, K / (slabs ? 256 : 512) > 0 ? K / (slabs ? 256 : 512) : 1);
   p.kchunk = ((K + split - 1) / split + kq - 1) / kq * kq;
   p.split = (K + p.kchunk - 1) / p.kchunk;
